@@ -1,0 +1,65 @@
+"""slate_amd: MI355X-native distributed dense linear algebra.
+
+A new implementation (not a port) of the capabilities of SLATE
+(xiaohunqupo/slate): tiled distributed matrices over a 2D block-cyclic grid
+of MI355X GPUs (one process per GPU, RCCL over xGMI), parallel BLAS-3,
+Cholesky / LU / QR / LQ factorizations and solvers, least squares,
+eigenvalue and singular value problems, norms and condition estimates,
+with every hot kernel hand-written in HIP for CDNA4 (gfx950).
+
+Public API mirrors `include/slate/slate.hh` and the simplified names of
+`include/slate/simplified_api.hh`.
+"""
+__version__ = "2026.10.0"
+
+from . import _native  # noqa: F401  (loads _host, tries _hip)
+from .core.enums import (  # noqa: F401
+    AllDevices, AnyDevice, Diag, Direction, Equed, GridOrder, HostNum, Job, Layout, LayoutConvert,
+    MethodCholQR, MethodEig, MethodGels, MethodGemm, MethodHemm, MethodLU, MethodSVD, MethodTrsm,
+    MOSI, Norm, NormScope, Op, Option, Side, Target, TileKind, Uplo)
+from .core.exceptions import (  # noqa: F401
+    CommError, HipError, NotImplementedYet, NumericalError, SlateError, slate_assert, slate_error,
+    slate_error_if)
+from .core.options import Options, get_option  # noqa: F401
+from .core.tile import Tile  # noqa: F401
+from .core.matrix import (  # noqa: F401
+    BandMatrix, BaseBandMatrix, BaseMatrix, BaseTrapezoidMatrix, BaseTriangularBandMatrix,
+    HermitianBandMatrix, HermitianMatrix, Matrix, Pivot, Pivots, SymmetricMatrix, TrapezoidMatrix,
+    TriangularBandMatrix, TriangularFactors, TriangularMatrix)
+from .core import func  # noqa: F401
+from .parallel.comm import Comm, ProcessGrid, finalize, init, world  # noqa: F401
+from .utils.matgen import MatgenParams, generate_matrix  # noqa: F401
+from .utils.trace import Trace, trace_block  # noqa: F401
+from .utils.timers import timers, timer  # noqa: F401
+
+from .models.blas3 import (  # noqa: F401
+    gemm, hemm, her2k, herk, multiply, rank_2k_update, rank_k_update, symm, syr2k, syrk,
+    triangular_multiply, triangular_solve, trmm, trsm)
+from .models.chol import posv, potrf, potri, potrs  # noqa: F401
+from .models.aux import (  # noqa: F401
+    add, colNorms, copy, gather, norm, redistribute, scale, scale_row_col, set)
+
+
+def version():
+    """SLATE `version()`: yyyymmdd-style integer."""
+    return 20261015
+
+
+def id():  # noqa: A001 - SLATE API name
+    return "slate_amd-" + __version__
+
+
+def chol_factor(A, opts=None):
+    return potrf(A, opts)
+
+
+def chol_solve(A, B, opts=None):
+    return posv(A, B, opts)
+
+
+def chol_solve_using_factor(A, B, opts=None):
+    return potrs(A, B, opts)
+
+
+def chol_inverse_using_factor(A, opts=None):
+    return potri(A, opts)

@@ -1,0 +1,108 @@
+"""In-tree native build of slate_amd's extensions.
+
+Two pybind11 extension modules are produced next to this file:
+
+* ``_hip.so``  -- every CDNA4 kernel, compiled by ``hipcc --offload-arch=gfx950``
+  (one translation unit per kernel family/dtype so builds run in parallel).
+* ``_host.so`` -- the native host runtime (tile/MOSI table, slab memory pool,
+  trace recorder, Philox matrix generator, host tile kernels for the
+  ``Target.Host*`` CPU path), compiled by ``g++ -fopenmp``.
+
+Objects are cached under ``build/`` and rebuilt when a source or any header
+of the same directory is newer.  Used by ``__graft_entry__.build()``,
+``setup.py`` and ``python -m slate_amd._build``.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+BUILD = os.path.join(ROOT, "build")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = "gfx950"
+
+
+def _pybind_includes():
+    import pybind11
+    return [pybind11.get_include(), sysconfig.get_paths()["include"]]
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("build failed:\n" + " ".join(cmd) + "\n" + r.stdout)
+    return r.stdout
+
+
+def _jobs():
+    for k in ("MAX_JOBS", "CMAKE_BUILD_PARALLEL_LEVEL"):
+        if os.environ.get(k, "").isdigit():
+            return max(1, min(16, int(os.environ[k])))
+    return max(1, min(16, os.cpu_count() or 4))
+
+
+def _build_module(name, srcdir, exts, compiler, cflags, ldflags, verbose=False):
+    srcs = sorted(sum((glob.glob(os.path.join(srcdir, "*" + e)) for e in exts), []))
+    headers = glob.glob(os.path.join(srcdir, "*.hpp")) + glob.glob(os.path.join(HERE, "csrc", "include", "*.hpp"))
+    objdir = os.path.join(BUILD, name)
+    os.makedirs(objdir, exist_ok=True)
+    ext_suffix = ".so"
+    target = os.path.join(HERE, name + ext_suffix)
+    objs, todo = [], []
+    for s in srcs:
+        o = os.path.join(objdir, os.path.basename(s) + ".o")
+        objs.append(o)
+        if _newer(o, [s] + headers):
+            todo.append((s, o))
+
+    def compile_one(so):
+        s, o = so
+        cmd = [compiler] + cflags + ["-c", s, "-o", o]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        _run(cmd)
+        return o
+
+    if todo:
+        with cf.ThreadPoolExecutor(_jobs()) as ex:
+            for f in [ex.submit(compile_one, so) for so in todo]:
+                f.result()
+    if todo or _newer(target, objs):
+        _run([compiler] + ["-shared", "-o", target] + objs + ldflags)
+    return target
+
+
+def build(verbose=False, hip=True, host=True):
+    inc = ["-I" + p for p in _pybind_includes()] + ["-I" + os.path.join(HERE, "csrc", "include")]
+    out = []
+    if host:
+        out.append(_build_module(
+            "_host", os.path.join(HERE, "csrc", "host"), [".cpp"], "g++",
+            ["-O3", "-std=c++17", "-fPIC", "-fopenmp", "-fvisibility=hidden", "-Wall", "-Wno-unused-function"] + inc,
+            ["-fopenmp"], verbose))
+    if hip:
+        hipcc = os.path.join(ROCM, "bin", "hipcc")
+        out.append(_build_module(
+            "_hip", os.path.join(HERE, "csrc", "hip"), [".hip"], hipcc,
+            ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
+             "-x", "hip"] + inc,
+            ["--offload-arch=" + ARCH, "-L" + os.path.join(ROCM, "lib"), "-lamdhip64"], verbose))
+    return out
+
+
+if __name__ == "__main__":
+    for t in build(verbose="-v" in sys.argv):
+        print("built", t)

@@ -1,0 +1,260 @@
+// Element-wise / data-movement kernels for gfx950 (SURVEY §2.5:
+// device_geset/tzset, gescale/tzscale, geadd/tzadd, gecopy/tzcopy with
+// precision conversion, transpose, gescale_row_col) and the row-permutation
+// kernel used by LU (replacing internal_swap.cc's per-row swaps).
+//
+// All operate on one strided column-major block (the rank's whole local
+// buffer or any sub-block of it), so a matrix-wide op is ONE launch; grids
+// are (rows/256) x (columns, grid-strided) with coalesced row access.
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace slate_hip {
+
+namespace {
+inline dim3 grid2(i64 m, i64 n) {
+    i64 gx = (m + 255) / 256;
+    i64 gy = std::min<i64>(n, 4096);
+    return dim3((unsigned)std::max<i64>(gx, 1), (unsigned)std::max<i64>(gy, 1));
+}
+__device__ inline bool in_uplo(char uplo, i64 i, i64 j) {
+    return uplo == 'L' ? i >= j : (uplo == 'U' ? i <= j : true);
+}
+}  // namespace
+
+template <typename T>
+__global__ void geset_kernel(char uplo, i64 m, i64 n, T off, T diag, T* A, i64 lda) {
+    i64 i = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    for (i64 j = blockIdx.y; j < n; j += gridDim.y)
+        if (in_uplo(uplo, i, j)) A[i + j * lda] = (i == j) ? diag : off;
+}
+
+template <typename T>
+__global__ void gescale_kernel(char uplo, i64 m, i64 n, T alpha, T* A, i64 lda) {
+    i64 i = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    for (i64 j = blockIdx.y; j < n; j += gridDim.y)
+        if (in_uplo(uplo, i, j)) A[i + j * lda] = s_mul(alpha, A[i + j * lda]);
+}
+
+template <typename T>
+__global__ void geadd_kernel(char uplo, i64 m, i64 n, T alpha, const T* A, i64 lda, T beta, T* B, i64 ldb) {
+    i64 i = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    const bool b0 = s_is_zero(beta);
+    for (i64 j = blockIdx.y; j < n; j += gridDim.y)
+        if (in_uplo(uplo, i, j)) {
+            T v = s_mul(alpha, A[i + j * lda]);
+            if (!b0) v = s_add(v, s_mul(beta, B[i + j * ldb]));
+            B[i + j * ldb] = v;
+        }
+}
+
+template <typename Ts, typename Td>
+__device__ inline Td convert(Ts v) {
+    if constexpr (scalar_traits<Ts>::is_complex && scalar_traits<Td>::is_complex) {
+        Td r; r.re = (typename scalar_traits<Td>::real)v.re; r.im = (typename scalar_traits<Td>::real)v.im; return r;
+    } else if constexpr (scalar_traits<Td>::is_complex) {
+        Td r; r.re = (typename scalar_traits<Td>::real)v; r.im = 0; return r;
+    } else if constexpr (scalar_traits<Ts>::is_complex) {
+        return (Td)v.re;
+    } else {
+        return (Td)v;
+    }
+}
+
+// B (m x n) = op(A) with precision conversion; uplo masks the destination.
+template <typename Ts, typename Td>
+__global__ void gecopy_kernel(char uplo, i64 m, i64 n, const Ts* A, i64 lda, Td* B, i64 ldb) {
+    i64 i = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    for (i64 j = blockIdx.y; j < n; j += gridDim.y)
+        if (in_uplo(uplo, i, j)) B[i + j * ldb] = convert<Ts, Td>(A[i + j * lda]);
+}
+
+// Transposed copy through a 32x33 LDS tile: B (m x n) = op(A), A is n x m.
+template <typename Ts, typename Td, bool CONJ>
+__global__ void transpose_kernel(char uplo, i64 m, i64 n, const Ts* A, i64 lda, Td* B, i64 ldb) {
+    __shared__ Td tile[32][33];
+    const i64 bi = (i64)blockIdx.x * 32, bj = (i64)blockIdx.y * 32;   // block of B
+    const int tx = threadIdx.x, ty = threadIdx.y;   // 32 x 8
+    // read A block (rows bj.., cols bi..) coalesced along A's rows
+    for (int r = ty; r < 32; r += 8) {
+        i64 ar = bj + tx, ac = bi + r;   // A(ar, ac) -> B(ac, ar)
+        if (ar < n && ac < m) {
+            Td v = convert<Ts, Td>(A[ar + ac * lda]);
+            if constexpr (CONJ) v = s_conj(v);
+            tile[r][tx] = v;
+        }
+    }
+    __syncthreads();
+    for (int c = ty; c < 32; c += 8) {
+        i64 brow = bi + tx, bcol = bj + c;
+        if (brow < m && bcol < n && in_uplo(uplo, brow, bcol)) B[brow + bcol * ldb] = tile[tx][c];
+    }
+}
+
+template <typename T, typename R>
+__global__ void scale_row_col_kernel(char equed, i64 m, i64 n, const R* r, const R* c, T* A, i64 lda) {
+    i64 i = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    for (i64 j = blockIdx.y; j < n; j += gridDim.y) {
+        R s = R(1);
+        if (equed == 'R' || equed == 'B') s *= r[i];
+        if (equed == 'C' || equed == 'B') s *= c[j];
+        A[i + j * lda] = s_mul(s_from_real(T(), s), A[i + j * lda]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Row interchanges.  The LAPACK-style swap sequence ipiv[k1..k2) (0-based
+// rows, ipiv[k] >= k) is first folded into a permutation of the touched rows
+// (open-addressing hash map in LDS, built by one thread: O(#swaps)), then
+// every workgroup moves a 32-column chunk: gather touched rows into LDS,
+// barrier, scatter to their new positions.  One launch for any n.
+namespace {
+constexpr int HSIZE = 2048;      // hash slots (>= 2 x max swaps per call)
+constexpr int MAXSW = 512;       // max swaps per call (more: split into calls)
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+laswp_kernel(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* __restrict__ ipiv, i64 ioff, int incx, int CCH) {
+    __shared__ i64 hkey[HSIZE];
+    __shared__ int hval[HSIZE];       // index into touched list
+    __shared__ i64 trow[2 * MAXSW];   // touched rows
+    __shared__ i64 tsrc[2 * MAXSW];   // original row now found at trow[t]
+    __shared__ int ntouched;
+    extern __shared__ __align__(16) unsigned char dyn[];
+    T* buf = reinterpret_cast<T*>(dyn);   // [2*MAXSW][CCH] gathered rows (sized at launch)
+    for (int h = threadIdx.x; h < HSIZE; h += blockDim.x) hkey[h] = -1;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int cnt = 0;
+        auto slot = [&](i64 row) -> int {
+            unsigned hsh = (unsigned)((row * 2654435761ull) >> 7) & (HSIZE - 1);
+            while (hkey[hsh] != -1 && hkey[hsh] != row) hsh = (hsh + 1) & (HSIZE - 1);
+            if (hkey[hsh] == -1) { hkey[hsh] = row; hval[hsh] = cnt; trow[cnt] = row; tsrc[cnt] = row; ++cnt; }
+            return hval[hsh];
+        };
+        const i64 ns = k2 - k1;
+        for (i64 s = 0; s < ns; ++s) {
+            i64 k = incx > 0 ? k1 + s : k2 - 1 - s;
+            i64 p = ipiv[k] - ioff;
+            if (p == k) continue;
+            int a = slot(k), b = slot(p);
+            i64 t = tsrc[a]; tsrc[a] = tsrc[b]; tsrc[b] = t;
+        }
+        ntouched = cnt;
+    }
+    __syncthreads();
+    const int nt = ntouched;
+    if (nt == 0) return;
+    const i64 c0 = (i64)blockIdx.x * CCH;
+    const int ncols = (int)min((i64)CCH, n - c0);
+    // gather: buf[t][c] = A[tsrc[t], c0 + c]
+    for (int idx = threadIdx.x; idx < nt * CCH; idx += blockDim.x) {
+        int t = idx % nt, c = idx / nt;
+        if (c < ncols) buf[t * CCH + c] = A[tsrc[t] + (c0 + c) * lda];
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < nt * CCH; idx += blockDim.x) {
+        int t = idx % nt, c = idx / nt;
+        if (c < ncols) A[trow[t] + (c0 + c) * lda] = buf[t * CCH + c];
+    }
+}
+
+template <typename T>
+__global__ void row_gather_kernel(i64 m, i64 n, const T* A, i64 lda, T* B, i64 ldb, const i64* perm) {
+    i64 i = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    const i64 src = perm[i];
+    for (i64 j = blockIdx.y; j < n; j += gridDim.y) B[i + j * ldb] = A[src + j * lda];
+}
+
+// ---------------------------------------------------------------------------
+template <typename T> void geset(char uplo, i64 m, i64 n, T off, T diag, T* A, i64 lda, hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    hipLaunchKernelGGL(geset_kernel<T>, grid2(m, n), dim3(256), 0, s, uplo, m, n, off, diag, A, lda);
+    HIP_LAUNCH_CHECK();
+}
+template <typename T> void gescale(char uplo, i64 m, i64 n, T alpha, T* A, i64 lda, hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    hipLaunchKernelGGL(gescale_kernel<T>, grid2(m, n), dim3(256), 0, s, uplo, m, n, alpha, A, lda);
+    HIP_LAUNCH_CHECK();
+}
+template <typename T>
+void geadd(char uplo, i64 m, i64 n, T alpha, const T* A, i64 lda, T beta, T* B, i64 ldb, hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    hipLaunchKernelGGL(geadd_kernel<T>, grid2(m, n), dim3(256), 0, s, uplo, m, n, alpha, A, lda, beta, B, ldb);
+    HIP_LAUNCH_CHECK();
+}
+template <typename Ts, typename Td>
+void gecopy(char uplo, char trans, i64 m, i64 n, const Ts* A, i64 lda, Td* B, i64 ldb, hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    if (trans == 'N') {
+        hipLaunchKernelGGL((gecopy_kernel<Ts, Td>), grid2(m, n), dim3(256), 0, s, uplo, m, n, A, lda, B, ldb);
+    } else {
+        dim3 grid((unsigned)((m + 31) / 32), (unsigned)((n + 31) / 32));
+        if (trans == 'C')
+            hipLaunchKernelGGL((transpose_kernel<Ts, Td, true>), grid, dim3(32, 8), 0, s, uplo, m, n, A, lda, B, ldb);
+        else
+            hipLaunchKernelGGL((transpose_kernel<Ts, Td, false>), grid, dim3(32, 8), 0, s, uplo, m, n, A, lda, B, ldb);
+    }
+    HIP_LAUNCH_CHECK();
+}
+template <typename T, typename R>
+void gescale_row_col(char equed, i64 m, i64 n, const R* r, const R* c, T* A, i64 lda, hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    hipLaunchKernelGGL((scale_row_col_kernel<T, R>), grid2(m, n), dim3(256), 0, s, equed, m, n, r, c, A, lda);
+    HIP_LAUNCH_CHECK();
+}
+template <typename T>
+void laswp_off(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, i64 ioff, hipStream_t s, int incx) {
+    if (n <= 0 || k2 <= k1) return;
+    if (k2 - k1 > MAXSW) {
+        if (incx > 0)
+            for (i64 k = k1; k < k2; k += MAXSW) laswp_off<T>(n, A, lda, k, std::min(k2, k + MAXSW), ipiv, ioff, s, incx);
+        else
+            for (i64 k = k2; k > k1; k -= MAXSW) laswp_off<T>(n, A, lda, std::max(k1, k - MAXSW), k, ipiv, ioff, s, incx);
+        return;
+    }
+    const size_t per_col = (size_t)2 * (k2 - k1) * sizeof(T);
+    int cch = (int)std::max<size_t>(1, std::min<size_t>(16, (96 * 1024) / per_col));
+    size_t shmem = per_col * cch;
+    unsigned g = (unsigned)((n + cch - 1) / cch);
+    hipLaunchKernelGGL(laswp_kernel<T>, dim3(g), dim3(256), shmem, s, n, A, lda, k1, k2, ipiv, ioff, incx, cch);
+    HIP_LAUNCH_CHECK();
+}
+template <typename T>
+void laswp(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, int incx, hipStream_t s) {
+    laswp_off<T>(n, A, lda, k1, k2, ipiv, 0, s, incx);
+}
+template <typename T>
+void permute_rows_gather(i64 m, i64 n, const T* A, i64 lda, T* B, i64 ldb, const i64* perm, hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    hipLaunchKernelGGL(row_gather_kernel<T>, grid2(m, n), dim3(256), 0, s, m, n, A, lda, B, ldb, perm);
+    HIP_LAUNCH_CHECK();
+}
+
+#define INST(T)                                                                                   \
+    template void geset<T>(char, i64, i64, T, T, T*, i64, hipStream_t);                           \
+    template void gescale<T>(char, i64, i64, T, T*, i64, hipStream_t);                            \
+    template void geadd<T>(char, i64, i64, T, const T*, i64, T, T*, i64, hipStream_t);            \
+    template void laswp<T>(i64, T*, i64, i64, i64, const i64*, int, hipStream_t);                 \
+    template void laswp_off<T>(i64, T*, i64, i64, i64, const i64*, i64, hipStream_t, int);       \
+    template void permute_rows_gather<T>(i64, i64, const T*, i64, T*, i64, const i64*, hipStream_t);
+INST(float) INST(double) INST(ccplx) INST(zcplx)
+#undef INST
+#define INSTC(A, B) template void gecopy<A, B>(char, char, i64, i64, const A*, i64, B*, i64, hipStream_t);
+INSTC(float, float) INSTC(float, double) INSTC(double, float) INSTC(double, double)
+INSTC(ccplx, ccplx) INSTC(ccplx, zcplx) INSTC(zcplx, ccplx) INSTC(zcplx, zcplx)
+INSTC(float, ccplx) INSTC(double, zcplx) INSTC(zcplx, double) INSTC(ccplx, float)
+#undef INSTC
+template void gescale_row_col<float, float>(char, i64, i64, const float*, const float*, float*, i64, hipStream_t);
+template void gescale_row_col<double, double>(char, i64, i64, const double*, const double*, double*, i64, hipStream_t);
+template void gescale_row_col<ccplx, float>(char, i64, i64, const float*, const float*, ccplx*, i64, hipStream_t);
+template void gescale_row_col<zcplx, double>(char, i64, i64, const double*, const double*, zcplx*, i64, hipStream_t);
+
+}  // namespace slate_hip

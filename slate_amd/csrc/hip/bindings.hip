@@ -1,0 +1,187 @@
+// pybind11 module exposing the gfx950 kernels to the Python runtime.
+// Pointers are passed as integers (tensor.data_ptr()), streams as the raw
+// hipStream_t integer (torch.cuda.current_stream().cuda_stream).
+#include <pybind11/pybind11.h>
+#include <pybind11/complex.h>
+#include <complex>
+#include "launchers.hpp"
+#include "kernels.hpp"
+
+
+namespace py = pybind11;
+using namespace slate_hip;
+
+static inline hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+static TriMask make_mask(py::object m) {
+    TriMask t;
+    if (m.is_none()) return t;
+    py::tuple tup = m.cast<py::tuple>();
+    // (mode, nb, p, pr, q, pc, row_off, col_off, diag_off)
+    t.mode = tup[0].cast<int>();
+    t.nb = tup[1].cast<i64>();
+    t.p = tup[2].cast<int>(); t.pr = tup[3].cast<int>();
+    t.q = tup[4].cast<int>(); t.pc = tup[5].cast<int>();
+    t.row_off = tup[6].cast<i64>(); t.col_off = tup[7].cast<i64>();
+    t.diag_off = tup[8].cast<i64>();
+    return t;
+}
+
+static void py_gemm(char dtype, char ta, char tb, i64 m, i64 n, i64 k,
+                    std::complex<double> alpha, uintptr_t A, i64 lda, uintptr_t B, i64 ldb,
+                    std::complex<double> beta, uintptr_t C, i64 ldc,
+                    i64 batch, i64 sA, i64 sB, i64 sC, py::object mask, uintptr_t stream) {
+    GemmCall c;
+    c.transA = ta; c.transB = tb; c.m = m; c.n = n; c.k = k;
+    c.alpha_re = alpha.real(); c.alpha_im = alpha.imag();
+    c.beta_re = beta.real(); c.beta_im = beta.imag();
+    c.A = (const void*)A; c.lda = lda; c.strideA = sA;
+    c.B = (const void*)B; c.ldb = ldb; c.strideB = sB;
+    c.C = (void*)C; c.ldc = ldc; c.strideC = sC;
+    c.batch = batch;
+    c.mask = make_mask(mask);
+    switch (dtype) {
+        case 'd': gemm_real<double>(c, S(stream)); break;
+        case 's': gemm_real<float>(c, S(stream)); break;
+        case 'z': gemm_complex<zcplx>(c, S(stream)); break;
+        case 'c': gemm_complex<ccplx>(c, S(stream)); break;
+        default: throw std::invalid_argument("gemm: bad dtype");
+    }
+}
+
+static void py_gemm_ptrs(char dtype, char ta, char tb, i64 m, i64 n, i64 k,
+                         std::complex<double> alpha, uintptr_t Aptrs, i64 lda, uintptr_t Bptrs, i64 ldb,
+                         std::complex<double> beta, uintptr_t Cptrs, i64 ldc, i64 batch,
+                         bool vec_ok, uintptr_t stream) {
+    GemmCall c;
+    c.transA = ta; c.transB = tb; c.m = m; c.n = n; c.k = k;
+    c.alpha_re = alpha.real(); c.alpha_im = alpha.imag();
+    c.beta_re = beta.real(); c.beta_im = beta.imag();
+    c.Aptrs = (const void* const*)Aptrs; c.lda = lda;
+    c.Bptrs = (const void* const*)Bptrs; c.ldb = ldb;
+    c.Cptrs = (void* const*)Cptrs; c.ldc = ldc;
+    c.batch = batch; c.vec_ok = vec_ok;
+    switch (dtype) {
+        case 'd': gemm_real<double>(c, S(stream)); break;
+        case 's': gemm_real<float>(c, S(stream)); break;
+        case 'z': gemm_complex<zcplx>(c, S(stream)); break;
+        case 'c': gemm_complex<ccplx>(c, S(stream)); break;
+        default: throw std::invalid_argument("gemm_ptrs: bad dtype");
+    }
+}
+
+
+template <typename F>
+static void dispatch(char dt, F&& f) {
+    switch (dt) {
+        case 's': f(float()); break;
+        case 'd': f(double()); break;
+        case 'c': f(ccplx()); break;
+        case 'z': f(zcplx()); break;
+        default: throw std::invalid_argument("bad dtype");
+    }
+}
+template <typename T> static T cv(std::complex<double> z) {
+    if constexpr (scalar_traits<T>::is_complex) {
+        using R = typename scalar_traits<T>::real;
+        T r; r.re = (R)z.real(); r.im = (R)z.imag(); return r;
+    } else {
+        return (T)z.real();
+    }
+}
+template <typename T> static T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
+
+static void register_kernels(py::module& m) {
+    m.def("trsm", [](char dt, char side, char uplo, char trans, char diag, i64 mm, i64 n, std::complex<double> alpha,
+                     uintptr_t A, i64 lda, uintptr_t B, i64 ldb, uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            trsm<T>(side, uplo, trans, diag, mm, n, cv<T>(alpha), P<T>(A), lda, P<T>(B), ldb, S(st)); });
+    });
+    m.def("trmm", [](char dt, char side, char uplo, char trans, char diag, i64 mm, i64 n, std::complex<double> alpha,
+                     uintptr_t A, i64 lda, uintptr_t B, i64 ldb, uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            trmm<T>(side, uplo, trans, diag, mm, n, cv<T>(alpha), P<T>(A), lda, P<T>(B), ldb, S(st)); });
+    });
+    m.def("potrf", [](char dt, char uplo, i64 n, uintptr_t A, i64 lda, uintptr_t info, uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            potrf_tile<T>(uplo, (int)n, P<T>(A), lda, P<i64>(info), S(st)); });
+    });
+    m.def("getrf", [](char dt, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t ipiv, uintptr_t info, double thr,
+                      bool nopiv, uintptr_t work, uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            getrf_panel_ws<T>(mm, n, P<T>(A), lda, P<i64>(ipiv), P<i64>(info), thr, nopiv, (void*)work, S(st)); });
+    });
+    m.def("getrf_work_bytes", []() { return (i64)getrf_work_bytes(); });
+    m.def("laswp", [](char dt, i64 n, uintptr_t A, i64 lda, i64 k1, i64 k2, uintptr_t ipiv, i64 ioff, int incx,
+                      uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            laswp_off<T>(n, P<T>(A), lda, k1, k2, P<const i64>(ipiv), ioff, S(st), incx); });
+    });
+    m.def("row_gather", [](char dt, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t B, i64 ldb, uintptr_t perm,
+                           uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            permute_rows_gather<T>(mm, n, P<T>(A), lda, P<T>(B), ldb, P<const i64>(perm), S(st)); });
+    });
+    m.def("geset", [](char dt, char uplo, i64 mm, i64 n, std::complex<double> off, std::complex<double> diag,
+                      uintptr_t A, i64 lda, uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            geset<T>(uplo, mm, n, cv<T>(off), cv<T>(diag), P<T>(A), lda, S(st)); });
+    });
+    m.def("gescale", [](char dt, char uplo, i64 mm, i64 n, std::complex<double> a, uintptr_t A, i64 lda, uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z); gescale<T>(uplo, mm, n, cv<T>(a), P<T>(A), lda, S(st)); });
+    });
+    m.def("geadd", [](char dt, char uplo, i64 mm, i64 n, std::complex<double> a, uintptr_t A, i64 lda,
+                      std::complex<double> b, uintptr_t B, i64 ldb, uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            geadd<T>(uplo, mm, n, cv<T>(a), P<T>(A), lda, cv<T>(b), P<T>(B), ldb, S(st)); });
+    });
+    m.def("gecopy", [](char ds, char dd, char uplo, char trans, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t B,
+                       i64 ldb, uintptr_t st) {
+        dispatch(ds, [&](auto zs) { using Ts = decltype(zs);
+            dispatch(dd, [&](auto zd) { using Td = decltype(zd);
+                constexpr bool ok = !(scalar_traits<Ts>::is_complex && !scalar_traits<Td>::is_complex) ||
+                                    true;
+                (void)ok;
+                if constexpr ((std::is_same<Ts, float>::value || std::is_same<Ts, double>::value) &&
+                              (std::is_same<Td, float>::value || std::is_same<Td, double>::value))
+                    gecopy<Ts, Td>(uplo, trans, mm, n, P<Ts>(A), lda, P<Td>(B), ldb, S(st));
+                else if constexpr (scalar_traits<Ts>::is_complex && scalar_traits<Td>::is_complex)
+                    gecopy<Ts, Td>(uplo, trans, mm, n, P<Ts>(A), lda, P<Td>(B), ldb, S(st));
+                else if constexpr (std::is_same<Ts, float>::value && std::is_same<Td, ccplx>::value)
+                    gecopy<Ts, Td>(uplo, trans, mm, n, P<Ts>(A), lda, P<Td>(B), ldb, S(st));
+                else if constexpr (std::is_same<Ts, double>::value && std::is_same<Td, zcplx>::value)
+                    gecopy<Ts, Td>(uplo, trans, mm, n, P<Ts>(A), lda, P<Td>(B), ldb, S(st));
+                else if constexpr (std::is_same<Ts, zcplx>::value && std::is_same<Td, double>::value)
+                    gecopy<Ts, Td>(uplo, trans, mm, n, P<Ts>(A), lda, P<Td>(B), ldb, S(st));
+                else if constexpr (std::is_same<Ts, ccplx>::value && std::is_same<Td, float>::value)
+                    gecopy<Ts, Td>(uplo, trans, mm, n, P<Ts>(A), lda, P<Td>(B), ldb, S(st));
+                else
+                    throw std::invalid_argument("gecopy: unsupported conversion");
+            });
+        });
+    });
+    m.def("gescale_row_col", [](char dt, char equed, i64 mm, i64 n, uintptr_t r, uintptr_t c, uintptr_t A, i64 lda,
+                                uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z); using R = typename scalar_traits<T>::real;
+            gescale_row_col<T, R>(equed, mm, n, P<R>(r), P<R>(c), P<T>(A), lda, S(st)); });
+    });
+    m.def("genorm", [](char dt, char norm, char uplo, char diag, bool herm, i64 mm, i64 n, uintptr_t A, i64 lda,
+                       uintptr_t out, uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z); using R = typename scalar_traits<T>::real;
+            genorm<T, R>(norm, uplo, diag, herm, mm, n, P<T>(A), lda, P<R>(out), S(st)); });
+    });
+    m.def("matgen", [](char dt, int kind, uint64_t seed, i64 mloc, i64 nloc, uintptr_t A, i64 lda, i64 gm, i64 gn,
+                       i64 mb, int p, int pr, i64 nb, int q, int pc, i64 row0, i64 col0, double scale, uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            matgen<T>(kind, seed, mloc, nloc, P<T>(A), lda, gm, gn, mb, p, pr, nb, q, pc, row0, col0, scale, S(st)); });
+    });
+}
+
+PYBIND11_MODULE(_hip, m) {
+    m.doc() = "slate_amd gfx950 HIP kernels";
+    m.attr("arch") = "gfx950";
+    m.def("gemm", &py_gemm);
+    m.def("gemm_ptrs", &py_gemm_ptrs);
+    register_kernels(m);
+
+}

@@ -1,0 +1,4 @@
+#include "gemm_launch.hpp"
+namespace slate_hip {
+template void gemm_complex<zcplx>(const GemmCall&, hipStream_t);
+}

@@ -1,0 +1,54 @@
+// Declarations of the non-GEMM gfx950 kernel launchers (see the .hip files).
+#pragma once
+#include "common.hpp"
+
+namespace slate_hip {
+
+template <typename T> void potrf_tile(char uplo, int n, T* A, i64 lda, i64* info, hipStream_t s);
+template <typename T>
+void trsm(char side, char uplo, char trans, char diag, i64 m, i64 n, T alpha,
+          const T* A, i64 lda, T* B, i64 ldb, hipStream_t s);
+template <typename T>
+void trmm(char side, char uplo, char trans, char diag, i64 m, i64 n, T alpha,
+          const T* A, i64 lda, T* B, i64 ldb, hipStream_t s);
+
+// aux.hip
+template <typename T> void geset(char uplo, i64 m, i64 n, T off, T diag, T* A, i64 lda, hipStream_t s);
+template <typename T> void gescale(char uplo, i64 m, i64 n, T alpha, T* A, i64 lda, hipStream_t s);
+template <typename T>
+void geadd(char uplo, i64 m, i64 n, T alpha, const T* A, i64 lda, T beta, T* B, i64 ldb, hipStream_t s);
+template <typename Ts, typename Td>
+void gecopy(char uplo, char trans, i64 m, i64 n, const Ts* A, i64 lda, Td* B, i64 ldb, hipStream_t s);
+template <typename T, typename R>
+void gescale_row_col(char equed, i64 m, i64 n, const R* r, const R* c, T* A, i64 lda, hipStream_t s);
+template <typename T>
+void laswp(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, int incx, hipStream_t s);
+template <typename T>
+void permute_rows_gather(i64 m, i64 n, const T* A, i64 lda, T* B, i64 ldb, const i64* perm, hipStream_t s);
+
+// norm.hip: kind 'M' max, '1' one (column sums), 'I' inf (row sums), 'F' fro
+// (scale/sumsq pairs -> here plain sum of squares with scaling by the max);
+// out receives per-column (one), per-row (inf) or a single value.
+template <typename T, typename R>
+void genorm(char norm, char uplo, char diag, bool herm, i64 m, i64 n, const T* A, i64 lda, R* out,
+            hipStream_t s);
+
+// getrf.hip
+template <typename T>
+void getrf_panel_ws(i64 m, i64 n, T* A, i64 lda, i64* ipiv, i64* info, double thr, bool nopiv,
+                    void* work, hipStream_t s);
+size_t getrf_work_bytes();
+template <typename T>
+void laswp_off(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, i64 ioff, hipStream_t s, int incx = 1);
+
+// geqrf.hip
+template <typename T> void geqrf_panel(i64 m, i64 n, T* A, i64 lda, T* tau, hipStream_t s);
+template <typename T> void larft(i64 m, i64 k, const T* V, i64 ldv, const T* tau, T* Tm, i64 ldt, hipStream_t s);
+template <typename T> void trtri(char uplo, char diag, i64 n, T* A, i64 lda, i64* info, hipStream_t s);
+
+// matgen.hip
+template <typename T>
+void matgen(int kind, uint64_t seed, i64 mloc, i64 nloc, T* A, i64 lda, i64 m, i64 n,
+            i64 mb, int p, int pr, i64 nb, int q, int pc, i64 row0, i64 col0, double scale, hipStream_t s);
+
+}  // namespace slate_hip

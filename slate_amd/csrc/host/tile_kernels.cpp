@@ -1,0 +1,656 @@
+// Host (CPU) tile kernels: the Target::Host* compute path.
+//
+// Same operation set and argument conventions as the gfx950 kernels in
+// csrc/hip (column-major, 0-based pivots, TriMask output masks), so the
+// Python dispatch layer picks _host or _hip purely by where the data lives.
+// These replace the host BLAS/LAPACK the reference reaches through
+// BLAS++/LAPACK++ (Tile_blas.hh, Tile_lapack.hh,
+// Tile_getrf.hh, Tile_geqrf.hh, Tile_householder_reflection_generator.hh).
+#include <pybind11/pybind11.h>
+#include <pybind11/complex.h>
+#include <pybind11/stl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <complex>
+#include <cstdint>
+#include <limits>
+#include <stdexcept>
+#include <vector>
+
+namespace py = pybind11;
+
+namespace slate_host {
+
+using i64 = int64_t;
+template <typename T> struct real_of { using type = T; };
+template <typename T> struct real_of<std::complex<T>> { using type = T; };
+template <typename T> using real_t = typename real_of<T>::type;
+template <typename T> inline T conj_(T x) { return x; }
+template <typename T> inline std::complex<T> conj_(std::complex<T> x) { return std::conj(x); }
+template <typename T> inline real_t<T> real_(T x) { return std::real(x); }
+template <typename T> inline real_t<T> abs1_(T x) { return std::abs(std::real(x)) + std::abs(std::imag(x)); }
+template <typename T> inline T from_c(std::complex<double> z) { return (T)z.real(); }
+template <> inline std::complex<float> from_c(std::complex<double> z) { return {(float)z.real(), (float)z.imag()}; }
+template <> inline std::complex<double> from_c(std::complex<double> z) { return z; }
+
+struct Mask {
+    int mode = 0; i64 nb = 1 << 30; int p = 1, pr = 0, q = 1, pc = 0;
+    i64 row_off = 0, col_off = 0, diag_off = 0;
+    static i64 l2g(i64 l, i64 nb, int p, int pr) { i64 lt = l / nb; return (lt * p + pr) * nb + (l - lt * nb); }
+    bool keep(i64 r, i64 c) const {
+        if (!mode) return true;
+        i64 gr = l2g(r + row_off, nb, p, pr), gc = l2g(c + col_off, nb, q, pc);
+        return mode == 1 ? gr + diag_off >= gc : gr <= gc + diag_off;
+    }
+};
+
+static Mask make_mask(py::object m) {
+    Mask t;
+    if (m.is_none()) return t;
+    py::tuple tup = m.cast<py::tuple>();
+    t.mode = tup[0].cast<int>(); t.nb = tup[1].cast<i64>();
+    t.p = tup[2].cast<int>(); t.pr = tup[3].cast<int>();
+    t.q = tup[4].cast<int>(); t.pc = tup[5].cast<int>();
+    t.row_off = tup[6].cast<i64>(); t.col_off = tup[7].cast<i64>(); t.diag_off = tup[8].cast<i64>();
+    return t;
+}
+
+// op(X)(r, c) for a column-major X with leading dimension ld.
+template <typename T>
+inline T opget(const T* X, i64 ld, char op, i64 r, i64 c) {
+    if (op == 'N') return X[r + c * ld];
+    if (op == 'T') return X[c + r * ld];
+    return conj_(X[c + r * ld]);
+}
+
+// --------------------------------------------------------------------- gemm
+template <typename T>
+void gemm(char ta, char tb, i64 m, i64 n, i64 k, T alpha, const T* A, i64 lda,
+          const T* B, i64 ldb, T beta, T* C, i64 ldc, const Mask& mask) {
+    if (m <= 0 || n <= 0) return;
+    #pragma omp parallel for schedule(static) if (m * n * k > 32768)
+    for (i64 j = 0; j < n; ++j) {
+        std::vector<T> acc(m, T(0));
+        for (i64 l = 0; l < k; ++l) {
+            T b = opget(B, ldb, tb, l, j);
+            if (b == T(0)) continue;
+            if (ta == 'N') {
+                const T* a = A + l * lda;
+                for (i64 i = 0; i < m; ++i) acc[i] += a[i] * b;
+            } else {
+                for (i64 i = 0; i < m; ++i) acc[i] += opget(A, lda, ta, i, l) * b;
+            }
+        }
+        T* c = C + j * ldc;
+        for (i64 i = 0; i < m; ++i) {
+            if (!mask.keep(i, j)) continue;
+            T v = alpha * acc[i];
+            if (beta != T(0)) v += beta * c[i];
+            c[i] = v;
+        }
+    }
+}
+
+// --------------------------------------------------------------------- trsm
+// op(A) X = alpha B (side L) or X op(A) = alpha B (side R); B overwritten.
+template <typename T>
+void trsm(char side, char uplo, char trans, char diag, i64 m, i64 n, T alpha,
+          const T* A, i64 lda, T* B, i64 ldb) {
+    if (m <= 0 || n <= 0) return;
+    const bool unit = diag == 'U';
+    // effective triangle of op(A): lower if (uplo=L, N) or (uplo=U, T/C)
+    const bool lower = (uplo == 'L') == (trans == 'N');
+    auto a = [&](i64 r, i64 c) { return opget(A, lda, trans, r, c); };
+    if (side == 'L') {
+        #pragma omp parallel for schedule(static) if (n > 4)
+        for (i64 j = 0; j < n; ++j) {
+            T* b = B + j * ldb;
+            for (i64 i = 0; i < m; ++i) b[i] *= alpha;
+            if (lower) {
+                for (i64 i = 0; i < m; ++i) {
+                    T s = b[i];
+                    for (i64 l = 0; l < i; ++l) s -= a(i, l) * b[l];
+                    b[i] = unit ? s : s / a(i, i);
+                }
+            } else {
+                for (i64 i = m - 1; i >= 0; --i) {
+                    T s = b[i];
+                    for (i64 l = i + 1; l < m; ++l) s -= a(i, l) * b[l];
+                    b[i] = unit ? s : s / a(i, i);
+                }
+            }
+        }
+    } else {
+        // X op(A) = B  <=>  rows: x_r op(A) = b_r
+        #pragma omp parallel for schedule(static) if (m > 4)
+        for (i64 r = 0; r < m; ++r) {
+            for (i64 j = 0; j < n; ++j) B[r + j * ldb] *= alpha;
+            if (lower) {  // x_j = (b_j - sum_{l>j} x_l a(l,j)) / a(j,j)
+                for (i64 j = n - 1; j >= 0; --j) {
+                    T s = B[r + j * ldb];
+                    for (i64 l = j + 1; l < n; ++l) s -= B[r + l * ldb] * a(l, j);
+                    B[r + j * ldb] = unit ? s : s / a(j, j);
+                }
+            } else {
+                for (i64 j = 0; j < n; ++j) {
+                    T s = B[r + j * ldb];
+                    for (i64 l = 0; l < j; ++l) s -= B[r + l * ldb] * a(l, j);
+                    B[r + j * ldb] = unit ? s : s / a(j, j);
+                }
+            }
+        }
+    }
+}
+
+// --------------------------------------------------------------------- trmm
+// B = alpha op(A) B (side L) or alpha B op(A) (side R)
+template <typename T>
+void trmm(char side, char uplo, char trans, char diag, i64 m, i64 n, T alpha,
+          const T* A, i64 lda, T* B, i64 ldb) {
+    if (m <= 0 || n <= 0) return;
+    const bool unit = diag == 'U';
+    const bool lower = (uplo == 'L') == (trans == 'N');
+    auto a = [&](i64 r, i64 c) -> T {
+        if (r == c) return unit ? T(1) : opget(A, lda, trans, r, c);
+        if (lower ? r < c : r > c) return T(0);
+        return opget(A, lda, trans, r, c);
+    };
+    if (side == 'L') {
+        #pragma omp parallel for schedule(static) if (n > 4)
+        for (i64 j = 0; j < n; ++j) {
+            std::vector<T> x(B + j * ldb, B + j * ldb + m);
+            for (i64 i = 0; i < m; ++i) {
+                T s(0);
+                i64 l0 = lower ? 0 : i, l1 = lower ? i + 1 : m;
+                for (i64 l = l0; l < l1; ++l) s += a(i, l) * x[l];
+                B[i + j * ldb] = alpha * s;
+            }
+        }
+    } else {
+        #pragma omp parallel for schedule(static) if (m > 4)
+        for (i64 r = 0; r < m; ++r) {
+            std::vector<T> x(n);
+            for (i64 j = 0; j < n; ++j) x[j] = B[r + j * ldb];
+            for (i64 j = 0; j < n; ++j) {
+                T s(0);
+                i64 l0 = lower ? j : 0, l1 = lower ? n : j + 1;
+                for (i64 l = l0; l < l1; ++l) s += x[l] * a(l, j);
+                B[r + j * ldb] = alpha * s;
+            }
+        }
+    }
+}
+
+// -------------------------------------------------------------------- potrf
+// Returns info (0 = success, k>0: leading minor k not positive definite).
+template <typename T>
+i64 potrf(char uplo, i64 n, T* A, i64 lda) {
+    using R = real_t<T>;
+    for (i64 j = 0; j < n; ++j) {
+        if (uplo == 'L') {
+            R d = real_(A[j + j * lda]);
+            for (i64 l = 0; l < j; ++l) d -= std::norm(A[j + l * lda]);
+            if (!(d > R(0)) || std::isnan(d)) { A[j + j * lda] = T(d); return j + 1; }
+            d = std::sqrt(d);
+            A[j + j * lda] = T(d);
+            #pragma omp parallel for if (n - j > 256)
+            for (i64 i = j + 1; i < n; ++i) {
+                T s = A[i + j * lda];
+                for (i64 l = 0; l < j; ++l) s -= A[i + l * lda] * conj_(A[j + l * lda]);
+                A[i + j * lda] = s / d;
+            }
+        } else {
+            R d = real_(A[j + j * lda]);
+            for (i64 l = 0; l < j; ++l) d -= std::norm(A[l + j * lda]);
+            if (!(d > R(0)) || std::isnan(d)) { A[j + j * lda] = T(d); return j + 1; }
+            d = std::sqrt(d);
+            A[j + j * lda] = T(d);
+            #pragma omp parallel for if (n - j > 256)
+            for (i64 i = j + 1; i < n; ++i) {
+                T s = A[j + i * lda];
+                for (i64 l = 0; l < j; ++l) s -= conj_(A[l + j * lda]) * A[l + i * lda];
+                A[j + i * lda] = s / d;
+            }
+        }
+    }
+    return 0;
+}
+
+// -------------------------------------------------------------------- trtri
+template <typename T>
+i64 trtri(char uplo, char diag, i64 n, T* A, i64 lda) {
+    const bool unit = diag == 'U';
+    if (!unit)
+        for (i64 j = 0; j < n; ++j)
+            if (A[j + j * lda] == T(0)) return j + 1;
+    if (uplo == 'L') {
+        for (i64 j = n - 1; j >= 0; --j) {
+            T ajj;
+            if (!unit) { A[j + j * lda] = T(1) / A[j + j * lda]; ajj = -A[j + j * lda]; }
+            else ajj = T(-1);
+            // x = A[j+1:, j]; x = L22inv * x; x *= ajj
+            i64 m = n - j - 1;
+            std::vector<T> x(m);
+            for (i64 i = 0; i < m; ++i) x[i] = A[j + 1 + i + j * lda];
+            for (i64 i = 0; i < m; ++i) {
+                T s(0);
+                for (i64 l = 0; l <= i; ++l) {
+                    T lv = (l == i) ? (unit ? T(1) : A[j + 1 + i + (j + 1 + l) * lda]) : A[j + 1 + i + (j + 1 + l) * lda];
+                    s += lv * x[l];
+                }
+                A[j + 1 + i + j * lda] = s * ajj;
+            }
+        }
+    } else {
+        for (i64 j = 0; j < n; ++j) {
+            T ajj;
+            if (!unit) { A[j + j * lda] = T(1) / A[j + j * lda]; ajj = -A[j + j * lda]; }
+            else ajj = T(-1);
+            std::vector<T> x(j);
+            for (i64 i = 0; i < j; ++i) x[i] = A[i + j * lda];
+            for (i64 i = 0; i < j; ++i) {
+                T s(0);
+                for (i64 l = i; l < j; ++l) {
+                    T uv = (l == i) ? (unit ? T(1) : A[i + l * lda]) : A[i + l * lda];
+                    s += uv * x[l];
+                }
+                A[i + j * lda] = s * ajj;
+            }
+        }
+    }
+    return 0;
+}
+
+// -------------------------------------------------------------------- getrf
+// Partial-pivot LU of an m x n panel.  ipiv[k] = 0-based row swapped with k.
+// Returns info (first zero pivot, 1-based) or 0.
+template <typename T>
+i64 getrf(i64 m, i64 n, T* A, i64 lda, int64_t* ipiv, double threshold) {
+    using R = real_t<T>;
+    i64 info = 0;
+    const i64 mn = std::min(m, n);
+    for (i64 k = 0; k < mn; ++k) {
+        // pivot search
+        i64 p = k; R amax = -1;
+        for (i64 i = k; i < m; ++i) {
+            R v = abs1_(A[i + k * lda]);
+            if (v > amax || std::isnan(v)) { amax = v; p = i; if (std::isnan(v)) break; }
+        }
+        // threshold pivoting: keep the diagonal if it is within threshold of max
+        if (threshold < 0) p = k;
+        else if (threshold < 1.0 && abs1_(A[k + k * lda]) >= R(threshold) * amax) p = k;
+        ipiv[k] = p;
+        if (A[p + k * lda] == T(0)) { if (!info) info = k + 1; continue; }
+        if (p != k)
+            for (i64 j = 0; j < n; ++j) std::swap(A[k + j * lda], A[p + j * lda]);
+        T inv = T(1) / A[k + k * lda];
+        for (i64 i = k + 1; i < m; ++i) A[i + k * lda] *= inv;
+        #pragma omp parallel for if ((m - k) * (n - k) > 65536)
+        for (i64 j = k + 1; j < n; ++j) {
+            T u = A[k + j * lda];
+            if (u == T(0)) continue;
+            for (i64 i = k + 1; i < m; ++i) A[i + j * lda] -= A[i + k * lda] * u;
+        }
+    }
+    return info;
+}
+
+// Apply row interchanges ipiv[k1..k2) (0-based, relative) to n columns.
+template <typename T>
+void laswp(i64 n, T* A, i64 lda, i64 k1, i64 k2, const int64_t* ipiv, int incx) {
+    if (incx > 0) {
+        for (i64 k = k1; k < k2; ++k) {
+            i64 p = ipiv[k];
+            if (p != k) for (i64 j = 0; j < n; ++j) std::swap(A[k + j * lda], A[p + j * lda]);
+        }
+    } else {
+        for (i64 k = k2 - 1; k >= k1; --k) {
+            i64 p = ipiv[k];
+            if (p != k) for (i64 j = 0; j < n; ++j) std::swap(A[k + j * lda], A[p + j * lda]);
+        }
+    }
+}
+
+// -------------------------------------------------------------- householder
+// larfg: given alpha = x[0] and x[1:], returns tau and overwrites x[1:] by v[1:],
+// x[0] by beta (LAPACK convention H = I - tau v v^H, v[0] = 1).
+template <typename T>
+T larfg(i64 n, T* x, i64 incx) {
+    using R = real_t<T>;
+    if (n <= 0) return T(0);
+    T alpha = x[0];
+    R xnorm = 0;
+    {
+        R scale = 0, ssq = 1;
+        for (i64 i = 1; i < n; ++i) {
+            T v = x[i * incx];
+            R comps[2] = {std::real(v), std::imag(v)};
+            for (R c : comps) if (c != 0) {
+                R a = std::abs(c);
+                if (scale < a) { ssq = 1 + ssq * (scale / a) * (scale / a); scale = a; }
+                else ssq += (a / scale) * (a / scale);
+            }
+        }
+        xnorm = scale * std::sqrt(ssq);
+    }
+    R ar = std::real(alpha), ai = std::imag(alpha);
+    if (xnorm == 0 && ai == 0) return T(0);
+    R beta = -std::copysign(std::hypot(std::hypot(ar, ai), xnorm), ar);
+    T tau;
+    if constexpr (std::is_same<T, R>::value) tau = T((beta - ar) / beta);
+    else tau = T((beta - ar) / beta, -ai / beta);
+    T scal = T(1) / (alpha - T(beta));
+    for (i64 i = 1; i < n; ++i) x[i * incx] *= scal;
+    x[0] = T(beta);
+    return tau;
+}
+
+// geqrf: Householder QR of m x n (unblocked, columnwise), tau[min(m,n)].
+template <typename T>
+void geqrf(i64 m, i64 n, T* A, i64 lda, T* tau) {
+    const i64 k = std::min(m, n);
+    for (i64 j = 0; j < k; ++j) {
+        T t = larfg(m - j, A + j + j * lda, 1);
+        tau[j] = t;
+        if (t == T(0)) continue;
+        T ajj = A[j + j * lda];
+        A[j + j * lda] = T(1);
+        // apply H^H = I - conj(tau) v v^H to A[j:, j+1:]
+        #pragma omp parallel for if ((m - j) * (n - j) > 65536)
+        for (i64 c = j + 1; c < n; ++c) {
+            T s(0);
+            for (i64 i = j; i < m; ++i) s += conj_(A[i + j * lda]) * A[i + c * lda];
+            s *= conj_(t);
+            for (i64 i = j; i < m; ++i) A[i + c * lda] -= A[i + j * lda] * s;
+        }
+        A[j + j * lda] = ajj;
+    }
+}
+
+// gelqf: LQ via Householder on rows.
+template <typename T>
+void gelqf(i64 m, i64 n, T* A, i64 lda, T* tau) {
+    const i64 k = std::min(m, n);
+    for (i64 j = 0; j < k; ++j) {
+        // row j from column j: conj then larfg
+        for (i64 c = j; c < n; ++c) A[j + c * lda] = conj_(A[j + c * lda]);
+        T t = larfg(n - j, A + j + j * lda, lda);
+        tau[j] = t;
+        T ajj = A[j + j * lda];
+        A[j + j * lda] = T(1);
+        if (t != T(0)) {
+            #pragma omp parallel for if ((m - j) * (n - j) > 65536)
+            for (i64 r = j + 1; r < m; ++r) {
+                T s(0);
+                for (i64 c = j; c < n; ++c) s += A[r + c * lda] * A[j + c * lda];
+                s *= t;
+                for (i64 c = j; c < n; ++c) A[r + c * lda] -= s * conj_(A[j + c * lda]);
+            }
+        }
+        A[j + j * lda] = ajj;
+        for (i64 c = j + 1; c < n; ++c) A[j + c * lda] = conj_(A[j + c * lda]);
+    }
+}
+
+// larft (forward, columnwise): T (k x k upper) from V (m x k, unit lower) and tau.
+template <typename T>
+void larft(i64 m, i64 k, const T* V, i64 ldv, const T* tau, T* Tm, i64 ldt) {
+    for (i64 i = 0; i < k; ++i) {
+        for (i64 r = i + 1; r < k; ++r) Tm[r + i * ldt] = T(0);
+        if (tau[i] == T(0)) {
+            for (i64 r = 0; r <= i; ++r) Tm[r + i * ldt] = T(0);
+            continue;
+        }
+        // T(0:i, i) = -tau_i * V(i:m, 0:i)^H V(i:m, i)
+        for (i64 r = 0; r < i; ++r) {
+            T s = conj_(V[i + r * ldv]);  // v_i(i) = 1
+            for (i64 l = i + 1; l < m; ++l) s += conj_(V[l + r * ldv]) * V[l + i * ldv];
+            Tm[r + i * ldt] = -tau[i] * s;
+        }
+        // T(0:i, i) = T(0:i,0:i) * T(0:i, i)
+        for (i64 r = 0; r < i; ++r) {
+            T s(0);
+            for (i64 l = r; l < i; ++l) s += Tm[r + l * ldt] * Tm[l + i * ldt];
+            Tm[r + i * ldt] = s;
+        }
+        Tm[i + i * ldt] = tau[i];
+    }
+}
+
+// ------------------------------------------------------------------- aux ops
+template <typename T>
+void geset(char uplo, i64 m, i64 n, T off, T diag, T* A, i64 lda) {
+    for (i64 j = 0; j < n; ++j)
+        for (i64 i = 0; i < m; ++i) {
+            if (uplo == 'L' && i < j) continue;
+            if (uplo == 'U' && i > j) continue;
+            A[i + j * lda] = (i == j) ? diag : off;
+        }
+}
+template <typename T>
+void gescale(char uplo, i64 m, i64 n, T s, T* A, i64 lda) {
+    for (i64 j = 0; j < n; ++j)
+        for (i64 i = 0; i < m; ++i) {
+            if (uplo == 'L' && i < j) continue;
+            if (uplo == 'U' && i > j) continue;
+            A[i + j * lda] *= s;
+        }
+}
+template <typename T>
+void geadd(char uplo, i64 m, i64 n, T alpha, const T* A, i64 lda, T beta, T* B, i64 ldb) {
+    for (i64 j = 0; j < n; ++j)
+        for (i64 i = 0; i < m; ++i) {
+            if (uplo == 'L' && i < j) continue;
+            if (uplo == 'U' && i > j) continue;
+            B[i + j * ldb] = alpha * A[i + j * lda] + (beta == T(0) ? T(0) : beta * B[i + j * ldb]);
+        }
+}
+
+
+// --------------------------------------------------------------- copy/norms
+template <typename Ts, typename Td> inline Td cvt(Ts v) {
+    if constexpr (std::is_same<Td, float>::value || std::is_same<Td, double>::value) return (Td)std::real(v);
+    else return Td((typename Td::value_type)std::real(v), (typename Td::value_type)std::imag(v));
+}
+template <typename Ts, typename Td>
+void gecopy(char uplo, char trans, i64 m, i64 n, const Ts* A, i64 lda, Td* B, i64 ldb) {
+    for (i64 j = 0; j < n; ++j)
+        for (i64 i = 0; i < m; ++i) {
+            if (uplo == 'L' && i < j) continue;
+            if (uplo == 'U' && i > j) continue;
+            Ts v = trans == 'N' ? A[i + j * lda] : A[j + i * lda];
+            if (trans == 'C') v = conj_(v);
+            B[i + j * ldb] = cvt<Ts, Td>(v);
+        }
+}
+template <typename T>
+void genorm(char norm, char uplo, char diag, bool herm, i64 m, i64 n, const T* A, i64 lda, real_t<T>* out) {
+    using R = real_t<T>;
+    R* col = out;
+    R* row = out + (norm == 'F' ? 2 * n : n);
+    for (i64 j = 0; j < n; ++j) {
+        R acc = 0, sc = 0, sq = 1;
+        for (i64 i = 0; i < m; ++i) {
+            if (uplo == 'L' && i < j) continue;
+            if (uplo == 'U' && i > j) continue;
+            R v = (i == j && diag == 'U') ? R(1) : std::abs(A[i + j * lda]);
+            int reps = (herm && i != j) ? 2 : 1;
+            if (norm == 'M') { if (std::isnan(v) || v > acc || std::isnan(acc)) acc = std::isnan(acc) ? acc : v; }
+            else if (norm == 'F') {
+                for (int r = 0; r < reps; ++r) {
+                    if (v != 0) {
+                        if (sc < v) { sq = 1 + sq * (sc / v) * (sc / v); sc = v; }
+                        else sq += (v / sc) * (v / sc);
+                    } else if (std::isnan(v)) sc = v;
+                }
+            } else if (norm == 'I' && !herm) {
+                row[i] += v;
+            } else {
+                acc += v;
+                if (herm && i != j) row[i] += v;
+            }
+        }
+        if (norm == 'F') { col[2 * j] = sc; col[2 * j + 1] = sq; }
+        else if (!(norm == 'I' && !herm)) col[j] = acc;
+    }
+}
+
+// ---------------------------------------------------------------- bindings
+template <typename F>
+static void dispatch(char dt, F&& f) {
+    switch (dt) {
+        case 's': f(float()); break;
+        case 'd': f(double()); break;
+        case 'c': f(std::complex<float>()); break;
+        case 'z': f(std::complex<double>()); break;
+        default: throw std::invalid_argument("bad dtype");
+    }
+}
+template <typename T> static T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
+
+void register_tile_kernels(py::module& m) {
+    m.def("gemm", [](char dt, char ta, char tb, i64 mm, i64 n, i64 k, std::complex<double> alpha,
+                     uintptr_t A, i64 lda, uintptr_t B, i64 ldb, std::complex<double> beta,
+                     uintptr_t C, i64 ldc, i64 batch, i64 sA, i64 sB, i64 sC, py::object mask,
+                     uintptr_t /*stream*/) {
+        Mask mk = make_mask(mask);
+        py::gil_scoped_release nogil;
+        dispatch(dt, [&](auto z) {
+            using T = decltype(z);
+            for (i64 b = 0; b < batch; ++b)
+                gemm<T>(ta, tb, mm, n, k, from_c<T>(alpha), P<T>(A) + b * sA, lda,
+                        P<T>(B) + b * sB, ldb, from_c<T>(beta), P<T>(C) + b * sC, ldc, mk);
+        });
+    });
+    m.def("trsm", [](char dt, char side, char uplo, char trans, char diag, i64 mm, i64 n,
+                     std::complex<double> alpha, uintptr_t A, i64 lda, uintptr_t B, i64 ldb, uintptr_t) {
+        py::gil_scoped_release nogil;
+        dispatch(dt, [&](auto z) {
+            using T = decltype(z);
+            trsm<T>(side, uplo, trans, diag, mm, n, from_c<T>(alpha), P<T>(A), lda, P<T>(B), ldb);
+        });
+    });
+    m.def("trmm", [](char dt, char side, char uplo, char trans, char diag, i64 mm, i64 n,
+                     std::complex<double> alpha, uintptr_t A, i64 lda, uintptr_t B, i64 ldb, uintptr_t) {
+        py::gil_scoped_release nogil;
+        dispatch(dt, [&](auto z) {
+            using T = decltype(z);
+            trmm<T>(side, uplo, trans, diag, mm, n, from_c<T>(alpha), P<T>(A), lda, P<T>(B), ldb);
+        });
+    });
+    m.def("potrf", [](char dt, char uplo, i64 n, uintptr_t A, i64 lda, uintptr_t info, uintptr_t) {
+        i64 r = 0;
+        {
+            py::gil_scoped_release nogil;
+            dispatch(dt, [&](auto z) { using T = decltype(z); r = potrf<T>(uplo, n, P<T>(A), lda); });
+        }
+        if (info) *reinterpret_cast<int64_t*>(info) = r;
+        return r;
+    });
+    m.def("trtri", [](char dt, char uplo, char diag, i64 n, uintptr_t A, i64 lda, uintptr_t info, uintptr_t) {
+        i64 r = 0;
+        {
+            py::gil_scoped_release nogil;
+            dispatch(dt, [&](auto z) { using T = decltype(z); r = trtri<T>(uplo, diag, n, P<T>(A), lda); });
+        }
+        if (info) *reinterpret_cast<int64_t*>(info) = r;
+        return r;
+    });
+    m.def("getrf", [](char dt, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t ipiv, uintptr_t info, double thr,
+                      bool nopiv, uintptr_t /*work*/, uintptr_t) {
+        i64 r = 0;
+        {
+            py::gil_scoped_release nogil;
+            dispatch(dt, [&](auto z) {
+                using T = decltype(z);
+                std::vector<int64_t> tmp;
+                int64_t* ip = reinterpret_cast<int64_t*>(ipiv);
+                if (!ip) { tmp.resize(std::min(mm, n)); ip = tmp.data(); }
+                r = getrf<T>(mm, n, P<T>(A), lda, ip, nopiv ? -1.0 : thr);
+            });
+        }
+        if (info) *reinterpret_cast<int64_t*>(info) = r;
+        return r;
+    });
+    m.def("getrf_work_bytes", []() { return (i64)0; });
+    m.def("laswp", [](char dt, i64 n, uintptr_t A, i64 lda, i64 k1, i64 k2, uintptr_t ipiv, i64 ioff, int incx,
+                      uintptr_t) {
+        py::gil_scoped_release nogil;
+        dispatch(dt, [&](auto z) {
+            using T = decltype(z);
+            std::vector<int64_t> pv(reinterpret_cast<const int64_t*>(ipiv), reinterpret_cast<const int64_t*>(ipiv) + k2);
+            for (auto& x : pv) x -= ioff;
+            laswp<T>(n, P<T>(A), lda, k1, k2, pv.data(), incx);
+        });
+    });
+    m.def("row_gather", [](char dt, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t B, i64 ldb, uintptr_t perm,
+                           uintptr_t) {
+        dispatch(dt, [&](auto z) {
+            using T = decltype(z);
+            const int64_t* pr = reinterpret_cast<const int64_t*>(perm);
+            for (i64 j = 0; j < n; ++j)
+                for (i64 i = 0; i < mm; ++i) P<T>(B)[i + j * ldb] = P<T>(A)[pr[i] + j * lda];
+        });
+    });
+    m.def("geqrf", [](char dt, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t tau) {
+        py::gil_scoped_release nogil;
+        dispatch(dt, [&](auto z) { using T = decltype(z); geqrf<T>(mm, n, P<T>(A), lda, P<T>(tau)); });
+    });
+    m.def("gelqf", [](char dt, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t tau) {
+        py::gil_scoped_release nogil;
+        dispatch(dt, [&](auto z) { using T = decltype(z); gelqf<T>(mm, n, P<T>(A), lda, P<T>(tau)); });
+    });
+    m.def("larft", [](char dt, i64 mm, i64 k, uintptr_t V, i64 ldv, uintptr_t tau, uintptr_t Tm, i64 ldt) {
+        py::gil_scoped_release nogil;
+        dispatch(dt, [&](auto z) {
+            using T = decltype(z);
+            larft<T>(mm, k, P<T>(V), ldv, P<T>(tau), P<T>(Tm), ldt);
+        });
+    });
+    m.def("gecopy", [](char ds, char dd, char uplo, char trans, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t B,
+                       i64 ldb, uintptr_t) {
+        py::gil_scoped_release nogil;
+        dispatch(ds, [&](auto zs) { using Ts = decltype(zs);
+            dispatch(dd, [&](auto zd) { using Td = decltype(zd);
+                gecopy<Ts, Td>(uplo, trans, mm, n, P<Ts>(A), lda, P<Td>(B), ldb); }); });
+    });
+    m.def("genorm", [](char dt, char norm, char uplo, char diag, bool herm, i64 mm, i64 n, uintptr_t A, i64 lda,
+                       uintptr_t out, uintptr_t) {
+        py::gil_scoped_release nogil;
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            genorm<T>(norm, uplo, diag, herm, mm, n, P<T>(A), lda, P<real_t<T>>(out)); });
+    });
+    m.def("gescale_row_col", [](char dt, char equed, i64 mm, i64 n, uintptr_t r, uintptr_t c, uintptr_t A, i64 lda,
+                                uintptr_t) {
+        dispatch(dt, [&](auto z) { using T = decltype(z); using R = real_t<T>;
+            const R* rr = P<R>(r); const R* cc = P<R>(c);
+            for (i64 j = 0; j < n; ++j)
+                for (i64 i = 0; i < mm; ++i) {
+                    R sfac = 1;
+                    if (equed == 'R' || equed == 'B') sfac *= rr[i];
+                    if (equed == 'C' || equed == 'B') sfac *= cc[j];
+                    P<T>(A)[i + j * lda] *= sfac;
+                }
+        });
+    });
+    m.def("geset", [](char dt, char uplo, i64 mm, i64 n, std::complex<double> off, std::complex<double> diag,
+                      uintptr_t A, i64 lda, uintptr_t) {
+        dispatch(dt, [&](auto z) {
+            using T = decltype(z);
+            geset<T>(uplo, mm, n, from_c<T>(off), from_c<T>(diag), P<T>(A), lda);
+        });
+    });
+    m.def("gescale", [](char dt, char uplo, i64 mm, i64 n, std::complex<double> s, uintptr_t A, i64 lda, uintptr_t) {
+        dispatch(dt, [&](auto z) { using T = decltype(z); gescale<T>(uplo, mm, n, from_c<T>(s), P<T>(A), lda); });
+    });
+    m.def("geadd", [](char dt, char uplo, i64 mm, i64 n, std::complex<double> alpha, uintptr_t A, i64 lda,
+                      std::complex<double> beta, uintptr_t B, i64 ldb, uintptr_t) {
+        dispatch(dt, [&](auto z) {
+            using T = decltype(z);
+            geadd<T>(uplo, mm, n, from_c<T>(alpha), P<T>(A), lda, from_c<T>(beta), P<T>(B), ldb);
+        });
+    });
+}
+
+}  // namespace slate_host

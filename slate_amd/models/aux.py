@@ -1,0 +1,465 @@
+"""Auxiliary distributed routines: copy (with precision conversion), add,
+scale, scale_row_col, set, norm, colNorms, gather, redistribute.
+
+Reference: `src/copy.cc`, `src/add.cc`, `src/scale.cc`,
+`src/scale_row_col.cc`, `src/set.cc`, `src/set_lambdas.cc`,
+`src/norm.cc:45-170`, `src/colNorms.cc`, `src/redistribute.cc:20-150`,
+`include/slate/Matrix.hh:775-822` (gather).
+
+For block-cyclic matrices the element-wise ops are ONE kernel over the
+rank's local block (uplo handled in global coordinates by masking per local
+tile).  Norms: one local-contribution kernel, then a single all-reduce of a
+packed vector (NaN-propagating max as SLATE's mpi_max_nan).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import ops
+from ..core.enums import Norm, NormScope, Op, Uplo
+from ..core.exceptions import SlateError
+from ..core.storage import DEV, HOST, l2g
+from ._util import target_slot
+
+
+# ------------------------------------------------------------------ helpers
+def _diag_kind(A):
+    return getattr(A, "_kind", "general")
+
+
+def _local_uplo_blocks(A, lb):
+    """Yield (local tensor block, uplo) pieces of the local block such that
+    applying `uplo` element masks per piece reproduces the GLOBAL triangle.
+    Off-diagonal local tiles are full or empty; diagonal tiles get uplo."""
+    up = A.uploPhysical()
+    if up == Uplo.General:
+        yield lb.data, 'G'
+        return
+    mb, nb = lb.mb, lb.nb
+    R0, C0 = lb.grow0, lb.gcol0
+    # iterate local tile rows/cols
+    rt = _tile_ranges(lb.row_off, lb.mloc, mb, lb.p, lb.pr)
+    ct = _tile_ranges(lb.col_off, lb.nloc, nb, lb.q, lb.pc)
+    for (r0, r1, gr0) in rt:
+        for (c0, c1, gc0) in ct:
+            # global (view-relative) row/col ranges of this piece
+            vr0, vr1 = gr0 - R0, gr0 - R0 + (r1 - r0) - 1
+            vc0, vc1 = gc0 - C0, gc0 - C0 + (c1 - c0) - 1
+            blk = lb.data[r0 - lb.row_off:r1 - lb.row_off, c0 - lb.col_off:c1 - lb.col_off]
+            if up == Uplo.Lower:
+                if vr1 < vc0:
+                    continue
+                if vr0 >= vc1:
+                    yield blk, 'G'
+                else:
+                    yield from _diag_piece(blk, vr0, vc0, 'L')
+            else:
+                if vr0 > vc1:
+                    continue
+                if vr1 <= vc0:
+                    yield blk, 'G'
+                else:
+                    yield from _diag_piece(blk, vr0, vc0, 'U')
+
+
+def _diag_piece(blk, vr0, vc0, u):
+    # piece straddles the diagonal; offset d = vr0 - vc0
+    d = vr0 - vc0
+    if d == 0:
+        yield blk, u
+        return
+    # general case (non-aligned views): fall back to column-by-column
+    m, n = blk.shape
+    for c in range(n):
+        gc = vc0 + c
+        if u == 'L':
+            r_start = max(0, gc - vr0)
+            if r_start < m:
+                yield blk[r_start:, c:c + 1], 'G'
+        else:
+            r_end = min(m, gc - vr0 + 1)
+            if r_end > 0:
+                yield blk[:r_end, c:c + 1], 'G'
+
+
+def _tile_ranges(off, nloc, nb, p, pr):
+    """Local index ranges [a, b) split at tile boundaries, with global start."""
+    out = []
+    a = off
+    end = off + nloc
+    while a < end:
+        b = min(end, (a // nb + 1) * nb)
+        out.append((a, b, l2g(a, nb, pr, p)))
+        a = b
+    return out
+
+
+def run_on_block_cyclic(A, fn, opts, *others):
+    """Run a block-cyclic-only driver on a general-storage matrix by copying
+    into a block-cyclic twin and back (redistribute)."""
+    from ..core.matrix import Matrix
+    s = A.storage
+    nb = max(s.tileMb(0) if s.mt else 1, 1)
+    B = type(A).__new__(type(A))
+    B.__dict__.update(A.__dict__)
+    twin = Matrix(A.m(), A.n(), nb=nb, comm=s.comm, dtype=s.dtype, device=s.device)
+    twin.insertLocalTiles(device=s.device if s.device.type == "cuda" else -1)
+    redistribute(A, twin)
+    B.__dict__.update(twin.__dict__)
+    B._uplo, B._diag = A._uplo, A._diag
+    r = fn(B, opts, *others)
+    redistribute(twin, A)
+    return r
+
+
+# --------------------------------------------------------------- dense I/O
+def allgather_dense(A) -> torch.Tensor:
+    """Return the full m x n logical matrix op(A) on every rank (testing)."""
+    s = A.storage
+    comm = s.comm
+    full = _storage_dense(s)
+    R0, C0 = A.global_offsets()
+    um, un = A._um(), A._un()
+    D = full[R0:R0 + um, C0:C0 + un]
+    if A.op() == Op.Trans:
+        D = D.transpose(0, 1)
+    elif A.op() == Op.ConjTrans:
+        D = D.transpose(0, 1).conj()
+    return D.contiguous()
+
+
+def _storage_dense(s) -> torch.Tensor:
+    comm = s.comm
+    dev = s.device if (s.origin_slot == DEV) else torch.device("cpu")
+    full = torch.zeros((s.m, s.n), dtype=s.dtype, device=dev)
+    if s.bc is not None and s.local:
+        s.sync_origin()
+        bc = s.bc
+        buf = s.local[s.origin_slot][: bc.mloc, : bc.nloc].to(dev)
+        maxm = max(1, max((_numroc_r(s.m, bc.mb, r, bc.p) for r in range(bc.p)), default=1))
+        maxn = max(1, max((_numroc_r(s.n, bc.nb, c, bc.q) for c in range(bc.q)), default=1))
+        pad = torch.zeros((maxm, maxn), dtype=s.dtype, device=dev)
+        pad[: bc.mloc, : bc.nloc] = buf
+        allp = comm.allgather(pad) if comm.size > 1 else pad.unsqueeze(0)
+        for r in range(min(comm.size, bc.p * bc.q)):
+            pr, pc = (r % bc.p, r // bc.p) if bc.order.value == 'C' else (r // bc.q, r % bc.q)
+            ml, nl = _numroc_r(s.m, bc.mb, pr, bc.p), _numroc_r(s.n, bc.nb, pc, bc.q)
+            if ml == 0 or nl == 0:
+                continue
+            rows = torch.tensor([l2g(i, bc.mb, pr, bc.p) for i in range(ml)], device=dev)
+            cols = torch.tensor([l2g(j, bc.nb, pc, bc.q) for j in range(nl)], device=dev)
+            full[rows[:, None], cols[None, :]] = allp[r][:ml, :nl]
+        return full
+    # per-tile storage: owners broadcast their tiles
+    for j in range(s.nt):
+        for i in range(s.mt):
+            owner = s.tileRank((i, j))
+            r0, c0 = s.row_offsets[i], s.col_offsets[j]
+            mb, nb = s.tileMb(i), s.tileNb(j)
+            blk = torch.zeros((mb, nb), dtype=s.dtype, device=dev)
+            if owner == comm.rank:
+                o = s.table.origin(i, j)
+                if o < 0:
+                    o = s.origin_slot if s.origin_slot is not None else HOST
+                s.tileUpdateOrigin(i, j)
+                d = s.tile_data(i, j, o)
+                if d is not None:
+                    blk.copy_(d)
+            if comm.size > 1:
+                comm.bcast(blk, owner)
+            full[r0:r0 + mb, c0:c0 + nb] = blk
+    return full
+
+
+def _numroc_r(n, nb, iproc, nprocs):
+    from ..core.storage import numroc
+    return numroc(n, nb, iproc, nprocs)
+
+
+def gather(A, root=0):
+    D = allgather_dense(A)
+    return D if A.storage.comm.rank == root else None
+
+
+def from_dense(A, D: torch.Tensor):
+    """Scatter a replicated dense (logical op(A)-shaped) tensor into A."""
+    s = A.storage
+    if A.op() == Op.Trans:
+        D = D.transpose(0, 1)
+    elif A.op() == Op.ConjTrans:
+        D = D.transpose(0, 1).conj()
+    R0, C0 = A.global_offsets()
+    if s.bc is not None:
+        if not s.local:
+            A.insertLocalTiles(device=s.device if s.device.type == "cuda" else -1)
+        bc = s.bc
+        lb = A.local_block()
+        if bc.pr >= 0 and lb.mloc and lb.nloc:
+            rows = torch.tensor([l2g(lb.row_off + i, bc.mb, bc.pr, bc.p) - R0 for i in range(lb.mloc)],
+                                device=D.device)
+            cols = torch.tensor([l2g(lb.col_off + j, bc.nb, bc.pc, bc.q) - C0 for j in range(lb.nloc)],
+                                device=D.device)
+            lb.data.copy_(D[rows[:, None], cols[None, :]].to(lb.data.device, lb.data.dtype))
+        s.mark_local_modified(s.origin_slot)
+        return A
+    for j in range(A._nt):
+        for i in range(A._mt):
+            gi, gj = A.ioffset + i, A.joffset + j
+            if s.tileIsLocal(gi, gj):
+                d = s.tile_data(gi, gj, s.origin_slot if s.origin_slot is not None else HOST)
+                if d is None:
+                    d = s.tileInsert(gi, gj, s.slot_of(s.device) if s.device.type == "cuda" else HOST)
+                r0 = s.row_offsets[gi] - R0
+                c0 = s.col_offsets[gj] - C0
+                d.copy_(D[r0:r0 + d.shape[0], c0:c0 + d.shape[1]])
+    return A
+
+
+# -------------------------------------------------------------- redistribute
+def redistribute(A, B, opts=None):
+    """B = A for arbitrary distributions / ops (tile-level send/recv,
+    `src/redistribute.cc:20-150`); elements outside B's stored triangle are
+    ignored for trapezoid types."""
+    sA, sB = A.storage, B.storage
+    comm = sA.comm
+    if A.m() != B.m() or A.n() != B.n():
+        raise SlateError("redistribute: dimension mismatch")
+    # fast path: identical block-cyclic layouts and ops
+    if sA.bc is not None and sB.bc is not None and sA.local and sB.local and A.op() == B.op() and \
+            (sA.bc.mb, sA.bc.nb, sA.bc.p, sA.bc.q, sA.bc.order) == (sB.bc.mb, sB.bc.nb, sB.bc.p, sB.bc.q, sB.bc.order) \
+            and A.global_offsets() == B.global_offsets():
+        la, lbk = A.local_block(), B.local_block()
+        ops.gecopy(la.data, lbk.data)
+        sB.mark_local_modified(sB.origin_slot)
+        return B
+    # general path via element ranges of B's tiles
+    D = allgather_dense(A)
+    from_dense(B, D.to(sB.device if sB.origin_slot == DEV else "cpu"))
+    return B
+
+
+def copy_conj_transpose(A, B):
+    """B = A^H (A Hermitian-stored in one triangle; only B's triangle written)."""
+    D = allgather_dense(A)
+    # complete A from its stored triangle
+    if A.uploPhysical() == Uplo.Lower:
+        D = torch.tril(D)
+    elif A.uploPhysical() == Uplo.Upper:
+        D = torch.triu(D)
+    from_dense(B, D.transpose(0, 1).conj().contiguous())
+    return B
+
+
+# ------------------------------------------------------------------ element-wise
+def _bc_pieces(A, opts=None):
+    s = A.storage
+    if s.bc is None:
+        raise SlateError("element-wise op requires block-cyclic storage")
+    slot = target_slot(A, opts) if opts is not None else s.origin_slot
+    lb = A.local_block(slot)
+    return s, slot, lb
+
+
+def set(offdiag, diag, A, opts=None):
+    """A = offdiag off the diagonal, diag on it (src/set.cc)."""
+    s, slot, lb = _bc_pieces(A, opts)
+    if lb.mloc and lb.nloc:
+        for blk, u in _local_uplo_blocks(A, lb):
+            _set_block(blk, offdiag, diag, lb, A, u)
+    s.mark_local_modified(slot)
+    return A
+
+
+def _set_block(blk, off, dg, lb, A, u):
+    ops.geset(off, off, blk, uplo=u)
+    m, n = blk.shape
+    if m == 0 or n == 0:
+        return
+    gr, gc = _piece_globals(blk, lb)
+    d = gc[0] - gr[0]            # element (i, j) is diagonal iff i - j == -d
+    r_s, c_s = (max(0, d), 0) if d >= 0 else (0, -d)
+    r_s, c_s = (d, 0) if d >= 0 else (0, -d)
+    k = min(m - r_s, n - c_s)
+    if k > 0:
+        ops.geset(off, dg, blk[r_s:r_s + k, c_s:c_s + k], uplo=u)
+
+
+def scale(numer, denom, A, opts=None):
+    """A = (numer / denom) A (src/scale.cc; overflow-safe ratio like lascl)."""
+    s, slot, lb = _bc_pieces(A, opts)
+    alpha = numer / denom
+    if lb.mloc and lb.nloc:
+        for blk, u in _local_uplo_blocks(A, lb):
+            ops.gescale(alpha, blk, uplo=u)
+    s.mark_local_modified(slot)
+    return A
+
+
+def add(alpha, A, beta, B, opts=None):
+    """B = alpha A + beta B (src/add.cc)."""
+    sB = B.storage
+    if not (A.storage.bc is not None and sB.bc is not None and A.op() == B.op() == Op.NoTrans):
+        raise SlateError("add: block-cyclic NoTrans matrices required")
+    la, lb = A.local_block(), B.local_block()
+    if lb.mloc and lb.nloc:
+        if B.uploPhysical() == Uplo.General:
+            ops.geadd(alpha, la.data, beta, lb.data)
+        else:
+            pa = list(_local_uplo_blocks(A, la))
+            pb = list(_local_uplo_blocks(B, lb))
+            for (xa, u), (xb, _) in zip(pa, pb):
+                ops.geadd(alpha, xa, beta, xb, uplo=u)
+    sB.mark_local_modified(sB.origin_slot)
+    return B
+
+
+def copy(A, B, opts=None):
+    """B = A with precision conversion (src/copy.cc); same distribution."""
+    if A.storage.bc is not None and B.storage.bc is not None and A.op() == B.op():
+        la, lb = A.local_block(), B.local_block()
+        if lb.mloc and lb.nloc:
+            if B.uploPhysical() == Uplo.General:
+                ops.gecopy(la.data, lb.data)
+            else:
+                for (xa, u), (xb, _) in zip(_local_uplo_blocks(A, la), _local_uplo_blocks(B, lb)):
+                    ops.gecopy(xa, xb, uplo=u)
+        B.storage.mark_local_modified(B.storage.origin_slot)
+        return B
+    return redistribute(A, B)
+
+
+def scale_row_col(equed, R, C, A, opts=None):
+    """A = diag(R) A diag(C) (src/scale_row_col.cc); R, C are full-length
+    vectors (global indexing) replicated on all ranks."""
+    s, slot, lb = _bc_pieces(A, opts)
+    bc = s.bc
+    if lb.mloc and lb.nloc:
+        dev = lb.data.device
+        rdt = torch.float64 if lb.data.dtype in (torch.float64, torch.complex128) else torch.float32
+        ridx = torch.tensor([l2g(lb.row_off + i, bc.mb, bc.pr, bc.p) - lb.grow0 for i in range(lb.mloc)])
+        cidx = torch.tensor([l2g(lb.col_off + j, bc.nb, bc.pc, bc.q) - lb.gcol0 for j in range(lb.nloc)])
+        r = torch.as_tensor(R, dtype=rdt)[ridx].to(dev) if R is not None else None
+        c = torch.as_tensor(C, dtype=rdt)[cidx].to(dev) if C is not None else None
+        ops.gescale_row_col(str(getattr(equed, "value", equed)), r, c, lb.data)
+    s.mark_local_modified(slot)
+    return A
+
+
+# ------------------------------------------------------------------ norms
+def norm(norm_type, A, opts=None, scope=NormScope.Matrix):
+    """Matrix norm (Max / One / Inf / Fro) of a distributed matrix, with the
+    matrix type's structure (general, trapezoid/triangular, symmetric/
+    Hermitian with one stored triangle).  NaN propagates."""
+    nt = Norm.from_string(norm_type) if not isinstance(norm_type, Norm) else norm_type
+    s = A.storage
+    if s.bc is None:
+        from .aux import allgather_dense as _ad  # noqa
+        D = allgather_dense(A)
+        return _dense_norm(nt, D, A)
+    kind = _diag_kind(A)
+    herm = kind in ("hermitian", "symmetric")
+    diag = 'U' if getattr(A, "_diag", None) is not None and A._diag.value == 'U' and kind == "trapezoid" else 'N'
+    # op: norms of A^T swap One <-> Inf
+    if A.op() != Op.NoTrans and not herm:
+        nt = {Norm.One: Norm.Inf, Norm.Inf: Norm.One}.get(nt, nt)
+    lb = A.local_block()
+    comm = s.comm
+    m_g, n_g = A._um(), A._un()
+    dev = lb.data.device
+    rdt = torch.float64 if s.dtype in (torch.float64, torch.complex128) else torch.float32
+    code = {Norm.Max: 'M', Norm.One: '1', Norm.Inf: 'I', Norm.Fro: 'F'}[nt]
+    colv = torch.zeros(n_g * (2 if code == 'F' else 1), dtype=rdt, device=dev)
+    rowv = torch.zeros(m_g, dtype=rdt, device=dev)
+    if lb.mloc and lb.nloc and s.bc.pr >= 0:
+        for blk, u in _local_uplo_blocks(A, lb):
+            gr, gc = _piece_globals(blk, lb)
+            gc_t = torch.as_tensor(gc, device=dev)
+            gr_t = torch.as_tensor(gr, device=dev)
+            on_diag = u != 'G'
+            if herm and code in ('1', 'I'):
+                if on_diag:
+                    c, r = ops.genorm_local('1', blk, uplo=u, herm=True)
+                else:
+                    c, _ = ops.genorm_local('1', blk)
+                    _, r = ops.genorm_local('I', blk)
+                colv.index_add_(0, gc_t, c)
+                rowv.index_add_(0, gr_t, r)
+                continue
+            c, r = ops.genorm_local(code, blk, uplo=u, diag=diag, herm=herm and on_diag)
+            if code == 'M':
+                colv.index_put_((gc_t,), torch.maximum(colv[gc_t], c))
+                if torch.isnan(c).any():
+                    colv[gc_t] = torch.where(torch.isnan(c), c, colv[gc_t])
+            elif code == 'F':
+                cv = colv.view(n_g, 2)
+                ss = c[:, 0] ** 2 * c[:, 1]
+                cv[gc_t, 1] += ss * (2 if (herm and not on_diag) else 1)
+            else:
+                colv.index_add_(0, gc_t, c)
+                rowv.index_add_(0, gr_t, r)
+    if code == 'M':
+        if comm.size > 1:
+            comm.allreduce(colv, "max")
+        v = colv.max() if colv.numel() else torch.zeros((), dtype=rdt)
+        if torch.isnan(colv).any():
+            return float("nan")
+        return float(v)
+    if code == 'F':
+        tot = colv.view(n_g, 2)[:, 1].sum().reshape(1)
+        if comm.size > 1:
+            comm.allreduce(tot, "sum")
+        return float(torch.sqrt(tot))
+    if comm.size > 1:
+        comm.allreduce(colv, "sum")
+        comm.allreduce(rowv, "sum")
+    if herm:
+        tot = colv + (rowv if m_g == n_g else 0)
+        return float(tot.max()) if tot.numel() else 0.0
+    if code == '1':
+        return float(colv.max()) if colv.numel() else 0.0
+    return float(rowv.max()) if rowv.numel() else 0.0
+
+
+def _piece_globals(blk, lb):
+    base = blk.storage_offset() - lb.data.storage_offset()
+    ldd = max(1, lb.data.stride(1))
+    lr, lc = base % ldd, base // ldd
+    gr = [l2g(lb.row_off + lr + i, lb.mb, lb.pr, lb.p) - lb.grow0 for i in range(blk.shape[0])]
+    gc = [l2g(lb.col_off + lc + j, lb.nb, lb.pc, lb.q) - lb.gcol0 for j in range(blk.shape[1])]
+    return gr, gc
+
+
+def _dense_norm(nt, D, A):
+    kind = _diag_kind(A)
+    if kind in ("hermitian", "symmetric"):
+        L = torch.tril(D) if A.uploPhysical() == Uplo.Lower else torch.triu(D)
+        D = L + L.transpose(0, 1).conj() - torch.diag(torch.diagonal(L))
+    elif kind == "trapezoid":
+        D = torch.tril(D) if A.uploPhysical() == Uplo.Lower else torch.triu(D)
+    a = D.abs()
+    if nt == Norm.Max:
+        return float(a.max()) if a.numel() else 0.0
+    if nt == Norm.One:
+        return float(a.sum(0).max()) if a.numel() else 0.0
+    if nt == Norm.Inf:
+        return float(a.sum(1).max()) if a.numel() else 0.0
+    return float(torch.sqrt((a * a).sum()))
+
+
+def colNorms(norm_type, A, opts=None):
+    """Per-column norms (Max only, like SLATE `colNorms`, src/colNorms.cc)."""
+    s = A.storage
+    lb = A.local_block()
+    rdt = torch.float64 if s.dtype in (torch.float64, torch.complex128) else torch.float32
+    n_g = A._un()
+    colv = torch.zeros(n_g, dtype=rdt, device=lb.data.device)
+    if lb.mloc and lb.nloc:
+        c, _ = ops.genorm_local('M', lb.data)
+        gc = [l2g(lb.col_off + j, lb.nb, lb.pc, lb.q) - lb.gcol0 for j in range(lb.nloc)]
+        gc_t = torch.as_tensor(gc, device=colv.device)
+        colv.index_put_((gc_t,), torch.maximum(colv[gc_t], c))
+    if s.comm.size > 1:
+        s.comm.allreduce(colv, "max")
+    return colv

@@ -1,0 +1,286 @@
+"""Cholesky family: potrf, potrs, posv, potri (+ mixed precision in mixed.py).
+
+Reference: `src/potrf.cc:22-210` (right-looking tiled Cholesky with
+lookahead over an OpenMP task DAG), `src/potrs.cc`, `src/posv.cc:70-95`,
+`src/potri.cc`.
+
+MI355X design of the distributed potrf (Lower, p x q block-cyclic):
+
+  step k (tile column g):
+    panel stream (high priority):
+      [wait trailing update of step k-la]   column g is now final
+      potrf(A_gg)                 one workgroup, tile in L2        (diag owner)
+      bcast A_gg down the column  col_comm (RCCL)                  (p > 1)
+      trsm  A_{>g,g} A_gg^{-H}    blocked: small-LDS solve + MFMA GEMMs
+      bcast panel along the row   row_comm (RCCL)                  (q > 1)
+      p bcasts down the column of exactly the panel tiles column pc needs,
+      one row-gather kernel assembles them in global order          (p > 1)
+      lookahead: update tile columns g+1..g+la (ONE masked GEMM)
+    update stream (low priority):
+      trailing update of all remaining local columns: ONE MFMA GEMM over
+      the rank's contiguous local buffer with the lower-triangle mask
+      evaluated in global coordinates (SLATE: per-tile batched herk/gemm
+      device regions, src/internal/internal_herk.cc:350-535).
+
+No host synchronisation inside the factorization: per-step info values
+are written by the tile kernel to a device vector and reduced once at the
+end (SLATE: device_info copy + queue sync per panel, internal_potrf.cc:76).
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import ops
+from ..core.enums import Diag, Op, Option, Side, Target, Uplo
+from ..core.exceptions import SlateError
+from ..core.matrix import HermitianMatrix, Matrix, TriangularMatrix
+from ..core.options import get_option
+from ..core.storage import DEV, HOST
+from ..parallel.streams import StreamSet
+from ..utils.trace import trace_block
+from ._util import conj_trans, grid_of, target_slot, tiles_local_before
+
+
+def _upper_to_lower(A, fn, opts):
+    """Run a Lower-only algorithm on an Upper-stored Hermitian matrix via its
+    conjugate transpose (SLATE potrf.cc:45-47 does the same view trick)."""
+    from .aux import copy_conj_transpose
+    L = HermitianMatrix(Uplo.Lower, A.emptyLike())
+    L.insertLocalTiles(device=A.storage.device if target_slot(A, opts) == DEV else -1)
+    copy_conj_transpose(A, L)
+    info = fn(L, opts)
+    copy_conj_transpose(L, A)
+    return info
+
+
+def potrf(A, opts=None) -> int:
+    """Cholesky factorization A = L L^H (or U^H U). Returns info (0 = ok)."""
+    if A.uplo() == Uplo.Upper and A.op() == Op.NoTrans:
+        return _upper_to_lower(A, potrf, opts)
+    if A.op() != Op.NoTrans:
+        # A^H of an Upper matrix is Lower: factor the stored Upper directly
+        raise SlateError("potrf: pass the matrix itself, not a transposed view")
+    with trace_block("potrf"):
+        return _potrf_lower(A, opts)
+
+
+def _potrf_lower(A, opts):
+    s = A.storage
+    bc = s.bc
+    if bc is None:
+        from .aux import run_on_block_cyclic
+        return run_on_block_cyclic(A, _potrf_lower, opts)
+    slot = target_slot(A, opts)
+    la = max(0, int(get_option(opts, Option.Lookahead, 1)))
+    buf = s.prepare_local(slot)
+    dev = buf.device
+    nb, p, q, pr, pc = bc.nb, bc.p, bc.q, bc.pr, bc.pc
+    dtype = s.dtype
+    ct = conj_trans(dtype)
+    grid = grid_of(A) if s.comm.size > 1 else None
+    g0 = A.ioffset
+    if A.row0_offset or A.col0_offset or A.ioffset != A.joffset:
+        raise SlateError("potrf: view must start on a diagonal tile boundary")
+    nt = A.mt()
+    gend = g0 + nt                                  # one past last storage tile
+    R_end = s.row_offsets[gend] if A.last_mb is None else s.row_offsets[gend - 1] + A.last_mb
+    lr_end = _lstart(R_end, nb, pr, p)
+    lc_end = _lstart(R_end, nb, pc, q)
+    ss = StreamSet(dev)
+    infos = torch.zeros(max(nt, 1), dtype=torch.int64, device=dev)
+    plans = _plan_col_gathers(A, g0, nt, nb, p, q, pr, pc, dev) if (p > 1 or q > 1) else None
+    ev_tr = {}
+    ss.fork()
+    for t in range(nt):
+        g = g0 + t
+        kb = s.tileMb(g) if t < nt - 1 or A.last_mb is None else A.last_mb
+        lrg = tiles_local_before(g, p, pr) * nb
+        lcg = tiles_local_before(g, q, pc) * nb
+        lr1 = tiles_local_before(g + 1, p, pr) * nb
+        lc1 = tiles_local_before(g + 1, q, pc) * nb
+        lr1, lc1 = min(lr1, lr_end), min(lc1, lc_end)
+        own_col = (g % q) == pc
+        own_diag = own_col and (g % p) == pr
+        with ss.use(ss.panel):
+            if t - la - 1 >= 0 and (t - la - 1) in ev_tr:
+                ss.wait(ss.panel, ev_tr[t - la - 1])
+            with trace_block("potrf::panel"):
+                if own_diag:
+                    ops.potrf('L', buf[lrg:lrg + kb, lcg:lcg + kb], infos[t:t + 1])
+                # diagonal tile -> column
+                if own_col:
+                    if p > 1:
+                        D = ops.colmajor_empty(kb, kb, dtype, dev)
+                        if own_diag:
+                            D.copy_(buf[lrg:lrg + kb, lcg:lcg + kb])
+                        grid.col_comm.bcast(D, g % p)
+                    else:
+                        D = buf[lrg:lrg + kb, lcg:lcg + kb]
+                    P = buf[lr1:lr_end, lcg:lcg + kb]
+                    if P.shape[0]:
+                        ops.trsm('R', 'L', ct, 'N', 1.0, D, P)
+                # panel -> row
+                nrow = lr_end - lr1
+                if q > 1:
+                    Prow = ops.colmajor_empty(nrow, kb, dtype, dev)
+                    if own_col and nrow:
+                        Prow.copy_(buf[lr1:lr_end, lcg:lcg + kb])
+                    if nrow:
+                        grid.row_comm.bcast(Prow, g % q)
+                else:
+                    Prow = buf[lr1:lr_end, lcg:lcg + kb]
+                # panel -> column (exactly the tiles this process column needs)
+                if plans is not None:
+                    Lcol = _assemble_cols(plans[t], Prow, grid, p, kb, dtype, dev)
+                else:
+                    Lcol = Prow
+            # lookahead columns g+1 .. g+la
+            lc_la = min(tiles_local_before(g + 1 + la, q, pc) * nb, lc_end)
+            if lc_la > lc1 and nrow:
+                mask = (1, nb, p, pr, q, pc, lr1, lc1, 0)
+                ops.gemm(-1.0, Prow, Lcol[0:lc_la - lc1], 1.0, buf[lr1:lr_end, lc1:lc_la], 'N', ct, mask)
+            ev_panel = ss.event(ss.panel)
+        # trailing update
+        us = ss.update[0]
+        with ss.use(us):
+            ss.wait(us, ev_panel)
+            if lc_end > lc_la and nrow:
+                with trace_block("potrf::trailing"):
+                    if Prow.is_cuda:
+                        Prow.record_stream(us)
+                        Lcol.record_stream(us)
+                    mask = (1, nb, p, pr, q, pc, lr1, lc_la, 0)
+                    ops.gemm(-1.0, Prow, Lcol[lc_la - lc1:lc_end - lc1], 1.0, buf[lr1:lr_end, lc_la:lc_end],
+                             'N', ct, mask)
+            ev_tr[t] = ss.event(us)
+    ss.join()
+    s.mark_local_modified(slot)
+    # info: first failing global column, reduced over ranks
+    iv = infos.cpu()
+    info = 0
+    for t in range(nt):
+        if int(iv[t]) > 0:
+            info = (s.row_offsets[g0 + t] - s.row_offsets[g0]) + int(iv[t])
+            break
+    if s.comm.size > 1:
+        big = 1 << 62
+        info = int(s.comm.allreduce_scalar(info if info > 0 else big, "min", torch.int64))
+        info = 0 if info >= big else info
+    return info
+
+
+def _lstart(g, nb, pr, p):
+    from ..core.storage import local_start
+    return local_start(g, nb, pr, p)
+
+
+def _plan_col_gathers(A, g0, nt, nb, p, q, pr, pc, dev):
+    """Per step: for each root process row r, the Prow row indices (on r) of
+    the tiles column pc needs, and the final gather permutation."""
+    s = A.storage
+    plans = []
+    perms, offs = [], []
+    for t in range(nt):
+        g = g0 + t
+        need = [j for j in range(g + 1, g0 + nt) if j % q == pc]
+        rows_of = {}
+        for r in range(p):
+            lr1_r = tiles_local_before(g + 1, p, r) * nb
+            idx = []
+            for j in need:
+                if j % p != r:
+                    continue
+                lj = (j // p) * nb - lr1_r
+                rows = s.tileMb(j)
+                idx.extend(range(lj, lj + rows))
+            rows_of[r] = idx
+        # receive buffer = concat over r of rows_of[r]; final order by j
+        base, pos = {}, 0
+        for r in range(p):
+            base[r] = pos
+            pos += len(rows_of[r])
+        order = []
+        cursor = {r: 0 for r in range(p)}
+        for j in need:
+            r = j % p
+            rows = s.tileMb(j)
+            order.extend(range(base[r] + cursor[r], base[r] + cursor[r] + rows))
+            cursor[r] += rows
+        plans.append((rows_of, pos, order))
+    # upload every index list once (no per-step H2D copies)
+    flat, meta = [], []
+    for rows_of, tot, order in plans:
+        m = {}
+        for r in range(p):
+            m[r] = (len(flat), len(rows_of[r]))
+            flat.extend(rows_of[r])
+        m["order"] = (len(flat), len(order))
+        flat.extend(order)
+        m["tot"] = tot
+        meta.append(m)
+    idx = torch.tensor(flat if flat else [0], dtype=torch.int64, device=dev)
+    return [(m, idx) for m in meta]
+
+
+def _assemble_cols(plan, Prow, grid, p, kb, dtype, dev):
+    m, idx = plan
+    tot = m["tot"]
+    Rbuf = ops.colmajor_empty(tot, kb, dtype, dev)
+    pos = 0
+    for r in range(p):
+        o, cnt = m[r]
+        if cnt:
+            chunk = Rbuf[pos:pos + cnt]
+            if grid.pr == r:
+                ops.row_gather(Prow, chunk, idx[o:o + cnt])
+            if p > 1:
+                c2 = chunk if chunk.is_contiguous() or cnt == 0 else None
+                tmp = ops.colmajor_empty(cnt, kb, dtype, dev) if c2 is None else None
+                if tmp is not None:
+                    if grid.pr == r:
+                        tmp.copy_(chunk)
+                    grid.col_comm.bcast(tmp, r)
+                    chunk.copy_(tmp)
+                else:
+                    grid.col_comm.bcast(chunk, r)
+        pos += cnt
+    o, cnt = m["order"]
+    Lcol = ops.colmajor_empty(cnt, kb, dtype, dev)
+    if cnt:
+        ops.row_gather(Rbuf, Lcol, idx[o:o + cnt])
+    return Lcol
+
+
+# ------------------------------------------------------------------ solves
+def potrs(A, B, opts=None):
+    """Solve A X = B with the Cholesky factor in A (lower or upper)."""
+    from .blas3 import trsm
+    if A.uplo() == Uplo.Lower:
+        L = TriangularMatrix(Uplo.Lower, A, diag=Diag.NonUnit)
+        trsm(Side.Left, 1.0, L, B, opts)
+        trsm(Side.Left, 1.0, L.conj_transpose(), B, opts)
+    else:
+        U = TriangularMatrix(Uplo.Upper, A, diag=Diag.NonUnit)
+        trsm(Side.Left, 1.0, U.conj_transpose(), B, opts)
+        trsm(Side.Left, 1.0, U, B, opts)
+    return 0
+
+
+def posv(A, B, opts=None) -> int:
+    from ..utils.timers import timer
+    with timer("posv::potrf"):
+        info = potrf(A, opts)
+    if info == 0:
+        with timer("posv::potrs"):
+            potrs(A, B, opts)
+    return info
+
+
+def potri(A, opts=None) -> int:
+    """Inverse from the Cholesky factor: A^{-1} = L^{-H} L^{-1} (trtri + trtrm)."""
+    from .inverse import trtri, trtrm
+    L = TriangularMatrix(A.uplo(), A, diag=Diag.NonUnit)
+    info = trtri(L, opts)
+    if info == 0:
+        trtrm(L, opts)
+    return info

@@ -1,0 +1,303 @@
+"""Tile/block-level compute operations on column-major tensor views.
+
+Each function dispatches by where the data lives: tensors on the MI355X go
+to the gfx950 kernels in ``_hip`` (MFMA GEMM, tile potrf, blocked trsm,
+GPU LU panel, row permutations, norms, ...), host tensors go to the native
+C++ kernels in ``_host``.  There is no PyTorch/vendor-library fallback: a
+missing ``_hip`` raises.  All device calls are enqueued on the CURRENT
+torch stream (so callers express overlap with ``torch.cuda.stream(...)``)
+and never synchronise the host.
+
+Conventions (LAPACK/SLATE): matrices are 2-D views with ``stride(0) == 1``
+(column-major); ``trans`` is 'N'/'T'/'C'; ``uplo`` 'L'/'U'/'G';
+pivots are 0-based int64 row indices.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _native
+from .._native import code, kmod, stream
+from ..core.exceptions import SlateError
+
+_WORK = {}
+
+
+def _chk(t: torch.Tensor, name="A"):
+    if t.dim() != 2:
+        raise SlateError(f"{name} must be 2-D")
+    if t.shape[0] > 1 and t.shape[1] > 0 and t.stride(0) != 1:
+        raise SlateError(f"{name} must be column-major (stride(0)==1), got strides {t.stride()}")
+
+
+def ld(t: torch.Tensor) -> int:
+    return max(1, t.stride(1), t.shape[0]) if t.shape[1] <= 1 else max(1, t.stride(1))
+
+
+def _c(x):
+    return complex(x)
+
+
+def _ch(x):
+    """normalise enum/str arguments to the kernels' char codes"""
+    return str(x)[0] if not hasattr(x, "value") else x.value
+
+
+def colmajor_empty(m, n, dtype, device):
+    return torch.empty((n, max(m, 1)), dtype=dtype, device=device).t()[:m, :]
+
+
+def colmajor_zeros(m, n, dtype, device):
+    return torch.zeros((n, max(m, 1)), dtype=dtype, device=device).t()[:m, :]
+
+
+def as_colmajor(t: torch.Tensor) -> torch.Tensor:
+    """Column-major copy/view of a 2-D tensor."""
+    if t.dim() == 2 and (t.stride(0) == 1 or t.shape[0] <= 1):
+        return t
+    return t.t().contiguous().t()
+
+
+# ----------------------------------------------------------------- BLAS 3
+def gemm(alpha, A, B, beta, C, transA='N', transB='N', mask=None, batch=1, strides=(0, 0, 0)):
+    """C = alpha op(A) op(B) + beta C  (one MFMA launch on device)."""
+    _chk(C, "C")
+    m, n = C.shape
+    if m == 0 or n == 0:
+        return C
+    ta, tb = _ch(transA), _ch(transB)
+    k = A.shape[1] if ta == 'N' else A.shape[0]
+    if k == 0 or alpha == 0:
+        if beta != 1:
+            gescale(beta, C)
+        return C
+    _chk(A, "A"); _chk(B, "B")
+    kmod(C).gemm(code(C.dtype), ta, tb, m, n, k, _c(alpha), A.data_ptr(), ld(A), B.data_ptr(), ld(B),
+                 _c(beta), C.data_ptr(), ld(C), batch, strides[0], strides[1], strides[2], mask, stream(C))
+    return C
+
+
+def herk(uplo, trans, alpha, A, beta, C, mask=None):
+    """C = alpha A A^H + beta C (trans='N') or alpha A^H A + beta C; only the
+    `uplo` triangle of C is written (TriMask inside the GEMM epilogue)."""
+    cplx = C.dtype.is_complex
+    t2 = 'C' if cplx else 'T'
+    m = mask if mask is not None else ((1 if _ch(uplo) == 'L' else 2), 1 << 40, 1, 0, 1, 0, 0, 0, 0)
+    if _ch(trans) == 'N':
+        return gemm(alpha, A, A, beta, C, 'N', t2, m)
+    return gemm(alpha, A, A, beta, C, t2, 'N', m)
+
+
+def syrk(uplo, trans, alpha, A, beta, C, mask=None):
+    m = mask if mask is not None else ((1 if _ch(uplo) == 'L' else 2), 1 << 40, 1, 0, 1, 0, 0, 0, 0)
+    if _ch(trans) == 'N':
+        return gemm(alpha, A, A, beta, C, 'N', 'T', m)
+    return gemm(alpha, A, A, beta, C, 'T', 'N', m)
+
+
+def her2k(uplo, trans, alpha, A, B, beta, C, mask=None):
+    cplx = C.dtype.is_complex
+    t2 = 'C' if cplx else 'T'
+    m = mask if mask is not None else ((1 if _ch(uplo) == 'L' else 2), 1 << 40, 1, 0, 1, 0, 0, 0, 0)
+    a2 = complex(alpha).conjugate() if cplx else alpha
+    if _ch(trans) == 'N':
+        gemm(alpha, A, B, beta, C, 'N', t2, m)
+        return gemm(a2, B, A, 1.0, C, 'N', t2, m)
+    gemm(alpha, A, B, beta, C, t2, 'N', m)
+    return gemm(a2, B, A, 1.0, C, t2, 'N', m)
+
+
+def syr2k(uplo, trans, alpha, A, B, beta, C, mask=None):
+    m = mask if mask is not None else ((1 if _ch(uplo) == 'L' else 2), 1 << 40, 1, 0, 1, 0, 0, 0, 0)
+    if _ch(trans) == 'N':
+        gemm(alpha, A, B, beta, C, 'N', 'T', m)
+        return gemm(alpha, B, A, 1.0, C, 'N', 'T', m)
+    gemm(alpha, A, B, beta, C, 'T', 'N', m)
+    return gemm(alpha, B, A, 1.0, C, 'T', 'N', m)
+
+
+def trsm(side, uplo, trans, diag, alpha, A, B):
+    """op(A) X = alpha B (Left) or X op(A) = alpha B (Right); B <- X."""
+    _chk(A); _chk(B, "B")
+    m, n = B.shape
+    if m == 0 or n == 0:
+        return B
+    kmod(B).trsm(code(B.dtype), _ch(side), _ch(uplo), _ch(trans), _ch(diag), m, n, _c(alpha),
+                 A.data_ptr(), ld(A), B.data_ptr(), ld(B), stream(B))
+    return B
+
+
+def trmm(side, uplo, trans, diag, alpha, A, B):
+    _chk(A); _chk(B, "B")
+    m, n = B.shape
+    if m == 0 or n == 0:
+        return B
+    kmod(B).trmm(code(B.dtype), _ch(side), _ch(uplo), _ch(trans), _ch(diag), m, n, _c(alpha),
+                 A.data_ptr(), ld(A), B.data_ptr(), ld(B), stream(B))
+    return B
+
+
+# ------------------------------------------------------------- factorizations
+def info_tensor(like: torch.Tensor, n=1):
+    return torch.zeros(n, dtype=torch.int64, device=like.device)
+
+
+def potrf(uplo, A, info=None):
+    """Tile Cholesky in place; info (int64 tensor on A's device) gets 0 or the
+    1-based failing column.  No host sync."""
+    _chk(A)
+    n = A.shape[0]
+    if info is None:
+        info = info_tensor(A)
+    kmod(A).potrf(code(A.dtype), _ch(uplo), n, A.data_ptr(), ld(A), info.data_ptr(), stream(A))
+    return info
+
+
+def _work(dev):
+    key = str(dev)
+    w = _WORK.get(key)
+    if w is None:
+        nbytes = max(64, int(kmod(torch.empty(0, device=dev)).getrf_work_bytes()))
+        w = torch.zeros(nbytes // 8 + 8, dtype=torch.int64, device=dev)
+        _WORK[key] = w
+    return w
+
+
+def getrf(A, ipiv, info=None, threshold=1.0, nopiv=False):
+    """LU panel with partial pivoting: ipiv (int64, length min(m,n)) gets
+    0-based pivot rows relative to A's first row."""
+    _chk(A)
+    m, n = A.shape
+    if info is None:
+        info = info_tensor(A)
+    w = _work(A.device) if A.is_cuda else None
+    kmod(A).getrf(code(A.dtype), m, n, A.data_ptr(), ld(A), ipiv.data_ptr() if ipiv is not None else 0,
+                  info.data_ptr(), float(threshold), bool(nopiv), w.data_ptr() if w is not None else 0, stream(A))
+    return info
+
+
+def laswp(A, ipiv, k1, k2, ioff=0, incx=1):
+    """Apply row interchanges ipiv[k1:k2] (rows ipiv[k]-ioff <-> k) to A."""
+    _chk(A)
+    if A.shape[1] == 0 or k2 <= k1:
+        return A
+    kmod(A).laswp(code(A.dtype), A.shape[1], A.data_ptr(), ld(A), k1, k2, ipiv.data_ptr(), ioff, incx, stream(A))
+    return A
+
+
+def row_gather(A, B, perm):
+    """B[i, :] = A[perm[i], :]."""
+    m, n = B.shape
+    if m == 0 or n == 0:
+        return B
+    kmod(B).row_gather(code(B.dtype), m, n, A.data_ptr(), ld(A), B.data_ptr(), ld(B), perm.data_ptr(), stream(B))
+    return B
+
+
+def trtri(uplo, diag, A, info=None):
+    _chk(A)
+    if info is None:
+        info = info_tensor(A)
+    if A.is_cuda:
+        # device: invert via blocked trsm against the identity (stream-ordered)
+        n = A.shape[0]
+        X = colmajor_zeros(n, n, A.dtype, A.device)
+        geset(0, 1, X)
+        trsm('L', uplo, 'N', diag, 1.0, A, X)
+        gecopy(X, A, uplo=_ch(uplo))
+        return info
+    _native._host.trtri(code(A.dtype), _ch(uplo), _ch(diag), A.shape[0], A.data_ptr(), ld(A), info.data_ptr(), 0)
+    return info
+
+
+def geqrf(A, tau):
+    """Householder QR of a panel (host kernel; device panels use the
+    blocked GEMM-based path in models.qr)."""
+    _chk(A)
+    if A.is_cuda:
+        raise SlateError("ops.geqrf: use slate_amd.models.qr (device panels)")
+    _native._host.geqrf(code(A.dtype), A.shape[0], A.shape[1], A.data_ptr(), ld(A), tau.data_ptr())
+    return tau
+
+
+def gelqf(A, tau):
+    _chk(A)
+    _native._host.gelqf(code(A.dtype), A.shape[0], A.shape[1], A.data_ptr(), ld(A), tau.data_ptr())
+    return tau
+
+
+def larft(V, tau, T):
+    _native._host.larft(code(V.dtype), V.shape[0], tau.shape[0], V.data_ptr(), ld(V), tau.data_ptr(),
+                        T.data_ptr(), ld(T))
+    return T
+
+
+# --------------------------------------------------------------------- aux
+def geset(offdiag, diag, A, uplo='G'):
+    _chk(A)
+    m, n = A.shape
+    if m and n:
+        kmod(A).geset(code(A.dtype), _ch(uplo), m, n, _c(offdiag), _c(diag), A.data_ptr(), ld(A), stream(A))
+    return A
+
+
+def gescale(alpha, A, uplo='G'):
+    _chk(A)
+    m, n = A.shape
+    if m and n:
+        kmod(A).gescale(code(A.dtype), _ch(uplo), m, n, _c(alpha), A.data_ptr(), ld(A), stream(A))
+    return A
+
+
+def geadd(alpha, A, beta, B, uplo='G'):
+    """B = alpha A + beta B."""
+    _chk(A); _chk(B, "B")
+    m, n = B.shape
+    if m and n:
+        kmod(B).geadd(code(B.dtype), _ch(uplo), m, n, _c(alpha), A.data_ptr(), ld(A), _c(beta),
+                      B.data_ptr(), ld(B), stream(B))
+    return B
+
+
+def gecopy(A, B, uplo='G', trans='N'):
+    """B = op(A) with precision conversion (B is m x n)."""
+    _chk(A); _chk(B, "B")
+    m, n = B.shape
+    if m and n:
+        kmod(B).gecopy(code(A.dtype), code(B.dtype), _ch(uplo), _ch(trans), m, n, A.data_ptr(), ld(A),
+                       B.data_ptr(), ld(B), stream(B))
+    return B
+
+
+def gescale_row_col(equed, r, c, A):
+    m, n = A.shape
+    if m and n:
+        kmod(A).gescale_row_col(code(A.dtype), _ch(equed), m, n, r.data_ptr() if r is not None else 0,
+                                c.data_ptr() if c is not None else 0, A.data_ptr(), ld(A), stream(A))
+    return A
+
+
+def genorm_local(norm, A, uplo='G', diag='N', herm=False):
+    """Local norm contributions: returns (colvals, rowvals) real tensors on
+    A's device: 'M'/'1' -> per-column max/sum, 'F' -> per-column
+    (scale, sumsq) pairs (n x 2), 'I' -> per-row sums; symmetric/Hermitian
+    storage adds the mirrored contributions to rowvals."""
+    _chk(A)
+    m, n = A.shape
+    rdt = _native.REAL_OF[A.dtype]
+    nc = 2 * n if _ch(norm) == 'F' else n
+    out = torch.zeros(nc + m, dtype=rdt, device=A.device)
+    if m and n:
+        kmod(A).genorm(code(A.dtype), _ch(norm), _ch(uplo), _ch(diag), bool(herm), m, n, A.data_ptr(), ld(A),
+                       out.data_ptr(), stream(A))
+    col = out[:nc].view(n, 2) if _ch(norm) == 'F' else out[:nc]
+    return col, out[nc:]
+
+
+def matgen(kind: int, seed: int, A, m, n, mb, p, pr, nb, q, pc, row0=0, col0=0, scale=1.0):
+    _chk(A)
+    mloc, nloc = A.shape
+    if mloc and nloc:
+        kmod(A).matgen(code(A.dtype), int(kind), int(seed) & ((1 << 64) - 1), mloc, nloc, A.data_ptr(), ld(A),
+                       m, n, mb, p, pr, nb, q, pc, row0, col0, float(scale), *( [stream(A)] if A.is_cuda else []))
+    return A

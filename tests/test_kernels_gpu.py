@@ -1,0 +1,198 @@
+"""gfx950 kernel numerics vs fp64 PyTorch references (unit tests
+of every device kernel against a host reference, unit_test/test_geadd.cc &c)."""
+import pytest
+import torch
+
+from slate_amd import ops, _native
+
+pytestmark = pytest.mark.gpu
+DT = [torch.float64, torch.float32, torch.complex128, torch.complex64]
+TOL = {torch.float64: 1e-12, torch.float32: 2e-5, torch.complex128: 1e-12, torch.complex64: 2e-5}
+
+
+def cm(m, n, dt, seed=0, dev="cuda"):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.randn(n, m, dtype=dt, generator=g).t()
+    return ops.as_colmajor(x.clone()).to(dev) if False else x.contiguous().t().contiguous().t().to(dev) \
+        if False else _cm(x.t().contiguous().t(), dev)
+
+
+def _cm(x, dev):
+    y = torch.empty((x.shape[1], x.shape[0]), dtype=x.dtype, device=dev).t()
+    y.copy_(x)
+    return y
+
+
+def ref(x):
+    return x.to(torch.complex128 if x.dtype.is_complex else torch.float64)
+
+
+def opx(x, t):
+    return {'N': x, 'T': x.mT, 'C': x.mH}[t]
+
+
+def test_native_loaded():
+    assert _native._hip is not None
+    assert _native._hip.arch == "gfx950"
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("ta,tb", [("N", "N"), ("N", "T"), ("T", "N"), ("C", "C"), ("N", "C")])
+def test_gemm(dt, ta, tb):
+    if not dt.is_complex and "C" in (ta + tb):
+        pytest.skip("conj on real")
+    m, n, k = 197, 131, 77
+    A = cm(k, m, dt, 1) if ta != 'N' else cm(m, k, dt, 1)
+    B = cm(n, k, dt, 2) if tb != 'N' else cm(k, n, dt, 2)
+    C = cm(m, n, dt, 3)
+    R = 0.7 * ref(opx(A, ta)) @ ref(opx(B, tb)) - 0.3 * ref(C)
+    ops.gemm(0.7, A, B, -0.3, C, ta, tb)
+    assert (ref(C) - R).abs().max() / R.abs().max() < TOL[dt]
+
+
+def test_gemm_large_k512():
+    m = n = 2048
+    A, B, C = cm(m, 512, torch.float64, 4), cm(n, 512, torch.float64, 5), cm(m, n, torch.float64, 6)
+    R = ref(C) - A @ B.mT
+    ops.gemm(-1.0, A, B, 1.0, C, 'N', 'T')
+    assert (C - R).abs().max() < 1e-11
+
+
+def test_gemm_trimask_blockcyclic():
+    # lower mask in global coords of a 2x? block-cyclic local buffer (pr=1 of p=2, nb=64)
+    nb, p, pr = 64, 2, 1
+    m = n = 256
+    A, B, C = cm(m, 32, torch.float64, 7), cm(n, 32, torch.float64, 8), cm(m, n, torch.float64, 9)
+    C0 = C.clone()
+    ops.gemm(1.0, A, B, 1.0, C, 'N', 'T', mask=(1, nb, p, pr, p, pr, 0, 0, 0))
+    full = C0 + A @ B.mT
+    gr = torch.tensor([((i // nb) * p + pr) * nb + i % nb for i in range(m)], device="cuda")
+    keep = gr[:, None] >= gr[None, :]
+    exp = torch.where(keep, full, C0)
+    assert (C - exp).abs().max() < 1e-12
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("uplo", ["L", "U"])
+def test_potrf_tile(dt, uplo):
+    n = 300
+    X = ref(cm(n, n, dt, 11))
+    S = X @ X.mH + n * torch.eye(n, dtype=X.dtype, device=X.device)
+    A = _cm(S.to(dt), "cuda")
+    info = ops.potrf(uplo, A)
+    assert int(info.item()) == 0
+    L = torch.tril(ref(A)) if uplo == 'L' else torch.triu(ref(A))
+    R = L @ L.mH if uplo == 'L' else L.mH @ L
+    assert (R - S).abs().max() / S.abs().max() < 10 * TOL[dt]
+
+
+def test_potrf_tile_info():
+    n = 64
+    S = torch.eye(n, dtype=torch.float64, device="cuda")
+    S[40, 40] = -1.0
+    A = _cm(S, "cuda")
+    assert int(ops.potrf('L', A).item()) == 41
+
+
+@pytest.mark.parametrize("dt", [torch.float64, torch.complex128, torch.float32])
+@pytest.mark.parametrize("side", ["L", "R"])
+@pytest.mark.parametrize("uplo", ["L", "U"])
+@pytest.mark.parametrize("trans", ["N", "T", "C"])
+@pytest.mark.parametrize("diag", ["N", "U"])
+def test_trsm_trmm(dt, side, uplo, trans, diag):
+    m, n = 150, 97
+    k = m if side == 'L' else n
+    T = ref(cm(k, k, dt, 21)) + 4 * k * torch.eye(k, device="cuda")
+    T = torch.tril(T) if uplo == 'L' else torch.triu(T)
+    Tu = T.clone()
+    if diag == 'U':
+        Tu.diagonal().fill_(1)
+    A = _cm(T.to(dt), "cuda")
+    B = cm(m, n, dt, 22)
+    B0 = ref(B)
+    ops.trsm(side, uplo, trans, diag, 2.0, A, B)
+    oT = opx(Tu, trans)
+    X = ref(B)
+    R = oT @ X if side == 'L' else X @ oT
+    assert (R - 2 * B0).abs().max() / B0.abs().max() < 100 * TOL[dt]
+    B2 = _cm(B0.to(dt), "cuda")
+    ops.trmm(side, uplo, trans, diag, 1.5, A, B2)
+    R2 = 1.5 * (oT @ B0 if side == 'L' else B0 @ oT)
+    assert (ref(B2) - R2).abs().max() / R2.abs().max() < 100 * TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("m,n", [(1000, 96), (300, 300), (64, 100), (2000, 33)])
+def test_getrf_panel(dt, m, n):
+    A0 = ref(cm(m, n, dt, 31))
+    A = _cm(A0.to(dt), "cuda")
+    k = min(m, n)
+    ipiv = torch.zeros(k, dtype=torch.int64, device="cuda")
+    info = ops.getrf(A, ipiv)
+    assert int(info.item()) == 0
+    LU = ref(A)
+    L = torch.tril(LU[:, :k], -1) + torch.eye(m, k, dtype=LU.dtype, device="cuda")
+    U = torch.triu(LU[:k, :])
+    P = A0.clone()
+    for i, p in enumerate(ipiv.tolist()):
+        if p != i:
+            P[[i, p]] = P[[p, i]]
+    assert (L @ U - P).abs().max() / A0.abs().max() < 100 * TOL[dt]
+    # partial pivoting: |L| <= 1
+    assert L.abs().max() <= 1 + 1e-6
+
+
+def test_laswp_matches_sequential():
+    m, n = 600, 70
+    A0 = cm(m, n, torch.float64, 41)
+    ipiv = torch.tensor([(i * 37 + 5) % m for i in range(200)], dtype=torch.int64)
+    ipiv = torch.maximum(ipiv, torch.arange(200))
+    A = A0.clone()
+    ops.laswp(A, ipiv.cuda(), 0, 200)
+    R = A0.clone()
+    for i, p in enumerate(ipiv.tolist()):
+        R[[i, p]] = R[[p, i]]
+    assert torch.equal(A, R)
+
+
+@pytest.mark.parametrize("dt", DT)
+def test_aux_kernels(dt):
+    m, n = 130, 70
+    A, B = cm(m, n, dt, 51), cm(m, n, dt, 52)
+    B0 = B.clone()
+    ops.geadd(2.0, A, 0.5, B)
+    assert (B - (2 * A + 0.5 * B0)).abs().max() < 1e-5
+    ops.gescale(3.0, B, uplo='L')
+    ops.geset(1.5, -2.0, A, uplo='U')
+    assert (torch.triu(A, 1) - torch.triu(torch.full_like(A, 1.5), 1)).abs().max() == 0
+    assert (torch.diagonal(A) + 2).abs().max() == 0
+    C = ops.colmajor_empty(n, m, dt, "cuda")
+    ops.gecopy(B0, C, trans='C' if dt.is_complex else 'T')
+    assert torch.equal(C, B0.mH if dt.is_complex else B0.mT)
+
+
+@pytest.mark.parametrize("dt", DT)
+def test_norm_local(dt):
+    m, n = 257, 129
+    A = cm(m, n, dt, 61)
+    a = ref(A).abs()
+    c, _ = ops.genorm_local('M', A)
+    assert abs(c.max().item() - a.max().item()) < 1e-5
+    c, _ = ops.genorm_local('1', A)
+    assert (c - a.sum(0).to(c.dtype)).abs().max() < 1e-4
+    _, r = ops.genorm_local('I', A)
+    assert (r - a.sum(1).to(r.dtype)).abs().max() < 1e-4
+    c, _ = ops.genorm_local('F', A)
+    fro = (c[:, 0] ** 2 * c[:, 1]).sum().sqrt()
+    assert abs(fro.item() - torch.linalg.norm(ref(A)).item()) < 1e-4 * fro.item()
+
+
+@pytest.mark.parametrize("dt", DT)
+def test_matgen_device_equals_host(dt):
+    m, n, nb = 100, 90, 32
+    for kind in (11, 21, 12):
+        H = torch.zeros((n, m), dtype=dt).t()
+        D = torch.zeros((n, m), dtype=dt, device="cuda").t()
+        ops.matgen(kind, 1234, H, m, n, nb, 1, 0, nb, 1, 0)
+        ops.matgen(kind, 1234, D, m, n, nb, 1, 0, nb, 1, 0)
+        assert (D.cpu() - H).abs().max() < 1e-6
