@@ -111,6 +111,10 @@ static void register_kernels(py::module& m) {
         dispatch(dt, [&](auto z) { using T = decltype(z);
             getrf_panel_ws<T>(mm, n, P<T>(A), lda, P<i64>(ipiv), P<i64>(info), thr, nopiv, (void*)work, S(st)); });
     });
+    m.def("trtri", [](char dt, char uplo, char diag, i64 n, uintptr_t A, i64 lda, uintptr_t info, uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            trtri<T>(uplo, diag, n, P<T>(A), lda, P<i64>(info), S(st)); });
+    });
     m.def("getrf_work_bytes", []() { return (i64)getrf_work_bytes(); });
     m.def("laswp", [](char dt, i64 n, uintptr_t A, i64 lda, i64 k1, i64 k2, uintptr_t ipiv, i64 ioff, int incx,
                       uintptr_t st) {

@@ -59,6 +59,7 @@ struct GemmArgs {
     T* const* Cptrs;
     int vecA, vecB;          // 16-byte vector loads allowed
     int group_m;             // tile-order group size
+    int remap;               // XCD-chunked block order (off for triangular masks: keeps XCDs balanced)
     TriMask mask;
 };
 
@@ -152,7 +153,7 @@ gemm_real_kernel(GemmArgs<T> a) {
 
     const int gm = (int)((a.m + BM - 1) / BM), gn = (int)((a.n + BN - 1) / BN);
     const int nblk = gm * gn;
-    int lin = xcd_remap(blockIdx.x, nblk);
+    int lin = a.remap ? xcd_remap(blockIdx.x, nblk) : (int)blockIdx.x;
     // grouped ordering: GROUP block-rows swept column by column
     const int G = a.group_m;
     int grp = lin / (G * gn);
@@ -264,7 +265,7 @@ gemm_complex_kernel(GemmArgs<T> a) {
     else { A = a.A + batch * a.strideA; B = a.B + batch * a.strideB; C = a.C + batch * a.strideC; }
 
     const int gm = (int)((a.m + BM - 1) / BM), gn = (int)((a.n + BN - 1) / BN);
-    int lin = xcd_remap(blockIdx.x, gm * gn);
+    int lin = a.remap ? xcd_remap(blockIdx.x, gm * gn) : (int)blockIdx.x;
     const int G = a.group_m;
     int grp = lin / (G * gn), first = grp * G, gsz = min(gm - first, G);
     int inner = lin - grp * G * gn;

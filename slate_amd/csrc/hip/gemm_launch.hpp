@@ -54,6 +54,7 @@ void gemm_real(const GemmCall& c, hipStream_t s) {
     a.vecB = c.vec_ok && (c.ldb % VEC == 0) && (ptrs || (aligned16(c.B) && c.strideB % VEC == 0));
     a.group_m = 8;
     a.mask = c.mask;
+    a.remap = c.mask.mode == 0 ? 1 : 0;
     if (c.m <= 0 || c.n <= 0) return;
     dispatch_real<T>(c.transA != 'N', c.transB != 'N', ptrs, a, (int)c.batch, s);
 }
@@ -99,6 +100,7 @@ void gemm_complex(const GemmCall& c, hipStream_t s) {
     a.vecB = c.vec_ok && (c.ldb % VEC == 0) && (ptrs || (aligned16(c.B) && c.strideB % VEC == 0));
     a.group_m = 8;
     a.mask = c.mask;
+    a.remap = c.mask.mode == 0 ? 1 : 0;
     if (c.m <= 0 || c.n <= 0) return;
     if (ptrs) dispatch_cplx<T, true>(c.transA, c.transB, a, (int)c.batch, s);
     else dispatch_cplx<T, false>(c.transA, c.transB, a, (int)c.batch, s);

@@ -58,8 +58,10 @@ getrf_base_step(i64 m, int c0, int c1, int j, T* A, i64 lda, i64* ipiv, i64 ioff
             if (!uz) { l = s_div(l, u); A[i + (i64)pc * lda] = l; }
             for (int c = j; c < c1; ++c) A[i + (i64)c * lda] = s_sub(A[i + (i64)c * lda], s_mul(l, prow[c - pc]));
         }
-        // every wave drains its stores before the workgroup's release below
+        // every wave drains its stores before the workgroup's release below,
+        // and the arg-max pass (different row->thread map) sees them
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
     }
     if (j >= c1) return;   // final launch: elimination only
     // ---- local arg-max of column j over rows >= j

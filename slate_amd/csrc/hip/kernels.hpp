@@ -45,6 +45,7 @@ void laswp_off(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, i64 ioff, 
 template <typename T> void geqrf_panel(i64 m, i64 n, T* A, i64 lda, T* tau, hipStream_t s);
 template <typename T> void larft(i64 m, i64 k, const T* V, i64 ldv, const T* tau, T* Tm, i64 ldt, hipStream_t s);
 template <typename T> void trtri(char uplo, char diag, i64 n, T* A, i64 lda, i64* info, hipStream_t s);
+template <typename T> void tri_inv(char uplo, char diag, i64 n, const T* A, i64 lda, T* W, i64 ldw, hipStream_t s);
 
 // matgen.hip
 template <typename T>

@@ -1,0 +1,35 @@
+// Per-stream grow-only device workspaces for multi-kernel launchers
+// (trsm, trtri, potrf tile, getrf panel).  Reuse on the same stream is safe by
+// stream order; different streams get different buffers; growth frees the
+// old buffer stream-ordered.  Avoids a hipMallocAsync/hipFreeAsync pair per
+// call on the factorization critical path.
+#pragma once
+#include <mutex>
+#include <unordered_map>
+#include "common.hpp"
+
+namespace slate_hip {
+
+struct WsKey {
+    hipStream_t s; int slot;
+    bool operator==(const WsKey& o) const { return s == o.s && slot == o.slot; }
+};
+struct WsHash {
+    size_t operator()(const WsKey& k) const { return std::hash<void*>()((void*)k.s) ^ (size_t)k.slot * 7919; }
+};
+
+inline void* workspace(hipStream_t s, size_t bytes, int slot) {
+    static std::mutex mu;
+    static std::unordered_map<WsKey, std::pair<void*, size_t>, WsHash> cache;
+    std::lock_guard<std::mutex> g(mu);
+    auto& e = cache[WsKey{s, slot}];
+    if (e.second < bytes) {
+        if (e.first) HIP_CHECK(hipFreeAsync(e.first, s));
+        size_t nb = std::max(bytes, e.second * 2);
+        HIP_CHECK(hipMallocAsync(&e.first, nb, s));
+        e.second = nb;
+    }
+    return e.first;
+}
+
+}  // namespace slate_hip

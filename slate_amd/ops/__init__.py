@@ -198,15 +198,7 @@ def trtri(uplo, diag, A, info=None):
     _chk(A)
     if info is None:
         info = info_tensor(A)
-    if A.is_cuda:
-        # device: invert via blocked trsm against the identity (stream-ordered)
-        n = A.shape[0]
-        X = colmajor_zeros(n, n, A.dtype, A.device)
-        geset(0, 1, X)
-        trsm('L', uplo, 'N', diag, 1.0, A, X)
-        gecopy(X, A, uplo=_ch(uplo))
-        return info
-    _native._host.trtri(code(A.dtype), _ch(uplo), _ch(diag), A.shape[0], A.data_ptr(), ld(A), info.data_ptr(), 0)
+    kmod(A).trtri(code(A.dtype), _ch(uplo), _ch(diag), A.shape[0], A.data_ptr(), ld(A), info.data_ptr(), stream(A))
     return info
 
 

@@ -102,14 +102,14 @@ def test_potrf_tile_info():
 def test_trsm_trmm(dt, side, uplo, trans, diag):
     m, n = 150, 97
     k = m if side == 'L' else n
-    T = ref(cm(k, k, dt, 21)) + 4 * k * torch.eye(k, device="cuda")
+    T = ref(cm(k, k, dt, 21)) / k + 2 * torch.eye(k, device="cuda")
     T = torch.tril(T) if uplo == 'L' else torch.triu(T)
     Tu = T.clone()
     if diag == 'U':
         Tu.diagonal().fill_(1)
     A = _cm(T.to(dt), "cuda")
     B = cm(m, n, dt, 22)
-    B0 = ref(B)
+    B0 = ref(B).clone()
     ops.trsm(side, uplo, trans, diag, 2.0, A, B)
     oT = opx(Tu, trans)
     X = ref(B)
@@ -124,7 +124,7 @@ def test_trsm_trmm(dt, side, uplo, trans, diag):
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("m,n", [(1000, 96), (300, 300), (64, 100), (2000, 33)])
 def test_getrf_panel(dt, m, n):
-    A0 = ref(cm(m, n, dt, 31))
+    A0 = ref(cm(m, n, dt, 31)).clone()
     A = _cm(A0.to(dt), "cuda")
     k = min(m, n)
     ipiv = torch.zeros(k, dtype=torch.int64, device="cuda")
@@ -138,8 +138,9 @@ def test_getrf_panel(dt, m, n):
         if p != i:
             P[[i, p]] = P[[p, i]]
     assert (L @ U - P).abs().max() / A0.abs().max() < 100 * TOL[dt]
-    # partial pivoting: |L| <= 1
-    assert L.abs().max() <= 1 + 1e-6
+    # partial pivoting (cabs1 as LAPACK izamax): |re(l)| + |im(l)| <= 1
+    bound = 2.0 if L.is_complex() else 1.0   # cabs1 pivoting bounds |l| by sqrt(2) -> cabs1(l) <= 2
+    assert (L.real.abs() + (L.imag.abs() if L.is_complex() else 0)).max() <= bound + 1e-6
 
 
 def test_laswp_matches_sequential():
