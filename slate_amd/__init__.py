@@ -63,3 +63,38 @@ def chol_solve_using_factor(A, B, opts=None):
 
 def chol_inverse_using_factor(A, opts=None):
     return potri(A, opts)
+
+from .models.lu import (  # noqa: F401,E402
+    gesv, gesv_nopiv, getrf, getrf_nopiv, getrf_tntpiv, getri, getriOOP, getrs, getrs_nopiv, permute_rows)
+
+
+def lu_factor(A, pivots, opts=None):
+    return getrf(A, pivots, opts)
+
+
+def lu_factor_nopiv(A, opts=None):
+    return getrf_nopiv(A, opts)
+
+
+def lu_solve(A, B, opts=None):
+    return gesv(A, Pivots(), B, opts)
+
+
+def lu_solve_nopiv(A, B, opts=None):
+    return gesv_nopiv(A, B, opts)
+
+
+def lu_solve_using_factor(A, pivots, B, opts=None):
+    return getrs(A, pivots, B, opts)
+
+
+def lu_solve_using_factor_nopiv(A, B, opts=None):
+    return getrs_nopiv(A, B, opts)
+
+
+def lu_inverse_using_factor(A, pivots, opts=None):
+    return getri(A, pivots, opts)
+
+
+def lu_inverse_using_factor_out_of_place(A, pivots, B, opts=None):
+    return getriOOP(A, pivots, B, opts)

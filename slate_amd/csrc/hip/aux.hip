@@ -173,6 +173,14 @@ __global__ void row_gather_kernel(i64 m, i64 n, const T* A, i64 lda, T* B, i64 l
     for (i64 j = blockIdx.y; j < n; j += gridDim.y) B[i + j * ldb] = A[src + j * lda];
 }
 
+template <typename T>
+__global__ void row_scatter_kernel(i64 m, i64 n, const T* A, i64 lda, T* B, i64 ldb, const i64* perm) {
+    i64 i = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    const i64 dst = perm[i];
+    for (i64 j = blockIdx.y; j < n; j += gridDim.y) B[dst + j * ldb] = A[i + j * lda];
+}
+
 // ---------------------------------------------------------------------------
 template <typename T> void geset(char uplo, i64 m, i64 n, T off, T diag, T* A, i64 lda, hipStream_t s) {
     if (m <= 0 || n <= 0) return;
@@ -238,7 +246,15 @@ void permute_rows_gather(i64 m, i64 n, const T* A, i64 lda, T* B, i64 ldb, const
     HIP_LAUNCH_CHECK();
 }
 
+template <typename T>
+void permute_rows_scatter(i64 m, i64 n, const T* A, i64 lda, T* B, i64 ldb, const i64* perm, hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    hipLaunchKernelGGL(row_scatter_kernel<T>, grid2(m, n), dim3(256), 0, s, m, n, A, lda, B, ldb, perm);
+    HIP_LAUNCH_CHECK();
+}
+
 #define INST(T)                                                                                   \
+    template void permute_rows_scatter<T>(i64, i64, const T*, i64, T*, i64, const i64*, hipStream_t); \
     template void geset<T>(char, i64, i64, T, T, T*, i64, hipStream_t);                           \
     template void gescale<T>(char, i64, i64, T, T*, i64, hipStream_t);                            \
     template void geadd<T>(char, i64, i64, T, const T*, i64, T, T*, i64, hipStream_t);            \

@@ -126,6 +126,11 @@ static void register_kernels(py::module& m) {
         dispatch(dt, [&](auto z) { using T = decltype(z);
             permute_rows_gather<T>(mm, n, P<T>(A), lda, P<T>(B), ldb, P<const i64>(perm), S(st)); });
     });
+    m.def("row_scatter", [](char dt, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t B, i64 ldb, uintptr_t perm,
+                            uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            permute_rows_scatter<T>(mm, n, P<T>(A), lda, P<T>(B), ldb, P<const i64>(perm), S(st)); });
+    });
     m.def("geset", [](char dt, char uplo, i64 mm, i64 n, std::complex<double> off, std::complex<double> diag,
                       uintptr_t A, i64 lda, uintptr_t st) {
         dispatch(dt, [&](auto z) { using T = decltype(z);

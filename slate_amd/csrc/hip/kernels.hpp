@@ -24,6 +24,8 @@ void gescale_row_col(char equed, i64 m, i64 n, const R* r, const R* c, T* A, i64
 template <typename T>
 void laswp(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, int incx, hipStream_t s);
 template <typename T>
+void permute_rows_scatter(i64 m, i64 n, const T* A, i64 lda, T* B, i64 ldb, const i64* perm, hipStream_t s);
+template <typename T>
 void permute_rows_gather(i64 m, i64 n, const T* A, i64 lda, T* B, i64 ldb, const i64* perm, hipStream_t s);
 
 // norm.hip: kind 'M' max, '1' one (column sums), 'I' inf (row sums), 'F' fro

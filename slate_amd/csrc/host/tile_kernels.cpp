@@ -574,6 +574,15 @@ void register_tile_kernels(py::module& m) {
         return r;
     });
     m.def("getrf_work_bytes", []() { return (i64)0; });
+    m.def("row_scatter", [](char dt, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t B, i64 ldb, uintptr_t perm,
+                            uintptr_t) {
+        dispatch(dt, [&](auto z) {
+            using T = decltype(z);
+            const int64_t* pr = reinterpret_cast<const int64_t*>(perm);
+            for (i64 j = 0; j < n; ++j)
+                for (i64 i = 0; i < mm; ++i) P<T>(B)[pr[i] + j * ldb] = P<T>(A)[i + j * lda];
+        });
+    });
     m.def("laswp", [](char dt, i64 n, uintptr_t A, i64 lda, i64 k1, i64 k2, uintptr_t ipiv, i64 ioff, int incx,
                       uintptr_t) {
         py::gil_scoped_release nogil;

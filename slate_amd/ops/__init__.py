@@ -194,6 +194,15 @@ def row_gather(A, B, perm):
     return B
 
 
+def row_scatter(A, B, perm):
+    """B[perm[i], :] = A[i, :]."""
+    m, n = A.shape
+    if m == 0 or n == 0:
+        return B
+    kmod(B).row_scatter(code(B.dtype), m, n, A.data_ptr(), ld(A), B.data_ptr(), ld(B), perm.data_ptr(), stream(B))
+    return B
+
+
 def trtri(uplo, diag, A, info=None):
     _chk(A)
     if info is None:
