@@ -1,3 +1,5 @@
+#include <vector>
+#include <pybind11/stl.h>
 // pybind11 module exposing the gfx950 kernels to the Python runtime.
 // Pointers are passed as integers (tensor.data_ptr()), streams as the raw
 // hipStream_t integer (torch.cuda.current_stream().cuda_stream).
@@ -116,6 +118,16 @@ static void register_kernels(py::module& m) {
             trtri<T>(uplo, diag, n, P<T>(A), lda, P<i64>(info), S(st)); });
     });
     m.def("getrf_work_bytes", []() { return (i64)getrf_work_bytes(); });
+    m.def("geqrf", [](char dt, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t tau, uintptr_t Tm, i64 ldt,
+                      uintptr_t V, i64 ldv, uintptr_t work, uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            geqrf_panel_ws<T>(mm, n, P<T>(A), lda, P<T>(tau), P<T>(Tm), ldt, P<T>(V), ldv, (void*)work, S(st)); });
+    });
+    m.def("geqrf_work_bytes", []() { return (i64)geqrf_work_bytes(); });
+    m.def("v_explicit", [](char dt, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t V, i64 ldv, uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            v_explicit<T>(mm, n, P<T>(A), lda, P<T>(V), ldv, S(st)); });
+    });
     m.def("laswp", [](char dt, i64 n, uintptr_t A, i64 lda, i64 k1, i64 k2, uintptr_t ipiv, i64 ioff, int incx,
                       uintptr_t st) {
         dispatch(dt, [&](auto z) { using T = decltype(z);
@@ -186,11 +198,46 @@ static void register_kernels(py::module& m) {
     });
 }
 
+__global__ void placement_probe_kernel(unsigned* out) {
+    if (threadIdx.x == 0) {
+        unsigned hw = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));    // HW_REG_HW_ID
+        unsigned xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11));  // HW_REG_XCC_ID
+        out[2 * blockIdx.x] = hw;
+        out[2 * blockIdx.x + 1] = xcc;
+        // keep the block resident briefly so blocks spread over CUs
+        __builtin_amdgcn_s_sleep(127);
+    }
+}
+
 PYBIND11_MODULE(_hip, m) {
     m.doc() = "slate_amd gfx950 HIP kernels";
     m.attr("arch") = "gfx950";
     m.def("gemm", &py_gemm);
     m.def("gemm_ptrs", &py_gemm_ptrs);
     register_kernels(m);
-
+    // CU-masked streams: isolate latency-bound panel kernels from the bulk
+    // trailing-update GEMM (hipExtStreamCreateWithCUMask).  Returns the raw
+    // handle for torch.cuda.ExternalStream.
+    m.def("stream_create_cu_mask", [](int device, std::vector<uint32_t> mask) {
+        int old = 0;
+        HIP_CHECK(hipGetDevice(&old));
+        HIP_CHECK(hipSetDevice(device));
+        hipStream_t st;
+        HIP_CHECK(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+        HIP_CHECK(hipSetDevice(old));
+        return (uintptr_t)st;
+    });
+    m.def("stream_destroy", [](uintptr_t st) { HIP_CHECK(hipStreamDestroy((hipStream_t)st)); });
+    m.def("cu_count", [](int device) {
+        hipDeviceProp_t pr;
+        HIP_CHECK(hipGetDeviceProperties(&pr, device));
+        return pr.multiProcessorCount;
+    });
+    m.def("placement_probe", [](uintptr_t out, int nblocks, uintptr_t st) {
+        // raw (HW_ID, XCC_ID) register values of each block: maps CU-mask
+        // bits / block ids to XCDs and CUs
+        hipLaunchKernelGGL(placement_probe_kernel, dim3(nblocks), dim3(64), 0, (hipStream_t)st,
+                           reinterpret_cast<unsigned*>(out));
+        HIP_LAUNCH_CHECK();
+    });
 }

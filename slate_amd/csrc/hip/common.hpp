@@ -127,6 +127,8 @@ __device__ inline R wave_sum(R v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+__device__ inline zcplx wave_sum(zcplx v) { return zcplx{wave_sum(v.re), wave_sum(v.im)}; }
+__device__ inline ccplx wave_sum(ccplx v) { return ccplx{wave_sum(v.re), wave_sum(v.im)}; }
 template <typename R>
 __device__ inline R wave_max(R v) {
     #pragma unroll

@@ -5,15 +5,20 @@
 // Recursive (Toledo) on the panel columns so almost all flops are MFMA
 // GEMMs / blocked TRSMs:
 //     getrf(A) = getrf(A_left); laswp(A_right); trsm; gemm; getrf(A22); laswp(A_left)
-// Base case (<= 32 columns) is one launch per column over many workgroups:
-// each workgroup eliminates the previous column on its rows (rank-1 update
-// of the base block), takes a local arg-max of the new column, publishes
-// it with an agent-scope release + atomic ticket; the LAST arriving
-// workgroup (acquire) picks the global pivot (NaN wins, lowest index on
-// ties, optional threshold pivoting), records ipiv/info and swaps the two
-// rows inside the base block.  Kernel boundaries order the columns, so no
-// grid barrier / co-residency assumption is needed and the whole thing is
-// stream-ordered (graph-capturable, no host sync).
+//
+// Base case (<= 32 columns): one launch per column over many workgroups
+// and NO intra-kernel synchronisation (no fences, atomics or grid barriers;
+// release/acquire fences cost microseconds each on gfx950):
+//   launch j: every workgroup (a) reduces the per-workgroup arg-max
+//   partials that launch j-1 left in a parity buffer -> pivot p of column
+//   j-1 and the winning candidate row (also left there); (b) applies the
+//   row interchange j-1 <-> p on the rows it owns (the old row j-1 was saved
+//   by launch j-1, so no two workgroups read a row another one writes);
+//   (c) eliminates column j-1 on its rows with the whole row segment held in
+//   registers; (d) publishes its local arg-max of column j plus that row and
+//   (owner of row j) the current row j.
+// Kernel boundaries order the columns, so the panel is stream-ordered
+// (graph-capturable, no host sync, no co-residency assumption).
 #include "common.hpp"
 #include "kernels.hpp"
 #include "launchers.hpp"
@@ -22,127 +27,151 @@ namespace slate_hip {
 
 namespace {
 constexpr int NBB = 32;          // base-case width
-constexpr int WG_ROWS = 512;     // target rows per workgroup
+constexpr int NTH = 256;         // threads per workgroup (one row each)
 constexpr int MAXG = 512;        // max workgroups per base launch
 
-struct PanelWork {               // device workspace layout
-    unsigned int counter;
-    unsigned int pad;
+template <typename T>
+struct PanelBuf {                // one parity half of the device workspace
     double val[MAXG];
     i64 idx[MAXG];
+    T cand[MAXG][NBB];
+    T diag[NBB];
 };
+constexpr size_t PANEL_BYTES = 2 * sizeof(PanelBuf<zcplx>);
 }  // namespace
 
 template <typename T>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(NTH)
 getrf_base_step(i64 m, int c0, int c1, int j, T* A, i64 lda, i64* ipiv, i64 ioff, i64* info,
-                i64 info_off, PanelWork* w, double thr, bool nopiv) {
+                i64 info_off, void* work, double thr, bool nopiv) {
     using R = typename scalar_traits<T>::real;
-    __shared__ R sv[256];
-    __shared__ i64 si[256];
+    __shared__ R sv[NTH];
+    __shared__ i64 si[NTH];
+    __shared__ int sg[NTH];
     __shared__ T prow[NBB];
-    __shared__ int s_last;
-    const int G = gridDim.x;
+    __shared__ T drow[NBB];
+    PanelBuf<T>* pb = reinterpret_cast<PanelBuf<T>*>(work);
+    const int G = gridDim.x, g = blockIdx.x, tid = threadIdx.x;
     const i64 rows_per = (m + G - 1) / G;
-    const i64 r0 = (i64)blockIdx.x * rows_per, r1 = min(m, r0 + rows_per);
-    // ---- eliminate column j-1 (its pivot row j-1 already swapped in place)
+    const i64 r0 = (i64)g * rows_per, r1 = min(m, r0 + rows_per);
+    const int w = c1 - c0;
+    i64 p = -1;
+    const int pc = j - 1;
     if (j > c0) {
-        const int pc = j - 1;
-        if (threadIdx.x < c1 - pc) prow[threadIdx.x] = A[pc + (i64)(pc + threadIdx.x) * lda];
+        // ---- (a) pivot of column j-1 from launch j-1's partials
+        PanelBuf<T>& in = pb[pc & 1];
+        R best = R(-1); i64 bi = pc; int bg = -1;
+        if (!nopiv)
+            for (int q = tid; q < G; q += NTH) {
+                R v = (R)in.val[q]; i64 ix = in.idx[q];
+                if ((v != v && best == best) || v > best || (v == best && ix < bi)) { best = v; bi = ix; bg = q; }
+            }
+        sv[tid] = best; si[tid] = bi; sg[tid] = bg;
+        if (tid < w) drow[tid] = in.diag[tid];
         __syncthreads();
-        const T u = prow[0];
-        const bool uz = s_is_zero(u);
-        for (i64 i = r0 + threadIdx.x; i < r1; i += 256) {
-            if (i <= pc) continue;
-            T l = A[i + (i64)pc * lda];
-            if (!uz) { l = s_div(l, u); A[i + (i64)pc * lda] = l; }
-            for (int c = j; c < c1; ++c) A[i + (i64)c * lda] = s_sub(A[i + (i64)c * lda], s_mul(l, prow[c - pc]));
+        for (int o = NTH / 2; o > 0; o >>= 1) {
+            if (tid < o) {
+                R a = sv[tid], b = sv[tid + o];
+                i64 ia = si[tid], ib = si[tid + o];
+                bool take = (b != b && a == a) || b > a || (b == a && ib < ia);
+                if (take) { sv[tid] = b; si[tid] = ib; sg[tid] = sg[tid + o]; }
+            }
+            __syncthreads();
         }
-        // every wave drains its stores before the workgroup's release below,
-        // and the arg-max pass (different row->thread map) sees them
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        p = si[0];
+        int gw = sg[0];
+        if (nopiv || gw < 0) { p = pc; }
+        else if (thr < 1.0) {
+            R dj = s_abs1(drow[pc - c0]);
+            if (dj == dj && (double)dj >= thr * (double)sv[0]) p = pc;
+        }
+        if (tid < w) prow[tid] = (p == pc) ? drow[tid] : in.cand[gw][tid];
         __syncthreads();
+        if (g == 0 && tid == 0) {
+            if (ipiv) ipiv[pc] = p + ioff;
+            if (s_is_zero(prow[pc - c0]) && info)
+                atomicCAS(reinterpret_cast<unsigned long long*>(info), 0ull,
+                          (unsigned long long)(pc + 1 + info_off));
+        }
+        // ---- (b) interchange: new row pc = pivot row (owner of pc writes it)
+        if (pc >= r0 && pc < r1 && tid < w) A[pc + (i64)(c0 + tid) * lda] = prow[tid];
     }
-    if (j >= c1) return;   // final launch: elimination only
-    // ---- local arg-max of column j over rows >= j
-    R best = R(-1);
-    i64 bi = j;
-    if (!nopiv) {
-        for (i64 i = max(r0, (i64)j) + threadIdx.x; i < r1; i += 256) {
-            R v = s_abs1(A[i + (i64)j * lda]);
-            if (v > best || (v != v && best == best)) { best = v; bi = i; }
+    const bool last = j >= c1;
+    PanelBuf<T>& out = pb[j & 1];
+    R best = R(-1); i64 bi = j;
+    const T u = (j > c0) ? prow[pc - c0] : s_zero(T());
+    const bool uz = s_is_zero(u);
+    for (i64 i = r0 + tid; i < r1; i += NTH) {
+        if (j == c0) {   // first column of the block: arg-max only
+            if (i >= j && !nopiv) {
+                R v = s_abs1(A[i + (i64)j * lda]);
+                if (v > best || (v != v && best == best)) { best = v; bi = i; }
+            }
+            continue;
+        }
+        if (i <= pc) continue;
+        T a[NBB];
+        const bool isp = (j > c0) && i == p && p != pc;
+        if (isp) {
+            #pragma unroll
+            for (int c = 0; c < NBB; ++c) if (c < w) a[c] = drow[c];
+        } else {
+            #pragma unroll
+            for (int c = 0; c < NBB; ++c) if (c < w && c0 + c >= pc) a[c] = A[i + (i64)(c0 + c) * lda];
+        }
+        {
+            // ---- (c) eliminate column pc
+            // (runtime-indexed reads of a[] would demote it to scratch: the
+            // two scalars needed by position are re-read from cache/LDS)
+            T l = isp ? drow[pc - c0] : A[i + (i64)pc * lda];
+            if (!uz) l = s_div(l, u);
+            #pragma unroll
+            for (int c = 0; c < NBB; ++c) {
+                if (c0 + c == pc) a[c] = l;
+                if (c < w && c0 + c > pc) a[c] = s_sub(a[c], s_mul(l, prow[c]));
+            }
+            if (!last && !nopiv) {
+                T aj = isp ? drow[j - c0] : A[i + (i64)j * lda];
+                R v = s_abs1(s_sub(aj, s_mul(l, prow[j - c0])));
+                if (v > best || (v != v && best == best)) { best = v; bi = i; }
+            }
+            if (isp) {
+                #pragma unroll
+                for (int c = 0; c < NBB; ++c) if (c < w) A[i + (i64)(c0 + c) * lda] = a[c];
+            } else {
+                #pragma unroll
+                for (int c = 0; c < NBB; ++c) if (c < w && c0 + c >= pc) A[i + (i64)(c0 + c) * lda] = a[c];
+            }
         }
     }
-    sv[threadIdx.x] = best; si[threadIdx.x] = bi;
+    if (last) return;
+    // ---- (d) publish arg-max of column j, the candidate row, and row j
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    sv[tid] = best; si[tid] = bi;
     __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (threadIdx.x < o) {
-            R a = sv[threadIdx.x], b = sv[threadIdx.x + o];
-            i64 ia = si[threadIdx.x], ib = si[threadIdx.x + o];
+    for (int o = NTH / 2; o > 0; o >>= 1) {
+        if (tid < o) {
+            R a = sv[tid], b = sv[tid + o];
+            i64 ia = si[tid], ib = si[tid + o];
             bool take = (b != b && a == a) || b > a || (b == a && ib < ia);
-            if (take) { sv[threadIdx.x] = b; si[threadIdx.x] = ib; }
+            if (take) { sv[tid] = b; si[tid] = ib; }
         }
         __syncthreads();
     }
-    // (the reduction's barriers above ordered every wave's drained stores)
-    if (threadIdx.x == 0) {
-        w->val[blockIdx.x] = (double)sv[0];
-        w->idx[blockIdx.x] = si[0];
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        unsigned old = __hip_atomic_fetch_add(&w->counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = (old == (unsigned)G - 1);
+    const i64 b = si[0];
+    if (tid == 0) { out.val[g] = (double)sv[0]; out.idx[g] = b; }
+    if (tid < w) {
+        if (sv[0] >= R(0) || sv[0] != sv[0]) out.cand[g][tid] = A[b + (i64)(c0 + tid) * lda];
+        if (j >= r0 && j < r1) out.diag[tid] = A[j + (i64)(c0 + tid) * lda];
     }
-    __syncthreads();
-    if (!s_last) return;
-    // ---- last arriver: global pivot, record, swap rows inside the base block
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        double bv = -1; i64 bidx = j;
-        if (!nopiv) {
-            for (int g = 0; g < G; ++g) {
-                double v = __hip_atomic_load(&w->val[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                i64 ix = __hip_atomic_load(&w->idx[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((v != v && bv == bv) || v > bv || (v == bv && ix < bidx)) { bv = v; bidx = ix; }
-            }
-            if (thr < 1.0) {
-                double dj = (double)s_abs1(A[j + (i64)j * lda]);
-                if (dj >= thr * bv && dj == dj) bidx = j;
-            }
-        }
-        si[0] = bidx;
-        if (ipiv) ipiv[j] = bidx + ioff;
-        T pv = A[bidx + (i64)j * lda];
-        if (s_is_zero(pv) && info) {
-            unsigned long long* ip = reinterpret_cast<unsigned long long*>(info);
-            atomicCAS(ip, 0ull, (unsigned long long)(j + 1 + info_off));
-        }
-        w->counter = 0;
-    }
-    __syncthreads();
-    const i64 p = si[0];
-    if (p != j) {
-        for (int c = c0 + threadIdx.x; c < c1; c += 256) {
-            T a = A[j + (i64)c * lda], b = A[p + (i64)c * lda];
-            A[j + (i64)c * lda] = b; A[p + (i64)c * lda] = a;
-        }
-    }
-}
-
-template <typename T>
-__global__ void ipiv_add_kernel(i64 n, i64* ipiv, i64 d) {
-    i64 i = (i64)blockIdx.x * 256 + threadIdx.x;
-    if (i < n) ipiv[i] += d;
 }
 
 template <typename T>
 static void base(i64 m, int c0, int c1, T* A, i64 lda, i64* ipiv, i64 ioff, i64* info, i64 info_off,
-                 PanelWork* w, double thr, bool nopiv, hipStream_t s) {
-    int G = (int)std::min<i64>(MAXG, std::max<i64>(1, (m + WG_ROWS - 1) / WG_ROWS));
+                 void* w, double thr, bool nopiv, hipStream_t s) {
+    int G = (int)std::min<i64>(MAXG, std::max<i64>(1, (m + NTH - 1) / NTH));
     for (int j = c0; j <= c1; ++j)
-        hipLaunchKernelGGL(getrf_base_step<T>, dim3(G), dim3(256), 0, s, m, c0, c1, j, A, lda, ipiv, ioff,
+        hipLaunchKernelGGL(getrf_base_step<T>, dim3(G), dim3(NTH), 0, s, m, c0, c1, j, A, lda, ipiv, ioff,
                            info, info_off, w, thr, nopiv);
     HIP_LAUNCH_CHECK();
 }
@@ -162,7 +191,7 @@ static void gemm_T(char ta, char tb, i64 m, i64 n, i64 k, double alpha, const T*
 // (ioff = row offset of this sub-panel); laswp at this level subtracts ioff.
 
 template <typename T>
-static void rec(i64 m, i64 n, T* A, i64 lda, i64* ipiv, i64 ioff, i64* info, i64 info_off, PanelWork* w,
+static void rec(i64 m, i64 n, T* A, i64 lda, i64* ipiv, i64 ioff, i64* info, i64 info_off, void* w,
                 double thr, bool nopiv, hipStream_t s) {
     if (n <= NBB) {
         base<T>(m, 0, (int)n, A, lda, ipiv, ioff, info, info_off, w, thr, nopiv, s);
@@ -186,8 +215,7 @@ static void rec(i64 m, i64 n, T* A, i64 lda, i64* ipiv, i64 ioff, i64* info, i64
 template <typename T>
 void getrf_panel_ws(i64 m, i64 n, T* A, i64 lda, i64* ipiv, i64* info, double thr, bool nopiv,
                     void* work, hipStream_t s) {
-    PanelWork* w = reinterpret_cast<PanelWork*>(work);
-    HIP_CHECK(hipMemsetAsync(&w->counter, 0, sizeof(unsigned), s));
+    void* w = work;
     if (info) HIP_CHECK(hipMemsetAsync(info, 0, sizeof(i64), s));
     if (m <= 0 || n <= 0) return;
     const i64 k = std::min(m, n);
@@ -198,7 +226,7 @@ void getrf_panel_ws(i64 m, i64 n, T* A, i64 lda, i64* ipiv, i64* info, double th
     }
 }
 
-size_t getrf_work_bytes() { return sizeof(PanelWork); }
+size_t getrf_work_bytes() { return PANEL_BYTES; }
 
 #define INST(T) \
     template void getrf_panel_ws<T>(i64, i64, T*, i64, i64*, i64*, double, bool, void*, hipStream_t);

@@ -44,8 +44,11 @@ template <typename T>
 void laswp_off(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, i64 ioff, hipStream_t s, int incx = 1);
 
 // geqrf.hip
-template <typename T> void geqrf_panel(i64 m, i64 n, T* A, i64 lda, T* tau, hipStream_t s);
-template <typename T> void larft(i64 m, i64 k, const T* V, i64 ldv, const T* tau, T* Tm, i64 ldt, hipStream_t s);
+template <typename T>
+void geqrf_panel_ws(i64 m, i64 n, T* A, i64 lda, T* tau, T* Tm, i64 ldt, T* V, i64 ldv, void* work,
+                    hipStream_t s);
+size_t geqrf_work_bytes();
+template <typename T> void v_explicit(i64 m, i64 n, const T* A, i64 lda, T* V, i64 ldv, hipStream_t s);
 template <typename T> void trtri(char uplo, char diag, i64 n, T* A, i64 lda, i64* info, hipStream_t s);
 template <typename T> void tri_inv(char uplo, char diag, i64 n, const T* A, i64 lda, T* W, i64 ldw, hipStream_t s);
 

@@ -55,9 +55,20 @@ potrf_small_kernel(int n, T* __restrict__ A, i64 lda, i64* info, i64 info_off) {
     __shared__ T S[NS * LD];       // S[c * LD + r] = L(r, c)
     __shared__ int s_fail;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    for (int idx = tid; idx < n * n; idx += NT) {
-        int r = idx % n, c = idx / n;
-        if (r >= c) S[c * LD + r] = UPPER ? s_conj(A[c + (i64)r * lda]) : A[r + (i64)c * lda];
+    // 2-D thread map (no integer division), loads batched by unrolling
+    {
+        constexpr int CPI = NT / NS;           // columns per pass
+        const int r = tid % NS, cb = tid / NS;
+        if (UPPER) {
+            // row r of the stored upper triangle is column r of L
+            #pragma unroll 8
+            for (int c = cb; c < NS; c += CPI)
+                if (c < n && r < n && r >= c) S[c * LD + r] = s_conj(A[c + (i64)r * lda]);
+        } else {
+            #pragma unroll 8
+            for (int c = cb; c < NS; c += CPI)
+                if (c < n && r < n && r >= c) S[c * LD + r] = A[r + (i64)c * lda];
+        }
     }
     if (tid == 0) s_fail = 0;
     __syncthreads();
@@ -104,6 +115,9 @@ potrf_small_kernel(int n, T* __restrict__ A, i64 lda, i64* info, i64 info_off) {
         if (s_fail) break;
         // ---- (2) panel: x D^H = a, one row per thread
         const int r0 = k0 + kb, m = n - r0;
+        __shared__ T rdiag[IB];
+        if (tid < kb) rdiag[tid] = s_div(s_from_real(T(), 1), S[(k0 + tid) * LD + k0 + tid]);
+        __syncthreads();
         for (int i = tid; i < m; i += NT) {
             T x[IB];
             #pragma unroll
@@ -113,7 +127,7 @@ potrf_small_kernel(int n, T* __restrict__ A, i64 lda, i64* info, i64 info_off) {
                     #pragma unroll
                     for (int l = 0; l < IB; ++l)
                         if (l < j) sacc = s_sub(sacc, s_mul(x[l], s_conj(S[(k0 + l) * LD + k0 + j])));
-                    x[j] = s_div(sacc, S[(k0 + j) * LD + k0 + j]);
+                    x[j] = s_mul(sacc, rdiag[j]);
                 } else {
                     x[j] = s_zero(T());
                 }
@@ -161,12 +175,15 @@ potrf_small_kernel(int n, T* __restrict__ A, i64 lda, i64* info, i64 info_off) {
         }
         __syncthreads();
     }
-    for (int idx = tid; idx < n * n; idx += NT) {
-        int r = idx % n, c = idx / n;
-        if (r >= c) {
-            if (UPPER) A[c + (i64)r * lda] = s_conj(S[c * LD + r]);
-            else A[r + (i64)c * lda] = S[c * LD + r];
-        }
+    {
+        constexpr int CPI = NT / NS;
+        const int r = tid % NS, cb = tid / NS;
+        #pragma unroll 8
+        for (int c = cb; c < NS; c += CPI)
+            if (c < n && r < n && r >= c) {
+                if (UPPER) A[c + (i64)r * lda] = s_conj(S[c * LD + r]);
+                else A[r + (i64)c * lda] = S[c * LD + r];
+            }
     }
     if (tid == 0 && s_fail && info)
         atomicCAS(reinterpret_cast<unsigned long long*>(info), 0ull, (unsigned long long)(s_fail + info_off));

@@ -24,7 +24,6 @@ namespace slate_hip {
 namespace {
 constexpr int KB = 64;       // diagonal-block size of the inverse kernel
 constexpr int BIG = 1024;    // largest triangle inverted as a whole
-enum { WS_X = 0, WS_W = 1, WS_T = 2, WS_I = 3 };
 }
 
 // W(b) = inv(D_b) (INV) or D_b with the other triangle zeroed (unit diag
@@ -42,21 +41,26 @@ tri_diag_kernel(char uplo, bool unit, i64 n, const T* __restrict__ A, i64 lda, T
     const int kb = (int)min((i64)KB, n - k0);
     const bool lower = uplo == 'L';
     const int j = threadIdx.x;
-    for (int r = 0; r < KB; ++r) {
+    // coalesced: thread j reads row j of every column
+    for (int c = 0; c < KB; ++c) {
+        const int r = j;
         T v = s_zero(T());
-        if (r < kb && j < kb) {
-            bool in = lower ? r >= j : r <= j;
-            if (in) v = A[k0 + r + (k0 + j) * lda];
-            if (r == j && unit) v = s_from_real(T(), 1);
+        if (r < kb && c < kb) {
+            bool in = lower ? r >= c : r <= c;
+            if (in) v = A[k0 + r + (k0 + c) * lda];
+            if (r == c && unit) v = s_from_real(T(), 1);
         }
-        if (r == j && r >= kb) v = s_from_real(T(), 1);
-        L[r][j] = v;
+        if (r == c && r >= kb) v = s_from_real(T(), 1);
+        L[r][c] = v;
     }
+    __shared__ T dinv[KB];
+    __syncthreads();
+    dinv[j] = s_div(s_from_real(T(), 1), L[j][j]);
     __syncthreads();
     T* Wb = strip ? W + k0 : W + k0 + k0 * ldw;   // strip: kt x KB stack of blocks
     if (!INV) {
         if (j < kb)
-            for (int r = 0; r < kb; ++r) Wb[r + (i64)j * ldw] = L[r][j];
+            for (int c = 0; c < kb; ++c) Wb[j + (i64)c * ldw] = L[j][c];
         return;
     }
     if constexpr (scalar_traits<T>::is_complex) {
@@ -67,17 +71,18 @@ tri_diag_kernel(char uplo, bool unit, i64 n, const T* __restrict__ A, i64 lda, T
             for (int i = 0; i < KB; ++i) {
                 T sacc = (i == j) ? s_from_real(T(), 1) : s_zero(T());
                 for (int l = j; l < i; ++l) sacc = s_sub(sacc, s_mul(L[i][l], X[l][j]));
-                X[i][j] = (i < j) ? s_zero(T()) : s_div(sacc, L[i][i]);
+                X[i][j] = (i < j) ? s_zero(T()) : s_mul(sacc, dinv[i]);
             }
         } else {
             for (int i = KB - 1; i >= 0; --i) {
                 T sacc = (i == j) ? s_from_real(T(), 1) : s_zero(T());
                 for (int l = i + 1; l <= j; ++l) sacc = s_sub(sacc, s_mul(L[i][l], X[l][j]));
-                X[i][j] = (i > j) ? s_zero(T()) : s_div(sacc, L[i][i]);
+                X[i][j] = (i > j) ? s_zero(T()) : s_mul(sacc, dinv[i]);
             }
         }
+        __syncthreads();
         if (j < kb)
-            for (int r = 0; r < kb; ++r) Wb[r + (i64)j * ldw] = X[r][j];
+            for (int c = 0; c < kb; ++c) Wb[j + (i64)c * ldw] = X[j][c];
     } else {
         // column j of inv(L), column-oriented substitution, x in registers
         T x[KB];
@@ -86,7 +91,7 @@ tri_diag_kernel(char uplo, bool unit, i64 n, const T* __restrict__ A, i64 lda, T
         if (lower) {
             #pragma unroll
             for (int l = 0; l < KB; ++l) {
-                x[l] = s_div(x[l], L[l][l]);
+                x[l] = s_mul(x[l], dinv[l]);
                 const T xl = x[l];
                 #pragma unroll
                 for (int i = l + 1; i < KB; ++i) x[i] = s_sub(x[i], s_mul(L[i][l], xl));
@@ -94,17 +99,19 @@ tri_diag_kernel(char uplo, bool unit, i64 n, const T* __restrict__ A, i64 lda, T
         } else {
             #pragma unroll
             for (int l = KB - 1; l >= 0; --l) {
-                x[l] = s_div(x[l], L[l][l]);
+                x[l] = s_mul(x[l], dinv[l]);
                 const T xl = x[l];
                 #pragma unroll
                 for (int i = 0; i < l; ++i) x[i] = s_sub(x[i], s_mul(L[i][l], xl));
             }
         }
-        if (j < kb) {
-            #pragma unroll
-            for (int r = 0; r < KB; ++r)
-                if (r < kb) Wb[r + (i64)j * ldw] = x[r];
-        }
+        // transpose through LDS for a coalesced store
+        __syncthreads();
+        #pragma unroll
+        for (int r = 0; r < KB; ++r) L[r][j] = x[r];
+        __syncthreads();
+        if (j < kb)
+            for (int c = 0; c < kb; ++c) Wb[j + (i64)c * ldw] = L[j][c];
     }
 }
 

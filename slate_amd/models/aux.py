@@ -277,13 +277,29 @@ def _set_block(blk, off, dg, lb, A, u):
     m, n = blk.shape
     if m == 0 or n == 0:
         return
+    # the global diagonal crosses a block-cyclic local block in runs (one per
+    # diagonal tile it owns): find them and set each run's square
+    for (i0, j0, k) in _diag_runs(blk, lb):
+        ops.geset(off, dg, blk[i0:i0 + k, j0:j0 + k], uplo=u)
+
+
+def _diag_runs(blk, lb):
     gr, gc = _piece_globals(blk, lb)
-    d = gc[0] - gr[0]            # element (i, j) is diagonal iff i - j == -d
-    r_s, c_s = (max(0, d), 0) if d >= 0 else (0, -d)
-    r_s, c_s = (d, 0) if d >= 0 else (0, -d)
-    k = min(m - r_s, n - c_s)
-    if k > 0:
-        ops.geset(off, dg, blk[r_s:r_s + k, c_s:c_s + k], uplo=u)
+    cpos = {g: j for j, g in enumerate(gc)}
+    runs = []
+    i = 0
+    m = len(gr)
+    while i < m:
+        j = cpos.get(gr[i])
+        if j is None:
+            i += 1
+            continue
+        k = 1
+        while i + k < m and j + k < len(gc) and gr[i + k] == gr[i] + k and gc[j + k] == gc[j] + k:
+            k += 1
+        runs.append((i, j, k))
+        i += k
+    return runs
 
 
 def scale(numer, denom, A, opts=None):

@@ -211,14 +211,54 @@ def trtri(uplo, diag, A, info=None):
     return info
 
 
-def geqrf(A, tau):
-    """Householder QR of a panel (host kernel; device panels use the
-    blocked GEMM-based path in models.qr)."""
+def _qr_work(dev):
+    key = "qr:" + str(dev)
+    w = _WORK.get(key)
+    if w is None:
+        nbytes = max(64, int(kmod(torch.empty(0, device=dev)).geqrf_work_bytes()))
+        w = torch.zeros(nbytes // 8 + 8, dtype=torch.int64, device=dev)
+        _WORK[key] = w
+    return w
+
+
+def geqrf(A, tau, T=None, V=None):
+    """Householder QR of a panel A (m x n) in place: R on/above the diagonal,
+    the reflectors below it, tau[min(m,n)].  Optionally also returns the
+    compact-WY factor T (k x k upper, I - V T V^H = H_0 ... H_{k-1}) and the
+    explicit unit-lower V (m x k).  Device: recursive MFMA panel
+    (csrc/hip/geqrf.hip); host: native Householder + larft."""
     _chk(A)
+    m, n = A.shape
+    k = min(m, n)
+    if T is None:
+        T = colmajor_empty(k, k, A.dtype, A.device)
+    if V is None:
+        V = colmajor_empty(m, k, A.dtype, A.device)
+    if m == 0 or n == 0:
+        return T, V
     if A.is_cuda:
-        raise SlateError("ops.geqrf: use slate_amd.models.qr (device panels)")
-    _native._host.geqrf(code(A.dtype), A.shape[0], A.shape[1], A.data_ptr(), ld(A), tau.data_ptr())
-    return tau
+        w = _qr_work(A.device)
+        kmod(A).geqrf(code(A.dtype), m, n, A.data_ptr(), ld(A), tau.data_ptr(), T.data_ptr(), ld(T),
+                      V.data_ptr(), ld(V), w.data_ptr(), stream(A))
+    else:
+        _native._host.geqrf(code(A.dtype), m, n, A.data_ptr(), ld(A), tau.data_ptr())
+        v_explicit(A[:, :k], V)
+        T.zero_()
+        larft(V, tau[:k], T)
+    return T, V
+
+
+def v_explicit(A, V):
+    """V = unit-lower-trapezoidal part of A (reflectors), zeros above."""
+    m, k = V.shape
+    if m == 0 or k == 0:
+        return V
+    if A.is_cuda:
+        kmod(A).v_explicit(code(A.dtype), m, k, A.data_ptr(), ld(A), V.data_ptr(), ld(V), stream(A))
+    else:
+        V.copy_(torch.tril(A[:m, :k], -1))
+        V.diagonal().fill_(1)
+    return V
 
 
 def gelqf(A, tau):

@@ -156,8 +156,15 @@ class Comm:
         if self.size == 1:
             return t.unsqueeze(0)
         x, _ = self._prep(t.contiguous())
-        out = torch.empty((self.size,) + tuple(x.shape), dtype=x.dtype, device=x.device)
-        dist.all_gather_into_tensor(out, x, group=self.group)
+        if x.numel() == 0:
+            return torch.empty((self.size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        x = x.reshape((-1,) + tuple(x.shape[1:])) if x.dim() else x.reshape(1)
+        flat = torch.empty((self.size * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        if self.backend == "gloo":
+            dist.all_gather(list(flat.chunk(self.size)), x, group=self.group)
+        else:
+            dist.all_gather_into_tensor(flat, x, group=self.group)
+        out = flat.view((self.size,) + tuple(t.shape))
         return out.to(t.device) if out.device != t.device else out
 
     def allgatherv(self, t: torch.Tensor) -> list:
