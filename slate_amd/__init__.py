@@ -98,3 +98,27 @@ def lu_inverse_using_factor(A, pivots, opts=None):
 
 def lu_inverse_using_factor_out_of_place(A, pivots, B, opts=None):
     return getriOOP(A, pivots, B, opts)
+
+
+from .models.qr import (  # noqa: F401,E402
+    cholqr, gelqf, gels, gels_cholqr, gels_qr, geqrf, unmlq, unmqr)
+
+
+def qr_factor(A, T, opts=None):
+    return geqrf(A, T, opts)
+
+
+def qr_multiply_by_q(side, op, A, T, C, opts=None):
+    return unmqr(side, op, A, T, C, opts)
+
+
+def lq_factor(A, T, opts=None):
+    return gelqf(A, T, opts)
+
+
+def lq_multiply_by_q(side, op, A, T, C, opts=None):
+    return unmlq(side, op, A, T, C, opts)
+
+
+def least_squares_solve(A, BX, opts=None):
+    return gels(A, TriangularFactors(), BX, opts)

@@ -3,8 +3,72 @@
 #pragma once
 #include "gemm.hpp"
 #include "launchers.hpp"
+#include "workspace.hpp"
 
 namespace slate_hip {
+
+// ---------------------------------------------------------------- split-K
+// Tall-skinny reductions (V^H C in QR, Gram matrices, the k = m reductions
+// of the panel recursions) have a few output tiles and a very long k: one
+// workgroup per tile would leave the chip idle.  Split k into chunks
+// computed as a strided batch into a workspace, then one deterministic
+// reduction kernel (fixed summation order -> bit-reproducible results).
+template <typename T>
+__global__ void splitk_reduce_kernel(i64 m, i64 n, int ks, const T* __restrict__ W, T alpha, T beta, T* C,
+                                     i64 ldc) {
+    const i64 i = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    const i64 mn = m * n;
+    for (i64 j = blockIdx.y; j < n; j += gridDim.y) {
+        T acc = W[i + j * m];
+        for (int s = 1; s < ks; ++s) acc = s_add(acc, W[s * mn + i + j * m]);
+        T v = s_mul(alpha, acc);
+        if (!s_is_zero(beta)) v = s_add(v, s_mul(beta, C[i + j * ldc]));
+        C[i + j * ldc] = v;
+    }
+}
+
+template <typename T, typename Launch>
+static bool gemm_splitk(const GemmCall& c, int tile, hipStream_t s, Launch&& launch) {
+    if (!c.allow_split || c.batch != 1 || c.Aptrs || c.mask.mode != 0) return false;
+    const i64 tiles = ((c.m + tile - 1) / tile) * ((c.n + tile - 1) / tile);
+    if (tiles >= 256 || c.k < 2048 || c.k < 8 * std::max(c.m, c.n)) return false;
+    i64 ks = std::min<i64>(c.k / 512, (512 + tiles - 1) / tiles);
+    if (ks < 2) return false;
+    const i64 kc = ((c.k + ks - 1) / ks + 63) / 64 * 64;
+    const i64 full = c.k / kc, rem = c.k - full * kc;
+    ks = full + (rem > 0 ? 1 : 0);
+    T* W = static_cast<T*>(workspace(s, sizeof(T) * (size_t)c.m * c.n * ks, WS_P));
+    GemmCall p = c;
+    p.allow_split = false;
+    p.alpha_re = 1; p.alpha_im = 0; p.beta_re = 0; p.beta_im = 0;
+    p.C = W; p.ldc = c.m; p.strideC = c.m * c.n;
+    p.k = kc; p.batch = full;
+    const i64 sa = (c.transA == 'N') ? kc * c.lda : kc;
+    const i64 sb = (c.transB == 'N') ? kc : kc * c.ldb;
+    p.strideA = sa; p.strideB = sb;
+    launch(p);
+    if (rem > 0) {
+        GemmCall r = p;
+        r.batch = 1; r.k = rem; r.strideA = r.strideB = r.strideC = 0;
+        r.A = static_cast<const T*>(c.A) + full * sa;
+        r.B = static_cast<const T*>(c.B) + full * sb;
+        r.C = W + full * c.m * c.n;
+        launch(r);
+    }
+    T alpha, beta;
+    if constexpr (scalar_traits<T>::is_complex) {
+        using R = typename scalar_traits<T>::real;
+        alpha = T{(R)c.alpha_re, (R)c.alpha_im}; beta = T{(R)c.beta_re, (R)c.beta_im};
+    } else {
+        alpha = (T)c.alpha_re; beta = (T)c.beta_re;
+    }
+    dim3 grid((unsigned)((c.m + 255) / 256), (unsigned)std::min<i64>(c.n, 1024));
+    hipLaunchKernelGGL(splitk_reduce_kernel<T>, grid, dim3(256), 0, s, c.m, c.n, (int)ks, W, alpha, beta,
+                       static_cast<T*>(c.C), c.ldc);
+    HIP_LAUNCH_CHECK();
+    return true;
+}
 
 template <typename T, bool TA, bool TB, bool PTRS>
 static void launch_real(const GemmArgs<T>& a, int batch, hipStream_t s) {
@@ -39,6 +103,8 @@ static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 template <typename T>
 void gemm_real(const GemmCall& c, hipStream_t s) {
+    if (c.m > 0 && c.n > 0 && gemm_splitk<T>(c, 128, s, [&](const GemmCall& p) { gemm_real<T>(p, s); }))
+        return;
     GemmArgs<T> a{};
     a.m = c.m; a.n = c.n; a.k = c.k;
     a.alpha = (T)c.alpha_re; a.beta = (T)c.beta_re;
@@ -86,6 +152,8 @@ static void dispatch_cplx(char ta, char tb, const GemmArgs<T>& a, int batch, hip
 
 template <typename T>
 void gemm_complex(const GemmCall& c, hipStream_t s) {
+    if (c.m > 0 && c.n > 0 && gemm_splitk<T>(c, 64, s, [&](const GemmCall& p) { gemm_complex<T>(p, s); }))
+        return;
     using R = typename scalar_traits<T>::real;
     GemmArgs<T> a{};
     a.m = c.m; a.n = c.n; a.k = c.k;

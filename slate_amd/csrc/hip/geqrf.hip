@@ -33,6 +33,7 @@ struct QrBuf {
     double npart[QMAXG];         // partial squared norms
     T wpart[QMAXG][QB];          // partial v^H A(:, c)
     T gpart[QMAXG][QB];          // partial V(:, l)^H v
+    T beta;                      // beta of the last reflector (written to A by the next launch)
 };
 constexpr size_t QR_BYTES = sizeof(QrBuf<zcplx>);
 
@@ -83,6 +84,7 @@ qr_step_a(i64 m, int c0, int c1, int j, T* A, i64 lda, T* tau, T* Tm, i64 ldt, v
         }
         __syncthreads();
         const T tp = tau[pc];
+        if (pc >= r0 && pc < r1 && tid == 0) A[pc + (i64)pc * lda] = qb->beta;
         if (tid < QB) wsum[tid] = s_mul(s_conj(tp), wsum[tid]);
         __syncthreads();
         // ---- WG 0 extends T: T(c0:pc, pc) = -tau T(c0:pc, c0:pc) g
@@ -97,10 +99,13 @@ qr_step_a(i64 m, int c0, int c1, int j, T* A, i64 lda, T* tau, T* Tm, i64 ldt, v
         for (i64 i = r0 + tid; i < r1; i += QT) {
             if (i < pc) continue;
             const T v = (i == pc) ? s_from_real(T(), 1) : A[i + (i64)pc * lda];
-            for (int c = j; c < c1; ++c) {
-                T a = A[i + (i64)c * lda];
-                A[i + (i64)c * lda] = s_sub(a, s_mul(v, wsum[c - c0]));
-            }
+            T a[QB];   // whole row segment in registers: loads issue together
+            #pragma unroll
+            for (int c = 0; c < QB; ++c)
+                if (c0 + c >= j && c0 + c < c1) a[c] = A[i + (i64)(c0 + c) * lda];
+            #pragma unroll
+            for (int c = 0; c < QB; ++c)
+                if (c0 + c >= j && c0 + c < c1) A[i + (i64)(c0 + c) * lda] = s_sub(a[c], s_mul(v, wsum[c]));
         }
     }
     // ---- partial ||A(j+1:m, j)||^2 over own rows (same thread wrote them)
@@ -156,11 +161,12 @@ qr_step_b(i64 m, int c0, int c1, int j, T* A, i64 lda, T* tau, T* Tm, i64 ldt, v
             }
         }
     }
-    __syncthreads();   // every thread has read alpha before row j is rewritten
-    if (j >= r0 && j < r1 && tid == 0) A[j + (i64)j * lda] = s_from_real(T(), beta);
+    // A(j, j) = beta is written by the NEXT launch: other workgroups of this
+    // one may still be reading alpha from it
     if (g == 0 && tid == 0) {
         tau[j] = tj;
         Tm[j + (i64)j * ldt] = tj;
+        qb->beta = s_from_real(T(), beta);
     }
     // ---- scale v on own rows, accumulate partials
     //   w_c = sum_i conj(v_i) A(i, c), c in (j, c1);  g_l = sum_i conj(V(i, l)) v_i, l in [c0, j)
@@ -216,7 +222,7 @@ void v_explicit(i64 m, i64 n, const T* A, i64 lda, T* V, i64 ldv, hipStream_t s)
 
 template <typename T>
 static void qr_base(i64 m, int n, T* A, i64 lda, T* tau, T* Tm, i64 ldt, void* w, hipStream_t s) {
-    const int G = (int)std::min<i64>(QMAXG, std::max<i64>(1, (m + 511) / 512));
+    const int G = (int)std::min<i64>(QMAXG, std::max<i64>(1, (m + QT - 1) / QT));
     for (int j = 0; j < n; ++j) {
         hipLaunchKernelGGL(qr_step_a<T>, dim3(G), dim3(QT), 0, s, m, 0, n, j, A, lda, tau, Tm, ldt, w);
         hipLaunchKernelGGL(qr_step_b<T>, dim3(G), dim3(QT), 0, s, m, 0, n, j, A, lda, tau, Tm, ldt, w);

@@ -18,6 +18,7 @@ struct GemmCall {
     void* const* Cptrs = nullptr;
     i64 batch = 1;
     bool vec_ok = true;
+    bool allow_split = true;           // split-K for small-output / long-k calls
     TriMask mask;
 };
 

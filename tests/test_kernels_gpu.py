@@ -50,6 +50,22 @@ def test_gemm(dt, ta, tb):
     assert (ref(C) - R).abs().max() / R.abs().max() < TOL[dt]
 
 
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("tt", ["TN", "NN", "NT"])
+def test_gemm_splitk(dt, tt):
+    # few output tiles + long k -> split-K path (+ ragged last chunk)
+    ta, tb = tt[0], tt[1]
+    if dt.is_complex:
+        ta = 'C' if ta == 'T' else ta
+    m, n, k = 200, 96, 20000 + 37
+    A = cm(k, m, dt, 1) if ta != 'N' else cm(m, k, dt, 1)
+    B = cm(n, k, dt, 2) if tb != 'N' else cm(k, n, dt, 2)
+    C = cm(m, n, dt, 3)
+    R = 0.5 * ref(opx(A, ta)) @ ref(opx(B, tb)) + 2.0 * ref(C)
+    ops.gemm(0.5, A, B, 2.0, C, ta, tb)
+    assert (ref(C) - R).abs().max() / R.abs().max() < 4 * TOL[dt]
+
+
 def test_gemm_large_k512():
     m = n = 2048
     A, B, C = cm(m, 512, torch.float64, 4), cm(n, 512, torch.float64, 5), cm(m, n, torch.float64, 6)
