@@ -37,7 +37,8 @@ from .models.blas3 import (  # noqa: F401
     triangular_multiply, triangular_solve, trmm, trsm)
 from .models.chol import posv, potrf, potri, potrs  # noqa: F401
 from .models.aux import (  # noqa: F401
-    add, colNorms, copy, gather, norm, redistribute, scale, scale_row_col, set)
+    add, allgather_dense, colNorms, copy, copy_conj_transpose, from_dense, gather, norm, redistribute, scale,
+    scale_row_col, set)
 
 
 def version():

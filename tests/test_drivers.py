@@ -1,0 +1,181 @@
+"""Distributed drivers on CPU: single rank and gloo grids 2x1, 1x2, 2x2.
+
+Reference test strategy (test/test_*.cc): run the routine on a random
+matrix, compare against a sequential reference (here PyTorch fp64 on the
+gathered matrix), residual-based tolerances.
+"""
+import pytest
+import torch
+
+import slate_amd as sl
+from slate_amd.core.enums import Diag, Norm, Op, Side, Uplo
+from slate_amd.models.aux import allgather_dense as D
+
+from dist_util import run_dist
+
+
+def mat(m, n, nb, seed, p=1, q=1, dt=torch.float64, kind="rands"):
+    A = sl.Matrix(m, n, nb=nb, p=p, q=q, dtype=dt)
+    A.insertLocalTiles()
+    sl.generate_matrix(A, kind, seed)
+    return A
+
+
+def herm(n, nb, seed, p=1, q=1, dt=torch.float64, uplo=Uplo.Lower):
+    A = sl.HermitianMatrix(uplo, n, nb=nb, p=p, q=q, dtype=dt)
+    A.insertLocalTiles()
+    sl.generate_matrix(A, "poev", seed)
+    return A
+
+
+def full_herm(A):
+    X = D(A)
+    L = torch.tril(X) if A.uploPhysical() == Uplo.Lower else torch.triu(X)
+    return L + L.mH - torch.diag(torch.diagonal(L))
+
+
+def close(a, b, tol=1e-10):
+    s = max(1.0, b.abs().max().item())
+    err = (a - b).abs().max().item() / s
+    assert err < tol, err
+
+
+# ----------------------------------------------------------------- checks
+def check_gemm(p, q, dt=torch.float64):
+    for ta, tb in [(Op.NoTrans, Op.NoTrans), (Op.ConjTrans, Op.NoTrans), (Op.NoTrans, Op.Trans)]:
+        A = mat(70, 50, 16, 1, p, q, dt) if ta == Op.NoTrans else mat(50, 70, 16, 1, p, q, dt)
+        B = mat(50, 40, 16, 2, p, q, dt) if tb == Op.NoTrans else mat(40, 50, 16, 2, p, q, dt)
+        C = mat(70, 40, 16, 3, p, q, dt)
+        Ad, Bd, Cd = D(A), D(B), D(C)
+        opA = A if ta == Op.NoTrans else A.conj_transpose()
+        opB = B if tb == Op.NoTrans else B.transpose()
+        sl.gemm(1.5, opA, opB, -0.5, C)
+        ref = 1.5 * (Ad if ta == Op.NoTrans else Ad.mH) @ (Bd if tb == Op.NoTrans else Bd.T) - 0.5 * Cd
+        close(D(C), ref)
+
+
+def check_herk_trsm_trmm(p, q, dt=torch.float64):
+    A = mat(60, 30, 16, 4, p, q, dt)
+    C = herm(60, 16, 5, p, q, dt)
+    Cf = full_herm(C)
+    Ad = D(A)
+    sl.herk(2.0, A, 0.5, C)
+    close(full_herm(C), 2.0 * Ad @ Ad.mH + 0.5 * Cf)
+    # trsm / trmm, left lower and right upper
+    T = mat(48, 48, 16, 6, p, q, dt)
+    sl.add(0.0, T, 1.0, T)
+    Td = D(T) + 48 * torch.eye(48, dtype=dt)
+    sl.from_dense(T, Td)
+    B = mat(48, 20, 16, 7, p, q, dt)
+    Bd = D(B)
+    L = sl.TriangularMatrix(Uplo.Lower, T, diag=Diag.NonUnit)
+    sl.trsm(Side.Left, 2.0, L, B)
+    close(D(B), torch.linalg.solve_triangular(torch.tril(Td), 2.0 * Bd, upper=False), 1e-9)
+    B2 = mat(20, 48, 16, 8, p, q, dt)
+    B2d = D(B2)
+    U = sl.TriangularMatrix(Uplo.Upper, T, diag=Diag.NonUnit)
+    sl.trmm(Side.Right, 1.0, U, B2)
+    close(D(B2), B2d @ torch.triu(Td))
+
+
+def check_potrf(p, q, dt=torch.float64, uplo=Uplo.Lower):
+    n, nb = 96, 16
+    A = herm(n, nb, 11, p, q, dt, uplo)
+    Af = full_herm(A)
+    assert sl.potrf(A) == 0
+    F = D(A)
+    if uplo == Uplo.Lower:
+        L = torch.tril(F)
+        close(L @ L.mH, Af, 1e-12)
+    else:
+        U = torch.triu(F)
+        close(U.mH @ U, Af, 1e-12)
+    B = mat(n, 5, nb, 12, p, q, dt)
+    Bd = D(B)
+    sl.potrs(A, B)
+    close(Af @ D(B), Bd, 1e-10)
+
+
+def check_lu(p, q, dt=torch.float64):
+    n, nb = 90, 16
+    A = mat(n, n, nb, 13, p, q, dt)
+    Ad = D(A)
+    piv = sl.Pivots()
+    B = mat(n, 4, nb, 14, p, q, dt)
+    Bd = D(B)
+    assert sl.gesv(A, piv, B) == 0
+    X = D(B)
+    close(Ad @ X, Bd, 1e-10)
+    # factor property P A = L U
+    F = D(A)
+    L = torch.tril(F, -1) + torch.eye(n, dtype=dt)
+    U = torch.triu(F)
+    PA = Ad.clone()
+    for i, pv in enumerate(piv.ipiv.tolist()):
+        if pv != i:
+            PA[[i, pv]] = PA[[pv, i]]
+    close(L @ U, PA, 1e-12)
+
+
+def check_norms(p, q, dt=torch.float64):
+    A = mat(77, 55, 16, 15, p, q, dt)
+    Ad = D(A)
+    for nt, ref in [(Norm.Max, Ad.abs().max()), (Norm.One, Ad.abs().sum(0).max()),
+                    (Norm.Inf, Ad.abs().sum(1).max()), (Norm.Fro, torch.linalg.norm(Ad))]:
+        v = sl.norm(nt, A)
+        assert abs(float(v) - ref.item()) < 1e-10 * max(1.0, ref.item()), (nt, float(v), ref.item())
+    H = herm(50, 16, 16, p, q, dt)
+    Hf = full_herm(H)
+    assert abs(float(sl.norm(Norm.One, H)) - Hf.abs().sum(0).max().item()) < 1e-9
+
+
+def check_aux(p, q, dt=torch.float64):
+    A = mat(40, 30, 16, 17, p, q, dt)
+    B = mat(40, 30, 16, 18, p, q, dt)
+    Ad, Bd = D(A), D(B)
+    sl.add(2.0, A, -1.0, B)
+    close(D(B), 2.0 * Ad - Bd)
+    sl.scale(3.0, 2.0, A)
+    close(D(A), 1.5 * Ad)
+    sl.set(0.5, 2.0, A)
+    E = torch.full((40, 30), 0.5, dtype=dt)
+    E.diagonal().fill_(2.0)
+    close(D(A), E)
+    C = sl.Matrix(40, 30, nb=8, p=q, q=p, dtype=dt)
+    C.insertLocalTiles()
+    sl.redistribute(B, C)
+    close(D(C), D(B))
+
+
+ALL = [check_gemm, check_herk_trsm_trmm, check_potrf, check_lu, check_norms, check_aux]
+
+
+def _run_all(rank, size, p, q):
+    for f in ALL:
+        f(p, q)
+    check_potrf(p, q, uplo=Uplo.Upper)
+    check_lu(p, q, torch.complex128)
+    check_gemm(p, q, torch.complex128)
+
+
+# ----------------------------------------------------------------- tests
+@pytest.mark.parametrize("check", ALL, ids=lambda f: f.__name__)
+def test_single_rank(check):
+    check(1, 1)
+
+
+def test_single_rank_complex():
+    check_gemm(1, 1, torch.complex128)
+    check_potrf(1, 1, torch.complex128)
+    check_potrf(1, 1, torch.complex128, Uplo.Upper)
+    check_lu(1, 1, torch.complex128)
+    check_herk_trsm_trmm(1, 1, torch.complex128)
+
+
+@pytest.mark.parametrize("grid", [(2, 1), (1, 2)])
+def test_two_ranks(grid):
+    run_dist(_run_all, 2, *grid)
+
+
+def test_four_ranks():
+    run_dist(_run_all, 4, 2, 2)
