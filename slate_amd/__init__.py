@@ -123,3 +123,8 @@ def lq_multiply_by_q(side, op, A, T, C, opts=None):
 
 def least_squares_solve(A, BX, opts=None):
     return gels(A, TriangularFactors(), BX, opts)
+
+
+from .models.eig import (  # noqa: F401,E402
+    eig, eig_vals, hb2st, he2hb, heev, hegst, hegv, stedc, steqr, sterf, unmtr_hb2st, unmtr_he2hb)
+from .models.svd import bdsqr, ge2tb, svd, svd_vals, tb2bd  # noqa: F401,E402

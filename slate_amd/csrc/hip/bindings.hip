@@ -123,6 +123,12 @@ static void register_kernels(py::module& m) {
         dispatch(dt, [&](auto z) { using T = decltype(z);
             geqrf_panel_ws<T>(mm, n, P<T>(A), lda, P<T>(tau), P<T>(Tm), ldt, P<T>(V), ldv, (void*)work, S(st)); });
     });
+    m.def("apply_refl", [](char dt, i64 ncols, uintptr_t Z, i64 ldz, uintptr_t V, i64 b, uintptr_t tau,
+                           uintptr_t row, uintptr_t len, i64 first, i64 count, bool conj_tau, uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            apply_refl_batch<T>(ncols, P<T>(Z), ldz, P<const T>(V), b, P<const T>(tau), P<const i64>(row),
+                                P<const i64>(len), first, count, conj_tau, S(st)); });
+    });
     m.def("geqrf_work_bytes", []() { return (i64)geqrf_work_bytes(); });
     m.def("v_explicit", [](char dt, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t V, i64 ldv, uintptr_t st) {
         dispatch(dt, [&](auto z) { using T = decltype(z);

@@ -1,0 +1,552 @@
+// Host kernels of the eigenvalue / SVD pipelines (stage 2 + tridiagonal /
+// bidiagonal solvers).  These are the parts SLATE also runs on the host:
+//   hb2st  -- Hermitian band -> real symmetric tridiagonal by bulge chasing
+//             (src/hb2st.cc, internal_hebr.cc: hebr1/2/3 tasks)
+//   tb2bd  -- upper triangular band -> real bidiagonal (src/tb2bd.cc,
+//             internal_gebr.cc: gebr1/2/3)
+//   sterf / steqr -- implicit-shift QL on a symmetric tridiagonal
+//             (src/sterf.cc, src/steqr.cc, steqr_impl.cc)
+//   bdsqr  -- implicit-shift QR SVD of a bidiagonal (src/bdsqr.cc)
+//   secular -- roots of the rank-one-update secular equation for the
+//             divide & conquer merge (src/stedc_secular.cc / laed4)
+// Design notes (MI355X framework): the chases keep the band in a dense
+// column-major window (simple, cache friendly at the band sizes used), and
+// every reflector is recorded so the back-transformations run on the GPU as
+// batched kernels/GEMMs; rotation sequences of steqr/bdsqr are applied to
+// the eigen/singular vector rows in parallel (OpenMP over rows).
+#include <pybind11/pybind11.h>
+#include <pybind11/complex.h>
+
+#include <algorithm>
+#include <cmath>
+#include <complex>
+#include <cstdint>
+#include <limits>
+#include <stdexcept>
+#include <vector>
+
+namespace py = pybind11;
+
+namespace slate_host {
+namespace {
+
+using i64 = int64_t;
+template <typename T> struct rl { using type = T; };
+template <typename T> struct rl<std::complex<T>> { using type = T; };
+template <typename T> using R_t = typename rl<T>::type;
+template <typename T> inline T cj(T x) { return x; }
+template <typename T> inline std::complex<T> cj(std::complex<T> x) { return std::conj(x); }
+
+// Householder generator: on entry x[0..k-1]; on exit v (v[0] = 1) in x,
+// returns tau, beta (real) with (I - tau v v^H)^H x_in = beta e1.
+template <typename T>
+void hgen(i64 k, T* x, T& tau, R_t<T>& beta) {
+    using R = R_t<T>;
+    T alpha = x[0];
+    R xn2 = 0;
+    for (i64 i = 1; i < k; ++i) xn2 += std::norm(x[i]);
+    R ar = std::real(alpha), ai = std::imag(alpha);
+    if (xn2 == R(0) && ai == R(0)) {
+        tau = T(0);
+        beta = ar;
+        x[0] = T(1);
+        return;
+    }
+    beta = -std::copysign(std::sqrt(ar * ar + ai * ai + xn2), ar);
+    if constexpr (std::is_same_v<T, R>) {
+        tau = (beta - ar) / beta;
+    } else {
+        tau = T((beta - ar) / beta, -ai / beta);
+    }
+    T sc = T(1) / (alpha - T(beta));
+    for (i64 i = 1; i < k; ++i) x[i] *= sc;
+    x[0] = T(1);
+}
+
+template <typename T>
+struct Dense {
+    T* a; i64 ld;
+    T& operator()(i64 r, i64 c) const { return a[r + c * ld]; }
+};
+
+// A[rows s..s+k-1, cols lo..hi] := H^H A[...]   (H = I - tau v v^H)
+template <typename T>
+void apply_left(Dense<T> A, i64 s, i64 k, const T* v, T tau, i64 lo, i64 hi) {
+    if (tau == T(0)) return;
+    const T ct = cj(tau);
+    for (i64 c = lo; c <= hi; ++c) {
+        T w = 0;
+        for (i64 r = 0; r < k; ++r) w += cj(v[r]) * A(s + r, c);
+        w *= ct;
+        if (w == T(0)) continue;
+        for (i64 r = 0; r < k; ++r) A(s + r, c) -= v[r] * w;
+    }
+}
+
+// A[rows lo..hi, cols s..s+k-1] := A[...] H
+template <typename T>
+void apply_right(Dense<T> A, i64 s, i64 k, const T* v, T tau, i64 lo, i64 hi) {
+    if (tau == T(0)) return;
+    for (i64 r = lo; r <= hi; ++r) {
+        T y = 0;
+        for (i64 c = 0; c < k; ++c) y += A(r, s + c) * v[c];
+        y *= tau;
+        if (y == T(0)) continue;
+        for (i64 c = 0; c < k; ++c) A(r, s + c) -= y * cj(v[c]);
+    }
+}
+
+struct Refl {            // reflector store (row-major count x b)
+    void* V; void* tau; i64* row; i64* len; i64 b; i64 cap; i64 cnt = 0;
+    template <typename T> void put(i64 r0, i64 k, const T* v, T t) {
+        if (cnt >= cap) throw std::runtime_error("reflector store overflow");
+        T* dst = static_cast<T*>(V) + cnt * b;
+        for (i64 i = 0; i < k; ++i) dst[i] = v[i];
+        for (i64 i = k; i < b; ++i) dst[i] = T(0);
+        static_cast<T*>(tau)[cnt] = t;
+        row[cnt] = r0; len[cnt] = k;
+        ++cnt;
+    }
+};
+
+// ---------------------------------------------------------------- hb2st
+// A: dense n x n Hermitian (both triangles) of lower bandwidth b.  Reduced
+// in place to Hermitian tridiagonal T = Q^H A Q, Q = prod of the recorded
+// reflectors in order; sweep_ptr[j] = first reflector of sweep j.
+template <typename T>
+i64 hb2st(i64 n, i64 b, T* a, i64 lda, Refl& st, i64* sweep_ptr) {
+    Dense<T> A{a, lda};
+    std::vector<T> v(b + 1), v2(b + 1);
+    const i64 w = 2 * b + 1;   // band + bulge half-width
+    for (i64 j = 0; j + 1 < n; ++j) {
+        sweep_ptr[j] = st.cnt;
+        i64 s = j + 1, e = std::min(j + b, n - 1), k = e - s + 1;
+        if (k <= 1) continue;            // nothing below the subdiagonal
+        for (i64 r = 0; r < k; ++r) v[r] = A(s + r, j);
+        T tau; R_t<T> beta;
+        hgen(k, v.data(), tau, beta);
+        // two-sided on rows/cols s..e over the window
+        i64 lo = std::max<i64>(0, s - w), hi = std::min(n - 1, e + w);
+        apply_left(A, s, k, v.data(), tau, lo, hi);
+        apply_right(A, s, k, v.data(), tau, lo, hi);
+        A(s, j) = T(beta); A(j, s) = T(beta);
+        for (i64 r = 1; r < k; ++r) { A(s + r, j) = T(0); A(j, s + r) = T(0); }
+        st.put(s, k, v.data(), tau);
+        // chase the bulge
+        while (true) {
+            i64 s2 = e + 1;
+            if (s2 > n - 1) break;
+            i64 e2 = std::min(e + b, n - 1), k2 = e2 - s2 + 1;
+            for (i64 r = 0; r < k2; ++r) v2[r] = A(s2 + r, s);
+            T tau2; R_t<T> beta2;
+            hgen(k2, v2.data(), tau2, beta2);
+            i64 lo2 = std::max<i64>(0, s2 - w), hi2 = std::min(n - 1, e2 + w);
+            apply_left(A, s2, k2, v2.data(), tau2, lo2, hi2);
+            apply_right(A, s2, k2, v2.data(), tau2, lo2, hi2);
+            A(s2, s) = T(beta2); A(s, s2) = T(beta2);
+            for (i64 r = 1; r < k2; ++r) { A(s2 + r, s) = T(0); A(s, s2 + r) = T(0); }
+            st.put(s2, k2, v2.data(), tau2);
+            s = s2; e = e2; k = k2;
+        }
+    }
+    if (n >= 1) sweep_ptr[n - 1] = st.cnt;
+    return st.cnt;
+}
+
+// ---------------------------------------------------------------- tb2bd
+// A: dense n x n upper triangular band (bandwidth b above the diagonal),
+// reduced in place to upper bidiagonal B = U^H A V.  Left reflectors go to
+// `ul` (U = prod), right reflectors to `vr` (V = prod); ptrs per sweep.
+template <typename T>
+void tb2bd(i64 n, i64 b, T* a, i64 lda, Refl& ul, Refl& vr, i64* uptr, i64* vptr) {
+    Dense<T> A{a, lda};
+    std::vector<T> v(b + 1), x(b + 1);
+    const i64 w = 2 * b + 1;
+    for (i64 j = 0; j + 1 < n; ++j) {
+        uptr[j] = ul.cnt; vptr[j] = vr.cnt;
+        // right reflector on row j, columns j+1..e
+        i64 cs = j + 1, ce = std::min(j + b, n - 1), k = ce - cs + 1;
+        i64 row = j;
+        while (true) {
+            for (i64 c = 0; c < k; ++c) v[c] = cj(A(row, cs + c));
+            T tau; R_t<T> beta;
+            hgen(k, v.data(), tau, beta);
+            i64 lo = std::max<i64>(0, cs - w), hi = std::min(n - 1, ce + w);
+            apply_right(A, cs, k, v.data(), tau, lo, hi);
+            A(row, cs) = T(beta);
+            for (i64 c = 1; c < k; ++c) A(row, cs + c) = T(0);
+            vr.put(cs, k, v.data(), tau);
+            // left reflector on rows cs..ce annihilating column cs below the diagonal
+            i64 rs = cs, re = std::min(cs + b - 1, n - 1);
+            re = std::min(re, ce);
+            i64 kr = re - rs + 1;
+            for (i64 r = 0; r < kr; ++r) x[r] = A(rs + r, cs);
+            T tl; R_t<T> bl;
+            hgen(kr, x.data(), tl, bl);
+            i64 lo2 = std::max<i64>(0, rs - w), hi2 = std::min(n - 1, re + w);
+            apply_left(A, rs, kr, x.data(), tl, lo2, hi2);
+            A(rs, cs) = T(bl);
+            for (i64 r = 1; r < kr; ++r) A(rs + r, cs) = T(0);
+            ul.put(rs, kr, x.data(), tl);
+            // next: row rs has fill beyond its band -> columns ce+1 .. ce+b
+            i64 ncs = ce + 1;
+            if (ncs > n - 1) break;
+            row = rs;
+            cs = ncs; ce = std::min(ncs + b - 1, n - 1); k = ce - cs + 1;
+        }
+    }
+    if (n >= 1) { uptr[n - 1] = ul.cnt; vptr[n - 1] = vr.cnt; }
+}
+
+// ---------------------------------------------------------------- rotations
+// apply a sequence of plane rotations to columns (i, i+1) of Z for all rows
+// in parallel: Z(:, i), Z(:, i+1) <- c*Z_i - s*Z_{i+1}, s*Z_i + c*Z_{i+1}
+template <typename Z_t, typename R>
+void rot_seq(i64 nrow, Z_t* z, i64 ldz, const std::vector<i64>& idx, const std::vector<R>& cs,
+             const std::vector<R>& sn) {
+    if (!z || idx.empty()) return;
+    const i64 nr = (i64)idx.size();
+    #pragma omp parallel for schedule(static) if (nrow * nr > 1 << 16)
+    for (i64 r = 0; r < nrow; ++r) {
+        for (i64 t = 0; t < nr; ++t) {
+            const i64 i = idx[t];
+            Z_t* zi = z + r + i * ldz;
+            Z_t* zj = z + r + (i + 1) * ldz;
+            const Z_t a = *zi, b2 = *zj;
+            *zi = cs[t] * a - sn[t] * b2;
+            *zj = sn[t] * a + cs[t] * b2;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- steqr
+// Implicit-shift QL/QR on the symmetric tridiagonal (d, e); optional
+// eigenvector accumulation Z (nz x n, columns rotated).  Eigenvalues sorted
+// ascending (with Z columns) on exit.  Returns 0 or #unconverged.
+template <typename Z_t>
+i64 steqr_impl(i64 n, double* d, double* e, Z_t* z, i64 ldz, i64 nz) {
+    using R = double;
+    if (n <= 1) return 0;
+    const R eps = std::numeric_limits<R>::epsilon();
+    std::vector<R> ew(n, 0);
+    for (i64 i = 0; i < n - 1; ++i) ew[i] = e[i];
+    i64 fails = 0;
+    std::vector<i64> idx; std::vector<R> cs, sn;
+    for (i64 l = 0; l < n; ++l) {
+        i64 iter = 0;
+        while (true) {
+            i64 m = l;
+            for (; m < n - 1; ++m) {
+                R dd = std::abs(d[m]) + std::abs(d[m + 1]);
+                if (std::abs(ew[m]) <= eps * dd || std::abs(ew[m]) < std::numeric_limits<R>::min()) break;
+            }
+            if (m == l) break;
+            if (++iter > 60) { ++fails; break; }
+            // Wilkinson-type shift from the leading 2x2
+            R g = (d[l + 1] - d[l]) / (2 * ew[l]);
+            R r = std::hypot(g, R(1));
+            g = d[m] - d[l] + ew[l] / (g + std::copysign(r, g));
+            R s = 1, c = 1, p = 0;
+            bool early = false;
+            idx.clear(); cs.clear(); sn.clear();
+            i64 i;
+            for (i = m - 1; i >= l; --i) {
+                R f = s * ew[i], bb = c * ew[i];
+                r = std::hypot(f, g);
+                ew[i + 1] = r;
+                if (r == 0) { d[i + 1] -= p; ew[m] = 0; early = true; break; }
+                s = f / r; c = g / r;
+                g = d[i + 1] - p;
+                r = (d[i] - g) * s + 2 * c * bb;
+                p = s * r;
+                d[i + 1] = g + p;
+                g = c * r - bb;
+                // rotation on columns (i, i+1):  z_{i+1} <- s z_i + c z_{i+1}; z_i <- c z_i - s z_{i+1}
+                idx.push_back(i); cs.push_back(c); sn.push_back(s);
+            }
+            // apply in generation order: (i, i+1) with (c, s): zi' = c zi - s zj ; zj' = s zi + c zj
+            if (z) {
+                #pragma omp parallel for schedule(static) if (nz * (i64)idx.size() > 1 << 16)
+                for (i64 rr = 0; rr < nz; ++rr) {
+                    for (size_t t = 0; t < idx.size(); ++t) {
+                        Z_t* zi = z + rr + idx[t] * ldz;
+                        Z_t* zj = zi + ldz;
+                        const Z_t a = *zi, b2 = *zj;
+                        *zj = sn[t] * a + cs[t] * b2;
+                        *zi = cs[t] * a - sn[t] * b2;
+                    }
+                }
+            }
+            if (early && i >= l) continue;
+            d[l] -= p; ew[l] = g; ew[m] = 0;
+        }
+    }
+    // sort ascending (selection sort on columns, O(n^2) swaps of Z columns)
+    for (i64 i = 0; i < n - 1; ++i) {
+        i64 k = i;
+        for (i64 j = i + 1; j < n; ++j) if (d[j] < d[k]) k = j;
+        if (k != i) {
+            std::swap(d[i], d[k]);
+            if (z) for (i64 r = 0; r < nz; ++r) std::swap(z[r + i * ldz], z[r + k * ldz]);
+        }
+    }
+    for (i64 i = 0; i < n - 1; ++i) e[i] = 0;
+    return fails;
+}
+
+// ---------------------------------------------------------------- bdsqr
+// SVD of the real upper bidiagonal (d, e): B = U S V^T.  U (nu x n) gets
+// right-multiplied by the left rotations, VT (n x nv) left-multiplied by the
+// right rotations (stored as columns of V = VT^T: we rotate rows of VT).
+// Golub-Kahan implicit-shift QR with a standard deflation test; singular
+// values made non-negative and sorted descending.
+i64 bdsqr_impl(i64 n, double* d, double* e, double* u, i64 ldu, i64 nu, double* vt, i64 ldvt, i64 nv) {
+    using R = double;
+    if (n == 0) return 0;
+    const R eps = std::numeric_limits<R>::epsilon();
+    const R tiny = std::numeric_limits<R>::min();
+    i64 fails = 0;
+    std::vector<i64> ui, vi; std::vector<R> uc, us, vc, vs;
+    auto flush = [&]() {
+        if (u && !ui.empty()) {
+            #pragma omp parallel for schedule(static) if (nu * (i64)ui.size() > 1 << 16)
+            for (i64 r = 0; r < nu; ++r)
+                for (size_t t = 0; t < ui.size(); ++t) {
+                    R* a = u + r + ui[t] * ldu; R* b2 = a + ldu;
+                    R x = *a, y = *b2;
+                    *a = uc[t] * x + us[t] * y;
+                    *b2 = -us[t] * x + uc[t] * y;
+                }
+        }
+        if (vt && !vi.empty()) {
+            #pragma omp parallel for schedule(static) if (nv * (i64)vi.size() > 1 << 16)
+            for (i64 c = 0; c < nv; ++c)
+                for (size_t t = 0; t < vi.size(); ++t) {
+                    R* a = vt + vi[t] + c * ldvt; R* b2 = a + 1;
+                    R x = *a, y = *b2;
+                    *a = vc[t] * x + vs[t] * y;
+                    *b2 = -vs[t] * x + vc[t] * y;
+                }
+        }
+        ui.clear(); uc.clear(); us.clear(); vi.clear(); vc.clear(); vs.clear();
+    };
+    auto givens = [](R f, R g, R& c, R& s, R& r) {
+        if (g == 0) { c = 1; s = 0; r = f; return; }
+        if (f == 0) { c = 0; s = 1; r = g; return; }
+        r = std::hypot(f, g); c = f / r; s = g / r;
+    };
+    i64 hi = n - 1;
+    i64 iter = 0, maxit = 40 * n * n + 100;
+    while (hi > 0) {
+        // deflate negligible superdiagonals
+        for (i64 i = 0; i < hi; ++i)
+            if (std::abs(e[i]) <= eps * (std::abs(d[i]) + std::abs(d[i + 1])) || std::abs(e[i]) < tiny) e[i] = 0;
+        if (e[hi - 1] == 0) { --hi; continue; }
+        i64 lo = hi - 1;
+        while (lo > 0 && e[lo - 1] != 0) --lo;
+        if (++iter > maxit) { fails = hi; break; }
+        // zero diagonal inside the block: chase the row out with rotations
+        bool zd = false;
+        for (i64 i = lo; i < hi; ++i) {
+            if (std::abs(d[i]) <= eps * 1e-3 * (std::abs(e[i]) + (i > lo ? std::abs(e[i - 1]) : 0))) {
+                d[i] = 0;
+                // rotate row i against rows i+1.. to annihilate e[i]
+                R f = e[i]; e[i] = 0;
+                for (i64 k = i + 1; k <= hi; ++k) {
+                    R c, s, r;
+                    givens(d[k], f, c, s, r);
+                    d[k] = r;
+                    // left rotation on rows (i, k): affects U columns i, k
+                    if (k < hi) { f = -s * e[k]; e[k] = c * e[k]; }
+                    if (u) {
+                        #pragma omp parallel for schedule(static) if (nu > 4096)
+                        for (i64 rr = 0; rr < nu; ++rr) {
+                            R* a = u + rr + i * ldu; R* b2 = u + rr + k * ldu;
+                            R x = *a, y = *b2;
+                            *a = c * x - s * y;
+                            *b2 = s * x + c * y;
+                        }
+                    }
+                }
+                zd = true;
+                break;
+            }
+        }
+        if (zd) continue;
+        // Wilkinson shift from the trailing 2x2 of B^T B
+        R dm = d[hi - 1], dn = d[hi], em = (hi - 1 > lo) ? e[hi - 2] : 0, en = e[hi - 1];
+        R t11 = dm * dm + em * em, t22 = dn * dn + en * en, t12 = dm * en;
+        R dl = (t11 - t22) / 2;
+        R mu = t22 - t12 * t12 / (dl + std::copysign(std::hypot(dl, t12), dl == 0 ? 1.0 : dl));
+        if (!std::isfinite(mu)) mu = t22;
+        R y = d[lo] * d[lo] - mu, z = d[lo] * e[lo];
+        for (i64 k = lo; k < hi; ++k) {
+            R c, s, r;
+            givens(y, z, c, s, r);
+            // right rotation on columns (k, k+1)
+            if (k > lo) e[k - 1] = r;
+            y = c * d[k] + s * e[k];
+            e[k] = -s * d[k] + c * e[k];
+            z = s * d[k + 1];
+            d[k + 1] = c * d[k + 1];
+            vi.push_back(k); vc.push_back(c); vs.push_back(s);
+            givens(y, z, c, s, r);
+            d[k] = r;
+            y = c * e[k] + s * d[k + 1];
+            d[k + 1] = -s * e[k] + c * d[k + 1];
+            if (k < hi - 1) { z = s * e[k + 1]; e[k + 1] = c * e[k + 1]; }
+            ui.push_back(k); uc.push_back(c); us.push_back(s);
+        }
+        e[hi - 1] = y;
+        flush();
+    }
+    flush();
+    // signs and descending order
+    for (i64 i = 0; i < n; ++i)
+        if (d[i] < 0) {
+            d[i] = -d[i];
+            if (vt) for (i64 c = 0; c < nv; ++c) vt[i + c * ldvt] = -vt[i + c * ldvt];
+        }
+    for (i64 i = 0; i < n - 1; ++i) {
+        i64 k = i;
+        for (i64 j = i + 1; j < n; ++j) if (d[j] > d[k]) k = j;
+        if (k != i) {
+            std::swap(d[i], d[k]);
+            if (u) for (i64 r = 0; r < nu; ++r) std::swap(u[r + i * ldu], u[r + k * ldu]);
+            if (vt) for (i64 c = 0; c < nv; ++c) std::swap(vt[i + c * ldvt], vt[k + c * ldvt]);
+        }
+    }
+    return fails;
+}
+
+// ---------------------------------------------------------------- secular
+// Roots of 1 + rho * sum_i z_i^2 / (d_i - lambda) = 0, d ascending,
+// rho > 0 (caller flips signs for rho < 0), all z_i != 0 (deflated before).
+// Root j lies in (d_j, d_{j+1}) (last: (d_{n-1}, d_{n-1} + rho |z|^2)).
+// Returned as origin index org[j] and offset mu[j] (lambda = d[org] + mu),
+// so that d_i - lambda_j = (d_i - d_org) - mu is formed without
+// cancellation (needed by the Gu-Eisenstat eigenvector formula).
+void secular(i64 n, const double* d, const double* z, double rho, i64* org, double* mu) {
+    double zz = 0;
+    for (i64 i = 0; i < n; ++i) zz += z[i] * z[i];
+    #pragma omp parallel for schedule(dynamic, 16) if (n > 64)
+    for (i64 j = 0; j < n; ++j) {
+        const double lo_d = d[j];
+        const double hi_d = (j + 1 < n) ? d[j + 1] : d[j] + rho * zz;
+        // choose the origin by the sign of f at the midpoint
+        const double mid = 0.5 * (hi_d - lo_d);
+        auto f_at = [&](i64 o, double m) {
+            double s = 1;
+            for (i64 i = 0; i < n; ++i) s += rho * z[i] * z[i] / ((d[i] - d[o]) - m);
+            return s;
+        };
+        i64 o;
+        double a, b;
+        if (j + 1 < n && f_at(j, mid) < 0) {   // f increasing in (d_j, d_j+1): root right of mid
+            o = j + 1; a = -mid; b = 0;
+        } else {
+            o = j; a = 0; b = (j + 1 < n) ? mid : (hi_d - lo_d);
+        }
+        // bisection on mu in (a, b) -- f is increasing in lambda on the interval
+        for (int it = 0; it < 200; ++it) {
+            double m = 0.5 * (a + b);
+            if (m == a || m == b) break;
+            double fv = f_at(o, m);
+            if (fv < 0) a = m; else b = m;
+        }
+        org[j] = o;
+        mu[j] = 0.5 * (a + b);
+    }
+}
+
+// Z := H_k Z for reflectors k in [first, first+count) (disjoint rows)
+template <typename T>
+void apply_refl_host(i64 ncols, T* Z, i64 ldz, const T* V, i64 b, const T* tau, const i64* row, const i64* len,
+                     i64 first, i64 count, bool conj_tau) {
+    #pragma omp parallel for schedule(static) if (ncols * count > 4096)
+    for (i64 c = 0; c < ncols; ++c) {
+        for (i64 k = first; k < first + count; ++k) {
+            T t = conj_tau ? cj(tau[k]) : tau[k];
+            if (t == T(0)) continue;
+            const T* v = V + k * b;
+            T* z = Z + row[k] + c * ldz;
+            T w = 0;
+            for (i64 i = 0; i < len[k]; ++i) w += cj(v[i]) * z[i];
+            w *= t;
+            for (i64 i = 0; i < len[k]; ++i) z[i] -= v[i] * w;
+        }
+    }
+}
+
+template <typename F>
+void dispatch(char dt, F&& f) {
+    switch (dt) {
+        case 's': f(float()); break;
+        case 'd': f(double()); break;
+        case 'c': f(std::complex<float>()); break;
+        case 'z': f(std::complex<double>()); break;
+        default: throw std::invalid_argument("bad dtype");
+    }
+}
+template <typename T> T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
+
+}  // namespace
+
+void register_eig(py::module& m) {
+    m.def("hb2st", [](char dt, i64 n, i64 b, uintptr_t A, i64 lda, uintptr_t V, uintptr_t tau, uintptr_t row,
+                      uintptr_t len, i64 cap, uintptr_t sweep_ptr) {
+        py::gil_scoped_release nogil;
+        i64 cnt = 0;
+        dispatch(dt, [&](auto z) {
+            using T = decltype(z);
+            Refl st{(void*)V, (void*)tau, P<i64>(row), P<i64>(len), b, cap};
+            cnt = hb2st<T>(n, b, P<T>(A), lda, st, P<i64>(sweep_ptr));
+        });
+        return cnt;
+    });
+    m.def("tb2bd", [](char dt, i64 n, i64 b, uintptr_t A, i64 lda, uintptr_t UV, uintptr_t Utau, uintptr_t Urow,
+                      uintptr_t Ulen, uintptr_t VV, uintptr_t Vtau, uintptr_t Vrow, uintptr_t Vlen, i64 cap,
+                      uintptr_t uptr, uintptr_t vptr) {
+        i64 cu = 0, cv = 0;
+        {
+            py::gil_scoped_release nogil;
+            dispatch(dt, [&](auto z) {
+                using T = decltype(z);
+                Refl ul{(void*)UV, (void*)Utau, P<i64>(Urow), P<i64>(Ulen), b, cap};
+                Refl vr{(void*)VV, (void*)Vtau, P<i64>(Vrow), P<i64>(Vlen), b, cap};
+                tb2bd<T>(n, b, P<T>(A), lda, ul, vr, P<i64>(uptr), P<i64>(vptr));
+                cu = ul.cnt; cv = vr.cnt;
+            });
+        }
+        return py::make_tuple(cu, cv);
+    });
+    m.def("apply_refl", [](char dt, i64 ncols, uintptr_t Z, i64 ldz, uintptr_t V, i64 b, uintptr_t tau,
+                           uintptr_t row, uintptr_t len, i64 first, i64 count, bool conj_tau, uintptr_t /*st*/) {
+        py::gil_scoped_release nogil;
+        dispatch(dt, [&](auto z) {
+            using T = decltype(z);
+            apply_refl_host<T>(ncols, P<T>(Z), ldz, P<const T>(V), b, P<const T>(tau), P<const i64>(row),
+                               P<const i64>(len), first, count, conj_tau);
+        });
+    });
+    m.def("steqr", [](i64 n, uintptr_t d, uintptr_t e, uintptr_t z, i64 ldz, i64 nz) {
+        py::gil_scoped_release nogil;
+        return steqr_impl<double>(n, P<double>(d), P<double>(e), z ? P<double>(z) : nullptr, ldz, nz);
+    });
+    m.def("sterf", [](i64 n, uintptr_t d, uintptr_t e) {
+        py::gil_scoped_release nogil;
+        return steqr_impl<double>(n, P<double>(d), P<double>(e), nullptr, 1, 0);
+    });
+    m.def("bdsqr", [](i64 n, uintptr_t d, uintptr_t e, uintptr_t u, i64 ldu, i64 nu, uintptr_t vt, i64 ldvt,
+                      i64 nv) {
+        py::gil_scoped_release nogil;
+        return bdsqr_impl(n, P<double>(d), P<double>(e), u ? P<double>(u) : nullptr, ldu, nu,
+                          vt ? P<double>(vt) : nullptr, ldvt, nv);
+    });
+    m.def("secular", [](i64 n, uintptr_t d, uintptr_t z, double rho, uintptr_t org, uintptr_t mu) {
+        py::gil_scoped_release nogil;
+        secular(n, P<double>(d), P<double>(z), rho, P<i64>(org), P<double>(mu));
+    });
+}
+
+}  // namespace slate_host

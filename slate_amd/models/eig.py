@@ -1,0 +1,457 @@
+"""Hermitian eigensolvers: heev (2-stage), hegst, hegv, and the stage
+components he2hb, hb2st, sterf, steqr, stedc, unmtr_he2hb, unmtr_hb2st.
+
+Reference: `src/heev.cc:66-225` (scale -> he2hb -> gather band -> hb2st ->
+sterf/steqr/stedc -> back-transforms), `src/he2hb.cc` (panel QR + two-sided
+trailing update, square grid required), `src/hb2st.cc` (bulge chasing on
+rank 0, multithreaded host), `src/unmtr_he2hb.cc`, `src/unmtr_hb2st.cc`,
+`src/stedc*.cc`, `src/steqr.cc`, `src/sterf.cc`, `src/hegst.cc`,
+`src/hegv.cc`.
+
+MI355X design:
+* stage 1 (he2hb, 4/3 n^3 flops) runs on ONE GPU on the full Hermitian
+  matrix (288 GB HBM holds n = 100k+): the panel is the GPU recursive QR,
+  the two-sided update is three MFMA GEMMs (Y = A V T, W = Y - V M/2,
+  A -= V W^H + W V^H) -- no hemm-on-host split like SLATE's he2hb_hemm;
+* stage 2 (hb2st, O(n^2 b)) is a native C++ bulge chase on the host (like
+  SLATE), recording every reflector;
+* tridiagonal: sterf / steqr (native C++, rotations applied row-parallel)
+  or divide & conquer (stedc: secular equations in C++, the eigenvector
+  merges are GEMMs on the GPU);
+* back-transforms on the GPU: unmtr_hb2st applies one whole sweep of
+  (disjoint) reflectors per launch; unmtr_he2hb is the blocked-WY GEMM
+  update per panel.
+Multi-rank: ranks gather the matrix and run stage 1/2 redundantly
+(deterministic kernels); each rank back-transforms only its own columns of
+Z (the O(n^3) part is split over ranks) and scatters them into the
+block-cyclic Z.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _native, ops
+from ..core.enums import MethodEig, Option, Uplo
+from ..core.exceptions import SlateError
+from ..core.options import get_option
+from ..utils.trace import trace_block
+from ._util import conj_trans
+
+# ------------------------------------------------------------------ helpers
+
+
+def _code(dt):
+    return {torch.float32: 's', torch.float64: 'd', torch.complex64: 'c', torch.complex128: 'z'}[dt]
+
+
+def _cm(t):
+    return t.t().contiguous().t() if t.dim() == 2 and not (t.stride(0) == 1) else t
+
+
+def _dense_hermitian(A):
+    """Full Hermitian (both triangles) dense copy of a Hermitian matrix."""
+    from .aux import allgather_dense
+    D = allgather_dense(A)
+    up = A.uploPhysical()
+    if up == Uplo.Lower:
+        L = torch.tril(D)
+    elif up == Uplo.Upper:
+        L = torch.triu(D).mH
+    else:
+        return D
+    H = L + torch.tril(L, -1).mH
+    if H.is_complex():          # Hermitian: imaginary part of the diagonal is ignored (LAPACK)
+        H.diagonal().imag.zero_()
+    return H
+
+
+class He2hbFactors:
+    """Panel reflectors of stage 1: per panel k the explicit V (rows
+    (k+1)nb..n) and T."""
+
+    def __init__(self, nb):
+        self.nb = nb
+        self.panels = []
+
+
+# ------------------------------------------------------------------ stage 1
+def he2hb(Af: torch.Tensor, nb: int):
+    """Reduce the dense Hermitian Af (n x n, column-major, both triangles)
+    in place to Hermitian band form (bandwidth nb); returns He2hbFactors."""
+    n = Af.shape[0]
+    F = He2hbFactors(nb)
+    ct = conj_trans(Af.dtype)
+    with trace_block("he2hb"):
+        for k0 in range(0, max(n - nb, 0), nb):
+            r0 = k0 + nb
+            kb = min(nb, n - k0)
+            m = n - r0
+            if m <= 0:
+                break
+            P = Af[r0:, k0:k0 + kb]
+            kk = min(m, kb)
+            tau = torch.zeros(kk, dtype=Af.dtype, device=Af.device)
+            T, V = ops.geqrf(P, tau)
+            F.panels.append((r0, V, T))
+            # band part: keep R, zero the reflectors, mirror to the upper triangle
+            _zero_strict_lower(P)
+            Af[k0:k0 + kb, r0:].copy_(P.mH)
+            # two-sided update of the trailing matrix
+            A22 = Af[r0:, r0:]
+            X = ops.colmajor_empty(m, kk, Af.dtype, Af.device)
+            X.copy_(V)
+            ops.trmm('R', 'U', 'N', 'N', 1.0, T, X)                 # X = V T
+            Y = ops.colmajor_empty(m, kk, Af.dtype, Af.device)
+            ops.gemm(1.0, A22, X, 0.0, Y)                            # Y = A V T
+            Mt = ops.colmajor_empty(kk, kk, Af.dtype, Af.device)
+            ops.gemm(1.0, X, Y, 0.0, Mt, transA=ct)                  # M = T^H V^H Y
+            ops.gemm(-0.5, V, Mt, 1.0, Y)                            # W = Y - V M / 2
+            ops.gemm(-1.0, V, Y, 1.0, A22, transB=ct)                # A -= V W^H
+            ops.gemm(-1.0, Y, V, 1.0, A22, transB=ct)                # A -= W V^H
+    return F
+
+
+def _zero_strict_lower(P):
+    m, k = P.shape
+    if m > 1:
+        mask = torch.ones(m, k, dtype=torch.bool, device=P.device).tril(-1)
+        P.masked_fill_(mask, 0)
+
+
+def unmtr_he2hb(F: He2hbFactors, Z: torch.Tensor):
+    """Z := Q1 Z (Q1 = Q_0 Q_1 ... from he2hb): panels applied last-to-first."""
+    with trace_block("unmtr_he2hb"):
+        for (r0, V, T) in reversed(F.panels):
+            from .qr import _apply_qh
+            _apply_qh(V, T, Z[r0:, :], conj=False)
+    return Z
+
+
+# ------------------------------------------------------------------ stage 2
+class Hb2stFactors:
+    def __init__(self, V, tau, row, length, sweep_ptr, count, phase):
+        self.V, self.tau, self.row, self.length = V, tau, row, length
+        self.sweep_ptr, self.count, self.phase = sweep_ptr, count, phase
+
+
+def hb2st(B: torch.Tensor, nb: int):
+    """Hermitian band (dense host copy, both triangles, bandwidth nb) ->
+    real symmetric tridiagonal (d, e) + reflectors.  Runs on the host."""
+    n = B.shape[0]
+    Bh = _cm(B.detach().to("cpu")).clone()
+    Bh = _cm(Bh)
+    b = max(1, nb)
+    cap = n * (n // b + 2) + 1
+    dt = Bh.dtype
+    V = torch.zeros(cap, b, dtype=dt)
+    tau = torch.zeros(cap, dtype=dt)
+    row = torch.zeros(cap, dtype=torch.int64)
+    ln = torch.zeros(cap, dtype=torch.int64)
+    sp = torch.zeros(max(n, 1), dtype=torch.int64)
+    with trace_block("hb2st"):
+        cnt = _native._host.hb2st(_code(dt), n, b, Bh.data_ptr(), max(1, Bh.stride(1)), V.data_ptr(),
+                                  tau.data_ptr(), row.data_ptr(), ln.data_ptr(), cap, sp.data_ptr())
+    d = Bh.diagonal().real.to(torch.float64).clone()
+    ec = Bh.diagonal(-1).clone()
+    ph = torch.ones(n, dtype=dt)
+    if dt.is_complex and n > 1:
+        a = ec.abs()
+        u = torch.where(a > 0, ec / torch.where(a > 0, a, torch.ones_like(a)), torch.ones_like(ec))
+        ph[1:] = torch.cumprod(u, 0)
+        e = a.to(torch.float64)
+    else:
+        e = ec.real.to(torch.float64) if dt.is_complex else ec.to(torch.float64)
+    return d, e, Hb2stFactors(V[:cnt], tau[:cnt], row[:cnt], ln[:cnt], sp, cnt, ph)
+
+
+def unmtr_hb2st(F: Hb2stFactors, Z: torch.Tensor):
+    """Z := Q2 Phase Z: one launch per sweep, sweeps last-to-first."""
+    if F.phase is not None and Z.dtype.is_complex:
+        Z.mul_(F.phase.to(Z.device)[:, None])
+    dev = Z.device
+    V, tau, row, ln = (x.to(dev) for x in (F.V, F.tau, F.row, F.length))
+    sp = F.sweep_ptr.tolist()
+    n = len(sp)
+    with trace_block("unmtr_hb2st"):
+        for j in range(n - 1, -1, -1):
+            first = sp[j]
+            last = sp[j + 1] if j + 1 < n else F.count
+            if last > first:
+                ops.apply_refl(Z, V, tau, row, ln, first, last - first)
+    return Z
+
+
+# ------------------------------------------------------------------ tridiagonal
+def sterf(d: torch.Tensor, e: torch.Tensor) -> torch.Tensor:
+    """Eigenvalues of the symmetric tridiagonal (d, e), ascending."""
+    d = d.to(torch.float64).cpu().clone()
+    e = e.to(torch.float64).cpu().clone()
+    n = d.numel()
+    if n and _native._host.sterf(n, d.data_ptr(), e.data_ptr() if n > 1 else d.data_ptr()):
+        raise SlateError("sterf: no convergence")
+    return d
+
+
+def steqr(d: torch.Tensor, e: torch.Tensor, Z0=None):
+    """Eigenvalues + vectors of the tridiagonal; Z0 (n x k host) is
+    rotated as Z0 Q (default: identity -> Q)."""
+    d = d.to(torch.float64).cpu().clone()
+    e = e.to(torch.float64).cpu().clone()
+    n = d.numel()
+    Z = torch.eye(n, dtype=torch.float64) if Z0 is None else Z0.to(torch.float64).cpu().clone()
+    Z = _cm(Z)
+    if n:
+        f = _native._host.steqr(n, d.data_ptr(), e.data_ptr() if n > 1 else d.data_ptr(), Z.data_ptr(),
+                                max(1, Z.stride(1)), Z.shape[0])
+        if f:
+            raise SlateError("steqr: no convergence")
+    return d, Z
+
+
+def stedc(d: torch.Tensor, e: torch.Tensor, device=None, leaf=64):
+    """Divide & conquer (Cuppen / Gu-Eisenstat) for the symmetric
+    tridiagonal (d, e): returns ascending eigenvalues (host fp64) and Z.
+    Merges (GEMMs) run on `device` (GPU when given)."""
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    d = d.to(torch.float64).cpu()
+    e = e.to(torch.float64).cpu()
+    with trace_block("stedc"):
+        w, Z = _dc(d, e, dev, leaf)
+    return w, Z
+
+
+def _dc(d, e, dev, leaf):
+    n = d.numel()
+    if n <= leaf:
+        w, Z = steqr(d, e)
+        return w, Z.to(dev)
+    m = n // 2
+    rho = float(e[m - 1])
+    d1 = d[:m].clone()
+    d2 = d[m:].clone()
+    d1[-1] -= rho
+    d2[0] -= rho
+    w1, Q1 = _dc(d1, e[:m - 1], dev, leaf)
+    w2, Q2 = _dc(d2, e[m:], dev, leaf)
+    z = torch.cat([Q1[-1, :].cpu(), Q2[0, :].cpu()]).to(torch.float64)
+    dd = torch.cat([w1, w2])
+    Qb = torch.zeros(n, n, dtype=torch.float64, device=dev)
+    Qb[:m, :m] = Q1
+    Qb[m:, m:] = Q2
+    w, U = _rank_one_eig(dd, z, rho, Qb)
+    return w, U
+
+
+def _rank_one_eig(dd, z, rho, Qb):
+    """Eigen-decomposition of Qb (diag(dd) + rho z z^T) Qb^T: returns
+    (ascending eigenvalues, Qb @ eigenvectors)."""
+    n = dd.numel()
+    dev = Qb.device
+    if rho == 0.0:
+        order = torch.argsort(dd)
+        return dd[order].clone(), Qb[:, order.to(dev)]
+    flip = rho < 0
+    if flip:
+        dd = -dd
+        rho = -rho
+    order = torch.argsort(dd)
+    dd = dd[order].clone()
+    z = z[order].clone()
+    Q = Qb[:, order.to(dev)].clone()
+    eps = torch.finfo(torch.float64).eps
+    tol = 8.0 * eps * max(dd.abs().max().item(), rho * float((z * z).sum()))
+    znorm = float(z.norm())
+    # deflation of tiny z components
+    defl = (rho * z.abs() * znorm <= tol)
+    # deflation of (nearly) equal poles: rotate z weight into one of them
+    idx = [i for i in range(n) if not defl[i]]
+    zl = z.tolist()
+    dl = dd.tolist()
+    keep = []
+    rots = []
+    prev = None
+    for i in idx:
+        if prev is not None and abs(dl[i] - dl[prev]) <= tol:
+            a, b = zl[prev], zl[i]
+            r = (a * a + b * b) ** 0.5
+            c, s = b / r, a / r
+            # new z_prev = 0, z_i = r ; columns (prev, i) rotated
+            rots.append((prev, i, c, s))
+            zl[prev], zl[i] = 0.0, r
+            dl[prev] = dl[prev]  # eigenvalue stays (deflated)
+            defl[prev] = True
+            keep[-1] = i
+            prev = i
+            continue
+        keep.append(i)
+        prev = i
+    for (i, j, c, s) in rots:
+        qi, qj = Q[:, i].clone(), Q[:, j].clone()
+        Q[:, i] = c * qi - s * qj
+        Q[:, j] = s * qi + c * qj
+    z = torch.tensor(zl, dtype=torch.float64)
+    K = torch.tensor(keep, dtype=torch.int64)
+    k = K.numel()
+    lam = dd.clone()
+    if k:
+        dK = dd[K].contiguous()
+        zK = z[K].contiguous()
+        org = torch.zeros(k, dtype=torch.int64)
+        mu = torch.zeros(k, dtype=torch.float64)
+        _native._host.secular(k, dK.data_ptr(), zK.data_ptr(), float(rho), org.data_ptr(), mu.data_ptr())
+        lamK = dK[org] + mu
+        # Gu-Eisenstat: z_hat from the computed roots (orthogonal vectors)
+        dorg = dK[org]                                   # (k,)
+        delta = (dorg[None, :] - dK[:, None]) + mu[None, :]   # lambda_j - d_i, (k x k)
+        dij = dK[None, :] - dK[:, None]                  # d_j - d_i
+        ratio = delta / torch.where(dij == 0, torch.ones_like(dij), dij)
+        ratio.fill_diagonal_(1.0)
+        zh2 = torch.diagonal(delta).clone() * torch.prod(ratio, dim=1) / rho
+        zh = torch.sign(zK) * zh2.abs().sqrt()
+        Vs = zh[:, None] / (-delta)                      # v_j[i] = z_i / (d_i - lambda_j)
+        Vs = Vs / Vs.norm(dim=0, keepdim=True)
+        lam[K] = lamK
+        QK = Q[:, K.to(dev)]
+        Q[:, K.to(dev)] = QK @ Vs.to(dev)
+    if flip:
+        lam = -lam
+    o2 = torch.argsort(lam)
+    return lam[o2].clone(), Q[:, o2.to(dev)].contiguous()
+
+
+# ------------------------------------------------------------------ drivers
+def heev(A, Lambda=None, Z=None, opts=None):
+    """Eigenvalues (ascending, returned and copied into Lambda if given) and,
+    if Z is given, eigenvectors of the Hermitian matrix A (A is destroyed
+    like in SLATE)."""
+    from .aux import from_dense
+    with trace_block("heev"):
+        s = A.storage
+        dev = s.device if s.device.type == "cuda" else torch.device("cpu")
+        nb = int(get_option(opts, Option.InnerBlocking, 0)) or min(s.bc.nb if s.bc else 64, 128)
+        method = get_option(opts, Option.MethodEig, MethodEig.DC)
+        Af = _cm(_dense_hermitian(A).to(dev))
+        n = Af.shape[0]
+        # scale to a safe range (heev.cc:66-80)
+        amax = Af.abs().max().item() if n else 0.0
+        scale = 1.0
+        if amax > 0 and (amax < 1e-140 or amax > 1e140):
+            scale = 1.0 / amax
+            Af.mul_(scale)
+        F1 = he2hb(Af, nb)
+        d, e, F2 = hb2st(_band_only(Af, nb), nb)
+        want = Z is not None
+        if not want:
+            w = sterf(d, e)
+        elif method in (MethodEig.QR, 'Q', "qr"):
+            w, Zt = steqr(d, e)
+        else:
+            w, Zt = stedc(d, e, device=dev)
+        if scale != 1.0:
+            w = w / scale
+        if want:
+            # back-transform only this rank's columns of Z
+            cols = _my_cols(Z)
+            Zl = _cm(Zt.to(dev)[:, cols].to(Af.dtype)) if len(cols) else \
+                torch.zeros(n, 0, dtype=Af.dtype, device=dev)
+            Zl = _cm(Zl.clone())
+            unmtr_hb2st(F2, Zl)
+            unmtr_he2hb(F1, Zl)
+            _scatter_cols(Z, Zl, cols)
+        if Lambda is not None:
+            Lambda.copy_(w.to(Lambda.dtype).to(Lambda.device))
+        return w
+
+
+def _band_only(Af, nb):
+    n = Af.shape[0]
+    i = torch.arange(n, device=Af.device)
+    mask = (i[:, None] - i[None, :]).abs() <= nb
+    return torch.where(mask, Af, torch.zeros_like(Af))
+
+
+def _my_cols(Z):
+    """Global column indices whose data this rank holds in Z's local block."""
+    s = Z.storage
+    if s.bc is None:
+        return list(range(Z.n()))
+    lb = Z.local_block()
+    return [lb.global_col(j) for j in range(lb.nloc)]
+
+
+def _scatter_cols(Z, Zl, cols):
+    """Write the n x len(cols) block Zl into this rank's local part of Z."""
+    s = Z.storage
+    lb = Z.local_block()
+    if s.bc is None or lb.mloc == 0 or lb.nloc == 0:
+        return
+    rows = torch.tensor([lb.global_row(i) for i in range(lb.mloc)], device=Zl.device)
+    lb.data.copy_(Zl[rows].to(lb.data.device, lb.data.dtype))
+    s.mark_local_modified(s.origin_slot)
+
+
+def eig_vals(A, Lambda=None, opts=None):
+    return heev(A, Lambda, None, opts)
+
+
+def eig(A, Lambda=None, Z=None, opts=None):
+    return heev(A, Lambda, Z, opts)
+
+
+def hegst(itype, A, B, opts=None):
+    """Reduce the generalized problem to standard form with the Cholesky
+    factor L of B (B = L L^H, from potrf): itype 1: A := L^{-1} A L^{-H};
+    itype 2/3: A := L^H A L."""
+    from .aux import from_dense, allgather_dense
+    with trace_block("hegst"):
+        Ad = _dense_hermitian(A)
+        Bd = allgather_dense(B)
+        L = torch.tril(Bd) if B.uploPhysical() == Uplo.Lower else torch.triu(Bd).mH
+        dev = Ad.device
+        Lc, Ac = _cm(L.clone()), _cm(Ad.clone())
+        if itype == 1:
+            ops.trsm('L', 'L', 'N', 'N', 1.0, Lc, Ac)
+            X = _cm(Ac.mH.contiguous())
+            ops.trsm('L', 'L', 'N', 'N', 1.0, Lc, X)
+            R = X.mH
+        else:
+            ops.trmm('L', 'L', 'C' if Ad.dtype.is_complex else 'T', 'N', 1.0, Lc, Ac)
+            X = _cm(Ac.mH.contiguous())
+            ops.trmm('L', 'L', 'C' if Ad.dtype.is_complex else 'T', 'N', 1.0, Lc, X)
+            R = X.mH
+        R = 0.5 * (R + R.mH)
+        from_dense(A, _store_tri(R, A))
+    return 0
+
+
+def _store_tri(R, A):
+    up = A.uploPhysical()
+    if up == Uplo.Lower:
+        return torch.tril(R)
+    if up == Uplo.Upper:
+        return torch.triu(R)
+    return R
+
+
+def hegv(itype, A, B, Lambda=None, Z=None, opts=None):
+    """Generalized Hermitian-definite eigenproblem (src/hegv.cc): potrf(B),
+    hegst, heev, back-substitution of the eigenvectors."""
+    from .chol import potrf
+    from .blas3 import trsm, trmm
+    from ..core.matrix import TriangularMatrix
+    from ..core.enums import Diag, Side
+    with trace_block("hegv"):
+        info = potrf(B, opts)
+        if info:
+            return None
+        hegst(itype, A, B, opts)
+        w = heev(A, Lambda, Z, opts)
+        if Z is not None:
+            lower = B.uploPhysical() == Uplo.Lower
+            Tb = TriangularMatrix(Uplo.Lower if lower else Uplo.Upper, B, diag=Diag.NonUnit)
+            L = Tb if lower else Tb.conj_transpose()          # B = L L^H
+            if itype in (1, 2):
+                trsm(Side.Left, 1.0, L.conj_transpose(), Z, opts)   # x = L^{-H} y
+            else:
+                trmm(Side.Left, 1.0, L, Z, opts)                    # x = L y
+        return w

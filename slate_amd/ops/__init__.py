@@ -342,3 +342,16 @@ def matgen(kind: int, seed: int, A, m, n, mb, p, pr, nb, q, pc, row0=0, col0=0, 
         kmod(A).matgen(code(A.dtype), int(kind), int(seed) & ((1 << 64) - 1), mloc, nloc, A.data_ptr(), ld(A),
                        m, n, mb, p, pr, nb, q, pc, row0, col0, float(scale), *( [stream(A)] if A.is_cuda else []))
     return A
+
+
+# ------------------------------------------------------------- eig / svd
+def apply_refl(Z, V, tau, row, length, first, count, conj_tau=False):
+    """Z := H_k Z for the recorded bulge-chasing reflectors k in
+    [first, first+count) (disjoint row ranges: one launch).  V is
+    (count_total x b) row-major, row/length int64."""
+    _chk(Z, "Z")
+    if count <= 0 or Z.shape[1] == 0:
+        return Z
+    kmod(Z).apply_refl(code(Z.dtype), Z.shape[1], Z.data_ptr(), ld(Z), V.data_ptr(), V.shape[1], tau.data_ptr(),
+                       row.data_ptr(), length.data_ptr(), int(first), int(count), bool(conj_tau), stream(Z))
+    return Z

@@ -1,0 +1,164 @@
+"""Eigenvalue / SVD drivers (reference: test/test_heev.cc, test_hegv.cc,
+test_svd.cc, test_stedc*.cc -- residual ||A Z - Z Lambda|| / (||A|| n),
+orthogonality ||Z^H Z - I|| / n, values vs. a sequential reference)."""
+import pytest
+import torch
+
+import slate_amd as sl
+from slate_amd.core.enums import MethodEig, Option, Uplo
+from slate_amd.models import eig as E
+from slate_amd.models import svd as S
+from slate_amd.models.aux import allgather_dense as D
+
+from dist_util import run_dist
+
+
+def _herm(n, nb, dt, uplo, p=1, q=1, seed=3, device=None):
+    A = sl.HermitianMatrix(uplo, n, nb=nb, p=p, q=q, dtype=dt, device=device)
+    A.insertLocalTiles(device=-1 if device is None else 0)
+    sl.generate_matrix(A, "rands", seed)
+    return A
+
+
+def _check_heev(n, nb, dt, uplo, method, p=1, q=1, device=None, ib=16):
+    A = _herm(n, nb, dt, uplo, p, q, device=device)
+    Af = E._dense_hermitian(A).cpu()
+    Z = sl.Matrix(n, n, nb=nb, p=p, q=q, dtype=dt, device=device)
+    Z.insertLocalTiles(device=-1 if device is None else 0)
+    w = sl.heev(A, None, Z, {Option.InnerBlocking: ib, Option.MethodEig: method})
+    Zd = D(Z).cpu()
+    wr = torch.linalg.eigvalsh(Af)
+    sc = max(1.0, Af.abs().max().item()) * n
+    assert (w.cpu() - wr).abs().max().item() / sc < 1e-13
+    assert (Af @ Zd - Zd * w.to(dt).cpu()).abs().max().item() / sc < 1e-13
+    assert (Zd.mH @ Zd - torch.eye(n, dtype=dt)).abs().max().item() / n < 1e-13
+
+
+@pytest.mark.parametrize("dt", [torch.float64, torch.complex128])
+@pytest.mark.parametrize("uplo", [Uplo.Lower, Uplo.Upper])
+@pytest.mark.parametrize("method", [MethodEig.DC, MethodEig.QR])
+def test_heev(dt, uplo, method):
+    _check_heev(130, 32, dt, uplo, method)
+
+
+def test_heev_values_only():
+    A = _herm(100, 32, torch.float64, Uplo.Lower)
+    Af = E._dense_hermitian(A)
+    w = sl.eig_vals(A)
+    assert (w - torch.linalg.eigvalsh(Af)).abs().max().item() < 1e-12
+
+
+def test_stedc_steqr_sterf():
+    torch.manual_seed(1)
+    n = 257
+    d, e = torch.randn(n, dtype=torch.float64), torch.randn(n - 1, dtype=torch.float64)
+    T = torch.diag(d) + torch.diag(e, 1) + torch.diag(e, -1)
+    wr = torch.linalg.eigvalsh(T)
+    assert (sl.sterf(d, e) - wr).abs().max() < 1e-12
+    for w, Z in (sl.steqr(d, e), sl.stedc(d, e, leaf=16)):
+        assert (w - wr).abs().max() < 1e-12
+        assert (T @ Z - Z * w).abs().max() < 1e-12
+        assert (Z.T @ Z - torch.eye(n, dtype=torch.float64)).abs().max() < 1e-12
+    # clustered / repeated eigenvalues (deflation paths)
+    d2 = torch.ones(n, dtype=torch.float64)
+    d2[::3] = 2.0
+    e2 = torch.full((n - 1,), 1e-9, dtype=torch.float64)
+    T2 = torch.diag(d2) + torch.diag(e2, 1) + torch.diag(e2, -1)
+    w, Z = sl.stedc(d2, e2, leaf=16)
+    assert (T2 @ Z - Z * w).abs().max() < 1e-12
+    assert (Z.T @ Z - torch.eye(n, dtype=torch.float64)).abs().max() < 1e-11
+
+
+@pytest.mark.parametrize("itype", [1, 2, 3])
+def test_hegv(itype):
+    n, nb = 80, 16
+    dt = torch.float64
+    A = _herm(n, nb, dt, Uplo.Lower, seed=4)
+    Bm = sl.HermitianMatrix(Uplo.Lower, n, nb=nb, dtype=dt)
+    Bm.insertLocalTiles()
+    sl.generate_matrix(Bm, "poev", 5)
+    Af, Bf = E._dense_hermitian(A), E._dense_hermitian(Bm)
+    Z = sl.Matrix(n, n, nb=nb, dtype=dt)
+    Z.insertLocalTiles()
+    w = sl.hegv(itype, A, Bm, None, Z, {Option.InnerBlocking: 16})
+    X = D(Z)
+    if itype == 1:
+        R = Af @ X - Bf @ X * w
+    elif itype == 2:
+        R = Af @ Bf @ X - X * w
+    else:
+        R = Bf @ Af @ X - X * w
+    assert R.abs().max().item() / (Af.abs().max() * Bf.abs().max() * n).item() < 1e-12
+
+
+@pytest.mark.parametrize("dt", [torch.float64, torch.complex128])
+@pytest.mark.parametrize("shape", [(120, 80), (80, 120), (64, 64)])
+def test_svd(dt, shape):
+    m, n = shape
+    k = min(m, n)
+    A = sl.Matrix(m, n, nb=32, dtype=dt)
+    A.insertLocalTiles()
+    sl.generate_matrix(A, "rands", 3)
+    Ad = D(A).clone()
+    U = sl.Matrix(m, k, nb=32, dtype=dt)
+    U.insertLocalTiles()
+    VH = sl.Matrix(k, n, nb=32, dtype=dt)
+    VH.insertLocalTiles()
+    s = sl.svd(A, None, U, VH, {Option.InnerBlocking: 16})
+    Ud, Vd = D(U), D(VH)
+    assert (s - torch.linalg.svdvals(Ad)).abs().max().item() < 1e-12
+    assert (Ud @ torch.diag(s.to(dt)) @ Vd - Ad).abs().max().item() < 1e-12
+    assert (Ud.mH @ Ud - torch.eye(k, dtype=dt)).abs().max().item() < 1e-12
+    assert (Vd @ Vd.mH - torch.eye(k, dtype=dt)).abs().max().item() < 1e-12
+
+
+def test_svd_vals_bdsqr():
+    torch.manual_seed(2)
+    n = 200
+    d, e = torch.randn(n, dtype=torch.float64), torch.randn(n - 1, dtype=torch.float64)
+    B = torch.diag(d) + torch.diag(e, 1)
+    s, U, VT = sl.bdsqr(d, e)
+    assert (s - torch.linalg.svdvals(B)).abs().max() < 1e-12
+    assert (U @ torch.diag(s) @ VT - B).abs().max() < 1e-12
+
+
+def _dist_eig(rank, size, p, q):
+    _check_heev(90, 16, torch.float64, Uplo.Lower, MethodEig.DC, p, q)
+    A = sl.Matrix(70, 50, nb=16, p=p, q=q)
+    A.insertLocalTiles()
+    sl.generate_matrix(A, "rands", 9)
+    Ad = D(A).clone()
+    U = sl.Matrix(70, 50, nb=16, p=p, q=q)
+    U.insertLocalTiles()
+    VH = sl.Matrix(50, 50, nb=16, p=p, q=q)
+    VH.insertLocalTiles()
+    s = sl.svd(A, None, U, VH, {Option.InnerBlocking: 8})
+    assert (D(U) @ torch.diag(s) @ D(VH) - Ad).abs().max().item() < 1e-12
+
+
+@pytest.mark.parametrize("grid", [(2, 1), (1, 2)])
+def test_eig_svd_distributed(grid):
+    run_dist(_dist_eig, 2, *grid)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float64, torch.complex128])
+def test_heev_gpu(dt):
+    _check_heev(600, 128, dt, Uplo.Lower, MethodEig.DC, device=torch.device("cuda"), ib=64)
+
+
+@pytest.mark.gpu
+def test_svd_gpu():
+    dev = torch.device("cuda")
+    m, n = 500, 300
+    A = sl.Matrix(m, n, nb=128, dtype=torch.float64, device=dev)
+    A.insertLocalTiles(device=0)
+    sl.generate_matrix(A, "rands", 3)
+    Ad = D(A).clone()
+    U = sl.Matrix(m, n, nb=128, device=dev)
+    U.insertLocalTiles(device=0)
+    VH = sl.Matrix(n, n, nb=128, device=dev)
+    VH.insertLocalTiles(device=0)
+    s = sl.svd(A, None, U, VH, {Option.InnerBlocking: 64})
+    assert (s.cpu() - torch.linalg.svdvals(Ad.cpu())).abs().max().item() < 1e-11
+    assert (D(U) @ torch.diag(s.to(dev)) @ D(VH) - Ad).abs().max().item() < 1e-11
