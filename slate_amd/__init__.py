@@ -128,3 +128,21 @@ def least_squares_solve(A, BX, opts=None):
 from .models.eig import (  # noqa: F401,E402
     eig, eig_vals, hb2st, he2hb, heev, hegst, hegv, stedc, steqr, sterf, unmtr_hb2st, unmtr_he2hb)
 from .models.svd import bdsqr, ge2tb, svd, svd_vals, tb2bd  # noqa: F401,E402
+
+
+from .models.inverse import trtri, trtrm  # noqa: F401,E402
+from .models.condest import gecondest, norm1est, pocondest, trcondest  # noqa: F401,E402
+from .models.mixed import (  # noqa: F401,E402
+    gerbt, gesv_mixed, gesv_mixed_gmres, gesv_rbt, posv_mixed, posv_mixed_gmres)
+
+
+def lu_rcondest_using_factor(norm_type, A, pivots, anorm, opts=None):
+    return gecondest(norm_type, A, pivots, anorm, opts)
+
+
+def chol_rcondest_using_factor(norm_type, A, anorm, opts=None):
+    return pocondest(norm_type, A, anorm, opts)
+
+
+def triangular_rcondest(norm_type, A, anorm=None, opts=None):
+    return trcondest(norm_type, A, anorm, opts)

@@ -1,0 +1,108 @@
+"""Triangular inverse and product: trtri, trtrm (used by potri / getri).
+
+Reference: `src/trtri.cc`, `src/trtrm.cc`, `internal_trtri.cc`,
+`internal_trtrm.cc`, `src/potri.cc`.
+
+MI355X design: on one GPU (or one rank) the inverse is the gfx950 tri_inv
+kernel chain (block-diagonal 64x64 inverses + doubling MFMA GEMMs) and
+trtrm is one trmm; on a grid both are expressed through the distributed
+trsm/trmm drivers (T^{-1} = trsm(T, I)), so no separate communication
+pattern is needed.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import ops
+from ..core.enums import Diag, Side, Uplo
+from ..core.exceptions import SlateError
+from ..core.matrix import TriangularMatrix
+from ..utils.trace import trace_block
+
+
+def _single(A):
+    s = A.storage
+    return s.comm.size == 1 or (s.bc is not None and s.bc.p * s.bc.q == 1)
+
+
+def trtri(A, opts=None) -> int:
+    """In-place inverse of a triangular matrix; returns info (first zero
+    diagonal, 1-based)."""
+    with trace_block("trtri"):
+        s = A.storage
+        uplo = A.uploPhysical()
+        diag = A.diag() if hasattr(A, "diag") else Diag.NonUnit
+        dch = 'U' if diag == Diag.Unit else 'N'
+        uch = 'L' if uplo == Uplo.Lower else 'U'
+        n = A.n()
+        if _single(A):
+            lb = A.local_block()
+            F = lb.data[:n, :n]
+            info = ops.trtri(uch, dch, F)
+            s.mark_local_modified(s.origin_slot)
+            return int(info.item()) if isinstance(info, torch.Tensor) else int(info)
+        # distributed: X = T^{-1} via trsm against the identity, written back
+        from .aux import allgather_dense, set as aset, copy
+        D = allgather_dense(A)
+        dg = torch.diagonal(D)
+        if dch == 'N':
+            z = (dg == 0).nonzero()
+            if z.numel():
+                return int(z[0].item()) + 1
+        from ..core.matrix import Matrix
+        bc = s.bc
+        X = Matrix(n, n, nb=bc.nb, p=bc.p, q=bc.q, comm=s.comm, dtype=s.dtype, device=s.device, order=bc.order)
+        X.insertLocalTiles(device=s.device.index if s.device.type == "cuda" else -1)
+        aset(0.0, 1.0, X)
+        from .blas3 import trsm
+        trsm(Side.Left, 1.0, A, X, opts)
+        _copy_tri(X, A)
+        return 0
+
+
+def _copy_tri(X, A):
+    """Copy the stored triangle of X into triangular A."""
+    from .aux import allgather_dense, from_dense
+    D = allgather_dense(X)
+    up = A.uploPhysical()
+    D = torch.tril(D) if up == Uplo.Lower else torch.triu(D)
+    from_dense(A, D)
+
+
+def trtrm(A, opts=None) -> int:
+    """A := L^H L (lower) or U U^H (upper), Hermitian result in the stored
+    triangle (LAPACK lauum)."""
+    with trace_block("trtrm"):
+        s = A.storage
+        uplo = A.uploPhysical()
+        n = A.n()
+        ct = 'C' if s.dtype.is_complex else 'T'
+        if _single(A):
+            lb = A.local_block()
+            F = lb.data[:n, :n]
+            if uplo == Uplo.Lower:
+                L = torch.tril(F)
+                X = ops.colmajor_empty(n, n, F.dtype, F.device)
+                X.copy_(L)
+                ops.trmm('L', 'L', ct, 'N', 1.0, F, X)          # X = L^H L
+                F.copy_(torch.where(torch.ones_like(F, dtype=torch.bool).tril(), X, F))
+            else:
+                U = torch.triu(F)
+                X = ops.colmajor_empty(n, n, F.dtype, F.device)
+                X.copy_(U)
+                ops.trmm('R', 'U', ct, 'N', 1.0, F, X)          # X = U U^H
+                F.copy_(torch.where(torch.ones_like(F, dtype=torch.bool).triu(), X, F))
+            s.mark_local_modified(s.origin_slot)
+            return 0
+        from .aux import allgather_dense, from_dense
+        D = ops.as_colmajor(allgather_dense(A).clone())
+        X = ops.colmajor_empty(n, n, D.dtype, D.device)
+        if uplo == Uplo.Lower:
+            X.copy_(torch.tril(D))
+            ops.trmm('L', 'L', ct, 'N', 1.0, D, X)
+            from_dense(A, torch.tril(X))
+        else:
+            X.copy_(torch.triu(D))
+            ops.trmm('R', 'U', ct, 'N', 1.0, D, X)
+            from_dense(A, torch.triu(X))
+        return 0

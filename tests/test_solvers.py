@@ -1,0 +1,113 @@
+"""Mixed precision (gesv_mixed[_gmres], posv_mixed[_gmres]), RBT, inverses
+(getri, potri, trtri), condition estimates (reference: test_gesv.cc with
+--method-gesv, test_posv.cc, test_getri.cc, test_potri.cc, test_gecondest.cc,
+test_pocondest.cc, test_trcondest.cc)."""
+import pytest
+import torch
+
+import slate_amd as sl
+from slate_amd.models.aux import allgather_dense as D
+
+from dist_util import run_dist
+
+
+def mk(kind, seed, m, n, nb=32, p=1, q=1, herm=False, dt=torch.float64):
+    M = sl.HermitianMatrix(sl.Uplo.Lower, m, nb=nb, p=p, q=q, dtype=dt) if herm else \
+        sl.Matrix(m, n, nb=nb, p=p, q=q, dtype=dt)
+    M.insertLocalTiles()
+    sl.generate_matrix(M, kind, seed)
+    return M
+
+
+def full(H):
+    X = D(H)
+    return torch.tril(X) + torch.tril(X, -1).mH
+
+
+def check_mixed(p=1, q=1):
+    n = 96
+    A = mk("rand_dominant", 1, n, n, p=p, q=q)
+    B = mk("rands", 2, n, 2, p=p, q=q)
+    X = sl.Matrix(n, 2, nb=32, p=p, q=q)
+    X.insertLocalTiles()
+    A0, B0 = D(A).clone(), D(B).clone()
+    info, it = sl.gesv_mixed(A, sl.Pivots(), B, X)
+    assert info == 0 and it >= 0
+    assert (A0 @ D(X) - B0).abs().max() < 1e-13
+    H = mk("poev", 3, n, n, p=p, q=q, herm=True)
+    Hf = full(H)
+    info, it = sl.posv_mixed(H, B, X)
+    assert info == 0 and (Hf @ D(X) - B0).abs().max() < 1e-13
+    B1 = mk("rands", 4, n, 1, p=p, q=q)
+    X1 = sl.Matrix(n, 1, nb=32, p=p, q=q)
+    X1.insertLocalTiles()
+    B1d = D(B1).clone()
+    info, it = sl.gesv_mixed_gmres(A, sl.Pivots(), B1, X1)
+    assert info == 0 and (A0 @ D(X1) - B1d).abs().max() < 1e-13
+    info, it = sl.posv_mixed_gmres(H, B1, X1)
+    assert info == 0 and (Hf @ D(X1) - B1d).abs().max() < 1e-13
+
+
+def check_inverses(p=1, q=1):
+    n = 80
+    A = mk("rands", 5, n, n, p=p, q=q)
+    A0 = D(A).clone()
+    piv = sl.Pivots()
+    assert sl.getrf(A, piv) == 0
+    sl.getri(A, piv)
+    assert (D(A) @ A0 - torch.eye(n, dtype=A0.dtype)).abs().max() < 1e-11
+    H = mk("poev", 6, n, n, p=p, q=q, herm=True)
+    Hf = full(H)
+    assert sl.potrf(H) == 0
+    assert sl.potri(H) == 0
+    assert (full(H) @ Hf - torch.eye(n, dtype=Hf.dtype)).abs().max() < 1e-11
+    T = mk("rands", 7, n, n, p=p, q=q)
+    Td = torch.tril(D(T)) + n * torch.eye(n, dtype=torch.float64)
+    sl.from_dense(T, Td)
+    L = sl.TriangularMatrix(sl.Uplo.Lower, T)
+    assert sl.trtri(L) == 0
+    assert (torch.tril(D(T)) @ Td - torch.eye(n, dtype=Td.dtype)).abs().max() < 1e-12
+
+
+def check_condest(p=1, q=1):
+    n = 64
+    A = mk("rands", 8, n, n, p=p, q=q)
+    Ad = D(A).clone()
+    anorm = float(sl.norm(sl.Norm.One, A))
+    piv = sl.Pivots()
+    sl.getrf(A, piv)
+    rc = sl.gecondest(sl.Norm.One, A, piv, anorm)
+    ref = 1 / (torch.linalg.norm(Ad, 1) * torch.linalg.norm(torch.linalg.inv(Ad), 1)).item()
+    assert ref / 3 <= rc <= 3 * ref
+
+
+def test_mixed():
+    check_mixed()
+
+
+def test_rbt():
+    n = 128
+    A = mk("rands", 9, n, n)
+    B = mk("rands", 10, n, 3)
+    A0, B0 = D(A).clone(), D(B).clone()
+    assert sl.gesv_rbt(A, B) == 0
+    assert (A0 @ D(B) - B0).abs().max() < 1e-11
+
+
+def test_inverses():
+    check_inverses()
+
+
+def test_condest():
+    check_condest()
+
+
+def _dist(rank, size, p, q):
+    check_mixed(p, q)
+    check_inverses(p, q)
+    check_condest(p, q)
+
+
+@pytest.mark.parametrize("grid", [(2, 1), (1, 2)])
+def test_solvers_distributed(grid):
+    run_dist(_dist, 2, *grid)
