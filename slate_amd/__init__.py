@@ -146,3 +146,20 @@ def chol_rcondest_using_factor(norm_type, A, anorm, opts=None):
 
 def triangular_rcondest(norm_type, A, anorm=None, opts=None):
     return trcondest(norm_type, A, anorm, opts)
+
+
+from .models.band import (  # noqa: F401,E402
+    band_mask, gbmm, gbsv, gbtrf, gbtrs, hbmm, pbsv, pbtrf, pbtrs, tbsm)
+from .models.hetrf import hesv, hetrf, hetrs, sysv, sytrf, sytrs  # noqa: F401,E402
+
+
+def indefinite_factor(A, pivots, T, pivots2, H, opts=None):
+    return hetrf(A, pivots, T, pivots2, H, opts)
+
+
+def indefinite_solve_using_factor(A, pivots, T, pivots2, B, opts=None):
+    return hetrs(A, pivots, T, pivots2, B, opts)
+
+
+def indefinite_solve(A, B, opts=None):
+    return hesv(A, Pivots(), None, None, None, B, opts)
