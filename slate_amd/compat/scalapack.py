@@ -1,0 +1,293 @@
+"""ScaLAPACK-style API: `pdpotrf(uplo, n, a, ia, ja, desca)` etc. on this
+rank's ScaLAPACK local arrays.
+
+Reference: `scalapack_api/` (`pdpotrf_`-style interposers that wrap the
+user's ScaLAPACK arrays with `fromScaLAPACK` + BLACS grid info, env
+SLATE_SCALAPACK_TARGET / LOOKAHEAD / VERBOSE,
+`scalapack_api/scalapack_slate.hh:30-131`).
+
+There is no MPI/BLACS here: the process grid comes from
+`blacs_gridinit(p, q, order)` over the torch.distributed world (RCCL on
+GPUs), which returns a context id used in descriptor slot 1.  Descriptors
+follow ScaLAPACK: desc = [dtype, ctxt, m, n, mb, nb, rsrc, csrc, lld].
+Local arrays (numpy or torch, host or device) are wrapped zero-copy when
+already on the target device; host arrays are staged to the rank's GPU
+for Target=devices (SLATE_AMD_SCALAPACK_TARGET=host|devices).  Global
+sub-matrix offsets ia, ja must be 1 (whole distributed matrices) and
+rsrc = csrc = 0.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from ..core.enums import Diag, GridOrder, Norm, Op, Option, Side, Target, Uplo
+from ..core.exceptions import SlateError
+from ..core.matrix import HermitianMatrix, Matrix, Pivots, TriangularFactors, TriangularMatrix
+from ..parallel import comm as _comm
+
+_PFX = {'s': torch.float32, 'd': torch.float64, 'c': torch.complex64, 'z': torch.complex128}
+_CTX = {}
+
+
+def blacs_gridinit(p, q, order="C"):
+    """Create a p x q process-grid context over the world communicator."""
+    world = _comm.world()
+    if p * q != world.size:
+        raise SlateError(f"grid {p}x{q} does not match world size {world.size}")
+    ctxt = len(_CTX) + 1
+    _CTX[ctxt] = (p, q, GridOrder.from_string(order) if isinstance(order, str) else order)
+    return ctxt
+
+
+def blacs_gridinfo(ctxt):
+    p, q, order = _CTX[ctxt]
+    r = _comm.world().rank
+    pr, pc = (r % p, r // p) if order == GridOrder.Col else (r // q, r % q)
+    return p, q, pr, pc
+
+
+def numroc(n, nb, iproc, isrcproc, nprocs):
+    from ..core.storage import numroc as _n
+    return _n(n, nb, (iproc - isrcproc) % nprocs, nprocs)
+
+
+def _target():
+    t = os.environ.get("SLATE_AMD_SCALAPACK_TARGET", "").lower()
+    if t in ("host", "cpu"):
+        return "host"
+    return "devices" if torch.cuda.is_available() else "host"
+
+
+def _opts():
+    la = int(os.environ.get("SLATE_AMD_SCALAPACK_LOOKAHEAD", "1"))
+    return {Option.Target: Target.Devices if _target() == "devices" else Target.HostTask, Option.Lookahead: la}
+
+
+class _Loc:
+    """This rank's local array (lld x nloc) staged to the target device."""
+
+    def __init__(self, a, desc, dtype):
+        _, ctxt, m, n, mb, nb, rsrc, csrc, lld = [int(x) for x in desc[:9]]
+        if rsrc or csrc:
+            raise SlateError("scalapack: rsrc = csrc = 0 required")
+        p, q, pr, pc = blacs_gridinfo(ctxt)
+        self.m, self.n, self.mb, self.nb, self.p, self.q = m, n, mb, nb, p, q
+        self.order = _CTX[ctxt][2]
+        nloc = numroc(n, nb, pc, 0, q)
+        t = torch.from_numpy(a) if isinstance(a, np.ndarray) else a
+        mloc = numroc(m, mb, pr, 0, p)
+        if nloc == 0 or t.numel() == 0:
+            t = torch.zeros((0, max(1, lld, mloc)), dtype=t.dtype, device=t.device).t()
+        flat = t.reshape(-1) if t.dim() == 1 else t.t().reshape(-1) if t.stride(0) != 1 else None
+        if t.dim() == 2 and t.stride(0) == 1:
+            self.user = t[:, :nloc]
+            lld = max(1, t.stride(1))
+        else:
+            lld = max(1, lld)
+            self.user = flat.as_strided((lld, nloc), (1, lld)) if nloc else flat[:0].reshape(0, 0)
+        dev = torch.device("cuda", torch.cuda.current_device()) if _target() == "devices" else t.device
+        if self.user.device == dev and self.user.dtype == dtype:
+            self.work = self.user
+            self.copy = False
+        else:
+            from .. import ops
+            self.work = ops.colmajor_empty(lld, nloc, dtype, dev)
+            if nloc:
+                self.work.copy_(self.user)
+            self.copy = True
+        self.lld = lld
+
+    def matrix(self, kind=Matrix, **kw):
+        comm = _comm.world()
+        if kind is Matrix:
+            return Matrix.fromScaLAPACK(self.m, self.n, self.work, self.lld, self.mb, self.nb, self.order,
+                                        self.p, self.q, comm)
+        if kind is HermitianMatrix:
+            return HermitianMatrix.fromScaLAPACK(kw["uplo"], self.n, self.work, self.lld, self.nb, self.p,
+                                                 self.q, comm, order=self.order)
+        if kind is TriangularMatrix:
+            return TriangularMatrix.fromScaLAPACK(kw["uplo"], kw["diag"], self.n, self.work, self.lld, self.nb,
+                                                  self.p, self.q, comm, order=self.order)
+        raise SlateError("bad kind")
+
+    def writeback(self):
+        if self.copy and self.user.numel():
+            self.user.copy_(self.work.to(self.user.device).to(self.user.dtype))
+
+
+def _chk(ia, ja):
+    if int(ia) != 1 or int(ja) != 1:
+        raise SlateError("scalapack: ia = ja = 1 required (whole matrices)")
+
+
+def _uplo(u):
+    return Uplo.Lower if str(u).upper()[0] == 'L' else Uplo.Upper
+
+
+def _op(t):
+    t = str(t).upper()[0]
+    return Op.NoTrans if t == 'N' else (Op.Trans if t == 'T' else Op.ConjTrans)
+
+
+def _opm(M, t):
+    return M if t == Op.NoTrans else (M.transpose() if t == Op.Trans else M.conj_transpose())
+
+
+def _make(pfx):
+    dt = _PFX[pfx]
+    g = {}
+
+    def gemm(transa, transb, m, n, k, alpha, a, ia, ja, desca, b, ib, jb, descb, beta, c, ic, jc, descc):
+        from ..models.blas3 import gemm as _g
+        _chk(ia, ja), _chk(ib, jb), _chk(ic, jc)
+        A, B, C = _Loc(a, desca, dt), _Loc(b, descb, dt), _Loc(c, descc, dt)
+        _g(alpha, _opm(A.matrix(), _op(transa)), _opm(B.matrix(), _op(transb)), beta, C.matrix(), _opts())
+        C.writeback()
+        return 0
+    g["gemm"] = gemm
+
+    def potrf(uplo, n, a, ia, ja, desca):
+        from ..models.chol import potrf as _p
+        _chk(ia, ja)
+        A = _Loc(a, desca, dt)
+        info = _p(A.matrix(HermitianMatrix, uplo=_uplo(uplo)), _opts())
+        A.writeback()
+        return info
+    g["potrf"] = potrf
+
+    def potrs(uplo, n, nrhs, a, ia, ja, desca, b, ib, jb, descb):
+        from ..models.chol import potrs as _p
+        _chk(ia, ja), _chk(ib, jb)
+        A, B = _Loc(a, desca, dt), _Loc(b, descb, dt)
+        _p(A.matrix(HermitianMatrix, uplo=_uplo(uplo)), B.matrix(), _opts())
+        B.writeback()
+        return 0
+    g["potrs"] = potrs
+
+    def posv(uplo, n, nrhs, a, ia, ja, desca, b, ib, jb, descb):
+        info = potrf(uplo, n, a, ia, ja, desca)
+        if info == 0:
+            potrs(uplo, n, nrhs, a, ia, ja, desca, b, ib, jb, descb)
+        return info
+    g["posv"] = posv
+
+    def getrf(m, n, a, ia, ja, desca, ipiv):
+        """ipiv: global 1-based pivots (length min(m, n)) on return."""
+        from ..models.lu import getrf as _g
+        _chk(ia, ja)
+        A = _Loc(a, desca, dt)
+        piv = Pivots()
+        info = _g(A.matrix(), piv, _opts())
+        A.writeback()
+        p = (piv.ipiv.cpu() + 1)
+        if isinstance(ipiv, np.ndarray):
+            ipiv[:p.numel()] = p.numpy()
+        else:
+            ipiv[:p.numel()] = p.to(ipiv.device, ipiv.dtype)
+        return info
+    g["getrf"] = getrf
+
+    def getrs(trans, n, nrhs, a, ia, ja, desca, ipiv, b, ib, jb, descb):
+        from ..models.lu import getrs as _g
+        _chk(ia, ja), _chk(ib, jb)
+        A, B = _Loc(a, desca, dt), _Loc(b, descb, dt)
+        ip = torch.as_tensor(np.asarray(ipiv) if isinstance(ipiv, np.ndarray) else ipiv.cpu()).to(torch.int64)
+        piv = Pivots()
+        piv.set(ip[:n] - 1, A.nb)
+        _g(_opm(A.matrix(), _op(trans)), piv, B.matrix(), _opts())
+        B.writeback()
+        return 0
+    g["getrs"] = getrs
+
+    def gesv(n, nrhs, a, ia, ja, desca, ipiv, b, ib, jb, descb):
+        info = getrf(n, n, a, ia, ja, desca, ipiv)
+        if info == 0:
+            getrs('N', n, nrhs, a, ia, ja, desca, ipiv, b, ib, jb, descb)
+        return info
+    g["gesv"] = gesv
+
+    def trsm(side, uplo, transa, diag, m, n, alpha, a, ia, ja, desca, b, ib, jb, descb):
+        from ..models.blas3 import trsm as _t
+        _chk(ia, ja), _chk(ib, jb)
+        A, B = _Loc(a, desca, dt), _Loc(b, descb, dt)
+        T = A.matrix(TriangularMatrix, uplo=_uplo(uplo), diag=Diag.Unit if str(diag).upper()[0] == 'U'
+                     else Diag.NonUnit)
+        _t(Side.Left if str(side).upper()[0] == 'L' else Side.Right, alpha, _opm(T, _op(transa)), B.matrix(),
+           _opts())
+        B.writeback()
+        return 0
+    g["trsm"] = trsm
+
+    def geqrf(m, n, a, ia, ja, desca, tau=None):
+        from ..models.qr import geqrf as _q
+        _chk(ia, ja)
+        A = _Loc(a, desca, dt)
+        T = TriangularFactors()
+        _q(A.matrix(), T, _opts())
+        A.writeback()
+        return T
+    g["geqrf"] = geqrf
+
+    def gels(trans, m, n, nrhs, a, ia, ja, desca, b, ib, jb, descb):
+        from ..models.qr import gels as _g
+        _chk(ia, ja), _chk(ib, jb)
+        A, B = _Loc(a, desca, dt), _Loc(b, descb, dt)
+        _g(_opm(A.matrix(), _op(trans)), TriangularFactors(), B.matrix(), _opts())
+        B.writeback()
+        return 0
+    g["gels"] = gels
+
+    def lange(norm, m, n, a, ia, ja, desca):
+        from ..models.aux import norm as _n
+        _chk(ia, ja)
+        return float(_n(Norm.from_string(str(norm)), _Loc(a, desca, dt).matrix()))
+    g["lange"] = lange
+
+    def heev(jobz, uplo, n, a, ia, ja, desca, w, z=None, iz=1, jz=1, descz=None):
+        from ..models.eig import heev as _h
+        _chk(ia, ja)
+        A = _Loc(a, desca, dt)
+        Z = _Loc(z, descz, dt) if str(jobz).upper()[0] == 'V' else None
+        vals = _h(A.matrix(HermitianMatrix, uplo=_uplo(uplo)), None, Z.matrix() if Z else None, _opts())
+        if Z:
+            Z.writeback()
+        if isinstance(w, np.ndarray):
+            w[:n] = vals.cpu().numpy()
+        else:
+            w[:n] = vals.to(w.device, w.dtype)
+        return 0
+    g["heev" if dt.is_complex else "syev"] = heev
+
+    def gesvd(jobu, jobvt, m, n, a, ia, ja, desca, s, u=None, iu=1, ju=1, descu=None, vt=None, ivt=1, jvt=1,
+              descvt=None):
+        from ..models.svd import svd as _s
+        _chk(ia, ja)
+        A = _Loc(a, desca, dt)
+        U = _Loc(u, descu, dt) if str(jobu).upper()[0] == 'V' else None
+        VT = _Loc(vt, descvt, dt) if str(jobvt).upper()[0] == 'V' else None
+        sv = _s(A.matrix(), None, U.matrix() if U else None, VT.matrix() if VT else None, _opts())
+        for x in (U, VT):
+            if x:
+                x.writeback()
+        k = min(m, n)
+        if isinstance(s, np.ndarray):
+            s[:k] = sv.cpu().numpy()
+        else:
+            s[:k] = sv.to(s.device, s.dtype)
+        return 0
+    g["gesvd"] = gesvd
+    return g
+
+
+def _install():
+    mod = globals()
+    for pfx in _PFX:
+        for name, fn in _make(pfx).items():
+            fn.__name__ = "p" + pfx + name
+            mod["p" + pfx + name] = fn
+
+
+_install()

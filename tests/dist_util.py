@@ -58,5 +58,5 @@ def run_dist(fn, nprocs=2, *args, timeout=300):
             if p.is_alive():
                 p.kill()
     if errs:
-        r = min(errs)
-        raise AssertionError(f"rank {r} failed:\n{errs[r]}")
+        msg = "\n".join(f"rank {r} failed:\n{errs[r]}" for r in sorted(errs))
+        raise AssertionError(msg)

@@ -1,0 +1,116 @@
+"""LAPACK / ScaLAPACK-style front-ends (reference: lapack_api/ and
+scalapack_api/ smoke tests run the interposed routines against the
+reference library; here against PyTorch fp64)."""
+import numpy as np
+import pytest
+import torch
+
+from slate_amd.compat import lapack as L
+from slate_amd.compat import scalapack as S
+
+from dist_util import run_dist
+
+
+def _spd(n, seed, dt=np.float64):
+    r = np.random.default_rng(seed)
+    X = r.standard_normal((n, n))
+    if np.dtype(dt).kind == 'c':
+        X = X + 1j * r.standard_normal((n, n))
+    return (X @ X.conj().T + n * np.eye(n)).astype(dt)
+
+
+def test_lapack_potrf_posv_gesv():
+    n = 70
+    A = np.asfortranarray(_spd(n, 1))
+    B = np.asfortranarray(np.random.default_rng(2).standard_normal((n, 3)))
+    A0, B0 = A.copy(), B.copy()
+    assert L.dposv('L', n, 3, A, n, B, n) == 0
+    assert np.abs(A0 @ B - B0).max() < 1e-10
+    M = np.asfortranarray(np.random.default_rng(3).standard_normal((n, n)))
+    M0 = M.copy()
+    B = B0.copy(order='F')
+    ipiv = np.zeros(n, dtype=np.int64)
+    assert L.dgesv(n, 3, M, n, ipiv, B, n) == 0
+    assert np.abs(M0 @ B - B0).max() < 1e-10
+    assert ipiv.min() >= 1
+
+
+def test_lapack_flat_storage_and_complex():
+    n, lda = 40, 45
+    A = _spd(n, 4, np.complex128)
+    flat = np.zeros(lda * n, dtype=np.complex128)
+    for j in range(n):
+        flat[j * lda:j * lda + n] = A[:, j]
+    assert L.zpotrf('L', n, flat, lda) == 0
+    Lf = np.tril(np.stack([flat[j * lda:j * lda + n] for j in range(n)], axis=1))
+    assert np.abs(Lf @ Lf.conj().T - A).max() < 1e-10
+
+
+def test_lapack_gemm_trsm_geqrf_gels_syev_gesvd():
+    r = np.random.default_rng(5)
+    m, n, k = 30, 20, 10
+    A, B, C = (np.asfortranarray(r.standard_normal(s)) for s in ((m, k), (k, n), (m, n)))
+    C0 = C.copy()
+    L.dgemm('N', 'N', m, n, k, 2.0, A, m, B, k, 0.5, C, m)
+    assert np.abs(C - (2 * A @ B + 0.5 * C0)).max() < 1e-12
+    T = np.asfortranarray(np.tril(r.standard_normal((n, n))) + n * np.eye(n))
+    X = np.asfortranarray(r.standard_normal((n, 4)))
+    X0 = X.copy()
+    L.dtrsm('L', 'L', 'N', 'N', n, 4, 1.0, T, n, X, n)
+    assert np.abs(T @ X - X0).max() < 1e-12
+    G = np.asfortranarray(r.standard_normal((m, n)))
+    G0 = G.copy()
+    Bg = np.asfortranarray(r.standard_normal((m, 2)))
+    Bg0 = Bg.copy()
+    L.dgels('N', m, n, 2, G, m, Bg, m)
+    assert np.abs(Bg[:n] - np.linalg.lstsq(G0, Bg0, rcond=None)[0]).max() < 1e-10
+    H = np.asfortranarray(_spd(25, 6) - 30 * np.eye(25))
+    H0 = H.copy()
+    w = np.zeros(25)
+    L.dsyev('V', 'L', 25, H, 25, w)
+    assert np.abs(w - np.linalg.eigvalsh(H0)).max() < 1e-10
+    assert np.abs(H0 @ H - H * w).max() < 1e-10
+    Sg = np.asfortranarray(r.standard_normal((m, n)))
+    Sg0 = Sg.copy()
+    s = np.zeros(n)
+    U = np.zeros((m, n), order='F')
+    VT = np.zeros((n, n), order='F')
+    L.dgesvd('S', 'S', m, n, Sg, m, s, U, m, VT, n)
+    assert np.abs(U @ np.diag(s) @ VT - Sg0).max() < 1e-10
+    assert abs(L.dlange('F', m, n, Sg0, m) - np.linalg.norm(Sg0)) < 1e-10
+
+
+def _local(Aglob, nb, p, q, pr, pc):
+    m, n = Aglob.shape
+    rows = [i for i in range(m) if (i // nb) % p == pr]
+    cols = [j for j in range(n) if (j // nb) % q == pc]
+    return np.asfortranarray(Aglob[np.ix_(rows, cols)]), rows, cols
+
+
+def _sca(rank, size, p, q):
+    ctxt = S.blacs_gridinit(p, q)
+    _, _, pr, pc = S.blacs_gridinfo(ctxt)
+    n, nb = 60, 16
+    A = _spd(n, 7)
+    B = np.random.default_rng(8).standard_normal((n, 2))
+    Al, _, _ = _local(A, nb, p, q, pr, pc)
+    Bl, rows, cols = _local(B, nb, p, q, pr, pc)
+    desca = [1, ctxt, n, n, nb, nb, 0, 0, max(1, Al.shape[0])]
+    descb = [1, ctxt, n, 2, nb, nb, 0, 0, max(1, Bl.shape[0])]
+    assert S.pdposv('L', n, 2, Al, 1, 1, desca, Bl, 1, 1, descb) == 0
+    X = np.linalg.solve(A, B)
+    if Bl.size:
+        assert np.abs(Bl - X[np.ix_(rows, cols)]).max() < 1e-10
+    M = np.random.default_rng(9).standard_normal((n, n))
+    Ml, _, _ = _local(M, nb, p, q, pr, pc)
+    Bl, rows, cols = _local(B, nb, p, q, pr, pc)
+    ipiv = np.zeros(n, dtype=np.int64)
+    assert S.pdgesv(n, 2, Ml, 1, 1, desca, ipiv, Bl, 1, 1, descb) == 0
+    X = np.linalg.solve(M, B)
+    if Bl.size:
+        assert np.abs(Bl - X[np.ix_(rows, cols)]).max() < 1e-10
+
+
+@pytest.mark.parametrize("grid", [(2, 1), (1, 2)])
+def test_scalapack_grid(grid):
+    run_dist(_sca, 2, *grid)
