@@ -93,6 +93,15 @@ def build(verbose=False, hip=True, host=True):
             "_host", os.path.join(HERE, "csrc", "host"), [".cpp"], "g++",
             ["-O3", "-std=c++17", "-fPIC", "-fopenmp", "-fvisibility=hidden", "-Wall", "-Wno-unused-function"] + inc,
             ["-fopenmp"], verbose))
+    if host:
+        # C ABI (include/slate_amd/c_api.h): embeds the Python runtime
+        pyinc = sysconfig.get_paths()["include"]
+        libdir = sysconfig.get_config_var("LIBDIR") or "/usr/lib"
+        pylib = "python" + sysconfig.get_config_var("LDVERSION")
+        out.append(_build_module(
+            "libslate_amd_c", os.path.join(HERE, "csrc", "capi"), [".cpp"], "g++",
+            ["-O2", "-std=c++17", "-fPIC", "-I" + pyinc],
+            ["-L" + libdir, "-l" + pylib], verbose))
     if hip:
         hipcc = os.path.join(ROCM, "bin", "hipcc")
         out.append(_build_module(

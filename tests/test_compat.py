@@ -114,3 +114,23 @@ def _sca(rank, size, p, q):
 @pytest.mark.parametrize("grid", [(2, 1), (1, 2)])
 def test_scalapack_grid(grid):
     run_dist(_sca, 2, *grid)
+
+
+def test_c_api(tmp_path):
+    """Compile and run the C example against libslate_amd_c.so."""
+    import os
+    import subprocess
+    import sysconfig
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "slate_amd")
+    exe = str(tmp_path / "ex_capi")
+    libdir = sysconfig.get_config_var("LIBDIR")
+    cmd = ["gcc", "-O1", os.path.join(root, "examples", "c", "ex_capi.c"), "-I", os.path.join(root, "include"),
+           "-L", lib, "-lslate_amd_c", "-Wl,-rpath," + lib, "-L", libdir,
+           "-l" + "python" + sysconfig.get_config_var("LDVERSION"), "-lm", "-o", exe]
+    subprocess.run(cmd, check=True)
+    env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""),
+               SLATE_AMD_LAPACK_TARGET="host")
+    r = subprocess.run([exe], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout
+    assert "dgesv info=0" in r.stdout
