@@ -163,3 +163,11 @@ def indefinite_solve_using_factor(A, pivots, T, pivots2, B, opts=None):
 
 def indefinite_solve(A, B, opts=None):
     return hesv(A, Pivots(), None, None, None, B, opts)
+
+
+from .models.aux import set_lambda  # noqa: F401,E402
+from .utils.printing import print_matrix, print_vector, format_matrix  # noqa: F401,E402
+from .utils.debug import Debug  # noqa: F401,E402
+from .models.svd import ge2tb as ge2tb_, svd_vals  # noqa: F401,E402
+from . import compat  # noqa: F401,E402
+print = print_matrix  # SLATE slate::print(label, A, opts)  # noqa: A001

@@ -646,6 +646,10 @@ class TriangularMatrix(TrapezoidMatrix):
         if isinstance(n_or_diag, (Diag, str)) and not isinstance(n_or_diag, int):
             diag = Diag(n_or_diag)
             n_or_diag = None
+            if args and isinstance(args[0], BaseMatrix):      # (uplo, diag, A)
+                matrix, args = args[0], args[1:]
+            elif args:                                         # (uplo, diag, n, ...)
+                n_or_diag, args = args[0], args[1:]
         if matrix is not None:
             TrapezoidMatrix.__init__(self, uplo, matrix=matrix, diag=diag)
             return

@@ -479,3 +479,29 @@ def colNorms(norm_type, A, opts=None):
     if s.comm.size > 1:
         s.comm.allreduce(colv, "max")
     return colv
+
+
+def set_lambda(fn, A, opts=None):
+    """A(i, j) = fn(i, j) for every stored element (src/set_lambdas.cc);
+    fn receives broadcastable global index tensors (rows[:, None],
+    cols[None, :]) and must return a tensor (or scalar)."""
+    s, slot, lb = _bc_pieces(A, opts)
+    if lb.mloc and lb.nloc:
+        dev = lb.data.device
+        gr = torch.tensor([lb.global_row(i) for i in range(lb.mloc)], device=dev)[:, None]
+        gc = torch.tensor([lb.global_col(j) for j in range(lb.nloc)], device=dev)[None, :]
+        v = fn(gr, gc)
+        v = torch.as_tensor(v, device=dev).to(lb.data.dtype).expand(lb.mloc, lb.nloc)
+        up = A.uploPhysical()
+        if up == Uplo.Lower:
+            keep = gr >= gc
+        elif up == Uplo.Upper:
+            keep = gr <= gc
+        else:
+            keep = None
+        if keep is None:
+            lb.data.copy_(v)
+        else:
+            lb.data.copy_(torch.where(keep, v, lb.data))
+    s.mark_local_modified(slot)
+    return A

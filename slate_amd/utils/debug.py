@@ -1,0 +1,93 @@
+"""Debug helpers (`src/auxiliary/Debug.hh:15-77`, `Debug.cc`): tile /
+MOSI-state dumps, memory-pool leak checks, matrix diffs.  Off unless
+`Debug.on()` (or SLATE_AMD_DEBUG=1)."""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from ..core.storage import DEV, HOST
+
+
+class Debug:
+    _on = os.environ.get("SLATE_AMD_DEBUG", "0") not in ("0", "")
+
+    @classmethod
+    def on(cls):
+        cls._on = True
+
+    @classmethod
+    def off(cls):
+        cls._on = False
+
+    @classmethod
+    def enabled(cls):
+        return cls._on
+
+    @staticmethod
+    def tile_states(A) -> str:
+        """One character per local tile and slot: M(odified) S(hared)
+        O(n hold) I(nvalid) . (absent) -- SLATE printTilesMOSI."""
+        from .. import _native
+        s = A.storage
+        H = _native._host
+        MOD, SH, INV, HOLD = H.MOSI_Modified, H.MOSI_Shared, H.MOSI_Invalid, H.MOSI_OnHold
+
+        def code(st):
+            c = "M" if st & MOD else ("S" if st & SH else ("I" if st & INV else "?"))
+            return c.lower() if st & HOLD else c
+        lines = []
+        for slot, name in ((HOST, "host"), (DEV, "dev")):
+            rows = []
+            for i in range(A.mt()):
+                row = []
+                for j in range(A.nt()):
+                    gi, gj = A._global_ij(i, j)
+                    if not s.tileIsLocal(gi, gj):
+                        row.append(" ")
+                    elif s.tileExists(gi, gj, slot):
+                        st = s.table.state(gi, gj, slot)
+                        row.append(code(int(st)))
+                    else:
+                        row.append(".")
+                rows.append("".join(row))
+            lines.append(f"{name}:\n" + "\n".join(rows))
+        return "\n".join(lines)
+
+    @staticmethod
+    def check_pool_leaks() -> dict:
+        """Bytes still allocated in the slab pools (should be 0 after all
+        matrices are freed)."""
+        from ..core import storage
+        out = {}
+        for key, pool in getattr(storage, "_POOLS", {}).items():
+            try:
+                out[str(key)] = int(pool.allocated_bytes())
+            except Exception:  # noqa: BLE001
+                out[str(key)] = -1
+        return out
+
+    @staticmethod
+    def diff(A, B, tol=0.0):
+        """Positions (i, j) where the gathered A and B differ by > tol."""
+        from ..models.aux import allgather_dense
+        X, Y = allgather_dense(A), allgather_dense(B)
+        d = (X - Y).abs()
+        idx = (d > tol).nonzero().tolist()
+        return idx, float(d.max()) if d.numel() else 0.0
+
+    @staticmethod
+    def diff_lapack(A: torch.Tensor, B: torch.Tensor, mb=None, nb=None, tol=0.0) -> str:
+        """Tile map of differences between two dense matrices (diffLapackMatrices)."""
+        m, n = A.shape
+        mb = mb or m
+        nb = nb or n
+        lines = []
+        for i0 in range(0, m, mb):
+            row = []
+            for j0 in range(0, n, nb):
+                dd = (A[i0:i0 + mb, j0:j0 + nb] - B[i0:i0 + mb, j0:j0 + nb]).abs().max().item()
+                row.append("X" if dd > tol else ".")
+            lines.append("".join(row))
+        return "\n".join(lines)
