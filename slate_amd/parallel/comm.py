@@ -74,6 +74,18 @@ class Comm:
             return t.cuda(), True
         return t, False
 
+    @staticmethod
+    def _flat_view(t: torch.Tensor):
+        """A contiguous alias of t's memory when one exists (column-major
+        matrices with ld == rows are contiguous as their transpose), else None."""
+        if t.is_contiguous():
+            return t
+        if t.dim() == 2 and t.stride(0) == 1 and (t.stride(1) == t.shape[0] or t.shape[1] <= 1):
+            v = t.t()
+            if v.is_contiguous():
+                return v
+        return None
+
     def _finish(self, t, staged, orig):
         if staged:
             orig.copy_(t)
@@ -96,14 +108,18 @@ class Comm:
         if self.size == 1:
             return None
         try:
-            x, staged = self._prep(t if t.is_contiguous() else t.contiguous())
+            fv = self._flat_view(t)
+            src = fv if fv is not None else t.contiguous()
+            x, staged = self._prep(src)
             w = dist.broadcast(x, src=self._g(root), group=self.group, async_op=async_op)
-            if async_op and not staged and x is t:
+            if async_op and not staged and x is src and fv is not None:
                 return w
             if async_op:
                 w.wait()
-            if x is not t:
-                t.copy_(x)
+            if x is not src:          # staged through host/device
+                src.copy_(x)
+            if fv is None:            # broadcast into a contiguous copy
+                t.copy_(src)
             return None
         except Exception as e:  # noqa: BLE001
             raise CommError(f"bcast failed: {e}") from e
@@ -113,19 +129,21 @@ class Comm:
             return t
         rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
                "min": dist.ReduceOp.MIN, "prod": dist.ReduceOp.PRODUCT}[op]
-        x, staged = self._prep(t if t.is_contiguous() else t.contiguous())
+        fv = self._flat_view(t)
+        src = fv if fv is not None else t.contiguous()
+        x, staged = self._prep(src)
         if op == "max" and x.dtype.is_floating_point:
             # NaN-propagating max (SLATE mpi_max_nan): reduce a NaN flag too.
             nanflag = torch.isnan(x).to(x.dtype)
             dist.all_reduce(nanflag, op=dist.ReduceOp.MAX, group=self.group)
             dist.all_reduce(x, op=rop, group=self.group)
-            x = torch.where(nanflag > 0, torch.full_like(x, float("nan")), x)
-            if x.data_ptr() != t.data_ptr():
-                t.copy_(x)
-            return t
-        dist.all_reduce(x, op=rop, group=self.group)
-        if x is not t:
-            t.copy_(x)
+            x.copy_(torch.where(nanflag > 0, torch.full_like(x, float("nan")), x))
+        else:
+            dist.all_reduce(x, op=rop, group=self.group)
+        if x is not src:              # staged through host/device
+            src.copy_(x)
+        if fv is None:                # reduced a contiguous copy
+            t.copy_(src)
         return t
 
     def allreduce_scalar(self, v, op="sum", dtype=torch.float64, device=None):
