@@ -27,8 +27,8 @@ namespace slate_hip {
 
 namespace {
 constexpr int NBB = 32;          // base-case width
-constexpr int NTH = 256;         // threads per workgroup (one row each)
-constexpr int MAXG = 512;        // max workgroups per base launch
+constexpr int NTH = 256;         // threads per workgroup (one row each per chunk)
+constexpr int MAXG = 128;        // max workgroups per base launch (candidate rows staged in LDS)
 
 template <typename T>
 struct PanelBuf {                // one parity half of the device workspace
@@ -38,54 +38,129 @@ struct PanelBuf {                // one parity half of the device workspace
     T diag[NBB];
 };
 constexpr size_t PANEL_BYTES = 2 * sizeof(PanelBuf<zcplx>);
+
+// (v, i) beats (w, k): NaN wins, then larger, then lower index
+template <typename R>
+__device__ inline bool beats(R v, i64 i, R w, i64 k) {
+    return (v != v && w == w) || v > w || (v == w && i < k);
+}
+template <typename X>
+__device__ inline X xshfl(X v, int o) {
+    static_assert(sizeof(X) % 4 == 0, "");
+    union U { X x; int w[sizeof(X) / 4]; } a, b;
+    a.x = v;
+    #pragma unroll
+    for (int k = 0; k < (int)(sizeof(X) / 4); ++k) b.w[k] = __shfl_xor(a.w[k], o, 64);
+    return b.x;
+}
+template <typename R>
+__device__ inline void wave_argmax(R& v, i64& i, int& g) {
+    #pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        R w = xshfl(v, o);
+        i64 k = xshfl(i, o);
+        int h = __shfl_xor(g, o, 64);
+        if (beats(w, k, v, i)) { v = w; i = k; g = h; }
+    }
+}
 }  // namespace
 
+// One launch per column j of the base block [c0, c1) (plus a final j = c1):
+//   prologue: every load this launch needs is issued at once -- this
+//     thread's row segment, launch j-1's arg-max partials, ALL candidate rows
+//     (<= 128 x 32, staged in LDS) and the saved row j-1;
+//   (a) pivot of column j-1 = reduction of the partials (wave shuffles);
+//   (b) row interchange: the pivot row comes from LDS, the owner of row p
+//     takes the saved old row j-1 -- no workgroup reads a row another writes;
+//   (c) elimination of column j-1 in registers;
+//   (d) arg-max of column j on the updated registers, the winning row and
+//     row j are published from registers (no global re-read).
+// Only two dependent global round trips per launch; ordering between columns
+// comes from kernel boundaries (no fences, atomics or grid barriers).
 template <typename T>
 __global__ void __launch_bounds__(NTH)
 getrf_base_step(i64 m, int c0, int c1, int j, T* A, i64 lda, i64* ipiv, i64 ioff, i64* info,
                 i64 info_off, void* work, double thr, bool nopiv) {
     using R = typename scalar_traits<T>::real;
-    __shared__ R sv[NTH];
-    __shared__ i64 si[NTH];
-    __shared__ int sg[NTH];
-    __shared__ T prow[NBB];
-    __shared__ T drow[NBB];
+    __shared__ T candL[MAXG * NBB];
+    __shared__ T prow[NBB], drow[NBB], orow[NBB];
+    __shared__ R wv[NTH / 64];
+    __shared__ i64 wi[NTH / 64];
+    __shared__ int wg[NTH / 64];
+    __shared__ i64 s_p;
+    __shared__ int s_gw, s_bt;
     PanelBuf<T>* pb = reinterpret_cast<PanelBuf<T>*>(work);
-    const int G = gridDim.x, g = blockIdx.x, tid = threadIdx.x;
+    const int G = gridDim.x, g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const i64 rows_per = (m + G - 1) / G;
     const i64 r0 = (i64)g * rows_per, r1 = min(m, r0 + rows_per);
     const int w = c1 - c0;
-    i64 p = -1;
     const int pc = j - 1;
-    if (j > c0) {
-        // ---- (a) pivot of column j-1 from launch j-1's partials
+    const bool first = (j == c0), last = (j >= c1);
+    const bool single = rows_per <= NTH;            // one row per thread: full register path
+    // ---------------- prologue: issue every independent load, partials first
+    // (the compiler then waits for them with vmcnt(N) while the row loads
+    // are still in flight)
+    R pv = R(-1); i64 pidx = pc; int pg = -1;
+    constexpr int PER = MAXG * NBB / NTH;
+    T cv[PER];
+    T dv = s_zero(T());
+    if (!first) {
         PanelBuf<T>& in = pb[pc & 1];
-        R best = R(-1); i64 bi = pc; int bg = -1;
-        if (!nopiv)
-            for (int q = tid; q < G; q += NTH) {
-                R v = (R)in.val[q]; i64 ix = in.idx[q];
-                if ((v != v && best == best) || v > best || (v == best && ix < bi)) { best = v; bi = ix; bg = q; }
-            }
-        sv[tid] = best; si[tid] = bi; sg[tid] = bg;
-        if (tid < w) drow[tid] = in.diag[tid];
+        if (!nopiv && tid < G) { pv = (R)in.val[tid]; pidx = in.idx[tid]; pg = tid; }
+        if (tid < w) dv = in.diag[tid];
+        // unconditional loads from clamped (always valid) addresses: a
+        // load under a runtime select makes hipcc wait for each one
+        #pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int e = tid + k * NTH, q = min(e / NBB, G - 1);
+            cv[k] = in.cand[q][e % NBB];
+        }
+    }
+    const i64 i0 = r0 + tid;
+    T a[NBB];
+    const bool mine = single && i0 < r1 && (first ? i0 >= j : i0 > pc);
+    {
+        const i64 ir = mine ? i0 : 0;
+        #pragma unroll
+        for (int c = 0; c < NBB; ++c) a[c] = A[ir + (i64)(c0 + min(c, w - 1)) * lda];
+    }
+    if (!first) {
+        if (tid < w) drow[tid] = dv;
+        #pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int e = tid + k * NTH, q = e / NBB, c = e % NBB;
+            if (q < G && c < w) candL[q * NBB + c] = cv[k];
+        }
+    }
+    // ---------------- (a) pivot of column j-1
+    i64 p = pc;
+    if (!first) {
+        if (!nopiv) {
+            wave_argmax(pv, pidx, pg);
+            if (lane == 0) { wv[wid] = pv; wi[wid] = pidx; wg[wid] = pg; }
+        }
         __syncthreads();
-        for (int o = NTH / 2; o > 0; o >>= 1) {
-            if (tid < o) {
-                R a = sv[tid], b = sv[tid + o];
-                i64 ia = si[tid], ib = si[tid + o];
-                bool take = (b != b && a == a) || b > a || (b == a && ib < ia);
-                if (take) { sv[tid] = b; si[tid] = ib; sg[tid] = sg[tid + o]; }
+        if (tid == 0) {
+            int gw = -1;
+            i64 pp = pc;
+            if (!nopiv) {
+                R bv = wv[0]; i64 bi = wi[0]; gw = wg[0];
+                for (int k = 1; k < NTH / 64; ++k)
+                    if (beats(wv[k], wi[k], bv, bi)) { bv = wv[k]; bi = wi[k]; gw = wg[k]; }
+                pp = bi;
+                if (gw < 0) pp = pc;
+                else if (thr < 1.0) {
+                    R dj = s_abs1(drow[pc - c0]);
+                    if (dj == dj && (double)dj >= thr * (double)bv) { pp = pc; gw = -1; }
+                }
+                if (pp == pc) gw = -1;
             }
-            __syncthreads();
+            s_p = pp; s_gw = gw;
         }
-        p = si[0];
-        int gw = sg[0];
-        if (nopiv || gw < 0) { p = pc; }
-        else if (thr < 1.0) {
-            R dj = s_abs1(drow[pc - c0]);
-            if (dj == dj && (double)dj >= thr * (double)sv[0]) p = pc;
-        }
-        if (tid < w) prow[tid] = (p == pc) ? drow[tid] : in.cand[gw][tid];
+        __syncthreads();
+        p = s_p;
+        const int gw = s_gw;
+        if (tid < w) prow[tid] = (gw < 0) ? drow[tid] : candL[gw * NBB + tid];
         __syncthreads();
         if (g == 0 && tid == 0) {
             if (ipiv) ipiv[pc] = p + ioff;
@@ -93,77 +168,115 @@ getrf_base_step(i64 m, int c0, int c1, int j, T* A, i64 lda, i64* ipiv, i64 ioff
                 atomicCAS(reinterpret_cast<unsigned long long*>(info), 0ull,
                           (unsigned long long)(pc + 1 + info_off));
         }
-        // ---- (b) interchange: new row pc = pivot row (owner of pc writes it)
+        // (b) new row pc = pivot row (its owner writes it)
         if (pc >= r0 && pc < r1 && tid < w) A[pc + (i64)(c0 + tid) * lda] = prow[tid];
     }
-    const bool last = j >= c1;
-    PanelBuf<T>& out = pb[j & 1];
-    R best = R(-1); i64 bi = j;
-    const T u = (j > c0) ? prow[pc - c0] : s_zero(T());
+    const T u = first ? s_zero(T()) : prow[pc - c0];
     const bool uz = s_is_zero(u);
-    for (i64 i = r0 + tid; i < r1; i += NTH) {
-        if (j == c0) {   // first column of the block: arg-max only
-            if (i >= j && !nopiv) {
-                R v = s_abs1(A[i + (i64)j * lda]);
-                if (v > best || (v != v && best == best)) { best = v; bi = i; }
+    R best = R(-1); i64 bi = j;
+    if (single) {
+        if (mine && !first) {
+            const bool isp = (i0 == p) && p != pc;
+            if (isp) {
+                #pragma unroll
+                for (int c = 0; c < NBB; ++c) if (c < w) a[c] = drow[c];
             }
-            continue;
-        }
-        if (i <= pc) continue;
-        T a[NBB];
-        const bool isp = (j > c0) && i == p && p != pc;
-        if (isp) {
+            // (c) eliminate column pc (compile-time indices only: no scratch)
+            T l = s_zero(T());
             #pragma unroll
-            for (int c = 0; c < NBB; ++c) if (c < w) a[c] = drow[c];
-        } else {
-            #pragma unroll
-            for (int c = 0; c < NBB; ++c) if (c < w && c0 + c >= pc) a[c] = A[i + (i64)(c0 + c) * lda];
-        }
-        {
-            // ---- (c) eliminate column pc
-            // (runtime-indexed reads of a[] would demote it to scratch: the
-            // two scalars needed by position are re-read from cache/LDS)
-            T l = isp ? drow[pc - c0] : A[i + (i64)pc * lda];
+            for (int c = 0; c < NBB; ++c) if (c0 + c == pc) l = a[c];
             if (!uz) l = s_div(l, u);
             #pragma unroll
             for (int c = 0; c < NBB; ++c) {
                 if (c0 + c == pc) a[c] = l;
-                if (c < w && c0 + c > pc) a[c] = s_sub(a[c], s_mul(l, prow[c]));
+                else if (c < w && c0 + c > pc) a[c] = s_sub(a[c], s_mul(l, prow[c]));
             }
-            if (!last && !nopiv) {
-                T aj = isp ? drow[j - c0] : A[i + (i64)j * lda];
-                R v = s_abs1(s_sub(aj, s_mul(l, prow[j - c0])));
-                if (v > best || (v != v && best == best)) { best = v; bi = i; }
-            }
+            #pragma unroll
+            for (int c = 0; c < NBB; ++c)
+                if (c < w && (isp || c0 + c >= pc)) A[i0 + (i64)(c0 + c) * lda] = a[c];
+        }
+        if (mine && !last && !nopiv) {
+            T aj = s_zero(T());
+            #pragma unroll
+            for (int c = 0; c < NBB; ++c) if (c0 + c == j) aj = a[c];
+            best = s_abs1(aj); bi = i0;
+        }
+    } else {
+        // many rows per thread (very tall panels): loop; the winning row is
+        // re-read from memory below
+        for (i64 i = r0 + tid; i < r1; i += NTH) {
+            if (first ? i < j : i <= pc) continue;
+            T b[NBB];
+            const bool isp = !first && i == p && p != pc;
+            #pragma unroll
+            for (int c = 0; c < NBB; ++c) if (c < w) b[c] = A[i + (i64)(c0 + c) * lda];
             if (isp) {
                 #pragma unroll
-                for (int c = 0; c < NBB; ++c) if (c < w) A[i + (i64)(c0 + c) * lda] = a[c];
-            } else {
+                for (int c = 0; c < NBB; ++c) if (c < w) b[c] = drow[c];
+            }
+            if (!first) {
+                T l = s_zero(T());
                 #pragma unroll
-                for (int c = 0; c < NBB; ++c) if (c < w && c0 + c >= pc) A[i + (i64)(c0 + c) * lda] = a[c];
+                for (int c = 0; c < NBB; ++c) if (c0 + c == pc) l = b[c];
+                if (!uz) l = s_div(l, u);
+                #pragma unroll
+                for (int c = 0; c < NBB; ++c) {
+                    if (c0 + c == pc) b[c] = l;
+                    else if (c < w && c0 + c > pc) b[c] = s_sub(b[c], s_mul(l, prow[c]));
+                }
+                #pragma unroll
+                for (int c = 0; c < NBB; ++c)
+                    if (c < w && (isp || c0 + c >= pc)) A[i + (i64)(c0 + c) * lda] = b[c];
+            }
+            if (!last && !nopiv) {
+                T aj = s_zero(T());
+                #pragma unroll
+                for (int c = 0; c < NBB; ++c) if (c0 + c == j) aj = b[c];
+                R v = s_abs1(aj);
+                if (beats(v, i, best, bi)) { best = v; bi = i; }
             }
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     if (last) return;
-    // ---- (d) publish arg-max of column j, the candidate row, and row j
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    sv[tid] = best; si[tid] = bi;
+    // ---------------- (d) arg-max of column j, publish winner row and row j
+    PanelBuf<T>& out = pb[j & 1];
+    if (single && mine && i0 == j) {
+        #pragma unroll
+        for (int c = 0; c < NBB; ++c) if (c < w) out.diag[c] = a[c];
+    }
+    if (!single) {
+        __syncthreads();                       // rows stored by other threads of this block
+        if (j >= r0 && j < r1 && tid < w) out.diag[tid] = A[j + (i64)(c0 + tid) * lda];
+    }
+    if (nopiv) {
+        if (tid == 0) { out.val[g] = -1.0; out.idx[g] = j; }
+        return;
+    }
+    int bt = tid;
+    wave_argmax(best, bi, bt);
+    if (lane == 0) { wv[wid] = best; wi[wid] = bi; wg[wid] = bt; }
     __syncthreads();
-    for (int o = NTH / 2; o > 0; o >>= 1) {
-        if (tid < o) {
-            R a = sv[tid], b = sv[tid + o];
-            i64 ia = si[tid], ib = si[tid + o];
-            bool take = (b != b && a == a) || b > a || (b == a && ib < ia);
-            if (take) { sv[tid] = b; si[tid] = ib; }
+    if (tid == 0) {
+        R bv = wv[0]; i64 bb = wi[0]; int t = wg[0];
+        for (int k = 1; k < NTH / 64; ++k)
+            if (beats(wv[k], wi[k], bv, bb)) { bv = wv[k]; bb = wi[k]; t = wg[k]; }
+        out.val[g] = (double)bv;
+        out.idx[g] = bb;
+        wi[0] = bb;
+        s_bt = (bv >= R(0) || bv != bv) ? t : -1;
+    }
+    __syncthreads();
+    if (single) {
+        if (tid == s_bt) {
+            #pragma unroll
+            for (int c = 0; c < NBB; ++c) if (c < w) orow[c] = a[c];
         }
-        __syncthreads();
+    } else if (s_bt >= 0 && tid < w) {
+        orow[tid] = A[wi[0] + (i64)(c0 + tid) * lda];
     }
-    const i64 b = si[0];
-    if (tid == 0) { out.val[g] = (double)sv[0]; out.idx[g] = b; }
-    if (tid < w) {
-        if (sv[0] >= R(0) || sv[0] != sv[0]) out.cand[g][tid] = A[b + (i64)(c0 + tid) * lda];
-        if (j >= r0 && j < r1) out.diag[tid] = A[j + (i64)(c0 + tid) * lda];
-    }
+    __syncthreads();
+    if (s_bt >= 0 && tid < w) out.cand[g][tid] = orow[tid];
 }
 
 template <typename T>
