@@ -124,7 +124,7 @@ def _gemm_summa(alpha, A, B, beta, C, opts):
     rA0, cA0 = A.global_offsets()
     rB0, _ = B.global_offsets()
     kt = A.nt()
-    ss = StreamSet(dev)
+    ss = StreamSet(dev, reserve_cus=0)
     ss.fork()
     la = max(0, int(get_option(opts, Option.Lookahead, 1)))
     panels = {}

@@ -102,7 +102,7 @@ def _getrf_p1(A, buf, thr, la, nopiv):
     nloc = bc.nloc
     ipiv = torch.zeros(max(min(m, n), 1), dtype=torch.int64, device=dev)   # panel-relative per step
     infos = torch.zeros(max(kt, 1), dtype=torch.int64, device=dev)
-    ss = StreamSet(dev)
+    ss = StreamSet(dev, reserve_cus=64)
     ev_tr = {}
     ss.fork()
     for k in range(kt):

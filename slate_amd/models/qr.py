@@ -116,7 +116,7 @@ def _geqrf_p1(A, buf, T, la):
     dev, dt = buf.device, s.dtype
     grid = grid_of(A) if q > 1 else None
     nloc = bc.nloc
-    ss = StreamSet(dev)
+    ss = StreamSet(dev, reserve_cus=64)
     ev_tr = {}
     ss.fork()
     for k in range(kt):
