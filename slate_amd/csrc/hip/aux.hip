@@ -8,6 +8,7 @@
 // are (rows/256) x (columns, grid-strided) with coalesced row access.
 #include "common.hpp"
 #include "kernels.hpp"
+#include "workspace.hpp"
 
 namespace slate_hip {
 
@@ -118,16 +119,20 @@ constexpr int HSIZE = 2048;      // hash slots (>= 2 x max swaps per call)
 constexpr int MAXSW = 512;       // max swaps per call (more: split into calls)
 }
 
-template <typename T>
+struct SwapPlan {                // folded permutation of one swap sequence
+    int nt;
+    int pad;
+    i64 trow[2 * MAXSW];         // touched rows
+    i64 tsrc[2 * MAXSW];         // original row now found at trow[t]
+};
+
+// Fold the swap sequence into the permutation ONCE (one workgroup; the
+// hash map lives in LDS), then laswp_apply_kernel streams the columns.
+// (Building the map in every column workgroup cost ~10-20 us per block.)
 __global__ void __launch_bounds__(256)
-laswp_kernel(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* __restrict__ ipiv, i64 ioff, int incx, int CCH) {
+laswp_setup_kernel(i64 k1, i64 k2, const i64* __restrict__ ipiv, i64 ioff, int incx, SwapPlan* plan) {
     __shared__ i64 hkey[HSIZE];
-    __shared__ int hval[HSIZE];       // index into touched list
-    __shared__ i64 trow[2 * MAXSW];   // touched rows
-    __shared__ i64 tsrc[2 * MAXSW];   // original row now found at trow[t]
-    __shared__ int ntouched;
-    extern __shared__ __align__(16) unsigned char dyn[];
-    T* buf = reinterpret_cast<T*>(dyn);   // [2*MAXSW][CCH] gathered rows (sized at launch)
+    __shared__ int hval[HSIZE];
     for (int h = threadIdx.x; h < HSIZE; h += blockDim.x) hkey[h] = -1;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -135,33 +140,40 @@ laswp_kernel(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* __restrict__ ipiv,
         auto slot = [&](i64 row) -> int {
             unsigned hsh = (unsigned)((row * 2654435761ull) >> 7) & (HSIZE - 1);
             while (hkey[hsh] != -1 && hkey[hsh] != row) hsh = (hsh + 1) & (HSIZE - 1);
-            if (hkey[hsh] == -1) { hkey[hsh] = row; hval[hsh] = cnt; trow[cnt] = row; tsrc[cnt] = row; ++cnt; }
+            if (hkey[hsh] == -1) { hkey[hsh] = row; hval[hsh] = cnt; plan->trow[cnt] = row; plan->tsrc[cnt] = row; ++cnt; }
             return hval[hsh];
         };
         const i64 ns = k2 - k1;
-        for (i64 s = 0; s < ns; ++s) {
-            i64 k = incx > 0 ? k1 + s : k2 - 1 - s;
+        for (i64 q = 0; q < ns; ++q) {
+            i64 k = incx > 0 ? k1 + q : k2 - 1 - q;
             i64 p = ipiv[k] - ioff;
             if (p == k) continue;
             int a = slot(k), b = slot(p);
-            i64 t = tsrc[a]; tsrc[a] = tsrc[b]; tsrc[b] = t;
+            i64 t = plan->tsrc[a]; plan->tsrc[a] = plan->tsrc[b]; plan->tsrc[b] = t;
         }
-        ntouched = cnt;
+        plan->nt = cnt;
     }
-    __syncthreads();
-    const int nt = ntouched;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+laswp_apply_kernel(i64 n, T* A, i64 lda, const SwapPlan* __restrict__ plan, int CCH) {
+    extern __shared__ __align__(16) unsigned char dyn[];
+    T* buf = reinterpret_cast<T*>(dyn);   // [nt][CCH] gathered rows
+    const int nt = plan->nt;
     if (nt == 0) return;
     const i64 c0 = (i64)blockIdx.x * CCH;
     const int ncols = (int)min((i64)CCH, n - c0);
-    // gather: buf[t][c] = A[tsrc[t], c0 + c]
+    // gather: buf[t][c] = A[tsrc[t], c0 + c]   (t fastest: the touched rows
+    // of one column; the row lists are read from L2, not rebuilt)
     for (int idx = threadIdx.x; idx < nt * CCH; idx += blockDim.x) {
         int t = idx % nt, c = idx / nt;
-        if (c < ncols) buf[t * CCH + c] = A[tsrc[t] + (c0 + c) * lda];
+        if (c < ncols) buf[t * CCH + c] = A[plan->tsrc[t] + (c0 + c) * lda];
     }
     __syncthreads();
     for (int idx = threadIdx.x; idx < nt * CCH; idx += blockDim.x) {
         int t = idx % nt, c = idx / nt;
-        if (c < ncols) A[trow[t] + (c0 + c) * lda] = buf[t * CCH + c];
+        if (c < ncols) A[plan->trow[t] + (c0 + c) * lda] = buf[t * CCH + c];
     }
 }
 
@@ -228,11 +240,13 @@ void laswp_off(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, i64 ioff, 
             for (i64 k = k2; k > k1; k -= MAXSW) laswp_off<T>(n, A, lda, std::max(k1, k - MAXSW), k, ipiv, ioff, s, incx);
         return;
     }
+    SwapPlan* plan = static_cast<SwapPlan*>(workspace(s, sizeof(SwapPlan), WS_L));
+    hipLaunchKernelGGL(laswp_setup_kernel, dim3(1), dim3(256), 0, s, k1, k2, ipiv, ioff, incx, plan);
     const size_t per_col = (size_t)2 * (k2 - k1) * sizeof(T);
-    int cch = (int)std::max<size_t>(1, std::min<size_t>(16, (96 * 1024) / per_col));
+    int cch = (int)std::max<size_t>(1, std::min<size_t>(32, (64 * 1024) / per_col));
     size_t shmem = per_col * cch;
     unsigned g = (unsigned)((n + cch - 1) / cch);
-    hipLaunchKernelGGL(laswp_kernel<T>, dim3(g), dim3(256), shmem, s, n, A, lda, k1, k2, ipiv, ioff, incx, cch);
+    hipLaunchKernelGGL(laswp_apply_kernel<T>, dim3(g), dim3(256), shmem, s, n, A, lda, plan, cch);
     HIP_LAUNCH_CHECK();
 }
 template <typename T>
