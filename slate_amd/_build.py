@@ -10,7 +10,7 @@ Two pybind11 extension modules are produced next to this file:
 
 Objects are cached under ``build/`` and rebuilt when a source or any header
 of the same directory is newer.  Used by ``__graft_entry__.build()``,
-``setup.py`` and ``python -m slate_amd._build``.
+``setup.py`` and ``python slate_amd/_build.py``.
 """
 from __future__ import annotations
 

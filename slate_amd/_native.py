@@ -17,7 +17,7 @@ try:
     from . import _host  # noqa: F401
 except ImportError as e:  # pragma: no cover - build problem
     raise ImportError(
-        "slate_amd._host is not built; run `python -m slate_amd._build` "
+        "slate_amd._host is not built; run `python slate_amd/_build.py` "
         f"(or __graft_entry__.build()): {e}") from e
 
 _hip = None
@@ -41,7 +41,7 @@ REAL_OF = {torch.float32: torch.float32, torch.float64: torch.float64,
 def hip():
     if _hip is None:
         raise HipError(f"slate_amd._hip (gfx950 kernels) failed to load: {_hip_error!r}; "
-                       "build it with `python -m slate_amd._build`")
+                       "build it with `python slate_amd/_build.py`")
     return _hip
 
 
