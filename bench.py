@@ -43,6 +43,42 @@ def grid_for(n):
     return {1: (1, 1), 2: (1, 2), 4: (2, 2), 8: (2, 4)}.get(n, (1, n))
 
 
+def _residual(args, A, A0, piv):
+    """Backward error of the last factorization (outside the timed region),
+    one rank only.  Mirrors the reference tester's checks
+    (test/test_posv.cc:304-345, test_gesv.cc:332-377): a random right-hand
+    side is pushed through the factors and ||A0 x - b|| / (||A0|| ||x|| n)
+    is reported; it must be O(eps)."""
+    F = A.storage.local[A.storage.origin_slot]
+    m, n = F.shape[0], F.shape[1]
+    g = torch.Generator(device=F.device).manual_seed(5)
+    if args.routine == "potrf":
+        L = torch.tril(F[:n, :n])
+        S = torch.tril(A0[:n, :n])
+        S = S + torch.tril(S, -1).mT
+        b = torch.rand(n, 1, dtype=F.dtype, device=F.device, generator=g)
+        y = torch.linalg.solve_triangular(L, b, upper=False)
+        x = torch.linalg.solve_triangular(L.mT, y, upper=True)
+        r = (S @ x - b).norm() / (S.norm() * x.norm() * n)
+    elif args.routine == "getrf":
+        b = torch.rand(n, 1, dtype=F.dtype, device=F.device, generator=g)
+        perm = list(range(n))
+        for i, j in enumerate(piv.ipiv.tolist()):     # LAPACK-style sequential swaps
+            perm[i], perm[j] = perm[j], perm[i]
+        pb = b[torch.as_tensor(perm, device=F.device)]
+        Lu = torch.tril(F[:n, :n], -1) + torch.eye(n, dtype=F.dtype, device=F.device)
+        y = torch.linalg.solve_triangular(Lu, pb, upper=False)
+        x = torch.linalg.solve_triangular(torch.triu(F[:n, :n]), y, upper=True)
+        r = (A0[:n, :n] @ x - b).norm() / (A0[:n, :n].norm() * x.norm() * n)
+    elif args.routine == "geqrf":
+        R = torch.triu(F[:n, :n])
+        # ||R^T R - A^T A|| / (||A||^2 n): Q-free backward-error proxy
+        r = (R.mT @ R - A0.mT @ A0).norm() / (A0.norm() ** 2 * n)
+    else:
+        return None
+    return float(f"{r.item():.3e}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -54,6 +90,7 @@ def main():
     ap.add_argument("--routine", default="potrf", choices=["potrf", "getrf", "gemm", "geqrf"])
     ap.add_argument("--lookahead", type=int, default=1)
     ap.add_argument("--grid", default=None, help="PxQ override")
+    ap.add_argument("--check", type=int, default=1, help="residual check after timing (1 rank)")
     args = ap.parse_args()
 
     import slate_amd as sl
@@ -63,9 +100,12 @@ def main():
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     p, q = grid_for(world) if args.grid is None else map(int, args.grid.lower().split("x"))
-    dev = torch.device("cuda", torch.cuda.current_device())
+    gpu = torch.cuda.is_available()
+    dev = torch.device("cuda", torch.cuda.current_device()) if gpu else torch.device("cpu")
+    sync = torch.cuda.synchronize if gpu else (lambda: None)
     n, nb = args.n, args.nb
-    opts = {sl.Option.Lookahead: args.lookahead, sl.Option.Target: sl.Target.Devices}
+    opts = {sl.Option.Lookahead: args.lookahead,
+            sl.Option.Target: sl.Target.Devices if gpu else sl.Target.HostTask}
 
     if args.routine == "potrf":
         A = sl.HermitianMatrix(sl.Uplo.Lower, n, nb=nb, p=p, q=q, device=dev)
@@ -104,14 +144,15 @@ def main():
     for _ in range(args.warmup):
         info = step()
     comm.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         info = step()
     comm.barrier()
-    torch.cuda.synchronize()
+    sync()
     dt = time.perf_counter() - t0
     dt_max = comm.allreduce_scalar(dt, "max") if world > 1 else dt
+    resid = _residual(args, A, backup, locals().get("piv")) if (world == 1 and args.check) else None
     fl = flops(args.routine, n, args.m)
     gflops = fl * args.steps / dt_max / 1e9
     ok = (info == 0) if isinstance(info, int) else True
@@ -131,6 +172,7 @@ def main():
             "data": "synthetic (Philox SPD/rand matrix generated on device)",
             "pct_fp64_peak": round(100 * gflops / 1e3 / (FP64_PEAK_TF * world), 2),
             "info_ok": bool(ok),
+            "residual": resid,
             "config": {"model": f"d{args.routine} n={n} nb={nb}", "global_batch": 1, "seq_len": n,
                        "n": n, "nb": nb, "grid": f"{p}x{q}", "lookahead": args.lookahead,
                        "parallelism": f"2d-block-cyclic {p}x{q}"},

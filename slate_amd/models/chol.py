@@ -102,7 +102,9 @@ def _potrf_lower(A, opts):
         own_col = (g % q) == pc
         own_diag = own_col and (g % p) == pr
         with ss.use(ss.panel):
-            if t - la - 1 >= 0 and (t - la - 1) in ev_tr:
+            # panel column g: every trailing update of steps <= t-la-1 (the
+            # first column of step t-la-1's trailing update is this one)
+            if t - la - 1 >= 0:
                 ss.wait(ss.panel, ev_tr[t - la - 1])
             with trace_block("potrf::panel"):
                 if own_diag:
@@ -136,6 +138,10 @@ def _potrf_lower(A, opts):
                     Lcol = Prow
             # lookahead columns g+1 .. g+la
             lc_la = min(tiles_local_before(g + 1 + la, q, pc) * nb, lc_end)
+            # the newest lookahead column g+la was in step t-1's trailing
+            # update (its first part): wait for exactly that part
+            if t >= 1 and la > 0:
+                ss.wait(ss.panel, ev_tr[t - 1])
             if lc_la > lc1 and nrow:
                 mask = (1, nb, p, pr, q, pc, lr1, lc1, 0)
                 ops.gemm(-1.0, Prow, Lcol[0:lc_la - lc1], 1.0, buf[lr1:lr_end, lc1:lc_la], 'N', ct, mask)
@@ -144,15 +150,21 @@ def _potrf_lower(A, opts):
         us = ss.update[0]
         with ss.use(us):
             ss.wait(us, ev_panel)
-            if lc_end > lc_la and nrow:
-                with trace_block("potrf::trailing"):
-                    if Prow.is_cuda:
-                        Prow.record_stream(us)
-                        Lcol.record_stream(us)
-                    mask = (1, nb, p, pr, q, pc, lr1, lc_la, 0)
-                    ops.gemm(-1.0, Prow, Lcol[lc_la - lc1:lc_end - lc1], 1.0, buf[lr1:lr_end, lc_la:lc_end],
-                             'N', ct, mask)
-            ev_tr[t] = ss.event(us)
+            # split: column g+1+la first (the next step's newest lookahead
+            # column and, la steps later, a panel), event, then the rest
+            lc_nx = min(tiles_local_before(g + 2 + la, q, pc) * nb, lc_end)
+            lc_nx = max(lc_nx, lc_la)
+            if Prow.is_cuda and lc_end > lc_la and nrow:
+                Prow.record_stream(us)
+                Lcol.record_stream(us)
+            with trace_block("potrf::trailing"):
+                for c0, c1 in ((lc_la, lc_nx), (lc_nx, lc_end)):
+                    if c1 > c0 and nrow:
+                        mask = (1, nb, p, pr, q, pc, lr1, c0, 0)
+                        ops.gemm(-1.0, Prow, Lcol[c0 - lc1:c1 - lc1], 1.0, buf[lr1:lr_end, c0:c1],
+                                 'N', ct, mask)
+                    if c0 == lc_la:
+                        ev_tr[t] = ss.event(us)
     ss.join()
     s.mark_local_modified(slot)
     # info: first failing global column, reduced over ranks

@@ -116,7 +116,9 @@ def _getrf_p1(A, buf, thr, la, nopiv):
         lcla = min(tiles_local_before(k + 1 + la, q, pc) * nb, nloc)
         piv = ipiv[r0:r0 + kb]
         with ss.use(ss.panel):
-            if k - la - 1 >= 0 and (k - la - 1) in ev_tr:
+            # panel column k: trailing updates of steps <= k-la-1 (column k is
+            # the first part of step k-la-1's trailing update)
+            if k - la - 1 >= 0:
                 ss.wait(ss.panel, ev_tr[k - la - 1])
             with trace_block("getrf::panel"):
                 if own:
@@ -129,22 +131,33 @@ def _getrf_p1(A, buf, thr, la, nopiv):
                     if not nopiv:
                         grid.row_comm.bcast(piv, k % q)
                     bcast_tile(grid.row_comm, Lp, k % q)
-                # swap the already-factored left columns (tiles < k)
-                if not nopiv and lck > 0:
-                    ops.laswp(buf[:m, 0:lck], ipiv, r0, r0 + kb, ioff=-r0)
-            # lookahead columns
+            # lookahead columns; the newest one (k+la) was the first part of
+            # step k-1's trailing update
+            if k >= 1 and la > 0:
+                ss.wait(ss.panel, ev_tr[k - 1])
             if lcla > lc1:
                 _update_cols(buf, Lp, ipiv, r0, kb, m, lc1, lcla, nopiv)
             ev_panel = ss.event(ss.panel)
         us = ss.update[0]
         with ss.use(us):
             ss.wait(us, ev_panel)
-            if nloc > lcla:
-                with trace_block("getrf::trailing"):
-                    if Lp.is_cuda:
-                        Lp.record_stream(us)
-                    _update_cols(buf, Lp, ipiv, r0, kb, m, lcla, nloc, nopiv)
-            ev_tr[k] = ss.event(us)
+            if nloc > lcla and Lp.is_cuda:
+                Lp.record_stream(us)
+            # column k+1+la first (next step's newest lookahead column), event,
+            # then the rest
+            lcnx = max(min(tiles_local_before(k + 2 + la, q, pc) * nb, nloc), lcla)
+            with trace_block("getrf::trailing"):
+                if lcnx > lcla:
+                    _update_cols(buf, Lp, ipiv, r0, kb, m, lcla, lcnx, nopiv)
+                ev_tr[k] = ss.event(us)
+                if nloc > lcnx:
+                    _update_cols(buf, Lp, ipiv, r0, kb, m, lcnx, nloc, nopiv)
+            # swap the already-factored left columns (tiles < k).  This runs
+            # on the update stream, after every trailing update that still
+            # reads an earlier panel's L rows (trailing j < k overlaps panel
+            # k; swapping those rows on the panel stream would race).
+            if not nopiv and lck > 0:
+                ops.laswp(buf[:m, 0:lck], ipiv, r0, r0 + kb, ioff=-r0)
     ss.join()
     # global pivots
     glob = ipiv.clone()

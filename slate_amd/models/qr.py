@@ -127,9 +127,9 @@ def _geqrf_p1(A, buf, T, la):
         lck = tiles_local_before(k, q, pc) * nb
         lc1 = min(tiles_local_before(k + 1, q, pc) * nb, nloc)
         lcla = min(tiles_local_before(k + 1 + la, q, pc) * nb, nloc)
-        tau = torch.zeros(kb, dtype=dt, device=dev)
         with ss.use(ss.panel):
-            if k - la - 1 >= 0 and (k - la - 1) in ev_tr:
+            tau = torch.zeros(kb, dtype=dt, device=dev)     # on the panel stream
+            if k - la - 1 >= 0:
                 ss.wait(ss.panel, ev_tr[k - la - 1])
             with trace_block("geqrf::panel"):
                 Tk = ops.colmajor_empty(kb, kb, dt, dev)
@@ -141,6 +141,9 @@ def _geqrf_p1(A, buf, T, la):
                     bcast_tile(grid.row_comm, V, k % q)
                     bcast_tile(grid.row_comm, Tk, k % q)
                     grid.row_comm.bcast(tau, k % q)
+            # newest lookahead column k+la: first part of step k-1's trailing
+            if k >= 1 and la > 0:
+                ss.wait(ss.panel, ev_tr[k - 1])
             if lcla > lc1:
                 _apply_qh(V, Tk, buf[r0:m, lc1:lcla])
             ev_panel = ss.event(ss.panel)
@@ -148,13 +151,16 @@ def _geqrf_p1(A, buf, T, la):
         us = ss.update[0]
         with ss.use(us):
             ss.wait(us, ev_panel)
-            if nloc > lcla:
-                with trace_block("geqrf::trailing"):
-                    if V.is_cuda:
-                        V.record_stream(us)
-                        Tk.record_stream(us)
-                    _apply_qh(V, Tk, buf[r0:m, lcla:nloc])
-            ev_tr[k] = ss.event(us)
+            if nloc > lcla and V.is_cuda:
+                V.record_stream(us)
+                Tk.record_stream(us)
+            lcnx = max(min(tiles_local_before(k + 2 + la, q, pc) * nb, nloc), lcla)
+            with trace_block("geqrf::trailing"):
+                if lcnx > lcla:
+                    _apply_qh(V, Tk, buf[r0:m, lcla:lcnx])
+                ev_tr[k] = ss.event(us)
+                if nloc > lcnx:
+                    _apply_qh(V, Tk, buf[r0:m, lcnx:nloc])
     ss.join()
 
 
