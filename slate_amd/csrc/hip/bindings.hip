@@ -117,6 +117,8 @@ static void register_kernels(py::module& m) {
         dispatch(dt, [&](auto z) { using T = decltype(z);
             trtri<T>(uplo, diag, n, P<T>(A), lda, P<i64>(info), S(st)); });
     });
+    m.def("potrf_lds_profile", [](i64 n, uintptr_t A, i64 lda, uintptr_t info, uintptr_t prof, uintptr_t st) {
+        potrf_lds_profile((int)n, P<double>(A), lda, P<i64>(info), P<i64>(prof), S(st)); });
     m.def("getrf_work_bytes", []() { return (i64)getrf_work_bytes(); });
     m.def("geqrf", [](char dt, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t tau, uintptr_t Tm, i64 ldt,
                       uintptr_t V, i64 ldv, uintptr_t work, uintptr_t st) {

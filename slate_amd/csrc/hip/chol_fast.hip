@@ -1,0 +1,415 @@
+// Latency-optimised fp64 kernels of the Cholesky panel on gfx950:
+//
+//   potrf_lds   ONE workgroup (512 threads, one CU) factors a lower n <= 512
+//               tile: left-looking over 32-wide column blocks; the block
+//               column (<= 512 x 32) lives in LDS (131 KB of the 160 KB), the
+//               left-looking update A(c0:, J) -= L(c0:, :c0) L(J, :c0)^T runs
+//               on the f64 MFMA (operands streamed from L2, where this CU just
+//               wrote them), the 16-wide diagonal sub-blocks are factored by
+//               one wave in registers (v_readlane broadcasts, no barriers) and
+//               the rows below are solved row-per-thread against them.  One
+//               launch replaces the 4 x (potrf_small + trsm + herk) chain of
+//               potrf.hip (measured 870 us for n = 512 on MI355X) and leaves
+//               every other CU to the trailing update.
+//   tri_inv32   inverses of the 32 x 32 diagonal blocks of a lower triangle
+//               (one wave per block, column-per-lane substitution).
+//   trsm_rlt    X L^T = alpha B for a tall B (the Cholesky panel solve,
+//               src/internal/internal_trsm.cc:244 in the reference): every
+//               workgroup owns 64 rows, walks 32-column blocks,
+//               R = alpha B_J - X_{<J} L_{J,<J}^T (MFMA, K = 32 J) and
+//               X_J = R inv(L_JJ)^T (MFMA against tri_inv32's output): every
+//               flop on the matrix cores, one launch, no copy-back.
+#include "common.hpp"
+#include "kernels.hpp"
+#include "launchers.hpp"
+#include "workspace.hpp"
+
+namespace slate_hip {
+
+namespace {
+constexpr int PN = 512;          // largest tile of potrf_lds
+constexpr int PB = 32;           // block-column width
+constexpr int PT = 512;          // threads of potrf_lds (8 waves: 256-VGPR budget)
+constexpr int PLD = PN + 1;      // LDS column stride (doubles)
+
+__device__ inline double rl(double v, int src) {
+    union { double d; int w[2]; } a, b;
+    a.d = v;
+    b.w[0] = __builtin_amdgcn_readlane(a.w[0], src);
+    b.w[1] = __builtin_amdgcn_readlane(a.w[1], src);
+    return b.d;
+}
+__device__ inline d4 mma(double x, double y, d4 c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, c, 0, 0, 0); }
+}  // namespace
+
+// acc[t] += sum_k X(r, k) Y(c, k) over k in [0, K), for one
+// 16-row strip (rows xr) and NT 16-column tiles (rows yr[t] of Y); lane
+// layout of the f64 MFMA: operand element (lane & 15, k + (lane >> 4)).
+// 32-k chunks double-buffered in registers: 24 loads per lane in flight
+// while the previous chunk's MFMAs issue.  Requires K % 32 == 0.
+typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+// raw buffer descriptor on a wave-uniform base (32-bit offsets: every operand
+// region here spans < 2 GiB from its base)
+__device__ inline __amdgpu_buffer_rsrc_t rsrc_of(const double* p) {
+    const uintptr_t a = (uintptr_t)p;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uintptr_t)hi << 32) | lo), 0, 0x7fffffff, 0x00020000);
+}
+__device__ inline double bld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+}
+
+// acc[s][t] += sum_k X(xr[s], k) Y(yr[t], k), k in [0, K), K % (8 U) == 0:
+// NS 16-row strips of X against NT 16-row tiles of Y, per-lane rows xr/yr
+// relative to wave-uniform bases.  Chunks of U k-steps (of 4) are
+// double-buffered in registers: one chunk's loads are in flight while the
+// previous chunk's NS*NT*U MFMAs issue.
+template <int NS, int NT, int U>
+__device__ inline void strip_update(d4 (&acc)[NS][NT], const double* Xb, const int (&xr)[NS], i64 ldx,
+                                    const double* Yb, const int (&yr)[NT], i64 ldy, int K, int lane) {
+    const int kq = lane >> 4;
+    const __amdgpu_buffer_rsrc_t rx = rsrc_of(Xb), ry = rsrc_of(Yb);
+    int vx[NS], vy[NT];
+    #pragma unroll
+    for (int s = 0; s < NS; ++s) vx[s] = (int)((xr[s] + kq * ldx) * 8);
+    #pragma unroll
+    for (int t = 0; t < NT; ++t) vy[t] = (int)((yr[t] + kq * ldy) * 8);
+    double a[2][NS][U], b[2][NT][U];
+    auto load = [&](int buf, int k) {
+        #pragma unroll
+        for (int u = 0; u < U; ++u) {
+            #pragma unroll
+            for (int s = 0; s < NS; ++s) a[buf][s][u] = bld(rx, vx[s], (int)((k + 4 * u) * ldx * 8));
+            #pragma unroll
+            for (int t = 0; t < NT; ++t) b[buf][t][u] = bld(ry, vy[t], (int)((k + 4 * u) * ldy * 8));
+        }
+    };
+    auto comp = [&](int buf) {
+        #pragma unroll
+        for (int u = 0; u < U; ++u)
+            #pragma unroll
+            for (int s = 0; s < NS; ++s)
+                #pragma unroll
+                for (int t = 0; t < NT; ++t) acc[s][t] = mma(b[buf][t][u], a[buf][s][u], acc[s][t]);
+    };
+    if (K <= 0) return;
+    load(0, 0);
+    int k = 0;
+    for (; k + 4 * U < K; k += 8 * U) {
+        load(1, k + 4 * U);
+        comp(0);
+        if (k + 8 * U < K) load(0, k + 8 * U);
+        comp(1);
+    }
+    if (k < K) comp(0);
+}
+
+// ---------------------------------------------------------------- potrf_lds
+__global__ void __launch_bounds__(PT)
+potrf_lds_kernel(int n, double* __restrict__ A, i64 lda, i64* info, i64 info_off, i64* prof) {
+    __shared__ double P[PB * PLD];          // P[c * PLD + r] = A(c0 + r, c0 + c)
+    __shared__ double Li[16][17];            // inverse of the current 16 x 16 diagonal sub-block
+    __shared__ __attribute__((aligned(16))) double Ld[16][18];   // factored sub-block (row-major, zero above)
+    __shared__ __attribute__((aligned(16))) double colb[16];
+    __shared__ double rdl[16];
+    __shared__ int s_fail;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) s_fail = 0;
+    // optional per-phase shader-clock totals (prof != nullptr: tools only)
+    i64 ph[6] = {0, 0, 0, 0, 0, 0};
+    i64 tlast = clock64();
+    const i64 t0 = tlast, w0 = wall_clock64();
+#define STAMP(i) do { if (prof && tid == 0) { const i64 t_ = clock64(); ph[i] += t_ - tlast; tlast = t_; } } while (0)
+    for (int c0 = 0; c0 < n; c0 += PB) {
+        const int jb = min(PB, n - c0), M = n - c0;
+        const int lr = tid;                               // one row per thread, 32 columns
+        // ---- load the block column (lower part): all 32 loads in flight at once
+        {
+            double v[PB];
+            const double* src = A + (c0 + min(lr, M - 1)) + (i64)c0 * lda;
+            #pragma unroll
+            for (int c = 0; c < PB; ++c) v[c] = src[(i64)min(c, jb - 1) * lda];
+            #pragma unroll
+            for (int c = 0; c < PB; ++c)
+                if (c < jb && lr < M && lr >= c) P[c * PLD + lr] = v[c];
+        }
+        __syncthreads();
+        STAMP(0);
+        // ---- left-looking update by the factored columns [0, c0)
+        if (c0 > 0) {
+            // strip pairs (2s, 2s+1) x both 16-column tiles per wave
+            for (int h = 0; h < 2; ++h) {
+                const int sp = w + 8 * h;
+                if (32 * sp >= M) continue;
+                const int xr[2] = {min(32 * sp + (lane & 15), M - 1), min(32 * sp + 16 + (lane & 15), M - 1)};
+                const int yr[2] = {min(lane & 15, M - 1), min(16 + (lane & 15), M - 1)};
+                d4 acc[2][2];
+                #pragma unroll
+                for (int u = 0; u < 2; ++u)
+                    #pragma unroll
+                    for (int t = 0; t < 2; ++t) acc[u][t] = d4{0, 0, 0, 0};
+                strip_update<2, 2, 4>(acc, A + c0, xr, lda, A + c0, yr, lda, c0, lane);
+                #pragma unroll
+                for (int u = 0; u < 2; ++u)
+                    #pragma unroll
+                    for (int t = 0; t < 2; ++t)
+                        #pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int m = 32 * sp + 16 * u + (lane & 15), c = 16 * t + (lane >> 4) + 4 * r;
+                            if (m < M && c < jb && m >= c) P[c * PLD + m] -= acc[u][t][r];
+                        }
+            }
+            __syncthreads();
+        }
+        STAMP(1);
+        // ---- factor the block column in LDS, 16 columns at a time:
+        //  (1) wave 0: 16 x 16 diagonal sub-block -> L_qq and inv(L_qq) in
+        //      registers (v_readlane broadcasts, no barriers);
+        //  (2) every wave: rows below, X = P inv(L_qq)^T on the MFMA;
+        //  (3) first half only: P(:, 16:32) -= X X(16:32, :)^T on the MFMA.
+        for (int q0 = 0; q0 < jb; q0 += 16) {
+            const int wq = min(16, jb - q0);
+            if (w == 0) {
+                // lane i < 16 owns row i; column j is broadcast through LDS
+                // (colb) -- 15 independent LDS reads per step instead of a
+                // chain of v_readlane hazards
+                double row[16];
+                #pragma unroll
+                for (int c = 0; c < 16; ++c)
+                    row[c] = (lane < wq && c <= lane) ? P[(q0 + c) * PLD + q0 + lane] : (lane == c ? 1.0 : 0.0);
+                int fail = 0;
+                #pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    double d = rl(row[j], j);
+                    if (j < wq && !(d > 0.0)) { if (!fail) fail = c0 + q0 + j + 1; d = 1.0; }
+                    const double sq = sqrt(d), inv = 1.0 / sq;
+                    if (lane == j) row[j] = sq;
+                    else if (lane > j) row[j] *= inv;
+                    if (lane < 16) colb[lane] = row[j];
+                    if (lane == 0) rdl[j] = inv;
+                    __builtin_amdgcn_wave_barrier();
+                    double cb[16];
+                    #pragma unroll
+                    for (int c = 0; c < 16; c += 2) {      // all reads issued before any use
+                        const d2 v = *reinterpret_cast<const d2*>(&colb[c]);
+                        cb[c] = v.x; cb[c + 1] = v.y;
+                    }
+                    #pragma unroll
+                    for (int c = j + 1; c < 16; ++c)
+                        if (lane >= c) row[c] -= row[j] * cb[c];
+                    __builtin_amdgcn_wave_barrier();
+                }
+                if (lane < 16) {
+                    #pragma unroll
+                    for (int c = 0; c < 16; ++c) Ld[lane][c] = (c <= lane) ? row[c] : 0.0;
+                }
+                if (lane < wq) {
+                    #pragma unroll
+                    for (int c = 0; c < 16; ++c)
+                        if (c <= lane) P[(q0 + c) * PLD + q0 + lane] = row[c];
+                }
+                __builtin_amdgcn_wave_barrier();
+                // inv(L_qq): lane c < 16 computes column c; L(r, l) are
+                // broadcast LDS reads independent of the x chain
+                double x[16];
+                #pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    double acc = (r == lane) ? 1.0 : 0.0;
+                    double lr_[16];
+                    #pragma unroll
+                    for (int l = 0; l < 16; l += 2) {
+                        if (l < r) {
+                            const d2 v = *reinterpret_cast<const d2*>(&Ld[r][l]);
+                            lr_[l] = v.x; lr_[l + 1] = v.y;
+                        }
+                    }
+                    #pragma unroll
+                    for (int l = 0; l < r; ++l) acc -= lr_[l] * x[l];
+                    x[r] = (r >= lane) ? acc * rdl[r] : 0.0;
+                }
+                if (lane < 16) {
+                    #pragma unroll
+                    for (int r = 0; r < 16; ++r) Li[r][lane] = x[r];     // Li[r][c] = inv(L_qq)(r, c)
+                }
+                if (lane == 0 && fail && !s_fail) s_fail = fail;
+            }
+            __syncthreads();
+            STAMP(2);
+            // (2) strips of 16 rows below the sub-block: X = P(:, q0:q0+16) inv^T
+            const int rb0 = q0 + wq;                          // first row below
+            const int nstrip = (M - rb0 + 15) / 16;
+            for (int st = w; st < nstrip; st += PT / 64) {
+                const int rb = rb0 + 16 * st;
+                const int rr = rb + (lane & 15);
+                const bool ok = rr < M;
+                double a[4];
+                #pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int k = 4 * u + (lane >> 4);
+                    a[u] = (ok && k < wq) ? P[(q0 + k) * PLD + rr] : 0.0;
+                }
+                d4 acc = {0, 0, 0, 0};
+                #pragma unroll
+                for (int u = 0; u < 4; ++u) acc = mma(Li[lane & 15][4 * u + (lane >> 4)], a[u], acc);
+                #pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int c = (lane >> 4) + 4 * r;
+                    if (ok && c < wq) P[(q0 + c) * PLD + rr] = acc[r];
+                }
+            }
+            __syncthreads();
+            STAMP(3);
+            // (3) second half of the block column by the first
+            if (q0 == 0 && jb > 16) {
+                const int ns3 = (M - 16 + 15) / 16;
+                for (int st = w; st < ns3; st += PT / 64) {
+                    const int rr = 16 + 16 * st + (lane & 15);
+                    const bool ok = rr < M;
+                    d4 acc = {0, 0, 0, 0};
+                    #pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int k = 4 * u + (lane >> 4);
+                        const double a = ok ? P[k * PLD + rr] : 0.0;
+                        acc = mma(P[k * PLD + 16 + (lane & 15)], a, acc);
+                    }
+                    #pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int c = (lane >> 4) + 4 * r;
+                        if (ok && 16 + c < jb) P[(16 + c) * PLD + rr] -= acc[r];
+                    }
+                }
+                __syncthreads();
+                STAMP(4);
+            }
+        }
+        // ---- write back (lower part); the next update reads it from L2
+        #pragma unroll 8
+        for (int c = 0; c < PB; ++c)
+            if (c < jb && lr < M && lr >= c) A[(c0 + lr) + (i64)(c0 + c) * lda] = P[c * PLD + lr];
+        __syncthreads();
+        STAMP(5);
+    }
+#undef STAMP
+    if (prof && tid == 0) {
+        for (int i = 0; i < 6; ++i) prof[i] = ph[i];
+        prof[6] = clock64() - t0;
+        prof[7] = wall_clock64() - w0;
+    }
+    if (tid == 0 && s_fail && info)
+        atomicCAS(reinterpret_cast<unsigned long long*>(info), 0ull, (unsigned long long)(s_fail + info_off));
+}
+
+// ---------------------------------------------------------------- tri_inv32
+// Winv[b] (32 x 32, column-major, zero above the diagonal) = inv(L_bb).
+__global__ void __launch_bounds__(64)
+tri_inv32_kernel(int n, const double* __restrict__ L, i64 ldl, double* __restrict__ Winv, bool unit) {
+    __shared__ double S[32][33];            // S[r][c] = L(c0 + r, c0 + c)
+    const int b = blockIdx.x, c0 = 32 * b, jb = min(32, n - c0), t = threadIdx.x;
+    if (t < 32) {
+        #pragma unroll 8
+        for (int c = 0; c < 32; ++c) {
+            double v = (t == c) ? 1.0 : 0.0;
+            if (t < jb && c < jb && t >= c && !(unit && t == c)) v = L[(c0 + t) + (i64)(c0 + c) * ldl];
+            S[t][c] = v;
+        }
+    }
+    __syncthreads();
+    if (t >= 32) return;
+    const int c = t;                          // column of the inverse
+    double x[32];
+    #pragma unroll
+    for (int r = 0; r < 32; ++r) {
+        double acc = (r == c) ? 1.0 : 0.0;
+        #pragma unroll
+        for (int l = 0; l < r; ++l)
+            if (l >= c) acc -= S[r][l] * x[l];
+        x[r] = (r >= c) ? acc / S[r][r] : 0.0;
+    }
+    double* W = Winv + (i64)b * 1024;
+    #pragma unroll
+    for (int r = 0; r < 32; ++r) W[r + 32 * c] = x[r];
+}
+
+// ---------------------------------------------------------------- trsm_rlt
+// X L^T = alpha B (B: m x n, L: n x n lower), X overwrites B.
+constexpr int TBM = 64;
+__global__ void __launch_bounds__(256)
+trsm_rlt_kernel(i64 m, int n, double alpha, const double* __restrict__ L, i64 ldl, const double* __restrict__ Winv,
+                double* __restrict__ B, i64 ldb) {
+    __shared__ double R[32][TBM + 1];       // R[c][r]
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const i64 r0 = (i64)blockIdx.x * TBM;
+    const int mr = (int)min((i64)TBM, m - r0);
+    const int ml = 16 * w + (lane & 15);     // this lane's row within the block (MFMA m index)
+    const i64 rx = r0 + min(ml, mr - 1);     // clamped (valid) row for loads
+    for (int c0 = 0; c0 < n; c0 += 32) {
+        const int jb = min(32, n - c0);
+        d4 acc2[1][2] = {{d4{0, 0, 0, 0}, d4{0, 0, 0, 0}}};
+        if (c0 > 0) {
+            const int xr[1] = {(int)(rx - r0)};
+            const int yr[2] = {min(lane & 15, n - 1 - c0), min(16 + (lane & 15), n - 1 - c0)};
+            strip_update<1, 2, 8>(acc2, B + r0, xr, ldb, L + c0, yr, ldl, c0, lane);
+        }
+        d4 (&acc)[2] = acc2[0];
+        #pragma unroll
+        for (int t = 0; t < 2; ++t)
+            #pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int c = 16 * t + (lane >> 4) + 4 * r;
+                double v = 0.0;
+                if (ml < mr && c < jb) v = alpha * B[(r0 + ml) + (i64)(c0 + c) * ldb] - acc[t][r];
+                R[c][ml] = v;
+            }
+        __syncthreads();
+        // X_J = R inv(L_JJ)^T
+        const double* W = Winv + (i64)(c0 / 32) * 1024;
+        d4 x[2] = {d4{0, 0, 0, 0}, d4{0, 0, 0, 0}};
+        #pragma unroll
+        for (int k = 0; k < 32; k += 4) {
+            const int kk = k + (lane >> 4);
+            const double a = R[kk][ml];
+            #pragma unroll
+            for (int t = 0; t < 2; ++t) x[t] = mma(W[(16 * t + (lane & 15)) + 32 * kk], a, x[t]);
+        }
+        #pragma unroll
+        for (int t = 0; t < 2; ++t)
+            #pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int c = 16 * t + (lane >> 4) + 4 * r;
+                if (ml < mr && c < jb) B[(r0 + ml) + (i64)(c0 + c) * ldb] = x[t][r];
+            }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------- launchers
+bool potrf_fast(int n, double* A, i64 lda, i64* info, i64 info_off, hipStream_t s) {
+    if (n <= 0 || n > PN) return false;
+    hipLaunchKernelGGL(potrf_lds_kernel, dim3(1), dim3(PT), 0, s, n, A, lda, info, info_off, (i64*)nullptr);
+    HIP_LAUNCH_CHECK();
+    return true;
+}
+
+// tools: phase totals (shader clocks: load, update, diag, solve, half, writeback,
+// total) and wall-clock ticks (100 MHz) of one potrf_lds launch
+void potrf_lds_profile(int n, double* A, i64 lda, i64* info, i64* prof, hipStream_t s) {
+    hipLaunchKernelGGL(potrf_lds_kernel, dim3(1), dim3(PT), 0, s, n, A, lda, info, (i64)0, prof);
+    HIP_LAUNCH_CHECK();
+}
+
+bool trsm_rlt_fast(i64 m, i64 n, double alpha, const double* L, i64 ldl, double* B, i64 ldb, bool unit,
+                   hipStream_t s) {
+    if (m <= 0 || n <= 0) return true;
+    if (n > 1024) return false;
+    const int nbj = (int)((n + 31) / 32);
+    double* W = static_cast<double*>(workspace(s, sizeof(double) * (size_t)nbj * 1024, WS_L));
+    hipLaunchKernelGGL(tri_inv32_kernel, dim3(nbj), dim3(64), 0, s, (int)n, L, ldl, W, unit);
+    HIP_LAUNCH_CHECK();
+    hipLaunchKernelGGL(trsm_rlt_kernel, dim3((unsigned)((m + TBM - 1) / TBM)), dim3(256), 0, s, m, (int)n, alpha, L,
+                       ldl, (const double*)W, B, ldb);
+    HIP_LAUNCH_CHECK();
+    return true;
+}
+
+}  // namespace slate_hip

@@ -12,6 +12,12 @@ template <typename T>
 void trmm(char side, char uplo, char trans, char diag, i64 m, i64 n, T alpha,
           const T* A, i64 lda, T* B, i64 ldb, hipStream_t s);
 
+// chol_fast.hip (fp64 fast paths; return false when the shape is not covered)
+bool potrf_fast(int n, double* A, i64 lda, i64* info, i64 info_off, hipStream_t s);
+void potrf_lds_profile(int n, double* A, i64 lda, i64* info, i64* prof, hipStream_t s);
+bool trsm_rlt_fast(i64 m, i64 n, double alpha, const double* L, i64 ldl, double* B, i64 ldb, bool unit,
+                   hipStream_t s);
+
 // aux.hip
 template <typename T> void geset(char uplo, i64 m, i64 n, T off, T diag, T* A, i64 lda, hipStream_t s);
 template <typename T> void gescale(char uplo, i64 m, i64 n, T alpha, T* A, i64 lda, hipStream_t s);

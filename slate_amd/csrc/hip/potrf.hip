@@ -10,6 +10,7 @@
 //   -> masked MFMA GEMM (herk) of the trailing triangle.
 // info (1-based first non-positive pivot, 0 on success) is kept in a device
 // int64 (first failure wins via atomicCAS) so the DAG never syncs the host.
+#include <type_traits>
 #include "common.hpp"
 #include "kernels.hpp"
 #include "launchers.hpp"
@@ -218,6 +219,23 @@ template <typename T>
 void potrf_tile(char uplo, int n, T* A, i64 lda, i64* info, hipStream_t s) {
     if (info) HIP_CHECK(hipMemsetAsync(info, 0, sizeof(i64), s));
     if (n <= 0) return;
+    if constexpr (std::is_same<T, double>::value) {
+        if (uplo == 'L') {
+            // 512-wide diagonal blocks by the one-CU LDS kernel, panel by the
+            // blocked-inverse MFMA trsm, trailing triangle by the masked GEMM
+            for (int k0 = 0; k0 < n; k0 += 512) {
+                const int kb = std::min(512, n - k0);
+                T* Akk = A + k0 + (i64)k0 * lda;
+                potrf_fast(kb, Akk, lda, info, k0, s);
+                const int m = n - k0 - kb;
+                if (m <= 0) break;
+                T* P = A + (k0 + kb) + (i64)k0 * lda;
+                trsm_rlt_fast(m, kb, 1.0, Akk, lda, P, lda, false, s);
+                herk_lower<T>('L', m, kb, P, lda, A + (k0 + kb) + (i64)(k0 + kb) * lda, lda, s);
+            }
+            return;
+        }
+    }
     constexpr int NS = ns_of<T>();
     const char ct = scalar_traits<T>::is_complex ? 'C' : 'T';
     const T one = s_from_real(T(), 1);

@@ -14,6 +14,7 @@
 //   trmm         diagonal blocks extracted once, then GEMMs into a workspace.
 // Workspaces come from the per-stream cache (workspace.hpp): no host sync,
 // no per-call allocation on the critical path.
+#include <type_traits>
 #include "common.hpp"
 #include "kernels.hpp"
 #include "launchers.hpp"
@@ -183,6 +184,12 @@ template <typename T>
 void trsm(char side, char uplo, char trans, char diag, i64 m, i64 n, T alpha,
           const T* A, i64 lda, T* B, i64 ldb, hipStream_t s) {
     if (m <= 0 || n <= 0) return;
+    if constexpr (std::is_same<T, double>::value) {
+        // X L^T = alpha B (the Cholesky panel): blocked-inverse MFMA kernel
+        if (side == 'R' && uplo == 'L' && trans != 'N' &&
+            trsm_rlt_fast(m, n, alpha, A, lda, B, ldb, diag == 'U', s))
+            return;
+    }
     const bool lower_eff = (uplo == 'L') == (trans == 'N');
     const i64 kt = side == 'L' ? m : n;
     const i64 nblk = (kt + BIG - 1) / BIG;

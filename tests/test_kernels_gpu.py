@@ -110,6 +110,46 @@ def test_potrf_tile_info():
     assert int(ops.potrf('L', A).item()) == 41
 
 
+@pytest.mark.parametrize("n", [1, 17, 32, 33, 100, 511, 512, 513, 1100])
+def test_potrf_tile_fp64_fast(n):
+    # one-CU LDS kernel (n <= 512) and its 512-blocked composition (n > 512);
+    # ragged 16/32-column edges, lda > n
+    X = ref(cm(n, n, torch.float64, 31))
+    S = X @ X.mT + n * torch.eye(n, dtype=torch.float64, device="cuda")
+    Abig = _cm(torch.zeros(n + 7, n, dtype=torch.float64, device="cuda"), "cuda")
+    Abig[:n].copy_(S)
+    A = Abig[:n]
+    info = ops.potrf('L', A)
+    assert int(info.item()) == 0
+    L = torch.tril(A)
+    assert (L @ L.mT - S).abs().max() / S.abs().max() < 1e-14
+    assert (torch.triu(A, 1) == torch.triu(S, 1)).all()          # upper triangle untouched
+
+
+@pytest.mark.parametrize("bad", [0, 15, 16, 40, 300])
+def test_potrf_tile_fp64_fast_info(bad):
+    n = 320
+    S = 4.0 * torch.eye(n, dtype=torch.float64, device="cuda")
+    S[bad, bad] = -1.0
+    A = _cm(S, "cuda")
+    assert int(ops.potrf('L', A).item()) == bad + 1
+
+
+@pytest.mark.parametrize("m,n", [(1, 1), (64, 32), (65, 33), (1000, 512), (4097, 100), (300, 1000)])
+@pytest.mark.parametrize("diag", ["N", "U"])
+def test_trsm_rlt_fp64_fast(m, n, diag):
+    # X L^T = alpha B: the Cholesky panel solve (tri_inv32 + trsm_rlt kernels)
+    T = torch.tril(ref(cm(n, n, torch.float64, 41))) / n + 2 * torch.eye(n, dtype=torch.float64, device="cuda")
+    Tu = T.clone()
+    if diag == 'U':
+        Tu.diagonal().fill_(1)
+    A = _cm(T, "cuda")
+    B = cm(m, n, torch.float64, 42)
+    B0 = B.clone()
+    ops.trsm('R', 'L', 'T', diag, -1.5, A, B)
+    assert ((B @ Tu.mT) + 1.5 * B0).abs().max() / B0.abs().max() < 1e-12
+
+
 @pytest.mark.parametrize("dt", [torch.float64, torch.complex128, torch.float32])
 @pytest.mark.parametrize("side", ["L", "R"])
 @pytest.mark.parametrize("uplo", ["L", "U"])

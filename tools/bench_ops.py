@@ -1,5 +1,5 @@
 """Isolated timings of the potrf-path device ops (one process, interleaved)."""
-import sys, time, torch
+import os, sys, time, torch
 sys.path.insert(0, '.')
 from slate_amd import ops
 
