@@ -86,7 +86,7 @@ def _potrf_lower(A, opts):
     R_end = s.row_offsets[gend] if A.last_mb is None else s.row_offsets[gend - 1] + A.last_mb
     lr_end = _lstart(R_end, nb, pr, p)
     lc_end = _lstart(R_end, nb, pc, q)
-    ss = StreamSet(dev)
+    ss = StreamSet(dev, reserve_cus=0)   # one-CU panel kernels: no reserved CUs (measured: 49.0 vs 45.1 TF/s with 32)
     infos = torch.zeros(max(nt, 1), dtype=torch.int64, device=dev)
     plans = _plan_col_gathers(A, g0, nt, nb, p, q, pr, pc, dev) if (p > 1 or q > 1) else None
     ev_tr = {}
