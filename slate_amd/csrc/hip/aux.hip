@@ -126,33 +126,63 @@ struct SwapPlan {                // folded permutation of one swap sequence
     i64 tsrc[2 * MAXSW];         // original row now found at trow[t]
 };
 
-// Fold the swap sequence into the permutation ONCE (one workgroup; the
-// hash map lives in LDS), then laswp_apply_kernel streams the columns.
-// (Building the map in every column workgroup cost ~10-20 us per block.)
-__global__ void __launch_bounds__(256)
+// Fold the swap sequence into the permutation ONCE, in parallel: swap k
+// exchanges rows k and p_k >= k and no later swap touches row k, so the row
+// finally at position k came from p_k "just before swap k", i.e. (walking the
+// swaps backwards) from the chain k'' = last earlier swap with p_k'' == row.
+// One thread per swap follows its chain over the sequence held in LDS; rows
+// >= k2 are emitted by the LAST swap targeting them.  (The former
+// single-thread hash-map fold cost 46-256 us per call.)
+__global__ void __launch_bounds__(MAXSW)
 laswp_setup_kernel(i64 k1, i64 k2, const i64* __restrict__ ipiv, i64 ioff, int incx, SwapPlan* plan) {
-    __shared__ i64 hkey[HSIZE];
-    __shared__ int hval[HSIZE];
-    for (int h = threadIdx.x; h < HSIZE; h += blockDim.x) hkey[h] = -1;
+    __shared__ int pv[MAXSW];                // relative pivot rows (relative to k1)
+    __shared__ int s_cnt;
+    const int ns = (int)(k2 - k1), q = threadIdx.x;
+    if (q == 0) s_cnt = ns;
+    if (q < ns) pv[q] = (int)(ipiv[k1 + q] - ioff - k1);
+    // incx < 0 applies the swaps in reverse order = the inverse permutation:
+    // same fold, source and destination exchanged
+    i64* dst = incx > 0 ? plan->trow : plan->tsrc;
+    i64* srcv = incx > 0 ? plan->tsrc : plan->trow;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        int cnt = 0;
-        auto slot = [&](i64 row) -> int {
-            unsigned hsh = (unsigned)((row * 2654435761ull) >> 7) & (HSIZE - 1);
-            while (hkey[hsh] != -1 && hkey[hsh] != row) hsh = (hsh + 1) & (HSIZE - 1);
-            if (hkey[hsh] == -1) { hkey[hsh] = row; hval[hsh] = cnt; plan->trow[cnt] = row; plan->tsrc[cnt] = row; ++cnt; }
-            return hval[hsh];
-        };
-        const i64 ns = k2 - k1;
-        for (i64 q = 0; q < ns; ++q) {
-            i64 k = incx > 0 ? k1 + q : k2 - 1 - q;
-            i64 p = ipiv[k] - ioff;
-            if (p == k) continue;
-            int a = slot(k), b = slot(p);
-            i64 t = plan->tsrc[a]; plan->tsrc[a] = plan->tsrc[b]; plan->tsrc[b] = t;
+    // source of the content found in row r right after swap t (t < ns, r == pv[t])
+    auto chain = [&](int t) -> int {
+        int row = t;                          // content of row t just before swap t ...
+        for (;;) {
+            int kk = -1;
+            for (int x = t - 1; x >= 0; --x)  // ... is what the last earlier swap targeting it put there
+                if (pv[x] == row) { kk = x; break; }
+            if (kk < 0) return row;
+            row = kk; t = kk;
         }
-        plan->nt = cnt;
+    };
+    if (q < ns) {
+        // position q: content of row pv[q] just before swap q
+        int r = pv[q], src;
+        if (r == q) {
+            src = chain(q);
+        } else {
+            int kk = -1;
+            for (int x = q - 1; x >= 0; --x)
+                if (pv[x] == r) { kk = x; break; }
+            src = (kk < 0) ? r : chain(kk);
+        }
+        dst[q] = k1 + q;
+        srcv[q] = k1 + src;
+        // rows beyond the sequence: emitted by the last swap that targets them
+        if (r >= ns) {
+            bool last = true;
+            for (int x = q + 1; x < ns; ++x)
+                if (pv[x] == r) { last = false; break; }
+            if (last) {
+                const int slot = atomicAdd(&s_cnt, 1);
+                dst[slot] = k1 + r;
+                srcv[slot] = k1 + chain(q);
+            }
+        }
     }
+    __syncthreads();
+    if (q == 0) plan->nt = s_cnt;
 }
 
 template <typename T>
@@ -241,7 +271,7 @@ void laswp_off(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, i64 ioff, 
         return;
     }
     SwapPlan* plan = static_cast<SwapPlan*>(workspace(s, sizeof(SwapPlan), WS_L));
-    hipLaunchKernelGGL(laswp_setup_kernel, dim3(1), dim3(256), 0, s, k1, k2, ipiv, ioff, incx, plan);
+    hipLaunchKernelGGL(laswp_setup_kernel, dim3(1), dim3(MAXSW), 0, s, k1, k2, ipiv, ioff, incx, plan);
     const size_t per_col = (size_t)2 * (k2 - k1) * sizeof(T);
     int cch = (int)std::max<size_t>(1, std::min<size_t>(32, (64 * 1024) / per_col));
     size_t shmem = per_col * cch;

@@ -403,7 +403,7 @@ bool trsm_rlt_fast(i64 m, i64 n, double alpha, const double* L, i64 ldl, double*
     if (m <= 0 || n <= 0) return true;
     if (n > 1024) return false;
     const int nbj = (int)((n + 31) / 32);
-    double* W = static_cast<double*>(workspace(s, sizeof(double) * (size_t)nbj * 1024, WS_L));
+    double* W = static_cast<double*>(workspace(s, sizeof(double) * (size_t)nbj * 1024, WS_C));
     hipLaunchKernelGGL(tri_inv32_kernel, dim3(nbj), dim3(64), 0, s, (int)n, L, ldl, W, unit);
     HIP_LAUNCH_CHECK();
     hipLaunchKernelGGL(trsm_rlt_kernel, dim3((unsigned)((m + TBM - 1) / TBM)), dim3(256), 0, s, m, (int)n, alpha, L,

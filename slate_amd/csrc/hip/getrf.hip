@@ -19,6 +19,7 @@
 //   (owner of row j) the current row j.
 // Kernel boundaries order the columns, so the panel is stream-ordered
 // (graph-capturable, no host sync, no co-residency assumption).
+#include <type_traits>
 #include "common.hpp"
 #include "kernels.hpp"
 #include "launchers.hpp"
@@ -279,9 +280,280 @@ getrf_base_step(i64 m, int c0, int c1, int j, T* A, i64 lda, i64* ipiv, i64 ioff
     if (s_bt >= 0 && tid < w) out.cand[g][tid] = orow[tid];
 }
 
+// ---------------------------------------------------------------------------
+// Persistent base case (fp64, partial pivoting): ONE launch factors all
+// (<= 32) columns of a base block.  PG <= 64 co-resident workgroups of 512
+// threads each hold one row of the block per thread in registers for the
+// whole launch; per column the only cross-CU traffic is
+//   publish: local arg-max (value, row) + the winning row + (owner) row j,
+//            all write-through (sc1) stores, drained, then ONE agent-scope
+//            atomic add per workgroup on a column counter;
+//   gather : one lane polls the counter (sc1 loads, bounded spin), then the
+//            partials and the winning row are read with sc1 loads.
+// (MI355X_MICROARCH.md "Valid forms", first row of the sc1 hand-off table.)
+// Replaces w+1 launches of getrf_base_step (one per column, each re-reading
+// the block from memory): the column chain is the critical path of getrf.
+constexpr int PG = 64;           // max workgroups (one per CU on the reserved CUs)
+constexpr int PT2 = 512;         // threads per workgroup = rows per workgroup
+struct PersistBuf {
+    double val[2][PG];
+    i64 idx[2][PG];
+    double cand[2][PG][NBB];
+    double diag[2][NBB];
+    unsigned long long cnt;
+    unsigned long long err;
+};
+
+__device__ inline double ld_sc1(const double* p) {
+    return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ inline i64 ld_sc1(const i64* p) {
+    return (i64)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void st_sc1(double* p, double v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void st_sc1(i64* p, i64 v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void __launch_bounds__(PT2)
+getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64 ioff, i64* info, i64 info_off,
+                   PersistBuf* pb, double thr, int N, int cabs) {
+    __shared__ double wv[PT2 / 64];
+    __shared__ i64 wi[PT2 / 64];
+    __shared__ int wt[PT2 / 64];
+    __shared__ double prow[NBB], drow[NBB];
+    __shared__ double candL[PG][NBB];
+    __shared__ i64 s_p;
+    __shared__ int s_gw, s_bt, s_abort;
+    __shared__ int piv_s[NBB], tr_s[2 * NBB], ts_s[2 * NBB], s_nt;
+    const int G = gridDim.x, g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const i64 i = (i64)g * PT2 + tid;                 // this thread's row
+    const bool have = i < m;
+    double a[NBB];
+    {
+        const i64 ir = have ? i : 0;
+        #pragma unroll
+        for (int c = 0; c < NBB; ++c) a[c] = A[ir + (i64)min(c, w - 1) * lda];
+    }
+    if (tid == 0) s_abort = 0;
+    for (int j = 0; j < w; ++j) {
+        const int par = j & 1;
+        // ---- local arg-max of column j over unpivoted rows (i >= j)
+        double v = -1.0;
+        #pragma unroll
+        for (int c = 0; c < NBB; ++c) if (c == j) v = (have && i >= j) ? fabs(a[c]) : -1.0;
+        i64 bi = i;
+        int bt = tid;
+        wave_argmax(v, bi, bt);
+        if (lane == 0) { wv[wid] = v; wi[wid] = bi; wt[wid] = bt; }
+        __syncthreads();
+        if (tid == 0) {
+            double bv = wv[0]; i64 bb = wi[0]; int t = wt[0];
+            for (int k = 1; k < PT2 / 64; ++k)
+                if (beats(wv[k], wi[k], bv, bb)) { bv = wv[k]; bb = wi[k]; t = wt[k]; }
+            s_bt = t;
+            st_sc1(&pb->val[par][g], bv);
+            st_sc1(&pb->idx[par][g], bb);
+        }
+        __syncthreads();
+        // ---- publish the winning row and (owner) row j, write-through
+        if (tid == s_bt) {
+            #pragma unroll
+            for (int c = 0; c < NBB; ++c) if (c < w) st_sc1(&pb->cand[par][g][c], a[c]);
+        }
+        if (have && i == j) {
+            #pragma unroll
+            for (int c = 0; c < NBB; ++c) if (c < w) st_sc1(&pb->diag[par][c], a[c]);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __hip_atomic_fetch_add(&pb->cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long target = (unsigned long long)(j + 1) * G;
+            int spins = 0;
+            while (__hip_atomic_load(&pb->cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1 << 22)) {          // not co-resident: give up, never hang
+                    __hip_atomic_store(&pb->err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    s_abort = 1;
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+        if (s_abort) break;
+        // ---- global pivot: every candidate row, the partials and row j are
+        //      fetched in ONE round of sc1 loads (no dependent second trip)
+        {
+            double cv[PG * NBB / PT2];
+            #pragma unroll
+            for (int k = 0; k < PG * NBB / PT2; ++k) {
+                const int e = tid + k * PT2, q = min(e / NBB, G - 1), c = e % NBB;
+                cv[k] = ld_sc1(&pb->cand[par][q][c]);
+            }
+            if (tid < w) drow[tid] = ld_sc1(&pb->diag[par][tid]);
+            #pragma unroll
+            for (int k = 0; k < PG * NBB / PT2; ++k) {
+                const int e = tid + k * PT2, q = e / NBB, c = e % NBB;
+                if (q < G) candL[q][c] = cv[k];
+            }
+        }
+        if (wid == 0) {
+            double pv = -1.0; i64 pi = j; int pg = -1;
+            if (lane < G) { pv = ld_sc1(&pb->val[par][lane]); pi = ld_sc1(&pb->idx[par][lane]); pg = lane; }
+            wave_argmax(pv, pi, pg);
+            if (lane == 0) {
+                i64 p = pi;
+                int gw = pg;
+                if (!(pv >= 0.0) && !(pv != pv)) { p = j; gw = -1; }
+                if (thr < 1.0 && gw >= 0) {
+                    const double dj = fabs(drow[j]);
+                    if (dj == dj && dj >= thr * pv) { p = j; gw = -1; }
+                }
+                if (p == j) gw = -1;
+                s_p = p; s_gw = gw;
+            }
+        }
+        __syncthreads();
+        const i64 p = s_p;
+        const int gw = s_gw;
+        if (tid < w) prow[tid] = (gw < 0) ? drow[tid] : candL[gw][tid];
+        __syncthreads();
+        if (tid == 0) piv_s[j] = (int)p;
+        if (g == 0 && tid == 0) {
+            if (ipiv) ipiv[j] = p + ioff;
+            if (prow[j] == 0.0 && info)
+                atomicCAS(reinterpret_cast<unsigned long long*>(info), 0ull, (unsigned long long)(j + 1 + info_off));
+        }
+        // ---- interchange rows j <-> p and eliminate column j (registers)
+        if (have && i >= j) {
+            if (i == j) {
+                #pragma unroll
+                for (int c = 0; c < NBB; ++c) if (c < w) a[c] = prow[c];
+            } else {
+                if (i == p) {
+                    #pragma unroll
+                    for (int c = 0; c < NBB; ++c) if (c < w) a[c] = drow[c];
+                }
+                const double u = prow[j];
+                double l = 0.0;
+                #pragma unroll
+                for (int c = 0; c < NBB; ++c) if (c == j) l = a[c];
+                if (u != 0.0) l = l / u;
+                #pragma unroll
+                for (int c = 0; c < NBB; ++c) {
+                    if (c == j) a[c] = l;
+                    else if (c > j && c < w) a[c] -= l * prow[c];
+                }
+            }
+        }
+    }
+    if (have) {
+        #pragma unroll
+        for (int c = 0; c < NBB; ++c) if (c < w) A[i + (i64)c * lda] = a[c];
+    }
+    // ---- the same w interchanges on every OTHER column of the panel (left:
+    // factored L, right: not yet factored), so the recursion needs no laswp.
+    // Every workgroup knows the whole swap sequence; workgroup g owns the
+    // other columns g, g + G, ...; nobody else touches them in this launch.
+    if (N <= w || s_abort) return;
+    __syncthreads();
+    if (tid == 0) s_nt = w;
+    __syncthreads();
+    if (tid < w) {
+        // parallel fold (see laswp_setup_kernel): the row finally at j came
+        // from piv_s[j] just before swap j
+        auto chain = [&](int t) -> int {
+            int row = t;
+            for (;;) {
+                int kk = -1;
+                for (int x = t - 1; x >= 0; --x)
+                    if (piv_s[x] == row) { kk = x; break; }
+                if (kk < 0) return row;
+                row = kk; t = kk;
+            }
+        };
+        const int q = tid, r = piv_s[q];
+        int src;
+        if (r == q) {
+            src = chain(q);
+        } else {
+            int kk = -1;
+            for (int x = q - 1; x >= 0; --x)
+                if (piv_s[x] == r) { kk = x; break; }
+            src = (kk < 0) ? r : chain(kk);
+        }
+        tr_s[q] = q;
+        ts_s[q] = src;
+        if (r >= w) {
+            bool last = true;
+            for (int x = q + 1; x < w; ++x)
+                if (piv_s[x] == r) { last = false; break; }
+            if (last) {
+                const int sl = atomicAdd(&s_nt, 1);
+                tr_s[sl] = r;
+                ts_s[sl] = chain(q);
+            }
+        }
+    }
+    __syncthreads();
+    const int nt = s_nt, nother = N - w;
+    if (g >= nother) return;
+    const int mycols = (nother - g + G - 1) / G;
+    const int cpc = max(1, PT2 / nt);                   // whole columns per chunk
+    double* Ap = A - (i64)cabs * lda;                   // panel column 0, sub-panel row 0
+    for (int k0 = 0; k0 < mycols; k0 += cpc) {
+        const int e = tid, t = e % nt, kk = k0 + e / nt;
+        const bool act = (e / nt) < cpc && kk < mycols;
+        double v = 0.0;
+        i64 dst = 0;
+        if (act) {
+            const int o = g + kk * G;
+            const i64 col = o < cabs ? o : o + w;
+            v = Ap[ts_s[t] + col * lda];
+            dst = tr_s[t] + col * lda;
+        }
+        __syncthreads();
+        if (act) Ap[dst] = v;
+        __syncthreads();
+    }
+}
+
+// the persistent form needs every row in a register slot of a co-resident
+// workgroup: m <= PG * PT2 rows; fp64 partial pivoting only
+// Panel-wide context of the recursion: N = panel width; full = the base
+// case applies its interchanges to all N columns (persistent kernel), so the
+// recursion levels skip their laswp calls.
+struct PanelCtx {
+    i64 N;
+    bool full;
+};
+
+template <typename T>
+static bool persist_ok(i64 m, bool nopiv) {
+    return std::is_same<T, double>::value && !nopiv && m <= (i64)PG * PT2 && m >= 1;
+}
+
 template <typename T>
 static void base(i64 m, int c0, int c1, T* A, i64 lda, i64* ipiv, i64 ioff, i64* info, i64 info_off,
-                 void* w, double thr, bool nopiv, hipStream_t s) {
+                 void* w, double thr, bool nopiv, hipStream_t s, const PanelCtx& ctx, i64 cabs) {
+    if constexpr (std::is_same<T, double>::value) {
+        if (ctx.full) {
+            PersistBuf* pb = reinterpret_cast<PersistBuf*>(static_cast<char*>(w) + PANEL_BYTES);
+            HIP_CHECK(hipMemsetAsync(&pb->cnt, 0, sizeof(unsigned long long), s));
+            const int G = (int)((m + PT2 - 1) / PT2);
+            hipLaunchKernelGGL(getrf_base_persist, dim3(G), dim3(PT2), 0, s, m, c1, A, lda, ipiv, ioff, info,
+                               info_off, pb, thr, (int)ctx.N, (int)cabs);
+            HIP_LAUNCH_CHECK();
+            return;
+        }
+    }
     int G = (int)std::min<i64>(MAXG, std::max<i64>(1, (m + NTH - 1) / NTH));
     for (int j = c0; j <= c1; ++j)
         hipLaunchKernelGGL(getrf_base_step<T>, dim3(G), dim3(NTH), 0, s, m, c0, c1, j, A, lda, ipiv, ioff,
@@ -305,23 +577,23 @@ static void gemm_T(char ta, char tb, i64 m, i64 n, i64 k, double alpha, const T*
 
 template <typename T>
 static void rec(i64 m, i64 n, T* A, i64 lda, i64* ipiv, i64 ioff, i64* info, i64 info_off, void* w,
-                double thr, bool nopiv, hipStream_t s) {
+                double thr, bool nopiv, hipStream_t s, const PanelCtx& ctx, i64 cabs) {
     if (n <= NBB) {
-        base<T>(m, 0, (int)n, A, lda, ipiv, ioff, info, info_off, w, thr, nopiv, s);
+        base<T>(m, 0, (int)n, A, lda, ipiv, ioff, info, info_off, w, thr, nopiv, s, ctx, cabs);
         return;
     }
     i64 n1 = ((n / 2 + NBB - 1) / NBB) * NBB;
     if (n1 >= n) n1 = n - NBB;
-    rec<T>(m, n1, A, lda, ipiv, ioff, info, info_off, w, thr, nopiv, s);
+    rec<T>(m, n1, A, lda, ipiv, ioff, info, info_off, w, thr, nopiv, s, ctx, cabs);
     T* A12 = A + n1 * lda;
-    if (!nopiv) laswp_off<T>(n - n1, A12, lda, 0, n1, ipiv, ioff, s);
+    if (!nopiv && !ctx.full) laswp_off<T>(n - n1, A12, lda, 0, n1, ipiv, ioff, s);
     trsm<T>('L', 'L', 'N', 'U', n1, n - n1, s_from_real(T(), 1), A, lda, A12, lda, s);
     if (m > n1)
         gemm_T<T>('N', 'N', m - n1, n - n1, n1, -1.0, A + n1, lda, A12, lda, 1.0, A12 + n1, lda, s);
     if (m > n1) {
         rec<T>(m - n1, n - n1, A12 + n1, lda, ipiv ? ipiv + n1 : nullptr, ioff + n1, info, info_off + n1, w,
-               thr, nopiv, s);
-        if (!nopiv) laswp_off<T>(n1, A, lda, n1, std::min(m, n), ipiv, ioff, s);
+               thr, nopiv, s, ctx, cabs + n1);
+        if (!nopiv && !ctx.full) laswp_off<T>(n1, A, lda, n1, std::min(m, n), ipiv, ioff, s);
     }
 }
 
@@ -332,14 +604,15 @@ void getrf_panel_ws(i64 m, i64 n, T* A, i64 lda, i64* ipiv, i64* info, double th
     if (info) HIP_CHECK(hipMemsetAsync(info, 0, sizeof(i64), s));
     if (m <= 0 || n <= 0) return;
     const i64 k = std::min(m, n);
-    rec<T>(m, k, A, lda, ipiv, 0, info, 0, w, thr, nopiv, s);
+    const PanelCtx ctx{n, persist_ok<T>(m, nopiv)};
+    rec<T>(m, k, A, lda, ipiv, 0, info, 0, w, thr, nopiv, s, ctx, 0);
     if (n > k) {   // wide panel: U12 = L11^{-1} P A12
-        if (!nopiv) laswp_off<T>(n - k, A + k * lda, lda, 0, k, ipiv, 0, s);
+        if (!nopiv && !ctx.full) laswp_off<T>(n - k, A + k * lda, lda, 0, k, ipiv, 0, s);
         trsm<T>('L', 'L', 'N', 'U', k, n - k, s_from_real(T(), 1), A, lda, A + k * lda, lda, s);
     }
 }
 
-size_t getrf_work_bytes() { return PANEL_BYTES; }
+size_t getrf_work_bytes() { return PANEL_BYTES + sizeof(PersistBuf); }
 
 #define INST(T) \
     template void getrf_panel_ws<T>(i64, i64, T*, i64, i64*, i64*, double, bool, void*, hipStream_t);

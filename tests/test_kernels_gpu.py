@@ -199,6 +199,41 @@ def test_getrf_panel(dt, m, n):
     assert (L.real.abs() + (L.imag.abs() if L.is_complex() else 0)).max() <= bound + 1e-6
 
 
+@pytest.mark.parametrize("m,n", [(2048, 32), (5000, 64), (20000, 100), (32768, 512)])
+def test_getrf_panel_persistent_fp64(m, n):
+    # tall fp64 panels take the persistent base case (co-resident workgroups,
+    # sc1 hand-offs); pivots must equal LAPACK's partial pivoting exactly
+    A0 = cm(m, n, torch.float64, 33)
+    A = A0.clone()
+    ipiv = torch.zeros(n, dtype=torch.int64, device="cuda")
+    info = ops.getrf(A, ipiv)
+    assert int(info.item()) == 0
+    LU_ref, piv_ref = torch.linalg.lu_factor(A0.cpu())
+    assert torch.equal(ipiv.cpu(), piv_ref[:n].to(torch.int64) - 1)
+    assert (A.cpu() - LU_ref).abs().max() / A0.abs().max() < 1e-12
+
+
+@pytest.mark.parametrize("ns,m,incx", [(1, 5, 1), (32, 40, 1), (512, 2000, 1), (700, 3000, 1), (300, 900, -1),
+                                       (1100, 5000, -1)])
+def test_laswp_random_sequences(ns, m, incx):
+    # parallel fold of the swap sequence (chains of repeated targets) vs sequential
+    g = torch.Generator().manual_seed(ns + m)
+    span = torch.randint(0, 4, (ns,), generator=g)
+    far = torch.randint(0, m, (ns,), generator=g)
+    ipiv = torch.tensor([min(m - 1, k + (int(far[k]) if span[k] == 3 else int(span[k]))) for k in range(ns)],
+                        dtype=torch.int64)
+    ipiv = torch.maximum(ipiv, torch.arange(ns))
+    A0 = cm(m, 7, torch.float64, 43)
+    A = A0.clone()
+    ops.laswp(A, ipiv.cuda(), 0, ns, incx=incx)
+    R = A0.clone()
+    order = range(ns) if incx > 0 else reversed(range(ns))
+    for i in order:
+        p = int(ipiv[i])
+        R[[i, p]] = R[[p, i]]
+    assert torch.equal(A, R)
+
+
 def test_laswp_matches_sequential():
     m, n = 600, 70
     A0 = cm(m, n, torch.float64, 41)
