@@ -6,8 +6,9 @@
 //               left-looking update A(c0:, J) -= L(c0:, :c0) L(J, :c0)^T runs
 //               on the f64 MFMA (operands streamed from L2, where this CU just
 //               wrote them), the 16-wide diagonal sub-blocks are factored by
-//               one wave in registers (v_readlane broadcasts, no barriers) and
-//               the rows below are solved row-per-thread against them.  One
+//               256 threads, one element each (one barrier per column, the
+//               inverse one column behind), and the rows below are solved on
+//               the MFMA against that inverse.  One
 //               launch replaces the 4 x (potrf_small + trsm + herk) chain of
 //               potrf.hip (measured 870 us for n = 512 on MI355X) and leaves
 //               every other CU to the trailing update.
@@ -32,13 +33,6 @@ constexpr int PB = 32;           // block-column width
 constexpr int PT = 512;          // threads of potrf_lds (8 waves: 256-VGPR budget)
 constexpr int PLD = PN + 1;      // LDS column stride (doubles)
 
-__device__ inline double rl(double v, int src) {
-    union { double d; int w[2]; } a, b;
-    a.d = v;
-    b.w[0] = __builtin_amdgcn_readlane(a.w[0], src);
-    b.w[1] = __builtin_amdgcn_readlane(a.w[1], src);
-    return b.d;
-}
 __device__ inline d4 mma(double x, double y, d4 c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, c, 0, 0, 0); }
 }  // namespace
 
@@ -110,9 +104,9 @@ __global__ void __launch_bounds__(PT)
 potrf_lds_kernel(int n, double* __restrict__ A, i64 lda, i64* info, i64 info_off, i64* prof) {
     __shared__ double P[PB * PLD];          // P[c * PLD + r] = A(c0 + r, c0 + c)
     __shared__ double Li[16][17];            // inverse of the current 16 x 16 diagonal sub-block
-    __shared__ __attribute__((aligned(16))) double Ld[16][18];   // factored sub-block (row-major, zero above)
-    __shared__ __attribute__((aligned(16))) double colb[16];
-    __shared__ double rdl[16];
+    __shared__ double Ld[16][17];            // its Cholesky factor (row-major, zero above)
+    __shared__ double Dd[16][17];            // working copy of the sub-block
+    __shared__ double rdl[16];               // 1 / L(j, j)
     __shared__ int s_fail;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (tid == 0) s_fail = 0;
@@ -121,27 +115,31 @@ potrf_lds_kernel(int n, double* __restrict__ A, i64 lda, i64* info, i64 info_off
     i64 tlast = clock64();
     const i64 t0 = tlast, w0 = wall_clock64();
 #define STAMP(i) do { if (prof && tid == 0) { const i64 t_ = clock64(); ph[i] += t_ - tlast; tlast = t_; } } while (0)
+    const int lr = tid;                                   // one row per thread, 32 columns
+    // raw A values of the next block column, loaded one block ahead: plain
+    // loads survive the barriers of the factorization phases (no LDS-DMA in
+    // flight), so their latency hides behind them
+    double v[PB];
+    auto fetch = [&](int cn) {
+        const int jbn = min(PB, n - cn), Mn = n - cn;
+        const __amdgpu_buffer_rsrc_t rs = rsrc_of(A + cn + (i64)cn * lda);   // 32-bit offsets: one VGPR
+        const int vo = min(lr, Mn - 1) * 8;
+        #pragma unroll
+        for (int c = 0; c < PB; ++c) v[c] = bld(rs, vo, (int)((i64)min(c, jbn - 1) * lda * 8));
+    };
+    fetch(0);
     for (int c0 = 0; c0 < n; c0 += PB) {
         const int jb = min(PB, n - c0), M = n - c0;
-        const int lr = tid;                               // one row per thread, 32 columns
-        // ---- load the block column (lower part): all 32 loads in flight at once
-        {
-            double v[PB];
-            const double* src = A + (c0 + min(lr, M - 1)) + (i64)c0 * lda;
-            #pragma unroll
-            for (int c = 0; c < PB; ++c) v[c] = src[(i64)min(c, jb - 1) * lda];
-            #pragma unroll
-            for (int c = 0; c < PB; ++c)
-                if (c < jb && lr < M && lr >= c) P[c * PLD + lr] = v[c];
-        }
+        // ---- stage the block column (lower part)
+        #pragma unroll
+        for (int c = 0; c < PB; ++c)
+            if (c < jb && lr < M && lr >= c) P[c * PLD + lr] = v[c];
         __syncthreads();
         STAMP(0);
         // ---- left-looking update by the factored columns [0, c0)
         if (c0 > 0) {
             // strip pairs (2s, 2s+1) x both 16-column tiles per wave
-            for (int h = 0; h < 2; ++h) {
-                const int sp = w + 8 * h;
-                if (32 * sp >= M) continue;
+            for (int sp = w; 32 * sp < M; sp += PT / 64) {
                 const int xr[2] = {min(32 * sp + (lane & 15), M - 1), min(32 * sp + 16 + (lane & 15), M - 1)};
                 const int yr[2] = {min(lane & 15, M - 1), min(16 + (lane & 15), M - 1)};
                 d4 acc[2][2];
@@ -163,76 +161,52 @@ potrf_lds_kernel(int n, double* __restrict__ A, i64 lda, i64* info, i64 info_off
             __syncthreads();
         }
         STAMP(1);
+        if (c0 + PB < n) fetch(c0 + PB);                  // in flight through the phases below
         // ---- factor the block column in LDS, 16 columns at a time:
-        //  (1) wave 0: 16 x 16 diagonal sub-block -> L_qq and inv(L_qq) in
-        //      registers (v_readlane broadcasts, no barriers);
+        //  (1) 256 threads: 16 x 16 diagonal sub-block -> L_qq and inv(L_qq);
         //  (2) every wave: rows below, X = P inv(L_qq)^T on the MFMA;
         //  (3) first half only: P(:, 16:32) -= X X(16:32, :)^T on the MFMA.
         for (int q0 = 0; q0 < jb; q0 += 16) {
             const int wq = min(16, jb - q0);
-            if (w == 0) {
-                // lane i < 16 owns row i; column j is broadcast through LDS
-                // (colb) -- 15 independent LDS reads per step instead of a
-                // chain of v_readlane hazards
-                double row[16];
-                #pragma unroll
-                for (int c = 0; c < 16; ++c)
-                    row[c] = (lane < wq && c <= lane) ? P[(q0 + c) * PLD + q0 + lane] : (lane == c ? 1.0 : 0.0);
+            {
+                // thread (di, dc) < 256 owns element (di, dc): right-looking
+                // Cholesky, one barrier per column; the inverse (forward
+                // substitution on I, scaling deferred) runs one column behind
+                const bool act = tid < 256;
+                const int di = tid & 15, dc = (tid >> 4) & 15;
+                if (act) {
+                    Dd[di][dc] = (di < wq && dc <= di) ? P[(q0 + dc) * PLD + q0 + di] : (di == dc ? 1.0 : 0.0);
+                    Li[di][dc] = (di == dc) ? 1.0 : 0.0;
+                }
+                __syncthreads();
+                double myl = 0.0;
                 int fail = 0;
-                #pragma unroll
+                #pragma unroll 1
                 for (int j = 0; j < 16; ++j) {
-                    double d = rl(row[j], j);
-                    if (j < wq && !(d > 0.0)) { if (!fail) fail = c0 + q0 + j + 1; d = 1.0; }
-                    const double sq = sqrt(d), inv = 1.0 / sq;
-                    if (lane == j) row[j] = sq;
-                    else if (lane > j) row[j] *= inv;
-                    if (lane < 16) colb[lane] = row[j];
-                    if (lane == 0) rdl[j] = inv;
-                    __builtin_amdgcn_wave_barrier();
-                    double cb[16];
-                    #pragma unroll
-                    for (int c = 0; c < 16; c += 2) {      // all reads issued before any use
-                        const d2 v = *reinterpret_cast<const d2*>(&colb[c]);
-                        cb[c] = v.x; cb[c + 1] = v.y;
-                    }
-                    #pragma unroll
-                    for (int c = j + 1; c < 16; ++c)
-                        if (lane >= c) row[c] -= row[j] * cb[c];
-                    __builtin_amdgcn_wave_barrier();
-                }
-                if (lane < 16) {
-                    #pragma unroll
-                    for (int c = 0; c < 16; ++c) Ld[lane][c] = (c <= lane) ? row[c] : 0.0;
-                }
-                if (lane < wq) {
-                    #pragma unroll
-                    for (int c = 0; c < 16; ++c)
-                        if (c <= lane) P[(q0 + c) * PLD + q0 + lane] = row[c];
-                }
-                __builtin_amdgcn_wave_barrier();
-                // inv(L_qq): lane c < 16 computes column c; L(r, l) are
-                // broadcast LDS reads independent of the x chain
-                double x[16];
-                #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    double acc = (r == lane) ? 1.0 : 0.0;
-                    double lr_[16];
-                    #pragma unroll
-                    for (int l = 0; l < 16; l += 2) {
-                        if (l < r) {
-                            const d2 v = *reinterpret_cast<const d2*>(&Ld[r][l]);
-                            lr_[l] = v.x; lr_[l + 1] = v.y;
+                    if (act) {
+                        double d = Dd[j][j];
+                        if (j < wq && !(d > 0.0)) {
+                            if (!fail) fail = c0 + q0 + j + 1;
+                            d = 1.0;
                         }
+                        const double sq = sqrt(d), inv = 1.0 / sq;
+                        const double lij = Dd[di][j] * inv;
+                        if (dc == j) {
+                            myl = di > j ? lij : (di == j ? sq : 0.0);
+                            Ld[di][j] = myl;
+                        } else if (dc > j && di >= dc) {
+                            Dd[di][dc] -= lij * (Dd[dc][j] * inv);
+                        }
+                        if (tid == 0) rdl[j] = inv;
+                        if (j > 0 && di >= j) Li[di][dc] -= Ld[di][j - 1] * (Li[j - 1][dc] * rdl[j - 1]);
                     }
-                    #pragma unroll
-                    for (int l = 0; l < r; ++l) acc -= lr_[l] * x[l];
-                    x[r] = (r >= lane) ? acc * rdl[r] : 0.0;
+                    __syncthreads();
                 }
-                if (lane < 16) {
-                    #pragma unroll
-                    for (int r = 0; r < 16; ++r) Li[r][lane] = x[r];     // Li[r][c] = inv(L_qq)(r, c)
+                if (act) {
+                    Li[di][dc] *= rdl[di];
+                    if (di < wq && dc <= di) P[(q0 + dc) * PLD + q0 + di] = myl;
                 }
-                if (lane == 0 && fail && !s_fail) s_fail = fail;
+                if (tid == 0 && fail && !s_fail) s_fail = fail;
             }
             __syncthreads();
             STAMP(2);

@@ -16,6 +16,7 @@
 //   B_j: reduce the norm partials -> larfg (beta, tau, 1/(alpha-beta)),
 //        identically in every workgroup; scale own rows of v_j; publish
 //        partials of v_j^H A(:, j+1:) and V(:, <j)^H v_j.
+#include <type_traits>
 #include "common.hpp"
 #include "kernels.hpp"
 #include "launchers.hpp"
@@ -282,6 +283,11 @@ void geqrf_panel_ws(i64 m, i64 n, T* A, i64 lda, T* tau, T* Tm, i64 ldt, T* V, i
                     hipStream_t s) {
     if (m <= 0 || n <= 0) return;
     const i64 k = std::min(m, n);
+    if constexpr (std::is_same<T, double>::value) {
+        // tall fp64 panel: shifted CholeskyQR3 + Householder reconstruction
+        // (qr_fast.hip); a breakdown restores the panel and lands here
+        if (m >= 8 * n && geqrf_cholqr(m, n, A, lda, tau, Tm, ldt, V, ldv, s)) return;
+    }
     // T is upper triangular: zero the strict lower part once
     geset<T>('L', k, k, s_zero(T()), s_zero(T()), Tm, ldt, s);
     T* W = static_cast<T*>(workspace(s, sizeof(T) * (size_t)k * k, WS_QW));

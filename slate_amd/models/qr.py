@@ -116,7 +116,7 @@ def _geqrf_p1(A, buf, T, la):
     dev, dt = buf.device, s.dtype
     grid = grid_of(A) if q > 1 else None
     nloc = bc.nloc
-    ss = StreamSet(dev, reserve_cus=64)
+    ss = StreamSet(dev, reserve_cus=0)   # GEMM-shaped CholeskyQR panel: no reserved CUs (measured 32.5 vs 29.8 TF/s with 64)
     ev_tr = {}
     ss.fork()
     for k in range(kt):

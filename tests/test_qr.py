@@ -166,3 +166,61 @@ def test_geqrf_panel_gpu(dt, mn):
 @pytest.mark.gpu
 def test_geqrf_gpu_driver():
     _check_qr(1500, 1000, 256, torch.float64, device=torch.device("cuda"))
+
+
+def _panel_checks(A0, A, tau, T, V):
+    """Q = I - V T V^T without forming it: Q [R; 0] = A0, and Q^T Q = I
+    (<=> T^T (V^T V) T = T + T^T, V unit lower hence full rank)."""
+    b = A.shape[1]
+    R = torch.triu(A)[:b]
+    QR = -(V @ (T @ (V[:b].t() @ R)))
+    QR[:b] += R
+    assert ((QR - A0).abs().max() / A0.abs().max()).item() < 1e-12
+    O = T.t() @ (V.t() @ V) @ T - T - T.t()
+    assert O.abs().max().item() < 1e-11
+    assert torch.equal(torch.diagonal(T), tau)
+    assert torch.equal(torch.triu(V[:b]), torch.eye(b, dtype=A.dtype, device=A.device))
+    assert torch.equal(torch.tril(A, -1), torch.tril(V, -1))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mb", [(16384, 256), (8192, 128), (65536, 256), (3000, 200), (1024, 16)])
+def test_geqrf_cholqr_panel(mb):
+    """Tall fp64 panels (m >= 8 b, b <= 256) take the shifted CholeskyQR3 +
+    Householder reconstruction path (csrc/hip/qr_fast.hip); the output has
+    the Householder panel's form (R, unit-lower V, tau = diag(T), T)."""
+    from slate_amd import ops
+    m, b = mb
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(m + b)
+    A0 = torch.randn(m, b, dtype=torch.float64, generator=g).to(dev)
+    A0[:, 1] *= 1e5                      # unequal column scales
+    A = A0.t().contiguous().t()
+    tau = torch.zeros(b, dtype=torch.float64, device=dev)
+    T, V = ops.geqrf(A, tau)
+    torch.cuda.synchronize()
+    _panel_checks(A0, A, tau, T, V)
+
+
+@pytest.mark.gpu
+def test_geqrf_cholqr_breakdown_falls_back():
+    """A rank-deficient panel breaks CholeskyQR down: detected on the device,
+    the panel is restored and factored by the Householder path."""
+    from slate_amd import ops
+    m, b = 8192, 64
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(3)
+    A0 = torch.randn(m, b, dtype=torch.float64, generator=g).to(dev)
+    A0[:, 10] = 0.0
+    A0[:, 20] = A0[:, 3]
+    A = A0.t().contiguous().t()
+    tau = torch.zeros(b, dtype=torch.float64, device=dev)
+    T, V = ops.geqrf(A, tau)
+    torch.cuda.synchronize()
+    _panel_checks(A0, A, tau, T, V)
+
+
+@pytest.mark.gpu
+def test_geqrf_gpu_driver_tall():
+    """Tall matrix: every panel takes the CholeskyQR path."""
+    _check_qr(8192, 512, 128, torch.float64, device=torch.device("cuda"))
