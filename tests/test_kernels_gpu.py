@@ -213,6 +213,27 @@ def test_getrf_panel_persistent_fp64(m, n):
     assert (A.cpu() - LU_ref).abs().max() / A0.abs().max() < 1e-12
 
 
+@pytest.mark.parametrize("m,n", [(20000, 64), (32768, 256)])
+def test_getrf_panel_persistent_under_load(m, n):
+    # granule hand-offs while a GEMM streams on another stream (uneven
+    # progress across the persistent workgroups): results must not change
+    X = cm(6144, 6144, torch.float64, 5)
+    side = torch.cuda.Stream()
+    A0 = cm(m, n, torch.float64, 35)
+    A = A0.clone()
+    ipiv = torch.zeros(n, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            X = (X @ X) * (1.0 / 6144)
+    info = ops.getrf(A, ipiv)
+    torch.cuda.synchronize()
+    assert int(info.item()) == 0
+    LU_ref, piv_ref = torch.linalg.lu_factor(A0.cpu())
+    assert torch.equal(ipiv.cpu(), piv_ref[:n].to(torch.int64) - 1)
+    assert (A.cpu() - LU_ref).abs().max() / A0.abs().max() < 1e-12
+
+
 @pytest.mark.parametrize("ns,m,incx", [(1, 5, 1), (32, 40, 1), (512, 2000, 1), (700, 3000, 1), (300, 900, -1),
                                        (1100, 5000, -1)])
 def test_laswp_random_sequences(ns, m, incx):
