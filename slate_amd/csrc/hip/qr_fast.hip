@@ -5,7 +5,8 @@
 // trailing update, unmqr and every other consumer of geqrf_panel_ws are
 // unchanged.
 //
-//   CholeskyQR, three times (the first one shifted):
+//   CholeskyQR2 (shifted CholeskyQR3 when the second factor shows that the
+//   first pass did not reach orthogonality):
 //       G = A^T A (+ s I)        split-K MFMA GEMM (gemm_launch.hpp)
 //       G = L L^T                potrf_lds, one CU (chol_fast.hip)
 //       A = A L^-T               trsm_rlt (chol_fast.hip)
@@ -27,8 +28,8 @@
 // Grigori, Jacquelin, Knight, Nguyen, IPDPS 2014).
 //
 // Breakdown (numerically rank-deficient panel: a Cholesky fails or the
-// third factor is not ~I) is detected on the device and read back once per
-// panel; the panel is then restored from a copy and the caller runs the
+// last factor is not ~I) is detected on the device and read back once per
+// attempt; the panel is then restored from a copy and the caller runs the
 // Householder panel instead.
 #include <cstdlib>
 #include <cstring>
@@ -67,13 +68,22 @@ __global__ void __launch_bounds__(256) qf_rt_kernel(int b, const double* L, i64 
     for (int i = threadIdx.x; i < b; i += 256) R[i + (i64)j * ldr] = (i <= j) ? L[j + (i64)i * ldl] : 0.0;
 }
 
-// flag = any Cholesky failed, or the third factor is not ~I (or not finite)
-__global__ void __launch_bounds__(256) qf_check_kernel(int b, const double* L, i64 ldl, const i64* info, int* flag) {
+// flag = one of the npass Cholesky factorizations failed, or the last
+// factor L is not I to within tol (max |L - I| over the lower triangle; NaN
+// fails): the Q it produced was not yet orthonormal
+__global__ void __launch_bounds__(256)
+qf_check_kernel(int b, const double* L, i64 ldl, const i64* info, int npass, double tol, int* flag) {
     __shared__ int bad;
-    if (threadIdx.x == 0) bad = (info[0] | info[1] | info[2]) != 0;
+    if (threadIdx.x == 0) {
+        int f = 0;
+        for (int p = 0; p < npass; ++p) f |= info[p] != 0;
+        bad = f;
+    }
     __syncthreads();
-    for (int i = threadIdx.x; i < b; i += 256)
-        if (!(fabs(L[i + (i64)i * ldl] - 1.0) < 1e-3)) atomicOr(&bad, 1);
+    for (int e = threadIdx.x; e < b * b; e += 256) {
+        const int i = e % b, j = e / b;
+        if (i >= j && !(fabs(L[i + (i64)j * ldl] - (i == j ? 1.0 : 0.0)) < tol)) atomicOr(&bad, 1);
+    }
     __syncthreads();
     if (threadIdx.x == 0) *flag = bad;
 }
@@ -228,32 +238,48 @@ bool geqrf_cholqr(i64 m, i64 b, double* A, i64 lda, double* tau, double* Tm, i64
     i64* inf = reinterpret_cast<i64*>(sgn + b);
     int* flag = reinterpret_cast<int*>(inf + 4);
     gecopy<double, double>('G', 'N', m, b, A, lda, Bk, m, s);
-    HIP_CHECK(hipMemsetAsync(inf, 0, 4 * sizeof(i64), s));
-    const double shift = 11.0 * ((double)m * b + (double)b * (b + 1)) * 0x1p-53;
-    for (int p = 0; p < 3; ++p) {
+    // one CholeskyQR pass: G = A^T A (+ shift I), G = L L^T, A = A L^-T, R = L^T R
+    auto pass = [&](int p, bool first, double shift) {
         gemm_d('T', 'N', b, b, m, 1.0, A, lda, A, lda, 0.0, G, b, s);
-        if (p == 0) {
+        if (shift > 0) {
             hipLaunchKernelGGL(qf_shift_kernel, dim3(1), dim3(256), 0, s, (int)b, G, (i64)b, shift);
             HIP_LAUNCH_CHECK();
         }
         potrf_fast((int)b, G, b, inf + p, 0, s);
         trsm_rlt_fast(m, b, 1.0, G, b, A, lda, false, s);
-        if (p == 0) {
+        if (first) {
             hipLaunchKernelGGL(qf_rt_kernel, dim3((unsigned)b), dim3(256), 0, s, (int)b, (const double*)G, (i64)b,
                                Rm, (i64)b);
             HIP_LAUNCH_CHECK();
         } else {
             trmm<double>('L', 'L', 'T', 'N', b, b, 1.0, G, b, Rm, b, s);
         }
-    }
-    hipLaunchKernelGGL(qf_check_kernel, dim3(1), dim3(256), 0, s, (int)b, (const double*)G, (i64)b,
-                       (const i64*)inf, flag);
-    HIP_LAUNCH_CHECK();
-    HIP_CHECK(hipMemcpyAsync(hflag, flag, sizeof(int), hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
-    if (*hflag) {
+    };
+    // breakdown / orthogonality check of the last pass, read back to the host
+    auto failed = [&](int npass, double tol) {
+        hipLaunchKernelGGL(qf_check_kernel, dim3(1), dim3(256), 0, s, (int)b, (const double*)G, (i64)b,
+                           (const i64*)inf, npass, tol, flag);
+        HIP_LAUNCH_CHECK();
+        HIP_CHECK(hipMemcpyAsync(hflag, flag, sizeof(int), hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        return *hflag != 0;
+    };
+    // CholeskyQR2 first: enough when kappa(A) << u^-1/2, recognised by the
+    // second factor being I to 1e-3 (then the final Q is orthonormal to O(u));
+    // otherwise restart from the copy with shifted CholeskyQR3
+    HIP_CHECK(hipMemsetAsync(inf, 0, 4 * sizeof(i64), s));
+    pass(0, true, 0.0);
+    pass(1, false, 0.0);
+    if (failed(2, 1e-3)) {
         gecopy<double, double>('G', 'N', m, b, Bk, m, A, lda, s);
-        return false;
+        HIP_CHECK(hipMemsetAsync(inf, 0, 4 * sizeof(i64), s));
+        pass(0, true, 11.0 * ((double)m * b + (double)b * (b + 1)) * 0x1p-53);
+        pass(1, false, 0.0);
+        pass(2, false, 0.0);
+        if (failed(3, 1e-3)) {
+            gecopy<double, double>('G', 'N', m, b, Bk, m, A, lda, s);
+            return false;
+        }
     }
     // ---- Householder reconstruction
     hipLaunchKernelGGL(lu_hr_kernel, dim3(1), dim3(HT), 0, s, (int)b, A, lda, sgn);
