@@ -84,8 +84,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=32768)
-    ap.add_argument("--m", type=int, default=None)
+    # --size / --rows: the same, usable after `python -m torch.distributed.run ... bench.py`
+    # (its parser takes --n / --m for ambiguous prefixes of its own options)
+    ap.add_argument("--n", "--size", dest="n", type=int, default=32768)
+    ap.add_argument("--m", "--rows", dest="m", type=int, default=None)
     ap.add_argument("--nb", type=int, default=512)
     ap.add_argument("--routine", default="potrf", choices=["potrf", "getrf", "gemm", "geqrf"])
     ap.add_argument("--lookahead", type=int, default=1)

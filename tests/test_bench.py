@@ -1,0 +1,45 @@
+"""bench.py contract on the CPU: one JSON line from rank 0 with the
+driver's fields, single rank and 2 ranks (gloo, 127.0.0.1) -- the same code
+path the driver runs per GPU count (RCCL there)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from dist_util import _free_port
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def _run(nproc, routine):
+    args = ["bench.py", "--gpus", str(nproc), "--routine", routine, "--size", "512", "--nb", "64", "--steps", "1",
+            "--warmup", "1"]
+    if routine == "geqrf":
+        args += ["--rows", "768"]
+    if nproc > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+               "--master-addr", "127.0.0.1", f"--master-port={_free_port()}"] + args
+    else:
+        cmd = [sys.executable] + args
+    env = dict(os.environ, OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="")
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("nproc", [1, 2])
+@pytest.mark.parametrize("routine", ["potrf", "getrf", "geqrf"])
+def test_bench_json(nproc, routine):
+    d = _run(nproc, routine)
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == nproc and d["steps"] == 1 and d["warmup"] == 1
+    assert d["value"] > 0 and d["higher_is_better"] is True
+    assert d["config"]["n"] == 512
+    if nproc == 1:
+        assert d["residual"] is not None and d["residual"] < 1e-12
