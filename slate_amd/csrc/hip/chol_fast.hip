@@ -357,6 +357,64 @@ trsm_rlt_kernel(i64 m, int n, double alpha, const double* __restrict__ L, i64 ld
     }
 }
 
+// ---------------------------------------------------------------- trsm_lln
+// L X = alpha B (L: m x m lower, B: m x n), X overwrites B -- the U rows of
+// LU (L unit lower) and the forward solves.  Every workgroup owns 64 columns
+// of B and walks 32-row blocks: R = alpha B_I - L_{I,<I} X_{<I} (MFMA,
+// K = 32 I, the solved rows re-read from L2), X_I = inv(L_II) R (MFMA
+// against tri_inv32's output).  One launch instead of the inverse + GEMM +
+// copy chain of trsm.hip.
+constexpr int TBN = 64;
+__global__ void __launch_bounds__(256)
+trsm_lln_kernel(int m, i64 n, double alpha, const double* __restrict__ L, i64 ldl, const double* __restrict__ Winv,
+                double* __restrict__ B, i64 ldb) {
+    __shared__ double R[32][TBN + 1];       // R[i][c]
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const i64 cb = (i64)blockIdx.x * TBN;
+    const int nc = (int)min((i64)TBN, n - cb);
+    const int cl = 16 * w + (lane & 15);     // this lane's column (MFMA m index)
+    const int cx = min(cl, nc - 1);          // clamped (valid) column for loads
+    double* Bc = B + cb * ldb;
+    for (int r0 = 0; r0 < m; r0 += 32) {
+        const int jb = min(32, m - r0);
+        d4 acc2[1][2] = {{d4{0, 0, 0, 0}, d4{0, 0, 0, 0}}};
+        if (r0 > 0) {
+            const int xr[1] = {(int)(cx * ldb)};
+            const int yr[2] = {min(lane & 15, m - 1 - r0), min(16 + (lane & 15), m - 1 - r0)};
+            strip_update<1, 2, 8>(acc2, Bc, xr, 1, L + r0, yr, ldl, r0, lane);
+        }
+        d4 (&acc)[2] = acc2[0];
+        #pragma unroll
+        for (int t = 0; t < 2; ++t)
+            #pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int i = 16 * t + (lane >> 4) + 4 * q;
+                double v = 0.0;
+                if (cl < nc && i < jb) v = alpha * Bc[(r0 + i) + (i64)cl * ldb] - acc[t][q];
+                R[i][cl] = v;
+            }
+        __syncthreads();
+        // X_I = inv(L_II) R
+        const double* W = Winv + (i64)(r0 / 32) * 1024;
+        d4 x[2] = {d4{0, 0, 0, 0}, d4{0, 0, 0, 0}};
+        #pragma unroll
+        for (int k = 0; k < 32; k += 4) {
+            const int kk = k + (lane >> 4);
+            const double rv = R[kk][cl];
+            #pragma unroll
+            for (int t = 0; t < 2; ++t) x[t] = mma(W[(16 * t + (lane & 15)) + 32 * kk], rv, x[t]);
+        }
+        #pragma unroll
+        for (int t = 0; t < 2; ++t)
+            #pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int i = 16 * t + (lane >> 4) + 4 * q;
+                if (cl < nc && i < jb) Bc[(r0 + i) + (i64)cl * ldb] = x[t][q];
+            }
+        __syncthreads();
+    }
+}
+
 // ---------------------------------------------------------------- launchers
 bool potrf_fast(int n, double* A, i64 lda, i64* info, i64 info_off, hipStream_t s) {
     if (n <= 0 || n > PN) return false;
@@ -381,6 +439,20 @@ bool trsm_rlt_fast(i64 m, i64 n, double alpha, const double* L, i64 ldl, double*
     hipLaunchKernelGGL(tri_inv32_kernel, dim3(nbj), dim3(64), 0, s, (int)n, L, ldl, W, unit);
     HIP_LAUNCH_CHECK();
     hipLaunchKernelGGL(trsm_rlt_kernel, dim3((unsigned)((m + TBM - 1) / TBM)), dim3(256), 0, s, m, (int)n, alpha, L,
+                       ldl, (const double*)W, B, ldb);
+    HIP_LAUNCH_CHECK();
+    return true;
+}
+
+bool trsm_lln_fast(i64 m, i64 n, double alpha, const double* L, i64 ldl, double* B, i64 ldb, bool unit,
+                   hipStream_t s) {
+    if (m <= 0 || n <= 0) return true;
+    if (m > 1024) return false;
+    const int nbj = (int)((m + 31) / 32);
+    double* W = static_cast<double*>(workspace(s, sizeof(double) * (size_t)nbj * 1024, WS_C));
+    hipLaunchKernelGGL(tri_inv32_kernel, dim3(nbj), dim3(64), 0, s, (int)m, L, ldl, W, unit);
+    HIP_LAUNCH_CHECK();
+    hipLaunchKernelGGL(trsm_lln_kernel, dim3((unsigned)((n + TBN - 1) / TBN)), dim3(256), 0, s, (int)m, n, alpha, L,
                        ldl, (const double*)W, B, ldb);
     HIP_LAUNCH_CHECK();
     return true;

@@ -17,6 +17,8 @@ bool potrf_fast(int n, double* A, i64 lda, i64* info, i64 info_off, hipStream_t 
 void potrf_lds_profile(int n, double* A, i64 lda, i64* info, i64* prof, hipStream_t s);
 bool trsm_rlt_fast(i64 m, i64 n, double alpha, const double* L, i64 ldl, double* B, i64 ldb, bool unit,
                    hipStream_t s);
+bool trsm_lln_fast(i64 m, i64 n, double alpha, const double* L, i64 ldl, double* B, i64 ldb, bool unit,
+                   hipStream_t s);
 // qr_fast.hip: tall fp64 QR panel (shifted CholeskyQR3 + Householder reconstruction);
 // false = not applicable, or broke down (panel restored)
 bool geqrf_cholqr(i64 m, i64 b, double* A, i64 lda, double* tau, double* Tm, i64 ldt, double* V, i64 ldv,

@@ -189,6 +189,9 @@ void trsm(char side, char uplo, char trans, char diag, i64 m, i64 n, T alpha,
         if (side == 'R' && uplo == 'L' && trans != 'N' &&
             trsm_rlt_fast(m, n, alpha, A, lda, B, ldb, diag == 'U', s))
             return;
+        // L X = alpha B (LU's U rows, forward solves): one-launch MFMA kernel
+        if (side == 'L' && uplo == 'L' && trans == 'N' && trsm_lln_fast(m, n, alpha, A, lda, B, ldb, diag == 'U', s))
+            return;
     }
     const bool lower_eff = (uplo == 'L') == (trans == 'N');
     const i64 kt = side == 'L' ? m : n;

@@ -213,6 +213,22 @@ def test_getrf_panel_persistent_fp64(m, n):
     assert (A.cpu() - LU_ref).abs().max() / A0.abs().max() < 1e-12
 
 
+@pytest.mark.parametrize("m,n", [(16, 1), (100, 50), (256, 300), (512, 4000), (1000, 70)])
+@pytest.mark.parametrize("unit", [False, True])
+def test_trsm_lln_fp64_fast(m, n, unit):
+    # L X = alpha B (lower, no-trans): one-launch blocked-inverse MFMA kernel
+    g = torch.Generator().manual_seed(m + n)
+    Lf = torch.randn(m + 5, m, dtype=torch.float64, generator=g)
+    Lf[:m] = torch.tril(Lf[:m]) + 2 * m ** 0.5 * torch.eye(m, dtype=torch.float64)
+    L = Lf.t().contiguous().t().cuda()[:m]                # lda > m
+    B0 = torch.randn(m, n, dtype=torch.float64, generator=g)
+    B = B0.t().contiguous().t().cuda()
+    ops.trsm('L', 'L', 'N', 'U' if unit else 'N', 0.5, L, B)
+    Lr = torch.tril(Lf[:m], -1) + torch.eye(m, dtype=torch.float64) if unit else torch.tril(Lf[:m])
+    X = torch.linalg.solve_triangular(Lr, 0.5 * B0, upper=False, unitriangular=unit)
+    assert (B.cpu() - X).abs().max() / X.abs().max() < 1e-12
+
+
 @pytest.mark.parametrize("m,n", [(20000, 64), (32768, 256)])
 def test_getrf_panel_persistent_under_load(m, n):
     # granule hand-offs while a GEMM streams on another stream (uneven
