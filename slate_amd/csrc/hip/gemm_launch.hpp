@@ -1,6 +1,7 @@
 // Host launchers for the MFMA GEMM kernels (see gemm.hpp); instantiated per
 // dtype in gemm_{s,d,c,z}.hip so the builds run in parallel.
 #pragma once
+#include <cstdlib>
 #include "gemm.hpp"
 #include "launchers.hpp"
 #include "workspace.hpp"
@@ -70,8 +71,33 @@ static bool gemm_splitk(const GemmCall& c, int tile, hipStream_t s, Launch&& lau
     return true;
 }
 
+// below this many 128 x 128 tiles (x batch) fp64 GEMMs use 64 x 64 tiles:
+// the trailing updates near the end of a factorization would otherwise leave
+// each CU with one or two workgroups, too few waves to hide the MFMA / LDS
+// latency (measured: masked 4096^2 x 512 update at 29 TF/s with 128 x 128).
+// SLATE_AMD_GEMM_SMALL overrides (0 = always 128 x 128).
+static inline i64 gemm_small_tiles() {
+    static const i64 v = [] {
+        const char* e = std::getenv("SLATE_AMD_GEMM_SMALL");
+        return e ? (i64)std::atoll(e) : (i64)2048;
+    }();
+    return v;
+}
+
 template <typename T, bool TA, bool TB, bool PTRS>
 static void launch_real(const GemmArgs<T>& a, int batch, hipStream_t s) {
+    if constexpr (sizeof(T) == 8) {
+        const i64 g128 = ((a.m + 127) / 128) * ((a.n + 127) / 128) * batch;
+        if (g128 < gemm_small_tiles()) {
+            constexpr int BM = 64, BN = 64, BK = 8;
+            const i64 gm = (a.m + BM - 1) / BM, gn = (a.n + BN - 1) / BN;
+            if (gm == 0 || gn == 0 || batch == 0) return;
+            hipLaunchKernelGGL((gemm_real_kernel<T, TA, TB, BM, BN, BK, PTRS, 2, 2>), dim3((unsigned)(gm * gn), (unsigned)batch),
+                               dim3(256), 0, s, a);
+            HIP_LAUNCH_CHECK();
+            return;
+        }
+    }
     // 128x128 macro tile, 8 waves (2x4) each 64x32, BK = 8: measured best of
     // the tile sweep in tools/exp/gemm_variants.hip on MI355X (more resident
     // waves per SIMD hide the f64 MFMA / LDS latency better than deeper K).
