@@ -136,25 +136,29 @@ struct SwapPlan {                // folded permutation of one swap sequence
 __global__ void __launch_bounds__(MAXSW)
 laswp_setup_kernel(i64 k1, i64 k2, const i64* __restrict__ ipiv, i64 ioff, int incx, SwapPlan* plan) {
     __shared__ int pv[MAXSW];                // relative pivot rows (relative to k1)
+    __shared__ int prv[MAXSW];               // prv[t]: last swap t' < t that targets row t (-1: none)
     __shared__ int s_cnt;
     const int ns = (int)(k2 - k1), q = threadIdx.x;
     if (q == 0) s_cnt = ns;
-    if (q < ns) pv[q] = (int)(ipiv[k1 + q] - ioff - k1);
+    if (q < ns) {
+        pv[q] = (int)(ipiv[k1 + q] - ioff - k1);
+        prv[q] = -1;
+    }
     // incx < 0 applies the swaps in reverse order = the inverse permutation:
     // same fold, source and destination exchanged
     i64* dst = incx > 0 ? plan->trow : plan->tsrc;
     i64* srcv = incx > 0 ? plan->tsrc : plan->trow;
     __syncthreads();
-    // source of the content found in row r right after swap t (t < ns, r == pv[t])
+    // every swap t' targets pv[t'] >= t', so the swaps targeting row t < ns all
+    // come before swap t: the last of them is a max
+    if (q < ns && pv[q] != q && pv[q] < ns) atomicMax(&prv[pv[q]], q);
+    __syncthreads();
+    // content of row t just before swap t: what the last earlier swap
+    // targeting row t put there, i.e. row prv[t]'s content just before swap
+    // prv[t] -- follow the pointers (O(1) per hop)
     auto chain = [&](int t) -> int {
-        int row = t;                          // content of row t just before swap t ...
-        for (;;) {
-            int kk = -1;
-            for (int x = t - 1; x >= 0; --x)  // ... is what the last earlier swap targeting it put there
-                if (pv[x] == row) { kk = x; break; }
-            if (kk < 0) return row;
-            row = kk; t = kk;
-        }
+        while (prv[t] >= 0) t = prv[t];
+        return t;
     };
     if (q < ns) {
         // position q: content of row pv[q] just before swap q

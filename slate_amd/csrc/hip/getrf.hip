@@ -331,7 +331,7 @@ getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64
     __shared__ double candL[PG][NBB];
     __shared__ i64 s_p;
     __shared__ int s_gw, s_bt, s_abort;
-    __shared__ int piv_s[NBB], tr_s[2 * NBB], ts_s[2 * NBB], s_nt;
+    __shared__ int piv_s[NBB], prv_s[NBB], tr_s[2 * NBB], ts_s[2 * NBB], s_nt;
     const int G = gridDim.x, g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const i64 i = (i64)g * PT2 + tid;                 // this thread's row
     const bool have = i < m;
@@ -465,19 +465,17 @@ getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64
     if (N <= w || s_abort) return;
     __syncthreads();
     if (tid == 0) s_nt = w;
+    if (tid < w) prv_s[tid] = -1;
+    __syncthreads();
+    if (tid < w && piv_s[tid] != tid && piv_s[tid] < w) atomicMax(&prv_s[piv_s[tid]], tid);
     __syncthreads();
     if (tid < w) {
         // parallel fold (see laswp_setup_kernel): the row finally at j came
-        // from piv_s[j] just before swap j
+        // from piv_s[j] just before swap j; prv_s[t] = last swap before t
+        // that targets row t
         auto chain = [&](int t) -> int {
-            int row = t;
-            for (;;) {
-                int kk = -1;
-                for (int x = t - 1; x >= 0; --x)
-                    if (piv_s[x] == row) { kk = x; break; }
-                if (kk < 0) return row;
-                row = kk; t = kk;
-            }
+            while (prv_s[t] >= 0) t = prv_s[t];
+            return t;
         };
         const int q = tid, r = piv_s[q];
         int src;
