@@ -117,6 +117,10 @@ static void register_kernels(py::module& m) {
         dispatch(dt, [&](auto z) { using T = decltype(z);
             trtri<T>(uplo, diag, n, P<T>(A), lda, P<i64>(info), S(st)); });
     });
+    m.def("lu_persist_profile", [](int enable) {
+        unsigned long long v[8];
+        lu_persist_profile(enable, v);
+        return std::vector<unsigned long long>(v, v + 8); });
     m.def("potrf_lds_profile", [](i64 n, uintptr_t A, i64 lda, uintptr_t info, uintptr_t prof, uintptr_t st) {
         potrf_lds_profile((int)n, P<double>(A), lda, P<i64>(info), P<i64>(prof), S(st)); });
     m.def("getrf_work_bytes", []() { return (i64)getrf_work_bytes(); });

@@ -304,6 +304,10 @@ struct PersistBuf {
     unsigned long long err;
 };
 
+// tools only: per-phase shader-clock totals of workgroup 0 (lu_persist_profile)
+__device__ int g_lu_prof_on = 0;
+__device__ unsigned long long g_lu_prof[8];
+
 __device__ inline double ld_sc1(const double* p) {
     return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -342,12 +346,22 @@ getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64
         for (int c = 0; c < NBB; ++c) a[c] = A[ir + (i64)min(c, w - 1) * lda];
     }
     if (tid == 0) s_abort = 0;
+    int zero_at = -1;
+    const bool prof = g_lu_prof_on && g == 0 && tid == 0;
+    unsigned long long tl = prof ? clock64() : 0, ph[5] = {0, 0, 0, 0, 0};
+#define LSTAMP(k) do { if (prof) { const unsigned long long t_ = clock64(); ph[k] += t_ - tl; tl = t_; } } while (0)
+    // w in a VGPR: per-lane compares give v_cndmask selects instead of 32
+    // uniform branches per column-indexed loop
+    int wv_; asm volatile("v_mov_b32 %0, %1" : "=v"(wv_) : "s"(w));
     for (int j = 0; j < w; ++j) {
         const int par = j & 1;
+        int jv; asm volatile("v_mov_b32 %0, %1" : "=v"(jv) : "s"(j));
         // ---- local arg-max of column j over unpivoted rows (i >= j)
         double v = -1.0;
+        double aj = 0.0;
         #pragma unroll
-        for (int c = 0; c < NBB; ++c) if (c == j) v = (have && i >= j) ? fabs(a[c]) : -1.0;
+        for (int c = 0; c < NBB; ++c) aj = (c == jv) ? a[c] : aj;
+        v = (have && i >= j) ? fabs(aj) : -1.0;
         i64 bi = i;
         int bt = tid;
         wave_argmax(v, bi, bt);
@@ -362,17 +376,19 @@ getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64
             st_sc1(&pb->idx[par][g], bb);
         }
         __syncthreads();
+        LSTAMP(0);                                      // local arg-max
         // ---- publish the winning row and (owner) row j, write-through
         if (tid == s_bt) {
             #pragma unroll
-            for (int c = 0; c < NBB; ++c) if (c < w) st_sc1(&pb->cand[par][g][c], a[c]);
+            for (int c = 0; c < NBB; ++c) st_sc1(&pb->cand[par][g][c], a[c]);   // all NBB: no uniform branches
         }
         if (have && i == j) {
             #pragma unroll
-            for (int c = 0; c < NBB; ++c) if (c < w) st_sc1(&pb->diag[par][c], a[c]);
+            for (int c = 0; c < NBB; ++c) st_sc1(&pb->diag[par][c], a[c]);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        LSTAMP(1);                                      // publish + drain
         if (tid == 0) {
             __hip_atomic_fetch_add(&pb->cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned long long target = (unsigned long long)(j + 1) * G;
@@ -386,6 +402,7 @@ getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64
                 }
             }
         }
+        LSTAMP(2);                                      // arrive + poll
         __syncthreads();
         if (s_abort) break;
         // ---- global pivot: every candidate row, the partials and row j are
@@ -421,38 +438,49 @@ getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64
             }
         }
         __syncthreads();
+        LSTAMP(3);                                      // gather + global arg-max
         const i64 p = s_p;
         const int gw = s_gw;
         if (tid < w) prow[tid] = (gw < 0) ? drow[tid] : candL[gw][tid];
         __syncthreads();
-        if (tid == 0) piv_s[j] = (int)p;
-        if (g == 0 && tid == 0) {
-            if (ipiv) ipiv[j] = p + ioff;
-            if (prow[j] == 0.0 && info)
-                atomicCAS(reinterpret_cast<unsigned long long*>(info), 0ull, (unsigned long long)(j + 1 + info_off));
+        if (tid == 0) {
+            piv_s[j] = (int)p;
+            if (prow[j] == 0.0 && zero_at < 0) zero_at = j;     // first exactly-zero pivot (reported at the end)
         }
         // ---- interchange rows j <-> p and eliminate column j (registers)
         if (have && i >= j) {
             if (i == j) {
                 #pragma unroll
-                for (int c = 0; c < NBB; ++c) if (c < w) a[c] = prow[c];
+                for (int c = 0; c < NBB; ++c) a[c] = (c < wv_) ? prow[c] : a[c];
             } else {
                 if (i == p) {
                     #pragma unroll
-                    for (int c = 0; c < NBB; ++c) if (c < w) a[c] = drow[c];
+                    for (int c = 0; c < NBB; ++c) a[c] = (c < wv_) ? drow[c] : a[c];
                 }
                 const double u = prow[j];
                 double l = 0.0;
                 #pragma unroll
-                for (int c = 0; c < NBB; ++c) if (c == j) l = a[c];
+                for (int c = 0; c < NBB; ++c) l = (c == jv) ? a[c] : l;
                 if (u != 0.0) l = l / u;
                 #pragma unroll
                 for (int c = 0; c < NBB; ++c) {
-                    if (c == j) a[c] = l;
-                    else if (c > j && c < w) a[c] -= l * prow[c];
+                    const double upd = a[c] - l * prow[c];
+                    a[c] = (c == jv) ? l : ((c > jv && c < wv_) ? upd : a[c]);
                 }
             }
         }
+        LSTAMP(4);                                      // interchange + elimination
+    }
+#undef LSTAMP
+    if (prof) {
+        #pragma unroll
+        for (int k = 0; k < 5; ++k) g_lu_prof[k] += ph[k];
+    }
+    // pivots and info once per launch (global stores kept out of the column loop)
+    if (g == 0 && !s_abort) {
+        if (ipiv && tid < w) ipiv[tid] = piv_s[tid] + ioff;
+        if (tid == 0 && zero_at >= 0 && info)
+            atomicCAS(reinterpret_cast<unsigned long long*>(info), 0ull, (unsigned long long)(zero_at + 1 + info_off));
     }
     if (have) {
         #pragma unroll
@@ -608,6 +636,15 @@ void getrf_panel_ws(i64 m, i64 n, T* A, i64 lda, i64* ipiv, i64* info, double th
         if (!nopiv && !ctx.full) laswp_off<T>(n - k, A + k * lda, lda, 0, k, ipiv, 0, s);
         trsm<T>('L', 'L', 'N', 'U', k, n - k, s_from_real(T(), 1), A, lda, A + k * lda, lda, s);
     }
+}
+
+// tools: enable (1) / disable (0) the per-phase clocks of the persistent
+// base case and read the totals accumulated so far (then reset them)
+void lu_persist_profile(int enable, unsigned long long* out) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (out) HIP_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lu_prof), sizeof(z)));
+    HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_lu_prof), z, sizeof(z)));
+    HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_lu_prof_on), &enable, sizeof(int)));
 }
 
 size_t getrf_work_bytes() { return PANEL_BYTES + sizeof(PersistBuf); }

@@ -52,6 +52,7 @@ template <typename T>
 void getrf_panel_ws(i64 m, i64 n, T* A, i64 lda, i64* ipiv, i64* info, double thr, bool nopiv,
                     void* work, hipStream_t s);
 size_t getrf_work_bytes();
+void lu_persist_profile(int enable, unsigned long long* out);
 template <typename T>
 void laswp_off(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, i64 ioff, hipStream_t s, int incx = 1);
 
