@@ -306,53 +306,50 @@ tri_inv32_kernel(int n, const double* __restrict__ L, i64 ldl, double* __restric
 }
 
 // ---------------------------------------------------------------- trsm_rlt
-// X L^T = alpha B (B: m x n, L: n x n lower), X overwrites B.
+// X L^T = alpha B (B: m x n, L: n x n lower), X overwrites B.  Eight waves
+// per 64-row block: wave (s, t) owns rows 16 s.. and, of each 32-column
+// block, the 16 columns 16 t..: twice the waves of one-wave-per-strip, so
+// each SIMD has four to hide the operand latency of the long K loops.
 constexpr int TBM = 64;
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(512)
 trsm_rlt_kernel(i64 m, int n, double alpha, const double* __restrict__ L, i64 ldl, const double* __restrict__ Winv,
                 double* __restrict__ B, i64 ldb) {
     __shared__ double R[32][TBM + 1];       // R[c][r]
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int st = w & 3, tt = w >> 2;       // row strip, column tile
     const i64 r0 = (i64)blockIdx.x * TBM;
     const int mr = (int)min((i64)TBM, m - r0);
-    const int ml = 16 * w + (lane & 15);     // this lane's row within the block (MFMA m index)
+    const int ml = 16 * st + (lane & 15);    // this lane's row within the block (MFMA m index)
     const i64 rx = r0 + min(ml, mr - 1);     // clamped (valid) row for loads
     for (int c0 = 0; c0 < n; c0 += 32) {
         const int jb = min(32, n - c0);
-        d4 acc2[1][2] = {{d4{0, 0, 0, 0}, d4{0, 0, 0, 0}}};
+        d4 acc1[1][1] = {{d4{0, 0, 0, 0}}};
         if (c0 > 0) {
             const int xr[1] = {(int)(rx - r0)};
-            const int yr[2] = {min(lane & 15, n - 1 - c0), min(16 + (lane & 15), n - 1 - c0)};
-            strip_update<1, 2, 8>(acc2, B + r0, xr, ldb, L + c0, yr, ldl, c0, lane);
+            const int yr[1] = {min(16 * tt + (lane & 15), n - 1 - c0)};
+            strip_update<1, 1, 8>(acc1, B + r0, xr, ldb, L + c0, yr, ldl, c0, lane);
         }
-        d4 (&acc)[2] = acc2[0];
         #pragma unroll
-        for (int t = 0; t < 2; ++t)
-            #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int c = 16 * t + (lane >> 4) + 4 * r;
-                double v = 0.0;
-                if (ml < mr && c < jb) v = alpha * B[(r0 + ml) + (i64)(c0 + c) * ldb] - acc[t][r];
-                R[c][ml] = v;
-            }
+        for (int r = 0; r < 4; ++r) {
+            const int c = 16 * tt + (lane >> 4) + 4 * r;
+            double v = 0.0;
+            if (ml < mr && c < jb) v = alpha * B[(r0 + ml) + (i64)(c0 + c) * ldb] - acc1[0][0][r];
+            R[c][ml] = v;
+        }
         __syncthreads();
-        // X_J = R inv(L_JJ)^T
+        // X_J(:, tile tt) = R inv(L_JJ)^T
         const double* W = Winv + (i64)(c0 / 32) * 1024;
-        d4 x[2] = {d4{0, 0, 0, 0}, d4{0, 0, 0, 0}};
+        d4 x = {0, 0, 0, 0};
         #pragma unroll
         for (int k = 0; k < 32; k += 4) {
             const int kk = k + (lane >> 4);
-            const double a = R[kk][ml];
-            #pragma unroll
-            for (int t = 0; t < 2; ++t) x[t] = mma(W[(16 * t + (lane & 15)) + 32 * kk], a, x[t]);
+            x = mma(W[(16 * tt + (lane & 15)) + 32 * kk], R[kk][ml], x);
         }
         #pragma unroll
-        for (int t = 0; t < 2; ++t)
-            #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int c = 16 * t + (lane >> 4) + 4 * r;
-                if (ml < mr && c < jb) B[(r0 + ml) + (i64)(c0 + c) * ldb] = x[t][r];
-            }
+        for (int r = 0; r < 4; ++r) {
+            const int c = 16 * tt + (lane >> 4) + 4 * r;
+            if (ml < mr && c < jb) B[(r0 + ml) + (i64)(c0 + c) * ldb] = x[r];
+        }
         __syncthreads();
     }
 }
@@ -438,7 +435,7 @@ bool trsm_rlt_fast(i64 m, i64 n, double alpha, const double* L, i64 ldl, double*
     double* W = static_cast<double*>(workspace(s, sizeof(double) * (size_t)nbj * 1024, WS_C));
     hipLaunchKernelGGL(tri_inv32_kernel, dim3(nbj), dim3(64), 0, s, (int)n, L, ldl, W, unit);
     HIP_LAUNCH_CHECK();
-    hipLaunchKernelGGL(trsm_rlt_kernel, dim3((unsigned)((m + TBM - 1) / TBM)), dim3(256), 0, s, m, (int)n, alpha, L,
+    hipLaunchKernelGGL(trsm_rlt_kernel, dim3((unsigned)((m + TBM - 1) / TBM)), dim3(512), 0, s, m, (int)n, alpha, L,
                        ldl, (const double*)W, B, ldb);
     HIP_LAUNCH_CHECK();
     return true;
