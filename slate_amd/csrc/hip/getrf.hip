@@ -308,6 +308,17 @@ struct PersistBuf {
 __device__ int g_lu_prof_on = 0;
 __device__ unsigned long long g_lu_prof[8];
 
+// wave arg-max of (|value|, row) with a 32-bit row: 3 dwords per shuffle
+// round instead of 5
+__device__ inline void wave_argmax32(double& v, int& i) {
+    #pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double w = xshfl(v, o);
+        const int k = __shfl_xor(i, o, 64);
+        if (beats(w, (i64)k, v, (i64)i)) { v = w; i = k; }
+    }
+}
+
 __device__ inline double ld_sc1(const double* p) {
     return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -362,10 +373,9 @@ getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64
         #pragma unroll
         for (int c = 0; c < NBB; ++c) aj = (c == jv) ? a[c] : aj;
         v = (have && i >= j) ? fabs(aj) : -1.0;
-        i64 bi = i;
-        int bt = tid;
-        wave_argmax(v, bi, bt);
-        if (lane == 0) { wv[wid] = v; wi[wid] = bi; wt[wid] = bt; }
+        int bi = (int)i;                              // rows < 2^31; the winner's thread is bi - g PT2
+        wave_argmax32(v, bi);
+        if (lane == 0) { wv[wid] = v; wi[wid] = bi; wt[wid] = bi - g * PT2; }
         __syncthreads();
         if (tid == 0) {
             double bv = wv[0]; i64 bb = wi[0]; int t = wt[0];
