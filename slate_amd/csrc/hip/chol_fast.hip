@@ -34,6 +34,12 @@ constexpr int PT = 512;          // threads of potrf_lds (8 waves: 256-VGPR budg
 constexpr int PLD = PN + 1;      // LDS column stride (doubles)
 
 __device__ inline d4 mma(double x, double y, d4 c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, c, 0, 0, 0); }
+// 1/sqrt(d) for d > 0: hardware estimate + two Newton steps (full fp64)
+__device__ inline double rsq_f64(double d) {
+    double r = __builtin_amdgcn_rsq(d);
+    r = r * (1.5 - 0.5 * d * r * r);
+    return r * (1.5 - 0.5 * d * r * r);
+}
 }  // namespace
 
 // acc[t] += sum_k X(r, k) Y(c, k) over k in [0, K), for one
@@ -106,6 +112,7 @@ potrf_lds_kernel(int n, double* __restrict__ A, i64 lda, i64* info, i64 info_off
     __shared__ double Li[16][17];            // inverse of the current 16 x 16 diagonal sub-block
     __shared__ double Ld[16][17];            // its Cholesky factor (row-major, zero above)
     __shared__ double Dd[16][17];            // working copy of the sub-block
+    __shared__ double Xf[16][17];            // final rows of the inverse
     __shared__ double rdl[16];               // 1 / L(j, j)
     __shared__ int s_fail;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -170,8 +177,10 @@ potrf_lds_kernel(int n, double* __restrict__ A, i64 lda, i64* info, i64 info_off
             const int wq = min(16, jb - q0);
             {
                 // thread (di, dc) < 256 owns element (di, dc): right-looking
-                // Cholesky, one barrier per column; the inverse (forward
-                // substitution on I, scaling deferred) runs one column behind
+                // Cholesky two columns per barrier (2x2 diagonal step, rank-2
+                // update); the inverse (forward substitution on I) runs one
+                // pair behind, final rows going to Xf (no row is read and
+                // written in the same interval)
                 const bool act = tid < 256;
                 const int di = tid & 15, dc = (tid >> 4) & 15;
                 if (act) {
@@ -182,30 +191,42 @@ potrf_lds_kernel(int n, double* __restrict__ A, i64 lda, i64* info, i64 info_off
                 double myl = 0.0;
                 int fail = 0;
                 #pragma unroll 1
-                for (int j = 0; j < 16; ++j) {
-                    if (act) {
-                        double d = Dd[j][j];
-                        if (j < wq && !(d > 0.0)) {
-                            if (!fail) fail = c0 + q0 + j + 1;
-                            d = 1.0;
-                        }
-                        const double sq = sqrt(d), inv = 1.0 / sq;
-                        const double lij = Dd[di][j] * inv;
+                for (int j = 0; j <= 16; j += 2) {
+                    if (act && j < 16) {
+                        double d0 = Dd[j][j];
+                        const double d10 = Dd[j + 1][j], d11 = Dd[j + 1][j + 1];
+                        const double a0 = Dd[di][j], a1 = Dd[di][j + 1], b0 = Dd[dc][j], b1 = Dd[dc][j + 1];
+                        if (j < wq && !(d0 > 0.0)) { if (!fail) fail = c0 + q0 + j + 1; d0 = 1.0; }
+                        const double i0 = rsq_f64(d0), s0 = d0 * i0;          // 1 / L(j, j), L(j, j)
+                        const double l10 = d10 * i0;
+                        double e = d11 - l10 * l10;
+                        if (j + 1 < wq && !(e > 0.0)) { if (!fail) fail = c0 + q0 + j + 2; e = 1.0; }
+                        const double i1 = rsq_f64(e), s1 = e * i1;
+                        const double ld0 = a0 * i0, ld1 = (a1 - ld0 * l10) * i1;   // L(di, j), L(di, j+1)
+                        const double lc0 = b0 * i0, lc1 = (b1 - lc0 * l10) * i1;   // L(dc, j), L(dc, j+1)
                         if (dc == j) {
-                            myl = di > j ? lij : (di == j ? sq : 0.0);
+                            myl = di > j ? ld0 : (di == j ? s0 : 0.0);
                             Ld[di][j] = myl;
-                        } else if (dc > j && di >= dc) {
-                            Dd[di][dc] -= lij * (Dd[dc][j] * inv);
+                        } else if (dc == j + 1) {
+                            myl = di > j + 1 ? ld1 : (di == j + 1 ? s1 : 0.0);
+                            Ld[di][j + 1] = myl;
+                        } else if (dc > j + 1 && di >= dc) {
+                            Dd[di][dc] -= ld0 * lc0 + ld1 * lc1;
                         }
-                        if (tid == 0) rdl[j] = inv;
-                        if (j > 0 && di >= j) Li[di][dc] -= Ld[di][j - 1] * (Li[j - 1][dc] * rdl[j - 1]);
+                        if (tid == 0) { rdl[j] = i0; rdl[j + 1] = i1; }
+                    }
+                    if (act && j > 0) {
+                        // substitution steps j-2, j-1 (their L columns were
+                        // written in the previous interval)
+                        const double x2 = Li[j - 2][dc] * rdl[j - 2];
+                        const double x1 = (Li[j - 1][dc] - Ld[j - 1][j - 2] * x2) * rdl[j - 1];
+                        if (di == j - 2) Xf[di][dc] = x2;
+                        else if (di == j - 1) Xf[di][dc] = x1;
+                        else if (di >= j) Li[di][dc] -= Ld[di][j - 2] * x2 + Ld[di][j - 1] * x1;
                     }
                     __syncthreads();
                 }
-                if (act) {
-                    Li[di][dc] *= rdl[di];
-                    if (di < wq && dc <= di) P[(q0 + dc) * PLD + q0 + di] = myl;
-                }
+                if (act && di < wq && dc <= di) P[(q0 + dc) * PLD + q0 + di] = myl;
                 if (tid == 0 && fail && !s_fail) s_fail = fail;
             }
             __syncthreads();
@@ -225,7 +246,7 @@ potrf_lds_kernel(int n, double* __restrict__ A, i64 lda, i64* info, i64 info_off
                 }
                 d4 acc = {0, 0, 0, 0};
                 #pragma unroll
-                for (int u = 0; u < 4; ++u) acc = mma(Li[lane & 15][4 * u + (lane >> 4)], a[u], acc);
+                for (int u = 0; u < 4; ++u) acc = mma(Xf[lane & 15][4 * u + (lane >> 4)], a[u], acc);
                 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int c = (lane >> 4) + 4 * r;
