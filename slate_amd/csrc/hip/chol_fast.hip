@@ -192,6 +192,16 @@ potrf_lds_kernel(int n, double* __restrict__ A, i64 lda, i64* info, i64 info_off
                 int fail = 0;
                 #pragma unroll 1
                 for (int j = 0; j <= 16; j += 2) {
+                    if (act && j > 0) {
+                        // substitution steps j-2, j-1 (their L columns were
+                        // written in the previous interval; issued first: its LDS reads
+                        // do not wait behind this interval's writes)
+                        const double x2 = Li[j - 2][dc] * rdl[j - 2];
+                        const double x1 = (Li[j - 1][dc] - Ld[j - 1][j - 2] * x2) * rdl[j - 1];
+                        if (di == j - 2) Xf[di][dc] = x2;
+                        else if (di == j - 1) Xf[di][dc] = x1;
+                        else if (di >= j) Li[di][dc] -= Ld[di][j - 2] * x2 + Ld[di][j - 1] * x1;
+                    }
                     if (act && j < 16) {
                         double d0 = Dd[j][j];
                         const double d10 = Dd[j + 1][j], d11 = Dd[j + 1][j + 1];
@@ -214,15 +224,6 @@ potrf_lds_kernel(int n, double* __restrict__ A, i64 lda, i64* info, i64 info_off
                             Dd[di][dc] -= ld0 * lc0 + ld1 * lc1;
                         }
                         if (tid == 0) { rdl[j] = i0; rdl[j + 1] = i1; }
-                    }
-                    if (act && j > 0) {
-                        // substitution steps j-2, j-1 (their L columns were
-                        // written in the previous interval)
-                        const double x2 = Li[j - 2][dc] * rdl[j - 2];
-                        const double x1 = (Li[j - 1][dc] - Ld[j - 1][j - 2] * x2) * rdl[j - 1];
-                        if (di == j - 2) Xf[di][dc] = x2;
-                        else if (di == j - 1) Xf[di][dc] = x1;
-                        else if (di >= j) Li[di][dc] -= Ld[di][j - 2] * x2 + Ld[di][j - 1] * x1;
                     }
                     __syncthreads();
                 }
