@@ -312,10 +312,12 @@ def world() -> Comm:
 def init(backend: Optional[str] = None):
     """Initialise torch.distributed from the torchrun environment (RANK,
     WORLD_SIZE, MASTER_ADDR/PORT, LOCAL_RANK) and bind this process to its
-    GPU.  Backend defaults to "nccl" (= RCCL) when GPUs are present."""
+    GPU.  Backend defaults to "nccl" (= RCCL) when GPUs are present;
+    SLATE_AMD_DIST_BACKEND=gloo forces gloo (rehearsing several ranks on one
+    GPU: every rank then uses the current device)."""
     if not _dist_ready() and int(os.environ.get("WORLD_SIZE", "1")) > 1:
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = os.environ.get("SLATE_AMD_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             lr = int(os.environ.get("LOCAL_RANK", "0"))
             torch.cuda.set_device(lr)
