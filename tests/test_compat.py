@@ -134,3 +134,28 @@ def test_c_api(tmp_path):
     r = subprocess.run([exe], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
     assert r.returncode == 0, r.stdout
     assert "dgesv info=0" in r.stdout
+
+
+def test_fortran_module(tmp_path):
+    """Compile the Fortran module (include/slate_amd/slate_amd.f90) and the
+    Fortran example with flang, link against libslate_amd_c.so and run it."""
+    import os
+    import shutil
+    import subprocess
+    import sysconfig
+    flang = shutil.which("flang") or ("/opt/rocm/llvm/bin/flang" if os.path.exists("/opt/rocm/llvm/bin/flang") else None)
+    if flang is None:
+        pytest.skip("no Fortran compiler")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "slate_amd")
+    exe = str(tmp_path / "ex_fortran")
+    cmd = [flang, "-O1", "-J", str(tmp_path), os.path.join(root, "include", "slate_amd", "slate_amd.f90"),
+           os.path.join(root, "examples", "fortran", "ex_fortran.f90"), "-L", lib, "-lslate_amd_c",
+           "-Wl,-rpath," + lib, "-L", sysconfig.get_config_var("LIBDIR"),
+           "-lpython" + sysconfig.get_config_var("LDVERSION"), "-o", exe]
+    subprocess.run(cmd, check=True, cwd=str(tmp_path))
+    env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""),
+               SLATE_AMD_LAPACK_TARGET="host")
+    r = subprocess.run([exe], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout
+    assert "dgesv info=0" in r.stdout and "dposv info=0" in r.stdout
