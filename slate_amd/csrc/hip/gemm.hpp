@@ -59,7 +59,8 @@ struct GemmArgs {
     T* const* Cptrs;
     int vecA, vecB;          // 16-byte vector loads allowed
     int group_m;             // tile-order group size
-    int remap;               // XCD-chunked block order (off for triangular masks: keeps XCDs balanced)
+    int remap;               // 0: plain order; 1: XCD-chunked grouped order (full output);
+                             // 2: compact lower triangle of 8x8 super-tiles (set by launch_real)
     TriMask mask;
 };
 
@@ -152,15 +153,32 @@ gemm_real_kernel(GemmArgs<T> a) {
     else { A = a.A + batch * a.strideA; B = a.B + batch * a.strideB; C = a.C + batch * a.strideC; }
 
     const int gm = (int)((a.m + BM - 1) / BM), gn = (int)((a.n + BN - 1) / BN);
-    const int nblk = gm * gn;
-    int lin = a.remap ? xcd_remap(blockIdx.x, nblk) : (int)blockIdx.x;
-    // grouped ordering: GROUP block-rows swept column by column
-    const int G = a.group_m;
-    int grp = lin / (G * gn);
-    int first = grp * G;
-    int gsz = min(gm - first, G);
-    int inner = lin - grp * G * gn;
-    const int bm = first + inner % gsz, bn = inner / gsz;
+    int bm, bn;
+    if (a.remap == 2) {
+        // compact lower triangle (launcher checked that no tile above the
+        // diagonal holds a kept element): the grid covers only the 8 x 8
+        // super-tiles I >= J, column by column, so the XCD chunks stay
+        // balanced and each chunk is a run of whole super-tiles (L2 reuse of
+        // 8 A and 8 B tiles per 64 outputs).
+        const int lin = xcd_remap(blockIdx.x, gridDim.x);
+        const int s = lin >> 6, w = lin & 63;
+        const int gsm = (gm + 7) >> 3;
+        int J = 0, rem = s;
+        while (rem >= gsm - J) { rem -= gsm - J; ++J; }
+        bm = (J + rem) * 8 + (w & 7);
+        bn = J * 8 + (w >> 3);
+        if (bm >= gm || bn >= gn) return;
+    } else {
+        const int nblk = gm * gn;
+        int lin = a.remap ? xcd_remap(blockIdx.x, nblk) : (int)blockIdx.x;
+        // grouped ordering: GROUP block-rows swept column by column
+        const int G = a.group_m;
+        int grp = lin / (G * gn);
+        int first = grp * G;
+        int gsz = min(gm - first, G);
+        int inner = lin - grp * G * gn;
+        bm = first + inner % gsz; bn = inner / gsz;
+    }
     const i64 m0 = (i64)bm * BM, n0 = (i64)bn * BN;
     if (a.mask.skip_block(m0, min(m0 + BM, a.m), n0, min(n0 + BN, a.n))) return;
 

@@ -84,14 +84,42 @@ static inline i64 gemm_small_tiles() {
     return v;
 }
 
+// Lower-triangular masks on one rank (the potrf/herk trailing update) launch
+// only the 8 x 8 super-tiles on or below the diagonal, XCD-remapped
+// (remap = 2 in gemm_real_kernel).  Valid when every tile holding a kept
+// element has bm >= bn: square tiles, no block-cyclic interleave, and
+// row - col >= d with d >= 0.  Returns the block count, or 0 if not eligible.
+// SLATE_AMD_GEMM_TRI=0 disables it.  Measured (tools/exp/gemm_trimask.py,
+// 128 x 128 tiles, k = 512): 31744 x 30720 58.8 -> 59.7 TF/s, 8192 x 7168
+// 53.3 -> 54.8 TF/s; used for the 128 x 128 variant only.
+static inline bool gemm_tri_enabled() {
+    const char* e = std::getenv("SLATE_AMD_GEMM_TRI");  // read per launch: tests and sweeps toggle it
+    return !(e && e[0] == '0');
+}
+
+template <typename T>
+static i64 tri_blocks(const GemmArgs<T>& a, int BM, int BN) {
+    const TriMask& k = a.mask;
+    if (!gemm_tri_enabled() || k.mode != 1 || k.p != 1 || k.q != 1 || BM != BN) return 0;
+    if (k.col_off - k.row_off - k.diag_off < 0) return 0;
+    const i64 gm = (a.m + BM - 1) / BM, gn = (a.n + BN - 1) / BN;
+    const i64 gsm = (gm + 7) / 8, gsn = (gn + 7) / 8;
+    i64 sup = 0;
+    for (i64 J = 0; J < std::min(gsm, gsn); ++J) sup += gsm - J;
+    return sup * 64;
+}
+
 template <typename T, bool TA, bool TB, bool PTRS>
-static void launch_real(const GemmArgs<T>& a, int batch, hipStream_t s) {
+static void launch_real(const GemmArgs<T>& a0, int batch, hipStream_t s) {
+    GemmArgs<T> a = a0;
     if constexpr (sizeof(T) == 8) {
         const i64 g128 = ((a.m + 127) / 128) * ((a.n + 127) / 128) * batch;
         if (g128 < gemm_small_tiles()) {
             constexpr int BM = 64, BN = 64, BK = 8;
             const i64 gm = (a.m + BM - 1) / BM, gn = (a.n + BN - 1) / BN;
             if (gm == 0 || gn == 0 || batch == 0) return;
+            // no compact triangle here: measured 4096 x 3072 x 512 masked,
+            // 52.9 TF/s full grid vs 50.7 compact (tools/exp/gemm_trimask.py)
             hipLaunchKernelGGL((gemm_real_kernel<T, TA, TB, BM, BN, BK, PTRS, 2, 2>), dim3((unsigned)(gm * gn), (unsigned)batch),
                                dim3(256), 0, s, a);
             HIP_LAUNCH_CHECK();
@@ -105,7 +133,9 @@ static void launch_real(const GemmArgs<T>& a, int batch, hipStream_t s) {
     constexpr int WVM = 2, WVN = (sizeof(T) == 8) ? 4 : 2;
     i64 gm = (a.m + BM - 1) / BM, gn = (a.n + BN - 1) / BN;
     if (gm == 0 || gn == 0 || batch == 0) return;
-    dim3 grid((unsigned)(gm * gn), (unsigned)batch);
+    i64 nblk = gm * gn;
+    if (i64 t = tri_blocks(a, BM, BN)) { a.remap = 2; nblk = t; }
+    dim3 grid((unsigned)nblk, (unsigned)batch);
     hipLaunchKernelGGL((gemm_real_kernel<T, TA, TB, BM, BN, BK, PTRS, WVM, WVN>), grid, dim3(64 * WVM * WVN), 0, s, a);
     HIP_LAUNCH_CHECK();
 }

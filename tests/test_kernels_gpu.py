@@ -88,6 +88,22 @@ def test_gemm_trimask_blockcyclic():
     assert (C - exp).abs().max() < 1e-12
 
 
+@pytest.mark.parametrize("m,n,roff,coff,doff", [
+    (256, 256, 0, 0, 0), (1000, 700, 0, 0, 0), (700, 1000, 0, 0, 0), (900, 900, 0, 128, 0),
+    (900, 900, 64, 64, -5), (6400, 6400, 0, 0, 0), (6500, 6300, 0, 0, 0), (6400, 6400, 0, 256, 0)])
+def test_gemm_trimask_compact(m, n, roff, coff, doff):
+    # one-rank lower mask: compact lower-triangle launch (remap = 2) for both
+    # fp64 tile variants (64 x 64 below 2048 128-tiles, 128 x 128 above)
+    A, B, C = cm(m, 32, torch.float64, 7), cm(n, 32, torch.float64, 8), cm(m, n, torch.float64, 9)
+    C0 = C.clone()
+    ops.gemm(1.0, A, B, 1.0, C, 'N', 'T', mask=(1, 1 << 40, 1, 0, 1, 0, roff, coff, doff))
+    full = C0 + A @ B.mT
+    r = torch.arange(m, device="cuda")[:, None] + roff
+    c = torch.arange(n, device="cuda")[None, :] + coff
+    exp = torch.where(r + doff >= c, full, C0)
+    assert (C - exp).abs().max() < 1e-12
+
+
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("uplo", ["L", "U"])
 def test_potrf_tile(dt, uplo):
