@@ -84,14 +84,16 @@ static inline i64 gemm_small_tiles() {
     return v;
 }
 
-// Lower-triangular masks on one rank (the potrf/herk trailing update) launch
-// only the 8 x 8 super-tiles on or below the diagonal, XCD-remapped
-// (remap = 2 in gemm_real_kernel).  Valid when every tile holding a kept
-// element has bm >= bn: square tiles, no block-cyclic interleave, and
-// row - col >= d with d >= 0.  Returns the block count, or 0 if not eligible.
-// SLATE_AMD_GEMM_TRI=0 disables it.  Measured (tools/exp/gemm_trimask.py,
-// 128 x 128 tiles, k = 512): 31744 x 30720 58.8 -> 59.7 TF/s, 8192 x 7168
-// 53.3 -> 54.8 TF/s; used for the 128 x 128 variant only.
+// Lower-triangular masks (the potrf/herk trailing updates) launch only the
+// 8 x 8 super-tiles on or below the tile diagonal, XCD-remapped (remap = 2 in
+// gemm_real_kernel).  Valid when no tile with bm < bn holds a kept element:
+// global rows and columns grow with local ones, so it suffices that tile
+// (min(bn - 1, gm - 1), bn) is empty for every bn >= 1 (exact host check,
+// covers block-cyclic grids with p <= q such as 2 x 4).  Returns the block
+// count, or 0 if not eligible.  SLATE_AMD_GEMM_TRI=0 disables it.  Measured
+// (tools/exp/gemm_trimask.py, 128 x 128 tiles, k = 512): 31744 x 30720
+// 59.0 -> 59.6 TF/s, 8192 x 7168 53.3 -> 54.7 TF/s; used for the 128 x 128
+// variant only.
 static inline bool gemm_tri_enabled() {
     const char* e = std::getenv("SLATE_AMD_GEMM_TRI");  // read per launch: tests and sweeps toggle it
     return !(e && e[0] == '0');
@@ -100,9 +102,13 @@ static inline bool gemm_tri_enabled() {
 template <typename T>
 static i64 tri_blocks(const GemmArgs<T>& a, int BM, int BN) {
     const TriMask& k = a.mask;
-    if (!gemm_tri_enabled() || k.mode != 1 || k.p != 1 || k.q != 1 || BM != BN) return 0;
-    if (k.col_off - k.row_off - k.diag_off < 0) return 0;
+    if (!gemm_tri_enabled() || k.mode != 1 || BM != BN) return 0;
     const i64 gm = (a.m + BM - 1) / BM, gn = (a.n + BN - 1) / BN;
+    for (i64 bn = 1; bn < gn; ++bn) {
+        const i64 bm = std::min(bn - 1, gm - 1);
+        const i64 r0 = bm * BM, c0 = bn * BN;
+        if (!k.skip_block(r0, std::min(r0 + BM, a.m), c0, std::min(c0 + BN, a.n))) return 0;
+    }
     const i64 gsm = (gm + 7) / 8, gsn = (gn + 7) / 8;
     i64 sup = 0;
     for (i64 J = 0; J < std::min(gsm, gsn); ++J) sup += gsm - J;

@@ -104,6 +104,24 @@ def test_gemm_trimask_compact(m, n, roff, coff, doff):
     assert (C - exp).abs().max() < 1e-12
 
 
+@pytest.mark.parametrize("p,pr,q,pc,roff,coff", [
+    (2, 1, 4, 2, 0, 0), (2, 0, 4, 3, 256, 512), (1, 0, 2, 1, 0, 0), (2, 1, 1, 0, 0, 0), (2, 0, 2, 0, 512, 256)])
+def test_gemm_trimask_compact_blockcyclic(p, pr, q, pc, roff, coff):
+    # block-cyclic lower mask, 128 x 128 tiles: the compact launch where no
+    # tile above the tile diagonal is live (p <= q), full grid otherwise
+    nb, m, n = 512, 6400, 6144
+    A, B, C = cm(m, 32, torch.float64, 7), cm(n, 32, torch.float64, 8), cm(m, n, torch.float64, 9)
+    C0 = C.clone()
+    ops.gemm(1.0, A, B, 1.0, C, 'N', 'T', mask=(1, nb, p, pr, q, pc, roff, coff, 0))
+    full = C0 + A @ B.mT
+    lr = torch.arange(m, device="cuda") + roff
+    lc = torch.arange(n, device="cuda") + coff
+    gr = ((lr // nb) * p + pr) * nb + lr % nb
+    gc = ((lc // nb) * q + pc) * nb + lc % nb
+    exp = torch.where(gr[:, None] >= gc[None, :], full, C0)
+    assert (C - exp).abs().max() < 1e-12
+
+
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("uplo", ["L", "U"])
 def test_potrf_tile(dt, uplo):
