@@ -7,8 +7,12 @@
  * slate_amd_initialize() once (it is also called lazily), and
  * slate_amd_finalize() at exit.  Arrays are column-major with leading
  * dimension ld*; complex arrays are interleaved (re, im) pairs.  Every
- * routine returns LAPACK's info (0 = success; < 0: the call failed, see
- * slate_amd_last_error()).
+ * routine returns LAPACK's info: 0 = success, > 0 = numerical failure
+ * (e.g. the first non-positive pivot), -i = argument i was illegal.
+ * Failures of the runtime itself use two reserved codes far outside the
+ * argument range, SLATE_AMD_ERR_INIT (the runtime could not be started)
+ * and SLATE_AMD_ERR_INTERNAL (an exception inside the library); the message
+ * is then in slate_amd_last_error().
  *
  * Each routine also has a Fortran-callable alias with a trailing
  * underscore and all arguments by reference (e.g. slate_dpotrf_).
@@ -21,6 +25,9 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+
+#define SLATE_AMD_ERR_INIT (-1000001)
+#define SLATE_AMD_ERR_INTERNAL (-1000000)
 
 int slate_amd_initialize(void);
 void slate_amd_finalize(void);

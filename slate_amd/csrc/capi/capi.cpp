@@ -32,6 +32,10 @@ bool ensure() {
         PyErr_Print();
         g_err = "cannot import slate_amd.compat.capi_bridge (is slate_amd on PYTHONPATH?)";
         PyGILState_Release(st);
+        // the thread that initialised the interpreter still holds the GIL:
+        // release it on the failure path too, or a later call from another
+        // thread deadlocks in PyGILState_Ensure
+        if (g_owned) { PyEval_SaveThread(); g_owned = false; }
         return false;
     }
     g_call = PyObject_GetAttrString(mod, "call");
@@ -44,13 +48,13 @@ bool ensure() {
 // fmt: Py_BuildValue format of the arguments after the routine name
 template <typename... A>
 double invoke(const char* name, const char* fmt, A... args) {
-    if (!ensure()) return -1000;
+    if (!ensure()) return SLATE_AMD_ERR_INIT;
     PyGILState_STATE st = PyGILState_Ensure();
     std::string f = std::string("(s") + fmt + ")";
     PyObject* targs = Py_BuildValue(f.c_str(), name, args...);
     PyObject* r = targs ? PyObject_CallObject(g_call, targs) : nullptr;
     Py_XDECREF(targs);
-    double out = -1001;
+    double out = SLATE_AMD_ERR_INTERNAL;
     if (!r) {
         PyObject *t, *v, *tb;
         PyErr_Fetch(&t, &v, &tb);

@@ -19,7 +19,8 @@ inline dim3 grid2(i64 m, i64 n) {
     return dim3((unsigned)std::max<i64>(gx, 1), (unsigned)std::max<i64>(gy, 1));
 }
 __device__ inline bool in_uplo(char uplo, i64 i, i64 j) {
-    return uplo == 'L' ? i >= j : (uplo == 'U' ? i <= j : true);
+    // 'L' lower, 'U' upper (both incl. the diagonal), 'D' diagonal only, else all
+    return uplo == 'L' ? i >= j : (uplo == 'U' ? i <= j : (uplo == 'D' ? i == j : true));
 }
 }  // namespace
 

@@ -425,6 +425,7 @@ void geset(char uplo, i64 m, i64 n, T off, T diag, T* A, i64 lda) {
         for (i64 i = 0; i < m; ++i) {
             if (uplo == 'L' && i < j) continue;
             if (uplo == 'U' && i > j) continue;
+            if (uplo == 'D' && i != j) continue;
             A[i + j * lda] = (i == j) ? diag : off;
         }
 }
@@ -434,6 +435,7 @@ void gescale(char uplo, i64 m, i64 n, T s, T* A, i64 lda) {
         for (i64 i = 0; i < m; ++i) {
             if (uplo == 'L' && i < j) continue;
             if (uplo == 'U' && i > j) continue;
+            if (uplo == 'D' && i != j) continue;
             A[i + j * lda] *= s;
         }
 }
@@ -443,6 +445,7 @@ void geadd(char uplo, i64 m, i64 n, T alpha, const T* A, i64 lda, T beta, T* B, 
         for (i64 i = 0; i < m; ++i) {
             if (uplo == 'L' && i < j) continue;
             if (uplo == 'U' && i > j) continue;
+            if (uplo == 'D' && i != j) continue;
             B[i + j * ldb] = alpha * A[i + j * lda] + (beta == T(0) ? T(0) : beta * B[i + j * ldb]);
         }
 }
@@ -459,6 +462,7 @@ void gecopy(char uplo, char trans, i64 m, i64 n, const Ts* A, i64 lda, Td* B, i6
         for (i64 i = 0; i < m; ++i) {
             if (uplo == 'L' && i < j) continue;
             if (uplo == 'U' && i > j) continue;
+            if (uplo == 'D' && i != j) continue;
             Ts v = trans == 'N' ? A[i + j * lda] : A[j + i * lda];
             if (trans == 'C') v = conj_(v);
             B[i + j * ldb] = cvt<Ts, Td>(v);
@@ -474,6 +478,7 @@ void genorm(char norm, char uplo, char diag, bool herm, i64 m, i64 n, const T* A
         for (i64 i = 0; i < m; ++i) {
             if (uplo == 'L' && i < j) continue;
             if (uplo == 'U' && i > j) continue;
+            if (uplo == 'D' && i != j) continue;
             R v = (i == j && diag == 'U') ? R(1) : std::abs(A[i + j * lda]);
             int reps = (herm && i != j) ? 2 : 1;
             if (norm == 'M') { if (std::isnan(v) || v > acc || std::isnan(acc)) acc = std::isnan(acc) ? acc : v; }

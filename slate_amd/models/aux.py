@@ -234,22 +234,19 @@ def redistribute(A, B, opts=None):
         ops.gecopy(la.data, lbk.data)
         sB.mark_local_modified(sB.origin_slot)
         return B
-    # general path via element ranges of B's tiles
-    D = allgather_dense(A)
-    from_dense(B, D.to(sB.device if sB.origin_slot == DEV else "cpu"))
-    return B
+    # general path: piece-level batched point-to-point (parallel/redist.py);
+    # trapezoid targets receive only their stored triangle
+    from ..parallel.redist import redistribute_pieces
+    up = B.uplo() if getattr(B, "_kind", "general") != "general" else None
+    return redistribute_pieces(A, B, uplo=up)
 
 
 def copy_conj_transpose(A, B):
-    """B = A^H (A Hermitian-stored in one triangle; only B's triangle written)."""
-    D = allgather_dense(A)
-    # complete A from its stored triangle
-    if A.uploPhysical() == Uplo.Lower:
-        D = torch.tril(D)
-    elif A.uploPhysical() == Uplo.Upper:
-        D = torch.triu(D)
-    from_dense(B, D.transpose(0, 1).conj().contiguous())
-    return B
+    """B = A^H restricted to B's stored triangle (A's matching triangle is
+    read; every other element of B is left untouched)."""
+    from ..parallel.redist import redistribute_pieces
+    up = B.uplo() if B.uploPhysical() != Uplo.General else None
+    return redistribute_pieces(A.conj_transpose(), B, uplo=up)
 
 
 # ------------------------------------------------------------------ element-wise
@@ -300,6 +297,30 @@ def _diag_runs(blk, lb):
         runs.append((i, j, k))
         i += k
     return runs
+
+
+def set_diag(A, value, opts=None):
+    """A(i, i) = value for the stored diagonal (block-cyclic): one geset per
+    run of locally owned diagonal elements."""
+    s, slot, lb = _bc_pieces(A, opts)
+    if lb.mloc and lb.nloc:
+        for (i0, j0, k) in _diag_runs(lb.data, lb):
+            blk = lb.data[i0:i0 + k, j0:j0 + k]
+            ops.geset(0.0, value, blk, uplo='D')
+    s.mark_local_modified(slot)
+    return A
+
+
+def set_diag_imag_zero(A, opts=None):
+    """Drop the imaginary part of the stored diagonal (Hermitian operands:
+    LAPACK assumes it is zero)."""
+    s, slot, lb = _bc_pieces(A, opts)
+    if lb.mloc and lb.nloc and s.dtype.is_complex:
+        for (i0, j0, k) in _diag_runs(lb.data, lb):
+            d = torch.diagonal(lb.data[i0:i0 + k, j0:j0 + k])
+            d.imag.zero_()
+    s.mark_local_modified(slot)
+    return A
 
 
 def scale(numer, denom, A, opts=None):

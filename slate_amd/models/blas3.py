@@ -29,6 +29,7 @@ from ..core.storage import DEV, l2g
 from ..parallel.streams import StreamSet
 from ..parallel.tilecomm import exchange_tiles
 from ..utils.trace import trace_block
+from ._panels import assemble_cols, plan_col_gather, row_bcast
 from ._util import conj_trans, grid_of, target_slot, tiles_local_before
 
 
@@ -47,23 +48,77 @@ def _done(*mats):
         M.storage.mark_local_modified(M.storage.origin_slot)
 
 
-def _dense(X):
-    from .aux import allgather_dense
-    return allgather_dense(X)
+def _grid_params(X):
+    """(mb, nb, p, q, order) of X's block-cyclic grid, or a default grid."""
+    bc = X.storage.bc
+    if bc is not None:
+        return bc.mb, bc.nb, bc.p, bc.q, bc.order
+    from ..core import func
+    from ..core.enums import GridOrder
+    nb = max(1, X.storage.tileMb(0) if X.storage.mt else 1)
+    p, q = func.grid_shape(X.storage.comm.size)
+    return nb, nb, p, q, GridOrder.Col
 
 
-def _dense_store(X, D):
-    from .aux import from_dense
-    from_dense(X, D)
+def _fresh(like, m, n, slot, dtype=None, cls=None, uplo=None):
+    """A new allocated block-cyclic m x n matrix on ``like``'s grid."""
+    from ..core.matrix import HermitianMatrix, Matrix
+    mb, nb, p, q, order = _grid_params(like)
+    s = like.storage
+    dt = dtype or s.dtype
+    if cls is not None and uplo is not None:
+        from ..core.storage import MatrixStorage
+        from ..core import func
+        st = MatrixStorage(m, n, func.uniform_blocksize(m, mb), func.uniform_blocksize(n, nb),
+                           func.process_2d_grid(order, p, q), s.comm, dt, s.device)
+        M = cls(uplo, _storage=st)
+    else:
+        M = Matrix(m, n, nb=nb, mb=mb, p=p, q=q, comm=s.comm, dtype=dt, device=s.device, order=order)
+    M.insertLocalTiles(device=s.device if slot == DEV else -1)
+    return M
 
 
-def _full_herm(D, uplo, herm=True):
-    L = torch.tril(D) if uplo == Uplo.Lower else torch.triu(D)
-    Dg = torch.diagonal(L)
-    F = L + (L.transpose(0, 1).conj() if herm else L.transpose(0, 1)) - torch.diag(Dg)
-    if herm and D.dtype.is_complex:
-        F.diagonal().imag.zero_()
+def _copy_in(X, like, slot, uplo=None):
+    """Fresh block-cyclic copy of the logical matrix op(X) on like's grid."""
+    from ..parallel.redist import redistribute_pieces
+    F = _fresh(like, X.m(), X.n(), slot, X.storage.dtype)
+    redistribute_pieces(X, F, uplo=uplo)
     return F
+
+
+def _copy_out(F, X, uplo=None):
+    from ..parallel.redist import redistribute_pieces
+    redistribute_pieces(F, X, uplo=uplo)
+
+
+def _same_grid(X, C):
+    a, c = X.storage.bc, C.storage.bc
+    return a is not None and c is not None and bool(X.storage.local) and \
+        (a.p, a.q, a.order, a.mb, a.nb) == (c.p, c.q, c.order, c.mb, c.nb) and a.mb == a.nb
+
+
+def _rows_aligned(A, C):
+    """op(A) = A, same grid, A's rows start where C's rows start, A's
+    columns start on a tile boundary."""
+    if A.op() != Op.NoTrans or not _same_grid(A, C):
+        return False
+    rA, cA = A.global_offsets()
+    rC, _ = C.global_offsets()
+    nb = C.storage.bc.nb
+    return rA == rC and cA % nb == 0
+
+
+def _cols_aligned(B, C):
+    if B.op() != Op.NoTrans or not _same_grid(B, C):
+        return False
+    rB, cB = B.global_offsets()
+    _, cC = C.global_offsets()
+    return cB == cC and rB % C.storage.bc.nb == 0
+
+
+def _at_origin(C):
+    return C.storage.bc is not None and bool(C.storage.local) and C.global_offsets() == (0, 0) \
+        and C.op() == Op.NoTrans and C.storage.bc.mb == C.storage.bc.nb
 
 
 # ------------------------------------------------------------------- gemm
@@ -83,35 +138,89 @@ def gemm(alpha, A, B, beta, C, opts=None):
             ops.gemm(alpha, a, b, beta, c, ta, tb)
             _done(C)
             return C
-        return _gemm_summa(alpha, A, B, beta, C, opts)
+        return _gemm_dist(alpha, A, B, beta, C, opts)
 
 
-def _aligned(A, B, C):
-    """SUMMA fast path: same grid & tile size, NoTrans, tile-aligned views,
-    A's rows aligned with C's rows and B's columns with C's columns."""
-    sA, sB, sC = A.storage.bc, B.storage.bc, C.storage.bc
-    if None in (sA, sB, sC) or A.op() != Op.NoTrans or B.op() != Op.NoTrans:
-        return False
-    if not (A.storage.local and B.storage.local and C.storage.local):
-        return False
-    if (sA.p, sA.q, sA.order) != (sC.p, sC.q, sC.order) or (sB.p, sB.q, sB.order) != (sC.p, sC.q, sC.order):
-        return False
-    if len({sA.mb, sA.nb, sB.mb, sB.nb, sC.mb, sC.nb}) != 1:
-        return False
-    rA, cA = A.global_offsets()
-    rB, cB = B.global_offsets()
-    rC, cC = C.global_offsets()
-    nb = sC.nb
-    return rA == rC and cB == cC and all(x % nb == 0 for x in (cA, rB, rC, cC))
+def _gemm_method(B, opts):
+    """src/gemm.cc:11-24: stationary A when B has a single block column
+    (one process per GPU here, so the reference's multi-GPU exception does
+    not apply)."""
+    m = get_option(opts, Option.MethodGemm, MethodGemm.Auto)
+    if m in (MethodGemm.A, MethodGemm.C):
+        return m
+    return MethodGemm.A if B.nt() < 2 else MethodGemm.C
+
+
+def _gemm_dist(alpha, A, B, beta, C, opts):
+    """Distributed gemm on any distributions / ops: operands that are not
+    already aligned with C's grid are redistributed (one batched p2p
+    exchange each, parallel/redist.py) -- never gathered."""
+    slot = target_slot(C, opts)
+    work = C
+    if not (_rows_aligned(A, C) and _cols_aligned(B, C)) and not _at_origin(C):
+        work = _fresh(C, C.m(), C.n(), slot)
+        if beta != 0:
+            _copy_out(C, work)
+    Aw = A if _rows_aligned(A, work) else _copy_in(A, work, slot)
+    Bw = B if _cols_aligned(B, work) else _copy_in(B, work, slot)
+    if _gemm_method(Bw, opts) == MethodGemm.A:
+        _gemmA(alpha, Aw, Bw, beta, work, opts)
+    else:
+        _gemm_summa(alpha, Aw, Bw, beta, work, opts)
+    if work is not C:
+        _copy_out(work, C)
+    return C
+
+
+def _gemmA(alpha, A, B, beta, C, opts):
+    """Stationary-A gemm (src/gemmA.cc, listReduce of partial C tiles):
+    for each block column jb of C, B(:, jb) is delivered to the owners of
+    the matching columns of A, each rank multiplies its local A block, and
+    the partial products are reduced over the process row onto the owner of
+    C(:, jb).  A never moves -- the right choice when B/C are skinny."""
+    if A.global_offsets()[1] != 0 or B.global_offsets()[0] != 0:
+        slot = target_slot(C, opts)
+        A = A if A.global_offsets()[1] == 0 else _copy_in(A, C, slot)
+        B = B if B.global_offsets()[0] == 0 else _copy_in(B, C, slot)
+    s = C.storage
+    bc = s.bc
+    grid = grid_of(C)
+    slot = target_slot(C, opts)
+    la_ = A.local_block(slot)
+    lb_ = B.local_block(slot)
+    lc_ = C.local_block(slot)
+    dev = lc_.data.device
+    nb, p, q, pr, pc = bc.nb, bc.p, bc.q, bc.pr, bc.pc
+    kt = A.nt()
+    plan = plan_col_gather(B.storage.tileMb, 0, kt, nb, p, q, pc, dev)
+    _, cB0 = B.global_offsets()
+    for jb in range(C.nt()):
+        gj = cB0 // nb + jb
+        owner = gj % q
+        wb = C.tileNb(jb)
+        # B(:, jb) local rows -> every rank of this process row
+        lcb = tiles_local_before(gj, q, pc) * nb - lb_.col_off
+        src = lb_.data[:, lcb:lcb + wb] if pc == owner else None
+        Prow = row_bcast(grid, src, owner, lb_.mloc, wb, s.dtype, dev)
+        # rows of B(:, jb) matching my local columns of A
+        Bq = assemble_cols(plan, Prow, grid, p, wb, s.dtype, dev)
+        P = ops.colmajor_zeros(la_.mloc, wb, s.dtype, dev)
+        if la_.mloc and la_.nloc:
+            ops.gemm(alpha, la_.data, Bq, 0.0, P)
+        if q > 1 and la_.mloc:
+            grid.row_comm.reduce(P, owner)
+        if pc == owner and lc_.mloc:
+            lcc = tiles_local_before(gj, q, pc) * nb - lc_.col_off
+            if beta == 0:
+                ops.gecopy(P, lc_.data[:, lcc:lcc + wb])     # C is not read when beta = 0
+            else:
+                ops.geadd(1.0, P, beta, lc_.data[:, lcc:lcc + wb])
+    _done(C)
+    return C
 
 
 def _gemm_summa(alpha, A, B, beta, C, opts):
-    if not _aligned(A, B, C):
-        # general distributions / transposed operands: gather-compute-scatter
-        Da, Db, Dc = _dense(A), _dense(B), _dense(C)
-        ops.gemm(alpha, ops.as_colmajor(Da), ops.as_colmajor(Db), beta, Dc_ := ops.as_colmajor(Dc.clone()))
-        _dense_store(C, Dc_)
-        return C
+    """SUMMA, stationary C (src/gemmC.cc:39-202) on aligned operands."""
     s = C.storage
     bc = s.bc
     grid = grid_of(C)
@@ -184,6 +293,99 @@ def multiply(alpha, A, B, beta, C, opts=None):
 
 
 # ---------------------------------------------------------------- herk etc.
+def _diag_aligned(C):
+    """C is a whole-tile diagonal block of a block-cyclic square storage."""
+    s = C.storage
+    return s.bc is not None and bool(s.local) and C.op() == Op.NoTrans and C.ioffset == C.joffset \
+        and C.row0_offset == 0 and C.col0_offset == 0 and C.last_mb is None and C.last_nb is None \
+        and s.bc.mb == s.bc.nb and s.m == s.n
+
+
+def _herm_work(C, slot):
+    """(work matrix, needs copy-back): a diagonal-aligned Hermitian work
+    view for the rank-k kernels."""
+    if _diag_aligned(C):
+        return C, False
+    from ..core.matrix import HermitianMatrix
+    W = _fresh(C, C.n(), C.n(), slot, cls=HermitianMatrix, uplo=C.uplo())
+    _copy_out(C, W, uplo=C.uplo())
+    return W, True
+
+
+def _rank_k_dist(alpha, pairs, beta, C, opts, sym):
+    """C = beta C + sum over (alpha_i, X_i, Y_i) of alpha_i X_i Y_i^H (^T if
+    sym), only C's stored triangle.  Per block column k of the X_i:
+    Prow(X_i) along the process row, Lcol(Y_i) down the process column
+    (potrf-style panel assembly, _panels.py), one masked MFMA GEMM each --
+    SLATE internal_herk.cc:350-535 / internal_her2k.cc, without the
+    per-tile batches."""
+    slot = target_slot(C, opts)
+    W, back = _herm_work(C, slot)
+    s = W.storage
+    bc = s.bc
+    grid = grid_of(W)
+    lbC = W.local_block(slot)
+    dev = lbC.data.device
+    nb, p, q, pr, pc = bc.nb, bc.p, bc.q, bc.pr, bc.pc
+    ct = 'T' if sym else conj_trans(s.dtype)
+    lower = W.uplo() == Uplo.Lower
+    mask = lbC.mask(1 if lower else 2)
+    g0, nt = W.ioffset, W.mt()
+    ops_ = []
+    for (al, X, Y) in pairs:
+        Xw = X if _rows_aligned(X, W) else _copy_in(X, W, slot)
+        Yw = Xw if Y is X else (Y if _rows_aligned(Y, W) else _copy_in(Y, W, slot))
+        ops_.append((al, Xw, Yw))
+    kt = ops_[0][1].nt() if ops_ else 0
+    if kt == 0 or all(a == 0 for a, _, _ in ops_):
+        if beta != 1:
+            from .aux import scale
+            scale(beta, 1.0, W)
+    else:
+        plan = plan_col_gather(s.tileMb, g0, g0 + nt, nb, p, q, pc, dev)
+        first = True
+        for kk in range(kt):
+            panels = {}
+            for (al, Xw, Yw) in ops_:
+                for M in (Xw, Yw):
+                    if id(M) in panels:
+                        continue
+                    lm = M.local_block(slot)
+                    gk = M.global_offsets()[1] // nb + kk
+                    kb = M.tileNb(kk)
+                    lc = tiles_local_before(gk, q, pc) * nb - lm.col_off
+                    src = lm.data[:, lc:lc + kb] if gk % q == pc else None
+                    Prow = row_bcast(grid, src, gk % q, lm.mloc, kb, s.dtype, dev)
+                    Lcol = assemble_cols(plan, Prow, grid, p, kb, s.dtype, dev)
+                    panels[id(M)] = (Prow, Lcol)
+            for (al, Xw, Yw) in ops_:
+                Prow, _ = panels[id(Xw)]
+                _, Lcol = panels[id(Yw)]
+                if lbC.mloc and lbC.nloc:
+                    ops.gemm(al, Prow, Lcol, beta if first else 1.0, lbC.data, 'N', ct, mask)
+                first = False
+    _done(W)
+    if back:
+        _copy_out(W, C, uplo=C.uplo())
+    return C
+
+
+def _real_diag(C, sym):
+    """zherk/zher2k semantics: the diagonal of the Hermitian result is real."""
+    if not sym and C.storage.dtype.is_complex and C.storage.bc is not None:
+        from .aux import set_diag_imag_zero
+        set_diag_imag_zero(C)
+    return C
+
+
+def _herm_base(C):
+    """herk/her2k act on the stored Hermitian matrix: a (conj-)transposed
+    Hermitian view is the same logical matrix."""
+    if C.op() == Op.NoTrans:
+        return C
+    return C.conj_transpose() if C.op() == Op.ConjTrans else C.transpose()
+
+
 def herk(alpha, A, beta, C, opts=None, _sym=False):
     """C = alpha op(A) op(A)^H + beta C, C Hermitian (stored triangle only)."""
     with trace_block("syrk" if _sym else "herk"):
@@ -196,15 +398,9 @@ def herk(alpha, A, beta, C, opts=None, _sym=False):
             else:
                 (ops.syrk if _sym else ops.herk)(up, 'C' if not _sym else 'T', alpha, a, beta, c)
             _done(C)
-            return C
-        Da = _dense(A)
-        Dc = _dense(C)
-        t = Da @ (Da.transpose(0, 1) if _sym else Da.transpose(0, 1).conj())
-        R = alpha * t + beta * Dc
-        tri = torch.tril if C.uploPhysical() == Uplo.Lower else torch.triu
-        R = tri(R) + (Dc - tri(Dc))
-        _dense_store(C, R)
-        return C
+            return _real_diag(C, _sym)
+        _rank_k_dist(alpha, [(alpha, A, A)], beta, _herm_base(C), opts, _sym)
+        return _real_diag(C, _sym)
 
 
 def syrk(alpha, A, beta, C, opts=None):
@@ -222,19 +418,34 @@ def her2k(alpha, A, B, beta, C, opts=None, _sym=False):
             fn = ops.syr2k if _sym else ops.her2k
             fn(up, 'N' if ta == 'N' else ('T' if _sym else 'C'), alpha, a, b, beta, c)
             _done(C)
-            return C
-        Da, Db, Dc = _dense(A), _dense(B), _dense(C)
-        H = (lambda X: X.transpose(0, 1)) if _sym else (lambda X: X.transpose(0, 1).conj())
+            return _real_diag(C, _sym)
         a2 = alpha if _sym else complex(alpha).conjugate()
-        R = alpha * (Da @ H(Db)) + a2 * (Db @ H(Da)) + beta * Dc
-        tri = torch.tril if C.uploPhysical() == Uplo.Lower else torch.triu
-        R = tri(R) + (Dc - tri(Dc))
-        _dense_store(C, R)
-        return C
+        if not C.storage.dtype.is_complex:
+            a2 = float(complex(a2).real)
+        _rank_k_dist(alpha, [(alpha, A, B), (a2, B, A)], beta, _herm_base(C), opts, _sym)
+        return _real_diag(C, _sym)
 
 
 def syr2k(alpha, A, B, beta, C, opts=None):
     return her2k(alpha, A, B, beta, C, opts, _sym=True)
+
+
+def _full_from_stored(A, slot, herm=True):
+    """General block-cyclic copy of a Hermitian/symmetric matrix with both
+    triangles filled: the mirrored triangle by one transposing
+    redistribution, the stored one (incl. the diagonal) on top."""
+    from ..parallel.redist import redistribute_pieces
+    n = A.n()
+    F = _fresh(A, n, n, slot)
+    u = A.uplo()
+    other = Uplo.Upper if u == Uplo.Lower else Uplo.Lower
+    H = A.conj_transpose() if herm else A.transpose()
+    redistribute_pieces(H, F, uplo=other)
+    redistribute_pieces(A, F, uplo=u)
+    if herm and F.storage.dtype.is_complex:
+        from .aux import set_diag_imag_zero
+        set_diag_imag_zero(F)
+    return F
 
 
 def hemm(side, alpha, A, B, beta, C, opts=None, _sym=False):
@@ -261,11 +472,13 @@ def hemm(side, alpha, A, B, beta, C, opts=None, _sym=False):
                 ops.gemm(alpha, b, F, beta, c, tb, 'N')
             _done(C)
             return C
-        Fa = _full_herm(_dense(A), A.uploPhysical(), herm=not _sym)
-        Db, Dc = _dense(B), _dense(C)
-        R = alpha * (Fa @ Db if side == Side.Left else Db @ Fa) + beta * Dc
-        _dense_store(C, R)
-        return C
+        # hemmC with both triangles materialised once (SLATE broadcasts A
+        # and A^H tiles per step and runs the diagonal tiles on the host,
+        # src/hemmC.cc:147-429): one transposing redistribution, then SUMMA
+        F = _full_from_stored(A, target_slot(C, opts), herm=not _sym)
+        if side == Side.Left:
+            return gemm(alpha, F, B, beta, C, opts)
+        return gemm(alpha, B, F, beta, C, opts)
 
 
 def symm(side, alpha, A, B, beta, C, opts=None):
@@ -279,6 +492,19 @@ def _tri_args(A):
     return uplo, diag
 
 
+def _tri_as_general(A, slot):
+    """op(A) of a triangular view as a general block-cyclic matrix with
+    explicit zeros outside the triangle (unit diagonal materialised)."""
+    from ..parallel.redist import redistribute_pieces
+    n = A.n()
+    F = _fresh(A, n, n, slot)           # zero-initialised
+    redistribute_pieces(A, F, uplo=A.uplo())
+    if A.diag() == Diag.Unit:
+        from .aux import set_diag
+        set_diag(F, 1.0)
+    return F
+
+
 def trmm(side, alpha, A, B, opts=None):
     """B = alpha op(A) B (Left) or alpha B op(A) (Right), A triangular."""
     side = Side.from_string(side) if not isinstance(side, Side) else side
@@ -290,17 +516,16 @@ def trmm(side, alpha, A, B, opts=None):
             ops.trmm(side.value, uplo, ta, diag, alpha, a, b)
             _done(B)
             return B
-        Da = _dense(A)
-        uplo, diag = A.uploPhysical(), A.diag()
-        # op(A) as a dense logical matrix: _dense already applies op;
-        # the stored triangle of op(A) is the logical triangle
-        tri = torch.tril if A.uploLogical() == Uplo.Lower else torch.triu
-        T = tri(Da)
-        if diag == Diag.Unit:
-            T = T - torch.diag(torch.diagonal(T)) + torch.eye(T.shape[0], dtype=T.dtype, device=T.device)
-        Db = _dense(B)
-        R = alpha * (T @ Db if side == Side.Left else Db @ T)
-        _dense_store(B, R)
+        # distributed (work::trmm analogue): the triangle as a general
+        # operand with zeros, one SUMMA product into a work matrix
+        slot = target_slot(B, opts)
+        T = _tri_as_general(A, slot)
+        X = _fresh(B, B.m(), B.n(), slot)
+        if side == Side.Left:
+            gemm(alpha, T, B, 0.0, X, opts)
+        else:
+            gemm(alpha, B, T, 0.0, X, opts)
+        _copy_out(X, B)
         return B
 
 
@@ -315,39 +540,62 @@ def trsm(side, alpha, A, B, opts=None):
             ops.trsm(side.value, uplo, ta, diag, alpha, a, b)
             _done(B)
             return B
-        if side == Side.Left and B.op() == Op.NoTrans and A.storage.bc is not None and B.storage.bc is not None:
-            return _trsm_left_dist(alpha, A, B, opts)
-        # Right side (or transposed B): X op(A) = B  <=>  op(A)^H X^H = B^H
-        Da = _dense(A)
-        tri = torch.tril if A.uploLogical() == Uplo.Lower else torch.triu
-        T = tri(Da)
-        if A.diag() == Diag.Unit:
-            T = T - torch.diag(torch.diagonal(T)) + torch.eye(T.shape[0], dtype=T.dtype, device=T.device)
-        Db = _dense(B)
-        Tm = ops.as_colmajor(T.clone())
-        X = ops.as_colmajor((alpha * Db).clone())
-        ops.trsm(side.value, 'L' if A.uploLogical() == Uplo.Lower else 'U', 'N', 'N', 1.0, Tm, X)
-        _dense_store(B, X)
-        return B
+        slot = target_slot(B, opts)
+        if side == Side.Right:
+            # X op(A) = alpha B  <=>  op(A)^H X^H = conj(alpha) B^H  (^T when
+            # op(A) = A^T): one transposing redistribution each way
+            use_h = A.op() != Op.Trans
+            tr = (lambda X: X.conj_transpose()) if use_h else (lambda X: X.transpose())
+            Bw = B if B.op() == Op.NoTrans else _copy_in(B, B, slot)
+            Bt = _copy_in(tr(Bw), Bw, slot)
+            a2 = complex(alpha).conjugate() if (use_h and B.storage.dtype.is_complex) else alpha
+            _trsm_left(a2, tr(A), Bt, slot)
+            _copy_out(tr(Bt), B)
+            return B
+        if B.op() != Op.NoTrans or B.storage.bc is None or not B.storage.local \
+                or B.global_offsets()[0] % B.storage.bc.nb:
+            Bw = _copy_in(B, B, slot)
+            _trsm_left(alpha, A, Bw, slot)
+            _copy_out(Bw, B)
+            return B
+        return _trsm_left(alpha, A, B, slot)
 
 
-def _trsm_left_dist(alpha, A, B, opts):
-    """Distributed Left trsm, any uplo/op of A (work::trsm analogue):
-    per tile row k: diag tile -> owners of B(k,:), local solve, X(k,:) down
-    each process column, A(:,k) panel tiles delivered to the owners of the
-    B rows they update (batched p2p), one local GEMM."""
+def _trsm_left(alpha, A, B, slot):
+    """Left solve on a block-cyclic NoTrans B whose rows start on a tile
+    boundary; A is redistributed onto B's grid when its tiles do not match
+    B's row tiles (stored triangle only)."""
+    nb = B.storage.bc.nb
+    sA = A.storage
+    ok = sA.bc is not None and sA.bc.mb == nb and sA.bc.nb == nb and \
+        all(x % nb == 0 for x in A.global_offsets()) and A.last_mb is None and A.last_nb is None
+    if not ok:
+        from ..core.matrix import TriangularMatrix
+        F = _fresh(B, A.m(), A.n(), slot)
+        from ..parallel.redist import redistribute_pieces
+        redistribute_pieces(A, F, uplo=A.uplo())
+        A = TriangularMatrix(A.uplo(), F, diag=A.diag())
+    return _trsm_left_dist(alpha, A, B, slot)
+
+
+def _trsm_left_dist(alpha, A, B, slot):
+    """Distributed Left trsm, any uplo/op of A (work::trsm analogue,
+    src/work/work_trsm.cc:102-265): per tile row k the diagonal tile goes to
+    the owners of B(k,:), they solve, X(k,:) goes down each process column,
+    the panel tiles A(:,k) are delivered (one batched p2p exchange) to the
+    owners of the B rows they update, packed in local-row order, and ONE
+    GEMM updates all of this rank's remaining rows."""
     sB = B.storage
     bcB = sB.bc
     comm = sB.comm
     grid = grid_of(B)
-    slot = target_slot(B, opts)
     lbB = B.local_block(slot)
     dev = lbB.data.device
     nb, p, q, pr, pc = bcB.nb, bcB.p, bcB.q, bcB.pr, bcB.pc
-    uplo_l = A.uploLogical()
-    lower = uplo_l == Uplo.Lower
+    lower = A.uploLogical() == Uplo.Lower
     diag = A.diag().value
     opA = A.op()
+    upl = A.uploPhysical().value if hasattr(A.uploPhysical(), "value") else 'L'
     mt = B.mt()
     rB0, _ = B.global_offsets()
     if rB0 % nb:
@@ -356,58 +604,54 @@ def _trsm_left_dist(alpha, A, B, opts):
     if alpha != 1 and lbB.mloc and lbB.nloc:
         ops.gescale(alpha, lbB.data)
     order = range(mt) if lower else range(mt - 1, -1, -1)
+    sA = A.storage
 
     def stored_key(i, k):
-        # view tile (i,k) of op(A) -> stored tile (global indices)
-        gi, gj = A._global_ij(i, k)
-        return (gi, gj)
+        return A._global_ij(i, k)
 
     def owner(key):
-        return A.storage.tileRank(key)
+        return sA.tileRank(key)
 
     def get_tile(key):
-        sA = A.storage
         return sA.tile_data(key[0], key[1], sA.origin_slot)
 
     def shape(key):
-        sA = A.storage
         return sA.tileMb(key[0]), sA.tileNb(key[1])
 
+    procrow_ranks = {}
+    for r in range(comm.size):
+        procrow_ranks.setdefault(grid.coords(r)[0], []).append(r)
     for k in order:
         gk = gb0 + k
         kb = B.tileMb(k)
-        # rows of B updated by step k
-        rows = [i for i in (range(k + 1, mt) if lower else range(0, k))]
-        # who needs what: diag tile -> process row of B(k,:); panel tile (i,k) -> process row of B(i,:)
+        rows = list(range(k + 1, mt)) if lower else list(range(0, k))
         needs = {}
-        for r in range(comm.size):
-            rpr, rpc = grid.coords(r)
-            ks = []
-            if (gk % p) == rpr:
-                ks.append(stored_key(k, k))
-            ks += [stored_key(i, k) for i in rows if ((gb0 + i) % p) == rpr]
-            needs[r] = ks
+        for rp in range(p):
+            ks = [stored_key(k, k)] if (gk % p) == rp else []
+            ks += [stored_key(i, k) for i in rows if ((gb0 + i) % p) == rp]
+            for r in procrow_ranks.get(rp, []):
+                needs[r] = ks
         got = exchange_tiles(comm, needs, owner, get_tile, shape, sB.dtype, dev)
-        # local solve on B(k,:) local columns
         Xk = ops.colmajor_empty(kb, lbB.nloc, sB.dtype, dev)
         if (gk % p) == pr and lbB.nloc:
             lr = tiles_local_before(gk, p, pr) * nb - lbB.row_off
             Bk = lbB.data[lr:lr + kb, :]
-            Dk = got[stored_key(k, k)]
-            ops.trsm('L', A.uploPhysical().value[0] if hasattr(A.uploPhysical(), "value") else 'L',
-                     opA.value, diag, 1.0, Dk, Bk)
+            ops.trsm('L', upl, opA.value, diag, 1.0, got[stored_key(k, k)], Bk)
             Xk.copy_(Bk)
-        if lbB.nloc:
-            grid.col_comm.bcast(Xk, gk % p) if p > 1 else None
-        # panel for my local rows that are updated
+        if lbB.nloc and p > 1:
+            grid.col_comm.bcast(Xk, gk % p)
         my_rows = [i for i in rows if ((gb0 + i) % p) == pr]
         if my_rows and lbB.nloc:
-            # local rows of those tiles form contiguous groups; do one GEMM per tile row
+            # my updated rows are one contiguous local range of B
+            lr0 = tiles_local_before(gb0 + my_rows[0], p, pr) * nb - lbB.row_off
+            tot = sum(B.tileMb(i) for i in my_rows)
+            Lm = ops.colmajor_empty(tot, kb, sB.dtype, dev)
+            off = 0
             for i in my_rows:
-                t = got[stored_key(i, k)]
-                lr = tiles_local_before(gb0 + i, p, pr) * nb - lbB.row_off
                 mi = B.tileMb(i)
-                ops.gemm(-1.0, t, Xk, 1.0, lbB.data[lr:lr + mi, :], opA.value, 'N')
+                ops.gecopy(got[stored_key(i, k)], Lm[off:off + mi], trans=opA.value)
+                off += mi
+            ops.gemm(-1.0, Lm, Xk, 1.0, lbB.data[lr0:lr0 + tot, :])
     _done(B)
     return B
 

@@ -46,11 +46,27 @@ def _like(A, dtype=None, cls=Matrix, **kw):
 
 
 def _converged(R, X, anorm, n):
-    """||R||_inf <= ||X||_inf * ||A||_inf * eps * sqrt(n) (iterRefConverged)."""
+    """Column-wise test of iterRefConverged (src/internal/internal_util.hh:121-136):
+    max|R_j| <= max|X_j| * ||A||_inf * eps * sqrt(n) for EVERY right-hand side j."""
+    from .aux import colNorms
     eps = torch.finfo(torch.float64).eps
-    rn = float(norm(Norm.Max, R))
-    xn = float(norm(Norm.Max, X))
-    return rn <= xn * anorm * eps * math.sqrt(n)
+    cte = anorm * eps * math.sqrt(n)
+    rn = colNorms(Norm.Max, R)
+    xn = colNorms(Norm.Max, X)
+    if torch.isnan(rn).any() or torch.isnan(xn).any():
+        return False
+    return bool((rn <= xn * cte).all())
+
+
+def _fallback(solver, args, B, X, opts, info_lo):
+    """Low-precision factorization failed (info_lo > 0): with
+    Option.UseFallbackSolver (default) solve in full precision into X and
+    report iter = -3 like SLATE; otherwise return the low-precision info."""
+    if not get_option(opts, Option.UseFallbackSolver, True):
+        return info_lo, -3
+    copy(B, X)
+    info = solver(*args, X, opts)
+    return info, -3
 
 
 def _refine(A, B, X, solve_lo, opts, anorm):
@@ -84,7 +100,9 @@ def gesv_mixed(A, pivots, B, X, opts=None):
         copy(A, Alo)
         info = getrf(Alo, pivots, opts)
         if info:
-            return info, 0
+            # the fp32 factor is singular although A may not be: iter = -3 and
+            # refactor in full precision (src/gesv_mixed.cc:185-187, 256-277)
+            return _fallback(gesv, (A, pivots), B, X, opts, info)
         anorm = float(norm(Norm.Inf, A))
 
         def solve_lo(R):
@@ -112,7 +130,7 @@ def posv_mixed(A, B, X, opts=None):
         copy(A, Alo)
         info = potrf(Alo, opts)
         if info:
-            return info, 0
+            return _fallback(posv, (A,), B, X, opts, info)
         anorm = float(norm(Norm.Inf, A))
 
         def solve_lo(R):
@@ -211,7 +229,7 @@ def gesv_mixed_gmres(A, pivots, B, X, opts=None):
         copy(A, Alo)
         info = getrf(Alo, pivots, opts)
         if info:
-            return info, 0
+            return _fallback(gesv, (A, pivots), B, X, opts, info)
         anorm = float(norm(Norm.Inf, A))
 
         def precond(v):
@@ -227,14 +245,14 @@ def gesv_mixed_gmres(A, pivots, B, X, opts=None):
 
 
 def posv_mixed_gmres(A, B, X, opts=None):
-    from .chol import potrf, potrs
+    from .chol import potrf, potrs, posv
     with trace_block("posv_mixed_gmres"):
         lo = _lo_dtype(A.storage.dtype)
         Alo = _like(A, lo, HermitianMatrix)
         copy(A, Alo)
         info = potrf(Alo, opts)
         if info:
-            return info, 0
+            return _fallback(posv, (A,), B, X, opts, info)
         anorm = float(norm(Norm.Inf, A))
 
         def precond(v):
