@@ -817,22 +817,45 @@ class Pivots:
     SLATE-style Pivot records of panel k."""
 
     def __init__(self, nb=256):
-        self.ipiv = torch.zeros(0, dtype=torch.int64)
+        self._host = torch.zeros(0, dtype=torch.int64)
         self.nb = nb
         self._dev = None
 
     def set(self, ipiv: torch.Tensor, nb):
-        self.ipiv = ipiv.to("cpu", torch.int64)
+        """Store the pivots where they were produced (a factorization leaves
+        them on the GPU: no host copy until someone reads ``ipiv``)."""
+        ipiv = ipiv.to(torch.int64)
         self.nb = nb
-        self._dev = None
+        if ipiv.is_cuda:
+            self._dev, self._host = ipiv, None
+        else:
+            self._dev, self._host = None, ipiv
+
+    @property
+    def ipiv(self) -> torch.Tensor:
+        if self._host is None:
+            self._host = self._dev.cpu()
+        return self._host
+
+    @ipiv.setter
+    def ipiv(self, v):
+        self.set(torch.as_tensor(v, dtype=torch.int64), self.nb)
 
     def device(self, dev):
-        if self._dev is None or self._dev.device != torch.device(dev):
-            self._dev = self.ipiv.to(dev)
+        dev = torch.device(dev)
+        if self._dev is None or self._dev.device != dev:
+            src = self._dev if self._dev is not None else self._host
+            self._dev = src.to(dev)
         return self._dev
 
     def __len__(self):
-        return -(-len(self.ipiv) // self.nb) if len(self.ipiv) else 0
+        n = self.size
+        return -(-n // self.nb) if n else 0
+
+    @property
+    def size(self) -> int:
+        """Number of pivots (no host copy)."""
+        return (self._dev if self._host is None else self._host).numel()
 
     def __getitem__(self, k):
         seg = self.ipiv[k * self.nb:(k + 1) * self.nb].tolist()

@@ -135,7 +135,8 @@ struct SwapPlan {                // folded permutation of one swap sequence
 // >= k2 are emitted by the LAST swap targeting them.  (The former
 // single-thread hash-map fold cost 46-256 us per call.)
 __global__ void __launch_bounds__(MAXSW)
-laswp_setup_kernel(i64 k1, i64 k2, const i64* __restrict__ ipiv, i64 ioff, int incx, SwapPlan* plan) {
+laswp_setup_kernel(i64 k1, i64 k2, const i64* __restrict__ ipiv, i64 ioff, int incx, SwapPlan* plan,
+                   bool fixed_slots) {
     __shared__ int pv[MAXSW];                // relative pivot rows (relative to k1)
     __shared__ int prv[MAXSW];               // prv[t]: last swap t' < t that targets row t (-1: none)
     __shared__ int s_cnt;
@@ -175,19 +176,24 @@ laswp_setup_kernel(i64 k1, i64 k2, const i64* __restrict__ ipiv, i64 ioff, int i
         dst[q] = k1 + q;
         srcv[q] = k1 + src;
         // rows beyond the sequence: emitted by the last swap that targets them
-        if (r >= ns) {
-            bool last = true;
-            for (int x = q + 1; x < ns; ++x)
-                if (pv[x] == r) { last = false; break; }
-            if (last) {
-                const int slot = atomicAdd(&s_cnt, 1);
-                dst[slot] = k1 + r;
-                srcv[slot] = k1 + chain(q);
-            }
+        bool emit = r >= ns;
+        for (int x = q + 1; emit && x < ns; ++x)
+            if (pv[x] == r) emit = false;
+        // fixed_slots: the emitting swap's own slot ns + q (-1 when it emits
+        // nothing), so every rank that folds the same sequence numbers the
+        // rows identically (the distributed exchange sums slot-wise);
+        // otherwise compacted in arrival order (local laswp)
+        if (emit) {
+            const int slot = fixed_slots ? ns + q : atomicAdd(&s_cnt, 1);
+            dst[slot] = k1 + r;
+            srcv[slot] = k1 + chain(q);
+        } else if (fixed_slots) {
+            dst[ns + q] = -1;
+            srcv[ns + q] = -1;
         }
     }
     __syncthreads();
-    if (q == 0) plan->nt = s_cnt;
+    if (q == 0) plan->nt = fixed_slots ? 2 * ns : s_cnt;
 }
 
 template <typename T>
@@ -276,7 +282,7 @@ void laswp_off(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, i64 ioff, 
         return;
     }
     SwapPlan* plan = static_cast<SwapPlan*>(workspace(s, sizeof(SwapPlan), WS_L));
-    hipLaunchKernelGGL(laswp_setup_kernel, dim3(1), dim3(MAXSW), 0, s, k1, k2, ipiv, ioff, incx, plan);
+    hipLaunchKernelGGL(laswp_setup_kernel, dim3(1), dim3(MAXSW), 0, s, k1, k2, ipiv, ioff, incx, plan, false);
     const size_t per_col = (size_t)2 * (k2 - k1) * sizeof(T);
     int cch = (int)std::max<size_t>(1, std::min<size_t>(32, (64 * 1024) / per_col));
     size_t shmem = per_col * cch;
@@ -287,6 +293,112 @@ void laswp_off(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, i64 ioff, 
 template <typename T>
 void laswp(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, int incx, hipStream_t s) {
     laswp_off<T>(n, A, lda, k1, k2, ipiv, 0, s, incx);
+}
+
+// ---------------------------------------------------------------------------
+// Distributed row interchange for LU on p > 1 process rows (no host round
+// trip).  The panel's swap sequence is folded ONCE into a device-resident
+// plan (SwapPlan layout with FIXED slots: window row q in slot q, the row a
+// swap q moves below the window in slot ns + q, -1 when none -- identical on
+// every rank, which the slot-wise all-reduce below relies on); every rank of
+// a process column then
+//   xchg_gather : packs the touched rows it OWNS (block-cyclic row owner)
+//                 into X (S x ncols, S = 2 kb slots), zeros elsewhere,
+//   <all-reduce of X over the column communicator: x + 0 is exact>,
+//   xchg_scatter: writes the rows it owns at their new positions.
+// The window slots [0, kb) of the reduced X are the new tile row k on every
+// rank of the column (the U row the trailing update needs anyway).
+void swap_plan(i64 k1, i64 k2, const i64* ipiv, i64 ioff, int incx, void* plan, hipStream_t s) {
+    if (k2 - k1 > MAXSW) throw std::invalid_argument("swap_plan: at most 512 swaps per plan");
+    HIP_CHECK(hipMemsetAsync(plan, 0, sizeof(SwapPlan), s));
+    if (k2 <= k1) return;
+    hipLaunchKernelGGL(laswp_setup_kernel, dim3(1), dim3(MAXSW), 0, s, k1, k2, ipiv, ioff, incx,
+                       static_cast<SwapPlan*>(plan), true);
+    HIP_LAUNCH_CHECK();
+}
+size_t swap_plan_bytes() { return sizeof(SwapPlan); }
+
+__device__ inline i64 bc_local_row(i64 g, i64 nb, int p, int pr) {
+    // local row of global row g on process row pr, -1 if another row owns it
+    const i64 tile = g / nb;
+    return (int)(tile % p) == pr ? (tile / p) * nb + g % nb : -1;
+}
+
+template <typename T>
+__global__ void xchg_gather_kernel(const SwapPlan* __restrict__ plan, i64 S, i64 n, const T* A, i64 lda,
+                                   T* X, i64 ldx, i64 nb, int p, int pr) {
+    const i64 t = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (t >= S) return;
+    const i64 src = t < plan->nt ? plan->tsrc[t] : -1;
+    const i64 lr = src >= 0 ? bc_local_row(src, nb, p, pr) : -1;
+    for (i64 j = blockIdx.y; j < n; j += gridDim.y)
+        X[t + j * ldx] = lr >= 0 ? A[lr + j * lda] : s_zero(T());
+}
+
+template <typename T>
+__global__ void xchg_scatter_kernel(const SwapPlan* __restrict__ plan, i64 S, i64 n, const T* X, i64 ldx,
+                                    T* A, i64 lda, i64 nb, int p, int pr) {
+    const i64 t = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (t >= S || t >= plan->nt || plan->trow[t] < 0) return;
+    const i64 lr = bc_local_row(plan->trow[t], nb, p, pr);
+    if (lr < 0) return;
+    for (i64 j = blockIdx.y; j < n; j += gridDim.y) A[lr + j * lda] = X[t + j * ldx];
+}
+
+template <typename T>
+void xchg_gather(const void* plan, i64 S, i64 n, const T* A, i64 lda, T* X, i64 ldx, i64 nb, int p, int pr,
+                 hipStream_t s) {
+    if (S <= 0 || n <= 0) return;
+    hipLaunchKernelGGL(xchg_gather_kernel<T>, grid2(S, n), dim3(256), 0, s, static_cast<const SwapPlan*>(plan),
+                       S, n, A, lda, X, ldx, nb, p, pr);
+    HIP_LAUNCH_CHECK();
+}
+template <typename T>
+void xchg_scatter(const void* plan, i64 S, i64 n, const T* X, i64 ldx, T* A, i64 lda, i64 nb, int p, int pr,
+                  hipStream_t s) {
+    if (S <= 0 || n <= 0) return;
+    hipLaunchKernelGGL(xchg_scatter_kernel<T>, grid2(S, n), dim3(256), 0, s, static_cast<const SwapPlan*>(plan),
+                       S, n, X, ldx, A, lda, nb, p, pr);
+    HIP_LAUNCH_CHECK();
+}
+
+// Tournament pivoting (CALU) picks the kb pivot rows of a panel as a SET in
+// order (sel[i] = global row that must end at row r0 + i).  LAPACK/SLATE
+// pivots are a swap SEQUENCE; convert: swap i exchanges row r0+i with the
+// current position of sel[i].  Only window rows are ever displaced (an
+// unselected outside row is never touched), so the state is three kb-long
+// LDS arrays and each step is O(1): one thread walks the sequence after a
+// parallel set-up.
+__global__ void __launch_bounds__(MAXSW)
+sel_to_ipiv_kernel(const i64* __restrict__ sel, int kb, i64 r0, i64* __restrict__ ipiv) {
+    __shared__ i64 at_win[MAXSW];     // original row currently at window position j
+    __shared__ i64 where[MAXSW];      // current position of original row sel[i]
+    __shared__ int idx_of_win[MAXSW]; // i with sel[i] == r0 + j (-1: not selected)
+    const int q = threadIdx.x;
+    if (q < kb) { at_win[q] = r0 + q; where[q] = sel[q]; idx_of_win[q] = -1; }
+    __syncthreads();
+    if (q < kb) {
+        const i64 w = sel[q] - r0;
+        if (w >= 0 && w < kb) idx_of_win[w] = q;
+    }
+    __syncthreads();
+    if (q == 0) {
+        for (int i = 0; i < kb; ++i) {
+            const i64 pos = where[i];
+            ipiv[i] = pos - r0;
+            const i64 o = at_win[i];          // an original window row: moves to pos
+            at_win[i] = sel[i];
+            if (pos - r0 < kb) at_win[pos - r0] = o;
+            const int i2 = idx_of_win[o - r0];
+            if (i2 > i) where[i2] = pos;
+        }
+    }
+}
+void sel_to_ipiv(const i64* sel, i64 kb, i64 r0, i64* ipiv, hipStream_t s) {
+    if (kb <= 0) return;
+    if (kb > MAXSW) throw std::invalid_argument("sel_to_ipiv: kb > 512");
+    hipLaunchKernelGGL(sel_to_ipiv_kernel, dim3(1), dim3(MAXSW), 0, s, sel, (int)kb, r0, ipiv);
+    HIP_LAUNCH_CHECK();
 }
 template <typename T>
 void permute_rows_gather(i64 m, i64 n, const T* A, i64 lda, T* B, i64 ldb, const i64* perm, hipStream_t s) {
@@ -309,7 +421,9 @@ void permute_rows_scatter(i64 m, i64 n, const T* A, i64 lda, T* B, i64 ldb, cons
     template void geadd<T>(char, i64, i64, T, const T*, i64, T, T*, i64, hipStream_t);            \
     template void laswp<T>(i64, T*, i64, i64, i64, const i64*, int, hipStream_t);                 \
     template void laswp_off<T>(i64, T*, i64, i64, i64, const i64*, i64, hipStream_t, int);       \
-    template void permute_rows_gather<T>(i64, i64, const T*, i64, T*, i64, const i64*, hipStream_t);
+    template void permute_rows_gather<T>(i64, i64, const T*, i64, T*, i64, const i64*, hipStream_t);    \
+    template void xchg_gather<T>(const void*, i64, i64, const T*, i64, T*, i64, i64, int, int, hipStream_t); \
+    template void xchg_scatter<T>(const void*, i64, i64, const T*, i64, T*, i64, i64, int, int, hipStream_t);
 INST(float) INST(double) INST(ccplx) INST(zcplx)
 #undef INST
 #define INSTC(A, B) template void gecopy<A, B>(char, char, i64, i64, const A*, i64, B*, i64, hipStream_t);

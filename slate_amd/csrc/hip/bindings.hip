@@ -123,6 +123,8 @@ static void register_kernels(py::module& m) {
         return std::vector<unsigned long long>(v, v + 8); });
     m.def("potrf_lds_profile", [](i64 n, uintptr_t A, i64 lda, uintptr_t info, uintptr_t prof, uintptr_t st) {
         potrf_lds_profile((int)n, P<double>(A), lda, P<i64>(info), P<i64>(prof), S(st)); });
+    m.def("lu_persist_fallbacks", [](int force) { return lu_persist_fallbacks(force); },
+          py::arg("force") = -1);
     m.def("getrf_work_bytes", []() { return (i64)getrf_work_bytes(); });
     m.def("geqrf", [](char dt, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t tau, uintptr_t Tm, i64 ldt,
                       uintptr_t V, i64 ldv, uintptr_t work, uintptr_t st) {
@@ -155,6 +157,21 @@ static void register_kernels(py::module& m) {
         dispatch(dt, [&](auto z) { using T = decltype(z);
             permute_rows_scatter<T>(mm, n, P<T>(A), lda, P<T>(B), ldb, P<const i64>(perm), S(st)); });
     });
+    m.def("swap_plan_bytes", []() { return (i64)swap_plan_bytes(); });
+    m.def("swap_plan", [](i64 k1, i64 k2, uintptr_t ipiv, i64 ioff, int incx, uintptr_t plan, uintptr_t st) {
+        swap_plan(k1, k2, P<const i64>(ipiv), ioff, incx, (void*)plan, S(st)); });
+    m.def("xchg_gather", [](char dt, uintptr_t plan, i64 nslot, i64 n, uintptr_t A, i64 lda, uintptr_t X, i64 ldx,
+                            i64 nb, int p, int pr, uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            xchg_gather<T>((const void*)plan, nslot, n, P<const T>(A), lda, P<T>(X), ldx, nb, p, pr, S(st)); });
+    });
+    m.def("xchg_scatter", [](char dt, uintptr_t plan, i64 nslot, i64 n, uintptr_t X, i64 ldx, uintptr_t A, i64 lda,
+                             i64 nb, int p, int pr, uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            xchg_scatter<T>((const void*)plan, nslot, n, P<const T>(X), ldx, P<T>(A), lda, nb, p, pr, S(st)); });
+    });
+    m.def("sel_to_ipiv", [](uintptr_t sel, i64 kb, i64 r0, uintptr_t ipiv, uintptr_t st) {
+        sel_to_ipiv(P<const i64>(sel), kb, r0, P<i64>(ipiv), S(st)); });
     m.def("geset", [](char dt, char uplo, i64 mm, i64 n, std::complex<double> off, std::complex<double> diag,
                       uintptr_t A, i64 lda, uintptr_t st) {
         dispatch(dt, [&](auto z) { using T = decltype(z);

@@ -19,6 +19,7 @@
 //   (owner of row j) the current row j.
 // Kernel boundaries order the columns, so the panel is stream-ordered
 // (graph-capturable, no host sync, no co-residency assumption).
+#include <cstdlib>
 #include <type_traits>
 #include "common.hpp"
 #include "kernels.hpp"
@@ -282,9 +283,10 @@ getrf_base_step(i64 m, int c0, int c1, int j, T* A, i64 lda, i64* ipiv, i64 ioff
 
 // ---------------------------------------------------------------------------
 // Persistent base case (fp64, partial pivoting): ONE launch factors all
-// (<= 32) columns of a base block.  PG <= 64 co-resident workgroups of 512
-// threads each hold one row of the block per thread in registers for the
-// whole launch; per column the only cross-CU traffic is
+// (<= 32) columns of a base block.  G <= 64 co-resident workgroups of 512
+// threads each hold R rows of the block per thread (R = 1: m <= 32768,
+// R = 2: m <= 65536) in registers for the whole launch; per column the only
+// cross-CU traffic is
 //   publish: local arg-max (value, row) + the winning row + (owner) row j,
 //            all write-through (sc1) stores, drained, then ONE agent-scope
 //            atomic add per workgroup on a column counter;
@@ -293,20 +295,35 @@ getrf_base_step(i64 m, int c0, int c1, int j, T* A, i64 lda, i64* ipiv, i64 ioff
 // (MI355X_MICROARCH.md "Valid forms", first row of the sc1 hand-off table.)
 // Replaces w+1 launches of getrf_base_step (one per column, each re-reading
 // the block from memory): the column chain is the critical path of getrf.
+//
+// Co-residency is not guaranteed (another process or a long kernel can hold
+// the CUs), so the launch ends by CONSENSUS on one state word:
+//   0 running -> 1 committed : the last workgroup to finish the column loop
+//                              (all G finished: nobody can abort any more)
+//   0 running -> 2 aborted   : a workgroup whose bounded spin ran out
+// Workgroups write the block back only when the state is 1.  On 2 the block
+// is untouched and the workgroup that won the abort CAS factors it alone
+// (single-workgroup global-memory LU, same pivoting rule): the result is
+// always correct, only slower; g_lu_fallbacks counts such launches.
 constexpr int PG = 64;           // max workgroups (one per CU on the reserved CUs)
-constexpr int PT2 = 512;         // threads per workgroup = rows per workgroup
+constexpr int PT2 = 512;         // threads per workgroup
 struct PersistBuf {
     double val[2][PG];
     i64 idx[2][PG];
     double cand[2][PG][NBB];
     double diag[2][NBB];
-    unsigned long long cnt;
-    unsigned long long err;
+    unsigned long long cnt;      // column arrivals   } reset before
+    unsigned long long state;    // 0/1/2 (above)     } every launch
+    unsigned long long done;     // loop completions  }
 };
 
 // tools only: per-phase shader-clock totals of workgroup 0 (lu_persist_profile)
 __device__ int g_lu_prof_on = 0;
 __device__ unsigned long long g_lu_prof[8];
+// failure handling: number of launches that fell back to the one-workgroup
+// LU, and a test knob that forces the abort path
+__device__ unsigned long long g_lu_fallbacks = 0;
+__device__ int g_lu_force_abort = 0;
 
 // wave arg-max of (|value|, row) with a 32-bit row: 3 dwords per shuffle
 // round instead of 5
@@ -335,7 +352,132 @@ __device__ inline void st_sc1(i64* p, i64 v) {
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ inline unsigned long long ld_state(const PersistBuf* pb) {
+    return __hip_atomic_load(&pb->state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// CAS running -> to; true if this caller decided the state
+__device__ inline bool decide(PersistBuf* pb, unsigned long long to) {
+    unsigned long long exp = 0;
+    return __hip_atomic_compare_exchange_strong(&pb->state, &exp, to, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+}
 
+// Apply the w interchanges piv_s of the block to the OTHER columns of the
+// panel (left: factored L, right: not yet factored); workgroup g of G owns
+// columns g, g + G, ...  tr_s/ts_s/prv_s/s_nt are LDS scratch.
+__device__ void persist_other_cols(double* Ap, i64 lda, const int* piv_s, int* prv_s, int* tr_s, int* ts_s,
+                                   int& s_nt, int w, int N, int cabs, int g, int G) {
+    const int tid = threadIdx.x;
+    if (tid == 0) s_nt = w;
+    if (tid < w) prv_s[tid] = -1;
+    __syncthreads();
+    if (tid < w && piv_s[tid] != tid && piv_s[tid] < w) atomicMax(&prv_s[piv_s[tid]], tid);
+    __syncthreads();
+    if (tid < w) {
+        // parallel fold (see laswp_setup_kernel): the row finally at j came
+        // from piv_s[j] just before swap j; prv_s[t] = last swap before t
+        // that targets row t
+        auto chain = [&](int t) -> int {
+            while (prv_s[t] >= 0) t = prv_s[t];
+            return t;
+        };
+        const int q = tid, r = piv_s[q];
+        int src;
+        if (r == q) {
+            src = chain(q);
+        } else {
+            int kk = -1;
+            for (int x = q - 1; x >= 0; --x)
+                if (piv_s[x] == r) { kk = x; break; }
+            src = (kk < 0) ? r : chain(kk);
+        }
+        tr_s[q] = q;
+        ts_s[q] = src;
+        if (r >= w) {
+            bool last = true;
+            for (int x = q + 1; x < w; ++x)
+                if (piv_s[x] == r) { last = false; break; }
+            if (last) {
+                const int sl = atomicAdd(&s_nt, 1);
+                tr_s[sl] = r;
+                ts_s[sl] = chain(q);
+            }
+        }
+    }
+    __syncthreads();
+    const int nt = s_nt, nother = N - w;
+    if (g >= nother) return;
+    const int mycols = (nother - g + G - 1) / G;
+    const int cpc = max(1, PT2 / nt);                   // whole columns per chunk
+    for (int k0 = 0; k0 < mycols; k0 += cpc) {
+        const int e = tid, t = e % nt, kk = k0 + e / nt;
+        const bool act = (e / nt) < cpc && kk < mycols;
+        double v = 0.0;
+        i64 dst = 0;
+        if (act) {
+            const int o = g + kk * G;
+            const i64 col = o < cabs ? o : o + w;
+            v = Ap[ts_s[t] + col * lda];
+            dst = tr_s[t] + col * lda;
+        }
+        __syncthreads();
+        if (act) Ap[dst] = v;
+        __syncthreads();
+    }
+}
+
+// The abort path: one workgroup factors the m x w block in global memory
+// with the same pivot rule (NaN wins, larger |a|, lower row on ties,
+// threshold pivoting) and reports pivots/info like the persistent path.
+__device__ void persist_fallback(i64 m, int w, double* A, i64 lda, int* piv_s, double thr, int& zero_at) {
+    __shared__ double fv[PT2 / 64];
+    __shared__ int fi[PT2 / 64];
+    __shared__ int s_piv;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (int j = 0; j < w; ++j) {
+        double v = -1.0;
+        int bi = j;
+        for (i64 i = j + tid; i < m; i += PT2) {
+            const double x = fabs(A[i + (i64)j * lda]);
+            if (beats(x, i, v, (i64)bi)) { v = x; bi = (int)i; }
+        }
+        wave_argmax32(v, bi);
+        if (lane == 0) { fv[wid] = v; fi[wid] = bi; }
+        __syncthreads();
+        if (tid == 0) {
+            double bv = fv[0]; int bb = fi[0];
+            for (int k = 1; k < PT2 / 64; ++k)
+                if (beats(fv[k], (i64)fi[k], bv, (i64)bb)) { bv = fv[k]; bb = fi[k]; }
+            int p = bb;
+            if (!(bv >= 0.0) && !(bv != bv)) p = j;
+            if (thr < 1.0 && p != j) {
+                const double dj = fabs(A[j + (i64)j * lda]);
+                if (dj == dj && dj >= thr * bv) p = j;
+            }
+            s_piv = p;
+            piv_s[j] = p;
+        }
+        __syncthreads();
+        const int p = s_piv;
+        if (p != j && tid < w) {
+            const double t = A[j + (i64)tid * lda];
+            A[j + (i64)tid * lda] = A[p + (i64)tid * lda];
+            A[p + (i64)tid * lda] = t;
+        }
+        __syncthreads();
+        const double u = A[j + (i64)j * lda];
+        if (tid == 0 && u == 0.0 && zero_at < 0) zero_at = j;
+        for (i64 i = j + 1 + tid; i < m; i += PT2) {
+            double l = A[i + (i64)j * lda];
+            if (u != 0.0) l = l / u;
+            A[i + (i64)j * lda] = l;
+            for (int c = j + 1; c < w; ++c) A[i + (i64)c * lda] -= l * A[j + (i64)c * lda];
+        }
+        __syncthreads();
+    }
+}
+
+template <int R>
 __global__ void __launch_bounds__(PT2)
 getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64 ioff, i64* info, i64 info_off,
                    PersistBuf* pb, double thr, int N, int cabs) {
@@ -345,18 +487,19 @@ getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64
     __shared__ double prow[NBB], drow[NBB];
     __shared__ double candL[PG][NBB];
     __shared__ i64 s_p;
-    __shared__ int s_gw, s_bt, s_abort;
+    __shared__ int s_gw, s_bt, s_abort, s_won, s_zero;
     __shared__ int piv_s[NBB], prv_s[NBB], tr_s[2 * NBB], ts_s[2 * NBB], s_nt;
     const int G = gridDim.x, g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const i64 i = (i64)g * PT2 + tid;                 // this thread's row
-    const bool have = i < m;
-    double a[NBB];
-    {
-        const i64 ir = have ? i : 0;
+    const i64 rbase = (i64)g * PT2 * R;
+    double a[R][NBB];
+    #pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const i64 i = rbase + r * PT2 + tid;
+        const i64 ir = i < m ? i : 0;
         #pragma unroll
-        for (int c = 0; c < NBB; ++c) a[c] = A[ir + (i64)min(c, w - 1) * lda];
+        for (int c = 0; c < NBB; ++c) a[r][c] = A[ir + (i64)min(c, w - 1) * lda];
     }
-    if (tid == 0) s_abort = 0;
+    if (tid == 0) { s_abort = 0; s_won = 0; }
     int zero_at = -1;
     const bool prof = g_lu_prof_on && g == 0 && tid == 0;
     unsigned long long tl = prof ? clock64() : 0, ph[5] = {0, 0, 0, 0, 0};
@@ -369,13 +512,19 @@ getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64
         int jv; asm volatile("v_mov_b32 %0, %1" : "=v"(jv) : "s"(j));
         // ---- local arg-max of column j over unpivoted rows (i >= j)
         double v = -1.0;
-        double aj = 0.0;
+        int bi = (int)(rbase + tid);                  // rows < 2^31
         #pragma unroll
-        for (int c = 0; c < NBB; ++c) aj = (c == jv) ? a[c] : aj;
-        v = (have && i >= j) ? fabs(aj) : -1.0;
-        int bi = (int)i;                              // rows < 2^31; the winner's thread is bi - g PT2
+        for (int r = 0; r < R; ++r) {
+            const i64 i = rbase + r * PT2 + tid;
+            double aj = 0.0;
+            #pragma unroll
+            for (int c = 0; c < NBB; ++c) aj = (c == jv) ? a[r][c] : aj;
+            const double vr = (i < m && i >= j) ? fabs(aj) : -1.0;
+            if (r == 0 || beats(vr, i, v, (i64)bi)) { v = vr; bi = (int)i; }
+        }
         wave_argmax32(v, bi);
-        if (lane == 0) { wv[wid] = v; wi[wid] = bi; wt[wid] = bi - g * PT2; }
+        // winner's thread (and register slot): row - rbase = slot * PT2 + thread
+        if (lane == 0) { wv[wid] = v; wi[wid] = bi; wt[wid] = (int)(bi - rbase); }
         __syncthreads();
         if (tid == 0) {
             double bv = wv[0]; i64 bb = wi[0]; int t = wt[0];
@@ -388,13 +537,16 @@ getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64
         __syncthreads();
         LSTAMP(0);                                      // local arg-max
         // ---- publish the winning row and (owner) row j, write-through
-        if (tid == s_bt) {
-            #pragma unroll
-            for (int c = 0; c < NBB; ++c) st_sc1(&pb->cand[par][g][c], a[c]);   // all NBB: no uniform branches
-        }
-        if (have && i == j) {
-            #pragma unroll
-            for (int c = 0; c < NBB; ++c) st_sc1(&pb->diag[par][c], a[c]);
+        #pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (tid + r * PT2 == s_bt) {
+                #pragma unroll
+                for (int c = 0; c < NBB; ++c) st_sc1(&pb->cand[par][g][c], a[r][c]);   // all NBB: no uniform branches
+            }
+            if (rbase + r * PT2 + tid == j) {
+                #pragma unroll
+                for (int c = 0; c < NBB; ++c) st_sc1(&pb->diag[par][c], a[r][c]);
+            }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -403,13 +555,15 @@ getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64
             __hip_atomic_fetch_add(&pb->cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned long long target = (unsigned long long)(j + 1) * G;
             int spins = 0;
-            while (__hip_atomic_load(&pb->cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins > (1 << 22)) {          // not co-resident: give up, never hang
-                    __hip_atomic_store(&pb->err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const bool force = g_lu_force_abort && g == 0 && j == 0;
+            while (force || __hip_atomic_load(&pb->cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                if (force || ++spins > (1 << 22)) {     // not co-resident: abort, never hang
+                    s_won = decide(pb, 2) ? 1 : 0;
                     s_abort = 1;
                     break;
                 }
+                if ((spins & 255) == 0 && ld_state(pb) == 2) { s_abort = 1; break; }
+                __builtin_amdgcn_s_sleep(1);
             }
         }
         LSTAMP(2);                                      // arrive + poll
@@ -458,24 +612,28 @@ getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64
             if (prow[j] == 0.0 && zero_at < 0) zero_at = j;     // first exactly-zero pivot (reported at the end)
         }
         // ---- interchange rows j <-> p and eliminate column j (registers)
-        if (have && i >= j) {
-            if (i == j) {
-                #pragma unroll
-                for (int c = 0; c < NBB; ++c) a[c] = (c < wv_) ? prow[c] : a[c];
-            } else {
-                if (i == p) {
+        #pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const i64 i = rbase + r * PT2 + tid;
+            if (i < m && i >= j) {
+                if (i == j) {
                     #pragma unroll
-                    for (int c = 0; c < NBB; ++c) a[c] = (c < wv_) ? drow[c] : a[c];
-                }
-                const double u = prow[j];
-                double l = 0.0;
-                #pragma unroll
-                for (int c = 0; c < NBB; ++c) l = (c == jv) ? a[c] : l;
-                if (u != 0.0) l = l / u;
-                #pragma unroll
-                for (int c = 0; c < NBB; ++c) {
-                    const double upd = a[c] - l * prow[c];
-                    a[c] = (c == jv) ? l : ((c > jv && c < wv_) ? upd : a[c]);
+                    for (int c = 0; c < NBB; ++c) a[r][c] = (c < wv_) ? prow[c] : a[r][c];
+                } else {
+                    if (i == p) {
+                        #pragma unroll
+                        for (int c = 0; c < NBB; ++c) a[r][c] = (c < wv_) ? drow[c] : a[r][c];
+                    }
+                    const double u = prow[j];
+                    double l = 0.0;
+                    #pragma unroll
+                    for (int c = 0; c < NBB; ++c) l = (c == jv) ? a[r][c] : l;
+                    if (u != 0.0) l = l / u;
+                    #pragma unroll
+                    for (int c = 0; c < NBB; ++c) {
+                        const double upd = a[r][c] - l * prow[c];
+                        a[r][c] = (c == jv) ? l : ((c > jv && c < wv_) ? upd : a[r][c]);
+                    }
                 }
             }
         }
@@ -486,79 +644,52 @@ getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64
         #pragma unroll
         for (int k = 0; k < 5; ++k) g_lu_prof[k] += ph[k];
     }
+    // ---- consensus: commit (every workgroup finished the loop) or abort
+    if (tid == 0 && !s_abort) {
+        const unsigned long long before =
+            __hip_atomic_fetch_add(&pb->done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (before + 1 == (unsigned long long)G) decide(pb, 1);
+        int spins = 0;
+        while (ld_state(pb) == 0) {
+            if (++spins > (1 << 22)) { s_won = decide(pb, 2) ? 1 : 0; break; }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        s_abort = ld_state(pb) == 2 ? 1 : 0;
+    }
+    __syncthreads();
+    if (s_abort) {
+        if (!s_won) return;                             // block untouched: the winner redoes it alone
+        if (tid == 0) { s_zero = -1; atomicAdd(&g_lu_fallbacks, 1ull); }
+        __syncthreads();
+        int zf = -1;
+        persist_fallback(m, w, A, lda, piv_s, thr, zf);
+        if (tid == 0) s_zero = zf;
+        __syncthreads();
+        if (ipiv && tid < w) ipiv[tid] = piv_s[tid] + ioff;
+        if (tid == 0 && s_zero >= 0 && info)
+            atomicCAS(reinterpret_cast<unsigned long long*>(info), 0ull, (unsigned long long)(s_zero + 1 + info_off));
+        if (N > w) persist_other_cols(A - (i64)cabs * lda, lda, piv_s, prv_s, tr_s, ts_s, s_nt, w, N, cabs, 0, 1);
+        return;
+    }
     // pivots and info once per launch (global stores kept out of the column loop)
-    if (g == 0 && !s_abort) {
+    if (g == 0) {
         if (ipiv && tid < w) ipiv[tid] = piv_s[tid] + ioff;
         if (tid == 0 && zero_at >= 0 && info)
             atomicCAS(reinterpret_cast<unsigned long long*>(info), 0ull, (unsigned long long)(zero_at + 1 + info_off));
     }
-    if (have) {
-        #pragma unroll
-        for (int c = 0; c < NBB; ++c) if (c < w) A[i + (i64)c * lda] = a[c];
-    }
-    // ---- the same w interchanges on every OTHER column of the panel (left:
-    // factored L, right: not yet factored), so the recursion needs no laswp.
-    // Every workgroup knows the whole swap sequence; workgroup g owns the
-    // other columns g, g + G, ...; nobody else touches them in this launch.
-    if (N <= w || s_abort) return;
-    __syncthreads();
-    if (tid == 0) s_nt = w;
-    if (tid < w) prv_s[tid] = -1;
-    __syncthreads();
-    if (tid < w && piv_s[tid] != tid && piv_s[tid] < w) atomicMax(&prv_s[piv_s[tid]], tid);
-    __syncthreads();
-    if (tid < w) {
-        // parallel fold (see laswp_setup_kernel): the row finally at j came
-        // from piv_s[j] just before swap j; prv_s[t] = last swap before t
-        // that targets row t
-        auto chain = [&](int t) -> int {
-            while (prv_s[t] >= 0) t = prv_s[t];
-            return t;
-        };
-        const int q = tid, r = piv_s[q];
-        int src;
-        if (r == q) {
-            src = chain(q);
-        } else {
-            int kk = -1;
-            for (int x = q - 1; x >= 0; --x)
-                if (piv_s[x] == r) { kk = x; break; }
-            src = (kk < 0) ? r : chain(kk);
-        }
-        tr_s[q] = q;
-        ts_s[q] = src;
-        if (r >= w) {
-            bool last = true;
-            for (int x = q + 1; x < w; ++x)
-                if (piv_s[x] == r) { last = false; break; }
-            if (last) {
-                const int sl = atomicAdd(&s_nt, 1);
-                tr_s[sl] = r;
-                ts_s[sl] = chain(q);
-            }
+    #pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const i64 i = rbase + r * PT2 + tid;
+        if (i < m) {
+            #pragma unroll
+            for (int c = 0; c < NBB; ++c) if (c < w) A[i + (i64)c * lda] = a[r][c];
         }
     }
+    // ---- the same w interchanges on every OTHER column of the panel, so the
+    // recursion needs no laswp.  Every workgroup knows the whole swap sequence.
+    if (N <= w) return;
     __syncthreads();
-    const int nt = s_nt, nother = N - w;
-    if (g >= nother) return;
-    const int mycols = (nother - g + G - 1) / G;
-    const int cpc = max(1, PT2 / nt);                   // whole columns per chunk
-    double* Ap = A - (i64)cabs * lda;                   // panel column 0, sub-panel row 0
-    for (int k0 = 0; k0 < mycols; k0 += cpc) {
-        const int e = tid, t = e % nt, kk = k0 + e / nt;
-        const bool act = (e / nt) < cpc && kk < mycols;
-        double v = 0.0;
-        i64 dst = 0;
-        if (act) {
-            const int o = g + kk * G;
-            const i64 col = o < cabs ? o : o + w;
-            v = Ap[ts_s[t] + col * lda];
-            dst = tr_s[t] + col * lda;
-        }
-        __syncthreads();
-        if (act) Ap[dst] = v;
-        __syncthreads();
-    }
+    persist_other_cols(A - (i64)cabs * lda, lda, piv_s, prv_s, tr_s, ts_s, s_nt, w, N, cabs, g, G);
 }
 
 // the persistent form needs every row in a register slot of a co-resident
@@ -573,7 +704,7 @@ struct PanelCtx {
 
 template <typename T>
 static bool persist_ok(i64 m, bool nopiv) {
-    return std::is_same<T, double>::value && !nopiv && m <= (i64)PG * PT2 && m >= 1;
+    return std::is_same<T, double>::value && !nopiv && m <= (i64)PG * PT2 * 2 && m >= 1;
 }
 
 template <typename T>
@@ -582,10 +713,16 @@ static void base(i64 m, int c0, int c1, T* A, i64 lda, i64* ipiv, i64 ioff, i64*
     if constexpr (std::is_same<T, double>::value) {
         if (ctx.full) {
             PersistBuf* pb = reinterpret_cast<PersistBuf*>(static_cast<char*>(w) + PANEL_BYTES);
-            HIP_CHECK(hipMemsetAsync(&pb->cnt, 0, sizeof(unsigned long long), s));
-            const int G = (int)((m + PT2 - 1) / PT2);
-            hipLaunchKernelGGL(getrf_base_persist, dim3(G), dim3(PT2), 0, s, m, c1, A, lda, ipiv, ioff, info,
-                               info_off, pb, thr, (int)ctx.N, (int)cabs);
+            HIP_CHECK(hipMemsetAsync(&pb->cnt, 0, 3 * sizeof(unsigned long long), s));   // cnt, state, done
+            if (m <= (i64)PG * PT2) {
+                const int G = (int)((m + PT2 - 1) / PT2);
+                hipLaunchKernelGGL(getrf_base_persist<1>, dim3(G), dim3(PT2), 0, s, m, c1, A, lda, ipiv, ioff,
+                                   info, info_off, pb, thr, (int)ctx.N, (int)cabs);
+            } else {
+                const int G = (int)((m + 2 * PT2 - 1) / (2 * PT2));
+                hipLaunchKernelGGL(getrf_base_persist<2>, dim3(G), dim3(PT2), 0, s, m, c1, A, lda, ipiv, ioff,
+                                   info, info_off, pb, thr, (int)ctx.N, (int)cabs);
+            }
             HIP_LAUNCH_CHECK();
             return;
         }
@@ -640,7 +777,9 @@ void getrf_panel_ws(i64 m, i64 n, T* A, i64 lda, i64* ipiv, i64* info, double th
     if (info) HIP_CHECK(hipMemsetAsync(info, 0, sizeof(i64), s));
     if (m <= 0 || n <= 0) return;
     const i64 k = std::min(m, n);
-    const PanelCtx ctx{n, persist_ok<T>(m, nopiv)};
+    // SLATE_AMD_LU_PERSIST=0 disables the persistent base case (diagnostics)
+    static const bool persist_env = [] { const char* e = std::getenv("SLATE_AMD_LU_PERSIST"); return !e || e[0] != '0'; }();
+    const PanelCtx ctx{n, persist_env && persist_ok<T>(m, nopiv)};
     rec<T>(m, k, A, lda, ipiv, 0, info, 0, w, thr, nopiv, s, ctx, 0);
     if (n > k) {   // wide panel: U12 = L11^{-1} P A12
         if (!nopiv && !ctx.full) laswp_off<T>(n - k, A + k * lda, lda, 0, k, ipiv, 0, s);
@@ -658,6 +797,16 @@ void lu_persist_profile(int enable, unsigned long long* out) {
 }
 
 size_t getrf_work_bytes() { return PANEL_BYTES + sizeof(PersistBuf); }
+
+// failure handling of the persistent base case (tests/tools): number of
+// launches that fell back to the one-workgroup LU; force = 1 makes every
+// following launch take the abort path
+unsigned long long lu_persist_fallbacks(int force) {
+    unsigned long long v = 0;
+    HIP_CHECK(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_lu_fallbacks), sizeof(v)));
+    if (force >= 0) HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_lu_force_abort), &force, sizeof(int)));
+    return v;
+}
 
 #define INST(T) \
     template void getrf_panel_ws<T>(i64, i64, T*, i64, i64*, i64*, double, bool, void*, hipStream_t);

@@ -40,6 +40,18 @@ void permute_rows_scatter(i64 m, i64 n, const T* A, i64 lda, T* B, i64 ldb, cons
 template <typename T>
 void permute_rows_gather(i64 m, i64 n, const T* A, i64 lda, T* B, i64 ldb, const i64* perm, hipStream_t s);
 
+// distributed row interchange (aux.hip): device-resident swap plan, owner-masked
+// pack/unpack around one column all-reduce; CALU selection -> LAPACK ipiv
+void swap_plan(i64 k1, i64 k2, const i64* ipiv, i64 ioff, int incx, void* plan, hipStream_t s);
+size_t swap_plan_bytes();
+template <typename T>
+void xchg_gather(const void* plan, i64 S, i64 n, const T* A, i64 lda, T* X, i64 ldx, i64 nb, int p, int pr,
+                 hipStream_t s);
+template <typename T>
+void xchg_scatter(const void* plan, i64 S, i64 n, const T* X, i64 ldx, T* A, i64 lda, i64 nb, int p, int pr,
+                  hipStream_t s);
+void sel_to_ipiv(const i64* sel, i64 kb, i64 r0, i64* ipiv, hipStream_t s);
+
 // norm.hip: kind 'M' max, '1' one (column sums), 'I' inf (row sums), 'F' fro
 // (scale/sumsq pairs -> here plain sum of squares with scaling by the max);
 // out receives per-column (one), per-row (inf) or a single value.
@@ -53,6 +65,7 @@ void getrf_panel_ws(i64 m, i64 n, T* A, i64 lda, i64* ipiv, i64* info, double th
                     void* work, hipStream_t s);
 size_t getrf_work_bytes();
 void lu_persist_profile(int enable, unsigned long long* out);
+unsigned long long lu_persist_fallbacks(int force);
 template <typename T>
 void laswp_off(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, i64 ioff, hipStream_t s, int incx = 1);
 

@@ -17,6 +17,8 @@
 #include <limits>
 #include <stdexcept>
 #include <vector>
+#include <map>
+#include <cstring>
 
 namespace py = pybind11;
 
@@ -502,6 +504,54 @@ void genorm(char norm, char uplo, char diag, bool herm, i64 m, i64 n, const T* A
 }
 
 // ---------------------------------------------------------------- bindings
+// ------------------------------------------------ distributed row interchange
+// Host twins of aux.hip's swap_plan / xchg_gather / xchg_scatter / sel_to_ipiv
+// (same plan layout, so the Target::HostTask + gloo path runs the same driver).
+struct HostSwapPlan {
+    int nt;
+    int pad;
+    int64_t trow[1024];
+    int64_t tsrc[1024];
+};
+
+static void host_swap_plan(i64 k1, i64 k2, const int64_t* ipiv, i64 ioff, int incx, HostSwapPlan* plan) {
+    // same FIXED-slot layout as aux.hip's swap_plan: window row q in slot q,
+    // the row that swap q (the last swap targeting it) leaves below the
+    // window in slot ns + q, -1 where none; incx < 0 = inverse permutation
+    std::memset(plan, 0, sizeof(HostSwapPlan));
+    const i64 ns = k2 - k1;
+    if (ns <= 0) return;
+    if (ns > 512) throw std::invalid_argument("swap_plan: at most 512 swaps per plan");
+    std::map<i64, i64> at;                       // position -> original row
+    auto get = [&](i64 r) { auto it = at.find(r); return it == at.end() ? r : it->second; };
+    std::map<i64, i64> last;                     // row below the window -> last swap targeting it
+    for (i64 k = k1; k < k2; ++k) {
+        const i64 pv = ipiv[k] - ioff;
+        const i64 a = get(k), b = get(pv);
+        at[k] = b;
+        at[pv] = a;
+        if (pv >= k2) last[pv] = k - k1;
+    }
+    int64_t* dst = incx > 0 ? plan->trow : plan->tsrc;
+    int64_t* src = incx > 0 ? plan->tsrc : plan->trow;
+    for (i64 q = 0; q < ns; ++q) {
+        dst[q] = k1 + q;
+        src[q] = get(k1 + q);
+        dst[ns + q] = -1;
+        src[ns + q] = -1;
+    }
+    for (auto& kv : last) {
+        dst[ns + kv.second] = kv.first;
+        src[ns + kv.second] = get(kv.first);
+    }
+    plan->nt = (int)(2 * ns);
+}
+
+static inline i64 host_bc_local_row(i64 g, i64 nb, int p, int pr) {
+    const i64 tile = g / nb;
+    return (int)(tile % p) == pr ? (tile / p) * nb + g % nb : -1;
+}
+
 template <typename F>
 static void dispatch(char dt, F&& f) {
     switch (dt) {
@@ -597,6 +647,51 @@ void register_tile_kernels(py::module& m) {
             for (auto& x : pv) x -= ioff;
             laswp<T>(n, P<T>(A), lda, k1, k2, pv.data(), incx);
         });
+    });
+    m.def("swap_plan_bytes", []() { return (i64)sizeof(HostSwapPlan); });
+    m.def("swap_plan", [](i64 k1, i64 k2, uintptr_t ipiv, i64 ioff, int incx, uintptr_t plan, uintptr_t) {
+        host_swap_plan(k1, k2, reinterpret_cast<const int64_t*>(ipiv), ioff, incx,
+                       reinterpret_cast<HostSwapPlan*>(plan));
+    });
+    m.def("xchg_gather", [](char dt, uintptr_t plan, i64 nslot, i64 n, uintptr_t A, i64 lda, uintptr_t X, i64 ldx,
+                            i64 nb, int p, int pr, uintptr_t) {
+        const HostSwapPlan* pl = reinterpret_cast<const HostSwapPlan*>(plan);
+        dispatch(dt, [&](auto z) {
+            using T = decltype(z);
+            for (i64 t = 0; t < nslot; ++t) {
+                const i64 src = t < pl->nt ? pl->tsrc[t] : -1;
+                const i64 lr = src >= 0 ? host_bc_local_row(src, nb, p, pr) : -1;
+                for (i64 j = 0; j < n; ++j) P<T>(X)[t + j * ldx] = lr >= 0 ? P<T>(A)[lr + j * lda] : T(0);
+            }
+        });
+    });
+    m.def("xchg_scatter", [](char dt, uintptr_t plan, i64 nslot, i64 n, uintptr_t X, i64 ldx, uintptr_t A, i64 lda,
+                             i64 nb, int p, int pr, uintptr_t) {
+        const HostSwapPlan* pl = reinterpret_cast<const HostSwapPlan*>(plan);
+        dispatch(dt, [&](auto z) {
+            using T = decltype(z);
+            for (i64 t = 0; t < std::min<i64>(nslot, pl->nt); ++t) {
+                if (pl->trow[t] < 0) continue;
+                const i64 lr = host_bc_local_row(pl->trow[t], nb, p, pr);
+                if (lr < 0) continue;
+                for (i64 j = 0; j < n; ++j) P<T>(A)[lr + j * lda] = P<T>(X)[t + j * ldx];
+            }
+        });
+    });
+    m.def("sel_to_ipiv", [](uintptr_t sel, i64 kb, i64 r0, uintptr_t ipiv, uintptr_t) {
+        const int64_t* sl = reinterpret_cast<const int64_t*>(sel);
+        int64_t* ip = reinterpret_cast<int64_t*>(ipiv);
+        std::map<i64, i64> at;   // position -> original row
+        std::map<i64, i64> pos;  // original row -> position
+        auto where = [&](i64 r) { auto it = pos.find(r); return it == pos.end() ? r : it->second; };
+        auto orig = [&](i64 x) { auto it = at.find(x); return it == at.end() ? x : it->second; };
+        for (i64 i = 0; i < kb; ++i) {
+            const i64 a = r0 + i, b = where(sl[i]);
+            ip[i] = b - r0;
+            const i64 oa = orig(a), ob = orig(b);
+            at[a] = ob; at[b] = oa;
+            pos[ob] = a; pos[oa] = b;
+        }
     });
     m.def("row_gather", [](char dt, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t B, i64 ldb, uintptr_t perm,
                            uintptr_t) {

@@ -44,20 +44,27 @@ def getrf(A, pivots: Pivots, opts=None) -> int:
     if method == MethodLU.CALU:
         return getrf_tntpiv(A, pivots, opts)
     with trace_block("getrf"):
-        return _getrf(A, pivots, opts, nopiv=False)
+        return _getrf(A, pivots, opts, mode="pp")
 
 
 def getrf_nopiv(A, opts=None) -> int:
     with trace_block("getrf_nopiv"):
-        return _getrf(A, None, opts, nopiv=True)
+        return _getrf(A, None, opts, mode="nopiv")
 
 
 def getrf_tntpiv(A, pivots, opts=None) -> int:
-    """CALU (tournament pivoting).  With one process row every candidate set
-    is local, so the tournament reduces to partial pivoting of the local
-    panel; with p > 1 the panel owner's GPU runs the final round."""
+    """CALU: LU with tournament pivoting (SLATE src/getrf_tntpiv.cc,
+    internal_getrf_tntpiv.cc).  Each panel's pivot rows are chosen by a
+    reduction tree: every leaf (a chunk of <= ``leaf`` local rows of one
+    rank) runs a partial-pivoting LU on a copy and nominates its kb pivot
+    rows; a rank's nominees play off locally, then the ranks of the process
+    column all-gather their nominees (p*kb rows, one collective) and every
+    rank factors the stack redundantly (deterministic => identical winners
+    everywhere, no broadcast of the result).  The winners are moved into the
+    diagonal block by the device row exchange, L21 = A21 U11^{-1}.  Leaf size:
+    Option.InnerBlocking rows (default 8 nb) or SLATE_AMD_CALU_LEAF."""
     with trace_block("getrf_tntpiv"):
-        return _getrf(A, pivots, opts, nopiv=False)
+        return _getrf(A, pivots, opts, mode="calu")
 
 
 def _check_view(A):
@@ -65,11 +72,11 @@ def _check_view(A):
         raise SlateError("getrf: pass a whole (non-transposed) block-cyclic matrix")
 
 
-def _getrf(A, pivots, opts, nopiv):
+def _getrf(A, pivots, opts, mode):
     s = A.storage
     if s.bc is None:
         from .aux import run_on_block_cyclic
-        return run_on_block_cyclic(A, lambda B, o: _getrf(B, pivots, o, nopiv), opts)
+        return run_on_block_cyclic(A, lambda B, o: _getrf(B, pivots, o, mode), opts)
     _check_view(A)
     bc = s.bc
     slot = target_slot(A, opts)
@@ -78,10 +85,13 @@ def _getrf(A, pivots, opts, nopiv):
         raise SlateError("getrf: square tiles required")
     thr = float(get_option(opts, Option.PivotThreshold, 1.0))
     la = max(0, int(get_option(opts, Option.Lookahead, 1)))
-    if bc.p == 1:
-        info, ipiv = _getrf_p1(A, buf, thr, la, nopiv)
+    if bc.p == 1 and mode != "calu":
+        info, ipiv = _getrf_p1(A, buf, thr, la, mode == "nopiv")
     else:
-        info, ipiv = _getrf_general(A, buf, thr, nopiv)
+        import os
+        leaf = int(os.environ.get("SLATE_AMD_CALU_LEAF", 0)) or \
+            int(get_option(opts, Option.InnerBlocking, 0) or 0) or 8 * bc.nb
+        info, ipiv = _getrf_general(A, buf, thr, la, mode, max(leaf, bc.nb))
     s.mark_local_modified(slot)
     if pivots is not None and ipiv is not None:
         pivots.set(ipiv, bc.nb)
@@ -159,21 +169,18 @@ def _getrf_p1(A, buf, thr, la, nopiv):
             if not nopiv and lck > 0:
                 ops.laswp(buf[:m, 0:lck], ipiv, r0, r0 + kb, ioff=-r0)
     ss.join()
-    # global pivots
-    glob = ipiv.clone()
-    for k in range(kt):
-        r0 = k * nb
-        kb = min(nb, n - r0, m - r0)
-        glob[r0:r0 + kb] += r0
     if nopiv:
         glob = torch.arange(min(m, n), dtype=torch.int64, device=dev)
+    else:
+        glob = _global_pivots(ipiv[:min(m, n)], nb)
     info = _reduce_info(A, infos, kt, nb)
-    return info, glob[:min(m, n)]
+    return info, glob
 
 
-def _bcast_strided(comm, t, root):
-    from ..parallel.tilecomm import bcast_tile
-    return bcast_tile(comm, t, root)
+def _global_pivots(ipiv, nb):
+    """Panel-relative pivots (panel k starts at row k*nb) -> global rows (device op)."""
+    idx = torch.arange(ipiv.numel(), dtype=torch.int64, device=ipiv.device)
+    return ipiv + torch.div(idx, nb, rounding_mode="floor") * nb
 
 
 def _update_cols(buf, Lp, ipiv, r0, kb, m, c0, c1, nopiv):
@@ -203,186 +210,342 @@ def _reduce_info(A, infos, kt, nb):
 
 
 # ------------------------------------------------------------------ p > 1
-def _getrf_general(A, buf, thr, nopiv):
-    """p x q grid: panel gathered to the diagonal owner's GPU, factored there,
-    scattered back; distributed row exchange; SUMMA-like update."""
+_PLAN_TSRC = 1 + 1024     # int64 offset of SwapPlan.tsrc (after {nt, pad} and trow[1024])
+
+
+class _Pack:
+    """One flat byte buffer holding several typed column-major blocks, so a
+    step's panel rows, diagonal factor and pivots travel in ONE collective
+    (SLATE sends them as separate tile messages, getrf.cc:120-160)."""
+
+    def __init__(self, parts, dev):
+        off, self.spec = 0, {}
+        for name, r, c, dt in parts:
+            es = torch.empty(0, dtype=dt).element_size()
+            off = (off + 15) // 16 * 16
+            self.spec[name] = (off, r, c, dt, es)
+            off += r * c * es
+        self.raw = torch.empty(max(off, 16), dtype=torch.uint8, device=dev)
+
+    def get(self, name):
+        off, r, c, dt, es = self.spec[name]
+        flat = self.raw[off:off + r * c * es].view(dt)
+        return flat.view(c, r).t()
+
+
+def _rows_global(lr0, lr1, nb, p, pr, r0, dev):
+    """Panel-relative global rows of local rows [lr0, lr1) of process row pr."""
+    import numpy as np
+    lr = np.arange(lr0, lr1, dtype=np.int64)
+    g = ((lr // nb) * p + pr) * nb + lr % nb - r0
+    return torch.from_numpy(g).to(dev)
+
+
+def _getrf_general(A, buf, thr, la, mode, leaf):
+    """p x q grid, host-synchronisation free, with lookahead.
+
+    step k (panel column k, owned by process column ck = k % q):
+      panel stream (high priority):
+        [wait for column k's last update]
+        panel on the ranks of column ck, one of
+          pp    : all-gather the panel inside the column, every rank factors
+                  it redundantly with the GPU partial-pivoting LU
+                  (deterministic -> identical pivots), keeps its own rows;
+          calu  : tournament pivoting (getrf_tntpiv);
+          nopiv : diagonal-block LU broadcast down the column, L21 by trsm;
+        ONE row broadcast of [my panel rows | L/U diagonal block | pivots]
+        swap plan folded on the device from the pivots
+        lookahead columns: row exchange + U-row trsm + GEMM
+      update stream (low priority, own column communicator):
+        rest of the trailing columns, then the left (already factored)
+        columns' row exchange.
+    The row exchange is swap-plan driven: each rank packs the touched rows it
+    owns, one all-reduce over the column, each rank writes its new rows; the
+    reduced window rows ARE the tile row k each rank needs for the update
+    (SLATE: internal::permuteRows + tileBcast of the U row, getrf.cc:160-210).
+    Nothing inside the loop reads device memory from the host."""
     s = A.storage
     bc = s.bc
-    comm = s.comm
     grid = grid_of(A)
     nb, p, q, pr, pc = bc.nb, bc.p, bc.q, bc.pr, bc.pc
     m, n = s.m, s.n
     kt = min(s.mt, s.nt)
-    dev = buf.device
-    dt = s.dtype
+    dev, dt = buf.device, s.dtype
     mloc, nloc = bc.mloc, bc.nloc
-    glob = torch.zeros(max(min(m, n), 1), dtype=torch.int64)
+    if nb > 512:
+        raise SlateError("getrf: more than one process row needs nb <= 512 (one swap plan per panel)")
+    from ..core.storage import numroc
+    nloc_r = [numroc(m, nb, r, p) for r in range(p)]
+    ipiv = torch.zeros(max(min(m, n), 1), dtype=torch.int64, device=dev)   # panel-relative
     infos = torch.zeros(max(kt, 1), dtype=torch.int64, device=dev)
-    for k in range(kt):
+    ss = StreamSet(dev, reserve_cus=0)
+    colc, rowc = grid.col_comm, grid.row_comm
+    colu = grid.col_comm_u if p > 1 else colc
+    ctx = dict(buf=buf, nb=nb, p=p, pr=pr, mloc=mloc, dt=dt, dev=dev, colc=colc, thr=thr, infos=infos,
+               nloc_r=nloc_r, leaf=leaf, m=m)
+    ev_tr = {}
+    ss.fork()
+    import os
+    kstop = int(os.environ.get("SLATE_AMD_DEBUG_LU_STEPS", kt))    # debugging: stop after k steps
+    for k in range(min(kt, kstop)):
         r0 = k * nb
         kb = min(nb, n - r0, m - r0)
         rk, ck = k % p, k % q
-        root = grid.rank_of(rk, ck)
-        lr_k = tiles_local_before(k, p, pr) * nb          # first local row at/after tile k
-        lc_k = tiles_local_before(k, q, pc) * nb
+        lr_k = min(tiles_local_before(k, p, pr) * nb, mloc)
+        lr1 = min(tiles_local_before(k + 1, p, pr) * nb, mloc)
+        lc_k = min(tiles_local_before(k, q, pc) * nb, nloc)
         lc1 = min(tiles_local_before(k + 1, q, pc) * nb, nloc)
-        # ---- gather panel rows [r0, m) of column k to the root (col_comm)
-        piv_k = torch.zeros(kb, dtype=torch.int64, device=dev)
-        with trace_block("getrf::panel"):
-            if pc == ck:
-                myrows = buf[lr_k:mloc, lc_k:lc_k + kb]
-                sizes = [max(0, _numroc(m, nb, r, p) - tiles_local_before(k, p, r) * nb) for r in range(p)]
-                mx = max(sizes)
-                pad = ops.colmajor_zeros(mx, kb, dt, dev)
-                if myrows.shape[0]:
-                    pad[:myrows.shape[0]].copy_(myrows)
-                allp = grid.col_comm.allgather(pad.t().contiguous()) if p > 1 else pad.t().unsqueeze(0)
-                # assemble in global order on every rank of the column (cheap, avoids a scatter step)
-                P = ops.colmajor_empty(m - r0, kb, dt, dev)
-                gidx, src = _panel_order(k, nb, p, m, sizes)
-                for r in range(p):
-                    if sizes[r]:
-                        rows = allp[r][:, :sizes[r]].t()
-                        P[torch.as_tensor(gidx[r], device=dev)] = rows
-                if pr == rk:
-                    ops.getrf(P, piv_k, infos[k:k + 1], threshold=thr, nopiv=nopiv)
-                grid.col_comm.bcast(P, rk) if p > 1 else None
-                grid.col_comm.bcast(piv_k, rk) if p > 1 else None
-                # write my rows back (already permuted by the panel's own swaps)
-                if myrows.shape[0]:
-                    myrows.copy_(P[torch.as_tensor(gidx[pr], device=dev)])
-                Lcol = P
-            else:
-                Lcol = ops.colmajor_empty(m - r0, kb, dt, dev)
-        # panel + pivots along process rows
-        if q > 1:
-            from ..parallel.tilecomm import bcast_tile
-            bcast_tile(grid.row_comm, Lcol, ck)
-            grid.row_comm.bcast(piv_k, ck)
-        pk = piv_k.cpu()
-        glob[r0:r0 + kb] = pk + r0
-        # ---- distributed row interchange on all local columns except panel col
-        perm = _perm_from_pivots(pk.tolist(), r0)
-        cols_mask = [(0, lc_k if pc == ck else lc1), (lc1, nloc)] if pc == ck else [(0, nloc)]
-        _swap_rows_dist(buf, perm, cols_mask, nb, p, pr, mloc, grid, dt, dev)
-        # ---- U row (tile row k) = L_kk^{-1} A(k, >k) on process row rk
-        Ukk = ops.colmajor_empty(kb, max(nloc - lc1, 0), dt, dev)
-        if pr == rk and nloc > lc1:
-            lrk = tiles_local_before(k, p, pr) * nb
-            ops.trsm('L', 'L', 'N', 'U', 1.0, Lcol[0:kb, 0:kb], buf[lrk:lrk + kb, lc1:nloc])
-            Ukk.copy_(buf[lrk:lrk + kb, lc1:nloc])
-        if p > 1 and Ukk.numel():
-            grid.col_comm.bcast(Ukk, rk)
-        # ---- trailing update of local rows > tile k, cols > tile k
-        lr1 = tiles_local_before(k + 1, p, pr) * nb
-        if mloc > lr1 and nloc > lc1:
-            # Lcol rows for my local rows > tile k
-            ridx = [l2g(i, nb, pr, p) - r0 for i in range(lr1, mloc)]
-            Lm = ops.colmajor_empty(len(ridx), kb, dt, dev)
-            ops.row_gather(Lcol, Lm, torch.as_tensor(ridx, dtype=torch.int64, device=dev))
-            ops.gemm(-1.0, Lm, Ukk, 1.0, buf[lr1:mloc, lc1:nloc])
+        lcla = min(tiles_local_before(k + 1 + la, q, pc) * nb, nloc)
+        lcnx = max(min(tiles_local_before(k + 2 + la, q, pc) * nb, nloc), lcla)
+        nmine = mloc - lr_k
+        piv = ipiv[r0:r0 + kb]
+        nslot = kb if mode == "nopiv" else 2 * kb
+        st = dict(k=k, r0=r0, kb=kb, rk=rk, lr_k=lr_k, lr1=lr1, lc_k=lc_k, nmine=nmine)
+        with ss.use(ss.panel):
+            if k - la - 1 >= 0:
+                ss.wait(ss.panel, ev_tr[k - la - 1])
+            pk = _Pack([("L", nmine + kb, kb, dt), ("piv", kb, 1, torch.int64)], dev)
+            Lp, pv = pk.get("L"), pk.get("piv")[:, 0]
+            with trace_block("getrf::panel"):
+                if pc == ck:
+                    {"pp": _panel_pp, "calu": _panel_calu, "nopiv": _panel_nopiv}[mode](ctx, st, ipiv, Lp, pv)
+                if q > 1:
+                    rowc.bcast(pk.raw, ck)
+                piv.copy_(pv)
+                plan = ops.swap_plan(ipiv, r0, r0 + kb, ioff=-r0)
+            Lkk = Lp[nmine:nmine + kb]
+            Lbelow = Lp[lr1 - lr_k:nmine]
+            upd = dict(plan=plan, nslot=nslot, kb=kb, Lkk=Lkk, Lbelow=Lbelow, rk=rk, lr_k=lr_k, lr1=lr1)
+            # newest lookahead column k+la: first part of step k-1's trailing update
+            if k >= 1 and la > 0:
+                ss.wait(ss.panel, ev_tr[k - 1])
+            _xchg_update(ctx, upd, [(lc1, lcla)], [], colc)
+            ev_panel = ss.event(ss.panel)
+        us = ss.update[0]
+        with ss.use(us):
+            ss.wait(us, ev_panel)
+            if buf.is_cuda:
+                pk.raw.record_stream(us)
+                plan.record_stream(us)
+            with trace_block("getrf::trailing"):
+                _xchg_update(ctx, upd, [(lcla, lcnx)], [], colu)
+                ev_tr[k] = ss.event(us)
+                left = [(0, lc_k)] if mode != "nopiv" else []
+                _xchg_update(ctx, upd, [(lcnx, nloc)], left, colu)
+    ss.join()
+    if mode == "nopiv":
+        glob = torch.arange(min(m, n), dtype=torch.int64, device=dev)
+    else:
+        glob = _global_pivots(ipiv[:min(m, n)], nb)
     info = _reduce_info(A, infos, kt, nb)
-    return info, glob[:min(m, n)].to(dev)
+    return info, glob
 
 
-def _numroc(n, nb, r, p):
-    from ..core.storage import numroc
-    return numroc(n, nb, r, p)
-
-
-def _panel_order(k, nb, p, m, sizes):
-    """Global (panel-relative) row index of each local panel row, per rank row."""
-    r0 = k * nb
-    gidx = {}
-    for r in range(p):
-        lr_k = tiles_local_before(k, p, r) * nb
-        gidx[r] = [l2g(lr_k + i, nb, r, p) - r0 for i in range(sizes[r])]
-    return gidx, None
-
-
-def _perm_from_pivots(piv, r0):
-    """Fold the swap sequence (panel-relative) into {dst_global_row: src_global_row}."""
-    cur = {}
-    for i, pv in enumerate(piv):
-        a, b = r0 + i, r0 + pv
-        if a == b:
-            continue
-        va, vb = cur.get(a, a), cur.get(b, b)
-        cur[a], cur[b] = vb, va
-    return {d: s_ for d, s_ in cur.items() if d != s_}
-
-
-def _swap_rows_dist(buf, perm, col_ranges, nb, p, pr, mloc, grid, dt, dev):
-    """new_row[d] = old_row[perm[d]] for the given local column ranges,
-    rows distributed block-cyclically over the p process rows."""
-    if not perm:
+def _xchg_update(ctx, upd, ranges, swap_only, comm):
+    """Row exchange of local column ranges (one all-reduce over the process
+    column), then for ``ranges`` the U-row trsm and the trailing GEMM."""
+    buf, nb, p, pr, mloc = ctx["buf"], ctx["nb"], ctx["p"], ctx["pr"], ctx["mloc"]
+    cols = [(c0, c1) for c0, c1 in list(ranges) + list(swap_only) if c1 > c0]
+    w = sum(c1 - c0 for c0, c1 in cols)
+    if w == 0:
         return
-    def owner(g): return (g // nb) % p
-    def lrow(g): return (g // nb // p) * nb + g % nb
-    for (c0, c1) in col_ranges:
+    S, kb, plan = upd["nslot"], upd["kb"], upd["plan"]
+    X = ops.colmajor_empty(S, w, ctx["dt"], ctx["dev"])
+    off = 0
+    for c0, c1 in cols:
+        ops.xchg_gather(plan, buf[:mloc, c0:c1], X[:, off:off + c1 - c0], nb, p, pr)
+        off += c1 - c0
+    comm.allreduce(X)
+    off = 0
+    for c0, c1 in cols:
+        ops.xchg_scatter(plan, X[:, off:off + c1 - c0], buf[:mloc, c0:c1], nb, p, pr)
+        off += c1 - c0
+    off = 0
+    lr_k, lr1, Lbelow = upd["lr_k"], upd["lr1"], upd["Lbelow"]
+    for c0, c1 in ranges:
         if c1 <= c0:
             continue
-        cols = buf[:, c0:c1]
-        w = c1 - c0
-        # rows I must send: src rows I own whose destination is elsewhere
-        sends, recvs, local_moves = {}, {}, []
-        send_rows, recv_rows = {}, {}
-        for d, s_ in sorted(perm.items()):
-            od, os_ = owner(d), owner(s_)
-            if od == pr and os_ == pr:
-                local_moves.append((lrow(d), lrow(s_)))
-            elif os_ == pr:
-                send_rows.setdefault(od, []).append(lrow(s_))
-            elif od == pr:
-                recv_rows.setdefault(os_, []).append(lrow(d))
-        for dst, rows in send_rows.items():
-            t = ops.colmajor_empty(len(rows), w, dt, dev)
-            ops.row_gather(cols, t, torch.as_tensor(rows, dtype=torch.int64, device=dev))
-            sends[dst] = t.t().contiguous()
-        for src, rows in recv_rows.items():
-            recvs[src] = torch.empty((w, len(rows)), dtype=dt, device=dev)
-        # local moves must read old values first
-        if local_moves:
-            dsts = torch.as_tensor([a for a, _ in local_moves], dtype=torch.int64, device=dev)
-            srcs = torch.as_tensor([b for _, b in local_moves], dtype=torch.int64, device=dev)
-            tmp = ops.colmajor_empty(len(local_moves), w, dt, dev)
-            ops.row_gather(cols, tmp, srcs)
-        grid.col_comm.exchange(sends, recvs)
-        if local_moves:
-            ops.row_scatter(tmp, cols, dsts)
-        for src, rows in recv_rows.items():
-            r = recvs[src].t()
-            ops.row_scatter(r, cols, torch.as_tensor(rows, dtype=torch.int64, device=dev))
+        U = X[0:kb, off:off + c1 - c0]
+        ops.trsm('L', 'L', 'N', 'U', 1.0, upd["Lkk"], U)
+        if pr == upd["rk"]:
+            buf[lr_k:lr_k + kb, c0:c1].copy_(U)
+        if Lbelow.shape[0]:
+            ops.gemm(-1.0, Lbelow, U, 1.0, buf[lr1:mloc, c0:c1])
+        off += c1 - c0
 
 
-# ------------------------------------------------------------------ solves
+def _panel_pp(ctx, st, ipiv, Lp, pv):
+    """Partial pivoting: the whole panel column is all-gathered inside the
+    process column and factored redundantly by every rank of the column."""
+    buf, nb, p, pr, mloc, dt, dev = (ctx[x] for x in ("buf", "nb", "p", "pr", "mloc", "dt", "dev"))
+    r0, kb, lr_k, lc_k, nmine, k = st["r0"], st["kb"], st["lr_k"], st["lc_k"], st["nmine"], st["k"]
+    m = ctx["m"]
+    cnt = [max(0, ctx["nloc_r"][r] - min(tiles_local_before(k, p, r) * nb, ctx["nloc_r"][r])) for r in range(p)]
+    mx = max(max(cnt), 1)
+    pad = ops.colmajor_zeros(mx, kb, dt, dev)
+    mine = buf[lr_k:mloc, lc_k:lc_k + kb]
+    if nmine:
+        pad[:nmine].copy_(mine)
+    allp = ctx["colc"].allgather(pad.t())            # (p, kb, mx): block r = rank r's rows
+    P = ops.colmajor_empty(m - r0, kb, dt, dev)
+    for r in range(p):
+        if cnt[r]:
+            lr0 = tiles_local_before(k, p, r) * nb
+            ops.row_scatter(allp[r].t()[:cnt[r]], P, _rows_global(lr0, lr0 + cnt[r], nb, p, r, r0, dev))
+    piv = ipiv[r0:r0 + kb]
+    ops.getrf(P, piv, ctx["infos"][k:k + 1], threshold=ctx["thr"])
+    if nmine:
+        ops.row_gather(P, mine, _rows_global(lr_k, mloc, nb, p, pr, r0, dev))
+        Lp[:nmine].copy_(mine)
+    Lp[nmine:nmine + kb].copy_(P[:kb])
+    pv.copy_(piv)
+
+
+def _panel_nopiv(ctx, st, ipiv, Lp, pv):
+    """No pivoting: LU of the diagonal block on its owner, broadcast down the
+    column, L21 = A21 U11^{-1} on every rank."""
+    buf, p, pr, mloc, dt, dev = (ctx[x] for x in ("buf", "p", "pr", "mloc", "dt", "dev"))
+    kb, lr_k, lr1, lc_k, nmine, rk, k = (st[x] for x in ("kb", "lr_k", "lr1", "lc_k", "nmine", "rk", "k"))
+    D = ops.colmajor_empty(kb, kb, dt, dev)
+    if pr == rk:
+        Dm = buf[lr_k:lr_k + kb, lc_k:lc_k + kb]
+        ops.getrf(Dm, None, ctx["infos"][k:k + 1], nopiv=True)
+        D.copy_(Dm)
+    if p > 1:
+        ctx["colc"].bcast(D, rk)
+    below = buf[lr1:mloc, lc_k:lc_k + kb]
+    if below.shape[0]:
+        ops.trsm('R', 'U', 'N', 'N', 1.0, D, below)
+    if nmine:
+        Lp[:nmine].copy_(buf[lr_k:mloc, lc_k:lc_k + kb])
+    Lp[nmine:nmine + kb].copy_(D)
+    pv.copy_(torch.arange(kb, dtype=torch.int64, device=dev))
+
+
+def _tournament(rows, gidx, kb, thr, dev):
+    """One play-off: partial-pivoting LU of a copy of ``rows`` (R x kb);
+    returns the min(R, kb) winners' ORIGINAL rows, their global indices and
+    the factored copy (whose top rows are the winners' L/U)."""
+    R = rows.shape[0]
+    c = min(R, kb)
+    W = ops.colmajor_empty(R, rows.shape[1], rows.dtype, dev)
+    W.copy_(rows)
+    lp = torch.zeros(c, dtype=torch.int64, device=dev)
+    scratch = torch.zeros(1, dtype=torch.int64, device=dev)
+    ops.getrf(W, lp, scratch, threshold=thr)
+    plan = ops.swap_plan(lp, 0, c, 0)
+    win = plan[_PLAN_TSRC:_PLAN_TSRC + c]
+    C = ops.colmajor_empty(c, rows.shape[1], rows.dtype, dev)
+    ops.row_gather(rows, C, win)
+    return C, gidx[win], W
+
+
+def _panel_calu(ctx, st, ipiv, Lp, pv):
+    buf, nb, p, pr, mloc, dt, dev, thr = (ctx[x] for x in ("buf", "nb", "p", "pr", "mloc", "dt", "dev", "thr"))
+    r0, kb, lr_k, lr1, lc_k, nmine, rk, k = (st[x] for x in ("r0", "kb", "lr_k", "lr1", "lc_k", "nmine", "rk", "k"))
+    leaf = ctx["leaf"]
+    colc = ctx["colc"]
+    mine = buf[lr_k:mloc, lc_k:lc_k + kb]
+    # 1. local rounds: leaves of <= leaf rows, then the nominees play off
+    if nmine:
+        g_all = _rows_global(lr_k, mloc, nb, p, pr, 0, dev)
+        noms, gids = [], []
+        for a in range(0, nmine, leaf):
+            b = min(nmine, a + leaf)
+            C, g, _ = _tournament(mine[a:b], g_all[a:b], kb, thr, dev)
+            noms.append(C)
+            gids.append(g)
+        while len(noms) > 1:
+            C = ops.colmajor_empty(sum(x.shape[0] for x in noms), kb, dt, dev)
+            o = 0
+            for x in noms:
+                C[o:o + x.shape[0]].copy_(x)
+                o += x.shape[0]
+            g = torch.cat(gids)
+            # pairwise would need log rounds; one flat round over the
+            # (few) local nominees is the same tournament with fan-in > 2
+            C, g, _ = _tournament(C, g, kb, thr, dev)
+            noms, gids = [C], [g]
+        Cm, gm = noms[0], gids[0]
+    else:
+        Cm = ops.colmajor_empty(0, kb, dt, dev)
+        gm = torch.zeros(0, dtype=torch.int64, device=dev)
+    # 2. cross-rank round: all-gather the nominees (fixed size kb rows each)
+    cnt = [min(kb, max(0, ctx["nloc_r"][r] - min(tiles_local_before(k, p, r) * nb, ctx["nloc_r"][r])))
+           for r in range(p)]
+    pk = _Pack([("C", kb, kb, dt), ("g", kb, 1, torch.int64)], dev)
+    pC, pg = pk.get("C"), pk.get("g")[:, 0]
+    if cnt[pr]:
+        pC[:cnt[pr]].copy_(Cm)
+        pg[:cnt[pr]].copy_(gm)
+    allb = colc.allgather(pk.raw)                    # (p, nbytes)
+    tot = sum(cnt)
+    Stk = ops.colmajor_empty(tot, kb, dt, dev)
+    Gst = torch.empty(tot, dtype=torch.int64, device=dev)
+    o = 0
+    for r in range(p):
+        if cnt[r]:
+            rb = _Pack.__new__(_Pack)
+            rb.spec, rb.raw = pk.spec, allb[r]
+            Stk[o:o + cnt[r]].copy_(rb.get("C")[:cnt[r]])
+            Gst[o:o + cnt[r]].copy_(rb.get("g")[:cnt[r], 0])
+            o += cnt[r]
+    # 3. final round, redundantly on every rank of the column
+    sp = torch.zeros(kb, dtype=torch.int64, device=dev)
+    ops.getrf(Stk, sp, ctx["infos"][k:k + 1], threshold=thr)
+    splan = ops.swap_plan(sp, 0, kb, 0)
+    sel = Gst[splan[_PLAN_TSRC:_PLAN_TSRC + kb]]
+    piv = ipiv[r0:r0 + kb]
+    ops.sel_to_ipiv(sel, r0, piv)
+    # 4. winners into the diagonal block (device row exchange on the panel column)
+    plan = ops.swap_plan(ipiv, r0, r0 + kb, ioff=-r0)
+    X = ops.colmajor_empty(2 * kb, kb, dt, dev)
+    ops.xchg_gather(plan, buf[:mloc, lc_k:lc_k + kb], X, nb, p, pr)
+    colc.allreduce(X)
+    ops.xchg_scatter(plan, X, buf[:mloc, lc_k:lc_k + kb], nb, p, pr)
+    LU = Stk[:kb]
+    if pr == rk:
+        buf[lr_k:lr_k + kb, lc_k:lc_k + kb].copy_(LU)
+    below = buf[lr1:mloc, lc_k:lc_k + kb]
+    if below.shape[0]:
+        ops.trsm('R', 'U', 'N', 'N', 1.0, LU, below)
+    if nmine:
+        Lp[:nmine].copy_(mine)
+    Lp[nmine:nmine + kb].copy_(LU)
+    pv.copy_(piv)
+
+
 def permute_rows(B, pivots: Pivots, forward=True):
-    """Apply P (forward) or P^T (backward) to the rows of B (internal::permuteRows)."""
+    """Apply P (forward) or P^T (backward) to the rows of B (internal::permuteRows).
+    p > 1: the swap sequence is folded on the device in chunks of <= 512
+    swaps and applied by the same owner-masked exchange as getrf (one column
+    all-reduce per chunk, no host round trip)."""
     s = B.storage
     bc = s.bc
     if bc is None:
         raise SlateError("permute_rows: block-cyclic B required")
     lb = B.local_block()
-    piv = pivots.ipiv.tolist()
-    npv = len(piv)
+    npv = pivots.size
     if bc.p == 1:
         ipv = pivots.device(lb.data.device)
         if npv:
             ops.laswp(lb.data, ipv, 0, npv, ioff=0, incx=1 if forward else -1)
-    else:
+    elif npv:
         grid = grid_of(B)
-        # fold all swaps into one permutation (global rows)
-        cur = {}
-        order = range(npv) if forward else range(npv - 1, -1, -1)
-        for i in order:
-            a, b = i, piv[i]
-            if a == b:
-                continue
-            va, vb = cur.get(a, a), cur.get(b, b)
-            cur[a], cur[b] = vb, va
-        perm = {d: s_ for d, s_ in cur.items() if d != s_}
-        _swap_rows_dist(s.local[s.origin_slot], perm, [(lb.col_off, lb.col_off + lb.nloc)], bc.nb, bc.p, bc.pr,
-                        bc.mloc, grid, s.dtype, lb.data.device)
+        buf = s.local[s.origin_slot]
+        ipv = pivots.device(buf.device)
+        cols = buf[:bc.mloc, lb.col_off:lb.col_off + lb.nloc]
+        chunks = [(a, min(npv, a + 512)) for a in range(0, npv, 512)]
+        for a, b in (chunks if forward else chunks[::-1]):
+            plan = ops.swap_plan(ipv, a, b, 0, incx=1 if forward else -1)
+            if cols.shape[1]:
+                X = ops.colmajor_empty(2 * (b - a), cols.shape[1], s.dtype, buf.device)
+                ops.xchg_gather(plan, cols, X, bc.nb, bc.p, bc.pr)
+            else:
+                X = ops.colmajor_empty(2 * (b - a), 0, s.dtype, buf.device)
+            grid.col_comm.allreduce(X) if X.numel() else None
+            if cols.shape[1]:
+                ops.xchg_scatter(plan, X, cols, bc.nb, bc.p, bc.pr)
     s.mark_local_modified(s.origin_slot)
     return B
 
@@ -457,7 +620,7 @@ def getri(A, pivots, opts=None) -> int:
         I = ops.colmajor_zeros(n, n, s.dtype, dev)
         ops.geset(0.0, 1.0, I)
         ipv = pivots.device(dev)
-        ops.laswp(I, ipv, 0, len(pivots.ipiv), ioff=0, incx=1)
+        ops.laswp(I, ipv, 0, pivots.size, ioff=0, incx=1)
         ops.trsm('L', 'L', 'N', 'U', 1.0, F, I)
         ops.trsm('L', 'U', 'N', 'N', 1.0, F, I)
         F.copy_(I)

@@ -203,6 +203,47 @@ def row_scatter(A, B, perm):
     return B
 
 
+# ------------------------------------------- distributed row interchange
+def swap_plan(ipiv, k1, k2, ioff=0, out=None, incx=1):
+    """Fold the swap sequence ipiv[k1:k2) (values - ioff are absolute rows)
+    into a plan of touched rows (SwapPlan layout, stays on ipiv's device)."""
+    mod = kmod(ipiv)
+    if out is None:
+        out = torch.empty(int(mod.swap_plan_bytes()) // 8 + 1, dtype=torch.int64, device=ipiv.device)
+    mod.swap_plan(int(k1), int(k2), ipiv.data_ptr(), int(ioff), int(incx), out.data_ptr(), stream(ipiv))
+    return out
+
+
+def xchg_gather(plan, A, X, nb, p, pr):
+    """X[t, :] = A[local(src_t), :] for the plan's touched rows owned by
+    process row pr (block-cyclic rows, tile nb), 0 elsewhere; X has 2kb rows."""
+    _chk(A); _chk(X, "X")
+    S, n = X.shape
+    if S and n:
+        kmod(X).xchg_gather(code(X.dtype), plan.data_ptr(), S, n, A.data_ptr(), ld(A), X.data_ptr(), ld(X),
+                            int(nb), int(p), int(pr), stream(X))
+    return X
+
+
+def xchg_scatter(plan, X, A, nb, p, pr):
+    """A[local(dst_t), :] = X[t, :] for the touched rows owned by pr."""
+    _chk(A); _chk(X, "X")
+    S, n = X.shape
+    if S and n:
+        kmod(A).xchg_scatter(code(A.dtype), plan.data_ptr(), S, n, X.data_ptr(), ld(X), A.data_ptr(), ld(A),
+                             int(nb), int(p), int(pr), stream(A))
+    return A
+
+
+def sel_to_ipiv(sel, r0, ipiv):
+    """Pivot SET sel (global rows, in order) -> LAPACK swap sequence ipiv
+    (relative to r0), as tournament pivoting needs."""
+    kb = sel.shape[0]
+    if kb:
+        kmod(sel).sel_to_ipiv(sel.data_ptr(), kb, int(r0), ipiv.data_ptr(), stream(sel))
+    return ipiv
+
+
 def trtri(uplo, diag, A, info=None):
     _chk(A)
     if info is None:

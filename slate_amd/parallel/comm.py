@@ -267,10 +267,15 @@ class Comm:
         return lst[0]
 
     # -- sub-communicators -----------------------------------------------
-    def split(self, color_of_rank: Sequence[int]):
+    def split(self, color_of_rank: Sequence[int], tag: str = ""):
         """Collectively create sub-communicators: ranks with equal color share
-        one.  Every member must call with the same list (MPI_Comm_split)."""
-        key = tuple(color_of_rank)
+        one.  Every member must call with the same list (MPI_Comm_split).
+        A different ``tag`` creates a second, independent communicator over
+        the same members (RCCL serialises the collectives of one communicator
+        on one internal stream: a pipeline's panel stream and update stream
+        each get their own, so a panel broadcast never queues behind a
+        trailing-update exchange)."""
+        key = (tuple(color_of_rank), tag)
         if key in self._subcache:
             return self._subcache[key]
         colors = sorted(set(color_of_rank))
@@ -372,6 +377,17 @@ class ProcessGrid:
         # row_comm: same process row (members ordered by pc)
         self.row_comm = comm.split(rows)
         self.col_comm = comm.split(cols)
+        self._rows, self._cols = rows, cols
+        self._col_comm_u = None
+
+    @property
+    def col_comm_u(self):
+        """Second column communicator for collectives issued from the
+        low-priority update stream (created on first use: every rank of the
+        grid runs the same driver code, so creation stays collective)."""
+        if self._col_comm_u is None:
+            self._col_comm_u = self.comm.split(self._cols, tag="update")
+        return self._col_comm_u
 
     def coords(self, rank):
         from ..core.enums import GridOrder

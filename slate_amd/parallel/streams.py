@@ -26,7 +26,7 @@ class StreamSet:
     def __new__(cls, device, n_update=1, reserve_cus=32):
         import os
         reserve_cus = int(os.environ.get("SLATE_AMD_PANEL_CUS", reserve_cus))
-        key = (str(device), n_update, reserve_cus)
+        key = (str(device), n_update, reserve_cus, os.environ.get("SLATE_AMD_SERIAL", "0"))
         s = cls._cache.get(key)
         if s is None:
             s = super().__new__(cls)
@@ -36,9 +36,19 @@ class StreamSet:
         return s
 
     def _init(self, device, n_update):
+        import os
         self.device = device
         self.gpu = device.type == "cuda"
-        if self.gpu:
+        # SLATE_AMD_SERIAL=1: every pipeline stream IS the current stream (all
+        # cross-stream overlap removed) -- the race-detection mode of SURVEY
+        # §5.2: a result that changes between serial and pipelined runs
+        # points at a missing event dependency.
+        self.serial = os.environ.get("SLATE_AMD_SERIAL", "0") == "1"
+        if self.gpu and self.serial:
+            cur = torch.cuda.current_stream(device)
+            self.panel = cur
+            self.update = [cur] * n_update
+        elif self.gpu:
             # torch: lower number = higher priority
             self.panel = torch.cuda.Stream(device=device, priority=-1)
             self.update = [self._update_stream(device, self.reserve_cus) for _ in range(n_update)]
@@ -68,8 +78,10 @@ class StreamSet:
                         words[b // 32] |= 1 << (b % 32)
                     handle = H.stream_create_cu_mask(idx, words)
                     return torch.cuda.ExternalStream(handle, device=device)
-            except Exception:  # noqa: BLE001 - fall back to a plain stream
-                pass
+            except Exception as e:  # noqa: BLE001 - plain stream, but say so
+                import warnings
+                warnings.warn(f"slate_amd: CU-masked update stream unavailable ({e!r}); "
+                              "the trailing update shares every CU with the panel kernels", RuntimeWarning)
         return torch.cuda.Stream(device=device, priority=0)
 
     def use(self, s):

@@ -117,6 +117,66 @@ def check_lu(p, q, dt=torch.float64):
     close(L @ U, PA, 1e-12)
 
 
+def _lu_check(Ad, F, piv, m, n, dt, tol=1e-12):
+    k = min(m, n)
+    L = torch.tril(F[:, :k], -1) + torch.eye(m, k, dtype=dt)
+    U = torch.triu(F[:k, :])
+    PA = Ad.clone()
+    for i, pv in enumerate(piv.ipiv.tolist()):
+        if pv != i:
+            PA[[i, pv]] = PA[[pv, i]]
+    close(L @ U, PA, tol)
+    return L
+
+
+def check_lu_methods(p, q, dt=torch.float64):
+    """getrf partial pivoting / CALU / no pivoting on non-square shapes and
+    lookahead depths; the distributed row exchange (swap plan + column
+    all-reduce) and the tournament both run on every grid."""
+    from slate_amd.core.enums import MethodLU, Option
+    for (m, n, la) in [(100, 70, 0), (64, 96, 2), (83, 83, 1)]:
+        A = mat(m, n, 16, 31, p, q, dt)
+        Ad = D(A)
+        piv = sl.Pivots()
+        assert sl.getrf(A, piv, {Option.Lookahead: la}) == 0
+        L = _lu_check(Ad, D(A), piv, m, n, dt)
+        assert L.abs().max().item() <= 1.0 + 1e-12          # partial pivoting: |L| <= 1
+    # CALU with small leaves (several play-off rounds per rank)
+    import os
+    os.environ["SLATE_AMD_CALU_LEAF"] = "16"
+    try:
+        for (m, n) in [(120, 80), (80, 80)]:
+            A = mat(m, n, 16, 32, p, q, dt)
+            Ad = D(A)
+            piv = sl.Pivots()
+            assert sl.getrf(A, piv, {Option.MethodLU: MethodLU.CALU}) == 0
+            L = _lu_check(Ad, D(A), piv, m, n, dt, 1e-11)
+            assert L.abs().max().item() < 10.0                   # tournament: bounded growth
+            B = mat(m, 3, 16, 33, p, q, dt)
+            if m == n:
+                Bd = D(B)
+                sl.getrs(A, piv, B)
+                close(Ad @ D(B), Bd, 1e-10)
+    finally:
+        del os.environ["SLATE_AMD_CALU_LEAF"]
+    # no pivoting on a diagonally dominant matrix
+    A = mat(80, 80, 16, 34, p, q, dt)
+    Ad = D(A) + 80 * torch.eye(80, dtype=dt)
+    sl.from_dense(A, Ad)
+    assert sl.getrf_nopiv(A) == 0
+    F = D(A)
+    close((torch.tril(F, -1) + torch.eye(80, dtype=dt)) @ torch.triu(F), Ad, 1e-12)
+    # transposed solve exercises the backward permutation
+    A = mat(64, 64, 16, 35, p, q, dt)
+    Ad = D(A)
+    piv = sl.Pivots()
+    assert sl.getrf(A, piv) == 0
+    B = mat(64, 2, 16, 36, p, q, dt)
+    Bd = D(B)
+    sl.getrs(A.transpose(), piv, B)
+    close(Ad.T @ D(B), Bd, 1e-10)
+
+
 def check_norms(p, q, dt=torch.float64):
     A = mat(77, 55, 16, 15, p, q, dt)
     Ad = D(A)
@@ -147,7 +207,7 @@ def check_aux(p, q, dt=torch.float64):
     close(D(C), D(B))
 
 
-ALL = [check_gemm, check_herk_trsm_trmm, check_potrf, check_lu, check_norms, check_aux]
+ALL = [check_gemm, check_herk_trsm_trmm, check_potrf, check_lu, check_lu_methods, check_norms, check_aux]
 
 
 def _run_all(rank, size, p, q):
@@ -179,3 +239,14 @@ def test_two_ranks(grid):
 
 def test_four_ranks():
     run_dist(_run_all, 4, 2, 2)
+
+
+def _run_8(rank, size, p, q):
+    for f in (check_gemm, check_potrf, check_lu, check_lu_methods):
+        f(p, q)
+
+
+@pytest.mark.parametrize("grid", [(2, 4), (1, 8), (8, 1)], ids=lambda g: f"{g[0]}x{g[1]}")
+def test_eight_ranks(grid):
+    """The 8-GPU node's grids (BASELINE: 2x4), rehearsed with 8 gloo ranks."""
+    run_dist(_run_8, 8, *grid, timeout=600)

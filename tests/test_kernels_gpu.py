@@ -247,6 +247,59 @@ def test_getrf_panel_persistent_fp64(m, n):
     assert (A.cpu() - LU_ref).abs().max() / A0.abs().max() < 1e-12
 
 
+@pytest.mark.parametrize("m,n", [(65536, 64), (40000, 96)])
+def test_getrf_panel_persistent_two_rows_per_thread(m, n):
+    # 32768 < m <= 65536: each persistent thread holds two rows
+    A0 = cm(m, n, torch.float64, 36)
+    A = A0.clone()
+    ipiv = torch.zeros(n, dtype=torch.int64, device="cuda")
+    before = _native.hip().lu_persist_fallbacks()
+    info = ops.getrf(A, ipiv)
+    assert int(info.item()) == 0
+    assert _native.hip().lu_persist_fallbacks() == before          # took the persistent path
+    LU_ref, piv_ref = torch.linalg.lu_factor(A0.cpu())
+    assert torch.equal(ipiv.cpu(), piv_ref[:n].to(torch.int64) - 1)
+    assert (A.cpu() - LU_ref).abs().max() / A0.abs().max() < 1e-12
+
+
+@pytest.mark.parametrize("m,n", [(5000, 64), (32768, 96)])
+def test_getrf_panel_persistent_abort_falls_back(m, n):
+    # a launch whose workgroups are not co-resident aborts by consensus and
+    # the CAS winner refactors the block alone: same pivots, same factors,
+    # counted in lu_persist_fallbacks (forced here through the test knob)
+    H = _native.hip()
+    A0 = cm(m, n, torch.float64, 37)
+    A = A0.clone()
+    ipiv = torch.zeros(n, dtype=torch.int64, device="cuda")
+    before = H.lu_persist_fallbacks(1)
+    try:
+        info = ops.getrf(A, ipiv)
+        torch.cuda.synchronize()
+    finally:
+        after = H.lu_persist_fallbacks(0)
+    assert after > before
+    assert int(info.item()) == 0
+    LU_ref, piv_ref = torch.linalg.lu_factor(A0.cpu())
+    assert torch.equal(ipiv.cpu(), piv_ref[:n].to(torch.int64) - 1)
+    assert (A.cpu() - LU_ref).abs().max() / A0.abs().max() < 1e-12
+
+
+def test_getrf_panel_persistent_abort_reports_singular():
+    H = _native.hip()
+    m, n = 3000, 40
+    A0 = cm(m, n, torch.float64, 38)
+    A0[:, 7] = 0.0
+    A = A0.clone()
+    ipiv = torch.zeros(n, dtype=torch.int64, device="cuda")
+    H.lu_persist_fallbacks(1)
+    try:
+        info = ops.getrf(A, ipiv)
+        torch.cuda.synchronize()
+    finally:
+        H.lu_persist_fallbacks(0)
+    assert int(info.item()) == 8
+
+
 @pytest.mark.parametrize("m,n", [(16, 1), (100, 50), (256, 300), (512, 4000), (1000, 70)])
 @pytest.mark.parametrize("unit", [False, True])
 def test_trsm_lln_fp64_fast(m, n, unit):
