@@ -39,7 +39,13 @@ def flops(routine, n, m=None):
     raise ValueError(routine)
 
 
-def grid_for(n):
+def grid_for(n, routine="potrf"):
+    """Default process grid per GPU count.  potrf/getrf/gemm: as square as
+    possible with q >= p (BASELINE: 2x4 at 8 GPUs); geqrf (tall-skinny QR,
+    m = 8n): one process column (p = N) -- the TSQR tree spans all GPUs and
+    the trailing update needs no row broadcast."""
+    if routine == "geqrf":
+        return (n, 1)
     return {1: (1, 1), 2: (1, 2), 4: (2, 2), 8: (2, 4)}.get(n, (1, n))
 
 
@@ -101,7 +107,7 @@ def main():
     rank = comm.rank
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    p, q = grid_for(world) if args.grid is None else map(int, args.grid.lower().split("x"))
+    p, q = grid_for(world, args.routine) if args.grid is None else map(int, args.grid.lower().split("x"))
     gpu = torch.cuda.is_available()
     dev = torch.device("cuda", torch.cuda.current_device()) if gpu else torch.device("cpu")
     sync = torch.cuda.synchronize if gpu else (lambda: None)
@@ -160,7 +166,8 @@ def main():
     ok = (info == 0) if isinstance(info, int) else True
     if rank == 0:
         out = {
-            "metric": f"d{args.routine} GFLOP/s (n={n}, nb={nb})",
+            "metric": (f"d{args.routine} GFLOP/s (m={args.m or n}, n={n}, nb={nb})" if args.routine == "geqrf"
+                       else f"d{args.routine} GFLOP/s (n={n}, nb={nb})"),
             "value": round(gflops, 2),
             "unit": "GFLOP/s",
             "n_gpus": world,

@@ -232,6 +232,16 @@ class _Pack:
         flat = self.raw[off:off + r * c * es].view(dt)
         return flat.view(c, r).t()
 
+    def prefix(self, upto):
+        """A copy of the parts before ``upto`` (one device copy), so the
+        small parts can outlive the big one."""
+        end = self.spec[upto][0]
+        names = list(self.spec)
+        out = _Pack.__new__(_Pack)
+        out.spec = {k: self.spec[k] for k in names[:names.index(upto)]}
+        out.raw = self.raw[:max(end, 16)].clone()
+        return out
+
 
 def _rows_global(lr0, lr1, nb, p, pr, r0, dev):
     """Panel-relative global rows of local rows [lr0, lr1) of process row pr."""

@@ -14,12 +14,19 @@ MI355X design:
 * one process row (p == 1, incl. a single GPU): lookahead pipeline like
   potrf/getrf -- panel + lookahead columns on the high-priority stream, the
   bulk update on the low-priority stream;
-* p > 1: instead of SLATE's per-tile TSQR tree, the panel column (m-k*nb
-  rows x nb, at most a few hundred MB even at m = 2^17) is all-gathered
-  inside the process column and factored redundantly by every rank of that
-  column (deterministic kernels => bit-identical V, T, R), so no broadcast of
-  the result is needed inside the column; V and T then go along the process
-  row, and the update's V^H C is one all-reduce over the process column.
+* p > 1: TSQR over the process column (SLATE: internal::geqrf per tile +
+  the ttqrt reduction tree, src/geqrf.cc:161-251).  Each rank of the panel's
+  process column QR-factors ITS OWN panel rows on its GPU (O(m/p nb^2)), the
+  kr x nb R factors are all-gathered (one collective of p nb^2 words) and
+  every rank of the column factors the stacked [R_rk; R_rk+1; ...] redundantly
+  (deterministic kernels => identical R^, V^, T^, so no broadcast inside the
+  column); R^ lands in the diagonal tile.  The flat p-way stack replaces
+  SLATE's binary tree: on a fully connected xGMI node one all-gather is one
+  hop.  Local V_r, T_r and the tree's V^_r, T^ go along the process row in
+  ONE packed broadcast; the trailing update is local (C_r -= V_r T_r^H V_r^H
+  C_r) plus the tree part on the top rows, whose V^H C is one all-reduce over
+  the column.  Lookahead as for p == 1, the update stream with its own
+  column communicator.
 * LQ is the conjugate transpose of QR: gelqf factors A^H (kept in the
   factor object) and unmlq applies Q^H of it.
 
@@ -55,26 +62,6 @@ def _apply_qh(V, Tk, C, conj=True):
     ops.gemm(-1.0, V, W, 1.0, C)
 
 
-def _apply_qh_dist(Vloc, Tk, Cloc, col_comm, conj=True):
-    """Distributed C -= V op(T) V^H C where rows of V and C are split over the
-    process column: W = sum_r V_r^H C_r is one all-reduce."""
-    ct = conj_trans(Cloc.dtype)
-    kb = Tk.shape[0]
-    nc = Cloc.shape[1]
-    if nc == 0:
-        return
-    W = ops.colmajor_zeros(kb, nc, Cloc.dtype, Cloc.device)
-    if Vloc.shape[0]:
-        ops.gemm(1.0, Vloc, Cloc, 0.0, W, transA=ct)
-    if col_comm is not None and col_comm.size > 1:
-        Wt = W.t().contiguous()
-        col_comm.allreduce(Wt)
-        W = Wt.t()
-    ops.trmm('L', 'U', ct if conj else 'N', 'N', 1.0, Tk, W)
-    if Vloc.shape[0]:
-        ops.gemm(-1.0, Vloc, W, 1.0, Cloc)
-
-
 def _check(A):
     if A.op() != Op.NoTrans or A.ioffset or A.joffset or A.row0_offset or A.col0_offset:
         raise SlateError("geqrf: pass a whole (non-transposed) block-cyclic matrix")
@@ -102,7 +89,7 @@ def geqrf(A, T: TriangularFactors, opts=None) -> int:
         if bc.p == 1:
             _geqrf_p1(A, buf, T, la)
         else:
-            _geqrf_general(A, buf, T)
+            _geqrf_general(A, buf, T, la)
         s.mark_local_modified(slot)
     return 0
 
@@ -147,7 +134,7 @@ def _geqrf_p1(A, buf, T, la):
             if lcla > lc1:
                 _apply_qh(V, Tk, buf[r0:m, lc1:lcla])
             ev_panel = ss.event(ss.panel)
-        T.append({"T": Tk, "tau": tau, "r0": r0, "kb": kb})
+        T.append({"T": Tk, "tau": tau, "r0": r0, "kb": kb, "kr": kb, "tree": None})
         us = ss.update[0]
         with ss.use(us):
             ss.wait(us, ev_panel)
@@ -164,31 +151,14 @@ def _geqrf_p1(A, buf, T, la):
     ss.join()
 
 
-def _gather_panel(buf, mloc, k, nb, m, p, pr, lc, kb, grid, dt, dev):
-    """All-gather rows [k*nb, m) of local columns [lc, lc+kb) within the
-    process column; returns (P in global row order, my-rows index)."""
+def _pack(parts, dev):
+    from .lu import _Pack
+    return _Pack(parts, dev)
+
+
+def _geqrf_general(A, buf, T, la):
+    """p > 1 process rows: TSQR panel + lookahead (see module docstring)."""
     from ..core.storage import numroc
-    r0 = k * nb
-    lr_k = tiles_local_before(k, p, pr) * nb
-    sizes = [max(0, numroc(m, nb, r, p) - tiles_local_before(k, p, r) * nb) for r in range(p)]
-    mx = max(sizes) if sizes else 0
-    pad = ops.colmajor_zeros(max(mx, 1), kb, dt, dev)
-    mine = buf[lr_k:mloc, lc:lc + kb] if mloc > lr_k else buf[0:0, lc:lc + kb]
-    if mine.shape[0]:
-        pad[:mine.shape[0]].copy_(mine)
-    allp = grid.col_comm.allgather(pad.t().contiguous())
-    P = ops.colmajor_empty(m - r0, kb, dt, dev)
-    idx = {}
-    for r in range(p):
-        lr = tiles_local_before(k, p, r) * nb
-        gi = [l2g(lr + i, nb, r, p) - r0 for i in range(sizes[r])]
-        idx[r] = torch.as_tensor(gi, dtype=torch.int64, device=dev)
-        if sizes[r]:
-            ops.row_scatter(allp[r][:, :sizes[r]].t(), P, idx[r])
-    return P, idx[pr], mine
-
-
-def _geqrf_general(A, buf, T):
     s = A.storage
     bc = s.bc
     grid = grid_of(A)
@@ -197,33 +167,127 @@ def _geqrf_general(A, buf, T):
     kt = min(s.mt, s.nt)
     dev, dt = buf.device, s.dtype
     mloc, nloc = bc.mloc, bc.nloc
+    nloc_r = [numroc(m, nb, r, p) for r in range(p)]
+    ss = StreamSet(dev, reserve_cus=0)
+    colc, rowc = grid.col_comm, grid.row_comm
+    colu = grid.col_comm_u
+    ev_tr = {}
+    ss.fork()
     for k in range(kt):
         r0 = k * nb
         kb = min(nb, n - r0, m - r0)
-        ck = k % q
-        lr_k = tiles_local_before(k, p, pr) * nb
-        lc_k = tiles_local_before(k, q, pc) * nb
+        rk, ck = k % p, k % q
+        lr_k = min(tiles_local_before(k, p, pr) * nb, mloc)
+        lc_k = min(tiles_local_before(k, q, pc) * nb, nloc)
         lc1 = min(tiles_local_before(k + 1, q, pc) * nb, nloc)
-        tau = torch.zeros(kb, dtype=dt, device=dev)
-        Tk = ops.colmajor_empty(kb, kb, dt, dev)
-        nmine = max(0, mloc - lr_k)
-        Vloc = ops.colmajor_empty(nmine, kb, dt, dev)
-        with trace_block("geqrf::panel"):
-            if pc == ck:
-                P, myidx, mine = _gather_panel(buf, mloc, k, nb, m, p, pr, lc_k, kb, grid, dt, dev)
-                V = ops.colmajor_empty(m - r0, kb, dt, dev)
-                ops.geqrf(P, tau, Tk, V)            # redundant in the column: identical results
-                if nmine:
-                    ops.row_gather(P, mine, myidx)
-                    ops.row_gather(V, Vloc, myidx)
-        if q > 1:
-            from ..parallel.tilecomm import bcast_tile
-            bcast_tile(grid.row_comm, Vloc, ck)
-            bcast_tile(grid.row_comm, Tk, ck)
-            grid.row_comm.bcast(tau, ck)
-        T.append({"T": Tk, "tau": tau, "r0": r0, "kb": kb})
-        with trace_block("geqrf::trailing"):
-            _apply_qh_dist(Vloc, Tk, buf[lr_k:mloc, lc1:nloc], grid.col_comm)
+        lcla = min(tiles_local_before(k + 1 + la, q, pc) * nb, nloc)
+        lcnx = max(min(tiles_local_before(k + 2 + la, q, pc) * nb, nloc), lcla)
+        cnt = [max(0, nloc_r[r] - min(tiles_local_before(k, p, r) * nb, nloc_r[r])) for r in range(p)]
+        kr = [min(c, kb) for c in cnt]                   # local reflectors = stacked rows per rank
+        order = [(rk + i) % p for i in range(p)]         # rk first: its top rows receive R^
+        soff, o = {}, 0
+        for r in order:
+            soff[r] = o
+            o += kr[r]
+        tot = o
+        ks = min(tot, kb)
+        tree = sum(1 for r in range(p) if kr[r]) > 1
+        nmine, km = cnt[pr], kr[pr]
+        st = dict(k=k, kb=kb, rk=rk, lr_k=lr_k, lc_k=lc_k, nmine=nmine, km=km, kr=kr, soff=soff,
+                  order=order, tot=tot, ks=ks, tree=tree)
+        with ss.use(ss.panel):
+            if k - la - 1 >= 0:
+                ss.wait(ss.panel, ev_tr[k - la - 1])
+            # small factors first (kept in T), the local V (re-derived from A
+            # by unmqr) last
+            parts = [("T", km, km, dt), ("tau", km, 1, dt)]
+            if tree:
+                parts += [("Vh", km, ks, dt), ("Th", ks, ks, dt), ("tauh", ks, 1, dt)]
+            parts += [("V", nmine, km, dt)]
+            pk = _pack(parts, dev)
+            with trace_block("geqrf::panel"):
+                if pc == ck:
+                    _tsqr_panel(buf, mloc, pr, p, colc, pk, st, dt, dev)
+                if q > 1:
+                    rowc.bcast(pk.raw, ck)
+            kp = pk.prefix("V")
+            f = {"T": kp.get("T"), "tau": kp.get("tau")[:, 0], "r0": r0, "kb": kb, "kr": km,
+                 "tree": ({"V": kp.get("Vh"), "T": kp.get("Th"), "tau": kp.get("tauh")[:, 0], "ks": ks}
+                          if tree else None)}
+            if k >= 1 and la > 0:
+                ss.wait(ss.panel, ev_tr[k - 1])
+            _tsqr_update(buf, lr_k, mloc, pk.get("V"), f, [(lc1, lcla)], colc, dt, dev)
+            ev_panel = ss.event(ss.panel)
+        T.append(f)
+        us = ss.update[0]
+        with ss.use(us):
+            ss.wait(us, ev_panel)
+            if buf.is_cuda:
+                pk.raw.record_stream(us)
+            with trace_block("geqrf::trailing"):
+                _tsqr_update(buf, lr_k, mloc, pk.get("V"), f, [(lcla, lcnx)], colu, dt, dev)
+                ev_tr[k] = ss.event(us)
+                _tsqr_update(buf, lr_k, mloc, pk.get("V"), f, [(lcnx, nloc)], colu, dt, dev)
+    ss.join()
+
+
+def _tsqr_panel(buf, mloc, pr, p, colc, pk, st, dt, dev):
+    """Ranks of the panel's process column: local QR of the own panel rows,
+    all-gather of the R factors, redundant QR of the stack."""
+    kb, lr_k, lc_k, nmine, km = st["kb"], st["lr_k"], st["lc_k"], st["nmine"], st["km"]
+    mine = buf[lr_k:mloc, lc_k:lc_k + kb]
+    if nmine:
+        ops.geqrf(mine, pk.get("tau")[:, 0], pk.get("T"), pk.get("V"))
+    if not st["tree"]:
+        return
+    Rb = ops.colmajor_zeros(kb, kb, dt, dev)
+    if km:
+        ops.gecopy(mine[:km], Rb[:km], uplo='U')
+    allR = colc.allgather(Rb.t())                     # (p, kb, kb): block r = rank r's R (transposed)
+    S = ops.colmajor_empty(st["tot"], kb, dt, dev)
+    for r in st["order"]:
+        if st["kr"][r]:
+            o = st["soff"][r]
+            S[o:o + st["kr"][r]].copy_(allR[r].t()[:st["kr"][r]])
+    ks = st["ks"]
+    Vf = ops.colmajor_empty(st["tot"], ks, dt, dev)
+    ops.geqrf(S, pk.get("tauh")[:, 0], pk.get("Th"), Vf)
+    if km:
+        o = st["soff"][pr]
+        pk.get("Vh").copy_(Vf[o:o + km])
+    if pr == st["rk"]:
+        ops.gecopy(S[:ks], mine[:ks], uplo='U')       # R^ over R_rk; reflectors below stay
+
+
+def _tsqr_update(buf, lr_k, mloc, Vl, f, ranges, comm, dt, dev, conj=True):
+    """C = Q^H C for local columns ``ranges`` of the rows >= tile k."""
+    for c0, c1 in ranges:
+        if c1 > c0:
+            _tsqr_apply(buf[lr_k:mloc, c0:c1], Vl, f, comm, conj)
+
+
+def _tsqr_apply(C, Vl, f, comm, conj=True):
+    """C = Q_k^H C (conj) or Q_k C with Q_k = diag(Q_r) Q^ (local block
+    reflector of this rank's panel rows, then the tree on the top kr rows;
+    the tree's V^H C is one all-reduce over the process column)."""
+    dt, dev = C.dtype, C.device
+    ct = conj_trans(dt)
+    km = f["kr"]
+    tr = f["tree"]
+    if C.shape[1] == 0:
+        return
+    if conj and km and C.shape[0]:
+        _apply_qh(Vl, f["T"], C, conj=True)
+    if tr is not None:
+        W = ops.colmajor_zeros(tr["ks"], C.shape[1], dt, dev)
+        if km:
+            ops.gemm(1.0, tr["V"], C[:km], 0.0, W, transA=ct)
+        comm.allreduce(W)
+        ops.trmm('L', 'U', ct if conj else 'N', 'N', 1.0, tr["T"], W)
+        if km:
+            ops.gemm(-1.0, tr["V"], W, 1.0, C[:km])
+    if not conj and km and C.shape[0]:
+        _apply_qh(Vl, f["T"], C, conj=False)
 
 
 # ------------------------------------------------------------------ unmqr
@@ -232,25 +296,22 @@ def _same_rows(A, C):
     return (a.mb, a.p, a.pr) == (c.mb, c.p, c.pr) and C.global_offsets()[0] == 0 and \
         a.order == c.order and A.storage.comm is C.storage.comm
 def _local_V(A, k, Tk):
-    """Explicit V rows of panel k for this rank's local rows >= k*nb,
-    available on every rank of the process row (bcast along the row)."""
+    """Explicit local reflectors V_r of panel k for this rank's local rows
+    >= tile k (unit lower trapezoidal, kr columns: TSQR leaves one local
+    block reflector per rank), available on every rank of the process row
+    (bcast along the row)."""
     s = A.storage
     bc = s.bc
     nb, p, q, pr, pc = bc.nb, bc.p, bc.q, bc.pr, bc.pc
-    kb = Tk["kb"]
-    lr_k = tiles_local_before(k, p, pr) * nb
+    km = Tk.get("kr", Tk["kb"])
+    lr_k = min(tiles_local_before(k, p, pr) * nb, bc.mloc)
     lc_k = tiles_local_before(k, q, pc) * nb
     mloc = bc.mloc
     buf = s.local[s.origin_slot]
     nmine = max(0, mloc - lr_k)
-    Vloc = ops.colmajor_empty(nmine, kb, s.dtype, buf.device)
-    if pc == k % q and nmine:
-        # rows of the global diagonal block need the unit-lower structure
-        src = buf[lr_k:mloc, lc_k:lc_k + kb]
-        if pr == k % p:
-            ops.v_explicit(src, Vloc)     # my first local rows ARE the diagonal block
-        else:
-            Vloc.copy_(src)
+    Vloc = ops.colmajor_empty(nmine, km, s.dtype, buf.device)
+    if pc == k % q and nmine and km:
+        ops.v_explicit(buf[lr_k:mloc, lc_k:lc_k + km], Vloc)
     if q > 1:
         from ..parallel.tilecomm import bcast_tile
         bcast_tile(grid_of(A).row_comm, Vloc, k % q)
@@ -282,7 +343,7 @@ def unmqr(side, op, A, T: TriangularFactors, C, opts=None):
             for k in order:
                 Vloc, lr_k = _local_V(A, k, T[k])
                 Cl = cbuf[lr_k - lbC.row_off:, :] if lr_k >= lbC.row_off else cbuf
-                _apply_qh_dist(Vloc, T[k]["T"], Cl, grid.col_comm, conj=conj)
+                _tsqr_apply(Cl, Vloc, T[k], grid.col_comm, conj=conj)
         else:
             # C op(Q) = (op(Q)^H C^H)^H: work on the conjugate transpose
             from .aux import copy_conj_transpose

@@ -241,8 +241,23 @@ def test_four_ranks():
     run_dist(_run_all, 4, 2, 2)
 
 
+def check_qr(p, q, dt=torch.float64):
+    from slate_amd.core.enums import Option
+    m, n, nb = 300, 120, 16
+    A = mat(m, n, nb, 21, p, q, dt)
+    A0 = D(A)
+    T = sl.TriangularFactors()
+    sl.geqrf(A, T, {Option.Lookahead: 2})
+    R = torch.triu(D(A))[:n]
+    close(R.mH @ R, A0.mH @ A0, 1e-12)
+    B = mat(m, 3, nb, 22, p, q, dt)
+    Bd = D(B)
+    sl.gels(mat(m, n, nb, 21, p, q, dt), sl.TriangularFactors(), B)
+    close(D(B)[:n], torch.linalg.lstsq(A0, Bd).solution, 1e-9)
+
+
 def _run_8(rank, size, p, q):
-    for f in (check_gemm, check_potrf, check_lu, check_lu_methods):
+    for f in (check_gemm, check_potrf, check_lu, check_lu_methods, check_qr):
         f(p, q)
 
 

@@ -137,9 +137,30 @@ def _dist_qr(rank, size, p, q):
         assert (X - torch.linalg.lstsq(A0, B0).solution).abs().max().item() < 1e-10
 
 
-@pytest.mark.parametrize("grid", [(2, 1), (1, 2)])
+@pytest.mark.parametrize("grid", [(2, 1), (1, 2), (2, 2), (4, 1)], ids=lambda g: f"{g[0]}x{g[1]}")
 def test_qr_distributed(grid):
-    run_dist(_dist_qr, 2, *grid)
+    run_dist(_dist_qr, grid[0] * grid[1], *grid)
+
+
+def _dist_qr_la(rank, size, p, q):
+    """TSQR with lookahead 0..2, ragged last tiles and ranks without rows."""
+    for (m, n, nb, la) in [(200, 120, 16, 0), (333, 90, 32, 2), (96, 96, 16, 1)]:
+        A = _mat(m, n, nb, torch.float64, 12, p, q)
+        A0 = D(A).clone()
+        T = TriangularFactors()
+        qr.geqrf(A, T, {Option.Lookahead: la})
+        R = torch.triu(D(A))[:n]
+        assert (R.T @ R - A0.T @ A0).abs().max().item() / (A0.abs().max().item() ** 2 * m) < 1e-13
+        C = _mat(m, 7, nb, torch.float64, 13, p, q)
+        C0 = D(C).clone()
+        qr.unmqr(Side.Left, Op.ConjTrans, A, T, C)
+        qr.unmqr(Side.Left, Op.NoTrans, A, T, C)
+        assert (D(C) - C0).abs().max().item() < 1e-12
+
+
+@pytest.mark.parametrize("grid", [(4, 1), (2, 2)], ids=lambda g: f"{g[0]}x{g[1]}")
+def test_tsqr_lookahead(grid):
+    run_dist(_dist_qr_la, grid[0] * grid[1], *grid)
 
 
 # ---------------------------------------------------------------- GPU
