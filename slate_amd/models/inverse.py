@@ -41,18 +41,14 @@ def trtri(A, opts=None) -> int:
             info = ops.trtri(uch, dch, F)
             s.mark_local_modified(s.origin_slot)
             return int(info.item()) if isinstance(info, torch.Tensor) else int(info)
-        # distributed: X = T^{-1} via trsm against the identity, written back
-        from .aux import allgather_dense, set as aset, copy
-        D = allgather_dense(A)
-        dg = torch.diagonal(D)
+        # distributed: X = T^{-1} via the distributed trsm against the
+        # identity, stored triangle copied back (no gather)
         if dch == 'N':
-            z = (dg == 0).nonzero()
-            if z.numel():
-                return int(z[0].item()) + 1
-        from ..core.matrix import Matrix
-        bc = s.bc
-        X = Matrix(n, n, nb=bc.nb, p=bc.p, q=bc.q, comm=s.comm, dtype=s.dtype, device=s.device, order=bc.order)
-        X.insertLocalTiles(device=s.device.index if s.device.type == "cuda" else -1)
+            z = _first_zero_diag(A)
+            if z:
+                return z
+        X = _general_like(A)
+        from .aux import set as aset
         aset(0.0, 1.0, X)
         from .blas3 import trsm
         trsm(Side.Left, 1.0, A, X, opts)
@@ -60,13 +56,40 @@ def trtri(A, opts=None) -> int:
         return 0
 
 
+def _general_like(A):
+    from ..core.matrix import Matrix
+    s = A.storage
+    bc = s.bc
+    n = A.n()
+    X = Matrix(n, n, nb=bc.nb, p=bc.p, q=bc.q, comm=s.comm, dtype=s.dtype, device=s.device, order=bc.order)
+    X.insertLocalTiles(device=s.device.index if s.device.type == "cuda" else -1)
+    return X
+
+
+def _first_zero_diag(A):
+    """1-based index of the first exactly-zero diagonal element (0: none);
+    each rank scans the diagonal runs it owns, one min-reduction."""
+    from .aux import _diag_runs
+    lb = A.local_block()
+    best = 1 << 62
+    if lb.mloc and lb.nloc:
+        for (i0, j0, k) in _diag_runs(lb.data, lb):
+            d = torch.diagonal(lb.data[i0:i0 + k, j0:j0 + k])
+            z = (d == 0).nonzero()
+            if z.numel():
+                best = min(best, lb.global_col(j0 + int(z[0].item())) + 1)
+    comm = A.storage.comm
+    if comm.size > 1:
+        best = int(comm.allreduce_scalar(best, "min", torch.int64))
+    return 0 if best >= (1 << 62) else best
+
+
 def _copy_tri(X, A):
-    """Copy the stored triangle of X into triangular A."""
-    from .aux import allgather_dense, from_dense
-    D = allgather_dense(X)
-    up = A.uploPhysical()
-    D = torch.tril(D) if up == Uplo.Lower else torch.triu(D)
-    from_dense(A, D)
+    """Copy the stored triangle of X into triangular A (same distribution:
+    one masked local copy, the other triangle of A untouched)."""
+    from .aux import copy
+    from ..core.matrix import TriangularMatrix as TM
+    copy(TM(A.uploPhysical(), X), A)
 
 
 def trtrm(A, opts=None) -> int:
@@ -94,15 +117,19 @@ def trtrm(A, opts=None) -> int:
                 F.copy_(torch.where(torch.ones_like(F, dtype=torch.bool).triu(), X, F))
             s.mark_local_modified(s.origin_slot)
             return 0
-        from .aux import allgather_dense, from_dense
-        D = ops.as_colmajor(allgather_dense(A).clone())
-        X = ops.colmajor_empty(n, n, D.dtype, D.device)
+        # distributed: X = stored triangle of A (zeros elsewhere), then the
+        # distributed trmm, stored triangle copied back
+        X = _general_like(A)
+        from .aux import set as aset
+        from .blas3 import trmm
+        aset(0.0, 0.0, X)
+        from ..core.matrix import TriangularMatrix as TM
+        from .aux import copy
+        copy(TM(uplo, A), TM(uplo, X))
+        T = TM(uplo, A, diag=Diag.NonUnit)
         if uplo == Uplo.Lower:
-            X.copy_(torch.tril(D))
-            ops.trmm('L', 'L', ct, 'N', 1.0, D, X)
-            from_dense(A, torch.tril(X))
+            trmm(Side.Left, 1.0, T.conj_transpose(), X, opts)      # X = L^H L
         else:
-            X.copy_(torch.triu(D))
-            ops.trmm('R', 'U', ct, 'N', 1.0, D, X)
-            from_dense(A, torch.triu(X))
+            trmm(Side.Right, 1.0, T.conj_transpose(), X, opts)     # X = U U^H
+        _copy_tri(X, A)
         return 0

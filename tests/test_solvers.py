@@ -111,3 +111,31 @@ def _dist(rank, size, p, q):
 @pytest.mark.parametrize("grid", [(2, 1), (1, 2)])
 def test_solvers_distributed(grid):
     run_dist(_dist, 2, *grid)
+
+
+def _potri_both_uplo(rank, size, p, q):
+    """potri / trtri / trtrm on the grid (distributed trsm/trmm, no gather):
+    inverse correct for both storage triangles, the other triangle untouched."""
+    from slate_amd.core.enums import Uplo
+    for uplo in (Uplo.Lower, Uplo.Upper):
+        n, nb = 70, 16
+        A = sl.HermitianMatrix(uplo, n, nb=nb, p=p, q=q)
+        A.insertLocalTiles()
+        sl.generate_matrix(A, "poev", 3)
+        X = D(A)
+        lo = uplo == Uplo.Lower
+        Af = (torch.tril(X) + torch.tril(X, -1).mT) if lo else (torch.triu(X) + torch.triu(X, 1).mT)
+        other = (torch.triu(X, 1) if lo else torch.tril(X, -1)).clone()
+        assert sl.potrf(A) == 0 and sl.potri(A) == 0
+        Y = D(A)
+        Yi = (torch.tril(Y) + torch.tril(Y, -1).mT) if lo else (torch.triu(Y) + torch.triu(Y, 1).mT)
+        assert (Yi @ Af - torch.eye(n, dtype=Af.dtype)).abs().max().item() < 1e-10
+        assert torch.equal(torch.triu(Y, 1) if lo else torch.tril(Y, -1), other)
+
+
+@pytest.mark.parametrize("grid", [(1, 1), (2, 1), (1, 2), (2, 2)], ids=lambda g: f"{g[0]}x{g[1]}")
+def test_potri_distributed(grid):
+    if grid == (1, 1):
+        _potri_both_uplo(0, 1, 1, 1)
+    else:
+        run_dist(_potri_both_uplo, grid[0] * grid[1], *grid)

@@ -20,7 +20,7 @@ float run(GemmArgs<double> a, int reps) {
 }
 
 int main() {
-    const long N = 8192;
+    const long N = 24576;
     double *A, *B, *C;
     hipMalloc(&A, N * N * 8); hipMalloc(&B, N * N * 8); hipMalloc(&C, N * N * 8);
     std::vector<double> h(N * N);
@@ -32,28 +32,22 @@ int main() {
     auto mk = [&](long m, long n, long k) {
         GemmArgs<double> a{}; a.m = m; a.n = n; a.k = k; a.alpha = 1; a.beta = 1;
         a.A = A; a.lda = m; a.B = B; a.ldb = std::max(k, n); a.C = C; a.ldc = m;
-        a.vecA = a.vecB = 1; a.group_m = 8; return a; };
+        a.vecA = a.vecB = 1; a.group_m = 8; a.remap = 1; return a; };
     struct Shape { long m, n, k; };
-    Shape shapes[] = {{8192, 8192, 8192}, {8192, 8192, 512}};
+    Shape shapes[] = {{16384, 16384, 4096}, {24576, 24576, 512}};
     for (auto s : shapes) {
         auto a = mk(s.m, s.n, s.k);
         double fl = 2.0 * s.m * s.n * s.k;
         int reps = s.k > 1000 ? 3 : 10;
 #define V(TA, TB, BM, BN, BK, WM, WN) { float ms = run<TA, TB, BM, BN, BK, WM, WN>(a, reps); \
         printf("%ldx%ldx%ld TA=%d TB=%d %dx%dx%d waves %dx%d: %.3f ms %.2f TF\n", s.m, s.n, s.k, TA, TB, BM, BN, BK, WM, WN, ms, fl / ms / 1e9); fflush(stdout); }
-        V(false, true, 128, 128, 16, 2, 4)
-        V(false, true, 128, 128, 16, 4, 4)
-        V(false, true, 128, 128, 32, 2, 4)
-        V(false, true, 128, 128, 32, 4, 4)
-        V(false, true, 256, 128, 16, 4, 4)
-        V(false, true, 128, 256, 16, 4, 4)
         V(false, true, 128, 128, 8, 2, 4)
-        V(false, true, 128, 64, 16, 2, 2)
-        V(false, true, 64, 128, 16, 2, 4)
-        V(false, false, 128, 128, 16, 2, 4)
-        V(false, false, 128, 128, 16, 4, 4)
-        V(false, false, 128, 128, 32, 2, 4)
-        V(true, false, 128, 128, 16, 2, 4)
+        V(false, true, 128, 128, 8, 2, 2)
+        V(false, true, 128, 128, 16, 2, 2)
+        V(false, true, 256, 128, 8, 4, 2)
+        V(false, true, 256, 128, 16, 4, 2)
+        V(false, true, 128, 256, 8, 2, 4)
+        V(false, true, 128, 256, 16, 2, 4)
     }
     return 0;
 }
