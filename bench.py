@@ -36,6 +36,8 @@ def flops(routine, n, m=None):
     if routine == "geqrf":
         m = m or n
         return 2 * m * n ** 2 + m * n - 2 * n ** 3 / 3 + n ** 2 + 14 * n / 3
+    if routine == "heev":
+        return 4 * n ** 3 / 3          # sytrd (stage-1 equivalent) flops, docs/latex/flops.tex:268
     raise ValueError(routine)
 
 
@@ -95,7 +97,8 @@ def main():
     ap.add_argument("--n", "--size", dest="n", type=int, default=32768)
     ap.add_argument("--m", "--rows", dest="m", type=int, default=None)
     ap.add_argument("--nb", type=int, default=512)
-    ap.add_argument("--routine", default="potrf", choices=["potrf", "getrf", "gemm", "geqrf"])
+    ap.add_argument("--routine", default="potrf", choices=["potrf", "getrf", "gemm", "geqrf", "heev"])
+    ap.add_argument("--vectors", type=int, default=1, help="heev: 1 = eigenvectors (dsyevd), 0 = values only")
     ap.add_argument("--lookahead", type=int, default=1)
     ap.add_argument("--grid", default=None, help="PxQ override")
     ap.add_argument("--check", type=int, default=1, help="residual check after timing (1 rank)")
@@ -133,6 +136,17 @@ def main():
         sl.generate_matrix(A, "rands", seed=7)
         T = sl.TriangularFactors()
         run = lambda: sl.geqrf(A, T, opts)
+    elif args.routine == "heev":
+        A = sl.HermitianMatrix(sl.Uplo.Lower, n, nb=nb, p=p, q=q, device=dev)
+        A.insertLocalTiles(device=dev)
+        sl.generate_matrix(A, "rands", seed=7)
+        Zm = None
+        if args.vectors:
+            Zm = sl.Matrix(n, n, nb=nb, p=p, q=q, device=dev)
+            Zm.insertLocalTiles(device=dev)
+        hopts = dict(opts)
+        hopts[sl.Option.InnerBlocking] = nb
+        run = lambda: sl.heev(A, None, Zm, hopts)
     else:
         A = sl.Matrix(n, n, nb=nb, p=p, q=q, device=dev)
         A.insertLocalTiles(device=dev)
@@ -164,7 +178,27 @@ def main():
     fl = flops(args.routine, n, args.m)
     gflops = fl * args.steps / dt_max / 1e9
     ok = (info == 0) if isinstance(info, int) else True
-    if rank == 0:
+    if rank == 0 and args.routine == "heev":
+        # BASELINE: time to solution (dsyevd n=16384 nb=256)
+        out = {
+            "metric": f"dsyev{'d' if args.vectors else ''} time to solution (n={n}, nb={nb})",
+            "value": round(dt_max / args.steps, 4),
+            "unit": "s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt_max / args.steps * 1e3, 3),
+            "higher_is_better": False,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "fp64",
+            "data": "synthetic (Philox random Hermitian matrix generated on device)",
+            "gflops_4n3_3": round(gflops, 2),
+            "config": {"model": f"dsyevd n={n} nb={nb}", "global_batch": 1, "seq_len": n, "n": n, "nb": nb,
+                       "grid": f"{p}x{q}", "parallelism": f"2d-block-cyclic {p}x{q}"},
+        }
+        print(json.dumps(out), flush=True)
+    elif rank == 0:
         out = {
             "metric": (f"d{args.routine} GFLOP/s (m={args.m or n}, n={n}, nb={nb})" if args.routine == "geqrf"
                        else f"d{args.routine} GFLOP/s (n={n}, nb={nb})"),

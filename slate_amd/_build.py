@@ -91,7 +91,8 @@ def build(verbose=False, hip=True, host=True):
     if host:
         out.append(_build_module(
             "_host", os.path.join(HERE, "csrc", "host"), [".cpp"], "g++",
-            ["-O3", "-std=c++17", "-fPIC", "-fopenmp", "-fvisibility=hidden", "-Wall", "-Wno-unused-function"] + inc,
+            ["-O3", "-march=x86-64-v3", "-fcx-limited-range", "-std=c++17", "-fPIC", "-fopenmp", "-fvisibility=hidden", "-Wall",
+             "-Wno-unused-function"] + inc,
             ["-fopenmp"], verbose))
     if host:
         # C ABI (include/slate_amd/c_api.h): embeds the Python runtime

@@ -20,6 +20,9 @@
 #include <algorithm>
 #include <cmath>
 #include <complex>
+#include <cstdlib>
+#include <thread>
+#include <atomic>
 #include <cstdint>
 #include <limits>
 #include <stdexcept>
@@ -83,29 +86,41 @@ void apply_left(Dense<T> A, i64 s, i64 k, const T* v, T tau, i64 lo, i64 hi) {
     }
 }
 
-// A[rows lo..hi, cols s..s+k-1] := A[...] H
+// A[rows lo..hi, cols s..s+k-1] := A[...] H, column-major friendly: y = A v
+// accumulated column by column (contiguous rows), then the rank-1 update
+// column by column (same summation order per row as the row-wise form)
 template <typename T>
 void apply_right(Dense<T> A, i64 s, i64 k, const T* v, T tau, i64 lo, i64 hi) {
-    if (tau == T(0)) return;
-    for (i64 r = lo; r <= hi; ++r) {
-        T y = 0;
-        for (i64 c = 0; c < k; ++c) y += A(r, s + c) * v[c];
-        y *= tau;
-        if (y == T(0)) continue;
-        for (i64 c = 0; c < k; ++c) A(r, s + c) -= y * cj(v[c]);
+    if (tau == T(0) || hi < lo) return;
+    const i64 nr = hi - lo + 1;
+    thread_local std::vector<T> y;
+    y.assign(nr, T(0));
+    for (i64 c = 0; c < k; ++c) {
+        const T vc = v[c];
+        const T* col = &A(lo, s + c);
+        for (i64 r = 0; r < nr; ++r) y[r] += col[r] * vc;
+    }
+    for (i64 r = 0; r < nr; ++r) y[r] *= tau;
+    for (i64 c = 0; c < k; ++c) {
+        const T vc = cj(v[c]);
+        T* col = &A(lo, s + c);
+        for (i64 r = 0; r < nr; ++r) col[r] -= y[r] * vc;
     }
 }
 
 struct Refl {            // reflector store (row-major count x b)
     void* V; void* tau; i64* row; i64* len; i64 b; i64 cap; i64 cnt = 0;
     template <typename T> void put(i64 r0, i64 k, const T* v, T t) {
-        if (cnt >= cap) throw std::runtime_error("reflector store overflow");
-        T* dst = static_cast<T*>(V) + cnt * b;
+        put_at(cnt, r0, k, v, t);
+        ++cnt;
+    }
+    template <typename T> void put_at(i64 idx, i64 r0, i64 k, const T* v, T t) {
+        if (idx >= cap) throw std::runtime_error("reflector store overflow");
+        T* dst = static_cast<T*>(V) + idx * b;
         for (i64 i = 0; i < k; ++i) dst[i] = v[i];
         for (i64 i = k; i < b; ++i) dst[i] = T(0);
-        static_cast<T*>(tau)[cnt] = t;
-        row[cnt] = r0; len[cnt] = k;
-        ++cnt;
+        static_cast<T*>(tau)[idx] = t;
+        row[idx] = r0; len[idx] = k;
     }
 };
 
@@ -151,6 +166,73 @@ i64 hb2st(i64 n, i64 b, T* a, i64 lda, Refl& st, i64* sweep_ptr) {
     }
     if (n >= 1) sweep_ptr[n - 1] = st.cnt;
     return st.cnt;
+}
+
+// Pipelined multi-threaded form (SLATE hb2st.cc runs the sweeps as OpenMP
+// tasks with the same progress dependencies).  Task t of sweep j (t = 0:
+// the column-j reflector, t >= 1: the t-th bulge) touches rows/columns
+// [s_t - w, e_t + w], s_t = j + 1 + t b; the windows of sweep j-1's tasks
+// t' > t + 1 + 2w/b lie strictly to the right.  So sweep j runs task t once
+// sweep j-1 has completed min(t + D, all) tasks: the result is bitwise the
+// sequential one (every pair of overlapping tasks keeps its order).  Thread
+// r owns sweeps r, r + T, ...; progress counters are release/acquire
+// atomics; reflectors go to fixed slots sweep_ptr[j] + t.
+template <typename T>
+i64 hb2st_mt(i64 n, i64 b, T* a, i64 lda, Refl& st, i64* sweep_ptr, int nthreads) {
+    Dense<T> A{a, lda};
+    const i64 w = 2 * b + 1;
+    const i64 D = 2 + (2 * w + b - 1) / b;
+    // task counts per sweep (same recurrence as the sequential chase)
+    std::vector<i64> ntask(std::max<i64>(n, 1), 0);
+    i64 total = 0;
+    for (i64 j = 0; j + 1 < n; ++j) {
+        sweep_ptr[j] = total;
+        i64 s = j + 1, e = std::min(j + b, n - 1);
+        if (e - s + 1 <= 1) continue;
+        i64 t = 1;
+        while (e + 1 <= n - 1) { e = std::min(e + b, n - 1); ++t; }
+        ntask[j] = t;
+        total += t;
+    }
+    if (n >= 1) sweep_ptr[n - 1] = total;
+    if (total > st.cap) throw std::runtime_error("reflector store overflow");
+    std::vector<std::atomic<i64>> done(std::max<i64>(n, 1));
+    for (auto& d : done) d.store(0, std::memory_order_relaxed);
+    const i64 nsw = std::max<i64>(n - 1, 0);
+    const int T_ = (int)std::max<i64>(1, std::min<i64>(nthreads, nsw));
+    auto worker = [&](int r) {
+        std::vector<T> v(b + 1);
+        for (i64 j = r; j < nsw; j += T_) {
+            const i64 nt = ntask[j];
+            i64 s = j + 1, e = std::min(j + b, n - 1), col = j;
+            for (i64 t = 0; t < nt; ++t) {
+                if (j > 0) {
+                    const i64 need = std::min(t + D, ntask[j - 1]);
+                    while (done[j - 1].load(std::memory_order_acquire) < need) std::this_thread::yield();
+                }
+                if (t > 0) { s = e + 1; e = std::min(e + b, n - 1); }
+                const i64 k = e - s + 1;
+                for (i64 q = 0; q < k; ++q) v[q] = A(s + q, col);
+                T tau; R_t<T> beta;
+                hgen(k, v.data(), tau, beta);
+                const i64 lo = std::max<i64>(0, s - w), hi = std::min(n - 1, e + w);
+                apply_left(A, s, k, v.data(), tau, lo, hi);
+                apply_right(A, s, k, v.data(), tau, lo, hi);
+                A(s, col) = T(beta); A(col, s) = T(beta);
+                for (i64 q = 1; q < k; ++q) { A(s + q, col) = T(0); A(col, s + q) = T(0); }
+                st.put_at(sweep_ptr[j] + t, s, k, v.data(), tau);
+                col = s;
+                done[j].store(t + 1, std::memory_order_release);
+            }
+            if (nt == 0) done[j].store(0, std::memory_order_release);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int r = 1; r < T_; ++r) th.emplace_back(worker, r);
+    worker(0);
+    for (auto& x : th) x.join();
+    st.cnt = total;
+    return total;
 }
 
 // ---------------------------------------------------------------- tb2bd
@@ -500,7 +582,11 @@ void register_eig(py::module& m) {
         dispatch(dt, [&](auto z) {
             using T = decltype(z);
             Refl st{(void*)V, (void*)tau, P<i64>(row), P<i64>(len), b, cap};
-            cnt = hb2st<T>(n, b, P<T>(A), lda, st, P<i64>(sweep_ptr));
+            int nth = 0;
+            if (const char* e = std::getenv("SLATE_AMD_HB2ST_THREADS")) nth = std::atoi(e);
+            if (nth <= 0) nth = (int)std::min<unsigned>(32u, std::max(1u, std::thread::hardware_concurrency()));
+            cnt = nth == 1 ? hb2st<T>(n, b, P<T>(A), lda, st, P<i64>(sweep_ptr))
+                           : hb2st_mt<T>(n, b, P<T>(A), lda, st, P<i64>(sweep_ptr), nth);
         });
         return cnt;
     });

@@ -136,3 +136,35 @@ def col_bcast(grid, src, owner_pr, kb, ncols, dtype, dev):
     if ncols:
         grid.col_comm.bcast(P, owner_pr)
     return P
+
+
+def rows_global(lr0, lr1, nb, p, pr, r0, dev):
+    """Panel-relative global rows (global - r0) of local rows [lr0, lr1) of
+    process row pr (block-cyclic, tile nb)."""
+    import numpy as np
+    lr = np.arange(lr0, lr1, dtype=np.int64)
+    g = ((lr // nb) * p + pr) * nb + lr % nb - r0
+    return torch.from_numpy(g).to(dev)
+
+
+def panel_allgather(colc, buf, mloc, t0, lc, kb, nb, p, pr, nloc_r, dt, dev):
+    """All-gather the rows at/after global tile t0 of the local columns
+    [lc, lc + kb) inside the process column; returns (P, myidx): P holds the
+    panel rows in GLOBAL order (row 0 = first row of tile t0), myidx the
+    panel rows of this rank's local rows (for the write-back)."""
+    cnt = [max(0, nloc_r[r] - min(tiles_local_before(t0, p, r) * nb, nloc_r[r])) for r in range(p)]
+    lr0 = min(tiles_local_before(t0, p, pr) * nb, mloc)
+    nmine = mloc - lr0
+    r0 = t0 * nb
+    mx = max(max(cnt), 1)
+    pad = ops.colmajor_zeros(mx, kb, dt, dev)
+    if nmine:
+        pad[:nmine].copy_(buf[lr0:mloc, lc:lc + kb])
+    allp = colc.allgather(pad.t()) if p > 1 else pad.t().unsqueeze(0)
+    P = ops.colmajor_empty(sum(cnt), kb, dt, dev)
+    for r in range(p):
+        if cnt[r]:
+            a = tiles_local_before(t0, p, r) * nb
+            ops.row_scatter(allp[r].t()[:cnt[r]], P, rows_global(a, a + cnt[r], nb, p, r, r0, dev))
+    myidx = rows_global(lr0, mloc, nb, p, pr, r0, dev)
+    return P, myidx

@@ -21,10 +21,9 @@ MI355X design:
 * back-transforms on the GPU: unmtr_hb2st applies one whole sweep of
   (disjoint) reflectors per launch; unmtr_he2hb is the blocked-WY GEMM
   update per panel.
-Multi-rank: ranks gather the matrix and run stage 1/2 redundantly
-(deterministic kernels); each rank back-transforms only its own columns of
-Z (the O(n^3) part is split over ranks) and scatters them into the
-block-cyclic Z.
+Multi-rank: `eig_dist.heev_dist` -- stage 1 on the process grid, the
+band reduced to rank 0 for stage 2, back-transforms on the grid; no rank
+holds the dense matrix.
 """
 from __future__ import annotations
 
@@ -311,8 +310,12 @@ def _rank_one_eig(dd, z, rho, Qb):
         Vs = zh[:, None] / (-delta)                      # v_j[i] = z_i / (d_i - lambda_j)
         Vs = Vs / Vs.norm(dim=0, keepdim=True)
         lam[K] = lamK
-        QK = Q[:, K.to(dev)]
-        Q[:, K.to(dev)] = QK @ Vs.to(dev)
+        Kd = K.to(dev)
+        QK = ops.as_colmajor(Q[:, Kd])
+        VsC = ops.as_colmajor(Vs.to(dev))
+        Out = ops.colmajor_empty(QK.shape[0], VsC.shape[1], Q.dtype, dev)
+        ops.gemm(1.0, QK, VsC, 0.0, Out)                 # merge GEMM on the MFMA kernels
+        Q[:, Kd] = Out
     if flip:
         lam = -lam
     o2 = torch.argsort(lam)
@@ -324,7 +327,12 @@ def heev(A, Lambda=None, Z=None, opts=None):
     """Eigenvalues (ascending, returned and copied into Lambda if given) and,
     if Z is given, eigenvectors of the Hermitian matrix A (A is destroyed
     like in SLATE)."""
+    import os
     from .aux import from_dense
+    s = A.storage
+    if s.bc is not None and (s.comm.size > 1 or os.environ.get("SLATE_AMD_EIG_DIST") == "1"):
+        from .eig_dist import heev_dist
+        return heev_dist(A, Lambda, Z, opts)
     with trace_block("heev"):
         s = A.storage
         dev = s.device if s.device.type == "cuda" else torch.device("cpu")
@@ -401,26 +409,26 @@ def eig(A, Lambda=None, Z=None, opts=None):
 def hegst(itype, A, B, opts=None):
     """Reduce the generalized problem to standard form with the Cholesky
     factor L of B (B = L L^H, from potrf): itype 1: A := L^{-1} A L^{-H};
-    itype 2/3: A := L^H A L."""
-    from .aux import from_dense, allgather_dense
+    itype 2/3: A := L^H A L (src/hegst.cc).  Works on a full-Hermitian
+    block-cyclic copy of A with the distributed trsm / trmm (no gather);
+    the stored triangle is copied back and the other one is untouched."""
+    from .blas3 import trsm, trmm
+    from .eig_dist import full_hermitian_copy
+    from .aux import copy
+    from ..core.matrix import TriangularMatrix
+    from ..core.enums import Diag, Side
     with trace_block("hegst"):
-        Ad = _dense_hermitian(A)
-        Bd = allgather_dense(B)
-        L = torch.tril(Bd) if B.uploPhysical() == Uplo.Lower else torch.triu(Bd).mH
-        dev = Ad.device
-        Lc, Ac = _cm(L.clone()), _cm(Ad.clone())
+        F = full_hermitian_copy(A)
+        lower = B.uploPhysical() == Uplo.Lower
+        Tb = TriangularMatrix(Uplo.Lower if lower else Uplo.Upper, B, diag=Diag.NonUnit)
+        L = Tb if lower else Tb.conj_transpose()          # B = L L^H
         if itype == 1:
-            ops.trsm('L', 'L', 'N', 'N', 1.0, Lc, Ac)
-            X = _cm(Ac.mH.contiguous())
-            ops.trsm('L', 'L', 'N', 'N', 1.0, Lc, X)
-            R = X.mH
+            trsm(Side.Left, 1.0, L, F, opts)                     # L^{-1} A
+            trsm(Side.Right, 1.0, L.conj_transpose(), F, opts)   # ... L^{-H}
         else:
-            ops.trmm('L', 'L', 'C' if Ad.dtype.is_complex else 'T', 'N', 1.0, Lc, Ac)
-            X = _cm(Ac.mH.contiguous())
-            ops.trmm('L', 'L', 'C' if Ad.dtype.is_complex else 'T', 'N', 1.0, Lc, X)
-            R = X.mH
-        R = 0.5 * (R + R.mH)
-        from_dense(A, _store_tri(R, A))
+            trmm(Side.Left, 1.0, L.conj_transpose(), F, opts)    # L^H A
+            trmm(Side.Right, 1.0, L, F, opts)                    # ... L
+        copy(TriangularMatrix(A.uploPhysical(), F), TriangularMatrix(A.uploPhysical(), A))
     return 0
 
 

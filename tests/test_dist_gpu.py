@@ -175,6 +175,19 @@ def _check_grid_gpu(rank, size, p, q):
     sl.geqrf(A, T)
     R = torch.triu(D(A)[: n // 2])
     assert ((R.mT @ R - A0.mT @ A0).norm() / (A0.norm() ** 2)).item() < 1e-14
+    # heev: he2hb on the grid, band to rank 0, grid back-transforms
+    m = 384
+    H = sl.HermitianMatrix(Uplo.Lower, m, nb=64, p=p, q=q, device=dev)
+    H.insertLocalTiles(device=0)
+    sl.generate_matrix(H, "rands", 6)
+    Hf = D(H)
+    Hf = torch.tril(Hf) + torch.tril(Hf, -1).mT
+    Z = sl.Matrix(m, m, nb=64, p=p, q=q, device=dev)
+    Z.insertLocalTiles(device=0)
+    w = sl.heev(H, None, Z)
+    Zd = D(Z)
+    w = w.to(Zd.device)
+    assert ((Hf @ Zd - Zd * w).abs().max() / (Hf.abs().max() * m)).item() < 1e-13
 
 
 @pytest.mark.parametrize("grid", [(2, 1), (1, 2), (2, 2)], ids=lambda g: f"{g[0]}x{g[1]}")

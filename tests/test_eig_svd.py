@@ -141,6 +141,36 @@ def test_eig_svd_distributed(grid):
     run_dist(_dist_eig, 2, *grid)
 
 
+def _dist_heev_only(rank, size, p, q):
+    for dt, uplo in ((torch.float64, Uplo.Lower), (torch.complex128, Uplo.Upper)):
+        _check_heev(100, 16, dt, uplo, MethodEig.DC, p, q)
+    _check_heev(77, 16, torch.float64, Uplo.Lower, MethodEig.QR, p, q)
+    # generalized problem: distributed hegst (trsm/trmm on a full copy)
+    n, nb = 64, 16
+    A = _herm(n, nb, torch.float64, Uplo.Lower, p, q, seed=4)
+    Bm = sl.HermitianMatrix(Uplo.Lower, n, nb=nb, p=p, q=q)
+    Bm.insertLocalTiles()
+    sl.generate_matrix(Bm, "poev", 5)
+    Af, Bf = E._dense_hermitian(A), E._dense_hermitian(Bm)
+    Z = sl.Matrix(n, n, nb=nb, p=p, q=q)
+    Z.insertLocalTiles()
+    w = sl.hegv(1, A, Bm, None, Z)
+    X = D(Z)
+    assert (Af @ X - Bf @ X * w).abs().max().item() / (Af.abs().max() * Bf.abs().max() * n).item() < 1e-12
+
+
+@pytest.mark.parametrize("grid", [(2, 2), (4, 1), (1, 3)], ids=lambda g: f"{g[0]}x{g[1]}")
+def test_heev_grid(grid):
+    """he2hb on the process grid (no dense gather), band to rank 0, grid back-transforms."""
+    run_dist(_dist_heev_only, grid[0] * grid[1], *grid)
+
+
+def test_heev_dist_path_one_rank(monkeypatch):
+    monkeypatch.setenv("SLATE_AMD_EIG_DIST", "1")
+    _check_heev(100, 16, torch.float64, Uplo.Lower, MethodEig.DC)
+    _check_heev(64, 16, torch.complex128, Uplo.Upper, MethodEig.QR)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("dt", [torch.float64, torch.complex128])
 def test_heev_gpu(dt):
