@@ -76,6 +76,109 @@ void slate_dgemm_(const char* ta, const char* tb, const int64_t* m, const int64_
                   const double* alpha, const double* a, const int64_t* lda, const double* b, const int64_t* ldb,
                   const double* beta, double* c, const int64_t* ldc);
 
+void slate_dposv_(const char* uplo, const int64_t* n, const int64_t* nrhs, double* a, const int64_t* lda,
+                  double* b, const int64_t* ldb, int64_t* info);
+void slate_dgetrf_(const int64_t* m, const int64_t* n, double* a, const int64_t* lda, int64_t* ipiv,
+                   int64_t* info);
+void slate_dgetrs_(const char* trans, const int64_t* n, const int64_t* nrhs, const double* a, const int64_t* lda,
+                   const int64_t* ipiv, double* b, const int64_t* ldb, int64_t* info);
+void slate_dpotrs_(const char* uplo, const int64_t* n, const int64_t* nrhs, const double* a, const int64_t* lda,
+                   double* b, const int64_t* ldb, int64_t* info);
+void slate_dpotri_(const char* uplo, const int64_t* n, double* a, const int64_t* lda, int64_t* info);
+void slate_dtrsm_(const char* side, const char* uplo, const char* transa, const char* diag, const int64_t* m,
+                  const int64_t* n, const double* alpha, const double* a, const int64_t* lda, double* b,
+                  const int64_t* ldb);
+void slate_dgels_(const char* trans, const int64_t* m, const int64_t* n, const int64_t* nrhs, double* a,
+                  const int64_t* lda, double* b, const int64_t* ldb, int64_t* info);
+void slate_dsyev_(const char* jobz, const char* uplo, const int64_t* n, double* a, const int64_t* lda, double* w,
+                  int64_t* info);
+double slate_dlange_(const char* norm, const int64_t* m, const int64_t* n, const double* a, const int64_t* lda);
+void slate_sgemm_(const char* ta, const char* tb, const int64_t* m, const int64_t* n, const int64_t* k,
+                  const float* alpha, const float* a, const int64_t* lda, const float* b, const int64_t* ldb,
+                  const float* beta, float* c, const int64_t* ldc);
+void slate_spotrf_(const char* uplo, const int64_t* n, float* a, const int64_t* lda, int64_t* info);
+void slate_sgesv_(const int64_t* n, const int64_t* nrhs, float* a, const int64_t* lda, int64_t* ipiv, float* b,
+                  const int64_t* ldb, int64_t* info);
+
+/* ------------------------------------------------------------------
+ * ScaLAPACK interface (SLATE scalapack_api/): p?xxx_ with the Fortran
+ * calling convention, 32-bit integers and 9-int descriptors
+ * [dtype, ctxt, m, n, mb, nb, rsrc, csrc, lld]; any global offsets ia/ja
+ * (1-based); rsrc = csrc = 0.  Each rank passes its local array.  Process
+ * grids come from the minimal BLACS below, over the ranks started with
+ * RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT (torchrun convention). */
+void Cblacs_pinfo(int* mypnum, int* nprocs);
+void Cblacs_get(int ctxt, int what, int* val);
+void Cblacs_gridinit(int* ctxt, const char* order, int nprow, int npcol);
+void Cblacs_gridinfo(int ctxt, int* nprow, int* npcol, int* myrow, int* mycol);
+void Cblacs_gridexit(int ctxt);
+void Cblacs_exit(int notdone);
+int numroc_(const int* n, const int* nb, const int* iproc, const int* isrcproc, const int* nprocs);
+void descinit_(int* desc, const int* m, const int* n, const int* mb, const int* nb, const int* irsrc,
+               const int* icsrc, const int* ictxt, const int* lld, int* info);
+
+#define SLATE_AMD_PDECL(X, T)                                                                                \
+    void p##X##potrf_(const char* uplo, const int* n, T* a, const int* ia, const int* ja, const int* desca,   \
+                      int* info);                                                                          \
+    void p##X##posv_(const char* uplo, const int* n, const int* nrhs, T* a, const int* ia, const int* ja,    \
+                     const int* desca, T* b, const int* ib, const int* jb, const int* descb, int* info);      \
+    void p##X##getrf_(const int* m, const int* n, T* a, const int* ia, const int* ja, const int* desca,      \
+                      int* ipiv, int* info);                                                               \
+    void p##X##gesv_(const int* n, const int* nrhs, T* a, const int* ia, const int* ja, const int* desca,    \
+                     int* ipiv, T* b, const int* ib, const int* jb, const int* descb, int* info);
+SLATE_AMD_PDECL(s, float)
+SLATE_AMD_PDECL(d, double)
+SLATE_AMD_PDECL(c, float)   /* complex: interleaved (re, im) */
+SLATE_AMD_PDECL(z, double)
+#undef SLATE_AMD_PDECL
+#define SLATE_AMD_PDECL_R(X, T)                                                                              \
+    void p##X##potrs_(const char* uplo, const int* n, const int* nrhs, const T* a, const int* ia,             \
+                      const int* ja, const int* desca, T* b, const int* ib, const int* jb, const int* descb,  \
+                      int* info);                                                                          \
+    void p##X##getrs_(const char* trans, const int* n, const int* nrhs, const T* a, const int* ia,           \
+                      const int* ja, const int* desca, const int* ipiv, T* b, const int* ib, const int* jb,  \
+                      const int* descb, int* info);                                                        \
+    void p##X##gemm_(const char* transa, const char* transb, const int* m, const int* n, const int* k,        \
+                     const T* alpha, const T* a, const int* ia, const int* ja, const int* desca, const T* b,  \
+                     const int* ib, const int* jb, const int* descb, const T* beta, T* c, const int* ic,      \
+                     const int* jc, const int* descc);                                                     \
+    void p##X##trsm_(const char* side, const char* uplo, const char* transa, const char* diag, const int* m, \
+                     const int* n, const T* alpha, const T* a, const int* ia, const int* ja, const int* desca, \
+                     T* b, const int* ib, const int* jb, const int* descb);                                 \
+    T p##X##lange_(const char* norm, const int* m, const int* n, const T* a, const int* ia, const int* ja,   \
+                   const int* desca, T* work);
+SLATE_AMD_PDECL_R(s, float)
+SLATE_AMD_PDECL_R(d, double)
+#undef SLATE_AMD_PDECL_R
+
+/* ------------------------------------------------------------------
+ * Distributed matrices by opaque handle (SLATE's slate_Matrix_create_* /
+ * slate_potrf_* C API, src/c_api/wrappers.cc).  kind: 'G' general,
+ * 'L' / 'U' Hermitian with that stored triangle; dtype 's','d','c','z';
+ * p x q process grid over all ranks; tiles nb x nb, 2D block-cyclic.
+ * The local data of this rank (mloc x nloc, column-major) is exchanged with
+ * host memory by get/set_local (device-resident under Target::Devices). */
+typedef int64_t slate_amd_matrix_t;
+typedef int64_t slate_amd_pivots_t;
+slate_amd_matrix_t slate_amd_matrix_create(char kind, char dtype, int64_t m, int64_t n, int64_t nb, int p, int q);
+int slate_amd_matrix_destroy(slate_amd_matrix_t A);
+int slate_amd_matrix_local_size(slate_amd_matrix_t A, int64_t* mloc, int64_t* nloc);
+int slate_amd_matrix_get_local(slate_amd_matrix_t A, void* dst, int64_t ld);
+int slate_amd_matrix_set_local(slate_amd_matrix_t A, const void* src, int64_t ld);
+/* kind 0: uniform random, 1: Hermitian positive definite, 2: normal */
+int slate_amd_matrix_generate(slate_amd_matrix_t A, int kind, int64_t seed);
+slate_amd_pivots_t slate_amd_pivots_create(void);
+int slate_amd_pivots_destroy(slate_amd_pivots_t piv);
+double slate_amd_norm(char norm, slate_amd_matrix_t A);
+int slate_amd_gemm(double alpha, slate_amd_matrix_t A, slate_amd_matrix_t B, double beta, slate_amd_matrix_t C);
+int slate_amd_potrf(slate_amd_matrix_t A);
+int slate_amd_posv(slate_amd_matrix_t A, slate_amd_matrix_t B);
+int slate_amd_getrf(slate_amd_matrix_t A, slate_amd_pivots_t piv);
+int slate_amd_getrs(slate_amd_matrix_t A, slate_amd_pivots_t piv, slate_amd_matrix_t B);
+int slate_amd_gesv(slate_amd_matrix_t A, slate_amd_pivots_t piv, slate_amd_matrix_t B);
+int slate_amd_gels(slate_amd_matrix_t A, slate_amd_matrix_t BX);
+int slate_amd_heev(slate_amd_matrix_t A, double* w, slate_amd_matrix_t Z);
+
 #ifdef __cplusplus
 }
 #endif

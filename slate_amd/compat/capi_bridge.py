@@ -71,3 +71,211 @@ def call(name, *args):
         nrm, m, n, a, lda = args
         return f(nrm, m, n, _arr(pfx, a, m, n, lda), lda)
     raise ValueError(name)
+
+
+# ---------------------------------------------------------------- ScaLAPACK
+# pd*_ symbols of libslate_amd_c.so: descriptors arrive as 9 ints, local
+# arrays as raw pointers sized from the descriptor (lld x local columns).
+def _desc_arr(pfx, ptr, desc):
+    from . import scalapack as S
+    ctxt, n, nb, csrc, lld = desc[1], desc[3], desc[5], desc[7], desc[8]
+    _, q, _, pc = S.blacs_gridinfo(ctxt)
+    nloc = S.numroc(n, nb, pc, csrc, q)
+    return _arr(pfx, ptr, max(lld, 1), nloc, max(lld, 1)) if nloc else np.zeros(0, dtype=_CT[pfx][1])
+
+
+def _local_rows(desc):
+    """(global row of each local row) of this rank for descriptor desc."""
+    from . import scalapack as S
+    ctxt, m, mb, rsrc = desc[1], desc[2], desc[4], desc[6]
+    p, _, pr, _ = S.blacs_gridinfo(ctxt)
+    mloc = S.numroc(m, mb, pr, rsrc, p)
+    lr = np.arange(mloc, dtype=np.int64)
+    return ((lr // mb) * p + pr) * mb + lr % mb
+
+
+def _ipiv_to_local(piv, ia, desc, ip):
+    """ScaLAPACK ipiv is distributed like the rows of A: local row i holds
+    the (1-based, global) pivot row of global row l2g(i).  piv: pivots of
+    the sub-matrix at ia, 1-based relative to it."""
+    g = _local_rows(desc)
+    out = np.ctypeslib.as_array((ctypes.c_int32 * max(len(g), 1)).from_address(ip))
+    off = int(ia) - 1
+    for i, gr in enumerate(g):
+        k = gr - off
+        if 0 <= k < len(piv):
+            out[i] = off + int(piv[k])
+
+
+def _ipiv_from_local(ip, ia, n, desc):
+    """Rebuild the sub-matrix pivot vector (1-based, relative to ia) from the
+    distributed ipiv: every rank contributes its rows, one max-reduction."""
+    import torch
+    from ..parallel import comm as C
+    g = _local_rows(desc)
+    loc = np.ctypeslib.as_array((ctypes.c_int32 * max(len(g), 1)).from_address(ip))
+    off = int(ia) - 1
+    full = torch.zeros(n, dtype=torch.int64)
+    for i, gr in enumerate(g):
+        k = gr - off
+        if 0 <= k < n:
+            full[k] = int(loc[i]) - off
+    w = C.world()
+    if w.size > 1:
+        w.allreduce(full, "max")
+    return full.numpy()
+
+
+def scalapack_call(name, *args):
+    """ScaLAPACK entry points by name ('pdpotrf', ...): args are plain values,
+    pointers and 9-int descriptors (as tuples)."""
+    from . import scalapack as S
+    pfx, rt = name[1], name[2:]
+    f = getattr(S, name)
+    if rt == "gemm":
+        ta, tb, m, n, k, al, a, ia, ja, da, b, ib, jb, db, be, c, ic, jc, dc = args
+        return f(ta, tb, m, n, k, al, _desc_arr(pfx, a, da), ia, ja, da, _desc_arr(pfx, b, db), ib, jb, db, be,
+                 _desc_arr(pfx, c, dc), ic, jc, dc)
+    if rt == "potrf":
+        uplo, n, a, ia, ja, da = args
+        return f(uplo, n, _desc_arr(pfx, a, da), ia, ja, da)
+    if rt in ("potrs", "posv"):
+        uplo, n, nrhs, a, ia, ja, da, b, ib, jb, db = args
+        return f(uplo, n, nrhs, _desc_arr(pfx, a, da), ia, ja, da, _desc_arr(pfx, b, db), ib, jb, db)
+    if rt == "getrf":
+        m, n, a, ia, ja, da, ip = args
+        piv = np.zeros(min(m, n), dtype=np.int64)
+        info = f(m, n, _desc_arr(pfx, a, da), ia, ja, da, piv)
+        _ipiv_to_local(piv, ia, da, ip)
+        return info
+    if rt in ("getrs", "gesv"):
+        if rt == "getrs":
+            t, n, nrhs, a, ia, ja, da, ip, b, ib, jb, db = args
+            piv = _ipiv_from_local(ip, ia, n, da)
+            return f(t, n, nrhs, _desc_arr(pfx, a, da), ia, ja, da, piv, _desc_arr(pfx, b, db), ib, jb, db)
+        n, nrhs, a, ia, ja, da, ip, b, ib, jb, db = args
+        piv = np.zeros(n, dtype=np.int64)
+        info = f(n, nrhs, _desc_arr(pfx, a, da), ia, ja, da, piv, _desc_arr(pfx, b, db), ib, jb, db)
+        _ipiv_to_local(piv, ia, da, ip)
+        return info
+    if rt == "trsm":
+        side, uplo, ta, diag, m, n, al, a, ia, ja, da, b, ib, jb, db = args
+        return f(side, uplo, ta, diag, m, n, al, _desc_arr(pfx, a, da), ia, ja, da, _desc_arr(pfx, b, db), ib, jb,
+                 db)
+    if rt == "lange":
+        nrm, m, n, a, ia, ja, da = args
+        return f(nrm, m, n, _desc_arr(pfx, a, da), ia, ja, da)
+    raise ValueError(name)
+
+
+def blacs(op, *args):
+    """Minimal BLACS over torch.distributed: pinfo, gridinit, gridinfo."""
+    from . import scalapack as S
+    from ..parallel import comm as C
+    import slate_amd
+    if op == "init":
+        slate_amd.init()
+        w = C.world()
+        return w.rank * 100000 + w.size        # packed (rank, size)
+    if op == "gridinit":
+        order, p, q = args
+        slate_amd.init()
+        return S.blacs_gridinit(p, q, chr(order))
+    if op == "gridinfo":
+        p, q, pr, pc = S.blacs_gridinfo(args[0])
+        return ((p * 10000 + q) * 10000 + pr) * 10000 + pc
+    raise ValueError(op)
+
+
+# ---------------------------------------------------------------- handles
+# Opaque matrix handles of the C API (SLATE's slate_Matrix_create_* family,
+# src/c_api/wrappers.cc): an integer id -> the distributed matrix object.
+_H = {}
+_NEXT = [1]
+
+
+def _tdt(pfx):
+    import torch
+    return {'s': torch.float32, 'd': torch.float64, 'c': torch.complex64, 'z': torch.complex128}[pfx]
+
+
+def _put(obj):
+    h = _NEXT[0]
+    _NEXT[0] += 1
+    _H[h] = obj
+    return h
+
+
+def handle(op, *args):
+    import torch
+    import slate_amd as sl
+    if op == "create":
+        kind, pfx, m, n, nb, p, q = args
+        sl.init()
+        dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+        dt = _tdt(chr(pfx))
+        k = chr(kind)
+        if k == 'G':
+            M = sl.Matrix(m, n, nb=nb, p=p, q=q, dtype=dt, device=dev)
+        elif k in ('L', 'U'):
+            M = sl.HermitianMatrix(sl.Uplo.Lower if k == 'L' else sl.Uplo.Upper, n, nb=nb, p=p, q=q, dtype=dt,
+                                   device=dev)
+        else:
+            raise ValueError(k)
+        M.insertLocalTiles(device=dev.index if dev.type == "cuda" else -1)
+        return _put(M)
+    if op == "destroy":
+        _H.pop(args[0], None)
+        return 0
+    if op == "pivots_create":
+        return _put(sl.Pivots())
+    if op == "local_size":
+        lb = _H[args[0]].local_block()
+        return lb.mloc * 1000000000 + lb.nloc
+    if op in ("get_local", "set_local"):
+        h, ptr, ld = args
+        M = _H[h]
+        lb = M.local_block()
+        pfx = {torch.float32: 's', torch.float64: 'd', torch.complex64: 'c', torch.complex128: 'z'}[M.storage.dtype]
+        if lb.mloc == 0 or lb.nloc == 0:
+            return 0
+        host = torch.from_numpy(_arr(pfx, ptr, lb.mloc, lb.nloc, ld)).as_strided((lb.mloc, lb.nloc), (1, ld))
+        if op == "get_local":
+            host.copy_(lb.data.cpu())
+        else:
+            lb.data.copy_(host.to(lb.data.device))
+            M.storage.mark_local_modified(M.storage.origin_slot)
+        return 0
+    if op == "generate":
+        h, kind, seed = args
+        sl.generate_matrix(_H[h], {0: "rands", 1: "poev", 2: "randn"}[kind], seed)
+        return 0
+    if op == "norm":
+        h, nrm = args
+        return float(sl.norm(sl.Norm.from_string(chr(nrm)), _H[h]))
+    if op == "gemm":
+        al, ha, hb, be, hc = args
+        sl.gemm(al, _H[ha], _H[hb], be, _H[hc])
+        return 0
+    if op == "potrf":
+        return sl.potrf(_H[args[0]])
+    if op == "posv":
+        return sl.posv(_H[args[0]], _H[args[1]])
+    if op == "getrf":
+        return sl.getrf(_H[args[0]], _H[args[1]])
+    if op == "getrs":
+        sl.getrs(_H[args[0]], _H[args[1]], _H[args[2]])
+        return 0
+    if op == "gesv":
+        ha, hp, hb = args
+        return sl.gesv(_H[ha], _H[hp], _H[hb])
+    if op == "geqrf_gels":
+        ha, hb = args
+        return sl.gels(_H[ha], sl.TriangularFactors(), _H[hb])
+    if op == "heev":
+        ha, wptr, hz = args
+        w = sl.heev(_H[ha], None, _H[hz] if hz else None)
+        n = w.numel()
+        np.ctypeslib.as_array((ctypes.c_double * max(n, 1)).from_address(wptr))[:n] = w.cpu().numpy()
+        return 0
+    raise ValueError(op)

@@ -13,7 +13,10 @@ follow ScaLAPACK: desc = [dtype, ctxt, m, n, mb, nb, rsrc, csrc, lld].
 Local arrays (numpy or torch, host or device) are wrapped zero-copy when
 already on the target device; host arrays are staged to the rank's GPU
 for Target=devices (SLATE_AMD_SCALAPACK_TARGET=host|devices).  Global
-sub-matrix offsets ia, ja must be 1 (whole distributed matrices) and
+sub-matrix offsets ia, ja (1-based) may be anything: a sub-matrix that does
+not start on a tile corner is moved into an aligned work matrix on the same
+grid by the piece-level redistribution (`parallel/redist.py`: each element
+moves at most once, nothing is gathered) and moved back afterwards.
 rsrc = csrc = 0.
 """
 from __future__ import annotations
@@ -118,9 +121,28 @@ class _Loc:
             self.user.copy_(self.work.to(self.user.device).to(self.user.dtype))
 
 
-def _chk(ia, ja):
-    if int(ia) != 1 or int(ja) != 1:
-        raise SlateError("scalapack: ia = ja = 1 required (whole matrices)")
+def _sub(L, ia, ja, m, n, kind=Matrix, **kw):
+    """The (m x n) global sub-matrix at 1-based (ia, ja) of the ScaLAPACK
+    array L as a driver-ready matrix of ``kind``, and a finisher that moves
+    an aligned work copy back (no-op for whole matrices)."""
+    ia, ja, m, n = int(ia), int(ja), int(m), int(n)
+    if ia == 1 and ja == 1 and m == L.m and n == L.n:
+        return L.matrix(kind, **kw), (lambda: None)
+    from ..models.aux import copy
+    full = L.matrix()
+    view = full.slice(ia - 1, ia - 1 + m - 1, ja - 1, ja - 1 + n - 1)
+    s = full.storage
+    W = Matrix(m, n, nb=L.nb, mb=L.mb, p=L.p, q=L.q, comm=_comm.world(), dtype=s.dtype, device=s.device,
+               order=L.order)
+    W.insertLocalTiles(device=s.device.index if s.device.type == "cuda" else -1)
+    copy(view, W)
+    if kind is HermitianMatrix:
+        M = HermitianMatrix(kw["uplo"], W)
+    elif kind is TriangularMatrix:
+        M = TriangularMatrix(kw["uplo"], W, diag=kw["diag"])
+    else:
+        M = W
+    return M, (lambda: copy(W, view))
 
 
 def _uplo(u):
@@ -142,27 +164,34 @@ def _make(pfx):
 
     def gemm(transa, transb, m, n, k, alpha, a, ia, ja, desca, b, ib, jb, descb, beta, c, ic, jc, descc):
         from ..models.blas3 import gemm as _g
-        _chk(ia, ja), _chk(ib, jb), _chk(ic, jc)
         A, B, C = _Loc(a, desca, dt), _Loc(b, descb, dt), _Loc(c, descc, dt)
-        _g(alpha, _opm(A.matrix(), _op(transa)), _opm(B.matrix(), _op(transb)), beta, C.matrix(), _opts())
+        ta, tb = _op(transa), _op(transb)
+        Am, _ = _sub(A, ia, ja, *((m, k) if ta == Op.NoTrans else (k, m)))
+        Bm, _ = _sub(B, ib, jb, *((k, n) if tb == Op.NoTrans else (n, k)))
+        Cm, done = _sub(C, ic, jc, m, n)
+        _g(alpha, _opm(Am, ta), _opm(Bm, tb), beta, Cm, _opts())
+        done()
         C.writeback()
         return 0
     g["gemm"] = gemm
 
     def potrf(uplo, n, a, ia, ja, desca):
         from ..models.chol import potrf as _p
-        _chk(ia, ja)
         A = _Loc(a, desca, dt)
-        info = _p(A.matrix(HermitianMatrix, uplo=_uplo(uplo)), _opts())
+        Am, done = _sub(A, ia, ja, n, n, HermitianMatrix, uplo=_uplo(uplo))
+        info = _p(Am, _opts())
+        done()
         A.writeback()
         return info
     g["potrf"] = potrf
 
     def potrs(uplo, n, nrhs, a, ia, ja, desca, b, ib, jb, descb):
         from ..models.chol import potrs as _p
-        _chk(ia, ja), _chk(ib, jb)
         A, B = _Loc(a, desca, dt), _Loc(b, descb, dt)
-        _p(A.matrix(HermitianMatrix, uplo=_uplo(uplo)), B.matrix(), _opts())
+        Am, _ = _sub(A, ia, ja, n, n, HermitianMatrix, uplo=_uplo(uplo))
+        Bm, done = _sub(B, ib, jb, n, nrhs)
+        _p(Am, Bm, _opts())
+        done()
         B.writeback()
         return 0
     g["potrs"] = potrs
@@ -175,12 +204,13 @@ def _make(pfx):
     g["posv"] = posv
 
     def getrf(m, n, a, ia, ja, desca, ipiv):
-        """ipiv: global 1-based pivots (length min(m, n)) on return."""
+        """ipiv: 1-based pivots relative to the sub-matrix (length min(m, n))."""
         from ..models.lu import getrf as _g
-        _chk(ia, ja)
         A = _Loc(a, desca, dt)
+        Am, done = _sub(A, ia, ja, m, n)
         piv = Pivots()
-        info = _g(A.matrix(), piv, _opts())
+        info = _g(Am, piv, _opts())
+        done()
         A.writeback()
         p = (piv.ipiv.cpu() + 1)
         if isinstance(ipiv, np.ndarray):
@@ -192,12 +222,14 @@ def _make(pfx):
 
     def getrs(trans, n, nrhs, a, ia, ja, desca, ipiv, b, ib, jb, descb):
         from ..models.lu import getrs as _g
-        _chk(ia, ja), _chk(ib, jb)
         A, B = _Loc(a, desca, dt), _Loc(b, descb, dt)
         ip = torch.as_tensor(np.asarray(ipiv) if isinstance(ipiv, np.ndarray) else ipiv.cpu()).to(torch.int64)
         piv = Pivots()
         piv.set(ip[:n] - 1, A.nb)
-        _g(_opm(A.matrix(), _op(trans)), piv, B.matrix(), _opts())
+        Am, _ = _sub(A, ia, ja, n, n)
+        Bm, done = _sub(B, ib, jb, n, nrhs)
+        _g(_opm(Am, _op(trans)), piv, Bm, _opts())
+        done()
         B.writeback()
         return 0
     g["getrs"] = getrs
@@ -211,47 +243,56 @@ def _make(pfx):
 
     def trsm(side, uplo, transa, diag, m, n, alpha, a, ia, ja, desca, b, ib, jb, descb):
         from ..models.blas3 import trsm as _t
-        _chk(ia, ja), _chk(ib, jb)
         A, B = _Loc(a, desca, dt), _Loc(b, descb, dt)
-        T = A.matrix(TriangularMatrix, uplo=_uplo(uplo), diag=Diag.Unit if str(diag).upper()[0] == 'U'
-                     else Diag.NonUnit)
-        _t(Side.Left if str(side).upper()[0] == 'L' else Side.Right, alpha, _opm(T, _op(transa)), B.matrix(),
-           _opts())
+        left = str(side).upper()[0] == 'L'
+        k = m if left else n
+        T, _ = _sub(A, ia, ja, k, k, TriangularMatrix, uplo=_uplo(uplo),
+                    diag=Diag.Unit if str(diag).upper()[0] == 'U' else Diag.NonUnit)
+        Bm, done = _sub(B, ib, jb, m, n)
+        _t(Side.Left if left else Side.Right, alpha, _opm(T, _op(transa)), Bm, _opts())
+        done()
         B.writeback()
         return 0
     g["trsm"] = trsm
 
     def geqrf(m, n, a, ia, ja, desca, tau=None):
         from ..models.qr import geqrf as _q
-        _chk(ia, ja)
         A = _Loc(a, desca, dt)
+        Am, done = _sub(A, ia, ja, m, n)
         T = TriangularFactors()
-        _q(A.matrix(), T, _opts())
+        _q(Am, T, _opts())
+        done()
         A.writeback()
         return T
     g["geqrf"] = geqrf
 
     def gels(trans, m, n, nrhs, a, ia, ja, desca, b, ib, jb, descb):
         from ..models.qr import gels as _g
-        _chk(ia, ja), _chk(ib, jb)
         A, B = _Loc(a, desca, dt), _Loc(b, descb, dt)
-        _g(_opm(A.matrix(), _op(trans)), TriangularFactors(), B.matrix(), _opts())
+        Am, done_a = _sub(A, ia, ja, m, n)
+        Bm, done = _sub(B, ib, jb, max(m, n), nrhs)
+        _g(_opm(Am, _op(trans)), TriangularFactors(), Bm, _opts())
+        done()
+        done_a()
+        A.writeback()
         B.writeback()
         return 0
     g["gels"] = gels
 
     def lange(norm, m, n, a, ia, ja, desca):
         from ..models.aux import norm as _n
-        _chk(ia, ja)
-        return float(_n(Norm.from_string(str(norm)), _Loc(a, desca, dt).matrix()))
+        Am, _ = _sub(_Loc(a, desca, dt), ia, ja, m, n)
+        return float(_n(Norm.from_string(str(norm)), Am))
     g["lange"] = lange
 
     def heev(jobz, uplo, n, a, ia, ja, desca, w, z=None, iz=1, jz=1, descz=None):
         from ..models.eig import heev as _h
-        _chk(ia, ja)
         A = _Loc(a, desca, dt)
         Z = _Loc(z, descz, dt) if str(jobz).upper()[0] == 'V' else None
-        vals = _h(A.matrix(HermitianMatrix, uplo=_uplo(uplo)), None, Z.matrix() if Z else None, _opts())
+        Am, _ = _sub(A, ia, ja, n, n, HermitianMatrix, uplo=_uplo(uplo))
+        Zm, done = _sub(Z, iz, jz, n, n) if Z else (None, lambda: None)
+        vals = _h(Am, None, Zm, _opts())
+        done()
         if Z:
             Z.writeback()
         if isinstance(w, np.ndarray):
@@ -264,7 +305,8 @@ def _make(pfx):
     def gesvd(jobu, jobvt, m, n, a, ia, ja, desca, s, u=None, iu=1, ju=1, descu=None, vt=None, ivt=1, jvt=1,
               descvt=None):
         from ..models.svd import svd as _s
-        _chk(ia, ja)
+        if int(ia) != 1 or int(ja) != 1:
+            raise SlateError("pgesvd: ia = ja = 1 required")
         A = _Loc(a, desca, dt)
         U = _Loc(u, descu, dt) if str(jobu).upper()[0] == 'V' else None
         VT = _Loc(vt, descvt, dt) if str(jobvt).upper()[0] == 'V' else None

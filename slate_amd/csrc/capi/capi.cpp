@@ -15,7 +15,10 @@
 namespace {
 
 std::mutex g_mu;
-PyObject* g_call = nullptr;
+PyObject* g_call = nullptr;       // capi_bridge.call            (LAPACK-style)
+PyObject* g_scal = nullptr;       // capi_bridge.scalapack_call  (p?xxx_)
+PyObject* g_blacs = nullptr;      // capi_bridge.blacs           (Cblacs_*)
+PyObject* g_handle = nullptr;     // capi_bridge.handle          (matrix handles)
 bool g_owned = false;
 thread_local std::string g_err;
 
@@ -39,6 +42,9 @@ bool ensure() {
         return false;
     }
     g_call = PyObject_GetAttrString(mod, "call");
+    g_scal = PyObject_GetAttrString(mod, "scalapack_call");
+    g_blacs = PyObject_GetAttrString(mod, "blacs");
+    g_handle = PyObject_GetAttrString(mod, "handle");
     Py_DECREF(mod);
     PyGILState_Release(st);
     if (g_owned) PyEval_SaveThread();   // release the GIL held by the init thread
@@ -47,12 +53,12 @@ bool ensure() {
 
 // fmt: Py_BuildValue format of the arguments after the routine name
 template <typename... A>
-double invoke(const char* name, const char* fmt, A... args) {
+double invoke_on(PyObject** fn, const char* name, const char* fmt, A... args) {
     if (!ensure()) return SLATE_AMD_ERR_INIT;
     PyGILState_STATE st = PyGILState_Ensure();
     std::string f = std::string("(s") + fmt + ")";
     PyObject* targs = Py_BuildValue(f.c_str(), name, args...);
-    PyObject* r = targs ? PyObject_CallObject(g_call, targs) : nullptr;
+    PyObject* r = targs ? PyObject_CallObject(*fn, targs) : nullptr;
     Py_XDECREF(targs);
     double out = SLATE_AMD_ERR_INTERNAL;
     if (!r) {
@@ -68,6 +74,9 @@ double invoke(const char* name, const char* fmt, A... args) {
     PyGILState_Release(st);
     return out;
 }
+
+template <typename... A>
+double invoke(const char* name, const char* fmt, A... args) { return invoke_on(&g_call, name, fmt, args...); }
 
 inline long long P(const void* p) { return (long long)(uintptr_t)p; }
 inline int I(double v) { return (int)v; }
@@ -178,6 +187,235 @@ void slate_dgemm_(const char* ta, const char* tb, const int64_t* m, const int64_
                   const double* alpha, const double* a, const int64_t* lda, const double* b, const int64_t* ldb,
                   const double* beta, double* c, const int64_t* ldc) {
     slate_dgemm(*ta, *tb, *m, *n, *k, *alpha, a, *lda, b, *ldb, *beta, c, *ldc);
+}
+void slate_dposv_(const char* uplo, const int64_t* n, const int64_t* nrhs, double* a, const int64_t* lda,
+                  double* b, const int64_t* ldb, int64_t* info) {
+    *info = slate_dposv(*uplo, *n, *nrhs, a, *lda, b, *ldb);
+}
+void slate_dgetrf_(const int64_t* m, const int64_t* n, double* a, const int64_t* lda, int64_t* ipiv,
+                   int64_t* info) {
+    *info = slate_dgetrf(*m, *n, a, *lda, ipiv);
+}
+void slate_dgetrs_(const char* t, const int64_t* n, const int64_t* nrhs, const double* a, const int64_t* lda,
+                   const int64_t* ipiv, double* b, const int64_t* ldb, int64_t* info) {
+    *info = slate_dgetrs(*t, *n, *nrhs, a, *lda, ipiv, b, *ldb);
+}
+void slate_dpotrs_(const char* uplo, const int64_t* n, const int64_t* nrhs, const double* a, const int64_t* lda,
+                   double* b, const int64_t* ldb, int64_t* info) {
+    *info = slate_dpotrs(*uplo, *n, *nrhs, a, *lda, b, *ldb);
+}
+void slate_dpotri_(const char* uplo, const int64_t* n, double* a, const int64_t* lda, int64_t* info) {
+    *info = slate_dpotri(*uplo, *n, a, *lda);
+}
+void slate_dtrsm_(const char* side, const char* uplo, const char* ta, const char* diag, const int64_t* m,
+                  const int64_t* n, const double* alpha, const double* a, const int64_t* lda, double* b,
+                  const int64_t* ldb) {
+    slate_dtrsm(*side, *uplo, *ta, *diag, *m, *n, *alpha, a, *lda, b, *ldb);
+}
+void slate_dgels_(const char* t, const int64_t* m, const int64_t* n, const int64_t* nrhs, double* a,
+                  const int64_t* lda, double* b, const int64_t* ldb, int64_t* info) {
+    *info = slate_dgels(*t, *m, *n, *nrhs, a, *lda, b, *ldb);
+}
+void slate_dsyev_(const char* jobz, const char* uplo, const int64_t* n, double* a, const int64_t* lda, double* w,
+                  int64_t* info) {
+    *info = slate_dsyev(*jobz, *uplo, *n, a, *lda, w);
+}
+double slate_dlange_(const char* norm, const int64_t* m, const int64_t* n, const double* a, const int64_t* lda) {
+    return slate_dlange(*norm, *m, *n, a, *lda);
+}
+void slate_sgemm_(const char* ta, const char* tb, const int64_t* m, const int64_t* n, const int64_t* k,
+                  const float* alpha, const float* a, const int64_t* lda, const float* b, const int64_t* ldb,
+                  const float* beta, float* c, const int64_t* ldc) {
+    slate_sgemm(*ta, *tb, *m, *n, *k, *alpha, a, *lda, b, *ldb, *beta, c, *ldc);
+}
+void slate_spotrf_(const char* uplo, const int64_t* n, float* a, const int64_t* lda, int64_t* info) {
+    *info = slate_spotrf(*uplo, *n, a, *lda);
+}
+void slate_sgesv_(const int64_t* n, const int64_t* nrhs, float* a, const int64_t* lda, int64_t* ipiv, float* b,
+                  const int64_t* ldb, int64_t* info) {
+    *info = slate_sgesv(*n, *nrhs, a, *lda, ipiv, b, *ldb);
+}
+
+// ------------------------------------------------------------------ BLACS
+// Minimal BLACS over torch.distributed (no MPI here): the process grid of a
+// context is created by Cblacs_gridinit over the world of ranks started with
+// RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT (torchrun convention).
+void Cblacs_pinfo(int* mypnum, int* nprocs) {
+    const double v = invoke_on(&g_blacs, "init", "");
+    const long long x = (long long)v;
+    *mypnum = (int)(x / 100000);
+    *nprocs = (int)(x % 100000);
+}
+void Cblacs_get(int /*ctxt*/, int /*what*/, int* val) { *val = 0; }
+void Cblacs_gridinit(int* ctxt, const char* order, int nprow, int npcol) {
+    const char o = (order && (order[0] == 'R' || order[0] == 'r')) ? 'R' : 'C';
+    *ctxt = (int)invoke_on(&g_blacs, "gridinit", "iii", (int)o, nprow, npcol);
+}
+void Cblacs_gridinfo(int ctxt, int* nprow, int* npcol, int* myrow, int* mycol) {
+    const long long x = (long long)invoke_on(&g_blacs, "gridinfo", "i", ctxt);
+    *mycol = (int)(x % 10000);
+    *myrow = (int)((x / 10000) % 10000);
+    *npcol = (int)((x / 100000000) % 10000);
+    *nprow = (int)(x / 1000000000000LL);
+}
+void Cblacs_gridexit(int) {}
+void Cblacs_exit(int) {}
+
+int numroc_(const int* n, const int* nb, const int* iproc, const int* isrcproc, const int* nprocs) {
+    const int mydist = (*nprocs + *iproc - *isrcproc) % *nprocs;
+    const int nblocks = *n / *nb;
+    int num = (nblocks / *nprocs) * *nb;
+    const int extra = nblocks % *nprocs;
+    if (mydist < extra) num += *nb;
+    else if (mydist == extra) num += *n % *nb;
+    return num;
+}
+void descinit_(int* desc, const int* m, const int* n, const int* mb, const int* nb, const int* irsrc,
+               const int* icsrc, const int* ictxt, const int* lld, int* info) {
+    desc[0] = 1; desc[1] = *ictxt; desc[2] = *m; desc[3] = *n; desc[4] = *mb; desc[5] = *nb;
+    desc[6] = *irsrc; desc[7] = *icsrc; desc[8] = *lld;
+    *info = (*m < 0) ? -2 : (*n < 0) ? -3 : (*mb < 1) ? -4 : (*nb < 1) ? -5 : 0;
+}
+
+// -------------------------------------------------------------- ScaLAPACK
+// p?xxx_ interposers (SLATE scalapack_api/scalapack_*.cc): Fortran calling
+// convention, 32-bit integers, descriptors of 9 ints.
+#define D9 "(iiiiiiiii)"
+#define DV(d) d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7], d[8]
+
+#define SLATE_AMD_SCALAPACK_REAL(X, T)                                                                     \
+    void p##X##potrf_(const char* uplo, const int* n, T* a, const int* ia, const int* ja, const int* desca,   \
+                      int* info) {                                                                         \
+        *info = I(invoke_on(&g_scal, "p" #X "potrf", "CiLii" D9, (int)*uplo, *n, P(a), *ia, *ja, DV(desca)));  \
+    }                                                                                                      \
+    void p##X##potrs_(const char* uplo, const int* n, const int* nrhs, const T* a, const int* ia,             \
+                      const int* ja, const int* desca, T* b, const int* ib, const int* jb, const int* descb,  \
+                      int* info) {                                                                         \
+        *info = I(invoke_on(&g_scal, "p" #X "potrs", "CiiLii" D9 "Lii" D9, (int)*uplo, *n, *nrhs, P(a), *ia,   \
+                            *ja, DV(desca), P(b), *ib, *jb, DV(descb)));                                    \
+    }                                                                                                      \
+    void p##X##posv_(const char* uplo, const int* n, const int* nrhs, T* a, const int* ia, const int* ja,    \
+                     const int* desca, T* b, const int* ib, const int* jb, const int* descb, int* info) {     \
+        *info = I(invoke_on(&g_scal, "p" #X "posv", "CiiLii" D9 "Lii" D9, (int)*uplo, *n, *nrhs, P(a), *ia,    \
+                            *ja, DV(desca), P(b), *ib, *jb, DV(descb)));                                    \
+    }                                                                                                      \
+    void p##X##getrf_(const int* m, const int* n, T* a, const int* ia, const int* ja, const int* desca,      \
+                      int* ipiv, int* info) {                                                              \
+        *info = I(invoke_on(&g_scal, "p" #X "getrf", "iiLii" D9 "L", *m, *n, P(a), *ia, *ja, DV(desca),      \
+                            P(ipiv)));                                                                      \
+    }                                                                                                      \
+    void p##X##getrs_(const char* t, const int* n, const int* nrhs, const T* a, const int* ia, const int* ja, \
+                      const int* desca, const int* ipiv, T* b, const int* ib, const int* jb,                 \
+                      const int* descb, int* info) {                                                       \
+        *info = I(invoke_on(&g_scal, "p" #X "getrs", "CiiLii" D9 "LLii" D9, (int)*t, *n, *nrhs, P(a), *ia,     \
+                            *ja, DV(desca), P(ipiv), P(b), *ib, *jb, DV(descb)));                           \
+    }                                                                                                      \
+    void p##X##gesv_(const int* n, const int* nrhs, T* a, const int* ia, const int* ja, const int* desca,    \
+                     int* ipiv, T* b, const int* ib, const int* jb, const int* descb, int* info) {           \
+        *info = I(invoke_on(&g_scal, "p" #X "gesv", "iiLii" D9 "LLii" D9, *n, *nrhs, P(a), *ia, *ja,          \
+                            DV(desca), P(ipiv), P(b), *ib, *jb, DV(descb)));                                \
+    }                                                                                                      \
+    void p##X##gemm_(const char* ta, const char* tb, const int* m, const int* n, const int* k,                \
+                     const T* alpha, const T* a, const int* ia, const int* ja, const int* desca, const T* b,  \
+                     const int* ib, const int* jb, const int* descb, const T* beta, T* c, const int* ic,      \
+                     const int* jc, const int* descc) {                                                    \
+        invoke_on(&g_scal, "p" #X "gemm", "CCiiidLii" D9 "Lii" D9 "dLii" D9, (int)*ta, (int)*tb, *m, *n, *k,   \
+                  (double)*alpha, P(a), *ia, *ja, DV(desca), P(b), *ib, *jb, DV(descb), (double)*beta, P(c),   \
+                  *ic, *jc, DV(descc));                                                                    \
+    }                                                                                                      \
+    void p##X##trsm_(const char* side, const char* uplo, const char* ta, const char* diag, const int* m,     \
+                     const int* n, const T* alpha, const T* a, const int* ia, const int* ja, const int* desca, \
+                     T* b, const int* ib, const int* jb, const int* descb) {                                \
+        invoke_on(&g_scal, "p" #X "trsm", "CCCCiidLii" D9 "Lii" D9, (int)*side, (int)*uplo, (int)*ta,          \
+                  (int)*diag, *m, *n, (double)*alpha, P(a), *ia, *ja, DV(desca), P(b), *ib, *jb, DV(descb));    \
+    }                                                                                                      \
+    T p##X##lange_(const char* norm, const int* m, const int* n, const T* a, const int* ia, const int* ja,   \
+                   const int* desca, T* /*work*/) {                                                        \
+        return (T)invoke_on(&g_scal, "p" #X "lange", "CiiLii" D9, (int)*norm, *m, *n, P(a), *ia, *ja,          \
+                            DV(desca));                                                                     \
+    }
+
+SLATE_AMD_SCALAPACK_REAL(s, float)
+SLATE_AMD_SCALAPACK_REAL(d, double)
+#undef SLATE_AMD_SCALAPACK_REAL
+
+// complex: the factorizations / solves (alpha-free), interleaved (re, im)
+#define SLATE_AMD_SCALAPACK_CPLX(X, R)                                                                     \
+    void p##X##potrf_(const char* uplo, const int* n, R* a, const int* ia, const int* ja, const int* desca,   \
+                      int* info) {                                                                         \
+        *info = I(invoke_on(&g_scal, "p" #X "potrf", "CiLii" D9, (int)*uplo, *n, P(a), *ia, *ja, DV(desca)));  \
+    }                                                                                                      \
+    void p##X##getrf_(const int* m, const int* n, R* a, const int* ia, const int* ja, const int* desca,      \
+                      int* ipiv, int* info) {                                                              \
+        *info = I(invoke_on(&g_scal, "p" #X "getrf", "iiLii" D9 "L", *m, *n, P(a), *ia, *ja, DV(desca),      \
+                            P(ipiv)));                                                                      \
+    }                                                                                                      \
+    void p##X##gesv_(const int* n, const int* nrhs, R* a, const int* ia, const int* ja, const int* desca,    \
+                     int* ipiv, R* b, const int* ib, const int* jb, const int* descb, int* info) {           \
+        *info = I(invoke_on(&g_scal, "p" #X "gesv", "iiLii" D9 "LLii" D9, *n, *nrhs, P(a), *ia, *ja,          \
+                            DV(desca), P(ipiv), P(b), *ib, *jb, DV(descb)));                                \
+    }                                                                                                      \
+    void p##X##posv_(const char* uplo, const int* n, const int* nrhs, R* a, const int* ia, const int* ja,    \
+                     const int* desca, R* b, const int* ib, const int* jb, const int* descb, int* info) {     \
+        *info = I(invoke_on(&g_scal, "p" #X "posv", "CiiLii" D9 "Lii" D9, (int)*uplo, *n, *nrhs, P(a), *ia,    \
+                            *ja, DV(desca), P(b), *ib, *jb, DV(descb)));                                    \
+    }
+
+SLATE_AMD_SCALAPACK_CPLX(c, float)
+SLATE_AMD_SCALAPACK_CPLX(z, double)
+#undef SLATE_AMD_SCALAPACK_CPLX
+
+// ------------------------------------------------------ matrix handles
+slate_amd_matrix_t slate_amd_matrix_create(char kind, char dtype, int64_t m, int64_t n, int64_t nb, int p, int q) {
+    return (slate_amd_matrix_t)invoke_on(&g_handle, "create", "iiLLLii", (int)kind, (int)dtype, (long long)m,
+                                         (long long)n, (long long)nb, p, q);
+}
+int slate_amd_matrix_destroy(slate_amd_matrix_t h) { return I(invoke_on(&g_handle, "destroy", "L", (long long)h)); }
+int slate_amd_matrix_local_size(slate_amd_matrix_t h, int64_t* mloc, int64_t* nloc) {
+    const double v = invoke_on(&g_handle, "local_size", "L", (long long)h);
+    if (v < 0) return I(v);
+    const long long x = (long long)v;
+    *mloc = x / 1000000000LL;
+    *nloc = x % 1000000000LL;
+    return 0;
+}
+int slate_amd_matrix_get_local(slate_amd_matrix_t h, void* dst, int64_t ld) {
+    return I(invoke_on(&g_handle, "get_local", "LLL", (long long)h, P(dst), (long long)ld));
+}
+int slate_amd_matrix_set_local(slate_amd_matrix_t h, const void* src, int64_t ld) {
+    return I(invoke_on(&g_handle, "set_local", "LLL", (long long)h, P(src), (long long)ld));
+}
+int slate_amd_matrix_generate(slate_amd_matrix_t h, int kind, int64_t seed) {
+    return I(invoke_on(&g_handle, "generate", "LiL", (long long)h, kind, (long long)seed));
+}
+slate_amd_pivots_t slate_amd_pivots_create(void) {
+    return (slate_amd_pivots_t)invoke_on(&g_handle, "pivots_create", "");
+}
+int slate_amd_pivots_destroy(slate_amd_pivots_t h) { return I(invoke_on(&g_handle, "destroy", "L", (long long)h)); }
+double slate_amd_norm(char norm, slate_amd_matrix_t A) {
+    return invoke_on(&g_handle, "norm", "Li", (long long)A, (int)norm);
+}
+int slate_amd_gemm(double alpha, slate_amd_matrix_t A, slate_amd_matrix_t B, double beta, slate_amd_matrix_t C) {
+    return I(invoke_on(&g_handle, "gemm", "dLLdL", alpha, (long long)A, (long long)B, beta, (long long)C));
+}
+int slate_amd_potrf(slate_amd_matrix_t A) { return I(invoke_on(&g_handle, "potrf", "L", (long long)A)); }
+int slate_amd_posv(slate_amd_matrix_t A, slate_amd_matrix_t B) {
+    return I(invoke_on(&g_handle, "posv", "LL", (long long)A, (long long)B));
+}
+int slate_amd_getrf(slate_amd_matrix_t A, slate_amd_pivots_t piv) {
+    return I(invoke_on(&g_handle, "getrf", "LL", (long long)A, (long long)piv));
+}
+int slate_amd_getrs(slate_amd_matrix_t A, slate_amd_pivots_t piv, slate_amd_matrix_t B) {
+    return I(invoke_on(&g_handle, "getrs", "LLL", (long long)A, (long long)piv, (long long)B));
+}
+int slate_amd_gesv(slate_amd_matrix_t A, slate_amd_pivots_t piv, slate_amd_matrix_t B) {
+    return I(invoke_on(&g_handle, "gesv", "LLL", (long long)A, (long long)piv, (long long)B));
+}
+int slate_amd_gels(slate_amd_matrix_t A, slate_amd_matrix_t BX) {
+    return I(invoke_on(&g_handle, "geqrf_gels", "LL", (long long)A, (long long)BX));
+}
+int slate_amd_heev(slate_amd_matrix_t A, double* w, slate_amd_matrix_t Z) {
+    return I(invoke_on(&g_handle, "heev", "LLL", (long long)A, P(w), (long long)Z));
 }
 
 }  // extern "C"

@@ -339,6 +339,12 @@ def add(alpha, A, beta, B, opts=None):
     sB = B.storage
     if not (A.storage.bc is not None and sB.bc is not None and A.op() == B.op() == Op.NoTrans):
         raise SlateError("add: block-cyclic NoTrans matrices required")
+    if not _same_layout(A, B):
+        # bring A onto B's layout first (piece-level exchange), then add locally
+        T = B.emptyLike()
+        T.insertLocalTiles(device=sB.device.index if sB.device.type == "cuda" else -1)
+        redistribute(A, T)
+        A = T
     la, lb = A.local_block(), B.local_block()
     if lb.mloc and lb.nloc:
         if B.uploPhysical() == Uplo.General:
@@ -352,9 +358,23 @@ def add(alpha, A, beta, B, opts=None):
     return B
 
 
+def _same_layout(A, B):
+    """True when op(A) and op(B) put every element on the same rank at the
+    same local position (then copies are purely local)."""
+    a, b = A.storage.bc, B.storage.bc
+    if a is None or b is None or A.op() != B.op():
+        return False
+    if (a.mb, a.nb, a.p, a.q, a.order, a.pr, a.pc) != (b.mb, b.nb, b.p, b.q, b.order, b.pr, b.pc):
+        return False
+    if A.storage.comm is not B.storage.comm and A.storage.comm.ranks != B.storage.comm.ranks:
+        return False
+    return A.global_offsets() == B.global_offsets() and (A.m(), A.n()) == (B.m(), B.n())
+
+
 def copy(A, B, opts=None):
-    """B = A with precision conversion (src/copy.cc); same distribution."""
-    if A.storage.bc is not None and B.storage.bc is not None and A.op() == B.op():
+    """B = A with precision conversion (src/copy.cc): a local copy when the
+    layouts coincide, the piece-level redistribution otherwise."""
+    if _same_layout(A, B):
         la, lb = A.local_block(), B.local_block()
         if lb.mloc and lb.nloc:
             if B.uploPhysical() == Uplo.General:

@@ -159,3 +159,48 @@ def test_fortran_module(tmp_path):
     r = subprocess.run([exe], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
     assert r.returncode == 0, r.stdout
     assert "dgesv info=0" in r.stdout and "dposv info=0" in r.stdout
+
+
+def _build_c(tmp_path, src, name):
+    import os
+    import subprocess
+    import sysconfig
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "slate_amd")
+    exe = str(tmp_path / name)
+    cmd = ["gcc", "-O1", os.path.join(root, "examples", "c", src), "-I", os.path.join(root, "include"),
+           "-L", lib, "-lslate_amd_c", "-Wl,-rpath," + lib, "-L", sysconfig.get_config_var("LIBDIR"),
+           "-lpython" + sysconfig.get_config_var("LDVERSION"), "-lm", "-o", exe]
+    subprocess.run(cmd, check=True)
+    return exe, root
+
+
+@pytest.mark.parametrize("grid", ["1x1", "1x2", "2x1"])
+def test_c_scalapack_and_handles(tmp_path, grid):
+    """pdposv_/pdgesv_ on sub-matrices starting inside a tile, pdgemm_, the
+    minimal BLACS and the handle API -- from C, one process per rank."""
+    import os
+    import subprocess
+    from dist_util import _free_port
+    exe, root = _build_c(tmp_path, "ex_scalapack.c", "ex_scalapack")
+    p, q = map(int, grid.split("x"))
+    size = p * q
+    port = str(_free_port())
+    procs = []
+    for r in range(size):
+        env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""),
+                   SLATE_AMD_SCALAPACK_TARGET="host", OMP_NUM_THREADS="2")
+        if size > 1:
+            env.update(RANK=str(r), WORLD_SIZE=str(size), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                       MASTER_PORT=port)
+        procs.append(subprocess.Popen([exe, grid], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                      text=True))
+    outs = [pr.communicate(timeout=300)[0] for pr in procs]
+    for pr, out in zip(procs, outs):
+        assert pr.returncode == 0, out
+        lines = [ln for ln in out.splitlines() if ln.startswith("rank ")]
+        assert len(lines) == 4, out
+        for ln in lines:
+            assert "info=0" in ln or "pdgemm" in ln, ln
+            val = float(ln.split("=")[-1])
+            assert val < 1e-9, ln
