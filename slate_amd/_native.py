@@ -13,8 +13,15 @@ import torch
 
 from .core.exceptions import HipError
 
+_host_override = os.environ.get("SLATE_AMD_HOST_LIB")    # e.g. the sanitizer build (tools/asan)
 try:
-    from . import _host  # noqa: F401
+    if _host_override:
+        import importlib.util as _ilu
+        _spec = _ilu.spec_from_file_location("slate_amd._host", _host_override)
+        _host = _ilu.module_from_spec(_spec)
+        _spec.loader.exec_module(_host)
+    else:
+        from . import _host  # noqa: F401
 except ImportError as e:  # pragma: no cover - build problem
     raise ImportError(
         "slate_amd._host is not built; run `python slate_amd/_build.py` "

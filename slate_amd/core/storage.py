@@ -312,8 +312,12 @@ class MatrixStorage:
                 self.tile_data(i, j, o).copy_(self.tile_data(i, j, src))
 
     def mark_local_modified(self, slot):
-        """After a whole-local-buffer kernel wrote `slot`."""
+        """After a whole-local-buffer kernel wrote `slot` (the post-condition
+        of every driver: with SLATE_AMD_DEBUG=1 the MOSI checker runs here)."""
         self.table.mark_all(slot, _host.MOSI_Modified)
+        from ..utils.debug import Debug
+        if Debug.enabled():
+            Debug.assert_mosi(self, "mark_local_modified")
 
     def prepare_local(self, slot) -> torch.Tensor:
         """Make the contiguous local buffer valid in `slot` and return it."""
@@ -346,6 +350,9 @@ class MatrixStorage:
                                                    (i, j, srcs[0]) not in self.tiles):
                             self.local_tile_view(slot, i, j).copy_(sd)
                     self.table.set_state(i, j, slot, _host.MOSI_Shared)
+            from ..utils.debug import Debug
+            if Debug.enabled():
+                Debug.assert_mosi(self, "prepare_local")
             return self.local[slot]
 
     def sync_origin(self):

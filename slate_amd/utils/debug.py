@@ -56,6 +56,47 @@ class Debug:
         return "\n".join(lines)
 
     @staticmethod
+    def check_mosi(storage, values=True) -> list:
+        """MOSI coherency checker (SURVEY §5.2 race/consistency detection;
+        SLATE checks the same invariants with asserts in MatrixStorage.hh):
+        for every local tile (a) at most one copy is Modified, (b) a
+        Modified copy has only Invalid siblings, (c) no copy is left OnHold,
+        and with ``values`` (d) copies that are both valid hold equal data.
+        Returns the violations as strings (empty: coherent)."""
+        from .. import _native
+        H = _native._host
+        MOD, SH, INV, HOLD = H.MOSI_Modified, H.MOSI_Shared, H.MOSI_Invalid, H.MOSI_OnHold
+        s = storage
+        bad = []
+        per = {}
+        for (i, j, slot) in s.table.instances():
+            if s.tileIsLocal(i, j):
+                per.setdefault((i, j), {})[slot] = int(s.table.state(i, j, slot))
+        for (i, j), st in per.items():
+            mods = [x for x, v in st.items() if v & MOD]
+            if len(mods) > 1:
+                bad.append(f"tile ({i},{j}): Modified in slots {mods}")
+            if mods and any(not (v & INV) for x, v in st.items() if x != mods[0]):
+                bad.append(f"tile ({i},{j}): Modified in slot {mods[0]} but a sibling is still valid {st}")
+            if any(v & HOLD for v in st.values()):
+                bad.append(f"tile ({i},{j}): left OnHold {st}")
+            if values and len(st) > 1:
+                valid = [x for x, v in st.items() if not (v & INV)]
+                if len(valid) > 1:
+                    a = s.tile_data(i, j, valid[0])
+                    b = s.tile_data(i, j, valid[1])
+                    if a is not None and b is not None and not torch.equal(a.cpu(), b.cpu()):
+                        bad.append(f"tile ({i},{j}): valid copies in slots {valid} differ")
+        return bad
+
+    @staticmethod
+    def assert_mosi(storage, where=""):
+        bad = Debug.check_mosi(storage)
+        if bad:
+            from ..core.exceptions import SlateError
+            raise SlateError(f"MOSI check failed{(' after ' + where) if where else ''}: " + "; ".join(bad[:8]))
+
+    @staticmethod
     def check_pool_leaks() -> dict:
         """Bytes still allocated in the slab pools (should be 0 after all
         matrices are freed)."""
