@@ -99,6 +99,7 @@ def main():
     ap.add_argument("--nb", type=int, default=512)
     ap.add_argument("--routine", default="potrf", choices=["potrf", "getrf", "gemm", "geqrf", "heev"])
     ap.add_argument("--vectors", type=int, default=1, help="heev: 1 = eigenvectors (dsyevd), 0 = values only")
+    ap.add_argument("--band", type=int, default=0, help="heev: stage-1 bandwidth (default min(nb, 64))")
     ap.add_argument("--lookahead", type=int, default=1)
     ap.add_argument("--grid", default=None, help="PxQ override")
     ap.add_argument("--check", type=int, default=1, help="residual check after timing (1 rank)")
@@ -145,7 +146,8 @@ def main():
             Zm = sl.Matrix(n, n, nb=nb, p=p, q=q, device=dev)
             Zm.insertLocalTiles(device=dev)
         hopts = dict(opts)
-        hopts[sl.Option.InnerBlocking] = nb
+        if args.band:
+            hopts[sl.Option.InnerBlocking] = args.band
         run = lambda: sl.heev(A, None, Zm, hopts)
     else:
         A = sl.Matrix(n, n, nb=nb, p=p, q=q, device=dev)

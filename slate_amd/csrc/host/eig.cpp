@@ -132,7 +132,6 @@ template <typename T>
 i64 hb2st(i64 n, i64 b, T* a, i64 lda, Refl& st, i64* sweep_ptr) {
     Dense<T> A{a, lda};
     std::vector<T> v(b + 1), v2(b + 1);
-    const i64 w = 2 * b + 1;   // band + bulge half-width
     for (i64 j = 0; j + 1 < n; ++j) {
         sweep_ptr[j] = st.cnt;
         i64 s = j + 1, e = std::min(j + b, n - 1), k = e - s + 1;
@@ -141,7 +140,7 @@ i64 hb2st(i64 n, i64 b, T* a, i64 lda, Refl& st, i64* sweep_ptr) {
         T tau; R_t<T> beta;
         hgen(k, v.data(), tau, beta);
         // two-sided on rows/cols s..e over the window
-        i64 lo = std::max<i64>(0, s - w), hi = std::min(n - 1, e + w);
+        i64 lo = j + 1, hi = std::min(n - 1, e + b);      // window: see hb2st_mt
         apply_left(A, s, k, v.data(), tau, lo, hi);
         apply_right(A, s, k, v.data(), tau, lo, hi);
         A(s, j) = T(beta); A(j, s) = T(beta);
@@ -155,7 +154,7 @@ i64 hb2st(i64 n, i64 b, T* a, i64 lda, Refl& st, i64* sweep_ptr) {
             for (i64 r = 0; r < k2; ++r) v2[r] = A(s2 + r, s);
             T tau2; R_t<T> beta2;
             hgen(k2, v2.data(), tau2, beta2);
-            i64 lo2 = std::max<i64>(0, s2 - w), hi2 = std::min(n - 1, e2 + w);
+            i64 lo2 = s + 1, hi2 = std::min(n - 1, e2 + b);
             apply_left(A, s2, k2, v2.data(), tau2, lo2, hi2);
             apply_right(A, s2, k2, v2.data(), tau2, lo2, hi2);
             A(s2, s) = T(beta2); A(s, s2) = T(beta2);
@@ -180,8 +179,11 @@ i64 hb2st(i64 n, i64 b, T* a, i64 lda, Refl& st, i64* sweep_ptr) {
 template <typename T>
 i64 hb2st_mt(i64 n, i64 b, T* a, i64 lda, Refl& st, i64* sweep_ptr, int nthreads) {
     Dense<T> A{a, lda};
-    const i64 w = 2 * b + 1;
-    const i64 D = 2 + (2 * w + b - 1) / b;
+    // task window: rows/columns [col + 1, e + b] (col: the column being
+    // annihilated, overwritten explicitly; e + b: band + the bulge the
+    // right application creates), width <= 3b; windows of sweep j-1 lie
+    // strictly right of sweep j's task t from its task t + 3 on
+    const i64 D = 4;
     // task counts per sweep (same recurrence as the sequential chase)
     std::vector<i64> ntask(std::max<i64>(n, 1), 0);
     i64 total = 0;
@@ -215,7 +217,7 @@ i64 hb2st_mt(i64 n, i64 b, T* a, i64 lda, Refl& st, i64* sweep_ptr, int nthreads
                 for (i64 q = 0; q < k; ++q) v[q] = A(s + q, col);
                 T tau; R_t<T> beta;
                 hgen(k, v.data(), tau, beta);
-                const i64 lo = std::max<i64>(0, s - w), hi = std::min(n - 1, e + w);
+                const i64 lo = col + 1, hi = std::min(n - 1, e + b);
                 apply_left(A, s, k, v.data(), tau, lo, hi);
                 apply_right(A, s, k, v.data(), tau, lo, hi);
                 A(s, col) = T(beta); A(col, s) = T(beta);

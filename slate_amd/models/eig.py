@@ -336,7 +336,10 @@ def heev(A, Lambda=None, Z=None, opts=None):
     with trace_block("heev"):
         s = A.storage
         dev = s.device if s.device.type == "cuda" else torch.device("cpu")
-        nb = int(get_option(opts, Option.InnerBlocking, 0)) or min(s.bc.nb if s.bc else 64, 128)
+        # stage-1 band: 64 by default, independent of the tile size (stage 2
+        # costs O(n^2 band) on the host; the bulge chase parallelises over
+        # n / (4 band) concurrent tasks)
+        nb = int(get_option(opts, Option.InnerBlocking, 0)) or min(s.bc.nb if s.bc else 64, 64)
         method = get_option(opts, Option.MethodEig, MethodEig.DC)
         Af = _cm(_dense_hermitian(A).to(dev))
         n = Af.shape[0]

@@ -54,13 +54,13 @@ def _new_general(A, m=None, n=None, p=None, q=None, nb=None):
     return M
 
 
-def full_hermitian_copy(A):
-    """General block-cyclic copy of Hermitian A holding both triangles
-    (piece-level redistribution of the stored triangle and its conjugate
-    transpose; no gather)."""
+def full_hermitian_copy(A, nb=None):
+    """General block-cyclic copy of Hermitian A holding both triangles, with
+    tile size nb (default A's) -- piece-level redistribution of the stored
+    triangle and its conjugate transpose; no gather."""
     from .aux import copy, copy_conj_transpose, set as aset, set_diag_imag_zero
     from ..core.matrix import TriangularMatrix as TM
-    F = _new_general(A)
+    F = _new_general(A, nb=nb)
     aset(0.0, 0.0, F)
     up = A.uploPhysical()
     stored = TM(up, A)
@@ -126,9 +126,6 @@ def he2hb_dist(F, opts=None):
                 if q > 1:
                     grid.row_comm.bcast(pk.raw, ck)
             Fac.panels.append((k, r0, kk, pk.prefix("V").get("T")))
-            if nloc - lc1 == 0 and nmine == 0:
-                # still take part in the collectives below
-                pass
             with trace_block("he2hb::update"):
                 plan = plan_col_gather(s.tileMb, k + 1, nt, nb, p, q, pc, dev)
                 X = ops.colmajor_empty(nmine, kk, dt, dev)
@@ -260,7 +257,9 @@ def heev_dist(A, Lambda=None, Z=None, opts=None):
     comm = s.comm
     n = A.n()
     with trace_block("heev"):
-        F = full_hermitian_copy(A)
+        # stage-1 band = F's tile size: InnerBlocking, default min(nb, 64)
+        band = int(get_option(opts, Option.InnerBlocking, 0) or 0) or min(s.bc.nb, 64)
+        F = full_hermitian_copy(A, nb=band)
         dev = F.storage.local[F.storage.origin_slot].device
         amax = float(norm(Norm.Max, F))
         sc = 1.0
@@ -312,9 +311,14 @@ def heev_dist(A, Lambda=None, Z=None, opts=None):
                 E.unmtr_hb2st(F2, Zl)
                 lb.data[:n, :lb.nloc].copy_(Zl)
             Zc.storage.mark_local_modified(Zc.storage.origin_slot)
-            if Z1 is not None:
-                redistribute(Z1, Z)
-            unmtr_he2hb_dist(F, Fac, Z)
+            # Q1 needs Z on F's row distribution (tile size = band)
+            same = Z.storage.bc.mb == nb and Z.storage.bc.p == F.storage.bc.p
+            Zg = Z if same else _new_general(F, n, n)
+            if Z1 is not None or not same:
+                redistribute(Z1 if Z1 is not None else Z, Zg)
+            unmtr_he2hb_dist(F, Fac, Zg)
+            if Zg is not Z:
+                redistribute(Zg, Z)
         if sc != 1.0:
             w = w / sc
         if Lambda is not None:
