@@ -72,19 +72,32 @@ def plan_col_gather(tileMb, tfirst, tend, nb, p, q, pc, dev, cols_from=None):
     return meta, torch.tensor(flat if flat else [0], dtype=torch.int64, device=dev)
 
 
-def plan_col_gathers_steps(tileMb, g0, nt, nb, p, q, pc, dev):
+def plan_col_gathers_steps(tileMb, g0, nt, nb, p, q, pc, dev, split=None):
     """One plan per factorization step t (potrf: the rows below the
-    diagonal tile g0+t), all uploaded as ONE index tensor."""
+    diagonal tile g0+t), all uploaded as ONE index tensor.  With ``split``
+    = la, each step gets two plans: the lookahead tiles g+1 .. g+la (the
+    critical path) and the rest (the trailing update, off the critical
+    path)."""
     flat, metas = [], []
     for t in range(nt):
         g = g0 + t
-        metas.append(_append_plan(flat, *_rows_plan(tileMb, g + 1, g0 + nt, nb, p, q, pc, g + 1), p))
+        if split is None:
+            metas.append(_append_plan(flat, *_rows_plan(tileMb, g + 1, g0 + nt, nb, p, q, pc, g + 1), p))
+        else:
+            e = min(g + 1 + split, g0 + nt)
+            metas.append((_append_plan(flat, *_rows_plan(tileMb, g + 1, e, nb, p, q, pc, g + 1), p),
+                          _append_plan(flat, *_rows_plan(tileMb, g + 1, g0 + nt, nb, p, q, pc, e), p)))
     idx = torch.tensor(flat if flat else [0], dtype=torch.int64, device=dev)
-    return [(m, idx) for m in metas]
+    if split is None:
+        return [(m, idx) for m in metas]
+    return [((a, idx), (b, idx)) for a, b in metas]
 
 
-def assemble_cols(plan, Prow, grid, p, kb, dtype, dev):
-    """Lcol (rows = this rank's local columns of the panel range)."""
+def assemble_cols(plan, Prow, grid, p, kb, dtype, dev, comm=None):
+    """Lcol (rows = this rank's local columns of the panel range); the
+    column broadcasts go over ``comm`` (default the grid's column
+    communicator)."""
+    comm = comm or grid.col_comm
     m, idx = plan
     tot = m["tot"]
     Rbuf = ops.colmajor_empty(tot, kb, dtype, dev)
@@ -97,12 +110,12 @@ def assemble_cols(plan, Prow, grid, p, kb, dtype, dev):
                 ops.row_gather(Prow, chunk, idx[o:o + cnt])
             if p > 1:
                 if chunk.is_contiguous() or cnt == 0:
-                    grid.col_comm.bcast(chunk, r)
+                    comm.bcast(chunk, r)
                 else:
                     tmp = ops.colmajor_empty(cnt, kb, dtype, dev)
                     if grid.pr == r:
                         tmp.copy_(chunk)
-                    grid.col_comm.bcast(tmp, r)
+                    comm.bcast(tmp, r)
                     chunk.copy_(tmp)
         pos += cnt
     o, cnt = m["order"]

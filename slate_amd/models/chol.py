@@ -89,7 +89,10 @@ def _potrf_lower(A, opts):
     lc_end = _lstart(R_end, nb, pc, q)
     ss = StreamSet(dev, reserve_cus=0)   # one-CU panel kernels: no reserved CUs (measured: 49.0 vs 45.1 TF/s with 32)
     infos = torch.zeros(max(nt, 1), dtype=torch.int64, device=dev)
-    plans = plan_col_gathers_steps(s.tileMb, g0, nt, nb, p, q, pc, dev) if (p > 1 or q > 1) else None
+    # per step: the lookahead tiles' transposed rows (critical path, panel
+    # stream) and the rest (update stream, its own column communicator)
+    plans = plan_col_gathers_steps(s.tileMb, g0, nt, nb, p, q, pc, dev, split=la) if (p > 1 or q > 1) else None
+    colu = grid.col_comm_u if (grid is not None and p > 1) else None
     ev_tr = {}
     ss.fork()
     for t in range(nt):
@@ -132,11 +135,12 @@ def _potrf_lower(A, opts):
                         grid.row_comm.bcast(Prow, g % q)
                 else:
                     Prow = buf[lr1:lr_end, lcg:lcg + kb]
-                # panel -> column (exactly the tiles this process column needs)
+                # panel -> column: the lookahead tiles' rows now, the rest on
+                # the update stream below
                 if plans is not None:
-                    Lcol = assemble_cols(plans[t], Prow, grid, p, kb, dtype, dev)
+                    Lla = assemble_cols(plans[t][0], Prow, grid, p, kb, dtype, dev)
                 else:
-                    Lcol = Prow
+                    Lla = Lcol = Prow
             # lookahead columns g+1 .. g+la
             lc_la = min(tiles_local_before(g + 1 + la, q, pc) * nb, lc_end)
             # the newest lookahead column g+la was in step t-1's trailing
@@ -145,7 +149,7 @@ def _potrf_lower(A, opts):
                 ss.wait(ss.panel, ev_tr[t - 1])
             if lc_la > lc1 and nrow:
                 mask = (1, nb, p, pr, q, pc, lr1, lc1, 0)
-                ops.gemm(-1.0, Prow, Lcol[0:lc_la - lc1], 1.0, buf[lr1:lr_end, lc1:lc_la], 'N', ct, mask)
+                ops.gemm(-1.0, Prow, Lla[0:lc_la - lc1], 1.0, buf[lr1:lr_end, lc1:lc_la], 'N', ct, mask)
             ev_panel = ss.event(ss.panel)
         # trailing update
         us = ss.update[0]
@@ -157,12 +161,16 @@ def _potrf_lower(A, opts):
             lc_nx = max(lc_nx, lc_la)
             if Prow.is_cuda and lc_end > lc_la and nrow:
                 Prow.record_stream(us)
-                Lcol.record_stream(us)
             with trace_block("potrf::trailing"):
+                if plans is not None:
+                    Lcol = assemble_cols(plans[t][1], Prow, grid, p, kb, dtype, dev, comm=colu)
+                    loff = lc_la            # Lcol row 0 = local column lc_la
+                else:
+                    loff = lc1
                 for c0, c1 in ((lc_la, lc_nx), (lc_nx, lc_end)):
                     if c1 > c0 and nrow:
                         mask = (1, nb, p, pr, q, pc, lr1, c0, 0)
-                        ops.gemm(-1.0, Prow, Lcol[c0 - lc1:c1 - lc1], 1.0, buf[lr1:lr_end, c0:c1],
+                        ops.gemm(-1.0, Prow, Lcol[c0 - loff:c1 - loff], 1.0, buf[lr1:lr_end, c0:c1],
                                  'N', ct, mask)
                     if c0 == lc_la:
                         ev_tr[t] = ss.event(us)
