@@ -132,7 +132,10 @@ def _getrf_p1(A, buf, thr, la, nopiv):
                 ss.wait(ss.panel, ev_tr[k - la - 1])
             with trace_block("getrf::panel"):
                 if own:
-                    ops.getrf(buf[r0:m, lck:lck + kb], piv, infos[k:k + 1], threshold=thr, nopiv=nopiv)
+                    # the whole tile width: a wide last panel (m - r0 < tile
+                    # width) also gets U12 = L11^{-1} P A12 of its extra columns
+                    wk = min(nb, n - r0)
+                    ops.getrf(buf[r0:m, lck:lck + wk], piv, infos[k:k + 1], threshold=thr, nopiv=nopiv)
                     Lp = buf[r0:m, lck:lck + kb]
                 else:
                     Lp = ops.colmajor_empty(mk, kb, dt, dev)
@@ -302,7 +305,9 @@ def _getrf_general(A, buf, thr, la, mode, leaf):
         kb = min(nb, n - r0, m - r0)
         rk, ck = k % p, k % q
         lr_k = min(tiles_local_before(k, p, pr) * nb, mloc)
-        lr1 = min(tiles_local_before(k + 1, p, pr) * nb, mloc)
+        # first local row after the kb-row window (a short last panel leaves
+        # rows of its own tile below the window)
+        lr1 = min(lr_k + kb, mloc) if pr == rk else lr_k
         lc_k = min(tiles_local_before(k, q, pc) * nb, nloc)
         lc1 = min(tiles_local_before(k + 1, q, pc) * nb, nloc)
         lcla = min(tiles_local_before(k + 1 + la, q, pc) * nb, nloc)
@@ -329,7 +334,11 @@ def _getrf_general(A, buf, thr, la, mode, leaf):
             # newest lookahead column k+la: first part of step k-1's trailing update
             if k >= 1 and la > 0:
                 ss.wait(ss.panel, ev_tr[k - 1])
-            _xchg_update(ctx, upd, [(lc1, lcla)], [], colc)
+            # (wide matrix, last panel: the tile's columns beyond kb get the
+            # row exchange and the U-row solve too)
+            wk = min(nb, n - r0)
+            part = [(lc_k + kb, lc_k + wk)] if (pc == ck and kb < wk) else []
+            _xchg_update(ctx, upd, part + [(lc1, lcla)], [], colc)
             ev_panel = ss.event(ss.panel)
         us = ss.update[0]
         with ss.use(us):

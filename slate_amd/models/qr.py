@@ -131,6 +131,10 @@ def _geqrf_p1(A, buf, T, la):
             # newest lookahead column k+la: first part of step k-1's trailing
             if k >= 1 and la > 0:
                 ss.wait(ss.panel, ev_tr[k - 1])
+            if own and lck + kb < lc1:
+                # wide matrix, last panel: fewer rows than the tile has
+                # columns -- the tile's remaining columns are trailing too
+                _apply_qh(V, Tk, buf[r0:m, lck + kb:lc1])
             if lcla > lc1:
                 _apply_qh(V, Tk, buf[r0:m, lc1:lcla])
             ev_panel = ss.event(ss.panel)
@@ -216,7 +220,9 @@ def _geqrf_general(A, buf, T, la):
                           if tree else None)}
             if k >= 1 and la > 0:
                 ss.wait(ss.panel, ev_tr[k - 1])
-            _tsqr_update(buf, lr_k, mloc, pk.get("V"), f, [(lc1, lcla)], colc, dt, dev)
+            # (wide matrix, last panel: the tile's columns beyond kb are trailing too)
+            part = [(lc_k + kb, lc1)] if (pc == ck and lc_k + kb < lc1) else []
+            _tsqr_update(buf, lr_k, mloc, pk.get("V"), f, part + [(lc1, lcla)], colc, dt, dev)
             ev_panel = ss.event(ss.panel)
         T.append(f)
         us = ss.update[0]

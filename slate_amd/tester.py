@@ -8,7 +8,13 @@ and timings.
 Options: --type s,d,c,z  --dim m[xn[xk]] or start:stop:step  --nb  --p --q
 --target h|d  --check y|n  --uplo l,u  --trans n,t,c  --side l,r
 --lookahead  --repeat.  One line per run: type, dims, nb, grid, error,
-time, Gflop/s, status; exit status 1 if any check failed.
+time, Gflop/s, % of the MI355X dense peak of all ranks (device target),
+status; exit status 1 if any check failed.  Routines (test/test.cc
+families): BLAS-3 gemm herk/syrk her2k/syr2k hemm/symm trmm trsm;
+Cholesky potrf potrs posv potri trtri posv_mixed; LU getrf getrs gesv
+getri gesv_nopiv gesv_tntpiv/calu gesv_rbt gesv_mixed; band gbsv; QR/LQ
+geqrf gelqf cholqr gels; eigen/SVD heev/syev hegv/sygv svd; indefinite
+hesv/sysv; aux norm colnorms add redistribute gecondest.
 """
 from __future__ import annotations
 
@@ -242,10 +248,229 @@ def t_hesv(c, m, n, k, **p):
     return err, t, n ** 3 / 3.0
 
 
+def _herm_mat(c, n, uplo, kind="rands", seed=1):
+    return c.mat(n, n, kind, seed, sl.HermitianMatrix, uplo=uplo)
+
+
+def t_her2k(c, m, n, k, uplo=Uplo.Lower, **p):
+    A, B = c.mat(n, k, seed=1), c.mat(n, k, seed=2)
+    C = _herm_mat(c, n, uplo, seed=3)
+    Ad, Bd, Cf = D(A), D(B), _herm_full(C)
+    _, t = c.timed(lambda: sl.her2k(1.0, A, B, 1.0, C, c.opts))
+    ref = Ad @ Bd.mH + Bd @ Ad.mH + Cf
+    err = _rel(_herm_full(C) - ref, Ad.abs().max() * Bd.abs().max() * k) if c.a.check == 'y' else None
+    return err, t, 2.0 * n * n * k
+
+
+def t_hemm(c, m, n, k, uplo=Uplo.Lower, side=Side.Left, **p):
+    kk = m if side == Side.Left else n
+    A = _herm_mat(c, kk, uplo, seed=1)
+    B, C = c.mat(m, n, seed=2), c.mat(m, n, seed=3)
+    Af, Bd, Cd = _herm_full(A), D(B), D(C)
+    _, t = c.timed(lambda: sl.hemm(side, 1.0, A, B, 1.0, C, c.opts))
+    ref = (Af @ Bd if side == Side.Left else Bd @ Af) + Cd
+    err = _rel(D(C) - ref, Af.abs().max() * Bd.abs().max() * kk) if c.a.check == 'y' else None
+    return err, t, 2.0 * m * n * kk
+
+
+def t_trmm(c, m, n, k, side=Side.Left, uplo=Uplo.Lower, **p):
+    kk = m if side == Side.Left else n
+    T = c.mat(kk, kk, seed=1)
+    Td = D(T)
+    B = c.mat(m, n, seed=2)
+    Bd = D(B)
+    L = sl.TriangularMatrix(uplo, T)
+    _, t = c.timed(lambda: sl.trmm(side, 1.0, L, B, c.opts))
+    Tt = torch.tril(Td) if uplo == Uplo.Lower else torch.triu(Td)
+    ref = Tt @ Bd if side == Side.Left else Bd @ Tt
+    return (_rel(D(B) - ref, Td.abs().max() * Bd.abs().max() * kk) if c.a.check == 'y' else None), t, \
+        1.0 * m * n * kk
+
+
+def t_potrs(c, m, n, k, uplo=Uplo.Lower, **p):
+    A = _herm_mat(c, n, uplo, "poev")
+    Af = _herm_full(A)
+    sl.potrf(A, c.opts)
+    B = c.mat(n, k, seed=2)
+    Bd = D(B)
+    _, t = c.timed(lambda: sl.potrs(A, B, c.opts))
+    err = _rel(Af @ D(B) - Bd, Af.abs().max() * D(B).abs().max() * n) if c.a.check == 'y' else None
+    return err, t, 2.0 * n * n * k
+
+
+def t_potri(c, m, n, k, uplo=Uplo.Lower, **p):
+    A = _herm_mat(c, n, uplo, "poev")
+    Af = _herm_full(A)
+    def run():
+        info = sl.potrf(A, c.opts)
+        return info if info else sl.potri(A, c.opts)
+    info, t = c.timed(run)
+    err = _rel(_herm_full(A) @ Af - torch.eye(n, dtype=c.dt, device=Af.device), n) if c.a.check == 'y' else None
+    return err if info == 0 else float("inf"), t, n ** 3
+
+
+def t_trtri(c, m, n, k, uplo=Uplo.Lower, **p):
+    T = c.mat(n, n, seed=1)
+    Td = D(T) + n * torch.eye(n, dtype=c.dt, device=D(T).device)
+    sl.from_dense(T, Td)
+    L = sl.TriangularMatrix(uplo, T)
+    info, t = c.timed(lambda: sl.trtri(L, c.opts))
+    Tt = torch.tril(Td) if uplo == Uplo.Lower else torch.triu(Td)
+    X = torch.tril(D(T)) if uplo == Uplo.Lower else torch.triu(D(T))
+    err = _rel(X @ Tt - torch.eye(n, dtype=c.dt, device=Tt.device), n) if c.a.check == 'y' else None
+    return err, t, n ** 3 / 3.0
+
+
+def _lu_solve_check(c, A0, X, B0, n):
+    return _rel(A0 @ X - B0, A0.abs().max() * X.abs().max() * n) if c.a.check == 'y' else None
+
+
+def t_getrs(c, m, n, k, **p):
+    A = c.mat(n, n, seed=1)
+    Ad = D(A)
+    piv = sl.Pivots()
+    sl.getrf(A, piv, c.opts)
+    B = c.mat(n, k, seed=2)
+    Bd = D(B)
+    _, t = c.timed(lambda: sl.getrs(A, piv, B, c.opts))
+    return _lu_solve_check(c, Ad, D(B), Bd, n), t, 2.0 * n * n * k
+
+
+def t_getri(c, m, n, k, **p):
+    A = c.mat(n, n, seed=1)
+    Ad = D(A)
+    piv = sl.Pivots()
+    def run():
+        sl.getrf(A, piv, c.opts)
+        return sl.getri(A, piv, c.opts)
+    _, t = c.timed(run)
+    err = _rel(D(A) @ Ad - torch.eye(n, dtype=c.dt, device=Ad.device), n * Ad.abs().max()) \
+        if c.a.check == 'y' else None
+    return err, t, 2.0 * n ** 3
+
+
+def _getrf_method(method):
+    def f(c, m, n, k, **p):
+        from slate_amd.core.enums import MethodLU
+        A, B = c.mat(n, n, "rand_dominant" if method == "nopiv" else "rands", 1), c.mat(n, k, seed=2)
+        Ad, Bd = D(A), D(B)
+        o = dict(c.opts)
+        o[Option.MethodLU] = {"nopiv": MethodLU.NoPiv, "calu": MethodLU.CALU, "rbt": MethodLU.RBT}[method]
+        _, t = c.timed(lambda: sl.gesv(A, sl.Pivots(), B, o))
+        return _lu_solve_check(c, Ad, D(B), Bd, n), t, 2.0 * n ** 3 / 3.0
+    return f
+
+
+def t_posv_mixed(c, m, n, k, uplo=Uplo.Lower, **p):
+    if c.t not in ('d', 'z'):
+        return None, 0.0, 0.0
+    A = _herm_mat(c, n, uplo, "poev")
+    Af = _herm_full(A)
+    B, X = c.mat(n, k, seed=2), c.mat(n, k, "zeros")
+    Bd = D(B)
+    _, t = c.timed(lambda: sl.posv_mixed(A, B, X, c.opts))
+    return _lu_solve_check(c, Af, D(X), Bd, n), t, n ** 3 / 3.0
+
+
+def t_gelqf(c, m, n, k, **p):
+    A = c.mat(m, n, seed=1)
+    Ad = D(A)
+    T = sl.TriangularFactors()
+    _, t = c.timed(lambda: sl.gelqf(A, T, c.opts))
+    err = None
+    if c.a.check == 'y':
+        Q = c.mat(n, n, "identity", 1)
+        sl.unmlq(Side.Left, Op.NoTrans, A, T, Q, c.opts)
+        kk = min(m, n)
+        err = _rel(torch.tril(D(A))[:, :kk] @ D(Q)[:kk] - Ad, Ad.abs().max() * n)
+    return err, t, 2.0 * n * m * m - 2.0 * m ** 3 / 3.0
+
+
+def t_cholqr(c, m, n, k, **p):
+    A = c.mat(m, n, seed=1)
+    Ad = D(A)
+    R = c.mat(n, n, "zeros")
+    info, t = c.timed(lambda: sl.cholqr(A, R, c.opts))
+    err = _rel(D(A) @ torch.triu(D(R)) - Ad, Ad.abs().max() * m) if c.a.check == 'y' else None
+    return err if info == 0 else float("inf"), t, 2.0 * m * n * n
+
+
+def t_hegv(c, m, n, k, uplo=Uplo.Lower, **p):
+    A = _herm_mat(c, n, uplo, seed=1)
+    B = _herm_mat(c, n, uplo, "poev", seed=2)
+    Af, Bf = _herm_full(A).cpu(), _herm_full(B).cpu()
+    Z = c.mat(n, n, "zeros")
+    w, t = c.timed(lambda: sl.hegv(1, A, B, None, Z, c.opts))
+    X = D(Z).cpu()
+    err = _rel(Af @ X - Bf @ X * w.cpu().to(c.dt), Af.abs().max() * Bf.abs().max() * n) \
+        if c.a.check == 'y' else None
+    return err, t, 14.0 * n ** 3 / 3.0
+
+
+def t_gecondest(c, m, n, k, **p):
+    A = c.mat(n, n, seed=1)
+    Ad = D(A).cpu()
+    anorm = float(sl.norm(Norm.One, A))
+    piv = sl.Pivots()
+    sl.getrf(A, piv, c.opts)
+    r, t = c.timed(lambda: sl.gecondest(Norm.One, A, piv, anorm, c.opts))
+    ref = 1.0 / (torch.linalg.norm(Ad, 1) * torch.linalg.norm(torch.linalg.inv(Ad), 1)).item()
+    err = abs(r - ref) / ref if c.a.check == 'y' else None
+    return (None if err is not None and err < 3.0 else err), t, 2.0 * n * n   # estimate within 3x
+
+
+def t_colnorms(c, m, n, k, **p):
+    A = c.mat(m, n, seed=1)
+    Ad = D(A)
+    v, t = c.timed(lambda: sl.colNorms(Norm.Max, A, c.opts))
+    err = _rel(v.to(Ad.device).reshape(-1) - Ad.abs().max(0).values, Ad.abs().max()) if c.a.check == 'y' else None
+    return err, t, 1.0 * m * n
+
+
+def t_add(c, m, n, k, **p):
+    A, B = c.mat(m, n, seed=1), c.mat(m, n, seed=2)
+    Ad, Bd = D(A), D(B)
+    _, t = c.timed(lambda: sl.add(2.0, A, -1.0, B, c.opts))
+    return (_rel(D(B) - (2.0 * Ad - Bd), Ad.abs().max()) if c.a.check == 'y' else None), t, 2.0 * m * n
+
+
+def t_redistribute(c, m, n, k, **p):
+    A = c.mat(m, n, seed=1)
+    B = sl.Matrix(m, n, nb=max(8, c.a.nb // 2 + 3), p=c.a.q, q=c.a.p, dtype=c.dt, device=c.dev)
+    B.insertLocalTiles(device=c.dev.index if c.dev.type == "cuda" else -1)
+    _, t = c.timed(lambda: sl.redistribute(A, B))
+    return (_rel(D(B) - D(A), 1.0) if c.a.check == 'y' else None), t, 0.0
+
+
+def t_gbsv(c, m, n, k, **p):
+    kl = ku = max(1, c.a.nb // 2)
+    A = sl.BandMatrix(n, n, kl, ku, nb=c.a.nb, p=c.a.p, q=c.a.q, dtype=c.dt, device=c.dev)
+    A.insertLocalTiles(device=c.dev.index if c.dev.type == "cuda" else -1)
+    sl.generate_matrix(A, "rand_dominant", 1)
+    Ad = D(A)
+    i = torch.arange(n, device=Ad.device)
+    Ad = torch.where(((i[:, None] - i[None, :]) <= kl) & ((i[None, :] - i[:, None]) <= ku), Ad,
+                     torch.zeros_like(Ad))                     # only the band is the operand
+    B = c.mat(n, k, seed=2)
+    Bd = D(B)
+    info, t = c.timed(lambda: sl.gbsv(A, sl.Pivots(), B, c.opts))
+    return _lu_solve_check(c, Ad, D(B), Bd, n), t, 2.0 * n * kl * (kl + ku)
+
+
 ROUTINES = {"gemm": t_gemm, "herk": t_herk, "syrk": t_herk, "trsm": t_trsm, "potrf": t_potrf,
             "posv": t_posv, "getrf": t_getrf, "gesv": t_gesv, "geqrf": t_geqrf, "gels": t_gels,
             "heev": t_heev, "syev": t_heev, "svd": t_svd, "norm": t_norm, "genorm": t_norm,
-            "gesv_mixed": t_gesv_mixed, "hesv": t_hesv, "sysv": t_hesv}
+            "gesv_mixed": t_gesv_mixed, "hesv": t_hesv, "sysv": t_hesv,
+            "her2k": t_her2k, "syr2k": t_her2k, "hemm": t_hemm, "symm": t_hemm, "trmm": t_trmm,
+            "potrs": t_potrs, "potri": t_potri, "trtri": t_trtri, "getrs": t_getrs, "getri": t_getri,
+            "gesv_nopiv": _getrf_method("nopiv"), "gesv_tntpiv": _getrf_method("calu"),
+            "gesv_calu": _getrf_method("calu"), "gesv_rbt": _getrf_method("rbt"),
+            "posv_mixed": t_posv_mixed, "gelqf": t_gelqf, "cholqr": t_cholqr, "hegv": t_hegv,
+            "sygv": t_hegv, "gecondest": t_gecondest, "colnorms": t_colnorms, "add": t_add,
+            "redistribute": t_redistribute, "gbsv": t_gbsv}
+
+# per-GPU dense peaks (MI355X spec, TFLOP/s): fp64 matrix = vector, fp32 matrix
+PEAK_TF = {'s': 157.3, 'd': 78.6, 'c': 157.3, 'z': 78.6}
 
 
 def main(argv=None):
@@ -271,7 +496,7 @@ def main(argv=None):
     fails = 0
     if comm.rank == 0:
         print(f"{'type':>4} {'m':>6} {'n':>6} {'k':>6} {'nb':>5} {'grid':>6} {'uplo':>4} {'error':>10} "
-              f"{'time(s)':>9} {'Gflop/s':>9}  status", flush=True)
+              f"{'time(s)':>9} {'Gflop/s':>9} {'%peak':>6}  status", flush=True)
     for t, (m, n, k), nb, up, sd in itertools.product(a.type.split(","), dims, a.nb.split(","),
                                                       a.uplo.split(","), a.side.split(",")):
         a.nb = int(nb)
@@ -290,8 +515,11 @@ def main(argv=None):
             if comm.rank == 0:
                 es = "-" if err is None else f"{err:10.2e}"
                 gf = fl / tm / 1e9 if tm > 0 else 0.0
+                # complex flops count 4 real ones (LAPACK++ Gflop<complex>)
+                gfr = gf * (4 if t in ('c', 'z') else 1)
+                pk = f"{100 * gfr / (1e3 * PEAK_TF[t] * comm.size):6.1f}" if ctx.dev.type == "cuda" else f"{'-':>6}"
                 print(f"{t:>4} {m:>6} {n:>6} {k:>6} {a.nb:>5} {f'{a.p}x{a.q}':>6} {up:>4} {es:>10} {tm:9.4f} "
-                      f"{gf:9.1f}  {'pass' if ok else 'FAILED'}", flush=True)
+                      f"{gf:9.1f} {pk}  {'pass' if ok else 'FAILED'}", flush=True)
     if comm.rank == 0:
         print("All tests passed." if fails == 0 else f"{fails} tests FAILED.", flush=True)
     sl.finalize()

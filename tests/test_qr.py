@@ -46,7 +46,7 @@ def _check_qr(m, n, nb, dt, p=1, q=1, device=None):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("mn", [(300, 200, 64), (128, 128, 32), (96, 160, 32)])
+@pytest.mark.parametrize("mn", [(300, 200, 64), (128, 128, 32), (96, 160, 32), (30, 40, 16)])
 def test_geqrf_unmqr(dt, mn):
     m, n, nb = mn
     _check_qr(m, n, nb, dt)
@@ -144,7 +144,7 @@ def test_qr_distributed(grid):
 
 def _dist_qr_la(rank, size, p, q):
     """TSQR with lookahead 0..2, ragged last tiles and ranks without rows."""
-    for (m, n, nb, la) in [(200, 120, 16, 0), (333, 90, 32, 2), (96, 96, 16, 1)]:
+    for (m, n, nb, la) in [(200, 120, 16, 0), (333, 90, 32, 2), (96, 96, 16, 1), (70, 100, 16, 1)]:
         A = _mat(m, n, nb, torch.float64, 12, p, q)
         A0 = D(A).clone()
         T = TriangularFactors()

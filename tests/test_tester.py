@@ -4,7 +4,7 @@ import pytest
 from slate_amd import tester
 
 
-@pytest.mark.parametrize("routine", ["gemm", "potrf", "gesv", "geqrf", "heev", "svd", "hesv"])
+@pytest.mark.parametrize("routine", sorted(tester.ROUTINES))
 def test_tester_routine(routine):
     assert tester.main([routine, "--type", "d,z", "--dim", "40x30x20", "--nb", "16", "--target", "h"]) == 0
 
