@@ -200,21 +200,22 @@ template <typename T>
 __global__ void __launch_bounds__(256)
 laswp_apply_kernel(i64 n, T* A, i64 lda, const SwapPlan* __restrict__ plan, int CCH) {
     extern __shared__ __align__(16) unsigned char dyn[];
-    T* buf = reinterpret_cast<T*>(dyn);   // [nt][CCH] gathered rows
+    T* buf = reinterpret_cast<T*>(dyn);   // [nt][CCH + 1] gathered rows
     const int nt = plan->nt;
     if (nt == 0) return;
     const i64 c0 = (i64)blockIdx.x * CCH;
     const int ncols = (int)min((i64)CCH, n - c0);
+    const int LD = CCH + 1;               // odd row pitch: t-consecutive lanes hit distinct banks
     // gather: buf[t][c] = A[tsrc[t], c0 + c]   (t fastest: the touched rows
     // of one column; the row lists are read from L2, not rebuilt)
     for (int idx = threadIdx.x; idx < nt * CCH; idx += blockDim.x) {
         int t = idx % nt, c = idx / nt;
-        if (c < ncols) buf[t * CCH + c] = A[plan->tsrc[t] + (c0 + c) * lda];
+        if (c < ncols) buf[t * LD + c] = A[plan->tsrc[t] + (c0 + c) * lda];
     }
     __syncthreads();
     for (int idx = threadIdx.x; idx < nt * CCH; idx += blockDim.x) {
         int t = idx % nt, c = idx / nt;
-        if (c < ncols) A[plan->trow[t] + (c0 + c) * lda] = buf[t * CCH + c];
+        if (c < ncols) A[plan->trow[t] + (c0 + c) * lda] = buf[t * LD + c];
     }
 }
 
@@ -284,8 +285,8 @@ void laswp_off(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, i64 ioff, 
     SwapPlan* plan = static_cast<SwapPlan*>(workspace(s, sizeof(SwapPlan), WS_L));
     hipLaunchKernelGGL(laswp_setup_kernel, dim3(1), dim3(MAXSW), 0, s, k1, k2, ipiv, ioff, incx, plan, false);
     const size_t per_col = (size_t)2 * (k2 - k1) * sizeof(T);
-    int cch = (int)std::max<size_t>(1, std::min<size_t>(32, (64 * 1024) / per_col));
-    size_t shmem = per_col * cch;
+    int cch = (int)std::max<size_t>(1, std::min<size_t>(32, (64 * 1024) / per_col - 1));
+    size_t shmem = per_col * (cch + 1);
     unsigned g = (unsigned)((n + cch - 1) / cch);
     hipLaunchKernelGGL(laswp_apply_kernel<T>, dim3(g), dim3(256), shmem, s, n, A, lda, plan, cch);
     HIP_LAUNCH_CHECK();

@@ -74,8 +74,14 @@ struct alignas(16) Vec16 { T e[16 / sizeof(T)]; };
 template <typename T, int R, int BK, bool ROWC, int NT, bool CONJ = false>
 struct Stage {
     static constexpr int VEC = 16 / sizeof(T);
-    static constexpr int PADM = (sizeof(T) == 16) ? 8 : 16, PADK = 1;
+    // KM image of 8-byte elements with BK = 8: no pad, XOR swizzle of k by
+    // 2 * ((r >> 2) & 3) -- the 32 lanes of a ds_read_b64 group (16 rows x
+    // 2 k's) then cover all 64 banks (the odd pad left 2-way conflicts:
+    // 11-14 % of LDS cycles in the NN GEMM, profiles/pmc_hot_kernels.md)
+    static constexpr bool SWZ = !ROWC && sizeof(T) == 8 && BK == 8;
+    static constexpr int PADM = (sizeof(T) == 16) ? 8 : 16, PADK = SWZ ? 0 : 1;
     static constexpr int LDS_ELEMS = ROWC ? BK * (R + PADM) : R * (BK + PADK);
+    __device__ static inline int kswz(int r, int k) { return SWZ ? (k ^ (2 * ((r >> 2) & 3))) : k; }
     static constexpr int NVEC = R * BK / VEC;
     static constexpr int PER_THREAD = NVEC / NT;
     static_assert(NVEC % NT == 0, "tile not divisible by threads");
@@ -120,15 +126,20 @@ struct Stage {
                 *reinterpret_cast<Vec16<T>*>(lds + kk * (R + PADM) + r) = reg[i];
             } else {
                 int r = v / (BK / VEC), kk = (v % (BK / VEC)) * VEC;
-                T* p = lds + r * (BK + PADK) + kk;
-                #pragma unroll
-                for (int e = 0; e < VEC; ++e) p[e] = reg[i].e[e];
+                if constexpr (SWZ) {
+                    // kk even, the swizzle even: the pair stays adjacent
+                    *reinterpret_cast<Vec16<T>*>(lds + r * BK + kswz(r, kk)) = reg[i];
+                } else {
+                    T* p = lds + r * (BK + PADK) + kk;
+                    #pragma unroll
+                    for (int e = 0; e < VEC; ++e) p[e] = reg[i].e[e];
+                }
             }
         }
     }
     // fragment element (r, k) from the LDS image
     __device__ static inline T frag(const T* lds, int r, int k) {
-        return ROWC ? lds[k * (R + PADM) + r] : lds[r * (BK + PADK) + k];
+        return ROWC ? lds[k * (R + PADM) + r] : lds[r * (BK + PADK) + kswz(r, k)];
     }
 };
 

@@ -5,6 +5,7 @@ from tools.bench_gemm import run
 
 for k in (256, 512, 1024, 2048):
     run('d', 'N', 'T', 24576, 24576, k, reps=3)
+    run('d', 'N', 'N', 24576, 24576, k, reps=3)
 for k in (512, 1024):
     a = torch.randn(24576, k, dtype=torch.float64, device='cuda'); c = torch.randn(24576, 24576, dtype=torch.float64, device='cuda')
     torch.addmm(c, a, a.t(), beta=1.0, alpha=-1.0, out=c); torch.cuda.synchronize()
