@@ -336,7 +336,10 @@ constexpr int TBM = 64;
 __global__ void __launch_bounds__(512)
 trsm_rlt_kernel(i64 m, int n, double alpha, const double* __restrict__ L, i64 ldl, const double* __restrict__ Winv,
                 double* __restrict__ B, i64 ldb) {
-    __shared__ double R[32][TBM + 1];       // R[c][r]
+    // row pitch = 16 mod 32 doubles: the two k rows of one ds_read_b64 lane
+    // group land in opposite bank halves (an odd pitch left 2-way conflicts:
+    // 33 % of LDS cycles, profiles/pmc_hot_kernels.md)
+    __shared__ double R[32][TBM + 16];      // R[c][r]
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int st = w & 3, tt = w >> 2;       // row strip, column tile
     const i64 r0 = (i64)blockIdx.x * TBM;
@@ -387,7 +390,7 @@ constexpr int TBN = 64;
 __global__ void __launch_bounds__(256)
 trsm_lln_kernel(int m, i64 n, double alpha, const double* __restrict__ L, i64 ldl, const double* __restrict__ Winv,
                 double* __restrict__ B, i64 ldb) {
-    __shared__ double R[32][TBN + 1];       // R[i][c]
+    __shared__ double R[32][TBN + 16];      // R[i][c] (pitch: see trsm_rlt_kernel)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const i64 cb = (i64)blockIdx.x * TBN;
     const int nc = (int)min((i64)TBN, n - cb);
