@@ -221,10 +221,15 @@ void potrf_tile(char uplo, int n, T* A, i64 lda, i64* info, hipStream_t s) {
     if (n <= 0) return;
     if constexpr (std::is_same<T, double>::value) {
         if (uplo == 'L') {
-            // 512-wide diagonal blocks by the one-CU LDS kernel, panel by the
+            // diagonal blocks (<= 512) by the one-CU LDS kernel, panel by the
             // blocked-inverse MFMA trsm, trailing triangle by the masked GEMM
-            for (int k0 = 0; k0 < n; k0 += 512) {
-                const int kb = std::min(512, n - k0);
+            static const int DB = [] {
+                const char* e = getenv("SLATE_AMD_POTRF_DIAG");
+                const int v = e ? atoi(e) : 256;   // 512 tile: 487 us vs 567 us (two 256 one-CU blocks + MFMA trsm/herk)
+                return (v >= 32 && v <= 512 && v % 32 == 0) ? v : 256;
+            }();
+            for (int k0 = 0; k0 < n; k0 += DB) {
+                const int kb = std::min(DB, n - k0);
                 T* Akk = A + k0 + (i64)k0 * lda;
                 potrf_fast(kb, Akk, lda, info, k0, s);
                 const int m = n - k0 - kb;
