@@ -179,6 +179,63 @@ int slate_amd_gesv(slate_amd_matrix_t A, slate_amd_pivots_t piv, slate_amd_matri
 int slate_amd_gels(slate_amd_matrix_t A, slate_amd_matrix_t BX);
 int slate_amd_heev(slate_amd_matrix_t A, double* w, slate_amd_matrix_t Z);
 
+/* Options applied to every later handle call (SLATE's per-call Options map,
+ * include/slate/types.hh:32-81): name as in slate::Option ("Lookahead",
+ * "MethodLU", "Target", "InnerBlocking", "MaxIterations", ...), value as
+ * text ("2", "CALU", "devices", "true"). */
+int slate_amd_set_option(const char* name, const char* value);
+int slate_amd_clear_options(void);
+/* Views sharing the parent's storage: tiles [i1, i2] x [j1, j2] (inclusive,
+ * as slate::Matrix::sub), and the transposed ('T') / conjugate-transposed
+ * ('C') view.  Destroy views like matrices (the storage stays alive while
+ * any handle refers to it). */
+slate_amd_matrix_t slate_amd_matrix_sub(slate_amd_matrix_t A, int64_t i1, int64_t i2, int64_t j1, int64_t j2);
+slate_amd_matrix_t slate_amd_matrix_op(slate_amd_matrix_t A, char op);
+int slate_amd_matrix_dims(slate_amd_matrix_t A, int64_t* m, int64_t* n);
+int slate_amd_matrix_tiles(slate_amd_matrix_t A, int64_t* mt, int64_t* nt);
+typedef int64_t slate_amd_tfactors_t;      /* QR/LQ block-reflector factors */
+slate_amd_tfactors_t slate_amd_tfactors_create(void);
+int slate_amd_tfactors_destroy(slate_amd_tfactors_t T);
+/* BLAS-3 (real scalars; complex matrices accept real alpha/beta).  A of
+ * trsm/trmm is read as triangular (uplo, diag 'N'/'U'); A of hemm and C of
+ * herk/her2k as Hermitian (their handle's stored triangle; general handles
+ * as Lower). */
+int slate_amd_trsm(char side, char uplo, char diag, double alpha, slate_amd_matrix_t A, slate_amd_matrix_t B);
+int slate_amd_trmm(char side, char uplo, char diag, double alpha, slate_amd_matrix_t A, slate_amd_matrix_t B);
+int slate_amd_herk(double alpha, slate_amd_matrix_t A, double beta, slate_amd_matrix_t C);
+int slate_amd_her2k(double alpha, slate_amd_matrix_t A, slate_amd_matrix_t B, double beta, slate_amd_matrix_t C);
+int slate_amd_hemm(char side, double alpha, slate_amd_matrix_t A, slate_amd_matrix_t B, double beta,
+                   slate_amd_matrix_t C);
+/* factorizations, solves, inverses */
+int slate_amd_potrs(slate_amd_matrix_t A, slate_amd_matrix_t B);
+int slate_amd_potri(slate_amd_matrix_t A);
+int slate_amd_trtri(char uplo, char diag, slate_amd_matrix_t A);
+int slate_amd_getri(slate_amd_matrix_t A, slate_amd_pivots_t piv);
+int slate_amd_geqrf(slate_amd_matrix_t A, slate_amd_tfactors_t T);
+int slate_amd_gelqf(slate_amd_matrix_t A, slate_amd_tfactors_t T);
+int slate_amd_unmqr(char side, char op, slate_amd_matrix_t A, slate_amd_tfactors_t T, slate_amd_matrix_t C);
+int slate_amd_unmlq(char side, char op, slate_amd_matrix_t A, slate_amd_tfactors_t T, slate_amd_matrix_t C);
+int slate_amd_gels_t(slate_amd_matrix_t A, slate_amd_tfactors_t T, slate_amd_matrix_t BX);
+int slate_amd_hesv(slate_amd_matrix_t A, slate_amd_matrix_t B);
+int slate_amd_gesv_mixed(slate_amd_matrix_t A, slate_amd_pivots_t piv, slate_amd_matrix_t B, slate_amd_matrix_t X,
+                         int64_t* iter);
+int slate_amd_gesv_mixed_gmres(slate_amd_matrix_t A, slate_amd_pivots_t piv, slate_amd_matrix_t B,
+                               slate_amd_matrix_t X, int64_t* iter);
+int slate_amd_posv_mixed(slate_amd_matrix_t A, slate_amd_matrix_t B, slate_amd_matrix_t X, int64_t* iter);
+int slate_amd_posv_mixed_gmres(slate_amd_matrix_t A, slate_amd_matrix_t B, slate_amd_matrix_t X, int64_t* iter);
+int slate_amd_gesv_rbt(slate_amd_matrix_t A, slate_amd_matrix_t B);
+int slate_amd_gesv_nopiv(slate_amd_matrix_t A, slate_amd_matrix_t B);
+/* spectra (s, w: host arrays of min(m, n) / n reals) */
+int slate_amd_svd_vals(slate_amd_matrix_t A, double* s);
+int slate_amd_hegv(int64_t itype, slate_amd_matrix_t A, slate_amd_matrix_t B, double* w, slate_amd_matrix_t Z);
+/* auxiliary */
+int slate_amd_add(double alpha, slate_amd_matrix_t A, double beta, slate_amd_matrix_t B);
+int slate_amd_copy(slate_amd_matrix_t A, slate_amd_matrix_t B);
+int slate_amd_scale(double numer, double denom, slate_amd_matrix_t A);
+int slate_amd_set(double offdiag, double diag, slate_amd_matrix_t A);
+double slate_amd_gecondest(char norm, slate_amd_matrix_t A, slate_amd_pivots_t piv, double anorm);
+double slate_amd_pocondest(char norm, slate_amd_matrix_t A, double anorm);
+
 #ifdef __cplusplus
 }
 #endif

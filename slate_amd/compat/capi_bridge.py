@@ -255,27 +255,168 @@ def handle(op, *args):
         return float(sl.norm(sl.Norm.from_string(chr(nrm)), _H[h]))
     if op == "gemm":
         al, ha, hb, be, hc = args
-        sl.gemm(al, _H[ha], _H[hb], be, _H[hc])
+        sl.gemm(al, _H[ha], _H[hb], be, _H[hc], _OPTS)
         return 0
     if op == "potrf":
-        return sl.potrf(_H[args[0]])
+        return sl.potrf(_herm(sl, args[0]), _OPTS)
     if op == "posv":
-        return sl.posv(_H[args[0]], _H[args[1]])
+        return sl.posv(_herm(sl, args[0]), _H[args[1]], _OPTS)
     if op == "getrf":
-        return sl.getrf(_H[args[0]], _H[args[1]])
+        return sl.getrf(_H[args[0]], _H[args[1]], _OPTS)
     if op == "getrs":
-        sl.getrs(_H[args[0]], _H[args[1]], _H[args[2]])
+        sl.getrs(_H[args[0]], _H[args[1]], _H[args[2]], _OPTS)
         return 0
     if op == "gesv":
         ha, hp, hb = args
-        return sl.gesv(_H[ha], _H[hp], _H[hb])
+        return sl.gesv(_H[ha], _H[hp], _H[hb], _OPTS)
     if op == "geqrf_gels":
         ha, hb = args
-        return sl.gels(_H[ha], sl.TriangularFactors(), _H[hb])
+        return sl.gels(_H[ha], sl.TriangularFactors(), _H[hb], _OPTS)
     if op == "heev":
         ha, wptr, hz = args
-        w = sl.heev(_H[ha], None, _H[hz] if hz else None)
-        n = w.numel()
-        np.ctypeslib.as_array((ctypes.c_double * max(n, 1)).from_address(wptr))[:n] = w.cpu().numpy()
+        w = sl.heev(_H[ha], None, _H[hz] if hz else None, _OPTS)
+        _put_reals(wptr, w)
         return 0
+    return _handle_more(sl, op, *args)
+
+
+# ---- options and the wider routine set of the handle API (C++ header
+# include/slate_amd/slate_amd.hh wraps these; SLATE's C API: one
+# slate_<routine>_c<type> per routine, src/c_api/wrappers.cc)
+_OPTS = {}
+
+
+def _put_reals(ptr, v):
+    n = v.numel()
+    if n:
+        np.ctypeslib.as_array((ctypes.c_double * n).from_address(ptr))[:] = v.real.double().cpu().numpy()
+
+
+def _tri(sl, h, uplo, diag):
+    """Triangular view (uplo, diag) of a handle's matrix; an op'd view keeps its op."""
+    M = _H[h]
+    return sl.TriangularMatrix(sl.Uplo(chr(uplo)), matrix=M, diag=sl.Diag(chr(diag)))
+
+
+def _herm(sl, h):
+    M = _H[h]
+    return M if isinstance(M, sl.HermitianMatrix) else sl.HermitianMatrix(sl.Uplo.Lower, matrix=M)
+
+
+def _handle_more(sl, op, *args):
+    if op == "set_option":
+        name, value = args
+        from ..core.options import _TYPES, _normalize_key
+        key = _normalize_key(name)
+        if key in _TYPES:
+            _OPTS[key] = _TYPES[key].from_string(value)
+        else:
+            v = value.strip().lower()
+            if v in ("true", "false"):
+                _OPTS[key] = v == "true"
+            else:
+                try:
+                    _OPTS[key] = int(v)
+                except ValueError:
+                    _OPTS[key] = float(v)
+        return 0
+    if op == "clear_options":
+        _OPTS.clear()
+        return 0
+    if op == "sub":
+        h, i1, i2, j1, j2 = args
+        return _put(_H[h].sub(i1, i2, j1, j2))
+    if op == "op_view":
+        h, t = args
+        M = _H[h]
+        return _put(M.conj_transpose() if chr(t) == 'C' else M.transpose())
+    if op == "dims":
+        M = _H[args[0]]
+        return M.m() * 1000000000 + M.n()
+    if op == "tiles":
+        M = _H[args[0]]
+        return M.mt() * 1000000000 + M.nt()
+    if op == "tfactors_create":
+        return _put(sl.TriangularFactors())
+    if op in ("trsm", "trmm"):
+        side, uplo, diag, al, ha, hb = args
+        getattr(sl, op)(sl.Side(chr(side)), al, _tri(sl, ha, uplo, diag), _H[hb], _OPTS)
+        return 0
+    if op == "herk":
+        al, ha, be, hc = args
+        sl.herk(al, _H[ha], be, _herm(sl, hc), _OPTS)
+        return 0
+    if op == "her2k":
+        al, ha, hb, be, hc = args
+        sl.her2k(al, _H[ha], _H[hb], be, _herm(sl, hc), _OPTS)
+        return 0
+    if op == "hemm":
+        side, al, ha, hb, be, hc = args
+        sl.hemm(sl.Side(chr(side)), al, _herm(sl, ha), _H[hb], be, _H[hc], _OPTS)
+        return 0
+    if op == "potrs":
+        sl.potrs(_herm(sl, args[0]), _H[args[1]], _OPTS)
+        return 0
+    if op == "potri":
+        return sl.potri(_herm(sl, args[0]), _OPTS)
+    if op == "trtri":
+        uplo, diag, ha = args
+        return sl.trtri(_tri(sl, ha, uplo, diag), _OPTS)
+    if op == "getri":
+        return sl.getri(_H[args[0]], _H[args[1]], _OPTS)
+    if op in ("geqrf", "gelqf"):
+        return getattr(sl, op)(_H[args[0]], _H[args[1]], _OPTS)
+    if op in ("unmqr", "unmlq"):
+        side, o, ha, ht, hc = args
+        getattr(sl, op)(sl.Side(chr(side)), sl.Op(chr(o)), _H[ha], _H[ht], _H[hc], _OPTS)
+        return 0
+    if op == "gels_t":
+        ha, ht, hb = args
+        return sl.gels(_H[ha], _H[ht], _H[hb], _OPTS)
+    if op == "hesv":
+        ha, hb = args
+        return sl.hesv(_herm(sl, ha), B=_H[hb], opts=_OPTS)
+    if op in ("gesv_mixed", "posv_mixed", "gesv_mixed_gmres", "posv_mixed_gmres"):
+        if op.startswith("gesv"):
+            ha, hp, hb, hx, itp = args
+            r = getattr(sl, op)(_H[ha], _H[hp], _H[hb], _H[hx], _OPTS)
+        else:
+            ha, hb, hx, itp = args
+            r = getattr(sl, op)(_herm(sl, ha), _H[hb], _H[hx], _OPTS)
+        info, it = (r if isinstance(r, tuple) else (r, 0))
+        if itp:
+            _iarr(itp, 1)[0] = int(it)
+        return int(info)
+    if op in ("gesv_rbt", "gesv_nopiv"):
+        return getattr(sl, op)(_H[args[0]], _H[args[1]], _OPTS)
+    if op == "svd_vals":
+        ha, sptr = args
+        _put_reals(sptr, sl.svd_vals(_H[ha], None, _OPTS))
+        return 0
+    if op == "hegv":
+        it, ha, hb, wptr, hz = args
+        w = sl.hegv(it, _herm(sl, ha), _herm(sl, hb), None, _H[hz] if hz else None, _OPTS)
+        _put_reals(wptr, w)
+        return 0
+    if op == "add":
+        al, ha, be, hb = args
+        sl.add(al, _H[ha], be, _H[hb], _OPTS)
+        return 0
+    if op == "copy":
+        sl.copy(_H[args[0]], _H[args[1]], _OPTS)
+        return 0
+    if op == "scale":
+        num, den, ha = args
+        sl.scale(num, den, _H[ha], _OPTS)
+        return 0
+    if op == "set":
+        off, dg, ha = args
+        sl.set(off, dg, _H[ha], _OPTS)
+        return 0
+    if op == "gecondest":
+        nrm, ha, hp, anorm = args
+        return float(sl.gecondest(sl.Norm.from_string(chr(nrm)), _H[ha], _H[hp], anorm, _OPTS))
+    if op == "pocondest":
+        nrm, ha, anorm = args
+        return float(sl.pocondest(sl.Norm.from_string(chr(nrm)), _herm(sl, ha), anorm, _OPTS))
     raise ValueError(op)

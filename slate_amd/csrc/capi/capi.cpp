@@ -418,4 +418,123 @@ int slate_amd_heev(slate_amd_matrix_t A, double* w, slate_amd_matrix_t Z) {
     return I(invoke_on(&g_handle, "heev", "LLL", (long long)A, P(w), (long long)Z));
 }
 
+// ---- options, views and the wider routine set
+#define H_(x) (long long)(x)
+int slate_amd_set_option(const char* name, const char* value) {
+    return I(invoke_on(&g_handle, "set_option", "ss", name, value));
+}
+int slate_amd_clear_options(void) { return I(invoke_on(&g_handle, "clear_options", "")); }
+slate_amd_matrix_t slate_amd_matrix_sub(slate_amd_matrix_t A, int64_t i1, int64_t i2, int64_t j1, int64_t j2) {
+    return (slate_amd_matrix_t)invoke_on(&g_handle, "sub", "LLLLL", H_(A), H_(i1), H_(i2), H_(j1), H_(j2));
+}
+slate_amd_matrix_t slate_amd_matrix_op(slate_amd_matrix_t A, char op) {
+    return (slate_amd_matrix_t)invoke_on(&g_handle, "op_view", "Li", H_(A), (int)op);
+}
+static int split_pair(double v, int64_t* a, int64_t* b) {
+    if (v < 0) return I(v);
+    const long long x = (long long)v;
+    *a = x / 1000000000LL;
+    *b = x % 1000000000LL;
+    return 0;
+}
+int slate_amd_matrix_dims(slate_amd_matrix_t A, int64_t* m, int64_t* n) {
+    return split_pair(invoke_on(&g_handle, "dims", "L", H_(A)), m, n);
+}
+int slate_amd_matrix_tiles(slate_amd_matrix_t A, int64_t* mt, int64_t* nt) {
+    return split_pair(invoke_on(&g_handle, "tiles", "L", H_(A)), mt, nt);
+}
+slate_amd_tfactors_t slate_amd_tfactors_create(void) {
+    return (slate_amd_tfactors_t)invoke_on(&g_handle, "tfactors_create", "");
+}
+int slate_amd_tfactors_destroy(slate_amd_tfactors_t T) { return slate_amd_matrix_destroy(T); }
+int slate_amd_trsm(char side, char uplo, char diag, double alpha, slate_amd_matrix_t A, slate_amd_matrix_t B) {
+    return I(invoke_on(&g_handle, "trsm", "iiidLL", (int)side, (int)uplo, (int)diag, alpha, H_(A), H_(B)));
+}
+int slate_amd_trmm(char side, char uplo, char diag, double alpha, slate_amd_matrix_t A, slate_amd_matrix_t B) {
+    return I(invoke_on(&g_handle, "trmm", "iiidLL", (int)side, (int)uplo, (int)diag, alpha, H_(A), H_(B)));
+}
+int slate_amd_herk(double alpha, slate_amd_matrix_t A, double beta, slate_amd_matrix_t C) {
+    return I(invoke_on(&g_handle, "herk", "dLdL", alpha, H_(A), beta, H_(C)));
+}
+int slate_amd_her2k(double alpha, slate_amd_matrix_t A, slate_amd_matrix_t B, double beta, slate_amd_matrix_t C) {
+    return I(invoke_on(&g_handle, "her2k", "dLLdL", alpha, H_(A), H_(B), beta, H_(C)));
+}
+int slate_amd_hemm(char side, double alpha, slate_amd_matrix_t A, slate_amd_matrix_t B, double beta,
+                   slate_amd_matrix_t C) {
+    return I(invoke_on(&g_handle, "hemm", "idLLdL", (int)side, alpha, H_(A), H_(B), beta, H_(C)));
+}
+int slate_amd_potrs(slate_amd_matrix_t A, slate_amd_matrix_t B) {
+    return I(invoke_on(&g_handle, "potrs", "LL", H_(A), H_(B)));
+}
+int slate_amd_potri(slate_amd_matrix_t A) { return I(invoke_on(&g_handle, "potri", "L", H_(A))); }
+int slate_amd_trtri(char uplo, char diag, slate_amd_matrix_t A) {
+    return I(invoke_on(&g_handle, "trtri", "iiL", (int)uplo, (int)diag, H_(A)));
+}
+int slate_amd_getri(slate_amd_matrix_t A, slate_amd_pivots_t piv) {
+    return I(invoke_on(&g_handle, "getri", "LL", H_(A), H_(piv)));
+}
+int slate_amd_geqrf(slate_amd_matrix_t A, slate_amd_tfactors_t T) {
+    return I(invoke_on(&g_handle, "geqrf", "LL", H_(A), H_(T)));
+}
+int slate_amd_gelqf(slate_amd_matrix_t A, slate_amd_tfactors_t T) {
+    return I(invoke_on(&g_handle, "gelqf", "LL", H_(A), H_(T)));
+}
+int slate_amd_unmqr(char side, char op, slate_amd_matrix_t A, slate_amd_tfactors_t T, slate_amd_matrix_t C) {
+    return I(invoke_on(&g_handle, "unmqr", "iiLLL", (int)side, (int)op, H_(A), H_(T), H_(C)));
+}
+int slate_amd_unmlq(char side, char op, slate_amd_matrix_t A, slate_amd_tfactors_t T, slate_amd_matrix_t C) {
+    return I(invoke_on(&g_handle, "unmlq", "iiLLL", (int)side, (int)op, H_(A), H_(T), H_(C)));
+}
+int slate_amd_gels_t(slate_amd_matrix_t A, slate_amd_tfactors_t T, slate_amd_matrix_t BX) {
+    return I(invoke_on(&g_handle, "gels_t", "LLL", H_(A), H_(T), H_(BX)));
+}
+int slate_amd_hesv(slate_amd_matrix_t A, slate_amd_matrix_t B) {
+    return I(invoke_on(&g_handle, "hesv", "LL", H_(A), H_(B)));
+}
+int slate_amd_gesv_mixed(slate_amd_matrix_t A, slate_amd_pivots_t piv, slate_amd_matrix_t B, slate_amd_matrix_t X,
+                         int64_t* iter) {
+    return I(invoke_on(&g_handle, "gesv_mixed", "LLLLL", H_(A), H_(piv), H_(B), H_(X), P(iter)));
+}
+int slate_amd_gesv_mixed_gmres(slate_amd_matrix_t A, slate_amd_pivots_t piv, slate_amd_matrix_t B,
+                               slate_amd_matrix_t X, int64_t* iter) {
+    return I(invoke_on(&g_handle, "gesv_mixed_gmres", "LLLLL", H_(A), H_(piv), H_(B), H_(X), P(iter)));
+}
+int slate_amd_posv_mixed(slate_amd_matrix_t A, slate_amd_matrix_t B, slate_amd_matrix_t X, int64_t* iter) {
+    return I(invoke_on(&g_handle, "posv_mixed", "LLLL", H_(A), H_(B), H_(X), P(iter)));
+}
+int slate_amd_posv_mixed_gmres(slate_amd_matrix_t A, slate_amd_matrix_t B, slate_amd_matrix_t X, int64_t* iter) {
+    return I(invoke_on(&g_handle, "posv_mixed_gmres", "LLLL", H_(A), H_(B), H_(X), P(iter)));
+}
+int slate_amd_gesv_rbt(slate_amd_matrix_t A, slate_amd_matrix_t B) {
+    return I(invoke_on(&g_handle, "gesv_rbt", "LL", H_(A), H_(B)));
+}
+int slate_amd_gesv_nopiv(slate_amd_matrix_t A, slate_amd_matrix_t B) {
+    return I(invoke_on(&g_handle, "gesv_nopiv", "LL", H_(A), H_(B)));
+}
+int slate_amd_svd_vals(slate_amd_matrix_t A, double* s) {
+    return I(invoke_on(&g_handle, "svd_vals", "LL", H_(A), P(s)));
+}
+int slate_amd_hegv(int64_t itype, slate_amd_matrix_t A, slate_amd_matrix_t B, double* w, slate_amd_matrix_t Z) {
+    return I(invoke_on(&g_handle, "hegv", "LLLLL", H_(itype), H_(A), H_(B), P(w), H_(Z)));
+}
+int slate_amd_add(double alpha, slate_amd_matrix_t A, double beta, slate_amd_matrix_t B) {
+    return I(invoke_on(&g_handle, "add", "dLdL", alpha, H_(A), beta, H_(B)));
+}
+int slate_amd_copy(slate_amd_matrix_t A, slate_amd_matrix_t B) {
+    return I(invoke_on(&g_handle, "copy", "LL", H_(A), H_(B)));
+}
+int slate_amd_scale(double numer, double denom, slate_amd_matrix_t A) {
+    return I(invoke_on(&g_handle, "scale", "ddL", numer, denom, H_(A)));
+}
+int slate_amd_set(double offdiag, double diag, slate_amd_matrix_t A) {
+    return I(invoke_on(&g_handle, "set", "ddL", offdiag, diag, H_(A)));
+}
+double slate_amd_gecondest(char norm, slate_amd_matrix_t A, slate_amd_pivots_t piv, double anorm) {
+    return invoke_on(&g_handle, "gecondest", "iLLd", (int)norm, H_(A), H_(piv), anorm);
+}
+double slate_amd_pocondest(char norm, slate_amd_matrix_t A, double anorm) {
+    return invoke_on(&g_handle, "pocondest", "iLd", (int)norm, H_(A), anorm);
+}
+#undef H_
+
 }  // extern "C"

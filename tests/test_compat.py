@@ -168,7 +168,9 @@ def _build_c(tmp_path, src, name):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     lib = os.path.join(root, "slate_amd")
     exe = str(tmp_path / name)
-    cmd = ["gcc", "-O1", os.path.join(root, "examples", "c", src), "-I", os.path.join(root, "include"),
+    cxx = src.endswith(".cc")
+    cmd = (["g++", "-std=c++17", "-O1", os.path.join(root, "examples", "cpp", src)] if cxx else
+           ["gcc", "-O1", os.path.join(root, "examples", "c", src)]) + ["-I", os.path.join(root, "include"),
            "-L", lib, "-lslate_amd_c", "-Wl,-rpath," + lib, "-L", sysconfig.get_config_var("LIBDIR"),
            "-lpython" + sysconfig.get_config_var("LDVERSION"), "-lm", "-o", exe]
     subprocess.run(cmd, check=True)
@@ -204,3 +206,34 @@ def test_c_scalapack_and_handles(tmp_path, grid):
             assert "info=0" in ln or "pdgemm" in ln, ln
             val = float(ln.split("=")[-1])
             assert val < 1e-9, ln
+
+
+@pytest.mark.parametrize("grid", ["1x1", "1x2", "2x1"])
+def test_cpp_api(tmp_path, grid):
+    """The C++ API (include/slate_amd/slate_amd.hh): posv/gesv/getri/trmm/
+    trsm/herk/gels/heev/svd_vals/gesv_mixed with sub-matrix and
+    conjugate-transposed views and options, one process per rank; every
+    residual is computed by library routines."""
+    import os
+    import subprocess
+    from dist_util import _free_port
+    exe, root = _build_c(tmp_path, "ex_cpp_api.cc", "ex_cpp_api")
+    p, q = map(int, grid.split("x"))
+    size = p * q
+    port = str(_free_port())
+    procs = []
+    for r in range(size):
+        env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""), OMP_NUM_THREADS="2")
+        if size > 1:
+            env.update(RANK=str(r), WORLD_SIZE=str(size), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                       MASTER_PORT=port)
+        procs.append(subprocess.Popen([exe, grid], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                      text=True))
+    outs = [pr.communicate(timeout=600)[0] for pr in procs]
+    for pr, out in zip(procs, outs):
+        assert pr.returncode == 0, out
+        lines = [ln for ln in out.splitlines() if ln.startswith("rank ") and "iterations" not in ln]
+        assert len(lines) == 9, out
+        for ln in lines:
+            assert "FAILED" not in ln, ln
+            assert float(ln.split()[-1]) < 1e-10, ln
