@@ -10,8 +10,9 @@ MI355X design: stage 1 on one GPU (column-panel QR and row-panel LQ by the
 recursive GPU QR, two-sided block-reflector updates as MFMA GEMMs), stage 2
 and the bidiagonal QR on the host (native C++, like SLATE), back-transforms
 on the GPU (one launch per bulge-chasing sweep; GEMM-blocked WY for
-stage 1).  Multi-rank: redundant stages 1/2, each rank back-transforms
-only its own columns of U / V^H.
+stage 1).  Multi-rank (and SLATE_AMD_SVD_DIST=1): the distributed path of
+svd_dist.py (ge2tb on the grid, band reduced to rank 0 for tb2bd, bdsqr on
+each rank's own rows, back-transforms on the grid).
 """
 from __future__ import annotations
 
@@ -155,9 +156,13 @@ def svd(A, S=None, U=None, VH=None, opts=None):
     """Singular values (descending; returned and copied into S) and
     optionally the singular vectors U (m x k) and VH (k x n), k = min(m, n).
     A is destroyed."""
+    import os
     from .aux import allgather_dense
+    st = A.storage
+    if st.bc is not None and (st.comm.size > 1 or os.environ.get("SLATE_AMD_SVD_DIST") == "1"):
+        from .svd_dist import svd_dist
+        return svd_dist(A, S, U, VH, opts)
     with trace_block("svd"):
-        st = A.storage
         dev = st.device if st.device.type == "cuda" else torch.device("cpu")
         m, n = A.m(), A.n()
         nb = int(get_option(opts, Option.InnerBlocking, 0)) or min(st.bc.nb if st.bc else 64, 128)

@@ -188,6 +188,18 @@ def _check_grid_gpu(rank, size, p, q):
     Zd = D(Z)
     w = w.to(Zd.device)
     assert ((Hf @ Zd - Zd * w).abs().max() / (Hf.abs().max() * m)).item() < 1e-13
+    # svd: ge2tb on the grid (QR + LQ panels), tb2bd on rank 0, bdsqr by rows
+    G = sl.Matrix(320, 200, nb=64, p=p, q=q, device=dev)
+    G.insertLocalTiles(device=0)
+    sl.generate_matrix(G, "rands", 7)
+    G0 = D(G)
+    U = sl.Matrix(320, 200, nb=64, p=p, q=q, device=dev)
+    U.insertLocalTiles(device=0)
+    VH = sl.Matrix(200, 200, nb=64, p=p, q=q, device=dev)
+    VH.insertLocalTiles(device=0)
+    s = sl.svd(G, None, U, VH, {Option.InnerBlocking: 32}).to(dev)
+    assert ((D(U) @ torch.diag(s) @ D(VH) - G0).abs().max() / (G0.abs().max() * 320)).item() < 1e-13
+    assert ((s.cpu() - torch.linalg.svdvals(G0.cpu())).abs().max() / s.max().cpu()).item() < 1e-13
 
 
 @pytest.mark.parametrize("grid", [(2, 1), (1, 2), (2, 2)], ids=lambda g: f"{g[0]}x{g[1]}")

@@ -192,3 +192,65 @@ def test_svd_gpu():
     s = sl.svd(A, None, U, VH, {Option.InnerBlocking: 64})
     assert (s.cpu() - torch.linalg.svdvals(Ad.cpu())).abs().max().item() < 1e-11
     assert (D(U) @ torch.diag(s.to(dev)) @ D(VH) - Ad).abs().max().item() < 1e-11
+
+
+def _check_svd_grid(m, n, nb, dt, p, q, band):
+    k = min(m, n)
+    A = sl.Matrix(m, n, nb=nb, p=p, q=q, dtype=dt)
+    A.insertLocalTiles()
+    sl.generate_matrix(A, "rands", 7 + m)
+    Ad = D(A).clone()
+    U = sl.Matrix(m, k, nb=nb, p=p, q=q, dtype=dt)
+    U.insertLocalTiles()
+    VH = sl.Matrix(k, n, nb=nb, p=p, q=q, dtype=dt)
+    VH.insertLocalTiles()
+    s = sl.svd(A, None, U, VH, {Option.InnerBlocking: band})
+    Ud, Vd = D(U), D(VH)
+    sc = Ad.abs().max().item() * max(m, n)
+    assert (s - torch.linalg.svdvals(Ad)).abs().max().item() < 1e-13 * sc
+    assert (Ud @ torch.diag(s.to(dt)) @ Vd - Ad).abs().max().item() < 1e-13 * sc
+    assert (Ud.mH @ Ud - torch.eye(k, dtype=dt)).abs().max().item() < 1e-12
+    assert (Vd @ Vd.mH - torch.eye(k, dtype=dt)).abs().max().item() < 1e-12
+    # values only, A untouched by the distributed path
+    assert (D(A) - Ad).abs().max().item() == 0
+    s2 = sl.svd_vals(A, None, {Option.InnerBlocking: band})
+    assert (s2 - s).abs().max().item() < 1e-13 * sc
+
+
+def _dist_svd_only(rank, size, p, q):
+    _check_svd_grid(90, 60, 16, torch.float64, p, q, 8)
+    _check_svd_grid(50, 77, 16, torch.float64, p, q, 16)
+    _check_svd_grid(64, 64, 16, torch.complex128, p, q, 8)
+
+
+@pytest.mark.parametrize("grid", [(2, 2), (4, 1), (1, 3)], ids=lambda g: f"{g[0]}x{g[1]}")
+def test_svd_grid(grid):
+    """ge2tb on the process grid (column QR + row LQ panels, no dense gather),
+    band to rank 0 for tb2bd, bdsqr on each rank's own rows, grid
+    back-transforms (V on the transposed grid)."""
+    run_dist(_dist_svd_only, grid[0] * grid[1], *grid)
+
+
+def test_svd_dist_path_one_rank(monkeypatch):
+    monkeypatch.setenv("SLATE_AMD_SVD_DIST", "1")
+    _check_svd_grid(70, 45, 16, torch.float64, 1, 1, 8)
+    _check_svd_grid(33, 70, 16, torch.complex128, 1, 1, 16)
+
+
+@pytest.mark.gpu
+def test_svd_dist_path_gpu(monkeypatch):
+    """The distributed SVD path on one GPU (HIP QR/GEMM/trmm kernels in
+    ge2tb, device back-transforms)."""
+    monkeypatch.setenv("SLATE_AMD_SVD_DIST", "1")
+    dev = torch.device("cuda", 0)
+    m, n, nb = 300, 200, 64
+    A = sl.Matrix(m, n, nb=nb, device=dev)
+    A.insertLocalTiles(device=0)
+    sl.generate_matrix(A, "rands", 3)
+    Ad = D(A).clone()
+    U = sl.Matrix(m, n, nb=nb, device=dev)
+    U.insertLocalTiles(device=0)
+    VH = sl.Matrix(n, n, nb=nb, device=dev)
+    VH.insertLocalTiles(device=0)
+    s = sl.svd(A, None, U, VH, {Option.InnerBlocking: 32}).to(dev)
+    assert ((D(U) @ torch.diag(s) @ D(VH) - Ad).abs().max() / (Ad.abs().max() * m)).item() < 1e-13
