@@ -110,6 +110,64 @@ __global__ void scale_row_col_kernel(char equed, i64 m, i64 n, const R* r, const
 }
 
 // ---------------------------------------------------------------------------
+// Recursive random butterfly transform (RBT, src/internal/internal_gerbt.cc
+// in the reference): D levels of block-diagonal butterflies
+// [R0 R1; R0 -R1] / sqrt 2 applied along one dimension (rows or columns) of
+// a local block.  The 2^D elements b + k nidx / 2^D (k < 2^D) are closed
+// under every level, so one thread loads them once, applies all D levels
+// in registers and stores once (one HBM pass instead of D).  On a process
+// grid the padded size makes every butterfly partner local (see
+// models/mixed.py), so the same kernel runs on each rank's local rows.
+template <typename T, typename R, int D>
+__global__ void __launch_bounds__(256)
+butterfly_kernel(bool trans, bool rows, i64 nidx, i64 nother, T* __restrict__ A, i64 lda,
+                 const R* __restrict__ diag, i64 ldd) {
+    constexpr int K = 1 << D;
+    const i64 quarter = nidx >> D;
+    const i64 b = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (b >= quarter) return;
+    const R sq = R(0.70710678118654752440);
+    R dg[D][K];
+    #pragma unroll
+    for (int l = 0; l < D; ++l)
+        #pragma unroll
+        for (int k = 0; k < K; ++k) dg[l][k] = diag[l * ldd + b + k * quarter];
+    for (i64 j = blockIdx.y; j < nother; j += gridDim.y) {
+        T v[K];
+        #pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const i64 idx = b + k * quarter;
+            v[k] = rows ? A[idx + j * lda] : A[j + idx * lda];
+        }
+        #pragma unroll
+        for (int s = 0; s < D; ++s) {
+            const int l = trans ? D - 1 - s : s;
+            const int half = 1 << (D - 1 - l);
+            #pragma unroll
+            for (int k = 0; k < K; ++k) {
+                if ((k & half) != 0) continue;          // k is the top of pair (k, k + half)
+                const T a = v[k], c = v[k + half];
+                const R ra = dg[l][k], rc = dg[l][k + half];
+                if (!trans) {
+                    const T x = s_mul(s_from_real(T(), ra * sq), a), y = s_mul(s_from_real(T(), rc * sq), c);
+                    v[k] = s_add(x, y);
+                    v[k + half] = s_sub(x, y);
+                } else {
+                    v[k] = s_mul(s_from_real(T(), ra * sq), s_add(a, c));
+                    v[k + half] = s_mul(s_from_real(T(), rc * sq), s_sub(a, c));
+                }
+            }
+        }
+        #pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const i64 idx = b + k * quarter;
+            if (rows) A[idx + j * lda] = v[k];
+            else A[j + idx * lda] = v[k];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Row interchanges.  The LAPACK-style swap sequence ipiv[k1..k2) (0-based
 // rows, ipiv[k] >= k) is first folded into a permutation of the touched rows
 // (open-addressing hash map in LDS, built by one thread: O(#swaps)), then
@@ -270,6 +328,21 @@ template <typename T, typename R>
 void gescale_row_col(char equed, i64 m, i64 n, const R* r, const R* c, T* A, i64 lda, hipStream_t s) {
     if (m <= 0 || n <= 0) return;
     hipLaunchKernelGGL((scale_row_col_kernel<T, R>), grid2(m, n), dim3(256), 0, s, equed, m, n, r, c, A, lda);
+    HIP_LAUNCH_CHECK();
+}
+template <typename T, typename R>
+void butterfly(bool trans, bool rows, int depth, i64 nidx, i64 nother, T* A, i64 lda, const R* diag, i64 ldd,
+               hipStream_t s) {
+    if (nidx <= 0 || nother <= 0 || depth <= 0) return;
+    if (depth > 4 || nidx % (1 << depth)) throw std::invalid_argument("butterfly: depth <= 4, n % 2^depth == 0");
+    const i64 quarter = nidx >> depth;
+    dim3 g((unsigned)((quarter + 255) / 256), (unsigned)std::min<i64>(nother, 1024));
+    switch (depth) {
+        case 1: hipLaunchKernelGGL((butterfly_kernel<T, R, 1>), g, dim3(256), 0, s, trans, rows, nidx, nother, A, lda, diag, ldd); break;
+        case 2: hipLaunchKernelGGL((butterfly_kernel<T, R, 2>), g, dim3(256), 0, s, trans, rows, nidx, nother, A, lda, diag, ldd); break;
+        case 3: hipLaunchKernelGGL((butterfly_kernel<T, R, 3>), g, dim3(256), 0, s, trans, rows, nidx, nother, A, lda, diag, ldd); break;
+        default: hipLaunchKernelGGL((butterfly_kernel<T, R, 4>), g, dim3(256), 0, s, trans, rows, nidx, nother, A, lda, diag, ldd); break;
+    }
     HIP_LAUNCH_CHECK();
 }
 template <typename T>
@@ -433,6 +506,10 @@ INSTC(ccplx, ccplx) INSTC(ccplx, zcplx) INSTC(zcplx, ccplx) INSTC(zcplx, zcplx)
 INSTC(float, ccplx) INSTC(double, zcplx) INSTC(zcplx, double) INSTC(ccplx, float)
 #undef INSTC
 template void gescale_row_col<float, float>(char, i64, i64, const float*, const float*, float*, i64, hipStream_t);
+template void butterfly<float, float>(bool, bool, int, i64, i64, float*, i64, const float*, i64, hipStream_t);
+template void butterfly<double, double>(bool, bool, int, i64, i64, double*, i64, const double*, i64, hipStream_t);
+template void butterfly<ccplx, float>(bool, bool, int, i64, i64, ccplx*, i64, const float*, i64, hipStream_t);
+template void butterfly<zcplx, double>(bool, bool, int, i64, i64, zcplx*, i64, const double*, i64, hipStream_t);
 template void gescale_row_col<double, double>(char, i64, i64, const double*, const double*, double*, i64, hipStream_t);
 template void gescale_row_col<ccplx, float>(char, i64, i64, const float*, const float*, ccplx*, i64, hipStream_t);
 template void gescale_row_col<zcplx, double>(char, i64, i64, const double*, const double*, zcplx*, i64, hipStream_t);

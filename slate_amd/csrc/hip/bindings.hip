@@ -215,6 +215,11 @@ static void register_kernels(py::module& m) {
         dispatch(dt, [&](auto z) { using T = decltype(z); using R = typename scalar_traits<T>::real;
             gescale_row_col<T, R>(equed, mm, n, P<R>(r), P<R>(c), P<T>(A), lda, S(st)); });
     });
+    m.def("butterfly", [](char dt, bool trans, bool rows, int depth, i64 nidx, i64 nother, uintptr_t A, i64 lda,
+                          uintptr_t diag, i64 ldd, uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z); using R = typename scalar_traits<T>::real;
+            butterfly<T, R>(trans, rows, depth, nidx, nother, P<T>(A), lda, P<R>(diag), ldd, S(st)); });
+    });
     m.def("genorm", [](char dt, char norm, char uplo, char diag, bool herm, i64 mm, i64 n, uintptr_t A, i64 lda,
                        uintptr_t out, uintptr_t st) {
         dispatch(dt, [&](auto z) { using T = decltype(z); using R = typename scalar_traits<T>::real;

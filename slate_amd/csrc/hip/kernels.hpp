@@ -32,6 +32,9 @@ void geadd(char uplo, i64 m, i64 n, T alpha, const T* A, i64 lda, T beta, T* B, 
 template <typename Ts, typename Td>
 void gecopy(char uplo, char trans, i64 m, i64 n, const Ts* A, i64 lda, Td* B, i64 ldb, hipStream_t s);
 template <typename T, typename R>
+void butterfly(bool trans, bool rows, int depth, i64 nidx, i64 nother, T* A, i64 lda, const R* diag, i64 ldd,
+               hipStream_t s);
+template <typename T, typename R>
 void gescale_row_col(char equed, i64 m, i64 n, const R* r, const R* c, T* A, i64 lda, hipStream_t s);
 template <typename T>
 void laswp(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, int incx, hipStream_t s);

@@ -730,6 +730,29 @@ void register_tile_kernels(py::module& m) {
         dispatch(dt, [&](auto z) { using T = decltype(z);
             genorm<T>(norm, uplo, diag, herm, mm, n, P<T>(A), lda, P<real_t<T>>(out)); });
     });
+    m.def("butterfly", [](char dt, bool trans, bool rows, int depth, i64 nidx, i64 nother, uintptr_t A, i64 lda,
+                          uintptr_t diag, i64 ldd, uintptr_t) {
+        dispatch(dt, [&](auto z) { using T = decltype(z); using R = real_t<T>;
+            if (depth <= 0 || nidx <= 0 || nother <= 0) return;
+            if (nidx % (i64(1) << depth)) throw std::invalid_argument("butterfly: n % 2^depth != 0");
+            const R* dg = P<R>(diag);
+            T* a = P<T>(A);
+            const R sq = R(0.70710678118654752440);
+            auto at = [&](i64 idx, i64 j) -> T& { return rows ? a[idx + j * lda] : a[j + idx * lda]; };
+            for (int s = 0; s < depth; ++s) {
+                const int l = trans ? depth - 1 - s : s;
+                const i64 size = nidx >> l, h = size / 2;
+                for (i64 o = 0; o < nidx; o += size)
+                    for (i64 j = 0; j < nother; ++j)
+                        for (i64 i = 0; i < h; ++i) {
+                            const T x = at(o + i, j), y = at(o + h + i, j);
+                            const R r0 = dg[l * ldd + o + i] * sq, r1 = dg[l * ldd + o + h + i] * sq;
+                            if (!trans) { at(o + i, j) = r0 * x + r1 * y; at(o + h + i, j) = r0 * x - r1 * y; }
+                            else { at(o + i, j) = r0 * (x + y); at(o + h + i, j) = r1 * (x - y); }
+                        }
+            }
+        });
+    });
     m.def("gescale_row_col", [](char dt, char equed, i64 mm, i64 n, uintptr_t r, uintptr_t c, uintptr_t A, i64 lda,
                                 uintptr_t) {
         dispatch(dt, [&](auto z) { using T = decltype(z); using R = real_t<T>;

@@ -269,7 +269,7 @@ def posv_mixed_gmres(A, B, X, opts=None):
 
 
 # ------------------------------------------------------------------ RBT
-def _butterfly_diag(n, depth, seed, dtype, device):
+def _butterfly_diag(n, depth, seed, dtype=torch.float64, device="cpu"):
     """Random diagonals of the recursive butterflies (depth levels):
     entries exp(r / 10), r uniform in [-1/2, 1/2) (Baboulin et al.)."""
     g = torch.Generator().manual_seed(int(seed))
@@ -277,83 +277,108 @@ def _butterfly_diag(n, depth, seed, dtype, device):
     return torch.exp(r / 10.0).to(dtype).to(device)
 
 
-def _apply_butterfly(D, diags, trans, side):
-    """Apply W = W_depth ... W_1 (each level block-diagonal with 2^l
-    butterflies [R0 R1; R0 -R1]/sqrt 2) to the rows (side 'L') or columns
-    ('R') of dense D in place; trans applies W^T."""
-    n = D.shape[0] if side == 'L' else D.shape[1]
-    depth = diags.shape[0]
-    X = D if side == 'L' else D.transpose(0, 1)
-    levels = range(depth) if not trans else range(depth - 1, -1, -1)
-    for lvl in levels:
-        nblk = 2 ** lvl
-        size = n // nblk
-        if size < 2:
-            continue
-        h = size // 2
-        for b in range(nblk):
-            o = b * size
-            r0 = diags[lvl, o:o + h][:, None]
-            r1 = diags[lvl, o + h:o + 2 * h][:, None]
-            top = X[o:o + h].clone()
-            bot = X[o + h:o + 2 * h].clone()
-            s = 1.0 / math.sqrt(2.0)
-            if not trans:
-                # [R0 R1; R0 -R1] / sqrt 2  applied to [top; bot]
-                X[o:o + h] = s * (r0 * top + r1 * bot)
-                X[o + h:o + 2 * h] = s * (r0 * top - r1 * bot)
-            else:
-                # transpose: [R0 R0; R1 -R1] / sqrt 2
-                X[o:o + h] = s * r0 * (top + bot)
-                X[o + h:o + 2 * h] = s * r1 * (top - bot)
-    return D
+def rbt_size(n, depth, nb, p=1, q=1):
+    """Order the butterflies act on: n padded to a multiple of
+    2^depth nb lcm(p, q).  Then every butterfly partner (global distance
+    >= N / 2^depth, a multiple of nb p and nb q) lies on the SAME process
+    row / column, at local distance (global distance) / p (or / q): the
+    transform is a purely local kernel on every rank, no communication
+    (SLATE pairs tiles across ranks with tile sends, internal_gerbt.cc)."""
+    unit = (1 << depth) * nb * (p * q // math.gcd(p, q))
+    return max(unit, -(-n // unit) * unit)
 
 
-def gerbt(U, A, V, depth=2, seed=7):
-    """A := U^T A V with random butterflies (returned diagonals (du, dv))."""
-    D = allgather_dense(A).clone()
-    n = D.shape[0]
-    du = _butterfly_diag(n, depth, seed, D.dtype, D.device)
-    dv = _butterfly_diag(n, depth, seed + 1, D.dtype, D.device)
-    _apply_butterfly(D, du, True, 'L')        # U^T A
-    _apply_butterfly(D, dv, True, 'R')        # (U^T A) V : columns
-    from_dense(A, D)
-    return du, dv
+class Butterfly:
+    """W = W_depth ... W_1 of order N (the RBT factor U or V); ``diag``
+    (depth x N host fp64) holds the random diagonals."""
+
+    def __init__(self, N, depth, seed):
+        self.N, self.depth = N, depth
+        self.diag = _butterfly_diag(N, depth, seed)
+
+    def local(self, rows_global, dtype, device):
+        rdt = torch.float32 if dtype in (torch.float32, torch.complex64) else torch.float64
+        d = self.diag[:, rows_global] if rows_global is not None else self.diag
+        return d.to(rdt).contiguous().to(device)
+
+
+def _local_index(M, dim):
+    lb = M.local_block()
+    if dim == 'row':
+        return lb, torch.as_tensor([lb.global_row(i) for i in range(lb.mloc)], dtype=torch.int64)
+    return lb, torch.as_tensor([lb.global_col(j) for j in range(lb.nloc)], dtype=torch.int64)
+
+
+def _apply_w(W: Butterfly, M, trans, side):
+    """M := op(W) M (side 'L', on M's rows) or M op(W)^T (side 'R', on M's
+    column index), op(W) = W^T when ``trans``; locally on every rank (see
+    rbt_size)."""
+    s = M.storage
+    if s.bc is None:
+        raise SlateError("RBT needs a block-cyclic matrix")
+    lb, idx = _local_index(M, 'row' if side == 'L' else 'col')
+    if idx.numel() == 0 or (lb.mloc == 0 or lb.nloc == 0):
+        return
+    X = lb.data[:lb.mloc, :lb.nloc]
+    ops.butterfly(X, W.local(idx, s.dtype, X.device), W.depth, trans, side)
+    s.mark_local_modified(s.origin_slot)
+
+
+def gerbt(U, A, V):
+    """A := U^T A V in place (SLATE gerbt(U, A, V), src/gerbt.cc); U, V are
+    :class:`Butterfly` of A's order (a multiple of rbt_size's unit)."""
+    with trace_block("gerbt"):
+        _apply_w(U, A, True, 'L')         # U^T A
+        _apply_w(V, A, True, 'R')         # (U^T A) V = (U^T A) (W^T)^T
+    return A
+
+
+def _padded(M, N, ncols=None, identity=False):
+    """N x ncols copy of M (zero padding; identity on the padded diagonal)."""
+    from .aux import set as aset
+    s, bc = M.storage, M.storage.bc
+    ncols = N if ncols is None else ncols
+    Pm = Matrix(N, ncols, nb=bc.nb, p=bc.p, q=bc.q, comm=s.comm, dtype=s.dtype, device=s.device, order=bc.order)
+    Pm.insertLocalTiles(device=s.device.index if s.device.type == "cuda" else -1)
+    aset(0.0, 1.0 if identity else 0.0, Pm)
+    copy(M, Pm.slice(0, M.m() - 1, 0, M.n() - 1))
+    return Pm
 
 
 def gesv_rbt(A, B, opts=None):
     """Solve A X = B with a random butterfly transform + LU without pivoting
-    + iterative refinement in working precision (src/gesv_rbt.cc)."""
-    from .lu import getrf_nopiv, getrs_nopiv, gesv
+    + iterative refinement in working precision (src/gesv_rbt.cc).  A is
+    embedded in diag(A, I) of the padded order when n is not a multiple of
+    rbt_size's unit (no silent switch to partial pivoting)."""
+    from .lu import getrf_nopiv, getrs_nopiv
     with trace_block("gesv_rbt"):
-        depth = int(get_option(opts, Option.Depth, 2))
+        depth = max(1, min(4, int(get_option(opts, Option.Depth, 2))))
         n = A.n()
-        pad = (1 << depth)
-        if n % pad:
-            # butterflies need n divisible by 2^depth: partial pivoting instead
-            from ..core.enums import MethodLU
-            o = dict(opts or {})
-            o[Option.MethodLU] = MethodLU.PartialPiv
-            return gesv(A, Pivots(), B, o)
+        bc = A.storage.bc
+        if bc is None:
+            from .aux import run_on_block_cyclic
+            return run_on_block_cyclic(A, lambda Ab, o: gesv_rbt(Ab, B, o), opts)
+        N = rbt_size(n, depth, bc.nb, bc.p, bc.q)
         A0 = _like(A)
         copy(A, A0)
-        du, dv = gerbt(None, A, None, depth)
-        info = getrf_nopiv(A, opts)
+        Ap = A if N == n else _padded(A, N, identity=True)
+        U = Butterfly(N, depth, 7)
+        V = Butterfly(N, depth, 8)
+        gerbt(U, Ap, V)
+        info = getrf_nopiv(Ap, opts)
         if info:
             return info
         anorm = float(norm(Norm.Inf, A0))
 
         def solve(R):
-            # x = V (LU)^{-1} U^T r
-            Rd = allgather_dense(R).clone()
-            _apply_butterfly(Rd, du, True, 'L')
-            Y = _like(R)
-            from_dense(Y, Rd)
-            getrs_nopiv(A, Y, opts)
-            Yd = allgather_dense(Y).clone()
-            _apply_butterfly(Yd, dv, False, 'L')
-            from_dense(Y, Yd)
-            return Y
+            # x = V (LU)^{-1} U^T r  (on the padded order)
+            Y = _padded(R, N, R.n())
+            _apply_w(U, Y, True, 'L')
+            getrs_nopiv(Ap, Y, opts)
+            _apply_w(V, Y, False, 'L')
+            D = _like(R)
+            copy(Y.slice(0, n - 1, 0, R.n() - 1), D)
+            return D
         X = solve(B)
         _refine(A0, B, X, solve, {**(opts or {}), Option.MaxIterations: int(get_option(opts, Option.MaxIterations,
                                                                                        10))}, anorm)

@@ -359,6 +359,22 @@ def gescale_row_col(equed, r, c, A):
     return A
 
 
+def butterfly(A, diag, depth, trans=False, side='L'):
+    """Random butterfly transform in place: side 'L' A := op(W) A (rows),
+    side 'R' A := A op(W)^T (op(W) applied to the column index), op(W) = W^T
+    when ``trans``; W = W_depth ... W_1, diag (depth x n real, row l = level
+    l's butterfly diagonals, n = length of the transformed dimension).  One
+    pass over A for all levels."""
+    _chk(A)
+    m, n = A.shape
+    rows = side.upper() == 'L'
+    nidx, nother = (m, n) if rows else (n, m)
+    if nidx and nother:
+        kmod(A).butterfly(code(A.dtype), bool(trans), rows, int(depth), nidx, nother, A.data_ptr(), ld(A),
+                          diag.data_ptr(), diag.stride(0), stream(A))
+    return A
+
+
 def genorm_local(norm, A, uplo='G', diag='N', herm=False):
     """Local norm contributions: returns (colvals, rowvals) real tensors on
     A's device: 'M'/'1' -> per-column max/sum, 'F' -> per-column

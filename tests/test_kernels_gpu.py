@@ -13,8 +13,7 @@ TOL = {torch.float64: 1e-12, torch.float32: 2e-5, torch.complex128: 1e-12, torch
 def cm(m, n, dt, seed=0, dev="cuda"):
     g = torch.Generator(device="cpu").manual_seed(seed)
     x = torch.randn(n, m, dtype=dt, generator=g).t()
-    return ops.as_colmajor(x.clone()).to(dev) if False else x.contiguous().t().contiguous().t().to(dev) \
-        if False else _cm(x.t().contiguous().t(), dev)
+    return _cm(x, dev)
 
 
 def _cm(x, dev):
@@ -412,3 +411,31 @@ def test_matgen_device_equals_host(dt):
         ops.matgen(kind, 1234, H, m, n, nb, 1, 0, nb, 1, 0)
         ops.matgen(kind, 1234, D, m, n, nb, 1, 0, nb, 1, 0)
         assert (D.cpu() - H).abs().max() < 1e-6
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("depth", [1, 2, 4])
+def test_butterfly_gpu(dt, depth):
+    """One-pass RBT kernel (all levels in registers) vs the explicit dense
+    butterfly product, rows and column index, W and W^T."""
+    from slate_amd.models.mixed import _butterfly_diag
+    n, m = 256, 40
+    dg = _butterfly_diag(n, depth, 5)
+    W = torch.eye(n, dtype=torch.float64)
+    for lvl in range(depth):
+        size, Wl = n >> lvl, torch.zeros(n, n, dtype=torch.float64)
+        h = size // 2
+        i = torch.arange(h)
+        for o in range(0, n, size):
+            r0, r1 = dg[lvl, o + i], dg[lvl, o + h + i]
+            Wl[o + i, o + i], Wl[o + i, o + h + i] = r0, r1
+            Wl[o + h + i, o + i], Wl[o + h + i, o + h + i] = r0, -r1
+        W = (Wl / 2 ** 0.5) @ W
+    rdt = torch.float32 if dt in (torch.float32, torch.complex64) else torch.float64
+    X, Y = cm(n, m, dt, 1), cm(m, n, dt, 2)
+    for trans in (False, True):
+        opW = (W.mT if trans else W).to(ref(X).dtype).cuda()
+        got = ops.butterfly(X.clone(), dg.to(rdt).cuda(), depth, trans, 'L')
+        assert (ref(got) - opW @ ref(X)).abs().max().item() < TOL[dt] * 10
+        got = ops.butterfly(Y.clone(), dg.to(rdt).cuda(), depth, trans, 'R')
+        assert (ref(got) - ref(Y) @ opW.mT).abs().max().item() < TOL[dt] * 10

@@ -6,6 +6,7 @@ import pytest
 import torch
 
 import slate_amd as sl
+from slate_amd.core.enums import Option
 from slate_amd.models.aux import allgather_dense as D
 
 from dist_util import run_dist
@@ -92,6 +93,61 @@ def test_rbt():
     A0, B0 = D(A).clone(), D(B).clone()
     assert sl.gesv_rbt(A, B) == 0
     assert (A0 @ D(B) - B0).abs().max() < 1e-11
+
+
+@pytest.mark.parametrize("dt", [torch.float64, torch.complex128, torch.float32])
+@pytest.mark.parametrize("depth", [1, 2, 3])
+def test_butterfly_op_vs_dense(dt, depth):
+    """ops.butterfly (all levels in one pass) against the explicit dense
+    W = W_depth ... W_1, on rows and on the column index, W and W^T."""
+    from slate_amd import ops
+    from slate_amd.models.mixed import _butterfly_diag
+    n, m = 48, 20
+    dg = _butterfly_diag(n, depth, 3)
+    W = torch.eye(n, dtype=torch.float64)
+    for lvl in range(depth):
+        size = n >> lvl
+        h = size // 2
+        Wl = torch.zeros(n, n, dtype=torch.float64)
+        for o in range(0, n, size):
+            for i in range(h):
+                r0, r1 = dg[lvl, o + i], dg[lvl, o + h + i]
+                Wl[o + i, o + i], Wl[o + i, o + h + i] = r0, r1
+                Wl[o + h + i, o + i], Wl[o + h + i, o + h + i] = r0, -r1
+        W = (Wl / 2 ** 0.5) @ W
+    W = W.to(dt)
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn(n, m, generator=g, dtype=torch.float64).to(dt).t().contiguous().t()
+    Y = torch.randn(m, n, generator=g, dtype=torch.float64).to(dt).t().contiguous().t()
+    rdt = torch.float32 if dt in (torch.float32, torch.complex64) else torch.float64
+    tol = 1e-5 if rdt == torch.float32 else 1e-13
+    for trans in (False, True):
+        opW = W.mT if trans else W
+        assert (ops.butterfly(X.clone(), dg.to(rdt), depth, trans, 'L') - opW @ X).abs().max() < tol
+        assert (ops.butterfly(Y.clone(), dg.to(rdt), depth, trans, 'R') - Y @ opW.mT).abs().max() < tol
+
+
+def _rbt_grid(rank, size, p, q):
+    for n, nb in ((100, 16), (128, 16), (37, 8)):
+        A = sl.Matrix(n, n, nb=nb, p=p, q=q)
+        A.insertLocalTiles()
+        sl.generate_matrix(A, "rands", 9)
+        B = sl.Matrix(n, 3, nb=nb, p=p, q=q)
+        B.insertLocalTiles()
+        sl.generate_matrix(B, "rands", 10)
+        A0, B0 = D(A).clone(), D(B).clone()
+        assert sl.gesv_rbt(A, B, {Option.Depth: 2}) == 0
+        assert (A0 @ D(B) - B0).abs().max() < 1e-11 * n
+
+
+@pytest.mark.parametrize("grid", [(1, 1), (2, 2), (1, 3), (2, 1)], ids=lambda g: f"{g[0]}x{g[1]}")
+def test_rbt_grid(grid):
+    """RBT on the grid with padding (n not a multiple of the unit): every
+    butterfly is local, no partial-pivoting fallback."""
+    if grid == (1, 1):
+        _rbt_grid(0, 1, 1, 1)
+    else:
+        run_dist(_rbt_grid, grid[0] * grid[1], *grid)
 
 
 def test_inverses():
