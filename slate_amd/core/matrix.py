@@ -707,12 +707,22 @@ class HermitianMatrix(_SquareSym):
 
 
 # ------------------------------------------------------------------ band
+def _band_storage(m, n, nb, kl_store, ku_store, comm, dtype, device):
+    """Compact band storage (core/band_storage.py): only the tiles within
+    kl_store / ku_store of the diagonal exist, 1-D column-cyclic over all
+    ranks (the p x q arguments of the band constructors only fix the
+    communicator, as ScaLAPACK's band routines use a 1-D grid)."""
+    from .band_storage import BandStorage, tiles_for
+    comm = comm or _comm.world()
+    return BandStorage(m, n, nb, tiles_for(kl_store, nb), tiles_for(ku_store, nb), comm, dtype, device)
+
+
 class BaseBandMatrix(BaseMatrix):
     """Band matrix: kl sub-, ku super-diagonals (`BaseBandMatrix.hh:27-368`).
 
-    Stored block-cyclically like a general matrix (only the tiles touching
-    the band are ever read or written by the band drivers); the bandwidths
-    are metadata, as in SLATE."""
+    Compact storage: only the tiles touching the band (plus, for general
+    band matrices, the kl extra upper tile diagonals of the LU fill-in) are
+    allocated, as per-column slabs (core/band_storage.py)."""
 
     def __init__(self, storage, kl, ku, **kw):
         super().__init__(storage, **kw)
@@ -747,7 +757,7 @@ class BandMatrix(BaseBandMatrix):
             self._kl, self._ku = kl, ku
             return
         if _storage is None:
-            _storage = _make_storage(m, n, nb, nb, p, q, comm, dtype, device)
+            _storage = _band_storage(m, n, nb, kl, ku + kl, comm, dtype, device)
         super().__init__(_storage, kl, ku, **kw)
 
     def _new_of_kind(self, st):
@@ -765,6 +775,8 @@ class BaseTriangularBandMatrix(BaseBandMatrix):
 
 
 class TriangularBandMatrix(BaseTriangularBandMatrix):
+    _kind = "trapezoid"
+
     def __init__(self, uplo=Uplo.Lower, diag=Diag.NonUnit, n=0, kd=0, nb=256, p=None, q=None, comm=None,
                  dtype=torch.float64, device=None, _storage=None, matrix=None, **kw):
         if matrix is not None:
@@ -773,11 +785,14 @@ class TriangularBandMatrix(BaseTriangularBandMatrix):
             self._kl, self._ku = (kd, 0) if self._uplo == Uplo.Lower else (0, kd)
             return
         if _storage is None:
-            _storage = _make_storage(n, n, nb, nb, p, q, comm, dtype, device)
+            lo = Uplo(uplo) == Uplo.Lower
+            _storage = _band_storage(n, n, nb, kd if lo else 0, 0 if lo else kd, comm, dtype, device)
         super().__init__(_storage, uplo, kd, diag=diag, **kw)
 
 
 class HermitianBandMatrix(BaseTriangularBandMatrix):
+    _kind = "hermitian"
+
     def __init__(self, uplo=Uplo.Lower, n=0, kd=0, nb=256, p=None, q=None, comm=None, dtype=torch.float64,
                  device=None, _storage=None, matrix=None, **kw):
         if matrix is not None:
@@ -786,7 +801,8 @@ class HermitianBandMatrix(BaseTriangularBandMatrix):
             self._kl, self._ku = (kd, 0) if self._uplo == Uplo.Lower else (0, kd)
             return
         if _storage is None:
-            _storage = _make_storage(n, n, nb, nb, p, q, comm, dtype, device)
+            lo = Uplo(uplo) == Uplo.Lower
+            _storage = _band_storage(n, n, nb, kd if lo else 0, 0 if lo else kd, comm, dtype, device)
         super().__init__(_storage, uplo, kd, **kw)
 
 

@@ -153,13 +153,16 @@ def _storage_dense(s) -> torch.Tensor:
             full[rows[:, None], cols[None, :]] = allp[r][:ml, :nl]
         return full
     # per-tile storage: owners broadcast their tiles
+    inw = getattr(s, "in_window", None)
     for j in range(s.nt):
         for i in range(s.mt):
+            if inw is not None and not inw(i, j):
+                continue                      # band storage: tile does not exist anywhere
             owner = s.tileRank((i, j))
             r0, c0 = s.row_offsets[i], s.col_offsets[j]
             mb, nb = s.tileMb(i), s.tileNb(j)
             blk = torch.zeros((mb, nb), dtype=s.dtype, device=dev)
-            if owner == comm.rank:
+            if owner == comm.rank and s.tileExists(i, j):
                 o = s.table.origin(i, j)
                 if o < 0:
                     o = s.origin_slot if s.origin_slot is not None else HOST
@@ -204,9 +207,12 @@ def from_dense(A, D: torch.Tensor):
             lb.data.copy_(D[rows[:, None], cols[None, :]].to(lb.data.device, lb.data.dtype))
         s.mark_local_modified(s.origin_slot)
         return A
+    inw = getattr(s, "in_window", None)
     for j in range(A._nt):
         for i in range(A._mt):
             gi, gj = A.ioffset + i, A.joffset + j
+            if inw is not None and not inw(gi, gj):
+                continue
             if s.tileIsLocal(gi, gj):
                 d = s.tile_data(gi, gj, s.origin_slot if s.origin_slot is not None else HOST)
                 if d is None:
@@ -411,8 +417,8 @@ def norm(norm_type, A, opts=None, scope=NormScope.Matrix):
     Hermitian with one stored triangle).  NaN propagates."""
     nt = Norm.from_string(norm_type) if not isinstance(norm_type, Norm) else norm_type
     s = A.storage
-    if s.bc is None:
-        from .aux import allgather_dense as _ad  # noqa
+    band = hasattr(s, "in_window") and not (A.ioffset or A.joffset or A.row0_offset or A.col0_offset)
+    if s.bc is None and not band:
         D = allgather_dense(A)
         return _dense_norm(nt, D, A)
     kind = _diag_kind(A)
@@ -421,17 +427,41 @@ def norm(norm_type, A, opts=None, scope=NormScope.Matrix):
     # op: norms of A^T swap One <-> Inf
     if A.op() != Op.NoTrans and not herm:
         nt = {Norm.One: Norm.Inf, Norm.Inf: Norm.One}.get(nt, nt)
-    lb = A.local_block()
     comm = s.comm
     m_g, n_g = A._um(), A._un()
-    dev = lb.data.device
+    if band:
+        # compact band storage: the stored tiles (outside entries are zero)
+        slot = s.band_slot()
+        dev = s.get_slab(slot).device
+        up = A.uploPhysical() if kind != "general" else None
+
+        def pieces():
+            for (i, j, sl) in list(s.tiles.keys()):
+                if sl != slot or not s.tileIsLocal(i, j):
+                    continue
+                if up is not None and ((i < j) if up == Uplo.Lower else (i > j)):
+                    continue
+                r0, c0 = s.row_offsets[i], s.col_offsets[j]
+                t = s.tiles[(i, j, sl)]
+                u = up.value if (up is not None and i == j) else 'G'
+                yield t, u, list(range(r0, r0 + t.shape[0])), list(range(c0, c0 + t.shape[1]))
+        if A.op() != Op.NoTrans:
+            m_g, n_g = n_g, m_g
+    else:
+        lb = A.local_block()
+        dev = lb.data.device
+
+        def pieces():
+            if lb.mloc and lb.nloc and s.bc.pr >= 0:
+                for blk, u in _local_uplo_blocks(A, lb):
+                    gr, gc = _piece_globals(blk, lb)
+                    yield blk, u, gr, gc
     rdt = torch.float64 if s.dtype in (torch.float64, torch.complex128) else torch.float32
     code = {Norm.Max: 'M', Norm.One: '1', Norm.Inf: 'I', Norm.Fro: 'F'}[nt]
     colv = torch.zeros(n_g * (2 if code == 'F' else 1), dtype=rdt, device=dev)
     rowv = torch.zeros(m_g, dtype=rdt, device=dev)
-    if lb.mloc and lb.nloc and s.bc.pr >= 0:
-        for blk, u in _local_uplo_blocks(A, lb):
-            gr, gc = _piece_globals(blk, lb)
+    if True:
+        for blk, u, gr, gc in pieces():
             gc_t = torch.as_tensor(gc, device=dev)
             gr_t = torch.as_tensor(gr, device=dev)
             on_diag = u != 'G'

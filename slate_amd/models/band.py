@@ -1,30 +1,49 @@
 """Band drivers: gbtrf / gbtrs / gbsv (band LU with partial pivoting),
-pbtrf / pbtrs / pbsv (band Cholesky), gbmm, hbmm, tbsm.
+pbtrf / pbtrs / pbsv (band Cholesky), tbsm (triangular band solve, with
+the gbtrf pivots: tbsmPivots), gbmm, hbmm, band_mask.
 
 Reference: `src/gbtrf.cc:20-348` (panel + band-limited trailing update,
-upper bandwidth grows to kl+ku), `src/gbtrs.cc`, `src/gbsv.cc`,
-`src/pbtrf.cc`, `src/pbtrs.cc`, `src/pbsv.cc`, `src/gbmm.cc`, `src/hbmm.cc`,
-`src/tbsm.cc`, `src/tbsmPivots.cc`.
+upper bandwidth grows to kl + ku), `src/gbtrs.cc`, `src/gbsv.cc`,
+`src/pbtrf.cc`, `src/pbtrs.cc`, `src/pbsv.cc`, `src/tbsm.cc`,
+`src/tbsmPivots.cc`, `src/gbmm.cc`, `src/hbmm.cc`.
 
-MI355X design: band matrices use the same block-cyclic local buffer as
-general ones (SLATE also stores whole tiles).  On one rank the
-factorizations run a band-limited step loop directly on the device buffer
-(the GPU LU panel over the kb+kl rows that can be non-zero, trailing TRSM +
-MFMA GEMM only inside the (kl+ku)-wide window), so the cost is
-O(n kl (kl+ku)) not O(n^3).  On a grid, entries outside the band are
-zeroed and the dense distributed drivers run (pivot rows can never leave
-the band because all rows below it are zero, so the result is the band
-factorization).  Solves and products go through the dense drivers on the
-zero-masked operands.
+MI355X design on the compact band storage (core/band_storage.py: tile
+columns 1-D cyclic over the ranks, each local tile column one contiguous
+slab of its band tiles):
+
+* factorizations: the panel of tile column k is ONE contiguous slab block
+  on its owner (GPU LU with partial pivoting over the kb + kl rows that can
+  be non-zero, or potrf + trsm); panel and pivots travel in one packed
+  broadcast; every rank then updates ITS tile columns inside the window
+  (k, k + KU] -- swaps, trsm and one MFMA GEMM per column, each on a
+  contiguous slab sub-block (the rows shift by one tile per column, so the
+  columns cannot share a launch).  The owner of column k + 1 updates it
+  first, so its next panel overlaps the other ranks' updates.  Cost
+  O(n kl (kl + ku)), memory O(n (kl + ku)).
+* solves: the right-hand side is replicated (O(n nrhs), vectors only) and
+  swept tile by tile; the owner of each factor column applies it and
+  broadcasts the rows it changed (kb + bandwidth rows), so every rank's
+  copy stays exact; each rank finally keeps its own part of B.
+* products: B is replicated in column chunks; each rank multiplies its
+  slabs, the partial results are summed with one all-reduce per chunk.
 """
 from __future__ import annotations
 
 import torch
 
 from .. import ops
-from ..core.enums import Diag, Side, Uplo
-from ..core.matrix import Pivots, TriangularMatrix
+from ..core.band_storage import BandStorage, tiles_for
+from ..core.enums import Diag, Op, Side, Uplo
+from ..core.exceptions import SlateError
+from ..core.matrix import Pivots
 from ..utils.trace import trace_block
+from ._util import conj_trans
+
+_LOWER_MASK = (1, 1 << 40, 1, 0, 1, 0, 0, 0, 0)      # element-level lower triangle of the output
+
+
+def _is_band(A):
+    return isinstance(A.storage, BandStorage)
 
 
 def _bands(A):
@@ -33,11 +52,58 @@ def _bands(A):
     return kl, ku
 
 
+def _need_band(A, who):
+    if not _is_band(A):
+        raise SlateError(f"{who}: needs a band matrix (BandMatrix / HermitianBandMatrix / TriangularBandMatrix)")
+    if A.ioffset or A.joffset or A.row0_offset or A.col0_offset:
+        raise SlateError(f"{who}: sub-matrix views of band matrices are not supported")
+
+
+# ------------------------------------------------------------------ masks
+def _zero_lower(t, s):
+    """Zero the entries (a, b) of tile t with a - b >= s."""
+    mb, nbt = t.shape
+    if mb == 0 or nbt == 0 or s > mb - 1:
+        return
+    if s >= 0:
+        ops.geset(0.0, 0.0, t[s:, :], uplo='L')
+        return
+    c = min(-s, nbt)
+    ops.geset(0.0, 0.0, t[:, :c])
+    if c < nbt:
+        ops.geset(0.0, 0.0, t[:, c:], uplo='L')
+
+
+def _zero_upper(t, s):
+    """Zero the entries (a, b) of tile t with b - a >= s."""
+    mb, nbt = t.shape
+    if mb == 0 or nbt == 0 or s > nbt - 1:
+        return
+    if s >= 0:
+        ops.geset(0.0, 0.0, t[:, s:], uplo='U')
+        return
+    r = min(-s, mb)
+    ops.geset(0.0, 0.0, t[:r, :])
+    if r < mb:
+        ops.geset(0.0, 0.0, t[r:, :], uplo='U')
+
+
 def band_mask(A, kl=None, ku=None):
-    """Zero every local entry outside -ku <= i - j <= kl (global indices)."""
+    """Zero every stored entry outside -ku <= i - j <= kl (global indices)."""
     s = A.storage
     if kl is None:
-        kl, ku = _bands(A)
+        kl, ku = (A._kl, A._ku) if hasattr(A, "_kl") else _bands(A)
+    if _is_band(A):
+        slot = s.band_slot()
+        for (i, j, sl) in list(s.tiles.keys()):
+            if sl != slot or not s.tileIsLocal(i, j):
+                continue
+            t = s.tiles[(i, j, sl)]
+            d = s.row_offsets[i] - s.col_offsets[j]
+            _zero_lower(t, kl - d + 1)
+            _zero_upper(t, ku + d + 1)
+        s.mark_local_modified(slot)
+        return A
     lb = A.local_block()
     if lb.mloc == 0 or lb.nloc == 0:
         return A
@@ -45,71 +111,200 @@ def band_mask(A, kl=None, ku=None):
     gr = torch.tensor([lb.global_row(i) for i in range(lb.mloc)], device=dev)
     gc = torch.tensor([lb.global_col(j) for j in range(lb.nloc)], device=dev)
     d = gr[:, None] - gc[None, :]
-    outside = (d > kl) | (d < -ku)
-    lb.data.masked_fill_(outside, 0)
+    lb.data.masked_fill_((d > kl) | (d < -ku), 0)
     s.mark_local_modified(s.origin_slot)
     return A
 
 
-def _single(A):
+# ------------------------------------------------------------------ helpers
+def _slab(A):
     s = A.storage
-    return s.comm.size == 1 or (s.bc is not None and s.bc.p * s.bc.q == 1)
+    slot = s.band_slot()
+    return s, slot, s.sync_slab(slot)
+
+
+def _col_block(s, buf, k, g_lo, g_hi):
+    """Slab block of tile column k holding global rows [g_lo, g_hi)."""
+    r = s.slab_row(g_lo, k)
+    c = s.local_col(k)
+    return buf[r:r + (g_hi - g_lo), c:c + s.tileNb(k)]
+
+
+def _bcast_rows(comm, X, lo, hi, root):
+    if comm.size == 1 or hi <= lo:
+        return
+    tmp = X[lo:hi].contiguous()
+    comm.bcast(tmp, root)
+    X[lo:hi].copy_(tmp)
+
+
+def _cm_copy(D, dev):
+    X = ops.colmajor_empty(D.shape[0], D.shape[1], D.dtype, dev)
+    X.copy_(D)
+    return X
+
+
+def _replicated(B, dev):
+    """B (thin right-hand side) replicated on every rank, column-major."""
+    from .aux import allgather_dense
+    return _cm_copy(allgather_dense(B), dev)
+
+
+def _store(B, X):
+    from .aux import from_dense
+    from_dense(B, X)
 
 
 # ------------------------------------------------------------------ LU
 def gbtrf(A, pivots: Pivots, opts=None) -> int:
-    """Band LU with partial pivoting; pivots are global row indices."""
-    from .lu import getrf
+    """Band LU with partial pivoting (pivots: global 0-based rows).  The
+    upper bandwidth of A becomes kl + ku (fill-in), as in SLATE."""
+    _need_band(A, "gbtrf")
+    if A.op() != Op.NoTrans:
+        raise SlateError("gbtrf: pass the band matrix itself")
     with trace_block("gbtrf"):
         kl, ku = _bands(A)
         band_mask(A, kl, ku)
-        if not _single(A):
-            info = getrf(A, pivots, opts)
-            return info
-        s = A.storage
-        from ._util import target_slot
-        slot = target_slot(A, opts)
-        buf = s.prepare_local(slot)
-        m, n = s.m, s.n
-        nb = s.bc.nb
-        kt = (min(m, n) + nb - 1) // nb
-        dev = buf.device
-        ipiv = torch.zeros(max(min(m, n), 1), dtype=torch.int64, device=dev)
+        s, slot, buf = _slab(A)
+        if s.KU < tiles_for(kl + ku, s.band_nb):
+            raise SlateError("gbtrf: storage has no room for the fill-in (construct with the final kl, ku)")
+        comm, Q, me = s.comm, s.Q, s.rank
+        m, n, nb, dt, dev = s.m, s.n, s.band_nb, s.dtype, buf.device
+        mn = min(m, n)
+        kt = -(-mn // nb)
+        ipiv = torch.zeros(max(mn, 1), dtype=torch.int64, device=dev)
         infos = torch.zeros(max(kt, 1), dtype=torch.int64, device=dev)
+        from .lu import _Pack
         for k in range(kt):
             r0 = k * nb
-            kb = min(nb, n - r0, m - r0)
+            kb = min(nb, mn - r0)
             rend = min(m, r0 + kb + kl)
-            cend = min(n, r0 + kb + kl + ku)
-            piv = ipiv[r0:r0 + kb]
-            ops.getrf(buf[r0:rend, r0:r0 + kb], piv, infos[k:k + 1])
-            if r0 > 0:
-                ops.laswp(buf[:m, 0:r0], ipiv, r0, r0 + kb, ioff=-r0)
-            if cend > r0 + kb:
-                C = buf[:m, r0 + kb:cend]
-                ops.laswp(C, ipiv, r0, r0 + kb, ioff=-r0)
-                ops.trsm('L', 'L', 'N', 'U', 1.0, buf[r0:r0 + kb, r0:r0 + kb], buf[r0:r0 + kb, r0 + kb:cend])
-                if rend > r0 + kb:
-                    ops.gemm(-1.0, buf[r0 + kb:rend, r0:r0 + kb], buf[r0:r0 + kb, r0 + kb:cend], 1.0,
-                             buf[r0 + kb:rend, r0 + kb:cend])
+            nr = rend - r0
+            owner = k % Q
+            pk = _Pack([("P", nr, kb, dt), ("piv", kb, 1, torch.int64)], dev)
+            P, pv = pk.get("P"), pk.get("piv")
+            with trace_block("gbtrf::panel"):
+                if me == owner:
+                    Pv = _col_block(s, buf, k, r0, rend)[:, :kb]
+                    ops.getrf(Pv, ipiv[r0:r0 + kb], infos[k:k + 1])
+                    P.copy_(Pv)
+                    pv[:, 0].copy_(ipiv[r0:r0 + kb])
+                if Q > 1:
+                    comm.bcast(pk.raw, owner)
+                    if me != owner:
+                        ipiv[r0:r0 + kb].copy_(pv[:, 0])
+            with trace_block("gbtrf::update"):
+                jhi = (r0 + kb - 1 + ku + kl) // nb
+                for j in s.my_cols(k + 1, jhi):
+                    C = _col_block(s, buf, j, r0, rend)
+                    ops.laswp(C, pv[:, 0], 0, kb)
+                    ops.trsm('L', 'L', 'N', 'U', 1.0, P[:kb], C[:kb])
+                    if nr > kb:
+                        ops.gemm(-1.0, P[kb:], C[:kb], 1.0, C[kb:])
+        # the fill-in tiles now hold U: make them part of the matrix
+        for j in s.my_cols():
+            lo, hi = s.window(j)
+            for i in range(lo, hi + 1):
+                if not s.tileExists(i, j, slot):
+                    s.tileInsert(i, j, slot, data=_col_block(s, buf, j, s.row_offsets[i], s.row_offsets[i + 1])[:, :s.tileNb(j)])
         s.mark_local_modified(slot)
+        A.setUpperBandwidth(kl + ku)
         glob = ipiv.clone()
         for k in range(kt):
             r0 = k * nb
-            kb = min(nb, n - r0, m - r0)
-            glob[r0:r0 + kb] += r0
-        pivots.set(glob[:min(m, n)], nb)
+            glob[r0:r0 + min(nb, mn - r0)] += r0
+        pivots.set(glob[:mn], nb)
         iv = infos[:kt].cpu().tolist()
-        for k, v in enumerate(iv):
-            if v > 0:
-                return k * nb + v
-        return 0
+        info = next((k * nb + v for k, v in enumerate(iv) if v > 0), 0)
+        if comm.size > 1:
+            big = 1 << 62
+            info = int(comm.allreduce_scalar(info if info > 0 else big, "min", torch.int64))
+            info = 0 if info >= big else info
+        return info
+
+
+def _lower_fwd(s, buf, X, kd, unit, gpiv=None):
+    """X := L^{-1} X (L lower band, bandwidth kd, in the slabs; with gbtrf
+    pivots applied step by step when gpiv is given).  Right-looking."""
+    n, nb, Q, me = s.n, s.band_nb, s.Q, s.rank
+    diag = 'U' if unit else 'N'
+    for k in range(-(-min(s.m, n) // nb)):
+        r0 = k * nb
+        kb = min(nb, n - r0)
+        rend = min(n, r0 + kb + kd)
+        owner = k % Q
+        if me == owner:
+            if gpiv is not None:
+                ops.laswp(X, gpiv, r0, r0 + kb)
+            Pk = _col_block(s, buf, k, r0, rend)[:, :kb]
+            ops.trsm('L', 'L', 'N', diag, 1.0, Pk[:kb], X[r0:r0 + kb])
+            if rend > r0 + kb:
+                ops.gemm(-1.0, Pk[kb:], X[r0:r0 + kb], 1.0, X[r0 + kb:rend])
+        _bcast_rows(s.comm, X, r0, rend, owner)
+
+
+def _lower_bwd_op(s, buf, X, kd, unit, opch):
+    """X := op(L)^{-1} X, op = T or C: left-looking, last tile first."""
+    n, nb, Q, me = s.n, s.band_nb, s.Q, s.rank
+    diag = 'U' if unit else 'N'
+    for k in range(-(-n // nb) - 1, -1, -1):
+        r0 = k * nb
+        kb = min(nb, n - r0)
+        rend = min(n, r0 + kb + kd)
+        owner = k % Q
+        if me == owner:
+            Pk = _col_block(s, buf, k, r0, rend)[:, :kb]
+            if rend > r0 + kb:
+                ops.gemm(-1.0, Pk[kb:], X[r0 + kb:rend], 1.0, X[r0:r0 + kb], transA=opch)
+            ops.trsm('L', 'L', opch, diag, 1.0, Pk[:kb], X[r0:r0 + kb])
+        _bcast_rows(s.comm, X, r0, r0 + kb, owner)
+
+
+def _upper_bwd(s, buf, X, ku, unit):
+    """X := U^{-1} X (U upper band, bandwidth ku): right-looking, last tile first."""
+    n, nb, Q, me = s.n, s.band_nb, s.Q, s.rank
+    diag = 'U' if unit else 'N'
+    for k in range(-(-n // nb) - 1, -1, -1):
+        r0 = k * nb
+        kb = min(nb, n - r0)
+        top = max(0, r0 - ku)
+        owner = k % Q
+        if me == owner:
+            Uk = _col_block(s, buf, k, top, r0 + kb)[:, :kb]
+            ops.trsm('L', 'U', 'N', diag, 1.0, Uk[r0 - top:], X[r0:r0 + kb])
+            if r0 > top:
+                ops.gemm(-1.0, Uk[:r0 - top], X[r0:r0 + kb], 1.0, X[top:r0])
+        _bcast_rows(s.comm, X, top, r0 + kb, owner)
+
+
+def _upper_fwd_op(s, buf, X, ku, unit, opch):
+    """X := op(U)^{-1} X, op = T or C: left-looking, first tile first."""
+    n, nb, Q, me = s.n, s.band_nb, s.Q, s.rank
+    diag = 'U' if unit else 'N'
+    for k in range(-(-n // nb)):
+        r0 = k * nb
+        kb = min(nb, n - r0)
+        top = max(0, r0 - ku)
+        owner = k % Q
+        if me == owner:
+            Uk = _col_block(s, buf, k, top, r0 + kb)[:, :kb]
+            if r0 > top:
+                ops.gemm(-1.0, Uk[:r0 - top], X[top:r0], 1.0, X[r0:r0 + kb], transA=opch)
+            ops.trsm('L', 'U', opch, diag, 1.0, Uk[r0 - top:], X[r0:r0 + kb])
+        _bcast_rows(s.comm, X, r0, r0 + kb, owner)
 
 
 def gbtrs(A, pivots, B, opts=None):
-    from .lu import getrs
+    """Solve A X = B with the gbtrf factors (B overwritten)."""
+    _need_band(A, "gbtrs")
     with trace_block("gbtrs"):
-        return getrs(A, pivots, B, opts)
+        s, slot, buf = _slab(A)
+        kl, kuf = _bands(A)                 # after gbtrf: ku = kl + ku (fill)
+        X = _replicated(B, buf.device)
+        _lower_fwd(s, buf, X, kl, True, pivots.device(buf.device))
+        _upper_bwd(s, buf, X, kuf, False)
+        _store(B, X)
+        return 0
 
 
 def gbsv(A, pivots, B, opts=None) -> int:
@@ -120,49 +315,116 @@ def gbsv(A, pivots, B, opts=None) -> int:
 
 
 # ------------------------------------------------------------------ Cholesky
+def _band_conj_transpose(src, dst):
+    """dst := src^H for square band storages with mirrored windows (tile
+    (i, j) of dst = tile (j, i) of src, conjugate-transposed).  The slabs
+    (O(n bandwidth) words) are exchanged by ONE all-gather."""
+    ss, sd = src.storage, dst.storage
+    sslot, buf = ss.band_slot(), None
+    buf = ss.sync_slab(sslot)
+    dslot = sd.band_slot()
+    dbuf = sd.get_slab(dslot)
+    comm = ss.comm
+    rows, ml = buf.shape[0], max(1, max(ss.nloc, 1))
+    from ..core.storage import numroc
+    mx = max(1, max(numroc(ss.n, ss.band_nb, r, ss.Q) for r in range(ss.Q)))
+    pad = torch.zeros((mx, rows), dtype=ss.dtype, device=buf.device)
+    if ss.nloc:
+        pad[:ss.nloc].copy_(buf[:, :ss.nloc].mT)
+    allp = comm.allgather(pad) if comm.size > 1 else pad.unsqueeze(0)
+    for j in sd.my_cols():
+        lo, hi = sd.window(j)
+        for i in range(lo, hi + 1):
+            # source tile (j, i): column i of src, owned by rank i % Q
+            r = ss.slab_row(ss.row_offsets[j], i)
+            c = (i // ss.Q) * ss.band_nb
+            src_t = allp[i % ss.Q][c:c + ss.tileNb(i), r:r + ss.tileMb(j)]      # (tile (j, i))^T
+            dt = _col_block(sd, dbuf, j, sd.row_offsets[i], sd.row_offsets[i + 1])[:, :sd.tileNb(j)]
+            tmp = ops.colmajor_empty(dt.shape[0], dt.shape[1], dt.dtype, dt.device)
+            tmp.copy_(src_t.conj() if dt.dtype.is_complex else src_t)
+            dt.copy_(tmp)
+    sd.mark_local_modified(dslot)
+
+
+def _to_lower_band(A):
+    """Lower-stored copy of an Upper-stored Hermitian band matrix."""
+    from ..core.matrix import HermitianBandMatrix
+    s = A.storage
+    L = HermitianBandMatrix(Uplo.Lower, s.n, A.bandwidth(), nb=s.band_nb, comm=s.comm, dtype=s.dtype,
+                            device=s.device)
+    L.insertLocalTiles(device=s.device.index if s.device.type == "cuda" else -1)
+    _band_conj_transpose(A, L)
+    return L
+
+
 def pbtrf(A, opts=None) -> int:
-    """Band Cholesky of a Hermitian band matrix (kd = bandwidth)."""
-    from .chol import potrf
+    """Band Cholesky A = L L^H of a Hermitian band matrix (kd = bandwidth)."""
+    _need_band(A, "pbtrf")
     with trace_block("pbtrf"):
-        kd = getattr(A, "_kd", max(_bands(A)))
-        if A.uploPhysical() == Uplo.Lower:
-            band_mask(A, kd, 0)
-        else:
-            band_mask(A, 0, kd)
-        if not _single(A) or A.uploPhysical() != Uplo.Lower:
-            return potrf(A, opts)
-        s = A.storage
-        from ._util import target_slot
-        slot = target_slot(A, opts)
-        buf = s.prepare_local(slot)
-        n = s.n
-        nb = s.bc.nb
-        dev = buf.device
-        kt = (n + nb - 1) // nb
+        if A.uploPhysical() == Uplo.Upper:
+            band_mask(A, 0, A.bandwidth())
+            L = _to_lower_band(A)
+            info = pbtrf(L, opts)
+            _band_conj_transpose(L, A)              # A = U = L^H
+            A._chol_lower = L
+            return info
+        kd = A.bandwidth()
+        band_mask(A, kd, 0)
+        s, slot, buf = _slab(A)
+        comm, Q, me = s.comm, s.Q, s.rank
+        n, nb, dt, dev = s.n, s.band_nb, s.dtype, buf.device
+        ct = conj_trans(dt)
+        kt = -(-n // nb)
         infos = torch.zeros(max(kt, 1), dtype=torch.int64, device=dev)
-        ct = 'C' if s.dtype.is_complex else 'T'
         for k in range(kt):
             r0 = k * nb
             kb = min(nb, n - r0)
             rend = min(n, r0 + kb + kd)
-            ops.potrf('L', buf[r0:r0 + kb, r0:r0 + kb], infos[k:k + 1])
-            if rend > r0 + kb:
-                P = buf[r0 + kb:rend, r0:r0 + kb]
-                ops.trsm('R', 'L', ct, 'N', 1.0, buf[r0:r0 + kb, r0:r0 + kb], P)
-                ops.gemm(-1.0, P, P, 1.0, buf[r0 + kb:rend, r0 + kb:rend], 'N', ct,
-                         mask=(1, 1 << 40, 1, 0, 1, 0, 0, 0, 0))
+            nr = rend - r0
+            owner = k % Q
+            P = ops.colmajor_empty(nr, kb, dt, dev)
+            with trace_block("pbtrf::panel"):
+                if me == owner:
+                    Pv = _col_block(s, buf, k, r0, rend)[:, :kb]
+                    ops.potrf('L', Pv[:kb], infos[k:k + 1])
+                    if nr > kb:
+                        ops.trsm('R', 'L', ct, 'N', 1.0, Pv[:kb], Pv[kb:])
+                    P.copy_(Pv)
+                if Q > 1:
+                    comm.bcast(P, owner)
+            with trace_block("pbtrf::update"):
+                for j in s.my_cols(k + 1, (rend - 1) // nb):
+                    off = s.col_offsets[j] - r0
+                    w = min(s.tileNb(j), nr - off)
+                    if w <= 0:
+                        continue
+                    Pj = P[off:nr]
+                    C = _col_block(s, buf, j, s.col_offsets[j], rend)[:, :w]
+                    ops.gemm(-1.0, Pj, Pj[:w], 1.0, C, 'N', ct, _LOWER_MASK)
         s.mark_local_modified(slot)
         iv = infos[:kt].cpu().tolist()
-        for k, v in enumerate(iv):
-            if v > 0:
-                return k * nb + v
-        return 0
+        info = next((k * nb + v for k, v in enumerate(iv) if v > 0), 0)
+        if comm.size > 1:
+            big = 1 << 62
+            info = int(comm.allreduce_scalar(info if info > 0 else big, "min", torch.int64))
+            info = 0 if info >= big else info
+        return info
 
 
 def pbtrs(A, B, opts=None):
-    from .chol import potrs
+    """Solve A X = B with the pbtrf factor (B overwritten)."""
+    _need_band(A, "pbtrs")
     with trace_block("pbtrs"):
-        return potrs(A, B, opts)
+        L = getattr(A, "_chol_lower", None) if A.uploPhysical() == Uplo.Upper else A
+        if L is None:
+            raise SlateError("pbtrs: factor with pbtrf first")
+        s, slot, buf = _slab(L)
+        kd = L.bandwidth()
+        X = _replicated(B, buf.device)
+        _lower_fwd(s, buf, X, kd, False)
+        _lower_bwd_op(s, buf, X, kd, False, conj_trans(s.dtype))
+        _store(B, X)
+        return 0
 
 
 def pbsv(A, B, opts=None) -> int:
@@ -172,32 +434,165 @@ def pbsv(A, B, opts=None) -> int:
     return info
 
 
+# ------------------------------------------------------------------ tbsm
+def tbsm(side, alpha, A, B, pivots=None, opts=None):
+    """op(A) X = alpha B (Left) or X op(A) = alpha B (Right) with A a
+    triangular band matrix; with ``pivots`` (gbtrf's, A its unit lower
+    factor) the row interchanges are applied step by step (tbsmPivots)."""
+    _need_band(A, "tbsm")
+    with trace_block("tbsm"):
+        side = Side(side) if not isinstance(side, Side) else side
+        s, slot, buf = _slab(A)
+        up = A.uploPhysical()
+        opA = A.op()
+        unit = getattr(A, "_diag", Diag.NonUnit) == Diag.Unit
+        kd = A._kl if up == Uplo.Lower else A._ku
+        if side == Side.Right:
+            # X op(A) = alpha B  <=>  op(A)^T X^T = alpha B^T
+            from .aux import allgather_dense, from_dense
+            Bt = allgather_dense(B).mT.to(buf.device)
+            X = ops.colmajor_empty(Bt.shape[0], Bt.shape[1], Bt.dtype, buf.device)
+            X.copy_(Bt)
+            opT = {Op.NoTrans: 'T', Op.Trans: 'N', Op.ConjTrans: 'N'}[opA]
+            conj = opA == Op.ConjTrans
+            if conj:
+                X.copy_(X.conj())
+            _tri_dispatch(s, buf, X, up, opT, kd, unit, None)
+            if conj:
+                X.copy_(X.conj())
+            if alpha != 1.0:
+                ops.gescale(alpha, X)
+            from_dense(B, X.mT)
+            return 0
+        X = _replicated(B, buf.device)
+        if alpha != 1.0:
+            ops.gescale(alpha, X)
+        opch = {Op.NoTrans: 'N', Op.Trans: 'T', Op.ConjTrans: 'C'}[opA]
+        _tri_dispatch(s, buf, X, up, opch, kd, unit, pivots.device(buf.device) if pivots is not None else None)
+        _store(B, X)
+        return 0
+
+
+def _tri_dispatch(s, buf, X, up, opch, kd, unit, gpiv):
+    if up == Uplo.Lower and opch == 'N':
+        _lower_fwd(s, buf, X, kd, unit, gpiv)
+    elif up == Uplo.Lower:
+        _lower_bwd_op(s, buf, X, kd, unit, opch)
+    elif opch == 'N':
+        _upper_bwd(s, buf, X, kd, unit)
+    else:
+        _upper_fwd_op(s, buf, X, kd, unit, opch)
+
+
 # ------------------------------------------------------------------ BLAS-3
+_CHUNK = 512
+
+
+def _write_cols(C, c0, c1, Cp, alpha, beta):
+    """C[:, c0:c1] = alpha Cp + beta C[:, c0:c1] on this rank's part (Cp
+    replicated, m x (c1 - c0))."""
+    from .aux import allgather_dense, from_dense
+    s = C.storage
+    Cs = C.slice(0, C.m() - 1, c0, c1 - 1)
+    if s.bc is None or C.op() != Op.NoTrans:
+        D = Cp * alpha + (allgather_dense(Cs).to(Cp.device) * beta if beta != 0 else 0)
+        from_dense(Cs, D)
+        return
+    lb = Cs.local_block()
+    if lb.mloc == 0 or lb.nloc == 0:
+        return
+    dev = lb.data.device
+    rows = torch.as_tensor([lb.global_row(i) for i in range(lb.mloc)], device=Cp.device)
+    cols = torch.as_tensor([lb.global_col(j) for j in range(lb.nloc)], device=Cp.device)
+    D = ops.colmajor_empty(lb.mloc, lb.nloc, Cp.dtype, dev)
+    D.copy_(Cp[rows][:, cols])
+    ops.geadd(alpha, D, beta, lb.data[:lb.mloc, :lb.nloc])
+    s.mark_local_modified(s.origin_slot)
+
+
+def _stored_rows(s, j):
+    lo, hi = s.window(j)
+    return s.row_offsets[lo], s.row_offsets[hi + 1]
+
+
 def gbmm(alpha, A, B, beta, C, opts=None):
-    """C = alpha A B + beta C with A a band matrix."""
-    from .blas3 import gemm
+    """C = alpha op(A) B + beta C with A a band matrix (op from A's view)."""
+    _need_band(A, "gbmm")
+    from .aux import allgather_dense
     with trace_block("gbmm"):
-        band_mask(A)
-        return gemm(alpha, A, B, beta, C, opts)
+        band_mask(A, A._kl, A._ku)
+        s, slot, buf = _slab(A)
+        dev, dt = buf.device, s.dtype
+        opA = A.op()
+        tr = {Op.Trans: 'T', Op.ConjTrans: 'C'}.get(opA)
+        mC = C.m()
+        for c0 in range(0, B.n(), _CHUNK):
+            c1 = min(B.n(), c0 + _CHUNK)
+            Bw = _cm_copy(allgather_dense(B.slice(0, B.m() - 1, c0, c1 - 1)), dev)
+            Cp = ops.colmajor_zeros(mC, c1 - c0, dt, dev)
+            for j in s.my_cols():
+                g0, g1 = _stored_rows(s, j)
+                S = _col_block(s, buf, j, g0, g1)
+                cj0, cj1 = s.col_offsets[j], s.col_offsets[j + 1]
+                if tr is None:
+                    ops.gemm(1.0, S, Bw[cj0:cj1], 1.0, Cp[g0:g1])
+                else:
+                    ops.gemm(1.0, S, Bw[g0:g1], 1.0, Cp[cj0:cj1], transA=tr)
+            if s.comm.size > 1:
+                s.comm.allreduce(Cp)
+            _write_cols(C, c0, c1, Cp, alpha, beta)
+        return C
+
+
+def _herm_band_apply(s, buf, Bw, Cp, up):
+    """Cp += A Bw for the Hermitian band A stored (triangle ``up``) in the
+    slabs of this rank: stored part of each column, then its conjugate
+    transpose with the diagonal counted once."""
+    ct = conj_trans(s.dtype)
+    for j in s.my_cols():
+        g0, g1 = _stored_rows(s, j)
+        S = _col_block(s, buf, j, g0, g1)
+        cj0, cj1 = s.col_offsets[j], s.col_offsets[j + 1]
+        ops.gemm(1.0, S, Bw[cj0:cj1], 1.0, Cp[g0:g1])
+        T = ops.colmajor_empty(S.shape[0], S.shape[1], S.dtype, S.device)
+        T.copy_(S)
+        d0 = cj0 - g0
+        ops.geset(0.0, 0.0, T[d0:d0 + (cj1 - cj0)], uplo='U' if up == Uplo.Lower else 'L')
+        ops.gemm(1.0, T, Bw[g0:g1], 1.0, Cp[cj0:cj1], transA=ct)
 
 
 def hbmm(side, alpha, A, B, beta, C, opts=None):
-    """C = alpha A B + beta C (Left) or alpha B A + beta C with A Hermitian band."""
-    from .blas3 import hemm
+    """C = alpha A B + beta C (Left) or alpha B A + beta C (Right), A a
+    Hermitian band matrix."""
+    _need_band(A, "hbmm")
+    from .aux import allgather_dense, from_dense
     with trace_block("hbmm"):
-        kd = getattr(A, "_kd", max(_bands(A)))
-        band_mask(A, kd, 0) if A.uploPhysical() == Uplo.Lower else band_mask(A, 0, kd)
-        return hemm(side, alpha, A, B, beta, C, opts)
-
-
-def tbsm(side, alpha, A, B, pivots=None, opts=None):
-    """Triangular band solve op(A) X = alpha B (optionally with the gbtrf
-    row pivots applied to B first, tbsmPivots)."""
-    from .blas3 import trsm
-    from .lu import permute_rows
-    with trace_block("tbsm"):
-        kd = getattr(A, "_kd", max(_bands(A)))
-        if pivots is not None:
-            permute_rows(B, pivots, forward=True)
-        band_mask(A, kd, 0) if A.uploPhysical() == Uplo.Lower else band_mask(A, 0, kd)
-        return trsm(side, alpha, A, B, opts)
+        side = Side(side) if not isinstance(side, Side) else side
+        kd = A.bandwidth()
+        up = A.uploPhysical()
+        band_mask(A, kd, 0) if up == Uplo.Lower else band_mask(A, 0, kd)
+        s, slot, buf = _slab(A)
+        dev, dt = buf.device, s.dtype
+        n = A.n()
+        if side == Side.Left:
+            for c0 in range(0, B.n(), _CHUNK):
+                c1 = min(B.n(), c0 + _CHUNK)
+                Bw = _cm_copy(allgather_dense(B.slice(0, B.m() - 1, c0, c1 - 1)), dev)
+                Cp = ops.colmajor_zeros(n, c1 - c0, dt, dev)
+                _herm_band_apply(s, buf, Bw, Cp, up)
+                if s.comm.size > 1:
+                    s.comm.allreduce(Cp)
+                _write_cols(C, c0, c1, Cp, alpha, beta)
+            return C
+        # Right: C^H = A B^H (A Hermitian), row chunks of B
+        for r0 in range(0, B.m(), _CHUNK):
+            r1 = min(B.m(), r0 + _CHUNK)
+            X = _cm_copy(allgather_dense(B.slice(r0, r1 - 1, 0, B.n() - 1)).mH, dev)
+            Cp = ops.colmajor_zeros(n, r1 - r0, dt, dev)
+            _herm_band_apply(s, buf, X, Cp, up)
+            if s.comm.size > 1:
+                s.comm.allreduce(Cp)
+            Cs = C.slice(r0, r1 - 1, 0, C.n() - 1)
+            D = Cp.mH * alpha + (allgather_dense(Cs).to(dev) * beta if beta != 0 else 0)
+            from_dense(Cs, D)
+        return C

@@ -124,3 +124,168 @@ def test_band_gpu():
     B0 = D(B).clone()
     assert sl.gbsv(A, sl.Pivots(), B) == 0
     assert (A0 @ D(B) - B0).abs().max().item() < 1e-10
+
+
+def _tri_band(uplo, diag, n, kd, nb, dt, seed, p=1, q=1):
+    T = sl.TriangularBandMatrix(uplo, diag, n, kd, nb=nb, p=p, q=q, dtype=dt)
+    T.insertLocalTiles()
+    sl.generate_matrix(T, "rands", seed)
+    lo = uplo == sl.Uplo.Lower
+    sl.band_mask(T, kd if lo else 0, 0 if lo else kd)
+    Td = D(T)
+    Td = Td + 4 * torch.eye(n, dtype=dt)
+    sl.from_dense(T, Td)
+    Td = torch.tril(Td) if lo else torch.triu(Td)
+    if diag == sl.Diag.Unit:
+        Td = Td - torch.diag(torch.diagonal(Td)) + torch.eye(n, dtype=dt)
+    return T, Td
+
+
+def check_band_full(p=1, q=1, dt=torch.float64):
+    """Compact storage + every band driver variant on a grid."""
+    n, nb = 133, 16
+    kl, ku = 21, 9
+    A = sl.BandMatrix(n, n, kl, ku, nb=nb, p=p, q=q, dtype=dt)
+    A.insertLocalTiles()
+    sl.generate_matrix(A, "rands", 11)
+    sl.band_mask(A)
+    # storage is O(n (kl + ku)): slab rows = (ceil(kl/nb) + ceil((kl+ku)/nb) + 1) nb
+    s = A.storage
+    assert s.get_slab(s.band_slot()).shape[0] == (2 + 2 + 1) * nb
+    A0 = D(A).clone()
+    # gbmm with op(A) = A^T and A^H
+    B = sl.Matrix(n, 5, nb=nb, p=p, q=q, dtype=dt)
+    B.insertLocalTiles()
+    sl.generate_matrix(B, "rands", 12)
+    B0 = D(B).clone()
+    for view, ref in ((A.transpose(), A0.mT), (A.conj_transpose(), A0.mH)):
+        C = sl.Matrix(n, 5, nb=nb, p=p, q=q, dtype=dt)
+        C.insertLocalTiles()
+        sl.generate_matrix(C, "rands", 13)
+        C0 = D(C).clone()
+        sl.gbmm(1.5, view, B, -1.0, C)
+        assert (D(C) - (1.5 * ref @ B0 - C0)).abs().max() < 1e-11
+    # gbtrf / gbtrs, then tbsm with the pivots on the unit-lower factor
+    piv = sl.Pivots()
+    assert sl.gbtrf(A, piv) == 0
+    X = sl.Matrix(n, 5, nb=nb, p=p, q=q, dtype=dt)
+    X.insertLocalTiles()
+    sl.copy(B, X)
+    sl.gbtrs(A, piv, X)
+    assert (A0 @ D(X) - B0).abs().max() < 1e-10
+    Lf = sl.TriangularBandMatrix(sl.Uplo.Lower, sl.Diag.Unit, matrix=A, kd=kl)
+    Uf = sl.TriangularBandMatrix(sl.Uplo.Upper, sl.Diag.NonUnit, matrix=A, kd=kl + ku)
+    Y = sl.Matrix(n, 5, nb=nb, p=p, q=q, dtype=dt)
+    Y.insertLocalTiles()
+    sl.copy(B, Y)
+    sl.tbsm(sl.Side.Left, 1.0, Lf, Y, piv)
+    sl.tbsm(sl.Side.Left, 1.0, Uf, Y)
+    assert (D(Y) - D(X)).abs().max() < 1e-10
+    # tbsm: all uplo x op x diag, left and right
+    for uplo in (sl.Uplo.Lower, sl.Uplo.Upper):
+        for diag in (sl.Diag.NonUnit, sl.Diag.Unit):
+            T, Td = _tri_band(uplo, diag, n, 13, nb, dt, 14, p, q)
+            for view, ref in ((T, Td), (T.transpose(), Td.mT), (T.conj_transpose(), Td.mH)):
+                Z = sl.Matrix(n, 3, nb=nb, p=p, q=q, dtype=dt)
+                Z.insertLocalTiles()
+                sl.generate_matrix(Z, "rands", 15)
+                Z0 = D(Z).clone()
+                sl.tbsm(sl.Side.Left, 2.0, view, Z)
+                Zd = D(Z)
+                assert (ref @ Zd - 2.0 * Z0).abs().max() / (ref.abs().max() * Zd.abs().max() * n) < 1e-15, \
+                    (uplo, diag)
+                W = sl.Matrix(4, n, nb=nb, p=p, q=q, dtype=dt)
+                W.insertLocalTiles()
+                sl.generate_matrix(W, "rands", 16)
+                W0 = D(W).clone()
+                sl.tbsm(sl.Side.Right, 1.0, view, W)
+                Wd = D(W)
+                assert (Wd @ ref - W0).abs().max() / (ref.abs().max() * Wd.abs().max() * n) < 1e-15, \
+                    (uplo, diag, "R")
+    # pbsv Upper, hbmm Right
+    kd = 11
+    H = sl.HermitianBandMatrix(sl.Uplo.Upper, n, kd, nb=nb, p=p, q=q, dtype=dt)
+    H.insertLocalTiles()
+    sl.generate_matrix(H, "poev", 17)
+    sl.band_mask(H, 0, kd)
+    Hf = _dense_hermitian(H)
+    Wr = sl.Matrix(6, n, nb=nb, p=p, q=q, dtype=dt)
+    Wr.insertLocalTiles()
+    sl.generate_matrix(Wr, "rands", 18)
+    Cr = sl.Matrix(6, n, nb=nb, p=p, q=q, dtype=dt)
+    Cr.insertLocalTiles()
+    sl.hbmm(sl.Side.Right, 1.0, H, Wr, 0.0, Cr)
+    assert (D(Cr) - D(Wr) @ Hf).abs().max() < 1e-11
+    Bh = sl.Matrix(n, 2, nb=nb, p=p, q=q, dtype=dt)
+    Bh.insertLocalTiles()
+    sl.generate_matrix(Bh, "rands", 19)
+    Bh0 = D(Bh).clone()
+    assert sl.pbsv(H, Bh) == 0
+    assert (Hf @ D(Bh) - Bh0).abs().max() < 1e-11
+    U = torch.triu(D(H))
+    assert (U.mH @ U - Hf).abs().max() < 1e-10 * Hf.abs().max()
+
+
+@pytest.mark.parametrize("dt", [torch.float64, torch.complex128])
+def test_band_full(dt):
+    check_band_full(dt=dt)
+
+
+def _band_full_dist(rank, size, p, q):
+    check_band_full(p, q)
+    check_band_full(p, q, torch.complex128)
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 4])
+def test_band_full_distributed(nranks):
+    """Band storage is 1-D column-cyclic over all ranks whatever p x q."""
+    run_dist(_band_full_dist, nranks, 1, nranks)
+
+
+def _band_norms(rank, size, p, q):
+    n, nb = 90, 16
+    A = sl.BandMatrix(n, n, 13, 7, nb=nb, p=p, q=q)
+    A.insertLocalTiles()
+    sl.generate_matrix(A, "rands", 3)
+    sl.band_mask(A)
+    Ad = D(A)
+    H = sl.HermitianBandMatrix(sl.Uplo.Lower, n, 10, nb=nb, p=p, q=q)
+    H.insertLocalTiles()
+    sl.generate_matrix(H, "rands", 4)
+    sl.band_mask(H, 10, 0)
+    Hd = _dense_hermitian(H)
+    for nt, f in ((sl.Norm.Max, lambda X: X.abs().max()), (sl.Norm.One, lambda X: X.abs().sum(0).max()),
+                  (sl.Norm.Inf, lambda X: X.abs().sum(1).max()), (sl.Norm.Fro, lambda X: X.norm())):
+        assert abs(sl.norm(nt, A) - float(f(Ad))) < 1e-12 * float(f(Ad))
+        assert abs(sl.norm(nt, H) - float(f(Hd))) < 1e-12 * float(f(Hd)), nt
+
+
+@pytest.mark.parametrize("nranks", [1, 3])
+def test_band_norms(nranks):
+    """Norms straight from the compact band tiles (no dense gather)."""
+    if nranks == 1:
+        _band_norms(0, 1, 1, 1)
+    else:
+        run_dist(_band_norms, nranks, 1, nranks)
+
+
+@pytest.mark.gpu
+def test_band_full_gpu():
+    """Compact band storage on the GPU: pbsv, tbsm, gbmm, hbmm (slab GEMMs)."""
+    dev = torch.device("cuda")
+    n, nb, kd = 1500, 128, 100
+    H = sl.HermitianBandMatrix(sl.Uplo.Lower, n, kd, nb=nb, device=dev)
+    H.insertLocalTiles(device=0)
+    sl.generate_matrix(H, "poev", 4)
+    sl.band_mask(H, kd, 0)
+    Hf = _dense_hermitian(H)
+    B = sl.Matrix(n, 4, nb=nb, device=dev)
+    B.insertLocalTiles(device=0)
+    sl.generate_matrix(B, "rands", 5)
+    B0 = D(B).clone()
+    C = sl.Matrix(n, 4, nb=nb, device=dev)
+    C.insertLocalTiles(device=0)
+    sl.hbmm(sl.Side.Left, 1.0, H, B, 0.0, C)
+    assert ((D(C) - Hf @ B0).abs().max() / (Hf.abs().max() * n)).item() < 1e-14
+    assert sl.pbsv(H, B) == 0
+    assert ((Hf @ D(B) - B0).abs().max() / (Hf.abs().max() * n)).item() < 1e-14
