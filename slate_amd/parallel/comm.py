@@ -306,6 +306,12 @@ class _SelfComm(Comm):
 _WORLD = None
 
 
+def self_comm() -> Comm:
+    """This rank alone (rank-local matrices inside multi-rank drivers)."""
+    me = dist.get_rank() if _dist_ready() else 0
+    return _SelfComm(me)
+
+
 def world() -> Comm:
     """The global communicator (all ranks; a size-1 comm without torch.distributed)."""
     global _WORLD

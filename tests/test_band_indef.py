@@ -289,3 +289,59 @@ def test_band_full_gpu():
     assert ((D(C) - Hf @ B0).abs().max() / (Hf.abs().max() * n)).item() < 1e-14
     assert sl.pbsv(H, B) == 0
     assert ((Hf @ D(B) - B0).abs().max() / (Hf.abs().max() * n)).item() < 1e-14
+
+
+@pytest.mark.parametrize("dt,uplo,n,nb", [(torch.float64, sl.Uplo.Lower, 200, 16),
+                                           (torch.complex128, sl.Uplo.Upper, 77, 8),
+                                           (torch.float64, sl.Uplo.Upper, 64, 16)])
+def test_hetrf_blocked_aasen(dt, uplo, n, nb):
+    """Blocked Aasen: P A P^H = L T L^H with T block tridiagonal, on a
+    matrix with a zero diagonal (pivoting required), padded orders."""
+    from slate_amd.models.hetrf import _blk
+    S = sl.HermitianMatrix(uplo, n, nb=nb, dtype=dt)
+    S.insertLocalTiles()
+    sl.generate_matrix(S, "rands", 21)
+    Sf = _dense_hermitian(S)
+    Sf = Sf - torch.diag(torch.diagonal(Sf))          # zero diagonal: indefinite, needs pivots
+    sl.from_dense(S, torch.tril(Sf) if uplo == sl.Uplo.Lower else torch.triu(Sf))
+    B = sl.Matrix(n, 4, nb=nb, dtype=dt)
+    B.insertLocalTiles()
+    sl.generate_matrix(B, "rands", 22)
+    Bd = D(B).clone()
+    piv = sl.Pivots()
+    assert sl.hetrf(S, piv) == 0
+    F = S._hetrf
+    N, k = F.N, F.N // F.nb
+    T = torch.zeros(N, N, dtype=dt)
+    for J in range(k):
+        T[J * F.nb:(J + 1) * F.nb, J * F.nb:(J + 1) * F.nb] = _blk(F.Td, J, F.nb).cpu()
+        if J + 1 < k:
+            T[(J + 1) * F.nb:(J + 2) * F.nb, J * F.nb:(J + 1) * F.nb] = _blk(F.Tl, J + 1, F.nb).cpu()
+            T[J * F.nb:(J + 1) * F.nb, (J + 1) * F.nb:(J + 2) * F.nb] = _blk(F.Tl, J + 1, F.nb).cpu().mH
+    Ap = torch.eye(N, dtype=dt)
+    Ap[:n, :n] = Sf
+    p = F.perm.cpu()
+    L = F.L.cpu()
+    assert ((L @ T @ L.mH - Ap[p][:, p]).abs().max() / Sf.abs().max()).item() < 1e-12
+    # partial pivoting: |l| <= 1 (real); cabs1 pivot choice bounds |l| by sqrt(2) (complex)
+    assert L.abs().max().item() <= (2 ** 0.5 if L.is_complex() else 1.0) + 1e-12
+    sl.hetrs(S, piv, None, None, B)
+    assert (Sf @ D(B) - Bd).abs().max() / (Sf.abs().max() * D(B).abs().max() * n) < 1e-13
+
+
+@pytest.mark.gpu
+def test_hesv_gpu():
+    """Blocked Aasen on the GPU (batched MFMA GEMMs, GPU LU panel, band T)."""
+    dev = torch.device("cuda")
+    n, nb = 1000, 64
+    S = sl.HermitianMatrix(sl.Uplo.Lower, n, nb=nb, device=dev)
+    S.insertLocalTiles(device=0)
+    sl.generate_matrix(S, "rands", 5)
+    Sf = _dense_hermitian(S)
+    B = sl.Matrix(n, 3, nb=nb, device=dev)
+    B.insertLocalTiles(device=0)
+    sl.generate_matrix(B, "rands", 6)
+    Bd = D(B).clone()
+    assert sl.hesv(S, sl.Pivots(), None, None, None, B) == 0
+    X = D(B)
+    assert ((Sf @ X - Bd).abs().max() / (Sf.abs().max() * X.abs().max() * n)).item() < 1e-13
