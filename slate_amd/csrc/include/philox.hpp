@@ -64,7 +64,61 @@ enum Kind : int {
     kPoev = 21,            // Hermitian rands + n*I (HPD)
     kHeRands = 22,         // Hermitian rands (indefinite)
     kMinij = 30, kHilb = 31, kLehmer = 32, kFrank = 33, kMoler = 34,
+    // Matlab-gallery test matrices (SLATE matgen/generate_matrix_ge.cc kinds)
+    kJordanT = 40, kChebspec = 41, kCircul = 42, kFiedler = 43, kGfpp = 44, kKms = 45, kOrthog = 46,
+    kRiemann = 47, kRis = 48, kZielkeNS = 49, kLotkin = 50, kRedheff = 51, kTriw = 52, kPei = 53,
+    kTridiag = 54, kToeppen = 55, kParter = 56, kCauchy = 57, kChow = 58, kClement = 59, kGcdmat = 60,
 };
+
+SLATE_HD int64_t gcd64(int64_t a, int64_t b) {
+    while (b) { const int64_t t = a % b; a = b; b = t; }
+    return a;
+}
+
+// Closed-form gallery entries (0-based i, j; N = max(m, n)); false if kind
+// is not a gallery kind.
+SLATE_HD bool gallery(int kind, int64_t i, int64_t j, int64_t m, int64_t n, double& re) {
+    const int64_t N = m > n ? m : n;
+    const int64_t d = i - j;
+    const double pi = 3.141592653589793;
+    switch (kind) {
+        case kJordanT: re = (d == 0 || d == 1) ? 1.0 : 0.0; return true;
+        case kChebspec: {
+            // Chebyshev spectral differentiation on the points cos(pi (k+1) / N)
+            const double xi = cos(pi * (double)(i + 1) / (double)N), xj = cos(pi * (double)(j + 1) / (double)N);
+            if (i != j) {
+                const double ci = (i == N - 1) ? 2.0 : 1.0, cj = (j == N - 1) ? 2.0 : 1.0;
+                re = (((i + j) & 1) ? -1.0 : 1.0) * ci / (cj * (xj - xi));
+            } else if (j == N - 1) {
+                re = -(double)(2 * N * N + 1) / 6.0;
+            } else {
+                re = -0.5 * xi / (1.0 - xi * xi);
+            }
+            return true;
+        }
+        case kCircul: re = (double)(((j - i) % N + N) % N + 1); return true;
+        case kFiedler: re = (double)(d < 0 ? -d : d); return true;
+        case kGfpp: re = (j == n - 1) ? 1.0 : (d > 0 ? -1.0 : (d == 0 ? 0.5 : 0.0)); return true;
+        case kKms: re = pow(0.5, (double)(d < 0 ? -d : d)); return true;
+        case kOrthog: re = sqrt(2.0 / (double)(N + 1)) * sin((double)(i + 1) * (double)(j + 1) * pi / (double)(N + 1));
+            return true;
+        case kRiemann: re = ((j + 2) % (i + 2) == 0) ? (double)(j + 1) : -1.0; return true;
+        case kRis: re = 0.5 / ((double)N - (double)i - (double)j - 0.5); return true;
+        case kZielkeNS: re = (j < i) ? 1.0 : ((i == 0 && j == N - 1) ? -1.0 : 0.0); return true;
+        case kLotkin: re = (i == 0) ? 1.0 : 1.0 / (double)(i + j + 1); return true;
+        case kRedheff: re = (j == 0 || (j + 1) % (i + 1) == 0) ? 1.0 : 0.0; return true;
+        case kTriw: re = (d == 0) ? 1.0 : (d > 0 ? 0.0 : -1.0); return true;
+        case kPei: re = (d == 0) ? 2.0 : 1.0; return true;
+        case kTridiag: re = (d == 0) ? 2.0 : ((d == 1 || d == -1) ? -1.0 : 0.0); return true;
+        case kToeppen: re = (d == -1) ? 10.0 : (d == 1 ? -10.0 : ((d == 2 || d == -2) ? 1.0 : 0.0)); return true;
+        case kParter: re = 1.0 / ((double)d + 0.5); return true;
+        case kCauchy: re = 1.0 / (double)(i + j + 2); return true;
+        case kChow: re = (d < -1) ? 0.0 : 1.0; return true;
+        case kClement: re = (d == 1) ? (double)(N - j - 1) : (d == -1 ? (double)j : 0.0); return true;
+        case kGcdmat: re = (double)gcd64(i + 1, j + 1); return true;
+        default: return false;
+    }
+}
 
 // Real and imaginary parts of entry (gi, gj) of an n x n (or m x n) matrix.
 SLATE_HD void entry(int kind, uint64_t seed, int64_t gi, int64_t gj, int64_t m, int64_t n,
@@ -74,7 +128,12 @@ SLATE_HD void entry(int kind, uint64_t seed, int64_t gi, int64_t gj, int64_t m, 
         case kZeros: return;
         case kOnes: re = 1; return;
         case kIdentity: re = (gi == gj) ? 1.0 : 0.0; return;
-        case kIJ: re = (double)gi + (double)gj / 1000.0; return;
+        case kIJ: {
+            // i + j s with s = 10^-ceil(log10 n): the column index in the fraction
+            double sc = 1.0;
+            for (int64_t t = 1; t < n; t *= 10) sc *= 0.1;
+            re = (double)gi + (double)gj * sc; return;
+        }
         case kJordan: re = (gi == gj) ? 1.0 : (gi + 1 == gj ? 1.0 : 0.0); return;
         case kMinij: re = (double)((gi < gj ? gi : gj) + 1); return;
         case kHilb: re = 1.0 / (double)(gi + gj + 1); return;
@@ -83,7 +142,9 @@ SLATE_HD void entry(int kind, uint64_t seed, int64_t gi, int64_t gj, int64_t m, 
             re = (jj >= ii - 1) ? (double)(nn + 1 - (ii > jj ? ii : jj)) : 0.0; return; }
         case kMoler: { double mn = (double)((gi < gj ? gi : gj) + 1);
             re = (gi == gj) ? mn : mn - 2.0; return; }
-        default: break;
+        default:
+            if (gallery(kind, gi, gj, m, n, re)) return;
+            break;
     }
     bool herm = (kind == kPoev || kind == kHeRands);
     int64_t ci = gi, cj = gj;

@@ -386,8 +386,13 @@ def copy(A, B, opts=None):
             if B.uploPhysical() == Uplo.General:
                 ops.gecopy(la.data, lb.data)
             else:
-                for (xa, u), (xb, _) in zip(_local_uplo_blocks(A, la), _local_uplo_blocks(B, lb)):
-                    ops.gecopy(xa, xb, uplo=u)
+                # B's stored-triangle pieces; A's data at the same local offsets
+                # (identical layouts), whatever A's own structure
+                ldb = max(1, lb.data.stride(1))
+                for xb, u in _local_uplo_blocks(B, lb):
+                    off = xb.storage_offset() - lb.data.storage_offset()
+                    r, c = off % ldb, off // ldb
+                    ops.gecopy(la.data[r:r + xb.shape[0], c:c + xb.shape[1]], xb, uplo=u)
         B.storage.mark_local_modified(B.storage.origin_slot)
         return B
     return redistribute(A, B)
