@@ -139,10 +139,17 @@ class MatrixStorage:
     def _detect_block_cyclic(self) -> Optional[BlockCyclic]:
         if getattr(self.tileMb, "kind", None) != "uniform" or getattr(self.tileNb, "kind", None) != "uniform":
             return None
-        ok, order, p, q = func.is_2d_cyclic_grid(self.mt, self.nt, self.tileRank)
+        tr = self.tileRank
+        if getattr(tr, "kind", None) == "2d" and getattr(tr, "mb", 0) == 1 and getattr(tr, "nb", 0) == 1 and \
+                tr.p * tr.q <= self.comm.size:
+            # the grid the constructor asked for (also for matrices with a
+            # single tile, whose ownership alone cannot reveal p x q)
+            ok, order, p, q = True, tr.order, tr.p, tr.q
+        else:
+            ok, order, p, q = func.is_2d_cyclic_grid(self.mt, self.nt, self.tileRank)
         if not ok:
             return None
-        if self.mt <= 1 and self.nt <= 1 and self.comm.size > 1:
+        if self.mt <= 1 and self.nt <= 1 and self.comm.size > 1 and getattr(tr, "kind", None) != "2d":
             # a single tile: rank from the function
             r = self.tileRank((0, 0)) if self.mt and self.nt else 0
             p = q = 1

@@ -58,6 +58,15 @@ def _converged(R, X, anorm, n):
     return bool((rn <= xn * cte).all())
 
 
+def _mul(alpha, A, X, beta, C, opts):
+    """C = alpha A X + beta C with A's structure honoured (hemm for a
+    Hermitian A: only its stored triangle is read)."""
+    from .blas3 import gemm, hemm
+    if isinstance(A, HermitianMatrix):
+        return hemm(Side.Left, alpha, A, X, beta, C, opts)
+    return gemm(alpha, A, X, beta, C, opts)
+
+
 def _fallback(solver, args, B, X, opts, info_lo):
     """Low-precision factorization failed (info_lo > 0): with
     Option.UseFallbackSolver (default) solve in full precision into X and
@@ -78,14 +87,14 @@ def _refine(A, B, X, solve_lo, opts, anorm):
     R = _like(B)
     for it in range(1, itermax + 1):
         copy(B, R)
-        gemm(-1.0, A, X, 1.0, R, opts)
+        _mul(-1.0, A, X, 1.0, R, opts)
         if _converged(R, X, anorm, n):
             return it - 1
         D = solve_lo(R)
         from .aux import add
         add(1.0, D, 1.0, X)
     copy(B, R)
-    gemm(-1.0, A, X, 1.0, R, opts)
+    _mul(-1.0, A, X, 1.0, R, opts)
     return itermax if _converged(R, X, anorm, n) else -itermax
 
 
@@ -149,76 +158,120 @@ def posv_mixed(A, B, X, opts=None):
 
 
 # ------------------------------------------------------------------ GMRES-IR
+def _col(M, j, j2=None):
+    return M.slice(0, M.m() - 1, j, j if j2 is None else j2)
+
+
+def _small(A, rows, dtype=None):
+    """rows x 1 matrix on A's grid (the Hessenberg column / GMRES weights)."""
+    s, bc = A.storage, A.storage.bc
+    M = Matrix(rows, 1, nb=bc.nb, p=bc.p, q=bc.q, comm=s.comm, dtype=dtype or s.dtype, device=s.device,
+               order=bc.order)
+    M.insertLocalTiles(device=s.device.index if s.device.type == "cuda" else -1)
+    return M
+
+
+def _givens(f, g):
+    """c, s, r with [c s; -conj(s) c] [f; g] = [r; 0] (c real)."""
+    import numpy as np
+    if g == 0:
+        return 1.0, 0.0, f
+    if f == 0:
+        return 0.0, np.conj(g) / abs(g), abs(g)
+    nf, ng = abs(f), abs(g)
+    rr = math.hypot(nf, ng)
+    c = nf / rr
+    sgn = f / nf
+    sv = sgn * np.conj(g) / rr
+    return c, sv, sgn * rr
+
+
 def _gmres_ir(A, B, X, precond, opts, anorm):
     """GMRES-based iterative refinement (right-preconditioned restarted
-    GMRES on A M^{-1} u = r, M = low-precision factorization), one RHS at a
-    time like SLATE (src/gesv_mixed_gmres.cc)."""
+    GMRES on A M^{-1} u = r, M = the low-precision factorization), one
+    right-hand side at a time like SLATE (src/gesv_mixed_gmres.cc).  The
+    Krylov basis V and the preconditioned vectors Z are distributed n x k
+    matrices on A's grid: orthogonalisation is classical Gram-Schmidt with
+    one re-orthogonalisation as two GEMMs per pass (V^H w, then w -= V h),
+    norms are distributed reductions; only the (restart + 1) x restart
+    Hessenberg least-squares problem (Givens rotations) lives on the host,
+    as in SLATE."""
+    import numpy as np
+    from .aux import scale as mscale
     from .blas3 import gemm
     itermax = int(get_option(opts, Option.MaxIterations, 30))
-    restart = min(30, itermax)
+    restart = max(1, min(30, itermax))
     n = A.n()
-    Xd = allgather_dense(X)
-    Bd = allgather_dense(B)
-    dev = Xd.device
+    dt = B.storage.dtype
+    npdt = np.complex128 if dt.is_complex else np.float64
+    V = _like(Matrix(n, restart + 1, nb=A.storage.bc.nb, p=A.storage.bc.p, q=A.storage.bc.q, comm=A.storage.comm,
+                     dtype=dt, device=A.storage.device, order=A.storage.bc.order), dt)
+    Z = _like(V, dt)
+    w = _small(A, n, dt)
     total = 0
-    R = _like(B)
     for col in range(B.n()):
-        for outer in range(max(1, itermax // max(restart, 1))):
-            # residual r = b - A x (fp64, distributed)
-            copy(B, R)
-            gemm(-1.0, A, X, 1.0, R, opts)
-            Rd = allgather_dense(R)[:, col]
-            Xc = allgather_dense(X)
-            if float(Rd.abs().max()) <= float(Xc[:, col].abs().max()) * anorm * torch.finfo(torch.float64).eps * \
-                    math.sqrt(n):
+        Bc, Xc = _col(B, col), _col(X, col)
+        for outer in range(max(1, itermax // restart)):
+            copy(Bc, w)
+            _mul(-1.0, A, Xc, 1.0, w, opts)                      # r = b - A x (working precision)
+            if _converged(w, Xc, anorm, n):
                 break
-            beta = float(torch.linalg.vector_norm(Rd))
+            beta = float(norm(Norm.Fro, w))
             if beta == 0:
                 break
-            Vb = [Rd / beta]
-            Hm = torch.zeros(restart + 1, restart, dtype=Rd.dtype)
-            g = torch.zeros(restart + 1, dtype=Rd.dtype)
+            v0 = _col(V, 0)
+            copy(w, v0)
+            mscale(1.0, beta, v0)
+            H = np.zeros((restart + 1, restart), dtype=npdt)
+            g = np.zeros(restart + 1, dtype=npdt)
             g[0] = beta
-            Zs = []
-            k_used = 0
+            cs, sn = np.zeros(restart), np.zeros(restart, dtype=npdt)
+            k = 0
             for j in range(restart):
-                z = precond(Vb[j])                     # z = M^{-1} v
-                Zs.append(z)
-                w = _matvec(A, z, opts)                # w = A z
-                for i in range(j + 1):
-                    Hm[i, j] = torch.dot(Vb[i].conj(), w).item()
-                    w = w - Hm[i, j] * Vb[i]
-                Hm[j + 1, j] = torch.linalg.vector_norm(w).item()
-                k_used = j + 1
+                precond(_col(V, j), _col(Z, j))                   # z_j = M^{-1} v_j
+                _mul(1.0, A, _col(Z, j), 0.0, w, opts)            # w = A z_j
+                Vj = _col(V, 0, j)
+                hsum = np.zeros(j + 1, dtype=npdt)
+                for _ in range(2):                                # CGS2
+                    h = _small(A, j + 1, dt)
+                    gemm(1.0, Vj.conj_transpose(), w, 0.0, h, opts)
+                    gemm(-1.0, Vj, h, 1.0, w, opts)
+                    hsum += allgather_dense(h).reshape(-1).cpu().numpy()
+                hn = float(norm(Norm.Fro, w))
+                H[:j + 1, j] = hsum
+                H[j + 1, j] = hn
+                for i in range(j):                                 # previous rotations
+                    a, b = H[i, j], H[i + 1, j]
+                    H[i, j] = cs[i] * a + sn[i] * b
+                    H[i + 1, j] = -np.conj(sn[i]) * a + cs[i] * b
+                cs[j], sn[j], H[j, j] = _givens(H[j, j], H[j + 1, j])
+                H[j + 1, j] = 0
+                g[j + 1] = -np.conj(sn[j]) * g[j]
+                g[j] = cs[j] * g[j]
+                k = j + 1
                 total += 1
-                # least-squares residual estimate
-                y = torch.linalg.lstsq(Hm[:j + 2, :j + 1], g[:j + 2, None]).solution
-                res = torch.linalg.vector_norm(Hm[:j + 2, :j + 1] @ y - g[:j + 2, None])
-                if float(Hm[j + 1, j]) == 0 or float(res) <= 1e-14 * beta:
+                if hn == 0 or abs(g[j + 1]) <= 1e-14 * beta:
                     break
-                Vb.append(w / Hm[j + 1, j])
-            y = torch.linalg.lstsq(Hm[:k_used + 1, :k_used], g[:k_used + 1, None]).solution.reshape(-1)
-            upd = sum(y[i] * Zs[i] for i in range(k_used))
-            Xc[:, col] = Xc[:, col] + upd
-            from_dense(X, Xc)
+                vn = _col(V, j + 1)
+                copy(w, vn)
+                mscale(1.0, hn, vn)
+            # y = R^{-1} g, x += Z y
+            y = np.zeros(k, dtype=npdt)
+            for i in range(k - 1, -1, -1):
+                y[i] = (g[i] - H[i, i + 1:k] @ y[i + 1:k]) / H[i, i]
+            Y = _small(A, k, dt)
+            from_dense(Y, torch.as_tensor(y.reshape(k, 1)).to(dt))
+            gemm(1.0, _col(Z, 0, k - 1), Y, 1.0, Xc, opts)
     return total
 
 
-def _matvec(A, z, opts):
-    from .blas3 import gemm
-    Z = _vec(A, z)
-    W = _vec(A, torch.zeros_like(z))
-    gemm(1.0, A, Z, 0.0, W, opts)
-    return allgather_dense(W)[:, 0]
-
-
-def _vec(A, v):
-    s = A.storage
-    bc = s.bc
-    V = Matrix(A.n(), 1, nb=bc.nb, p=bc.p, q=bc.q, comm=s.comm, dtype=v.dtype, device=s.device, order=bc.order)
-    V.insertLocalTiles(device=s.device.index if s.device.type == "cuda" else -1)
-    from_dense(V, v.reshape(-1, 1))
-    return V
+def _lo_solve_into(Alo, solve, v, z, lo):
+    """z = M^{-1} v with the low-precision factors (distributed copies with
+    precision conversion around the solve)."""
+    t = _like(v, lo)
+    copy(v, t)
+    solve(t)
+    copy(t, z)
 
 
 def gesv_mixed_gmres(A, pivots, B, X, opts=None):
@@ -232,10 +285,8 @@ def gesv_mixed_gmres(A, pivots, B, X, opts=None):
             return _fallback(gesv, (A, pivots), B, X, opts, info)
         anorm = float(norm(Norm.Inf, A))
 
-        def precond(v):
-            V = _vec(Alo, v.to(lo))
-            getrs(Alo, pivots, V, opts)
-            return allgather_dense(V)[:, 0].to(v.dtype)
+        def precond(v, z):
+            _lo_solve_into(Alo, lambda t: getrs(Alo, pivots, t, opts), v, z, lo)
         Xlo = _like(B, lo)
         copy(B, Xlo)
         getrs(Alo, pivots, Xlo, opts)
@@ -255,16 +306,13 @@ def posv_mixed_gmres(A, B, X, opts=None):
             return _fallback(posv, (A,), B, X, opts, info)
         anorm = float(norm(Norm.Inf, A))
 
-        def precond(v):
-            V = _vec(Alo, v.to(lo))
-            potrs(Alo, V, opts)
-            return allgather_dense(V)[:, 0].to(v.dtype)
+        def precond(v, z):
+            _lo_solve_into(Alo, lambda t: potrs(Alo, t, opts), v, z, lo)
         Xlo = _like(B, lo)
         copy(B, Xlo)
         potrs(Alo, Xlo, opts)
         copy(Xlo, X)
-        Ah = A
-        iters = _gmres_ir(Ah, B, X, precond, opts, anorm)
+        iters = _gmres_ir(A, B, X, precond, opts, anorm)
         return info, iters
 
 
