@@ -12,9 +12,11 @@ time, Gflop/s, % of the MI355X dense peak of all ranks (device target),
 status; exit status 1 if any check failed.  Routines (test/test.cc
 families): BLAS-3 gemm herk/syrk her2k/syr2k hemm/symm trmm trsm;
 Cholesky potrf potrs posv potri trtri posv_mixed; LU getrf getrs gesv
-getri gesv_nopiv gesv_tntpiv/calu gesv_rbt gesv_mixed; band gbsv; QR/LQ
-geqrf gelqf cholqr gels; eigen/SVD heev/syev hegv/sygv svd; indefinite
-hesv/sysv; aux norm colnorms add redistribute gecondest.
+getri gesv_nopiv gesv_tntpiv/calu gesv_rbt gesv_mixed gesv_mixed_gmres;
+band gbsv pbsv gbmm hbmm tbsm; QR/LQ geqrf unmqr gelqf cholqr gels;
+eigen/SVD heev/syev heev_vals hegv/sygv svd svd_vals; indefinite
+hesv/sysv; aux norm colnorms add redistribute gecondest pocondest
+trcondest matgen.
 """
 from __future__ import annotations
 
@@ -457,6 +459,137 @@ def t_gbsv(c, m, n, k, **p):
     return _lu_solve_check(c, Ad, D(B), Bd, n), t, 2.0 * n * kl * (kl + ku)
 
 
+def _band(c, n, kl, ku, seed=1):
+    A = sl.BandMatrix(n, n, kl, ku, nb=c.a.nb, p=c.a.p, q=c.a.q, dtype=c.dt, device=c.dev)
+    A.insertLocalTiles(device=c.dev.index if c.dev.type == "cuda" else -1)
+    sl.generate_matrix(A, "rand_dominant", seed)
+    sl.band_mask(A)
+    return A
+
+
+def t_pbsv(c, m, n, k, uplo=Uplo.Lower, **p):
+    kd = max(1, c.a.nb // 2)
+    A = sl.HermitianBandMatrix(uplo, n, kd, nb=c.a.nb, p=c.a.p, q=c.a.q, dtype=c.dt, device=c.dev)
+    A.insertLocalTiles(device=c.dev.index if c.dev.type == "cuda" else -1)
+    sl.generate_matrix(A, "poev", 1)
+    sl.band_mask(A, kd, 0) if uplo == Uplo.Lower else sl.band_mask(A, 0, kd)
+    Af = _herm_full(A)
+    B = c.mat(n, k, seed=2)
+    Bd = D(B)
+    info, t = c.timed(lambda: sl.pbsv(A, B, c.opts))
+    err = _rel(Af @ D(B) - Bd, Af.abs().max() * D(B).abs().max() * n) if c.a.check == 'y' else None
+    return err, t, n * kd * kd + 4.0 * n * kd * k
+
+
+def t_gbmm(c, m, n, k, **p):
+    kl = ku = max(1, c.a.nb // 2)
+    A = _band(c, n, kl, ku)
+    B, C = c.mat(n, k, seed=2), c.mat(n, k, seed=3)
+    Ad, Bd, Cd = D(A), D(B), D(C)
+    _, t = c.timed(lambda: sl.gbmm(2.0, A, B, 0.5, C, c.opts))
+    ref = 2.0 * Ad @ Bd + 0.5 * Cd
+    err = _rel(D(C) - ref, ref.abs().max() * n) if c.a.check == 'y' else None
+    return err, t, 2.0 * n * (kl + ku + 1) * k
+
+
+def t_hbmm(c, m, n, k, uplo=Uplo.Lower, side=Side.Left, **p):
+    kd = max(1, c.a.nb // 2)
+    A = sl.HermitianBandMatrix(uplo, n, kd, nb=c.a.nb, p=c.a.p, q=c.a.q, dtype=c.dt, device=c.dev)
+    A.insertLocalTiles(device=c.dev.index if c.dev.type == "cuda" else -1)
+    sl.generate_matrix(A, "rands_hermitian", 1)
+    sl.band_mask(A, kd, 0) if uplo == Uplo.Lower else sl.band_mask(A, 0, kd)
+    Af = _herm_full(A)
+    B = c.mat(n, k, seed=2) if side == Side.Left else c.mat(k, n, seed=2)
+    C = c.mat(n, k, "zeros") if side == Side.Left else c.mat(k, n, "zeros")
+    Bd = D(B)
+    _, t = c.timed(lambda: sl.hbmm(side, 1.0, A, B, 0.0, C, c.opts))
+    ref = Af @ Bd if side == Side.Left else Bd @ Af
+    err = _rel(D(C) - ref, ref.abs().max() * n) if c.a.check == 'y' else None
+    return err, t, 2.0 * n * (2 * kd + 1) * k
+
+
+def t_tbsm(c, m, n, k, uplo=Uplo.Lower, side=Side.Left, **p):
+    kd = max(1, c.a.nb // 2)
+    T = sl.TriangularBandMatrix(uplo, Diag.NonUnit, n, kd, nb=c.a.nb, p=c.a.p, q=c.a.q, dtype=c.dt, device=c.dev)
+    T.insertLocalTiles(device=c.dev.index if c.dev.type == "cuda" else -1)
+    sl.generate_matrix(T, "rand_dominant", 1)
+    sl.band_mask(T, kd, 0) if uplo == Uplo.Lower else sl.band_mask(T, 0, kd)
+    Td = D(T)
+    B = c.mat(n, k, seed=2) if side == Side.Left else c.mat(k, n, seed=2)
+    Bd = D(B)
+    _, t = c.timed(lambda: sl.tbsm(side, 1.0, T, B, None, c.opts))
+    X = D(B)
+    ref = Td @ X if side == Side.Left else X @ Td
+    err = _rel(ref - Bd, Td.abs().max() * X.abs().max() * n) if c.a.check == 'y' else None
+    return err, t, 1.0 * n * kd * k * 2
+
+
+def t_pocondest(c, m, n, k, uplo=Uplo.Lower, **p):
+    A = _herm_mat(c, n, uplo, "poev")
+    Af = _herm_full(A)
+    anorm = sl.norm(Norm.One, A)
+    sl.potrf(A, c.opts)
+    rc, t = c.timed(lambda: sl.pocondest(Norm.One, A, anorm, c.opts))
+    ref = 1.0 / float(torch.linalg.cond(Af.cpu(), 1))
+    return (0.0 if ref / 3 <= rc <= 3 * ref else 1.0) if c.a.check == 'y' else None, t, 4.0 * n * n
+
+
+def t_trcondest(c, m, n, k, uplo=Uplo.Lower, **p):
+    A = c.mat(n, n, "rand_dominant", 1)
+    T = sl.TriangularMatrix(uplo, A, diag=Diag.NonUnit)
+    Td = torch.tril(D(A)) if uplo == Uplo.Lower else torch.triu(D(A))
+    rc, t = c.timed(lambda: sl.trcondest(Norm.One, T, None, c.opts))
+    ref = 1.0 / float(torch.linalg.cond(Td.cpu(), 1))
+    return (0.0 if ref / 3 <= rc <= 3 * ref else 1.0) if c.a.check == 'y' else None, t, 4.0 * n * n
+
+
+def t_unmqr(c, m, n, k, side=Side.Left, **p):
+    A = c.mat(m, n, seed=1)
+    T = sl.TriangularFactors()
+    sl.geqrf(A, T, c.opts)
+    C = c.mat(m, k, seed=2) if side == Side.Left else c.mat(k, m, seed=2)
+    Cd = D(C)
+    _, t = c.timed(lambda: sl.unmqr(side, Op.ConjTrans, A, T, C, c.opts))
+    sl.unmqr(side, Op.NoTrans, A, T, C, c.opts)                     # Q Q^H C = C
+    err = _rel(D(C) - Cd, Cd.abs().max() * m) if c.a.check == 'y' else None
+    return err, t, 4.0 * m * n * k
+
+
+def t_gesv_mixed_gmres(c, m, n, k, **p):
+    if c.t not in ('d', 'z'):
+        return None, 0.0, 0.0
+    A, B = c.mat(n, n, "rand_dominant", 1), c.mat(n, k, seed=2)
+    X = c.mat(n, k, "zeros")
+    Ad, Bd = D(A), D(B)
+    r, t = c.timed(lambda: sl.gesv_mixed_gmres(A, sl.Pivots(), B, X, c.opts))
+    err = _rel(Ad @ D(X) - Bd, Ad.abs().max() * D(X).abs().max() * n) if c.a.check == 'y' else None
+    return err, t, 2.0 * n ** 3 / 3.0
+
+
+def t_svd_vals(c, m, n, k, **p):
+    A = c.mat(m, n, "svd_geo", 1)
+    s0 = torch.linalg.svdvals(D(A).cpu())
+    s, t = c.timed(lambda: sl.svd_vals(A, None, c.opts))
+    err = _rel(s.cpu() - s0, s0.max() * max(m, n)) if c.a.check == 'y' else None
+    return err, t, 4.0 * m * n * n
+
+
+def t_heev_vals(c, m, n, k, uplo=Uplo.Lower, **p):
+    A = c.mat(n, n, "heev_arith", 1, sl.HermitianMatrix, uplo=uplo)
+    w0 = torch.linalg.eigvalsh(_herm_full(A).cpu())
+    w, t = c.timed(lambda: sl.heev(A, None, None, c.opts))
+    err = _rel(w.cpu() - w0, w0.abs().max() * n) if c.a.check == 'y' else None
+    return err, t, 4.0 * n ** 3 / 3.0
+
+
+def t_matgen(c, m, n, k, **p):
+    """Generation rate of the spectral svd kind (two distributed QRs)."""
+    A = c.mat(m, n, "zeros")
+    s, t = c.timed(lambda: sl.generate_matrix(A, "svd_geo", 1, cond=1e3))
+    err = _rel(torch.linalg.svdvals(D(A).cpu()) - s.sort(descending=True).values, 1.0) if c.a.check == 'y' else None
+    return err, t, 8.0 * m * n * n
+
+
 ROUTINES = {"gemm": t_gemm, "herk": t_herk, "syrk": t_herk, "trsm": t_trsm, "potrf": t_potrf,
             "posv": t_posv, "getrf": t_getrf, "gesv": t_gesv, "geqrf": t_geqrf, "gels": t_gels,
             "heev": t_heev, "syev": t_heev, "svd": t_svd, "norm": t_norm, "genorm": t_norm,
@@ -467,7 +600,10 @@ ROUTINES = {"gemm": t_gemm, "herk": t_herk, "syrk": t_herk, "trsm": t_trsm, "pot
             "gesv_calu": _getrf_method("calu"), "gesv_rbt": _getrf_method("rbt"),
             "posv_mixed": t_posv_mixed, "gelqf": t_gelqf, "cholqr": t_cholqr, "hegv": t_hegv,
             "sygv": t_hegv, "gecondest": t_gecondest, "colnorms": t_colnorms, "add": t_add,
-            "redistribute": t_redistribute, "gbsv": t_gbsv}
+            "redistribute": t_redistribute, "gbsv": t_gbsv, "pbsv": t_pbsv, "gbmm": t_gbmm, "hbmm": t_hbmm,
+            "tbsm": t_tbsm, "pocondest": t_pocondest, "trcondest": t_trcondest, "unmqr": t_unmqr,
+            "gesv_mixed_gmres": t_gesv_mixed_gmres, "svd_vals": t_svd_vals, "heev_vals": t_heev_vals,
+            "syev_vals": t_heev_vals, "matgen": t_matgen}
 
 # per-GPU dense peaks (MI355X spec, TFLOP/s): fp64 matrix = vector, fp32 matrix
 PEAK_TF = {'s': 157.3, 'd': 78.6, 'c': 157.3, 'z': 78.6}
