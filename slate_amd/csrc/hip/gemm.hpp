@@ -143,8 +143,8 @@ struct Stage {
     }
 };
 
-template <typename T, bool TA, bool TB, int BM, int BN, int BK, bool PTRS, int WVM = 2, int WVN = 2>
-__global__ void __launch_bounds__(64 * WVM * WVN, 2)
+template <typename T, bool TA, bool TB, int BM, int BN, int BK, bool PTRS, int WVM = 2, int WVN = 2, int OCC = 2>
+__global__ void __launch_bounds__(64 * WVM * WVN, OCC)
 gemm_real_kernel(GemmArgs<T> a) {
     using MF = mfma_real<T>;
     using acc_t = typename MF::acc_t;

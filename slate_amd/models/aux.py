@@ -182,8 +182,37 @@ def _numroc_r(n, nb, iproc, nprocs):
 
 
 def gather(A, root=0):
-    D = allgather_dense(A)
-    return D if A.storage.comm.rank == root else None
+    """The whole matrix on ``root`` only (Matrix::gather): a piece-level
+    redistribution onto a one-process grid owned by rank 0 (other roots
+    get it from rank 0 by one broadcast-free send through the same
+    engine)."""
+    s = A.storage
+    if s.comm.size == 1:
+        return allgather_dense(A)
+    from ..core.matrix import Matrix
+    nb = s.bc.nb if s.bc is not None else max(s.tileNb(0) if s.nt else 1, 1)
+    R = Matrix(A.m(), A.n(), nb=nb, p=1, q=1, comm=s.comm, dtype=s.dtype, device=s.device)
+    R.insertLocalTiles(device=s.device.index if s.device.type == "cuda" else -1)
+    redistribute(A, R)
+    D = None
+    if s.comm.rank == 0:
+        lb = R.local_block()
+        D = lb.data[:A.m(), :A.n()].clone()
+    if root != 0:
+        import torch.distributed as dist
+        if s.comm.rank in (0, root):
+            buf = D if s.comm.rank == 0 else torch.empty((A.n(), A.m()), dtype=s.dtype, device=s.device).t()
+            t = buf.t().contiguous() if s.comm.rank == 0 else torch.empty((A.n(), A.m()), dtype=s.dtype,
+                                                                            device=s.device)
+            if s.comm.rank == 0:
+                dist.send(t, s.comm.ranks[root] if hasattr(s.comm, "ranks") else root, group=s.comm.group)
+                D = None
+            else:
+                dist.recv(t, s.comm.ranks[0] if hasattr(s.comm, "ranks") else 0, group=s.comm.group)
+                D = t.t()
+        else:
+            D = None
+    return D
 
 
 def from_dense(A, D: torch.Tensor):

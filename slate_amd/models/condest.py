@@ -8,8 +8,8 @@ distributed solves).
 MI355X design: the estimator works on distributed n x 1 vectors with the
 same row distribution as the factor, and each "apply A^{-1}" / "apply
 A^{-H}" is one call of the existing distributed solve (getrs / potrs /
-trsm), so all the O(n^2) work stays on the GPUs; only the O(n) vector
-reductions (sign, arg-max) are gathered.
+trsm), so all the O(n^2) work stays on the GPUs; the O(n) vector steps
+run on each rank's local part with scalar reductions only.
 """
 from __future__ import annotations
 
@@ -18,7 +18,6 @@ import torch
 from ..core.enums import Diag, Norm, Op, Side, Uplo
 from ..core.matrix import Matrix, TriangularMatrix
 from ..utils.trace import trace_block
-from .aux import allgather_dense, from_dense
 
 
 def _vec_like(A, dtype=None):
@@ -31,39 +30,96 @@ def _vec_like(A, dtype=None):
     return v
 
 
+class _DistVec:
+    """This rank's part of a distributed n x 1 vector X (the local rows and
+    their global indices): the estimator's O(n) vector operations run on
+    the local parts, with scalar reductions only."""
+
+    def __init__(self, X):
+        self.X = X
+        lb = X.local_block()
+        self.lb = lb
+        self.comm = X.storage.comm
+        self.owner = lb.nloc > 0 and lb.mloc > 0
+        self.rows = torch.as_tensor([lb.global_row(i) for i in range(lb.mloc)], dtype=torch.int64) \
+            if self.owner else torch.zeros(0, dtype=torch.int64)
+
+    @property
+    def v(self):
+        return self.lb.data[:self.lb.mloc, 0] if self.owner else None
+
+    def fill(self, fn):
+        """v[i] = fn(global index tensor) (host values)."""
+        if self.owner:
+            self.v.copy_(fn(self.rows).to(self.v.dtype).to(self.v.device))
+        self.X.storage.mark_local_modified(self.X.storage.origin_slot)
+
+    def sum_abs(self):
+        loc = float(self.v.abs().sum()) if self.owner else 0.0
+        return self.comm.allreduce_scalar(loc) if self.comm.size > 1 else loc
+
+    def argmax_abs(self):
+        if self.owner and self.v.numel():
+            a = self.v.abs()
+            i = int(a.argmax())
+            val, idx = float(a[i]), int(self.rows[i])
+        else:
+            val, idx = -1.0, 1 << 62
+        return self.comm.maxloc(val, idx) if self.comm.size > 1 else (val, idx)
+
+    def dot_real(self, fn_x):
+        """sum_i real(conj(v_i) x_i) with x given by its global-index function."""
+        loc = 0.0
+        if self.owner:
+            x = fn_x(self.rows).to(self.v.dtype).to(self.v.device)
+            loc = float((self.v.conj() * x).real.sum())
+        return self.comm.allreduce_scalar(loc) if self.comm.size > 1 else loc
+
+    def to_sign(self):
+        """v := v / |v| (1 where v = 0), in place on the local part."""
+        if self.owner:
+            v = self.v
+            a = v.abs()
+            one = torch.ones_like(v)
+            v.copy_(torch.where(a > 0, v / torch.where(a > 0, a, torch.ones_like(a)).to(v.dtype), one))
+        self.X.storage.mark_local_modified(self.X.storage.origin_slot)
+
+
 def norm1est(solve, solve_h, n, like):
-    """Estimate ||A^{-1}||_1 given x -> A^{-1} x and x -> A^{-H} x acting on
-    distributed n x 1 matrices (Higham's refinement of Hager's method)."""
-    dt = like.storage.dtype
-    cplx = dt.is_complex
+    """Estimate ||A^{-1}||_1 given X -> A^{-1} X and X -> A^{-H} X acting on
+    distributed n x 1 matrices (Higham's refinement of Hager's method,
+    LAPACK lacn2).  The vectors never leave their ranks: 1-norms, the
+    sign vector, the arg-max and the dot products are local operations
+    plus scalar reductions (SLATE internal_norm1est.cc: MPI_Bcast of
+    isave/kase/est and an MPI_Allreduce MAXLOC)."""
     X = _vec_like(like)
-    x = torch.full((n, 1), 1.0 / n, dtype=dt)
+    V = _DistVec(X)
+    V.fill(lambda g: torch.full((g.numel(),), 1.0 / n, dtype=torch.float64))
+    xfn = lambda g: torch.full((g.numel(),), 1.0 / n, dtype=torch.float64)   # noqa: E731
     est = 0.0
     jlast = -1
     for it in range(5):
-        from_dense(X, x)
         solve(X)
-        y = allgather_dense(X).cpu()
-        ny = float(y.abs().sum())
+        V = _DistVec(X)
+        ny = V.sum_abs()
         if it > 0 and ny <= est:
             break
         est = ny
-        xi = torch.where(y.abs() > 0, y / torch.where(y.abs() > 0, y.abs(), torch.ones_like(y.abs())),
-                         torch.ones_like(y)) if cplx else torch.where(y >= 0, torch.ones_like(y), -torch.ones_like(y))
-        from_dense(X, xi)
+        V.to_sign()
         solve_h(X)
-        z = allgather_dense(X).cpu()
-        j = int(z.abs().argmax())
-        if it > 0 and (j == jlast or float(z.abs()[j]) <= float((z.conj() * x).real.sum())):
+        V = _DistVec(X)
+        zj, j = V.argmax_abs()
+        if it > 0 and (j == jlast or zj <= V.dot_real(xfn)):
             break
         jlast = j
-        x = torch.zeros((n, 1), dtype=dt)
-        x[j] = 1
+        xfn = (lambda jj: (lambda g: (g == jj).to(torch.float64)))(j)
+        V.fill(xfn)
     # alternating-sign test vector
-    alt = torch.tensor([(-1) ** i * (1.0 + i / max(n - 1, 1)) for i in range(n)], dtype=dt).reshape(n, 1)
-    from_dense(X, alt)
+    V = _DistVec(X)
+    V.fill(lambda g: torch.where(g % 2 == 0, 1.0, -1.0).to(torch.float64) * (1.0 + g.to(torch.float64) /
+                                                                              max(n - 1, 1)))
     solve(X)
-    t = 2.0 * float(allgather_dense(X).abs().sum()) / (3.0 * n)
+    t = 2.0 * _DistVec(X).sum_abs() / (3.0 * n)
     return max(est, t)
 
 

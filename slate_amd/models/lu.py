@@ -629,7 +629,6 @@ def gesv_nopiv(A, B, opts=None) -> int:
 
 def getri(A, pivots, opts=None) -> int:
     """In-place inverse from the LU factors: inv(A) = inv(U) inv(L) P."""
-    from .aux import allgather_dense, from_dense
     s = A.storage
     if s.comm.size == 1 or (s.bc is not None and s.bc.p * s.bc.q == 1):
         lb = A.local_block()

@@ -250,3 +250,24 @@ def test_four_ranks():
 
 def test_eight_ranks_2x4():
     run_dist(_run, 8, 2, 4, [f.__name__ for f in ALL], False, timeout=900)
+
+
+def _gather_roots(rank, size, p, q):
+    import slate_amd as sl
+    from slate_amd.models.aux import allgather_dense
+    A = sl.Matrix(37, 29, nb=8, p=p, q=q)
+    A.insertLocalTiles()
+    sl.generate_matrix(A, "rands", 3)
+    ref = allgather_dense(A)
+    for root in range(size):
+        D = sl.gather(A, root)
+        if rank == root:
+            assert D is not None and (D.cpu() - ref.cpu()).abs().max() == 0
+        else:
+            assert D is None
+
+
+def test_gather_to_root():
+    """Matrix::gather: the whole matrix on the root only (piece-level
+    redistribution onto rank 0, then one send to another root)."""
+    run_dist(_gather_roots, 4, 2, 2)
