@@ -133,9 +133,59 @@ class Hb2stFactors:
         self.sweep_ptr, self.count, self.phase = sweep_ptr, count, phase
 
 
-def hb2st(B: torch.Tensor, nb: int):
-    """Hermitian band (dense host copy, both triangles, bandwidth nb) ->
-    real symmetric tridiagonal (d, e) + reflectors.  Runs on the host."""
+def _hb2st_schedule(n, b):
+    """Tasks per sweep (same recurrence as the chase) and the first
+    reflector slot of every sweep."""
+    j = torch.arange(max(n - 1, 0), dtype=torch.int64)
+    e0 = torch.clamp(j + b, max=n - 1)
+    k0 = e0 - j
+    nt = torch.where(k0 <= 1, torch.zeros_like(j), 1 + torch.div(n - 1 - e0 + b - 1, b, rounding_mode="floor"))
+    sp = torch.zeros(max(n, 1), dtype=torch.int64)
+    if n > 1:
+        sp[1:n] = torch.cumsum(nt, 0)
+    return nt, sp
+
+
+def _hb2st_device(B: torch.Tensor, nb: int, dev):
+    """Bulge chasing on the GPU (csrc/hip/hb2st.hip): persistent
+    workgroups, one per concurrently chased sweep, ordered by an atomic
+    ticket, progress counters between consecutive sweeps."""
+    from .. import _native
+    n = B.shape[0]
+    b = max(1, nb)
+    dt = B.dtype
+    A = ops.colmajor_empty(n, n, dt, dev)
+    A.copy_(B.to(dev))
+    nt, sp = _hb2st_schedule(n, b)
+    total = int(nt.sum()) if nt.numel() else 0
+    V = torch.zeros(max(total, 1), b, dtype=dt, device=dev)
+    tau = torch.zeros(max(total, 1), dtype=dt, device=dev)
+    row = torch.zeros(max(total, 1), dtype=torch.int64, device=dev)
+    ln = torch.zeros(max(total, 1), dtype=torch.int64, device=dev)
+    nsw = max(n - 1, 0)
+    work = torch.zeros(nsw + 2, dtype=torch.int32, device=dev)
+    ntd, spd = nt.to(dev), sp.to(dev)
+    props = torch.cuda.get_device_properties(dev)
+    nwg = int(min(max(nsw, 1), 2 * props.multi_processor_count))
+    with trace_block("hb2st"):
+        if nsw > 0:
+            _native._hip.hb2st(_code(dt), n, b, A.data_ptr(), A.stride(1), V.data_ptr(), tau.data_ptr(),
+                               row.data_ptr(), ln.data_ptr(), spd.data_ptr(), ntd.data_ptr(), work.data_ptr(),
+                               nsw, nwg, torch.cuda.current_stream(dev).cuda_stream)
+    Bh = A
+    return Bh, V[:total], tau[:total], row[:total], ln[:total], sp, total
+
+
+def hb2st(B: torch.Tensor, nb: int, device=None):
+    """Hermitian band (dense copy, both triangles, bandwidth nb) -> real
+    symmetric tridiagonal (d, e) + reflectors.  On the GPU when ``device``
+    is a CUDA device and SLATE_AMD_HB2ST=device, otherwise on the pipelined
+    host threads."""
+    import os
+    if device is not None and torch.device(device).type == "cuda" and \
+            os.environ.get("SLATE_AMD_HB2ST", "host") != "host" and max(1, nb) <= 128:
+        Bh, V, tau, row, ln, sp, cnt = _hb2st_device(B, nb, torch.device(device))
+        return _hb2st_finish(Bh, V, tau, row, ln, sp, cnt)
     n = B.shape[0]
     Bh = _cm(B.detach().to("cpu")).clone()
     Bh = _cm(Bh)
@@ -150,8 +200,14 @@ def hb2st(B: torch.Tensor, nb: int):
     with trace_block("hb2st"):
         cnt = _native._host.hb2st(_code(dt), n, b, Bh.data_ptr(), max(1, Bh.stride(1)), V.data_ptr(),
                                   tau.data_ptr(), row.data_ptr(), ln.data_ptr(), cap, sp.data_ptr())
-    d = Bh.diagonal().real.to(torch.float64).clone()
-    ec = Bh.diagonal(-1).clone()
+    return _hb2st_finish(Bh, V, tau, row, ln, sp, cnt)
+
+
+def _hb2st_finish(Bh, V, tau, row, ln, sp, cnt):
+    n = Bh.shape[0]
+    dt = Bh.dtype
+    d = Bh.diagonal().real.to(torch.float64).cpu().clone()
+    ec = Bh.diagonal(-1).cpu().clone()
     ph = torch.ones(n, dtype=dt)
     if dt.is_complex and n > 1:
         a = ec.abs()
@@ -350,7 +406,7 @@ def heev(A, Lambda=None, Z=None, opts=None):
             scale = 1.0 / amax
             Af.mul_(scale)
         F1 = he2hb(Af, nb)
-        d, e, F2 = hb2st(_band_only(Af, nb), nb)
+        d, e, F2 = hb2st(_band_only(Af, nb), nb, device=Af.device if Af.is_cuda else None)
         want = Z is not None
         if not want:
             w = sterf(d, e)

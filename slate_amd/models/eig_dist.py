@@ -273,7 +273,7 @@ def heev_dist(A, Lambda=None, Z=None, opts=None):
         method = get_option(opts, Option.MethodEig, MethodEig.DC)
         # stage 2 on rank 0, results broadcast
         if comm.rank == 0:
-            d, e, F2 = E.hb2st(B, nb)
+            d, e, F2 = E.hb2st(B, nb, device=dev if dev.type == "cuda" else None)
             meta = torch.tensor([F2.count], dtype=torch.int64)
         else:
             d = e = F2 = None
