@@ -28,6 +28,8 @@ end (SLATE: device_info copy + queue sync per panel, internal_potrf.cc:76).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import ops
@@ -89,7 +91,6 @@ def _potrf_lower(A, opts):
     lc_end = _lstart(R_end, nb, pc, q)
     ss = StreamSet(dev, reserve_cus=0)   # one-CU panel kernels: no reserved CUs (measured: 49.0 vs 45.1 TF/s with 32)
     infos = torch.zeros(max(nt, 1), dtype=torch.int64, device=dev)
-    import os
     group = int(os.environ.get("SLATE_AMD_POTRF_GROUP", "2"))
     if p == 1 and q == 1 and group > 1 and nt > 2:
         _potrf_1x1_grouped(A, s, buf, nb, g0, nt, R_end, la, group, ss, infos, ct, dev)
@@ -99,6 +100,12 @@ def _potrf_lower(A, opts):
     # stream) and the rest (update stream, its own column communicator)
     plans = plan_col_gathers_steps(s.tileMb, g0, nt, nb, p, q, pc, dev, split=la) if (p > 1 or q > 1) else None
     colu = grid.col_comm_u if (grid is not None and p > 1) else None
+    # diag-first (needs a lookahead column): right after the panel solve of
+    # step t, the rows of tile g+1 travel to the next diagonal owner, which
+    # updates and factors A(g+1, g+1) on the diag stream while the big
+    # panel broadcast and the lookahead update proceed on the panel stream
+    diag_first = la >= 1 and nt > 1 and os.environ.get("SLATE_AMD_POTRF_DIAGFIRST", "1") != "0"
+    ev_diag = {}
     ev_tr = {}
     ss.fork()
     for t in range(nt):
@@ -118,7 +125,10 @@ def _potrf_lower(A, opts):
                 ss.wait(ss.panel, ev_tr[t - la - 1])
             with trace_block("potrf::panel"):
                 if own_diag:
-                    ops.potrf('L', buf[lrg:lrg + kb, lcg:lcg + kb], infos[t:t + 1])
+                    if t in ev_diag:
+                        ss.wait(ss.panel, ev_diag.pop(t))       # factored during step t-1 (diag-first)
+                    else:
+                        ops.potrf('L', buf[lrg:lrg + kb, lcg:lcg + kb], infos[t:t + 1])
                 # diagonal tile -> column
                 if own_col:
                     if p > 1:
@@ -131,6 +141,28 @@ def _potrf_lower(A, opts):
                     P = buf[lr1:lr_end, lcg:lcg + kb]
                     if P.shape[0]:
                         ops.trsm('R', 'L', ct, 'N', 1.0, D, P)
+                # diag-first: the next diagonal tile, on its own stream
+                kb1 = 0
+                if diag_first and t + 1 < nt:
+                    g1 = g + 1
+                    kb1 = s.tileMb(g1) if t + 1 < nt - 1 or A.last_mb is None else A.last_mb
+                    if pr == g1 % p:
+                        ev_solve = ss.event(ss.panel)
+                        with ss.use(ss.diag):
+                            ss.wait(ss.diag, ev_solve)
+                            with trace_block("potrf::diag_first"):
+                                if q > 1:
+                                    Pt = ops.colmajor_empty(kb1, kb, dtype, dev)
+                                    if own_col:
+                                        Pt.copy_(buf[lr1:lr1 + kb1, lcg:lcg + kb])
+                                    grid.row_comm.bcast(Pt, g % q)
+                                else:
+                                    Pt = buf[lr1:lr1 + kb1, lcg:lcg + kb]
+                                if pc == g1 % q:
+                                    D1 = buf[lr1:lr1 + kb1, lc1:lc1 + kb1]
+                                    ops.gemm(-1.0, Pt, Pt, 1.0, D1, 'N', ct, (1, 1 << 40, 1, 0, 1, 0, 0, 0, 0))
+                                    ops.potrf('L', D1, infos[t + 1:t + 2])
+                                    ev_diag[t + 1] = ss.event(ss.diag)
                 # panel -> row
                 nrow = lr_end - lr1
                 if q > 1:
@@ -154,8 +186,18 @@ def _potrf_lower(A, opts):
             if t >= 1 and la > 0:
                 ss.wait(ss.panel, ev_tr[t - 1])
             if lc_la > lc1 and nrow:
-                mask = (1, nb, p, pr, q, pc, lr1, lc1, 0)
-                ops.gemm(-1.0, Prow, Lla[0:lc_la - lc1], 1.0, buf[lr1:lr_end, lc1:lc_la], 'N', ct, mask)
+                if kb1 and t + 1 in ev_diag and pr == (g + 1) % p and pc == (g + 1) % q:
+                    # the diagonal tile of g+1 is already updated and factored:
+                    # its column below it, then the other lookahead columns
+                    if nrow > kb1:
+                        ops.gemm(-1.0, Prow[kb1:], Lla[0:kb1], 1.0, buf[lr1 + kb1:lr_end, lc1:lc1 + kb1], 'N', ct,
+                                 (1, nb, p, pr, q, pc, lr1 + kb1, lc1, 0))
+                    if lc_la > lc1 + kb1:
+                        ops.gemm(-1.0, Prow, Lla[kb1:lc_la - lc1], 1.0, buf[lr1:lr_end, lc1 + kb1:lc_la], 'N', ct,
+                                 (1, nb, p, pr, q, pc, lr1, lc1 + kb1, 0))
+                else:
+                    mask = (1, nb, p, pr, q, pc, lr1, lc1, 0)
+                    ops.gemm(-1.0, Prow, Lla[0:lc_la - lc1], 1.0, buf[lr1:lr_end, lc1:lc_la], 'N', ct, mask)
             ev_panel = ss.event(ss.panel)
         # trailing update
         us = ss.update[0]

@@ -46,14 +46,17 @@ class StreamSet:
         self.serial = os.environ.get("SLATE_AMD_SERIAL", "0") == "1"
         if self.gpu and self.serial:
             cur = torch.cuda.current_stream(device)
-            self.panel = cur
+            self.panel = self.diag = cur
             self.update = [cur] * n_update
         elif self.gpu:
-            # torch: lower number = higher priority
+            # torch: lower number = higher priority; ``diag`` carries the
+            # next step's diagonal-tile chain concurrently with the panel's
+            # broadcasts (potrf diag-first)
             self.panel = torch.cuda.Stream(device=device, priority=-1)
+            self.diag = torch.cuda.Stream(device=device, priority=-1)
             self.update = [self._update_stream(device, self.reserve_cus) for _ in range(n_update)]
         else:
-            self.panel = None
+            self.panel = self.diag = None
             self.update = [None] * n_update
 
     @staticmethod
@@ -108,6 +111,8 @@ class StreamSet:
             return
         ev = self.event()
         self.panel.wait_event(ev)
+        if self.diag is not self.panel:
+            self.diag.wait_event(ev)
         for u in self.update:
             u.wait_event(ev)
 
@@ -116,5 +121,5 @@ class StreamSet:
         if not self.gpu:
             return
         cur = torch.cuda.current_stream(self.device)
-        for s in [self.panel] + self.update:
+        for s in [self.panel, self.diag] + self.update:
             cur.wait_event(self.event(s))
