@@ -20,6 +20,9 @@
 // the left update one wave per column (lanes over rows: coalesced), the
 // right update one thread per row.  The matrix is a dense n x n
 // column-major copy holding both triangles (only the band is non-zero).
+#include <cstdlib>
+#include <cstring>
+
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -28,6 +31,7 @@ namespace slate_hip {
 namespace {
 constexpr int HT = 256;   // threads per workgroup
 constexpr int HMAXB = 128;
+constexpr i64 HLDS = 96 * 1024;   // bytes of the LDS staging buffer
 }
 
 template <typename T>
@@ -37,6 +41,8 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
              const i64* __restrict__ ntask, int* ticket, int* done, i64 nsw, int D) {
     using R = typename scalar_traits<T>::real;
     __shared__ T v[HMAXB];
+    extern __shared__ unsigned char hb_smem[];
+    T* L = reinterpret_cast<T*>(hb_smem);           // staging buffer, HLDS bytes
     __shared__ T s_tau;
     __shared__ R s_beta;
     __shared__ int s_j;
@@ -53,9 +59,12 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
         for (i64 t = 0; t < nt; ++t) {
             if (j > 0) {
                 const i64 need = min(t + (i64)D, ntask[j - 1]);
+                // poll with relaxed loads (an acquire per poll would invalidate
+                // the XCD's L2 every time, thrashing the working sweeps), then
+                // ONE acquire fence
                 if (tid == 0)
-                    while (__hip_atomic_load(&done[j - 1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < need)
-                        __builtin_amdgcn_s_sleep(1);
+                    while (__hip_atomic_load(&done[j - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need)
+                        __builtin_amdgcn_s_sleep(2);
                 __syncthreads();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // every wave sees the producer's writes
             }
@@ -101,21 +110,54 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
             const T tau = s_tau;
             const i64 lo = col + 1, hi = min(n - 1, e + (i64)b);
             if (!s_is_zero(tau)) {
-                // ---- left: A(s..e, c) -= v (conj(tau) v^H A(s..e, c)), c in [lo, hi]; a wave per column
+                // ---- left: A(s..e, c) -= v (conj(tau) v^H A(s..e, c)), c in [lo, hi].
+                // Column chunks staged in LDS (one bulk coalesced load: every
+                // load in flight at once), a wave per column, bulk store.
                 const T ct = s_conj(tau);
-                for (i64 c = lo + w; c <= hi; c += HT / 64) {
-                    T acc = s_zero(T());
-                    for (int r = lane; r < k; r += 64) acc = s_add(acc, s_mul(s_conj(v[r]), At(s + r, c)));
-                    acc = s_mul(ct, wave_sum(acc));
-                    for (int r = lane; r < k; r += 64) At(s + r, c) = s_sub(At(s + r, c), s_mul(v[r], acc));
+                const i64 cw = max<i64>(1, min<i64>(hi - lo + 1, HLDS / ((i64)k * (i64)sizeof(T))));
+                for (i64 c0 = lo; c0 <= hi; c0 += cw) {
+                    const int nc = (int)min<i64>(cw, hi - c0 + 1);
+                    for (int idx = tid; idx < k * nc; idx += HT) {
+                        const int r = idx % k, c = idx / k;
+                        L[idx] = At(s + r, c0 + c);
+                    }
+                    __syncthreads();
+                    for (int c = w; c < nc; c += HT / 64) {
+                        T acc = s_zero(T());
+                        for (int r = lane; r < k; r += 64) acc = s_add(acc, s_mul(s_conj(v[r]), L[c * k + r]));
+                        acc = s_mul(ct, wave_sum(acc));
+                        for (int r = lane; r < k; r += 64) L[c * k + r] = s_sub(L[c * k + r], s_mul(v[r], acc));
+                    }
+                    __syncthreads();
+                    for (int idx = tid; idx < k * nc; idx += HT) {
+                        const int r = idx % k, c = idx / k;
+                        At(s + r, c0 + c) = L[idx];
+                    }
+                    __syncthreads();
                 }
-                __syncthreads();
-                // ---- right: A(r, s..e) -= (tau A(r, s..e) v) v^H, r in [lo, hi]; a thread per row
-                for (i64 r = lo + tid; r <= hi; r += HT) {
-                    T y = s_zero(T());
-                    for (int c = 0; c < k; ++c) y = s_add(y, s_mul(At(r, s + c), v[c]));
-                    y = s_mul(y, tau);
-                    for (int c = 0; c < k; ++c) At(r, s + c) = s_sub(At(r, s + c), s_mul(y, s_conj(v[c])));
+                // ---- right: A(r, s..e) -= (tau A(r, s..e) v) v^H, r in [lo, hi]:
+                // row chunks staged in LDS ([c][r]: a thread per row reads
+                // consecutive banks)
+                const i64 rw = max<i64>(1, min<i64>(hi - lo + 1, min<i64>(HT, HLDS / ((i64)k * (i64)sizeof(T)))));
+                for (i64 r0 = lo; r0 <= hi; r0 += rw) {
+                    const int nr = (int)min<i64>(rw, hi - r0 + 1);
+                    for (int idx = tid; idx < k * nr; idx += HT) {
+                        const int r = idx % nr, c = idx / nr;
+                        L[idx] = At(r0 + r, s + c);
+                    }
+                    __syncthreads();
+                    if (tid < nr) {
+                        T y = s_zero(T());
+                        for (int c = 0; c < k; ++c) y = s_add(y, s_mul(L[c * nr + tid], v[c]));
+                        y = s_mul(y, tau);
+                        for (int c = 0; c < k; ++c) L[c * nr + tid] = s_sub(L[c * nr + tid], s_mul(y, s_conj(v[c])));
+                    }
+                    __syncthreads();
+                    for (int idx = tid; idx < k * nr; idx += HT) {
+                        const int r = idx % nr, c = idx / nr;
+                        At(r0 + r, s + c) = L[idx];
+                    }
+                    __syncthreads();
                 }
             }
             __syncthreads();
@@ -129,9 +171,8 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
             }
             for (int r = tid; r < b; r += HT) V[slot * b + r] = (r < k) ? v[r] : s_zero(T());
             if (tid == 0) { tauv[slot] = tau; rowv[slot] = s; lenv[slot] = k; }
-            __threadfence();                                    // this wave's writes visible device-wide
-            __syncthreads();
-            if (tid == 0)
+            __syncthreads();                                    // all waves' stores issued and complete
+            if (tid == 0)                                        // one release: writes back this XCD's L2
                 __hip_atomic_store(&done[j], (int)(t + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             col = s;
         }
@@ -144,9 +185,36 @@ void hb2st_device(i64 n, int b, T* A, i64 lda, T* V, T* tau, i64* row, i64* len,
     if (nsw <= 0) return;
     if (b > HMAXB) throw std::invalid_argument("hb2st_device: bandwidth > 128");
     // work = [ticket, done[0..nsw)] zero-initialised by the caller
-    hipLaunchKernelGGL(hb2st_kernel<T>, dim3((unsigned)nwg), dim3(HT), 0, s, n, b, A, lda, V, tau, row, len,
+    static bool attr = false;
+    if (!attr) {
+        HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&hb2st_kernel<T>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)HLDS));
+        attr = true;
+    }
+    // The chase hands windows between workgroups on different XCDs: with
+    // the default (L2-cached, non-coherent across XCDs) memory every hand-off
+    // writes back and invalidates a whole L2.  SLATE_AMD_HB2ST_MEM=uncached
+    // (default) or finegrained runs on a coherent working copy instead.
+    static const int mode = [] {
+        const char* e = getenv("SLATE_AMD_HB2ST_MEM");
+        if (!e || !strcmp(e, "uncached")) return 2;
+        return strcmp(e, "finegrained") == 0 ? 1 : 0;
+    }();
+    T* W = A;
+    const size_t bytes = sizeof(T) * (size_t)lda * (size_t)n;
+    if (mode) {
+        HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&W), bytes,
+                                        mode == 2 ? hipDeviceMallocUncached : hipDeviceMallocFinegrained));
+        HIP_CHECK(hipMemcpyAsync(W, A, bytes, hipMemcpyDeviceToDevice, s));
+    }
+    hipLaunchKernelGGL(hb2st_kernel<T>, dim3((unsigned)nwg), dim3(HT), HLDS, s, n, b, W, lda, V, tau, row, len,
                        sweep_ptr, ntask, work, work + 1, nsw, 4);
     HIP_LAUNCH_CHECK();
+    if (mode) {
+        HIP_CHECK(hipMemcpyAsync(A, W, bytes, hipMemcpyDeviceToDevice, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        HIP_CHECK(hipFree(W));
+    }
 }
 
 #define INST(T) \

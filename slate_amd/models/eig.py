@@ -150,6 +150,7 @@ def _hb2st_device(B: torch.Tensor, nb: int, dev):
     """Bulge chasing on the GPU (csrc/hip/hb2st.hip): persistent
     workgroups, one per concurrently chased sweep, ordered by an atomic
     ticket, progress counters between consecutive sweeps."""
+    import os
     from .. import _native
     n = B.shape[0]
     b = max(1, nb)
@@ -166,7 +167,11 @@ def _hb2st_device(B: torch.Tensor, nb: int, dev):
     work = torch.zeros(nsw + 2, dtype=torch.int32, device=dev)
     ntd, spd = nt.to(dev), sp.to(dev)
     props = torch.cuda.get_device_properties(dev)
-    nwg = int(min(max(nsw, 1), 2 * props.multi_processor_count))
+    # sweeps in flight are bounded by (tasks of a sweep) / lag: more
+    # workgroups would only poll
+    nt0 = int(nt[0]) if nt.numel() else 1
+    nwg = int(min(max(nsw, 1), props.multi_processor_count, max(8, nt0 // 4 + 8)))
+    nwg = int(os.environ.get("SLATE_AMD_HB2ST_WG", nwg))
     with trace_block("hb2st"):
         if nsw > 0:
             _native._hip.hb2st(_code(dt), n, b, A.data_ptr(), A.stride(1), V.data_ptr(), tau.data_ptr(),
