@@ -133,11 +133,13 @@ static void register_kernels(py::module& m) {
     });
     m.def("hb2st", [](char dt, i64 n, int b, uintptr_t A, i64 lda, uintptr_t V, uintptr_t tau, uintptr_t row,
                       uintptr_t len, uintptr_t sweep_ptr, uintptr_t ntask, uintptr_t work, i64 nsw, int nwg,
-                      uintptr_t st) {
+                      uintptr_t st, uintptr_t prof) {
         dispatch(dt, [&](auto z) { using T = decltype(z);
             hb2st_device<T>(n, b, P<T>(A), lda, P<T>(V), P<T>(tau), P<i64>(row), P<i64>(len), P<const i64>(sweep_ptr),
-                            P<const i64>(ntask), P<int>(work), nsw, nwg, S(st)); });
-    });
+                            P<const i64>(ntask), P<int>(work), nsw, nwg, S(st), P<i64>(prof)); });
+    }, py::arg("dt"), py::arg("n"), py::arg("b"), py::arg("A"), py::arg("lda"), py::arg("V"), py::arg("tau"),
+       py::arg("row"), py::arg("len"), py::arg("sweep_ptr"), py::arg("ntask"), py::arg("work"), py::arg("nsw"),
+       py::arg("nwg"), py::arg("st"), py::arg("prof") = 0);
     m.def("apply_refl", [](char dt, i64 ncols, uintptr_t Z, i64 ldz, uintptr_t V, i64 b, uintptr_t tau,
                            uintptr_t row, uintptr_t len, i64 first, i64 count, bool conj_tau, uintptr_t st) {
         dispatch(dt, [&](auto z) { using T = decltype(z);

@@ -34,11 +34,47 @@ constexpr int HMAXB = 128;
 constexpr i64 HLDS = 96 * 1024;   // bytes of the LDS staging buffer
 }
 
+// 2-D block moves between global memory and LDS: lanes run along the rows
+// (coalesced), waves along the columns; the (row group, column) pair index
+// is wave-uniform, so the index arithmetic stays on the scalar unit, and U
+// global loads are in flight before the LDS writes (a plain loop waits for
+// each load in turn: the window then streams at a few GB/s).
+template <int U, typename F>
+__device__ inline void for_pairs(int nrow, int ncol, int lane, int w, F&& body) {
+    const int npr = (nrow + 63) >> 6;                     // row groups of 64
+    const int ncw = (ncol - w + 3) >> 2;                   // this wave's columns
+    const int tot = ncw * npr;
+    for (int base = 0; base < tot; base += U) body(base, npr, min(U, tot - base));
+    (void)lane;
+}
+
+template <typename T, typename Src, typename Dst>
+__device__ inline void move2d(int nrow, int ncol, int lane, int w, Src src, Dst dst) {
+    constexpr int U = 12;
+    for_pairs<U>(nrow, ncol, lane, w, [&](int base, int npr, int cnt) {
+        T tmp[U];
+        #pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (u < cnt) {
+                const int p = base + u, c = w + 4 * (p / npr), r = lane + 64 * (p % npr);
+                if (r < nrow) tmp[u] = src(r, c);
+            }
+        }
+        #pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (u < cnt) {
+                const int p = base + u, c = w + 4 * (p / npr), r = lane + 64 * (p % npr);
+                if (r < nrow) dst(r, c) = tmp[u];
+            }
+        }
+    });
+}
+
 template <typename T>
 __global__ void __launch_bounds__(HT)
 hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __restrict__ tauv,
              i64* __restrict__ rowv, i64* __restrict__ lenv, const i64* __restrict__ sweep_ptr,
-             const i64* __restrict__ ntask, int* ticket, int* done, i64 nsw, int D) {
+             const i64* __restrict__ ntask, int* ticket, int* done, i64 nsw, int D, i64* prof) {
     using R = typename scalar_traits<T>::real;
     __shared__ T v[HMAXB];
     extern __shared__ unsigned char hb_smem[];
@@ -48,12 +84,21 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
     __shared__ int s_j;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     auto At = [&](i64 r, i64 c) -> T& { return A[r + c * lda]; };
+    // optional per-phase shader-clock totals (prof != nullptr: tools only)
+    i64 ph[5] = {0, 0, 0, 0, 0};
+    i64 tl = clock64();
+#define HSTAMP(i) do { if (prof && tid == 0) { const i64 t_ = clock64(); ph[i] += t_ - tl; tl = t_; } } while (0)
     for (;;) {
         if (tid == 0) s_j = atomicAdd(ticket, 1);
         __syncthreads();
         const i64 j = s_j;
         __syncthreads();
-        if (j >= nsw) return;
+        if (j >= nsw) {
+            if (prof && tid == 0)
+                for (int i = 0; i < 5; ++i) atomicAdd(reinterpret_cast<unsigned long long*>(prof + i),
+                                                      (unsigned long long)ph[i]);
+            return;
+        }
         const i64 nt = ntask[j];
         i64 s = j + 1, e = min(j + (i64)b, n - 1), col = j;
         for (i64 t = 0; t < nt; ++t) {
@@ -68,6 +113,7 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
                 __syncthreads();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // every wave sees the producer's writes
             }
+            HSTAMP(0);
             if (t > 0) { s = e + 1; e = min(e + (i64)b, n - 1); }
             const int k = (int)(e - s + 1);
             // ---- reflector (wave 0): x = A(s..e, col)
@@ -107,6 +153,7 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
                 if (lane == 0) { s_tau = tau; s_beta = beta; }
             }
             __syncthreads();
+            HSTAMP(1);
             const T tau = s_tau;
             const i64 lo = col + 1, hi = min(n - 1, e + (i64)b);
             if (!s_is_zero(tau)) {
@@ -114,53 +161,88 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
                 // Column chunks staged in LDS (one bulk coalesced load: every
                 // load in flight at once), a wave per column, bulk store.
                 const T ct = s_conj(tau);
-                const i64 cw = max<i64>(1, min<i64>(hi - lo + 1, HLDS / ((i64)k * (i64)sizeof(T))));
+                // thread per column over LDS columns padded to k + 1 (no
+                // per-column wave reductions: a shuffle tree per column is a
+                // chain of LDS-crossbar round trips)
+                const int KP = k + 1;
+                const i64 cw = max<i64>(1, min<i64>(min<i64>(hi - lo + 1, HT),
+                                                   HLDS / ((i64)KP * (i64)sizeof(T))));
                 for (i64 c0 = lo; c0 <= hi; c0 += cw) {
                     const int nc = (int)min<i64>(cw, hi - c0 + 1);
-                    for (int idx = tid; idx < k * nc; idx += HT) {
-                        const int r = idx % k, c = idx / k;
-                        L[idx] = At(s + r, c0 + c);
-                    }
+                    T* Ab = &At(s, c0);
+                    move2d<T>(k, nc, lane, w, [&](int r, int c) -> T { return Ab[r + c * lda]; },
+                              [&](int r, int c) -> T& { return L[c * KP + r]; });
                     __syncthreads();
-                    for (int c = w; c < nc; c += HT / 64) {
+                    if (tid < nc) {
+                        // unrolled by 8 with independent partial sums: the LDS
+                        // reads of a group are in flight together
+                        T* Lc = L + tid * KP;
+                        T part[8];
+                        #pragma unroll
+                        for (int u = 0; u < 8; ++u) part[u] = s_zero(T());
+                        int r = 0;
+                        for (; r + 8 <= k; r += 8) {
+                            #pragma unroll
+                            for (int u = 0; u < 8; ++u) part[u] = s_add(part[u], s_mul(s_conj(v[r + u]), Lc[r + u]));
+                        }
+                        for (; r < k; ++r) part[0] = s_add(part[0], s_mul(s_conj(v[r]), Lc[r]));
                         T acc = s_zero(T());
-                        for (int r = lane; r < k; r += 64) acc = s_add(acc, s_mul(s_conj(v[r]), L[c * k + r]));
-                        acc = s_mul(ct, wave_sum(acc));
-                        for (int r = lane; r < k; r += 64) L[c * k + r] = s_sub(L[c * k + r], s_mul(v[r], acc));
+                        #pragma unroll
+                        for (int u = 0; u < 8; ++u) acc = s_add(acc, part[u]);
+                        acc = s_mul(ct, acc);
+                        r = 0;
+                        for (; r + 8 <= k; r += 8) {
+                            #pragma unroll
+                            for (int u = 0; u < 8; ++u) Lc[r + u] = s_sub(Lc[r + u], s_mul(v[r + u], acc));
+                        }
+                        for (; r < k; ++r) Lc[r] = s_sub(Lc[r], s_mul(v[r], acc));
                     }
                     __syncthreads();
-                    for (int idx = tid; idx < k * nc; idx += HT) {
-                        const int r = idx % k, c = idx / k;
-                        At(s + r, c0 + c) = L[idx];
-                    }
+                    move2d<T>(k, nc, lane, w, [&](int r, int c) -> T { return L[c * KP + r]; },
+                              [&](int r, int c) -> T& { return Ab[r + c * lda]; });
                     __syncthreads();
                 }
+                HSTAMP(2);
                 // ---- right: A(r, s..e) -= (tau A(r, s..e) v) v^H, r in [lo, hi]:
                 // row chunks staged in LDS ([c][r]: a thread per row reads
                 // consecutive banks)
                 const i64 rw = max<i64>(1, min<i64>(hi - lo + 1, min<i64>(HT, HLDS / ((i64)k * (i64)sizeof(T)))));
                 for (i64 r0 = lo; r0 <= hi; r0 += rw) {
                     const int nr = (int)min<i64>(rw, hi - r0 + 1);
-                    for (int idx = tid; idx < k * nr; idx += HT) {
-                        const int r = idx % nr, c = idx / nr;
-                        L[idx] = At(r0 + r, s + c);
-                    }
+                    T* Ab = &At(r0, s);
+                    move2d<T>(nr, k, lane, w, [&](int r, int c) -> T { return Ab[r + c * lda]; },
+                              [&](int r, int c) -> T& { return L[c * nr + r]; });
                     __syncthreads();
                     if (tid < nr) {
+                        T part[8];
+                        #pragma unroll
+                        for (int u = 0; u < 8; ++u) part[u] = s_zero(T());
+                        int c = 0;
+                        for (; c + 8 <= k; c += 8) {
+                            #pragma unroll
+                            for (int u = 0; u < 8; ++u) part[u] = s_add(part[u], s_mul(L[(c + u) * nr + tid], v[c + u]));
+                        }
+                        for (; c < k; ++c) part[0] = s_add(part[0], s_mul(L[c * nr + tid], v[c]));
                         T y = s_zero(T());
-                        for (int c = 0; c < k; ++c) y = s_add(y, s_mul(L[c * nr + tid], v[c]));
+                        #pragma unroll
+                        for (int u = 0; u < 8; ++u) y = s_add(y, part[u]);
                         y = s_mul(y, tau);
-                        for (int c = 0; c < k; ++c) L[c * nr + tid] = s_sub(L[c * nr + tid], s_mul(y, s_conj(v[c])));
+                        c = 0;
+                        for (; c + 8 <= k; c += 8) {
+                            #pragma unroll
+                            for (int u = 0; u < 8; ++u)
+                                L[(c + u) * nr + tid] = s_sub(L[(c + u) * nr + tid], s_mul(y, s_conj(v[c + u])));
+                        }
+                        for (; c < k; ++c) L[c * nr + tid] = s_sub(L[c * nr + tid], s_mul(y, s_conj(v[c])));
                     }
                     __syncthreads();
-                    for (int idx = tid; idx < k * nr; idx += HT) {
-                        const int r = idx % nr, c = idx / nr;
-                        At(r0 + r, s + c) = L[idx];
-                    }
+                    move2d<T>(nr, k, lane, w, [&](int r, int c) -> T { return L[c * nr + r]; },
+                              [&](int r, int c) -> T& { return Ab[r + c * lda]; });
                     __syncthreads();
                 }
             }
             __syncthreads();
+            HSTAMP(3);
             // ---- annihilated column / row, reflector slot
             const R beta = s_beta;
             const i64 slot = sweep_ptr[j] + t;
@@ -174,6 +256,7 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
             __syncthreads();                                    // all waves' stores issued and complete
             if (tid == 0)                                        // one release: writes back this XCD's L2
                 __hip_atomic_store(&done[j], (int)(t + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            HSTAMP(4);
             col = s;
         }
     }
@@ -181,7 +264,7 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
 
 template <typename T>
 void hb2st_device(i64 n, int b, T* A, i64 lda, T* V, T* tau, i64* row, i64* len, const i64* sweep_ptr,
-                  const i64* ntask, int* work, i64 nsw, int nwg, hipStream_t s) {
+                  const i64* ntask, int* work, i64 nsw, int nwg, hipStream_t s, i64* prof) {
     if (nsw <= 0) return;
     if (b > HMAXB) throw std::invalid_argument("hb2st_device: bandwidth > 128");
     // work = [ticket, done[0..nsw)] zero-initialised by the caller
@@ -208,7 +291,7 @@ void hb2st_device(i64 n, int b, T* A, i64 lda, T* V, T* tau, i64* row, i64* len,
         HIP_CHECK(hipMemcpyAsync(W, A, bytes, hipMemcpyDeviceToDevice, s));
     }
     hipLaunchKernelGGL(hb2st_kernel<T>, dim3((unsigned)nwg), dim3(HT), HLDS, s, n, b, W, lda, V, tau, row, len,
-                       sweep_ptr, ntask, work, work + 1, nsw, 4);
+                       sweep_ptr, ntask, work, work + 1, nsw, 4, prof);
     HIP_LAUNCH_CHECK();
     if (mode) {
         HIP_CHECK(hipMemcpyAsync(A, W, bytes, hipMemcpyDeviceToDevice, s));
@@ -219,7 +302,7 @@ void hb2st_device(i64 n, int b, T* A, i64 lda, T* V, T* tau, i64* row, i64* len,
 
 #define INST(T) \
     template void hb2st_device<T>(i64, int, T*, i64, T*, T*, i64*, i64*, const i64*, const i64*, int*, i64, int, \
-                                  hipStream_t);
+                                  hipStream_t, i64*);
 INST(float) INST(double) INST(ccplx) INST(zcplx)
 #undef INST
 

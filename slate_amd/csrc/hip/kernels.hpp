@@ -79,7 +79,7 @@ void geqrf_panel_ws(i64 m, i64 n, T* A, i64 lda, T* tau, T* Tm, i64 ldt, T* V, i
 size_t geqrf_work_bytes();
 template <typename T>
 void hb2st_device(i64 n, int b, T* A, i64 lda, T* V, T* tau, i64* row, i64* len, const i64* sweep_ptr,
-                  const i64* ntask, int* work, i64 nsw, int nwg, hipStream_t s);
+                  const i64* ntask, int* work, i64 nsw, int nwg, hipStream_t s, i64* prof = nullptr);
 template <typename T>
 void apply_refl_batch(i64 ncols, T* Z, i64 ldz, const T* V, i64 b, const T* tau, const i64* row, const i64* len,
                       i64 first, i64 count, bool conj_tau, hipStream_t s);

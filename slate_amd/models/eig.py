@@ -146,6 +146,9 @@ def _hb2st_schedule(n, b):
     return nt, sp
 
 
+_HB2ST_PROF = {}     # tools: {"buf": int64 device tensor(5)} -> per-phase clock totals
+
+
 def _hb2st_device(B: torch.Tensor, nb: int, dev):
     """Bulge chasing on the GPU (csrc/hip/hb2st.hip): persistent
     workgroups, one per concurrently chased sweep, ordered by an atomic
@@ -155,7 +158,11 @@ def _hb2st_device(B: torch.Tensor, nb: int, dev):
     n = B.shape[0]
     b = max(1, nb)
     dt = B.dtype
-    A = ops.colmajor_empty(n, n, dt, dev)
+    # leading dimension off powers of two: the chase touches ~3b columns of
+    # one row band at a time, which a 2^k stride would put on one memory
+    # channel
+    ldp = -(-n // 8) * 8 + 72
+    A = torch.empty((n, ldp), dtype=dt, device=dev).t()[:n]
     A.copy_(B.to(dev))
     nt, sp = _hb2st_schedule(n, b)
     total = int(nt.sum()) if nt.numel() else 0
@@ -174,9 +181,11 @@ def _hb2st_device(B: torch.Tensor, nb: int, dev):
     nwg = int(os.environ.get("SLATE_AMD_HB2ST_WG", nwg))
     with trace_block("hb2st"):
         if nsw > 0:
+            prof = _HB2ST_PROF.get("buf")
             _native._hip.hb2st(_code(dt), n, b, A.data_ptr(), A.stride(1), V.data_ptr(), tau.data_ptr(),
                                row.data_ptr(), ln.data_ptr(), spd.data_ptr(), ntd.data_ptr(), work.data_ptr(),
-                               nsw, nwg, torch.cuda.current_stream(dev).cuda_stream)
+                               nsw, nwg, torch.cuda.current_stream(dev).cuda_stream,
+                               prof.data_ptr() if prof is not None else 0)
     Bh = A
     return Bh, V[:total], tau[:total], row[:total], ln[:total], sp, total
 

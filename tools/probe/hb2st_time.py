@@ -26,6 +26,14 @@ for wg in wgs:
     d, e, F = E.hb2st(H, b, device=dev)
     torch.cuda.synchronize()
     print(f"device n={n} b={b} wg={wg or 'auto'}: {time.perf_counter() - t0:.3f} s", flush=True)
+# per-phase clock totals (wait, reflector, left, right, finish) of one run
+E._HB2ST_PROF["buf"] = torch.zeros(5, dtype=torch.int64, device=dev)
+E.hb2st(H, b, device=dev)
+torch.cuda.synchronize()
+pv = E._HB2ST_PROF.pop("buf").cpu().tolist()
+tot = max(sum(pv), 1)
+print("phases (wait, reflector, left, right, finish):", ", ".join(f"{100 * x / tot:.1f}%" for x in pv),
+      f"total {tot:.3e} cycles", flush=True)
 os.environ["SLATE_AMD_HB2ST"] = "host"
 t0 = time.perf_counter()
 d2, e2, F2 = E.hb2st(H, b, device=dev)
