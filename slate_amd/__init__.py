@@ -31,6 +31,7 @@ from .parallel.comm import Comm, ProcessGrid, finalize, init, world  # noqa: F40
 from .utils.matgen import MatgenParams, generate_matrix  # noqa: F401
 from .utils.trace import Trace, trace_block  # noqa: F401
 from .utils.timers import timers, timer  # noqa: F401
+from .utils.watchdog import Watchdog  # noqa: F401
 
 from .models.blas3 import (  # noqa: F401
     gemm, hemm, her2k, herk, multiply, rank_2k_update, rank_k_update, symm, syr2k, syrk,

@@ -20,7 +20,10 @@ MI355X-first layout decisions
   of SLATE's per-tile batched-BLAS device regions.
 * Other distributions (lambdas, non-uniform tiles, band storage) keep
   per-tile tensors; workspace (received remote tiles) comes from a
-  per-storage slab pool (:class:`_host.SlabPool` bookkeeping).
+  per-storage slab pool: on the GPU the native stream-ordered
+  :class:`_hip.DevicePool` (hipMalloc'd chunks under an HBM cap, event-
+  ordered frees, csrc/hip/devpool.hip); on the host :class:`_host.SlabPool`
+  bookkeeping over torch chunks.
 """
 from __future__ import annotations
 
@@ -222,11 +225,28 @@ class MatrixStorage:
             nb = max((self.tileNb(j) for j in range(self.nt)), default=1)
             elems = max(1, mb * nb)
             per_chunk = max(1, min(256, (1 << 28) // (elems * self._itemsize())))
-            p = _host.SlabPool(elems * self._itemsize(), per_chunk)
+            dev = self.device_of(slot)
+            if dev.type == "cuda":
+                import os
+                cap = int(float(os.environ.get("SLATE_AMD_POOL_GIB", "0")) * (1 << 30))
+                p = _native.hip().DevicePool(dev.index if dev.index is not None else torch.cuda.current_device(),
+                                             elems * self._itemsize(), per_chunk, cap)
+            else:
+                p = _host.SlabPool(elems * self._itemsize(), per_chunk)
             self.pools[slot] = p
             self.pool_chunks[slot] = []
             self._pool_geom = (mb, nb)
         return p
+
+    def pool_stats(self, slot=DEV) -> dict:
+        """Occupancy of a slot's workspace pool (empty dict if none yet)."""
+        p = self.pools.get(slot)
+        if p is None:
+            return {}
+        if hasattr(p, "stats"):
+            return dict(p.stats())
+        return {"in_use": p.in_use(), "peak": p.peak(), "chunks": p.chunks(),
+                "capacity": p.capacity(), "block_bytes": p.block_bytes()}
 
     def _itemsize(self):
         return torch.empty((), dtype=self.dtype).element_size()
@@ -235,21 +255,37 @@ class MatrixStorage:
         mb, nb = self.tileMb(i), self.tileNb(j)
         if kind == TileKind.Workspace:
             pool = self._pool(slot)
-            chunk, idx, grew = pool.alloc()
             chunks = self.pool_chunks[slot]
-            if grew:
-                pmb, pnb = self._pool_geom
-                chunks.append(torch.empty((pool.blocks_per_chunk(), pmb * pnb), dtype=self.dtype,
-                                          device=self.device_of(slot)))
+            pmb, pnb = self._pool_geom
+            dev = self.device_of(slot)
+            if dev.type == "cuda":
+                # stream-ordered native pool: blocks of block_bytes (>= tile bytes,
+                # 256-byte aligned) inside hipMalloc'd chunks exported by DLPack
+                chunk, idx, off, grew = pool.alloc(torch.cuda.current_stream(dev).cuda_stream)
+                while len(chunks) <= chunk:
+                    raw = torch.utils.dlpack.from_dlpack(pool.chunk_view(len(chunks)))
+                    chunks.append(raw.view(self.dtype))
+                per = pool.block_bytes() // self._itemsize()
+                flat = chunks[chunk][idx * per: idx * per + mb * nb]
+            else:
+                chunk, idx, grew = pool.alloc()
+                if grew:
+                    chunks.append(torch.empty((pool.blocks_per_chunk(), pmb * pnb), dtype=self.dtype,
+                                              device=dev))
+                flat = chunks[chunk][idx, : mb * nb]
             self.pool_blocks[(i, j, slot)] = (chunk, idx)
-            flat = chunks[chunk][idx, : mb * nb]
             return flat.view(nb, mb).t() if mb > 0 and nb > 0 else flat.view(mb, nb)
         return torch.zeros((nb, max(mb, 1)), dtype=self.dtype, device=self.device_of(slot)).t()[:mb, :]
 
     def _free_tile(self, i, j, slot):
         blk = self.pool_blocks.pop((i, j, slot), None)
         if blk is not None:
-            self.pools[slot].free(*blk)
+            dev = self.device_of(slot)
+            if dev.type == "cuda":
+                # stream-ordered: reusable by this stream at once, by others after its event
+                self.pools[slot].free(*blk, torch.cuda.current_stream(dev).cuda_stream)
+            else:
+                self.pools[slot].free(*blk)
         self.tiles.pop((i, j, slot), None)
 
     def tileInsert(self, i, j, slot, data: Optional[torch.Tensor] = None, kind=TileKind.SlateOwned,

@@ -13,6 +13,8 @@
 namespace py = pybind11;
 using namespace slate_hip;
 
+void register_devpool(py::module& m);   // devpool.hip
+
 static inline hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 
 static TriMask make_mask(py::object m) {
@@ -258,6 +260,7 @@ PYBIND11_MODULE(_hip, m) {
     m.def("gemm", &py_gemm);
     m.def("gemm_ptrs", &py_gemm_ptrs);
     register_kernels(m);
+    register_devpool(m);
     // CU-masked streams: isolate latency-bound panel kernels from the bulk
     // trailing-update GEMM (hipExtStreamCreateWithCUMask).  Returns the raw
     // handle for torch.cuda.ExternalStream.

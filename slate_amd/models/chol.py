@@ -42,6 +42,7 @@ from ..parallel.streams import StreamSet
 from ..utils.trace import trace_block
 from ._panels import assemble_cols, plan_col_gathers_steps
 from ._util import conj_trans, grid_of, target_slot, tiles_local_before
+from ..utils import watchdog as _wd
 
 
 def _upper_to_lower(A, fn, opts):
@@ -109,6 +110,7 @@ def _potrf_lower(A, opts):
     ev_tr = {}
     ss.fork()
     for t in range(nt):
+        _wd.beat(f"potrf step {t}")
         g = g0 + t
         kb = s.tileMb(g) if t < nt - 1 or A.last_mb is None else A.last_mb
         lrg = tiles_local_before(g, p, pr) * nb
@@ -232,6 +234,7 @@ def _potrf_info(s, infos, g0, nt):
     iv = infos.cpu()
     info = 0
     for t in range(nt):
+        _wd.beat(f"potrf step {t}")
         if int(iv[t]) > 0:
             info = (s.row_offsets[g0 + t] - s.row_offsets[g0]) + int(iv[t])
             break
@@ -273,6 +276,7 @@ def _potrf_1x1_grouped(A, s, buf, nb, g0, nt, R_end, la, G, ss, infos, ct, dev):
     ev_tr = {}
     ss.fork()
     for gi, tiles in enumerate(groups):
+        _wd.beat(f"potrf group {gi}")
         c0, c2 = gstart(gi), gstart(gi + 1)
         with ss.use(ss.panel):
             if gi - la - 1 >= 0:

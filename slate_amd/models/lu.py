@@ -34,6 +34,7 @@ from ..core.storage import DEV, l2g, local_start
 from ..parallel.streams import StreamSet
 from ..utils.trace import trace_block
 from ._util import grid_of, target_slot, tiles_local_before
+from ..utils import watchdog as _wd
 
 
 def getrf(A, pivots: Pivots, opts=None) -> int:
@@ -116,6 +117,7 @@ def _getrf_p1(A, buf, thr, la, nopiv):
     ev_tr = {}
     ss.fork()
     for k in range(kt):
+        _wd.beat(f"getrf step {k}")
         r0 = k * nb
         kb = min(nb, n - r0, m - r0)
         mk = m - r0
@@ -201,6 +203,7 @@ def _reduce_info(A, infos, kt, nb):
     iv = infos[:kt].cpu()
     info = 0
     for k in range(kt):
+        _wd.beat(f"getrf step {k}")
         if int(iv[k]) > 0:
             info = k * nb + int(iv[k])
             break
@@ -301,6 +304,7 @@ def _getrf_general(A, buf, thr, la, mode, leaf):
     import os
     kstop = int(os.environ.get("SLATE_AMD_DEBUG_LU_STEPS", kt))    # debugging: stop after k steps
     for k in range(min(kt, kstop)):
+        _wd.beat(f"getrf step {k}")
         r0 = k * nb
         kb = min(nb, n - r0, m - r0)
         rk, ck = k % p, k % q

@@ -47,6 +47,7 @@ from ..core.storage import l2g
 from ..parallel.streams import StreamSet
 from ..utils.trace import trace_block
 from ._util import conj_trans, grid_of, target_slot, tiles_local_before
+from ..utils import watchdog as _wd
 
 
 # ------------------------------------------------------------------ helpers
@@ -107,6 +108,7 @@ def _geqrf_p1(A, buf, T, la):
     ev_tr = {}
     ss.fork()
     for k in range(kt):
+        _wd.beat(f"geqrf step {k}")
         r0 = k * nb
         kb = min(nb, n - r0, m - r0)
         mk = m - r0
@@ -178,6 +180,7 @@ def _geqrf_general(A, buf, T, la):
     ev_tr = {}
     ss.fork()
     for k in range(kt):
+        _wd.beat(f"geqrf step {k}")
         r0 = k * nb
         kb = min(nb, n - r0, m - r0)
         rk, ck = k % p, k % q

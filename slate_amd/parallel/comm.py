@@ -32,6 +32,7 @@ import torch
 import torch.distributed as dist
 
 from ..core.exceptions import CommError
+from ..utils import watchdog as _wd
 
 
 def _dist_ready() -> bool:
@@ -95,6 +96,7 @@ class Comm:
 
     # -- collectives -----------------------------------------------------
     def barrier(self):
+        _wd.beat("comm.barrier")
         if self.size > 1:
             if self.backend == "nccl":
                 # device-side barrier: tiny allreduce on the current stream
@@ -105,6 +107,7 @@ class Comm:
 
     def bcast(self, t: torch.Tensor, root: int, async_op=False):
         """Broadcast t from comm-rank root (in place)."""
+        _wd.beat("comm.bcast")
         if self.size == 1:
             return None
         try:
@@ -125,6 +128,7 @@ class Comm:
             raise CommError(f"bcast failed: {e}") from e
 
     def allreduce(self, t: torch.Tensor, op: str = "sum"):
+        _wd.beat("comm.allreduce")
         if self.size == 1:
             return t
         rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
@@ -171,6 +175,7 @@ class Comm:
 
     def allgather(self, t: torch.Tensor) -> torch.Tensor:
         """Concatenate equal-size tensors from all ranks along a new dim 0."""
+        _wd.beat("comm.allgather")
         if self.size == 1:
             return t.unsqueeze(0)
         x, _ = self._prep(t.contiguous())
@@ -187,6 +192,7 @@ class Comm:
 
     def allgatherv(self, t: torch.Tensor) -> list:
         """All-gather of variable-length 1-D tensors (SLATE stedc Allgatherv)."""
+        _wd.beat("comm.allgatherv")
         if self.size == 1:
             return [t]
         x, _ = self._prep(t.contiguous().reshape(-1))
@@ -199,6 +205,7 @@ class Comm:
         return [allb[r, : ns[r]].to(t.device) for r in range(self.size)]
 
     def reduce(self, t: torch.Tensor, root: int, op="sum"):
+        _wd.beat("comm.reduce")
         if self.size == 1:
             return t
         x, staged = self._prep(t.contiguous())
@@ -209,6 +216,7 @@ class Comm:
         return t
 
     def send(self, t: torch.Tensor, dst: int, tag: int = 0):
+        _wd.beat("comm.send")
         if self.size == 1:
             return
         x, _ = self._prep(t.contiguous())
@@ -216,6 +224,7 @@ class Comm:
             dist.send(x, dst=self._g(dst), group=self.group)
 
     def recv(self, t: torch.Tensor, src: int, tag: int = 0):
+        _wd.beat("comm.recv")
         if self.size == 1:
             return t
         x, _ = self._prep(t if t.is_contiguous() else t.contiguous())
@@ -229,6 +238,7 @@ class Comm:
 
     def sendrecv(self, send_t: torch.Tensor, dst: int, recv_t: torch.Tensor, src: int):
         """Simultaneous exchange (MPI_Sendrecv) via batched p2p."""
+        _wd.beat("comm.sendrecv")
         if self.size == 1:
             recv_t.copy_(send_t)
             return recv_t
@@ -243,6 +253,7 @@ class Comm:
 
     def exchange(self, sends: dict, recvs: dict):
         """Batched point-to-point: sends {dst: tensor}, recvs {src: tensor}."""
+        _wd.beat("comm.exchange")
         if self.size == 1 or (not sends and not recvs):
             return
         ops, fix = [], []
@@ -329,16 +340,21 @@ def init(backend: Optional[str] = None):
     if not _dist_ready() and int(os.environ.get("WORLD_SIZE", "1")) > 1:
         if backend is None:
             backend = os.environ.get("SLATE_AMD_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        # explicit collective timeout: RCCL's watchdog aborts a collective
+        # stuck past it (a dead or deadlocked peer) instead of hanging the job
+        from datetime import timedelta
+        tmo = timedelta(seconds=float(os.environ.get("SLATE_AMD_COMM_TIMEOUT", "600")))
         if backend == "nccl":
             lr = int(os.environ.get("LOCAL_RANK", "0"))
             torch.cuda.set_device(lr)
-            dist.init_process_group(backend, device_id=torch.device("cuda", lr))
+            dist.init_process_group(backend, device_id=torch.device("cuda", lr), timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
     elif torch.cuda.is_available() and "LOCAL_RANK" in os.environ:
         torch.cuda.set_device(int(os.environ["LOCAL_RANK"]))
     global _WORLD
     _WORLD = None
+    _wd.from_env()
     return world()
 
 

@@ -97,16 +97,16 @@ class Debug:
             raise SlateError(f"MOSI check failed{(' after ' + where) if where else ''}: " + "; ".join(bad[:8]))
 
     @staticmethod
-    def check_pool_leaks() -> dict:
-        """Bytes still allocated in the slab pools (should be 0 after all
-        matrices are freed)."""
-        from ..core import storage
+    def check_pool_leaks(*matrices) -> dict:
+        """Workspace blocks still handed out by the matrices' slab pools
+        (checkDeviceMemoryLeaks analog, src/core/Memory.cc:111): after a
+        driver released its workspace every count should be 0."""
         out = {}
-        for key, pool in getattr(storage, "_POOLS", {}).items():
-            try:
-                out[str(key)] = int(pool.allocated_bytes())
-            except Exception:  # noqa: BLE001
-                out[str(key)] = -1
+        for A in matrices:
+            st = A.storage
+            for slot in list(st.pools):
+                stats = st.pool_stats(slot)
+                out[(id(st), slot)] = int(stats.get("in_use", 0))
         return out
 
     @staticmethod
