@@ -119,6 +119,10 @@ static void register_kernels(py::module& m) {
         dispatch(dt, [&](auto z) { using T = decltype(z);
             trtri<T>(uplo, diag, n, P<T>(A), lda, P<i64>(info), S(st)); });
     });
+    m.def("stedc_secular", [](i64 n, uintptr_t d, uintptr_t z, double rho, double zz, uintptr_t org, uintptr_t mu,
+                              uintptr_t zh, uintptr_t V, i64 ldv, uintptr_t st) {
+        stedc_secular(n, P<double>(d), P<double>(z), rho, zz, P<i64>(org), P<double>(mu), P<double>(zh),
+                      P<double>(V), ldv, S(st)); });
     m.def("lu_persist_profile", [](int enable) {
         unsigned long long v[8];
         lu_persist_profile(enable, v);
@@ -142,6 +146,14 @@ static void register_kernels(py::module& m) {
     }, py::arg("dt"), py::arg("n"), py::arg("b"), py::arg("A"), py::arg("lda"), py::arg("V"), py::arg("tau"),
        py::arg("row"), py::arg("len"), py::arg("sweep_ptr"), py::arg("ntask"), py::arg("work"), py::arg("nsw"),
        py::arg("nwg"), py::arg("st"), py::arg("prof") = 0);
+    m.def("unmtr_hb2st_blocked", [](char dt, i64 n, i64 ncols, uintptr_t Z, i64 ldz, uintptr_t V, i64 b,
+                                    uintptr_t tau, uintptr_t sp, uintptr_t nt, i64 nsw, bool conj_tau, uintptr_t st) {
+        bool ok = false;
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            ok = unmtr_hb2st_blocked<T>(n, ncols, P<T>(Z), ldz, P<const T>(V), b, P<const T>(tau), P<const i64>(sp),
+                                        P<const i64>(nt), nsw, conj_tau, S(st)); });
+        return ok;
+    });
     m.def("apply_refl", [](char dt, i64 ncols, uintptr_t Z, i64 ldz, uintptr_t V, i64 b, uintptr_t tau,
                            uintptr_t row, uintptr_t len, i64 first, i64 count, bool conj_tau, uintptr_t st) {
         dispatch(dt, [&](auto z) { using T = decltype(z);

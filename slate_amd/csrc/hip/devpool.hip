@@ -19,6 +19,7 @@
 //    trim() only when no block of it is in use and no exported view of it is
 //    alive.
 #include <deque>
+#include <iterator>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -136,20 +137,27 @@ public:
         auto* s = st_.get();
         hipStream_t stream = reinterpret_cast<hipStream_t>(stream_u);
         std::lock_guard<std::mutex> g(s->mu);
-        // 1) a block last freed on this stream (or never used), 2) one whose
+        // 1) the block most recently freed on this stream (stream order makes
+        //    it safe; likely still in L2), 2) a never-used block, 3) one whose
         //    free event has completed
+        for (auto it = s->freelist.rbegin(); it != s->freelist.rend(); ++it) {
+            if (it->ev == nullptr || it->stream != stream) continue;
+            FreeBlock f = *it;
+            s->freelist.erase(std::next(it).base());
+            s->reuse_same++;
+            return hand_out(f, false);
+        }
         for (int pass = 0; pass < 2; ++pass) {
             for (auto it = s->freelist.begin(); it != s->freelist.end(); ++it) {
-                bool ok = pass == 0 ? (it->stream == stream || it->ev == nullptr)
-                                    : hipEventQuery(it->ev) == hipSuccess;
+                bool ok = pass == 0 ? it->ev == nullptr : hipEventQuery(it->ev) == hipSuccess;
                 if (!ok) continue;
                 FreeBlock f = *it;
                 s->freelist.erase(it);
-                (pass == 0 ? s->reuse_same : s->reuse_done)++;
+                if (pass == 1) s->reuse_done++;
                 return hand_out(f, false);
             }
         }
-        // 3) grow while under the HBM cap
+        // 4) grow while under the HBM cap
         size_t chunk_bytes = s->block_bytes * (size_t)s->blocks_per_chunk;
         const bool under_cap = (s->chunks.size() + 1) * chunk_bytes <= s->max_bytes;
         if (!under_cap && s->freelist.empty())
@@ -169,7 +177,7 @@ public:
                 s->freelist.push_back(FreeBlock{ci, i, nullptr, nullptr});
             return hand_out(FreeBlock{ci, 0, nullptr, nullptr}, true);
         }
-        // 4) at the cap: take the oldest pending block, ordered behind its
+        // 5) at the cap: take the oldest pending block, ordered behind its
         //    free on the device (no host wait)
         FreeBlock f = s->freelist.front();
         s->freelist.pop_front();

@@ -58,4 +58,151 @@ void apply_refl_batch(i64 ncols, T* Z, i64 ldz, const T* V, i64 b, const T* tau,
 INST(float) INST(double) INST(ccplx) INST(zcplx)
 #undef INST
 
+
+__device__ inline float shfl_xor_t(float v, int m) { return __shfl_xor(v, m, 64); }
+__device__ inline double shfl_xor_t(double v, int m) { return __shfl_xor(v, m, 64); }
+__device__ inline ccplx shfl_xor_t(ccplx v, int m) { return {__shfl_xor(v.re, m, 64), __shfl_xor(v.im, m, 64)}; }
+__device__ inline zcplx shfl_xor_t(zcplx v, int m) { return {__shfl_xor(v.re, m, 64), __shfl_xor(v.im, m, 64)}; }
+
+// ---------------------------------------------------------------------------
+// Blocked back-transformation: Z := Q2 Z for ALL sweeps in ONE launch.
+//
+// Task t of sweep j acts on rows [j+1+t b, j+t b+b].  For a block J of b
+// consecutive sweeps j0..j0+b-1, H(j,t) only overlaps H(j',t) and H(j',t-1)
+// (j' > j); tasks of one sweep are disjoint.  So the block's product is
+// G(T)...G(1)G(0) with G(t) = H(j0,t) H(j0+1,t) ... H(j0+b-1,t), and G(t)
+// lives in the 2b-row window starting at j0+1+t b.  Columns of Z are
+// independent, so each workgroup owns 32 columns and walks the whole
+// sequence -- blocks J last-to-first, groups t = 0, 1, ... (window sliding
+// down by b rows), reflectors of a group last-to-first -- with its window in
+// registers (8 threads per column, b/4 rows each).  Z is read and written
+// once per block instead of once per sweep; the reflectors of a group are
+// staged through LDS once and read as broadcasts.
+template <typename T, int B>
+__global__ void __launch_bounds__(256)
+unmtr_hb2st_blk_kernel(i64 n, i64 ncols, T* __restrict__ Z, i64 ldz, const T* __restrict__ V,
+                       const T* __restrict__ tau, const i64* __restrict__ sp, const i64* __restrict__ nt,
+                       i64 nsw, int conj_tau) {
+    // 8 threads per column, B/4 window rows each (2B-row window); 32 columns
+    constexpr int TPC = 8, CW = 32, NT = TPC * CW, RPT = 2 * B / TPC, HALF = TPC / 2;
+    __shared__ T Vs[B * B];
+    __shared__ T taus[B];
+    __shared__ T xfer[B * CW];
+    __shared__ i64 sslot[B];
+    const int tid = threadIdx.x, q = tid & (TPC - 1), c = tid / TPC;
+    const i64 col = (i64)blockIdx.x * CW + c;
+    const bool colok = col < ncols;
+    T* zc = Z + (colok ? col : 0) * ldz;
+    T z[RPT];
+    for (i64 J = (nsw - 1) / B; J >= 0; --J) {
+        const i64 j0 = J * B, jn = min((i64)B, nsw - j0);
+        const i64 TJ = nt[j0];                      // tasks per sweep do not grow with j
+        if (TJ <= 0) continue;
+        i64 w0 = j0 + 1;
+        #pragma unroll
+        for (int r = 0; r < RPT; ++r) {
+            const i64 row = w0 + q * RPT + r;
+            z[r] = (colok && row < n) ? zc[row] : s_zero(T());
+        }
+        for (i64 t = 0; t < TJ; ++t) {
+            __syncthreads();
+            if (tid < B) {
+                const int jj = tid;
+                i64 slot = -1;
+                if (jj < jn && t < nt[j0 + jj]) slot = sp[j0 + jj] + t;
+                sslot[jj] = slot;
+                const T tv = slot >= 0 ? tau[slot] : s_zero(T());
+                taus[jj] = conj_tau ? s_conj(tv) : tv;
+            }
+            __syncthreads();
+            for (int idx = tid; idx < B * B; idx += NT) {
+                const int jj = idx / B, vi = idx - jj * B;
+                const i64 slot = sslot[jj];
+                Vs[idx] = slot >= 0 ? V[slot * B + vi] : s_zero(T());
+            }
+            __syncthreads();
+            for (int jj = B - 1; jj >= 0; --jj) {
+                const T tj = taus[jj];
+                if (s_is_zero(tj)) continue;           // uniform
+                // every lane runs the same code (the shuffles below read all 8
+                // lanes of a column); rows outside the reflector see v = 0
+                const int v0 = q * RPT - jj;           // v index of this thread's first row
+                T vr[RPT];
+                T dp[4] = {s_zero(T()), s_zero(T()), s_zero(T()), s_zero(T())};
+                #pragma unroll
+                for (int r = 0; r < RPT; ++r) {
+                    const int vi = v0 + r;
+                    const bool in = vi >= 0 && vi < B;
+                    const T v = Vs[jj * B + (in ? vi : 0)];
+                    vr[r] = in ? v : s_zero(T());
+                    dp[r & 3] = s_add(dp[r & 3], s_mul(s_conj(vr[r]), z[r]));
+                }
+                T dot = s_add(s_add(dp[0], dp[1]), s_add(dp[2], dp[3]));
+                dot = s_add(dot, shfl_xor_t(dot, 1));
+                dot = s_add(dot, shfl_xor_t(dot, 2));
+                dot = s_add(dot, shfl_xor_t(dot, 4));
+                const T w = s_mul(tj, dot);
+                #pragma unroll
+                for (int r = 0; r < RPT; ++r) z[r] = s_sub(z[r], s_mul(vr[r], w));
+            }
+            if (t + 1 < TJ) {
+                // slide the window down by B rows: the top half is final for
+                // this block, the bottom half moves up, B new rows come in
+                if (q < HALF) {
+                    #pragma unroll
+                    for (int r = 0; r < RPT; ++r) {
+                        const i64 row = w0 + q * RPT + r;
+                        if (colok && row < n) zc[row] = z[r];
+                    }
+                } else {
+                    #pragma unroll
+                    for (int r = 0; r < RPT; ++r) xfer[((q - HALF) * RPT + r) * CW + c] = z[r];
+                }
+                __syncthreads();
+                w0 += B;
+                if (q < HALF) {
+                    #pragma unroll
+                    for (int r = 0; r < RPT; ++r) z[r] = xfer[(q * RPT + r) * CW + c];
+                } else {
+                    #pragma unroll
+                    for (int r = 0; r < RPT; ++r) {
+                        const i64 row = w0 + q * RPT + r;
+                        z[r] = (colok && row < n) ? zc[row] : s_zero(T());
+                    }
+                }
+            }
+        }
+        #pragma unroll
+        for (int r = 0; r < RPT; ++r) {
+            const i64 row = w0 + q * RPT + r;
+            if (colok && row < n) zc[row] = z[r];
+        }
+        __syncthreads();      // this block's rows are read by other threads in the next one
+    }
+}
+
+template <typename T>
+bool unmtr_hb2st_blocked(i64 n, i64 ncols, T* Z, i64 ldz, const T* V, i64 b, const T* tau, const i64* sp,
+                         const i64* nt, i64 nsw, bool conj_tau, hipStream_t s) {
+    if (ncols <= 0 || nsw <= 0) return true;
+    dim3 grid((unsigned)((ncols + 31) / 32));     // 32 columns, 256 threads per workgroup
+    if (b == 64) {
+        hipLaunchKernelGGL((unmtr_hb2st_blk_kernel<T, 64>), grid, dim3(256), 0, s, n, ncols, Z, ldz, V, tau, sp,
+                           nt, nsw, conj_tau ? 1 : 0);
+    } else if (b == 32) {
+        hipLaunchKernelGGL((unmtr_hb2st_blk_kernel<T, 32>), grid, dim3(256), 0, s, n, ncols, Z, ldz, V, tau, sp,
+                           nt, nsw, conj_tau ? 1 : 0);
+    } else {
+        return false;                               // caller falls back to one launch per sweep
+    }
+    HIP_LAUNCH_CHECK();
+    return true;
+}
+
+#define INST2(T) \
+    template bool unmtr_hb2st_blocked<T>(i64, i64, T*, i64, const T*, i64, const T*, const i64*, const i64*, i64, \
+                                         bool, hipStream_t);
+INST2(float) INST2(double) INST2(ccplx) INST2(zcplx)
+#undef INST2
+
 }  // namespace slate_hip

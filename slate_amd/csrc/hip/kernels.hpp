@@ -83,9 +83,16 @@ void hb2st_device(i64 n, int b, T* A, i64 lda, T* V, T* tau, i64* row, i64* len,
 template <typename T>
 void apply_refl_batch(i64 ncols, T* Z, i64 ldz, const T* V, i64 b, const T* tau, const i64* row, const i64* len,
                       i64 first, i64 count, bool conj_tau, hipStream_t s);
+template <typename T>
+bool unmtr_hb2st_blocked(i64 n, i64 ncols, T* Z, i64 ldz, const T* V, i64 b, const T* tau, const i64* sp,
+                         const i64* nt, i64 nsw, bool conj_tau, hipStream_t s);
 template <typename T> void v_explicit(i64 m, i64 n, const T* A, i64 lda, T* V, i64 ldv, hipStream_t s);
 template <typename T> void trtri(char uplo, char diag, i64 n, T* A, i64 lda, i64* info, hipStream_t s);
 template <typename T> void tri_inv(char uplo, char diag, i64 n, const T* A, i64 lda, T* W, i64 ldw, hipStream_t s);
+
+// stedc.hip
+void stedc_secular(i64 n, const double* d, const double* z, double rho, double zz, i64* org, double* mu,
+                   double* zh, double* V, i64 ldv, hipStream_t s);
 
 // matgen.hip
 template <typename T>

@@ -225,7 +225,7 @@ void potrf_tile(char uplo, int n, T* A, i64 lda, i64* info, hipStream_t s) {
             // blocked-inverse MFMA trsm, trailing triangle by the masked GEMM
             static const int DB = [] {
                 const char* e = getenv("SLATE_AMD_POTRF_DIAG");
-                const int v = e ? atoi(e) : 256;   // 512 tile: 487 us vs 567 us (two 256 one-CU blocks + MFMA trsm/herk)
+                const int v = e ? atoi(e) : 512;   // standalone 256 is faster (487 vs 567 us) but dpotrf n=32768 end to end: 52.4 (512) vs 50.8 TF/s (256)
                 return (v >= 32 && v <= 512 && v % 32 == 0) ? v : 256;
             }();
             for (int k0 = 0; k0 < n; k0 += DB) {

@@ -1,0 +1,150 @@
+// Divide & conquer merge kernels for the symmetric tridiagonal eigensolver
+// (roles of SLATE's stedc_secular / stedc_z_vector / stedc_merge,
+// src/stedc_secular.cc:132-148, src/stedc_merge.cc; LAPACK laed4/laed3).
+//
+// A merge of size k solves the secular equation
+//     f(lambda) = 1 + rho * sum_i z_i^2 / (d_i - lambda) = 0
+// for its k roots, recomputes z (Gu-Eisenstat) from the roots so the
+// eigenvectors are orthogonal to working precision, and forms the k x k
+// eigenvector matrix of the rank-one update that the merge GEMM applies.
+// All three steps are O(k^2) and were host-bound (k = 16384 at the top of an
+// n = 16384 problem: ~10^10 divisions in the bisection alone).  Here:
+//
+//  * secular: one thread per root, bisection on the offset mu from the
+//    nearer pole (lambda = d[org] + mu, so d_i - lambda = (d_i - d_org) - mu
+//    has no cancellation).  d and z^2 are streamed through LDS in chunks that
+//    the whole wave reads as broadcasts (no bank conflicts); one 64-thread
+//    workgroup per 64 roots, so k = 16384 fills 256 CUs.
+//  * zhat: one thread per pole, the product formula over all roots, same
+//    LDS streaming.
+//  * vectors: one workgroup per root j: v_i = zhat_i / (d_i - lambda_j),
+//    column norm by a workgroup reduction, normalised column written
+//    column-major (coalesced) straight into the GEMM operand.
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace slate_hip {
+
+namespace {
+constexpr int SEC_T = 64;        // roots per workgroup (one wave)
+constexpr int SEC_CH = 2048;     // poles per LDS chunk (2 x 16 KiB)
+constexpr int SEC_ITMAX = 200;   // bisection cap (the host solver's)
+}
+
+__global__ void __launch_bounds__(SEC_T)
+secular_kernel(i64 n, const double* __restrict__ d, const double* __restrict__ z, double rho, double zz,
+               i64* __restrict__ org, double* __restrict__ mu) {
+    __shared__ double sd[SEC_CH], sz2[SEC_CH];
+    const i64 j = (i64)blockIdx.x * SEC_T + threadIdx.x;
+    const bool live = j < n;
+    const i64 jj = live ? j : n - 1;
+    // bracket: root j in (d_j, d_j+1) (last one: (d_n-1, d_n-1 + rho |z|^2))
+    const double lo_d = d[jj];
+    const double hi_d = (jj + 1 < n) ? d[jj + 1] : d[jj] + rho * zz;
+    const double mid = 0.5 * (hi_d - lo_d);
+    // pass 0 decides the origin from the sign of f at the midpoint (origin j);
+    // passes 1.. bisect mu in (a, b) around the chosen origin
+    i64 o = jj;
+    double a = 0.0, b = mid;
+    bool done = !live;
+    for (int it = 0; it <= SEC_ITMAX; ++it) {
+        const double dorg = d[o];
+        const double m = (it == 0) ? mid : 0.5 * (a + b);
+        if (it > 0 && (m == a || m == b)) done = true;
+        // the workgroup stops when every root has converged
+        if (__syncthreads_and(done ? 1 : 0)) break;
+        double s = 0.0;
+        for (i64 c0 = 0; c0 < n; c0 += SEC_CH) {
+            const int cn = (int)min((i64)SEC_CH, n - c0);
+            __syncthreads();
+            for (int i = threadIdx.x; i < cn; i += SEC_T) {
+                sd[i] = d[c0 + i];
+                const double zi = z[c0 + i];
+                sz2[i] = zi * zi;
+            }
+            __syncthreads();
+            if (!done) {
+                #pragma unroll 8
+                for (int i = 0; i < cn; ++i) s += sz2[i] / ((sd[i] - dorg) - m);
+            }
+        }
+        if (done) continue;
+        const double fv = 1.0 + rho * s;
+        if (it == 0) {
+            if (jj + 1 < n && fv < 0) { o = jj + 1; a = -mid; b = 0.0; }   // root right of the midpoint
+            else { o = jj; a = 0.0; b = (jj + 1 < n) ? mid : (hi_d - lo_d); }
+        } else {
+            if (fv < 0) a = m; else b = m;
+        }
+    }
+    if (live) { org[j] = o; mu[j] = 0.5 * (a + b); }
+}
+
+// zhat_i^2 = (lambda_i - d_i) prod_{j != i} (lambda_j - d_i) / (d_j - d_i) / rho
+__global__ void __launch_bounds__(SEC_T)
+zhat_kernel(i64 n, const double* __restrict__ d, const double* __restrict__ z, double rho,
+            const i64* __restrict__ org, const double* __restrict__ mu, double* __restrict__ zh) {
+    __shared__ double sd[SEC_CH], sl[SEC_CH], sdj[SEC_CH];
+    const i64 i = (i64)blockIdx.x * SEC_T + threadIdx.x;
+    const bool live = i < n;
+    const double di = live ? d[i] : 0.0;
+    double prod = 1.0, dii = 1.0;
+    for (i64 c0 = 0; c0 < n; c0 += SEC_CH) {
+        const int cn = (int)min((i64)SEC_CH, n - c0);
+        __syncthreads();
+        for (int t = threadIdx.x; t < cn; t += SEC_T) {
+            sdj[t] = d[c0 + t];
+            sd[t] = d[org[c0 + t]];
+            sl[t] = mu[c0 + t];
+        }
+        __syncthreads();
+        if (live) {
+            for (int t = 0; t < cn; ++t) {
+                const double delta = (sd[t] - di) + sl[t];          // lambda_j - d_i
+                if (c0 + t == i) { dii = delta; continue; }
+                prod *= delta / (sdj[t] - di);
+            }
+        }
+    }
+    if (live) {
+        const double v = sqrt(fabs(dii * prod / rho));
+        zh[i] = z[i] < 0 ? -v : v;
+    }
+}
+
+// column j of the rank-one eigenvector matrix, normalised: V[i + j*ldv]
+__global__ void __launch_bounds__(256)
+secvec_kernel(i64 n, const double* __restrict__ d, const double* __restrict__ zh,
+              const i64* __restrict__ org, const double* __restrict__ mu, double* __restrict__ V, i64 ldv) {
+    __shared__ double red[4];
+    const i64 j = blockIdx.x;
+    const double dorg = d[org[j]], mj = mu[j];
+    double* col = V + j * ldv;
+    double ss = 0.0;
+    for (i64 i = threadIdx.x; i < n; i += 256) {
+        const double v = zh[i] / ((d[i] - dorg) - mj);            // z_i / (d_i - lambda_j)
+        col[i] = v;
+        ss += v * v;
+    }
+    ss = wave_sum(ss);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    const double inv = 1.0 / sqrt(red[0] + red[1] + red[2] + red[3]);
+    for (i64 i = threadIdx.x; i < n; i += 256) col[i] *= inv;
+}
+
+void stedc_secular(i64 n, const double* d, const double* z, double rho, double zz, i64* org, double* mu,
+                   double* zh, double* V, i64 ldv, hipStream_t s) {
+    if (n <= 0) return;
+    const unsigned g = (unsigned)((n + SEC_T - 1) / SEC_T);
+    hipLaunchKernelGGL(secular_kernel, dim3(g), dim3(SEC_T), 0, s, n, d, z, rho, zz, org, mu);
+    HIP_LAUNCH_CHECK();
+    hipLaunchKernelGGL(zhat_kernel, dim3(g), dim3(SEC_T), 0, s, n, d, z, rho, org, mu, zh);
+    HIP_LAUNCH_CHECK();
+    if (V != nullptr) {
+        hipLaunchKernelGGL(secvec_kernel, dim3((unsigned)n), dim3(256), 0, s, n, d, zh, org, mu, V, ldv);
+        HIP_LAUNCH_CHECK();
+    }
+}
+
+}  // namespace slate_hip

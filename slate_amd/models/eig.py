@@ -27,6 +27,8 @@ holds the dense matrix.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import _native, ops
@@ -239,8 +241,20 @@ def unmtr_hb2st(F: Hb2stFactors, Z: torch.Tensor):
         Z.mul_(F.phase.to(Z.device)[:, None])
     dev = Z.device
     V, tau, row, ln = (x.to(dev) for x in (F.V, F.tau, F.row, F.length))
+    n = F.sweep_ptr.numel()
+    b = V.shape[1] if V.dim() == 2 else 0
+    if Z.is_cuda and n > 1 and F.count > 0 and Z.shape[0] == n and \
+            os.environ.get("SLATE_AMD_UNMTR_BLOCKED", "1") != "0":
+        # all sweeps in one launch, blocks of b sweeps (csrc/hip/eig.hip)
+        spd = F.sweep_ptr.to(dev).contiguous()
+        ntd = (spd[1:] - spd[:-1]).contiguous()
+        with trace_block("unmtr_hb2st"):
+            if _native.hip().unmtr_hb2st_blocked(_code(Z.dtype), n, Z.shape[1], Z.data_ptr(), max(1, Z.stride(1)),
+                                                 V.contiguous().data_ptr(), b, tau.contiguous().data_ptr(),
+                                                 spd.data_ptr(), ntd.data_ptr(), n - 1, False,
+                                                 torch.cuda.current_stream(dev).cuda_stream):
+                return Z
     sp = F.sweep_ptr.tolist()
-    n = len(sp)
     with trace_block("unmtr_hb2st"):
         for j in range(n - 1, -1, -1):
             first = sp[j]
@@ -362,7 +376,25 @@ def _rank_one_eig(dd, z, rho, Qb):
     K = torch.tensor(keep, dtype=torch.int64)
     k = K.numel()
     lam = dd.clone()
-    if k:
+    if k and dev.type == "cuda":
+        # secular roots, Gu-Eisenstat z and the normalised k x k eigenvector
+        # matrix on the GPU (csrc/hip/stedc.hip), straight into the GEMM operand
+        dKd = dd[K].contiguous().to(dev)
+        zKd = z[K].contiguous().to(dev)
+        org = torch.empty(k, dtype=torch.int64, device=dev)
+        mu = torch.empty(k, dtype=torch.float64, device=dev)
+        zh = torch.empty(k, dtype=torch.float64, device=dev)
+        VsC = ops.colmajor_empty(k, k, torch.float64, dev)
+        _native.hip().stedc_secular(k, dKd.data_ptr(), zKd.data_ptr(), float(rho), float((z[K] * z[K]).sum()),
+                                    org.data_ptr(), mu.data_ptr(), zh.data_ptr(), VsC.data_ptr(), VsC.stride(1),
+                                    torch.cuda.current_stream(dev).cuda_stream)
+        lam[K] = (dKd[org] + mu).cpu()
+        Kd = K.to(dev)
+        QK = ops.as_colmajor(Q[:, Kd])
+        Out = ops.colmajor_empty(QK.shape[0], k, Q.dtype, dev)
+        ops.gemm(1.0, QK, VsC, 0.0, Out)                 # merge GEMM on the MFMA kernels
+        Q[:, Kd] = Out
+    elif k:
         dK = dd[K].contiguous()
         zK = z[K].contiguous()
         org = torch.zeros(k, dtype=torch.int64)

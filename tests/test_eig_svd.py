@@ -285,3 +285,50 @@ def test_hb2st_gpu(dt, n, b, monkeypatch):
     d2, e2, _ = E.hb2st(H.clone(), b, device=torch.device("cuda"))
     T2 = torch.diag(d2) + torch.diag(e2, -1) + torch.diag(e2, 1)
     assert (torch.linalg.eigvalsh(T2) - torch.linalg.eigvalsh(T)).abs().max() / w0.abs().max() < 1e-13
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [257, 3000])
+def test_stedc_gpu_secular(n):
+    """Merges on the GPU (secular roots / Gu-Eisenstat z / vectors by the
+    stedc.hip kernels) vs an fp64 host reference."""
+    torch.manual_seed(2)
+    d, e = torch.randn(n, dtype=torch.float64), torch.randn(n - 1, dtype=torch.float64)
+    T = torch.diag(d) + torch.diag(e, 1) + torch.diag(e, -1)
+    wr = torch.linalg.eigvalsh(T)
+    w, Z = sl.stedc(d, e, device="cuda", leaf=32)
+    Z = Z.cpu()
+    tol = 1e-13 * n
+    assert (w - wr).abs().max() < tol
+    assert (T @ Z - Z * w).abs().max() < tol
+    assert (Z.T @ Z - torch.eye(n, dtype=torch.float64)).abs().max() < tol
+    d2 = torch.ones(n, dtype=torch.float64)
+    d2[::3] = 2.0
+    e2 = torch.full((n - 1,), 1e-9, dtype=torch.float64)
+    T2 = torch.diag(d2) + torch.diag(e2, 1) + torch.diag(e2, -1)
+    w, Z = sl.stedc(d2, e2, device="cuda", leaf=32)
+    Z = Z.cpu()
+    assert (T2 @ Z - Z * w).abs().max() < tol
+    assert (Z.T @ Z - torch.eye(n, dtype=torch.float64)).abs().max() < tol
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float64, torch.complex128])
+@pytest.mark.parametrize("n,b", [(300, 32), (517, 64), (200, 64)])
+def test_unmtr_hb2st_blocked_gpu(monkeypatch, dt, n, b):
+    """One-launch blocked back-transform (blocks of b sweeps, sliding
+    register window) == one launch per sweep."""
+    g = torch.Generator().manual_seed(7)
+    A = torch.randn(n, n, dtype=dt, generator=g)
+    A = A + A.mH
+    i = torch.arange(n)
+    A = torch.where((i[:, None] - i[None, :]).abs() <= b, A, torch.zeros_like(A))
+    d, e, F = E.hb2st(E._cm(A.clone()), b)
+    Z0 = torch.randn(n, 77, dtype=dt, generator=g)
+    Za = E._cm(Z0.cuda())
+    Zb = E._cm(Z0.cuda())
+    monkeypatch.setenv("SLATE_AMD_UNMTR_BLOCKED", "0")
+    E.unmtr_hb2st(F, Za)
+    monkeypatch.setenv("SLATE_AMD_UNMTR_BLOCKED", "1")
+    E.unmtr_hb2st(F, Zb)
+    assert (Za - Zb).abs().max().item() < 1e-12 * n

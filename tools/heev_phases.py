@@ -13,6 +13,7 @@ from slate_amd.utils.trace import Trace  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
 nb = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+band = int(sys.argv[3]) if len(sys.argv) > 3 else 0
 dev = torch.device("cuda", 0)
 
 
@@ -24,19 +25,19 @@ def one():
     Z.insertLocalTiles(device=dev)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    sl.heev(A, None, Z, {})
+    sl.heev(A, None, Z, {sl.Option.InnerBlocking: band} if band else {})
     torch.cuda.synchronize()
     return time.perf_counter() - t0
 
 
 one()                                   # warmup (kernels, workspaces)
-Trace.on()
+Trace.on(device_timing=True)
 t = one()
 Trace.off()
 agg = defaultdict(float)
 for e in Trace.events():
-    agg[(e["nest"], e["name"])] += e["stop"] - e["start"]
-print(f"heev n={n} nb={nb}: {t:.3f} s")
-for (nest, name), v in sorted(agg.items(), key=lambda kv: (kv[0][0], -kv[1])):
+    agg[(e["kind"] + (" " * 2 * e["nest"]), e["name"])] += e["stop"] - e["start"]
+print(f"heev n={n} nb={nb} band={band or 'default'}: {t:.3f} s")
+for (kind, name), v in sorted(agg.items(), key=lambda kv: (kv[0][0], -kv[1])):
     if v > 1e-3 * t:
-        print(f"  {'  ' * nest}{name:30s} {v:8.3f} s")
+        print(f"  {kind:8s} {name:30s} {v:8.3f} s")
