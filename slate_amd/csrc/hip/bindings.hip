@@ -154,6 +154,13 @@ static void register_kernels(py::module& m) {
                                         P<const i64>(nt), nsw, conj_tau, S(st)); });
         return ok;
     });
+    m.def("unmtr_hb2st_mfma", [](i64 n, i64 ncols, uintptr_t Z, i64 ldz, uintptr_t V, i64 b, uintptr_t tau,
+                                 uintptr_t sp, uintptr_t nt, uintptr_t gJ, uintptr_t gt, uintptr_t gptr, i64 ngroups,
+                                 uintptr_t Tg, i64 nsw, uintptr_t st) {
+        return unmtr_hb2st_mfma(n, ncols, P<double>(Z), ldz, P<const double>(V), b, P<const double>(tau),
+                                P<const i64>(sp), P<const i64>(nt), P<const i64>(gJ), P<const i64>(gt),
+                                P<const i64>(gptr), ngroups, P<double>(Tg), nsw, S(st));
+    });
     m.def("apply_refl", [](char dt, i64 ncols, uintptr_t Z, i64 ldz, uintptr_t V, i64 b, uintptr_t tau,
                            uintptr_t row, uintptr_t len, i64 first, i64 count, bool conj_tau, uintptr_t st) {
         dispatch(dt, [&](auto z) { using T = decltype(z);

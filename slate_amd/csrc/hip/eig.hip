@@ -205,4 +205,227 @@ bool unmtr_hb2st_blocked(i64 n, i64 ncols, T* Z, i64 ldz, const T* V, i64 b, con
 INST2(float) INST2(double) INST2(ccplx) INST2(zcplx)
 #undef INST2
 
+
+// ---------------------------------------------------------------------------
+// MFMA form of the blocked back-transformation (real double, b = 64).
+//
+// Same grouping as above -- G(J,t) = H(j0,t) ... H(j0+b-1,t) in the 2b-row
+// window at j0+1+t b -- but each group is applied as ONE block reflector
+// G = I - V T V^H (forward compact WY, T upper triangular):
+//   W = V^H Z_win (b x CW),  W = T W,  Z_win -= V W,
+// three small GEMMs on v_mfma_f64_16x16x4.  V is the parallelogram of the
+// group's reflectors (reflector jj occupies window rows jj..jj+b-1); T of
+// every group is built once by hb2st_tfac_kernel (one workgroup per group).
+//
+// MFMA f64 16x16x4 lane layout: first operand A[i = l & 15][k = l >> 4],
+// second operand B[k = l >> 4][j = l & 15], accumulator register r of lane l
+// holds D[(l >> 4) + 4 r][l & 15].
+namespace {
+constexpr int TB = 64;            // band / sweeps per block
+constexpr int TCW = 64;           // Z columns per workgroup
+constexpr int SV = TB + 2;        // LDS row pitch of the raw reflectors
+constexpr int SZ = 2 * TB + 4;    // LDS column pitch of the Z window (column-major)
+constexpr int SW = TCW + 16;      // LDS row pitch of W
+}
+
+__global__ void __launch_bounds__(256)
+hb2st_tfac_kernel(const double* __restrict__ V, const double* __restrict__ tau, const i64* __restrict__ sp,
+                  const i64* __restrict__ nt, const i64* __restrict__ gJ, const i64* __restrict__ gt, i64 nsw,
+                  double* __restrict__ Tout) {
+    __shared__ double Vr[TB * SV];
+    __shared__ double G[TB * (TB + 1)];
+    __shared__ double Tm[TB * (TB + 1)];
+    __shared__ double taus[TB];
+    __shared__ i64 sslot[TB];
+    const int tid = threadIdx.x;
+    const i64 g = blockIdx.x;
+    const i64 j0 = gJ[g] * TB, t = gt[g];
+    const i64 jn = min((i64)TB, nsw - j0);
+    if (tid < TB) {
+        i64 slot = -1;
+        if (tid < jn && t < nt[j0 + tid]) slot = sp[j0 + tid] + t;
+        sslot[tid] = slot;
+        taus[tid] = slot >= 0 ? tau[slot] : 0.0;
+    }
+    __syncthreads();
+    for (int idx = tid; idx < TB * TB; idx += 256) {
+        const int jj = idx / TB, vi = idx - jj * TB;
+        const i64 slot = sslot[jj];
+        Vr[jj * SV + vi] = slot >= 0 ? V[slot * TB + vi] : 0.0;
+    }
+    __syncthreads();
+    // G[i][k] = v_i . v_k (i < k): v_i covers window rows i..i+b-1
+    for (int idx = tid; idx < TB * TB; idx += 256) {
+        const int i = idx / TB, k = idx - i * TB;
+        double acc = 0.0;
+        if (i < k) {
+            for (int r = k; r < i + TB; ++r) acc += Vr[i * SV + (r - i)] * Vr[k * SV + (r - k)];
+        }
+        G[i * (TB + 1) + k] = acc;
+        Tm[i * (TB + 1) + k] = 0.0;
+    }
+    __syncthreads();
+    // forward larft: T[0:k, k] = -tau_k T[0:k, 0:k] G[0:k, k], T[k][k] = tau_k
+    for (int k = 0; k < TB; ++k) {
+        double acc = 0.0;
+        if (tid < k) {
+            for (int l = tid; l < k; ++l) acc += Tm[tid * (TB + 1) + l] * G[l * (TB + 1) + k];
+        }
+        __syncthreads();
+        if (tid < k) Tm[tid * (TB + 1) + k] = -taus[k] * acc;
+        if (tid == k) Tm[k * (TB + 1) + k] = taus[k];
+        __syncthreads();
+    }
+    double* To = Tout + g * TB * TB;
+    for (int idx = tid; idx < TB * TB; idx += 256) {
+        const int i = idx % TB, k = idx / TB;           // column-major store
+        To[idx] = Tm[i * (TB + 1) + k];
+    }
+}
+
+__global__ void __launch_bounds__(256)
+unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const double* __restrict__ V,
+                        const i64* __restrict__ sp, const i64* __restrict__ nt, const i64* __restrict__ gptr,
+                        const double* __restrict__ Tg, i64 nsw) {
+    __shared__ double Vr[TB * SV];
+    __shared__ double Zs[TCW * SZ];
+    __shared__ double Ws[TB * SW];
+    __shared__ i64 sslot[TB];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int li = lane & 15, lk = lane >> 4;
+    const i64 c0 = (i64)blockIdx.x * TCW;
+    const int ncw = (int)min((i64)TCW, ncols - c0);
+    // window row w of group t lives in Zs at column-major row ((w >> 6) + t) & 1) * 64 + (w & 63)
+    auto zrow = [](int w, i64 t) { return (int)((((w >> 6) + t) & 1) * TB + (w & (TB - 1))); };
+    // global <-> LDS: one wave streams 64 consecutive rows of a column
+    auto load_half = [&](i64 row0, int phys) {
+        for (int cc = wv; cc < TCW; cc += 4) {
+            const i64 row = row0 + lane;
+            double v = 0.0;
+            if (cc < ncw && row < n) v = Z[(c0 + cc) * ldz + row];
+            Zs[cc * SZ + phys * TB + lane] = v;
+        }
+    };
+    auto store_half = [&](i64 row0, int phys) {
+        for (int cc = wv; cc < TCW; cc += 4) {
+            const i64 row = row0 + lane;
+            if (cc < ncw && row < n) Z[(c0 + cc) * ldz + row] = Zs[cc * SZ + phys * TB + lane];
+        }
+    };
+    for (i64 J = (nsw - 1) / TB; J >= 0; --J) {
+        const i64 j0 = J * TB, jn = min((i64)TB, nsw - j0);
+        const i64 TJ = nt[j0];
+        if (TJ <= 0) continue;
+        i64 w0 = j0 + 1;
+        __syncthreads();
+        load_half(w0, 0);
+        load_half(w0 + TB, 1);
+        for (i64 t = 0; t < TJ; ++t) {
+            if (tid < TB) {
+                i64 slot = -1;
+                if (tid < jn && t < nt[j0 + tid]) slot = sp[j0 + tid] + t;
+                sslot[tid] = slot;
+            }
+            __syncthreads();
+            for (int idx = tid; idx < TB * TB; idx += 256) {
+                const int jj = idx / TB, vi = idx - jj * TB;
+                const i64 slot = sslot[jj];
+                Vr[jj * SV + vi] = slot >= 0 ? V[slot * TB + vi] : 0.0;
+            }
+            __syncthreads();
+            const double* T = Tg + (gptr[J] + t) * TB * TB;
+            // V(w, jj) of the parallelogram
+            auto vg = [&](int w, int jj) {
+                const int vi = w - jj;
+                return (vi >= 0 && vi < TB) ? Vr[jj * SV + vi] : 0.0;
+            };
+            // (1) W = V^T Z: wave wv owns W rows 16 wv..16 wv+15, 4 column tiles
+            d4 acc[4];
+            #pragma unroll
+            for (int j = 0; j < 4; ++j) acc[j] = d4{0.0, 0.0, 0.0, 0.0};
+            for (int k0 = 0; k0 < 2 * TB; k0 += 4) {
+                const int w = k0 + lk;
+                const double a = vg(w, 16 * wv + li);
+                const int pr = zrow(w, t);
+                #pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const double b = Zs[(16 * j + li) * SZ + pr];
+                    acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[j], 0, 0, 0);
+                }
+            }
+            #pragma unroll
+            for (int j = 0; j < 4; ++j)
+                #pragma unroll
+                for (int r = 0; r < 4; ++r) Ws[(16 * wv + lk + 4 * r) * SW + 16 * j + li] = acc[j][r];
+            __syncthreads();
+            // (2) W = T W
+            #pragma unroll
+            for (int j = 0; j < 4; ++j) acc[j] = d4{0.0, 0.0, 0.0, 0.0};
+            for (int k0 = 0; k0 < TB; k0 += 4) {
+                const int kk = k0 + lk;
+                const double a = T[(16 * wv + li) + (i64)kk * TB];
+                #pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const double b = Ws[kk * SW + 16 * j + li];
+                    acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[j], 0, 0, 0);
+                }
+            }
+            __syncthreads();
+            #pragma unroll
+            for (int j = 0; j < 4; ++j)
+                #pragma unroll
+                for (int r = 0; r < 4; ++r) Ws[(16 * wv + lk + 4 * r) * SW + 16 * j + li] = acc[j][r];
+            __syncthreads();
+            // (3) Z -= V W: wave wv owns window rows 32 wv..32 wv+31 (2 x 4 tiles)
+            #pragma unroll
+            for (int ri = 0; ri < 2; ++ri) {
+                d4 zc[4];
+                const int wb = 32 * wv + 16 * ri;
+                #pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    #pragma unroll
+                    for (int r = 0; r < 4; ++r) zc[j][r] = Zs[(16 * j + li) * SZ + zrow(wb + lk + 4 * r, t)];
+                for (int k0 = 0; k0 < TB; k0 += 4) {
+                    const int jj = k0 + lk;
+                    const double a = -vg(wb + li, jj);
+                    #pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const double b = Ws[jj * SW + 16 * j + li];
+                        zc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, zc[j], 0, 0, 0);
+                    }
+                }
+                #pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    #pragma unroll
+                    for (int r = 0; r < 4; ++r) Zs[(16 * j + li) * SZ + zrow(wb + lk + 4 * r, t)] = zc[j][r];
+            }
+            __syncthreads();
+            if (t + 1 < TJ) {
+                // the top half (physical t & 1) is final: out, and the next B rows in
+                const int ph = (int)(t & 1);
+                store_half(w0, ph);
+                load_half(w0 + 2 * TB, ph);
+                w0 += TB;
+            }
+        }
+        const i64 tl = TJ - 1;
+        store_half(w0, (int)(tl & 1));
+        store_half(w0 + TB, (int)((tl + 1) & 1));
+        __syncthreads();      // next block reads rows written by other threads
+    }
+}
+
+bool unmtr_hb2st_mfma(i64 n, i64 ncols, double* Z, i64 ldz, const double* V, i64 b, const double* tau,
+                      const i64* sp, const i64* nt, const i64* gJ, const i64* gt, const i64* gptr, i64 ngroups,
+                      double* Tg, i64 nsw, hipStream_t s) {
+    if (b != TB) return false;
+    if (ncols <= 0 || nsw <= 0 || ngroups <= 0) return true;
+    hipLaunchKernelGGL(hb2st_tfac_kernel, dim3((unsigned)ngroups), dim3(256), 0, s, V, tau, sp, nt, gJ, gt, nsw, Tg);
+    HIP_LAUNCH_CHECK();
+    hipLaunchKernelGGL(unmtr_hb2st_mfma_kernel, dim3((unsigned)((ncols + TCW - 1) / TCW)), dim3(256), 0, s, n, ncols,
+                       Z, ldz, V, sp, nt, gptr, Tg, nsw);
+    HIP_LAUNCH_CHECK();
+    return true;
+}
+
 }  // namespace slate_hip

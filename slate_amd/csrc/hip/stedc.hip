@@ -10,8 +10,8 @@
 // All three steps are O(k^2) and were host-bound (k = 16384 at the top of an
 // n = 16384 problem: ~10^10 divisions in the bisection alone).  Here:
 //
-//  * secular: one thread per root, bisection on the offset mu from the
-//    nearer pole (lambda = d[org] + mu, so d_i - lambda = (d_i - d_org) - mu
+//  * secular: one thread per root, Bunch-Nielsen-Sorensen steps (bisection
+//    fallback) on the offset mu from the nearer pole (lambda = d[org] + mu, so d_i - lambda = (d_i - d_org) - mu
 //    has no cancellation).  d and z^2 are streamed through LDS in chunks that
 //    the whole wave reads as broadcasts (no bank conflicts); one 64-thread
 //    workgroup per 64 roots, so k = 16384 fills 256 CUs.
@@ -38,22 +38,26 @@ secular_kernel(i64 n, const double* __restrict__ d, const double* __restrict__ z
     const i64 j = (i64)blockIdx.x * SEC_T + threadIdx.x;
     const bool live = j < n;
     const i64 jj = live ? j : n - 1;
+    const bool right = jj + 1 < n;                 // a pole on the right of the interval
     // bracket: root j in (d_j, d_j+1) (last one: (d_n-1, d_n-1 + rho |z|^2))
     const double lo_d = d[jj];
-    const double hi_d = (jj + 1 < n) ? d[jj + 1] : d[jj] + rho * zz;
+    const double hi_d = right ? d[jj + 1] : d[jj] + rho * zz;
     const double mid = 0.5 * (hi_d - lo_d);
-    // pass 0 decides the origin from the sign of f at the midpoint (origin j);
-    // passes 1.. bisect mu in (a, b) around the chosen origin
+    // pass 0 decides the origin (nearer pole) from the sign of f at the
+    // midpoint.  Then Bunch-Nielsen-Sorensen steps: the poles left of the
+    // interval (psi) and right of it (phi) are each modelled by one pole at
+    // the interval end plus a constant, matched in value and slope at the
+    // current point, and the model's root is taken -- quadratic convergence
+    // also for roots next to a pole, where Newton crawls.  Every evaluation
+    // shrinks the bracket (a, b); a step leaving it falls back to bisection.
     i64 o = jj;
-    double a = 0.0, b = mid;
+    double a = 0.0, b = mid, m = mid;
     bool done = !live;
+    const double eps = 2.220446049250313e-16;
     for (int it = 0; it <= SEC_ITMAX; ++it) {
-        const double dorg = d[o];
-        const double m = (it == 0) ? mid : 0.5 * (a + b);
-        if (it > 0 && (m == a || m == b)) done = true;
-        // the workgroup stops when every root has converged
         if (__syncthreads_and(done ? 1 : 0)) break;
-        double s = 0.0;
+        const double dorg = d[o];
+        double ps = 0.0, dps = 0.0, ph = 0.0, dph = 0.0;
         for (i64 c0 = 0; c0 < n; c0 += SEC_CH) {
             const int cn = (int)min((i64)SEC_CH, n - c0);
             __syncthreads();
@@ -64,20 +68,57 @@ secular_kernel(i64 n, const double* __restrict__ d, const double* __restrict__ z
             }
             __syncthreads();
             if (!done) {
-                #pragma unroll 8
-                for (int i = 0; i < cn; ++i) s += sz2[i] / ((sd[i] - dorg) - m);
+                const i64 split = jj - c0;             // local indices <= split are left poles
+                #pragma unroll 4
+                for (int i = 0; i < cn; ++i) {
+                    const double r = 1.0 / ((sd[i] - dorg) - m);
+                    const double t = sz2[i] * r;
+                    const bool L = i <= split;
+                    ps += L ? t : 0.0;
+                    dps += L ? t * r : 0.0;
+                    ph += L ? 0.0 : t;
+                    dph += L ? 0.0 : t * r;
+                }
             }
         }
         if (done) continue;
-        const double fv = 1.0 + rho * s;
+        const double psi = rho * ps, dpsi = rho * dps, phi = rho * ph, dphi = rho * dph;
+        const double fv = 1.0 + psi + phi;
         if (it == 0) {
-            if (jj + 1 < n && fv < 0) { o = jj + 1; a = -mid; b = 0.0; }   // root right of the midpoint
-            else { o = jj; a = 0.0; b = (jj + 1 < n) ? mid : (hi_d - lo_d); }
-        } else {
-            if (fv < 0) a = m; else b = m;
+            if (right && fv < 0) { o = jj + 1; a = -mid; b = 0.0; }   // root right of the midpoint
+            else { o = jj; a = 0.0; b = right ? mid : (hi_d - lo_d); }
+            m = 0.5 * (a + b);
+            continue;
         }
+        // converged when f is below its own rounding error (psi / phi are
+        // sums of same-sign terms: their magnitudes bound it, as laed4's erretm)
+        if (fabs(fv) <= 8.0 * eps * (1.0 + fabs(psi) + fabs(phi))) { done = true; continue; }
+        if (fv < 0) a = m; else b = m;
+        const double Dlo = (lo_d - dorg) - m;       // < 0
+        const double b1 = dpsi * Dlo * Dlo, a1 = psi - dpsi * Dlo;
+        double h;
+        if (!right) {
+            const double c = 1.0 + a1 + phi;
+            h = Dlo + b1 / c;
+        } else {
+            const double Dhi = (hi_d - dorg) - m;   // > 0
+            const double b2 = dphi * Dhi * Dhi, a2 = phi - dphi * Dhi;
+            const double c = 1.0 + a1 + a2;
+            // c (Dlo - h)(Dhi - h) + b1 (Dhi - h) + b2 (Dlo - h) = 0
+            const double qa = c, qb = c * (Dlo + Dhi) + b1 + b2, qc = c * Dlo * Dhi + b1 * Dhi + b2 * Dlo;
+            const double disc = fmax(qb * qb - 4.0 * qa * qc, 0.0), sq = sqrt(disc);
+            double h1, h2;
+            if (qb >= 0) { h1 = (qb + sq) / (2.0 * qa); h2 = 2.0 * qc / (qb + sq); }
+            else { h1 = 2.0 * qc / (qb - sq); h2 = (qb - sq) / (2.0 * qa); }
+            const bool ok1 = h1 > Dlo && h1 < Dhi, ok2 = h2 > Dlo && h2 < Dhi;
+            h = ok2 ? h2 : (ok1 ? h1 : -fv / (dpsi + dphi));
+        }
+        double mn = m + h;
+        if (!(mn > a && mn < b)) mn = 0.5 * (a + b);
+        if (mn == a || mn == b || fabs(mn - m) <= 4.0 * eps * fabs(mn)) done = true;
+        m = mn;
     }
-    if (live) { org[j] = o; mu[j] = 0.5 * (a + b); }
+    if (live) { org[j] = o; mu[j] = m; }
 }
 
 // zhat_i^2 = (lambda_i - d_i) prod_{j != i} (lambda_j - d_i) / (d_j - d_i) / rho

@@ -248,6 +248,24 @@ def unmtr_hb2st(F: Hb2stFactors, Z: torch.Tensor):
         # all sweeps in one launch, blocks of b sweeps (csrc/hip/eig.hip)
         spd = F.sweep_ptr.to(dev).contiguous()
         ntd = (spd[1:] - spd[:-1]).contiguous()
+        if Z.dtype == torch.float64 and b == 64 and os.environ.get("SLATE_AMD_UNMTR_MFMA", "1") != "0":
+            # groups of b reflectors as block reflectors I - V T V^H on MFMA:
+            # group g = (block J, task t); T of every group built once
+            nsw = n - 1
+            TJ = ntd[::b].contiguous()
+            ng = int(TJ.sum())
+            gJ = torch.repeat_interleave(torch.arange(TJ.numel(), device=dev), TJ)
+            gptr = torch.zeros(TJ.numel() + 1, dtype=torch.int64, device=dev)
+            gptr[1:] = torch.cumsum(TJ, 0)
+            gt = torch.arange(ng, device=dev) - gptr[gJ]
+            Tg = torch.empty(max(ng, 1) * b * b, dtype=torch.float64, device=dev)
+            with trace_block("unmtr_hb2st"):
+                _native.hip().unmtr_hb2st_mfma(n, Z.shape[1], Z.data_ptr(), max(1, Z.stride(1)),
+                                               V.contiguous().data_ptr(), b, tau.contiguous().data_ptr(),
+                                               spd.data_ptr(), ntd.data_ptr(), gJ.data_ptr(), gt.data_ptr(),
+                                               gptr.data_ptr(), ng, Tg.data_ptr(), nsw,
+                                               torch.cuda.current_stream(dev).cuda_stream)
+            return Z
         with trace_block("unmtr_hb2st"):
             if _native.hip().unmtr_hb2st_blocked(_code(Z.dtype), n, Z.shape[1], Z.data_ptr(), max(1, Z.stride(1)),
                                                  V.contiguous().data_ptr(), b, tau.contiguous().data_ptr(),

@@ -314,7 +314,7 @@ def test_stedc_gpu_secular(n):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dt", [torch.float64, torch.complex128])
-@pytest.mark.parametrize("n,b", [(300, 32), (517, 64), (200, 64)])
+@pytest.mark.parametrize("n,b", [(300, 32), (517, 64), (200, 64), (1000, 64)])
 def test_unmtr_hb2st_blocked_gpu(monkeypatch, dt, n, b):
     """One-launch blocked back-transform (blocks of b sweeps, sliding
     register window) == one launch per sweep."""
@@ -330,5 +330,11 @@ def test_unmtr_hb2st_blocked_gpu(monkeypatch, dt, n, b):
     monkeypatch.setenv("SLATE_AMD_UNMTR_BLOCKED", "0")
     E.unmtr_hb2st(F, Za)
     monkeypatch.setenv("SLATE_AMD_UNMTR_BLOCKED", "1")
+    monkeypatch.setenv("SLATE_AMD_UNMTR_MFMA", "0")
     E.unmtr_hb2st(F, Zb)
     assert (Za - Zb).abs().max().item() < 1e-12 * n
+    # block reflectors on MFMA (real, b = 64)
+    Zc = E._cm(Z0.cuda())
+    monkeypatch.setenv("SLATE_AMD_UNMTR_MFMA", "1")
+    E.unmtr_hb2st(F, Zc)
+    assert (Za - Zc).abs().max().item() < 1e-12 * n

@@ -4,7 +4,11 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 timeout -k 10 200 python -u -m pytest tests/test_eig_svd.py -x -v --timeout 150 --timeout-method thread -m gpu > gpurun_out/pytest_eig.log 2>&1 || { tail -40 gpurun_out/pytest_eig.log; exit 1; }
 tail -2 gpurun_out/pytest_eig.log
-for band in 64 32; do
+for band in 64; do
   SLATE_AMD_HB2ST=device timeout -k 10 300 python -u tools/heev_phases.py 16384 256 $band > gpurun_out/heev_phases_$band.log 2>&1 || { cat gpurun_out/heev_phases_$band.log; exit 1; }
   grep -v amdgpu.ids gpurun_out/heev_phases_$band.log | grep -v "  host"
 done
+mkdir -p gpurun_out/pc_heev2
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pc_heev2 -o heev -- python3 tools/heev_phases.py 16384 256 > gpurun_out/pc_heev2/run.log 2>&1
+find gpurun_out/pc_heev2 -name "*kernel_trace.csv" -size +50M -delete
+python3 tools/prof_csv_summary.py gpurun_out/pc_heev2 14 || true
