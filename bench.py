@@ -101,6 +101,7 @@ def main():
     ap.add_argument("--vectors", type=int, default=1, help="heev: 1 = eigenvectors (dsyevd), 0 = values only")
     ap.add_argument("--band", type=int, default=0, help="heev: stage-1 bandwidth (default min(nb, 64))")
     ap.add_argument("--lookahead", type=int, default=1)
+    ap.add_argument("--method", default="pp", choices=["pp", "calu", "nopiv"], help="getrf: pivoting method")
     ap.add_argument("--grid", default=None, help="PxQ override")
     ap.add_argument("--check", type=int, default=1, help="residual check after timing (1 rank)")
     args = ap.parse_args()
@@ -129,6 +130,8 @@ def main():
         A.insertLocalTiles(device=dev)
         sl.generate_matrix(A, "rands", seed=7)
         piv = sl.Pivots()
+        opts[sl.Option.MethodLU] = {"pp": sl.MethodLU.PartialPiv, "calu": sl.MethodLU.CALU,
+                                    "nopiv": sl.MethodLU.NoPiv}[args.method]
         run = lambda: sl.getrf(A, piv, opts)
     elif args.routine == "geqrf":
         m = args.m or n

@@ -290,24 +290,41 @@ unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const
     __shared__ double Vr[TB * SV];
     __shared__ double Zs[TCW * SZ];
     __shared__ double Ws[TB * SW];
-    __shared__ i64 sslot[TB];
+    __shared__ i64 ssp[TB], snt[TB];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int li = lane & 15, lk = lane >> 4;
     const i64 c0 = (i64)blockIdx.x * TCW;
     const int ncw = (int)min((i64)TCW, ncols - c0);
     // window row w of group t lives in Zs at column-major row ((w >> 6) + t) & 1) * 64 + (w & 63)
     auto zrow = [](int w, i64 t) { return (int)((((w >> 6) + t) & 1) * TB + (w & (TB - 1))); };
-    // global <-> LDS: one wave streams 64 consecutive rows of a column
-    auto load_half = [&](i64 row0, int phys) {
-        for (int cc = wv; cc < TCW; cc += 4) {
-            const i64 row = row0 + lane;
-            double v = 0.0;
-            if (cc < ncw && row < n) v = Z[(c0 + cc) * ldz + row];
-            Zs[cc * SZ + phys * TB + lane] = v;
+    // register staging (software pipeline): thread (wv, lane) moves element
+    // (row lane, column wv + 4 i) of a Z half and reflector element
+    // (jj = wv + 4 i, vi = lane) of a group, i < 16
+    constexpr int PR = TB * TB / 256;
+    double pv[PR], pt[PR], pz[PR];
+    auto fetch_v = [&](i64 t) {
+        #pragma unroll
+        for (int i = 0; i < PR; ++i) {
+            const int jj = wv + 4 * i;
+            pv[i] = (t < snt[jj]) ? V[(ssp[jj] + t) * TB + lane] : 0.0;
         }
     };
+    auto fetch_z = [&](i64 row0) {
+        #pragma unroll
+        for (int i = 0; i < PR; ++i) {
+            const int cc = wv + 4 * i;
+            const i64 row = row0 + lane;
+            pz[i] = (cc < ncw && row < n) ? Z[(c0 + cc) * ldz + row] : 0.0;
+        }
+    };
+    auto put_z = [&](int phys) {
+        #pragma unroll
+        for (int i = 0; i < PR; ++i) Zs[(wv + 4 * i) * SZ + phys * TB + lane] = pz[i];
+    };
     auto store_half = [&](i64 row0, int phys) {
-        for (int cc = wv; cc < TCW; cc += 4) {
+        #pragma unroll
+        for (int i = 0; i < PR; ++i) {
+            const int cc = wv + 4 * i;
             const i64 row = row0 + lane;
             if (cc < ncw && row < n) Z[(c0 + cc) * ldz + row] = Zs[cc * SZ + phys * TB + lane];
         }
@@ -318,23 +335,28 @@ unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const
         if (TJ <= 0) continue;
         i64 w0 = j0 + 1;
         __syncthreads();
-        load_half(w0, 0);
-        load_half(w0 + TB, 1);
+        if (tid < TB) {
+            ssp[tid] = tid < jn ? sp[j0 + tid] : 0;
+            snt[tid] = tid < jn ? nt[j0 + tid] : 0;       // missing sweeps: no tasks
+        }
+        fetch_z(w0);
+        put_z(0);
+        fetch_z(w0 + TB);
+        put_z(1);
+        __syncthreads();
+        fetch_v(0);
         for (i64 t = 0; t < TJ; ++t) {
-            if (tid < TB) {
-                i64 slot = -1;
-                if (tid < jn && t < nt[j0 + tid]) slot = sp[j0 + tid] + t;
-                sslot[tid] = slot;
-            }
-            __syncthreads();
-            for (int idx = tid; idx < TB * TB; idx += 256) {
-                const int jj = idx / TB, vi = idx - jj * TB;
-                const i64 slot = sslot[jj];
-                Vr[jj * SV + vi] = slot >= 0 ? V[slot * TB + vi] : 0.0;
-            }
-            __syncthreads();
             const double* T = Tg + (gptr[J] + t) * TB * TB;
-            // V(w, jj) of the parallelogram
+            #pragma unroll
+            for (int i = 0; i < PR; ++i) pt[i] = T[(16 * wv + li) + (i64)(4 * i + lk) * TB];
+            #pragma unroll
+            for (int i = 0; i < PR; ++i) Vr[(wv + 4 * i) * SV + lane] = pv[i];
+            __syncthreads();
+            const bool more = t + 1 < TJ;
+            if (more) {
+                fetch_v(t + 1);                  // in flight during this group's GEMMs
+                fetch_z(w0 + 2 * TB);
+            }
             auto vg = [&](int w, int jj) {
                 const int vi = w - jj;
                 return (vi >= 0 && vi < TB) ? Vr[jj * SV + vi] : 0.0;
@@ -343,6 +365,7 @@ unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const
             d4 acc[4];
             #pragma unroll
             for (int j = 0; j < 4; ++j) acc[j] = d4{0.0, 0.0, 0.0, 0.0};
+            #pragma unroll 4
             for (int k0 = 0; k0 < 2 * TB; k0 += 4) {
                 const int w = k0 + lk;
                 const double a = vg(w, 16 * wv + li);
@@ -358,16 +381,16 @@ unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const
                 #pragma unroll
                 for (int r = 0; r < 4; ++r) Ws[(16 * wv + lk + 4 * r) * SW + 16 * j + li] = acc[j][r];
             __syncthreads();
-            // (2) W = T W
+            // (2) W = T W (T rows of this wave prefetched into pt)
             #pragma unroll
             for (int j = 0; j < 4; ++j) acc[j] = d4{0.0, 0.0, 0.0, 0.0};
-            for (int k0 = 0; k0 < TB; k0 += 4) {
-                const int kk = k0 + lk;
-                const double a = T[(16 * wv + li) + (i64)kk * TB];
+            #pragma unroll
+            for (int i = 0; i < PR; ++i) {
+                const int kk = 4 * i + lk;
                 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const double b = Ws[kk * SW + 16 * j + li];
-                    acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[j], 0, 0, 0);
+                    acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(pt[i], b, acc[j], 0, 0, 0);
                 }
             }
             __syncthreads();
@@ -385,6 +408,7 @@ unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const
                 for (int j = 0; j < 4; ++j)
                     #pragma unroll
                     for (int r = 0; r < 4; ++r) zc[j][r] = Zs[(16 * j + li) * SZ + zrow(wb + lk + 4 * r, t)];
+                #pragma unroll 4
                 for (int k0 = 0; k0 < TB; k0 += 4) {
                     const int jj = k0 + lk;
                     const double a = -vg(wb + li, jj);
@@ -400,11 +424,12 @@ unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const
                     for (int r = 0; r < 4; ++r) Zs[(16 * j + li) * SZ + zrow(wb + lk + 4 * r, t)] = zc[j][r];
             }
             __syncthreads();
-            if (t + 1 < TJ) {
-                // the top half (physical t & 1) is final: out, and the next B rows in
+            if (more) {
+                // the top half (physical t & 1) is final: out, and the
+                // prefetched next B rows in
                 const int ph = (int)(t & 1);
                 store_half(w0, ph);
-                load_half(w0 + 2 * TB, ph);
+                put_z(ph);
                 w0 += TB;
             }
         }

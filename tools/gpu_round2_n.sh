@@ -12,3 +12,5 @@ mkdir -p gpurun_out/pc_heev2
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pc_heev2 -o heev -- python3 tools/heev_phases.py 16384 256 > gpurun_out/pc_heev2/run.log 2>&1
 find gpurun_out/pc_heev2 -name "*kernel_trace.csv" -size +50M -delete
 python3 tools/prof_csv_summary.py gpurun_out/pc_heev2 14 || true
+timeout -k 10 240 python -u bench.py --routine getrf --method calu --lookahead 2 --steps 2 --warmup 1 > gpurun_out/bench_getrf_calu.log 2>&1 || { tail -20 gpurun_out/bench_getrf_calu.log; exit 1; }
+grep -h '"metric"' gpurun_out/bench_getrf_calu.log
