@@ -29,7 +29,6 @@
 namespace slate_hip {
 
 namespace {
-constexpr int HT = 256;   // threads per workgroup
 constexpr int HMAXB = 128;
 constexpr i64 HLDS = 96 * 1024;   // bytes of the LDS staging buffer
 }
@@ -39,38 +38,38 @@ constexpr i64 HLDS = 96 * 1024;   // bytes of the LDS staging buffer
 // is wave-uniform, so the index arithmetic stays on the scalar unit, and U
 // global loads are in flight before the LDS writes (a plain loop waits for
 // each load in turn: the window then streams at a few GB/s).
-template <int U, typename F>
+template <int U, int NW, typename F>
 __device__ inline void for_pairs(int nrow, int ncol, int lane, int w, F&& body) {
     const int npr = (nrow + 63) >> 6;                     // row groups of 64
-    const int ncw = (ncol - w + 3) >> 2;                   // this wave's columns
+    const int ncw = (ncol - w + NW - 1) / NW;              // this wave's columns
     const int tot = ncw * npr;
     for (int base = 0; base < tot; base += U) body(base, npr, min(U, tot - base));
     (void)lane;
 }
 
-template <typename T, typename Src, typename Dst>
+template <typename T, int NW, typename Src, typename Dst>
 __device__ inline void move2d(int nrow, int ncol, int lane, int w, Src src, Dst dst) {
     constexpr int U = 12;
-    for_pairs<U>(nrow, ncol, lane, w, [&](int base, int npr, int cnt) {
+    for_pairs<U, NW>(nrow, ncol, lane, w, [&](int base, int npr, int cnt) {
         T tmp[U];
         #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (u < cnt) {
-                const int p = base + u, c = w + 4 * (p / npr), r = lane + 64 * (p % npr);
+                const int p = base + u, c = w + NW * (p / npr), r = lane + 64 * (p % npr);
                 if (r < nrow) tmp[u] = src(r, c);
             }
         }
         #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (u < cnt) {
-                const int p = base + u, c = w + 4 * (p / npr), r = lane + 64 * (p % npr);
+                const int p = base + u, c = w + NW * (p / npr), r = lane + 64 * (p % npr);
                 if (r < nrow) dst(r, c) = tmp[u];
             }
         }
     });
 }
 
-template <typename T>
+template <typename T, int HT>
 __global__ void __launch_bounds__(HT)
 hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __restrict__ tauv,
              i64* __restrict__ rowv, i64* __restrict__ lenv, const i64* __restrict__ sweep_ptr,
@@ -170,7 +169,7 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
                 for (i64 c0 = lo; c0 <= hi; c0 += cw) {
                     const int nc = (int)min<i64>(cw, hi - c0 + 1);
                     T* Ab = &At(s, c0);
-                    move2d<T>(k, nc, lane, w, [&](int r, int c) -> T { return Ab[r + c * lda]; },
+                    move2d<T, HT / 64>(k, nc, lane, w, [&](int r, int c) -> T { return Ab[r + c * lda]; },
                               [&](int r, int c) -> T& { return L[c * KP + r]; });
                     __syncthreads();
                     if (tid < nc) {
@@ -198,7 +197,7 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
                         for (; r < k; ++r) Lc[r] = s_sub(Lc[r], s_mul(v[r], acc));
                     }
                     __syncthreads();
-                    move2d<T>(k, nc, lane, w, [&](int r, int c) -> T { return L[c * KP + r]; },
+                    move2d<T, HT / 64>(k, nc, lane, w, [&](int r, int c) -> T { return L[c * KP + r]; },
                               [&](int r, int c) -> T& { return Ab[r + c * lda]; });
                     __syncthreads();
                 }
@@ -210,7 +209,7 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
                 for (i64 r0 = lo; r0 <= hi; r0 += rw) {
                     const int nr = (int)min<i64>(rw, hi - r0 + 1);
                     T* Ab = &At(r0, s);
-                    move2d<T>(nr, k, lane, w, [&](int r, int c) -> T { return Ab[r + c * lda]; },
+                    move2d<T, HT / 64>(nr, k, lane, w, [&](int r, int c) -> T { return Ab[r + c * lda]; },
                               [&](int r, int c) -> T& { return L[c * nr + r]; });
                     __syncthreads();
                     if (tid < nr) {
@@ -236,7 +235,7 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
                         for (; c < k; ++c) L[c * nr + tid] = s_sub(L[c * nr + tid], s_mul(y, s_conj(v[c])));
                     }
                     __syncthreads();
-                    move2d<T>(nr, k, lane, w, [&](int r, int c) -> T { return L[c * nr + r]; },
+                    move2d<T, HT / 64>(nr, k, lane, w, [&](int r, int c) -> T { return L[c * nr + r]; },
                               [&](int r, int c) -> T& { return Ab[r + c * lda]; });
                     __syncthreads();
                 }
@@ -268,12 +267,6 @@ void hb2st_device(i64 n, int b, T* A, i64 lda, T* V, T* tau, i64* row, i64* len,
     if (nsw <= 0) return;
     if (b > HMAXB) throw std::invalid_argument("hb2st_device: bandwidth > 128");
     // work = [ticket, done[0..nsw)] zero-initialised by the caller
-    static bool attr = false;
-    if (!attr) {
-        HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&hb2st_kernel<T>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)HLDS));
-        attr = true;
-    }
     // The chase hands windows between workgroups on different XCDs: with
     // the default (L2-cached, non-coherent across XCDs) memory every hand-off
     // writes back and invalidates a whole L2.  SLATE_AMD_HB2ST_MEM=uncached
@@ -290,8 +283,23 @@ void hb2st_device(i64 n, int b, T* A, i64 lda, T* V, T* tau, i64* row, i64* len,
                                         mode == 2 ? hipDeviceMallocUncached : hipDeviceMallocFinegrained));
         HIP_CHECK(hipMemcpyAsync(W, A, bytes, hipMemcpyDeviceToDevice, s));
     }
-    hipLaunchKernelGGL(hb2st_kernel<T>, dim3((unsigned)nwg), dim3(HT), HLDS, s, n, b, W, lda, V, tau, row, len,
-                       sweep_ptr, ntask, work, work + 1, nsw, 4, prof);
+    // threads per workgroup: the task's window moves are latency bound (loads
+    // in flight per workgroup), SLATE_AMD_HB2ST_THREADS = 256 | 512 | 1024;
+    // dsyevd n = 16384, b = 64: chase 3.93 / 2.78 / 2.61 s
+    static const int threads = [] {
+        const char* e = getenv("SLATE_AMD_HB2ST_THREADS");
+        const int v = e ? atoi(e) : 1024;
+        return (v == 256 || v == 512) ? v : 1024;
+    }();
+    auto launch = [&](auto kern, int ht) {
+        HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)HLDS));
+        hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(ht), HLDS, s, n, b, W, lda, V, tau, row, len,
+                           sweep_ptr, ntask, work, work + 1, nsw, 4, prof);
+    };
+    if (threads == 1024) launch(hb2st_kernel<T, 1024>, 1024);
+    else if (threads == 512) launch(hb2st_kernel<T, 512>, 512);
+    else launch(hb2st_kernel<T, 256>, 256);
     HIP_LAUNCH_CHECK();
     if (mode) {
         HIP_CHECK(hipMemcpyAsync(A, W, bytes, hipMemcpyDeviceToDevice, s));

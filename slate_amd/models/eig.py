@@ -195,11 +195,11 @@ def _hb2st_device(B: torch.Tensor, nb: int, dev):
 def hb2st(B: torch.Tensor, nb: int, device=None):
     """Hermitian band (dense copy, both triangles, bandwidth nb) -> real
     symmetric tridiagonal (d, e) + reflectors.  On the GPU when ``device``
-    is a CUDA device and SLATE_AMD_HB2ST=device, otherwise on the pipelined
-    host threads."""
+    is a CUDA device (SLATE_AMD_HB2ST=host forces the pipelined host
+    threads: 4.6 s vs 2.6 s on the GPU at n = 16384, b = 64)."""
     import os
     if device is not None and torch.device(device).type == "cuda" and \
-            os.environ.get("SLATE_AMD_HB2ST", "host") != "host" and max(1, nb) <= 128:
+            os.environ.get("SLATE_AMD_HB2ST", "device") != "host" and max(1, nb) <= 128:
         Bh, V, tau, row, ln, sp, cnt = _hb2st_device(B, nb, torch.device(device))
         return _hb2st_finish(Bh, V, tau, row, ln, sp, cnt)
     n = B.shape[0]
