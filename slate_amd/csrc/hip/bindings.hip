@@ -168,6 +168,12 @@ static void register_kernels(py::module& m) {
                                 P<const i64>(len), first, count, conj_tau, S(st)); });
     });
     m.def("geqrf_work_bytes", []() { return (i64)geqrf_work_bytes(); });
+    m.def("tpqrt_panel", [](char dt, i64 mm, i64 l, i64 j0, int ib, uintptr_t A, i64 lda, uintptr_t B, i64 ldb,
+                            uintptr_t V, i64 ldv, uintptr_t tau, uintptr_t Tm, i64 ldt, uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            tpqrt_panel<T>(mm, l, j0, ib, P<T>(A), lda, P<T>(B), ldb, P<T>(V), ldv, P<T>(tau), P<T>(Tm), ldt,
+                           S(st)); });
+    });
     m.def("v_explicit", [](char dt, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t V, i64 ldv, uintptr_t st) {
         dispatch(dt, [&](auto z) { using T = decltype(z);
             v_explicit<T>(mm, n, P<T>(A), lda, P<T>(V), ldv, S(st)); });

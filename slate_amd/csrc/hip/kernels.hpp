@@ -77,6 +77,10 @@ template <typename T>
 void geqrf_panel_ws(i64 m, i64 n, T* A, i64 lda, T* tau, T* Tm, i64 ldt, T* V, i64 ldv, void* work,
                     hipStream_t s);
 size_t geqrf_work_bytes();
+// tpqrt.hip
+template <typename T>
+void tpqrt_panel(i64 m, i64 l, i64 j0, int ib, T* A, i64 lda, T* B, i64 ldb, T* V, i64 ldv, T* tau, T* Tm,
+                 i64 ldt, hipStream_t s);
 template <typename T>
 void hb2st_device(i64 n, int b, T* A, i64 lda, T* V, T* tau, i64* row, i64* len, const i64* sweep_ptr,
                   const i64* ntask, int* work, i64 nsw, int nwg, hipStream_t s, i64* prof = nullptr);

@@ -282,6 +282,73 @@ void tb2bd(i64 n, i64 b, T* a, i64 lda, Refl& ul, Refl& vr, i64* uptr, i64* vptr
     if (n >= 1) { uptr[n - 1] = ul.cnt; vptr[n - 1] = vr.cnt; }
 }
 
+// Pipelined multi-threaded tb2bd (SLATE src/tb2bd.cc:159, 280-289 runs the
+// sweeps as OpenMP tasks guarded by a progress vector).  Task t of sweep j is
+// one iteration of the sequential loop above (a right reflector on a row,
+// then a left reflector on the columns it filled); its windows lie in
+// [j + (t - 2) b, j + (t + 3) b + 1], so every task of sweep j - 1 from
+// t + 8 on is strictly to the right: sweep j runs task t once sweep j - 1
+// has completed min(t + 8, all) tasks, which keeps every pair of
+// overlapping tasks in the sequential order (bitwise the sequential
+// result).  Thread r owns sweeps r, r + T, ...; reflectors go to the fixed
+// slots uptr[j] + t / vptr[j] + t, i.e. the sequential layout.
+template <typename T>
+void tb2bd_mt(i64 n, i64 b, T* a, i64 lda, Refl& ul, Refl& vr, i64* uptr, i64* vptr, int nthreads) {
+    Dense<T> A{a, lda};
+    const i64 w = 2 * b + 1, D = 8;
+    const i64 nsw = std::max<i64>(n - 1, 0);
+    std::vector<i64> ntask(std::max<i64>(nsw, 1), 0);
+    i64 total = 0;
+    for (i64 j = 0; j < nsw; ++j) {
+        uptr[j] = vptr[j] = total;
+        i64 ce = std::min(j + b, n - 1), t = 1;
+        while (ce + 1 <= n - 1) { ce = std::min(ce + b, n - 1); ++t; }
+        ntask[j] = t;
+        total += t;
+    }
+    if (n >= 1) uptr[n - 1] = vptr[n - 1] = total;
+    if (total > ul.cap || total > vr.cap) throw std::runtime_error("reflector store overflow");
+    std::vector<std::atomic<i64>> done(std::max<i64>(nsw, 1));
+    for (auto& d : done) d.store(0, std::memory_order_relaxed);
+    const int T_ = (int)std::max<i64>(1, std::min<i64>(nthreads, nsw));
+    auto worker = [&](int r) {
+        std::vector<T> v(b + 1), x(b + 1);
+        for (i64 j = r; j < nsw; j += T_) {
+            i64 cs = j + 1, ce = std::min(j + b, n - 1), row = j;
+            for (i64 t = 0; t < ntask[j]; ++t) {
+                if (j > 0) {
+                    const i64 need = std::min(t + D, ntask[j - 1]);
+                    while (done[j - 1].load(std::memory_order_acquire) < need) std::this_thread::yield();
+                }
+                if (t > 0) { cs = ce + 1; ce = std::min(cs + b - 1, n - 1); }
+                const i64 k = ce - cs + 1;
+                for (i64 c = 0; c < k; ++c) v[c] = cj(A(row, cs + c));
+                T tau; R_t<T> beta;
+                hgen(k, v.data(), tau, beta);
+                apply_right(A, cs, k, v.data(), tau, std::max<i64>(0, cs - w), std::min(n - 1, ce + w));
+                A(row, cs) = T(beta);
+                for (i64 c = 1; c < k; ++c) A(row, cs + c) = T(0);
+                vr.put_at(vptr[j] + t, cs, k, v.data(), tau);
+                const i64 rs = cs, re = std::min(std::min(cs + b - 1, n - 1), ce), kr = re - rs + 1;
+                for (i64 q = 0; q < kr; ++q) x[q] = A(rs + q, cs);
+                T tl; R_t<T> bl;
+                hgen(kr, x.data(), tl, bl);
+                apply_left(A, rs, kr, x.data(), tl, std::max<i64>(0, rs - w), std::min(n - 1, re + w));
+                A(rs, cs) = T(bl);
+                for (i64 q = 1; q < kr; ++q) A(rs + q, cs) = T(0);
+                ul.put_at(uptr[j] + t, rs, kr, x.data(), tl);
+                row = rs;
+                done[j].store(t + 1, std::memory_order_release);
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int r = 1; r < T_; ++r) th.emplace_back(worker, r);
+    worker(0);
+    for (auto& x : th) x.join();
+    ul.cnt = vr.cnt = total;
+}
+
 // ---------------------------------------------------------------- rotations
 // apply a sequence of plane rotations to columns (i, i+1) of Z for all rows
 // in parallel: Z(:, i), Z(:, i+1) <- c*Z_i - s*Z_{i+1}, s*Z_i + c*Z_{i+1}
@@ -602,7 +669,11 @@ void register_eig(py::module& m) {
                 using T = decltype(z);
                 Refl ul{(void*)UV, (void*)Utau, P<i64>(Urow), P<i64>(Ulen), b, cap};
                 Refl vr{(void*)VV, (void*)Vtau, P<i64>(Vrow), P<i64>(Vlen), b, cap};
-                tb2bd<T>(n, b, P<T>(A), lda, ul, vr, P<i64>(uptr), P<i64>(vptr));
+                int nth = 0;
+                if (const char* e = std::getenv("SLATE_AMD_TB2BD_THREADS")) nth = std::atoi(e);
+                if (nth <= 0) nth = (int)std::min<unsigned>(32u, std::max(1u, std::thread::hardware_concurrency()));
+                if (nth == 1) tb2bd<T>(n, b, P<T>(A), lda, ul, vr, P<i64>(uptr), P<i64>(vptr));
+                else tb2bd_mt<T>(n, b, P<T>(A), lda, ul, vr, P<i64>(uptr), P<i64>(vptr), nth);
                 cu = ul.cnt; cv = vr.cnt;
             });
         }

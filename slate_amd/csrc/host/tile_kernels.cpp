@@ -370,6 +370,68 @@ void geqrf(i64 m, i64 n, T* A, i64 lda, T* tau) {
     }
 }
 
+// tpqrt panel (host form of csrc/hip/tpqrt.hip): QR of [A; B] for the ib
+// columns j0.. of an n x n upper triangle A (pointer at A(j0, j0)) over an
+// m x n pentagon B (pointer at B(0, j0)); explicit V (m x ib, zeros outside
+// the pentagon), tau, and the panel's ib x ib compact-WY T.
+template <typename T>
+void tpqrt_panel(i64 m, i64 l, i64 j0, i64 ib, T* A, i64 lda, T* B, i64 ldb, T* V, i64 ldv, T* tau, T* Tm,
+                 i64 ldt) {
+    using R = typename real_of<T>::type;
+    auto rows = [&](i64 gc) { return std::min(m, m - l + std::min(l, gc + 1)); };
+    for (i64 i = 0; i < ib; ++i) {
+        const i64 pi = rows(j0 + i);
+        const T x0 = A[i + i * lda];
+        R xn2 = 0;
+        for (i64 r = 0; r < pi; ++r) xn2 += std::norm(B[r + i * ldb]);
+        const R ar = std::real(x0), ai = std::imag(x0);
+        T t(0);
+        R beta = ar;
+        const bool trivial = (xn2 == R(0) && ai == R(0));
+        if (!trivial) {
+            beta = -std::copysign(std::sqrt(ar * ar + ai * ai + xn2), ar);
+            if constexpr (std::is_same<T, R>::value) t = T((beta - ar) / beta);
+            else t = T((beta - ar) / beta, -ai / beta);
+        }
+        const T den = x0 - T(beta);
+        for (i64 r = 0; r < m; ++r) {
+            T v(0);
+            if (r < pi) {
+                v = trivial ? T(0) : B[r + i * ldb] / den;
+                B[r + i * ldb] = v;
+            }
+            V[r + i * ldv] = v;
+        }
+        A[i + i * lda] = T(beta);
+        tau[i] = t;
+        const T ct = conj_(t);
+        if (ct == T(0)) continue;
+        for (i64 c = i + 1; c < ib; ++c) {
+            T acc(0);
+            for (i64 r = 0; r < pi; ++r) acc += conj_(V[r + i * ldv]) * B[r + c * ldb];
+            const T wv = ct * (A[i + c * lda] + acc);
+            for (i64 r = 0; r < pi; ++r) B[r + c * ldb] -= V[r + i * ldv] * wv;
+            A[i + c * lda] -= wv;
+        }
+    }
+    const i64 pmax = ib ? rows(j0 + ib - 1) : 0;
+    for (i64 i = 0; i < ib; ++i) {
+        for (i64 a = 0; a < ib; ++a) if (a > i) Tm[a + i * ldt] = T(0);
+        std::vector<T> g(i);
+        for (i64 a = 0; a < i; ++a) {
+            T acc(0);
+            for (i64 r = 0; r < pmax; ++r) acc += conj_(V[r + a * ldv]) * V[r + i * ldv];
+            g[a] = acc;
+        }
+        for (i64 a = 0; a < i; ++a) {
+            T acc(0);
+            for (i64 k = a; k < i; ++k) acc += Tm[a + k * ldt] * g[k];
+            Tm[a + i * ldt] = -tau[i] * acc;
+        }
+        Tm[i + i * ldt] = tau[i];
+    }
+}
+
 // gelqf: LQ via Householder on rows.
 template <typename T>
 void gelqf(i64 m, i64 n, T* A, i64 lda, T* tau) {
@@ -705,6 +767,12 @@ void register_tile_kernels(py::module& m) {
     m.def("geqrf", [](char dt, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t tau) {
         py::gil_scoped_release nogil;
         dispatch(dt, [&](auto z) { using T = decltype(z); geqrf<T>(mm, n, P<T>(A), lda, P<T>(tau)); });
+    });
+    m.def("tpqrt_panel", [](char dt, i64 mm, i64 l, i64 j0, int ib, uintptr_t A, i64 lda, uintptr_t B, i64 ldb,
+                            uintptr_t V, i64 ldv, uintptr_t tau, uintptr_t Tm, i64 ldt, uintptr_t) {
+        py::gil_scoped_release nogil;
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            tpqrt_panel<T>(mm, l, j0, ib, P<T>(A), lda, P<T>(B), ldb, P<T>(V), ldv, P<T>(tau), P<T>(Tm), ldt); });
     });
     m.def("gelqf", [](char dt, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t tau) {
         py::gil_scoped_release nogil;

@@ -240,6 +240,11 @@ def _geqrf_general(A, buf, T, la):
     ss.join()
 
 
+import os as _os
+# stacked-R reduction of the TSQR tree by tpqrt (default) or a plain QR of the stack
+_TREE_TPQRT = _os.environ.get("SLATE_AMD_TSQR_TPQRT", "1") != "0"
+
+
 def _tsqr_panel(buf, mloc, pr, p, colc, pk, st, dt, dev):
     """Ranks of the panel's process column: local QR of the own panel rows,
     all-gather of the R factors, redundant QR of the stack."""
@@ -259,8 +264,16 @@ def _tsqr_panel(buf, mloc, pr, p, colc, pk, st, dt, dev):
             o = st["soff"][r]
             S[o:o + st["kr"][r]].copy_(allR[r].t()[:st["kr"][r]])
     ks = st["ks"]
-    Vf = ops.colmajor_empty(st["tot"], ks, dt, dev)
-    ops.geqrf(S, pk.get("tauh")[:, 0], pk.get("Th"), Vf)
+    if st["kr"][st["rk"]] == kb == ks and _TREE_TPQRT:
+        # the stack's top block is R_rk (upper triangular): triangle-
+        # pentagonal QR (tile::tpqrt) -- the reflectors' top parts are unit
+        # vectors, the triangle is never filled, and V = [I; V_B]
+        Vf = ops.colmajor_zeros(st["tot"], ks, dt, dev)
+        Vf[:ks].diagonal().fill_(1)
+        ops.tpqrt(0, S[:ks], S[ks:], pk.get("Th"), Vf[ks:], pk.get("tauh")[:, 0])
+    else:
+        Vf = ops.colmajor_empty(st["tot"], ks, dt, dev)
+        ops.geqrf(S, pk.get("tauh")[:, 0], pk.get("Th"), Vf)
     if km:
         o = st["soff"][pr]
         pk.get("Vh").copy_(Vf[o:o + km])

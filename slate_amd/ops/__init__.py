@@ -289,6 +289,117 @@ def geqrf(A, tau, T=None, V=None):
     return T, V
 
 
+def tpqrt(l, A, B, T=None, V=None, tau=None, ib=32):
+    """Triangle-pentagonal QR (tile::tpqrt, src/internal/Tile_tpqrt.hh:142):
+    QR of [A; B] with A n x n upper triangular and B m x n pentagonal (the
+    last ``l`` rows upper trapezoidal, l = 0: B full, l = min(m, n): B
+    triangular).  R overwrites A's upper triangle, the reflectors' B parts
+    overwrite B's pentagon; Q = I - [I; V] T [I; V]^H.  Returns (T, V, tau)
+    with T the full n x n compact-WY factor and V the explicit m x n
+    reflector block (zeros outside the pentagon).
+
+    Blocked: each ib-column panel by one workgroup (csrc/hip/tpqrt.hip),
+    the tile's trailing columns by the block reflector as MFMA GEMM/TRMM
+    (tprfb), and the panel T's merged into the full T by
+    T12 = -T11 (V1^H V2) T22 (the unit top parts of the reflectors are
+    disjoint, so only V_B enters)."""
+    _chk(A); _chk(B, "B")
+    m, n = B.shape
+    if A.shape[0] < n or A.shape[1] != n:
+        raise SlateError("tpqrt: A must be n x n with n = B.shape[1]")
+    if not 0 <= l <= min(m, n) and not (l == m == 0):
+        raise SlateError("tpqrt: need 0 <= l <= min(m, n)")
+    dt, dev = B.dtype, B.device
+    if T is None:
+        T = colmajor_zeros(n, n, dt, dev)
+    if V is None:
+        V = colmajor_zeros(m, n, dt, dev)
+    if tau is None:
+        tau = torch.zeros(n, dtype=dt, device=dev)
+    if n == 0:
+        return T, V, tau
+    if m == 0:
+        tau.zero_()
+        T.zero_()
+        return T, V, tau
+    ib = max(1, min(int(ib), 64))
+    mod = kmod(B)
+    ct = 'C' if dt.is_complex else 'T'
+    for j0 in range(0, n, ib):
+        jb = min(ib, n - j0)
+        mod.tpqrt_panel(code(dt), m, int(l), j0, jb, A[j0:, j0:].data_ptr(), ld(A), B[:, j0:].data_ptr(), ld(B),
+                        V[:, j0:].data_ptr(), ld(V), tau[j0:].data_ptr(), T[j0:, j0:].data_ptr(), ld(T), stream(B))
+        if j0 + jb < n:
+            tpmqrt('L', 'C', V[:, j0:j0 + jb], T[j0:j0 + jb, j0:j0 + jb], A[j0:j0 + jb, j0 + jb:], B[:, j0 + jb:])
+        if j0:
+            G = T[:j0, j0:j0 + jb]
+            gemm(1.0, V[:, :j0], V[:, j0:j0 + jb], 0.0, G, transA=ct)
+            trmm('L', 'U', 'N', 'N', 1.0, T[:j0, :j0], G)
+            trmm('R', 'U', 'N', 'N', -1.0, T[j0:j0 + jb, j0:j0 + jb], G)
+    return T, V, tau
+
+
+def tpmqrt(side, trans, V, T, A, B):
+    """Apply Q (trans 'N') or Q^H ('C'/'T') of a tpqrt factorization,
+    Q = I - [I; V] T [I; V]^H, to the stacked pair (tile::tpmqrt,
+    src/internal/Tile_tpmqrt.hh:99): side 'L' acts on [A; B] (A k x nc,
+    B m x nc), side 'R' on [A B] (A nr x k, B nr x m).  Three MFMA
+    GEMM-class launches plus a copy: W = A + V^H B (or A + B V),
+    W = op(T) W (or W op(T)), A -= W, B -= V W (or W V^H)."""
+    _chk(A); _chk(B, "B"); _chk(V, "V")
+    dt = B.dtype
+    ct = 'C' if dt.is_complex else 'T'
+    conj = _ch(trans) != 'N'
+    k = T.shape[0]
+    if k == 0:
+        return A, B
+    if _ch(side) == 'L':
+        nc = A.shape[1]
+        if nc == 0:
+            return A, B
+        W = colmajor_empty(k, nc, dt, A.device)
+        W.copy_(A)
+        gemm(1.0, V, B, 1.0, W, transA=ct)
+        trmm('L', 'U', ct if conj else 'N', 'N', 1.0, T, W)
+        geadd(-1.0, W, 1.0, A)
+        gemm(-1.0, V, W, 1.0, B)
+    else:
+        nr = A.shape[0]
+        if nr == 0:
+            return A, B
+        W = colmajor_empty(nr, k, dt, A.device)
+        W.copy_(A)
+        gemm(1.0, B, V, 1.0, W)
+        trmm('R', 'U', ct if conj else 'N', 'N', 1.0, T, W)
+        geadd(-1.0, W, 1.0, A)
+        gemm(-1.0, W, V, 1.0, B, transB=ct)
+    return A, B
+
+
+def tplqt(l, A, B, ib=32):
+    """Triangle-pentagonal LQ (tile::tplqt, src/internal/Tile_tplqt.hh:145):
+    LQ of [A B] with A k x k lower triangular and B k x m pentagonal (the
+    last ``l`` columns lower trapezoidal).  Computed as the tpqrt of the
+    conjugate transposes; L overwrites A's lower triangle, the reflectors'
+    B parts overwrite B.  Returns (T, W, tau): Q = I - [I W] T^H [I W]^H
+    acting on the right, W = V^H (k x m)."""
+    Ah = as_colmajor(A.mH.contiguous())
+    Bh = as_colmajor(B.mH.contiguous())
+    T, V, tau = tpqrt(l, Ah, Bh, ib=ib)
+    A.copy_(Ah.mH)
+    B.copy_(Bh.mH)
+    return T, as_colmajor(V.mH.contiguous()), tau
+
+
+def tpmlqt(side, trans, W, T, A, B):
+    """Apply Q or Q^H of a tplqt factorization (tile::tpmlqt,
+    src/internal/Tile_tpmlqt.hh:99).  The LQ factor of [A B] is the
+    conjugate transpose of the QR factor of [A; B]^H, so Q_lq = Q_qr^H with
+    V = W^H: this is tpmqrt with the transposition flipped."""
+    V = as_colmajor(W.mH.contiguous())
+    return tpmqrt(side, 'N' if _ch(trans) != 'N' else 'C', V, T, A, B)
+
+
 def v_explicit(A, V):
     """V = unit-lower-trapezoidal part of A (reflectors), zeros above."""
     m, k = V.shape
