@@ -146,6 +146,14 @@ static void register_kernels(py::module& m) {
     }, py::arg("dt"), py::arg("n"), py::arg("b"), py::arg("A"), py::arg("lda"), py::arg("V"), py::arg("tau"),
        py::arg("row"), py::arg("len"), py::arg("sweep_ptr"), py::arg("ntask"), py::arg("work"), py::arg("nsw"),
        py::arg("nwg"), py::arg("st"), py::arg("prof") = 0);
+    m.def("tb2bd", [](char dt, i64 n, int b, uintptr_t A, i64 lda, uintptr_t UV, uintptr_t Utau, uintptr_t Urow,
+                      uintptr_t Ulen, uintptr_t VV, uintptr_t Vtau, uintptr_t Vrow, uintptr_t Vlen, uintptr_t sweep_ptr,
+                      uintptr_t ntask, uintptr_t work, i64 nsw, int nwg, uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            tb2bd_device<T>(n, b, P<T>(A), lda, P<T>(UV), P<T>(Utau), P<i64>(Urow), P<i64>(Ulen), P<T>(VV), P<T>(Vtau),
+                            P<i64>(Vrow), P<i64>(Vlen), P<const i64>(sweep_ptr), P<const i64>(ntask), P<int>(work),
+                            nsw, nwg, S(st)); });
+    });
     m.def("unmtr_hb2st_blocked", [](char dt, i64 n, i64 ncols, uintptr_t Z, i64 ldz, uintptr_t V, i64 b,
                                     uintptr_t tau, uintptr_t sp, uintptr_t nt, i64 nsw, bool conj_tau, uintptr_t st) {
         bool ok = false;

@@ -308,6 +308,197 @@ void hb2st_device(i64 n, int b, T* A, i64 lda, T* V, T* tau, i64* row, i64* len,
     }
 }
 
+// ---------------------------------------------------------------- tb2bd
+// Upper band -> upper bidiagonal (SVD stage 2; SLATE src/tb2bd.cc with
+// internal_gebr.cc gebr1/2/3 on host threads).  Same task graph as the
+// host pipeline (csrc/host/eig.cpp tb2bd_mt): task t of sweep j generates
+// the right reflector that annihilates row `row` beyond column cs and
+// applies it to the rows of columns cs..ce, then the left reflector that
+// annihilates column cs below the diagonal and applies it to the columns
+// of rows cs..re.  Sweep j runs task t once sweep j-1 has completed
+// min(t + 8, all) tasks.  The windows are the exact non-zero extents:
+// columns cs..ce hold rows [row, ce] (band + the fill of the previous left
+// reflector), rows cs..re hold columns [cs, re + b].
+template <typename T, int HT>
+__global__ void __launch_bounds__(HT)
+tb2bd_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ UV, T* __restrict__ Utau,
+             i64* __restrict__ Urow, i64* __restrict__ Ulen, T* __restrict__ VV, T* __restrict__ Vtau,
+             i64* __restrict__ Vrow, i64* __restrict__ Vlen, const i64* __restrict__ sweep_ptr,
+             const i64* __restrict__ ntask, int* ticket, int* done, i64 nsw, int D) {
+    using R = typename scalar_traits<T>::real;
+    __shared__ T v[HMAXB];
+    extern __shared__ unsigned char hb_smem[];
+    T* L = reinterpret_cast<T*>(hb_smem);
+    __shared__ T s_tau;
+    __shared__ R s_beta;
+    __shared__ int s_j;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    auto At = [&](i64 r, i64 c) -> T& { return A[r + c * lda]; };
+    // Householder generator on v[0..k) (wave 0): v <- v / (v0 - beta), v0 = 1
+    auto hgen = [&](int k) {
+        T x0 = s_zero(T());
+        R xn2 = 0;
+        for (int r = lane; r < k; r += 64) {
+            const T x = v[r];
+            if (r == 0) x0 = x;
+            else xn2 += s_real(s_mul(s_conj(x), x));
+        }
+        xn2 = wave_sum(xn2);
+        x0 = wave_sum(x0);
+        const R ar = s_real(x0);
+        R ai = 0;
+        if constexpr (scalar_traits<T>::is_complex) ai = x0.im;
+        T tau;
+        R beta;
+        const bool trivial = (xn2 == R(0) && ai == R(0));
+        if (trivial) {
+            tau = s_zero(T());
+            beta = ar;
+        } else {
+            beta = -copysign(sqrt(ar * ar + ai * ai + xn2), ar);
+            if constexpr (scalar_traits<T>::is_complex) tau = T{(beta - ar) / beta, -ai / beta};
+            else tau = (beta - ar) / beta;
+        }
+        T den = x0;
+        if constexpr (scalar_traits<T>::is_complex) den.re -= beta;
+        else den -= beta;
+        for (int r = lane; r < k; r += 64) {
+            if (r == 0) v[0] = s_from_real(T(), R(1));
+            else if (!trivial) v[r] = s_div(v[r], den);
+        }
+        if (lane == 0) { s_tau = tau; s_beta = beta; }
+    };
+    for (;;) {
+        if (tid == 0) s_j = atomicAdd(ticket, 1);
+        __syncthreads();
+        const i64 j = s_j;
+        __syncthreads();
+        if (j >= nsw) return;
+        const i64 nt = ntask[j];
+        i64 cs = j + 1, ce = min(j + (i64)b, n - 1), row = j;
+        for (i64 t = 0; t < nt; ++t) {
+            if (j > 0) {
+                const i64 need = min(t + (i64)D, ntask[j - 1]);
+                if (tid == 0)
+                    while (__hip_atomic_load(&done[j - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need)
+                        __builtin_amdgcn_s_sleep(2);
+                __syncthreads();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            }
+            if (t > 0) { cs = ce + 1; ce = min(cs + (i64)b - 1, n - 1); }
+            const int k = (int)(ce - cs + 1);
+            const i64 slot = sweep_ptr[j] + t;
+            // ---- right reflector: x = conj(A(row, cs..ce))
+            if (w == 0) {
+                for (int c = lane; c < k; c += 64) v[c] = s_conj(At(row, cs + c));
+                hgen(k);
+            }
+            __syncthreads();
+            {
+                const T tau = s_tau;
+                const i64 lo = row, hi = ce;                 // rows holding columns cs..ce
+                if (!s_is_zero(tau)) {
+                    // A(r, cs..ce) -= (tau A(r, cs..ce) v) v^H, a thread per row
+                    const i64 rw = max<i64>(1, min<i64>(hi - lo + 1, min<i64>(HT, HLDS / ((i64)k * (i64)sizeof(T)))));
+                    for (i64 r0 = lo; r0 <= hi; r0 += rw) {
+                        const int nr = (int)min<i64>(rw, hi - r0 + 1);
+                        T* Ab = &At(r0, cs);
+                        move2d<T, HT / 64>(nr, k, lane, w, [&](int r, int c) -> T { return Ab[r + c * lda]; },
+                                           [&](int r, int c) -> T& { return L[c * nr + r]; });
+                        __syncthreads();
+                        if (tid < nr) {
+                            T y = s_zero(T());
+                            for (int c = 0; c < k; ++c) y = s_add(y, s_mul(L[c * nr + tid], v[c]));
+                            y = s_mul(y, tau);
+                            for (int c = 0; c < k; ++c)
+                                L[c * nr + tid] = s_sub(L[c * nr + tid], s_mul(y, s_conj(v[c])));
+                        }
+                        __syncthreads();
+                        move2d<T, HT / 64>(nr, k, lane, w, [&](int r, int c) -> T { return L[c * nr + r]; },
+                                           [&](int r, int c) -> T& { return Ab[r + c * lda]; });
+                        __syncthreads();
+                    }
+                }
+                for (int c = tid; c < k; c += HT) At(row, cs + c) = c == 0 ? s_from_real(T(), s_beta) : s_zero(T());
+                for (int c = tid; c < b; c += HT) VV[slot * b + c] = c < k ? v[c] : s_zero(T());
+                if (tid == 0) { Vtau[slot] = tau; Vrow[slot] = cs; Vlen[slot] = k; }
+            }
+            __syncthreads();
+            // ---- left reflector: x = A(cs..re, cs)
+            const i64 rs = cs, re = min(min(cs + (i64)b - 1, n - 1), ce);
+            const int kr = (int)(re - rs + 1);
+            if (w == 0) {
+                for (int r = lane; r < kr; r += 64) v[r] = At(rs + r, cs);
+                hgen(kr);
+            }
+            __syncthreads();
+            {
+                const T tau = s_tau;
+                const i64 lo = cs, hi = min(n - 1, re + (i64)b);   // columns holding rows rs..re
+                if (!s_is_zero(tau)) {
+                    const T ct = s_conj(tau);
+                    const int KP = kr + 1;
+                    const i64 cw = max<i64>(1, min<i64>(min<i64>(hi - lo + 1, HT), HLDS / ((i64)KP * (i64)sizeof(T))));
+                    for (i64 c0 = lo; c0 <= hi; c0 += cw) {
+                        const int nc = (int)min<i64>(cw, hi - c0 + 1);
+                        T* Ab = &At(rs, c0);
+                        move2d<T, HT / 64>(kr, nc, lane, w, [&](int r, int c) -> T { return Ab[r + c * lda]; },
+                                           [&](int r, int c) -> T& { return L[c * KP + r]; });
+                        __syncthreads();
+                        if (tid < nc) {
+                            T* Lc = L + tid * KP;
+                            T acc = s_zero(T());
+                            for (int r = 0; r < kr; ++r) acc = s_add(acc, s_mul(s_conj(v[r]), Lc[r]));
+                            acc = s_mul(ct, acc);
+                            for (int r = 0; r < kr; ++r) Lc[r] = s_sub(Lc[r], s_mul(v[r], acc));
+                        }
+                        __syncthreads();
+                        move2d<T, HT / 64>(kr, nc, lane, w, [&](int r, int c) -> T { return L[c * KP + r]; },
+                                           [&](int r, int c) -> T& { return Ab[r + c * lda]; });
+                        __syncthreads();
+                    }
+                }
+                for (int r = tid; r < kr; r += HT) At(rs + r, cs) = r == 0 ? s_from_real(T(), s_beta) : s_zero(T());
+                for (int r = tid; r < b; r += HT) UV[slot * b + r] = r < kr ? v[r] : s_zero(T());
+                if (tid == 0) { Utau[slot] = tau; Urow[slot] = rs; Ulen[slot] = kr; }
+            }
+            row = rs;
+            __syncthreads();
+            if (tid == 0)
+                __hip_atomic_store(&done[j], (int)(t + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+template <typename T>
+void tb2bd_device(i64 n, int b, T* A, i64 lda, T* UV, T* Utau, i64* Urow, i64* Ulen, T* VV, T* Vtau, i64* Vrow,
+                  i64* Vlen, const i64* sweep_ptr, const i64* ntask, int* work, i64 nsw, int nwg, hipStream_t s) {
+    if (nsw <= 0) return;
+    if (b > HMAXB) throw std::invalid_argument("tb2bd_device: bandwidth > 128");
+    // work = [ticket, done[0..nsw)] zero-initialised by the caller; the
+    // chase runs on an uncached working copy (cross-XCD hand-offs, as hb2st)
+    T* W = nullptr;
+    const size_t bytes = sizeof(T) * (size_t)lda * (size_t)n;
+    HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&W), bytes, hipDeviceMallocUncached));
+    HIP_CHECK(hipMemcpyAsync(W, A, bytes, hipMemcpyDeviceToDevice, s));
+    constexpr int HT = 256;
+    auto kern = tb2bd_kernel<T, HT>;
+    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)HLDS));
+    hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(HT), HLDS, s, n, b, W, lda, UV, Utau, Urow, Ulen, VV, Vtau,
+                       Vrow, Vlen, sweep_ptr, ntask, work, work + 1, nsw, 8);
+    HIP_LAUNCH_CHECK();
+    HIP_CHECK(hipMemcpyAsync(A, W, bytes, hipMemcpyDeviceToDevice, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    HIP_CHECK(hipFree(W));
+}
+
+#define INST(T) \
+    template void tb2bd_device<T>(i64, int, T*, i64, T*, T*, i64*, i64*, T*, T*, i64*, i64*, const i64*, \
+                                  const i64*, int*, i64, int, hipStream_t);
+INST(float) INST(double) INST(ccplx) INST(zcplx)
+#undef INST
+
 #define INST(T) \
     template void hb2st_device<T>(i64, int, T*, i64, T*, T*, i64*, i64*, const i64*, const i64*, int*, i64, int, \
                                   hipStream_t, i64*);

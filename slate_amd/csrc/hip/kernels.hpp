@@ -85,6 +85,9 @@ template <typename T>
 void hb2st_device(i64 n, int b, T* A, i64 lda, T* V, T* tau, i64* row, i64* len, const i64* sweep_ptr,
                   const i64* ntask, int* work, i64 nsw, int nwg, hipStream_t s, i64* prof = nullptr);
 template <typename T>
+void tb2bd_device(i64 n, int b, T* A, i64 lda, T* UV, T* Utau, i64* Urow, i64* Ulen, T* VV, T* Vtau, i64* Vrow,
+                  i64* Vlen, const i64* sweep_ptr, const i64* ntask, int* work, i64 nsw, int nwg, hipStream_t s);
+template <typename T>
 void apply_refl_batch(i64 ncols, T* Z, i64 ldz, const T* V, i64 b, const T* tau, const i64* row, const i64* len,
                       i64 first, i64 count, bool conj_tau, hipStream_t s);
 template <typename T>

@@ -77,29 +77,84 @@ class Tb2bdFactors:
         self.U, self.V, self.pu, self.pv = U, V, pu, pv
 
 
-def tb2bd(B: torch.Tensor, nb: int):
-    """Upper band (dense host copy, bandwidth nb) -> real bidiagonal (d, e)
-    plus reflectors and phases (host native bulge chase)."""
+def _tb2bd_schedule(n, b):
+    """Tasks per sweep of the bidiagonal chase (one right + one left
+    reflector each) and the first reflector slot of every sweep."""
+    j = torch.arange(max(n - 1, 0), dtype=torch.int64)
+    ce0 = torch.clamp(j + b, max=n - 1)
+    nt = 1 + torch.div(n - 1 - ce0 + b - 1, b, rounding_mode="floor")
+    sp = torch.zeros(max(n, 1), dtype=torch.int64)
+    if n > 1:
+        sp[1:n] = torch.cumsum(nt, 0)
+    return nt, sp
+
+
+def _tb2bd_device(B: torch.Tensor, b: int, dev):
+    """Bidiagonal bulge chasing on the GPU (csrc/hip/hb2st.hip tb2bd_kernel):
+    persistent workgroups take sweeps from an atomic ticket, progress
+    counters between consecutive sweeps (lag 8), reflectors in the host
+    pipeline's slots."""
     n = B.shape[0]
-    Bh = _cm(B.detach().to("cpu").clone())
-    Bh = _cm(Bh)
-    b = max(1, nb)
-    cap = n * (n // b + 2) + 1
-    dt = Bh.dtype
+    dt = B.dtype
+    ldp = -(-n // 8) * 8 + 72                  # leading dimension off powers of two
+    A = torch.empty((n, ldp), dtype=dt, device=dev).t()[:n]
+    A.copy_(B.to(dev))
+    nt, sp = _tb2bd_schedule(n, b)
+    total = int(nt.sum()) if nt.numel() else 0
+    cap = max(total, 1)
 
     def store():
-        return (torch.zeros(cap, b, dtype=dt), torch.zeros(cap, dtype=dt), torch.zeros(cap, dtype=torch.int64),
-                torch.zeros(cap, dtype=torch.int64))
-    UV, Ut, Ur, Ul = store()
-    VV, Vt, Vr, Vl = store()
-    up = torch.zeros(max(n, 1), dtype=torch.int64)
-    vp = torch.zeros(max(n, 1), dtype=torch.int64)
+        return (torch.zeros(cap, b, dtype=dt, device=dev), torch.zeros(cap, dtype=dt, device=dev),
+                torch.zeros(cap, dtype=torch.int64, device=dev), torch.zeros(cap, dtype=torch.int64, device=dev))
+    U = store()
+    V = store()
+    nsw = max(n - 1, 0)
+    work = torch.zeros(nsw + 2, dtype=torch.int32, device=dev)
+    ntd, spd = nt.to(dev), sp.to(dev)
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    nt0 = int(nt[0]) if nt.numel() else 1
+    nwg = int(min(max(nsw, 1), cus, max(8, nt0 // 8 + 8)))
     with trace_block("tb2bd"):
-        cu, cv = _native._host.tb2bd(_code(dt), n, b, Bh.data_ptr(), max(1, Bh.stride(1)), UV.data_ptr(),
-                                     Ut.data_ptr(), Ur.data_ptr(), Ul.data_ptr(), VV.data_ptr(), Vt.data_ptr(),
-                                     Vr.data_ptr(), Vl.data_ptr(), cap, up.data_ptr(), vp.data_ptr())
-    dc = Bh.diagonal().clone()
-    ec = Bh.diagonal(1).clone()
+        if nsw > 0:
+            _native._hip.tb2bd(_code(dt), n, b, A.data_ptr(), A.stride(1), *(x.data_ptr() for x in U),
+                               *(x.data_ptr() for x in V), spd.data_ptr(), ntd.data_ptr(), work.data_ptr(), nsw, nwg,
+                               torch.cuda.current_stream(dev).cuda_stream)
+    return A, U, V, sp, total
+
+
+def tb2bd(B: torch.Tensor, nb: int):
+    """Upper band (dense copy, bandwidth nb) -> real bidiagonal (d, e) plus
+    reflectors and phases.  On the GPU when B is there (bandwidth <= 128;
+    SLATE_AMD_TB2BD=host forces the pipelined host threads)."""
+    import os
+    n = B.shape[0]
+    b = max(1, nb)
+    if B.is_cuda and b <= 128 and os.environ.get("SLATE_AMD_TB2BD", "device") != "host":
+        Ad, (UV, Ut, Ur, Ul), (VV, Vt, Vr, Vl), up, cu = _tb2bd_device(B, b, B.device)
+        cv = cu
+        vp = up
+        dt = Ad.dtype
+        dc = Ad.diagonal().cpu().clone()
+        ec = Ad.diagonal(1).cpu().clone()
+    else:
+        Bh = _cm(B.detach().to("cpu").clone())
+        Bh = _cm(Bh)
+        cap = n * (n // b + 2) + 1
+        dt = Bh.dtype
+
+        def store():
+            return (torch.zeros(cap, b, dtype=dt), torch.zeros(cap, dtype=dt), torch.zeros(cap, dtype=torch.int64),
+                    torch.zeros(cap, dtype=torch.int64))
+        UV, Ut, Ur, Ul = store()
+        VV, Vt, Vr, Vl = store()
+        up = torch.zeros(max(n, 1), dtype=torch.int64)
+        vp = torch.zeros(max(n, 1), dtype=torch.int64)
+        with trace_block("tb2bd"):
+            cu, cv = _native._host.tb2bd(_code(dt), n, b, Bh.data_ptr(), max(1, Bh.stride(1)), UV.data_ptr(),
+                                         Ut.data_ptr(), Ur.data_ptr(), Ul.data_ptr(), VV.data_ptr(), Vt.data_ptr(),
+                                         Vr.data_ptr(), Vl.data_ptr(), cap, up.data_ptr(), vp.data_ptr())
+        dc = Bh.diagonal().clone()
+        ec = Bh.diagonal(1).clone()
     d = torch.zeros(n, dtype=torch.float64)
     e = torch.zeros(max(n - 1, 0), dtype=torch.float64)
     pu = torch.ones(n, dtype=dt)

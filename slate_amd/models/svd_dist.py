@@ -346,7 +346,7 @@ def svd_dist(A, S=None, U=None, VH=None, opts=None):
             for which, cnt in (("U", int(meta[0])), ("V", int(meta[1]))):
                 if comm.rank == 0:
                     F = getattr(F2, which)
-                    t = (F.V, F.tau, F.row, F.length, F.sweep_ptr)
+                    t = tuple(x.cpu() for x in (F.V, F.tau, F.row, F.length, F.sweep_ptr))
                 else:
                     t = (torch.zeros(cnt, band, dtype=dt), torch.zeros(cnt, dtype=dt),
                          torch.zeros(cnt, dtype=torch.int64), torch.zeros(cnt, dtype=torch.int64),

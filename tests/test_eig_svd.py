@@ -364,3 +364,49 @@ def test_tb2bd_pipelined_equals_sequential(dt, n, b, monkeypatch):
     s_ref = torch.linalg.svdvals(A)
     Bd = torch.diag(d1) + torch.diag(e1, 1)
     assert torch.allclose(torch.linalg.svdvals(Bd), s_ref, atol=1e-12 * s_ref[0].item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float64, torch.complex128])
+@pytest.mark.parametrize("n,b", [(300, 8), (257, 64), (100, 1), (130, 128)])
+def test_tb2bd_gpu_equals_host(dt, n, b, monkeypatch):
+    """GPU bidiagonal chase (tight windows, persistent workgroups) against
+    the host pipeline: same bidiagonal and reflectors to rounding."""
+    g = torch.Generator().manual_seed(n * b)
+    A = torch.randn(n, n, dtype=dt, generator=g)
+    i = torch.arange(n)
+    dlt = i[None, :] - i[:, None]
+    A = torch.where((dlt >= 0) & (dlt <= b), A, torch.zeros_like(A))
+    d1, e1, F1 = S.tb2bd(A.clone(), b)
+    d2, e2, F2 = S.tb2bd(A.clone().cuda(), b)
+    sc = A.abs().max().item() * n
+    assert (d1 - d2).abs().max().item() < 1e-13 * sc
+    assert (e1 - e2).abs().max().item() < 1e-13 * sc
+    for a, c in ((F1.U, F2.U), (F1.V, F2.V)):
+        assert a.count == c.count
+        assert torch.equal(a.row, c.row.cpu()) and torch.equal(a.length, c.length.cpu())
+    # the device reflectors reproduce the band (reflectors of near-zero
+    # columns are only defined to rounding, so compare their action):
+    # A = Q_U diag(pu) B diag(pv)^H Q_V^H with B the real bidiagonal
+    QU = E.unmtr_hb2st(F2.U, torch.eye(n, dtype=dt, device="cuda").t())
+    QV = E.unmtr_hb2st(F2.V, torch.eye(n, dtype=dt, device="cuda").t())
+    Bd = (torch.diag(d2) + torch.diag(e2, 1)).to(dt)
+    R = QU.cpu() @ torch.diag(F2.pu) @ Bd @ torch.diag(F2.pv).mH @ QV.cpu().mH - A
+    assert R.abs().max().item() < 1e-13 * sc
+
+
+@pytest.mark.gpu
+def test_svd_gpu_complex():
+    dev = torch.device("cuda")
+    m, n = 260, 200
+    A = sl.Matrix(m, n, nb=64, dtype=torch.complex128, device=dev)
+    A.insertLocalTiles(device=0)
+    sl.generate_matrix(A, "rands", 11)
+    Ad = D(A).clone()
+    U = sl.Matrix(m, n, nb=64, dtype=torch.complex128, device=dev)
+    U.insertLocalTiles(device=0)
+    VH = sl.Matrix(n, n, nb=64, dtype=torch.complex128, device=dev)
+    VH.insertLocalTiles(device=0)
+    s = sl.svd(A, None, U, VH, {Option.InnerBlocking: 32})
+    assert (s.cpu() - torch.linalg.svdvals(Ad.cpu())).abs().max().item() < 1e-11
+    assert (D(U) @ torch.diag(s.to(dev).to(torch.complex128)) @ D(VH) - Ad).abs().max().item() < 1e-11
