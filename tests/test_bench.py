@@ -43,3 +43,14 @@ def test_bench_json(nproc, routine):
     assert d["config"]["n"] == 512
     if nproc == 1:
         assert d["residual"] is not None and d["residual"] < 1e-12
+
+
+@pytest.mark.parametrize("nproc,grid", [(4, "2x2"), (8, "2x4")])
+@pytest.mark.parametrize("routine", ["potrf", "getrf"])
+def test_bench_json_many_ranks(nproc, grid, routine):
+    """The driver's N = 4 / 8 launches: the default grids (BASELINE: 2x4 at
+    8 GPUs), one JSON line, info 0 on every rank."""
+    d = _run(nproc, routine)
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == nproc and d["config"]["grid"] == grid
+    assert d["info_ok"] is True and d["value"] > 0
