@@ -86,6 +86,11 @@ def lu_solve_nopiv(A, B, opts=None):
     return gesv_nopiv(A, B, opts)
 
 
+def getrs_tntpiv(A, pivots, B, opts=None):
+    """Solve with CALU factors (the pivots are an ordinary row permutation)."""
+    return getrs(A, pivots, B, opts)
+
+
 def lu_solve_using_factor(A, pivots, B, opts=None):
     return getrs(A, pivots, B, opts)
 
@@ -127,8 +132,9 @@ def least_squares_solve(A, BX, opts=None):
 
 
 from .models.eig import (  # noqa: F401,E402
-    eig, eig_vals, hb2st, he2hb, heev, hegst, hegv, stedc, steqr, sterf, unmtr_hb2st, unmtr_he2hb)
-from .models.svd import bdsqr, ge2tb, svd, svd_vals, tb2bd  # noqa: F401,E402
+    eig, eig_vals, hb2st, he2hb, heev, hegst, hegv, stedc, stedc_deflate, stedc_secular, stedc_sort,
+    stedc_z_vector, steqr, sterf, unmtr_hb2st, unmtr_he2hb)
+from .models.svd import bdsqr, ge2tb, svd, svd_vals, tb2bd, unmbr_ge2tb, unmbr_tb2bd  # noqa: F401,E402
 
 
 from .models.inverse import trtri, trtrm  # noqa: F401,E402
@@ -167,6 +173,16 @@ def indefinite_solve(A, B, opts=None):
 
 
 from .models.aux import set_lambda  # noqa: F401,E402
+
+
+def gbnorm(norm_type, A, opts=None):
+    """Norm of a general band matrix (computed from the in-band tiles)."""
+    return norm(norm_type, A, opts)
+
+
+def hbnorm(norm_type, A, opts=None):
+    """Norm of a Hermitian band matrix (stored triangle + its reflection)."""
+    return norm(norm_type, A, opts)
 from .utils.printing import print_matrix, print_vector, format_matrix  # noqa: F401,E402
 from .utils.debug import Debug  # noqa: F401,E402
 from .models.svd import ge2tb as ge2tb_, svd_vals  # noqa: F401,E402

@@ -264,7 +264,7 @@ static void register_kernels(py::module& m) {
         dispatch(dt, [&](auto z) { using T = decltype(z); using R = typename scalar_traits<T>::real;
             butterfly<T, R>(trans, rows, depth, nidx, nother, P<T>(A), lda, P<R>(diag), ldd, S(st)); });
     });
-    m.def("genorm", [](char dt, char norm, char uplo, char diag, bool herm, i64 mm, i64 n, uintptr_t A, i64 lda,
+    m.def("genorm", [](char dt, char norm, char uplo, char diag, int herm, i64 mm, i64 n, uintptr_t A, i64 lda,
                        uintptr_t out, uintptr_t st) {
         dispatch(dt, [&](auto z) { using T = decltype(z); using R = typename scalar_traits<T>::real;
             genorm<T, R>(norm, uplo, diag, herm, mm, n, P<T>(A), lda, P<R>(out), S(st)); });

@@ -59,7 +59,7 @@ void sel_to_ipiv(const i64* sel, i64 kb, i64 r0, i64* ipiv, hipStream_t s);
 // (scale/sumsq pairs -> here plain sum of squares with scaling by the max);
 // out receives per-column (one), per-row (inf) or a single value.
 template <typename T, typename R>
-void genorm(char norm, char uplo, char diag, bool herm, i64 m, i64 n, const T* A, i64 lda, R* out,
+void genorm(char norm, char uplo, char diag, int herm, i64 m, i64 n, const T* A, i64 lda, R* out,
             hipStream_t s);
 
 // getrf.hip

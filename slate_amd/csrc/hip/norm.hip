@@ -42,14 +42,15 @@ __device__ inline void ssq_combine(R& s1, R& q1, R s2, R q2) {
 
 template <typename T, typename R>
 __global__ void __launch_bounds__(256)
-norm_col_kernel(char norm, char uplo, bool unit, bool herm, i64 m, i64 n, const T* A, i64 lda,
+norm_col_kernel(char norm, char uplo, bool unit, int herm, i64 m, i64 n, const T* A, i64 lda,
                 R* colout, R* rowout) {
     __shared__ R s1[256], s2[256];
     for (i64 j = blockIdx.x; j < n; j += gridDim.x) {
         R acc = 0, sc = 0, sq = 1;
         for (i64 i = threadIdx.x; i < m; i += 256) {
             if (!keep(uplo, i, j)) continue;
-            R v = (i == j && unit) ? R(1) : s_abs(A[i + j * lda]);
+            // herm 2: Hermitian -- only the real part of the diagonal is referenced (LAPACK lanhe)
+            R v = (i == j && unit) ? R(1) : (i == j && herm == 2) ? fabs(s_real(A[i + j * lda])) : s_abs(A[i + j * lda]);
             if (norm == 'M') acc = nmax(acc, v);
             else if (norm == 'F') {
                 R w = (herm && i != j) ? v : v;
@@ -96,7 +97,7 @@ __global__ void norm_row_kernel(char uplo, bool unit, i64 m, i64 n, const T* A, 
 }
 
 template <typename T, typename R>
-void genorm(char norm, char uplo, char diag, bool herm, i64 m, i64 n, const T* A, i64 lda, R* out,
+void genorm(char norm, char uplo, char diag, int herm, i64 m, i64 n, const T* A, i64 lda, R* out,
             hipStream_t s) {
     // out layout: [ colout (n, or 2n for 'F') | rowout (m) ]  -- zeroed by caller
     if (m <= 0 || n <= 0) return;
@@ -116,9 +117,9 @@ void genorm(char norm, char uplo, char diag, bool herm, i64 m, i64 n, const T* A
     HIP_LAUNCH_CHECK();
 }
 
-template void genorm<float, float>(char, char, char, bool, i64, i64, const float*, i64, float*, hipStream_t);
-template void genorm<double, double>(char, char, char, bool, i64, i64, const double*, i64, double*, hipStream_t);
-template void genorm<ccplx, float>(char, char, char, bool, i64, i64, const ccplx*, i64, float*, hipStream_t);
-template void genorm<zcplx, double>(char, char, char, bool, i64, i64, const zcplx*, i64, double*, hipStream_t);
+template void genorm<float, float>(char, char, char, int, i64, i64, const float*, i64, float*, hipStream_t);
+template void genorm<double, double>(char, char, char, int, i64, i64, const double*, i64, double*, hipStream_t);
+template void genorm<ccplx, float>(char, char, char, int, i64, i64, const ccplx*, i64, float*, hipStream_t);
+template void genorm<zcplx, double>(char, char, char, int, i64, i64, const zcplx*, i64, double*, hipStream_t);
 
 }  // namespace slate_hip

@@ -533,7 +533,7 @@ void gecopy(char uplo, char trans, i64 m, i64 n, const Ts* A, i64 lda, Td* B, i6
         }
 }
 template <typename T>
-void genorm(char norm, char uplo, char diag, bool herm, i64 m, i64 n, const T* A, i64 lda, real_t<T>* out) {
+void genorm(char norm, char uplo, char diag, int herm, i64 m, i64 n, const T* A, i64 lda, real_t<T>* out) {
     using R = real_t<T>;
     R* col = out;
     R* row = out + (norm == 'F' ? 2 * n : n);
@@ -543,7 +543,9 @@ void genorm(char norm, char uplo, char diag, bool herm, i64 m, i64 n, const T* A
             if (uplo == 'L' && i < j) continue;
             if (uplo == 'U' && i > j) continue;
             if (uplo == 'D' && i != j) continue;
-            R v = (i == j && diag == 'U') ? R(1) : std::abs(A[i + j * lda]);
+            // herm 2: Hermitian -- only the real part of the diagonal is referenced (LAPACK lanhe)
+            R v = (i == j && diag == 'U') ? R(1) : (i == j && herm == 2) ? std::abs(std::real(A[i + j * lda]))
+                                                                    : std::abs(A[i + j * lda]);
             int reps = (herm && i != j) ? 2 : 1;
             if (norm == 'M') { if (std::isnan(v) || v > acc || std::isnan(acc)) acc = std::isnan(acc) ? acc : v; }
             else if (norm == 'F') {
@@ -792,7 +794,7 @@ void register_tile_kernels(py::module& m) {
             dispatch(dd, [&](auto zd) { using Td = decltype(zd);
                 gecopy<Ts, Td>(uplo, trans, mm, n, P<Ts>(A), lda, P<Td>(B), ldb); }); });
     });
-    m.def("genorm", [](char dt, char norm, char uplo, char diag, bool herm, i64 mm, i64 n, uintptr_t A, i64 lda,
+    m.def("genorm", [](char dt, char norm, char uplo, char diag, int herm, i64 mm, i64 n, uintptr_t A, i64 lda,
                        uintptr_t out, uintptr_t) {
         py::gil_scoped_release nogil;
         dispatch(dt, [&](auto z) { using T = decltype(z);

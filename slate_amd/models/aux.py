@@ -457,6 +457,7 @@ def norm(norm_type, A, opts=None, scope=NormScope.Matrix):
         return _dense_norm(nt, D, A)
     kind = _diag_kind(A)
     herm = kind in ("hermitian", "symmetric")
+    hv = (2 if kind == "hermitian" and s.dtype.is_complex else 1) if herm else 0   # kernel flag
     diag = 'U' if getattr(A, "_diag", None) is not None and A._diag.value == 'U' and kind == "trapezoid" else 'N'
     # op: norms of A^T swap One <-> Inf
     if A.op() != Op.NoTrans and not herm:
@@ -501,14 +502,14 @@ def norm(norm_type, A, opts=None, scope=NormScope.Matrix):
             on_diag = u != 'G'
             if herm and code in ('1', 'I'):
                 if on_diag:
-                    c, r = ops.genorm_local('1', blk, uplo=u, herm=True)
+                    c, r = ops.genorm_local('1', blk, uplo=u, herm=hv)
                 else:
                     c, _ = ops.genorm_local('1', blk)
                     _, r = ops.genorm_local('I', blk)
                 colv.index_add_(0, gc_t, c)
                 rowv.index_add_(0, gr_t, r)
                 continue
-            c, r = ops.genorm_local(code, blk, uplo=u, diag=diag, herm=herm and on_diag)
+            c, r = ops.genorm_local(code, blk, uplo=u, diag=diag, herm=hv if on_diag else 0)
             if code == 'M':
                 colv.index_put_((gc_t,), torch.maximum(colv[gc_t], c))
                 if torch.isnan(c).any():
@@ -556,7 +557,12 @@ def _dense_norm(nt, D, A):
     kind = _diag_kind(A)
     if kind in ("hermitian", "symmetric"):
         L = torch.tril(D) if A.uploPhysical() == Uplo.Lower else torch.triu(D)
-        D = L + L.transpose(0, 1).conj() - torch.diag(torch.diagonal(L))
+        if kind == "hermitian":
+            # only the real part of the diagonal is referenced (LAPACK lanhe)
+            D = L + L.mH
+            D.diagonal().copy_(torch.diagonal(L).real.to(D.dtype))
+        else:
+            D = L + L.transpose(0, 1) - torch.diag(torch.diagonal(L))
     elif kind == "trapezoid":
         D = torch.tril(D) if A.uploPhysical() == Uplo.Lower else torch.triu(D)
     a = D.abs()

@@ -343,44 +343,35 @@ def _dc(d, e, dev, leaf):
     return w, U
 
 
-def _rank_one_eig(dd, z, rho, Qb):
-    """Eigen-decomposition of Qb (diag(dd) + rho z z^T) Qb^T: returns
-    (ascending eigenvalues, Qb @ eigenvectors)."""
-    n = dd.numel()
-    dev = Qb.device
-    if rho == 0.0:
-        order = torch.argsort(dd)
-        return dd[order].clone(), Qb[:, order.to(dev)]
-    flip = rho < 0
-    if flip:
-        dd = -dd
-        rho = -rho
+def stedc_sort(dd, z, Q):
+    """Merge step 1 (src/stedc_sort.cc role): poles ascending, z and the
+    columns of Q permuted alike."""
     order = torch.argsort(dd)
-    dd = dd[order].clone()
-    z = z[order].clone()
-    Q = Qb[:, order.to(dev)].clone()
+    return dd[order].clone(), z[order].clone(), Q[:, order.to(Q.device)].clone()
+
+
+def stedc_deflate(dd, z, rho, Q):
+    """Merge step 2 (src/stedc_deflate.cc): deflate tiny z components and
+    (nearly) equal poles; equal poles get a Givens rotation that moves their
+    z weight into one of them (the rotation is applied to Q's columns).
+    Returns (z, keep): the non-deflated indices in ascending pole order."""
+    n = dd.numel()
     eps = torch.finfo(torch.float64).eps
-    tol = 8.0 * eps * max(dd.abs().max().item(), rho * float((z * z).sum()))
+    tol = 8.0 * eps * max(dd.abs().max().item() if n else 0.0, rho * float((z * z).sum()))
     znorm = float(z.norm())
-    # deflation of tiny z components
     defl = (rho * z.abs() * znorm <= tol)
-    # deflation of (nearly) equal poles: rotate z weight into one of them
     idx = [i for i in range(n) if not defl[i]]
     zl = z.tolist()
     dl = dd.tolist()
-    keep = []
-    rots = []
+    keep, rots = [], []
     prev = None
     for i in idx:
         if prev is not None and abs(dl[i] - dl[prev]) <= tol:
             a, b = zl[prev], zl[i]
             r = (a * a + b * b) ** 0.5
             c, s = b / r, a / r
-            # new z_prev = 0, z_i = r ; columns (prev, i) rotated
-            rots.append((prev, i, c, s))
+            rots.append((prev, i, c, s))           # new z_prev = 0, z_i = r
             zl[prev], zl[i] = 0.0, r
-            dl[prev] = dl[prev]  # eigenvalue stays (deflated)
-            defl[prev] = True
             keep[-1] = i
             prev = i
             continue
@@ -390,13 +381,57 @@ def _rank_one_eig(dd, z, rho, Qb):
         qi, qj = Q[:, i].clone(), Q[:, j].clone()
         Q[:, i] = c * qi - s * qj
         Q[:, j] = s * qi + c * qj
-    z = torch.tensor(zl, dtype=torch.float64)
-    K = torch.tensor(keep, dtype=torch.int64)
+    return torch.tensor(zl, dtype=torch.float64), torch.tensor(keep, dtype=torch.int64)
+
+
+def stedc_secular(dK, zK, rho):
+    """Merge step 3 (src/stedc_secular.cc): roots of the secular equation
+    1 + rho sum z_i^2 / (d_i - lambda) = 0 for ascending poles dK (host fp64,
+    native C++).  Returns (lambda, org, mu) with lambda_j = dK[org_j] + mu_j
+    (the root stored relative to its closest pole, as LAPACK laed4)."""
+    k = dK.numel()
+    dK = dK.to(torch.float64).contiguous()
+    zK = zK.to(torch.float64).contiguous()
+    org = torch.zeros(k, dtype=torch.int64)
+    mu = torch.zeros(k, dtype=torch.float64)
+    if k:
+        _native._host.secular(k, dK.data_ptr(), zK.data_ptr(), float(rho), org.data_ptr(), mu.data_ptr())
+    return dK[org] + mu, org, mu
+
+
+def stedc_z_vector(dK, zK, rho, org, mu):
+    """Merge step 4 (src/stedc_z_vector.cc role, Gu-Eisenstat): the z_hat
+    for which the computed roots are exact, and the normalised eigenvector
+    matrix of the rank-one problem, v_j[i] = z_hat_i / (d_i - lambda_j)."""
+    dorg = dK[org]
+    delta = (dorg[None, :] - dK[:, None]) + mu[None, :]   # lambda_j - d_i, (k x k)
+    dij = dK[None, :] - dK[:, None]                        # d_j - d_i
+    ratio = delta / torch.where(dij == 0, torch.ones_like(dij), dij)
+    ratio.fill_diagonal_(1.0)
+    zh2 = torch.diagonal(delta).clone() * torch.prod(ratio, dim=1) / rho
+    zh = torch.sign(zK) * zh2.abs().sqrt()
+    Vs = zh[:, None] / (-delta)
+    return zh, Vs / Vs.norm(dim=0, keepdim=True)
+
+
+def _rank_one_eig(dd, z, rho, Qb):
+    """Eigen-decomposition of Qb (diag(dd) + rho z z^T) Qb^T: returns
+    (ascending eigenvalues, Qb @ eigenvectors).  Sort, deflate, secular
+    roots, Gu-Eisenstat vectors, one merge GEMM (on the GPU: roots, z_hat
+    and the vector matrix by csrc/hip/stedc.hip)."""
+    dev = Qb.device
+    if rho == 0.0:
+        order = torch.argsort(dd)
+        return dd[order].clone(), Qb[:, order.to(dev)]
+    flip = rho < 0
+    if flip:
+        dd = -dd
+        rho = -rho
+    dd, z, Q = stedc_sort(dd, z, Qb)
+    z, K = stedc_deflate(dd, z, rho, Q)
     k = K.numel()
     lam = dd.clone()
     if k and dev.type == "cuda":
-        # secular roots, Gu-Eisenstat z and the normalised k x k eigenvector
-        # matrix on the GPU (csrc/hip/stedc.hip), straight into the GEMM operand
         dKd = dd[K].contiguous().to(dev)
         zKd = z[K].contiguous().to(dev)
         org = torch.empty(k, dtype=torch.int64, device=dev)
@@ -407,33 +442,16 @@ def _rank_one_eig(dd, z, rho, Qb):
                                     org.data_ptr(), mu.data_ptr(), zh.data_ptr(), VsC.data_ptr(), VsC.stride(1),
                                     torch.cuda.current_stream(dev).cuda_stream)
         lam[K] = (dKd[org] + mu).cpu()
+    elif k:
+        dK, zK = dd[K].contiguous(), z[K].contiguous()
+        lamK, org, mu = stedc_secular(dK, zK, rho)
+        _, Vs = stedc_z_vector(dK, zK, rho, org, mu)
+        lam[K] = lamK
+        VsC = ops.as_colmajor(Vs.to(dev))
+    if k:
         Kd = K.to(dev)
         QK = ops.as_colmajor(Q[:, Kd])
         Out = ops.colmajor_empty(QK.shape[0], k, Q.dtype, dev)
-        ops.gemm(1.0, QK, VsC, 0.0, Out)                 # merge GEMM on the MFMA kernels
-        Q[:, Kd] = Out
-    elif k:
-        dK = dd[K].contiguous()
-        zK = z[K].contiguous()
-        org = torch.zeros(k, dtype=torch.int64)
-        mu = torch.zeros(k, dtype=torch.float64)
-        _native._host.secular(k, dK.data_ptr(), zK.data_ptr(), float(rho), org.data_ptr(), mu.data_ptr())
-        lamK = dK[org] + mu
-        # Gu-Eisenstat: z_hat from the computed roots (orthogonal vectors)
-        dorg = dK[org]                                   # (k,)
-        delta = (dorg[None, :] - dK[:, None]) + mu[None, :]   # lambda_j - d_i, (k x k)
-        dij = dK[None, :] - dK[:, None]                  # d_j - d_i
-        ratio = delta / torch.where(dij == 0, torch.ones_like(dij), dij)
-        ratio.fill_diagonal_(1.0)
-        zh2 = torch.diagonal(delta).clone() * torch.prod(ratio, dim=1) / rho
-        zh = torch.sign(zK) * zh2.abs().sqrt()
-        Vs = zh[:, None] / (-delta)                      # v_j[i] = z_i / (d_i - lambda_j)
-        Vs = Vs / Vs.norm(dim=0, keepdim=True)
-        lam[K] = lamK
-        Kd = K.to(dev)
-        QK = ops.as_colmajor(Q[:, Kd])
-        VsC = ops.as_colmajor(Vs.to(dev))
-        Out = ops.colmajor_empty(QK.shape[0], VsC.shape[1], Q.dtype, dev)
         ops.gemm(1.0, QK, VsC, 0.0, Out)                 # merge GEMM on the MFMA kernels
         Q[:, Kd] = Out
     if flip:

@@ -202,6 +202,28 @@ def bdsqr(d: torch.Tensor, e: torch.Tensor, want_u=True, want_vt=True):
     return d, U, VT
 
 
+def unmbr_ge2tb(side, F: Ge2tbFactors, Z: torch.Tensor):
+    """Back-transform of stage 1 (src/unmbr_ge2tb.cc): side 'L' applies
+    Z := Q Z with Q the product of ge2tb's column-panel reflectors (A = Q B
+    P^H), side 'R' applies Z := P Z (the row-panel reflectors; V of the SVD
+    is P times the band's V).  Block reflectors, MFMA GEMMs."""
+    fac = F.left if str(getattr(side, "value", side))[0] in "Ll" else F.right
+    for (r0, V, T) in reversed(fac):
+        _apply_qh(V, T, Z[r0:, :], conj=False)
+    return Z
+
+
+def unmbr_tb2bd(side, F: "Tb2bdFactors", Z: torch.Tensor):
+    """Back-transform of stage 2 (src/unmbr_tb2bd.cc): side 'L' applies
+    Z := Q_U diag(pu) Z, side 'R' applies Z := Q_V diag(pv) Z, so that the
+    band B = Q_U diag(pu) Bd diag(pv)^H Q_V^H with Bd the real bidiagonal
+    (on the GPU: one blocked launch over all sweeps, csrc/hip/eig.hip)."""
+    left = str(getattr(side, "value", side))[0] in "Ll"
+    ph = F.pu if left else F.pv
+    Z.mul_(ph.to(Z.device, Z.dtype)[:, None])
+    return _unmtr_refl(F.U if left else F.V, Z)
+
+
 def _unmtr_refl(F, Z):
     from .eig import unmtr_hb2st
     return unmtr_hb2st(F, Z)

@@ -486,18 +486,19 @@ def butterfly(A, diag, depth, trans=False, side='L'):
     return A
 
 
-def genorm_local(norm, A, uplo='G', diag='N', herm=False):
+def genorm_local(norm, A, uplo='G', diag='N', herm=0):
     """Local norm contributions: returns (colvals, rowvals) real tensors on
     A's device: 'M'/'1' -> per-column max/sum, 'F' -> per-column
     (scale, sumsq) pairs (n x 2), 'I' -> per-row sums; symmetric/Hermitian
-    storage adds the mirrored contributions to rowvals."""
+    storage adds the mirrored contributions to rowvals (herm 1: symmetric,
+    2: Hermitian -- the diagonal's real part only, as LAPACK lanhe)."""
     _chk(A)
     m, n = A.shape
     rdt = _native.REAL_OF[A.dtype]
     nc = 2 * n if _ch(norm) == 'F' else n
     out = torch.zeros(nc + m, dtype=rdt, device=A.device)
     if m and n:
-        kmod(A).genorm(code(A.dtype), _ch(norm), _ch(uplo), _ch(diag), bool(herm), m, n, A.data_ptr(), ld(A),
+        kmod(A).genorm(code(A.dtype), _ch(norm), _ch(uplo), _ch(diag), int(herm), m, n, A.data_ptr(), ld(A),
                        out.data_ptr(), stream(A))
     col = out[:nc].view(n, 2) if _ch(norm) == 'F' else out[:nc]
     return col, out[nc:]

@@ -590,6 +590,436 @@ def t_matgen(c, m, n, k, **p):
     return err, t, 8.0 * m * n * n
 
 
+# ------------------------------------------------------- aux by structure
+def _struct(c, kind, m, n, uplo, seed):
+    """A general matrix of the tester's grid viewed as `kind`: ge | tz | tr |
+    he | sy (test/test_add.cc, test_copy.cc, test_scale.cc, test_set.cc,
+    test_norm.cc sweep the same five)."""
+    if kind in ("tr", "he", "sy"):
+        m = n
+    M = c.mat(m, n, seed=seed)
+    if kind == "ge":
+        return M, torch.ones(m, n, dtype=torch.bool)
+    i = torch.arange(m)[:, None]
+    j = torch.arange(n)[None, :]
+    mask = (i >= j) if uplo == Uplo.Lower else (i <= j)
+    if kind == "tz":
+        return sl.TrapezoidMatrix(uplo, matrix=M), mask
+    if kind == "tr":
+        return sl.TriangularMatrix(uplo, M), mask
+    return (sl.HermitianMatrix if kind == "he" else sl.SymmetricMatrix)(uplo, M), mask
+
+
+def _full_of(kind, Dm, mask):
+    """The operand the structure represents (Hermitian/symmetric: both
+    triangles from the stored one)."""
+    if kind in ("he", "sy"):
+        L = torch.where(mask.to(Dm.device), Dm, torch.zeros_like(Dm))
+        R = L.mH if kind == "he" else L.mT
+        F = L + R
+        F.diagonal().copy_(Dm.diagonal().real.to(Dm.dtype) if kind == "he" else Dm.diagonal())
+        return F
+    return torch.where(mask.to(Dm.device), Dm, torch.zeros_like(Dm))
+
+
+def _aux(kind, op):
+    def f(c, m, n, k, uplo=Uplo.Lower, **p):
+        A, mask = _struct(c, kind, m, n, uplo, 1)
+        Ad = D(A).clone()
+        mk = mask.to(Ad.device)
+        mm, nn = Ad.shape
+        chk = c.a.check == 'y'
+        if op == "norm":
+            v, t = c.timed(lambda: sl.norm(Norm.Fro, A, c.opts))
+            ref = torch.linalg.norm(_full_of(kind, Ad, mask))
+            return (abs(float(v) - float(ref)) / max(float(ref), 1e-300) if chk else None), t, 2.0 * mm * nn
+        if op in ("add", "copy"):
+            B, _ = _struct(c, kind, m, n, uplo, 2)
+            Bd = D(B).clone()
+            if op == "add":
+                _, t = c.timed(lambda: sl.add(2.0, A, -1.0, B, c.opts))
+                ref = torch.where(mk, 2.0 * Ad - Bd, Bd)
+            else:
+                _, t = c.timed(lambda: sl.copy(A, B, c.opts))
+                ref = torch.where(mk, Ad, Bd)
+            got = D(B)
+            return (_rel(torch.where(mk, got - ref, torch.zeros_like(got)), Ad.abs().max() + Bd.abs().max())
+                    if chk else None), t, 2.0 * mm * nn
+        if op == "scale":
+            _, t = c.timed(lambda: sl.scale(3.0, 2.0, A, c.opts))
+            ref = torch.where(mk, Ad * 1.5, Ad)
+        else:                                              # set
+            _, t = c.timed(lambda: sl.set(0.5, 2.0, A, c.opts))
+            i = torch.arange(mm, device=Ad.device)[:, None]
+            j = torch.arange(nn, device=Ad.device)[None, :]
+            val = torch.where(i == j, torch.full_like(Ad, 2.0), torch.full_like(Ad, 0.5))
+            ref = torch.where(mk, val, Ad)
+        got = D(A)
+        return (_rel(torch.where(mk, got - ref, torch.zeros_like(got)), Ad.abs().max() + 2.0) if chk else None), \
+            t, 1.0 * mm * nn
+    return f
+
+
+def t_scale_row_col(c, m, n, k, **p):
+    A = c.mat(m, n, seed=1)
+    Ad = D(A)
+    R = torch.rand(m, dtype=torch.float64, generator=torch.Generator().manual_seed(3)) + 0.5
+    Cc = torch.rand(n, dtype=torch.float64, generator=torch.Generator().manual_seed(4)) + 0.5
+    from slate_amd.core.enums import Equed
+    _, t = c.timed(lambda: sl.scale_row_col(Equed.Both, R, Cc, A, c.opts))
+    ref = Ad * R.to(Ad.device, c.dt)[:, None] * Cc.to(Ad.device, c.dt)[None, :]
+    return (_rel(D(A) - ref, Ad.abs().max() * 2.25) if c.a.check == 'y' else None), t, 2.0 * m * n
+
+
+def t_bandnorm(herm):
+    def f(c, m, n, k, uplo=Uplo.Lower, **p):
+        kd = max(1, c.a.nb // 2)
+        if herm:
+            A = sl.HermitianBandMatrix(uplo, n, kd, nb=c.a.nb, p=c.a.p, q=c.a.q, dtype=c.dt, device=c.dev)
+        else:
+            A = sl.BandMatrix(n, n, kd, kd, nb=c.a.nb, p=c.a.p, q=c.a.q, dtype=c.dt, device=c.dev)
+        A.insertLocalTiles(device=c.dev.index if c.dev.type == "cuda" else -1)
+        sl.generate_matrix(A, "rands", 1)
+        if herm:
+            sl.band_mask(A, kd, 0) if uplo == Uplo.Lower else sl.band_mask(A, 0, kd)
+            F = _herm_full(A)
+        else:
+            sl.band_mask(A)
+            F = D(A)
+        v, t = c.timed(lambda: (sl.hbnorm if herm else sl.gbnorm)(Norm.One, A, c.opts))
+        ref = torch.linalg.matrix_norm(F, 1)
+        return (abs(float(v) - float(ref)) / float(ref) if c.a.check == 'y' else None), t, 2.0 * n * kd
+    return f
+
+
+# ----------------------------------------------------- factor/solve pieces
+def t_getrf_variant(method):
+    def f(c, m, n, k, **p):
+        A = c.mat(n, n, "rand_dominant" if method == "nopiv" else "rands", 1)
+        Ad = D(A)
+        piv = sl.Pivots()
+        fn = {"nopiv": lambda: sl.getrf_nopiv(A, c.opts), "tntpiv": lambda: sl.getrf_tntpiv(A, piv, c.opts)}[method]
+        _, t = c.timed(fn)
+        if c.a.check != 'y':
+            return None, t, 2.0 * n ** 3 / 3.0
+        F = D(A)
+        L = torch.tril(F, -1) + torch.eye(n, dtype=c.dt, device=F.device)
+        PA = Ad.clone()
+        if method != "nopiv":
+            for i, pv in enumerate(piv.ipiv.tolist()):
+                if pv != i:
+                    PA[[i, pv]] = PA[[pv, i]]
+        return _rel(L @ torch.triu(F) - PA, Ad.abs().max() * n), t, 2.0 * n ** 3 / 3.0
+    return f
+
+
+def t_getrs_variant(method):
+    def f(c, m, n, k, **p):
+        A = c.mat(n, n, "rand_dominant" if method == "nopiv" else "rands", 1)
+        Ad = D(A)
+        piv = sl.Pivots()
+        if method == "nopiv":
+            sl.getrf_nopiv(A, c.opts)
+        else:
+            sl.getrf_tntpiv(A, piv, c.opts)
+        B = c.mat(n, k, seed=2)
+        Bd = D(B)
+        run = (lambda: sl.getrs_nopiv(A, B, c.opts)) if method == "nopiv" else (lambda: sl.getrs_tntpiv(A, piv, B, c.opts))
+        _, t = c.timed(run)
+        return _lu_solve_check(c, Ad, D(B), Bd, n), t, 2.0 * n * n * k
+    return f
+
+
+def t_gbtrf_gbtrs(solve):
+    def f(c, m, n, k, **p):
+        kl = ku = max(1, c.a.nb // 2)
+        A = _band(c, n, kl, ku)
+        Ad = D(A)
+        piv = sl.Pivots()
+        if not solve:
+            info, t = c.timed(lambda: sl.gbtrf(A, piv, c.opts))
+            B = c.mat(n, 1, seed=2)
+            Bd = D(B)
+            sl.gbtrs(A, piv, B, c.opts)
+            return _lu_solve_check(c, Ad, D(B), Bd, n), t, 2.0 * n * kl * (kl + ku)
+        sl.gbtrf(A, piv, c.opts)
+        B = c.mat(n, k, seed=2)
+        Bd = D(B)
+        _, t = c.timed(lambda: sl.gbtrs(A, piv, B, c.opts))
+        return _lu_solve_check(c, Ad, D(B), Bd, n), t, 2.0 * n * (2 * kl + ku) * k
+    return f
+
+
+def t_pbtrf_pbtrs(solve):
+    def f(c, m, n, k, uplo=Uplo.Lower, **p):
+        kd = max(1, c.a.nb // 2)
+        A = sl.HermitianBandMatrix(uplo, n, kd, nb=c.a.nb, p=c.a.p, q=c.a.q, dtype=c.dt, device=c.dev)
+        A.insertLocalTiles(device=c.dev.index if c.dev.type == "cuda" else -1)
+        sl.generate_matrix(A, "poev", 1)
+        sl.band_mask(A, kd, 0) if uplo == Uplo.Lower else sl.band_mask(A, 0, kd)
+        Af = _herm_full(A)
+        B = c.mat(n, k, seed=2)
+        Bd = D(B)
+        if solve:
+            sl.pbtrf(A, c.opts)
+            _, t = c.timed(lambda: sl.pbtrs(A, B, c.opts))
+        else:
+            _, t = c.timed(lambda: sl.pbtrf(A, c.opts))
+            sl.pbtrs(A, B, c.opts)
+        err = _rel(Af @ D(B) - Bd, Af.abs().max() * D(B).abs().max() * n) if c.a.check == 'y' else None
+        return err, t, (4.0 * n * kd * k) if solve else (n * kd * kd)
+    return f
+
+
+def t_hetrf_hetrs(solve):
+    def f(c, m, n, k, **p):
+        A, B = c.mat(n, n, seed=1, cls=sl.HermitianMatrix), c.mat(n, k, seed=2)
+        Af, Bd = _herm_full(A), D(B)
+        piv = sl.Pivots()
+        if solve:
+            sl.hetrf(A, piv, None, None, None, c.opts)
+            _, t = c.timed(lambda: sl.hetrs(A, piv, None, None, B, c.opts))
+        else:
+            _, t = c.timed(lambda: sl.hetrf(A, piv, None, None, None, c.opts))
+            sl.hetrs(A, piv, None, None, B, c.opts)
+        err = _rel(Af @ D(B) - Bd, Af.abs().max() * D(B).abs().max() * n) if c.a.check == 'y' else None
+        return err, t, (2.0 * n * n * k) if solve else (n ** 3 / 3.0)
+    return f
+
+
+def t_posv_mixed_gmres(c, m, n, k, uplo=Uplo.Lower, **p):
+    if c.t not in ('d', 'z'):
+        return None, 0.0, 0.0
+    A = _herm_mat(c, n, uplo, "poev")
+    Af = _herm_full(A)
+    B, X = c.mat(n, 1, seed=2), c.mat(n, 1, "zeros")
+    Bd = D(B)
+    _, t = c.timed(lambda: sl.posv_mixed_gmres(A, B, X, c.opts))
+    return _lu_solve_check(c, Af, D(X), Bd, n), t, n ** 3 / 3.0
+
+
+def t_hegst(c, m, n, k, uplo=Uplo.Lower, **p):
+    A = _herm_mat(c, n, uplo, seed=1)
+    B = _herm_mat(c, n, uplo, "poev", seed=2)
+    Af, Bf = _herm_full(A), _herm_full(B)
+    sl.potrf(B, c.opts)
+    _, t = c.timed(lambda: sl.hegst(1, A, B, c.opts))
+    if c.a.check != 'y':
+        return None, t, n ** 3
+    Fb = D(B)
+    L = torch.tril(Fb) if uplo == Uplo.Lower else torch.triu(Fb).mH
+    # itype 1: C = L^{-1} A L^{-H}; check L C L^H = A
+    C = _herm_full(A)
+    return _rel(L @ C @ L.mH - Af, Af.abs().max() * n), t, 1.0 * n ** 3
+
+
+# ------------------------------------------------ two-stage eig / SVD stages
+def _dense_cm(c, m, n, seed, herm=False):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randn(m, n, dtype=c.dt, generator=g)
+    if herm:
+        X = X + X.mH
+    return X.to(c.dev).t().contiguous().t()
+
+
+def t_he2hb(c, m, n, k, **p):
+    from slate_amd.models import eig as E
+    nb = max(2, min(c.a.nb, 64))
+    A0 = _dense_cm(c, n, n, 1, herm=True)
+    Af = A0.clone()
+    F, t = c.timed(lambda: sl.he2hb(Af, nb))
+    if c.a.check != 'y':
+        return None, t, 4.0 * n ** 3 / 3.0
+    band = E._band_only(Af, nb)
+    w0, w1 = torch.linalg.eigvalsh(A0.cpu()), torch.linalg.eigvalsh(band.cpu())
+    return _rel(w1 - w0, w0.abs().max() * n), t, 4.0 * n ** 3 / 3.0
+
+
+def _band_herm(c, n, b, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randn(n, n, dtype=c.dt, generator=g)
+    X = X + X.mH
+    i = torch.arange(n)
+    X = torch.where((i[:, None] - i[None, :]).abs() <= b, X, torch.zeros_like(X))
+    return X.to(c.dev).t().contiguous().t()
+
+
+def t_hb2st(c, m, n, k, **p):
+    b = max(1, min(c.a.nb, 64))
+    B0 = _band_herm(c, n, b)
+    (d, e, F), t = c.timed(lambda: sl.hb2st(B0.clone(), b, device=c.dev if c.dev.type == "cuda" else None))
+    if c.a.check != 'y':
+        return None, t, 6.0 * n * n * b
+    w0 = torch.linalg.eigvalsh(B0.cpu())
+    w1 = torch.linalg.eigvalsh(torch.diag(d) + torch.diag(e, 1) + torch.diag(e, -1))
+    return _rel(w1 - w0, w0.abs().max() * n), t, 6.0 * n * n * b
+
+
+def t_unmtr_hb2st(c, m, n, k, **p):
+    b = max(1, min(c.a.nb, 64))
+    B0 = _band_herm(c, n, b)
+    d, e, F = sl.hb2st(B0.clone(), b, device=c.dev if c.dev.type == "cuda" else None)
+    w, Zt = sl.stedc(d, e, device=c.dev)
+    Z = Zt.to(c.dt).to(c.dev).t().contiguous().t()
+    _, t = c.timed(lambda: sl.unmtr_hb2st(F, Z))
+    err = _rel(B0 @ Z - Z * w.to(c.dev, c.dt), B0.abs().max() * n) if c.a.check == 'y' else None
+    return err, t, 2.0 * n * n * b
+
+
+def t_unmtr_he2hb(c, m, n, k, **p):
+    from slate_amd.models import eig as E
+    nb = max(2, min(c.a.nb, 64))
+    A0 = _dense_cm(c, n, n, 1, herm=True)
+    Af = A0.clone()
+    F = sl.he2hb(Af, nb)
+    band = E._band_only(Af, nb)
+    w, V = torch.linalg.eigh(band.cpu())
+    Z = V.to(c.dev).t().contiguous().t()
+    _, t = c.timed(lambda: sl.unmtr_he2hb(F, Z))
+    err = _rel(A0 @ Z - Z * w.to(c.dev, c.dt), A0.abs().max() * n) if c.a.check == 'y' else None
+    return err, t, 2.0 * n ** 3
+
+
+def _tridiag(n, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(n, dtype=torch.float64, generator=g), torch.randn(max(n - 1, 0), dtype=torch.float64, generator=g)
+
+
+def _trid_check(c, d, e, w, Z=None):
+    T = torch.diag(d) + torch.diag(e, 1) + torch.diag(e, -1)
+    w0 = torch.linalg.eigvalsh(T)
+    sc = w0.abs().max() * d.numel()
+    err = _rel(w.cpu() - w0, sc)
+    if Z is not None:
+        Zc = Z.cpu().to(torch.float64)
+        err = max(err, _rel(T @ Zc - Zc * w.cpu(), sc))
+    return err
+
+
+def t_sterf(c, m, n, k, **p):
+    d, e = _tridiag(n)
+    w, t = c.timed(lambda: sl.sterf(d, e))
+    return (_trid_check(c, d, e, w) if c.a.check == 'y' else None), t, 30.0 * n * n
+
+
+def t_steqr(c, m, n, k, **p):
+    d, e = _tridiag(n)
+    (w, Z), t = c.timed(lambda: sl.steqr(d, e))
+    return (_trid_check(c, d, e, w, Z) if c.a.check == 'y' else None), t, 6.0 * n ** 3
+
+
+def t_stedc(c, m, n, k, **p):
+    d, e = _tridiag(n)
+    (w, Z), t = c.timed(lambda: sl.stedc(d, e, device=c.dev))
+    return (_trid_check(c, d, e, w, Z) if c.a.check == 'y' else None), t, 4.0 * n ** 3 / 3.0
+
+
+def _secular_problem(n, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    dd = torch.sort(torch.randn(n, dtype=torch.float64, generator=g)).values
+    z = torch.randn(n, dtype=torch.float64, generator=g)
+    return dd, z / z.norm(), 0.75
+
+
+def t_stedc_sort(c, m, n, k, **p):
+    g = torch.Generator().manual_seed(2)
+    dd = torch.randn(n, dtype=torch.float64, generator=g)
+    z = torch.randn(n, dtype=torch.float64, generator=g)
+    Q = torch.eye(n, dtype=torch.float64)
+    (ds, zs, Qs), t = c.timed(lambda: sl.stedc_sort(dd, z, Q))
+    ok = bool((ds[1:] >= ds[:-1]).all()) and torch.allclose(Qs.T @ dd, ds) and torch.allclose(Qs.T @ z, zs)
+    return (0.0 if ok else 1.0) if c.a.check == 'y' else None, t, 0.0
+
+
+def t_stedc_deflate(c, m, n, k, **p):
+    dd, z, rho = _secular_problem(n)
+    dd[1::4] = dd[0::4][:dd[1::4].numel()]              # repeated poles
+    dd = torch.sort(dd).values
+    z[2::5] = 0.0                                         # zero weights
+    Q = torch.eye(n, dtype=torch.float64)
+    M0 = torch.diag(dd) + rho * torch.outer(z, z)
+    (z2, K), t = c.timed(lambda: sl.stedc_deflate(dd, z.clone(), rho, Q))
+    # the deflated problem is similar to the original: Q^T M0 Q = diag(dd) + rho z2 z2^T
+    M1 = torch.diag(dd) + rho * torch.outer(z2, z2)
+    err = _rel(Q.T @ M0 @ Q - M1, M0.abs().max() * n) if c.a.check == 'y' else None
+    return err, t, 0.0
+
+
+def t_stedc_secular(c, m, n, k, **p):
+    dd, z, rho = _secular_problem(n)
+    (lam, org, mu), t = c.timed(lambda: sl.stedc_secular(dd, z, rho))
+    w0 = torch.linalg.eigvalsh(torch.diag(dd) + rho * torch.outer(z, z))
+    return (_rel(torch.sort(lam).values - w0, w0.abs().max() * n) if c.a.check == 'y' else None), t, 20.0 * n * n
+
+
+def t_stedc_z_vector(c, m, n, k, **p):
+    dd, z, rho = _secular_problem(n)
+    lam, org, mu = sl.stedc_secular(dd, z, rho)
+    (zh, V), t = c.timed(lambda: sl.stedc_z_vector(dd, z, rho, org, mu))
+    M = torch.diag(dd) + rho * torch.outer(z, z)
+    err = _rel(M @ V - V * lam, M.abs().max() * n) if c.a.check == 'y' else None
+    return err, t, 3.0 * n * n
+
+
+def t_ge2tb(c, m, n, k, **p):
+    nb = max(2, min(c.a.nb, 64))
+    mm = max(m, n)
+    A0 = _dense_cm(c, mm, n, 1)
+    Af = A0.clone()
+    F, t = c.timed(lambda: sl.ge2tb(Af, nb))
+    if c.a.check != 'y':
+        return None, t, 4.0 * mm * n * n
+    i = torch.arange(n, device=Af.device)
+    dl = i[None, :] - i[:, None]
+    band = torch.where((dl >= 0) & (dl <= nb), Af[:n], torch.zeros_like(Af[:n]))
+    s0, s1 = torch.linalg.svdvals(A0.cpu()), torch.linalg.svdvals(band.cpu())
+    return _rel(s1 - s0, s0.max() * mm), t, 4.0 * mm * n * n
+
+
+def _band_upper(c, n, b, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randn(n, n, dtype=c.dt, generator=g)
+    i = torch.arange(n)
+    dl = i[None, :] - i[:, None]
+    X = torch.where((dl >= 0) & (dl <= b), X, torch.zeros_like(X))
+    return X.to(c.dev).t().contiguous().t()
+
+
+def t_tb2bd(c, m, n, k, **p):
+    b = max(1, min(c.a.nb, 64))
+    B0 = _band_upper(c, n, b)
+    (d, e, F), t = c.timed(lambda: sl.tb2bd(B0.clone(), b))
+    if c.a.check != 'y':
+        return None, t, 8.0 * n * n * b
+    s0 = torch.linalg.svdvals(B0.cpu())
+    s1 = torch.linalg.svdvals(torch.diag(d) + torch.diag(e, 1))
+    return _rel(s1 - s0, s0.max() * n), t, 8.0 * n * n * b
+
+
+def t_unmbr_tb2bd(c, m, n, k, **p):
+    b = max(1, min(c.a.nb, 64))
+    B0 = _band_upper(c, n, b)
+    d, e, F = sl.tb2bd(B0.clone(), b)
+    Bd = (torch.diag(d) + torch.diag(e, 1)).to(c.dt)
+    ZU = torch.eye(n, dtype=c.dt, device=c.dev).t()
+    ZV = torch.eye(n, dtype=c.dt, device=c.dev).t()
+    _, t = c.timed(lambda: (sl.unmbr_tb2bd('L', F, ZU), sl.unmbr_tb2bd('R', F, ZV)))
+    err = _rel(ZU.cpu() @ Bd @ ZV.cpu().mH - B0.cpu(), B0.abs().max() * n) if c.a.check == 'y' else None
+    return err, t, 4.0 * n * n * b
+
+
+def t_bdsqr(c, m, n, k, **p):
+    d, e = _tridiag(n)
+    (s, U, VT), t = c.timed(lambda: sl.bdsqr(d, e))
+    if c.a.check != 'y':
+        return None, t, 12.0 * n ** 3
+    B = torch.diag(d) + torch.diag(e, 1)
+    s0 = torch.linalg.svdvals(B)
+    err = max(_rel(torch.sort(s, descending=True).values - s0, s0.max() * n),
+              _rel(U @ torch.diag(s) @ VT - B, s0.max() * n))
+    return err, t, 12.0 * n ** 3
+
+
 ROUTINES = {"gemm": t_gemm, "herk": t_herk, "syrk": t_herk, "trsm": t_trsm, "potrf": t_potrf,
             "posv": t_posv, "getrf": t_getrf, "gesv": t_gesv, "geqrf": t_geqrf, "gels": t_gels,
             "heev": t_heev, "syev": t_heev, "svd": t_svd, "norm": t_norm, "genorm": t_norm,
@@ -603,7 +1033,23 @@ ROUTINES = {"gemm": t_gemm, "herk": t_herk, "syrk": t_herk, "trsm": t_trsm, "pot
             "redistribute": t_redistribute, "gbsv": t_gbsv, "pbsv": t_pbsv, "gbmm": t_gbmm, "hbmm": t_hbmm,
             "tbsm": t_tbsm, "pocondest": t_pocondest, "trcondest": t_trcondest, "unmqr": t_unmqr,
             "gesv_mixed_gmres": t_gesv_mixed_gmres, "svd_vals": t_svd_vals, "heev_vals": t_heev_vals,
-            "syev_vals": t_heev_vals, "matgen": t_matgen}
+            "syev_vals": t_heev_vals, "matgen": t_matgen,
+            "scale_row_col": t_scale_row_col, "gbnorm": t_bandnorm(False), "hbnorm": t_bandnorm(True),
+            "getrf_nopiv": t_getrf_variant("nopiv"), "getrf_tntpiv": t_getrf_variant("tntpiv"),
+            "getrs_nopiv": t_getrs_variant("nopiv"), "getrs_tntpiv": t_getrs_variant("tntpiv"),
+            "gbtrf": t_gbtrf_gbtrs(False), "gbtrs": t_gbtrf_gbtrs(True), "pbtrf": t_pbtrf_pbtrs(False),
+            "pbtrs": t_pbtrf_pbtrs(True), "hetrf": t_hetrf_hetrs(False), "hetrs": t_hetrf_hetrs(True),
+            "sytrf": t_hetrf_hetrs(False), "sytrs": t_hetrf_hetrs(True), "posv_mixed_gmres": t_posv_mixed_gmres,
+            "hegst": t_hegst, "he2hb": t_he2hb, "hb2st": t_hb2st, "unmtr_hb2st": t_unmtr_hb2st,
+            "unmtr_he2hb": t_unmtr_he2hb, "sterf": t_sterf, "steqr": t_steqr, "stedc": t_stedc,
+            "stedc_sort": t_stedc_sort, "stedc_deflate": t_stedc_deflate, "stedc_secular": t_stedc_secular,
+            "stedc_z_vector": t_stedc_z_vector, "ge2tb": t_ge2tb, "tb2bd": t_tb2bd, "unmbr_tb2bd": t_unmbr_tb2bd,
+            "bdsqr": t_bdsqr}
+for _k, _pfx in (("ge", ""), ("tz", "tz"), ("tr", "tr"), ("he", "he"), ("sy", "sy")):
+    for _op in ("add", "copy", "scale", "set", "norm"):
+        if _k == "ge" and _op in ("add", "norm"):
+            continue                                   # generic add / genorm above
+        ROUTINES[(_pfx or "") + _op] = _aux(_k, _op)
 
 # per-GPU dense peaks (MI355X spec, TFLOP/s): fp64 matrix = vector, fp32 matrix
 PEAK_TF = {'s': 157.3, 'd': 78.6, 'c': 157.3, 'z': 78.6}
