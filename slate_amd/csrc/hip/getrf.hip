@@ -704,7 +704,8 @@ struct PanelCtx {
 
 template <typename T>
 static bool persist_ok(i64 m, bool nopiv) {
-    return std::is_same<T, double>::value && !nopiv && m <= (i64)PG * PT2 * 2 && m >= 1;
+    return std::is_same<T, double>::value && !nopiv && m <= (i64)PG * PT2 * 4 && m >= 1 &&
+           (m <= (i64)PG * PT2 * 2 || [] { const char* e = std::getenv("SLATE_AMD_LU_RPT"); return e && std::atoi(e) == 4; }());
 }
 
 template <typename T>
@@ -714,7 +715,21 @@ static void base(i64 m, int c0, int c1, T* A, i64 lda, i64* ipiv, i64 ioff, i64*
         if (ctx.full) {
             PersistBuf* pb = reinterpret_cast<PersistBuf*>(static_cast<char*>(w) + PANEL_BYTES);
             HIP_CHECK(hipMemsetAsync(&pb->cnt, 0, 3 * sizeof(unsigned long long), s));   // cnt, state, done
-            if (m <= (i64)PG * PT2) {
+            // rows per thread: 2 by default (SLATE_AMD_LU_RPT = 1 / 2 / 4):
+            // half the workgroups of one row per thread -- half the arrivals
+            // per column and half the CUs the panel stream reserves (dgetrf
+            // n = 32768 on one MI355X: 36.1 TF/s with 2 rows / 32 reserved
+            // CUs vs 34.0 with 1 row / 64; 4 rows spill: 21)
+            static const int rpt = [] {
+                const char* e = std::getenv("SLATE_AMD_LU_RPT");
+                const int v = e ? std::atoi(e) : 2;
+                return (v == 2 || v == 4) ? v : 1;
+            }();
+            if (rpt == 4 && m <= (i64)PG * PT2 * 4) {
+                const int G = (int)((m + 4 * PT2 - 1) / (4 * PT2));
+                hipLaunchKernelGGL(getrf_base_persist<4>, dim3(G), dim3(PT2), 0, s, m, c1, A, lda, ipiv, ioff,
+                                   info, info_off, pb, thr, (int)ctx.N, (int)cabs);
+            } else if (rpt == 1 && m <= (i64)PG * PT2) {
                 const int G = (int)((m + PT2 - 1) / PT2);
                 hipLaunchKernelGGL(getrf_base_persist<1>, dim3(G), dim3(PT2), 0, s, m, c1, A, lda, ipiv, ioff,
                                    info, info_off, pb, thr, (int)ctx.N, (int)cabs);

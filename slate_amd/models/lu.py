@@ -113,7 +113,8 @@ def _getrf_p1(A, buf, thr, la, nopiv):
     nloc = bc.nloc
     ipiv = torch.zeros(max(min(m, n), 1), dtype=torch.int64, device=dev)   # panel-relative per step
     infos = torch.zeros(max(kt, 1), dtype=torch.int64, device=dev)
-    ss = StreamSet(dev, reserve_cus=64)
+    # 32 CUs: the persistent fp64 panel runs <= 32 workgroups (2 rows per thread)
+    ss = StreamSet(dev, reserve_cus=32)
     ev_tr = {}
     ss.fork()
     for k in range(kt):
