@@ -725,7 +725,19 @@ static void base(i64 m, int c0, int c1, T* A, i64 lda, i64* ipiv, i64 ioff, i64*
                 const int v = e ? std::atoi(e) : 2;
                 return (v == 2 || v == 4) ? v : 1;
             }();
-            if (rpt == 4 && m <= (i64)PG * PT2 * 4) {
+            // short panels (the panel-bound tail of a factorization): one row
+            // per thread while that still fits the 32 reserved CUs, m <= 32 *
+            // 512 (SLATE_AMD_LU_RPT1_ROWS; measured 0 / 8192 / 16384 / 24576:
+            // 36.2 / 36.9 / 37.5 / 33.5 TF/s)
+            static const i64 rpt1_rows = [] {
+                const char* e = std::getenv("SLATE_AMD_LU_RPT1_ROWS");
+                return e ? (i64)std::atoll(e) : (i64)32 * PT2;
+            }();
+            if (rpt != 4 && m <= rpt1_rows && m <= (i64)PG * PT2) {
+                const int G = (int)((m + PT2 - 1) / PT2);
+                hipLaunchKernelGGL(getrf_base_persist<1>, dim3(G), dim3(PT2), 0, s, m, c1, A, lda, ipiv, ioff,
+                                   info, info_off, pb, thr, (int)ctx.N, (int)cabs);
+            } else if (rpt == 4 && m <= (i64)PG * PT2 * 4) {
                 const int G = (int)((m + 4 * PT2 - 1) / (4 * PT2));
                 hipLaunchKernelGGL(getrf_base_persist<4>, dim3(G), dim3(PT2), 0, s, m, c1, A, lda, ipiv, ioff,
                                    info, info_off, pb, thr, (int)ctx.N, (int)cabs);
