@@ -20,6 +20,7 @@
 // the left update one wave per column (lanes over rows: coalesced), the
 // right update one thread per row.  The matrix is a dense n x n
 // column-major copy holding both triangles (only the band is non-zero).
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -30,7 +31,16 @@ namespace slate_hip {
 
 namespace {
 constexpr int HMAXB = 128;
-constexpr i64 HLDS = 96 * 1024;   // bytes of the LDS staging buffer
+// bytes of the LDS staging buffer: SLATE_AMD_HB2ST_LDS (KB, 32..152),
+// default 128: the 3b-wide window of b = 64 is one chunk (96 KB: two)
+inline i64 hb_lds_bytes() {
+    static const i64 v = [] {
+        const char* e = std::getenv("SLATE_AMD_HB2ST_LDS");
+        const i64 kb = e ? std::atoll(e) : 128;
+        return std::min<i64>(152, std::max<i64>(32, kb)) * 1024;
+    }();
+    return v;
+}
 }
 
 // 2-D block moves between global memory and LDS: lanes run along the rows
@@ -73,7 +83,7 @@ template <typename T, int HT>
 __global__ void __launch_bounds__(HT)
 hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __restrict__ tauv,
              i64* __restrict__ rowv, i64* __restrict__ lenv, const i64* __restrict__ sweep_ptr,
-             const i64* __restrict__ ntask, int* ticket, int* done, i64 nsw, int D, i64* prof) {
+             const i64* __restrict__ ntask, int* ticket, int* done, i64 nsw, int D, i64* prof, i64 HLDS) {
     using R = typename scalar_traits<T>::real;
     __shared__ T v[HMAXB];
     extern __shared__ unsigned char hb_smem[];
@@ -292,10 +302,11 @@ void hb2st_device(i64 n, int b, T* A, i64 lda, T* V, T* tau, i64* row, i64* len,
         return (v == 256 || v == 512) ? v : 1024;
     }();
     auto launch = [&](auto kern, int ht) {
+        const i64 HLDS = hb_lds_bytes();
         HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)HLDS));
         hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(ht), HLDS, s, n, b, W, lda, V, tau, row, len,
-                           sweep_ptr, ntask, work, work + 1, nsw, 4, prof);
+                           sweep_ptr, ntask, work, work + 1, nsw, 4, prof, HLDS);
     };
     if (threads == 1024) launch(hb2st_kernel<T, 1024>, 1024);
     else if (threads == 512) launch(hb2st_kernel<T, 512>, 512);
@@ -316,7 +327,7 @@ void hb2st_device(i64 n, int b, T* A, i64 lda, T* V, T* tau, i64* row, i64* len,
 // applies it to the rows of columns cs..ce, then the left reflector that
 // annihilates column cs below the diagonal and applies it to the columns
 // of rows cs..re.  Sweep j runs task t once sweep j-1 has completed
-// min(t + 8, all) tasks.  The windows are the exact non-zero extents:
+// min(t + 4, all) tasks (see tb2bd_device).  The windows are the exact non-zero extents:
 // columns cs..ce hold rows [row, ce] (band + the fill of the previous left
 // reflector), rows cs..re hold columns [cs, re + b].
 template <typename T, int HT>
@@ -324,7 +335,7 @@ __global__ void __launch_bounds__(HT)
 tb2bd_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ UV, T* __restrict__ Utau,
              i64* __restrict__ Urow, i64* __restrict__ Ulen, T* __restrict__ VV, T* __restrict__ Vtau,
              i64* __restrict__ Vrow, i64* __restrict__ Vlen, const i64* __restrict__ sweep_ptr,
-             const i64* __restrict__ ntask, int* ticket, int* done, i64 nsw, int D) {
+             const i64* __restrict__ ntask, int* ticket, int* done, i64 nsw, int D, i64 HLDS) {
     using R = typename scalar_traits<T>::real;
     __shared__ T v[HMAXB];
     extern __shared__ unsigned char hb_smem[];
@@ -481,12 +492,21 @@ void tb2bd_device(i64 n, int b, T* A, i64 lda, T* UV, T* Utau, i64* Urow, i64* U
     const size_t bytes = sizeof(T) * (size_t)lda * (size_t)n;
     HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&W), bytes, hipDeviceMallocUncached));
     HIP_CHECK(hipMemcpyAsync(W, A, bytes, hipMemcpyDeviceToDevice, s));
-    constexpr int HT = 256;
+    // 1024 threads (the window moves are latency bound, as hb2st); lag 4:
+    // with the exact windows task t of sweep j stays inside
+    // [j + (t - 1) b + 1, j + (t + 2) b] and sweep j-1's tasks from t + 4 on
+    // start at j + (t + 3) b (SLATE_AMD_TB2BD_LAG overrides, >= 4)
+    constexpr int HT = 1024;
+    static const int lag = [] {
+        const char* e = std::getenv("SLATE_AMD_TB2BD_LAG");
+        return std::max(4, e ? std::atoi(e) : 4);
+    }();
     auto kern = tb2bd_kernel<T, HT>;
+    const i64 HLDS = hb_lds_bytes();
     HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)HLDS));
     hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(HT), HLDS, s, n, b, W, lda, UV, Utau, Urow, Ulen, VV, Vtau,
-                       Vrow, Vlen, sweep_ptr, ntask, work, work + 1, nsw, 8);
+                       Vrow, Vlen, sweep_ptr, ntask, work, work + 1, nsw, lag, HLDS);
     HIP_LAUNCH_CHECK();
     HIP_CHECK(hipMemcpyAsync(A, W, bytes, hipMemcpyDeviceToDevice, s));
     HIP_CHECK(hipStreamSynchronize(s));

@@ -113,7 +113,7 @@ def _tb2bd_device(B: torch.Tensor, b: int, dev):
     ntd, spd = nt.to(dev), sp.to(dev)
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
     nt0 = int(nt[0]) if nt.numel() else 1
-    nwg = int(min(max(nsw, 1), cus, max(8, nt0 // 8 + 8)))
+    nwg = int(min(max(nsw, 1), cus, max(8, nt0 // 4 + 8)))
     with trace_block("tb2bd"):
         if nsw > 0:
             _native._hip.tb2bd(_code(dt), n, b, A.data_ptr(), A.stride(1), *(x.data_ptr() for x in U),
