@@ -83,7 +83,8 @@ template <typename T, int HT>
 __global__ void __launch_bounds__(HT)
 hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __restrict__ tauv,
              i64* __restrict__ rowv, i64* __restrict__ lenv, const i64* __restrict__ sweep_ptr,
-             const i64* __restrict__ ntask, int* ticket, int* done, i64 nsw, int D, i64* prof, i64 HLDS) {
+             const i64* __restrict__ ntask, int* ticket, int* done, i64 nsw, int D, i64* prof, i64 HLDS,
+             int fused) {
     using R = typename scalar_traits<T>::real;
     __shared__ T v[HMAXB];
     extern __shared__ unsigned char hb_smem[];
@@ -165,7 +166,71 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
             HSTAMP(1);
             const T tau = s_tau;
             const i64 lo = col + 1, hi = min(n - 1, e + (i64)b);
-            if (!s_is_zero(tau)) {
+            const int KPf = k + 1;
+            const bool one_chunk = fused && (hi - lo + 1) <= min<i64>(HT, HLDS / ((i64)KPf * (i64)sizeof(T)));
+            if (!s_is_zero(tau) && one_chunk) {
+                // ---- fused two-sided update (A Hermitian, both triangles):
+                // ONE load of the row block A(s..e, lo..hi); left update
+                // H^H A on it; the right update A H only changes columns
+                // s..e, i.e. inside the block just the k x k diagonal block
+                // (a thread per row); the rest of A' = H^H A H in columns
+                // s..e is the conjugate transpose of the row block (A' is
+                // Hermitian), stored as the mirror of its off-diagonal part.
+                const T ct = s_conj(tau);
+                const int nc = (int)(hi - lo + 1), d0 = (int)(s - lo);
+                T* Ab = &At(s, lo);
+                move2d<T, HT / 64>(k, nc, lane, w, [&](int r, int c) -> T { return Ab[r + c * lda]; },
+                                   [&](int r, int c) -> T& { return L[c * KPf + r]; });
+                __syncthreads();
+                if (tid < nc) {
+                    T* Lc = L + tid * KPf;
+                    T part[8];
+                    #pragma unroll
+                    for (int u = 0; u < 8; ++u) part[u] = s_zero(T());
+                    int r = 0;
+                    for (; r + 8 <= k; r += 8) {
+                        #pragma unroll
+                        for (int u = 0; u < 8; ++u) part[u] = s_add(part[u], s_mul(s_conj(v[r + u]), Lc[r + u]));
+                    }
+                    for (; r < k; ++r) part[0] = s_add(part[0], s_mul(s_conj(v[r]), Lc[r]));
+                    T acc = s_zero(T());
+                    #pragma unroll
+                    for (int u = 0; u < 8; ++u) acc = s_add(acc, part[u]);
+                    acc = s_mul(ct, acc);
+                    for (r = 0; r < k; ++r) Lc[r] = s_sub(Lc[r], s_mul(v[r], acc));
+                }
+                __syncthreads();
+                HSTAMP(2);
+                if (tid < k) {
+                    T* Ld = L + (i64)d0 * KPf + tid;        // row tid of the diagonal block
+                    T part[8];
+                    #pragma unroll
+                    for (int u = 0; u < 8; ++u) part[u] = s_zero(T());
+                    int c = 0;
+                    for (; c + 8 <= k; c += 8) {
+                        #pragma unroll
+                        for (int u = 0; u < 8; ++u) part[u] = s_add(part[u], s_mul(Ld[(c + u) * KPf], v[c + u]));
+                    }
+                    for (; c < k; ++c) part[0] = s_add(part[0], s_mul(Ld[c * KPf], v[c]));
+                    T y = s_zero(T());
+                    #pragma unroll
+                    for (int u = 0; u < 8; ++u) y = s_add(y, part[u]);
+                    y = s_mul(y, tau);
+                    for (c = 0; c < k; ++c) Ld[c * KPf] = s_sub(Ld[c * KPf], s_mul(y, s_conj(v[c])));
+                }
+                __syncthreads();
+                move2d<T, HT / 64>(k, nc, lane, w, [&](int r, int c) -> T { return L[c * KPf + r]; },
+                                   [&](int r, int c) -> T& { return Ab[r + c * lda]; });
+                // mirror: A(lo + q, s + r) = conj(A'(s + r, lo + q)) for the rows
+                // q outside the diagonal block (above it, then below it)
+                move2d<T, HT / 64>(d0, k, lane, w, [&](int q, int r) -> T { return s_conj(L[q * KPf + r]); },
+                                   [&](int q, int r) -> T& { return At(lo + q, s + r); });
+                const int nb2 = nc - d0 - k;
+                move2d<T, HT / 64>(nb2, k, lane, w,
+                                   [&](int q, int r) -> T { return s_conj(L[(d0 + k + q) * KPf + r]); },
+                                   [&](int q, int r) -> T& { return At(e + 1 + q, s + r); });
+                __syncthreads();
+            } else if (!s_is_zero(tau)) {
                 // ---- left: A(s..e, c) -= v (conj(tau) v^H A(s..e, c)), c in [lo, hi].
                 // Column chunks staged in LDS (one bulk coalesced load: every
                 // load in flight at once), a wave per column, bulk store.
@@ -303,10 +368,12 @@ void hb2st_device(i64 n, int b, T* A, i64 lda, T* V, T* tau, i64* row, i64* len,
     }();
     auto launch = [&](auto kern, int ht) {
         const i64 HLDS = hb_lds_bytes();
+        // SLATE_AMD_HB2ST_FUSED=0: separate left / right passes (4 window moves per task instead of 3)
+        static const int fused = [] { const char* e = getenv("SLATE_AMD_HB2ST_FUSED"); return (e && e[0] == '0') ? 0 : 1; }();
         HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)HLDS));
         hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(ht), HLDS, s, n, b, W, lda, V, tau, row, len,
-                           sweep_ptr, ntask, work, work + 1, nsw, 4, prof, HLDS);
+                           sweep_ptr, ntask, work, work + 1, nsw, 4, prof, HLDS, fused);
     };
     if (threads == 1024) launch(hb2st_kernel<T, 1024>, 1024);
     else if (threads == 512) launch(hb2st_kernel<T, 512>, 512);
