@@ -237,3 +237,22 @@ def test_cpp_api(tmp_path, grid):
         for ln in lines:
             assert "FAILED" not in ln, ln
             assert float(ln.split()[-1]) < 1e-10, ln
+
+
+def test_lapack_upper_potrf_potri_keep_other_triangle():
+    """LAPACK never touches the unreferenced triangle: after potrf('U') /
+    potri('U') the strictly-lower part is exactly what the caller left."""
+    import numpy as np
+    from slate_amd.compat import lapack
+    n = 7
+    g = np.random.default_rng(1)
+    M = g.standard_normal((n, n))
+    A = np.asfortranarray(M @ M.T + n * np.eye(n))
+    S = A.copy()
+    A[np.tril_indices(n, -1)] = 77.0
+    assert lapack.dpotrf('U', n, A, n) == 0
+    assert np.all(A[np.tril_indices(n, -1)] == 77.0)
+    R = np.triu(A)
+    assert np.abs(R.T @ R - S).max() < 1e-12 * np.abs(S).max() * n
+    assert lapack.dpotri('U', n, A, n) == 0
+    assert np.all(A[np.tril_indices(n, -1)] == 77.0)
