@@ -36,6 +36,8 @@ exactly as in LAPACK/SLATE.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import ops
@@ -51,14 +53,18 @@ from ..utils import watchdog as _wd
 
 
 # ------------------------------------------------------------------ helpers
-def _apply_qh(V, Tk, C, conj=True):
-    """C -= V op(T) (V^H C), op = ^H (apply Q^H) or none (apply Q)."""
+def _apply_qh(V, Tk, C, conj=True, Vh=None):
+    """C -= V op(T) (V^H C), op = ^H (apply Q^H) or none (apply Q).  Vh:
+    optional explicit V^H (kb x m), making V^H C an NN GEMM."""
     if C.shape[1] == 0 or C.shape[0] == 0:
         return
     ct = conj_trans(C.dtype)
     kb = Tk.shape[0]
     W = ops.colmajor_empty(kb, C.shape[1], C.dtype, C.device)
-    ops.gemm(1.0, V, C, 0.0, W, transA=ct)
+    if Vh is not None:
+        ops.gemm(1.0, Vh, C, 0.0, W)
+    else:
+        ops.gemm(1.0, V, C, 0.0, W, transA=ct)
     ops.trmm('L', 'U', ct if conj else 'N', 'N', 1.0, Tk, W)
     ops.gemm(-1.0, V, W, 1.0, C)
 
@@ -93,6 +99,10 @@ def geqrf(A, T: TriangularFactors, opts=None) -> int:
             _geqrf_general(A, buf, T, la)
         s.mark_local_modified(slot)
     return 0
+
+
+# panels at least this tall get an explicit V^H (SLATE_AMD_QR_VH_ROWS; 0 = never)
+_VH_MIN_ROWS = int(os.environ.get("SLATE_AMD_QR_VH_ROWS", "4096")) or (1 << 62)
 
 
 def _geqrf_p1(A, buf, T, la):
@@ -130,15 +140,21 @@ def _geqrf_p1(A, buf, T, la):
                     bcast_tile(grid.row_comm, V, k % q)
                     bcast_tile(grid.row_comm, Tk, k % q)
                     grid.row_comm.bcast(tau, k % q)
+                # explicit V^H (one LDS-tiled transpose per step): the
+                # V^H C GEMMs of this step run as NN instead of TN
+                Vh = None
+                if V.is_cuda and mk >= _VH_MIN_ROWS and nloc > lc1:
+                    Vh = ops.colmajor_empty(kb, mk, dt, dev)
+                    ops.gecopy(V, Vh, trans=conj_trans(dt))
             # newest lookahead column k+la: first part of step k-1's trailing
             if k >= 1 and la > 0:
                 ss.wait(ss.panel, ev_tr[k - 1])
             if own and lck + kb < lc1:
                 # wide matrix, last panel: fewer rows than the tile has
                 # columns -- the tile's remaining columns are trailing too
-                _apply_qh(V, Tk, buf[r0:m, lck + kb:lc1])
+                _apply_qh(V, Tk, buf[r0:m, lck + kb:lc1], Vh=Vh)
             if lcla > lc1:
-                _apply_qh(V, Tk, buf[r0:m, lc1:lcla])
+                _apply_qh(V, Tk, buf[r0:m, lc1:lcla], Vh=Vh)
             ev_panel = ss.event(ss.panel)
         T.append({"T": Tk, "tau": tau, "r0": r0, "kb": kb, "kr": kb, "tree": None})
         us = ss.update[0]
@@ -147,13 +163,15 @@ def _geqrf_p1(A, buf, T, la):
             if nloc > lcla and V.is_cuda:
                 V.record_stream(us)
                 Tk.record_stream(us)
+                if Vh is not None:
+                    Vh.record_stream(us)
             lcnx = max(min(tiles_local_before(k + 2 + la, q, pc) * nb, nloc), lcla)
             with trace_block("geqrf::trailing"):
                 if lcnx > lcla:
-                    _apply_qh(V, Tk, buf[r0:m, lcla:lcnx])
+                    _apply_qh(V, Tk, buf[r0:m, lcla:lcnx], Vh=Vh)
                 ev_tr[k] = ss.event(us)
                 if nloc > lcnx:
-                    _apply_qh(V, Tk, buf[r0:m, lcnx:nloc])
+                    _apply_qh(V, Tk, buf[r0:m, lcnx:nloc], Vh=Vh)
     ss.join()
 
 
@@ -221,11 +239,16 @@ def _geqrf_general(A, buf, T, la):
             f = {"T": kp.get("T"), "tau": kp.get("tau")[:, 0], "r0": r0, "kb": kb, "kr": km,
                  "tree": ({"V": kp.get("Vh"), "T": kp.get("Th"), "tau": kp.get("tauh")[:, 0], "ks": ks}
                           if tree else None)}
+            Vloc = pk.get("V")
+            Vh = None
+            if Vloc.is_cuda and nmine >= _VH_MIN_ROWS and km and nloc > lc1:
+                Vh = ops.colmajor_empty(km, nmine, dt, dev)       # NN V^H C (see _geqrf_p1)
+                ops.gecopy(Vloc, Vh, trans=conj_trans(dt))
             if k >= 1 and la > 0:
                 ss.wait(ss.panel, ev_tr[k - 1])
             # (wide matrix, last panel: the tile's columns beyond kb are trailing too)
             part = [(lc_k + kb, lc1)] if (pc == ck and lc_k + kb < lc1) else []
-            _tsqr_update(buf, lr_k, mloc, pk.get("V"), f, part + [(lc1, lcla)], colc, dt, dev)
+            _tsqr_update(buf, lr_k, mloc, Vloc, f, part + [(lc1, lcla)], colc, dt, dev, Vh=Vh)
             ev_panel = ss.event(ss.panel)
         T.append(f)
         us = ss.update[0]
@@ -233,10 +256,12 @@ def _geqrf_general(A, buf, T, la):
             ss.wait(us, ev_panel)
             if buf.is_cuda:
                 pk.raw.record_stream(us)
+                if Vh is not None:
+                    Vh.record_stream(us)
             with trace_block("geqrf::trailing"):
-                _tsqr_update(buf, lr_k, mloc, pk.get("V"), f, [(lcla, lcnx)], colu, dt, dev)
+                _tsqr_update(buf, lr_k, mloc, Vloc, f, [(lcla, lcnx)], colu, dt, dev, Vh=Vh)
                 ev_tr[k] = ss.event(us)
-                _tsqr_update(buf, lr_k, mloc, pk.get("V"), f, [(lcnx, nloc)], colu, dt, dev)
+                _tsqr_update(buf, lr_k, mloc, Vloc, f, [(lcnx, nloc)], colu, dt, dev, Vh=Vh)
     ss.join()
 
 
@@ -281,14 +306,14 @@ def _tsqr_panel(buf, mloc, pr, p, colc, pk, st, dt, dev):
         ops.gecopy(S[:ks], mine[:ks], uplo='U')       # R^ over R_rk; reflectors below stay
 
 
-def _tsqr_update(buf, lr_k, mloc, Vl, f, ranges, comm, dt, dev, conj=True):
+def _tsqr_update(buf, lr_k, mloc, Vl, f, ranges, comm, dt, dev, conj=True, Vh=None):
     """C = Q^H C for local columns ``ranges`` of the rows >= tile k."""
     for c0, c1 in ranges:
         if c1 > c0:
-            _tsqr_apply(buf[lr_k:mloc, c0:c1], Vl, f, comm, conj)
+            _tsqr_apply(buf[lr_k:mloc, c0:c1], Vl, f, comm, conj, Vh=Vh)
 
 
-def _tsqr_apply(C, Vl, f, comm, conj=True):
+def _tsqr_apply(C, Vl, f, comm, conj=True, Vh=None):
     """C = Q_k^H C (conj) or Q_k C with Q_k = diag(Q_r) Q^ (local block
     reflector of this rank's panel rows, then the tree on the top kr rows;
     the tree's V^H C is one all-reduce over the process column)."""
@@ -299,7 +324,7 @@ def _tsqr_apply(C, Vl, f, comm, conj=True):
     if C.shape[1] == 0:
         return
     if conj and km and C.shape[0]:
-        _apply_qh(Vl, f["T"], C, conj=True)
+        _apply_qh(Vl, f["T"], C, conj=True, Vh=Vh)
     if tr is not None:
         W = ops.colmajor_zeros(tr["ks"], C.shape[1], dt, dev)
         if km:
@@ -309,7 +334,7 @@ def _tsqr_apply(C, Vl, f, comm, conj=True):
         if km:
             ops.gemm(-1.0, tr["V"], W, 1.0, C[:km])
     if not conj and km and C.shape[0]:
-        _apply_qh(Vl, f["T"], C, conj=False)
+        _apply_qh(Vl, f["T"], C, conj=False, Vh=Vh)
 
 
 # ------------------------------------------------------------------ unmqr
