@@ -102,13 +102,19 @@ def he2hb(Af: torch.Tensor, nb: int):
             X = ops.colmajor_empty(m, kk, Af.dtype, Af.device)
             X.copy_(V)
             ops.trmm('R', 'U', 'N', 'N', 1.0, T, X)                 # X = V T
-            Y = ops.colmajor_empty(m, kk, Af.dtype, Af.device)
+            # [V W] and [W V] side by side: the rank-2kk update A -= V W^H +
+            # W V^H is ONE GEMM with K = 2 kk (A22 streamed once, not twice)
+            VW = ops.colmajor_empty(m, 2 * kk, Af.dtype, Af.device)
+            WV = ops.colmajor_empty(m, 2 * kk, Af.dtype, Af.device)
+            Y = VW[:, kk:]
             ops.gemm(1.0, A22, X, 0.0, Y)                            # Y = A V T
             Mt = ops.colmajor_empty(kk, kk, Af.dtype, Af.device)
             ops.gemm(1.0, X, Y, 0.0, Mt, transA=ct)                  # M = T^H V^H Y
             ops.gemm(-0.5, V, Mt, 1.0, Y)                            # W = Y - V M / 2
-            ops.gemm(-1.0, V, Y, 1.0, A22, transB=ct)                # A -= V W^H
-            ops.gemm(-1.0, Y, V, 1.0, A22, transB=ct)                # A -= W V^H
+            VW[:, :kk].copy_(V)
+            WV[:, :kk].copy_(Y)
+            WV[:, kk:].copy_(V)
+            ops.gemm(-1.0, VW, WV, 1.0, A22, transB=ct)              # A -= V W^H + W V^H
     return F
 
 
@@ -122,9 +128,9 @@ def _zero_strict_lower(P):
 def unmtr_he2hb(F: He2hbFactors, Z: torch.Tensor):
     """Z := Q1 Z (Q1 = Q_0 Q_1 ... from he2hb): panels applied last-to-first."""
     with trace_block("unmtr_he2hb"):
+        from .qr import _apply_qh, _vh
         for (r0, V, T) in reversed(F.panels):
-            from .qr import _apply_qh
-            _apply_qh(V, T, Z[r0:, :], conj=False)
+            _apply_qh(V, T, Z[r0:, :], conj=False, Vh=_vh(V))
     return Z
 
 

@@ -69,6 +69,16 @@ def _apply_qh(V, Tk, C, conj=True, Vh=None):
     ops.gemm(-1.0, V, W, 1.0, C)
 
 
+def _vh(V):
+    """Explicit V^H (kb x m) of a tall device reflector block, or None: with
+    it the V^H C GEMM of _apply_qh runs as NN (see _geqrf_p1)."""
+    if not V.is_cuda or V.shape[0] < _VH_MIN_ROWS or V.shape[1] == 0:
+        return None
+    Vh = ops.colmajor_empty(V.shape[1], V.shape[0], V.dtype, V.device)
+    ops.gecopy(V, Vh, trans=conj_trans(V.dtype))
+    return Vh
+
+
 def _check(A):
     if A.op() != Op.NoTrans or A.ioffset or A.joffset or A.row0_offset or A.col0_offset:
         raise SlateError("geqrf: pass a whole (non-transposed) block-cyclic matrix")

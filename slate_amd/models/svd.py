@@ -25,7 +25,7 @@ from ..core.enums import Option
 from ..utils.trace import trace_block
 from ._util import conj_trans
 from .eig import _cm, _code, _my_cols, _zero_strict_lower
-from .qr import _apply_qh
+from .qr import _apply_qh, _vh
 
 
 class Ge2tbFactors:
@@ -49,7 +49,7 @@ def ge2tb(A: torch.Tensor, nb: int):
             T, V = ops.geqrf(P, tau)
             F.left.append((k0, V, T))
             if k0 + kb < n:
-                _apply_qh(V, T, A[k0:, k0 + kb:], conj=True)
+                _apply_qh(V, T, A[k0:, k0 + kb:], conj=True, Vh=_vh(V))
             _zero_strict_lower(P)
             c0 = k0 + kb
             if c0 >= n:
@@ -209,7 +209,7 @@ def unmbr_ge2tb(side, F: Ge2tbFactors, Z: torch.Tensor):
     is P times the band's V).  Block reflectors, MFMA GEMMs."""
     fac = F.left if str(getattr(side, "value", side))[0] in "Ll" else F.right
     for (r0, V, T) in reversed(fac):
-        _apply_qh(V, T, Z[r0:, :], conj=False)
+        _apply_qh(V, T, Z[r0:, :], conj=False, Vh=_vh(V))
     return Z
 
 
@@ -274,13 +274,13 @@ def svd(A, S=None, U=None, VH=None, opts=None):
             Zu[:k].copy_((F2.pu[:, None] * Ub.to(dt)).to(dev))
             _unmtr_refl(F2.U, Zu[:k])
             for (r0, V, T) in reversed(F1.left):
-                _apply_qh(V, T, Zu[r0:, :], conj=False)
+                _apply_qh(V, T, Zu[r0:, :], conj=False, Vh=_vh(V))
         if wantV:
             Zv = ops.colmajor_empty(k, k, dt, dev)
             Zv.copy_((F2.pv[:, None] * VTb.T.to(dt)).to(dev))
             _unmtr_refl(F2.V, Zv)
             for (c0, V, T) in reversed(F1.right):
-                _apply_qh(V, T, Zv[c0:, :], conj=False)
+                _apply_qh(V, T, Zv[c0:, :], conj=False, Vh=_vh(V))
         # write the outputs: (U, VH) of op(A)
         if trans:
             # A^H = Uu S Vv^H  ->  A = Vv S Uu^H  (U/VH were swapped above:
