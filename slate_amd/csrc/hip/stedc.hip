@@ -20,6 +20,8 @@
 //  * vectors: one workgroup per root j: v_i = zhat_i / (d_i - lambda_j),
 //    column norm by a workgroup reduction, normalised column written
 //    column-major (coalesced) straight into the GEMM operand.
+#include <cstdlib>
+
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -121,6 +123,99 @@ secular_kernel(i64 n, const double* __restrict__ d, const double* __restrict__ z
     if (live) { org[j] = o; mu[j] = m; }
 }
 
+// Wave-per-root form of secular_kernel (default): the 64 lanes of a wave
+// split the pole sums of ONE root and combine them by shuffles; the bracket
+// and model-step logic is wave-uniform.  k roots -> k waves (k = 16384 gives
+// 64 waves per CU instead of one), each pole sum 64x shorter per lane.
+__device__ inline double wave_prod(double v) {
+    #pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v *= __shfl_xor(v, o, 64);
+    return v;
+}
+
+__global__ void __launch_bounds__(256)
+secular_wave_kernel(i64 n, const double* __restrict__ d, const double* __restrict__ z, double rho, double zz,
+                    i64* __restrict__ org, double* __restrict__ mu) {
+    const int lane = threadIdx.x & 63;
+    const i64 jj = (i64)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (jj >= n) return;                           // the whole wave: no block barriers below
+    const bool right = jj + 1 < n;
+    const double lo_d = d[jj];
+    const double hi_d = right ? d[jj + 1] : d[jj] + rho * zz;
+    const double mid = 0.5 * (hi_d - lo_d);
+    i64 o = jj;
+    double a = 0.0, b = mid, m = mid;
+    const double eps = 2.220446049250313e-16;
+    for (int it = 0; it <= SEC_ITMAX; ++it) {
+        const double dorg = d[o];
+        double ps = 0.0, dps = 0.0, ph = 0.0, dph = 0.0;
+        for (i64 i = lane; i < n; i += 64) {
+            const double r = 1.0 / ((d[i] - dorg) - m);
+            const double zi = z[i];
+            const double t = zi * zi * r;
+            if (i <= jj) { ps += t; dps += t * r; }
+            else { ph += t; dph += t * r; }
+        }
+        ps = wave_sum(ps); dps = wave_sum(dps); ph = wave_sum(ph); dph = wave_sum(dph);
+        const double psi = rho * ps, dpsi = rho * dps, phi = rho * ph, dphi = rho * dph;
+        const double fv = 1.0 + psi + phi;
+        if (it == 0) {
+            if (right && fv < 0) { o = jj + 1; a = -mid; b = 0.0; }
+            else { o = jj; a = 0.0; b = right ? mid : (hi_d - lo_d); }
+            m = 0.5 * (a + b);
+            continue;
+        }
+        if (fabs(fv) <= 8.0 * eps * (1.0 + fabs(psi) + fabs(phi))) break;
+        if (fv < 0) a = m; else b = m;
+        const double Dlo = (lo_d - dorg) - m;
+        const double b1 = dpsi * Dlo * Dlo, a1 = psi - dpsi * Dlo;
+        double h;
+        if (!right) {
+            const double c = 1.0 + a1 + phi;
+            h = Dlo + b1 / c;
+        } else {
+            const double Dhi = (hi_d - dorg) - m;
+            const double b2 = dphi * Dhi * Dhi, a2 = phi - dphi * Dhi;
+            const double c = 1.0 + a1 + a2;
+            const double qa = c, qb = c * (Dlo + Dhi) + b1 + b2, qc = c * Dlo * Dhi + b1 * Dhi + b2 * Dlo;
+            const double disc = fmax(qb * qb - 4.0 * qa * qc, 0.0), sq = sqrt(disc);
+            double h1, h2;
+            if (qb >= 0) { h1 = (qb + sq) / (2.0 * qa); h2 = 2.0 * qc / (qb + sq); }
+            else { h1 = 2.0 * qc / (qb - sq); h2 = (qb - sq) / (2.0 * qa); }
+            const bool ok1 = h1 > Dlo && h1 < Dhi, ok2 = h2 > Dlo && h2 < Dhi;
+            h = ok2 ? h2 : (ok1 ? h1 : -fv / (dpsi + dphi));
+        }
+        double mn = m + h;
+        if (!(mn > a && mn < b)) mn = 0.5 * (a + b);
+        const bool stop = (mn == a || mn == b || fabs(mn - m) <= 4.0 * eps * fabs(mn));
+        m = mn;
+        if (stop) break;
+    }
+    if (lane == 0) { org[jj] = o; mu[jj] = m; }
+}
+
+// wave-per-pole form of zhat_kernel
+__global__ void __launch_bounds__(256)
+zhat_wave_kernel(i64 n, const double* __restrict__ d, const double* __restrict__ z, double rho,
+                 const i64* __restrict__ org, const double* __restrict__ mu, double* __restrict__ zh) {
+    const int lane = threadIdx.x & 63;
+    const i64 i = (i64)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const double di = d[i];
+    double prod = 1.0, dii = 0.0;
+    for (i64 t = lane; t < n; t += 64) {
+        const double delta = (d[org[t]] - di) + mu[t];             // lambda_t - d_i
+        if (t == i) { dii = delta; continue; }
+        prod *= delta / (d[t] - di);
+    }
+    prod = wave_prod(prod);
+    dii = wave_sum(dii);                                           // one lane holds it
+    if (lane == 0) {
+        const double v = sqrt(fabs(dii * prod / rho));
+        zh[i] = z[i] < 0 ? -v : v;
+    }
+}
+
 // zhat_i^2 = (lambda_i - d_i) prod_{j != i} (lambda_j - d_i) / (d_j - d_i) / rho
 __global__ void __launch_bounds__(SEC_T)
 zhat_kernel(i64 n, const double* __restrict__ d, const double* __restrict__ z, double rho,
@@ -177,11 +272,21 @@ secvec_kernel(i64 n, const double* __restrict__ d, const double* __restrict__ zh
 void stedc_secular(i64 n, const double* d, const double* z, double rho, double zz, i64* org, double* mu,
                    double* zh, double* V, i64 ldv, hipStream_t s) {
     if (n <= 0) return;
-    const unsigned g = (unsigned)((n + SEC_T - 1) / SEC_T);
-    hipLaunchKernelGGL(secular_kernel, dim3(g), dim3(SEC_T), 0, s, n, d, z, rho, zz, org, mu);
-    HIP_LAUNCH_CHECK();
-    hipLaunchKernelGGL(zhat_kernel, dim3(g), dim3(SEC_T), 0, s, n, d, z, rho, org, mu, zh);
-    HIP_LAUNCH_CHECK();
+    // SLATE_AMD_SECULAR_WAVE=0: one thread per root / pole (the older form)
+    static const bool wave = [] { const char* e = std::getenv("SLATE_AMD_SECULAR_WAVE"); return !(e && e[0] == '0'); }();
+    if (wave) {
+        const unsigned g4 = (unsigned)((n + 3) / 4);
+        hipLaunchKernelGGL(secular_wave_kernel, dim3(g4), dim3(256), 0, s, n, d, z, rho, zz, org, mu);
+        HIP_LAUNCH_CHECK();
+        hipLaunchKernelGGL(zhat_wave_kernel, dim3(g4), dim3(256), 0, s, n, d, z, rho, org, mu, zh);
+        HIP_LAUNCH_CHECK();
+    } else {
+        const unsigned g = (unsigned)((n + SEC_T - 1) / SEC_T);
+        hipLaunchKernelGGL(secular_kernel, dim3(g), dim3(SEC_T), 0, s, n, d, z, rho, zz, org, mu);
+        HIP_LAUNCH_CHECK();
+        hipLaunchKernelGGL(zhat_kernel, dim3(g), dim3(SEC_T), 0, s, n, d, z, rho, org, mu, zh);
+        HIP_LAUNCH_CHECK();
+    }
     if (V != nullptr) {
         hipLaunchKernelGGL(secvec_kernel, dim3((unsigned)n), dim3(256), 0, s, n, d, zh, org, mu, V, ldv);
         HIP_LAUNCH_CHECK();

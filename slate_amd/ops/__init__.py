@@ -414,12 +414,25 @@ def v_explicit(A, V):
 
 
 def gelqf(A, tau):
+    """Householder LQ of a panel in place (L on/below the diagonal, the
+    reflectors' conjugates to the right, LAPACK layout).  Host: native
+    kernel; device: the GPU QR of A^H written back as its conjugate
+    transpose (gelqf(A) is geqrf(A^H)^H)."""
     _chk(A)
+    if A.is_cuda:
+        Ah = as_colmajor(A.mH.contiguous())
+        geqrf(Ah, tau)
+        A.copy_(Ah.mH)
+        return tau
     _native._host.gelqf(code(A.dtype), A.shape[0], A.shape[1], A.data_ptr(), ld(A), tau.data_ptr())
     return tau
 
 
 def larft(V, tau, T):
+    """Compact-WY T of the reflectors V (host tensors; the device QR panels
+    return T themselves)."""
+    if V.is_cuda:
+        raise SlateError("larft: host tensors only (device panels produce T in ops.geqrf)")
     _native._host.larft(code(V.dtype), V.shape[0], tau.shape[0], V.data_ptr(), ld(V), tau.data_ptr(),
                         T.data_ptr(), ld(T))
     return T

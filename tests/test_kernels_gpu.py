@@ -439,3 +439,22 @@ def test_butterfly_gpu(dt, depth):
         assert (ref(got) - opW @ ref(X)).abs().max().item() < TOL[dt] * 10
         got = ops.butterfly(Y.clone(), dg.to(rdt).cuda(), depth, trans, 'R')
         assert (ref(got) - ref(Y) @ opW.mT).abs().max().item() < TOL[dt] * 10
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float64, torch.complex128])
+def test_gelqf_panel_device_matches_host(dt):
+    """ops.gelqf on the device (QR of A^H) gives the host LQ: same L and
+    tau (LAPACK layout)."""
+    from slate_amd import ops
+    g = torch.Generator().manual_seed(4)
+    A = torch.randn(40, 90, dtype=dt, generator=g)
+    Ah = ops.as_colmajor(A.clone())
+    th = torch.zeros(40, dtype=dt)
+    ops.gelqf(Ah, th)
+    Ad = ops.as_colmajor(A.clone()).cuda()
+    Ad = ops.as_colmajor(Ad)
+    td = torch.zeros(40, dtype=dt, device="cuda")
+    ops.gelqf(Ad, td)
+    assert torch.allclose(torch.tril(Ad.cpu()), torch.tril(Ah), atol=1e-12)
+    assert torch.allclose(td.cpu(), th, atol=1e-12)
