@@ -79,6 +79,13 @@ __device__ inline void move2d(int nrow, int ncol, int lane, int w, Src src, Dst 
     });
 }
 
+// xor shuffle inside a quad of lanes (any scalar type)
+template <typename T>
+__device__ inline T quad_xor(T v, int m) {
+    if constexpr (scalar_traits<T>::is_complex) return T{__shfl_xor(v.re, m, 64), __shfl_xor(v.im, m, 64)};
+    else return __shfl_xor(v, m, 64);
+}
+
 template <typename T, int HT>
 __global__ void __launch_bounds__(HT)
 hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __restrict__ tauv,
@@ -182,41 +189,42 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
                 move2d<T, HT / 64>(k, nc, lane, w, [&](int r, int c) -> T { return Ab[r + c * lda]; },
                                    [&](int r, int c) -> T& { return L[c * KPf + r]; });
                 __syncthreads();
-                if (tid < nc) {
-                    T* Lc = L + tid * KPf;
-                    T part[8];
-                    #pragma unroll
-                    for (int u = 0; u < 8; ++u) part[u] = s_zero(T());
-                    int r = 0;
-                    for (; r + 8 <= k; r += 8) {
-                        #pragma unroll
-                        for (int u = 0; u < 8; ++u) part[u] = s_add(part[u], s_mul(s_conj(v[r + u]), Lc[r + u]));
+                // left: four lanes per column (rows q, q + 4, ...), partial
+                // dot products combined by two xor shuffles inside the quad
+                for (int e = tid; e < 4 * nc; e += HT) {
+                    T* Lc = L + (e >> 2) * KPf;
+                    const int q = e & 3;
+                    T p0 = s_zero(T()), p1 = s_zero(T());
+                    int r = q;
+                    for (; r + 4 < k; r += 8) {
+                        p0 = s_add(p0, s_mul(s_conj(v[r]), Lc[r]));
+                        p1 = s_add(p1, s_mul(s_conj(v[r + 4]), Lc[r + 4]));
                     }
-                    for (; r < k; ++r) part[0] = s_add(part[0], s_mul(s_conj(v[r]), Lc[r]));
-                    T acc = s_zero(T());
-                    #pragma unroll
-                    for (int u = 0; u < 8; ++u) acc = s_add(acc, part[u]);
+                    if (r < k) p0 = s_add(p0, s_mul(s_conj(v[r]), Lc[r]));
+                    T acc = s_add(p0, p1);
+                    acc = s_add(acc, quad_xor(acc, 1));
+                    acc = s_add(acc, quad_xor(acc, 2));
                     acc = s_mul(ct, acc);
-                    for (r = 0; r < k; ++r) Lc[r] = s_sub(Lc[r], s_mul(v[r], acc));
+                    for (r = q; r < k; r += 4) Lc[r] = s_sub(Lc[r], s_mul(v[r], acc));
                 }
                 __syncthreads();
                 HSTAMP(2);
-                if (tid < k) {
-                    T* Ld = L + (i64)d0 * KPf + tid;        // row tid of the diagonal block
-                    T part[8];
-                    #pragma unroll
-                    for (int u = 0; u < 8; ++u) part[u] = s_zero(T());
-                    int c = 0;
-                    for (; c + 8 <= k; c += 8) {
-                        #pragma unroll
-                        for (int u = 0; u < 8; ++u) part[u] = s_add(part[u], s_mul(Ld[(c + u) * KPf], v[c + u]));
+                // right on the diagonal block: four lanes per row
+                for (int e = tid; e < 4 * k; e += HT) {
+                    T* Ld = L + (i64)d0 * KPf + (e >> 2);   // row e/4 of the diagonal block
+                    const int q = e & 3;
+                    T p0 = s_zero(T()), p1 = s_zero(T());
+                    int c = q;
+                    for (; c + 4 < k; c += 8) {
+                        p0 = s_add(p0, s_mul(Ld[c * KPf], v[c]));
+                        p1 = s_add(p1, s_mul(Ld[(c + 4) * KPf], v[c + 4]));
                     }
-                    for (; c < k; ++c) part[0] = s_add(part[0], s_mul(Ld[c * KPf], v[c]));
-                    T y = s_zero(T());
-                    #pragma unroll
-                    for (int u = 0; u < 8; ++u) y = s_add(y, part[u]);
+                    if (c < k) p0 = s_add(p0, s_mul(Ld[c * KPf], v[c]));
+                    T y = s_add(p0, p1);
+                    y = s_add(y, quad_xor(y, 1));
+                    y = s_add(y, quad_xor(y, 2));
                     y = s_mul(y, tau);
-                    for (c = 0; c < k; ++c) Ld[c * KPf] = s_sub(Ld[c * KPf], s_mul(y, s_conj(v[c])));
+                    for (c = q; c < k; c += 4) Ld[c * KPf] = s_sub(Ld[c * KPf], s_mul(y, s_conj(v[c])));
                 }
                 __syncthreads();
                 move2d<T, HT / 64>(k, nc, lane, w, [&](int r, int c) -> T { return L[c * KPf + r]; },
