@@ -492,12 +492,16 @@ tb2bd_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ UV, T* __
                         move2d<T, HT / 64>(nr, k, lane, w, [&](int r, int c) -> T { return Ab[r + c * lda]; },
                                            [&](int r, int c) -> T& { return L[c * nr + r]; });
                         __syncthreads();
-                        if (tid < nr) {
+                        // four lanes per row (columns q, q + 4, ...), quad reductions
+                        for (int e = tid; e < 4 * nr; e += HT) {
+                            const int rr = e >> 2, q = e & 3;
                             T y = s_zero(T());
-                            for (int c = 0; c < k; ++c) y = s_add(y, s_mul(L[c * nr + tid], v[c]));
+                            for (int c = q; c < k; c += 4) y = s_add(y, s_mul(L[c * nr + rr], v[c]));
+                            y = s_add(y, quad_xor(y, 1));
+                            y = s_add(y, quad_xor(y, 2));
                             y = s_mul(y, tau);
-                            for (int c = 0; c < k; ++c)
-                                L[c * nr + tid] = s_sub(L[c * nr + tid], s_mul(y, s_conj(v[c])));
+                            for (int c = q; c < k; c += 4)
+                                L[c * nr + rr] = s_sub(L[c * nr + rr], s_mul(y, s_conj(v[c])));
                         }
                         __syncthreads();
                         move2d<T, HT / 64>(nr, k, lane, w, [&](int r, int c) -> T { return L[c * nr + r]; },
@@ -531,12 +535,16 @@ tb2bd_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ UV, T* __
                         move2d<T, HT / 64>(kr, nc, lane, w, [&](int r, int c) -> T { return Ab[r + c * lda]; },
                                            [&](int r, int c) -> T& { return L[c * KP + r]; });
                         __syncthreads();
-                        if (tid < nc) {
-                            T* Lc = L + tid * KP;
+                        // four lanes per column (rows q, q + 4, ...), quad reductions
+                        for (int e = tid; e < 4 * nc; e += HT) {
+                            T* Lc = L + (e >> 2) * KP;
+                            const int q = e & 3;
                             T acc = s_zero(T());
-                            for (int r = 0; r < kr; ++r) acc = s_add(acc, s_mul(s_conj(v[r]), Lc[r]));
+                            for (int r = q; r < kr; r += 4) acc = s_add(acc, s_mul(s_conj(v[r]), Lc[r]));
+                            acc = s_add(acc, quad_xor(acc, 1));
+                            acc = s_add(acc, quad_xor(acc, 2));
                             acc = s_mul(ct, acc);
-                            for (int r = 0; r < kr; ++r) Lc[r] = s_sub(Lc[r], s_mul(v[r], acc));
+                            for (int r = q; r < kr; r += 4) Lc[r] = s_sub(Lc[r], s_mul(v[r], acc));
                         }
                         __syncthreads();
                         move2d<T, HT / 64>(kr, nc, lane, w, [&](int r, int c) -> T { return L[c * KP + r]; },

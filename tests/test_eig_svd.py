@@ -380,8 +380,9 @@ def test_tb2bd_gpu_equals_host(dt, n, b, monkeypatch):
     d1, e1, F1 = S.tb2bd(A.clone(), b)
     d2, e2, F2 = S.tb2bd(A.clone().cuda(), b)
     sc = A.abs().max().item() * n
-    assert (d1 - d2).abs().max().item() < 1e-13 * sc
-    assert (e1 - e2).abs().max().item() < 1e-13 * sc
+    # different summation orders (host: serial, device: quad-lane partial sums)
+    assert (d1 - d2).abs().max().item() < 1e-12 * sc
+    assert (e1 - e2).abs().max().item() < 1e-12 * sc
     for a, c in ((F1.U, F2.U), (F1.V, F2.V)):
         assert a.count == c.count
         assert torch.equal(a.row, c.row.cpu()) and torch.equal(a.length, c.length.cpu())
