@@ -51,40 +51,108 @@ def grid_for(n, routine="potrf"):
     return {1: (1, 1), 2: (1, 2), 4: (2, 2), 8: (2, 4)}.get(n, (1, n))
 
 
-def _residual(args, A, A0, piv):
+class _DistVec:
+    """Matrix-vector products with a block-cyclic local buffer, for the
+    correctness check after the timed region (no gather of the matrix: each
+    rank multiplies its local block, one all-reduce of an n-vector)."""
+
+    def __init__(self, M, comm):
+        st = M.storage
+        bc = st.bc
+        self.comm = comm
+        self.dev = st.local[st.origin_slot].device
+        lr = torch.arange(bc.mloc, device=self.dev)
+        lc = torch.arange(bc.nloc, device=self.dev)
+        self.gr = ((lr // bc.mb) * bc.p + bc.pr) * bc.mb + lr % bc.mb
+        self.gc = ((lc // bc.nb) * bc.q + bc.pc) * bc.nb + lc % bc.nb
+        self.m, self.n = st.m, st.n
+        self.mloc, self.nloc = bc.mloc, bc.nloc
+
+    def local(self, buf):
+        return buf[:self.mloc, :self.nloc]
+
+    def _sum(self, y):
+        if self.comm.size > 1:
+            self.comm.allreduce(y)
+        return y
+
+    def mv(self, F, v):
+        """y = F v (F: masked local block of an m x n matrix, v: n)."""
+        y = torch.zeros(self.m, dtype=v.dtype, device=v.device)
+        if F.numel():
+            y[self.gr] = F @ v[self.gc]
+        return self._sum(y)
+
+    def mvT(self, F, v):
+        """w = F^T v (v: m)."""
+        w = torch.zeros(self.n, dtype=v.dtype, device=v.device)
+        if F.numel():
+            w[self.gc] = F.mT @ v[self.gr]
+        return self._sum(w)
+
+    def fro2(self, F):
+        t = (F * F).sum().reshape(1)
+        return float(self._sum(t).item())
+
+
+def _residual(args, A, A0, piv, comm, extra=None):
     """Backward error of the last factorization (outside the timed region),
-    one rank only.  Mirrors the reference tester's checks
-    (test/test_posv.cc:304-345, test_gesv.cc:332-377): a random right-hand
-    side is pushed through the factors and ||A0 x - b|| / (||A0|| ||x|| n)
-    is reported; it must be O(eps)."""
-    F = A.storage.local[A.storage.origin_slot]
-    m, n = F.shape[0], F.shape[1]
-    g = torch.Generator(device=F.device).manual_seed(5)
+    computed on the grid: a random vector v is pushed through the factors
+    and through the saved input.  Tester-style checks (reference
+    test/test_posv.cc:304-345, test_gesv.cc:332-377):
+      potrf  ||L L^T v - A v|| / (||A|| ||v|| n)
+      getrf  ||L U v - P A v|| / (||A|| ||v|| n)
+      geqrf  ||R^T R v - A^T A v|| / (||A||^2 ||v|| n)     (Q-free)
+      gemm   ||C v - A (B v)|| / (||A|| ||B|| ||v||)
+    Must be O(eps): bench.py exits non-zero above 3 eps (the reference
+    tester's default tolerance factor)."""
+    D = _DistVec(A, comm)
+    st = A.storage
+    F = D.local(st.local[st.origin_slot])
+    F0 = D.local(A0)
+    gr, gc = D.gr[:, None], D.gc[None, :]
+    g = torch.Generator(device="cpu").manual_seed(5)
+    n = st.n
     if args.routine == "potrf":
-        L = torch.tril(F[:n, :n])
-        S = torch.tril(A0[:n, :n])
-        S = S + torch.tril(S, -1).mT
-        b = torch.rand(n, 1, dtype=F.dtype, device=F.device, generator=g)
-        y = torch.linalg.solve_triangular(L, b, upper=False)
-        x = torch.linalg.solve_triangular(L.mT, y, upper=True)
-        r = (S @ x - b).norm() / (S.norm() * x.norm() * n)
+        v = torch.rand(n, 1, generator=g, dtype=torch.float64).to(D.dev)[:, 0]
+        L = torch.where(gr >= gc, F, torch.zeros((), dtype=F.dtype, device=F.device))
+        y = D.mv(L, D.mvT(L, v))
+        Lo = torch.where(gr >= gc, F0, torch.zeros((), dtype=F0.dtype, device=F0.device))
+        So = torch.where(gr > gc, F0, torch.zeros((), dtype=F0.dtype, device=F0.device))
+        sv = D.mv(Lo, v) + D.mvT(So, v)
+        nA = (D.fro2(Lo) + D.fro2(So)) ** 0.5
+        r = (y - sv).norm() / (nA * v.norm() * n)
     elif args.routine == "getrf":
-        b = torch.rand(n, 1, dtype=F.dtype, device=F.device, generator=g)
+        v = torch.rand(n, 1, generator=g, dtype=torch.float64).to(D.dev)[:, 0]
+        z = torch.zeros((), dtype=F.dtype, device=F.device)
+        U = torch.where(gr <= gc, F, z)
+        Ls = torch.where(gr > gc, F, z)
+        u = D.mv(U, v)
+        y = D.mv(Ls, u) + u
+        a = D.mv(F0, v).cpu()
         perm = list(range(n))
-        for i, j in enumerate(piv.ipiv.tolist()):     # LAPACK-style sequential swaps
+        for i, j in enumerate(piv.ipiv.tolist()):      # LAPACK-style sequential swaps
             perm[i], perm[j] = perm[j], perm[i]
-        pb = b[torch.as_tensor(perm, device=F.device)]
-        Lu = torch.tril(F[:n, :n], -1) + torch.eye(n, dtype=F.dtype, device=F.device)
-        y = torch.linalg.solve_triangular(Lu, pb, upper=False)
-        x = torch.linalg.solve_triangular(torch.triu(F[:n, :n]), y, upper=True)
-        r = (A0[:n, :n] @ x - b).norm() / (A0[:n, :n].norm() * x.norm() * n)
+        pa = a[torch.as_tensor(perm)].to(D.dev)
+        r = (y - pa).norm() / (D.fro2(F0) ** 0.5 * v.norm() * n)
     elif args.routine == "geqrf":
-        R = torch.triu(F[:n, :n])
-        # ||R^T R - A^T A|| / (||A||^2 n): Q-free backward-error proxy
-        r = (R.mT @ R - A0.mT @ A0).norm() / (A0.norm() ** 2 * n)
+        v = torch.rand(n, 1, generator=g, dtype=torch.float64).to(D.dev)[:, 0]
+        R = torch.where(gr <= gc, F, torch.zeros((), dtype=F.dtype, device=F.device))
+        z1 = D.mvT(F0, D.mv(F0, v))
+        z2 = D.mvT(R, D.mv(R, v))
+        r = (z1 - z2).norm() / (D.fro2(F0) * v.norm() * n)
+    elif args.routine == "gemm":
+        Bm, Cm = extra
+        DB = _DistVec(Bm, comm)
+        v = torch.rand(n, 1, generator=g, dtype=torch.float64).to(D.dev)[:, 0]
+        FB = DB.local(Bm.storage.local[Bm.storage.origin_slot])
+        FC = DB.local(Cm.storage.local[Cm.storage.origin_slot])
+        y = DB.mv(FC, v)
+        x = D.mv(F0, DB.mv(FB, v))
+        r = (y - x).norm() / ((D.fro2(F0) * DB.fro2(FB)) ** 0.5 * v.norm())
     else:
         return None
-    return float(f"{r.item():.3e}")
+    return float(f"{float(r):.3e}")
 
 
 def main():
@@ -103,8 +171,14 @@ def main():
     ap.add_argument("--lookahead", type=int, default=1)
     ap.add_argument("--method", default="pp", choices=["pp", "calu", "nopiv"], help="getrf: pivoting method")
     ap.add_argument("--grid", default=None, help="PxQ override")
-    ap.add_argument("--check", type=int, default=1, help="residual check after timing (1 rank)")
+    ap.add_argument("--check", type=int, default=1, help="residual check after timing (0 = skip)")
     args = ap.parse_args()
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and "SLATE_AMD_KEEP_HW_QUEUES" not in os.environ:
+        # one process per GPU drives ~7 streams (panel, diag, update, the
+        # default stream and one RCCL stream per communicator): give each its
+        # own hardware queue instead of multiplexing them onto HIP's default 4
+        # (set before the first HIP call of this process)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(max(8, int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)))
 
     import slate_amd as sl
     comm = sl.init()
@@ -175,11 +249,15 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         info = step()
+    t_host = time.perf_counter() - t0     # host time to issue the K steps (drivers return after their final info read)
     comm.barrier()
     sync()
     dt = time.perf_counter() - t0
     dt_max = comm.allreduce_scalar(dt, "max") if world > 1 else dt
-    resid = _residual(args, A, backup, locals().get("piv")) if (world == 1 and args.check) else None
+    host_max = comm.allreduce_scalar(t_host, "max") if world > 1 else t_host
+    extra = (B, C) if args.routine == "gemm" else None
+    resid = _residual(args, A, backup, locals().get("piv"), comm, extra) if args.check else None
+    tol = 3 * 2.0 ** -52                 # reference tester default: tol 3 x eps
     fl = flops(args.routine, n, args.m)
     gflops = fl * args.steps / dt_max / 1e9
     ok = (info == 0) if isinstance(info, int) else True
@@ -221,12 +299,19 @@ def main():
             "pct_fp64_peak": round(100 * gflops / 1e3 / (FP64_PEAK_TF * world), 2),
             "info_ok": bool(ok),
             "residual": resid,
+            "residual_ok": None if resid is None else bool(resid <= tol),
+            "host_ms_per_step": round(host_max / args.steps * 1e3, 3),
             "config": {"model": f"d{args.routine} n={n} nb={nb}", "global_batch": 1, "seq_len": n,
                        "n": n, "nb": nb, "grid": f"{p}x{q}", "lookahead": args.lookahead,
                        "parallelism": f"2d-block-cyclic {p}x{q}"},
         }
         print(json.dumps(out), flush=True)
     sl.finalize()
+    bad = (not ok) or (resid is not None and not resid <= tol)
+    if bad:
+        print(f"bench: FAILED correctness check (info_ok={ok}, residual={resid}, tol={tol:.2e})",
+              file=sys.stderr, flush=True)
+        sys.exit(1)
 
 
 if __name__ == "__main__":

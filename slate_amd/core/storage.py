@@ -282,8 +282,19 @@ class MatrixStorage:
         if blk is not None:
             dev = self.device_of(slot)
             if dev.type == "cuda":
-                # stream-ordered: reusable by this stream at once, by others after its event
-                self.pools[slot].free(*blk, torch.cuda.current_stream(dev).cuda_stream)
+                # stream-ordered: reusable by this stream at once, by others
+                # after its event.  A workspace tile may have been last read on
+                # a pipeline stream (panel / diag / update) other than the
+                # freeing one: the freeing stream first waits for all of them,
+                # so the block cannot be handed out while one still reads it
+                # (ADVICE r2).  Frees are rare (workspace release), the joins
+                # cheap (event record + wait per stream).
+                cur = torch.cuda.current_stream(dev)
+                from ..parallel.streams import StreamSet
+                for other in StreamSet.streams_of(dev):
+                    if other is not None and other != cur:
+                        cur.wait_event(other.record_event())
+                self.pools[slot].free(*blk, cur.cuda_stream)
             else:
                 self.pools[slot].free(*blk)
         self.tiles.pop((i, j, slot), None)

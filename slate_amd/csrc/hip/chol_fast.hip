@@ -107,7 +107,13 @@ __device__ inline void strip_update(d4 (&acc)[NS][NT], const double* Xb, const i
 
 // ---------------------------------------------------------------- potrf_lds
 __global__ void __launch_bounds__(PT)
-potrf_lds_kernel(int n, double* __restrict__ A, i64 lda, i64* info, i64 info_off, i64* prof) {
+potrf_lds_kernel(int n, double* __restrict__ A, i64 lda, i64* info, i64 info_off, i64* prof, const int* gate,
+                 const double* floorp) {
+    // gate: device predicate (0 = skip the launch); floorp: regularised mode
+    // -- a pivot <= *floorp is replaced by *floorp instead of failing (the
+    // CholeskyQR fallback, qr_fast.hip)
+    if (gate && *gate == 0) return;
+    const double pfloor = floorp ? *floorp : 0.0;
     __shared__ double P[PB * PLD];          // P[c * PLD + r] = A(c0 + r, c0 + c)
     __shared__ double Li[16][17];            // inverse of the current 16 x 16 diagonal sub-block
     __shared__ double Ld[16][17];            // its Cholesky factor (row-major, zero above)
@@ -206,11 +212,17 @@ potrf_lds_kernel(int n, double* __restrict__ A, i64 lda, i64* info, i64 info_off
                         double d0 = Dd[j][j];
                         const double d10 = Dd[j + 1][j], d11 = Dd[j + 1][j + 1];
                         const double a0 = Dd[di][j], a1 = Dd[di][j + 1], b0 = Dd[dc][j], b1 = Dd[dc][j + 1];
-                        if (j < wq && !(d0 > 0.0)) { if (!fail) fail = c0 + q0 + j + 1; d0 = 1.0; }
+                        if (j < wq && !(d0 > pfloor)) {
+                            if (pfloor > 0.0) d0 = pfloor;
+                            else { if (!fail) fail = c0 + q0 + j + 1; d0 = 1.0; }
+                        }
                         const double i0 = rsq_f64(d0), s0 = d0 * i0;          // 1 / L(j, j), L(j, j)
                         const double l10 = d10 * i0;
                         double e = d11 - l10 * l10;
-                        if (j + 1 < wq && !(e > 0.0)) { if (!fail) fail = c0 + q0 + j + 2; e = 1.0; }
+                        if (j + 1 < wq && !(e > pfloor)) {
+                            if (pfloor > 0.0) e = pfloor;
+                            else { if (!fail) fail = c0 + q0 + j + 2; e = 1.0; }
+                        }
                         const double i1 = rsq_f64(e), s1 = e * i1;
                         const double ld0 = a0 * i0, ld1 = (a1 - ld0 * l10) * i1;   // L(di, j), L(di, j+1)
                         const double lc0 = b0 * i0, lc1 = (b1 - lc0 * l10) * i1;   // L(dc, j), L(dc, j+1)
@@ -299,7 +311,9 @@ potrf_lds_kernel(int n, double* __restrict__ A, i64 lda, i64* info, i64 info_off
 // ---------------------------------------------------------------- tri_inv32
 // Winv[b] (32 x 32, column-major, zero above the diagonal) = inv(L_bb).
 __global__ void __launch_bounds__(64)
-tri_inv32_kernel(int n, const double* __restrict__ L, i64 ldl, double* __restrict__ Winv, bool unit) {
+tri_inv32_kernel(int n, const double* __restrict__ L, i64 ldl, double* __restrict__ Winv, bool unit,
+                 const int* gate) {
+    if (gate && *gate == 0) return;
     __shared__ double S[32][33];            // S[r][c] = L(c0 + r, c0 + c)
     const int b = blockIdx.x, c0 = 32 * b, jb = min(32, n - c0), t = threadIdx.x;
     if (t < 32) {
@@ -335,7 +349,8 @@ tri_inv32_kernel(int n, const double* __restrict__ L, i64 ldl, double* __restric
 constexpr int TBM = 64;
 __global__ void __launch_bounds__(512)
 trsm_rlt_kernel(i64 m, int n, double alpha, const double* __restrict__ L, i64 ldl, const double* __restrict__ Winv,
-                double* __restrict__ B, i64 ldb) {
+                double* __restrict__ B, i64 ldb, const int* gate) {
+    if (gate && *gate == 0) return;
     // row pitch = 16 mod 32 doubles: the two k rows of one ds_read_b64 lane
     // group land in opposite bank halves (an odd pitch left 2-way conflicts:
     // 33 % of LDS cycles, profiles/pmc_hot_kernels.md)
@@ -438,9 +453,11 @@ trsm_lln_kernel(int m, i64 n, double alpha, const double* __restrict__ L, i64 ld
 }
 
 // ---------------------------------------------------------------- launchers
-bool potrf_fast(int n, double* A, i64 lda, i64* info, i64 info_off, hipStream_t s) {
+bool potrf_fast(int n, double* A, i64 lda, i64* info, i64 info_off, hipStream_t s, const int* gate,
+                const double* floorp) {
     if (n <= 0 || n > PN) return false;
-    hipLaunchKernelGGL(potrf_lds_kernel, dim3(1), dim3(PT), 0, s, n, A, lda, info, info_off, (i64*)nullptr);
+    hipLaunchKernelGGL(potrf_lds_kernel, dim3(1), dim3(PT), 0, s, n, A, lda, info, info_off, (i64*)nullptr, gate,
+                       floorp);
     HIP_LAUNCH_CHECK();
     return true;
 }
@@ -448,20 +465,21 @@ bool potrf_fast(int n, double* A, i64 lda, i64* info, i64 info_off, hipStream_t 
 // tools: phase totals (shader clocks: load, update, diag, solve, half, writeback,
 // total) and wall-clock ticks (100 MHz) of one potrf_lds launch
 void potrf_lds_profile(int n, double* A, i64 lda, i64* info, i64* prof, hipStream_t s) {
-    hipLaunchKernelGGL(potrf_lds_kernel, dim3(1), dim3(PT), 0, s, n, A, lda, info, (i64)0, prof);
+    hipLaunchKernelGGL(potrf_lds_kernel, dim3(1), dim3(PT), 0, s, n, A, lda, info, (i64)0, prof, (const int*)nullptr,
+                       (const double*)nullptr);
     HIP_LAUNCH_CHECK();
 }
 
 bool trsm_rlt_fast(i64 m, i64 n, double alpha, const double* L, i64 ldl, double* B, i64 ldb, bool unit,
-                   hipStream_t s) {
+                   hipStream_t s, const int* gate) {
     if (m <= 0 || n <= 0) return true;
     if (n > 1024) return false;
     const int nbj = (int)((n + 31) / 32);
     double* W = static_cast<double*>(workspace(s, sizeof(double) * (size_t)nbj * 1024, WS_C));
-    hipLaunchKernelGGL(tri_inv32_kernel, dim3(nbj), dim3(64), 0, s, (int)n, L, ldl, W, unit);
+    hipLaunchKernelGGL(tri_inv32_kernel, dim3(nbj), dim3(64), 0, s, (int)n, L, ldl, W, unit, gate);
     HIP_LAUNCH_CHECK();
     hipLaunchKernelGGL(trsm_rlt_kernel, dim3((unsigned)((m + TBM - 1) / TBM)), dim3(512), 0, s, m, (int)n, alpha, L,
-                       ldl, (const double*)W, B, ldb);
+                       ldl, (const double*)W, B, ldb, gate);
     HIP_LAUNCH_CHECK();
     return true;
 }
@@ -472,7 +490,7 @@ bool trsm_lln_fast(i64 m, i64 n, double alpha, const double* L, i64 ldl, double*
     if (m > 1024) return false;
     const int nbj = (int)((m + 31) / 32);
     double* W = static_cast<double*>(workspace(s, sizeof(double) * (size_t)nbj * 1024, WS_C));
-    hipLaunchKernelGGL(tri_inv32_kernel, dim3(nbj), dim3(64), 0, s, (int)m, L, ldl, W, unit);
+    hipLaunchKernelGGL(tri_inv32_kernel, dim3(nbj), dim3(64), 0, s, (int)m, L, ldl, W, unit, (const int*)nullptr);
     HIP_LAUNCH_CHECK();
     hipLaunchKernelGGL(trsm_lln_kernel, dim3((unsigned)((n + TBN - 1) / TBN)), dim3(256), 0, s, (int)m, n, alpha, L,
                        ldl, (const double*)W, B, ldb);

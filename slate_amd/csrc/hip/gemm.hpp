@@ -62,6 +62,7 @@ struct GemmArgs {
     int remap;               // 0: plain order; 1: XCD-chunked grouped order (full output);
                              // 2: compact lower triangle of 8x8 super-tiles (set by launch_real)
     TriMask mask;
+    const int* gate;         // optional device predicate (GemmCall::gate)
 };
 
 // ---------------------------------------------------------------------------
@@ -148,6 +149,7 @@ __global__ void __launch_bounds__(64 * WVM * WVN, OCC)
 gemm_real_kernel(GemmArgs<T> a) {
     using MF = mfma_real<T>;
     using acc_t = typename MF::acc_t;
+    if (a.gate && *a.gate == 0) return;
     constexpr int NT = 64 * WVM * WVN;
     constexpr int WM = BM / WVM, WN = BN / WVN;
     constexpr int MI = WM / 16, NI = WN / 16;
@@ -280,6 +282,7 @@ gemm_complex_kernel(GemmArgs<T> a) {
     using R = typename scalar_traits<T>::real;
     using MF = mfma_real<R>;
     using acc_t = typename MF::acc_t;
+    if (a.gate && *a.gate == 0) return;
     constexpr int NT = 256;
     constexpr int WM = BM / 2, WN = BN / 2;
     constexpr int MI = WM / 16, NI = WN / 16;

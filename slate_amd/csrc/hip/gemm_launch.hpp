@@ -16,7 +16,8 @@ namespace slate_hip {
 // reduction kernel (fixed summation order -> bit-reproducible results).
 template <typename T>
 __global__ void splitk_reduce_kernel(i64 m, i64 n, int ks, const T* __restrict__ W, T alpha, T beta, T* C,
-                                     i64 ldc) {
+                                     i64 ldc, const int* gate) {
+    if (gate && *gate == 0) return;
     const i64 i = (i64)blockIdx.x * 256 + threadIdx.x;
     if (i >= m) return;
     const i64 mn = m * n;
@@ -66,7 +67,7 @@ static bool gemm_splitk(const GemmCall& c, int tile, hipStream_t s, Launch&& lau
     }
     dim3 grid((unsigned)((c.m + 255) / 256), (unsigned)std::min<i64>(c.n, 1024));
     hipLaunchKernelGGL(splitk_reduce_kernel<T>, grid, dim3(256), 0, s, c.m, c.n, (int)ks, W, alpha, beta,
-                       static_cast<T*>(c.C), c.ldc);
+                       static_cast<T*>(c.C), c.ldc, c.gate);
     HIP_LAUNCH_CHECK();
     return true;
 }
@@ -183,6 +184,7 @@ void gemm_real(const GemmCall& c, hipStream_t s) {
     a.group_m = 8;
     a.mask = c.mask;
     a.remap = c.mask.mode == 0 ? 1 : 0;
+    a.gate = c.gate;
     if (c.m <= 0 || c.n <= 0) return;
     dispatch_real<T>(c.transA != 'N', c.transB != 'N', ptrs, a, (int)c.batch, s);
 }
@@ -231,6 +233,7 @@ void gemm_complex(const GemmCall& c, hipStream_t s) {
     a.group_m = 8;
     a.mask = c.mask;
     a.remap = c.mask.mode == 0 ? 1 : 0;
+    a.gate = c.gate;
     if (c.m <= 0 || c.n <= 0) return;
     if (ptrs) dispatch_cplx<T, true>(c.transA, c.transB, a, (int)c.batch, s);
     else dispatch_cplx<T, false>(c.transA, c.transB, a, (int)c.batch, s);

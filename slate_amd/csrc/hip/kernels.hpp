@@ -13,14 +13,16 @@ void trmm(char side, char uplo, char trans, char diag, i64 m, i64 n, T alpha,
           const T* A, i64 lda, T* B, i64 ldb, hipStream_t s);
 
 // chol_fast.hip (fp64 fast paths; return false when the shape is not covered)
-bool potrf_fast(int n, double* A, i64 lda, i64* info, i64 info_off, hipStream_t s);
+bool potrf_fast(int n, double* A, i64 lda, i64* info, i64 info_off, hipStream_t s, const int* gate = nullptr,
+                const double* floorp = nullptr);
 void potrf_lds_profile(int n, double* A, i64 lda, i64* info, i64* prof, hipStream_t s);
 bool trsm_rlt_fast(i64 m, i64 n, double alpha, const double* L, i64 ldl, double* B, i64 ldb, bool unit,
-                   hipStream_t s);
+                   hipStream_t s, const int* gate = nullptr);
 bool trsm_lln_fast(i64 m, i64 n, double alpha, const double* L, i64 ldl, double* B, i64 ldb, bool unit,
                    hipStream_t s);
-// qr_fast.hip: tall fp64 QR panel (shifted CholeskyQR3 + Householder reconstruction);
-// false = not applicable, or broke down (panel restored)
+// qr_fast.hip: tall fp64 QR panel (CholeskyQR2, device-decided fallback to a
+// perturbed shifted CholeskyQR3, Householder reconstruction); false = not
+// applicable (shape / SLATE_AMD_QR_PANEL=householder).  No host read-back.
 bool geqrf_cholqr(i64 m, i64 b, double* A, i64 lda, double* tau, double* Tm, i64 ldt, double* V, i64 ldv,
                   hipStream_t s);
 

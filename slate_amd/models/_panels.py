@@ -19,47 +19,72 @@ index tensor, so no host->device copy happens inside the step loop.
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from .. import ops
 from ._util import tiles_local_before
 
 
-def _rows_plan(tileMb, tfirst, tend, nb, p, q, pc, cols_from):
-    need = [j for j in range(cols_from, tend) if j % q == pc]
-    rows_of = {}
+def _ranges(starts, lens):
+    """Concatenation of arange(s, s + l) over (s, l) pairs (numpy, no loop)."""
+    starts = np.asarray(starts, dtype=np.int64)
+    lens = np.asarray(lens, dtype=np.int64)
+    tot = int(lens.sum()) if lens.size else 0
+    if tot == 0:
+        return np.zeros(0, dtype=np.int64)
+    first = np.cumsum(lens) - lens                  # output position of each range
+    return np.repeat(starts - first, lens) + np.arange(tot, dtype=np.int64)
+
+
+def _rows_plan(mbs, tfirst, tend, nb, p, q, pc, cols_from):
+    """``mbs[j]`` = row count of tile j.  Returns (rows_of[r] arrays, total,
+    order array): the local rows (relative to the local start of tile
+    ``tfirst``) process row r contributes, and where each needed tile's rows
+    land in the gathered buffer, in tile order."""
+    need = np.arange(cols_from, tend, dtype=np.int64)
+    need = need[need % q == pc]
+    mb = np.asarray([mbs[j] for j in need.tolist()], dtype=np.int64)
+    r_of = need % p
+    rows_of, base, pos = {}, {}, 0
+    start_in_r = np.zeros(need.size, dtype=np.int64)
     for r in range(p):
+        sel = r_of == r
         base_r = tiles_local_before(tfirst, p, r) * nb
-        idx = []
-        for j in need:
-            if j % p != r:
-                continue
-            lj = (j // p) * nb - base_r
-            idx.extend(range(lj, lj + tileMb(j)))
-        rows_of[r] = idx
-    base, pos = {}, 0
-    for r in range(p):
+        lj = (need[sel] // p) * nb - base_r
+        rows_of[r] = _ranges(lj, mb[sel])
+        start_in_r[sel] = np.cumsum(mb[sel]) - mb[sel]
         base[r] = pos
-        pos += len(rows_of[r])
-    order = []
-    cursor = {r: 0 for r in range(p)}
-    for j in need:
-        r = j % p
-        rows = tileMb(j)
-        order.extend(range(base[r] + cursor[r], base[r] + cursor[r] + rows))
-        cursor[r] += rows
+        pos += int(rows_of[r].size)
+    bases = np.asarray([base[r] for r in range(p)], dtype=np.int64)
+    order = _ranges(bases[r_of] + start_in_r, mb) if need.size else np.zeros(0, dtype=np.int64)
     return rows_of, pos, order
 
 
 def _append_plan(flat, rows_of, tot, order, p):
+    """Append one plan's index arrays to ``flat`` (a list of arrays; its
+    running length is flat[0])."""
     meta = {}
     for r in range(p):
-        meta[r] = (len(flat), len(rows_of[r]))
-        flat.extend(rows_of[r])
-    meta["order"] = (len(flat), len(order))
-    flat.extend(order)
+        meta[r] = (flat[0], int(rows_of[r].size))
+        flat.append(rows_of[r])
+        flat[0] += int(rows_of[r].size)
+    meta["order"] = (flat[0], int(order.size))
+    flat.append(order)
+    flat[0] += int(order.size)
     meta["tot"] = tot
     return meta
+
+
+def _upload(flat, dev):
+    arrs = flat[1:]
+    cat = np.concatenate(arrs) if arrs else np.zeros(0, dtype=np.int64)
+    if cat.size == 0:
+        cat = np.zeros(1, dtype=np.int64)
+    t = torch.from_numpy(cat)
+    if torch.device(dev).type == "cuda":
+        t = t.pin_memory().to(dev, non_blocking=True)
+    return t
 
 
 def plan_col_gather(tileMb, tfirst, tend, nb, p, q, pc, dev, cols_from=None):
@@ -67,9 +92,40 @@ def plan_col_gather(tileMb, tfirst, tend, nb, p, q, pc, dev, cols_from=None):
     with j % q == pc from Prow buffers whose row 0 is the local start of tile
     ``tfirst`` on each process row.  Returns (meta, idx_tensor)."""
     cols_from = tfirst if cols_from is None else cols_from
-    flat = []
-    meta = _append_plan(flat, *_rows_plan(tileMb, tfirst, tend, nb, p, q, pc, cols_from), p)
-    return meta, torch.tensor(flat if flat else [0], dtype=torch.int64, device=dev)
+    key = ("one", tfirst, tend, nb, p, q, pc, cols_from, _mb_sig(tileMb, tfirst, tend), str(dev))
+    hit = _PLAN_CACHE.get(key)
+    if hit is not None:
+        return hit
+    mbs = {j: tileMb(j) for j in range(tfirst, tend)}
+    flat = [0]
+    meta = _append_plan(flat, *_rows_plan(mbs, tfirst, tend, nb, p, q, pc, cols_from), p)
+    out = (meta, _upload(flat, dev))
+    _cache_put(key, out)
+    return out
+
+
+# Plans depend only on the geometry: cached across driver calls (the bench
+# and every solver factor the same shape repeatedly).  Cached index tensors
+# are read-only.
+_PLAN_CACHE = {}
+_PLAN_CACHE_MAX = 64
+
+
+def _cache_put(key, val):
+    if len(_PLAN_CACHE) >= _PLAN_CACHE_MAX:
+        _PLAN_CACHE.pop(next(iter(_PLAN_CACHE)))
+    _PLAN_CACHE[key] = val
+
+
+def _mb_sig(tileMb, t0, t1):
+    """Row-count signature of tiles [t0, t1): uniform runs compress to
+    (first, last, count) so the key stays small."""
+    if t1 <= t0:
+        return ()
+    first, last = tileMb(t0), tileMb(t1 - 1)
+    if t1 - t0 <= 2 or all(tileMb(j) == first for j in range(t0 + 1, t1 - 1)):
+        return (first, last, t1 - t0)
+    return tuple(tileMb(j) for j in range(t0, t1))
 
 
 def plan_col_gathers_steps(tileMb, g0, nt, nb, p, q, pc, dev, split=None):
@@ -77,20 +133,30 @@ def plan_col_gathers_steps(tileMb, g0, nt, nb, p, q, pc, dev, split=None):
     diagonal tile g0+t), all uploaded as ONE index tensor.  With ``split``
     = la, each step gets two plans: the lookahead tiles g+1 .. g+la (the
     critical path) and the rest (the trailing update, off the critical
-    path)."""
-    flat, metas = [], []
+    path).  Built with numpy range arithmetic and cached per geometry, so a
+    repeated call costs a dictionary lookup (the round-2 list-of-ints build
+    took ~40 ms per call at n = 32768 on a 2 x 4 grid)."""
+    key = ("steps", g0, nt, nb, p, q, pc, split, _mb_sig(tileMb, g0, g0 + nt), str(dev))
+    hit = _PLAN_CACHE.get(key)
+    if hit is not None:
+        return hit
+    mbs = {j: tileMb(j) for j in range(g0, g0 + nt)}
+    flat, metas = [0], []
     for t in range(nt):
         g = g0 + t
         if split is None:
-            metas.append(_append_plan(flat, *_rows_plan(tileMb, g + 1, g0 + nt, nb, p, q, pc, g + 1), p))
+            metas.append(_append_plan(flat, *_rows_plan(mbs, g + 1, g0 + nt, nb, p, q, pc, g + 1), p))
         else:
             e = min(g + 1 + split, g0 + nt)
-            metas.append((_append_plan(flat, *_rows_plan(tileMb, g + 1, e, nb, p, q, pc, g + 1), p),
-                          _append_plan(flat, *_rows_plan(tileMb, g + 1, g0 + nt, nb, p, q, pc, e), p)))
-    idx = torch.tensor(flat if flat else [0], dtype=torch.int64, device=dev)
+            metas.append((_append_plan(flat, *_rows_plan(mbs, g + 1, e, nb, p, q, pc, g + 1), p),
+                          _append_plan(flat, *_rows_plan(mbs, g + 1, g0 + nt, nb, p, q, pc, e), p)))
+    idx = _upload(flat, dev)
     if split is None:
-        return [(m, idx) for m in metas]
-    return [((a, idx), (b, idx)) for a, b in metas]
+        out = [(m, idx) for m in metas]
+    else:
+        out = [((a, idx), (b, idx)) for a, b in metas]
+    _cache_put(key, out)
+    return out
 
 
 def assemble_cols(plan, Prow, grid, p, kb, dtype, dev, comm=None):
@@ -151,13 +217,27 @@ def col_bcast(grid, src, owner_pr, kb, ncols, dtype, dev):
     return P
 
 
+_GROWS = {}
+
+
 def rows_global(lr0, lr1, nb, p, pr, r0, dev):
     """Panel-relative global rows (global - r0) of local rows [lr0, lr1) of
-    process row pr (block-cyclic, tile nb)."""
-    import numpy as np
-    lr = np.arange(lr0, lr1, dtype=np.int64)
-    g = ((lr // nb) * p + pr) * nb + lr % nb - r0
-    return torch.from_numpy(g).to(dev)
+    process row pr (block-cyclic, tile nb).  The local->global row table is
+    uploaded once per (nb, p, pr, device) and sliced on the device, so the
+    step loops of getrf / he2hb issue no host->device copy (the round-2
+    version built and uploaded a fresh numpy range per step: a pageable copy
+    that blocked the host until the stream caught up)."""
+    key = (nb, p, pr, str(dev))
+    tab = _GROWS.get(key)
+    if tab is None or tab.numel() < lr1:
+        L = max(lr1, 2 * (tab.numel() if tab is not None else 0), 1024)
+        lr = np.arange(L, dtype=np.int64)
+        g = torch.from_numpy(((lr // nb) * p + pr) * nb + lr % nb)
+        if torch.device(dev).type == "cuda":
+            g = g.pin_memory().to(dev, non_blocking=True)
+        _GROWS[key] = tab = g
+    v = tab[lr0:lr1]
+    return v - r0 if r0 else v
 
 
 def panel_allgather(colc, buf, mloc, t0, lc, kb, nb, p, pr, nloc_r, dt, dev):

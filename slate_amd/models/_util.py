@@ -51,3 +51,20 @@ def uplo_char(u):
 
 def conj_trans(dtype):
     return 'C' if dtype.is_complex else 'T'
+
+
+def read_to_host(t):
+    """Host copy of a (small) device tensor at the END of a driver: a
+    non-blocking copy into pinned memory, then one event wait.  This is the
+    only point where a factorization waits for the GPU (info values), and it
+    is not a torch "synchronizing op" (tests run the drivers under
+    torch.cuda.set_sync_debug_mode("error"))."""
+    import torch
+    if not t.is_cuda:
+        return t
+    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    h.copy_(t, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    ev.synchronize()
+    return h

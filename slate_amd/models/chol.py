@@ -97,10 +97,10 @@ def _potrf_lower(A, opts):
         _potrf_1x1_grouped(A, s, buf, nb, g0, nt, R_end, la, group, ss, infos, ct, dev)
         s.mark_local_modified(slot)
         return _potrf_info(s, infos, g0, nt)
-    # per step: the lookahead tiles' transposed rows (critical path, panel
-    # stream) and the rest (update stream, its own column communicator)
+    # per step: the lookahead tiles' transposed rows (critical path) and the
+    # rest (the trailing update's operand); both gathered from the panel
+    # stream.  Plans are cached per geometry (_panels.plan_col_gathers_steps).
     plans = plan_col_gathers_steps(s.tileMb, g0, nt, nb, p, q, pc, dev, split=la) if (p > 1 or q > 1) else None
-    colu = grid.col_comm_u if (grid is not None and p > 1) else None
     # diag-first (needs a lookahead column): right after the panel solve of
     # step t, the rows of tile g+1 travel to the next diagonal owner, which
     # updates and factors A(g+1, g+1) on the diag stream while the big
@@ -149,17 +149,30 @@ def _potrf_lower(A, opts):
                     g1 = g + 1
                     kb1 = s.tileMb(g1) if t + 1 < nt - 1 or A.last_mb is None else A.last_mb
                     if pr == g1 % p:
+                        # the rows of tile g+1 of the solved panel: a small
+                        # broadcast issued from the PANEL stream (every
+                        # collective of this driver is issued from the panel
+                        # stream in one program order on every rank; the diag
+                        # stream carries compute only)
+                        if q > 1:
+                            Pt = ops.colmajor_empty(kb1, kb, dtype, dev)
+                            if own_col:
+                                Pt.copy_(buf[lr1:lr1 + kb1, lcg:lcg + kb])
+                            grid.row_comm.bcast(Pt, g % q)
+                        else:
+                            Pt = buf[lr1:lr1 + kb1, lcg:lcg + kb]
                         ev_solve = ss.event(ss.panel)
                         with ss.use(ss.diag):
                             ss.wait(ss.diag, ev_solve)
+                            # A(g+1, g+1) must also hold every earlier trailing
+                            # update: with la < 2 column g+1 was not a lookahead
+                            # column of step t-1, so its update by panel t-1
+                            # ran on the update stream (first part, ev_tr[t-1])
+                            if la < 2 and t >= 1:
+                                ss.wait(ss.diag, ev_tr[t - 1])
+                            if Pt.is_cuda and q > 1:
+                                Pt.record_stream(ss.diag)
                             with trace_block("potrf::diag_first"):
-                                if q > 1:
-                                    Pt = ops.colmajor_empty(kb1, kb, dtype, dev)
-                                    if own_col:
-                                        Pt.copy_(buf[lr1:lr1 + kb1, lcg:lcg + kb])
-                                    grid.row_comm.bcast(Pt, g % q)
-                                else:
-                                    Pt = buf[lr1:lr1 + kb1, lcg:lcg + kb]
                                 if pc == g1 % q:
                                     D1 = buf[lr1:lr1 + kb1, lc1:lc1 + kb1]
                                     ops.gemm(-1.0, Pt, Pt, 1.0, D1, 'N', ct, (1, 1 << 40, 1, 0, 1, 0, 0, 0, 0))
@@ -200,6 +213,15 @@ def _potrf_lower(A, opts):
                 else:
                     mask = (1, nb, p, pr, q, pc, lr1, lc1, 0)
                     ops.gemm(-1.0, Prow, Lla[0:lc_la - lc1], 1.0, buf[lr1:lr_end, lc1:lc_la], 'N', ct, mask)
+            # the trailing update's transposed rows: gathered over the same
+            # column communicator, from the panel stream, AFTER the lookahead
+            # update (off the critical chain; one issue order of collectives
+            # on every rank, no second communicator per dimension)
+            if plans is not None:
+                Lcol = assemble_cols(plans[t][1], Prow, grid, p, kb, dtype, dev)
+                loff = lc_la            # Lcol row 0 = local column lc_la
+            else:
+                loff = lc1
             ev_panel = ss.event(ss.panel)
         # trailing update
         us = ss.update[0]
@@ -211,12 +233,9 @@ def _potrf_lower(A, opts):
             lc_nx = max(lc_nx, lc_la)
             if Prow.is_cuda and lc_end > lc_la and nrow:
                 Prow.record_stream(us)
+                if Lcol is not Prow:
+                    Lcol.record_stream(us)
             with trace_block("potrf::trailing"):
-                if plans is not None:
-                    Lcol = assemble_cols(plans[t][1], Prow, grid, p, kb, dtype, dev, comm=colu)
-                    loff = lc_la            # Lcol row 0 = local column lc_la
-                else:
-                    loff = lc1
                 for c0, c1 in ((lc_la, lc_nx), (lc_nx, lc_end)):
                     if c1 > c0 and nrow:
                         mask = (1, nb, p, pr, q, pc, lr1, c0, 0)
@@ -231,7 +250,8 @@ def _potrf_lower(A, opts):
 
 def _potrf_info(s, infos, g0, nt):
     """First failing global column (1-based), reduced over ranks."""
-    iv = infos.cpu()
+    from ._util import read_to_host
+    iv = read_to_host(infos).tolist()
     info = 0
     for t in range(nt):
         _wd.beat(f"potrf step {t}")

@@ -201,7 +201,8 @@ def _update_cols(buf, Lp, ipiv, r0, kb, m, c0, c1, nopiv):
 
 
 def _reduce_info(A, infos, kt, nb):
-    iv = infos[:kt].cpu()
+    from ._util import read_to_host
+    iv = read_to_host(infos[:kt]).tolist()
     info = 0
     for k in range(kt):
         _wd.beat(f"getrf step {k}")
@@ -251,11 +252,10 @@ class _Pack:
 
 
 def _rows_global(lr0, lr1, nb, p, pr, r0, dev):
-    """Panel-relative global rows of local rows [lr0, lr1) of process row pr."""
-    import numpy as np
-    lr = np.arange(lr0, lr1, dtype=np.int64)
-    g = ((lr // nb) * p + pr) * nb + lr % nb - r0
-    return torch.from_numpy(g).to(dev)
+    """Panel-relative global rows of local rows [lr0, lr1) of process row pr
+    (a device slice of a table uploaded once per geometry)."""
+    from ._panels import rows_global
+    return rows_global(lr0, lr1, nb, p, pr, r0, dev)
 
 
 def _getrf_general(A, buf, thr, la, mode, leaf):

@@ -87,6 +87,19 @@ class StreamSet:
                               "the trailing update shares every CU with the panel kernels", RuntimeWarning)
         return torch.cuda.Stream(device=device, priority=0)
 
+    @classmethod
+    def streams_of(cls, device):
+        """Every pipeline stream created for ``device`` (distinct objects)."""
+        dev = torch.device(device)
+        out, seen = [], set()
+        for key, ss in cls._cache.items():
+            if ss.gpu and ss.device == dev or (ss.gpu and dev.index is None and ss.device.type == dev.type):
+                for st in [ss.panel, ss.diag] + list(ss.update):
+                    if st is not None and id(st) not in seen:
+                        seen.add(id(st))
+                        out.append(st)
+        return out
+
     def use(self, s):
         if s is None or not self.gpu:
             return contextlib.nullcontext()

@@ -19,6 +19,8 @@ import time
 
 import torch
 
+from . import watchdog as _wd
+
 from .. import _native
 
 _rec = _native._host.TraceRecorder()
@@ -124,9 +126,20 @@ def _write_svg(path, allev, width=1600, row_h=20):
 
 @contextlib.contextmanager
 def trace_block(name):
-    if not _rec.is_on():
-        yield
-        return
+    # every traced region is also a library region for the watchdog: it
+    # checks staleness only while some driver is running, and every region
+    # entry / exit is a heartbeat
+    _wd.enter(name)
+    try:
+        if not _rec.is_on():
+            yield
+            return
+        yield from _traced(name)
+    finally:
+        _wd.leave(name)
+
+
+def _traced(name):
     depth = getattr(_nest, "d", 0)
     _nest.d = depth + 1
     e0 = None

@@ -17,6 +17,14 @@ a lost peer shows up as a stream that never drains.  Two layers:
   status 3 so the launcher (torchrun) tears the job down.
 
 ``SLATE_AMD_WATCHDOG=<seconds>`` arms it from ``comm.init``.
+
+Staleness is only checked while the process is INSIDE the library: every
+driver region (``trace_block``) calls :func:`enter` / :func:`leave`, which
+keep a depth count and beat.  Time the application spends outside
+slate_amd -- its own compute, I/O, waiting for input -- never fires the
+watchdog.  Inside, the limit must exceed the longest single phase that
+cannot beat (one GPU call such as the bulge chase of heev, a few seconds at
+n = 16384); the default collective timeout is 600 s.
 """
 from __future__ import annotations
 
@@ -37,6 +45,24 @@ def beat(tag: str = "") -> None:
     _state["t"] = time.monotonic()
     _state["tag"] = tag
     _state["n"] += 1
+
+
+_depth = [0]
+
+
+def enter(tag: str = "") -> None:
+    """Entering a library region (nestable)."""
+    _depth[0] += 1
+    beat(tag)
+
+
+def leave(tag: str = "") -> None:
+    _depth[0] = max(0, _depth[0] - 1)
+    beat(tag)
+
+
+def inside() -> bool:
+    return _depth[0] > 0
 
 
 def last_beat():
@@ -92,7 +118,7 @@ class Watchdog:
     def _run(self):
         while not self._stop.wait(self.poll):
             tag, age, n = last_beat()
-            if age <= self.timeout:
+            if age <= self.timeout or not inside():
                 continue
             self.fired = self._report(tag, age, n)
             if self.callback is not None:

@@ -1,0 +1,108 @@
+"""The factorization loops never wait for the GPU.
+
+potrf / getrf / geqrf run under ``torch.cuda.set_sync_debug_mode("error")``:
+any synchronising torch operation inside a driver (a pageable host->device
+copy, ``.item()``, ``.cpu()``, ``nonzero``) raises.  The one wait a driver
+does -- the info values at its end -- goes through a pinned non-blocking copy
+and an event wait (``models/_util.read_to_host``), which is not such an op.
+The CholeskyQR panel's fallback decision is taken on the device
+(csrc/hip/qr_fast.hip), so the tall-QR case covers it too.
+
+The multi-rank case is covered on the CPU (gloo stages every collective
+through host memory by construction, so it cannot run under this mode)."""
+import os
+
+import pytest
+import torch
+
+import slate_amd as sl
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_nosync(fn):
+    torch.cuda.synchronize()
+    old = torch.cuda.get_sync_debug_mode()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        return fn()
+    finally:
+        torch.cuda.set_sync_debug_mode(old)
+        torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("group", ["2", "1"])
+def test_potrf_no_host_sync(group, monkeypatch):
+    monkeypatch.setenv("SLATE_AMD_POTRF_GROUP", group)
+    dev = torch.device("cuda")
+    n, nb = 2048, 256
+    A = sl.HermitianMatrix(sl.Uplo.Lower, n, nb=nb, device=dev)
+    A.insertLocalTiles(device=dev)
+    sl.generate_matrix(A, "poev", seed=3)
+    F0 = A.storage.local[A.storage.origin_slot][:n, :n].clone()
+    info = _run_nosync(lambda: sl.potrf(A, {sl.Option.Lookahead: 1}))
+    assert info == 0
+    L = torch.tril(A.storage.local[A.storage.origin_slot][:n, :n])
+    S = torch.tril(F0) + torch.tril(F0, -1).mT
+    assert ((L @ L.mT - S).norm() / S.norm()).item() < 1e-14
+
+
+def test_getrf_no_host_sync():
+    dev = torch.device("cuda")
+    n, nb = 2048, 256
+    A = sl.Matrix(n, n, nb=nb, device=dev)
+    A.insertLocalTiles(device=dev)
+    sl.generate_matrix(A, "rands", seed=4)
+    F0 = A.storage.local[A.storage.origin_slot][:n, :n].clone()
+    piv = sl.Pivots()
+    info = _run_nosync(lambda: sl.getrf(A, piv, {sl.Option.Lookahead: 2}))
+    assert info == 0
+    F = A.storage.local[A.storage.origin_slot][:n, :n]
+    L = torch.tril(F, -1) + torch.eye(n, dtype=F.dtype, device=dev)
+    U = torch.triu(F)
+    perm = list(range(n))
+    for i, j in enumerate(piv.ipiv.tolist()):
+        perm[i], perm[j] = perm[j], perm[i]
+    PA = F0[torch.as_tensor(perm, device=dev)]
+    assert ((L @ U - PA).norm() / F0.norm()).item() < 1e-13
+
+
+@pytest.mark.parametrize("mn", [(4096, 1024), (16384, 512)])
+def test_geqrf_no_host_sync(mn):
+    m, n = mn
+    dev = torch.device("cuda")
+    nb = 256 if n > 512 else 128
+    A = sl.Matrix(m, n, nb=nb, device=dev)
+    A.insertLocalTiles(device=dev)
+    sl.generate_matrix(A, "rands", seed=5)
+    F0 = A.storage.local[A.storage.origin_slot][:m, :n].clone()
+    T = sl.TriangularFactors()
+    info = _run_nosync(lambda: sl.geqrf(A, T))
+    assert info == 0
+    R = torch.triu(A.storage.local[A.storage.origin_slot][:n, :n])
+    assert ((R.mT @ R - F0.mT @ F0).norm() / F0.norm() ** 2).item() < 1e-14
+
+
+@pytest.mark.parametrize("la", [1, 2])
+def test_potrf_diag_first_matches_serial(la, monkeypatch):
+    """Regression for the diag-first race: with la = 1
+    the next diagonal tile was factored on the diag stream before step t-1's
+    trailing update had written it.  Pipelined and fully serial
+    (SLATE_AMD_SERIAL=1: every stream is the current stream) runs must agree
+    to rounding, on a size where the trailing GEMMs are long."""
+    monkeypatch.setenv("SLATE_AMD_POTRF_GROUP", "1")
+    dev = torch.device("cuda")
+    n, nb = 8192, 512
+
+    def run():
+        A = sl.HermitianMatrix(sl.Uplo.Lower, n, nb=nb, device=dev)
+        A.insertLocalTiles(device=dev)
+        sl.generate_matrix(A, "poev", seed=9)
+        assert sl.potrf(A, {sl.Option.Lookahead: la}) == 0
+        torch.cuda.synchronize()
+        return torch.tril(A.storage.local[A.storage.origin_slot][:n, :n]).clone()
+
+    Lp = run()
+    monkeypatch.setenv("SLATE_AMD_SERIAL", "1")
+    Ls = run()
+    assert ((Lp - Ls).abs().max() / Ls.abs().max()).item() < 1e-13

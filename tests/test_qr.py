@@ -224,16 +224,27 @@ def test_geqrf_cholqr_panel(mb):
 
 
 @pytest.mark.gpu
-def test_geqrf_cholqr_breakdown_falls_back():
-    """A rank-deficient panel breaks CholeskyQR down: detected on the device,
-    the panel is restored and factored by the Householder path."""
+@pytest.mark.parametrize("kind", ["zero_dup", "rank10", "graded"])
+def test_geqrf_cholqr_breakdown_falls_back(kind):
+    """Panels that break CholeskyQR2 down (rank-deficient, or kappa beyond
+    u^-1/2): decided on the device without a host read-back, the panel is
+    restored, perturbed by 10 u ||A|| and factored by the gated shifted
+    CholeskyQR3 with a pivot floor (csrc/hip/qr_fast.hip); the result must
+    still be a backward-stable QR with orthonormal Q."""
     from slate_amd import ops
     m, b = 8192, 64
     dev = torch.device("cuda")
     g = torch.Generator().manual_seed(3)
-    A0 = torch.randn(m, b, dtype=torch.float64, generator=g).to(dev)
-    A0[:, 10] = 0.0
-    A0[:, 20] = A0[:, 3]
+    A0 = torch.randn(m, b, dtype=torch.float64, generator=g)
+    if kind == "zero_dup":
+        A0[:, 10] = 0.0
+        A0[:, 20] = A0[:, 3]
+    elif kind == "rank10":
+        A0 = torch.randn(m, 10, dtype=torch.float64, generator=g) @ torch.randn(10, b, dtype=torch.float64,
+                                                                                  generator=g)
+    else:
+        A0 = A0 * torch.logspace(0, -13, b, dtype=torch.float64)
+    A0 = A0.to(dev)
     A = A0.t().contiguous().t()
     tau = torch.zeros(b, dtype=torch.float64, device=dev)
     T, V = ops.geqrf(A, tau)

@@ -11,10 +11,25 @@ from slate_amd.utils import watchdog as wd
 def test_watchdog_fires_on_stall():
     seen = []
     w = sl.Watchdog(0.3, abort=False, callback=seen.append, poll=0.05).start()
-    wd.beat("potrf step 3")
-    time.sleep(1.0)
-    w.stop()
+    wd.enter("potrf")
+    try:
+        wd.beat("potrf step 3")
+        time.sleep(1.0)
+    finally:
+        wd.leave("potrf")
+        w.stop()
     assert seen and seen[0]["tag"] == "potrf step 3" and seen[0]["age_s"] > 0.3
+
+
+def test_watchdog_quiet_outside_library():
+    """Application time outside any slate_amd region never fires it
+    (an armed watchdog killed healthy ranks between calls)."""
+    seen = []
+    w = sl.Watchdog(0.2, abort=False, callback=seen.append, poll=0.05).start()
+    assert not wd.inside()
+    time.sleep(0.8)
+    w.stop()
+    assert not seen
 
 
 def test_watchdog_quiet_while_beating():
@@ -34,3 +49,4 @@ def test_driver_steps_beat():
     assert sl.potrf(A, {sl.Option.Target: sl.Target.HostTask}) == 0
     tag, age, n = wd.last_beat()
     assert n > n0 and tag.startswith("potrf")
+    assert not wd.inside()          # every region left
