@@ -127,6 +127,14 @@ static void register_kernels(py::module& m) {
         unsigned long long v[8];
         lu_persist_profile(enable, v);
         return std::vector<unsigned long long>(v, v + 8); });
+    // tile Cholesky variants (tools / tests): 0 = one-CU potrf_lds, 1 = multi-WG potrf_mc
+    m.def("potrf_tile_variant", [](int variant, i64 n, uintptr_t A, i64 lda, uintptr_t info, uintptr_t st) {
+        HIP_CHECK(hipMemsetAsync(P<i64>(info), 0, sizeof(i64), S(st)));
+        bool ok = variant == 1 ? potrf_mc((int)n, P<double>(A), lda, P<i64>(info), 0, S(st))
+                               : potrf_lds((int)n, P<double>(A), lda, P<i64>(info), 0, S(st));
+        if (!ok) throw std::invalid_argument("potrf_tile_variant: n out of range");
+    });
+    m.def("potrf_mc_set_prof", [](uintptr_t p) { potrf_mc_set_prof(reinterpret_cast<i64*>(p)); });
     m.def("potrf_lds_profile", [](i64 n, uintptr_t A, i64 lda, uintptr_t info, uintptr_t prof, uintptr_t st) {
         potrf_lds_profile((int)n, P<double>(A), lda, P<i64>(info), P<i64>(prof), S(st)); });
     m.def("lu_persist_fallbacks", [](int force) { return lu_persist_fallbacks(force); },

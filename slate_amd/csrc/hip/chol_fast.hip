@@ -20,6 +20,8 @@
 //               R = alpha B_J - X_{<J} L_{J,<J}^T (MFMA, K = 32 J) and
 //               X_J = R inv(L_JJ)^T (MFMA against tri_inv32's output): every
 //               flop on the matrix cores, one launch, no copy-back.
+#include <cstdlib>
+#include <cstring>
 #include "common.hpp"
 #include "kernels.hpp"
 #include "launchers.hpp"
@@ -121,7 +123,7 @@ potrf_lds_kernel(int n, double* __restrict__ A, i64 lda, i64* info, i64 info_off
     __shared__ double Xf[16][17];            // final rows of the inverse
     __shared__ double rdl[16];               // 1 / L(j, j)
     __shared__ int s_fail;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR): w-derived branches stay scalar
     if (tid == 0) s_fail = 0;
     // optional per-phase shader-clock totals (prof != nullptr: tools only)
     i64 ph[6] = {0, 0, 0, 0, 0, 0};
@@ -355,7 +357,7 @@ trsm_rlt_kernel(i64 m, int n, double alpha, const double* __restrict__ L, i64 ld
     // group land in opposite bank halves (an odd pitch left 2-way conflicts:
     // 33 % of LDS cycles, profiles/pmc_hot_kernels.md)
     __shared__ double R[32][TBM + 16];      // R[c][r]
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR): w-derived branches stay scalar
     const int st = w & 3, tt = w >> 2;       // row strip, column tile
     const i64 r0 = (i64)blockIdx.x * TBM;
     const int mr = (int)min((i64)TBM, m - r0);
@@ -406,7 +408,7 @@ __global__ void __launch_bounds__(256)
 trsm_lln_kernel(int m, i64 n, double alpha, const double* __restrict__ L, i64 ldl, const double* __restrict__ Winv,
                 double* __restrict__ B, i64 ldb) {
     __shared__ double R[32][TBN + 16];      // R[i][c] (pitch: see trsm_rlt_kernel)
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR): w-derived branches stay scalar
     const i64 cb = (i64)blockIdx.x * TBN;
     const int nc = (int)min((i64)TBN, n - cb);
     const int cl = 16 * w + (lane & 15);     // this lane's column (MFMA m index)
@@ -453,8 +455,25 @@ trsm_lln_kernel(int m, i64 n, double alpha, const double* __restrict__ L, i64 ld
 }
 
 // ---------------------------------------------------------------- launchers
+// SLATE_AMD_POTRF_TILE=lds: the one-CU kernel above; default: the
+// multi-workgroup blocked kernel of potrf_mc.hip
+static bool tile_mc() {
+    static const bool mc = [] {
+        const char* e = std::getenv("SLATE_AMD_POTRF_TILE");
+        return !(e && std::strcmp(e, "lds") == 0);
+    }();
+    return mc;
+}
+
 bool potrf_fast(int n, double* A, i64 lda, i64* info, i64 info_off, hipStream_t s, const int* gate,
                 const double* floorp) {
+    if (n <= 0 || n > PN) return false;
+    if (tile_mc()) return potrf_mc(n, A, lda, info, info_off, s, gate, floorp);
+    return potrf_lds(n, A, lda, info, info_off, s, gate, floorp);
+}
+
+bool potrf_lds(int n, double* A, i64 lda, i64* info, i64 info_off, hipStream_t s, const int* gate,
+               const double* floorp) {
     if (n <= 0 || n > PN) return false;
     hipLaunchKernelGGL(potrf_lds_kernel, dim3(1), dim3(PT), 0, s, n, A, lda, info, info_off, (i64*)nullptr, gate,
                        floorp);

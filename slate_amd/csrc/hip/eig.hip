@@ -29,7 +29,7 @@ apply_refl_kernel(i64 ncols, T* Z, i64 ldz, const T* V, i64 b, const T* tau, con
     if (s_is_zero(t)) return;
     for (i64 i = threadIdx.x; i < L; i += 64 * RW) vs[i] = V[k * b + i];
     __syncthreads();
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const i64 c0 = (i64)blockIdx.y * RCOLS;
     const i64 c1 = min(ncols, c0 + RCOLS);
     for (i64 c = c0 + wv; c < c1; c += RW) {
@@ -291,7 +291,7 @@ unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const
     __shared__ double Zs[TCW * SZ];
     __shared__ double Ws[TB * SW];
     __shared__ i64 ssp[TB], snt[TB];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
     const i64 c0 = (i64)blockIdx.x * TCW;
     const int ncw = (int)min((i64)TCW, ncols - c0);

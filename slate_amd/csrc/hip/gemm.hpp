@@ -195,7 +195,7 @@ gemm_real_kernel(GemmArgs<T> a) {
     const i64 m0 = (i64)bm * BM, n0 = (i64)bn * BN;
     if (a.mask.skip_block(m0, min(m0 + BM, a.m), n0, min(n0 + BN, a.n))) return;
 
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wid / WVN, wn = wid % WVN;
 
     acc_t acc[MI][NI];
@@ -305,7 +305,7 @@ gemm_complex_kernel(GemmArgs<T> a) {
     const i64 m0 = (i64)bm * BM, n0 = (i64)bn * BN;
     if (a.mask.skip_block(m0, min(m0 + BM, a.m), n0, min(n0 + BN, a.n))) return;
 
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wid >> 1, wn = wid & 1;
     acc_t are[MI][NI], aim[MI][NI];
     #pragma unroll

@@ -129,7 +129,7 @@ qr_step_b(i64 m, int c0, int c1, int j, T* A, i64 lda, T* tau, T* Tm, i64 ldt, v
     QrBuf<T>* qb = reinterpret_cast<QrBuf<T>*>(work);
     __shared__ double dd[QT];
     __shared__ T red[4][QB];
-    const int G = gridDim.x, g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int G = gridDim.x, g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const i64 rows_per = (m + G - 1) / G;
     const i64 r0 = (i64)g * rows_per, r1 = min(m, r0 + rows_per);
     // ---- larfg, identically in every workgroup

@@ -92,7 +92,7 @@ getrf_base_step(i64 m, int c0, int c1, int j, T* A, i64 lda, i64* ipiv, i64 ioff
     __shared__ i64 s_p;
     __shared__ int s_gw, s_bt;
     PanelBuf<T>* pb = reinterpret_cast<PanelBuf<T>*>(work);
-    const int G = gridDim.x, g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int G = gridDim.x, g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const i64 rows_per = (m + G - 1) / G;
     const i64 r0 = (i64)g * rows_per, r1 = min(m, r0 + rows_per);
     const int w = c1 - c0;
@@ -433,7 +433,7 @@ __device__ void persist_fallback(i64 m, int w, double* A, i64 lda, int* piv_s, d
     __shared__ double fv[PT2 / 64];
     __shared__ int fi[PT2 / 64];
     __shared__ int s_piv;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     for (int j = 0; j < w; ++j) {
         double v = -1.0;
         int bi = j;
@@ -489,7 +489,7 @@ getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64
     __shared__ i64 s_p;
     __shared__ int s_gw, s_bt, s_abort, s_won, s_zero;
     __shared__ int piv_s[NBB], prv_s[NBB], tr_s[2 * NBB], ts_s[2 * NBB], s_nt;
-    const int G = gridDim.x, g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int G = gridDim.x, g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const i64 rbase = (i64)g * PT2 * R;
     double a[R][NBB];
     #pragma unroll

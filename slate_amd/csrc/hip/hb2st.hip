@@ -99,7 +99,7 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
     __shared__ T s_tau;
     __shared__ R s_beta;
     __shared__ int s_j;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR): w-derived branches stay scalar
     auto At = [&](i64 r, i64 c) -> T& { return A[r + c * lda]; };
     // optional per-phase shader-clock totals (prof != nullptr: tools only)
     i64 ph[5] = {0, 0, 0, 0, 0};
@@ -418,7 +418,7 @@ tb2bd_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ UV, T* __
     __shared__ T s_tau;
     __shared__ R s_beta;
     __shared__ int s_j;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR): w-derived branches stay scalar
     auto At = [&](i64 r, i64 c) -> T& { return A[r + c * lda]; };
     // Householder generator on v[0..k) (wave 0): v <- v / (v0 - beta), v0 = 1
     auto hgen = [&](int k) {

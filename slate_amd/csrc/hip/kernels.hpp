@@ -16,6 +16,12 @@ void trmm(char side, char uplo, char trans, char diag, i64 m, i64 n, T alpha,
 bool potrf_fast(int n, double* A, i64 lda, i64* info, i64 info_off, hipStream_t s, const int* gate = nullptr,
                 const double* floorp = nullptr);
 void potrf_lds_profile(int n, double* A, i64 lda, i64* info, i64* prof, hipStream_t s);
+// potrf_mc.hip: multi-workgroup 64-blocked tile Cholesky (n <= 512)
+bool potrf_mc(int n, double* A, i64 lda, i64* info, i64 info_off, hipStream_t s, const int* gate = nullptr,
+              const double* floorp = nullptr);
+void potrf_mc_set_prof(i64* prof);
+bool potrf_lds(int n, double* A, i64 lda, i64* info, i64 info_off, hipStream_t s, const int* gate = nullptr,
+               const double* floorp = nullptr);
 bool trsm_rlt_fast(i64 m, i64 n, double alpha, const double* L, i64 ldl, double* B, i64 ldb, bool unit,
                    hipStream_t s, const int* gate = nullptr);
 bool trsm_lln_fast(i64 m, i64 n, double alpha, const double* L, i64 ldl, double* B, i64 ldb, bool unit,

@@ -55,7 +55,7 @@ potrf_small_kernel(int n, T* __restrict__ A, i64 lda, i64* info, i64 info_off) {
     constexpr int LD = NS + 1;
     __shared__ T S[NS * LD];       // S[c * LD + r] = L(r, c)
     __shared__ int s_fail;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     // 2-D thread map (no integer division), loads batched by unrolling
     {
         constexpr int CPI = NT / NS;           // columns per pass

@@ -152,7 +152,7 @@ __global__ void __launch_bounds__(HT) lu_hr_kernel(int b, double* __restrict__ A
     __shared__ double Ls[32][HB + 1];       // Ls[k][r] = L(j0 + r, j0 + k), r < M
     __shared__ double Us[32][HB + 1];       // Us[k][c] = U(j0 + k, j0 + 32 + c)
     __shared__ double rb[2][32];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
     for (int j0 = 0; j0 < b; j0 += 32) {
         const int jb = min(32, b - j0), M = b - j0, N2 = b - j0 - jb;
         // ---- (a) panel: thread r owns row j0 + r

@@ -41,7 +41,7 @@ tpqrt_panel_kernel(i64 m, i64 l, i64 j0, int ib, T* __restrict__ A, i64 lda, T* 
     __shared__ T s_tau[TP_MAXIB];
     __shared__ T s_G[TP_MAXIB * TP_MAXIB];
     __shared__ T s_T[TP_MAXIB * TP_MAXIB];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
     auto Ab = [&](i64 r, i64 c) -> T& { return A[r + c * lda]; };
     auto Bb = [&](i64 r, i64 c) -> T& { return B[r + c * ldb]; };
     for (int i = 0; i < ib; ++i) {

@@ -11,7 +11,7 @@
 namespace slate_hip {
 
 // workspace slots (one buffer per stream per slot)
-enum { WS_X = 0, WS_W = 1, WS_T = 2, WS_I = 3, WS_QW = 4, WS_QW2 = 5, WS_P = 6, WS_L = 7, WS_C = 8, WS_QF = 9 };
+enum { WS_X = 0, WS_W = 1, WS_T = 2, WS_I = 3, WS_QW = 4, WS_QW2 = 5, WS_P = 6, WS_L = 7, WS_C = 8, WS_QF = 9, WS_PM = 10 };
 
 struct WsKey {
     hipStream_t s; int slot;

@@ -521,8 +521,15 @@ def gels_cholqr(A, BX, opts=None):
 
 
 def _dev_index(A):
-    d = A.storage.device
-    return d.index if d.type == "cuda" else -1
+    """Where A's tiles live (its origin instance): new workspaces go to the
+    same memory, so a host-origin matrix on a GPU machine does not get
+    device-resident companions (mixed host / device operands)."""
+    from ..core.storage import HOST
+    st = A.storage
+    d = st.device
+    if st.origin_slot == HOST or d.type != "cuda":
+        return -1
+    return d.index if d.index is not None else 0
 
 
 def _new_like(A, m, n):

@@ -458,3 +458,41 @@ def test_gelqf_panel_device_matches_host(dt):
     ops.gelqf(Ad, td)
     assert torch.allclose(torch.tril(Ad.cpu()), torch.tril(Ah), atol=1e-12)
     assert torch.allclose(td.cpu(), th, atol=1e-12)
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 130, 200, 448, 500, 512])
+@pytest.mark.parametrize("variant", [0, 1])
+def test_potrf_tile_variants(n, variant):
+    """Both fp64 tile Cholesky kernels (0 = one-CU potrf_lds, 1 = the
+    multi-workgroup 64-blocked potrf_mc) against the fp64 torch reference;
+    lda > n, upper triangle untouched."""
+    from slate_amd import _native
+    X = ref(cm(n, n, torch.float64, 77))
+    S = X @ X.mT + n * torch.eye(n, dtype=torch.float64, device="cuda")
+    Abig = _cm(torch.zeros(n + 9, n, dtype=torch.float64, device="cuda"), "cuda")
+    Abig[:n].copy_(S)
+    A = Abig[:n]
+    info = torch.zeros(1, dtype=torch.int64, device="cuda")
+    _native.hip().potrf_tile_variant(variant, n, A.data_ptr(), A.stride(1), info.data_ptr(),
+                                     torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert int(info.item()) == 0
+    L = torch.tril(A)
+    Lr = torch.linalg.cholesky(S)
+    assert (L - Lr).abs().max() / Lr.abs().max() < 1e-13
+    assert (torch.triu(A, 1) == torch.triu(S, 1)).all()
+
+
+@pytest.mark.parametrize("bad", [0, 1, 62, 63, 64, 65, 127, 300, 511])
+def test_potrf_mc_info(bad):
+    from slate_amd import _native
+    n = 512
+    S = 4.0 * torch.eye(n, dtype=torch.float64, device="cuda")
+    S[bad, bad] = -1.0
+    if bad + 3 < n:
+        S[bad + 3, bad + 3] = -2.0          # a later failure must not win
+    A = _cm(S, "cuda")
+    info = torch.zeros(1, dtype=torch.int64, device="cuda")
+    _native.hip().potrf_tile_variant(1, n, A.data_ptr(), A.stride(1), info.data_ptr(),
+                                     torch.cuda.current_stream().cuda_stream)
+    assert int(info.item()) == bad + 1
