@@ -54,7 +54,7 @@ def _jobs():
     return max(1, min(16, os.cpu_count() or 4))
 
 
-def _build_module(name, srcdir, exts, compiler, cflags, ldflags, verbose=False):
+def _build_module(name, srcdir, exts, compiler, cflags, ldflags, verbose=False, extra_objs=()):
     srcs = sorted(sum((glob.glob(os.path.join(srcdir, "*" + e)) for e in exts), []))
     headers = glob.glob(os.path.join(srcdir, "*.hpp")) + glob.glob(os.path.join(HERE, "csrc", "include", "*.hpp"))
     objdir = os.path.join(BUILD, name)
@@ -84,6 +84,7 @@ def _build_module(name, srcdir, exts, compiler, cflags, ldflags, verbose=False):
         with cf.ThreadPoolExecutor(_jobs()) as ex:
             for f in [ex.submit(compile_one, so) for so in todo]:
                 f.result()
+    objs = objs + list(extra_objs)
     if todo or _newer(target, objs):
         _run([compiler] + ["-shared", "-o", target] + objs + ldflags)
     if old_flags != flags:
@@ -127,7 +128,37 @@ def build(verbose=False, hip=True, host=True):
             ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
              "-x", "hip"] + inc,
             ["--offload-arch=" + ARCH, "-L" + os.path.join(ROCM, "lib"), "-lamdhip64"], verbose))
+        # Python-free native library (include/slate_amd/slate_native.hh): the
+        # same kernel objects (minus the pybind11 units) + the C++ host
+        # runtime / drivers of csrc/native, linked against HIP and RCCL only
+        kobjs = [o for o in sorted(glob.glob(os.path.join(BUILD, "_hip", "*.hip.o")))
+                 if os.path.basename(o) not in ("bindings.hip.o", "devpool.hip.o")]
+        out.append(_build_module(
+            "libslate_amd_native", os.path.join(HERE, "csrc", "native"), [".hip"], hipcc,
+            ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-x", "hip",
+             "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROCM, "include")],
+            ["--offload-arch=" + ARCH, "-L" + os.path.join(ROCM, "lib"), "-lamdhip64", "-lrccl",
+             "-Wl,-rpath," + os.path.join(ROCM, "lib")], verbose, extra_objs=kobjs))
+        out.append(_build_native_example(verbose))
     return out
+
+
+def _build_native_example(verbose=False):
+    """examples/cpp/ex_native.cc -> slate_amd/ex_native: a plain g++ C++17
+    program against include/slate_amd/slate_native.hh and
+    libslate_amd_native.so (rpath $ORIGIN), no Python.  Built in-tree next
+    to the library so it travels to the GPU box with the snapshot."""
+    src = os.path.join(ROOT, "examples", "cpp", "ex_native.cc")
+    lib = os.path.join(HERE, "libslate_amd_native.so")
+    target = os.path.join(HERE, "ex_native")
+    hdr = os.path.join(ROOT, "include", "slate_amd", "slate_native.hh")
+    if _newer(target, [src, lib, hdr]):
+        cmd = ["g++", "-O2", "-std=c++17", "-I" + os.path.join(ROOT, "include"), src, "-o", target,
+               "-L" + HERE, "-lslate_amd_native", "-Wl,-rpath,$ORIGIN"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        _run(cmd)
+    return target
 
 
 if __name__ == "__main__":
