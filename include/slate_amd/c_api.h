@@ -100,6 +100,41 @@ void slate_spotrf_(const char* uplo, const int64_t* n, float* a, const int64_t* 
 void slate_sgesv_(const int64_t* n, const int64_t* nrhs, float* a, const int64_t* lda, int64_t* ipiv, float* b,
                   const int64_t* ldb, int64_t* info);
 
+/* LAPACK-style routines added in round 3 (lapack_api/lapack_trmm.cc, _syrk,
+ * _syr2k, _symm, _getri, _lansy, _lantr, _gecon, _pocon, _trcon, _heevd,
+ * _gesv_mixed, _hemm, _herk, _her2k, _lanhe).  Return LAPACK info; the
+ * condition numbers / refinement iterations go to the output pointers. */
+#define SLATE_AMD_DECL2(X, T)                                                                                \
+    int slate_##X##trmm(char side, char uplo, char ta, char diag, int64_t m, int64_t n, T alpha, const T* a,  \
+                        int64_t lda, T* b, int64_t ldb);                                                      \
+    int slate_##X##syrk(char uplo, char trans, int64_t n, int64_t k, T alpha, const T* a, int64_t lda, T beta, \
+                        T* c, int64_t ldc);                                                                   \
+    int slate_##X##syr2k(char uplo, char trans, int64_t n, int64_t k, T alpha, const T* a, int64_t lda,       \
+                         const T* b, int64_t ldb, T beta, T* c, int64_t ldc);                                 \
+    int slate_##X##symm(char side, char uplo, int64_t m, int64_t n, T alpha, const T* a, int64_t lda,         \
+                        const T* b, int64_t ldb, T beta, T* c, int64_t ldc);                                  \
+    int slate_##X##getri(int64_t n, T* a, int64_t lda, const int64_t* ipiv);                                  \
+    double slate_##X##lansy(char norm, char uplo, int64_t n, const T* a, int64_t lda);                        \
+    double slate_##X##lantr(char norm, char uplo, char diag, int64_t m, int64_t n, const T* a, int64_t lda);  \
+    int slate_##X##gecon(char norm, int64_t n, const T* a, int64_t lda, T anorm, T* rcond);                  \
+    int slate_##X##pocon(char uplo, int64_t n, const T* a, int64_t lda, T anorm, T* rcond);                  \
+    int slate_##X##trcon(char norm, char uplo, char diag, int64_t n, const T* a, int64_t lda, T* rcond);     \
+    int slate_##X##syevd(char jobz, char uplo, int64_t n, T* a, int64_t lda, T* w);
+SLATE_AMD_DECL2(s, float)
+SLATE_AMD_DECL2(d, double)
+#undef SLATE_AMD_DECL2
+int slate_dsgesv(int64_t n, int64_t nrhs, double* a, int64_t lda, int64_t* ipiv, double* b, int64_t ldb, double* x,
+                 int64_t ldx, int64_t* iter);
+/* complex<double>, interleaved (re, im); complex scalars by pointer */
+int slate_zhemm(char side, char uplo, int64_t m, int64_t n, const double* alpha, const double* a, int64_t lda,
+                const double* b, int64_t ldb, const double* beta, double* c, int64_t ldc);
+int slate_zherk(char uplo, char trans, int64_t n, int64_t k, double alpha, const double* a, int64_t lda, double beta,
+                double* c, int64_t ldc);
+int slate_zher2k(char uplo, char trans, int64_t n, int64_t k, const double* alpha, const double* a, int64_t lda,
+                 const double* b, int64_t ldb, double beta, double* c, int64_t ldc);
+double slate_zlanhe(char norm, char uplo, int64_t n, const double* a, int64_t lda);
+int slate_zheevd(char jobz, char uplo, int64_t n, double* a, int64_t lda, double* w);
+
 /* ------------------------------------------------------------------
  * ScaLAPACK interface (SLATE scalapack_api/): p?xxx_ with the Fortran
  * calling convention, 32-bit integers and 9-int descriptors
@@ -150,6 +185,76 @@ SLATE_AMD_PDECL(z, double)
 SLATE_AMD_PDECL_R(s, float)
 SLATE_AMD_PDECL_R(d, double)
 #undef SLATE_AMD_PDECL_R
+
+/* ScaLAPACK interposers added in round 3 (scalapack_api/scalapack_trmm.cc,
+ * _syrk, _syr2k, _symm, _potri, _getri, _lansy, _lantr, _gecon, _pocon,
+ * _trcon, _syev, _syevd, _gesvd, _gels, _gesv_mixed; complex _herk, _her2k,
+ * _hemm, _lanhe, _heevd).  Workspace queries (lwork = -1) return 1. */
+#define SLATE_AMD_PDECL2(X, T)                                                                               \
+    void p##X##trmm_(const char* side, const char* uplo, const char* ta, const char* diag, const int* m,     \
+                     const int* n, const T* alpha, const T* a, const int* ia, const int* ja, const int* desca, \
+                     T* b, const int* ib, const int* jb, const int* descb);                                 \
+    void p##X##syrk_(const char* uplo, const char* tr, const int* n, const int* k, const T* alpha,            \
+                     const T* a, const int* ia, const int* ja, const int* desca, const T* beta, T* c,          \
+                     const int* ic, const int* jc, const int* descc);                                      \
+    void p##X##syr2k_(const char* uplo, const char* tr, const int* n, const int* k, const T* alpha,           \
+                      const T* a, const int* ia, const int* ja, const int* desca, const T* b, const int* ib,    \
+                      const int* jb, const int* descb, const T* beta, T* c, const int* ic, const int* jc,     \
+                      const int* descc);                                                                   \
+    void p##X##symm_(const char* side, const char* uplo, const int* m, const int* n, const T* alpha,          \
+                     const T* a, const int* ia, const int* ja, const int* desca, const T* b, const int* ib,     \
+                     const int* jb, const int* descb, const T* beta, T* c, const int* ic, const int* jc,      \
+                     const int* descc);                                                                    \
+    void p##X##potri_(const char* uplo, const int* n, T* a, const int* ia, const int* ja, const int* desca,   \
+                      int* info);                                                                          \
+    void p##X##getri_(const int* n, T* a, const int* ia, const int* ja, const int* desca, const int* ipiv,    \
+                      T* work, const int* lwork, int* iwork, const int* liwork, int* info);                \
+    T p##X##lansy_(const char* norm, const char* uplo, const int* n, const T* a, const int* ia, const int* ja, \
+                   const int* desca, T* work);                                                             \
+    T p##X##lantr_(const char* norm, const char* uplo, const char* diag, const int* m, const int* n,          \
+                   const T* a, const int* ia, const int* ja, const int* desca, T* work);                   \
+    void p##X##gecon_(const char* norm, const int* n, const T* a, const int* ia, const int* ja,              \
+                      const int* desca, const T* anorm, T* rcond, T* work, const int* lwork, int* iwork,      \
+                      const int* liwork, int* info);                                                       \
+    void p##X##pocon_(const char* uplo, const int* n, const T* a, const int* ia, const int* ja,              \
+                      const int* desca, const T* anorm, T* rcond, T* work, const int* lwork, int* iwork,      \
+                      const int* liwork, int* info);                                                       \
+    void p##X##trcon_(const char* norm, const char* uplo, const char* diag, const int* n, const T* a,         \
+                      const int* ia, const int* ja, const int* desca, T* rcond, T* work, const int* lwork,    \
+                      int* iwork, const int* liwork, int* info);                                           \
+    void p##X##syev_(const char* jobz, const char* uplo, const int* n, T* a, const int* ia, const int* ja,    \
+                     const int* desca, T* w, T* z, const int* iz, const int* jz, const int* descz, T* work,   \
+                     const int* lwork, int* info);                                                         \
+    void p##X##syevd_(const char* jobz, const char* uplo, const int* n, T* a, const int* ia, const int* ja,   \
+                      const int* desca, T* w, T* z, const int* iz, const int* jz, const int* descz, T* work,  \
+                      const int* lwork, int* iwork, const int* liwork, int* info);                         \
+    void p##X##gesvd_(const char* jobu, const char* jobvt, const int* m, const int* n, T* a, const int* ia,  \
+                      const int* ja, const int* desca, T* s, T* u, const int* iu, const int* ju,              \
+                      const int* descu, T* vt, const int* ivt, const int* jvt, const int* descvt, T* work,    \
+                      const int* lwork, int* info);                                                        \
+    void p##X##gels_(const char* t, const int* m, const int* n, const int* nrhs, T* a, const int* ia,        \
+                     const int* ja, const int* desca, T* b, const int* ib, const int* jb, const int* descb,   \
+                     T* work, const int* lwork, int* info);
+SLATE_AMD_PDECL2(s, float)
+SLATE_AMD_PDECL2(d, double)
+#undef SLATE_AMD_PDECL2
+void pdsgesv_(const int* n, const int* nrhs, double* a, const int* ia, const int* ja, const int* desca, int* ipiv,
+              double* b, const int* ib, const int* jb, const int* descb, double* x, const int* ix, const int* jx,
+              const int* descx, int* iter, int* info);
+void pzherk_(const char* uplo, const char* tr, const int* n, const int* k, const double* alpha, const double* a,
+             const int* ia, const int* ja, const int* desca, const double* beta, double* c, const int* ic,
+             const int* jc, const int* descc);
+void pzher2k_(const char* uplo, const char* tr, const int* n, const int* k, const double* alpha, const double* a,
+              const int* ia, const int* ja, const int* desca, const double* b, const int* ib, const int* jb,
+              const int* descb, const double* beta, double* c, const int* ic, const int* jc, const int* descc);
+void pzhemm_(const char* side, const char* uplo, const int* m, const int* n, const double* alpha, const double* a,
+             const int* ia, const int* ja, const int* desca, const double* b, const int* ib, const int* jb,
+             const int* descb, const double* beta, double* c, const int* ic, const int* jc, const int* descc);
+double pzlanhe_(const char* norm, const char* uplo, const int* n, const double* a, const int* ia, const int* ja,
+                const int* desca, double* work);
+void pzheevd_(const char* jobz, const char* uplo, const int* n, double* a, const int* ia, const int* ja,
+              const int* desca, double* w, double* z, const int* iz, const int* jz, const int* descz, double* work,
+              const int* lwork, double* rwork, const int* lrwork, int* iwork, const int* liwork, int* info);
 
 /* ------------------------------------------------------------------
  * Distributed matrices by opaque handle (SLATE's slate_Matrix_create_* /

@@ -70,7 +70,83 @@ def call(name, *args):
     if rt == "lange":
         nrm, m, n, a, lda = args
         return f(nrm, m, n, _arr(pfx, a, m, n, lda), lda)
-    raise ValueError(name)
+    return _call_more(pfx, rt, f, *args)
+
+
+_RT = {'s': 's', 'd': 'd', 'c': 's', 'z': 'd'}       # real type of each prefix
+
+
+def _scalar(pfx, re, im=0.0):
+    return complex(re, im) if pfx in "cz" else re
+
+
+def _out(pfx, ptr, v):
+    """Write one real (s/d -> float/double) or int64 ('i') output value."""
+    ct = {'s': ctypes.c_float, 'd': ctypes.c_double, 'i': ctypes.c_int64, 'i32': ctypes.c_int32}[pfx]
+    if ptr:
+        ct.from_address(ptr).value = v
+
+
+def _call_more(pfx, rt, f, *args):
+    """LAPACK-style routines added in round 3 (lapack_api/lapack_trmm.cc,
+    _syrk, _syr2k, _symm, _hemm, _herk, _her2k, _getri, _gesv_mixed, _lansy,
+    _lanhe, _lantr, _gecon, _pocon, _trcon, _heevd).  Complex scalars arrive
+    as (re, im) pairs; condition numbers / iteration counts are written to
+    the caller's output pointers."""
+    if rt == "trmm":
+        side, uplo, ta, diag, m, n, al, a, lda, b, ldb = args
+        k = m if side.upper() == 'L' else n
+        return f(side, uplo, ta, diag, m, n, al, _arr(pfx, a, k, k, lda), lda,
+                 _arr(pfx, b, m, n, ldb), ldb)
+    if rt in ("syrk", "herk"):
+        uplo, tr, n, k, al, a, lda, be, c, ldc = args
+        ar, ac = (n, k) if tr.upper() == 'N' else (k, n)
+        return f(uplo, tr, n, k, al, _arr(pfx, a, ar, ac, lda), lda, be, _arr(pfx, c, n, n, ldc), ldc)
+    if rt in ("syr2k", "her2k"):
+        uplo, tr, n, k, are, aim, a, lda, b, ldb, be, c, ldc = args
+        ar, ac = (n, k) if tr.upper() == 'N' else (k, n)
+        return f(uplo, tr, n, k, _scalar(pfx, are, aim), _arr(pfx, a, ar, ac, lda), lda,
+                 _arr(pfx, b, ar, ac, ldb), ldb, be, _arr(pfx, c, n, n, ldc), ldc)
+    if rt in ("symm", "hemm"):
+        side, uplo, m, n, are, aim, a, lda, b, ldb, bre, bim, c, ldc = args
+        k = m if side.upper() == 'L' else n
+        return f(side, uplo, m, n, _scalar(pfx, are, aim), _arr(pfx, a, k, k, lda), lda,
+                 _arr(pfx, b, m, n, ldb), ldb, _scalar(pfx, bre, bim), _arr(pfx, c, m, n, ldc), ldc)
+    if rt == "getri":
+        n, a, lda, ip = args
+        return f(n, _arr(pfx, a, n, n, lda), lda, _iarr(ip, n))
+    if rt == "gesv_mixed":
+        n, nrhs, a, lda, ip, b, ldb, x, ldx, it = args
+        info, iters = f(n, nrhs, _arr(pfx, a, n, n, lda), lda, _iarr(ip, n), _arr(pfx, b, n, nrhs, ldb), ldb,
+                        _arr(pfx, x, n, nrhs, ldx), ldx)
+        _out('i', it, int(iters))
+        return info
+    if rt in ("lansy", "lanhe"):
+        nrm, uplo, n, a, lda = args
+        return f(nrm, uplo, n, _arr(pfx, a, n, n, lda), lda)
+    if rt == "lantr":
+        nrm, uplo, diag, m, n, a, lda = args
+        return f(nrm, uplo, diag, m, n, _arr(pfx, a, m, n, lda), lda)
+    if rt == "gecon":
+        nrm, n, a, lda, anorm, rc = args
+        info, r = f(nrm, n, _arr(pfx, a, n, n, lda), lda, anorm)
+        _out(_RT[pfx], rc, r)
+        return info
+    if rt == "pocon":
+        uplo, n, a, lda, anorm, rc = args
+        info, r = f(uplo, n, _arr(pfx, a, n, n, lda), lda, anorm)
+        _out(_RT[pfx], rc, r)
+        return info
+    if rt == "trcon":
+        nrm, uplo, diag, n, a, lda, rc = args
+        info, r = f(nrm, uplo, diag, n, _arr(pfx, a, n, n, lda), lda)
+        _out(_RT[pfx], rc, r)
+        return info
+    if rt in ("syevd", "heevd"):
+        jobz, uplo, n, a, lda, w = args
+        wv = np.ctypeslib.as_array((_CT[_RT[pfx]][0] * n).from_address(w))
+        return f(jobz, uplo, n, _arr(pfx, a, n, n, lda), lda, wv)
+    raise ValueError(pfx + rt)
 
 
 # ---------------------------------------------------------------- ScaLAPACK
@@ -165,7 +241,89 @@ def scalapack_call(name, *args):
     if rt == "lange":
         nrm, m, n, a, ia, ja, da = args
         return f(nrm, m, n, _desc_arr(pfx, a, da), ia, ja, da)
-    raise ValueError(name)
+    return _scalapack_more(pfx, rt, f, *args)
+
+
+def _rvec(pfx, ptr, n):
+    """Replicated real vector (eigen / singular values) at ptr."""
+    return np.ctypeslib.as_array((_CT[_RT[pfx]][0] * max(n, 1)).from_address(ptr))[:n]
+
+
+def _scalapack_more(pfx, rt, f, *args):
+    """p?xxx_ interposers added in round 3 (scalapack_api/scalapack_trmm.cc,
+    _herk, _syrk, _her2k, _syr2k, _hemm, _symm, _potri, _getri, _lanhe,
+    _lansy, _lantr, _gecon, _pocon, _trcon, _gesv_mixed, _heev, _heevd,
+    _gesvd, _gels).  Workspace arguments of the Fortran interfaces are
+    ignored (a workspace query, lwork = -1, is answered in the C layer)."""
+    D = lambda ptr, d: _desc_arr(pfx, ptr, d)      # noqa: E731
+    if rt == "trmm":
+        side, uplo, ta, diag, m, n, al, a, ia, ja, da, b, ib, jb, db = args
+        return f(side, uplo, ta, diag, m, n, al, D(a, da), ia, ja, da, D(b, db), ib, jb, db)
+    if rt in ("syrk", "herk"):
+        uplo, tr, n, k, al, a, ia, ja, da, be, c, ic, jc, dc = args
+        return f(uplo, tr, n, k, al, D(a, da), ia, ja, da, be, D(c, dc), ic, jc, dc)
+    if rt in ("syr2k", "her2k"):
+        uplo, tr, n, k, are, aim, a, ia, ja, da, b, ib, jb, db, be, c, ic, jc, dc = args
+        return f(uplo, tr, n, k, _scalar(pfx, are, aim), D(a, da), ia, ja, da, D(b, db), ib, jb, db, be,
+                 D(c, dc), ic, jc, dc)
+    if rt in ("symm", "hemm"):
+        side, uplo, m, n, are, aim, a, ia, ja, da, b, ib, jb, db, bre, bim, c, ic, jc, dc = args
+        return f(side, uplo, m, n, _scalar(pfx, are, aim), D(a, da), ia, ja, da, D(b, db), ib, jb, db,
+                 _scalar(pfx, bre, bim), D(c, dc), ic, jc, dc)
+    if rt == "potri":
+        uplo, n, a, ia, ja, da = args
+        return f(uplo, n, D(a, da), ia, ja, da)
+    if rt == "getri":
+        n, a, ia, ja, da, ip = args
+        piv = _ipiv_from_local(ip, ia, n, da)
+        return f(n, D(a, da), ia, ja, da, piv)
+    if rt in ("lansy", "lanhe"):
+        nrm, uplo, n, a, ia, ja, da = args
+        return f(nrm, uplo, n, D(a, da), ia, ja, da)
+    if rt == "lantr":
+        nrm, uplo, diag, m, n, a, ia, ja, da = args
+        return f(nrm, uplo, diag, m, n, D(a, da), ia, ja, da)
+    if rt == "gecon":
+        nrm, n, a, ia, ja, da, anorm, rc = args
+        info, r = f(nrm, n, D(a, da), ia, ja, da, anorm)
+        _out(_RT[pfx], rc, r)
+        return info
+    if rt == "pocon":
+        uplo, n, a, ia, ja, da, anorm, rc = args
+        info, r = f(uplo, n, D(a, da), ia, ja, da, anorm)
+        _out(_RT[pfx], rc, r)
+        return info
+    if rt == "trcon":
+        nrm, uplo, diag, n, a, ia, ja, da, rc = args
+        info, r = f(nrm, uplo, diag, n, D(a, da), ia, ja, da)
+        _out(_RT[pfx], rc, r)
+        return info
+    if rt == "gesv_mixed":
+        n, nrhs, a, ia, ja, da, ip, b, ib, jb, db, x, ix, jx, dx, it = args
+        piv = np.zeros(n, dtype=np.int64)
+        info, iters = f(n, nrhs, D(a, da), ia, ja, da, piv, D(b, db), ib, jb, db, D(x, dx), ix, jx, dx)
+        _ipiv_to_local(piv, ia, da, ip)
+        _out('i32', it, int(iters))
+        return info
+    if rt in ("syev", "heev", "syevd", "heevd"):
+        jobz, uplo, n, a, ia, ja, da, w, z, iz, jz, dz = args
+        want = str(jobz).upper()[0] == 'V'
+        return f(jobz, uplo, n, D(a, da), ia, ja, da, _rvec(pfx, w, n), D(z, dz) if want else None, iz, jz,
+                 dz if want else None)
+    if rt == "gesvd":
+        ju, jv, m, n, a, ia, ja, da, s, u, iu, ju_, du, vt, ivt, jvt, dvt = args
+        wu, wv = str(ju).upper()[0] == 'V', str(jv).upper()[0] == 'V'
+        return f(ju, jv, m, n, D(a, da), ia, ja, da, _rvec(pfx, s, min(m, n)), D(u, du) if wu else None, iu, ju_,
+                 du if wu else None, D(vt, dvt) if wv else None, ivt, jvt, dvt if wv else None)
+    if rt == "gels":
+        t, m, n, nrhs, a, ia, ja, da, b, ib, jb, db = args
+        return f(t, m, n, nrhs, D(a, da), ia, ja, da, D(b, db), ib, jb, db)
+    raise ValueError("p" + pfx + rt)
+
+
+def _ch(x):
+    """A character argument: Py_BuildValue's 'C' gives str, 'i' gives int."""
+    return chr(x) if isinstance(x, int) else x
 
 
 def blacs(op, *args):
@@ -180,7 +338,7 @@ def blacs(op, *args):
     if op == "gridinit":
         order, p, q = args
         slate_amd.init()
-        return S.blacs_gridinit(p, q, chr(order))
+        return S.blacs_gridinit(p, q, _ch(order))
     if op == "gridinfo":
         p, q, pr, pc = S.blacs_gridinfo(args[0])
         return ((p * 10000 + q) * 10000 + pr) * 10000 + pc
@@ -213,8 +371,8 @@ def handle(op, *args):
         kind, pfx, m, n, nb, p, q = args
         sl.init()
         dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
-        dt = _tdt(chr(pfx))
-        k = chr(kind)
+        dt = _tdt(_ch(pfx))
+        k = _ch(kind)
         if k == 'G':
             M = sl.Matrix(m, n, nb=nb, p=p, q=q, dtype=dt, device=dev)
         elif k in ('L', 'U'):
@@ -252,7 +410,7 @@ def handle(op, *args):
         return 0
     if op == "norm":
         h, nrm = args
-        return float(sl.norm(sl.Norm.from_string(chr(nrm)), _H[h]))
+        return float(sl.norm(sl.Norm.from_string(_ch(nrm)), _H[h]))
     if op == "gemm":
         al, ha, hb, be, hc = args
         sl.gemm(al, _H[ha], _H[hb], be, _H[hc], _OPTS)
@@ -295,7 +453,7 @@ def _put_reals(ptr, v):
 def _tri(sl, h, uplo, diag):
     """Triangular view (uplo, diag) of a handle's matrix; an op'd view keeps its op."""
     M = _H[h]
-    return sl.TriangularMatrix(sl.Uplo(chr(uplo)), matrix=M, diag=sl.Diag(chr(diag)))
+    return sl.TriangularMatrix(sl.Uplo(_ch(uplo)), matrix=M, diag=sl.Diag(_ch(diag)))
 
 
 def _herm(sl, h):
@@ -329,7 +487,7 @@ def _handle_more(sl, op, *args):
     if op == "op_view":
         h, t = args
         M = _H[h]
-        return _put(M.conj_transpose() if chr(t) == 'C' else M.transpose())
+        return _put(M.conj_transpose() if _ch(t) == 'C' else M.transpose())
     if op == "dims":
         M = _H[args[0]]
         return M.m() * 1000000000 + M.n()
@@ -340,7 +498,7 @@ def _handle_more(sl, op, *args):
         return _put(sl.TriangularFactors())
     if op in ("trsm", "trmm"):
         side, uplo, diag, al, ha, hb = args
-        getattr(sl, op)(sl.Side(chr(side)), al, _tri(sl, ha, uplo, diag), _H[hb], _OPTS)
+        getattr(sl, op)(sl.Side(_ch(side)), al, _tri(sl, ha, uplo, diag), _H[hb], _OPTS)
         return 0
     if op == "herk":
         al, ha, be, hc = args
@@ -352,7 +510,7 @@ def _handle_more(sl, op, *args):
         return 0
     if op == "hemm":
         side, al, ha, hb, be, hc = args
-        sl.hemm(sl.Side(chr(side)), al, _herm(sl, ha), _H[hb], be, _H[hc], _OPTS)
+        sl.hemm(sl.Side(_ch(side)), al, _herm(sl, ha), _H[hb], be, _H[hc], _OPTS)
         return 0
     if op == "potrs":
         sl.potrs(_herm(sl, args[0]), _H[args[1]], _OPTS)
@@ -368,7 +526,7 @@ def _handle_more(sl, op, *args):
         return getattr(sl, op)(_H[args[0]], _H[args[1]], _OPTS)
     if op in ("unmqr", "unmlq"):
         side, o, ha, ht, hc = args
-        getattr(sl, op)(sl.Side(chr(side)), sl.Op(chr(o)), _H[ha], _H[ht], _H[hc], _OPTS)
+        getattr(sl, op)(sl.Side(_ch(side)), sl.Op(_ch(o)), _H[ha], _H[ht], _H[hc], _OPTS)
         return 0
     if op == "gels_t":
         ha, ht, hb = args
@@ -415,8 +573,8 @@ def _handle_more(sl, op, *args):
         return 0
     if op == "gecondest":
         nrm, ha, hp, anorm = args
-        return float(sl.gecondest(sl.Norm.from_string(chr(nrm)), _H[ha], _H[hp], anorm, _OPTS))
+        return float(sl.gecondest(sl.Norm.from_string(_ch(nrm)), _H[ha], _H[hp], anorm, _OPTS))
     if op == "pocondest":
         nrm, ha, anorm = args
-        return float(sl.pocondest(sl.Norm.from_string(chr(nrm)), _herm(sl, ha), anorm, _OPTS))
+        return float(sl.pocondest(sl.Norm.from_string(_ch(nrm)), _herm(sl, ha), anorm, _OPTS))
     raise ValueError(op)

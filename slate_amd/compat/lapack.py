@@ -83,7 +83,14 @@ class _Arr:
 
 
 def _M(arr, m, n):
-    return Matrix.fromLAPACK(m, n, arr.work, arr.lda, nb=_nb())
+    return Matrix.fromLAPACK(m, n, arr.work, arr.lda, nb=_nb(), comm=_self())
+
+
+def _self():
+    """LAPACK-style calls are per process (the reference builds them on
+    MPI_COMM_SELF, lapack_api/lapack_slate.hh): never a collective."""
+    from ..parallel.comm import self_comm
+    return self_comm()
 
 
 def _opts():
@@ -124,7 +131,7 @@ def _make(pfx):
         _verbose(pfx + "potrf", n)
         from ..models.chol import potrf as _p
         A = _Arr(a, n, n, lda, dt)
-        H = HermitianMatrix.fromLAPACK(_uplo(uplo), n, A.work, A.lda, nb=_nb())
+        H = HermitianMatrix.fromLAPACK(_uplo(uplo), n, A.work, A.lda, nb=_nb(), comm=_self())
         info = _p(H, _opts())
         A.writeback()
         return info
@@ -134,7 +141,7 @@ def _make(pfx):
         from ..models.chol import potrs as _p
         A = _Arr(a, n, n, lda, dt)
         B = _Arr(b, n, nrhs, ldb, dt)
-        H = HermitianMatrix.fromLAPACK(_uplo(uplo), n, A.work, A.lda, nb=_nb())
+        H = HermitianMatrix.fromLAPACK(_uplo(uplo), n, A.work, A.lda, nb=_nb(), comm=_self())
         _p(H, _M(B, n, nrhs), _opts())
         B.writeback()
         return 0
@@ -150,7 +157,7 @@ def _make(pfx):
     def potri(uplo, n, a, lda):
         from ..models.chol import potri as _p
         A = _Arr(a, n, n, lda, dt)
-        H = HermitianMatrix.fromLAPACK(_uplo(uplo), n, A.work, A.lda, nb=_nb())
+        H = HermitianMatrix.fromLAPACK(_uplo(uplo), n, A.work, A.lda, nb=_nb(), comm=_self())
         info = _p(H, _opts())
         A.writeback()
         return info
@@ -201,7 +208,7 @@ def _make(pfx):
         A = _Arr(a, k, k, lda, dt)
         B = _Arr(b, m, n, ldb, dt)
         T = TriangularMatrix.fromLAPACK(_uplo(uplo), Diag.Unit if str(diag).upper()[0] == 'U' else Diag.NonUnit,
-                                        k, A.work, A.lda, nb=_nb())
+                                        k, A.work, A.lda, nb=_nb(), comm=_self())
         t = _op(transa)
         T = T if t == Op.NoTrans else (T.transpose() if t == Op.Trans else T.conj_transpose())
         _t(Side.Left if str(side).upper()[0] == 'L' else Side.Right, alpha, T, _M(B, m, n), _opts())
@@ -215,7 +222,7 @@ def _make(pfx):
         A = _Arr(a, k, k, lda, dt)
         B = _Arr(b, m, n, ldb, dt)
         T = TriangularMatrix.fromLAPACK(_uplo(uplo), Diag.Unit if str(diag).upper()[0] == 'U' else Diag.NonUnit,
-                                        k, A.work, A.lda, nb=_nb())
+                                        k, A.work, A.lda, nb=_nb(), comm=_self())
         t = _op(transa)
         T = T if t == Op.NoTrans else (T.transpose() if t == Op.Trans else T.conj_transpose())
         _t(Side.Left if str(side).upper()[0] == 'L' else Side.Right, alpha, T, _M(B, m, n), _opts())
@@ -230,11 +237,10 @@ def _make(pfx):
         C = _Arr(c, n, n, ldc, dt)
         MA = _M(A, A.rows, A.cols)
         MA = MA if t == Op.NoTrans else MA.conj_transpose() if not real or t == Op.ConjTrans else MA.transpose()
-        H = HermitianMatrix.fromLAPACK(_uplo(uplo), n, C.work, C.lda, nb=_nb())
+        H = HermitianMatrix.fromLAPACK(_uplo(uplo), n, C.work, C.lda, nb=_nb(), comm=_self())
         (_h if (not real or True) else _s)(alpha, MA, beta, H, _opts())
         C.writeback()
         return 0
-    g["herk" if not real else "syrk"] = herk
 
     def geqrf(m, n, a, lda, tau):
         from ..models.qr import geqrf as _q
@@ -265,10 +271,10 @@ def _make(pfx):
     def heev(jobz, uplo, n, a, lda, w):
         from ..models.eig import heev as _h
         A = _Arr(a, n, n, lda, dt)
-        H = HermitianMatrix.fromLAPACK(_uplo(uplo), n, A.work, A.lda, nb=_nb())
+        H = HermitianMatrix.fromLAPACK(_uplo(uplo), n, A.work, A.lda, nb=_nb(), comm=_self())
         Z = None
         if str(jobz).upper()[0] == 'V':
-            Z = Matrix(n, n, nb=_nb(), dtype=dt, device=A.work.device)
+            Z = Matrix(n, n, nb=_nb(), comm=_self(), dtype=dt, device=A.work.device)
             Z.insertLocalTiles(device=A.work.device.index if A.work.is_cuda else -1)
         vals = _h(H, None, Z, _opts())
         if Z is not None:
@@ -292,10 +298,10 @@ def _make(pfx):
         dev = A.work.device
         di = dev.index if dev.type == "cuda" else -1
         if str(jobu).upper()[0] in 'AS':
-            U = Matrix(m, k, nb=_nb(), dtype=dt, device=dev)
+            U = Matrix(m, k, nb=_nb(), comm=_self(), dtype=dt, device=dev)
             U.insertLocalTiles(device=di)
         if str(jobvt).upper()[0] in 'AS':
-            VH = Matrix(k, n, nb=_nb(), dtype=dt, device=dev)
+            VH = Matrix(k, n, nb=_nb(), comm=_self(), dtype=dt, device=dev)
             VH.insertLocalTiles(device=di)
         sv = _s(_M(A, m, n), None, U, VH, _opts())
         if U is not None:
@@ -320,11 +326,157 @@ def _make(pfx):
         return float(_n(Norm.from_string(str(norm)), _M(A, m, n)))
     g["lange"] = lange
 
+    # ---- BLAS-3 on symmetric / Hermitian operands (lapack_api/lapack_hemm.cc,
+    #      lapack_symm.cc, lapack_her2k.cc, lapack_syr2k.cc, lapack_syrk.cc)
+    def _side(sd):
+        return Side.Left if str(sd).upper()[0] == 'L' else Side.Right
+
+    def _hsmm(herm):
+        def mm(side, uplo, m, n, alpha, a, lda, b, ldb, beta, c, ldc):
+            from ..models.blas3 import hemm as _h, symm as _s
+            k = m if _side(side) == Side.Left else n
+            A = _Arr(a, k, k, lda, dt)
+            B = _Arr(b, m, n, ldb, dt)
+            C = _Arr(c, m, n, ldc, dt)
+            cls = HermitianMatrix if herm else SymmetricMatrix
+            H = cls.fromLAPACK(_uplo(uplo), k, A.work, A.lda, nb=_nb(), comm=_self())
+            (_h if herm else _s)(_side(side), alpha, H, _M(B, m, n), beta, _M(C, m, n), _opts())
+            C.writeback()
+            return 0
+        return mm
+    g["hemm"] = _hsmm(True)
+    g["symm"] = _hsmm(False)
+
+    def _rk(herm):
+        def rk(uplo, trans, n, k, alpha, a, lda, beta, c, ldc):
+            from ..models.blas3 import herk as _h, syrk as _s
+            t = _op(trans)
+            A = _Arr(a, n if t == Op.NoTrans else k, k if t == Op.NoTrans else n, lda, dt)
+            C = _Arr(c, n, n, ldc, dt)
+            MA = _M(A, A.rows, A.cols)
+            if t != Op.NoTrans:
+                MA = MA.conj_transpose() if herm else MA.transpose()
+            cls = HermitianMatrix if herm else SymmetricMatrix
+            H = cls.fromLAPACK(_uplo(uplo), n, C.work, C.lda, nb=_nb(), comm=_self())
+            (_h if herm else _s)(alpha, MA, beta, H, _opts())
+            C.writeback()
+            return 0
+        return rk
+    g["herk"] = _rk(True)
+    g["syrk"] = _rk(False)
+
+    def _r2k(herm):
+        def r2k(uplo, trans, n, k, alpha, a, lda, b, ldb, beta, c, ldc):
+            from ..models.blas3 import her2k as _h, syr2k as _s
+            t = _op(trans)
+            r, cc = (n, k) if t == Op.NoTrans else (k, n)
+            A = _Arr(a, r, cc, lda, dt)
+            B = _Arr(b, r, cc, ldb, dt)
+            C = _Arr(c, n, n, ldc, dt)
+            MA, MB = _M(A, r, cc), _M(B, r, cc)
+            if t != Op.NoTrans:
+                MA = MA.conj_transpose() if herm else MA.transpose()
+                MB = MB.conj_transpose() if herm else MB.transpose()
+            cls = HermitianMatrix if herm else SymmetricMatrix
+            H = cls.fromLAPACK(_uplo(uplo), n, C.work, C.lda, nb=_nb(), comm=_self())
+            (_h if herm else _s)(alpha, MA, MB, beta, H, _opts())
+            C.writeback()
+            return 0
+        return r2k
+    g["her2k"] = _r2k(True)
+    g["syr2k"] = _r2k(False)
+
+    # ---- inverses, mixed precision, eigenvalues (lapack_getri.cc,
+    #      lapack_gesv_mixed.cc, lapack_heevd.cc)
+    def getri(n, a, lda, ipiv):
+        """Inverse from getrf's factors; ipiv 1-based (LAPACK)."""
+        from ..models.lu import getri as _g
+        A = _Arr(a, n, n, lda, dt)
+        ip = torch.as_tensor(np.asarray(ipiv) if isinstance(ipiv, np.ndarray) else ipiv.cpu()).to(torch.int64)[:n] - 1
+        piv = Pivots()
+        piv.set(ip, _nb())
+        info = _g(_M(A, n, n), piv, _opts())
+        A.writeback()
+        return info
+    g["getri"] = getri
+
+    if pfx in "dz":
+        def gesv_mixed(n, nrhs, a, lda, ipiv, b, ldb, x, ldx):
+            """LAPACK dsgesv / zcgesv: returns (info, iter) -- iter < 0 means
+            the refinement fell back to full precision."""
+            from ..models.mixed import gesv_mixed as _g
+            A = _Arr(a, n, n, lda, dt)
+            B = _Arr(b, n, nrhs, ldb, dt)
+            X = _Arr(x, n, nrhs, ldx, dt)
+            piv = Pivots()
+            info, it = _g(_M(A, n, n), piv, _M(B, n, nrhs), _M(X, n, nrhs), _opts())
+            X.writeback()
+            p = (piv.ipiv.cpu() + 1).numpy()
+            if isinstance(ipiv, np.ndarray):
+                ipiv[:len(p)] = p
+            else:
+                ipiv[:len(p)] = torch.from_numpy(p).to(ipiv.device, ipiv.dtype)
+            return info, it
+        g["gesv_mixed"] = gesv_mixed
+
+    # ---- norms of structured matrices (lapack_lanhe.cc, lapack_lansy.cc,
+    #      lapack_lantr.cc)
+    def _lan_sym(herm):
+        def lan(norm, uplo, n, a, lda):
+            from ..models.aux import norm as _n
+            A = _Arr(a, n, n, lda, dt)
+            cls = HermitianMatrix if herm else SymmetricMatrix
+            return float(_n(Norm.from_string(str(norm)), cls.fromLAPACK(_uplo(uplo), n, A.work, A.lda, nb=_nb(), comm=_self())))
+        return lan
+    g["lanhe"] = _lan_sym(True)
+    g["lansy"] = _lan_sym(False)
+
+    def lantr(norm, uplo, diag, m, n, a, lda):
+        from ..models.aux import norm as _n
+        from ..core.matrix import TrapezoidMatrix
+        A = _Arr(a, m, n, lda, dt)
+        T = TrapezoidMatrix.fromLAPACK(_uplo(uplo), m, n, A.work, A.lda, nb=_nb(), comm=_self(),
+                                       diag=Diag.Unit if str(diag).upper()[0] == 'U' else Diag.NonUnit)
+        return float(_n(Norm.from_string(str(norm)), T))
+    g["lantr"] = lantr
+
+    # ---- condition estimates (lapack_gecon.cc, lapack_pocon.cc, lapack_trcon.cc):
+    #      return (info, rcond)
+    def gecon(norm, n, a, lda, anorm):
+        """a holds getrf's factors with the pivots applied (LAPACK gecon
+        takes no pivots: the estimate needs only the L and U solves)."""
+        from ..models.condest import gecondest as _g
+        A = _Arr(a, n, n, lda, dt)
+        piv = Pivots()
+        piv.set(torch.arange(n, dtype=torch.int64), _nb())
+        return 0, float(_g(Norm.from_string(str(norm)), _M(A, n, n), piv, anorm, _opts()))
+    g["gecon"] = gecon
+
+    def pocon(uplo, n, a, lda, anorm):
+        from ..models.condest import pocondest as _p
+        A = _Arr(a, n, n, lda, dt)
+        H = HermitianMatrix.fromLAPACK(_uplo(uplo), n, A.work, A.lda, nb=_nb(), comm=_self())
+        return 0, float(_p(Norm.One, H, anorm, _opts()))
+    g["pocon"] = pocon
+
+    def trcon(norm, uplo, diag, n, a, lda):
+        from ..models.condest import trcondest as _t
+        A = _Arr(a, n, n, lda, dt)
+        T = TriangularMatrix.fromLAPACK(_uplo(uplo), Diag.Unit if str(diag).upper()[0] == 'U' else Diag.NonUnit,
+                                        n, A.work, A.lda, nb=_nb(), comm=_self())
+        return 0, float(_t(Norm.from_string(str(norm)), T, None, _opts()))
+    g["trcon"] = trcon
+
+    def heevd(jobz, uplo, n, a, lda, w):
+        """Divide and conquer is heev's default method (MethodEig.DC)."""
+        return heev(jobz, uplo, n, a, lda, w)
+    g["heevd" if not real else "syevd"] = heevd
+
     def trtri(uplo, diag, n, a, lda):
         from ..models.inverse import trtri as _t
         A = _Arr(a, n, n, lda, dt)
         T = TriangularMatrix.fromLAPACK(_uplo(uplo), Diag.Unit if str(diag).upper()[0] == 'U' else Diag.NonUnit,
-                                        n, A.work, A.lda, nb=_nb())
+                                        n, A.work, A.lda, nb=_nb(), comm=_self())
         info = _t(T, _opts())
         A.writeback()
         return info

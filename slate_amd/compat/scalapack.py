@@ -28,7 +28,8 @@ import torch
 
 from ..core.enums import Diag, GridOrder, Norm, Op, Option, Side, Target, Uplo
 from ..core.exceptions import SlateError
-from ..core.matrix import HermitianMatrix, Matrix, Pivots, TriangularFactors, TriangularMatrix
+from ..core.matrix import (HermitianMatrix, Matrix, Pivots, SymmetricMatrix, TrapezoidMatrix, TriangularFactors,
+                           TriangularMatrix)
 from ..parallel import comm as _comm
 
 _PFX = {'s': torch.float32, 'd': torch.float64, 'c': torch.complex64, 'z': torch.complex128}
@@ -114,6 +115,13 @@ class _Loc:
         if kind is TriangularMatrix:
             return TriangularMatrix.fromScaLAPACK(kw["uplo"], kw["diag"], self.n, self.work, self.lld, self.nb,
                                                   self.p, self.q, comm, order=self.order)
+        if kind is SymmetricMatrix:
+            return SymmetricMatrix.fromScaLAPACK(kw["uplo"], self.n, self.work, self.lld, self.nb, self.p,
+                                                 self.q, comm, order=self.order)
+        if kind is TrapezoidMatrix:
+            M = Matrix.fromScaLAPACK(self.m, self.n, self.work, self.lld, self.mb, self.nb, self.order,
+                                     self.p, self.q, comm)
+            return TrapezoidMatrix(kw["uplo"], matrix=M, diag=kw["diag"])
         raise SlateError("bad kind")
 
     def writeback(self):
@@ -138,8 +146,12 @@ def _sub(L, ia, ja, m, n, kind=Matrix, **kw):
     copy(view, W)
     if kind is HermitianMatrix:
         M = HermitianMatrix(kw["uplo"], W)
+    elif kind is SymmetricMatrix:
+        M = SymmetricMatrix(kw["uplo"], W)
     elif kind is TriangularMatrix:
         M = TriangularMatrix(kw["uplo"], W, diag=kw["diag"])
+    elif kind is TrapezoidMatrix:
+        M = TrapezoidMatrix(kw["uplo"], matrix=W, diag=kw["diag"])
     else:
         M = W
     return M, (lambda: copy(W, view))
@@ -321,6 +333,167 @@ def _make(pfx):
             s[:k] = sv.to(s.device, s.dtype)
         return 0
     g["gesvd"] = gesvd
+
+    # ---- BLAS-3 (scalapack_api/scalapack_trmm.cc, _herk, _syrk, _her2k,
+    #      _syr2k, _hemm, _symm)
+    def _diag(d):
+        return Diag.Unit if str(d).upper()[0] == 'U' else Diag.NonUnit
+
+    def trmm(side, uplo, transa, diag, m, n, alpha, a, ia, ja, desca, b, ib, jb, descb):
+        from ..models.blas3 import trmm as _t
+        A, B = _Loc(a, desca, dt), _Loc(b, descb, dt)
+        left = str(side).upper()[0] == 'L'
+        k = m if left else n
+        T, _ = _sub(A, ia, ja, k, k, TriangularMatrix, uplo=_uplo(uplo), diag=_diag(diag))
+        Bm, done = _sub(B, ib, jb, m, n)
+        _t(Side.Left if left else Side.Right, alpha, _opm(T, _op(transa)), Bm, _opts())
+        done()
+        B.writeback()
+        return 0
+    g["trmm"] = trmm
+
+    def _rk(herm):
+        def rk(uplo, trans, n, k, alpha, a, ia, ja, desca, beta, c, ic, jc, descc):
+            from ..models.blas3 import herk as _h, syrk as _s
+            A, C = _Loc(a, desca, dt), _Loc(c, descc, dt)
+            t = _op(trans)
+            Am, _ = _sub(A, ia, ja, *((n, k) if t == Op.NoTrans else (k, n)))
+            if t != Op.NoTrans:
+                Am = Am.conj_transpose() if herm else Am.transpose()
+            Cm, done = _sub(C, ic, jc, n, n, HermitianMatrix if herm else SymmetricMatrix, uplo=_uplo(uplo))
+            (_h if herm else _s)(alpha, Am, beta, Cm, _opts())
+            done()
+            C.writeback()
+            return 0
+        return rk
+    g["herk"] = _rk(True)
+    g["syrk"] = _rk(False)
+
+    def _r2k(herm):
+        def r2k(uplo, trans, n, k, alpha, a, ia, ja, desca, b, ib, jb, descb, beta, c, ic, jc, descc):
+            from ..models.blas3 import her2k as _h, syr2k as _s
+            A, B, C = _Loc(a, desca, dt), _Loc(b, descb, dt), _Loc(c, descc, dt)
+            t = _op(trans)
+            shp = (n, k) if t == Op.NoTrans else (k, n)
+            Am, _ = _sub(A, ia, ja, *shp)
+            Bm, _ = _sub(B, ib, jb, *shp)
+            if t != Op.NoTrans:
+                Am = Am.conj_transpose() if herm else Am.transpose()
+                Bm = Bm.conj_transpose() if herm else Bm.transpose()
+            Cm, done = _sub(C, ic, jc, n, n, HermitianMatrix if herm else SymmetricMatrix, uplo=_uplo(uplo))
+            (_h if herm else _s)(alpha, Am, Bm, beta, Cm, _opts())
+            done()
+            C.writeback()
+            return 0
+        return r2k
+    g["her2k"] = _r2k(True)
+    g["syr2k"] = _r2k(False)
+
+    def _mm(herm):
+        def mm(side, uplo, m, n, alpha, a, ia, ja, desca, b, ib, jb, descb, beta, c, ic, jc, descc):
+            from ..models.blas3 import hemm as _h, symm as _s
+            A, B, C = _Loc(a, desca, dt), _Loc(b, descb, dt), _Loc(c, descc, dt)
+            left = str(side).upper()[0] == 'L'
+            k = m if left else n
+            Am, _ = _sub(A, ia, ja, k, k, HermitianMatrix if herm else SymmetricMatrix, uplo=_uplo(uplo))
+            Bm, _ = _sub(B, ib, jb, m, n)
+            Cm, done = _sub(C, ic, jc, m, n)
+            (_h if herm else _s)(Side.Left if left else Side.Right, alpha, Am, Bm, beta, Cm, _opts())
+            done()
+            C.writeback()
+            return 0
+        return mm
+    g["hemm"] = _mm(True)
+    g["symm"] = _mm(False)
+
+    # ---- inverses (scalapack_potri.cc, scalapack_getri.cc)
+    def potri(uplo, n, a, ia, ja, desca):
+        from ..models.chol import potri as _p
+        A = _Loc(a, desca, dt)
+        Am, done = _sub(A, ia, ja, n, n, HermitianMatrix, uplo=_uplo(uplo))
+        info = _p(Am, _opts())
+        done()
+        A.writeback()
+        return info
+    g["potri"] = potri
+
+    def getri(n, a, ia, ja, desca, ipiv):
+        from ..models.lu import getri as _g
+        A = _Loc(a, desca, dt)
+        ip = torch.as_tensor(np.asarray(ipiv) if isinstance(ipiv, np.ndarray) else ipiv.cpu()).to(torch.int64)
+        piv = Pivots()
+        piv.set(ip[:n] - 1, A.nb)
+        Am, done = _sub(A, ia, ja, n, n)
+        info = _g(Am, piv, _opts())
+        done()
+        A.writeback()
+        return info
+    g["getri"] = getri
+
+    # ---- norms (scalapack_lanhe.cc, _lansy, _lantr)
+    def _lan(herm):
+        def lan(norm, uplo, n, a, ia, ja, desca):
+            from ..models.aux import norm as _n
+            Am, _ = _sub(_Loc(a, desca, dt), ia, ja, n, n, HermitianMatrix if herm else SymmetricMatrix,
+                         uplo=_uplo(uplo))
+            return float(_n(Norm.from_string(str(norm)), Am))
+        return lan
+    g["lanhe"] = _lan(True)
+    g["lansy"] = _lan(False)
+
+    def lantr(norm, uplo, diag, m, n, a, ia, ja, desca):
+        from ..models.aux import norm as _n
+        Am, _ = _sub(_Loc(a, desca, dt), ia, ja, m, n, TrapezoidMatrix, uplo=_uplo(uplo), diag=_diag(diag))
+        return float(_n(Norm.from_string(str(norm)), Am))
+    g["lantr"] = lantr
+
+    # ---- condition estimates: (info, rcond) (scalapack_gecon.cc, _pocon, _trcon)
+    def gecon(norm, n, a, ia, ja, desca, anorm):
+        from ..models.condest import gecondest as _g
+        A = _Loc(a, desca, dt)
+        Am, _ = _sub(A, ia, ja, n, n)
+        piv = Pivots()
+        piv.set(torch.arange(n, dtype=torch.int64), A.nb)
+        return 0, float(_g(Norm.from_string(str(norm)), Am, piv, anorm, _opts()))
+    g["gecon"] = gecon
+
+    def pocon(uplo, n, a, ia, ja, desca, anorm):
+        from ..models.condest import pocondest as _p
+        Am, _ = _sub(_Loc(a, desca, dt), ia, ja, n, n, HermitianMatrix, uplo=_uplo(uplo))
+        return 0, float(_p(Norm.One, Am, anorm, _opts()))
+    g["pocon"] = pocon
+
+    def trcon(norm, uplo, diag, n, a, ia, ja, desca):
+        from ..models.condest import trcondest as _t
+        Am, _ = _sub(_Loc(a, desca, dt), ia, ja, n, n, TriangularMatrix, uplo=_uplo(uplo), diag=_diag(diag))
+        return 0, float(_t(Norm.from_string(str(norm)), Am, None, _opts()))
+    g["trcon"] = trcon
+
+    # ---- mixed precision (scalapack_gesv_mixed.cc: pdsgesv / pzcgesv)
+    if pfx in "dz":
+        def gesv_mixed(n, nrhs, a, ia, ja, desca, ipiv, b, ib, jb, descb, x, ix, jx, descx):
+            """(info, iter); ipiv 1-based relative to the sub-matrix."""
+            from ..models.mixed import gesv_mixed as _g
+            A, B, X = _Loc(a, desca, dt), _Loc(b, descb, dt), _Loc(x, descx, dt)
+            Am, _ = _sub(A, ia, ja, n, n)
+            Bm, _ = _sub(B, ib, jb, n, nrhs)
+            Xm, done = _sub(X, ix, jx, n, nrhs)
+            piv = Pivots()
+            info, it = _g(Am, piv, Bm, Xm, _opts())
+            done()
+            X.writeback()
+            p = (piv.ipiv.cpu() + 1)
+            if isinstance(ipiv, np.ndarray):
+                ipiv[:p.numel()] = p.numpy()
+            else:
+                ipiv[:p.numel()] = p.to(ipiv.device, ipiv.dtype)
+            return info, it
+        g["gesv_mixed"] = gesv_mixed
+
+    # ---- eigenvalues by divide and conquer (scalapack_heevd.cc)
+    def heevd(jobz, uplo, n, a, ia, ja, desca, w, z=None, iz=1, jz=1, descz=None):
+        return heev(jobz, uplo, n, a, ia, ja, desca, w, z, iz, jz, descz)
+    g["heevd" if dt.is_complex else "syevd"] = heevd
     return g
 
 

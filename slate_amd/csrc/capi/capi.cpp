@@ -6,6 +6,7 @@
 #include <Python.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -66,7 +67,13 @@ double invoke_on(PyObject** fn, const char* name, const char* fmt, A... args) {
         PyErr_Fetch(&t, &v, &tb);
         PyObject* s = v ? PyObject_Str(v) : nullptr;
         g_err = s ? PyUnicode_AsUTF8(s) : "unknown error";
-        Py_XDECREF(s); Py_XDECREF(t); Py_XDECREF(v); Py_XDECREF(tb);
+        Py_XDECREF(s);
+        if (std::getenv("SLATE_AMD_CAPI_TRACEBACK")) {   // full Python traceback on stderr
+            PyErr_Restore(t, v, tb);                       // steals the references
+            PyErr_Print();
+        } else {
+            Py_XDECREF(t); Py_XDECREF(v); Py_XDECREF(tb);
+        }
     } else {
         out = PyFloat_Check(r) ? PyFloat_AsDouble(r) : (double)PyLong_AsLongLong(r);
         Py_DECREF(r);
@@ -236,6 +243,143 @@ void slate_sgesv_(const int64_t* n, const int64_t* nrhs, float* a, const int64_t
     *info = slate_sgesv(*n, *nrhs, a, *lda, ipiv, b, *ldb);
 }
 
+// --------------------------------------------- round-3 LAPACK-style ABI
+// lapack_api/lapack_{trmm,syrk,syr2k,symm,getri,lansy,lantr,gecon,pocon,
+// trcon,heevd,gesv_mixed,hemm,herk,her2k,lanhe}.cc.  Condition numbers and
+// iteration counts are written to output pointers, info is returned.
+#define SLATE_AMD_REAL2(X, T)                                                                                \
+    int slate_##X##trmm(char side, char uplo, char ta, char diag, int64_t m, int64_t n, T alpha, const T* a,  \
+                        int64_t lda, T* b, int64_t ldb) {                                                      \
+        return I(invoke(#X "trmm", "CCCCLLdLLLL", (int)side, (int)uplo, (int)ta, (int)diag, (long long)m,      \
+                        (long long)n, (double)alpha, P(a), (long long)lda, P(b), (long long)ldb));            \
+    }                                                                                                        \
+    int slate_##X##syrk(char uplo, char tr, int64_t n, int64_t k, T alpha, const T* a, int64_t lda, T beta,  \
+                        T* c, int64_t ldc) {                                                                   \
+        return I(invoke(#X "syrk", "CCLLdLLdLL", (int)uplo, (int)tr, (long long)n, (long long)k, (double)alpha, \
+                        P(a), (long long)lda, (double)beta, P(c), (long long)ldc));                           \
+    }                                                                                                        \
+    int slate_##X##syr2k(char uplo, char tr, int64_t n, int64_t k, T alpha, const T* a, int64_t lda,         \
+                         const T* b, int64_t ldb, T beta, T* c, int64_t ldc) {                                 \
+        return I(invoke(#X "syr2k", "CCLLddLLLLdLL", (int)uplo, (int)tr, (long long)n, (long long)k,           \
+                        (double)alpha, 0.0, P(a), (long long)lda, P(b), (long long)ldb, (double)beta, P(c),    \
+                        (long long)ldc));                                                                     \
+    }                                                                                                        \
+    int slate_##X##symm(char side, char uplo, int64_t m, int64_t n, T alpha, const T* a, int64_t lda,        \
+                        const T* b, int64_t ldb, T beta, T* c, int64_t ldc) {                                  \
+        return I(invoke(#X "symm", "CCLLddLLLLddLL", (int)side, (int)uplo, (long long)m, (long long)n,         \
+                        (double)alpha, 0.0, P(a), (long long)lda, P(b), (long long)ldb, (double)beta, 0.0,     \
+                        P(c), (long long)ldc));                                                               \
+    }                                                                                                        \
+    int slate_##X##getri(int64_t n, T* a, int64_t lda, const int64_t* ipiv) {                                \
+        return I(invoke(#X "getri", "LLLL", (long long)n, P(a), (long long)lda, P(ipiv)));                    \
+    }                                                                                                        \
+    double slate_##X##lansy(char norm, char uplo, int64_t n, const T* a, int64_t lda) {                      \
+        return invoke(#X "lansy", "CCLLL", (int)norm, (int)uplo, (long long)n, P(a), (long long)lda);         \
+    }                                                                                                        \
+    double slate_##X##lantr(char norm, char uplo, char diag, int64_t m, int64_t n, const T* a, int64_t lda) { \
+        return invoke(#X "lantr", "CCCLLLL", (int)norm, (int)uplo, (int)diag, (long long)m, (long long)n, P(a), \
+                      (long long)lda);                                                                        \
+    }                                                                                                        \
+    int slate_##X##gecon(char norm, int64_t n, const T* a, int64_t lda, T anorm, T* rcond) {                 \
+        return I(invoke(#X "gecon", "CLLLdL", (int)norm, (long long)n, P(a), (long long)lda, (double)anorm,   \
+                        P(rcond)));                                                                           \
+    }                                                                                                        \
+    int slate_##X##pocon(char uplo, int64_t n, const T* a, int64_t lda, T anorm, T* rcond) {                 \
+        return I(invoke(#X "pocon", "CLLLdL", (int)uplo, (long long)n, P(a), (long long)lda, (double)anorm,   \
+                        P(rcond)));                                                                           \
+    }                                                                                                        \
+    int slate_##X##trcon(char norm, char uplo, char diag, int64_t n, const T* a, int64_t lda, T* rcond) {    \
+        return I(invoke(#X "trcon", "CCCLLLL", (int)norm, (int)uplo, (int)diag, (long long)n, P(a),            \
+                        (long long)lda, P(rcond)));                                                           \
+    }                                                                                                        \
+    int slate_##X##syevd(char jobz, char uplo, int64_t n, T* a, int64_t lda, T* w) {                         \
+        return I(invoke(#X "syevd", "CCLLLL", (int)jobz, (int)uplo, (long long)n, P(a), (long long)lda, P(w))); \
+    }
+
+SLATE_AMD_REAL2(s, float)
+SLATE_AMD_REAL2(d, double)
+#undef SLATE_AMD_REAL2
+
+int slate_dsgesv(int64_t n, int64_t nrhs, double* a, int64_t lda, int64_t* ipiv, double* b, int64_t ldb, double* x,
+                 int64_t ldx, int64_t* iter) {
+    return I(invoke("dgesv_mixed", "LLLLLLLLLL", (long long)n, (long long)nrhs, P(a), (long long)lda, P(ipiv), P(b),
+                    (long long)ldb, P(x), (long long)ldx, P(iter)));
+}
+
+// complex<double> (interleaved re, im); complex scalars by pointer to (re, im)
+int slate_zhemm(char side, char uplo, int64_t m, int64_t n, const double* alpha, const double* a, int64_t lda,
+                const double* b, int64_t ldb, const double* beta, double* c, int64_t ldc) {
+    return I(invoke("zhemm", "CCLLddLLLLddLL", (int)side, (int)uplo, (long long)m, (long long)n, alpha[0], alpha[1],
+                    P(a), (long long)lda, P(b), (long long)ldb, beta[0], beta[1], P(c), (long long)ldc));
+}
+int slate_zherk(char uplo, char tr, int64_t n, int64_t k, double alpha, const double* a, int64_t lda, double beta,
+                double* c, int64_t ldc) {
+    return I(invoke("zherk", "CCLLdLLdLL", (int)uplo, (int)tr, (long long)n, (long long)k, alpha, P(a),
+                    (long long)lda, beta, P(c), (long long)ldc));
+}
+int slate_zher2k(char uplo, char tr, int64_t n, int64_t k, const double* alpha, const double* a, int64_t lda,
+                 const double* b, int64_t ldb, double beta, double* c, int64_t ldc) {
+    return I(invoke("zher2k", "CCLLddLLLLdLL", (int)uplo, (int)tr, (long long)n, (long long)k, alpha[0], alpha[1],
+                    P(a), (long long)lda, P(b), (long long)ldb, beta, P(c), (long long)ldc));
+}
+double slate_zlanhe(char norm, char uplo, int64_t n, const double* a, int64_t lda) {
+    return invoke("zlanhe", "CCLLL", (int)norm, (int)uplo, (long long)n, P(a), (long long)lda);
+}
+int slate_zheevd(char jobz, char uplo, int64_t n, double* a, int64_t lda, double* w) {
+    return I(invoke("zheevd", "CCLLLL", (int)jobz, (int)uplo, (long long)n, P(a), (long long)lda, P(w)));
+}
+
+// Fortran-callable aliases (all arguments by reference)
+void slate_dtrmm_(const char* side, const char* uplo, const char* ta, const char* diag, const int64_t* m,
+                  const int64_t* n, const double* alpha, const double* a, const int64_t* lda, double* b,
+                  const int64_t* ldb) {
+    slate_dtrmm(*side, *uplo, *ta, *diag, *m, *n, *alpha, a, *lda, b, *ldb);
+}
+void slate_dsyrk_(const char* uplo, const char* tr, const int64_t* n, const int64_t* k, const double* alpha,
+                  const double* a, const int64_t* lda, const double* beta, double* c, const int64_t* ldc) {
+    slate_dsyrk(*uplo, *tr, *n, *k, *alpha, a, *lda, *beta, c, *ldc);
+}
+void slate_dsyr2k_(const char* uplo, const char* tr, const int64_t* n, const int64_t* k, const double* alpha,
+                   const double* a, const int64_t* lda, const double* b, const int64_t* ldb, const double* beta,
+                   double* c, const int64_t* ldc) {
+    slate_dsyr2k(*uplo, *tr, *n, *k, *alpha, a, *lda, b, *ldb, *beta, c, *ldc);
+}
+void slate_dsymm_(const char* side, const char* uplo, const int64_t* m, const int64_t* n, const double* alpha,
+                  const double* a, const int64_t* lda, const double* b, const int64_t* ldb, const double* beta,
+                  double* c, const int64_t* ldc) {
+    slate_dsymm(*side, *uplo, *m, *n, *alpha, a, *lda, b, *ldb, *beta, c, *ldc);
+}
+void slate_dgetri_(const int64_t* n, double* a, const int64_t* lda, const int64_t* ipiv, int64_t* info) {
+    *info = slate_dgetri(*n, a, *lda, ipiv);
+}
+double slate_dlansy_(const char* norm, const char* uplo, const int64_t* n, const double* a, const int64_t* lda) {
+    return slate_dlansy(*norm, *uplo, *n, a, *lda);
+}
+double slate_dlantr_(const char* norm, const char* uplo, const char* diag, const int64_t* m, const int64_t* n,
+                     const double* a, const int64_t* lda) {
+    return slate_dlantr(*norm, *uplo, *diag, *m, *n, a, *lda);
+}
+void slate_dgecon_(const char* norm, const int64_t* n, const double* a, const int64_t* lda, const double* anorm,
+                   double* rcond, int64_t* info) {
+    *info = slate_dgecon(*norm, *n, a, *lda, *anorm, rcond);
+}
+void slate_dpocon_(const char* uplo, const int64_t* n, const double* a, const int64_t* lda, const double* anorm,
+                   double* rcond, int64_t* info) {
+    *info = slate_dpocon(*uplo, *n, a, *lda, *anorm, rcond);
+}
+void slate_dtrcon_(const char* norm, const char* uplo, const char* diag, const int64_t* n, const double* a,
+                   const int64_t* lda, double* rcond, int64_t* info) {
+    *info = slate_dtrcon(*norm, *uplo, *diag, *n, a, *lda, rcond);
+}
+void slate_dsyevd_(const char* jobz, const char* uplo, const int64_t* n, double* a, const int64_t* lda, double* w,
+                   int64_t* info) {
+    *info = slate_dsyevd(*jobz, *uplo, *n, a, *lda, w);
+}
+void slate_dsgesv_(const int64_t* n, const int64_t* nrhs, double* a, const int64_t* lda, int64_t* ipiv, double* b,
+                   const int64_t* ldb, double* x, const int64_t* ldx, int64_t* iter, int64_t* info) {
+    *info = slate_dsgesv(*n, *nrhs, a, *lda, ipiv, b, *ldb, x, *ldx, iter);
+}
+
 // ------------------------------------------------------------------ BLACS
 // Minimal BLACS over torch.distributed (no MPI here): the process grid of a
 // context is created by Cblacs_gridinit over the world of ranks started with
@@ -364,6 +508,164 @@ SLATE_AMD_SCALAPACK_REAL(d, double)
 SLATE_AMD_SCALAPACK_CPLX(c, float)
 SLATE_AMD_SCALAPACK_CPLX(z, double)
 #undef SLATE_AMD_SCALAPACK_CPLX
+
+// ------------------------------------- round-3 ScaLAPACK interposers
+// scalapack_api/scalapack_{trmm,syrk,syr2k,symm,potri,getri,lansy,lantr,
+// gecon,pocon,trcon,syev,syevd,gesvd,gels,gesv_mixed}.cc (+ the complex
+// herk / her2k / hemm / lanhe / heev / heevd).  Workspace queries
+// (lwork = -1) return a workspace size of 1 (the library allocates its own).
+#define QUERY(lw, work, info)                                                                              \
+    if (*(lw) == -1) { if (work) (work)[0] = 1; *(info) = 0; return; }
+
+#define SLATE_AMD_SCALAPACK_REAL2(X, T)                                                                    \
+    void p##X##trmm_(const char* side, const char* uplo, const char* ta, const char* diag, const int* m,     \
+                     const int* n, const T* alpha, const T* a, const int* ia, const int* ja, const int* desca, \
+                     T* b, const int* ib, const int* jb, const int* descb) {                                \
+        invoke_on(&g_scal, "p" #X "trmm", "CCCCiidLii" D9 "Lii" D9, (int)*side, (int)*uplo, (int)*ta,          \
+                  (int)*diag, *m, *n, (double)*alpha, P(a), *ia, *ja, DV(desca), P(b), *ib, *jb, DV(descb));    \
+    }                                                                                                      \
+    void p##X##syrk_(const char* uplo, const char* tr, const int* n, const int* k, const T* alpha,            \
+                     const T* a, const int* ia, const int* ja, const int* desca, const T* beta, T* c,          \
+                     const int* ic, const int* jc, const int* descc) {                                     \
+        invoke_on(&g_scal, "p" #X "syrk", "CCiidLii" D9 "dLii" D9, (int)*uplo, (int)*tr, *n, *k,               \
+                  (double)*alpha, P(a), *ia, *ja, DV(desca), (double)*beta, P(c), *ic, *jc, DV(descc));        \
+    }                                                                                                      \
+    void p##X##syr2k_(const char* uplo, const char* tr, const int* n, const int* k, const T* alpha,           \
+                      const T* a, const int* ia, const int* ja, const int* desca, const T* b, const int* ib,    \
+                      const int* jb, const int* descb, const T* beta, T* c, const int* ic, const int* jc,     \
+                      const int* descc) {                                                                  \
+        invoke_on(&g_scal, "p" #X "syr2k", "CCiiddLii" D9 "Lii" D9 "dLii" D9, (int)*uplo, (int)*tr, *n, *k,    \
+                  (double)*alpha, 0.0, P(a), *ia, *ja, DV(desca), P(b), *ib, *jb, DV(descb), (double)*beta,    \
+                  P(c), *ic, *jc, DV(descc));                                                              \
+    }                                                                                                      \
+    void p##X##symm_(const char* side, const char* uplo, const int* m, const int* n, const T* alpha,          \
+                     const T* a, const int* ia, const int* ja, const int* desca, const T* b, const int* ib,     \
+                     const int* jb, const int* descb, const T* beta, T* c, const int* ic, const int* jc,      \
+                     const int* descc) {                                                                   \
+        invoke_on(&g_scal, "p" #X "symm", "CCiiddLii" D9 "Lii" D9 "ddLii" D9, (int)*side, (int)*uplo, *m, *n,  \
+                  (double)*alpha, 0.0, P(a), *ia, *ja, DV(desca), P(b), *ib, *jb, DV(descb), (double)*beta,    \
+                  0.0, P(c), *ic, *jc, DV(descc));                                                         \
+    }                                                                                                      \
+    void p##X##potri_(const char* uplo, const int* n, T* a, const int* ia, const int* ja, const int* desca,   \
+                      int* info) {                                                                         \
+        *info = I(invoke_on(&g_scal, "p" #X "potri", "CiLii" D9, (int)*uplo, *n, P(a), *ia, *ja, DV(desca)));  \
+    }                                                                                                      \
+    void p##X##getri_(const int* n, T* a, const int* ia, const int* ja, const int* desca, const int* ipiv,    \
+                      T* work, const int* lwork, int* iwork, const int* liwork, int* info) {               \
+        (void)iwork; (void)liwork;                                                                         \
+        QUERY(lwork, work, info)                                                                            \
+        *info = I(invoke_on(&g_scal, "p" #X "getri", "iLii" D9 "L", *n, P(a), *ia, *ja, DV(desca), P(ipiv)));  \
+    }                                                                                                      \
+    T p##X##lansy_(const char* norm, const char* uplo, const int* n, const T* a, const int* ia, const int* ja, \
+                   const int* desca, T* /*work*/) {                                                        \
+        return (T)invoke_on(&g_scal, "p" #X "lansy", "CCiLii" D9, (int)*norm, (int)*uplo, *n, P(a), *ia, *ja,   \
+                            DV(desca));                                                                     \
+    }                                                                                                      \
+    T p##X##lantr_(const char* norm, const char* uplo, const char* diag, const int* m, const int* n,          \
+                   const T* a, const int* ia, const int* ja, const int* desca, T* /*work*/) {              \
+        return (T)invoke_on(&g_scal, "p" #X "lantr", "CCCiiLii" D9, (int)*norm, (int)*uplo, (int)*diag, *m,     \
+                            *n, P(a), *ia, *ja, DV(desca));                                                 \
+    }                                                                                                      \
+    void p##X##gecon_(const char* norm, const int* n, const T* a, const int* ia, const int* ja,              \
+                      const int* desca, const T* anorm, T* rcond, T* work, const int* lwork, int* iwork,      \
+                      const int* liwork, int* info) {                                                      \
+        (void)iwork; (void)liwork;                                                                         \
+        QUERY(lwork, work, info)                                                                            \
+        *info = I(invoke_on(&g_scal, "p" #X "gecon", "CiLii" D9 "dL", (int)*norm, *n, P(a), *ia, *ja,          \
+                            DV(desca), (double)*anorm, P(rcond)));                                          \
+    }                                                                                                      \
+    void p##X##pocon_(const char* uplo, const int* n, const T* a, const int* ia, const int* ja,              \
+                      const int* desca, const T* anorm, T* rcond, T* work, const int* lwork, int* iwork,      \
+                      const int* liwork, int* info) {                                                      \
+        (void)iwork; (void)liwork;                                                                         \
+        QUERY(lwork, work, info)                                                                            \
+        *info = I(invoke_on(&g_scal, "p" #X "pocon", "CiLii" D9 "dL", (int)*uplo, *n, P(a), *ia, *ja,          \
+                            DV(desca), (double)*anorm, P(rcond)));                                          \
+    }                                                                                                      \
+    void p##X##trcon_(const char* norm, const char* uplo, const char* diag, const int* n, const T* a,         \
+                      const int* ia, const int* ja, const int* desca, T* rcond, T* work, const int* lwork,    \
+                      int* iwork, const int* liwork, int* info) {                                          \
+        (void)iwork; (void)liwork;                                                                         \
+        QUERY(lwork, work, info)                                                                            \
+        *info = I(invoke_on(&g_scal, "p" #X "trcon", "CCCiLii" D9 "L", (int)*norm, (int)*uplo, (int)*diag, *n, \
+                            P(a), *ia, *ja, DV(desca), P(rcond)));                                          \
+    }                                                                                                      \
+    void p##X##syev_(const char* jobz, const char* uplo, const int* n, T* a, const int* ia, const int* ja,    \
+                     const int* desca, T* w, T* z, const int* iz, const int* jz, const int* descz, T* work,   \
+                     const int* lwork, int* info) {                                                        \
+        QUERY(lwork, work, info)                                                                            \
+        *info = I(invoke_on(&g_scal, "p" #X "syev", "CCiLii" D9 "LLii" D9, (int)*jobz, (int)*uplo, *n, P(a),    \
+                            *ia, *ja, DV(desca), P(w), P(z), *iz, *jz, DV(descz)));                         \
+    }                                                                                                      \
+    void p##X##syevd_(const char* jobz, const char* uplo, const int* n, T* a, const int* ia, const int* ja,   \
+                      const int* desca, T* w, T* z, const int* iz, const int* jz, const int* descz, T* work,  \
+                      const int* lwork, int* iwork, const int* liwork, int* info) {                        \
+        (void)iwork; (void)liwork;                                                                         \
+        QUERY(lwork, work, info)                                                                            \
+        *info = I(invoke_on(&g_scal, "p" #X "syevd", "CCiLii" D9 "LLii" D9, (int)*jobz, (int)*uplo, *n, P(a),   \
+                            *ia, *ja, DV(desca), P(w), P(z), *iz, *jz, DV(descz)));                         \
+    }                                                                                                      \
+    void p##X##gesvd_(const char* jobu, const char* jobvt, const int* m, const int* n, T* a, const int* ia,  \
+                      const int* ja, const int* desca, T* s, T* u, const int* iu, const int* ju,              \
+                      const int* descu, T* vt, const int* ivt, const int* jvt, const int* descvt, T* work,    \
+                      const int* lwork, int* info) {                                                       \
+        QUERY(lwork, work, info)                                                                            \
+        *info = I(invoke_on(&g_scal, "p" #X "gesvd", "CCiiLii" D9 "LLii" D9 "Lii" D9, (int)*jobu, (int)*jobvt,  \
+                            *m, *n, P(a), *ia, *ja, DV(desca), P(s), P(u), *iu, *ju, DV(descu), P(vt), *ivt,   \
+                            *jvt, DV(descvt)));                                                             \
+    }                                                                                                      \
+    void p##X##gels_(const char* t, const int* m, const int* n, const int* nrhs, T* a, const int* ia,        \
+                     const int* ja, const int* desca, T* b, const int* ib, const int* jb, const int* descb,   \
+                     T* work, const int* lwork, int* info) {                                               \
+        QUERY(lwork, work, info)                                                                            \
+        *info = I(invoke_on(&g_scal, "p" #X "gels", "CiiiLii" D9 "Lii" D9, (int)*t, *m, *n, *nrhs, P(a), *ia,  \
+                            *ja, DV(desca), P(b), *ib, *jb, DV(descb)));                                    \
+    }
+
+SLATE_AMD_SCALAPACK_REAL2(s, float)
+SLATE_AMD_SCALAPACK_REAL2(d, double)
+#undef SLATE_AMD_SCALAPACK_REAL2
+
+void pdsgesv_(const int* n, const int* nrhs, double* a, const int* ia, const int* ja, const int* desca, int* ipiv,
+              double* b, const int* ib, const int* jb, const int* descb, double* x, const int* ix, const int* jx,
+              const int* descx, int* iter, int* info) {
+    *info = I(invoke_on(&g_scal, "pdgesv_mixed", "iiLii" D9 "LLii" D9 "Lii" D9 "L", *n, *nrhs, P(a), *ia, *ja,
+                        DV(desca), P(ipiv), P(b), *ib, *jb, DV(descb), P(x), *ix, *jx, DV(descx), P(iter)));
+}
+
+// complex<double> (interleaved): Hermitian BLAS-3, norms, eigenvalues
+void pzherk_(const char* uplo, const char* tr, const int* n, const int* k, const double* alpha, const double* a,
+             const int* ia, const int* ja, const int* desca, const double* beta, double* c, const int* ic,
+             const int* jc, const int* descc) {
+    invoke_on(&g_scal, "pzherk", "CCiidLii" D9 "dLii" D9, (int)*uplo, (int)*tr, *n, *k, *alpha, P(a), *ia, *ja,
+              DV(desca), *beta, P(c), *ic, *jc, DV(descc));
+}
+void pzher2k_(const char* uplo, const char* tr, const int* n, const int* k, const double* alpha, const double* a,
+              const int* ia, const int* ja, const int* desca, const double* b, const int* ib, const int* jb,
+              const int* descb, const double* beta, double* c, const int* ic, const int* jc, const int* descc) {
+    invoke_on(&g_scal, "pzher2k", "CCiiddLii" D9 "Lii" D9 "dLii" D9, (int)*uplo, (int)*tr, *n, *k, alpha[0],
+              alpha[1], P(a), *ia, *ja, DV(desca), P(b), *ib, *jb, DV(descb), *beta, P(c), *ic, *jc, DV(descc));
+}
+void pzhemm_(const char* side, const char* uplo, const int* m, const int* n, const double* alpha, const double* a,
+             const int* ia, const int* ja, const int* desca, const double* b, const int* ib, const int* jb,
+             const int* descb, const double* beta, double* c, const int* ic, const int* jc, const int* descc) {
+    invoke_on(&g_scal, "pzhemm", "CCiiddLii" D9 "Lii" D9 "ddLii" D9, (int)*side, (int)*uplo, *m, *n, alpha[0],
+              alpha[1], P(a), *ia, *ja, DV(desca), P(b), *ib, *jb, DV(descb), beta[0], beta[1], P(c), *ic, *jc,
+              DV(descc));
+}
+double pzlanhe_(const char* norm, const char* uplo, const int* n, const double* a, const int* ia, const int* ja,
+                const int* desca, double* /*work*/) {
+    return invoke_on(&g_scal, "pzlanhe", "CCiLii" D9, (int)*norm, (int)*uplo, *n, P(a), *ia, *ja, DV(desca));
+}
+void pzheevd_(const char* jobz, const char* uplo, const int* n, double* a, const int* ia, const int* ja,
+              const int* desca, double* w, double* z, const int* iz, const int* jz, const int* descz, double* work,
+              const int* lwork, double* rwork, const int* lrwork, int* iwork, const int* liwork, int* info) {
+    (void)rwork; (void)lrwork; (void)iwork; (void)liwork;
+    QUERY(lwork, work, info)
+    *info = I(invoke_on(&g_scal, "pzheevd", "CCiLii" D9 "LLii" D9, (int)*jobz, (int)*uplo, *n, P(a), *ia, *ja,
+                        DV(desca), P(w), P(z), *iz, *jz, DV(descz)));
+}
+#undef QUERY
 
 // ------------------------------------------------------ matrix handles
 slate_amd_matrix_t slate_amd_matrix_create(char kind, char dtype, int64_t m, int64_t n, int64_t nb, int p, int q) {

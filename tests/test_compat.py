@@ -208,6 +208,40 @@ def test_c_scalapack_and_handles(tmp_path, grid):
             assert val < 1e-9, ln
 
 
+@pytest.mark.parametrize("grid", ["1x1", "2x1"])
+def test_c_compat_more(tmp_path, grid):
+    """Round-3 LAPACK-style (trmm/syrk/symm/getri/gecon/lansy/lantr/syevd/
+    dsgesv/zherk/zlanhe) and ScaLAPACK (pdtrmm/pdsymm/pdsyrk/pdgetri/pdgecon/
+    pdpotri/pdlansy/pdsyev/pdsyevd/pdsgesv) entry points, from C."""
+    import os
+    import subprocess
+    from dist_util import _free_port
+    exe, root = _build_c(tmp_path, "ex_compat_more.c", "ex_compat_more")
+    p, q = map(int, grid.split("x"))
+    size = p * q
+    port = str(_free_port())
+    procs = []
+    for r in range(size):
+        env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""),
+                   SLATE_AMD_SCALAPACK_TARGET="host", SLATE_AMD_LAPACK_TARGET="host", OMP_NUM_THREADS="2")
+        if size > 1:
+            env.update(RANK=str(r), WORLD_SIZE=str(size), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                       MASTER_PORT=port)
+        procs.append(subprocess.Popen([exe, grid], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                      text=True))
+    outs = [pr.communicate(timeout=600)[0] for pr in procs]
+    for r, (pr, out) in enumerate(zip(procs, outs)):
+        assert pr.returncode == 0, out
+        lines = [ln for ln in out.splitlines() if ln.startswith("rank ")]
+        assert len(lines) == (20 if r == 0 else 9), out
+        for ln in lines:
+            assert "FAILED" not in ln, ln
+            if "info=" in ln:
+                assert "info=0" in ln, ln
+            else:
+                assert float(ln.split()[-1]) < 1e-9, ln
+
+
 @pytest.mark.parametrize("grid", ["1x1", "1x2", "2x1"])
 def test_cpp_api(tmp_path, grid):
     """The C++ API (include/slate_amd/slate_amd.hh): posv/gesv/getri/trmm/
