@@ -22,14 +22,13 @@ from __future__ import annotations
 import torch
 
 from .. import ops
-from ..core.enums import Diag, MethodGemm, Op, Option, Side, Uplo
+from ..core.enums import Diag, MethodGemm, MethodHemm, MethodTrsm, Op, Option, Side, Uplo
 from ..core.exceptions import SlateError
 from ..core.options import get_option
 from ..core.storage import DEV, l2g
 from ..parallel.streams import StreamSet
-from ..parallel.tilecomm import exchange_tiles
 from ..utils.trace import trace_block
-from ._panels import assemble_cols, plan_col_gather, row_bcast
+from ._panels import assemble_cols, col_bcast, plan_col_gather, row_bcast
 from ._util import conj_trans, grid_of, target_slot, tiles_local_before
 
 
@@ -472,6 +471,8 @@ def hemm(side, alpha, A, B, beta, C, opts=None, _sym=False):
                 ops.gemm(alpha, b, F, beta, c, tb, 'N')
             _done(C)
             return C
+        if _hemm_method(B, opts) == MethodHemm.A:
+            return _hemmA(side, alpha, A, B, beta, C, opts, _sym)
         # hemmC with both triangles materialised once (SLATE broadcasts A
         # and A^H tiles per step and runs the diagonal tiles on the host,
         # src/hemmC.cc:147-429): one transposing redistribution, then SUMMA
@@ -479,6 +480,131 @@ def hemm(side, alpha, A, B, beta, C, opts=None, _sym=False):
         if side == Side.Left:
             return gemm(alpha, F, B, beta, C, opts)
         return gemm(alpha, B, F, beta, C, opts)
+
+
+def _hemm_method(B, opts):
+    """src/hemm.cc:11-24: stationary A when B has a single block column."""
+    m = get_option(opts, Option.MethodHemm, MethodHemm.Auto)
+    if m in (MethodHemm.A, MethodHemm.C):
+        return m
+    return MethodHemm.A if B.nt() < 2 else MethodHemm.C
+
+
+def _hemmA(side, alpha, A, B, beta, C, opts, sym):
+    """Right side through the transposed Left problem: C = alpha B A + beta
+    C  <=>  C^H = conj(alpha) A B^H + conj(beta) C^H  (A Hermitian; ^T and
+    no conjugation for symmetric A)."""
+    slot = target_slot(C, opts)
+    if side == Side.Right:
+        cplx = C.storage.dtype.is_complex and not sym
+        tr = (lambda X: X.conj_transpose()) if cplx else (lambda X: X.transpose())
+        cj = (lambda v: complex(v).conjugate()) if cplx else (lambda v: v)
+        Bt = _copy_in(tr(B), C, slot)
+        Ct = _copy_in(tr(C), C, slot)
+        _hemmA_left(cj(alpha), A, Bt, cj(beta), Ct, slot, sym)
+        _copy_out(tr(Ct), C)
+        return C
+    Bw = B if (_at_origin(B) and _same_grid(B, C)) else _copy_in(B, C, slot)
+    Cw = C if _at_origin(C) else _fresh(C, C.m(), C.n(), slot)
+    if Cw is not C and beta != 0:
+        _copy_out(C, Cw)
+    _hemmA_left(alpha, A, Bw, beta, Cw, slot, sym)
+    if Cw is not C:
+        _copy_out(Cw, C)
+    return C
+
+
+def _hemmA_left(alpha, A, B, beta, C, slot, sym):
+    """Stationary-A hemm (src/hemmA.cc): only the stored triangle of A is
+    read and A never moves.  With T = stored triangle (diagonal included)
+    and S = strict stored triangle, A = T + S^H, so per block column jb of
+    B:  P = T_loc B(my A cols, jb)  is a partial sum for my local C rows and
+    Q = S_loc^H B(my A rows, jb)  one for the C rows of my local A columns.
+    Q is summed down the process column, its rows that belong to my process
+    row are added into P, and P is reduced along the process row onto the
+    owner of C(:, jb) (tile reduce, the reference's listReduce)."""
+    import numpy as np
+    from ._panels import _ranges
+    if not (_same_grid(A, C) and A.global_offsets() == (0, 0) and A.op() == Op.NoTrans
+            and A.local_block(slot).mloc == C.local_block(slot).mloc):
+        A = _copy_herm(A, C, slot)
+    sC = C.storage
+    bc = sC.bc
+    grid = grid_of(C)
+    lbA = A.local_block(slot)
+    lbB = B.local_block(slot)
+    lbC = C.local_block(slot)
+    dev = lbC.data.device
+    dt = sC.dtype
+    nb, p, q, pr, pc = bc.nb, bc.p, bc.q, bc.pr, bc.pc
+    n = A.n()
+    mloc, nlocA = lbA.mloc, lbA.nloc
+    lower = A.uploPhysical() == Uplo.Lower
+    gr = torch.from_numpy(_local_globals(mloc, nb, p, pr, n)).to(dev)
+    gc = torch.from_numpy(_local_globals(nlocA, nb, q, pc, n)).to(dev)
+    keep = (gr[:, None] >= gc[None, :]) if lower else (gr[:, None] <= gc[None, :])
+    strict = keep & (gr[:, None] != gc[None, :])
+    Aloc = lbA.data
+    T = ops.colmajor_empty(mloc, nlocA, dt, dev)
+    Sx = ops.colmajor_empty(mloc, nlocA, dt, dev)
+    if mloc and nlocA:
+        zero = torch.zeros((), dtype=dt, device=dev)
+        T.copy_(torch.where(keep, Aloc, zero))
+        Sx.copy_(torch.where(strict, Aloc, zero))
+        if dt.is_complex and not sym:
+            d = keep & ~strict
+            T.copy_(torch.where(d, T.real.to(dt), T))
+    # rows of Q (my local A column tiles k) that land in my process row:
+    # local A column offset t*nb -> local C row offset of tile k
+    ks = np.arange(pc, (n + nb - 1) // nb, q, dtype=np.int64)
+    lens = np.minimum(nb, n - ks * nb)
+    qoff = np.cumsum(lens) - lens
+    mine = ks % p == pr
+    lrow = np.asarray([tiles_local_before(int(k), p, pr) * nb for k in ks[mine]], dtype=np.int64)
+    src_rows = torch.from_numpy(_ranges(qoff[mine], lens[mine])).to(dev)
+    dst_rows = torch.from_numpy(_ranges(lrow, lens[mine])).to(dev)
+    plan = plan_col_gather(B.storage.tileMb, 0, A.nt(), nb, p, q, pc, dev)
+    ct = 'T' if sym else conj_trans(dt)
+    for jb in range(C.nt()):
+        owner = jb % q
+        wb = C.tileNb(jb)
+        lcb = tiles_local_before(jb, q, pc) * nb - lbB.col_off
+        src = lbB.data[:, lcb:lcb + wb] if pc == owner else None
+        Prow = row_bcast(grid, src, owner, lbB.mloc, wb, dt, dev)
+        Bq = assemble_cols(plan, Prow, grid, p, wb, dt, dev)
+        P = ops.colmajor_zeros(mloc, wb, dt, dev)
+        Q = ops.colmajor_zeros(nlocA, wb, dt, dev)
+        if mloc and nlocA:
+            ops.gemm(1.0, T, Bq, 0.0, P)
+            ops.gemm(1.0, Sx, Prow, 0.0, Q, ct, 'N')
+        if p > 1 and nlocA:
+            grid.col_comm.allreduce(Q)
+        if src_rows.numel():
+            P.index_add_(0, dst_rows, Q.index_select(0, src_rows))
+        if q > 1 and mloc:
+            grid.row_comm.reduce(P, owner)
+        if pc == owner and lbC.mloc:
+            lcc = tiles_local_before(jb, q, pc) * nb - lbC.col_off
+            Cj = lbC.data[:, lcc:lcc + wb]
+            if beta == 0:                       # C is not read when beta = 0
+                ops.gecopy(P, Cj)
+                if alpha != 1:
+                    ops.gescale(alpha, Cj)
+            else:
+                ops.geadd(alpha, P, beta, Cj)
+    _done(C)
+    return C
+
+
+def _copy_herm(A, like, slot):
+    """Stored triangle of a Hermitian/symmetric A on like's grid, at the
+    storage origin."""
+    from ..core.matrix import HermitianMatrix
+    from ..parallel.redist import redistribute_pieces
+    W = _fresh(like, A.n(), A.n(), slot, cls=HermitianMatrix, uplo=A.uploPhysical())
+    Ab = A if A.op() == Op.NoTrans else (A.conj_transpose() if A.op() == Op.ConjTrans else A.transpose())
+    redistribute_pieces(Ab, W, uplo=A.uploPhysical())
+    return W
 
 
 def symm(side, alpha, A, B, beta, C, opts=None):
@@ -492,19 +618,6 @@ def _tri_args(A):
     return uplo, diag
 
 
-def _tri_as_general(A, slot):
-    """op(A) of a triangular view as a general block-cyclic matrix with
-    explicit zeros outside the triangle (unit diagonal materialised)."""
-    from ..parallel.redist import redistribute_pieces
-    n = A.n()
-    F = _fresh(A, n, n, slot)           # zero-initialised
-    redistribute_pieces(A, F, uplo=A.uplo())
-    if A.diag() == Diag.Unit:
-        from .aux import set_diag
-        set_diag(F, 1.0)
-    return F
-
-
 def trmm(side, alpha, A, B, opts=None):
     """B = alpha op(A) B (Left) or alpha B op(A) (Right), A triangular."""
     side = Side.from_string(side) if not isinstance(side, Side) else side
@@ -516,21 +629,14 @@ def trmm(side, alpha, A, B, opts=None):
             ops.trmm(side.value, uplo, ta, diag, alpha, a, b)
             _done(B)
             return B
-        # distributed (work::trmm analogue): the triangle as a general
-        # operand with zeros, one SUMMA product into a work matrix
-        slot = target_slot(B, opts)
-        T = _tri_as_general(A, slot)
-        X = _fresh(B, B.m(), B.n(), slot)
-        if side == Side.Left:
-            gemm(alpha, T, B, 0.0, X, opts)
-        else:
-            gemm(alpha, B, T, 0.0, X, opts)
-        _copy_out(X, B)
-        return B
+        return _tri_dist("mm", side, alpha, A, B, opts)
 
 
 def trsm(side, alpha, A, B, opts=None):
-    """Solve op(A) X = alpha B (Left) or X op(A) = alpha B (Right); B <- X."""
+    """Solve op(A) X = alpha B (Left) or X op(A) = alpha B (Right); B <- X.
+    Option.MethodTrsm: B (stationary B, work::trsm), A (stationary A with
+    partial-sum reduces, work::trsmA); Auto picks A when B has a single
+    block column (src/trsm.cc:12-21)."""
     side = Side.from_string(side) if not isinstance(side, Side) else side
     with trace_block("trsm"):
         if _single(A, B) and B.op() == Op.NoTrans:
@@ -540,118 +646,181 @@ def trsm(side, alpha, A, B, opts=None):
             ops.trsm(side.value, uplo, ta, diag, alpha, a, b)
             _done(B)
             return B
-        slot = target_slot(B, opts)
-        if side == Side.Right:
-            # X op(A) = alpha B  <=>  op(A)^H X^H = conj(alpha) B^H  (^T when
-            # op(A) = A^T): one transposing redistribution each way
-            use_h = A.op() != Op.Trans
-            tr = (lambda X: X.conj_transpose()) if use_h else (lambda X: X.transpose())
-            Bw = B if B.op() == Op.NoTrans else _copy_in(B, B, slot)
-            Bt = _copy_in(tr(Bw), Bw, slot)
-            a2 = complex(alpha).conjugate() if (use_h and B.storage.dtype.is_complex) else alpha
-            _trsm_left(a2, tr(A), Bt, slot)
-            _copy_out(tr(Bt), B)
-            return B
-        if B.op() != Op.NoTrans or B.storage.bc is None or not B.storage.local \
-                or B.global_offsets()[0] % B.storage.bc.nb:
-            Bw = _copy_in(B, B, slot)
-            _trsm_left(alpha, A, Bw, slot)
-            _copy_out(Bw, B)
-            return B
-        return _trsm_left(alpha, A, B, slot)
+        return _tri_dist("sm", side, alpha, A, B, opts)
 
 
-def _trsm_left(alpha, A, B, slot):
-    """Left solve on a block-cyclic NoTrans B whose rows start on a tile
-    boundary; A is redistributed onto B's grid when its tiles do not match
-    B's row tiles (stored triangle only)."""
-    nb = B.storage.bc.nb
-    sA = A.storage
-    ok = sA.bc is not None and sA.bc.mb == nb and sA.bc.nb == nb and \
-        all(x % nb == 0 for x in A.global_offsets()) and A.last_mb is None and A.last_nb is None
-    if not ok:
-        from ..core.matrix import TriangularMatrix
-        F = _fresh(B, A.m(), A.n(), slot)
-        from ..parallel.redist import redistribute_pieces
-        redistribute_pieces(A, F, uplo=A.uplo())
-        A = TriangularMatrix(A.uplo(), F, diag=A.diag())
-    return _trsm_left_dist(alpha, A, B, slot)
+def _trsm_method(B, opts):
+    m = get_option(opts, Option.MethodTrsm, MethodTrsm.Auto)
+    if m in (MethodTrsm.A, MethodTrsm.B):
+        return m
+    return MethodTrsm.A if B.nt() < 2 else MethodTrsm.B
 
 
-def _trsm_left_dist(alpha, A, B, slot):
-    """Distributed Left trsm, any uplo/op of A (work::trsm analogue,
-    src/work/work_trsm.cc:102-265): per tile row k the diagonal tile goes to
-    the owners of B(k,:), they solve, X(k,:) goes down each process column,
-    the panel tiles A(:,k) are delivered (one batched p2p exchange) to the
-    owners of the B rows they update, packed in local-row order, and ONE
-    GEMM updates all of this rank's remaining rows."""
+def _tri_dist(kind, side, alpha, A, B, opts):
+    """Distributed trmm ("mm") / trsm ("sm").  Right side by the transposed
+    Left problem: X op(A) = alpha B  <=>  op(A)^H X^H = conj(alpha) B^H
+    (^T when op(A) = A^T), one transposing redistribution each way.  The
+    Left problem runs on B's grid with B at its storage origin (a sub-view B
+    is copied into a fresh matrix and back) and op(A) as a NoTrans
+    triangle whose tile rows coincide with B's (_tri_work)."""
+    slot = target_slot(B, opts)
+    if side == Side.Right:
+        use_h = A.op() != Op.Trans
+        tr = (lambda X: X.conj_transpose()) if use_h else (lambda X: X.transpose())
+        Bw = B if B.op() == Op.NoTrans else _copy_in(B, B, slot)
+        Bt = _copy_in(tr(Bw), Bw, slot)
+        a2 = complex(alpha).conjugate() if (use_h and B.storage.dtype.is_complex) else alpha
+        _tri_left(kind, a2, tr(A), Bt, slot, opts)
+        _copy_out(tr(Bt), B)
+        return B
+    if not _at_origin(B):
+        Bw = _copy_in(B, B, slot)
+        _tri_left(kind, alpha, A, Bw, slot, opts)
+        _copy_out(Bw, B)
+        return B
+    return _tri_left(kind, alpha, A, B, slot, opts)
+
+
+def _tri_work(A, B, slot):
+    """op(A) as a NoTrans triangular matrix on B's grid, at its storage
+    origin, so that its tile row i lives on the process row of B's tile row
+    i: A itself when it already is, else ONE redistribution of the stored
+    triangle (transposing / conjugating when op(A) != NoTrans)."""
+    from ..core.matrix import TriangularMatrix
+    ok = A.op() == Op.NoTrans and _same_grid(A, B) and A.global_offsets() == (0, 0) \
+        and A.last_mb is None and A.last_nb is None and A.m() == B.m() \
+        and A.local_block(slot).mloc == B.local_block(slot).mloc
+    if ok:
+        return A
+    from ..parallel.redist import redistribute_pieces
+    F = _fresh(B, A.m(), A.n(), slot)
+    redistribute_pieces(A, F, uplo=A.uplo())
+    return TriangularMatrix(A.uplo(), F, diag=A.diag())
+
+
+def _tri_left(kind, alpha, A, B, slot, opts):
+    A = _tri_work(A, B, slot)
+    if kind == "sm" and _trsm_method(B, opts) == MethodTrsm.A:
+        return _trsmA_left(alpha, A, B, slot)
+    return _tri_left_panels(kind, alpha, A, B, slot)
+
+
+def _tri_left_panels(kind, alpha, A, B, slot):
+    """Stationary-B Left trmm / trsm (src/work/work_trmm.cc,
+    src/work/work_trsm.cc:102-265) with A and B tile-row aligned.  Step k:
+    the block column A(:, k) goes along each process row (one row
+    broadcast of the local rows), the block row X(k, :) down each process
+    column (one column broadcast), then ONE GEMM updates this rank's rows
+    on the triangle's side of k -- the updates touch only the stored
+    triangle, so trmm costs the triangular flop count (m^2 n), not a dense
+    product.  trsm solves tile row k on its owners first (forward for
+    Lower); trmm runs the other way (backward for Lower) so that X(k, :) is
+    still the input row when it is read, and applies A(k, k) last."""
     sB = B.storage
-    bcB = sB.bc
-    comm = sB.comm
+    bc = sB.bc
     grid = grid_of(B)
+    lbA = A.local_block(slot)
     lbB = B.local_block(slot)
     dev = lbB.data.device
-    nb, p, q, pr, pc = bcB.nb, bcB.p, bcB.q, bcB.pr, bcB.pc
-    lower = A.uploLogical() == Uplo.Lower
-    diag = A.diag().value
-    opA = A.op()
-    upl = A.uploPhysical().value if hasattr(A.uploPhysical(), "value") else 'L'
+    dt = sB.dtype
+    nb, p, q, pr, pc = bc.nb, bc.p, bc.q, bc.pr, bc.pc
+    mloc, nloc = lbB.mloc, lbB.nloc
+    lower = A.uplo() == Uplo.Lower
+    upl, diag = ('L' if lower else 'U'), A.diag().value
+    solve = kind == "sm"
     mt = B.mt()
-    rB0, _ = B.global_offsets()
-    if rB0 % nb:
-        raise SlateError("trsm: B must start on a tile boundary")
-    gb0 = rB0 // nb
-    if alpha != 1 and lbB.mloc and lbB.nloc:
+    if solve and alpha != 1 and mloc and nloc:
         ops.gescale(alpha, lbB.data)
-    order = range(mt) if lower else range(mt - 1, -1, -1)
-    sA = A.storage
-
-    def stored_key(i, k):
-        return A._global_ij(i, k)
-
-    def owner(key):
-        return sA.tileRank(key)
-
-    def get_tile(key):
-        return sA.tile_data(key[0], key[1], sA.origin_slot)
-
-    def shape(key):
-        return sA.tileMb(key[0]), sA.tileNb(key[1])
-
-    procrow_ranks = {}
-    for r in range(comm.size):
-        procrow_ranks.setdefault(grid.coords(r)[0], []).append(r)
-    for k in order:
-        gk = gb0 + k
+    forward = lower if solve else not lower
+    for k in (range(mt) if forward else range(mt - 1, -1, -1)):
         kb = B.tileMb(k)
-        rows = list(range(k + 1, mt)) if lower else list(range(0, k))
-        needs = {}
-        for rp in range(p):
-            ks = [stored_key(k, k)] if (gk % p) == rp else []
-            ks += [stored_key(i, k) for i in rows if ((gb0 + i) % p) == rp]
-            for r in procrow_ranks.get(rp, []):
-                needs[r] = ks
-        got = exchange_tiles(comm, needs, owner, get_tile, shape, sB.dtype, dev)
-        Xk = ops.colmajor_empty(kb, lbB.nloc, sB.dtype, dev)
-        if (gk % p) == pr and lbB.nloc:
-            lr = tiles_local_before(gk, p, pr) * nb - lbB.row_off
-            Bk = lbB.data[lr:lr + kb, :]
-            ops.trsm('L', upl, opA.value, diag, 1.0, got[stored_key(k, k)], Bk)
-            Xk.copy_(Bk)
-        if lbB.nloc and p > 1:
-            grid.col_comm.bcast(Xk, gk % p)
-        my_rows = [i for i in rows if ((gb0 + i) % p) == pr]
-        if my_rows and lbB.nloc:
-            # my updated rows are one contiguous local range of B
-            lr0 = tiles_local_before(gb0 + my_rows[0], p, pr) * nb - lbB.row_off
-            tot = sum(B.tileMb(i) for i in my_rows)
-            Lm = ops.colmajor_empty(tot, kb, sB.dtype, dev)
-            off = 0
-            for i in my_rows:
-                mi = B.tileMb(i)
-                ops.gecopy(got[stored_key(i, k)], Lm[off:off + mi], trans=opA.value)
-                off += mi
-            ops.gemm(-1.0, Lm, Xk, 1.0, lbB.data[lr0:lr0 + tot, :])
+        lrk = tiles_local_before(k, p, pr) * nb
+        own = k % p == pr
+        lc = tiles_local_before(k, q, pc) * nb - lbA.col_off
+        src = lbA.data[:, lc:lc + kb] if k % q == pc else None
+        Prow = row_bcast(grid, src, k % q, mloc, kb, dt, dev)
+        r0, r1 = (tiles_local_before(k + 1, p, pr) * nb, mloc) if lower else (0, lrk)
+        Bk = lbB.data[lrk:lrk + kb, :] if own else None
+        if solve:
+            if own and nloc:
+                ops.trsm('L', upl, 'N', diag, 1.0, Prow[lrk:lrk + kb], Bk)
+            Xk = col_bcast(grid, Bk, k % p, kb, nloc, dt, dev)
+            if r1 > r0 and nloc:
+                ops.gemm(-1.0, Prow[r0:r1], Xk, 1.0, lbB.data[r0:r1])
+        else:
+            Xk = col_bcast(grid, Bk, k % p, kb, nloc, dt, dev)
+            if r1 > r0 and nloc:
+                ops.gemm(alpha, Prow[r0:r1], Xk, 1.0, lbB.data[r0:r1])
+            if own and nloc:
+                ops.trmm('L', upl, 'N', diag, alpha, Prow[lrk:lrk + kb], Bk)
+    _done(B)
+    return B
+
+
+def _local_globals(nloc, nb, p, pr, n):
+    """Global indices of the nloc local rows of process row pr (numpy)."""
+    import numpy as np
+    from ._panels import _ranges
+    tiles = np.arange(pr, (n + nb - 1) // nb, p, dtype=np.int64)
+    lens = np.minimum(nb, n - tiles * nb)
+    return _ranges(tiles * nb, lens)[:nloc]
+
+
+def _trsmA_left(alpha, A, B, slot):
+    """Stationary-A Left trsm (src/work/work_trsmA.cc): A never moves.  The
+    update A(i, k) X(k) runs on the owner of A(i, k) and accumulates into a
+    per-rank partial sum W of its local rows; before tile row k is solved,
+    the partial sums of that row are reduced over the process row onto the
+    owner of A(k, k) together with alpha B(k, :), which solves and
+    broadcasts X(k, :) back along its process row (to B's owners) and down
+    its process column (to the owners of A(:, k)).  Used when B is skinny
+    (one block column), where stationary B would leave all but one process
+    column idle."""
+    sB = B.storage
+    bc = sB.bc
+    grid = grid_of(B)
+    lbA = A.local_block(slot)
+    lbB = B.local_block(slot)
+    dev = lbB.data.device
+    dt = sB.dtype
+    nb, p, q, pr, pc = bc.nb, bc.p, bc.q, bc.pr, bc.pc
+    mloc, nloc = lbB.mloc, lbB.nloc
+    n = B.n()
+    lower = A.uplo() == Uplo.Lower
+    upl, diag = ('L' if lower else 'U'), A.diag().value
+    mt = B.mt()
+    gcols = torch.from_numpy(_local_globals(nloc, nb, q, pc, n)).to(dev)
+    W = ops.colmajor_zeros(mloc, n, dt, dev)
+    for k in (range(mt) if lower else range(mt - 1, -1, -1)):
+        kb = B.tileMb(k)
+        lrk = tiles_local_before(k, p, pr) * nb
+        dq = k % q
+        if k % p == pr:
+            S = ops.colmajor_zeros(kb, n, dt, dev)
+            if nloc:
+                S.index_copy_(1, gcols, lbB.data[lrk:lrk + kb, :])
+                if alpha != 1:
+                    ops.gescale(alpha, S)
+            S -= W[lrk:lrk + kb]
+            if q > 1:
+                grid.row_comm.reduce(S, dq)
+            if pc == dq:
+                lc = tiles_local_before(k, q, pc) * nb - lbA.col_off
+                ops.trsm('L', upl, 'N', diag, 1.0, lbA.data[lrk:lrk + kb, lc:lc + kb], S)
+            if q > 1:
+                grid.row_comm.bcast(S, dq)
+            if nloc:
+                lbB.data[lrk:lrk + kb, :].copy_(S.index_select(1, gcols))
+            Xk = S
+        else:
+            Xk = ops.colmajor_empty(kb, n, dt, dev) if pc == dq else None
+        if pc == dq:
+            if p > 1:
+                grid.col_comm.bcast(Xk, k % p)
+            r0, r1 = (tiles_local_before(k + 1, p, pr) * nb, mloc) if lower else (0, lrk)
+            if r1 > r0:
+                lc = tiles_local_before(k, q, pc) * nb - lbA.col_off
+                ops.gemm(1.0, lbA.data[r0:r1, lc:lc + kb], Xk, 1.0, W[r0:r1])
     _done(B)
     return B
 

@@ -21,6 +21,24 @@ from .._native import code, kmod, stream
 from ..core.exceptions import SlateError
 
 _WORK = {}
+_FLOPS = None     # [count] while a flop_counter() is active
+
+
+class flop_counter:
+    """Count the multiply-add flops the BLAS-3 ops of this process issue
+    (2 m n k per GEMM, m^2 n per triangular multiply / solve), e.g. to check
+    that a distributed trmm does the triangular, not the dense, count."""
+
+    def __enter__(self):
+        global _FLOPS
+        self._prev, _FLOPS = _FLOPS, [0]
+        return self
+
+    def __exit__(self, *exc):
+        global _FLOPS
+        self.flops = _FLOPS[0]
+        _FLOPS = self._prev
+        return False
 
 
 def _chk(t: torch.Tensor, name="A"):
@@ -72,6 +90,8 @@ def gemm(alpha, A, B, beta, C, transA='N', transB='N', mask=None, batch=1, strid
             gescale(beta, C)
         return C
     _chk(A, "A"); _chk(B, "B")
+    if _FLOPS is not None:
+        _FLOPS[0] += 2 * m * n * k * max(1, batch)
     kmod(C).gemm(code(C.dtype), ta, tb, m, n, k, _c(alpha), A.data_ptr(), ld(A), B.data_ptr(), ld(B),
                  _c(beta), C.data_ptr(), ld(C), batch, strides[0], strides[1], strides[2], mask, stream(C))
     return C
@@ -122,6 +142,8 @@ def trsm(side, uplo, trans, diag, alpha, A, B):
     m, n = B.shape
     if m == 0 or n == 0:
         return B
+    if _FLOPS is not None:
+        _FLOPS[0] += (m * m * n) if _ch(side) == 'L' else (m * n * n)
     kmod(B).trsm(code(B.dtype), _ch(side), _ch(uplo), _ch(trans), _ch(diag), m, n, _c(alpha),
                  A.data_ptr(), ld(A), B.data_ptr(), ld(B), stream(B))
     return B
@@ -132,6 +154,8 @@ def trmm(side, uplo, trans, diag, alpha, A, B):
     m, n = B.shape
     if m == 0 or n == 0:
         return B
+    if _FLOPS is not None:
+        _FLOPS[0] += (m * m * n) if _ch(side) == 'L' else (m * n * n)
     kmod(B).trmm(code(B.dtype), _ch(side), _ch(uplo), _ch(trans), _ch(diag), m, n, _c(alpha),
                  A.data_ptr(), ld(A), B.data_ptr(), ld(B), stream(B))
     return B

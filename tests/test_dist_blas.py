@@ -12,7 +12,7 @@ import pytest
 import torch
 
 import slate_amd as sl
-from slate_amd.core.enums import Diag, MethodGemm, Op, Option, Side, Uplo
+from slate_amd.core.enums import Diag, MethodGemm, MethodHemm, MethodTrsm, Op, Option, Side, Uplo
 from slate_amd.models.aux import allgather_dense as D
 
 from dist_util import run_dist
@@ -221,8 +221,55 @@ def check_trmm_trsm(p, q, dt=torch.float64):
                     close(Tl @ X if side == Side.Left else X @ Tl, 0.5 * Bd, 1e-10)
 
 
+def check_methods_and_trmm_flops(p, q, dt=torch.float64):
+    """trsmA and trsmB (work_trsmA.cc / work_trsm.cc), hemmA and hemmC
+    agree with the fp64 oracle on skinny and wide right-hand sides, and the
+    distributed trmm multiplies only the stored triangle: the GEMM + TRMM
+    flops summed over all ranks equal m^2 n exactly (a dense product would
+    be 2 m^2 n)."""
+    import torch.distributed as dist
+    from slate_amd import ops
+    n = 64
+    T = mat(n, n, 16, 30, p, q, dt)
+    Td = D(T) + 8.0 * torch.eye(n, dtype=dt)
+    sl.from_dense(T, Td)
+    for uplo in (Uplo.Lower, Uplo.Upper):
+        Tl = tri(Td, uplo)
+        for nrhs in (9, 40):
+            for meth in (MethodTrsm.A, MethodTrsm.B):
+                for side in (Side.Left, Side.Right):
+                    B = mat(n, nrhs, 16, 31, p, q, dt) if side == Side.Left else mat(nrhs, n, 16, 31, p, q, dt)
+                    Bd = D(B)
+                    sl.trsm(side, 0.5, sl.TriangularMatrix(uplo, T), B, {Option.MethodTrsm: meth})
+                    X = D(B)
+                    close(Tl @ X if side == Side.Left else X @ Tl, 0.5 * Bd, 1e-10)
+        nrhs = 24
+        B = mat(n, nrhs, 16, 32, p, q, dt)
+        Bd = D(B)
+        with ops.flop_counter() as fc:
+            sl.trmm(Side.Left, 1.0, sl.TriangularMatrix(uplo, T), B)
+        tot = torch.tensor([fc.flops], dtype=torch.int64)
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            dist.all_reduce(tot)
+        assert int(tot) == n * n * nrhs, (int(tot), n * n * nrhs)
+        close(D(B), Tl @ Bd)
+    for meth in (MethodHemm.A, MethodHemm.C):
+        for side in (Side.Left, Side.Right):
+            for uplo in (Uplo.Lower, Uplo.Upper):
+                for sym in (False, True):
+                    cls = sl.SymmetricMatrix if sym else sl.HermitianMatrix
+                    A = herm(48, 16, 33, p, q, dt, uplo, cls)
+                    Afull = full(D(sl.Matrix(_storage=A.storage)), uplo, not sym)
+                    for w in (11, 40):
+                        B = mat(48, w, 16, 34, p, q, dt) if side == Side.Left else mat(w, 48, 16, 34, p, q, dt)
+                        C = mat(B.m(), B.n(), 16, 35, p, q, dt)
+                        Bd, Cd = D(B), D(C)
+                        (sl.symm if sym else sl.hemm)(side, 1.5, A, B, 0.5, C, {Option.MethodHemm: meth})
+                        close(D(C), 1.5 * (Afull @ Bd if side == Side.Left else Bd @ Afull) + 0.5 * Cd)
+
+
 ALL = [check_redistribute, check_conj_transpose_keeps_other_triangle, check_potrf_upper_keeps_lower,
-       check_gemm_all, check_gemmA, check_rank_k, check_hemm, check_trmm_trsm]
+       check_gemm_all, check_gemmA, check_rank_k, check_hemm, check_trmm_trsm, check_methods_and_trmm_flops]
 
 
 def _run(rank, size, p, q, names, complex_too):
