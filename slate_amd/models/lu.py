@@ -23,6 +23,7 @@ Pivots: `Pivots` holds 0-based GLOBAL pivot rows (LAPACK ipiv - 1).
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from .. import ops
@@ -276,11 +277,20 @@ def _getrf_general(A, buf, thr, la, mode, leaf):
       update stream (low priority, own column communicator):
         rest of the trailing columns, then the left (already factored)
         columns' row exchange.
-    The row exchange is swap-plan driven: each rank packs the touched rows it
-    owns, one all-reduce over the column, each rank writes its new rows; the
-    reduced window rows ARE the tile row k each rank needs for the update
-    (SLATE: internal::permuteRows + tileBcast of the U row, getrf.cc:160-210).
-    Nothing inside the loop reads device memory from the host."""
+    Row exchange, two forms:
+      * lookahead columns (the critical path): swap-plan driven on the
+        device -- each rank packs the touched rows it owns, one all-reduce
+        over the column (2kb rows x (la+1) tiles), each rank writes its new
+        rows; the reduced window rows ARE the U row the update needs;
+      * bulk trailing columns (off the critical path) and the left
+        (factored) columns: an exact point-to-point exchange of only the
+        rows that change process row (_p2p_rows), the U row then goes down
+        the column in one broadcast (SLATE internal::permuteRows +
+        tileBcast, getrf.cc:155-215).  Its plan needs the pivots on the
+        host: they travel through a pinned buffer and are read one step
+        late, when the panel that produced them has finished, so the host
+        never waits on the critical path.  The left columns' interchanges
+        are applied once, after the loop, in step order."""
     s = A.storage
     bc = s.bc
     grid = grid_of(A)
@@ -301,9 +311,17 @@ def _getrf_general(A, buf, thr, la, mode, leaf):
     ctx = dict(buf=buf, nb=nb, p=p, pr=pr, mloc=mloc, dt=dt, dev=dev, colc=colc, thr=thr, infos=infos,
                nloc_r=nloc_r, leaf=leaf, m=m)
     ev_tr = {}
+    # pivots reach the host through one pinned buffer (non-blocking copy on
+    # the panel stream + an event), read one step late, when the bulk of the
+    # previous step's trailing update is issued -- by then the panel that
+    # produced them has long finished, so the host does not stall the GPU
+    pin = torch.empty(ipiv.numel(), dtype=torch.int64, pin_memory=buf.is_cuda)
+    piv_ev, moves, pend = {}, {}, None
+    XCHG_STATS.clear()
     ss.fork()
     import os
     kstop = int(os.environ.get("SLATE_AMD_DEBUG_LU_STEPS", kt))    # debugging: stop after k steps
+    us = ss.update[0]
     for k in range(min(kt, kstop)):
         _wd.beat(f"getrf step {k}")
         r0 = k * nb
@@ -332,10 +350,14 @@ def _getrf_general(A, buf, thr, la, mode, leaf):
                 if q > 1:
                     rowc.bcast(pk.raw, ck)
                 piv.copy_(pv)
+                if mode != "nopiv":
+                    pin[r0:r0 + kb].copy_(piv, non_blocking=True)
+                    piv_ev[k] = ss.event(ss.panel)
                 plan = ops.swap_plan(ipiv, r0, r0 + kb, ioff=-r0)
             Lkk = Lp[nmine:nmine + kb]
             Lbelow = Lp[lr1 - lr_k:nmine]
-            upd = dict(plan=plan, nslot=nslot, kb=kb, Lkk=Lkk, Lbelow=Lbelow, rk=rk, lr_k=lr_k, lr1=lr1)
+            upd = dict(plan=plan, nslot=nslot, kb=kb, Lkk=Lkk, Lbelow=Lbelow, rk=rk, lr_k=lr_k, lr1=lr1, k=k,
+                       r0=r0, pk=pk)
             # newest lookahead column k+la: first part of step k-1's trailing update
             if k >= 1 and la > 0:
                 ss.wait(ss.panel, ev_tr[k - 1])
@@ -345,17 +367,32 @@ def _getrf_general(A, buf, thr, la, mode, leaf):
             part = [(lc_k + kb, lc_k + wk)] if (pc == ck and kb < wk) else []
             _xchg_update(ctx, upd, part + [(lc1, lcla)], [], colc)
             ev_panel = ss.event(ss.panel)
-        us = ss.update[0]
         with ss.use(us):
             ss.wait(us, ev_panel)
             if buf.is_cuda:
                 pk.raw.record_stream(us)
                 plan.record_stream(us)
             with trace_block("getrf::trailing"):
+                # the bulk of step k-1 (exact point-to-point row exchange)
+                # must precede step k's first trailing column, which was part
+                # of it
+                if pend is not None:
+                    _bulk_update(ctx, pend, mode, pin, piv_ev, moves, colu)
                 _xchg_update(ctx, upd, [(lcla, lcnx)], [], colu)
                 ev_tr[k] = ss.event(us)
-                left = [(0, lc_k)] if mode != "nopiv" else []
-                _xchg_update(ctx, upd, [(lcnx, nloc)], left, colu)
+            upd["c0"], upd["c1"] = lcnx, nloc
+            pend = upd
+    with ss.use(us):
+        if pend is not None:
+            _bulk_update(ctx, pend, mode, pin, piv_ev, moves, colu)
+        # left (already factored) columns: the interchanges of every later
+        # step, applied once at the end in step order (SLATE's separate
+        # left-pivot task), by the same exact exchange
+        if mode != "nopiv":
+            for k in range(min(kt, kstop)):
+                lc_k = min(tiles_local_before(k, q, pc) * nb, nloc)
+                _p2p_rows(ctx, _moves_of(k, pin, piv_ev, moves, nb, min(nb, n - k * nb, m - k * nb)),
+                          0, lc_k, colu, k, "left")
     ss.join()
     if mode == "nopiv":
         glob = torch.arange(min(m, n), dtype=torch.int64, device=dev)
@@ -363,6 +400,122 @@ def _getrf_general(A, buf, thr, la, mode, leaf):
         glob = _global_pivots(ipiv[:min(m, n)], nb)
     info = _reduce_info(A, infos, kt, nb)
     return info, glob
+
+
+# per-step record of the point-to-point row exchanges of the last p > 1
+# getrf on this rank: {"step", "part", "rows_cross", "bytes_sent", "ncols"}
+XCHG_STATS = []
+
+
+def _moves_of(k, pin, piv_ev, moves, nb, kb):
+    """Row moves of step k as (dst, src) global rows, dst sorted: new row dst
+    holds old row src.  The pivots are read from the pinned host copy once
+    the panel's event has completed."""
+    mv = moves.get(k)
+    if mv is None:
+        if piv_ev.get(k) is not None:
+            piv_ev[k].synchronize()
+        r0 = k * nb
+        pv = pin[r0:r0 + kb].numpy()
+        cur = {}
+        for i in range(kb):
+            a, b = r0 + i, r0 + int(pv[i])
+            if a != b:
+                ca, cb = cur.get(a, a), cur.get(b, b)
+                cur[a], cur[b] = cb, ca
+        mv = sorted((d, s_) for d, s_ in cur.items() if d != s_)
+        moves[k] = mv
+    return mv
+
+
+def _p2p_rows(ctx, mv, c0, c1, comm, k, part):
+    """Apply the row moves ``mv`` to local columns [c0, c1): rows that stay
+    inside this process row move locally, rows that change process row go
+    point-to-point (one batched send/recv per peer, rows in dst order on
+    both sides) -- only the rows that actually change owner travel
+    (internal::permuteRows, src/internal/internal_swap.cc)."""
+    w = c1 - c0
+    if w <= 0 or not mv:
+        return
+    buf, nb, p, pr, mloc, dt, dev = (ctx[x] for x in ("buf", "nb", "p", "pr", "mloc", "dt", "dev"))
+
+    def own(g):
+        return (g // nb) % p
+
+    def loc(g):
+        return (g // (nb * p)) * nb + g % nb
+
+    sends, recvs, ld_, ls_ = {}, {}, [], []
+    cross = 0
+    for d, s_ in mv:
+        od, os_ = own(d), own(s_)
+        cross += od != os_
+        if os_ == pr and od != pr:
+            sends.setdefault(od, []).append(loc(s_))
+        elif od == pr and os_ != pr:
+            recvs.setdefault(os_, []).append(loc(d))
+        elif od == pr and os_ == pr:
+            ld_.append(loc(d))
+            ls_.append(loc(s_))
+    peers_s, peers_r = sorted(sends), sorted(recvs)
+    parts = [sends[r] for r in peers_s] + [recvs[r] for r in peers_r] + [ls_, ld_]
+    flat = np.concatenate([np.asarray(x, dtype=np.int64) for x in parts]) if parts else np.zeros(0, np.int64)
+    nbytes = 0
+    if flat.size:
+        idx = torch.from_numpy(flat)
+        if buf.is_cuda:
+            idx = idx.pin_memory().to(dev, non_blocking=True)
+        block = buf[:mloc, c0:c1]
+        off, sb, rb = 0, {}, {}
+        es = torch.empty(0, dtype=dt).element_size()
+        for r in peers_s:
+            c = len(sends[r])
+            t = torch.empty(w, c, dtype=dt, device=dev)           # (w, c) = column-major c x w
+            ops.row_gather(block, t.t(), idx[off:off + c])
+            sb[r] = t
+            off += c
+            nbytes += c * w * es
+        rofs = {}
+        for r in peers_r:
+            c = len(recvs[r])
+            rb[r] = torch.empty(w, c, dtype=dt, device=dev)
+            rofs[r] = (off, c)
+            off += c
+        nl = len(ls_)
+        if nl:
+            tmp = ops.colmajor_empty(nl, w, dt, dev)
+            ops.row_gather(block, tmp, idx[off:off + nl])
+        if sb or rb:
+            comm.exchange(sb, rb)
+        for r in peers_r:
+            o, c = rofs[r]
+            ops.row_scatter(rb[r].t(), block, idx[o:o + c])
+        if nl:
+            ops.row_scatter(tmp, block, idx[off + nl:off + 2 * nl])
+    XCHG_STATS.append(dict(step=k, part=part, rows_cross=cross, bytes_sent=nbytes, ncols=w))
+
+
+def _bulk_update(ctx, upd, mode, pin, piv_ev, moves, comm):
+    """Trailing update of local columns [c0, c1) for step upd["k"]: exact row
+    exchange, U row = L_kk^{-1} (window rows) on the window's process row,
+    broadcast down the column, one GEMM."""
+    c0, c1 = upd["c0"], upd["c1"]
+    if c1 <= c0:
+        return
+    buf, nb, p, pr, mloc, dt, dev = (ctx[x] for x in ("buf", "nb", "p", "pr", "mloc", "dt", "dev"))
+    k, kb, rk, lr_k, lr1 = upd["k"], upd["kb"], upd["rk"], upd["lr_k"], upd["lr1"]
+    if mode != "nopiv":
+        _p2p_rows(ctx, _moves_of(k, pin, piv_ev, moves, nb, kb), c0, c1, comm, k, "bulk")
+    W = buf[lr_k:lr_k + kb, c0:c1] if pr == rk else None
+    if W is not None:
+        ops.trsm('L', 'L', 'N', 'U', 1.0, upd["Lkk"], W)
+    U = ops.colmajor_empty(kb, c1 - c0, dt, dev)
+    if W is not None:
+        U.copy_(W)
+    comm.bcast(U, rk)
+    Lb = upd["Lbelow"]
+    if Lb.shape[0]:
+        ops.gemm(-1.0, Lb, U, 1.0, buf[lr1:mloc, c0:c1])
 
 
 def _xchg_update(ctx, upd, ranges, swap_only, comm):

@@ -139,6 +139,18 @@ def check_lu_methods(p, q, dt=torch.float64):
         Ad = D(A)
         piv = sl.Pivots()
         assert sl.getrf(A, piv, {Option.Lookahead: la}) == 0
+        if p > 1:
+            # exact point-to-point row exchange: per step,
+            # the bytes this rank sends are at most (rows that change
+            # process row) x (local columns) x element size
+            from slate_amd.models import lu as _lu
+            es = torch.empty(0, dtype=dt).element_size()
+            for rec in _lu.XCHG_STATS:
+                assert rec["bytes_sent"] <= rec["rows_cross"] * A.storage.bc.nloc * es, rec
+            import torch.distributed as dist
+            cnt = torch.tensor([len(_lu.XCHG_STATS)])
+            dist.all_reduce(cnt)
+            assert int(cnt) > 0
         L = _lu_check(Ad, D(A), piv, m, n, dt)
         assert L.abs().max().item() <= 1.0 + 1e-12          # partial pivoting: |L| <= 1
     # CALU with small leaves (several play-off rounds per rank)
