@@ -263,7 +263,11 @@ laswp_apply_kernel(i64 n, T* A, i64 lda, const SwapPlan* __restrict__ plan, int 
     if (nt == 0) return;
     const i64 c0 = (i64)blockIdx.x * CCH;
     const int ncols = (int)min((i64)CCH, n - c0);
-    const int LD = CCH + 1;               // odd row pitch: t-consecutive lanes hit distinct banks
+    // odd row pitch (in doubles): t-consecutive lanes then step an odd
+    // number of 2-bank words, i.e. hit distinct banks.  (CCH + 1 was even
+    // for the 7-column chunks of 512-swap plans: a 16-way conflict, 87 % of
+    // LDS cycles in the round-2 PMC of laswp_apply_kernel.)
+    const int LD = CCH | 1;
     // gather: buf[t][c] = A[tsrc[t], c0 + c]   (t fastest: the touched rows
     // of one column; the row lists are read from L2, not rebuilt)
     for (int idx = threadIdx.x; idx < nt * CCH; idx += blockDim.x) {

@@ -123,6 +123,22 @@ static void register_kernels(py::module& m) {
                               uintptr_t zh, uintptr_t V, i64 ldv, uintptr_t st) {
         stedc_secular(n, P<double>(d), P<double>(z), rho, zz, P<i64>(org), P<double>(mu), P<double>(zh),
                       P<double>(V), ldv, S(st)); });
+    m.def("steqr_leaves", [](i64 nleaf, uintptr_t lo, uintptr_t hi, uintptr_t d, uintptr_t e, uintptr_t w,
+                             uintptr_t Q, i64 ldq, i64 r0, i64 r1, uintptr_t fails, uintptr_t st) {
+        steqr_leaves(nleaf, P<const i64>(lo), P<const i64>(hi), P<const double>(d), P<const double>(e), P<double>(w),
+                     P<double>(Q), ldq, r0, r1, P<i64>(fails), S(st)); });
+    m.def("stedc_runs", [](i64 nn, uintptr_t c, uintptr_t dd, uintptr_t z, uintptr_t ty, double tol, uintptr_t cs,
+                           uintptr_t sn, uintptr_t rot, uintptr_t keep, uintptr_t st) {
+        stedc_runs(nn, P<const i64>(c), P<const double>(dd), P<double>(z), P<int>(ty), tol, P<double>(cs),
+                   P<double>(sn), P<int>(rot), P<int>(keep), S(st)); });
+    m.def("rot_cols", [](i64 m_, uintptr_t Q, i64 ldq, i64 nrot, uintptr_t I, uintptr_t J, uintptr_t C, uintptr_t Sn,
+                         uintptr_t st) {
+        rot_cols(m_, P<double>(Q), ldq, nrot, P<const i64>(I), P<const i64>(J), P<const double>(C),
+                 P<const double>(Sn), S(st)); });
+    m.def("stedc_vectors", [](i64 n, uintptr_t d, uintptr_t zh, uintptr_t org, uintptr_t mu, i64 j0, i64 nc,
+                              uintptr_t V, i64 ldv, uintptr_t st) {
+        stedc_vectors(n, P<const double>(d), P<const double>(zh), P<const i64>(org), P<const double>(mu), j0, nc,
+                      P<double>(V), ldv, S(st)); });
     m.def("lu_persist_profile", [](int enable) {
         unsigned long long v[8];
         lu_persist_profile(enable, v);

@@ -293,4 +293,193 @@ void stedc_secular(i64 n, const double* d, const double* z, double rho, double z
     }
 }
 
+// ---------------------------------------------------------------------------
+// Leaves of the divide & conquer tree, all in ONE launch: one wave per leaf
+// (n_leaf <= 64), implicit-shift QL with Wilkinson shifts (the host steqr's
+// iteration).  The scalar recurrence (d, e in LDS) is computed redundantly
+// and identically by the 64 lanes; lane r owns row r of the leaf's
+// eigenvector matrix (LDS, column-major, pitch 64) and applies every Givens
+// rotation to it as it is generated.  Eigenvalues ascending with their
+// columns.  Only the rows in [r0, r1) (this rank's rows) are written, to
+// Q(row - r0, col) with ld ldq; w gets the eigenvalues at the leaf's global
+// positions.  (The host solved one leaf after another: 256 leaves of 64 at
+// n = 16384.)
+constexpr int LEAF = 64;
+
+__global__ void __launch_bounds__(64)
+steqr_leaf_kernel(const i64* __restrict__ lo, const i64* __restrict__ hi, const double* __restrict__ d_in,
+                  const double* __restrict__ e_in, double* __restrict__ w, double* __restrict__ Q, i64 ldq, i64 r0,
+                  i64 r1, i64* fails) {
+    __shared__ double Z[LEAF * LEAF];
+    __shared__ double d[LEAF], ew[LEAF];
+    const int lane = threadIdx.x;
+    const i64 a = lo[blockIdx.x];
+    const int n = (int)(hi[blockIdx.x] - a);
+    if (lane < n) {
+        d[lane] = d_in[a + lane];
+        ew[lane] = lane < n - 1 ? e_in[a + lane] : 0.0;
+    }
+    for (int c = 0; c < n; ++c) Z[c * LEAF + lane] = (lane == c) ? 1.0 : 0.0;
+    __syncthreads();
+    const double eps = 2.220446049250313e-16, tiny = 2.2250738585072014e-308;
+    int nfail = 0;
+    for (int l = 0; l < n; ++l) {
+        int iter = 0;
+        while (true) {
+            int m = l;
+            for (; m < n - 1; ++m) {
+                const double dd = fabs(d[m]) + fabs(d[m + 1]);
+                if (fabs(ew[m]) <= eps * dd || fabs(ew[m]) < tiny) break;
+            }
+            if (m == l) break;
+            if (++iter > 60) { ++nfail; break; }
+            double g = (d[l + 1] - d[l]) / (2.0 * ew[l]);
+            double r = hypot(g, 1.0);
+            g = d[m] - d[l] + ew[l] / (g + copysign(r, g));
+            double s = 1.0, c = 1.0, p = 0.0;
+            bool early = false;
+            int i;
+            for (i = m - 1; i >= l; --i) {
+                const double f = s * ew[i], bb = c * ew[i];
+                r = hypot(f, g);
+                __syncthreads();                       // every lane has read ew[i] / d[]
+                if (lane == 0) ew[i + 1] = r;
+                if (r == 0.0) {
+                    if (lane == 0) { d[i + 1] -= p; ew[m] = 0.0; }
+                    __syncthreads();
+                    early = true;
+                    break;
+                }
+                s = f / r; c = g / r;
+                g = d[i + 1] - p;
+                r = (d[i] - g) * s + 2.0 * c * bb;
+                p = s * r;
+                __syncthreads();
+                if (lane == 0) d[i + 1] = g + p;
+                g = c * r - bb;
+                // rotation on columns (i, i+1) of this lane's row
+                if (lane < n) {
+                    const double zi = Z[i * LEAF + lane], zj = Z[(i + 1) * LEAF + lane];
+                    Z[(i + 1) * LEAF + lane] = s * zi + c * zj;
+                    Z[i * LEAF + lane] = c * zi - s * zj;
+                }
+                __syncthreads();
+            }
+            if (early && i >= l) continue;
+            __syncthreads();
+            if (lane == 0) { d[l] -= p; ew[l] = g; ew[m] = 0.0; }
+            __syncthreads();
+        }
+    }
+    // ascending order (selection sort, columns swapped row-wise by each lane)
+    for (int i = 0; i < n - 1; ++i) {
+        int k = i;
+        for (int j = i + 1; j < n; ++j) if (d[j] < d[k]) k = j;
+        __syncthreads();
+        if (k != i) {
+            if (lane == 0) { const double t = d[i]; d[i] = d[k]; d[k] = t; }
+            if (lane < n) {
+                const double t = Z[i * LEAF + lane];
+                Z[i * LEAF + lane] = Z[k * LEAF + lane];
+                Z[k * LEAF + lane] = t;
+            }
+        }
+        __syncthreads();
+    }
+    if (lane < n) w[a + lane] = d[lane];
+    const i64 row = a + lane;
+    if (lane < n && row >= r0 && row < r1)
+        for (int c = 0; c < n; ++c) Q[(row - r0) + (a + c) * ldq] = Z[c * LEAF + lane];
+    if (lane == 0 && nfail) atomicAdd(reinterpret_cast<unsigned long long*>(fails), (unsigned long long)nfail);
+}
+
+// Deflation of close poles (Gu-Eisenstat / LAPACK laed2), all runs at once:
+// in ascending pole order, a non-deflated pole within tol of the previous
+// non-deflated one is rotated into it -- its z weight moves to the later
+// pole, the earlier one deflates.  A run of such poles is a sequential chain
+// (each rotation uses the accumulated weight); runs are independent, so one
+// thread walks each run.  start[t] marks run heads among the nn compacted
+// non-deflated positions c[]; for the rotation that pairs c[t-1] with c[t]
+// the kernel writes (cs[t], sn[t]) and marks rot[t] = 1; z is updated in
+// place and the type bitmask of the surviving column accumulates (bit 0:
+// rows of the top half, bit 1: bottom half -- a rotation mixing the halves
+// makes the column dense in both, which the split merge GEMM must know).
+__global__ void __launch_bounds__(256)
+stedc_runs_kernel(i64 nn, const i64* __restrict__ c, const double* __restrict__ dd, double* __restrict__ z,
+                  int* __restrict__ ty, double tol, double* __restrict__ cs, double* __restrict__ sn,
+                  int* __restrict__ rot, int* __restrict__ keep) {
+    const i64 t = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (t >= nn) return;
+    const bool head = t == 0 || !(dd[c[t]] - dd[c[t - 1]] <= tol);
+    rot[t] = 0;
+    if (!head) return;
+    double acc = z[c[t]];
+    int tacc = ty[c[t]];
+    i64 u = t + 1;
+    while (u < nn && dd[c[u]] - dd[c[u - 1]] <= tol) {
+        const double b = z[c[u]];
+        const double r = hypot(acc, b);
+        const double cc = r == 0.0 ? 1.0 : b / r, ss = r == 0.0 ? 0.0 : acc / r;
+        cs[u] = cc; sn[u] = ss; rot[u] = 1;
+        z[c[u - 1]] = 0.0;
+        z[c[u]] = r;
+        tacc |= ty[c[u]];
+        ty[c[u]] = tacc;
+        keep[u - 1] = 0;
+        acc = r;
+        ++u;
+    }
+    keep[u - 1] = 1;
+}
+
+// Givens rotations on column pairs (I[t], J[t]) in order t = 0 .. nrot-1:
+// q_I' = c q_I - s q_J, q_J' = s q_I + c q_J, one thread per row.
+__global__ void __launch_bounds__(256)
+rot_cols_kernel(i64 m, double* __restrict__ Q, i64 ldq, i64 nrot, const i64* __restrict__ I,
+                const i64* __restrict__ J, const double* __restrict__ C, const double* __restrict__ S) {
+    const i64 r = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (r >= m) return;
+    for (i64 t = 0; t < nrot; ++t) {
+        double* qi = Q + r + I[t] * ldq;
+        double* qj = Q + r + J[t] * ldq;
+        const double a = *qi, b = *qj, c = C[t], s = S[t];
+        *qi = c * a - s * b;
+        *qj = s * a + c * b;
+    }
+}
+
+void steqr_leaves(i64 nleaf, const i64* lo, const i64* hi, const double* d, const double* e, double* w, double* Q,
+                  i64 ldq, i64 r0, i64 r1, i64* fails, hipStream_t s) {
+    if (nleaf <= 0) return;
+    hipLaunchKernelGGL(steqr_leaf_kernel, dim3((unsigned)nleaf), dim3(64), 0, s, lo, hi, d, e, w, Q, ldq, r0, r1,
+                       fails);
+    HIP_LAUNCH_CHECK();
+}
+
+void stedc_runs(i64 nn, const i64* c, const double* dd, double* z, int* ty, double tol, double* cs, double* sn,
+                int* rot, int* keep, hipStream_t s) {
+    if (nn <= 0) return;
+    hipLaunchKernelGGL(stedc_runs_kernel, dim3((unsigned)((nn + 255) / 256)), dim3(256), 0, s, nn, c, dd, z, ty, tol,
+                       cs, sn, rot, keep);
+    HIP_LAUNCH_CHECK();
+}
+
+void rot_cols(i64 m, double* Q, i64 ldq, i64 nrot, const i64* I, const i64* J, const double* C, const double* S,
+              hipStream_t s) {
+    if (m <= 0 || nrot <= 0) return;
+    hipLaunchKernelGGL(rot_cols_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, m, Q, ldq, nrot, I, J, C,
+                       S);
+    HIP_LAUNCH_CHECK();
+}
+
+// normalised rank-one eigenvector columns j0 .. j0+nc-1 (chunk of the merge
+// GEMM's right operand): V[i + (j - j0) ldv] = zh_i / (d_i - lambda_j) / norm
+void stedc_vectors(i64 n, const double* d, const double* zh, const i64* org, const double* mu, i64 j0, i64 nc,
+                   double* V, i64 ldv, hipStream_t s) {
+    if (n <= 0 || nc <= 0) return;
+    hipLaunchKernelGGL(secvec_kernel, dim3((unsigned)nc), dim3(256), 0, s, n, d, zh, org + j0, mu + j0, V, ldv);
+    HIP_LAUNCH_CHECK();
+}
+
+
 }  // namespace slate_hip

@@ -94,7 +94,10 @@ def _potrf_lower(A, opts):
     infos = torch.zeros(max(nt, 1), dtype=torch.int64, device=dev)
     group = int(os.environ.get("SLATE_AMD_POTRF_GROUP", "2"))
     if p == 1 and q == 1 and group > 1 and nt > 2:
-        _potrf_1x1_grouped(A, s, buf, nb, g0, nt, R_end, la, group, ss, infos, ct, dev)
+        if get_option(opts, Option.UseGraph, False) and buf.is_cuda:
+            infos = _potrf_graph_run(A, s, buf, nb, g0, nt, R_end, la, group, ss, ct, dev)
+        else:
+            _potrf_1x1_grouped(A, s, buf, nb, g0, nt, R_end, la, group, ss, infos, ct, dev)
         s.mark_local_modified(slot)
         return _potrf_info(s, infos, g0, nt)
     # per step: the lookahead tiles' transposed rows (critical path) and the
@@ -246,6 +249,35 @@ def _potrf_lower(A, opts):
     ss.join()
     s.mark_local_modified(slot)
     return _potrf_info(s, infos, g0, nt)
+
+
+_GRAPHS = {}
+
+
+def _potrf_graph_run(A, s, buf, nb, g0, nt, R_end, la, group, ss, ct, dev):
+    """Option.UseGraph: the one-rank potrf DAG (panel / diag / update
+    streams and their events) captured once into a hipGraph per (buffer,
+    geometry) and replayed -- one launch for the whole factorization, no
+    host work per kernel.  The capture runs on a side stream that forks into
+    the pipeline streams and joins them back; the info vector is zeroed
+    inside the graph and lives with it.  Replays read whatever A holds at
+    the time (same buffer)."""
+    key = (buf.data_ptr(), buf.stride(1), g0, nt, nb, R_end, la, group, buf.dtype, str(dev))
+    ent = _GRAPHS.get(key)
+    if ent is None:
+        infos = torch.zeros(max(nt, 1), dtype=torch.int64, device=dev)
+        g = torch.cuda.CUDAGraph()
+        cs = torch.cuda.Stream(device=dev)
+        cs.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(cs):
+            with torch.cuda.graph(g, stream=cs, capture_error_mode="relaxed"):
+                infos.zero_()
+                _potrf_1x1_grouped(A, s, buf, nb, g0, nt, R_end, la, group, ss, infos, ct, dev)
+        torch.cuda.current_stream(dev).wait_stream(cs)
+        ent = _GRAPHS[key] = (g, infos)
+    g, infos = ent
+    g.replay()
+    return infos
 
 
 def _potrf_info(s, infos, g0, nt):

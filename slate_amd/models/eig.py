@@ -317,14 +317,13 @@ def steqr(d: torch.Tensor, e: torch.Tensor, Z0=None):
 
 def stedc(d: torch.Tensor, e: torch.Tensor, device=None, leaf=64):
     """Divide & conquer (Cuppen / Gu-Eisenstat) for the symmetric
-    tridiagonal (d, e): returns ascending eigenvalues (host fp64) and Z.
-    Merges (GEMMs) run on `device` (GPU when given)."""
-    dev = torch.device(device) if device is not None else torch.device("cpu")
+    tridiagonal (d, e): returns ascending eigenvalues (host fp64) and Z on
+    ``device`` (models/stedc.py: GPU leaves, device deflation, split merge
+    GEMMs; the distributed form keeps Z row-distributed)."""
+    from .stedc import stedc as _stedc
     d = d.to(torch.float64).cpu()
     e = e.to(torch.float64).cpu()
-    with trace_block("stedc"):
-        w, Z = _dc(d, e, dev, leaf)
-    return w, Z
+    return _stedc(d.numpy(), e.numpy(), device=device, leaf=leaf)
 
 
 def _dc(d, e, dev, leaf):

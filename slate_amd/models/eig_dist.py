@@ -294,22 +294,35 @@ def heev_dist(A, Lambda=None, Z=None, opts=None):
                          torch.zeros(max(n, 1), dtype=torch.int64), torch.ones(n, dtype=dt))
             parts = tuple(_bcast_host(comm, t.contiguous(), 0) for t in parts)
             F2 = E.Hb2stFactors(parts[0], parts[1], parts[2], parts[3], parts[4], cnt, parts[5])
-            if method in (MethodEig.QR, 'Q', "qr"):
-                w, Zt = E.steqr(d, e)
-            else:
-                w, Zt = E.stedc(d, e, device=dev)
             # Q2 on this rank's columns of a 1 x P column-cyclic Z, then onto Z's grid
             P = comm.size
             Z1 = _new_general(Z, n, n, 1, P, nb) if P > 1 else None
             Zc = Z1 if Z1 is not None else Z
             lb = Zc.local_block()
-            cols = [lb.global_col(j) for j in range(lb.nloc)]
-            if cols:
-                idx = torch.as_tensor(cols, device=Zt.device)
-                Zl = ops.as_colmajor(Zt[:, idx].to(dt).to(dev).contiguous())
-                Zl = Zl.t().contiguous().t()
-                E.unmtr_hb2st(F2, Zl)
-                lb.data[:n, :lb.nloc].copy_(Zl)
+            if P > 1 and method not in (MethodEig.QR, 'Q', "qr"):
+                # distributed D&C: the tridiagonal eigenvectors stay
+                # row-distributed (no n x n on any rank, models/stedc.py),
+                # then ONE redistribution to the column-cyclic layout the
+                # back-transform runs on
+                from .stedc import stedc_matrix
+                w, Zr = stedc_matrix(d.numpy(), e.numpy(), comm, dev, nb, dtype=dt)
+                redistribute(Zr, Z1)
+                del Zr
+                if lb.nloc:
+                    Zl = lb.data[:n, :lb.nloc]
+                    E.unmtr_hb2st(F2, Zl)
+            else:
+                if method in (MethodEig.QR, 'Q', "qr"):
+                    w, Zt = E.steqr(d, e)
+                else:
+                    w, Zt = E.stedc(d, e, device=dev)
+                cols = [lb.global_col(j) for j in range(lb.nloc)]
+                if cols:
+                    idx = torch.as_tensor(cols, device=Zt.device)
+                    Zl = ops.as_colmajor(Zt[:, idx].to(dt).to(dev).contiguous())
+                    Zl = Zl.t().contiguous().t()
+                    E.unmtr_hb2st(F2, Zl)
+                    lb.data[:n, :lb.nloc].copy_(Zl)
             Zc.storage.mark_local_modified(Zc.storage.origin_slot)
             # Q1 needs Z on F's row distribution (tile size = band)
             same = Z.storage.bc.mb == nb and Z.storage.bc.p == F.storage.bc.p

@@ -117,6 +117,9 @@ def _getrf_p1(A, buf, thr, la, nopiv):
     # 32 CUs: the persistent fp64 panel runs <= 32 workgroups (2 rows per thread)
     ss = StreamSet(dev, reserve_cus=32)
     ev_tr = {}
+    left = []
+    import os
+    tail = int(kt * float(os.environ.get("SLATE_AMD_LU_LEFT_TAIL", "0.6")))
     ss.fork()
     for k in range(kt):
         _wd.beat(f"getrf step {k}")
@@ -173,8 +176,21 @@ def _getrf_p1(A, buf, thr, la, nopiv):
             # on the update stream, after every trailing update that still
             # reads an earlier panel's L rows (trailing j < k overlaps panel
             # k; swapping those rows on the panel stream would race).
+            # Nothing reads the left columns again before the end, so the
+            # swaps are deferred into the panel-bound tail of the
+            # factorization, where the update stream idles (the first ~2/3 of
+            # the steps are GEMM-bound): there they are spread evenly over
+            # the remaining steps, in step order.
             if not nopiv and lck > 0:
-                ops.laswp(buf[:m, 0:lck], ipiv, r0, r0 + kb, ioff=-r0)
+                left.append((k, r0, kb, lck))
+            if k >= tail:
+                todo = -(-len(left) // max(1, kt - k))
+                for _ in range(min(todo, len(left))):
+                    _, j0, jb, jc = left.pop(0)
+                    ops.laswp(buf[:m, 0:jc], ipiv, j0, j0 + jb, ioff=-j0)
+    with ss.use(ss.update[0]):
+        for _, j0, jb, jc in left:
+            ops.laswp(buf[:m, 0:jc], ipiv, j0, j0 + jb, ioff=-j0)
     ss.join()
     if nopiv:
         glob = torch.arange(min(m, n), dtype=torch.int64, device=dev)

@@ -20,6 +20,17 @@ import contextlib
 import torch
 
 
+# the work streams of this process, per device: ONE high-priority panel
+# stream, ONE diag stream and ONE update stream, shared by every pipeline
+# (potrf, getrf, geqrf, SUMMA, ...) -- with the current stream that is 4
+# streams, the box's GPU_MAX_HW_QUEUES default, so no two streams share a
+# hardware queue (RCCL kernels of different
+# communicators queued behind one another in different orders on different
+# ranks can deadlock).
+_SHARED = {}
+MAX_WORK_STREAMS = 4
+
+
 class StreamSet:
     _cache = {}
 
@@ -49,12 +60,21 @@ class StreamSet:
             self.panel = self.diag = cur
             self.update = [cur] * n_update
         elif self.gpu:
-            # torch: lower number = higher priority; ``diag`` carries the
-            # next step's diagonal-tile chain concurrently with the panel's
-            # broadcasts (potrf diag-first)
-            self.panel = torch.cuda.Stream(device=device, priority=-1)
-            self.diag = torch.cuda.Stream(device=device, priority=-1)
-            self.update = [self._update_stream(device, self.reserve_cus) for _ in range(n_update)]
+            sh = _SHARED.get(str(device))
+            if sh is None:
+                # torch: lower number = higher priority; ``diag`` carries the
+                # next step's diagonal-tile chain concurrently with the
+                # panel's broadcasts (potrf diag-first).  The update stream
+                # is created with the CU reservation of the first pipeline
+                # that runs in this process and then shared: a later routine
+                # asking for another reservation reuses it rather than adding
+                # a fourth work stream.
+                sh = dict(panel=torch.cuda.Stream(device=device, priority=-1),
+                          diag=torch.cuda.Stream(device=device, priority=-1),
+                          update=self._update_stream(device, self.reserve_cus), reserve=self.reserve_cus)
+                _SHARED[str(device)] = sh
+            self.panel, self.diag = sh["panel"], sh["diag"]
+            self.update = [sh["update"]] * n_update
         else:
             self.panel = self.diag = None
             self.update = [None] * n_update
@@ -100,6 +120,27 @@ class StreamSet:
                         out.append(st)
         return out
 
+    @classmethod
+    def census(cls, device):
+        """Distinct work streams this process drives on ``device``: the
+        pipeline streams plus the current stream."""
+        dev = torch.device(device)
+        cur = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
+        ids = {id(st) for st in cls.streams_of(dev)}
+        if cur is not None and not any(st == cur for st in cls.streams_of(dev)):
+            ids.add(id(cur))
+        return len(ids)
+
+    def check_census(self):
+        """Raise if this process drives more work streams than the hardware
+        queues it may map them to (MAX_WORK_STREAMS)."""
+        if self.gpu:
+            n = StreamSet.census(self.device)
+            if n > MAX_WORK_STREAMS:
+                from ..core.exceptions import SlateError
+                raise SlateError(f"{n} work streams on {self.device} > {MAX_WORK_STREAMS}")
+        return self
+
     def use(self, s):
         if s is None or not self.gpu:
             return contextlib.nullcontext()
@@ -122,6 +163,7 @@ class StreamSet:
         """All streams wait for the current stream's work so far."""
         if not self.gpu:
             return
+        self.check_census()
         ev = self.event()
         self.panel.wait_event(ev)
         if self.diag is not self.panel:
