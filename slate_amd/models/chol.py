@@ -266,6 +266,14 @@ def _potrf_graph_run(A, s, buf, nb, g0, nt, R_end, la, group, ss, ct, dev):
     ent = _GRAPHS.get(key)
     if ent is None:
         infos = torch.zeros(max(nt, 1), dtype=torch.int64, device=dev)
+        # warm-up on a scratch copy first: the launchers' per-stream
+        # workspaces (csrc/hip/workspace.hpp) must exist before the capture
+        # -- a hipMallocAsync inside it would become a graph allocation that
+        # the workspace cache then keeps for eager calls
+        scratch = buf.clone()
+        _potrf_1x1_grouped(A, s, scratch, nb, g0, nt, R_end, la, group, ss, infos, ct, dev)
+        torch.cuda.current_stream(dev).synchronize()
+        del scratch
         g = torch.cuda.CUDAGraph()
         cs = torch.cuda.Stream(device=dev)
         cs.wait_stream(torch.cuda.current_stream(dev))
@@ -317,16 +325,18 @@ def _potrf_1x1_grouped(A, s, buf, nb, g0, nt, R_end, la, G, ss, infos, ct, dev):
     def mask(r, c):
         return (1, nb, 1, 0, 1, 0, r, c, 0)
 
+    skip = os.environ.get("SLATE_AMD_DEBUG_POTRF_SKIP", "")      # capture bisection (tools/probe)
+
     def upd(P, c_lo, c_hi):
         """buf[c_lo:end, c_lo:c_hi] -= P[c_lo:, :] P[c_lo:c_hi, :]^H (lower mask);
         P's rows are indexed from its own first row ``P0``."""
         Pm, P0 = P
-        if c_hi > c_lo:
+        if c_hi > c_lo and "gemm" not in skip:
             ops.gemm(-1.0, Pm[c_lo - P0:end - P0], Pm[c_lo - P0:c_hi - P0], 1.0, buf[c_lo:end, c_lo:c_hi], 'N', ct,
                      mask(c_lo, c_lo))
 
     ev_tr = {}
-    ss.fork()
+    ss.fork(diag=False)
     for gi, tiles in enumerate(groups):
         _wd.beat(f"potrf group {gi}")
         c0, c2 = gstart(gi), gstart(gi + 1)
@@ -339,8 +349,9 @@ def _potrf_1x1_grouped(A, s, buf, nb, g0, nt, R_end, la, G, ss, infos, ct, dev):
                     if cu > c0:
                         # the group's earlier panels -> column u (rows >= cu)
                         upd((buf[c0:end, c0:cu], c0), cu, cu1)
-                    ops.potrf('L', buf[cu:cu1, cu:cu1], infos[u:u + 1])
-                    if end > cu1:
+                    if "potrf" not in skip:
+                        ops.potrf('L', buf[cu:cu1, cu:cu1], infos[u:u + 1])
+                    if end > cu1 and "trsm" not in skip:
                         ops.trsm('R', 'L', ct, 'N', 1.0, buf[cu:cu1, cu:cu1], buf[cu1:end, cu:cu1])
             P = (buf[c0:end, c0:c2], c0)
             la_end = gstart(gi + 1 + la)

@@ -25,8 +25,8 @@ launches -- no per-column work on the host:
 The order is padded to a multiple of nb with an identity block (never
 selected as pivot).  T is stored as compact band storage and factored by
 gbtrf (models/band.py); hetrs is trsm + gbtrs + trsm.  On a process grid
-every rank factors the same gathered matrix (deterministic kernels) -- as
-SLATE, the indefinite solver is not a scaling path.
+the distributed form in models/hetrf_dist.py runs instead (no rank holds
+the dense matrix).
 """
 from __future__ import annotations
 
@@ -171,6 +171,15 @@ def hetrf(A, pivots: Pivots = None, T=None, pivots2=None, H=None, opts=None):
     one block left, as SLATE); the permutation goes to ``pivots``, the
     block-tridiagonal T to the band matrix ``T`` if given.  Returns info."""
     from .band import gbtrf
+    s = A.storage
+    if s.comm.size > 1 and s.bc is not None and s.bc.mb == s.bc.nb:
+        # on a grid: the distributed Aasen (models/hetrf_dist.py), no gather
+        from .hetrf_dist import hetrf_dist
+        info, F = hetrf_dist(A, opts)
+        A._hetrf = F
+        if pivots is not None:
+            pivots.set(torch.as_tensor(F.perm[:F.n].copy(), dtype=torch.int64), 1)
+        return info
     with trace_block("hetrf"):
         s = A.storage
         n = A.n()
@@ -219,6 +228,9 @@ def hetrs(A, pivots=None, T=None, pivots2=None, B=None, opts=None):
     """Solve A X = B with the factors of hetrf (B overwritten):
     x = P^T L^{-H} T^{-1} L^{-1} P b."""
     from .band import gbtrs
+    if getattr(A._hetrf, "distributed", False):
+        from .hetrf_dist import hetrs_dist
+        return hetrs_dist(A._hetrf, B, opts)
     with trace_block("hetrs"):
         F = A._hetrf
         dev = F.L.device

@@ -159,22 +159,35 @@ class StreamSet:
             return
         (s if s is not None else torch.cuda.current_stream(self.device)).wait_event(ev)
 
-    def fork(self):
-        """All streams wait for the current stream's work so far."""
+    def _members(self, diag=True):
+        out = []
+        for st in [self.panel] + ([self.diag] if diag else []) + list(self.update):
+            if all(st is not o for o in out):
+                out.append(st)
+        return out
+
+    def fork(self, diag=True):
+        """All streams wait for the current stream's work so far.  diag=False
+        leaves the diag stream out of the fork (and of the matching join): a
+        pipeline that never uses it must not open an empty branch, which the
+        HIP stream-capture of Option.UseGraph does not survive."""
         if not self.gpu:
             return
         self.check_census()
+        members = self._members(diag)
+        if not hasattr(self, "_fstack"):
+            self._fstack = []
+        self._fstack.append(members)           # fork / join pairs nest
         ev = self.event()
-        self.panel.wait_event(ev)
-        if self.diag is not self.panel:
-            self.diag.wait_event(ev)
-        for u in self.update:
-            u.wait_event(ev)
+        for st in members:
+            st.wait_event(ev)
 
     def join(self):
         """Current stream waits for all streams."""
         if not self.gpu:
             return
         cur = torch.cuda.current_stream(self.device)
-        for s in [self.panel, self.diag] + self.update:
-            cur.wait_event(self.event(s))
+        stack = getattr(self, "_fstack", None)
+        for s in (stack.pop() if stack else self._members()):
+            if s != cur:
+                cur.wait_event(self.event(s))

@@ -102,6 +102,54 @@ def test_tbsm_hbmm():
 def _dist(rank, size, p, q):
     check_band(p, q)
     check_indef(p, q)
+    check_hetrf_dist(p, q)
+
+
+def check_hetrf_dist(p, q):
+    """Distributed Aasen (models/hetrf_dist.py): zero diagonal (pivoting
+    needed), padded orders, both uplos, complex; P A P^H = L T L^H from the
+    grid factors and hesv residuals -- no rank gathers A."""
+    from slate_amd.models.hetrf import _blk
+    for dt, uplo, n, nb in [(torch.float64, sl.Uplo.Lower, 70, 16), (torch.complex128, sl.Uplo.Upper, 45, 8),
+                            (torch.float64, sl.Uplo.Upper, 64, 16)]:
+        S = sl.HermitianMatrix(uplo, n, nb=nb, p=p, q=q, dtype=dt)
+        S.insertLocalTiles()
+        sl.generate_matrix(S, "rands", 21)
+        Sf = _dense_hermitian(S)
+        Sf = Sf - torch.diag(torch.diagonal(Sf))
+        sl.from_dense(S, torch.tril(Sf) if uplo == sl.Uplo.Lower else torch.triu(Sf))
+        B = sl.Matrix(n, 3, nb=nb, p=p, q=q, dtype=dt)
+        B.insertLocalTiles()
+        sl.generate_matrix(B, "rands", 22)
+        Bd = D(B).clone()
+        piv = sl.Pivots()
+        assert sl.hetrf(S, piv) == 0
+        F = S._hetrf
+        if p * q > 1:
+            assert getattr(F, "distributed", False)
+        N, k = F.N, F.N // F.nb
+        T = torch.zeros(N, N, dtype=dt)
+        for J in range(k):
+            T[J * F.nb:(J + 1) * F.nb, J * F.nb:(J + 1) * F.nb] = _blk(F.Td, J, F.nb).cpu()
+            if J + 1 < k:
+                T[(J + 1) * F.nb:(J + 2) * F.nb, J * F.nb:(J + 1) * F.nb] = _blk(F.Tl, J + 1, F.nb).cpu()
+                T[J * F.nb:(J + 1) * F.nb, (J + 1) * F.nb:(J + 2) * F.nb] = _blk(F.Tl, J + 1, F.nb).cpu().mH
+        Ap = torch.eye(N, dtype=dt)
+        Ap[:n, :n] = Sf
+        pm = torch.as_tensor(F.perm).cpu()
+        L = (D(F.L) if hasattr(F.L, "storage") else F.L).cpu()
+        assert ((L @ T @ L.mH - Ap[pm][:, pm]).abs().max() / Sf.abs().max()).item() < 1e-12
+        sl.hetrs(S, piv, None, None, B)
+        assert (Sf @ D(B) - Bd).abs().max() / (Sf.abs().max() * D(B).abs().max() * n) < 1e-13
+
+
+def _dist_hetrf(rank, size, p, q):
+    check_hetrf_dist(p, q)
+
+
+@pytest.mark.parametrize("grid", [(2, 2), (2, 4)])
+def test_hetrf_distributed_grids(grid):
+    run_dist(_dist_hetrf, grid[0] * grid[1], *grid)
 
 
 @pytest.mark.parametrize("grid", [(2, 1), (1, 2)])
