@@ -254,36 +254,63 @@ def _potrf_lower(A, opts):
 _GRAPHS = {}
 
 
+class _SerialStreams:
+    """StreamSet stand-in that keeps every step on the current stream."""
+    gpu = True
+    panel = diag = None
+    update = [None]
+
+    def use(self, st):
+        import contextlib
+        return contextlib.nullcontext()
+
+    def wait(self, st, ev):
+        pass
+
+    def event(self, st=None):
+        return None
+
+    def fork(self, diag=True):
+        pass
+
+    def join(self):
+        pass
+
+
 def _potrf_graph_run(A, s, buf, nb, g0, nt, R_end, la, group, ss, ct, dev):
-    """Option.UseGraph: the one-rank potrf DAG (panel / diag / update
-    streams and their events) captured once into a hipGraph per (buffer,
-    geometry) and replayed -- one launch for the whole factorization, no
-    host work per kernel.  The capture runs on a side stream that forks into
-    the pipeline streams and joins them back; the info vector is zeroed
-    inside the graph and lives with it.  Replays read whatever A holds at
-    the time (same buffer)."""
+    """Option.UseGraph: the one-rank potrf captured once into a hipGraph per
+    (buffer, geometry) and replayed -- one launch for the whole
+    factorization, no host work per kernel: the form for launch-bound
+    (small) orders, where the eager loop's ~30 launches per tile cost more
+    than the kernels.  The capture records the single-stream form of the
+    DAG: a capture that forks into the panel / update streams is not
+    survived by this HIP runtime (hipStreamEndCapture segfaults on it,
+    tools/probe/graph_probe2.py; a plain two-stream fork/join captures
+    fine), so inside the graph the panel and the trailing update are
+    ordered; large orders keep the eager pipelined path.  The info vector
+    lives with the graph and is zeroed before each replay; replays read
+    whatever A holds (same buffer)."""
     key = (buf.data_ptr(), buf.stride(1), g0, nt, nb, R_end, la, group, buf.dtype, str(dev))
     ent = _GRAPHS.get(key)
     if ent is None:
         infos = torch.zeros(max(nt, 1), dtype=torch.int64, device=dev)
         # warm-up on a scratch copy first: the launchers' per-stream
-        # workspaces (csrc/hip/workspace.hpp) must exist before the capture
-        # -- a hipMallocAsync inside it would become a graph allocation that
-        # the workspace cache then keeps for eager calls
-        scratch = buf.clone()
-        _potrf_1x1_grouped(A, s, scratch, nb, g0, nt, R_end, la, group, ss, infos, ct, dev)
-        torch.cuda.current_stream(dev).synchronize()
-        del scratch
+        # workspaces (csrc/hip/workspace.hpp) must exist for the capture
+        # stream before the capture
         g = torch.cuda.CUDAGraph()
         cs = torch.cuda.Stream(device=dev)
         cs.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(cs):
+            scratch = buf.clone()
+            _potrf_1x1_grouped(A, s, scratch, nb, g0, nt, R_end, la, group, ss, infos, ct, dev, serial=True)
+            cs.synchronize()
+            del scratch
             with torch.cuda.graph(g, stream=cs, capture_error_mode="relaxed"):
-                infos.zero_()
-                _potrf_1x1_grouped(A, s, buf, nb, g0, nt, R_end, la, group, ss, infos, ct, dev)
+                _potrf_1x1_grouped(A, s, buf, nb, g0, nt, R_end, la, group, ss, infos, ct, dev, serial=True)
         torch.cuda.current_stream(dev).wait_stream(cs)
         ent = _GRAPHS[key] = (g, infos)
     g, infos = ent
+    infos.zero_()              # eagerly: a memset node inside the graph replays stale
     g.replay()
     return infos
 
@@ -305,7 +332,7 @@ def _potrf_info(s, infos, g0, nt):
     return info
 
 
-def _potrf_1x1_grouped(A, s, buf, nb, g0, nt, R_end, la, G, ss, infos, ct, dev):
+def _potrf_1x1_grouped(A, s, buf, nb, g0, nt, R_end, la, G, ss, infos, ct, dev, serial=False):
     """One rank owning the whole matrix: panels are factored one tile at a
     time, but the trailing update is applied once per GROUP of G tiles with
     K = G nb (the G panel columns are adjacent in the local buffer, so the
@@ -325,17 +352,17 @@ def _potrf_1x1_grouped(A, s, buf, nb, g0, nt, R_end, la, G, ss, infos, ct, dev):
     def mask(r, c):
         return (1, nb, 1, 0, 1, 0, r, c, 0)
 
-    skip = os.environ.get("SLATE_AMD_DEBUG_POTRF_SKIP", "")      # capture bisection (tools/probe)
-
     def upd(P, c_lo, c_hi):
         """buf[c_lo:end, c_lo:c_hi] -= P[c_lo:, :] P[c_lo:c_hi, :]^H (lower mask);
         P's rows are indexed from its own first row ``P0``."""
         Pm, P0 = P
-        if c_hi > c_lo and "gemm" not in skip:
+        if c_hi > c_lo:
             ops.gemm(-1.0, Pm[c_lo - P0:end - P0], Pm[c_lo - P0:c_hi - P0], 1.0, buf[c_lo:end, c_lo:c_hi], 'N', ct,
                      mask(c_lo, c_lo))
 
     ev_tr = {}
+    if serial:
+        ss = _SerialStreams()
     ss.fork(diag=False)
     for gi, tiles in enumerate(groups):
         _wd.beat(f"potrf group {gi}")
@@ -349,9 +376,8 @@ def _potrf_1x1_grouped(A, s, buf, nb, g0, nt, R_end, la, G, ss, infos, ct, dev):
                     if cu > c0:
                         # the group's earlier panels -> column u (rows >= cu)
                         upd((buf[c0:end, c0:cu], c0), cu, cu1)
-                    if "potrf" not in skip:
-                        ops.potrf('L', buf[cu:cu1, cu:cu1], infos[u:u + 1])
-                    if end > cu1 and "trsm" not in skip:
+                    ops.potrf('L', buf[cu:cu1, cu:cu1], infos[u:u + 1])
+                    if end > cu1:
                         ops.trsm('R', 'L', ct, 'N', 1.0, buf[cu:cu1, cu:cu1], buf[cu1:end, cu:cu1])
             P = (buf[c0:end, c0:c2], c0)
             la_end = gstart(gi + 1 + la)

@@ -100,6 +100,15 @@ def he2hb_dist(F, opts=None):
     nloc_r = [numroc(n, nb, r, p) for r in range(p)]
     Fac = He2hbDistFactors(nb)
     from .lu import _Pack
+    from ..parallel.streams import StreamSet
+    # lookahead (src/he2hb.cc:172-610): the rank-2k update of step k first
+    # touches the next panel's tile column (event), then the rest; panel
+    # k+1 (all-gather, QR, broadcast) runs on the high-priority panel stream
+    # as soon as that column is done, concurrently with step k's bulk GEMMs
+    ss = StreamSet(dev, reserve_cus=0)
+    us = ss.update[0]
+    ev_la = {}
+    ss.fork(diag=False)
     with trace_block("he2hb"):
         for k in range(nt - 1):
             r0 = (k + 1) * nb
@@ -110,47 +119,61 @@ def he2hb_dist(F, opts=None):
             lr0 = min(tiles_local_before(k + 1, p, pr) * nb, mloc)
             lc_k = min(tiles_local_before(k, q, pc) * nb, nloc)
             lc1 = min(tiles_local_before(k + 1, q, pc) * nb, nloc)
+            lc2 = min(tiles_local_before(k + 2, q, pc) * nb, nloc)
             nmine = mloc - lr0
-            pk = _Pack([("T", kk, kk, dt), ("V", nmine, kk, dt)], dev)
-            Tk, Vloc = pk.get("T"), pk.get("V")
-            with trace_block("he2hb::panel"):
-                if pc == ck:
-                    P, myidx = panel_allgather(grid.col_comm, buf, mloc, k + 1, lc_k, kb, nb, p, pr, nloc_r,
-                                               dt, dev)
-                    tau = torch.zeros(kk, dtype=dt, device=dev)
-                    Vf = ops.colmajor_empty(m2, kk, dt, dev)
-                    ops.geqrf(P, tau, Tk, Vf)
+            with ss.use(ss.panel):
+                if k >= 1:
+                    ss.wait(ss.panel, ev_la[k - 1])
+                pk = _Pack([("T", kk, kk, dt), ("V", nmine, kk, dt)], dev)
+                Tk, Vloc = pk.get("T"), pk.get("V")
+                with trace_block("he2hb::panel"):
+                    if pc == ck:
+                        P, myidx = panel_allgather(grid.col_comm, buf, mloc, k + 1, lc_k, kb, nb, p, pr, nloc_r,
+                                                   dt, dev)
+                        tau = torch.zeros(kk, dtype=dt, device=dev)
+                        Vf = ops.colmajor_empty(m2, kk, dt, dev)
+                        ops.geqrf(P, tau, Tk, Vf)
+                        if nmine:
+                            ops.row_gather(P, buf[lr0:mloc, lc_k:lc_k + kb], myidx)
+                            ops.row_gather(Vf, Vloc, myidx)
+                    if q > 1:
+                        grid.row_comm.bcast(pk.raw, ck)
+                Fac.panels.append((k, r0, kk, pk.prefix("V").get("T")))
+                ev_panel = ss.event(ss.panel)
+            with ss.use(us):
+                ss.wait(us, ev_panel)
+                if buf.is_cuda:
+                    pk.raw.record_stream(us)
+                with trace_block("he2hb::update"):
+                    plan = plan_col_gather(s.tileMb, k + 1, nt, nb, p, q, pc, dev)
+                    X = ops.colmajor_empty(nmine, kk, dt, dev)
                     if nmine:
-                        ops.row_gather(P, buf[lr0:mloc, lc_k:lc_k + kb], myidx)
-                        ops.row_gather(Vf, Vloc, myidx)
-                if q > 1:
-                    grid.row_comm.bcast(pk.raw, ck)
-            Fac.panels.append((k, r0, kk, pk.prefix("V").get("T")))
-            with trace_block("he2hb::update"):
-                plan = plan_col_gather(s.tileMb, k + 1, nt, nb, p, q, pc, dev)
-                X = ops.colmajor_empty(nmine, kk, dt, dev)
-                if nmine:
-                    X.copy_(Vloc)
-                    ops.trmm('R', 'U', 'N', 'N', 1.0, Tk, X)                      # X = V T
-                Xc = assemble_cols(plan, X, grid, p, kk, dt, dev)
-                A22 = buf[lr0:mloc, lc1:nloc]
-                Y = ops.colmajor_zeros(nmine, kk, dt, dev)
-                if nmine and A22.shape[1]:
-                    ops.gemm(1.0, A22, Xc, 0.0, Y)                                 # partial A V T
-                if q > 1 and nmine:
-                    grid.row_comm.allreduce(Y)
-                M = ops.colmajor_zeros(kk, kk, dt, dev)
-                if nmine:
-                    ops.gemm(1.0, X, Y, 0.0, M, transA=ct)                         # partial T^H V^H Y
-                if p > 1:
-                    grid.col_comm.allreduce(M)
-                if nmine:
-                    ops.gemm(-0.5, Vloc, M, 1.0, Y)                                # W = Y - V M / 2
-                Wc = assemble_cols(plan, Y, grid, p, kk, dt, dev)
-                Vc = assemble_cols(plan, Vloc, grid, p, kk, dt, dev)
-                if nmine and A22.shape[1]:
-                    ops.gemm(-1.0, Vloc, Wc, 1.0, A22, transB=ct)                  # A -= V W^H
-                    ops.gemm(-1.0, Y, Vc, 1.0, A22, transB=ct)                     # A -= W V^H
+                        X.copy_(Vloc)
+                        ops.trmm('R', 'U', 'N', 'N', 1.0, Tk, X)                      # X = V T
+                    Xc = assemble_cols(plan, X, grid, p, kk, dt, dev)
+                    A22 = buf[lr0:mloc, lc1:nloc]
+                    Y = ops.colmajor_zeros(nmine, kk, dt, dev)
+                    if nmine and A22.shape[1]:
+                        ops.gemm(1.0, A22, Xc, 0.0, Y)                                 # partial A V T
+                    if q > 1 and nmine:
+                        grid.row_comm.allreduce(Y)
+                    M = ops.colmajor_zeros(kk, kk, dt, dev)
+                    if nmine:
+                        ops.gemm(1.0, X, Y, 0.0, M, transA=ct)                         # partial T^H V^H Y
+                    if p > 1:
+                        grid.col_comm.allreduce(M)
+                    if nmine:
+                        ops.gemm(-0.5, Vloc, M, 1.0, Y)                                # W = Y - V M / 2
+                    Wc = assemble_cols(plan, Y, grid, p, kk, dt, dev)
+                    Vc = assemble_cols(plan, Vloc, grid, p, kk, dt, dev)
+                    for (a, b) in ((lc1, lc2), (lc2, nloc)):
+                        if nmine and b > a:
+                            Ab = buf[lr0:mloc, a:b]
+                            ops.gemm(-1.0, Vloc, Wc[a - lc1:b - lc1], 1.0, Ab, transB=ct)   # A -= V W^H
+                            ops.gemm(-1.0, Y, Vc[a - lc1:b - lc1], 1.0, Ab, transB=ct)      # A -= W V^H
+                        if a == lc1:
+                            ev_la[k] = ss.event(us)
+    ss.join()
     s.mark_local_modified(slot)
     return Fac
 

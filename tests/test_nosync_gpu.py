@@ -129,3 +129,27 @@ def test_stream_census():
     sl.geqrf(Q, sl.TriangularFactors())
     torch.cuda.synchronize()
     assert StreamSet.census(dev) <= MAX_WORK_STREAMS, StreamSet.census(dev)
+
+
+def test_potrf_use_graph():
+    """Option.UseGraph: the one-rank potrf is captured once into a hipGraph
+    and replayed; every replay on fresh input matches the eager factor and
+    reports info through the graph's own info vector."""
+    dev = torch.device("cuda")
+    n, nb = 2048, 256
+    A = sl.HermitianMatrix(sl.Uplo.Lower, n, nb=nb, device=dev)
+    A.insertLocalTiles(device=dev)
+    buf = A.storage.local[A.storage.origin_slot]
+    for seed in (3, 4, 5):
+        sl.generate_matrix(A, "poev", seed=seed)
+        F0 = buf[:n, :n].clone()
+        assert sl.potrf(A, {sl.Option.Lookahead: 1, sl.Option.UseGraph: True}) == 0
+        Lg = torch.tril(buf[:n, :n]).clone()
+        buf[:n, :n].copy_(F0)
+        assert sl.potrf(A, {sl.Option.Lookahead: 1}) == 0
+        Le = torch.tril(buf[:n, :n])
+        assert (Lg - Le).abs().max().item() <= 1e-12 * Le.abs().max().item()
+    # a non-SPD input: info through the graph
+    buf[:n, :n].copy_(F0)
+    buf[100, 100] = -1.0
+    assert sl.potrf(A, {sl.Option.Lookahead: 1, sl.Option.UseGraph: True}) == 101
