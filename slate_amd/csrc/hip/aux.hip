@@ -178,6 +178,11 @@ constexpr int HSIZE = 2048;      // hash slots (>= 2 x max swaps per call)
 constexpr int MAXSW = 512;       // max swaps per call (more: split into calls)
 }
 
+__global__ void zero_words_kernel(unsigned long long* p, long long n) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) p[i] = 0ull;
+}
+
 struct SwapPlan {                // folded permutation of one swap sequence
     int nt;
     int pad;
@@ -388,7 +393,7 @@ void laswp(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, int incx, hipS
 // rank of the column (the U row the trailing update needs anyway).
 void swap_plan(i64 k1, i64 k2, const i64* ipiv, i64 ioff, int incx, void* plan, hipStream_t s) {
     if (k2 - k1 > MAXSW) throw std::invalid_argument("swap_plan: at most 512 swaps per plan");
-    HIP_CHECK(hipMemsetAsync(plan, 0, sizeof(SwapPlan), s));
+    zero_words(plan, (long long)(sizeof(SwapPlan) / 8), s);
     if (k2 <= k1) return;
     hipLaunchKernelGGL(laswp_setup_kernel, dim3(1), dim3(MAXSW), 0, s, k1, k2, ipiv, ioff, incx,
                        static_cast<SwapPlan*>(plan), true);

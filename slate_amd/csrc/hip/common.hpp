@@ -32,6 +32,19 @@ struct ccplx { float re, im; };
 
 #define HIP_LAUNCH_CHECK() HIP_CHECK(hipGetLastError())
 
+// Zero n 8-byte words with a kernel instead of hipMemsetAsync: inside a
+// hipGraph capture a memset becomes a memset node, and on this runtime such
+// nodes replay with stale parameters (the potrf info words came back as
+// bytes 0x08 / 0x10 after the first replay, tools/probe/graph_time.py);
+// kernel nodes replay exactly.
+__global__ void zero_words_kernel(unsigned long long* p, long long n);
+inline void zero_words(void* p, long long n, hipStream_t s) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(zero_words_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       static_cast<unsigned long long*>(p), n);
+    HIP_LAUNCH_CHECK();
+}
+
 // ---------------------------------------------------------------------------
 // Scalar helpers usable for real and complex element types.
 template <typename T> struct scalar_traits;

@@ -217,7 +217,7 @@ static void herk_lower(char uplo, i64 n, i64 k, const T* P, i64 ldp, T* C, i64 l
 
 template <typename T>
 void potrf_tile(char uplo, int n, T* A, i64 lda, i64* info, hipStream_t s) {
-    if (info) HIP_CHECK(hipMemsetAsync(info, 0, sizeof(i64), s));
+    if (info) zero_words(info, 1, s);
     if (n <= 0) return;
     if constexpr (std::is_same<T, double>::value) {
         if (uplo == 'L') {

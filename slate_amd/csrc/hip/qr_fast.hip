@@ -290,7 +290,7 @@ bool geqrf_cholqr(i64 m, i64 b, double* A, i64 lda, double* tau, double* Tm, i64
     i64* inf = reinterpret_cast<i64*>(pfloor + 1);
     int* flag = reinterpret_cast<int*>(inf + 4);
     gecopy<double, double>('G', 'N', m, b, A, lda, Bk, m, s);
-    HIP_CHECK(hipMemsetAsync(inf, 0, 4 * sizeof(i64), s));
+    zero_words(inf, 4, s);
     // ---- CholeskyQR2 (always): G = A^T A, G = L L^T, A = A L^-T, R = L^T R
     auto gram = [&](const int* gate) { gemm_d('T', 'N', b, b, m, 1.0, A, lda, A, lda, 0.0, G, b, s, gate); };
     gram(nullptr);
