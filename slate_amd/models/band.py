@@ -24,8 +24,11 @@ slab of its band tiles):
   swept tile by tile; the owner of each factor column applies it and
   broadcasts the rows it changed (kb + bandwidth rows), so every rank's
   copy stays exact; each rank finally keeps its own part of B.
-* products: B is replicated in column chunks; each rank multiplies its
-  slabs, the partial results are summed with one all-reduce per chunk.
+* products: B and C move to 1-D row-cyclic work layouts matched to the
+  band's column ownership (one redistribution each); each rank multiplies
+  its slabs and the partial blocks travel point-to-point to the owners of
+  their rows (op(A) = A), or the B tiles of each column's window travel to
+  the column's owner (op(A) = A^T / A^H) -- no replication, no all-reduce.
 """
 from __future__ import annotations
 
@@ -488,111 +491,213 @@ def _tri_dispatch(s, buf, X, up, opch, kd, unit, gpiv):
 _CHUNK = 512
 
 
-def _write_cols(C, c0, c1, Cp, alpha, beta):
-    """C[:, c0:c1] = alpha Cp + beta C[:, c0:c1] on this rank's part (Cp
-    replicated, m x (c1 - c0))."""
-    from .aux import allgather_dense, from_dense
-    s = C.storage
-    Cs = C.slice(0, C.m() - 1, c0, c1 - 1)
-    if s.bc is None or C.op() != Op.NoTrans:
-        D = Cp * alpha + (allgather_dense(Cs).to(Cp.device) * beta if beta != 0 else 0)
-        from_dense(Cs, D)
-        return
-    lb = Cs.local_block()
-    if lb.mloc == 0 or lb.nloc == 0:
-        return
-    dev = lb.data.device
-    rows = torch.as_tensor([lb.global_row(i) for i in range(lb.mloc)], device=Cp.device)
-    cols = torch.as_tensor([lb.global_col(j) for j in range(lb.nloc)], device=Cp.device)
-    D = ops.colmajor_empty(lb.mloc, lb.nloc, Cp.dtype, dev)
-    D.copy_(Cp[rows][:, cols])
-    ops.geadd(alpha, D, beta, lb.data[:lb.mloc, :lb.nloc])
-    s.mark_local_modified(s.origin_slot)
-
-
 def _stored_rows(s, j):
     lo, hi = s.window(j)
     return s.row_offsets[lo], s.row_offsets[hi + 1]
 
 
+def _row_cyclic(rows, cols, s, dt, dev):
+    """A rows x cols matrix 1-D row-cyclic over the band's ranks with the
+    band tile size: tile row i lives on rank i % Q at local rows
+    (i // Q) nb -- the rows of B / C that meet band tile column i."""
+    from ..core.matrix import Matrix
+    M = Matrix(rows, cols, nb=max(1, cols), mb=s.band_nb, p=s.Q, q=1, comm=s.comm, dtype=dt, device=dev)
+    M.insertLocalTiles(device=dev if dev.type == "cuda" else -1)
+    return M
+
+
+def _lrow(s, i):
+    return (i // s.Q) * s.band_nb
+
+
+def _exchange_pieces(s, sends, recv_shapes, dt, dev):
+    """sends {peer: [tensor, ...]}, recv_shapes {peer: [(r, c), ...]}, both
+    in an order every rank derives from the same global enumeration: one
+    batched send/recv per peer (flattened), returns {peer: [tensor, ...]}."""
+    sb, rb = {}, {}
+    for r, ts in sends.items():
+        sb[r] = torch.cat([t.t().contiguous().reshape(-1) for t in ts]) if ts else None
+    for r, shp in recv_shapes.items():
+        rb[r] = torch.empty(sum(a * b for a, b in shp), dtype=dt, device=dev)
+    sb = {r: t for r, t in sb.items() if t is not None and t.numel()}
+    rb = {r: t for r, t in rb.items() if t.numel()}
+    if sb or rb:
+        s.comm.exchange(sb, rb)
+    out = {}
+    for r, shp in recv_shapes.items():
+        buf, o, lst = rb.get(r), 0, []
+        for (a, b) in shp:
+            lst.append(buf[o:o + a * b].reshape(b, a).t() if a * b else torch.empty(a, b, dtype=dt, device=dev))
+            o += a * b
+        out[r] = lst
+    return out
+
+
+def _band_product(s, buf, Bl, Cl, w, mode, up=None):
+    """Cl (this rank's row-cyclic part of C, w columns) += the band product
+    with Bl (row-cyclic part of B):
+      mode 'N': C += A B -- each local column j gives a partial block for
+                the tile rows of its window, routed to their owners;
+      mode 'T'/'C': C += op(A) B -- column j needs the B tiles of its
+                window (fetched from their owners), produces tile row j;
+      mode 'H': A Hermitian stored in triangle ``up``: the stored part as
+                'N' and its conjugate transpose (diagonal tile counted
+                once) as 'C'.
+    Every transfer is point-to-point between the owners; nothing is
+    replicated or all-reduced."""
+    dt, dev = buf.dtype, buf.device
+    me, Q = s.rank, s.Q
+    ct = conj_trans(dt)
+    cols = list(range(s.nt))
+
+    def tile_rows(i):
+        return s.row_offsets[i], s.row_offsets[i + 1]
+
+    do_n = mode in ('N', 'H')
+    do_t = mode in ('T', 'C', 'H')
+    tch = ct if mode in ('C', 'H') else 'T'
+    # ---- 'N' part: pieces (i, j) from owner(j) to owner(i)
+    if do_n:
+        sends, shapes, mine = {}, {}, []
+        for j in cols:
+            lo, hi = s.window(j)
+            oj = j % Q
+            for i in range(lo, hi + 1):
+                oi = i % Q
+                if oj == me and oi != me:
+                    sends.setdefault(oi, []).append((i, j))
+                elif oi == me and oj != me:
+                    shapes.setdefault(oj, []).append((i, j))
+                elif oi == me and oj == me:
+                    mine.append((i, j))
+        parts = {}
+        for j in s.my_cols():
+            g0, g1 = _stored_rows(s, j)
+            S = _col_block(s, buf, j, g0, g1)
+            cj0, cj1 = s.col_offsets[j], s.col_offsets[j + 1]
+            if mode == 'H' and dt.is_complex:
+                # the diagonal of a Hermitian matrix is real (its stored
+                # imaginary part is ignored, as in hemm)
+                S2 = ops.colmajor_empty(S.shape[0], S.shape[1], dt, dev)
+                S2.copy_(S)
+                d0 = cj0 - g0
+                torch.diagonal(S2[d0:d0 + (cj1 - cj0)]).imag.zero_()
+                S = S2
+            P = ops.colmajor_zeros(g1 - g0, w, dt, dev)
+            if w:
+                ops.gemm(1.0, S, Bl[_lrow(s, j):_lrow(s, j) + (cj1 - cj0)], 0.0, P)
+            parts[j] = (g0, P)
+
+        def piece(i, j):
+            g0, P = parts[j]
+            r0, r1 = tile_rows(i)
+            return P[r0 - g0:r1 - g0]
+        snd = {r: [piece(i, j) for (i, j) in lst] for r, lst in sends.items()}
+        rsh = {r: [(tile_rows(i)[1] - tile_rows(i)[0], w) for (i, j) in lst] for r, lst in shapes.items()}
+        got = _exchange_pieces(s, snd, rsh, dt, dev)
+        for (i, j) in mine:
+            r0, r1 = tile_rows(i)
+            Cl[_lrow(s, i):_lrow(s, i) + (r1 - r0)] += piece(i, j)
+        for r, lst in shapes.items():
+            for (i, j), T in zip(lst, got[r]):
+                r0, r1 = tile_rows(i)
+                Cl[_lrow(s, i):_lrow(s, i) + (r1 - r0)] += T
+    # ---- 'T' part: B tiles (i) of column j's window from owner(i) to owner(j)
+    if do_t:
+        sends, shapes = {}, {}
+        for j in cols:
+            lo, hi = s.window(j)
+            oj = j % Q
+            for i in range(lo, hi + 1):
+                oi = i % Q
+                if oi == me and oj != me:
+                    sends.setdefault(oj, []).append((i, j))
+                elif oj == me and oi != me:
+                    shapes.setdefault(oi, []).append((i, j))
+        snd = {r: [Bl[_lrow(s, i):_lrow(s, i) + (tile_rows(i)[1] - tile_rows(i)[0])] for (i, j) in lst]
+               for r, lst in sends.items()}
+        rsh = {r: [(tile_rows(i)[1] - tile_rows(i)[0], w) for (i, j) in lst] for r, lst in shapes.items()}
+        got = _exchange_pieces(s, snd, rsh, dt, dev)
+        halo = {}
+        for r, lst in shapes.items():
+            for (i, j), T in zip(lst, got[r]):
+                halo[(i, j)] = T
+        for j in s.my_cols():
+            g0, g1 = _stored_rows(s, j)
+            lo, hi = s.window(j)
+            S = _col_block(s, buf, j, g0, g1)
+            cj0, cj1 = s.col_offsets[j], s.col_offsets[j + 1]
+            Bh = ops.colmajor_empty(g1 - g0, w, dt, dev)
+            for i in range(lo, hi + 1):
+                r0, r1 = tile_rows(i)
+                src = Bl[_lrow(s, i):_lrow(s, i) + (r1 - r0)] if i % Q == me else halo[(i, j)]
+                Bh[r0 - g0:r1 - g0].copy_(src)
+            Sx = S
+            if mode == 'H':
+                Sx = ops.colmajor_empty(S.shape[0], S.shape[1], dt, dev)
+                Sx.copy_(S)
+                d0 = cj0 - g0
+                ops.geset(0.0, 0.0, Sx[d0:d0 + (cj1 - cj0)], uplo='U' if up == Uplo.Lower else 'L')
+            if w:
+                ops.gemm(1.0, Sx, Bh, 1.0, Cl[_lrow(s, j):_lrow(s, j) + (cj1 - cj0)], transA=tch)
+
+
+def _band_mm(alpha, s, buf, B, beta, C, mode, up=None):
+    """C = alpha op(A) B + beta C for the band A in slabs ``buf`` (Left)."""
+    from ..parallel.redist import redistribute_pieces
+    dt, dev = buf.dtype, buf.device
+    w = B.n()
+    Bw = _row_cyclic(B.m(), w, s, dt, dev)
+    redistribute_pieces(B, Bw)
+    Cw = _row_cyclic(C.m(), w, s, dt, dev)
+    lbB, lbC = Bw.local_block(), Cw.local_block()
+    Cl = lbC.data[:lbC.mloc, :lbC.nloc]
+    Cl.zero_()
+    _band_product(s, buf, lbB.data[:lbB.mloc, :lbB.nloc], Cl, w, mode, up)
+    if beta != 0:
+        Ct = _row_cyclic(C.m(), w, s, dt, dev)
+        redistribute_pieces(C, Ct)
+        lt = Ct.local_block()
+        if lt.mloc and lt.nloc:
+            ops.geadd(alpha, Cl, beta, lt.data[:lt.mloc, :lt.nloc])
+        Ct.storage.mark_local_modified(Ct.storage.origin_slot)
+        redistribute_pieces(Ct, C)
+    else:
+        if alpha != 1 and lbC.mloc and lbC.nloc:
+            ops.gescale(alpha, Cl)
+        Cw.storage.mark_local_modified(Cw.storage.origin_slot)
+        redistribute_pieces(Cw, C)
+    return C
+
+
 def gbmm(alpha, A, B, beta, C, opts=None):
-    """C = alpha op(A) B + beta C with A a band matrix (op from A's view)."""
+    """C = alpha op(A) B + beta C with A a band matrix (op from A's view):
+    B and C in 1-D row-cyclic work layouts matched to the band's column
+    ownership, point-to-point pieces between owners (_band_product)."""
     _need_band(A, "gbmm")
-    from .aux import allgather_dense
     with trace_block("gbmm"):
         band_mask(A, A._kl, A._ku)
         s, slot, buf = _slab(A)
-        dev, dt = buf.device, s.dtype
         opA = A.op()
-        tr = {Op.Trans: 'T', Op.ConjTrans: 'C'}.get(opA)
-        mC = C.m()
-        for c0 in range(0, B.n(), _CHUNK):
-            c1 = min(B.n(), c0 + _CHUNK)
-            Bw = _cm_copy(allgather_dense(B.slice(0, B.m() - 1, c0, c1 - 1)), dev)
-            Cp = ops.colmajor_zeros(mC, c1 - c0, dt, dev)
-            for j in s.my_cols():
-                g0, g1 = _stored_rows(s, j)
-                S = _col_block(s, buf, j, g0, g1)
-                cj0, cj1 = s.col_offsets[j], s.col_offsets[j + 1]
-                if tr is None:
-                    ops.gemm(1.0, S, Bw[cj0:cj1], 1.0, Cp[g0:g1])
-                else:
-                    ops.gemm(1.0, S, Bw[g0:g1], 1.0, Cp[cj0:cj1], transA=tr)
-            if s.comm.size > 1:
-                s.comm.allreduce(Cp)
-            _write_cols(C, c0, c1, Cp, alpha, beta)
-        return C
-
-
-def _herm_band_apply(s, buf, Bw, Cp, up):
-    """Cp += A Bw for the Hermitian band A stored (triangle ``up``) in the
-    slabs of this rank: stored part of each column, then its conjugate
-    transpose with the diagonal counted once."""
-    ct = conj_trans(s.dtype)
-    for j in s.my_cols():
-        g0, g1 = _stored_rows(s, j)
-        S = _col_block(s, buf, j, g0, g1)
-        cj0, cj1 = s.col_offsets[j], s.col_offsets[j + 1]
-        ops.gemm(1.0, S, Bw[cj0:cj1], 1.0, Cp[g0:g1])
-        T = ops.colmajor_empty(S.shape[0], S.shape[1], S.dtype, S.device)
-        T.copy_(S)
-        d0 = cj0 - g0
-        ops.geset(0.0, 0.0, T[d0:d0 + (cj1 - cj0)], uplo='U' if up == Uplo.Lower else 'L')
-        ops.gemm(1.0, T, Bw[g0:g1], 1.0, Cp[cj0:cj1], transA=ct)
+        mode = {Op.NoTrans: 'N', Op.Trans: 'T', Op.ConjTrans: 'C'}[opA]
+        return _band_mm(alpha, s, buf, B, beta, C, mode)
 
 
 def hbmm(side, alpha, A, B, beta, C, opts=None):
     """C = alpha A B + beta C (Left) or alpha B A + beta C (Right), A a
-    Hermitian band matrix."""
+    Hermitian band matrix: the stored triangle is read twice (as is and
+    conjugate-transposed, diagonal once), no replication of B."""
     _need_band(A, "hbmm")
-    from .aux import allgather_dense, from_dense
     with trace_block("hbmm"):
         side = Side(side) if not isinstance(side, Side) else side
         kd = A.bandwidth()
         up = A.uploPhysical()
         band_mask(A, kd, 0) if up == Uplo.Lower else band_mask(A, 0, kd)
         s, slot, buf = _slab(A)
-        dev, dt = buf.device, s.dtype
-        n = A.n()
         if side == Side.Left:
-            for c0 in range(0, B.n(), _CHUNK):
-                c1 = min(B.n(), c0 + _CHUNK)
-                Bw = _cm_copy(allgather_dense(B.slice(0, B.m() - 1, c0, c1 - 1)), dev)
-                Cp = ops.colmajor_zeros(n, c1 - c0, dt, dev)
-                _herm_band_apply(s, buf, Bw, Cp, up)
-                if s.comm.size > 1:
-                    s.comm.allreduce(Cp)
-                _write_cols(C, c0, c1, Cp, alpha, beta)
-            return C
-        # Right: C^H = A B^H (A Hermitian), row chunks of B
-        for r0 in range(0, B.m(), _CHUNK):
-            r1 = min(B.m(), r0 + _CHUNK)
-            X = _cm_copy(allgather_dense(B.slice(r0, r1 - 1, 0, B.n() - 1)).mH, dev)
-            Cp = ops.colmajor_zeros(n, r1 - r0, dt, dev)
-            _herm_band_apply(s, buf, X, Cp, up)
-            if s.comm.size > 1:
-                s.comm.allreduce(Cp)
-            Cs = C.slice(r0, r1 - 1, 0, C.n() - 1)
-            D = Cp.mH * alpha + (allgather_dense(Cs).to(dev) * beta if beta != 0 else 0)
-            from_dense(Cs, D)
-        return C
+            return _band_mm(alpha, s, buf, B, beta, C, 'H', up)
+        # Right: C^H = A B^H + ... (A Hermitian)
+        cplx = s.dtype.is_complex
+        tr = (lambda X: X.conj_transpose()) if cplx else (lambda X: X.transpose())
+        cj = (lambda v: complex(v).conjugate()) if cplx else (lambda v: v)
+        return _band_mm(cj(alpha), s, buf, tr(B), cj(beta), tr(C), 'H', up) and C

@@ -103,6 +103,61 @@ def _dist(rank, size, p, q):
     check_band(p, q)
     check_indef(p, q)
     check_hetrf_dist(p, q)
+    check_band_products(p, q)
+
+
+def check_band_products(p=1, q=1):
+    """gbmm (all ops) and hbmm (both sides, both triangles) on any grid:
+    point-to-point band products (no replicated B, no all-reduced C)."""
+    for dt in (torch.float64, torch.complex128):
+        n, nb, kl, ku = 90, 16, 20, 11
+        A = sl.BandMatrix(n, n, kl, ku, nb=nb, p=p, q=q, dtype=dt)
+        A.insertLocalTiles()
+        sl.generate_matrix(A, "rands", 31)
+        sl.band_mask(A)
+        Ad = D(A)
+        for op in (sl.Op.NoTrans, sl.Op.Trans, sl.Op.ConjTrans):
+            B = sl.Matrix(n, 7, nb=nb, p=p, q=q, dtype=dt)
+            B.insertLocalTiles()
+            sl.generate_matrix(B, "rands", 32)
+            C = sl.Matrix(n, 7, nb=nb, p=p, q=q, dtype=dt)
+            C.insertLocalTiles()
+            sl.generate_matrix(C, "rands", 33)
+            Bd, Cd = D(B), D(C)
+            Av = A if op == sl.Op.NoTrans else (A.transpose() if op == sl.Op.Trans else A.conj_transpose())
+            Ao = Ad if op == sl.Op.NoTrans else (Ad.T if op == sl.Op.Trans else Ad.mH)
+            sl.gbmm(2.0, Av, B, 0.5, C)
+            assert (D(C) - (2.0 * Ao @ Bd + 0.5 * Cd)).abs().max() < 1e-12
+        for uplo in (sl.Uplo.Lower, sl.Uplo.Upper):
+            H = sl.HermitianBandMatrix(uplo, n, 13, nb=nb, p=p, q=q, dtype=dt)
+            H.insertLocalTiles()
+            sl.generate_matrix(H, "rands", 34)
+            sl.band_mask(H, 13, 0) if uplo == sl.Uplo.Lower else sl.band_mask(H, 0, 13)
+            Hf = _dense_hermitian(H)
+            for side in (sl.Side.Left, sl.Side.Right):
+                B = sl.Matrix(n, 5, nb=nb, p=p, q=q, dtype=dt) if side == sl.Side.Left else \
+                    sl.Matrix(5, n, nb=nb, p=p, q=q, dtype=dt)
+                B.insertLocalTiles()
+                sl.generate_matrix(B, "rands", 35)
+                C = sl.Matrix(B.m(), B.n(), nb=nb, p=p, q=q, dtype=dt)
+                C.insertLocalTiles()
+                sl.generate_matrix(C, "rands", 36)
+                Bd, Cd = D(B), D(C)
+                sl.hbmm(side, 1.5, H, B, -1.0, C)
+                ref = 1.5 * (Hf @ Bd if side == sl.Side.Left else Bd @ Hf) - Cd
+                assert (D(C) - ref).abs().max() < 1e-12
+
+
+def test_band_products_one_rank():
+    check_band_products()
+
+
+def _dist_prod(rank, size):
+    check_band_products(1, size)
+
+
+def test_band_products_four_ranks():
+    run_dist(_dist_prod, 4)
 
 
 def check_hetrf_dist(p, q):
