@@ -224,7 +224,11 @@ namespace {
 constexpr int TB = 64;            // band / sweeps per block
 constexpr int TCW = 64;           // Z columns per workgroup
 constexpr int SV = TB + 2;        // LDS row pitch of the raw reflectors
-constexpr int SZ = 2 * TB + 4;    // LDS column pitch of the Z window (column-major)
+// LDS column pitch of the Z window (column-major): = 2 (mod 32) doubles, so
+// the B-operand reads Zs[(16 j + li) SZ + row(lk)] of a half-wave (li 0..15,
+// lk 0..1) land on 2 li + lk = 32 distinct bank pairs (2 TB + 4 = 4 mod 32
+// put li and li + 8 on the same banks: 2-way, PMC 57.6 % conflict cycles)
+constexpr int SZ = 2 * TB + 2;
 constexpr int SW = TCW + 16;      // LDS row pitch of W
 }
 

@@ -173,9 +173,14 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
             HSTAMP(1);
             const T tau = s_tau;
             const i64 lo = col + 1, hi = min(n - 1, e + (i64)b);
-            const int KPf = k + 1;
+            // LDS pitch of the staged row block: the next value = 4 (mod 32)
+            // doubles >= k + 1, so the left update's (column, quad-lane) pairs
+            // of a half-wave hit 32 distinct bank pairs (the odd pitch k + 1,
+            // SLATE_AMD_HB2ST_PITCH=odd, collides col + q: ~3-way; PMC 55.6 %
+            // bank-conflict cycles; dsyevd n = 16384: 4.01 -> 3.88 s)
+            const int KPf = ((fused & 2) && sizeof(T) == 8) ? (k + 1) + (((4 - (k + 1)) % 32) + 32) % 32 : k + 1;
             const bool one_chunk = fused && (hi - lo + 1) <= min<i64>(HT, HLDS / ((i64)KPf * (i64)sizeof(T)));
-            if (!s_is_zero(tau) && one_chunk) {
+            if (!s_is_zero(tau) && one_chunk && (fused & 1)) {
                 // ---- fused two-sided update (A Hermitian, both triangles):
                 // ONE load of the row block A(s..e, lo..hi); left update
                 // H^H A on it; the right update A H only changes columns
@@ -377,7 +382,11 @@ void hb2st_device(i64 n, int b, T* A, i64 lda, T* V, T* tau, i64* row, i64* len,
     auto launch = [&](auto kern, int ht) {
         const i64 HLDS = hb_lds_bytes();
         // SLATE_AMD_HB2ST_FUSED=0: separate left / right passes (4 window moves per task instead of 3)
-        static const int fused = [] { const char* e = getenv("SLATE_AMD_HB2ST_FUSED"); return (e && e[0] == '0') ? 0 : 1; }();
+        static const int fused = [] {
+            const char* e = getenv("SLATE_AMD_HB2ST_FUSED");
+            const char* pt = getenv("SLATE_AMD_HB2ST_PITCH");
+            return ((e && e[0] == '0') ? 0 : 1) | ((pt && pt[0] == 'o') ? 0 : 2);   // default: 4 (mod 32)
+        }();
         HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)HLDS));
         hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(ht), HLDS, s, n, b, W, lda, V, tau, row, len,
