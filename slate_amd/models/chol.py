@@ -68,6 +68,28 @@ def potrf(A, opts=None) -> int:
         return _potrf_lower(A, opts)
 
 
+def _maybe_ooc(A, s, slot, la):
+    """Host-origin matrix, device target, one rank, larger than the device
+    budget (or SLATE_AMD_OOC_COLS set): the out-of-core left-looking
+    factorization streams block columns instead of staging the whole local
+    buffer (models/chol_ooc.py).  Returns info, or None for the in-core path."""
+    from ..core.storage import DEV, HOST
+    bc = s.bc
+    if slot != DEV or s.origin_slot != HOST or bc.p * bc.q != 1 or A.ioffset or A.joffset \
+            or A.row0_offset or A.col0_offset or A.last_mb is not None or A.n() != s.n:
+        return None
+    from .chol_ooc import ooc_columns, potrf_ooc
+    dev = torch.device("cuda", torch.cuda.current_device())
+    n = s.n
+    W = ooc_columns(n, bc.nb, s.dtype, dev)
+    if not W or W >= n:
+        return None
+    s.sync_origin()
+    info = potrf_ooc(s.local[HOST][:n, :n], n, bc.nb, W, dev, la)
+    s.mark_local_modified(HOST)
+    return info
+
+
 def _potrf_lower(A, opts):
     s = A.storage
     bc = s.bc
@@ -76,6 +98,9 @@ def _potrf_lower(A, opts):
         return run_on_block_cyclic(A, _potrf_lower, opts)
     slot = target_slot(A, opts)
     la = max(0, int(get_option(opts, Option.Lookahead, 1)))
+    ooc = _maybe_ooc(A, s, slot, la)
+    if ooc is not None:
+        return ooc
     buf = s.prepare_local(slot)
     dev = buf.device
     nb, p, q, pr, pc = bc.nb, bc.p, bc.q, bc.pr, bc.pc

@@ -153,3 +153,20 @@ def test_potrf_use_graph():
     buf[:n, :n].copy_(F0)
     buf[100, 100] = -1.0
     assert sl.potrf(A, {sl.Option.Lookahead: 1, sl.Option.UseGraph: True}) == 101
+
+
+@pytest.mark.parametrize("W", [512, 1536])
+def test_potrf_out_of_core(W, monkeypatch):
+    """Host-origin matrix, device target, forced out-of-core block columns
+    (models/chol_ooc.py): same factor as the in-core path."""
+    monkeypatch.setenv("SLATE_AMD_OOC_COLS", str(W))
+    n, nb = 3000, 256
+    A = sl.HermitianMatrix(sl.Uplo.Lower, n, nb=nb)
+    A.insertLocalTiles()                                # host origin
+    sl.generate_matrix(A, "poev", seed=9)
+    H = A.storage.local[A.storage.origin_slot]
+    S0 = H[:n, :n].clone()
+    assert sl.potrf(A, {sl.Option.Target: sl.Target.Devices}) == 0
+    L = torch.tril(A.storage.local[A.storage.origin_slot][:n, :n])
+    S = torch.tril(S0) + torch.tril(S0, -1).mT
+    assert ((L @ L.mT - S).norm() / S.norm()).item() < 1e-14

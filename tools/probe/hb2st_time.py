@@ -34,6 +34,8 @@ pv = E._HB2ST_PROF.pop("buf").cpu().tolist()
 tot = max(sum(pv), 1)
 print("phases (wait, reflector, left, right, finish):", ", ".join(f"{100 * x / tot:.1f}%" for x in pv),
       f"total {tot:.3e} cycles", flush=True)
+if os.environ.get("HB2ST_PROBE_NOHOST"):
+    sys.exit(0)
 os.environ["SLATE_AMD_HB2ST"] = "host"
 t0 = time.perf_counter()
 d2, e2, F2 = E.hb2st(H, b, device=dev)
