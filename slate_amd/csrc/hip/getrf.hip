@@ -307,14 +307,19 @@ getrf_base_step(i64 m, int c0, int c1, int j, T* A, i64 lda, i64* ipiv, i64 ioff
 // always correct, only slower; g_lu_fallbacks counts such launches.
 constexpr int PG = 64;           // max workgroups (one per CU on the reserved CUs)
 constexpr int PT2 = 512;         // threads per workgroup
+// Launch words: cnt = column arrivals, state = 0/1/2 (above), done = loop
+// completions.  One 32-byte slot per base launch of a panel, all zeroed by ONE
+// memset per panel (not a memset dispatch before every launch).
+constexpr int MAXL = 256;        // base launches per panel (N <= MAXL * NBB)
+struct LaunchWords {
+    unsigned long long cnt, state, done, pad;
+};
 struct PersistBuf {
     double val[2][PG];
     i64 idx[2][PG];
     double cand[2][PG][NBB];
     double diag[2][NBB];
-    unsigned long long cnt;      // column arrivals   } reset before
-    unsigned long long state;    // 0/1/2 (above)     } every launch
-    unsigned long long done;     // loop completions  }
+    LaunchWords lw[MAXL];
 };
 
 // tools only: per-phase shader-clock totals of workgroup 0 (lu_persist_profile)
@@ -336,6 +341,46 @@ __device__ inline void wave_argmax32(double& v, int& i) {
     }
 }
 
+// Wave arg-max with DPP row permutations (quad xor 1, xor 2, half-row and
+// row mirror: every lane of a 16-lane row then holds the row's winner) and
+// four v_readlane of the row winners -- no LDS-crossbar (ds_bpermute)
+// round trips.  Returns the wave winner in every lane (uniform).
+template <int CTRL>
+__device__ inline int dpp_i(int x) { return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, false); }
+template <int CTRL>
+__device__ inline double dpp_d(double x) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, x);
+    const int lo = dpp_i<CTRL>((int)(u & 0xffffffffu)), hi = dpp_i<CTRL>((int)(u >> 32));
+    return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+template <int CTRL>
+__device__ inline void dpp_argmax_step(double& v, int& i, int& g) {
+    const double w = dpp_d<CTRL>(v);
+    const int k = dpp_i<CTRL>(i), h = dpp_i<CTRL>(g);
+    if (beats(w, (i64)k, v, (i64)i)) { v = w; i = k; g = h; }
+}
+__device__ inline double rdlane_d(double x, int l) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, x);
+    const unsigned lo = __builtin_amdgcn_readlane((int)(u & 0xffffffffu), l);
+    const unsigned hi = __builtin_amdgcn_readlane((int)(u >> 32), l);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ inline void wave_argmax_dpp(double& v, int& i, int& g) {
+    dpp_argmax_step<0xB1>(v, i, g);      // quad_perm [1,0,3,2]
+    dpp_argmax_step<0x4E>(v, i, g);      // quad_perm [2,3,0,1]
+    dpp_argmax_step<0x141>(v, i, g);     // row_half_mirror
+    dpp_argmax_step<0x140>(v, i, g);     // row_mirror
+    double bv = rdlane_d(v, 0);
+    int bi = __builtin_amdgcn_readlane(i, 0), bg = __builtin_amdgcn_readlane(g, 0);
+    #pragma unroll
+    for (int r = 1; r < 4; ++r) {
+        const double w = rdlane_d(v, 16 * r);
+        const int k = __builtin_amdgcn_readlane(i, 16 * r), h = __builtin_amdgcn_readlane(g, 16 * r);
+        if (beats(w, (i64)k, bv, (i64)bi)) { bv = w; bi = k; bg = h; }
+    }
+    v = bv; i = bi; g = bg;
+}
+
 __device__ inline double ld_sc1(const double* p) {
     return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -352,13 +397,13 @@ __device__ inline void st_sc1(i64* p, i64 v) {
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ inline unsigned long long ld_state(const PersistBuf* pb) {
-    return __hip_atomic_load(&pb->state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ inline unsigned long long ld_state(const LaunchWords* lw) {
+    return __hip_atomic_load(&lw->state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // CAS running -> to; true if this caller decided the state
-__device__ inline bool decide(PersistBuf* pb, unsigned long long to) {
+__device__ inline bool decide(LaunchWords* lw, unsigned long long to) {
     unsigned long long exp = 0;
-    return __hip_atomic_compare_exchange_strong(&pb->state, &exp, to, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+    return __hip_atomic_compare_exchange_strong(&lw->state, &exp, to, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -480,14 +525,13 @@ __device__ void persist_fallback(i64 m, int w, double* A, i64 lda, int* piv_s, d
 template <int R>
 __global__ void __launch_bounds__(PT2)
 getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64 ioff, i64* info, i64 info_off,
-                   PersistBuf* pb, double thr, int N, int cabs) {
-    __shared__ double wv[PT2 / 64];
-    __shared__ i64 wi[PT2 / 64];
-    __shared__ int wt[PT2 / 64];
-    __shared__ double prow[NBB], drow[NBB];
+                   PersistBuf* pb, LaunchWords* lw, double thr, int N, int cabs) {
+    __shared__ double wv[2 * (PT2 / 64)];          // wave partials, per column parity
+    __shared__ i64 wi[2 * (PT2 / 64)];
+    __shared__ double prow[NBB], drow[NBB], qrow[NBB], ud_s[NBB];
     __shared__ double candL[PG][NBB];
     __shared__ i64 s_p;
-    __shared__ int s_gw, s_bt, s_abort, s_won, s_zero;
+    __shared__ int s_gw, s_abort, s_won, s_zero;
     __shared__ int piv_s[NBB], prv_s[NBB], tr_s[2 * NBB], ts_s[2 * NBB], s_nt;
     const int G = gridDim.x, g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const i64 rbase = (i64)g * PT2 * R;
@@ -510,38 +554,49 @@ getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64
     for (int j = 0; j < w; ++j) {
         const int par = j & 1;
         int jv; asm volatile("v_mov_b32 %0, %1" : "=v"(jv) : "s"(j));
-        // ---- local arg-max of column j over unpivoted rows (i >= j)
+        // ---- local arg-max of column j over unpivoted rows (i >= j); the
+        //      raw column value is kept for the elimination below
         double v = -1.0;
         int bi = (int)(rbase + tid);                  // rows < 2^31
+        double aj[R];
         #pragma unroll
         for (int r = 0; r < R; ++r) {
             const i64 i = rbase + r * PT2 + tid;
-            double aj = 0.0;
+            double x = 0.0;
             #pragma unroll
-            for (int c = 0; c < NBB; ++c) aj = (c == jv) ? a[r][c] : aj;
-            const double vr = (i < m && i >= j) ? fabs(aj) : -1.0;
+            for (int c = 0; c < NBB; ++c) x = (c == jv) ? a[r][c] : x;
+            aj[r] = x;
+            const double vr = (i < m && i >= j) ? fabs(x) : -1.0;
             if (r == 0 || beats(vr, i, v, (i64)bi)) { v = vr; bi = (int)i; }
         }
-        wave_argmax32(v, bi);
-        // winner's thread (and register slot): row - rbase = slot * PT2 + thread
-        if (lane == 0) { wv[wid] = v; wi[wid] = bi; wt[wid] = (int)(bi - rbase); }
-        __syncthreads();
-        if (tid == 0) {
-            double bv = wv[0]; i64 bb = wi[0]; int t = wt[0];
-            for (int k = 1; k < PT2 / 64; ++k)
-                if (beats(wv[k], wi[k], bv, bb)) { bv = wv[k]; bb = wi[k]; t = wt[k]; }
-            s_bt = t;
-            st_sc1(&pb->val[par][g], bv);
-            st_sc1(&pb->idx[par][g], bb);
+        {
+            int dummy = 0;
+            wave_argmax_dpp(v, bi, dummy);
         }
+        // winner's thread (and register slot): row - rbase = slot * PT2 + thread
+        if (lane == 0) { wv[par * 8 + wid] = v; wi[par * 8 + wid] = bi; }
         __syncthreads();
+        // every thread reduces the 8 wave partials (LDS broadcast reads): the
+        // winning thread publishes without a second barrier
+        double bv = wv[par * 8];
+        int bb = (int)wi[par * 8];
+        #pragma unroll
+        for (int k = 1; k < PT2 / 64; ++k) {
+            const double x = wv[par * 8 + k];
+            const int y = (int)wi[par * 8 + k];
+            if (beats(x, (i64)y, bv, (i64)bb)) { bv = x; bb = y; }
+        }
+        const int s_bt_ = bb - (int)rbase;
         LSTAMP(0);                                      // local arg-max
-        // ---- publish the winning row and (owner) row j, write-through
+        // ---- publish the winning row (+ its value and row index) and (owner)
+        //      row j, write-through
         #pragma unroll
         for (int r = 0; r < R; ++r) {
-            if (tid + r * PT2 == s_bt) {
+            if (tid + r * PT2 == s_bt_) {
                 #pragma unroll
                 for (int c = 0; c < NBB; ++c) st_sc1(&pb->cand[par][g][c], a[r][c]);   // all NBB: no uniform branches
+                st_sc1(&pb->val[par][g], bv);
+                st_sc1(&pb->idx[par][g], (i64)bb);
             }
             if (rbase + r * PT2 + tid == j) {
                 #pragma unroll
@@ -552,17 +607,17 @@ getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64
         __syncthreads();
         LSTAMP(1);                                      // publish + drain
         if (tid == 0) {
-            __hip_atomic_fetch_add(&pb->cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&lw->cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned long long target = (unsigned long long)(j + 1) * G;
             int spins = 0;
             const bool force = g_lu_force_abort && g == 0 && j == 0;
-            while (force || __hip_atomic_load(&pb->cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            while (force || __hip_atomic_load(&lw->cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
                 if (force || ++spins > (1 << 22)) {     // not co-resident: abort, never hang
-                    s_won = decide(pb, 2) ? 1 : 0;
+                    s_won = decide(lw, 2) ? 1 : 0;
                     s_abort = 1;
                     break;
                 }
-                if ((spins & 255) == 0 && ld_state(pb) == 2) { s_abort = 1; break; }
+                if ((spins & 255) == 0 && ld_state(lw) == 2) { s_abort = 1; break; }
                 __builtin_amdgcn_s_sleep(1);
             }
         }
@@ -586,9 +641,9 @@ getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64
             }
         }
         if (wid == 0) {
-            double pv = -1.0; i64 pi = j; int pg = -1;
-            if (lane < G) { pv = ld_sc1(&pb->val[par][lane]); pi = ld_sc1(&pb->idx[par][lane]); pg = lane; }
-            wave_argmax(pv, pi, pg);
+            double pv = -1.0; int pi = j; int pg = -1;
+            if (lane < G) { pv = ld_sc1(&pb->val[par][lane]); pi = (int)ld_sc1(&pb->idx[par][lane]); pg = lane; }
+            wave_argmax_dpp(pv, pi, pg);
             if (lane == 0) {
                 i64 p = pi;
                 int gw = pg;
@@ -605,13 +660,25 @@ getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64
         LSTAMP(3);                                      // gather + global arg-max
         const i64 p = s_p;
         const int gw = s_gw;
-        if (tid < w) prow[tid] = (gw < 0) ? drow[tid] : candL[gw][tid];
+        // pivot row, and its trailing part (columns j < c < w; zeros elsewhere)
+        // as the multiplier row of the elimination
+        if (tid < NBB) {
+            const double x = (tid < w) ? ((gw < 0) ? drow[tid] : candL[gw][tid]) : 0.0;
+            prow[tid] = x;
+            qrow[tid] = (tid > j && tid < w) ? x : 0.0;
+        }
         __syncthreads();
+        const double u = prow[j];
         if (tid == 0) {
             piv_s[j] = (int)p;
-            if (prow[j] == 0.0 && zero_at < 0) zero_at = j;     // first exactly-zero pivot (reported at the end)
+            ud_s[j] = u;
+            if (u == 0.0 && zero_at < 0) zero_at = j;     // first exactly-zero pivot (reported at the end)
         }
-        // ---- interchange rows j <-> p and eliminate column j (registers)
+        // ---- interchange rows j <-> p and eliminate column j (registers).
+        // The L entry stays UNSCALED in the register (qrow[j] = 0, so the
+        // update below leaves column j and every factored column untouched:
+        // 32 FMAs per row, no per-column selects); the write-back divides by
+        // the pivot ud_s[c] -- bitwise the l = x / u used here.
         #pragma unroll
         for (int r = 0; r < R; ++r) {
             const i64 i = rbase + r * PT2 + tid;
@@ -620,20 +687,15 @@ getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64
                     #pragma unroll
                     for (int c = 0; c < NBB; ++c) a[r][c] = (c < wv_) ? prow[c] : a[r][c];
                 } else {
+                    double x = aj[r];
                     if (i == p) {
                         #pragma unroll
                         for (int c = 0; c < NBB; ++c) a[r][c] = (c < wv_) ? drow[c] : a[r][c];
+                        x = drow[j];
                     }
-                    const double u = prow[j];
-                    double l = 0.0;
+                    const double l = (u != 0.0) ? x / u : x;
                     #pragma unroll
-                    for (int c = 0; c < NBB; ++c) l = (c == jv) ? a[r][c] : l;
-                    if (u != 0.0) l = l / u;
-                    #pragma unroll
-                    for (int c = 0; c < NBB; ++c) {
-                        const double upd = a[r][c] - l * prow[c];
-                        a[r][c] = (c == jv) ? l : ((c > jv && c < wv_) ? upd : a[r][c]);
-                    }
+                    for (int c = 0; c < NBB; ++c) a[r][c] = fma(-l, qrow[c], a[r][c]);
                 }
             }
         }
@@ -647,14 +709,14 @@ getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64
     // ---- consensus: commit (every workgroup finished the loop) or abort
     if (tid == 0 && !s_abort) {
         const unsigned long long before =
-            __hip_atomic_fetch_add(&pb->done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (before + 1 == (unsigned long long)G) decide(pb, 1);
+            __hip_atomic_fetch_add(&lw->done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (before + 1 == (unsigned long long)G) decide(lw, 1);
         int spins = 0;
-        while (ld_state(pb) == 0) {
-            if (++spins > (1 << 22)) { s_won = decide(pb, 2) ? 1 : 0; break; }
+        while (ld_state(lw) == 0) {
+            if (++spins > (1 << 22)) { s_won = decide(lw, 2) ? 1 : 0; break; }
             __builtin_amdgcn_s_sleep(1);
         }
-        s_abort = ld_state(pb) == 2 ? 1 : 0;
+        s_abort = ld_state(lw) == 2 ? 1 : 0;
     }
     __syncthreads();
     if (s_abort) {
@@ -677,12 +739,20 @@ getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64
         if (tid == 0 && zero_at >= 0 && info)
             atomicCAS(reinterpret_cast<unsigned long long*>(info), 0ull, (unsigned long long)(zero_at + 1 + info_off));
     }
+    // write-back: L entries (row below the column) scaled by their pivot now
     #pragma unroll
     for (int r = 0; r < R; ++r) {
         const i64 i = rbase + r * PT2 + tid;
         if (i < m) {
             #pragma unroll
-            for (int c = 0; c < NBB; ++c) if (c < w) A[i + (i64)c * lda] = a[r][c];
+            for (int c = 0; c < NBB; ++c) {
+                if (c < w) {
+                    double x = a[r][c];
+                    const double d = ud_s[c];
+                    if (i > c && d != 0.0) x = x / d;
+                    A[i + (i64)c * lda] = x;
+                }
+            }
         }
     }
     // ---- the same w interchanges on every OTHER column of the panel, so the
@@ -700,6 +770,7 @@ getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64
 struct PanelCtx {
     i64 N;
     bool full;
+    mutable int launch;          // next base launch's LaunchWords slot
 };
 
 template <typename T>
@@ -714,7 +785,13 @@ static void base(i64 m, int c0, int c1, T* A, i64 lda, i64* ipiv, i64 ioff, i64*
     if constexpr (std::is_same<T, double>::value) {
         if (ctx.full) {
             PersistBuf* pb = reinterpret_cast<PersistBuf*>(static_cast<char*>(w) + PANEL_BYTES);
-            HIP_CHECK(hipMemsetAsync(&pb->cnt, 0, 3 * sizeof(unsigned long long), s));   // cnt, state, done
+            // launch words: zeroed once per panel (getrf_panel_ws); a panel
+            // with more than MAXL base launches wraps and re-zeroes
+            if (ctx.launch >= MAXL) {
+                HIP_CHECK(hipMemsetAsync(pb->lw, 0, sizeof(pb->lw), s));
+                ctx.launch = 0;
+            }
+            LaunchWords* lw = pb->lw + ctx.launch++;
             // rows per thread: 2 by default (SLATE_AMD_LU_RPT = 1 / 2 / 4):
             // half the workgroups of one row per thread -- half the arrivals
             // per column and half the CUs the panel stream reserves (dgetrf
@@ -736,19 +813,19 @@ static void base(i64 m, int c0, int c1, T* A, i64 lda, i64* ipiv, i64 ioff, i64*
             if (rpt != 4 && m <= rpt1_rows && m <= (i64)PG * PT2) {
                 const int G = (int)((m + PT2 - 1) / PT2);
                 hipLaunchKernelGGL(getrf_base_persist<1>, dim3(G), dim3(PT2), 0, s, m, c1, A, lda, ipiv, ioff,
-                                   info, info_off, pb, thr, (int)ctx.N, (int)cabs);
+                                   info, info_off, pb, lw, thr, (int)ctx.N, (int)cabs);
             } else if (rpt == 4 && m <= (i64)PG * PT2 * 4) {
                 const int G = (int)((m + 4 * PT2 - 1) / (4 * PT2));
                 hipLaunchKernelGGL(getrf_base_persist<4>, dim3(G), dim3(PT2), 0, s, m, c1, A, lda, ipiv, ioff,
-                                   info, info_off, pb, thr, (int)ctx.N, (int)cabs);
+                                   info, info_off, pb, lw, thr, (int)ctx.N, (int)cabs);
             } else if (rpt == 1 && m <= (i64)PG * PT2) {
                 const int G = (int)((m + PT2 - 1) / PT2);
                 hipLaunchKernelGGL(getrf_base_persist<1>, dim3(G), dim3(PT2), 0, s, m, c1, A, lda, ipiv, ioff,
-                                   info, info_off, pb, thr, (int)ctx.N, (int)cabs);
+                                   info, info_off, pb, lw, thr, (int)ctx.N, (int)cabs);
             } else {
                 const int G = (int)((m + 2 * PT2 - 1) / (2 * PT2));
                 hipLaunchKernelGGL(getrf_base_persist<2>, dim3(G), dim3(PT2), 0, s, m, c1, A, lda, ipiv, ioff,
-                                   info, info_off, pb, thr, (int)ctx.N, (int)cabs);
+                                   info, info_off, pb, lw, thr, (int)ctx.N, (int)cabs);
             }
             HIP_LAUNCH_CHECK();
             return;
@@ -806,7 +883,11 @@ void getrf_panel_ws(i64 m, i64 n, T* A, i64 lda, i64* ipiv, i64* info, double th
     const i64 k = std::min(m, n);
     // SLATE_AMD_LU_PERSIST=0 disables the persistent base case (diagnostics)
     static const bool persist_env = [] { const char* e = std::getenv("SLATE_AMD_LU_PERSIST"); return !e || e[0] != '0'; }();
-    const PanelCtx ctx{n, persist_env && persist_ok<T>(m, nopiv)};
+    const PanelCtx ctx{n, persist_env && persist_ok<T>(m, nopiv), 0};
+    if (ctx.full) {
+        PersistBuf* pb = reinterpret_cast<PersistBuf*>(static_cast<char*>(w) + PANEL_BYTES);
+        HIP_CHECK(hipMemsetAsync(pb->lw, 0, sizeof(pb->lw), s));
+    }
     rec<T>(m, k, A, lda, ipiv, 0, info, 0, w, thr, nopiv, s, ctx, 0);
     if (n > k) {   // wide panel: U12 = L11^{-1} P A12
         if (!nopiv && !ctx.full) laswp_off<T>(n - k, A + k * lda, lda, 0, k, ipiv, 0, s);
