@@ -212,10 +212,12 @@ INST2(float) INST2(double) INST2(ccplx) INST2(zcplx)
 // Same grouping as above -- G(J,t) = H(j0,t) ... H(j0+b-1,t) in the 2b-row
 // window at j0+1+t b -- but each group is applied as ONE block reflector
 // G = I - V T V^H (forward compact WY, T upper triangular):
-//   W = V^H Z_win (b x CW),  W = T W,  Z_win -= V W,
-// three small GEMMs on v_mfma_f64_16x16x4.  V is the parallelogram of the
-// group's reflectors (reflector jj occupies window rows jj..jj+b-1); T of
-// every group is built once by hb2st_tfac_kernel (one workgroup per group).
+//   W = V^H Z_win (b x CW),  Z_win -= Y W  with Y = V T (2b x b),
+// two small GEMMs on v_mfma_f64_16x16x4.  V is the parallelogram of the
+// group's reflectors (reflector jj occupies window rows jj..jj+b-1); T and
+// Y of every group are built once by hb2st_tfac_kernel (one workgroup per
+// group), so the apply kernel has no T W product (20 % of its MFMA work)
+// and no W round trip through LDS for it.
 //
 // MFMA f64 16x16x4 lane layout: first operand A[i = l & 15][k = l >> 4],
 // second operand B[k = l >> 4][j = l & 15], accumulator register r of lane l
@@ -280,10 +282,18 @@ hb2st_tfac_kernel(const double* __restrict__ V, const double* __restrict__ tau, 
         if (tid == k) Tm[k * (TB + 1) + k] = taus[k];
         __syncthreads();
     }
-    double* To = Tout + g * TB * TB;
-    for (int idx = tid; idx < TB * TB; idx += 256) {
-        const int i = idx % TB, k = idx / TB;           // column-major store
-        To[idx] = Tm[i * (TB + 1) + k];
+    // Y = V T (2 TB x TB): the apply kernel then runs Z -= Y (V^H Z), two
+    // GEMMs instead of three.  Stored in that kernel's MFMA A-operand order:
+    // element (wr, ks, lane) = Y[16 wr + (lane & 15)][4 ks + (lane >> 4)],
+    // wr = 2 wave + row tile, so every prefetch is one coalesced 512-B load.
+    double* Yo = Tout + g * (2 * TB * TB);
+    for (int f = tid; f < 2 * TB * TB; f += 256) {
+        const int lf = f & 63, ks = (f >> 6) & 15, wr = f >> 10;
+        const int row = 16 * wr + (lf & 15), k = 4 * ks + (lf >> 4);
+        double acc = 0.0;
+        for (int l = max(0, row - TB + 1); l <= min(k, row); ++l)
+            acc += Vr[l * SV + (row - l)] * Tm[l * (TB + 1) + k];
+        Yo[f] = acc;
     }
 }
 
@@ -305,7 +315,7 @@ unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const
     // (row lane, column wv + 4 i) of a Z half and reflector element
     // (jj = wv + 4 i, vi = lane) of a group, i < 16
     constexpr int PR = TB * TB / 256;
-    double pv[PR], pt[PR], pz[PR];
+    double pv[PR], py[2 * PR], pz[PR];
     auto fetch_v = [&](i64 t) {
         #pragma unroll
         for (int i = 0; i < PR; ++i) {
@@ -350,9 +360,9 @@ unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const
         __syncthreads();
         fetch_v(0);
         for (i64 t = 0; t < TJ; ++t) {
-            const double* T = Tg + (gptr[J] + t) * TB * TB;
+            const double* Yg = Tg + (gptr[J] + t) * (2 * TB * TB) + (i64)(2 * wv) * 16 * 64 + lane;
             #pragma unroll
-            for (int i = 0; i < PR; ++i) pt[i] = T[(16 * wv + li) + (i64)(4 * i + lk) * TB];
+            for (int i = 0; i < 2 * PR; ++i) py[i] = Yg[i * 64];          // (row tile i / 16, k step i % 16)
             #pragma unroll
             for (int i = 0; i < PR; ++i) Vr[(wv + 4 * i) * SV + lane] = pv[i];
             __syncthreads();
@@ -385,25 +395,7 @@ unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const
                 #pragma unroll
                 for (int r = 0; r < 4; ++r) Ws[(16 * wv + lk + 4 * r) * SW + 16 * j + li] = acc[j][r];
             __syncthreads();
-            // (2) W = T W (T rows of this wave prefetched into pt)
-            #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[j] = d4{0.0, 0.0, 0.0, 0.0};
-            #pragma unroll
-            for (int i = 0; i < PR; ++i) {
-                const int kk = 4 * i + lk;
-                #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const double b = Ws[kk * SW + 16 * j + li];
-                    acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(pt[i], b, acc[j], 0, 0, 0);
-                }
-            }
-            __syncthreads();
-            #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                #pragma unroll
-                for (int r = 0; r < 4; ++r) Ws[(16 * wv + lk + 4 * r) * SW + 16 * j + li] = acc[j][r];
-            __syncthreads();
-            // (3) Z -= V W: wave wv owns window rows 32 wv..32 wv+31 (2 x 4 tiles)
+            // (2) Z -= Y W: wave wv owns window rows 32 wv..32 wv+31 (2 x 4 tiles)
             #pragma unroll
             for (int ri = 0; ri < 2; ++ri) {
                 d4 zc[4];
@@ -412,10 +404,10 @@ unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const
                 for (int j = 0; j < 4; ++j)
                     #pragma unroll
                     for (int r = 0; r < 4; ++r) zc[j][r] = Zs[(16 * j + li) * SZ + zrow(wb + lk + 4 * r, t)];
-                #pragma unroll 4
+                #pragma unroll
                 for (int k0 = 0; k0 < TB; k0 += 4) {
                     const int jj = k0 + lk;
-                    const double a = -vg(wb + li, jj);
+                    const double a = -py[ri * 16 + k0 / 4];
                     #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const double b = Ws[jj * SW + 16 * j + li];

@@ -120,7 +120,13 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
         i64 s = j + 1, e = min(j + (i64)b, n - 1), col = j;
         for (i64 t = 0; t < nt; ++t) {
             if (j > 0) {
-                const i64 need = min(t + (i64)D, ntask[j - 1]);
+                // early mode (fused & 8): done[j-1] = u + 1 says sweep j-1
+                // finished tasks < u and PUBLISHED task u's annihilated
+                // entries (see below); task t needs tasks <= t+1 finished and
+                // task t+2 published (all tasks if sweep j-1 has no t+2)
+                const i64 ntp = ntask[j - 1];
+                const i64 need = (fused & 8) ? (ntp == 0 ? 0 : (t + 2 < ntp ? t + 3 : ntp + 1))
+                                             : min(t + (i64)D, ntp);
                 // poll with relaxed loads (an acquire per poll would invalidate
                 // the XCD's L2 every time, thrashing the working sweeps), then
                 // ONE acquire fence
@@ -133,6 +139,25 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
             HSTAMP(0);
             if (t > 0) { s = e + 1; e = min(e + (i64)b, n - 1); }
             const int k = (int)(e - s + 1);
+            const i64 lo = col + 1, hi = min(n - 1, e + (i64)b);
+            // LDS pitch of the staged row block: the next value = 4 (mod 32)
+            // doubles >= k + 1, so the left update's (column, quad-lane) pairs
+            // of a half-wave hit 32 distinct bank pairs (the odd pitch k + 1,
+            // SLATE_AMD_HB2ST_PITCH=odd, collides col + q: ~3-way; PMC 55.6 %
+            // bank-conflict cycles; dsyevd n = 16384: 4.01 -> 3.88 s)
+            const int KPf = ((fused & 2) && sizeof(T) == 8) ? (k + 1) + (((4 - (k + 1)) % 32) + 32) % 32 : k + 1;
+            const bool one_chunk = fused && (hi - lo + 1) <= min<i64>(HT, HLDS / ((i64)KPf * (i64)sizeof(T)));
+            const bool fuse = one_chunk && (fused & 1);
+            // fused path: the row block A(s..e, lo..hi) does not depend on the
+            // reflector, so its load is issued BEFORE wave 0 loads the column
+            // -- one memory round trip per task instead of two in sequence
+            // (a task whose reflector turns out trivial just drops it)
+            if (fuse) {
+                const int nc = (int)(hi - lo + 1);
+                T* Ab = &At(s, lo);
+                move2d<T, HT / 64>(k, nc, lane, w, [&](int r, int c) -> T { return Ab[r + c * lda]; },
+                                   [&](int r, int c) -> T& { return L[c * KPf + r]; });
+            }
             // ---- reflector (wave 0): x = A(s..e, col)
             if (w == 0) {
                 T x0 = s_zero(T());
@@ -167,20 +192,29 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
                     if (r == 0) v[0] = s_from_real(T(), R(1));
                     else if (!trivial) v[r] = s_div(v[r], den);
                 }
-                if (lane == 0) { s_tau = tau; s_beta = beta; }
+                if (lane == 0) {
+                    s_tau = tau; s_beta = beta;
+                    if (fused & 8) {
+                        // Early publication.  Task (j+1, t-2) -- the one
+                        // that waits for this task -- shares exactly two
+                        // entries with it: A(s, col) and A(col, s) (its
+                        // window is [col' .. s] with col' = col - b + 1;
+                        // this task writes rows s..e / columns lo = col + 1..
+                        // of its row block, their mirror and the column
+                        // below/right of (s, col)).  So once this column is
+                        // read and those two entries hold beta, the next
+                        // sweep may go; tasks < t finished (their stores
+                        // drained at their final barrier).
+                        At(s, col) = s_from_real(T(), beta);
+                        At(col, s) = s_from_real(T(), beta);
+                        __hip_atomic_store(&done[j], (int)(t + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
             }
             __syncthreads();
             HSTAMP(1);
             const T tau = s_tau;
-            const i64 lo = col + 1, hi = min(n - 1, e + (i64)b);
-            // LDS pitch of the staged row block: the next value = 4 (mod 32)
-            // doubles >= k + 1, so the left update's (column, quad-lane) pairs
-            // of a half-wave hit 32 distinct bank pairs (the odd pitch k + 1,
-            // SLATE_AMD_HB2ST_PITCH=odd, collides col + q: ~3-way; PMC 55.6 %
-            // bank-conflict cycles; dsyevd n = 16384: 4.01 -> 3.88 s)
-            const int KPf = ((fused & 2) && sizeof(T) == 8) ? (k + 1) + (((4 - (k + 1)) % 32) + 32) % 32 : k + 1;
-            const bool one_chunk = fused && (hi - lo + 1) <= min<i64>(HT, HLDS / ((i64)KPf * (i64)sizeof(T)));
-            if (!s_is_zero(tau) && one_chunk && (fused & 1)) {
+            if (!s_is_zero(tau) && fuse) {
                 // ---- fused two-sided update (A Hermitian, both triangles):
                 // ONE load of the row block A(s..e, lo..hi); left update
                 // H^H A on it; the right update A H only changes columns
@@ -191,9 +225,8 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
                 const T ct = s_conj(tau);
                 const int nc = (int)(hi - lo + 1), d0 = (int)(s - lo);
                 T* Ab = &At(s, lo);
-                move2d<T, HT / 64>(k, nc, lane, w, [&](int r, int c) -> T { return Ab[r + c * lda]; },
-                                   [&](int r, int c) -> T& { return L[c * KPf + r]; });
-                __syncthreads();
+                // (the row block was staged before the reflector; the
+                // barrier after the reflector covers its LDS writes)
                 // left: four lanes per column (rows q, q + 4, ...), partial
                 // dot products combined by two xor shuffles inside the quad
                 for (int e = tid; e < 4 * nc; e += HT) {
@@ -333,7 +366,9 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
             // ---- annihilated column / row, reflector slot
             const R beta = s_beta;
             const i64 slot = sweep_ptr[j] + t;
-            for (int r = tid; r < k; r += HT) {
+            // (early mode: (s, col) was stored at publication and may since
+            // have been updated by sweep j+1 -- not rewritten)
+            for (int r = ((fused & 8) ? 1 : 0) + tid; r < k; r += HT) {
                 const T val = (r == 0) ? s_from_real(T(), beta) : s_zero(T());
                 At(s + r, col) = val;
                 At(col, s + r) = val;
@@ -341,8 +376,9 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
             for (int r = tid; r < b; r += HT) V[slot * b + r] = (r < k) ? v[r] : s_zero(T());
             if (tid == 0) { tauv[slot] = tau; rowv[slot] = s; lenv[slot] = k; }
             __syncthreads();                                    // all waves' stores issued and complete
-            if (tid == 0)                                        // one release: writes back this XCD's L2
-                __hip_atomic_store(&done[j], (int)(t + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            if (tid == 0 && (!(fused & 8) || t + 1 == nt))      // one release: writes back this XCD's L2
+                __hip_atomic_store(&done[j], (int)((fused & 8) ? nt + 1 : t + 1), __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_AGENT);
             HSTAMP(4);
             col = s;
         }
@@ -382,15 +418,31 @@ void hb2st_device(i64 n, int b, T* A, i64 lda, T* V, T* tau, i64* row, i64* len,
     auto launch = [&](auto kern, int ht) {
         const i64 HLDS = hb_lds_bytes();
         // SLATE_AMD_HB2ST_FUSED=0: separate left / right passes (4 window moves per task instead of 3)
-        static const int fused = [] {
+        const int fused = [] {
             const char* e = getenv("SLATE_AMD_HB2ST_FUSED");
             const char* pt = getenv("SLATE_AMD_HB2ST_PITCH");
-            return ((e && e[0] == '0') ? 0 : 1) | ((pt && pt[0] == 'o') ? 0 : 2);   // default: 4 (mod 32)
+            const char* ea = getenv("SLATE_AMD_HB2ST_EARLY");
+            return ((e && e[0] == '0') ? 0 : 1) | ((pt && pt[0] == 'o') ? 0 : 2) |  // default: 4 (mod 32)
+                   ((ea && ea[0] == '0') ? 0 : 8);                                   // early publication
         }();
         HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)HLDS));
+        // lag: sweep j runs task t once sweep j-1 finished t + lag tasks.
+        // Task t of sweep j touches rows/columns [j+1+(t-1)b, j+(t+2)b]; task
+        // t' of sweep j-1 touches [j+(t'-1)b, j-1+(t'+2)b]: they share
+        // indices only for t' <= t + 3, and at t' = t + 3 only index
+        // j+(t+2)b, which the two tasks use in disjoint rows / columns
+        // (sweep j: rows s..e <= j+(t+1)b of column hi and their mirror;
+        // sweep j-1: rows >= j+(t+3)b of its column col' = hi) -- so lag 3
+        // keeps the sequential order (SLATE_AMD_HB2ST_LAG, default 3; 4 was
+        // the conservative choice of round 2)
+        const int lag = [] {
+            const char* e = getenv("SLATE_AMD_HB2ST_LAG");
+            const int v = e ? atoi(e) : 3;
+            return v < 3 ? 3 : v;
+        }();
         hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(ht), HLDS, s, n, b, W, lda, V, tau, row, len,
-                           sweep_ptr, ntask, work, work + 1, nsw, 4, prof, HLDS, fused);
+                           sweep_ptr, ntask, work, work + 1, nsw, lag, prof, HLDS, fused);
     };
     if (threads == 1024) launch(hb2st_kernel<T, 1024>, 1024);
     else if (threads == 512) launch(hb2st_kernel<T, 512>, 512);

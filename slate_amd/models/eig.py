@@ -185,7 +185,12 @@ def _hb2st_device(B: torch.Tensor, nb: int, dev):
     # sweeps in flight are bounded by (tasks of a sweep) / lag: more
     # workgroups would only poll
     nt0 = int(nt[0]) if nt.numel() else 1
-    nwg = int(min(max(nsw, 1), props.multi_processor_count, max(8, nt0 // 4 + 8)))
+    # = the kernel's (hb2st.hip): early publication keeps sweeps 2 tasks
+    # apart, else `lag` tasks
+    lag = max(3, int(os.environ.get("SLATE_AMD_HB2ST_LAG", 3)))
+    if os.environ.get("SLATE_AMD_HB2ST_EARLY", "1") != "0":
+        lag = 2
+    nwg = int(min(max(nsw, 1), props.multi_processor_count, max(8, nt0 // lag + 8)))
     nwg = int(os.environ.get("SLATE_AMD_HB2ST_WG", nwg))
     with trace_block("hb2st"):
         if nsw > 0:
@@ -264,7 +269,7 @@ def unmtr_hb2st(F: Hb2stFactors, Z: torch.Tensor):
             gptr = torch.zeros(TJ.numel() + 1, dtype=torch.int64, device=dev)
             gptr[1:] = torch.cumsum(TJ, 0)
             gt = torch.arange(ng, device=dev) - gptr[gJ]
-            Tg = torch.empty(max(ng, 1) * b * b, dtype=torch.float64, device=dev)
+            Tg = torch.empty(max(ng, 1) * 2 * b * b, dtype=torch.float64, device=dev)   # Y = V T per group
             with trace_block("unmtr_hb2st"):
                 _native.hip().unmtr_hb2st_mfma(n, Z.shape[1], Z.data_ptr(), max(1, Z.stride(1)),
                                                V.contiguous().data_ptr(), b, tau.contiguous().data_ptr(),

@@ -120,6 +120,11 @@ def _getrf_p1(A, buf, thr, la, nopiv):
     left = []
     import os
     tail = int(kt * float(os.environ.get("SLATE_AMD_LU_LEFT_TAIL", "0.6")))
+    # GEMM-bound first steps (SLATE_AMD_LU_UNMASKED = fraction of the steps,
+    # default 0): their trailing update runs on the unmasked diag stream --
+    # all CUs -- while the panel still has slack; the CU-masked update
+    # stream takes over where the panel chain becomes critical
+    unmasked = int(kt * float(os.environ.get("SLATE_AMD_LU_UNMASKED", "0"))) if ss.gpu else 0
     ss.fork()
     for k in range(kt):
         _wd.beat(f"getrf step {k}")
@@ -158,7 +163,9 @@ def _getrf_p1(A, buf, thr, la, nopiv):
             if lcla > lc1:
                 _update_cols(buf, Lp, ipiv, r0, kb, m, lc1, lcla, nopiv)
             ev_panel = ss.event(ss.panel)
-        us = ss.update[0]
+        us = ss.diag if k < unmasked else ss.update[0]
+        if k == unmasked and unmasked > 0:
+            ss.wait(us, ss.event(ss.diag))      # the earlier updates touch the same columns
         with ss.use(us):
             ss.wait(us, ev_panel)
             if nloc > lcla and Lp.is_cuda:

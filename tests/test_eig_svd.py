@@ -453,3 +453,29 @@ def test_stedc_rows_one_rank():
     T = torch.diag(torch.from_numpy(d)) + torch.diag(torch.from_numpy(e), 1) + torch.diag(torch.from_numpy(e), -1)
     assert (r0, r1) == (0, n)
     assert float((T @ Q - Q * w).abs().max()) < 1e-12 * n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("early,lag", [("1", "3"), ("0", "3"), ("0", "4")])
+def test_hb2st_gpu_matches_host_chase(early, lag, monkeypatch):
+    """The pipelined GPU chase equals the sequential host chase up to the
+    summation order inside a task: a dependency rule (early publication of
+    a task's annihilated entries, or a lag of whole tasks) that let
+    overlapping tasks of two sweeps run out of order would change the
+    tridiagonal entries, not only round them (n = 2000 with b = 64: 31 tasks
+    in the first sweep, up to ~24 sweeps in flight)."""
+    monkeypatch.setenv("SLATE_AMD_HB2ST_EARLY", early)
+    monkeypatch.setenv("SLATE_AMD_HB2ST_LAG", lag)
+    n, b = 2000, 64
+    g = torch.Generator().manual_seed(11)
+    X = torch.randn(n, n, generator=g, dtype=torch.float64)
+    H = X + X.T
+    i = torch.arange(n)
+    H = torch.where((i[:, None] - i[None, :]).abs() <= b, H, torch.zeros_like(H))
+    monkeypatch.setenv("SLATE_AMD_HB2ST", "device")
+    d, e, _ = E.hb2st(H.clone(), b, device=torch.device("cuda"))
+    monkeypatch.setenv("SLATE_AMD_HB2ST", "host")
+    d2, e2, _ = E.hb2st(H.clone(), b, device=torch.device("cuda"))
+    scale = H.abs().max().item()
+    assert (d.cpu() - d2.cpu()).abs().max().item() / scale < 1e-11
+    assert (e.cpu().abs() - e2.cpu().abs()).abs().max().item() / scale < 1e-11

@@ -299,7 +299,7 @@ def test_getrf_panel_persistent_abort_reports_singular():
     assert int(info.item()) == 8
 
 
-@pytest.mark.parametrize("m,n", [(16, 1), (100, 50), (256, 300), (512, 4000), (1000, 70)])
+@pytest.mark.parametrize("m,n", [(16, 1), (32, 32), (45, 7), (64, 64), (64, 1000), (100, 50), (256, 300), (512, 4000), (1000, 70)])
 @pytest.mark.parametrize("unit", [False, True])
 def test_trsm_lln_fp64_fast(m, n, unit):
     # L X = alpha B (lower, no-trans): one-launch blocked-inverse MFMA kernel
