@@ -115,6 +115,11 @@ static void register_kernels(py::module& m) {
         dispatch(dt, [&](auto z) { using T = decltype(z);
             getrf_panel_ws<T>(mm, n, P<T>(A), lda, P<i64>(ipiv), P<i64>(info), thr, nopiv, (void*)work, S(st)); });
     });
+    m.def("tri_inv", [](char dt, char uplo, char diag, i64 n, uintptr_t A, i64 lda, uintptr_t W, i64 ldw,
+                        uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            tri_inv<T>(uplo, diag, n, P<const T>(A), lda, P<T>(W), ldw, S(st)); });
+    });
     m.def("trtri", [](char dt, char uplo, char diag, i64 n, uintptr_t A, i64 lda, uintptr_t info, uintptr_t st) {
         dispatch(dt, [&](auto z) { using T = decltype(z);
             trtri<T>(uplo, diag, n, P<T>(A), lda, P<i64>(info), S(st)); });

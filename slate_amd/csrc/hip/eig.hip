@@ -379,8 +379,10 @@ unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const
             d4 acc[4];
             #pragma unroll
             for (int j = 0; j < 4; ++j) acc[j] = d4{0.0, 0.0, 0.0, 0.0};
+            // reflectors 16 wv..16 wv+15 are zero outside window rows
+            // 16 wv..16 wv+78: 20 of the 32 k-steps (V is a parallelogram)
             #pragma unroll 4
-            for (int k0 = 0; k0 < 2 * TB; k0 += 4) {
+            for (int k0 = 16 * wv; k0 < 16 * wv + TB + 16; k0 += 4) {
                 const int w = k0 + lk;
                 const double a = vg(w, 16 * wv + li);
                 const int pr = zrow(w, t);
@@ -395,29 +397,38 @@ unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const
                 #pragma unroll
                 for (int r = 0; r < 4; ++r) Ws[(16 * wv + lk + 4 * r) * SW + 16 * j + li] = acc[j][r];
             __syncthreads();
-            // (2) Z -= Y W: wave wv owns window rows 32 wv..32 wv+31 (2 x 4 tiles)
-            #pragma unroll
-            for (int ri = 0; ri < 2; ++ri) {
-                d4 zc[4];
-                const int wb = 32 * wv + 16 * ri;
+            // (2) Z -= Y W: wave wv owns window rows 32 wv..32 wv+31 (2 x 4
+            // tiles); each W fragment read from LDS feeds both row tiles
+            {
+                d4 zc[2][4];
                 #pragma unroll
-                for (int j = 0; j < 4; ++j)
+                for (int ri = 0; ri < 2; ++ri)
                     #pragma unroll
-                    for (int r = 0; r < 4; ++r) zc[j][r] = Zs[(16 * j + li) * SZ + zrow(wb + lk + 4 * r, t)];
+                    for (int j = 0; j < 4; ++j)
+                        #pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            zc[ri][j][r] = Zs[(16 * j + li) * SZ + zrow(32 * wv + 16 * ri + lk + 4 * r, t)];
                 #pragma unroll
                 for (int k0 = 0; k0 < TB; k0 += 4) {
                     const int jj = k0 + lk;
-                    const double a = -py[ri * 16 + k0 / 4];
+                    double bw[4];
                     #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const double b = Ws[jj * SW + 16 * j + li];
-                        zc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, zc[j], 0, 0, 0);
+                    for (int j = 0; j < 4; ++j) bw[j] = Ws[jj * SW + 16 * j + li];
+                    #pragma unroll
+                    for (int ri = 0; ri < 2; ++ri) {
+                        const double a = -py[ri * 16 + k0 / 4];
+                        #pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            zc[ri][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bw[j], zc[ri][j], 0, 0, 0);
                     }
                 }
                 #pragma unroll
-                for (int j = 0; j < 4; ++j)
+                for (int ri = 0; ri < 2; ++ri)
                     #pragma unroll
-                    for (int r = 0; r < 4; ++r) Zs[(16 * j + li) * SZ + zrow(wb + lk + 4 * r, t)] = zc[j][r];
+                    for (int j = 0; j < 4; ++j)
+                        #pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            Zs[(16 * j + li) * SZ + zrow(32 * wv + 16 * ri + lk + 4 * r, t)] = zc[ri][j][r];
             }
             __syncthreads();
             if (more) {

@@ -30,12 +30,33 @@ __global__ void splitk_reduce_kernel(i64 m, i64 n, int ks, const T* __restrict__
     }
 }
 
+// below this many 128 x 128 tiles (x batch) fp64 GEMMs use 64 x 64 tiles:
+// the trailing updates near the end of a factorization would otherwise leave
+// each CU with one or two workgroups, too few waves to hide the MFMA / LDS
+// latency (measured: masked 4096^2 x 512 update at 29 TF/s with 128 x 128).
+// SLATE_AMD_GEMM_SMALL overrides (0 = always 128 x 128).
+static inline i64 gemm_small_tiles() {
+    static const i64 v = [] {
+        const char* e = std::getenv("SLATE_AMD_GEMM_SMALL");
+        return e ? (i64)std::atoll(e) : (i64)2048;
+    }();
+    return v;
+}
+
 template <typename T, typename Launch>
 static bool gemm_splitk(const GemmCall& c, int tile, hipStream_t s, Launch&& launch) {
     if (!c.allow_split || c.batch != 1 || c.Aptrs || c.mask.mode != 0) return false;
     const i64 tiles = ((c.m + tile - 1) / tile) * ((c.n + tile - 1) / tile);
-    if (tiles >= 256 || c.k < 2048 || c.k < 8 * std::max(c.m, c.n)) return false;
-    i64 ks = std::min<i64>(c.k / 512, (512 + tiles - 1) / tiles);
+    // (b) fp64 outputs of at most 512 64 x 64 tiles (the 64 x 64 kernel: one
+    // or two workgroups per CU) with a long K, e.g. the 64-row V^H Z products
+    // of the eigensolver back-transforms (64 x 16384 x K, K up to n): split K
+    // until there are ~1024 workgroups; the m n ks partial-sum traffic is
+    // small next to the 2 m n k flops once k >= 4096
+    const i64 t64 = ((c.m + 63) / 64) * ((c.n + 63) / 64);
+    const bool wide = std::is_same<T, double>::value && t64 <= 512 && c.k >= 4096 && tiles < gemm_small_tiles();
+    if (!wide && (tiles >= 256 || c.k < 2048 || c.k < 8 * std::max(c.m, c.n))) return false;
+    i64 ks = wide ? std::min<i64>(c.k / 1024, (1024 + t64 - 1) / t64)
+                  : std::min<i64>(c.k / 512, (512 + tiles - 1) / tiles);
     if (ks < 2) return false;
     const i64 kc = ((c.k + ks - 1) / ks + 63) / 64 * 64;
     const i64 full = c.k / kc, rem = c.k - full * kc;
@@ -72,18 +93,6 @@ static bool gemm_splitk(const GemmCall& c, int tile, hipStream_t s, Launch&& lau
     return true;
 }
 
-// below this many 128 x 128 tiles (x batch) fp64 GEMMs use 64 x 64 tiles:
-// the trailing updates near the end of a factorization would otherwise leave
-// each CU with one or two workgroups, too few waves to hide the MFMA / LDS
-// latency (measured: masked 4096^2 x 512 update at 29 TF/s with 128 x 128).
-// SLATE_AMD_GEMM_SMALL overrides (0 = always 128 x 128).
-static inline i64 gemm_small_tiles() {
-    static const i64 v = [] {
-        const char* e = std::getenv("SLATE_AMD_GEMM_SMALL");
-        return e ? (i64)std::atoll(e) : (i64)2048;
-    }();
-    return v;
-}
 
 // Lower-triangular masks (the potrf/herk trailing updates) launch only the
 // 8 x 8 super-tiles on or below the tile diagonal, XCD-remapped (remap = 2 in

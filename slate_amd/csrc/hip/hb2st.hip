@@ -152,6 +152,16 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
             // reflector, so its load is issued BEFORE wave 0 loads the column
             // -- one memory round trip per task instead of two in sequence
             // (a task whose reflector turns out trivial just drops it)
+            // wave 0 issues its column loads (k <= 128 rows: two per lane)
+            // before its share of the row block, so both are in flight at once
+            T xc[HMAXB / 64];
+            if (w == 0) {
+                #pragma unroll
+                for (int u = 0; u < HMAXB / 64; ++u) {
+                    const int r = lane + 64 * u;
+                    xc[u] = (r < k) ? At(s + r, col) : s_zero(T());
+                }
+            }
             if (fuse) {
                 const int nc = (int)(hi - lo + 1);
                 T* Ab = &At(s, lo);
@@ -163,7 +173,7 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
                 T x0 = s_zero(T());
                 R xn2 = 0;
                 for (int r = lane; r < k; r += 64) {
-                    const T x = At(s + r, col);
+                    const T x = xc[r >> 6];
                     v[r] = x;
                     if (r == 0) x0 = x;
                     else xn2 += s_real(s_mul(s_conj(x), x));

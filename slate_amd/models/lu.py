@@ -125,6 +125,10 @@ def _getrf_p1(A, buf, thr, la, nopiv):
     # all CUs -- while the panel still has slack; the CU-masked update
     # stream takes over where the panel chain becomes critical
     unmasked = int(kt * float(os.environ.get("SLATE_AMD_LU_UNMASKED", "0"))) if ss.gpu else 0
+    # trailing widths of at least SLATE_AMD_LU_INV_MIN local columns solve
+    # their U rows with the explicit L11 inverse (one GEMM; 0 = never;
+    # dgetrf n = 32768 on one MI355X: 0 / 2048 / 8192 -> 39.4 / 40.3 / 40.4 TF/s)
+    inv_min = int(os.environ.get("SLATE_AMD_LU_INV_MIN", "4096")) if ss.gpu and not nopiv else 0
     ss.fork()
     for k in range(kt):
         _wd.beat(f"getrf step {k}")
@@ -156,12 +160,15 @@ def _getrf_p1(A, buf, thr, la, nopiv):
                     if not nopiv:
                         grid.row_comm.bcast(piv, k % q)
                     bcast_tile(grid.row_comm, Lp, k % q)
+            Linv = None
+            if inv_min and nloc - lcla >= inv_min and kb == nb:
+                Linv = ops.tri_inv('L', 'U', Lp[0:kb, 0:kb])
             # lookahead columns; the newest one (k+la) was the first part of
             # step k-1's trailing update
             if k >= 1 and la > 0:
                 ss.wait(ss.panel, ev_tr[k - 1])
             if lcla > lc1:
-                _update_cols(buf, Lp, ipiv, r0, kb, m, lc1, lcla, nopiv)
+                _update_cols(buf, Lp, ipiv, r0, kb, m, lc1, lcla, nopiv, Linv)
             ev_panel = ss.event(ss.panel)
         us = ss.diag if k < unmasked else ss.update[0]
         if k == unmasked and unmasked > 0:
@@ -170,15 +177,17 @@ def _getrf_p1(A, buf, thr, la, nopiv):
             ss.wait(us, ev_panel)
             if nloc > lcla and Lp.is_cuda:
                 Lp.record_stream(us)
+                if Linv is not None:
+                    Linv.record_stream(us)
             # column k+1+la first (next step's newest lookahead column), event,
             # then the rest
             lcnx = max(min(tiles_local_before(k + 2 + la, q, pc) * nb, nloc), lcla)
             with trace_block("getrf::trailing"):
                 if lcnx > lcla:
-                    _update_cols(buf, Lp, ipiv, r0, kb, m, lcla, lcnx, nopiv)
+                    _update_cols(buf, Lp, ipiv, r0, kb, m, lcla, lcnx, nopiv, Linv)
                 ev_tr[k] = ss.event(us)
                 if nloc > lcnx:
-                    _update_cols(buf, Lp, ipiv, r0, kb, m, lcnx, nloc, nopiv)
+                    _update_cols(buf, Lp, ipiv, r0, kb, m, lcnx, nloc, nopiv, Linv)
             # swap the already-factored left columns (tiles < k).  This runs
             # on the update stream, after every trailing update that still
             # reads an earlier panel's L rows (trailing j < k overlaps panel
@@ -213,13 +222,21 @@ def _global_pivots(ipiv, nb):
     return ipiv + torch.div(idx, nb, rounding_mode="floor") * nb
 
 
-def _update_cols(buf, Lp, ipiv, r0, kb, m, c0, c1, nopiv):
-    """Apply step pivots, U-row trsm and the GEMM update to local columns [c0, c1)."""
+def _update_cols(buf, Lp, ipiv, r0, kb, m, c0, c1, nopiv, Linv=None):
+    """Apply step pivots, U-row trsm and the GEMM update to local columns [c0, c1).
+    With Linv (the explicit inverse of the unit-lower L11, |L| <= 1 under
+    partial pivoting) the U rows are one MFMA GEMM, U12 = Linv P A12, instead
+    of the latency-bound blocked substitution."""
     cols = buf[:m, c0:c1]
     if not nopiv:
         ops.laswp(cols, ipiv, r0, r0 + kb, ioff=-r0)
     Ukk = buf[r0:r0 + kb, c0:c1]
-    ops.trsm('L', 'L', 'N', 'U', 1.0, Lp[0:kb, 0:kb], Ukk)
+    if Linv is not None:
+        tmp = ops.colmajor_empty(kb, c1 - c0, Ukk.dtype, Ukk.device)
+        ops.gecopy(Ukk, tmp)
+        ops.gemm(1.0, Linv, tmp, 0.0, Ukk)
+    else:
+        ops.trsm('L', 'L', 'N', 'U', 1.0, Lp[0:kb, 0:kb], Ukk)
     if m > r0 + kb:
         ops.gemm(-1.0, Lp[kb:, :], Ukk, 1.0, buf[r0 + kb:m, c0:c1])
 

@@ -268,6 +268,19 @@ def sel_to_ipiv(sel, r0, ipiv):
     return ipiv
 
 
+def tri_inv(uplo, diag, A, W=None):
+    """W = inverse of the uplo triangle of A (diag 'U': unit, A's diagonal
+    not read); A untouched.  W: n x n column-major (allocated if None), its
+    other triangle zero."""
+    _chk(A)
+    n = A.shape[0]
+    if W is None:
+        W = colmajor_empty(n, n, A.dtype, A.device)
+    if n:
+        kmod(A).tri_inv(code(A.dtype), _ch(uplo), _ch(diag), n, A.data_ptr(), ld(A), W.data_ptr(), ld(W), stream(A))
+    return W
+
+
 def trtri(uplo, diag, A, info=None):
     _chk(A)
     if info is None:

@@ -51,12 +51,14 @@ def test_gemm(dt, ta, tb):
 
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("tt", ["TN", "NN", "NT"])
-def test_gemm_splitk(dt, tt):
-    # few output tiles + long k -> split-K path (+ ragged last chunk)
+@pytest.mark.parametrize("mnk", [(200, 96, 20000 + 37), (64, 4100, 6000 + 13), (3000, 64, 4096)])
+def test_gemm_splitk(dt, tt, mnk):
+    # few output tiles + long k -> split-K path (+ ragged last chunk); the
+    # wide 64-row / 64-column shapes take the fp64 split for <= 512 64 x 64 tiles
     ta, tb = tt[0], tt[1]
     if dt.is_complex:
         ta = 'C' if ta == 'T' else ta
-    m, n, k = 200, 96, 20000 + 37
+    m, n, k = mnk
     A = cm(k, m, dt, 1) if ta != 'N' else cm(m, k, dt, 1)
     B = cm(n, k, dt, 2) if tb != 'N' else cm(k, n, dt, 2)
     C = cm(m, n, dt, 3)

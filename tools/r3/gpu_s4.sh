@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 D=gpurun_out/${TAG:-s4}; mkdir -p $D
-timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_native_gpu.py tests/test_nosync_gpu.py tests/test_eig_svd.py -m gpu -x -q --timeout 120 --timeout-method thread -k "getrf or lu or gesv or hb2st or heev or unmtr" > $D/pytest.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_native_gpu.py tests/test_nosync_gpu.py tests/test_eig_svd.py -m gpu -x -q --timeout 120 --timeout-method thread -k "getrf or lu or gesv or hb2st or heev or unmtr or trsm" > $D/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 $D/pytest.log
 [ $rc -ne 0 ] && exit 1
 timeout -k 10 200 python -u tools/probe/lu_panel_time.py > $D/lu_panel_time.log 2>&1 || { tail $D/lu_panel_time.log; exit 1; }
