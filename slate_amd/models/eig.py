@@ -78,44 +78,87 @@ class He2hbFactors:
 # ------------------------------------------------------------------ stage 1
 def he2hb(Af: torch.Tensor, nb: int):
     """Reduce the dense Hermitian Af (n x n, column-major, both triangles)
-    in place to Hermitian band form (bandwidth nb); returns He2hbFactors."""
+    in place to Hermitian band form (bandwidth nb); returns He2hbFactors.
+
+    On a GPU the panels are pipelined one step ahead (SLATE overlaps them
+    with OpenMP tasks, src/he2hb.cc:172-610): the update stream applies the
+    rank-2kk update of step k to the NEXT panel's columns first, the panel
+    stream then QR-factors that panel while the update stream streams the
+    rest of the trailing matrix.  The rows of the next panel's band block
+    (A22[0:nb, nb:]) are skipped by that bulk GEMM: the next step overwrites
+    them with R^H, and nothing reads them before."""
     n = Af.shape[0]
     F = He2hbFactors(nb)
     ct = conj_trans(Af.dtype)
+    from ..parallel.streams import StreamSet
+    pipe = Af.is_cuda and os.environ.get("SLATE_AMD_HE2HB_PIPE", "1") != "0"
+    ss = StreamSet(Af.device) if pipe else None
+    ev_cols = None                      # step k-1's update of this step's panel columns
     with trace_block("he2hb"):
+        if pipe:
+            ss.fork(diag=False)
         for k0 in range(0, max(n - nb, 0), nb):
             r0 = k0 + nb
             kb = min(nb, n - k0)
             m = n - r0
             if m <= 0:
                 break
-            P = Af[r0:, k0:k0 + kb]
             kk = min(m, kb)
-            tau = torch.zeros(kk, dtype=Af.dtype, device=Af.device)
-            T, V = ops.geqrf(P, tau)
-            F.panels.append((r0, V, T))
-            # band part: keep R, zero the reflectors, mirror to the upper triangle
-            _zero_strict_lower(P)
-            Af[k0:k0 + kb, r0:].copy_(P.mH)
-            # two-sided update of the trailing matrix
-            A22 = Af[r0:, r0:]
-            X = ops.colmajor_empty(m, kk, Af.dtype, Af.device)
-            X.copy_(V)
-            ops.trmm('R', 'U', 'N', 'N', 1.0, T, X)                 # X = V T
-            # [V W] and [W V] side by side: the rank-2kk update A -= V W^H +
-            # W V^H is ONE GEMM with K = 2 kk (A22 streamed once, not twice)
-            VW = ops.colmajor_empty(m, 2 * kk, Af.dtype, Af.device)
-            WV = ops.colmajor_empty(m, 2 * kk, Af.dtype, Af.device)
-            Y = VW[:, kk:]
-            ops.gemm(1.0, A22, X, 0.0, Y)                            # Y = A V T
-            Mt = ops.colmajor_empty(kk, kk, Af.dtype, Af.device)
-            ops.gemm(1.0, X, Y, 0.0, Mt, transA=ct)                  # M = T^H V^H Y
-            ops.gemm(-0.5, V, Mt, 1.0, Y)                            # W = Y - V M / 2
-            VW[:, :kk].copy_(V)
-            WV[:, :kk].copy_(Y)
-            WV[:, kk:].copy_(V)
-            ops.gemm(-1.0, VW, WV, 1.0, A22, transB=ct)              # A -= V W^H + W V^H
+            with (ss.use(ss.panel) if pipe else _nullctx()):
+                if pipe and ev_cols is not None:
+                    ss.wait(ss.panel, ev_cols)
+                P = Af[r0:, k0:k0 + kb]
+                tau = torch.zeros(kk, dtype=Af.dtype, device=Af.device)
+                T, V = ops.geqrf(P, tau)
+                F.panels.append((r0, V, T))
+                # band part: keep R, zero the reflectors, mirror to the upper triangle
+                _zero_strict_lower(P)
+                Af[k0:k0 + kb, r0:].copy_(P.mH)
+                X = ops.colmajor_empty(m, kk, Af.dtype, Af.device)
+                X.copy_(V)
+                ops.trmm('R', 'U', 'N', 'N', 1.0, T, X)                 # X = V T
+                ev_qr = ss.event(ss.panel) if pipe else None
+            us = ss.update[0] if pipe else None
+            with (ss.use(us) if pipe else _nullctx()):
+                if pipe:
+                    ss.wait(us, ev_qr)
+                    for t_ in (V, T, X):
+                        t_.record_stream(us)
+                # two-sided update of the trailing matrix
+                A22 = Af[r0:, r0:]
+                # [V W] and [W V] side by side: the rank-2kk update A -= V W^H +
+                # W V^H is ONE GEMM with K = 2 kk (A22 streamed once, not twice)
+                VW = ops.colmajor_empty(m, 2 * kk, Af.dtype, Af.device)
+                WV = ops.colmajor_empty(m, 2 * kk, Af.dtype, Af.device)
+                Y = VW[:, kk:]
+                ops.gemm(1.0, A22, X, 0.0, Y)                            # Y = A V T
+                Mt = ops.colmajor_empty(kk, kk, Af.dtype, Af.device)
+                ops.gemm(1.0, X, Y, 0.0, Mt, transA=ct)                  # M = T^H V^H Y
+                ops.gemm(-0.5, V, Mt, 1.0, Y)                            # W = Y - V M / 2
+                VW[:, :kk].copy_(V)
+                WV[:, :kk].copy_(Y)
+                WV[:, kk:].copy_(V)
+                nxt = min(nb, m) if pipe and m > nb else 0
+                if nxt:
+                    # the next panel's columns first (all rows), then the rest
+                    # below the next band block
+                    ops.gemm(-1.0, VW, WV[:nxt], 1.0, A22[:, :nxt], transB=ct)
+                    ev_cols = ss.event(us)
+                    ops.gemm(-1.0, VW[nxt:], WV[nxt:], 1.0, A22[nxt:, nxt:], transB=ct)
+                else:
+                    ops.gemm(-1.0, VW, WV, 1.0, A22, transB=ct)          # A -= V W^H + W V^H
+                    ev_cols = ss.event(us) if pipe else None
+        if pipe:
+            ss.join()
     return F
+
+
+class _nullctx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
 
 
 def _zero_strict_lower(P):
@@ -126,12 +169,56 @@ def _zero_strict_lower(P):
 
 
 def unmtr_he2hb(F: He2hbFactors, Z: torch.Tensor):
-    """Z := Q1 Z (Q1 = Q_0 Q_1 ... from he2hb): panels applied last-to-first."""
+    """Z := Q1 Z (Q1 = Q_0 Q_1 ... from he2hb): panels applied last-to-first.
+
+    On a GPU, groups of SLATE_AMD_UNMTR_HE2HB_GROUP (default 4) consecutive
+    panels are merged into one block reflector I - V T V^H (forward larft
+    merge, T = [[T1, -T1 V1^H V2 T2], [0, T2]]): Z is streamed once per
+    group with K = 4 nb instead of once per panel with K = nb."""
     with trace_block("unmtr_he2hb"):
         from .qr import _apply_qh, _vh
-        for (r0, V, T) in reversed(F.panels):
-            _apply_qh(V, T, Z[r0:, :], conj=False, Vh=_vh(V))
+        panels = F.panels
+        grp = max(1, int(os.environ.get("SLATE_AMD_UNMTR_HE2HB_GROUP", "4" if Z.is_cuda else "1")))
+        i1 = len(panels)
+        while i1 > 0:
+            i0 = max(0, i1 - grp)
+            if i1 - i0 == 1:
+                r0, V, T = panels[i0]
+                _apply_qh(V, T, Z[r0:, :], conj=False, Vh=_vh(V))
+            else:
+                r0, Vg, Tg = _merge_reflectors(panels[i0:i1])
+                _apply_qh(Vg, Tg, Z[r0:, :], conj=False, Vh=_vh(Vg))
+            i1 = i0
     return Z
+
+
+def _merge_reflectors(group):
+    """One block reflector for the product H_0 H_1 ... of consecutive panel
+    reflectors (r_i, V_i, T_i) (V_i explicit, rows r_i..n-1; T_i upper)."""
+    ct = None
+    r0 = group[0][0]
+    m = group[0][1].shape[0]
+    dt, dev = group[0][1].dtype, group[0][1].device
+    ct = conj_trans(dt)
+    ktot = sum(V.shape[1] for _, V, _ in group)
+    Vg = ops.colmajor_zeros(m, ktot, dt, dev)
+    Tg = ops.colmajor_zeros(ktot, ktot, dt, dev)
+    c = 0
+    for (r, V, T) in group:
+        kb = V.shape[1]
+        off = r - r0
+        Vg[off:, c:c + kb].copy_(V)
+        Ti = torch.triu(T[:kb, :kb])
+        Tg[c:c + kb, c:c + kb].copy_(Ti)
+        if c:
+            # T12 = -T_prev (V_prev^H V_i) T_i over the rows V_i spans
+            S = ops.colmajor_empty(c, kb, dt, dev)
+            ops.gemm(1.0, Vg[off:, :c], V, 0.0, S, transA=ct)
+            S2 = ops.colmajor_empty(c, kb, dt, dev)
+            ops.gemm(1.0, S, Tg[c:c + kb, c:c + kb], 0.0, S2)
+            ops.gemm(-1.0, Tg[:c, :c], S2, 0.0, Tg[:c, c:c + kb])
+        c += kb
+    return r0, Vg, Tg
 
 
 # ------------------------------------------------------------------ stage 2

@@ -479,3 +479,25 @@ def test_hb2st_gpu_matches_host_chase(early, lag, monkeypatch):
     scale = H.abs().max().item()
     assert (d.cpu() - d2.cpu()).abs().max().item() / scale < 1e-11
     assert (e.cpu().abs() - e2.cpu().abs()).abs().max().item() / scale < 1e-11
+
+
+@pytest.mark.parametrize("group", ["1", "3", "4"])
+@pytest.mark.parametrize("dt", [torch.float64, torch.complex128])
+def test_unmtr_he2hb_grouped_panels(group, dt, monkeypatch):
+    """Stage-1 back-transform with consecutive panels merged into one block
+    reflector (forward larft merge) equals the panel-by-panel application."""
+    from slate_amd.models.qr import _apply_qh
+    monkeypatch.setenv("SLATE_AMD_UNMTR_HE2HB_GROUP", group)
+    n, nb = 260, 16
+    g = torch.Generator().manual_seed(5)
+    X = torch.randn(n, n, generator=g, dtype=torch.float64).to(dt)
+    if dt.is_complex:
+        X = X + 1j * torch.randn(n, n, generator=g, dtype=torch.float64)
+    H = (X + X.mH).t().contiguous().t()
+    F = E.he2hb(H.clone().t().contiguous().t(), nb)
+    Z0 = torch.randn(n, 9, generator=g, dtype=torch.float64).to(dt).t().contiguous().t()
+    Za = Z0.clone().t().contiguous().t()
+    for (r0, V, T) in reversed(F.panels):
+        _apply_qh(V, T, Za[r0:, :], conj=False)
+    Zb = E.unmtr_he2hb(F, Z0.clone().t().contiguous().t())
+    assert (Za - Zb).abs().max().item() < 1e-12
