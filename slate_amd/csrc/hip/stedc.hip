@@ -304,13 +304,15 @@ void stedc_secular(i64 n, const double* d, const double* z, double rho, double z
 // Q(row - r0, col) with ld ldq; w gets the eigenvalues at the leaf's global
 // positions.  (The host solved one leaf after another: 256 leaves of 64 at
 // n = 16384.)
-constexpr int LEAF = 64;
-
-__global__ void __launch_bounds__(64)
+// LEAF = 64 (one wave) or 128 (two waves; Z = 128 KB of dynamic LDS):
+// larger leaves halve the number of merges of the first tree level, whose
+// per-merge host work dominated small merges (n = 16384: 255 -> 127 merges).
+template <int LEAF>
+__global__ void __launch_bounds__(LEAF)
 steqr_leaf_kernel(const i64* __restrict__ lo, const i64* __restrict__ hi, const double* __restrict__ d_in,
                   const double* __restrict__ e_in, double* __restrict__ w, double* __restrict__ Q, i64 ldq, i64 r0,
                   i64 r1, i64* fails) {
-    __shared__ double Z[LEAF * LEAF];
+    extern __shared__ double Z[];                  // LEAF * LEAF, column-major
     __shared__ double d[LEAF], ew[LEAF];
     const int lane = threadIdx.x;
     const i64 a = lo[blockIdx.x];
@@ -449,10 +451,22 @@ rot_cols_kernel(i64 m, double* __restrict__ Q, i64 ldq, i64 nrot, const i64* __r
 }
 
 void steqr_leaves(i64 nleaf, const i64* lo, const i64* hi, const double* d, const double* e, double* w, double* Q,
-                  i64 ldq, i64 r0, i64 r1, i64* fails, hipStream_t s) {
+                  i64 ldq, i64 r0, i64 r1, i64* fails, hipStream_t s, int maxleaf) {
     if (nleaf <= 0) return;
-    hipLaunchKernelGGL(steqr_leaf_kernel, dim3((unsigned)nleaf), dim3(64), 0, s, lo, hi, d, e, w, Q, ldq, r0, r1,
-                       fails);
+    if (maxleaf <= 64) {
+        hipLaunchKernelGGL(steqr_leaf_kernel<64>, dim3((unsigned)nleaf), dim3(64), 64 * 64 * sizeof(double), s, lo, hi,
+                           d, e, w, Q, ldq, r0, r1, fails);
+    } else {
+        if (maxleaf > 128) throw std::invalid_argument("steqr_leaves: leaves of at most 128 rows");
+        static bool attr = [] {
+            HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(steqr_leaf_kernel<128>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 128 * sizeof(double)));
+            return true;
+        }();
+        (void)attr;
+        hipLaunchKernelGGL(steqr_leaf_kernel<128>, dim3((unsigned)nleaf), dim3(128), 128 * 128 * sizeof(double), s, lo,
+                           hi, d, e, w, Q, ldq, r0, r1, fails);
+    }
     HIP_LAUNCH_CHECK();
 }
 

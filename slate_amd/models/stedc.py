@@ -34,6 +34,8 @@ MI355X design
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -43,6 +45,9 @@ from ..core.exceptions import SlateError
 from ..utils.trace import trace_block
 
 LEAF = 64
+# leaves solved on the GPU (steqr_leaf_kernel, <= 128 rows): 128 halves the
+# merges of the first level (SLATE_AMD_STEDC_LEAF = 64 keeps one wave each)
+GPU_LEAF = min(128, max(16, int(os.environ.get("SLATE_AMD_STEDC_LEAF", "128"))))
 CHUNK = 4096          # rank-one vector columns formed per merge GEMM
 
 
@@ -101,7 +106,10 @@ def stedc_rows(d, e, comm=None, device=None, leaf=LEAF):
     if n == 0:
         return w.cpu(), Q, r0, r1, mb
     with trace_block("stedc"):
-        leaves, levels = _tree(n, min(int(leaf), LEAF))
+        # GPU leaves: up to GPU_LEAF rows (one workgroup each, stedc.hip);
+        # host leaves: LEAF
+        cap = GPU_LEAF if dev.type == "cuda" else LEAF
+        leaves, levels = _tree(n, min(int(leaf), cap))
         dl = _split_diag(d, e, levels)
         own = [(a, b) for (a, b) in leaves if a < r1 and b > r0] if P > 1 else leaves
         _leaves(own, dl, e, w, Q, r0, r1, dev)
@@ -124,7 +132,7 @@ def _leaves(own, dl, e, w, Q, r0, r1, dev):
         fails = torch.zeros(1, dtype=torch.int64, device=dev)
         _hip().steqr_leaves(len(own), lo.data_ptr(), hi.data_ptr(), dd.data_ptr(), ee.data_ptr(), w.data_ptr(),
                             Q.data_ptr(), max(1, Q.stride(1)), r0, r1, fails.data_ptr(),
-                            torch.cuda.current_stream(dev).cuda_stream)
+                            torch.cuda.current_stream(dev).cuda_stream, max(b - a for a, b in own))
         return
     from .eig import steqr
     for (a, b) in own:

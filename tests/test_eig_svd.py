@@ -288,15 +288,16 @@ def test_hb2st_gpu(dt, n, b, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("leaf", [32, 128])
 @pytest.mark.parametrize("n", [257, 3000])
-def test_stedc_gpu_secular(n):
+def test_stedc_gpu_secular(n, leaf):
     """Merges on the GPU (secular roots / Gu-Eisenstat z / vectors by the
     stedc.hip kernels) vs an fp64 host reference."""
     torch.manual_seed(2)
     d, e = torch.randn(n, dtype=torch.float64), torch.randn(n - 1, dtype=torch.float64)
     T = torch.diag(d) + torch.diag(e, 1) + torch.diag(e, -1)
     wr = torch.linalg.eigvalsh(T)
-    w, Z = sl.stedc(d, e, device="cuda", leaf=32)
+    w, Z = sl.stedc(d, e, device="cuda", leaf=leaf)      # 128: two-wave leaf kernel
     Z = Z.cpu()
     tol = 1e-13 * n
     assert (w - wr).abs().max() < tol
@@ -306,7 +307,7 @@ def test_stedc_gpu_secular(n):
     d2[::3] = 2.0
     e2 = torch.full((n - 1,), 1e-9, dtype=torch.float64)
     T2 = torch.diag(d2) + torch.diag(e2, 1) + torch.diag(e2, -1)
-    w, Z = sl.stedc(d2, e2, device="cuda", leaf=32)
+    w, Z = sl.stedc(d2, e2, device="cuda", leaf=leaf)
     Z = Z.cpu()
     assert (T2 @ Z - Z * w).abs().max() < tol
     assert (Z.T @ Z - torch.eye(n, dtype=torch.float64)).abs().max() < tol

@@ -1,0 +1,16 @@
+#!/bin/bash
+# stedc with 128-row GPU leaves: eig GPU tests, stedc timing, heev phases + bench
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+D=gpurun_out/${TAG:-s12}; mkdir -p $D
+timeout -k 10 300 python -u -m pytest tests/test_eig_svd.py -m gpu -x -q --timeout 120 --timeout-method thread > $D/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -2 $D/pytest.log
+[ $rc -ne 0 ] && exit 1
+for l in 64 128; do
+  PYTHONPATH=. SLATE_AMD_STEDC_LEAF=$l timeout -k 10 200 python -u tools/probe/stedc_time.py > $D/stedc_$l.log 2>&1 || { tail $D/stedc_$l.log; exit 1; }
+  echo "leaf $l:"; grep -v amdgpu.ids $D/stedc_$l.log
+done
+timeout -k 10 300 python -u tools/heev_phases.py 16384 256 > $D/heev_phases.log 2>&1 || { tail $D/heev_phases.log; exit 1; }
+cat $D/heev_phases.log
+timeout -k 10 300 python -u bench.py --routine heev --n 16384 --nb 256 --steps 2 --warmup 1 > $D/bench_heev.log 2>&1 || { tail $D/bench_heev.log; exit 1; }
+tail -1 $D/bench_heev.log | cut -c1-200
