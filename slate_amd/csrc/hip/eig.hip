@@ -297,7 +297,7 @@ hb2st_tfac_kernel(const double* __restrict__ V, const double* __restrict__ tau, 
     }
 }
 
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(512)
 unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const double* __restrict__ V,
                         const i64* __restrict__ sp, const i64* __restrict__ nt, const i64* __restrict__ gptr,
                         const double* __restrict__ Tg, i64 nsw) {
@@ -307,38 +307,42 @@ unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const
     __shared__ i64 ssp[TB], snt[TB];
     const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
+    // 8 waves, two per SIMD (MFMA latency hidden across waves): wave wv
+    // owns W / Z row tiles of wr = wv & 3 and the column tiles 2 wc, 2 wc + 1
+    // (wc = wv >> 2)
+    const int wr = wv & 3, wc = wv >> 2;
     const i64 c0 = (i64)blockIdx.x * TCW;
     const int ncw = (int)min((i64)TCW, ncols - c0);
     // window row w of group t lives in Zs at column-major row ((w >> 6) + t) & 1) * 64 + (w & 63)
     auto zrow = [](int w, i64 t) { return (int)((((w >> 6) + t) & 1) * TB + (w & (TB - 1))); };
     // register staging (software pipeline): thread (wv, lane) moves element
-    // (row lane, column wv + 4 i) of a Z half and reflector element
-    // (jj = wv + 4 i, vi = lane) of a group, i < 16
-    constexpr int PR = TB * TB / 256;
-    double pv[PR], py[2 * PR], pz[PR];
+    // (row lane, column wv + 8 i) of a Z half and reflector element
+    // (jj = wv + 8 i, vi = lane) of a group, i < 8
+    constexpr int PR = TB * TB / 512;
+    double pv[PR], py[32], pz[PR];
     auto fetch_v = [&](i64 t) {
         #pragma unroll
         for (int i = 0; i < PR; ++i) {
-            const int jj = wv + 4 * i;
+            const int jj = wv + 8 * i;
             pv[i] = (t < snt[jj]) ? V[(ssp[jj] + t) * TB + lane] : 0.0;
         }
     };
     auto fetch_z = [&](i64 row0) {
         #pragma unroll
         for (int i = 0; i < PR; ++i) {
-            const int cc = wv + 4 * i;
+            const int cc = wv + 8 * i;
             const i64 row = row0 + lane;
             pz[i] = (cc < ncw && row < n) ? Z[(c0 + cc) * ldz + row] : 0.0;
         }
     };
     auto put_z = [&](int phys) {
         #pragma unroll
-        for (int i = 0; i < PR; ++i) Zs[(wv + 4 * i) * SZ + phys * TB + lane] = pz[i];
+        for (int i = 0; i < PR; ++i) Zs[(wv + 8 * i) * SZ + phys * TB + lane] = pz[i];
     };
     auto store_half = [&](i64 row0, int phys) {
         #pragma unroll
         for (int i = 0; i < PR; ++i) {
-            const int cc = wv + 4 * i;
+            const int cc = wv + 8 * i;
             const i64 row = row0 + lane;
             if (cc < ncw && row < n) Z[(c0 + cc) * ldz + row] = Zs[cc * SZ + phys * TB + lane];
         }
@@ -360,11 +364,11 @@ unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const
         __syncthreads();
         fetch_v(0);
         for (i64 t = 0; t < TJ; ++t) {
-            const double* Yg = Tg + (gptr[J] + t) * (2 * TB * TB) + (i64)(2 * wv) * 16 * 64 + lane;
+            const double* Yg = Tg + (gptr[J] + t) * (2 * TB * TB) + (i64)(2 * wr) * 16 * 64 + lane;
             #pragma unroll
-            for (int i = 0; i < 2 * PR; ++i) py[i] = Yg[i * 64];          // (row tile i / 16, k step i % 16)
+            for (int i = 0; i < 32; ++i) py[i] = Yg[i * 64];              // (row tile i / 16, k step i % 16)
             #pragma unroll
-            for (int i = 0; i < PR; ++i) Vr[(wv + 4 * i) * SV + lane] = pv[i];
+            for (int i = 0; i < PR; ++i) Vr[(wv + 8 * i) * SV + lane] = pv[i];
             __syncthreads();
             const bool more = t + 1 < TJ;
             if (more) {
@@ -375,60 +379,60 @@ unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const
                 const int vi = w - jj;
                 return (vi >= 0 && vi < TB) ? Vr[jj * SV + vi] : 0.0;
             };
-            // (1) W = V^T Z: wave wv owns W rows 16 wv..16 wv+15, 4 column tiles
-            d4 acc[4];
+            // (1) W = V^T Z: W rows 16 wr..16 wr+15, column tiles 2 wc, 2 wc+1
+            d4 acc[2];
             #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[j] = d4{0.0, 0.0, 0.0, 0.0};
-            // reflectors 16 wv..16 wv+15 are zero outside window rows
-            // 16 wv..16 wv+78: 20 of the 32 k-steps (V is a parallelogram)
+            for (int j = 0; j < 2; ++j) acc[j] = d4{0.0, 0.0, 0.0, 0.0};
+            // reflectors 16 wr..16 wr+15 are zero outside window rows
+            // 16 wr..16 wr+78: 20 of the 32 k-steps (V is a parallelogram)
             #pragma unroll 4
-            for (int k0 = 16 * wv; k0 < 16 * wv + TB + 16; k0 += 4) {
+            for (int k0 = 16 * wr; k0 < 16 * wr + TB + 16; k0 += 4) {
                 const int w = k0 + lk;
-                const double a = vg(w, 16 * wv + li);
+                const double a = vg(w, 16 * wr + li);
                 const int pr = zrow(w, t);
                 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const double b = Zs[(16 * j + li) * SZ + pr];
+                for (int j = 0; j < 2; ++j) {
+                    const double b = Zs[(16 * (2 * wc + j) + li) * SZ + pr];
                     acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[j], 0, 0, 0);
                 }
             }
             #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < 2; ++j)
                 #pragma unroll
-                for (int r = 0; r < 4; ++r) Ws[(16 * wv + lk + 4 * r) * SW + 16 * j + li] = acc[j][r];
+                for (int r = 0; r < 4; ++r) Ws[(16 * wr + lk + 4 * r) * SW + 16 * (2 * wc + j) + li] = acc[j][r];
             __syncthreads();
-            // (2) Z -= Y W: wave wv owns window rows 32 wv..32 wv+31 (2 x 4
-            // tiles); each W fragment read from LDS feeds both row tiles
+            // (2) Z -= Y W: window rows 32 wr..32 wr+31 (2 row tiles) x
+            // column tiles 2 wc, 2 wc+1; each W fragment feeds both row tiles
             {
-                d4 zc[2][4];
+                d4 zc[2][2];
                 #pragma unroll
                 for (int ri = 0; ri < 2; ++ri)
                     #pragma unroll
-                    for (int j = 0; j < 4; ++j)
+                    for (int j = 0; j < 2; ++j)
                         #pragma unroll
                         for (int r = 0; r < 4; ++r)
-                            zc[ri][j][r] = Zs[(16 * j + li) * SZ + zrow(32 * wv + 16 * ri + lk + 4 * r, t)];
+                            zc[ri][j][r] = Zs[(16 * (2 * wc + j) + li) * SZ + zrow(32 * wr + 16 * ri + lk + 4 * r, t)];
                 #pragma unroll
                 for (int k0 = 0; k0 < TB; k0 += 4) {
                     const int jj = k0 + lk;
-                    double bw[4];
+                    double bw[2];
                     #pragma unroll
-                    for (int j = 0; j < 4; ++j) bw[j] = Ws[jj * SW + 16 * j + li];
+                    for (int j = 0; j < 2; ++j) bw[j] = Ws[jj * SW + 16 * (2 * wc + j) + li];
                     #pragma unroll
                     for (int ri = 0; ri < 2; ++ri) {
                         const double a = -py[ri * 16 + k0 / 4];
                         #pragma unroll
-                        for (int j = 0; j < 4; ++j)
+                        for (int j = 0; j < 2; ++j)
                             zc[ri][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bw[j], zc[ri][j], 0, 0, 0);
                     }
                 }
                 #pragma unroll
                 for (int ri = 0; ri < 2; ++ri)
                     #pragma unroll
-                    for (int j = 0; j < 4; ++j)
+                    for (int j = 0; j < 2; ++j)
                         #pragma unroll
                         for (int r = 0; r < 4; ++r)
-                            Zs[(16 * j + li) * SZ + zrow(32 * wv + 16 * ri + lk + 4 * r, t)] = zc[ri][j][r];
+                            Zs[(16 * (2 * wc + j) + li) * SZ + zrow(32 * wr + 16 * ri + lk + 4 * r, t)] = zc[ri][j][r];
             }
             __syncthreads();
             if (more) {
@@ -454,7 +458,7 @@ bool unmtr_hb2st_mfma(i64 n, i64 ncols, double* Z, i64 ldz, const double* V, i64
     if (ncols <= 0 || nsw <= 0 || ngroups <= 0) return true;
     hipLaunchKernelGGL(hb2st_tfac_kernel, dim3((unsigned)ngroups), dim3(256), 0, s, V, tau, sp, nt, gJ, gt, nsw, Tg);
     HIP_LAUNCH_CHECK();
-    hipLaunchKernelGGL(unmtr_hb2st_mfma_kernel, dim3((unsigned)((ncols + TCW - 1) / TCW)), dim3(256), 0, s, n, ncols,
+    hipLaunchKernelGGL(unmtr_hb2st_mfma_kernel, dim3((unsigned)((ncols + TCW - 1) / TCW)), dim3(512), 0, s, n, ncols,
                        Z, ldz, V, sp, nt, gptr, Tg, nsw);
     HIP_LAUNCH_CHECK();
     return true;
