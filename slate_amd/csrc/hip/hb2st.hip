@@ -118,6 +118,16 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
         }
         const i64 nt = ntask[j];
         i64 s = j + 1, e = min(j + (i64)b, n - 1), col = j;
+        // sweep-resident window (fused & 16): the previous task's final row
+        // block is still in L; this task takes its reflector column and the
+        // first d0 = k_prev - 1 columns of its row block from there (the
+        // conjugate transpose of the previous block's columns s..e), and
+        // loads only its diagonal block and the bulge columns.  The previous
+        // task's stores are then drained just before this task's early
+        // publication instead of at its own end.
+        bool prev_ok = false;
+        i64 p_lo = 0;
+        int p_k = 0, p_KPf = 0;
         for (i64 t = 0; t < nt; ++t) {
             if (j > 0) {
                 // early mode (fused & 8): done[j-1] = u + 1 says sweep j-1
@@ -155,18 +165,46 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
             // wave 0 issues its column loads (k <= 128 rows: two per lane)
             // before its share of the row block, so both are in flight at once
             T xc[HMAXB / 64];
-            if (w == 0) {
-                #pragma unroll
-                for (int u = 0; u < HMAXB / 64; ++u) {
-                    const int r = lane + 64 * u;
-                    xc[u] = (r < k) ? At(s + r, col) : s_zero(T());
+            const bool reuse = (fused & 16) && fuse && prev_ok && b <= 64 && k <= 64 && p_k <= 64;
+            const int nc = (int)(hi - lo + 1);
+            if (reuse) {
+                constexpr int NBR = (64 * 64 + HT - 1) / HT;
+                const int cb = (int)(s - p_lo), d0 = p_k - 1;    // d0 = s - lo
+                if (w == 0) {
+                    #pragma unroll
+                    for (int u = 0; u < HMAXB / 64; ++u) {
+                        const int r = lane + 64 * u;
+                        xc[u] = (r < k) ? s_conj(L[(cb + r) * p_KPf]) : s_zero(T());
+                    }
                 }
-            }
-            if (fuse) {
-                const int nc = (int)(hi - lo + 1);
-                T* Ab = &At(s, lo);
-                move2d<T, HT / 64>(k, nc, lane, w, [&](int r, int c) -> T { return Ab[r + c * lda]; },
-                                   [&](int r, int c) -> T& { return L[c * KPf + r]; });
+                T br[NBR];
+                #pragma unroll
+                for (int q = 0; q < NBR; ++q) {
+                    const int idx = tid + q * HT, r = 1 + idx / k, cc = idx % k;
+                    br[q] = (r < p_k) ? L[(cb + cc) * p_KPf + r] : s_zero(T());
+                }
+                __syncthreads();                                   // every read of the previous block done
+                #pragma unroll
+                for (int q = 0; q < NBR; ++q) {
+                    const int idx = tid + q * HT, r = 1 + idx / k, cc = idx % k;
+                    if (r < p_k) L[(r - 1) * KPf + cc] = s_conj(br[q]);   // A(s + cc, lo + r - 1)
+                }
+                T* Ab = &At(s, lo + d0);
+                move2d<T, HT / 64>(k, nc - d0, lane, w, [&](int r, int c) -> T { return Ab[r + c * lda]; },
+                                   [&](int r, int c) -> T& { return L[(c + d0) * KPf + r]; });
+            } else {
+                if (w == 0) {
+                    #pragma unroll
+                    for (int u = 0; u < HMAXB / 64; ++u) {
+                        const int r = lane + 64 * u;
+                        xc[u] = (r < k) ? At(s + r, col) : s_zero(T());
+                    }
+                }
+                if (fuse) {
+                    T* Ab = &At(s, lo);
+                    move2d<T, HT / 64>(k, nc, lane, w, [&](int r, int c) -> T { return Ab[r + c * lda]; },
+                                       [&](int r, int c) -> T& { return L[c * KPf + r]; });
+                }
             }
             // ---- reflector (wave 0): x = A(s..e, col)
             if (w == 0) {
@@ -202,26 +240,28 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
                     if (r == 0) v[0] = s_from_real(T(), R(1));
                     else if (!trivial) v[r] = s_div(v[r], den);
                 }
-                if (lane == 0) {
-                    s_tau = tau; s_beta = beta;
-                    if (fused & 8) {
-                        // Early publication.  Task (j+1, t-2) -- the one
-                        // that waits for this task -- shares exactly two
-                        // entries with it: A(s, col) and A(col, s) (its
-                        // window is [col' .. s] with col' = col - b + 1;
-                        // this task writes rows s..e / columns lo = col + 1..
-                        // of its row block, their mirror and the column
-                        // below/right of (s, col)).  So once this column is
-                        // read and those two entries hold beta, the next
-                        // sweep may go; tasks < t finished (their stores
-                        // drained at their final barrier).
-                        At(s, col) = s_from_real(T(), beta);
-                        At(col, s) = s_from_real(T(), beta);
-                        __hip_atomic_store(&done[j], (int)(t + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                }
+                if (lane == 0) { s_tau = tau; s_beta = beta; }
             }
-            __syncthreads();
+            if (fused & 8) {
+                // Early publication.  Task (j+1, t-2) -- the one that waits
+                // for this task -- shares exactly two entries with it:
+                // A(s, col) and A(col, s) (its window is [col' .. s] with
+                // col' = col - b + 1; this task writes rows s..e / columns
+                // lo = col + 1.. of its row block, their mirror and the
+                // column below/right of (s, col)).  So once this column is
+                // read and those two entries hold beta, the next sweep may
+                // go.  Every wave first drains its stores (the previous
+                // task's, deferred) -- a barrier alone does not.
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (tid == 0) {
+                    At(s, col) = s_from_real(T(), s_beta);
+                    At(col, s) = s_from_real(T(), s_beta);
+                    __hip_atomic_store(&done[j], (int)(t + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            } else {
+                __syncthreads();
+            }
             HSTAMP(1);
             const T tau = s_tau;
             if (!s_is_zero(tau) && fuse) {
@@ -233,7 +273,7 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
                 // s..e is the conjugate transpose of the row block (A' is
                 // Hermitian), stored as the mirror of its off-diagonal part.
                 const T ct = s_conj(tau);
-                const int nc = (int)(hi - lo + 1), d0 = (int)(s - lo);
+                const int d0 = (int)(s - lo);
                 T* Ab = &At(s, lo);
                 // (the row block was staged before the reflector; the
                 // barrier after the reflector covers its LDS writes)
@@ -385,11 +425,18 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
             }
             for (int r = tid; r < b; r += HT) V[slot * b + r] = (r < k) ? v[r] : s_zero(T());
             if (tid == 0) { tauv[slot] = tau; rowv[slot] = s; lenv[slot] = k; }
-            __syncthreads();                                    // all waves' stores issued and complete
-            if (tid == 0 && (!(fused & 8) || t + 1 == nt))      // one release: writes back this XCD's L2
+            const bool publish = !(fused & 8) || t + 1 == nt;
+            // the next task of this sweep reads back what this one stored
+            // unless it takes it from L; early mode drains at the next
+            // publication (or here, at the sweep's last task)
+            if (publish || !(fused & 16) || !fuse) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0 && publish)                             // one release: writes back this XCD's L2
                 __hip_atomic_store(&done[j], (int)((fused & 8) ? nt + 1 : t + 1), __ATOMIC_RELEASE,
                                    __HIP_MEMORY_SCOPE_AGENT);
             HSTAMP(4);
+            prev_ok = fuse;
+            p_lo = lo; p_k = k; p_KPf = KPf;
             col = s;
         }
     }
@@ -432,8 +479,10 @@ void hb2st_device(i64 n, int b, T* A, i64 lda, T* V, T* tau, i64* row, i64* len,
             const char* e = getenv("SLATE_AMD_HB2ST_FUSED");
             const char* pt = getenv("SLATE_AMD_HB2ST_PITCH");
             const char* ea = getenv("SLATE_AMD_HB2ST_EARLY");
+            const char* ru = getenv("SLATE_AMD_HB2ST_REUSE");
+            const int early = (ea && ea[0] == '0') ? 0 : 8;                           // early publication
             return ((e && e[0] == '0') ? 0 : 1) | ((pt && pt[0] == 'o') ? 0 : 2) |  // default: 4 (mod 32)
-                   ((ea && ea[0] == '0') ? 0 : 8);                                   // early publication
+                   early | ((early && !(ru && ru[0] == '0')) ? 16 : 0);              // sweep-resident window
         }();
         HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)HLDS));

@@ -92,7 +92,7 @@ def he2hb(Af: torch.Tensor, nb: int):
     ct = conj_trans(Af.dtype)
     from ..parallel.streams import StreamSet
     pipe = Af.is_cuda and os.environ.get("SLATE_AMD_HE2HB_PIPE", "1") != "0"
-    ss = StreamSet(Af.device) if pipe else None
+    ss = StreamSet(Af.device, reserve_cus=0) if pipe else None   # GEMM-shaped QR panel: no reserved CUs
     ev_cols = None                      # step k-1's update of this step's panel columns
     with trace_block("he2hb"):
         if pipe:

@@ -457,8 +457,8 @@ def test_stedc_rows_one_rank():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("early,lag", [("1", "3"), ("0", "3"), ("0", "4")])
-def test_hb2st_gpu_matches_host_chase(early, lag, monkeypatch):
+@pytest.mark.parametrize("early,lag,reuse", [("1", "3", "1"), ("1", "3", "0"), ("0", "3", "0"), ("0", "4", "0")])
+def test_hb2st_gpu_matches_host_chase(early, lag, reuse, monkeypatch):
     """The pipelined GPU chase equals the sequential host chase up to the
     summation order inside a task: a dependency rule (early publication of
     a task's annihilated entries, or a lag of whole tasks) that let
@@ -467,6 +467,7 @@ def test_hb2st_gpu_matches_host_chase(early, lag, monkeypatch):
     in the first sweep, up to ~24 sweeps in flight)."""
     monkeypatch.setenv("SLATE_AMD_HB2ST_EARLY", early)
     monkeypatch.setenv("SLATE_AMD_HB2ST_LAG", lag)
+    monkeypatch.setenv("SLATE_AMD_HB2ST_REUSE", reuse)      # sweep-resident window (early mode only)
     n, b = 2000, 64
     g = torch.Generator().manual_seed(11)
     X = torch.randn(n, n, generator=g, dtype=torch.float64)

@@ -1,0 +1,16 @@
+#!/bin/bash
+# fp64 split-K on 128 x 128 tiles for long-K small outputs: GEMM/QR/eig tests; dgeqrf, dsyevd, dgetrf, dpotrf benches
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+D=gpurun_out/${TAG:-s16}; mkdir -p $D
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_qr.py tests/test_eig_svd.py -m gpu -x -q --timeout 120 --timeout-method thread > $D/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -2 $D/pytest.log
+[ $rc -ne 0 ] && exit 1
+timeout -k 10 200 python -u bench.py --routine geqrf --rows 65536 --size 8192 --nb 256 --steps 3 --warmup 1 > $D/bench_geqrf.log 2>&1 || { tail $D/bench_geqrf.log; exit 1; }
+tail -1 $D/bench_geqrf.log | cut -c1-250
+timeout -k 10 300 python -u bench.py --routine heev --n 16384 --nb 256 --steps 2 --warmup 1 > $D/bench_heev.log 2>&1 || { tail $D/bench_heev.log; exit 1; }
+tail -1 $D/bench_heev.log | cut -c1-150
+timeout -k 10 200 python -u bench.py --routine getrf --lookahead 2 --steps 3 --warmup 1 > $D/bench_getrf.log 2>&1 || { tail $D/bench_getrf.log; exit 1; }
+tail -1 $D/bench_getrf.log | cut -c1-150
+timeout -k 10 200 python -u bench.py > $D/bench_potrf.log 2>&1 || { tail $D/bench_potrf.log; exit 1; }
+tail -1 $D/bench_potrf.log | cut -c1-150
