@@ -677,6 +677,9 @@ tb2bd_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ UV, T* __
                 if (tid == 0) { Utau[slot] = tau; Urow[slot] = rs; Ulen[slot] = kr; }
             }
             row = rs;
+            // every wave drains its stores before the flag (a barrier alone
+            // waits for LDS traffic only)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (tid == 0)
                 __hip_atomic_store(&done[j], (int)(t + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
