@@ -126,6 +126,14 @@ def _geqrf_p1(A, buf, T, la):
     nloc = bc.nloc
     ss = StreamSet(dev, reserve_cus=0)   # GEMM-shaped CholeskyQR panel: no reserved CUs (measured 32.5 vs 29.8 TF/s with 64)
     ev_tr = {}
+    # grouped bulk updates (SLATE_AMD_QR_GROUP=2, one process column; off by
+    # default: dgeqrf 65536 x 8192 on one MI355X 38.3 vs 38.9 TF/s): the
+    # bulk trailing columns of an even step wait one step and then take the
+    # two panels as ONE block reflector (K = 2 nb: half the passes over the
+    # trailing matrix, twice the GEMM depth); the lookahead columns and the
+    # next step's newest lookahead column are updated per panel as before
+    group = int(os.environ.get("SLATE_AMD_QR_GROUP", "1")) if q == 1 else 1
+    pending = None
     ss.fork()
     for k in range(kt):
         _wd.beat(f"geqrf step {k}")
@@ -177,11 +185,30 @@ def _geqrf_p1(A, buf, T, la):
                     Vh.record_stream(us)
             lcnx = max(min(tiles_local_before(k + 2 + la, q, pc) * nb, nloc), lcla)
             with trace_block("geqrf::trailing"):
-                if lcnx > lcla:
-                    _apply_qh(V, Tk, buf[r0:m, lcla:lcnx], Vh=Vh)
-                ev_tr[k] = ss.event(us)
-                if nloc > lcnx:
-                    _apply_qh(V, Tk, buf[r0:m, lcnx:nloc], Vh=Vh)
+                if pending is not None:
+                    # columns [lcla, nloc) still lack the previous panel:
+                    # apply both panels as one block reflector
+                    from .eig import _merge_reflectors
+                    pr0, pV, pT = pending
+                    g0, Vg, Tg = _merge_reflectors([(pr0, pV, pT), (r0, V, Tk)])
+                    Vgh = _vh(Vg)
+                    if lcnx > lcla:
+                        _apply_qh(Vg, Tg, buf[g0:m, lcla:lcnx], Vh=Vgh)
+                    ev_tr[k] = ss.event(us)
+                    if nloc > lcnx:
+                        _apply_qh(Vg, Tg, buf[g0:m, lcnx:nloc], Vh=Vgh)
+                    pending = None
+                else:
+                    if lcnx > lcla:
+                        _apply_qh(V, Tk, buf[r0:m, lcla:lcnx], Vh=Vh)
+                    ev_tr[k] = ss.event(us)
+                    if nloc > lcnx:
+                        if group > 1 and k + 1 < kt and kb == nb and m - r0 > nb:
+                            pending = (r0, V, Tk)          # the bulk waits for the next panel
+                        else:
+                            _apply_qh(V, Tk, buf[r0:m, lcnx:nloc], Vh=Vh)
+    if pending is not None:
+        raise SlateError("geqrf: grouped update left pending")
     ss.join()
 
 

@@ -256,3 +256,14 @@ def test_geqrf_cholqr_breakdown_falls_back(kind):
 def test_geqrf_gpu_driver_tall():
     """Tall matrix: every panel takes the CholeskyQR path."""
     _check_qr(8192, 512, 128, torch.float64, device=torch.device("cuda"))
+
+
+@pytest.mark.parametrize("dt", [torch.float64, torch.complex128])
+@pytest.mark.parametrize("mn", [(300, 200, 32), (512, 256, 32), (200, 300, 32)])
+def test_geqrf_grouped_bulk_update(dt, mn, monkeypatch):
+    """Bulk trailing updates of two panels applied as one merged block
+    reflector (SLATE_AMD_QR_GROUP=2, the GPU default on one process column)
+    give the same factorization as per-panel updates."""
+    monkeypatch.setenv("SLATE_AMD_QR_GROUP", "2")
+    m, n, nb = mn
+    _check_qr(m, n, nb, dt)
