@@ -407,7 +407,7 @@ def steqr(d: torch.Tensor, e: torch.Tensor, Z0=None):
     return d, Z
 
 
-def stedc(d: torch.Tensor, e: torch.Tensor, device=None, leaf=64):
+def stedc(d: torch.Tensor, e: torch.Tensor, device=None, leaf=None):
     """Divide & conquer (Cuppen / Gu-Eisenstat) for the symmetric
     tridiagonal (d, e): returns ascending eigenvalues (host fp64) and Z on
     ``device`` (models/stedc.py: GPU leaves, device deflation, split merge

@@ -17,9 +17,9 @@ MI355X design
   Allgatherv of lambda).  No rank holds an n x n matrix (the final
   row -> column redistribution for the back-transforms is one batched p2p
   exchange, parallel/redist.py).
-* Leaves (<= 64) are solved all at once on the GPU: one wave per leaf,
-  implicit QL with each lane owning a row of the leaf's vectors
-  (csrc/hip/stedc.hip steqr_leaf_kernel).
+* Leaves (<= 128 rows on the GPU, 64 on the host) are solved all at once on
+  the GPU: one workgroup per leaf, implicit QL with each thread owning a
+  row of the leaf's vectors (csrc/hip/stedc.hip steqr_leaf_kernel).
 * Per merge: sort (device argsort), deflation by the tolerance test
   (device) and close-pole Givens chains (one thread per run,
   stedc_runs_kernel; rotations applied to the rows by rot_cols_kernel),
@@ -89,7 +89,7 @@ def _row_range(n, P, r):
     return min(r * mb, n), min((r + 1) * mb, n), mb
 
 
-def stedc_rows(d, e, comm=None, device=None, leaf=LEAF):
+def stedc_rows(d, e, comm=None, device=None, leaf=None):
     """Eigenvalues (ascending, host fp64, on every rank) and this rank's
     block of rows of the eigenvector matrix: returns (w, Qloc, r0, r1, mb)
     with Qloc (r1 - r0) x n column-major on ``device``; rank r owns rows
@@ -109,7 +109,7 @@ def stedc_rows(d, e, comm=None, device=None, leaf=LEAF):
         # GPU leaves: up to GPU_LEAF rows (one workgroup each, stedc.hip);
         # host leaves: LEAF
         cap = GPU_LEAF if dev.type == "cuda" else LEAF
-        leaves, levels = _tree(n, min(int(leaf), cap))
+        leaves, levels = _tree(n, cap if leaf is None else min(int(leaf), cap))
         dl = _split_diag(d, e, levels)
         own = [(a, b) for (a, b) in leaves if a < r1 and b > r0] if P > 1 else leaves
         _leaves(own, dl, e, w, Q, r0, r1, dev)
@@ -193,16 +193,23 @@ def _merge(a, m, b, rho, W, Z, w, Q, r0, r1, dev):
     Qs = ops.colmajor_empty(nr, s, torch.float64, dev)
     if nr:
         Qs.copy_(Qm[:, order])
-    # ---- deflation: tiny z components, then close-pole Givens chains
+    # ---- deflation: tiny z components, then close-pole Givens chains.
+    # Two host round trips per merge: (poles, z) for the tolerance test, then
+    # (z after the rotations, rotation / keep flags, column types) -- every
+    # index set is formed on the host and uploaded (pinned, stream-ordered)
     eps = float(np.finfo(np.float64).eps)
-    st = torch.stack([dd.abs().max(), (z * z).sum()]).cpu().tolist()     # host sync
-    zz = st[1]
-    tolf = 8.0 * eps * max(st[0], rho * zz)
-    nd = ~(rho * z.abs() * (zz ** 0.5) <= tolf)
-    c = torch.nonzero(nd).reshape(-1)                                      # host sync
-    nn = c.numel()
-    keepflag = torch.ones(nn, dtype=torch.int32, device=dev)
+    hz = torch.cat([dd, z]).cpu().numpy()                                   # host sync 1
+    dd_h, z_h = hz[:s], hz[s:]
+    zz = float(np.dot(z_h, z_h))
+    tolf = 8.0 * eps * max(float(np.abs(dd_h).max()), rho * zz)
+    c_h = np.nonzero(~(rho * np.abs(z_h) * (zz ** 0.5) <= tolf))[0]
+    nn = c_h.size
+    c = _upload(c_h, dev)
+    K_h = c_h
+    ty_h = None
+    z2_h = z_h
     if nn:
+        keepflag = torch.ones(nn, dtype=torch.int32, device=dev)
         cs = torch.zeros(nn, dtype=torch.float64, device=dev)
         sn = torch.zeros(nn, dtype=torch.float64, device=dev)
         rot = torch.zeros(nn, dtype=torch.int32, device=dev)
@@ -212,21 +219,27 @@ def _merge(a, m, b, rho, W, Z, w, Q, r0, r1, dev):
                               torch.cuda.current_stream(dev).cuda_stream)
         else:
             _runs_host(c, dd, z, ty, tolf, cs, sn, rot, keepflag)
-        ridx = torch.nonzero(rot).reshape(-1)
-        if ridx.numel() and nr:
-            I, J = c[ridx - 1].contiguous(), c[ridx].contiguous()
-            C, S = cs[ridx].contiguous(), sn[ridx].contiguous()
+        hb = torch.cat([z, rot.to(torch.float64), keepflag.to(torch.float64),
+                        ty.to(torch.float64)]).cpu().numpy()                # host sync 2
+        z2_h, rot_h, keep_h = hb[:s], hb[s:s + nn], hb[s + nn:s + 2 * nn]
+        ty_h = hb[s + 2 * nn:].astype(np.int64)
+        ridx_h = np.nonzero(rot_h)[0]
+        if ridx_h.size and nr:
+            I, J = _upload(c_h[ridx_h - 1], dev), _upload(c_h[ridx_h], dev)
+            rsel = _upload(ridx_h, dev)
+            C, S = cs[rsel].contiguous(), sn[rsel].contiguous()
             if dev.type == "cuda":
-                _hip().rot_cols(nr, Qs.data_ptr(), max(1, Qs.stride(1)), ridx.numel(), I.data_ptr(), J.data_ptr(),
+                _hip().rot_cols(nr, Qs.data_ptr(), max(1, Qs.stride(1)), ridx_h.size, I.data_ptr(), J.data_ptr(),
                                 C.data_ptr(), S.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
             else:
-                for t in range(ridx.numel()):
-                    i, j, cc, ss = int(I[t]), int(J[t]), float(C[t]), float(S[t])
-                    qi, qj = Qs[:, i].clone(), Qs[:, j].clone()
-                    Qs[:, i] = cc * qi - ss * qj
-                    Qs[:, j] = ss * qi + cc * qj
-    K = c[keepflag.bool()] if nn else c
-    k = K.numel()
+                for t in range(ridx_h.size):
+                    ii, jj, cc, ss = int(I[t]), int(J[t]), float(C[t]), float(S[t])
+                    qi, qj = Qs[:, ii].clone(), Qs[:, jj].clone()
+                    Qs[:, ii] = cc * qi - ss * qj
+                    Qs[:, jj] = ss * qi + cc * qj
+        K_h = c_h[keep_h != 0]
+    K = _upload(K_h, dev)
+    k = K_h.size
     lam = dd.clone()
     if k:
         dK, zK = dd[K].contiguous(), z[K].contiguous()
@@ -235,7 +248,8 @@ def _merge(a, m, b, rho, W, Z, w, Q, r0, r1, dev):
         zh = torch.empty(k, dtype=torch.float64, device=dev)
         if dev.type == "cuda":
             st = torch.cuda.current_stream(dev).cuda_stream
-            _hip().stedc_secular(k, dK.data_ptr(), zK.data_ptr(), rho, float((zK * zK).sum()), org.data_ptr(),
+            zzK = float(np.dot(z2_h[K_h], z2_h[K_h]))
+            _hip().stedc_secular(k, dK.data_ptr(), zK.data_ptr(), rho, zzK, org.data_ptr(),
                                  mu.data_ptr(), zh.data_ptr(), 0, 0, st)
         else:
             from .eig import stedc_secular as _sec
@@ -251,7 +265,7 @@ def _merge(a, m, b, rho, W, Z, w, Q, r0, r1, dev):
             zh.copy_(torch.sign(zK) * zh2.abs().sqrt())
         lam[K] = dK[org] + mu
         if nr:
-            _merge_gemm(Qs, K, ty, dK, zh, org, mu, lo, m, hi, dev)
+            _merge_gemm(Qs, K, ty_h[K_h], dK, zh, org, mu, lo, m, hi, dev)
     if flip:
         lam = -lam
     o2 = torch.argsort(lam, stable=True)
@@ -260,17 +274,17 @@ def _merge(a, m, b, rho, W, Z, w, Q, r0, r1, dev):
         Q[lo - r0:hi - r0, a:b] = Qs[:, o2]
 
 
-def _merge_gemm(Qs, K, ty, dK, zh, org, mu, lo, m, hi, dev):
+def _merge_gemm(Qs, K, tyK_h, dK, zh, org, mu, lo, m, hi, dev):
     """Qs[:, K] <- Qs[:, K] V, V the k x k rank-one vectors (normalised),
     formed CHUNK columns at a time; the rows above m multiply only the K
-    columns nonzero there (type 1 or 3), the rows below only type 2 or 3."""
+    columns nonzero there (type 1 or 3), the rows below only type 2 or 3
+    (tyK_h: the K columns' types, host)."""
     k = K.numel()
-    tyK = ty[K]
     parts = []
     if lo < m:
-        parts.append((0, min(hi, m) - lo, torch.nonzero(tyK & 1).reshape(-1)))
+        parts.append((0, min(hi, m) - lo, _upload(np.nonzero(tyK_h & 1)[0], dev)))
     if hi > m:
-        parts.append((max(lo, m) - lo, hi - lo, torch.nonzero(tyK & 2).reshape(-1)))
+        parts.append((max(lo, m) - lo, hi - lo, _upload(np.nonzero(tyK_h & 2)[0], dev)))
     srcs = []
     for (ra, rb, sel) in parts:
         if sel.numel() == 0:
@@ -301,6 +315,15 @@ def _merge_gemm(Qs, K, ty, dK, zh, org, mu, lo, m, hi, dev):
             Qs[ra:rb, cols] = out
 
 
+def _upload(idx, dev):
+    """Host index array -> int64 tensor on dev (pinned, stream-ordered: no
+    host synchronisation)."""
+    t = torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int64))
+    if dev.type != "cuda":
+        return t
+    return t.pin_memory().to(dev, non_blocking=True)
+
+
 def _runs_host(c, dd, z, ty, tol, cs, sn, rot, keep):
     """CPU form of stedc_runs_kernel (same arithmetic)."""
     cl = c.tolist()
@@ -329,7 +352,7 @@ def _runs_host(c, dd, z, ty, tol, cs, sn, rot, keep):
         t = u
 
 
-def stedc(d, e, device=None, leaf=LEAF):
+def stedc(d, e, device=None, leaf=None):
     """One process: (ascending eigenvalues on the host, n x n eigenvectors
     on ``device``)."""
     w, Q, _, _, _ = stedc_rows(d, e, None, device, leaf)
