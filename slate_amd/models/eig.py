@@ -27,6 +27,7 @@ holds the dense matrix.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -104,7 +105,7 @@ def he2hb(Af: torch.Tensor, nb: int):
             if m <= 0:
                 break
             kk = min(m, kb)
-            with (ss.use(ss.panel) if pipe else _nullctx()):
+            with (ss.use(ss.panel) if pipe else contextlib.nullcontext()):
                 if pipe and ev_cols is not None:
                     ss.wait(ss.panel, ev_cols)
                 P = Af[r0:, k0:k0 + kb]
@@ -119,7 +120,7 @@ def he2hb(Af: torch.Tensor, nb: int):
                 ops.trmm('R', 'U', 'N', 'N', 1.0, T, X)                 # X = V T
                 ev_qr = ss.event(ss.panel) if pipe else None
             us = ss.update[0] if pipe else None
-            with (ss.use(us) if pipe else _nullctx()):
+            with (ss.use(us) if pipe else contextlib.nullcontext()):
                 if pipe:
                     ss.wait(us, ev_qr)
                     for t_ in (V, T, X):
@@ -151,14 +152,6 @@ def he2hb(Af: torch.Tensor, nb: int):
         if pipe:
             ss.join()
     return F
-
-
-class _nullctx:
-    def __enter__(self):
-        return None
-
-    def __exit__(self, *a):
-        return False
 
 
 def _zero_strict_lower(P):
