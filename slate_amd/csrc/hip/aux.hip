@@ -286,6 +286,45 @@ laswp_apply_kernel(i64 n, T* A, i64 lda, const SwapPlan* __restrict__ plan, int 
     }
 }
 
+// The same folded plan applied to COLUMNS: the row interchanges of a matrix
+// held transposed (RowMajor rows = contiguous columns here, the storage the
+// LU trailing update uses -- SLATE switches its GPU tiles to RowMajor for the
+// same reason, src/getrf.cc:51-55).  Every workgroup owns a 128-byte row
+// segment of every touched column: gather all of them into LDS, barrier,
+// write them to their new columns -- whole cache lines both ways, no strided
+// 8-byte accesses.
+template <typename T>
+__global__ void __launch_bounds__(256)
+laswp_cols_kernel(i64 nrows, T* A, i64 lda, const SwapPlan* __restrict__ plan) {
+    constexpr int R = 128 / sizeof(T);                    // rows per workgroup: one cache line
+    constexpr int PER = 2 * MAXSW * R / 256;              // elements per thread (128 VGPRs)
+    __shared__ int src_s[2 * MAXSW], dst_s[2 * MAXSW];
+    const int nt = plan->nt;
+    if (nt == 0) return;
+    for (int t = threadIdx.x; t < nt; t += 256) {
+        src_s[t] = (int)plan->tsrc[t];
+        dst_s[t] = (int)plan->trow[t];
+    }
+    __syncthreads();
+    const i64 r0 = (i64)blockIdx.x * R;
+    const int nr = (int)min((i64)R, nrows - r0), tot = nt * R;
+    // every load of this workgroup in flight at once (registers, no LDS
+    // round trip), then -- after ALL of them have landed -- every store
+    T v[PER];
+    #pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int idx = threadIdx.x + k * 256, t = idx / R, r = idx % R;
+        if (idx < tot && r < nr && src_s[t] >= 0) v[k] = A[r0 + r + (i64)src_s[t] * lda];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    #pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int idx = threadIdx.x + k * 256, t = idx / R, r = idx % R;
+        if (idx < tot && r < nr && src_s[t] >= 0) A[r0 + r + (i64)dst_s[t] * lda] = v[k];
+    }
+}
+
 template <typename T>
 __global__ void row_gather_kernel(i64 m, i64 n, const T* A, i64 lda, T* B, i64 ldb, const i64* perm) {
     i64 i = (i64)blockIdx.x * 256 + threadIdx.x;
@@ -376,6 +415,37 @@ void laswp_off(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, i64 ioff, 
 template <typename T>
 void laswp(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, int incx, hipStream_t s) {
     laswp_off<T>(n, A, lda, k1, k2, ipiv, 0, s, incx);
+}
+// column interchanges col k <-> col ipiv[k] - ioff (k in [k1, k2)) over rows
+// [0, nrows): laswp of the transposed matrix
+template <typename T>
+void laswp_cols(i64 nrows, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, i64 ioff, hipStream_t s, int incx) {
+    if (nrows <= 0 || k2 <= k1) return;
+    if (k2 - k1 > MAXSW) {
+        if (incx > 0)
+            for (i64 k = k1; k < k2; k += MAXSW) laswp_cols<T>(nrows, A, lda, k, std::min(k2, k + MAXSW), ipiv, ioff, s, incx);
+        else
+            for (i64 k = k2; k > k1; k -= MAXSW) laswp_cols<T>(nrows, A, lda, std::max(k1, k - MAXSW), k, ipiv, ioff, s, incx);
+        return;
+    }
+    SwapPlan* plan = static_cast<SwapPlan*>(workspace(s, sizeof(SwapPlan), WS_L));
+    hipLaunchKernelGGL(laswp_setup_kernel, dim3(1), dim3(MAXSW), 0, s, k1, k2, ipiv, ioff, incx, plan, false);
+    constexpr int R = 128 / sizeof(T);
+    const unsigned g = (unsigned)((nrows + R - 1) / R);
+    hipLaunchKernelGGL(laswp_cols_kernel<T>, dim3(g), dim3(256), 0, s, nrows, A, lda, plan);
+    HIP_LAUNCH_CHECK();
+}
+
+// the same with a plan folded once per panel (swap_plan, fixed slots: -1
+// entries are skipped), for several column ranges of one step
+template <typename T>
+void laswp_cols_plan(i64 nrows, T* A, i64 lda, const void* plan, hipStream_t s) {
+    if (nrows <= 0) return;
+    constexpr int R = 128 / sizeof(T);
+    const unsigned g = (unsigned)((nrows + R - 1) / R);
+    hipLaunchKernelGGL(laswp_cols_kernel<T>, dim3(g), dim3(256), 0, s, nrows, A, lda,
+                       static_cast<const SwapPlan*>(plan));
+    HIP_LAUNCH_CHECK();
 }
 
 // ---------------------------------------------------------------------------
@@ -504,6 +574,8 @@ void permute_rows_scatter(i64 m, i64 n, const T* A, i64 lda, T* B, i64 ldb, cons
     template void geadd<T>(char, i64, i64, T, const T*, i64, T, T*, i64, hipStream_t);            \
     template void laswp<T>(i64, T*, i64, i64, i64, const i64*, int, hipStream_t);                 \
     template void laswp_off<T>(i64, T*, i64, i64, i64, const i64*, i64, hipStream_t, int);       \
+    template void laswp_cols<T>(i64, T*, i64, i64, i64, const i64*, i64, hipStream_t, int);      \
+    template void laswp_cols_plan<T>(i64, T*, i64, const void*, hipStream_t);                      \
     template void permute_rows_gather<T>(i64, i64, const T*, i64, T*, i64, const i64*, hipStream_t);    \
     template void xchg_gather<T>(const void*, i64, i64, const T*, i64, T*, i64, i64, int, int, hipStream_t); \
     template void xchg_scatter<T>(const void*, i64, i64, const T*, i64, T*, i64, i64, int, int, hipStream_t);

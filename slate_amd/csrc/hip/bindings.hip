@@ -222,6 +222,15 @@ static void register_kernels(py::module& m) {
         dispatch(dt, [&](auto z) { using T = decltype(z);
             laswp_off<T>(n, P<T>(A), lda, k1, k2, P<const i64>(ipiv), ioff, S(st), incx); });
     });
+    m.def("laswp_cols", [](char dt, i64 nrows, uintptr_t A, i64 lda, i64 k1, i64 k2, uintptr_t ipiv, i64 ioff,
+                           int incx, uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            laswp_cols<T>(nrows, P<T>(A), lda, k1, k2, P<const i64>(ipiv), ioff, S(st), incx); });
+    });
+    m.def("laswp_cols_plan", [](char dt, i64 nrows, uintptr_t A, i64 lda, uintptr_t plan, uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            laswp_cols_plan<T>(nrows, P<T>(A), lda, (const void*)plan, S(st)); });
+    });
     m.def("row_gather", [](char dt, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t B, i64 ldb, uintptr_t perm,
                            uintptr_t st) {
         dispatch(dt, [&](auto z) { using T = decltype(z);
@@ -338,6 +347,18 @@ PYBIND11_MODULE(_hip, m) {
         return (uintptr_t)st;
     });
     m.def("stream_destroy", [](uintptr_t st) { HIP_CHECK(hipStreamDestroy((hipStream_t)st)); });
+    // a private non-blocking stream (not from torch's round-robin pool): a
+    // captured graph owns one, so no other launcher ever shares the
+    // per-stream workspaces its kernels point into (workspace.hpp)
+    m.def("stream_create", [](int device) {
+        int old = 0;
+        HIP_CHECK(hipGetDevice(&old));
+        HIP_CHECK(hipSetDevice(device));
+        hipStream_t st;
+        HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        HIP_CHECK(hipSetDevice(old));
+        return (uintptr_t)st;
+    });
     m.def("cu_count", [](int device) {
         hipDeviceProp_t pr;
         HIP_CHECK(hipGetDeviceProperties(&pr, device));

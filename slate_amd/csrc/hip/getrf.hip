@@ -19,7 +19,9 @@
 //   (owner of row j) the current row j.
 // Kernel boundaries order the columns, so the panel is stream-ordered
 // (graph-capturable, no host sync, no co-residency assumption).
+#include <atomic>
 #include <cstdlib>
+#include <string>
 #include <type_traits>
 #include "common.hpp"
 #include "kernels.hpp"
@@ -762,6 +764,271 @@ getrf_base_persist(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64
     persist_other_cols(A - (i64)cabs * lda, lda, piv_s, prv_s, tr_s, ts_s, s_nt, w, N, cabs, g, G);
 }
 
+// ---------------------------------------------------------------------------
+// Tagged persistent base case (fp64, partial pivoting) -- ONE hand-off per
+// column instead of three.  getrf_base_persist publishes (drain) -> arrives
+// on a counter -> polls -> gathers: three dependent memory round trips plus
+// five barriers per column (~7 us).  Here every workgroup's per-column record
+// (winning row, |value|, row index) is written as 8-byte DATA-TAGGED granules
+// {tag = column epoch : 32-bit payload} (MI355X_MICROARCH.md hand-off table,
+// handoff-1to1 / R2: the data IS the flag -- no drain, no counter, no
+// fence).  Every workgroup sweeps the G records (each wave a few of them)
+// until every tag carries this column's epoch, assembles the candidates in
+// LDS, and picks the pivot redundantly (deterministic: same choice
+// everywhere).  The column loop is unrolled over the 32 columns, so column
+// j of the register-resident rows is a compile-time register (no per-column
+// select chains) and the elimination only touches the columns right of j.
+// A double travels as two granules (low / high word); 2-slot parity is safe
+// because a workgroup writes column j+2's record only after every workgroup
+// published j+1, i.e. after everyone consumed column j.
+// Epochs are unique per launch (a host counter advanced by w + 2 per launch;
+// never 0), so no slot ever needs zeroing.
+struct TagRec {                  // one workgroup's record of one column
+    unsigned long long g[68];    // [2c] / [2c+1] = lo / hi word of row value c; [64..65] |v|; [66] row
+    unsigned long long pad[4];
+};
+struct TagBuf {
+    TagRec rec[2][PG];
+    unsigned long long diag[2][64];   // row j (its owner): lo / hi words
+};
+
+__device__ inline void st_tag(unsigned long long* p, unsigned ep, unsigned v) {
+    __hip_atomic_store(p, ((unsigned long long)ep << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline unsigned long long ld_tag(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline unsigned lo32(double x) { return (unsigned)(__builtin_bit_cast(unsigned long long, x) & 0xffffffffu); }
+__device__ inline unsigned hi32(double x) { return (unsigned)(__builtin_bit_cast(unsigned long long, x) >> 32); }
+__device__ inline double mk_d(unsigned lo, unsigned hi) {
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+template <int R>
+__global__ void __launch_bounds__(PT2)
+getrf_base_tag(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64 ioff, i64* info, i64 info_off,
+               TagBuf* tb, LaunchWords* lw, double thr, int N, int cabs, unsigned ep0) {
+    __shared__ double wv[PT2 / 64];
+    __shared__ int wi[PT2 / 64];
+    __shared__ double candL[PG][NBB + 1];
+    __shared__ double pvL[PG];
+    __shared__ int piL[PG];
+    __shared__ double drow[NBB], ud_s[NBB];
+    __shared__ int s_abort, s_won, s_zero;
+    __shared__ int piv_s[NBB], prv_s[NBB], tr_s[2 * NBB], ts_s[2 * NBB], s_nt;
+    const int G = gridDim.x, g = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const i64 rbase = (i64)g * PT2 * R;
+    double a[R][NBB];
+    #pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const i64 i = rbase + r * PT2 + tid;
+        const i64 ir = i < m ? i : 0;
+        #pragma unroll
+        for (int c = 0; c < NBB; ++c) a[r][c] = A[ir + (i64)min(c, w - 1) * lda];
+    }
+    if (tid == 0) { s_abort = 0; s_won = 0; }
+    int zero_at = -1;
+    const bool prof = g_lu_prof_on && g == 0 && tid == 0;
+    unsigned long long tl = prof ? clock64() : 0, ph[5] = {0, 0, 0, 0, 0};
+#define TSTAMP(k) do { if (prof) { const unsigned long long t_ = clock64(); ph[k] += t_ - tl; tl = t_; } } while (0)
+    __syncthreads();                                   // s_abort / s_won initialised
+    // fully unrolled: j is a compile-time constant in every copy, so a[r][j]
+    // is a fixed register and the elimination touches columns > j only
+    #pragma clang loop unroll(full)
+    for (int j = 0; j < NBB; ++j) {
+        if (j < w && !s_abort) {
+            const int par = j & 1;
+            const unsigned ep = ep0 + (unsigned)j + 1u;
+            // ---- local arg-max of column j over unpivoted rows (i >= j)
+            double bv, v = -1.0;
+            int bb, bi = (int)(rbase + tid);
+            #pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const i64 i = rbase + r * PT2 + tid;
+                const double vr = (i < m && i >= j) ? fabs(a[r][j]) : -1.0;
+                if (r == 0 || beats(vr, i, v, (i64)bi)) { v = vr; bi = (int)i; }
+            }
+            {
+                int dummy = 0;
+                wave_argmax_dpp(v, bi, dummy);
+            }
+            if (lane == 0) { wv[wid] = v; wi[wid] = bi; }
+            __syncthreads();
+            bv = wv[0]; bb = wi[0];
+            #pragma unroll
+            for (int k = 1; k < PT2 / 64; ++k)
+                if (beats(wv[k], (i64)wi[k], bv, (i64)bb)) { bv = wv[k]; bb = wi[k]; }
+            TSTAMP(0);
+            // ---- publish: the winning thread writes its row + (|v|, row); the
+            //      owner of row j writes row j -- tagged granules, no drain
+            const int s_bt_ = bb - (int)rbase;
+            TagRec& my = tb->rec[par][g];
+            #pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (tid + r * PT2 == s_bt_) {
+                    #pragma unroll
+                    for (int c = 0; c < NBB; ++c) {
+                        st_tag(&my.g[2 * c], ep, lo32(a[r][c]));
+                        st_tag(&my.g[2 * c + 1], ep, hi32(a[r][c]));
+                    }
+                    st_tag(&my.g[64], ep, lo32(bv));
+                    st_tag(&my.g[65], ep, hi32(bv));
+                    st_tag(&my.g[66], ep, (unsigned)bb);
+                }
+                if (rbase + r * PT2 + tid == j) {
+                    #pragma unroll
+                    for (int c = 0; c < NBB; ++c) {
+                        st_tag(&tb->diag[par][2 * c], ep, lo32(a[r][c]));
+                        st_tag(&tb->diag[par][2 * c + 1], ep, hi32(a[r][c]));
+                    }
+                }
+            }
+            TSTAMP(1);
+            // ---- sweep: wave q polls records q, q + 8, ...; wave (G % 8) also
+            //      the row-j record.  Each lane owns one row granule (+ lanes
+            //      0..2 the value / index granules) of each of its records.
+            {
+                const bool dwave = wid == (G & 7);
+                int spins = 0;
+                const bool force = g_lu_force_abort && g == 0 && j == 0;
+                for (;;) {
+                    bool ok = true;
+                    for (int q = wid; q < G; q += PT2 / 64) {
+                        const unsigned long long x = ld_tag(&tb->rec[par][q].g[lane]);
+                        const unsigned long long y = lane < 3 ? ld_tag(&tb->rec[par][q].g[64 + lane])
+                                                              : ((unsigned long long)ep << 32);
+                        ok &= (unsigned)(x >> 32) == ep && (unsigned)(y >> 32) == ep;
+                        // lanes 2c / 2c + 1 hold lo / hi of value c
+                        const unsigned o = (unsigned)__shfl_xor((int)(unsigned)x, 1, 64);
+                        if ((lane & 1) == 0) candL[q][lane >> 1] = mk_d((unsigned)x, o);
+                        const unsigned y1 = (unsigned)__shfl((int)(unsigned)y, 1, 64);
+                        if (lane == 0) pvL[q] = mk_d((unsigned)y, y1);
+                        if (lane == 2) piL[q] = (int)(unsigned)y;
+                    }
+                    if (dwave) {
+                        const unsigned long long x = ld_tag(&tb->diag[par][lane]);
+                        ok &= (unsigned)(x >> 32) == ep;
+                        const unsigned o = (unsigned)__shfl_xor((int)(unsigned)x, 1, 64);
+                        if ((lane & 1) == 0) drow[lane >> 1] = mk_d((unsigned)x, o);
+                    }
+                    if (__all(ok) && !force) break;
+                    if (force || ++spins > (1 << 20)) {           // not co-resident: abort, never hang
+                        if (lane == 0) {
+                            if (decide(lw, 2)) s_won = 1;
+                            s_abort = 1;
+                        }
+                        break;
+                    }
+                    if ((spins & 255) == 0 && ld_state(lw) == 2) {
+                        if (lane == 0) s_abort = 1;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            __syncthreads();
+            TSTAMP(2);
+            if (!s_abort) {
+                // ---- global pivot, redundantly in every wave (DPP over the G partials)
+                double pv = -1.0;
+                int pi = j, pg = -1;
+                if (lane < G) { pv = pvL[lane]; pi = piL[lane]; pg = lane; }
+                wave_argmax_dpp(pv, pi, pg);
+                i64 p = pi;
+                int gw = pg;
+                if (!(pv >= 0.0) && !(pv != pv)) { p = j; gw = -1; }
+                if (thr < 1.0 && gw >= 0) {
+                    const double dj = fabs(drow[j]);
+                    if (dj == dj && dj >= thr * pv) { p = j; gw = -1; }
+                }
+                if (p == j) gw = -1;
+                const double* prow = gw < 0 ? drow : &candL[gw][0];
+                const double u = prow[j];
+                if (tid == 0) {
+                    piv_s[j] = (int)p;
+                    ud_s[j] = u;
+                }
+                if (u == 0.0 && zero_at < 0) zero_at = j;
+                TSTAMP(3);
+                // ---- interchange rows j <-> p, eliminate column j (columns > j only)
+                #pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const i64 i = rbase + r * PT2 + tid;
+                    if (i < m && i >= j) {
+                        if (i == j) {
+                            #pragma unroll
+                            for (int c = 0; c < NBB; ++c) a[r][c] = prow[c];
+                        } else {
+                            if (i == p) {
+                                #pragma unroll
+                                for (int c = 0; c < NBB; ++c) a[r][c] = drow[c];
+                            }
+                            const double l = (u != 0.0) ? a[r][j] / u : a[r][j];
+                            a[r][j] = l;
+                            #pragma unroll
+                            for (int c = j + 1; c < NBB; ++c) a[r][c] = fma(-l, prow[c], a[r][c]);
+                        }
+                    }
+                }
+            }
+            // the next column's sweep rewrites candL / drow / pvL
+            __syncthreads();
+            TSTAMP(4);
+        }
+    }
+#undef TSTAMP
+    if (prof) {
+        #pragma unroll
+        for (int k = 0; k < 5; ++k) g_lu_prof[k] += ph[k];
+    }
+    // ---- consensus: commit (every workgroup finished the loop) or abort
+    if (tid == 0 && !s_abort) {
+        const unsigned long long before =
+            __hip_atomic_fetch_add(&lw->done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (before + 1 == (unsigned long long)G) decide(lw, 1);
+        int spins = 0;
+        while (ld_state(lw) == 0) {
+            if (++spins > (1 << 22)) { s_won = decide(lw, 2) ? 1 : 0; break; }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        s_abort = ld_state(lw) == 2 ? 1 : 0;
+    }
+    __syncthreads();
+    if (s_abort) {
+        if (!s_won) return;                             // block untouched: the winner redoes it alone
+        if (tid == 0) { s_zero = -1; atomicAdd(&g_lu_fallbacks, 1ull); }
+        __syncthreads();
+        int zf = -1;
+        persist_fallback(m, w, A, lda, piv_s, thr, zf);
+        if (tid == 0) s_zero = zf;
+        __syncthreads();
+        if (ipiv && tid < w) ipiv[tid] = piv_s[tid] + ioff;
+        if (tid == 0 && s_zero >= 0 && info)
+            atomicCAS(reinterpret_cast<unsigned long long*>(info), 0ull, (unsigned long long)(s_zero + 1 + info_off));
+        if (N > w) persist_other_cols(A - (i64)cabs * lda, lda, piv_s, prv_s, tr_s, ts_s, s_nt, w, N, cabs, 0, 1);
+        return;
+    }
+    if (g == 0) {
+        if (ipiv && tid < w) ipiv[tid] = piv_s[tid] + ioff;
+        if (tid == 0 && zero_at >= 0 && info)
+            atomicCAS(reinterpret_cast<unsigned long long*>(info), 0ull, (unsigned long long)(zero_at + 1 + info_off));
+    }
+    // write-back (L already scaled in the column loop)
+    #pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const i64 i = rbase + r * PT2 + tid;
+        if (i < m) {
+            #pragma unroll
+            for (int c = 0; c < NBB; ++c)
+                if (c < w) A[i + (i64)c * lda] = a[r][c];
+        }
+    }
+    if (N <= w) return;
+    __syncthreads();
+    persist_other_cols(A - (i64)cabs * lda, lda, piv_s, prv_s, tr_s, ts_s, s_nt, w, N, cabs, g, G);
+}
+
 // the persistent form needs every row in a register slot of a co-resident
 // workgroup: m <= PG * PT2 rows; fp64 partial pivoting only
 // Panel-wide context of the recursion: N = panel width; full = the base
@@ -810,6 +1077,29 @@ static void base(i64 m, int c0, int c1, T* A, i64 lda, i64* ipiv, i64 ioff, i64*
                 const char* e = std::getenv("SLATE_AMD_LU_RPT1_ROWS");
                 return e ? (i64)std::atoll(e) : (i64)32 * PT2;
             }();
+            // tagged one-hand-off form (SLATE_AMD_LU_PANEL=counter: the
+            // counter/gather form above)
+            static const bool tagged = [] {
+                const char* e = std::getenv("SLATE_AMD_LU_PANEL");
+                return !e || std::string(e) != "counter";
+            }();
+            if (tagged && rpt != 4) {
+                TagBuf* tb = reinterpret_cast<TagBuf*>(reinterpret_cast<char*>(pb) + sizeof(PersistBuf));
+                static std::atomic<unsigned> g_ep{1};
+                unsigned ep0 = g_ep.fetch_add((unsigned)(NBB + 2));
+                if (ep0 == 0 || ep0 + (unsigned)(NBB + 2) < ep0) ep0 = g_ep.fetch_add((unsigned)(NBB + 2));
+                if (m <= rpt1_rows && m <= (i64)PG * PT2) {
+                    const int G = (int)((m + PT2 - 1) / PT2);
+                    hipLaunchKernelGGL(getrf_base_tag<1>, dim3(G), dim3(PT2), 0, s, m, c1, A, lda, ipiv, ioff,
+                                       info, info_off, tb, lw, thr, (int)ctx.N, (int)cabs, ep0);
+                } else {
+                    const int G = (int)((m + 2 * PT2 - 1) / (2 * PT2));
+                    hipLaunchKernelGGL(getrf_base_tag<2>, dim3(G), dim3(PT2), 0, s, m, c1, A, lda, ipiv, ioff,
+                                       info, info_off, tb, lw, thr, (int)ctx.N, (int)cabs, ep0);
+                }
+                HIP_LAUNCH_CHECK();
+                return;
+            }
             if (rpt != 4 && m <= rpt1_rows && m <= (i64)PG * PT2) {
                 const int G = (int)((m + PT2 - 1) / PT2);
                 hipLaunchKernelGGL(getrf_base_persist<1>, dim3(G), dim3(PT2), 0, s, m, c1, A, lda, ipiv, ioff,
@@ -904,7 +1194,7 @@ void lu_persist_profile(int enable, unsigned long long* out) {
     HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_lu_prof_on), &enable, sizeof(int)));
 }
 
-size_t getrf_work_bytes() { return PANEL_BYTES + sizeof(PersistBuf); }
+size_t getrf_work_bytes() { return PANEL_BYTES + sizeof(PersistBuf) + sizeof(TagBuf); }
 
 // failure handling of the persistent base case (tests/tools): number of
 // launches that fell back to the one-workgroup LU; force = 1 makes every

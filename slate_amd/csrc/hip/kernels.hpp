@@ -79,6 +79,10 @@ void lu_persist_profile(int enable, unsigned long long* out);
 unsigned long long lu_persist_fallbacks(int force);
 template <typename T>
 void laswp_off(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, i64 ioff, hipStream_t s, int incx = 1);
+template <typename T>
+void laswp_cols(i64 nrows, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, i64 ioff, hipStream_t s, int incx = 1);
+template <typename T>
+void laswp_cols_plan(i64 nrows, T* A, i64 lda, const void* plan, hipStream_t s);
 
 // geqrf.hip
 template <typename T>

@@ -323,7 +323,14 @@ def _potrf_graph_run(A, s, buf, nb, g0, nt, R_end, la, group, ss, ct, dev):
         # workspaces (csrc/hip/workspace.hpp) must exist for the capture
         # stream before the capture
         g = torch.cuda.CUDAGraph()
-        cs = torch.cuda.Stream(device=dev)
+        # a PRIVATE stream, owned by the graph entry for its whole life: a
+        # pooled torch stream can be handed to other code later, whose larger
+        # workspace request on the same handle would free the buffers the
+        # captured kernels point into (csrc/hip/workspace.hpp)
+        from .. import _native
+        cs = torch.cuda.ExternalStream(_native.hip().stream_create(dev.index if dev.index is not None
+                                                                   else torch.cuda.current_device()),
+                                       device=dev)
         cs.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(cs):
             scratch = buf.clone()
@@ -333,8 +340,8 @@ def _potrf_graph_run(A, s, buf, nb, g0, nt, R_end, la, group, ss, ct, dev):
             with torch.cuda.graph(g, stream=cs, capture_error_mode="relaxed"):
                 _potrf_1x1_grouped(A, s, buf, nb, g0, nt, R_end, la, group, ss, infos, ct, dev, serial=True)
         torch.cuda.current_stream(dev).wait_stream(cs)
-        ent = _GRAPHS[key] = (g, infos)
-    g, infos = ent
+        ent = _GRAPHS[key] = (g, infos, cs)
+    g, infos, _cs = ent
     infos.zero_()              # eagerly: a memset node inside the graph replays stale
     g.replay()
     return infos

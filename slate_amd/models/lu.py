@@ -11,8 +11,9 @@ MI355X design:
   pivot search with last-arriver reduction + MFMA GEMM/TRSM for the blocked
   updates -- csrc/hip/getrf.hip); SLATE always factors it on the host;
 * row interchanges use one permutation-gather kernel per column block (the
-  swap sequence is folded into a permutation in LDS), column-major storage,
-  no RowMajor tile conversion;
+  swap sequence is folded into a permutation in LDS); on the GPU the 1 x q
+  form factors the local block TRANSPOSED (RowMajor rows, as SLATE's GPU
+  tiles, getrf.cc:51-55), so every interchange moves contiguous memory;
 * p == 1 grids (1 x q, and a single GPU) keep the whole step on device,
   stream-ordered with lookahead: panel + lookahead columns on the
   high-priority stream, trailing swaps/trsm/GEMM on the low-priority stream;
@@ -26,7 +27,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from .. import ops
+from .. import _native, ops
 from ..core.enums import Diag, MethodLU, Op, Option, Side, Uplo
 from ..core.exceptions import SlateError
 from ..core.matrix import Matrix, Pivots, TriangularMatrix
@@ -88,7 +89,13 @@ def _getrf(A, pivots, opts, mode):
     thr = float(get_option(opts, Option.PivotThreshold, 1.0))
     la = max(0, int(get_option(opts, Option.Lookahead, 1)))
     if bc.p == 1 and mode != "calu":
-        info, ipiv = _getrf_p1(A, buf, thr, la, mode == "nopiv")
+        info, ipiv = None, None
+        if _rowmajor_ok(buf, bc):
+            T = _alloc_transposed(buf, bc, s.m)
+            if T is not None:
+                info, ipiv = _getrf_p1(A, buf, thr, la, mode == "nopiv", T=T)
+        if info is None:
+            info, ipiv = _getrf_p1(A, buf, thr, la, mode == "nopiv")
     else:
         import os
         leaf = int(os.environ.get("SLATE_AMD_CALU_LEAF", 0)) or \
@@ -101,8 +108,39 @@ def _getrf(A, pivots, opts, mode):
 
 
 # ------------------------------------------------------------------ p == 1
-def _getrf_p1(A, buf, thr, la, nopiv):
-    """1 x q grid (incl. one GPU): every rank owns every row of its columns."""
+def _rowmajor_ok(buf, bc):
+    """The RowMajor (transposed-storage) form of the 1 x q LU: GPU only,
+    SLATE_AMD_LU_ROWMAJOR=0 turns it off."""
+    import os
+    return buf.is_cuda and bc.p == 1 and os.environ.get("SLATE_AMD_LU_ROWMAJOR", "1") != "0"
+
+
+def _alloc_transposed(buf, bc, m):
+    """nloc x m column-major workspace for the transposed local block (the
+    rows of A contiguous), or None when the device cannot hold a second copy
+    of the local block (then the column-major path runs)."""
+    nloc = bc.nloc
+    ldt = (nloc + 7) // 8 * 8
+    try:
+        return torch.empty((max(m, 1), ldt), dtype=buf.dtype, device=buf.device).t()[:nloc, :m]
+    except torch.cuda.OutOfMemoryError:
+        return None
+
+
+# growth values of the explicit-inverse steps that forced a redo (tests)
+LU_INV_REDO = []
+
+
+def _getrf_p1(A, buf, thr, la, nopiv, T=None, no_inv=False):
+    """1 x q grid (incl. one GPU): every rank owns every row of its columns.
+
+    With ``T`` (GPU) the local block is factored TRANSPOSED, i.e. with
+    RowMajor rows as SLATE does on GPUs (src/getrf.cc:51-55): T = buf^T, so
+    a row interchange of A moves two contiguous columns of T (whole cache
+    lines; column-major row swaps are strided 8-byte accesses, ~60 ms per
+    n = 32768 factorization) and the trailing update is the NT GEMM
+    T22 -= U12^T L21^T.  Each panel is copied out to a column-major block
+    for the panel kernel and written back; T goes back to buf at the end."""
     s = A.storage
     bc = s.bc
     nb, q, pc = bc.nb, bc.q, bc.pc
@@ -112,12 +150,18 @@ def _getrf_p1(A, buf, thr, la, nopiv):
     dt = s.dtype
     grid = grid_of(A) if q > 1 else None
     nloc = bc.nloc
+    rm = T is not None
     ipiv = torch.zeros(max(min(m, n), 1), dtype=torch.int64, device=dev)   # panel-relative per step
     infos = torch.zeros(max(kt, 1), dtype=torch.int64, device=dev)
+    if rm and nloc and m:
+        ops.gecopy(buf[:m, :nloc], T, trans='T')
+    upd = _update_cols_rm if rm else _update_cols
+    M = T if rm else buf
     # 32 CUs: the persistent fp64 panel runs <= 32 workgroups (2 rows per thread)
     ss = StreamSet(dev, reserve_cus=32)
     ev_tr = {}
     left = []
+    plans = {}
     import os
     tail = int(kt * float(os.environ.get("SLATE_AMD_LU_LEFT_TAIL", "0.6")))
     # GEMM-bound first steps (SLATE_AMD_LU_UNMASKED = fraction of the steps,
@@ -128,7 +172,10 @@ def _getrf_p1(A, buf, thr, la, nopiv):
     # trailing widths of at least SLATE_AMD_LU_INV_MIN local columns solve
     # their U rows with the explicit L11 inverse (one GEMM; 0 = never;
     # dgetrf n = 32768 on one MI355X: 0 / 2048 / 8192 -> 39.4 / 40.3 / 40.4 TF/s)
-    inv_min = int(os.environ.get("SLATE_AMD_LU_INV_MIN", "4096")) if ss.gpu and not nopiv else 0
+    # Only the RowMajor form uses it: its input (buf) is intact until the end,
+    # so a step whose inverse grew too much is redone with the trsm form.
+    inv_min = int(os.environ.get("SLATE_AMD_LU_INV_MIN", "4096")) if rm and not nopiv and not no_inv else 0
+    growth = torch.zeros(max(kt, 1), dtype=_native.REAL_OF[dt], device=dev)
     ss.fork()
     for k in range(kt):
         _wd.beat(f"getrf step {k}")
@@ -151,8 +198,15 @@ def _getrf_p1(A, buf, thr, la, nopiv):
                     # the whole tile width: a wide last panel (m - r0 < tile
                     # width) also gets U12 = L11^{-1} P A12 of its extra columns
                     wk = min(nb, n - r0)
-                    ops.getrf(buf[r0:m, lck:lck + wk], piv, infos[k:k + 1], threshold=thr, nopiv=nopiv)
-                    Lp = buf[r0:m, lck:lck + kb]
+                    if rm:
+                        Pk = ops.colmajor_empty(mk, wk, dt, dev)
+                        ops.gecopy(T[lck:lck + wk, r0:m], Pk, trans='T')
+                        ops.getrf(Pk, piv, infos[k:k + 1], threshold=thr, nopiv=nopiv)
+                        ops.gecopy(Pk, T[lck:lck + wk, r0:m], trans='T')
+                        Lp = Pk[:, 0:kb]
+                    else:
+                        ops.getrf(buf[r0:m, lck:lck + wk], piv, infos[k:k + 1], threshold=thr, nopiv=nopiv)
+                        Lp = buf[r0:m, lck:lck + kb]
                 else:
                     Lp = ops.colmajor_empty(mk, kb, dt, dev)
                 if q > 1:
@@ -160,15 +214,20 @@ def _getrf_p1(A, buf, thr, la, nopiv):
                     if not nopiv:
                         grid.row_comm.bcast(piv, k % q)
                     bcast_tile(grid.row_comm, Lp, k % q)
+                # RowMajor: the step's swap sequence folded ONCE, used by every
+                # column range of this step (and later by the left columns)
+                sw = ipiv
+                if rm and not nopiv:
+                    sw = plans[k] = ops.swap_plan(ipiv, r0, r0 + kb, ioff=-r0)
             Linv = None
             if inv_min and nloc - lcla >= inv_min and kb == nb:
-                Linv = ops.tri_inv('L', 'U', Lp[0:kb, 0:kb])
+                Linv = _l11_inverse(Lp[0:kb, 0:kb], growth[k:k + 1])
             # lookahead columns; the newest one (k+la) was the first part of
             # step k-1's trailing update
             if k >= 1 and la > 0:
                 ss.wait(ss.panel, ev_tr[k - 1])
             if lcla > lc1:
-                _update_cols(buf, Lp, ipiv, r0, kb, m, lc1, lcla, nopiv, Linv)
+                upd(M, Lp, sw, r0, kb, m, lc1, lcla, nopiv, Linv)
             ev_panel = ss.event(ss.panel)
         us = ss.diag if k < unmasked else ss.update[0]
         if k == unmasked and unmasked > 0:
@@ -179,15 +238,17 @@ def _getrf_p1(A, buf, thr, la, nopiv):
                 Lp.record_stream(us)
                 if Linv is not None:
                     Linv.record_stream(us)
+            if rm and not nopiv:
+                sw.record_stream(us)
             # column k+1+la first (next step's newest lookahead column), event,
             # then the rest
             lcnx = max(min(tiles_local_before(k + 2 + la, q, pc) * nb, nloc), lcla)
             with trace_block("getrf::trailing"):
                 if lcnx > lcla:
-                    _update_cols(buf, Lp, ipiv, r0, kb, m, lcla, lcnx, nopiv, Linv)
+                    upd(M, Lp, sw, r0, kb, m, lcla, lcnx, nopiv, Linv)
                 ev_tr[k] = ss.event(us)
                 if nloc > lcnx:
-                    _update_cols(buf, Lp, ipiv, r0, kb, m, lcnx, nloc, nopiv, Linv)
+                    upd(M, Lp, sw, r0, kb, m, lcnx, nloc, nopiv, Linv)
             # swap the already-factored left columns (tiles < k).  This runs
             # on the update stream, after every trailing update that still
             # reads an earlier panel's L rows (trailing j < k overlaps panel
@@ -202,18 +263,61 @@ def _getrf_p1(A, buf, thr, la, nopiv):
             if k >= tail:
                 todo = -(-len(left) // max(1, kt - k))
                 for _ in range(min(todo, len(left))):
-                    _, j0, jb, jc = left.pop(0)
-                    ops.laswp(buf[:m, 0:jc], ipiv, j0, j0 + jb, ioff=-j0)
+                    _swap_left(M, rm, m, left.pop(0), plans if rm else ipiv)
     with ss.use(ss.update[0]):
-        for _, j0, jb, jc in left:
-            ops.laswp(buf[:m, 0:jc], ipiv, j0, j0 + jb, ioff=-j0)
+        for item in left:
+            _swap_left(M, rm, m, item, plans if rm else ipiv)
     ss.join()
+    if inv_min:
+        from ._util import read_to_host
+        lim = float(os.environ.get("SLATE_AMD_LU_INV_GROWTH", "1e6"))
+        gmax = float(read_to_host(growth).max())
+        if not gmax <= lim:
+            LU_INV_REDO.append(gmax)
+            return _getrf_p1(A, buf, thr, la, nopiv, T=T, no_inv=True)
+    if rm and nloc and m:
+        ops.gecopy(T, buf[:m, :nloc], trans='T')
     if nopiv:
         glob = torch.arange(min(m, n), dtype=torch.int64, device=dev)
     else:
         glob = _global_pivots(ipiv[:min(m, n)], nb)
     info = _reduce_info(A, infos, kt, nb)
     return info, glob
+
+
+def _swap_left(M, rm, m, item, sw):
+    """Step k's interchanges on the factored columns left of its panel (sw:
+    the per-step plans of the RowMajor form, else the pivot vector)."""
+    k, j0, jb, jc = item
+    if rm:
+        ops.laswp_cols_plan(M[0:jc, :m], sw[k])
+    else:
+        ops.laswp(M[:m, 0:jc], sw, j0, j0 + jb, ioff=-j0)
+
+
+def _l11_inverse(L11, growth):
+    """Explicit inverse of the unit-lower L11 for the U-row GEMM, and its
+    growth max |L11^{-1}| written to the one-element device view ``growth``
+    (no host sync).  |L| <= 1 under partial pivoting, but |L11^{-1}| can grow
+    like 2^(kb-1), and Linv A12 then loses the backward
+    stability of the substitution: the driver reads the growth vector once
+    at the end and redoes the factorization with the trsm form if any step
+    exceeded SLATE_AMD_LU_INV_GROWTH (default 1e6)."""
+    Linv = ops.tri_inv('L', 'U', L11)
+    kb = L11.shape[0]
+    kmod_ = _native_mod(Linv)
+    # column maxima (one workgroup per column), then the max of those
+    cols = torch.empty(kb, dtype=growth.dtype, device=growth.device)
+    kmod_.genorm(ops.code(Linv.dtype), 'M', 'G', 'N', 0, kb, kb, Linv.data_ptr(), ops.ld(Linv),
+                 cols.data_ptr(), ops.stream(Linv))
+    kmod_.genorm(ops.code(cols.dtype), 'M', 'G', 'N', 0, kb, 1, cols.data_ptr(), kb,
+                 growth.data_ptr(), ops.stream(Linv))
+    return Linv
+
+
+def _native_mod(t):
+    from .._native import kmod
+    return kmod(t)
 
 
 def _global_pivots(ipiv, nb):
@@ -239,6 +343,25 @@ def _update_cols(buf, Lp, ipiv, r0, kb, m, c0, c1, nopiv, Linv=None):
         ops.trsm('L', 'L', 'N', 'U', 1.0, Lp[0:kb, 0:kb], Ukk)
     if m > r0 + kb:
         ops.gemm(-1.0, Lp[kb:, :], Ukk, 1.0, buf[r0 + kb:m, c0:c1])
+
+
+def _update_cols_rm(T, Lp, ipiv, r0, kb, m, c0, c1, nopiv, Linv=None):
+    """_update_cols on the transposed block T = A^T: local columns [c0, c1)
+    of A are rows [c0, c1) of T.  Row interchanges swap whole columns of T;
+    U12^T = A12^T L11^{-T} (GEMM with the explicit inverse, else trsm from
+    the right); then T22 -= U12^T L21^T, one NT GEMM."""
+    cols = T[c0:c1, :m]
+    if not nopiv:
+        ops.laswp_cols_plan(cols, ipiv)          # ipiv: the step's folded plan
+    Ut = T[c0:c1, r0:r0 + kb]
+    if Linv is not None:
+        tmp = ops.colmajor_empty(c1 - c0, kb, Ut.dtype, Ut.device)
+        ops.gecopy(Ut, tmp)
+        ops.gemm(1.0, tmp, Linv, 0.0, Ut, 'N', 'T')
+    else:
+        ops.trsm('R', 'L', 'T', 'U', 1.0, Lp[0:kb, 0:kb], Ut)
+    if m > r0 + kb:
+        ops.gemm(-1.0, Ut, Lp[kb:, :], 1.0, T[c0:c1, r0 + kb:m], 'N', 'T')
 
 
 def _reduce_info(A, infos, kt, nb):

@@ -209,6 +209,25 @@ def laswp(A, ipiv, k1, k2, ioff=0, incx=1):
     return A
 
 
+def laswp_cols(A, ipiv, k1, k2, ioff=0, incx=1):
+    """Apply column interchanges ipiv[k1:k2] (cols ipiv[k]-ioff <-> k) to A:
+    the row interchanges of A^T, with whole-cache-line accesses."""
+    _chk(A)
+    if A.shape[0] == 0 or k2 <= k1:
+        return A
+    kmod(A).laswp_cols(code(A.dtype), A.shape[0], A.data_ptr(), ld(A), k1, k2, ipiv.data_ptr(), ioff, incx,
+                       stream(A))
+    return A
+
+
+def laswp_cols_plan(A, plan):
+    """laswp_cols with a plan from swap_plan (folded once per panel)."""
+    _chk(A)
+    if A.shape[0] and A.shape[1]:
+        kmod(A).laswp_cols_plan(code(A.dtype), A.shape[0], A.data_ptr(), ld(A), plan.data_ptr(), stream(A))
+    return A
+
+
 def row_gather(A, B, perm):
     """B[i, :] = A[perm[i], :]."""
     m, n = B.shape

@@ -113,6 +113,8 @@ class StreamSet:
         dev = torch.device(device)
         out, seen = [], set()
         for key, ss in cls._cache.items():
+            if ss.serial:
+                continue          # runs on the caller's stream: not a library stream
             if ss.gpu and ss.device == dev or (ss.gpu and dev.index is None and ss.device.type == dev.type):
                 for st in [ss.panel, ss.diag] + list(ss.update):
                     if st is not None and id(st) not in seen:
@@ -135,7 +137,11 @@ class StreamSet:
         """Raise if this process drives more work streams than the hardware
         queues it may map them to (MAX_WORK_STREAMS)."""
         if self.gpu:
-            n = StreamSet.census(self.device)
+            # the library's own streams plus ONE caller stream (whichever
+            # stream the caller enqueues on -- a side stream of theirs is
+            # as legitimate as the default one)
+            cur = torch.cuda.current_stream(self.device)
+            n = len([st for st in StreamSet.streams_of(self.device) if st != cur]) + 1
             if n > MAX_WORK_STREAMS:
                 from ..core.exceptions import SlateError
                 raise SlateError(f"{n} work streams on {self.device} > {MAX_WORK_STREAMS}")

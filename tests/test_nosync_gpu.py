@@ -155,6 +155,42 @@ def test_potrf_use_graph():
     assert sl.potrf(A, {sl.Option.Lookahead: 1, sl.Option.UseGraph: True}) == 101
 
 
+def test_potrf_use_graph_workspace_survives_other_streams():
+    """the captured kernels point into per-stream
+    workspaces; the graph owns a private capture stream, so a larger eager
+    potrf/trsm on fresh torch streams afterwards (which may be handed the
+    pooled handles) cannot free them.  Capture, run bigger eager work on new
+    streams, replay, compare."""
+    dev = torch.device("cuda")
+    n, nb = 2048, 256
+    A = sl.HermitianMatrix(sl.Uplo.Lower, n, nb=nb, device=dev)
+    A.insertLocalTiles(device=dev)
+    buf = A.storage.local[A.storage.origin_slot]
+    sl.generate_matrix(A, "poev", seed=11)
+    F0 = buf[:n, :n].clone()
+    assert sl.potrf(A, {sl.Option.Lookahead: 1, sl.Option.UseGraph: True}) == 0
+    from slate_amd import ops
+    n2 = 3072
+    B = sl.HermitianMatrix(sl.Uplo.Lower, n2, nb=512, device=dev)
+    B.insertLocalTiles(device=dev)
+    T = torch.eye(3000, dtype=torch.float64, device=dev).mT.contiguous().mT
+    X = torch.randn(3000, 3000, dtype=torch.float64, device=dev).mT.contiguous().mT
+    for _ in range(34):          # cycle through torch's round-robin stream pool
+        st = torch.cuda.Stream(device=dev)
+        with torch.cuda.stream(st):
+            sl.generate_matrix(B, "poev", seed=12)
+            assert sl.potrf(B, {sl.Option.Lookahead: 1}) == 0
+            ops.trsm('L', 'L', 'N', 'N', 1.0, T, X)
+        st.synchronize()
+    buf[:n, :n].copy_(F0)
+    assert sl.potrf(A, {sl.Option.Lookahead: 1, sl.Option.UseGraph: True}) == 0
+    Lg = torch.tril(buf[:n, :n]).clone()
+    buf[:n, :n].copy_(F0)
+    assert sl.potrf(A, {sl.Option.Lookahead: 1}) == 0
+    Le = torch.tril(buf[:n, :n])
+    assert (Lg - Le).abs().max().item() <= 1e-12 * Le.abs().max().item()
+
+
 @pytest.mark.parametrize("W", [512, 1536])
 def test_potrf_out_of_core(W, monkeypatch):
     """Host-origin matrix, device target, forced out-of-core block columns
