@@ -129,11 +129,11 @@ static void register_kernels(py::module& m) {
         stedc_secular(n, P<double>(d), P<double>(z), rho, zz, P<i64>(org), P<double>(mu), P<double>(zh),
                       P<double>(V), ldv, S(st)); });
     m.def("steqr_leaves", [](i64 nleaf, uintptr_t lo, uintptr_t hi, uintptr_t d, uintptr_t e, uintptr_t w,
-                             uintptr_t Q, i64 ldq, i64 r0, i64 r1, uintptr_t fails, uintptr_t st, int maxleaf) {
+                             uintptr_t Q, i64 ldq, i64 r0, i64 r1, uintptr_t fails, uintptr_t st, int maxleaf, int maxit) {
         steqr_leaves(nleaf, P<const i64>(lo), P<const i64>(hi), P<const double>(d), P<const double>(e), P<double>(w),
-                     P<double>(Q), ldq, r0, r1, P<i64>(fails), S(st), maxleaf); }, py::arg("nleaf"), py::arg("lo"),
+                     P<double>(Q), ldq, r0, r1, P<i64>(fails), S(st), maxleaf, maxit); }, py::arg("nleaf"), py::arg("lo"),
           py::arg("hi"), py::arg("d"), py::arg("e"), py::arg("w"), py::arg("Q"), py::arg("ldq"), py::arg("r0"),
-          py::arg("r1"), py::arg("fails"), py::arg("st"), py::arg("maxleaf") = 64);
+          py::arg("r1"), py::arg("fails"), py::arg("st"), py::arg("maxleaf") = 64, py::arg("maxit") = 60);
     m.def("stedc_runs", [](i64 nn, uintptr_t c, uintptr_t dd, uintptr_t z, uintptr_t ty, double tol, uintptr_t cs,
                            uintptr_t sn, uintptr_t rot, uintptr_t keep, uintptr_t st) {
         stedc_runs(nn, P<const i64>(c), P<const double>(dd), P<double>(z), P<int>(ty), tol, P<double>(cs),

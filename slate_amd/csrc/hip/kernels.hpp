@@ -116,7 +116,7 @@ template <typename T> void tri_inv(char uplo, char diag, i64 n, const T* A, i64 
 void stedc_secular(i64 n, const double* d, const double* z, double rho, double zz, i64* org, double* mu,
                    double* zh, double* V, i64 ldv, hipStream_t s);
 void steqr_leaves(i64 nleaf, const i64* lo, const i64* hi, const double* d, const double* e, double* w, double* Q,
-                  i64 ldq, i64 r0, i64 r1, i64* fails, hipStream_t s, int maxleaf = 64);
+                  i64 ldq, i64 r0, i64 r1, i64* fails, hipStream_t s, int maxleaf, int maxit = 60);
 void stedc_runs(i64 nn, const i64* c, const double* dd, double* z, int* ty, double tol, double* cs, double* sn,
                 int* rot, int* keep, hipStream_t s);
 void rot_cols(i64 m, double* Q, i64 ldq, i64 nrot, const i64* I, const i64* J, const double* C, const double* S,

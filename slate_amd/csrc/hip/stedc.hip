@@ -311,7 +311,7 @@ template <int LEAF>
 __global__ void __launch_bounds__(LEAF)
 steqr_leaf_kernel(const i64* __restrict__ lo, const i64* __restrict__ hi, const double* __restrict__ d_in,
                   const double* __restrict__ e_in, double* __restrict__ w, double* __restrict__ Q, i64 ldq, i64 r0,
-                  i64 r1, i64* fails) {
+                  i64 r1, i64* fails, int maxit) {
     extern __shared__ double Z[];                  // LEAF * LEAF, column-major
     __shared__ double d[LEAF], ew[LEAF];
     const int lane = threadIdx.x;
@@ -334,7 +334,7 @@ steqr_leaf_kernel(const i64* __restrict__ lo, const i64* __restrict__ hi, const 
                 if (fabs(ew[m]) <= eps * dd || fabs(ew[m]) < tiny) break;
             }
             if (m == l) break;
-            if (++iter > 60) { ++nfail; break; }
+            if (++iter > maxit) { ++nfail; break; }
             double g = (d[l + 1] - d[l]) / (2.0 * ew[l]);
             double r = hypot(g, 1.0);
             g = d[m] - d[l] + ew[l] / (g + copysign(r, g));
@@ -451,11 +451,11 @@ rot_cols_kernel(i64 m, double* __restrict__ Q, i64 ldq, i64 nrot, const i64* __r
 }
 
 void steqr_leaves(i64 nleaf, const i64* lo, const i64* hi, const double* d, const double* e, double* w, double* Q,
-                  i64 ldq, i64 r0, i64 r1, i64* fails, hipStream_t s, int maxleaf) {
+                  i64 ldq, i64 r0, i64 r1, i64* fails, hipStream_t s, int maxleaf, int maxit) {
     if (nleaf <= 0) return;
     if (maxleaf <= 64) {
         hipLaunchKernelGGL(steqr_leaf_kernel<64>, dim3((unsigned)nleaf), dim3(64), 64 * 64 * sizeof(double), s, lo, hi,
-                           d, e, w, Q, ldq, r0, r1, fails);
+                           d, e, w, Q, ldq, r0, r1, fails, maxit);
     } else {
         if (maxleaf > 128) throw std::invalid_argument("steqr_leaves: leaves of at most 128 rows");
         static bool attr = [] {
@@ -465,7 +465,7 @@ void steqr_leaves(i64 nleaf, const i64* lo, const i64* hi, const double* d, cons
         }();
         (void)attr;
         hipLaunchKernelGGL(steqr_leaf_kernel<128>, dim3((unsigned)nleaf), dim3(128), 128 * 128 * sizeof(double), s, lo,
-                           hi, d, e, w, Q, ldq, r0, r1, fails);
+                           hi, d, e, w, Q, ldq, r0, r1, fails, maxit);
     }
     HIP_LAUNCH_CHECK();
 }

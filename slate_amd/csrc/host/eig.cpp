@@ -371,6 +371,12 @@ void rot_seq(i64 nrow, Z_t* z, i64 ldz, const std::vector<i64>& idx, const std::
 }
 
 // ---------------------------------------------------------------- steqr
+// QL sweeps per eigenvalue before giving up (LAPACK: 30 n total); the
+// SLATE_AMD_STEQR_MAXIT override lets tests force non-convergence
+static int steqr_maxit() {
+    const char* e = std::getenv("SLATE_AMD_STEQR_MAXIT");
+    return e ? std::atoi(e) : 60;
+}
 // Implicit-shift QL/QR on the symmetric tridiagonal (d, e); optional
 // eigenvector accumulation Z (nz x n, columns rotated).  Eigenvalues sorted
 // ascending (with Z columns) on exit.  Returns 0 or #unconverged.
@@ -382,6 +388,7 @@ i64 steqr_impl(i64 n, double* d, double* e, Z_t* z, i64 ldz, i64 nz) {
     std::vector<R> ew(n, 0);
     for (i64 i = 0; i < n - 1; ++i) ew[i] = e[i];
     i64 fails = 0;
+    const int maxit = steqr_maxit();
     std::vector<i64> idx; std::vector<R> cs, sn;
     for (i64 l = 0; l < n; ++l) {
         i64 iter = 0;
@@ -392,7 +399,7 @@ i64 steqr_impl(i64 n, double* d, double* e, Z_t* z, i64 ldz, i64 nz) {
                 if (std::abs(ew[m]) <= eps * dd || std::abs(ew[m]) < std::numeric_limits<R>::min()) break;
             }
             if (m == l) break;
-            if (++iter > 60) { ++fails; break; }
+            if (++iter > maxit) { ++fails; break; }
             // Wilkinson-type shift from the leading 2x2
             R g = (d[l + 1] - d[l]) / (2 * ew[l]);
             R r = std::hypot(g, R(1));

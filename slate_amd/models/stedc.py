@@ -112,12 +112,13 @@ def stedc_rows(d, e, comm=None, device=None, leaf=None):
         leaves, levels = _tree(n, cap if leaf is None else min(int(leaf), cap))
         dl = _split_diag(d, e, levels)
         own = [(a, b) for (a, b) in leaves if a < r1 and b > r0] if P > 1 else leaves
-        _leaves(own, dl, e, w, Q, r0, r1, dev)
+        fails = _leaves(own, dl, e, w, Q, r0, r1, dev)
         for t in range(len(levels) - 1, -1, -1):
             mine = [(a, m, b) for (a, m, b) in levels[t] if a < r1 and b > r0]
             W, Z = _level_inputs(levels[t], w, Q, r0, r1, comm, dev)
             for (a, m, b) in mine:
                 _merge(a, m, b, float(e[m - 1]), W, Z, w, Q, r0, r1, dev)
+        _check_leaves(fails, comm if P > 1 else None)
     return w.cpu(), Q, r0, r1, mb
 
 
@@ -130,17 +131,39 @@ def _leaves(own, dl, e, w, Q, r0, r1, dev):
         dd = torch.from_numpy(dl).pin_memory().to(dev, non_blocking=True)
         ee = torch.from_numpy(np.concatenate([e, [0.0]])).pin_memory().to(dev, non_blocking=True)
         fails = torch.zeros(1, dtype=torch.int64, device=dev)
+        import os
         _hip().steqr_leaves(len(own), lo.data_ptr(), hi.data_ptr(), dd.data_ptr(), ee.data_ptr(), w.data_ptr(),
                             Q.data_ptr(), max(1, Q.stride(1)), r0, r1, fails.data_ptr(),
-                            torch.cuda.current_stream(dev).cuda_stream, max(b - a for a, b in own))
-        return
+                            torch.cuda.current_stream(dev).cuda_stream, max(b - a for a, b in own),
+                            int(os.environ.get("SLATE_AMD_STEQR_MAXIT", "60")))
+        return fails
+    nfail = 0
     from .eig import steqr
     for (a, b) in own:
-        wl, Zl = steqr(torch.from_numpy(dl[a:b].copy()), torch.from_numpy(e[a:b - 1].copy()))
+        try:
+            wl, Zl = steqr(torch.from_numpy(dl[a:b].copy()), torch.from_numpy(e[a:b - 1].copy()))
+        except SlateError:
+            nfail += 1
+            continue
         w[a:b] = wl
         lo, hi = max(a, r0), min(b, r1)
         if hi > lo:
             Q[lo - r0:hi - r0, a:b] = Zl[lo - a:hi - a, :].to(Q.dtype)
+    return torch.tensor([nfail], dtype=torch.int64)
+
+
+def _check_leaves(fails, comm):
+    """a leaf whose QL iteration did not converge leaves wrong
+    eigenpairs behind -- read the device counter once at the end (pinned,
+    non-blocking: no extra sync point inside the D&C), reduce it over the
+    ranks and fail like LAPACK stedc (info > 0) instead of returning them."""
+    from ._util import read_to_host
+    nf = int(read_to_host(fails)[0]) if fails is not None else 0
+    if comm is not None and comm.size > 1:
+        nf = int(comm.allreduce_scalar(nf, "max", torch.int64))
+    if nf:
+        from ..core.exceptions import NumericalError
+        raise NumericalError(f"stedc: {nf} leaf eigenproblem(s) did not converge", nf)
 
 
 def _level_inputs(merges, w, Q, r0, r1, comm, dev):

@@ -95,6 +95,7 @@ class Comm:
         return f"Comm(size={self.size}, rank={self.rank}, backend={self.backend})"
 
     # -- collectives -----------------------------------------------------
+    @_wd.watched("comm.barrier")
     def barrier(self):
         _wd.beat("comm.barrier")
         if self.size > 1:
@@ -105,6 +106,7 @@ class Comm:
             else:
                 dist.barrier(group=self.group)
 
+    @_wd.watched("comm.bcast")
     def bcast(self, t: torch.Tensor, root: int, async_op=False):
         """Broadcast t from comm-rank root (in place)."""
         _wd.beat("comm.bcast")
@@ -127,6 +129,7 @@ class Comm:
         except Exception as e:  # noqa: BLE001
             raise CommError(f"bcast failed: {e}") from e
 
+    @_wd.watched("comm.allreduce")
     def allreduce(self, t: torch.Tensor, op: str = "sum"):
         _wd.beat("comm.allreduce")
         if self.size == 1:
@@ -150,6 +153,7 @@ class Comm:
             t.copy_(src)
         return t
 
+    @_wd.watched("comm.allreduce_scalar")
     def allreduce_scalar(self, v, op="sum", dtype=torch.float64, device=None):
         if self.size == 1:
             return v
@@ -158,6 +162,7 @@ class Comm:
         self.allreduce(t, op)
         return t.item()
 
+    @_wd.watched("comm.maxloc")
     def maxloc(self, value: float, index: int):
         """Global (max value, index of max) over ranks; NaN wins, ties -> lowest index."""
         if self.size == 1:
@@ -173,6 +178,7 @@ class Comm:
                 best_v, best_i = v, i
         return best_v, best_i
 
+    @_wd.watched("comm.allgather")
     def allgather(self, t: torch.Tensor) -> torch.Tensor:
         """Concatenate equal-size tensors from all ranks along a new dim 0."""
         _wd.beat("comm.allgather")
@@ -190,6 +196,7 @@ class Comm:
         out = flat.view((self.size,) + tuple(t.shape))
         return out.to(t.device) if out.device != t.device else out
 
+    @_wd.watched("comm.allgatherv")
     def allgatherv(self, t: torch.Tensor) -> list:
         """All-gather of variable-length 1-D tensors (SLATE stedc Allgatherv)."""
         _wd.beat("comm.allgatherv")
@@ -204,6 +211,7 @@ class Comm:
         allb = self.allgather(buf)
         return [allb[r, : ns[r]].to(t.device) for r in range(self.size)]
 
+    @_wd.watched("comm.reduce")
     def reduce(self, t: torch.Tensor, root: int, op="sum"):
         _wd.beat("comm.reduce")
         if self.size == 1:
@@ -215,6 +223,7 @@ class Comm:
             t.copy_(x)
         return t
 
+    @_wd.watched("comm.send")
     def send(self, t: torch.Tensor, dst: int, tag: int = 0):
         _wd.beat("comm.send")
         if self.size == 1:
@@ -223,6 +232,7 @@ class Comm:
         dist.send(x, dst=self._g(dst), group=self.group, tag=tag) if self.backend != "nccl" else \
             dist.send(x, dst=self._g(dst), group=self.group)
 
+    @_wd.watched("comm.recv")
     def recv(self, t: torch.Tensor, src: int, tag: int = 0):
         _wd.beat("comm.recv")
         if self.size == 1:
@@ -236,6 +246,7 @@ class Comm:
             t.copy_(x)
         return t
 
+    @_wd.watched("comm.sendrecv")
     def sendrecv(self, send_t: torch.Tensor, dst: int, recv_t: torch.Tensor, src: int):
         """Simultaneous exchange (MPI_Sendrecv) via batched p2p."""
         _wd.beat("comm.sendrecv")
@@ -251,6 +262,7 @@ class Comm:
         recv_t.copy_(xr)
         return recv_t
 
+    @_wd.watched("comm.exchange")
     def exchange(self, sends: dict, recvs: dict):
         """Batched point-to-point: sends {dst: tensor}, recvs {src: tensor}."""
         _wd.beat("comm.exchange")
@@ -270,6 +282,7 @@ class Comm:
         for x, t in fix:
             t.copy_(x)
 
+    @_wd.watched("comm.bcast_object")
     def bcast_object(self, obj, root: int):
         if self.size == 1:
             return obj

@@ -47,18 +47,40 @@ def beat(tag: str = "") -> None:
     _state["n"] += 1
 
 
-_depth = [0]
+_depth = [0]          # library regions open in this PROCESS (all threads; under _lock)
 
 
 def enter(tag: str = "") -> None:
-    """Entering a library region (nestable)."""
-    _depth[0] += 1
+    """Entering a library region (nestable, thread-safe)."""
+    with _lock:
+        _depth[0] += 1
     beat(tag)
 
 
 def leave(tag: str = "") -> None:
-    _depth[0] = max(0, _depth[0] - 1)
+    with _lock:
+        _depth[0] = max(0, _depth[0] - 1)
     beat(tag)
+
+
+def watched(tag: str):
+    """Decorator: the call is a library region (enter / leave around it).
+    Every Comm collective and point-to-point call carries it, so a peer lost
+    in a barrier or all-reduce OUTSIDE any driver -- bench's timing
+    barriers, finalize, user-level comm calls -- still trips the watchdog
+    (ADVICE r3)."""
+    import functools
+
+    def deco(fn):
+        @functools.wraps(fn)
+        def wrapped(*a, **k):
+            enter(tag)
+            try:
+                return fn(*a, **k)
+            finally:
+                leave(tag)
+        return wrapped
+    return deco
 
 
 def inside() -> bool:

@@ -456,6 +456,34 @@ def test_stedc_rows_one_rank():
     assert float((T @ Q - Q * w).abs().max()) < 1e-12 * n
 
 
+def test_stedc_leaf_nonconvergence_raises(monkeypatch):
+    """a leaf QL that hits its iteration cap must not return
+    wrong eigenpairs silently -- stedc raises with info = #failed leaves."""
+    import numpy as np
+    from slate_amd.core.exceptions import NumericalError
+    from slate_amd.models.stedc import stedc_rows
+    monkeypatch.setenv("SLATE_AMD_STEQR_MAXIT", "0")
+    rng = np.random.default_rng(6)
+    n = 100
+    d, e = rng.standard_normal(n), rng.standard_normal(n - 1)
+    with pytest.raises(NumericalError) as ei:
+        stedc_rows(d, e, None, "cpu", leaf=32)
+    assert ei.value.info >= 1
+
+
+@pytest.mark.gpu
+def test_stedc_leaf_nonconvergence_raises_gpu(monkeypatch):
+    import numpy as np
+    from slate_amd.core.exceptions import NumericalError
+    from slate_amd.models.stedc import stedc_rows
+    monkeypatch.setenv("SLATE_AMD_STEQR_MAXIT", "0")
+    rng = np.random.default_rng(6)
+    n = 300
+    d, e = rng.standard_normal(n), rng.standard_normal(n - 1)
+    with pytest.raises(NumericalError):
+        stedc_rows(d, e, None, "cuda")
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("early,lag,reuse", [("1", "3", "1"), ("1", "3", "0"), ("0", "3", "0"), ("0", "4", "0")])
 def test_hb2st_gpu_matches_host_chase(early, lag, reuse, monkeypatch):

@@ -41,6 +41,51 @@ def test_watchdog_quiet_while_beating():
     assert not seen
 
 
+def test_watchdog_fires_in_comm_call_outside_driver():
+    """a collective issued outside any driver (a timing barrier,
+    finalize, user-level comm) is a library region: a peer lost there fires
+    the watchdog.  The hang is simulated by a Comm method that sleeps."""
+    from slate_amd.parallel.comm import Comm
+
+    class Stuck(Comm):
+        def __init__(self):
+            pass
+
+        @wd.watched("comm.barrier")
+        def barrier(self):
+            time.sleep(1.0)
+
+    seen = []
+    w = sl.Watchdog(0.3, abort=False, callback=seen.append, poll=0.05).start()
+    try:
+        assert not wd.inside()
+        Stuck().barrier()
+    finally:
+        w.stop()
+    assert seen and seen[0]["tag"] == "comm.barrier"
+    assert not wd.inside()
+
+
+def test_comm_methods_are_watched_regions():
+    from slate_amd.parallel.comm import Comm
+    for name in ("barrier", "bcast", "allreduce", "allgather", "reduce", "send", "recv", "exchange"):
+        assert getattr(Comm, name).__wrapped__ is not None, name
+
+
+def test_watchdog_depth_thread_safe():
+    import threading
+
+    def worker():
+        for _ in range(2000):
+            wd.enter("x")
+            wd.leave("x")
+
+    ts = [threading.Thread(target=worker) for _ in range(8)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert not wd.inside()
+
+
 def test_driver_steps_beat():
     n0 = wd.last_beat()[2]
     A = sl.HermitianMatrix(sl.Uplo.Lower, 64, nb=16, device=torch.device("cpu"))
