@@ -136,9 +136,15 @@ def _potrf_lower(A, opts):
     diag_first = la >= 1 and nt > 1 and os.environ.get("SLATE_AMD_POTRF_DIAGFIRST", "1") != "0"
     ev_diag = {}
     ev_tr = {}
+    # tile rows per row-broadcast chunk after the first (SLATE_AMD_POTRF_CHUNK)
+    chunk_tiles = max(1, int(os.environ.get("SLATE_AMD_POTRF_CHUNK", "4")))
+    esz = torch.empty(0, dtype=dtype).element_size()
+    POTRF_BCAST_STATS.clear()
     ss.fork()
     for t in range(nt):
         _wd.beat(f"potrf step {t}")
+        st_step = {"step": t, "row_bytes_first": 0, "col_bytes_first": 0, "row_msgs": 0, "row_bytes": 0}
+        POTRF_BCAST_STATS.append(st_step)
         g = g0 + t
         kb = s.tileMb(g) if t < nt - 1 or A.last_mb is None else A.last_mb
         lrg = tiles_local_before(g, p, pr) * nb
@@ -171,24 +177,28 @@ def _potrf_lower(A, opts):
                     P = buf[lr1:lr_end, lcg:lcg + kb]
                     if P.shape[0]:
                         ops.trsm('R', 'L', ct, 'N', 1.0, D, P)
-                # diag-first: the next diagonal tile, on its own stream
+                # panel -> row, TILE-GRANULAR (SLATE's per-tile listBcastMT,
+                # potrf.cc:122-132): chunk 0 = the first tile row(s) of this
+                # process row -- the lookahead tiles' rows on their owners and
+                # the next diagonal tile's rows -- then chunks of CH tile rows,
+                # all issued asynchronously on the row communicator; each
+                # lookahead GEMM row block waits for its own chunk only, so the
+                # GEMM starts after ~one tile instead of the whole nrow x kb
+                # panel (67 MB per early step at n = 32768 on 2 x 4).
+                nrow = lr_end - lr1
+                chunks = _row_chunks(nrow, nb, la, p, chunk_tiles)
+                Prow, land = _bcast_panel_rows(grid, q, buf, lr1, lr_end, lcg, kb, own_col, g % q, chunks,
+                                               dtype, dev, st_step)
+                if chunks:
+                    land(0)
+                # diag-first: the next diagonal tile, on its own stream; its
+                # rows are the first rows of chunk 0 on the owning process row
                 kb1 = 0
                 if diag_first and t + 1 < nt:
                     g1 = g + 1
                     kb1 = s.tileMb(g1) if t + 1 < nt - 1 or A.last_mb is None else A.last_mb
                     if pr == g1 % p:
-                        # the rows of tile g+1 of the solved panel: a small
-                        # broadcast issued from the PANEL stream (every
-                        # collective of this driver is issued from the panel
-                        # stream in one program order on every rank; the diag
-                        # stream carries compute only)
-                        if q > 1:
-                            Pt = ops.colmajor_empty(kb1, kb, dtype, dev)
-                            if own_col:
-                                Pt.copy_(buf[lr1:lr1 + kb1, lcg:lcg + kb])
-                            grid.row_comm.bcast(Pt, g % q)
-                        else:
-                            Pt = buf[lr1:lr1 + kb1, lcg:lcg + kb]
+                        Pt = Prow[0:kb1]
                         ev_solve = ss.event(ss.panel)
                         with ss.use(ss.diag):
                             ss.wait(ss.diag, ev_solve)
@@ -199,27 +209,18 @@ def _potrf_lower(A, opts):
                             if la < 2 and t >= 1:
                                 ss.wait(ss.diag, ev_tr[t - 1])
                             if Pt.is_cuda and q > 1:
-                                Pt.record_stream(ss.diag)
+                                Prow.record_stream(ss.diag)
                             with trace_block("potrf::diag_first"):
                                 if pc == g1 % q:
                                     D1 = buf[lr1:lr1 + kb1, lc1:lc1 + kb1]
                                     ops.gemm(-1.0, Pt, Pt, 1.0, D1, 'N', ct, (1, 1 << 40, 1, 0, 1, 0, 0, 0, 0))
                                     ops.potrf('L', D1, infos[t + 1:t + 2])
                                     ev_diag[t + 1] = ss.event(ss.diag)
-                # panel -> row
-                nrow = lr_end - lr1
-                if q > 1:
-                    Prow = ops.colmajor_empty(nrow, kb, dtype, dev)
-                    if own_col and nrow:
-                        Prow.copy_(buf[lr1:lr_end, lcg:lcg + kb])
-                    if nrow:
-                        grid.row_comm.bcast(Prow, g % q)
-                else:
-                    Prow = buf[lr1:lr_end, lcg:lcg + kb]
-                # panel -> column: the lookahead tiles' rows now, the rest on
-                # the update stream below
+                # panel -> column: the lookahead tiles' rows now (they are in
+                # chunk 0), the rest after the lookahead update
                 if plans is not None:
                     Lla = assemble_cols(plans[t][0], Prow, grid, p, kb, dtype, dev)
+                    st_step["col_bytes_first"] = sum(plans[t][0][0][r][1] for r in range(p)) * kb * esz
                 else:
                     Lla = Lcol = Prow
             # lookahead columns g+1 .. g+la
@@ -228,19 +229,26 @@ def _potrf_lower(A, opts):
             # update (its first part): wait for exactly that part
             if t >= 1 and la > 0:
                 ss.wait(ss.panel, ev_tr[t - 1])
-            if lc_la > lc1 and nrow:
-                if kb1 and t + 1 in ev_diag and pr == (g + 1) % p and pc == (g + 1) % q:
+            diag_done = bool(kb1 and t + 1 in ev_diag and pr == (g + 1) % p and pc == (g + 1) % q)
+            for ci, (ra, rb) in enumerate(chunks):
+                if ci:
+                    land(ci)
+                if lc_la <= lc1:
+                    continue
+                if diag_done:
                     # the diagonal tile of g+1 is already updated and factored:
                     # its column below it, then the other lookahead columns
-                    if nrow > kb1:
-                        ops.gemm(-1.0, Prow[kb1:], Lla[0:kb1], 1.0, buf[lr1 + kb1:lr_end, lc1:lc1 + kb1], 'N', ct,
-                                 (1, nb, p, pr, q, pc, lr1 + kb1, lc1, 0))
+                    a1 = max(ra, kb1)
+                    if rb > a1:
+                        ops.gemm(-1.0, Prow[a1:rb], Lla[0:kb1], 1.0, buf[lr1 + a1:lr1 + rb, lc1:lc1 + kb1], 'N', ct,
+                                 (1, nb, p, pr, q, pc, lr1 + a1, lc1, 0))
                     if lc_la > lc1 + kb1:
-                        ops.gemm(-1.0, Prow, Lla[kb1:lc_la - lc1], 1.0, buf[lr1:lr_end, lc1 + kb1:lc_la], 'N', ct,
-                                 (1, nb, p, pr, q, pc, lr1, lc1 + kb1, 0))
+                        ops.gemm(-1.0, Prow[ra:rb], Lla[kb1:lc_la - lc1], 1.0, buf[lr1 + ra:lr1 + rb, lc1 + kb1:lc_la],
+                                 'N', ct, (1, nb, p, pr, q, pc, lr1 + ra, lc1 + kb1, 0))
                 else:
-                    mask = (1, nb, p, pr, q, pc, lr1, lc1, 0)
-                    ops.gemm(-1.0, Prow, Lla[0:lc_la - lc1], 1.0, buf[lr1:lr_end, lc1:lc_la], 'N', ct, mask)
+                    mask = (1, nb, p, pr, q, pc, lr1 + ra, lc1, 0)
+                    ops.gemm(-1.0, Prow[ra:rb], Lla[0:lc_la - lc1], 1.0, buf[lr1 + ra:lr1 + rb, lc1:lc_la], 'N', ct,
+                             mask)
             # the trailing update's transposed rows: gathered over the same
             # column communicator, from the panel stream, AFTER the lookahead
             # update (off the critical chain; one issue order of collectives
@@ -274,6 +282,59 @@ def _potrf_lower(A, opts):
     ss.join()
     s.mark_local_modified(slot)
     return _potrf_info(s, infos, g0, nt)
+
+
+# per step of the last distributed potrf on this rank: bytes of the row
+# broadcast the first lookahead GEMM waits for (chunk 0), of the column
+# broadcasts assembling its operand, and the whole row broadcast
+POTRF_BCAST_STATS = []
+
+
+def _row_chunks(nrow, nb, la, p, ch):
+    """Row ranges of the tile-granular panel broadcast: chunk 0 = the tiles
+    holding this process row's lookahead rows (ceil(la / p) tile rows, at
+    least one), then ``ch`` tile rows per chunk."""
+    if nrow <= 0:
+        return []
+    first = min(nrow, nb * max(1, -(-la // p)))
+    out, a = [(0, first)], first
+    while a < nrow:
+        b = min(nrow, a + ch * nb)
+        out.append((a, b))
+        a = b
+    return out
+
+
+def _bcast_panel_rows(grid, q, buf, lr1, lr_end, lcg, kb, own_col, root, chunks, dtype, dev, st):
+    """Issue every chunk's row broadcast asynchronously (the owner sends
+    contiguous copies of its rows); returns (Prow, land) where land(i) makes
+    the current stream wait for chunk i and places it in Prow.  q == 1:
+    Prow is the buffer itself."""
+    if q == 1:
+        return buf[lr1:lr_end, lcg:lcg + kb], (lambda i: None)
+    nrow = lr_end - lr1
+    Prow = buf[lr1:lr_end, lcg:lcg + kb] if own_col else ops.colmajor_empty(nrow, kb, dtype, dev)
+    esz = torch.empty(0, dtype=dtype).element_size()
+    pend = []
+    for ci, (a, b) in enumerate(chunks):
+        cb = ops.colmajor_empty(b - a, kb, dtype, dev)
+        if own_col:
+            cb.copy_(buf[lr1 + a:lr1 + b, lcg:lcg + kb])
+        w = grid.row_comm.bcast(cb, root, async_op=True)
+        pend.append((a, b, cb, w))
+        nbytes = (b - a) * kb * esz
+        st["row_msgs"] += 1
+        st["row_bytes"] += nbytes
+        if ci == 0:
+            st["row_bytes_first"] = nbytes
+
+    def land(i):
+        a, b, cb, w = pend[i]
+        if w is not None:
+            w.wait()
+        if not own_col:
+            Prow[a:b].copy_(cb)
+    return Prow, land
 
 
 _GRAPHS = {}

@@ -273,6 +273,31 @@ def _run_8(rank, size, p, q):
         f(p, q)
 
 
+def _potrf_bcast_granularity(rank, size, p, q):
+    """on the 2 x 4 grid, the first lookahead GEMM of a
+    step waits for at most one tile row of the panel's row broadcast plus
+    the lookahead tiles' column broadcast -- the equivalent of <= 4 MB at
+    nb = 512 -- not for the whole nrow x kb panel; the rest of the row
+    broadcast travels in several tile-granular messages behind it."""
+    from slate_amd.models import chol
+    n, nb = 2048, 128
+    A = herm(n, nb, 31, p, q, torch.float64, Uplo.Lower)
+    Af = full_herm(A)
+    assert sl.potrf(A, {sl.Option.Lookahead: 1}) == 0
+    L = torch.tril(D(A))
+    close(L @ L.mH, Af, 1e-12)
+    lim = 2 * nb * nb * 8                     # = 4 MB at nb = 512
+    st = chol.POTRF_BCAST_STATS
+    assert st and all(s["row_bytes_first"] + s["col_bytes_first"] <= lim for s in st), st
+    early = st[0]
+    assert early["row_bytes"] > lim, early     # the panel itself is larger ...
+    assert early["row_msgs"] >= 3, early       # ... and goes in several messages
+
+
+def test_potrf_tile_granular_bcast_2x4():
+    run_dist(_potrf_bcast_granularity, 8, 2, 4, timeout=600)
+
+
 @pytest.mark.parametrize("grid", [(2, 4), (1, 8), (8, 1)], ids=lambda g: f"{g[0]}x{g[1]}")
 def test_eight_ranks(grid):
     """The 8-GPU node's grids (BASELINE: 2x4), rehearsed with 8 gloo ranks."""

@@ -16,3 +16,5 @@ tail -1 $D/bench_getrf.log
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/prof -o run -- python3 -u bench.py --routine getrf --lookahead 2 --steps 1 --warmup 1 > $D/prof.log 2>&1 || { tail -5 $D/prof.log; exit 1; }
 echo prof ok
+timeout -k 10 300 python -u tools/check_dist_gpu.py 4 > $D/dist4.log 2>&1 || { tail -20 $D/dist4.log; exit 1; }
+tail -8 $D/dist4.log
