@@ -231,6 +231,13 @@ static void register_kernels(py::module& m) {
         dispatch(dt, [&](auto z) { using T = decltype(z);
             laswp_cols_plan<T>(nrows, P<T>(A), lda, (const void*)plan, S(st)); });
     });
+    m.def("lu_dist_step", [](char dt, i64 nr, uintptr_t W, i64 ldw, uintptr_t grow, int c0, int c1, int j,
+                             uintptr_t recs, int p, uintptr_t Tt, i64 ldt, uintptr_t ipiv, uintptr_t info,
+                             i64 info_off, double thr, uintptr_t rec, uintptr_t part, i64 diag_local, uintptr_t st) {
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            lu_dist_step<T>(nr, P<T>(W), ldw, P<const i64>(grow), c0, c1, j, P<const T>(recs), p, P<T>(Tt), ldt,
+                            P<i64>(ipiv), P<i64>(info), info_off, thr, P<T>(rec), (void*)part, diag_local, S(st)); });
+    });
     m.def("row_gather", [](char dt, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t B, i64 ldb, uintptr_t perm,
                            uintptr_t st) {
         dispatch(dt, [&](auto z) { using T = decltype(z);

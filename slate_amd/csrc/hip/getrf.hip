@@ -810,21 +810,25 @@ getrf_base_tag(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64 iof
                TagBuf* tb, LaunchWords* lw, double thr, int N, int cabs, unsigned ep0) {
     __shared__ double wv[PT2 / 64];
     __shared__ int wi[PT2 / 64];
-    __shared__ double candL[PG][NBB + 1];
-    __shared__ double pvL[PG];
-    __shared__ int piL[PG];
-    __shared__ double drow[NBB], ud_s[NBB];
+    // parity double-buffered: column j+1's sweep fills one half while
+    // late waves still eliminate column j from the other
+    __shared__ double candL[2][PG][NBB + 1];
+    __shared__ double pvL[2][PG];
+    __shared__ int piL[2][PG];
+    __shared__ double drowL[2][NBB];
+    __shared__ double stg[2][NBB];          // staged winner row / next diagonal row
+    __shared__ double ud_s[NBB];
     __shared__ int s_abort, s_won, s_zero;
     __shared__ int piv_s[NBB], prv_s[NBB], tr_s[2 * NBB], ts_s[2 * NBB], s_nt;
     const int G = gridDim.x, g = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const i64 rbase = (i64)g * PT2 * R;
     double a[R][NBB];
-    #pragma unroll
+    #pragma clang loop unroll(full)
     for (int r = 0; r < R; ++r) {
         const i64 i = rbase + r * PT2 + tid;
         const i64 ir = i < m ? i : 0;
-        #pragma unroll
+        #pragma clang loop unroll(full)
         for (int c = 0; c < NBB; ++c) a[r][c] = A[ir + (i64)min(c, w - 1) * lda];
     }
     if (tid == 0) { s_abort = 0; s_won = 0; }
@@ -832,59 +836,70 @@ getrf_base_tag(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64 iof
     const bool prof = g_lu_prof_on && g == 0 && tid == 0;
     unsigned long long tl = prof ? clock64() : 0, ph[5] = {0, 0, 0, 0, 0};
 #define TSTAMP(k) do { if (prof) { const unsigned long long t_ = clock64(); ph[k] += t_ - tl; tl = t_; } } while (0)
+    // local arg-max of column JJ over rows i >= JJ, block winner (bv, bb)
+    // uniform after the barrier
+#define TAG_ARGMAX(JJ)                                                                       \
+    double bv, v = -1.0;                                                                     \
+    int bb, bi = (int)(rbase + tid);                                                          \
+    _Pragma("clang loop unroll(full)") for (int r = 0; r < R; ++r) {                                          \
+        const i64 i = rbase + r * PT2 + tid;                                                  \
+        const double vr = (i < m && i >= (JJ)) ? fabs(a[r][(JJ)]) : -1.0;                    \
+        if (r == 0 || beats(vr, i, v, (i64)bi)) { v = vr; bi = (int)i; }                      \
+    }                                                                                        \
+    { int dummy = 0; wave_argmax_dpp(v, bi, dummy); }                                        \
+    if (lane == 0) { wv[wid] = v; wi[wid] = bi; }                                            \
+    __syncthreads();                                                                         \
+    bv = wv[0]; bb = wi[0];                                                                  \
+    _Pragma("clang loop unroll(full)") for (int k = 1; k < PT2 / 64; ++k)                                     \
+        if (beats(wv[k], (i64)wi[k], bv, (i64)bb)) { bv = wv[k]; bb = wi[k]; }
+    // the staged rows (stg) go out as tagged granules, one or two per lane:
+    // wave 0 the winning row and (|v|, row), wave 1 the row JJ (its owner)
+#define TAG_PUBLISH(JJ)                                                                      \
+    {                                                                                        \
+        const int par_ = (JJ) & 1;                                                           \
+        const unsigned ep_ = ep0 + (unsigned)(JJ) + 1u;                                      \
+        const bool own_d = (JJ) >= rbase && (JJ) < rbase + (i64)R * PT2;                      \
+        if (wid == 0) {                                                                      \
+            const double x = stg[0][lane >> 1];                                              \
+            st_tag(&tb->rec[par_][g].g[lane], ep_, (lane & 1) ? hi32(x) : lo32(x));          \
+            if (lane < 2) st_tag(&tb->rec[par_][g].g[64 + lane], ep_, lane ? hi32(bv) : lo32(bv)); \
+            if (lane == 2) st_tag(&tb->rec[par_][g].g[66], ep_, (unsigned)bb);               \
+        } else if (wid == 1 && own_d) {                                                      \
+            const double x = stg[1][lane >> 1];                                              \
+            st_tag(&tb->diag[par_][lane], ep_, (lane & 1) ? hi32(x) : lo32(x));              \
+        }                                                                                    \
+    }
     __syncthreads();                                   // s_abort / s_won initialised
+    // ---- column 0: arg-max, stage, publish
+    if (w > 0) {
+        TAG_ARGMAX(0)
+        #pragma clang loop unroll(full)
+        for (int r = 0; r < R; ++r) {
+            const i64 i = rbase + r * PT2 + tid;
+            if (i == bb) {
+                #pragma clang loop unroll(full)
+                for (int c = 0; c < NBB; ++c) stg[0][c] = a[r][c];
+            }
+            if (i == 0) {
+                #pragma clang loop unroll(full)
+                for (int c = 0; c < NBB; ++c) stg[1][c] = a[r][c];
+            }
+        }
+        __syncthreads();
+        TAG_PUBLISH(0)
+    }
+    TSTAMP(1);
     // fully unrolled: j is a compile-time constant in every copy, so a[r][j]
-    // is a fixed register and the elimination touches columns > j only
+    // is a fixed register and the elimination touches columns > j only.
+    // Per column: sweep(j) -> pivot(j) -> interchange, multipliers and
+    // column j+1 only -> arg-max(j+1) -> the two publishing rows finish
+    // their elimination, are staged and go out -> everyone else finishes
+    // the elimination of column j while the records are in flight.
     #pragma clang loop unroll(full)
     for (int j = 0; j < NBB; ++j) {
         if (j < w && !s_abort) {
             const int par = j & 1;
             const unsigned ep = ep0 + (unsigned)j + 1u;
-            // ---- local arg-max of column j over unpivoted rows (i >= j)
-            double bv, v = -1.0;
-            int bb, bi = (int)(rbase + tid);
-            #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const i64 i = rbase + r * PT2 + tid;
-                const double vr = (i < m && i >= j) ? fabs(a[r][j]) : -1.0;
-                if (r == 0 || beats(vr, i, v, (i64)bi)) { v = vr; bi = (int)i; }
-            }
-            {
-                int dummy = 0;
-                wave_argmax_dpp(v, bi, dummy);
-            }
-            if (lane == 0) { wv[wid] = v; wi[wid] = bi; }
-            __syncthreads();
-            bv = wv[0]; bb = wi[0];
-            #pragma unroll
-            for (int k = 1; k < PT2 / 64; ++k)
-                if (beats(wv[k], (i64)wi[k], bv, (i64)bb)) { bv = wv[k]; bb = wi[k]; }
-            TSTAMP(0);
-            // ---- publish: the winning thread writes its row + (|v|, row); the
-            //      owner of row j writes row j -- tagged granules, no drain
-            const int s_bt_ = bb - (int)rbase;
-            TagRec& my = tb->rec[par][g];
-            #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                if (tid + r * PT2 == s_bt_) {
-                    #pragma unroll
-                    for (int c = 0; c < NBB; ++c) {
-                        st_tag(&my.g[2 * c], ep, lo32(a[r][c]));
-                        st_tag(&my.g[2 * c + 1], ep, hi32(a[r][c]));
-                    }
-                    st_tag(&my.g[64], ep, lo32(bv));
-                    st_tag(&my.g[65], ep, hi32(bv));
-                    st_tag(&my.g[66], ep, (unsigned)bb);
-                }
-                if (rbase + r * PT2 + tid == j) {
-                    #pragma unroll
-                    for (int c = 0; c < NBB; ++c) {
-                        st_tag(&tb->diag[par][2 * c], ep, lo32(a[r][c]));
-                        st_tag(&tb->diag[par][2 * c + 1], ep, hi32(a[r][c]));
-                    }
-                }
-            }
-            TSTAMP(1);
             // ---- sweep: wave q polls records q, q + 8, ...; wave (G % 8) also
             //      the row-j record.  Each lane owns one row granule (+ lanes
             //      0..2 the value / index granules) of each of its records.
@@ -901,16 +916,16 @@ getrf_base_tag(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64 iof
                         ok &= (unsigned)(x >> 32) == ep && (unsigned)(y >> 32) == ep;
                         // lanes 2c / 2c + 1 hold lo / hi of value c
                         const unsigned o = (unsigned)__shfl_xor((int)(unsigned)x, 1, 64);
-                        if ((lane & 1) == 0) candL[q][lane >> 1] = mk_d((unsigned)x, o);
+                        if ((lane & 1) == 0) candL[par][q][lane >> 1] = mk_d((unsigned)x, o);
                         const unsigned y1 = (unsigned)__shfl((int)(unsigned)y, 1, 64);
-                        if (lane == 0) pvL[q] = mk_d((unsigned)y, y1);
-                        if (lane == 2) piL[q] = (int)(unsigned)y;
+                        if (lane == 0) pvL[par][q] = mk_d((unsigned)y, y1);
+                        if (lane == 2) piL[par][q] = (int)(unsigned)y;
                     }
                     if (dwave) {
                         const unsigned long long x = ld_tag(&tb->diag[par][lane]);
                         ok &= (unsigned)(x >> 32) == ep;
                         const unsigned o = (unsigned)__shfl_xor((int)(unsigned)x, 1, 64);
-                        if ((lane & 1) == 0) drow[lane >> 1] = mk_d((unsigned)x, o);
+                        if ((lane & 1) == 0) drowL[par][lane >> 1] = mk_d((unsigned)x, o);
                     }
                     if (__all(ok) && !force) break;
                     if (force || ++spins > (1 << 20)) {           // not co-resident: abort, never hang
@@ -933,17 +948,18 @@ getrf_base_tag(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64 iof
                 // ---- global pivot, redundantly in every wave (DPP over the G partials)
                 double pv = -1.0;
                 int pi = j, pg = -1;
-                if (lane < G) { pv = pvL[lane]; pi = piL[lane]; pg = lane; }
+                if (lane < G) { pv = pvL[par][lane]; pi = piL[par][lane]; pg = lane; }
                 wave_argmax_dpp(pv, pi, pg);
                 i64 p = pi;
                 int gw = pg;
+                const double* drow = drowL[par];
                 if (!(pv >= 0.0) && !(pv != pv)) { p = j; gw = -1; }
                 if (thr < 1.0 && gw >= 0) {
                     const double dj = fabs(drow[j]);
                     if (dj == dj && dj >= thr * pv) { p = j; gw = -1; }
                 }
                 if (p == j) gw = -1;
-                const double* prow = gw < 0 ? drow : &candL[gw][0];
+                const double* prow = gw < 0 ? drow : &candL[par][gw][0];
                 const double u = prow[j];
                 if (tid == 0) {
                     piv_s[j] = (int)p;
@@ -951,32 +967,69 @@ getrf_base_tag(i64 m, int w, double* __restrict__ A, i64 lda, i64* ipiv, i64 iof
                 }
                 if (u == 0.0 && zero_at < 0) zero_at = j;
                 TSTAMP(3);
-                // ---- interchange rows j <-> p, eliminate column j (columns > j only)
-                #pragma unroll
+                // ---- interchange rows j <-> p, multipliers, column j+1 only
+                double lsv[R];
+                bool pend[R];
+                #pragma clang loop unroll(full)
                 for (int r = 0; r < R; ++r) {
                     const i64 i = rbase + r * PT2 + tid;
+                    pend[r] = false;
+                    lsv[r] = 0.0;
                     if (i < m && i >= j) {
                         if (i == j) {
-                            #pragma unroll
+                            #pragma clang loop unroll(full)
                             for (int c = 0; c < NBB; ++c) a[r][c] = prow[c];
                         } else {
                             if (i == p) {
-                                #pragma unroll
+                                #pragma clang loop unroll(full)
                                 for (int c = 0; c < NBB; ++c) a[r][c] = drow[c];
                             }
                             const double l = (u != 0.0) ? a[r][j] / u : a[r][j];
                             a[r][j] = l;
-                            #pragma unroll
-                            for (int c = j + 1; c < NBB; ++c) a[r][c] = fma(-l, prow[c], a[r][c]);
+                            lsv[r] = l;
+                            if (j + 1 < NBB) a[r][j + 1] = fma(-l, prow[j + 1], a[r][j + 1]);
+                            pend[r] = true;
                         }
                     }
                 }
+                if (j + 1 < w) {
+                    TAG_ARGMAX(j + 1)
+                    // the winner and the owner of row j+1 finish their rows now
+                    #pragma clang loop unroll(full)
+                    for (int r = 0; r < R; ++r) {
+                        const i64 i = rbase + r * PT2 + tid;
+                        if (pend[r] && (i == bb || i == j + 1)) {
+                            #pragma clang loop unroll(full)
+                            for (int c = j + 2; c < NBB; ++c) a[r][c] = fma(-lsv[r], prow[c], a[r][c]);
+                            pend[r] = false;
+                        }
+                        if (i == bb) {
+                            #pragma clang loop unroll(full)
+                            for (int c = 0; c < NBB; ++c) stg[0][c] = a[r][c];
+                        }
+                        if (i == j + 1) {
+                            #pragma clang loop unroll(full)
+                            for (int c = 0; c < NBB; ++c) stg[1][c] = a[r][c];
+                        }
+                    }
+                    __syncthreads();
+                    TAG_PUBLISH(j + 1)
+                }
+                // ---- everyone else: the rest of column j's elimination,
+                //      overlapping the records' flight
+                #pragma clang loop unroll(full)
+                for (int r = 0; r < R; ++r) {
+                    if (pend[r]) {
+                        #pragma clang loop unroll(full)
+                        for (int c = j + 2; c < NBB; ++c) a[r][c] = fma(-lsv[r], prow[c], a[r][c]);
+                    }
+                }
             }
-            // the next column's sweep rewrites candL / drow / pvL
-            __syncthreads();
             TSTAMP(4);
         }
     }
+#undef TAG_ARGMAX
+#undef TAG_PUBLISH
 #undef TSTAMP
     if (prof) {
         #pragma unroll

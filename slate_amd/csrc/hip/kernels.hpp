@@ -84,6 +84,12 @@ void laswp_cols(i64 nrows, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, i64 i
 template <typename T>
 void laswp_cols_plan(i64 nrows, T* A, i64 lda, const void* plan, hipStream_t s);
 
+// lu_dist.hip: one column step of the distributed partial-pivoting panel
+template <typename T>
+void lu_dist_step(i64 nr, T* W, i64 ldw, const i64* grow, int c0, int c1, int j, const T* recs, int p, T* Tt,
+                  i64 ldt, i64* ipiv, i64* info, i64 info_off, double thr, T* rec, void* part, i64 diag_local,
+                  hipStream_t s);
+
 // geqrf.hip
 template <typename T>
 void geqrf_panel_ws(i64 m, i64 n, T* A, i64 lda, T* tau, T* Tm, i64 ldt, T* V, i64 ldv, void* work,

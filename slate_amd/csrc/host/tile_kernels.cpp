@@ -628,7 +628,89 @@ static void dispatch(char dt, F&& f) {
 }
 template <typename T> static T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
 
+// One column step of the distributed partial-pivoting LU panel (host form
+// of csrc/hip/lu_dist.hip, same record layout and pivot rule): apply column
+// j-1 from the p gathered records, then this rank's record of column j.
+template <typename T>
+static void host_lu_dist_step(i64 nr, T* W, i64 ldw, const int64_t* grow, int c0, int c1, int j, const T* recs,
+                              int p, T* Tt, i64 ldt, int64_t* ipiv, int64_t* info, i64 info_off, double thr, T* rec,
+                              i64 diag_local) {
+    using R = real_t<T>;
+    const int b = c1 - c0, recn = 3 + 2 * b;
+    auto beats = [](R v, int64_t i, R w, int64_t k) { return (v != v && w == w) || v > w || (v == w && i < k); };
+    if (j > c0) {
+        const int jp = j - 1, jc = jp - c0;
+        R bv = R(-1);
+        int64_t bi = (int64_t)1 << 62;
+        int win = -1, dwn = -1;
+        for (int r = 0; r < p; ++r) {
+            const T* rc = recs + (i64)r * recn;
+            const R v = std::real(rc[0]);
+            if (std::real(rc[2]) != R(0)) dwn = r;
+            if (v >= R(0) || v != v) {
+                const int64_t gi = (int64_t)std::real(rc[1]);
+                if (win < 0 || beats(v, gi, bv, bi)) { bv = v; bi = gi; win = r; }
+            }
+        }
+        bool use_diag = win < 0;
+        if (!use_diag && thr < 1.0 && dwn >= 0) {
+            const R dj = abs1_(recs[(i64)dwn * recn + 3 + b + jc]);
+            if (dj == dj && (double)dj >= thr * (double)bv) use_diag = true;
+        }
+        const T* drow = recs + (i64)dwn * recn + 3 + b;
+        const T* prow = use_diag ? drow : recs + (i64)win * recn + 3;
+        const int64_t pg = use_diag ? jp : bi;
+        const T u = prow[jc];
+        for (i64 i = 0; i < nr; ++i) {
+            const int64_t gi = grow[i];
+            if (gi < jp) continue;
+            T* row = W + i;
+            if (gi == jp) {
+                for (int c = 0; c < b; ++c) row[c * ldw] = prow[c];
+                continue;
+            }
+            if (gi == pg)
+                for (int c = 0; c < b; ++c) row[c * ldw] = drow[c];
+            T l = row[jc * ldw];
+            if (u != T(0)) l /= u;
+            row[jc * ldw] = l;
+            for (int c = jc + 1; c < b; ++c) row[c * ldw] -= l * prow[c];
+        }
+        for (int c = 0; c < b; ++c) Tt[jp + (i64)(c0 + c) * ldt] = prow[c];
+        if (ipiv) ipiv[jp] = pg;
+        if (u == T(0) && info && *info == 0) *info = jp + 1 + info_off;
+    }
+    if (j < c1) {
+        const int jc = j - c0;
+        R v = R(-1);
+        i64 bi = -1;
+        for (i64 i = 0; i < nr; ++i) {
+            if (grow[i] < j) continue;
+            const R x = abs1_(W[i + (i64)jc * ldw]);
+            if (bi < 0 || beats(x, grow[i], v, grow[bi])) { v = x; bi = i; }
+        }
+        rec[0] = T(bi >= 0 ? v : R(-1));
+        rec[1] = T(bi >= 0 ? (R)grow[bi] : R(1e30));
+        rec[2] = T(diag_local >= 0 ? R(1) : R(0));
+        for (int c = 0; c < b; ++c) {
+            rec[3 + c] = bi >= 0 ? W[bi + (i64)c * ldw] : T(0);
+            rec[3 + b + c] = diag_local >= 0 ? W[diag_local + (i64)c * ldw] : T(0);
+        }
+    }
+}
+
 void register_tile_kernels(py::module& m) {
+    m.def("lu_dist_step", [](char dt, i64 nr, uintptr_t W, i64 ldw, uintptr_t grow, int c0, int c1, int j,
+                             uintptr_t recs, int p, uintptr_t Tt, i64 ldt, uintptr_t ipiv, uintptr_t info,
+                             i64 info_off, double thr, uintptr_t rec, uintptr_t /*part*/, i64 diag_local,
+                             uintptr_t /*stream*/) {
+        dispatch(dt, [&](auto z) {
+            using T = decltype(z);
+            host_lu_dist_step<T>(nr, P<T>(W), ldw, reinterpret_cast<const int64_t*>(grow), c0, c1, j, P<const T>(recs),
+                                 p, P<T>(Tt), ldt, reinterpret_cast<int64_t*>(ipiv),
+                                 reinterpret_cast<int64_t*>(info), info_off, thr, P<T>(rec), diag_local);
+        });
+    });
     m.def("gemm", [](char dt, char ta, char tb, i64 mm, i64 n, i64 k, std::complex<double> alpha,
                      uintptr_t A, i64 lda, uintptr_t B, i64 ldb, std::complex<double> beta,
                      uintptr_t C, i64 ldc, i64 batch, i64 sA, i64 sB, i64 sC, py::object mask,

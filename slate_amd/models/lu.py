@@ -17,9 +17,11 @@ MI355X design:
 * p == 1 grids (1 x q, and a single GPU) keep the whole step on device,
   stream-ordered with lookahead: panel + lookahead columns on the
   high-priority stream, trailing swaps/trsm/GEMM on the low-priority stream;
-* p > 1: the panel is gathered to the diagonal owner (one col-communicator
-  gather), factored there, scattered back; pivots are broadcast and the row
-  exchange between process rows is one batched point-to-point step.
+* p > 1: the panel rows stay on their owners -- per column one device step
+  and one all-gather of p small (|v|, row, candidate row) records over the
+  column communicator, every rank picking the same pivot (_panel_pp_dist);
+  pivots are broadcast and the row exchange between process rows is one
+  batched point-to-point step.
 Pivots: `Pivots` holds 0-based GLOBAL pivot rows (LAPACK ipiv - 1).
 """
 from __future__ import annotations
@@ -481,6 +483,13 @@ def _getrf_general(A, buf, thr, la, mode, leaf):
     pin = torch.empty(ipiv.numel(), dtype=torch.int64, pin_memory=buf.is_cuda)
     piv_ev, moves, pend = {}, {}, None
     XCHG_STATS.clear()
+    # partial pivoting: the panel rows stay on their owners (per-column
+    # record all-gather, _panel_pp_dist); SLATE_AMD_LU_PANEL_GATHER=1 selects
+    # the all-gather + redundant factor form (_panel_pp)
+    import os
+    pp_dist = os.environ.get("SLATE_AMD_LU_PANEL_GATHER", "0") != "1"
+    for key in LU_DIST_STATS:
+        LU_DIST_STATS[key] = 0
     ss.fork()
     import os
     kstop = int(os.environ.get("SLATE_AMD_DEBUG_LU_STEPS", kt))    # debugging: stop after k steps
@@ -509,7 +518,8 @@ def _getrf_general(A, buf, thr, la, mode, leaf):
             Lp, pv = pk.get("L"), pk.get("piv")[:, 0]
             with trace_block("getrf::panel"):
                 if pc == ck:
-                    {"pp": _panel_pp, "calu": _panel_calu, "nopiv": _panel_nopiv}[mode](ctx, st, ipiv, Lp, pv)
+                    {"pp": _panel_pp_dist if pp_dist else _panel_pp, "calu": _panel_calu,
+                     "nopiv": _panel_nopiv}[mode](ctx, st, ipiv, Lp, pv)
                 if q > 1:
                     rowc.bcast(pk.raw, ck)
                 piv.copy_(pv)
@@ -739,6 +749,99 @@ def _panel_pp(ctx, st, ipiv, Lp, pv):
         Lp[:nmine].copy_(mine)
     Lp[nmine:nmine + kb].copy_(P[:kb])
     pv.copy_(piv)
+
+
+def _panel_pp_dist(ctx, st, ipiv, Lp, pv):
+    """Partial pivoting with the panel rows staying on their owners (SLATE's
+    distributed panel: Tile_getrf.hh:160-447, internal_getrf.cc:20-121).
+
+    Recursive over the panel columns.  A base block of b columns is factored
+    column by column: one device step per column (apply the previous
+    column's pivot + rank-1 update on my rows, then my arg-max record:
+    |v|, global row, candidate row, and row j from its owner;
+    csrc/hip/lu_dist.hip) and ONE all-gather of the p small records over the
+    column communicator -- every rank then picks the same pivot, so no
+    MAXLOC + broadcast pair is needed.  Between the halves of a recursion
+    level, the left half's interchanges reach the right half's columns (and
+    the right half's the left half's) by the owner-masked row exchange of
+    the trailing update (xchg_gather / all-reduce / xchg_scatter: only the
+    touched rows travel); U12 = L11^{-1} A12 comes out of that exchange on
+    every rank, A22 -= L21 U12 is local.  No rank ever holds another rank's
+    panel rows: the bytes per column are p (2b + 3) scalars, not m x nb per
+    panel.  Every rank keeps the same copy T of the kb x kb top block."""
+    import os
+    from .._native import kmod, code, stream
+    buf, nb, p, pr, mloc, dt, dev = (ctx[x] for x in ("buf", "nb", "p", "pr", "mloc", "dt", "dev"))
+    r0, kb, lr_k, lc_k, nmine, k, rk = (st[x] for x in ("r0", "kb", "lr_k", "lc_k", "nmine", "k", "rk"))
+    colc, thr = ctx["colc"], ctx["thr"]
+    b = max(1, int(os.environ.get("SLATE_AMD_LU_DIST_B", "32")))
+    W = buf[lr_k:mloc, lc_k:lc_k + kb]
+    ldw = max(1, buf.stride(1))
+    grow = _rows_global(lr_k, mloc, nb, p, pr, r0, dev)
+    T = ops.colmajor_zeros(kb, kb, dt, dev)
+    piv = ipiv[r0:r0 + kb]
+    info = ctx["infos"][k:k + 1]
+    part = torch.empty(2 * 1024 + 8, dtype=torch.int64, device=dev)
+    mod = kmod(buf)
+    cd = code(dt)
+
+    def base(c0, c1):
+        recn = 3 + 2 * (c1 - c0)
+        recs = None
+        for j in range(c0, c1 + 1):
+            nxt = j < c1
+            rec = torch.empty(recn, dtype=dt, device=dev)
+            dl = j if (pr == rk and nxt) else -1
+            mod.lu_dist_step(cd, nmine, W[:, c0:c1].data_ptr() if nmine else buf.data_ptr(), ldw, grow.data_ptr(),
+                             c0, c1, j, recs.data_ptr() if recs is not None else 0, p, T.data_ptr(), max(1, kb),
+                             piv.data_ptr(), info.data_ptr(), 0, float(thr), rec.data_ptr(), part.data_ptr(), dl,
+                             stream(buf))
+            if nxt:
+                recs = colc.allgather(rec).contiguous()
+                LU_DIST_STATS["columns"] += 1
+                LU_DIST_STATS["record_bytes"] += recs.numel() * recs.element_size()
+
+    def exchange(a, bnd, ca, cb):
+        """interchanges of panel columns [a, bnd) applied to panel columns
+        [ca, cb) on every rank; returns the new window rows (bnd - a)."""
+        plan = ops.swap_plan(ipiv, r0 + a, r0 + bnd, ioff=-r0)
+        X = ops.colmajor_empty(2 * (bnd - a), cb - ca, dt, dev)
+        cols = buf[:mloc, lc_k + ca:lc_k + cb]
+        ops.xchg_gather(plan, cols, X, nb, p, pr)
+        colc.allreduce(X)
+        ops.xchg_scatter(plan, X, cols, nb, p, pr)
+        LU_DIST_STATS["exchange_bytes"] += X.numel() * X.element_size()
+        return X[0:bnd - a]
+
+    def rec(c0, c1):
+        if c1 - c0 <= b:
+            base(c0, c1)
+            return
+        cm = c0 + ((c1 - c0) // 2 + b - 1) // b * b
+        if cm >= c1:
+            cm = c1 - b
+        rec(c0, cm)
+        U = exchange(c0, cm, cm, c1)
+        ops.trsm('L', 'L', 'N', 'U', 1.0, T[c0:cm, c0:cm], U)
+        T[c0:cm, cm:c1].copy_(U)
+        if pr == rk:
+            W[c0:cm, cm:c1].copy_(U)
+        i0 = cm if pr == rk else 0
+        if nmine > i0:
+            ops.gemm(-1.0, W[i0:, c0:cm], U, 1.0, W[i0:, cm:c1])
+        rec(cm, c1)
+        T[cm:c1, c0:cm].copy_(exchange(cm, c1, c0, cm))
+
+    rec(0, kb)
+    if nmine:
+        Lp[:nmine].copy_(W)
+    Lp[nmine:nmine + kb].copy_(T)
+    pv.copy_(piv)
+
+
+# counters of the distributed panel on this rank (tests): columns factored,
+# record bytes all-gathered, exchange bytes all-reduced
+LU_DIST_STATS = {"columns": 0, "record_bytes": 0, "exchange_bytes": 0}
 
 
 def _panel_nopiv(ctx, st, ipiv, Lp, pv):

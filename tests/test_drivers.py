@@ -294,6 +294,44 @@ def _potrf_bcast_granularity(rank, size, p, q):
     assert early["row_msgs"] >= 3, early       # ... and goes in several messages
 
 
+def _lu_no_panel_allgather(rank, size, p, q):
+    """with p > 1 the partial-pivoting panel rows stay
+    on their owners -- the only all-gathers are the per-column records
+    (p (2b + 3) scalars); no rank receives another rank's m x nb panel."""
+    from slate_amd.models import lu as lu_mod
+    from slate_amd.parallel.comm import Comm
+    seen = []
+    orig = Comm.allgather
+
+    def spy(self, t):
+        seen.append(t.numel() * t.element_size())
+        return orig(self, t)
+
+    n, nb = 640, 64
+    A = mat(n, n, nb, 41, p, q, torch.float64)
+    A0 = D(A)
+    Comm.allgather = spy
+    try:
+        piv = sl.Pivots()
+        assert sl.getrf(A, piv, {sl.Option.Lookahead: 1}) == 0
+    finally:
+        Comm.allgather = orig
+    F = D(A)
+    L = torch.tril(F, -1) + torch.eye(n, dtype=F.dtype)
+    U = torch.triu(F)
+    perm = list(range(n))
+    for i, j in enumerate(piv.ipiv.tolist()):
+        perm[i], perm[j] = perm[j], perm[i]
+    close(L @ U, A0[torch.as_tensor(perm)], 1e-12)
+    b = 32
+    assert seen and max(seen) <= (2 * b + 3) * 8, max(seen)       # one record per call, never a panel
+    assert lu_mod.LU_DIST_STATS["columns"] > 0
+
+
+def test_lu_distributed_panel_2x4():
+    run_dist(_lu_no_panel_allgather, 8, 2, 4, timeout=600)
+
+
 def test_potrf_tile_granular_bcast_2x4():
     run_dist(_potrf_bcast_granularity, 8, 2, 4, timeout=600)
 
