@@ -173,12 +173,11 @@ def main():
     ap.add_argument("--grid", default=None, help="PxQ override")
     ap.add_argument("--check", type=int, default=1, help="residual check after timing (0 = skip)")
     args = ap.parse_args()
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and "SLATE_AMD_KEEP_HW_QUEUES" not in os.environ:
-        # one process per GPU drives ~7 streams (panel, diag, update, the
-        # default stream and one RCCL stream per communicator): give each its
-        # own hardware queue instead of multiplexing them onto HIP's default 4
-        # (set before the first HIP call of this process)
-        os.environ["GPU_MAX_HW_QUEUES"] = str(max(8, int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)))
+    # No GPU_MAX_HW_QUEUES override: a process drives the panel, diag and
+    # update streams plus the caller's -- the box default of 4 hardware
+    # queues.  RCCL adds none: torch runs every synchronous collective on
+    # the issuing stream (profiles/r4/nccl_stream_probe.txt) and each
+    # communicator is issued from one stream only (tests/test_dist_gpu.py).
 
     import slate_amd as sl
     comm = sl.init()

@@ -181,14 +181,15 @@ def _potrf_lower(A, opts):
                 # potrf.cc:122-132): chunk 0 = the first tile row(s) of this
                 # process row -- the lookahead tiles' rows on their owners and
                 # the next diagonal tile's rows -- then chunks of CH tile rows,
-                # all issued asynchronously on the row communicator; each
-                # lookahead GEMM row block waits for its own chunk only, so the
-                # GEMM starts after ~one tile instead of the whole nrow x kb
-                # panel (67 MB per early step at n = 32768 on 2 x 4).
+                # all on the diag stream (the row communicator's stream) while
+                # the panel stream runs the lookahead GEMM row block of each
+                # chunk as it lands: the GEMM starts after ~one tile instead of
+                # the whole nrow x kb panel (67 MB per early step at n = 32768
+                # on 2 x 4).
                 nrow = lr_end - lr1
                 chunks = _row_chunks(nrow, nb, la, p, chunk_tiles)
-                Prow, land = _bcast_panel_rows(grid, q, buf, lr1, lr_end, lcg, kb, own_col, g % q, chunks,
-                                               dtype, dev, st_step)
+                Prow, land, first = _bcast_panel_rows(grid, q, buf, lr1, lr_end, lcg, kb, own_col, g % q, chunks,
+                                                      dtype, dev, st_step, ss)
                 if chunks:
                     land(0)
                 # diag-first: the next diagonal tile, on its own stream; its
@@ -198,7 +199,9 @@ def _potrf_lower(A, opts):
                     g1 = g + 1
                     kb1 = s.tileMb(g1) if t + 1 < nt - 1 or A.last_mb is None else A.last_mb
                     if pr == g1 % p:
-                        Pt = Prow[0:kb1]
+                        # chunk 0 itself, on the diag stream right behind its
+                        # broadcast (q == 1: the panel rows)
+                        Pt = first[0:kb1]
                         ev_solve = ss.event(ss.panel)
                         with ss.use(ss.diag):
                             ss.wait(ss.diag, ev_solve)
@@ -209,7 +212,7 @@ def _potrf_lower(A, opts):
                             if la < 2 and t >= 1:
                                 ss.wait(ss.diag, ev_tr[t - 1])
                             if Pt.is_cuda and q > 1:
-                                Prow.record_stream(ss.diag)
+                                first.record_stream(ss.diag)
                             with trace_block("potrf::diag_first"):
                                 if pc == g1 % q:
                                     D1 = buf[lr1:lr1 + kb1, lc1:lc1 + kb1]
@@ -305,13 +308,18 @@ def _row_chunks(nrow, nb, la, p, ch):
     return out
 
 
-def _bcast_panel_rows(grid, q, buf, lr1, lr_end, lcg, kb, own_col, root, chunks, dtype, dev, st):
-    """Issue every chunk's row broadcast asynchronously (the owner sends
-    contiguous copies of its rows); returns (Prow, land) where land(i) makes
-    the current stream wait for chunk i and places it in Prow.  q == 1:
-    Prow is the buffer itself."""
+def _bcast_panel_rows(grid, q, buf, lr1, lr_end, lcg, kb, own_col, root, chunks, dtype, dev, st, ss):
+    """Issue every chunk's row broadcast on the DIAG stream -- the row
+    communicator's one stream (torch runs a synchronous RCCL collective on
+    the issuing stream, profiles/r4/nccl_stream_probe.txt, so a
+    communicator used from one stream adds no hardware queue and its
+    collectives keep one order on every rank); the owner sends contiguous
+    copies of its rows.  Returns (Prow, land, first): land(i) makes the
+    panel stream wait for chunk i and places it in Prow; ``first`` is chunk
+    0's buffer, on the diag stream.  q == 1: Prow is the buffer itself."""
     if q == 1:
-        return buf[lr1:lr_end, lcg:lcg + kb], (lambda i: None)
+        P = buf[lr1:lr_end, lcg:lcg + kb]
+        return P, (lambda i: None), P
     nrow = lr_end - lr1
     Prow = buf[lr1:lr_end, lcg:lcg + kb] if own_col else ops.colmajor_empty(nrow, kb, dtype, dev)
     esz = torch.empty(0, dtype=dtype).element_size()
@@ -320,8 +328,14 @@ def _bcast_panel_rows(grid, q, buf, lr1, lr_end, lcg, kb, own_col, root, chunks,
         cb = ops.colmajor_empty(b - a, kb, dtype, dev)
         if own_col:
             cb.copy_(buf[lr1 + a:lr1 + b, lcg:lcg + kb])
-        w = grid.row_comm.bcast(cb, root, async_op=True)
-        pend.append((a, b, cb, w))
+        ev_src = ss.event(ss.panel)
+        with ss.use(ss.diag):
+            ss.wait(ss.diag, ev_src)
+            if cb.is_cuda:
+                cb.record_stream(ss.diag)
+            grid.row_comm.bcast(cb, root)
+            ev = ss.event(ss.diag)
+        pend.append((a, b, cb, ev))
         nbytes = (b - a) * kb * esz
         st["row_msgs"] += 1
         st["row_bytes"] += nbytes
@@ -329,12 +343,11 @@ def _bcast_panel_rows(grid, q, buf, lr1, lr_end, lcg, kb, own_col, root, chunks,
             st["row_bytes_first"] = nbytes
 
     def land(i):
-        a, b, cb, w = pend[i]
-        if w is not None:
-            w.wait()
+        a, b, cb, ev = pend[i]
+        ss.wait(ss.panel, ev)
         if not own_col:
             Prow[a:b].copy_(cb)
-    return Prow, land
+    return Prow, land, (pend[0][2] if pend else Prow)
 
 
 _GRAPHS = {}

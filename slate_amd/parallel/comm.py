@@ -35,6 +35,10 @@ from ..core.exceptions import CommError
 from ..utils import watchdog as _wd
 
 
+# per-communicator issuing streams while "on" (tests: one stream per comm)
+STREAM_LOG = {"on": False, "used": {}}
+
+
 def _dist_ready() -> bool:
     return dist.is_available() and dist.is_initialized()
 
@@ -66,6 +70,15 @@ class Comm:
     # -- helpers ---------------------------------------------------------
     def _g(self, r):
         return self.ranks[r]
+
+    def _note(self, t):
+        """Stream log (tests): torch runs a synchronous RCCL collective on
+        the ISSUING stream (profiles/r4/nccl_stream_probe.txt), so the
+        drivers keep each communicator on one stream -- its collectives
+        then keep one order on every rank and add no hardware queue.  While
+        STREAM_LOG is enabled, record which streams issued on this comm."""
+        if STREAM_LOG["on"] and isinstance(t, torch.Tensor) and t.is_cuda and self.size > 1:
+            STREAM_LOG["used"].setdefault(id(self), set()).add(torch.cuda.current_stream(t.device).cuda_stream)
 
     def _prep(self, t: torch.Tensor):
         """gloo cannot move device tensors and RCCL cannot move host ones."""
@@ -110,6 +123,7 @@ class Comm:
     def bcast(self, t: torch.Tensor, root: int, async_op=False):
         """Broadcast t from comm-rank root (in place)."""
         _wd.beat("comm.bcast")
+        self._note(t)
         if self.size == 1:
             return None
         try:
@@ -132,6 +146,7 @@ class Comm:
     @_wd.watched("comm.allreduce")
     def allreduce(self, t: torch.Tensor, op: str = "sum"):
         _wd.beat("comm.allreduce")
+        self._note(t)
         if self.size == 1:
             return t
         rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
@@ -182,6 +197,7 @@ class Comm:
     def allgather(self, t: torch.Tensor) -> torch.Tensor:
         """Concatenate equal-size tensors from all ranks along a new dim 0."""
         _wd.beat("comm.allgather")
+        self._note(t)
         if self.size == 1:
             return t.unsqueeze(0)
         x, _ = self._prep(t.contiguous())
@@ -200,6 +216,7 @@ class Comm:
     def allgatherv(self, t: torch.Tensor) -> list:
         """All-gather of variable-length 1-D tensors (SLATE stedc Allgatherv)."""
         _wd.beat("comm.allgatherv")
+        self._note(t)
         if self.size == 1:
             return [t]
         x, _ = self._prep(t.contiguous().reshape(-1))
@@ -214,6 +231,7 @@ class Comm:
     @_wd.watched("comm.reduce")
     def reduce(self, t: torch.Tensor, root: int, op="sum"):
         _wd.beat("comm.reduce")
+        self._note(t)
         if self.size == 1:
             return t
         x, staged = self._prep(t.contiguous())
@@ -226,6 +244,7 @@ class Comm:
     @_wd.watched("comm.send")
     def send(self, t: torch.Tensor, dst: int, tag: int = 0):
         _wd.beat("comm.send")
+        self._note(t)
         if self.size == 1:
             return
         x, _ = self._prep(t.contiguous())
@@ -235,6 +254,7 @@ class Comm:
     @_wd.watched("comm.recv")
     def recv(self, t: torch.Tensor, src: int, tag: int = 0):
         _wd.beat("comm.recv")
+        self._note(t)
         if self.size == 1:
             return t
         x, _ = self._prep(t if t.is_contiguous() else t.contiguous())
@@ -250,6 +270,7 @@ class Comm:
     def sendrecv(self, send_t: torch.Tensor, dst: int, recv_t: torch.Tensor, src: int):
         """Simultaneous exchange (MPI_Sendrecv) via batched p2p."""
         _wd.beat("comm.sendrecv")
+        self._note(send_t)
         if self.size == 1:
             recv_t.copy_(send_t)
             return recv_t
@@ -266,6 +287,8 @@ class Comm:
     def exchange(self, sends: dict, recvs: dict):
         """Batched point-to-point: sends {dst: tensor}, recvs {src: tensor}."""
         _wd.beat("comm.exchange")
+        for t in list(sends.values()) + list(recvs.values()):
+            self._note(t)
         if self.size == 1 or (not sends and not recvs):
             return
         ops, fix = [], []

@@ -64,17 +64,20 @@ class StreamSet:
             if sh is None:
                 # torch: lower number = higher priority; ``diag`` carries the
                 # next step's diagonal-tile chain concurrently with the
-                # panel's broadcasts (potrf diag-first).  The update stream
-                # is created with the CU reservation of the first pipeline
-                # that runs in this process and then shared: a later routine
-                # asking for another reservation reuses it rather than adding
-                # a fourth work stream.
+                # panel's broadcasts (potrf diag-first).
                 sh = dict(panel=torch.cuda.Stream(device=device, priority=-1),
-                          diag=torch.cuda.Stream(device=device, priority=-1),
-                          update=self._update_stream(device, self.reserve_cus), reserve=self.reserve_cus)
+                          diag=torch.cuda.Stream(device=device, priority=-1), update={})
                 _SHARED[str(device)] = sh
+            # one update stream per CU reservation (a shared one
+            # kept the mask of whichever pipeline ran first, e.g. geqrf after
+            # getrf inherited its 32-CU reservation).  A pipeline drives only
+            # its own set -- panel, diag, one update stream -- plus the
+            # caller's stream: 4, the box's hardware queues (check_census).
+            up = sh["update"].get(self.reserve_cus)
+            if up is None:
+                up = sh["update"][self.reserve_cus] = self._update_stream(device, self.reserve_cus)
             self.panel, self.diag = sh["panel"], sh["diag"]
-            self.update = [sh["update"]] * n_update
+            self.update = [up] * n_update
         else:
             self.panel = self.diag = None
             self.update = [None] * n_update
@@ -136,12 +139,13 @@ class StreamSet:
     def check_census(self):
         """Raise if this process drives more work streams than the hardware
         queues it may map them to (MAX_WORK_STREAMS)."""
-        if self.gpu:
-            # the library's own streams plus ONE caller stream (whichever
+        if self.gpu and not self.serial:
+            # this pipeline's own streams plus ONE caller stream (whichever
             # stream the caller enqueues on -- a side stream of theirs is
-            # as legitimate as the default one)
+            # as legitimate as the default one).  RCCL adds none: synchronous
+            # collectives run on the issuing stream (nccl_stream_probe).
             cur = torch.cuda.current_stream(self.device)
-            n = len([st for st in StreamSet.streams_of(self.device) if st != cur]) + 1
+            n = len([st for st in self._members() if st != cur]) + 1
             if n > MAX_WORK_STREAMS:
                 from ..core.exceptions import SlateError
                 raise SlateError(f"{n} work streams on {self.device} > {MAX_WORK_STREAMS}")

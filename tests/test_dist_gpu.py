@@ -146,26 +146,44 @@ def _check_grid_gpu(rank, size, p, q):
     dev = torch.device("cuda", 0)
     from slate_amd.models.aux import allgather_dense as D
     n, nb = 1024, 128
+    from slate_amd.parallel import comm as comm_mod
+
+    def one_stream_per_comm(fn):
+        """every communicator is driven from ONE stream
+        inside a driver (sync RCCL collectives run on the issuing stream)."""
+        comm_mod.STREAM_LOG["used"].clear()
+        comm_mod.STREAM_LOG["on"] = True
+        try:
+            out = fn()
+        finally:
+            comm_mod.STREAM_LOG["on"] = False
+        bad = {k: v for k, v in comm_mod.STREAM_LOG["used"].items() if len(v) > 1}
+        assert not bad, bad
+        return out
     # potrf
     A = sl.HermitianMatrix(Uplo.Lower, n, nb=nb, p=p, q=q, device=dev)
     A.insertLocalTiles(device=0)
     sl.generate_matrix(A, "poev", 3)
     Af = D(A)
     Af = torch.tril(Af) + torch.tril(Af, -1).mT
-    assert sl.potrf(A, {Option.Lookahead: 1}) == 0
+    assert one_stream_per_comm(lambda: sl.potrf(A, {Option.Lookahead: 1})) == 0
     L = torch.tril(D(A))
     assert ((L @ L.mT - Af).norm() / Af.norm()).item() < 1e-14
-    # getrf: partial pivoting (lookahead 2) and CALU
-    for opts in ({Option.Lookahead: 2}, {Option.MethodLU: MethodLU.CALU}):
+    # getrf: partial pivoting (lookahead 2; rows-on-owners panel, then the
+    # all-gather form) and CALU
+    for opts, gather in (({Option.Lookahead: 2}, "0"), ({Option.Lookahead: 2}, "1"),
+                         ({Option.MethodLU: MethodLU.CALU}, "0")):
         os.environ["SLATE_AMD_CALU_LEAF"] = "256"
+        os.environ["SLATE_AMD_LU_PANEL_GATHER"] = gather
         A = sl.Matrix(n, n, nb=nb, p=p, q=q, device=dev)
         A.insertLocalTiles(device=0)
         sl.generate_matrix(A, "rands", 4)
         A0 = D(A)
         piv = sl.Pivots()
-        assert sl.getrf(A, piv, opts) == 0
+        assert one_stream_per_comm(lambda: sl.getrf(A, piv, opts)) == 0
         r, _ = _lu_residual(A0, D(A), piv, n)
         assert r < 1e-12, (opts, r)
+    os.environ["SLATE_AMD_LU_PANEL_GATHER"] = "0"
     # geqrf
     A = sl.Matrix(2 * n, n // 2, nb=nb, p=p, q=q, device=dev)
     A.insertLocalTiles(device=0)

@@ -128,7 +128,17 @@ def test_stream_census():
     sl.generate_matrix(Q, "rands", seed=3)
     sl.geqrf(Q, sl.TriangularFactors())
     torch.cuda.synchronize()
-    assert StreamSet.census(dev) <= MAX_WORK_STREAMS, StreamSet.census(dev)
+    # every pipeline drives its own set (panel, diag, one update stream per
+    # CU reservation) plus the caller's stream: at most the 4 hardware queues
+    sets = [s for s in StreamSet._cache.values() if s.gpu and not s.serial]
+    assert sets
+    for s in sets:
+        assert len(s._members()) + 1 <= MAX_WORK_STREAMS
+        s.check_census()
+    # getrf (32 reserved CUs) and potrf / geqrf (none) use different update
+    # streams (the first pipeline's mask no longer leaks)
+    ups = {id(s.update[0]) for s in sets}
+    assert len(ups) == len({s.reserve_cus for s in sets})
 
 
 def test_potrf_use_graph():

@@ -3,6 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 D=gpurun_out/${TAG:-lu2}; mkdir -p $D
+NCCL_DEBUG=INFO NCCL_DEBUG_SUBSYS=COLL timeout -k 10 120 python -u tools/probe/nccl_stream_probe.py > $D/nccl_probe.log 2>&1; grep -E "side stream|opCount" $D/nccl_probe.log | tail -8
 
 timeout -k 10 120 python -u tools/probe/lu_panel_time.py > $D/panel_tag.log 2>&1 || { tail $D/panel_tag.log; exit 1; }
 cat $D/panel_tag.log | grep -v amdgpu.ids
