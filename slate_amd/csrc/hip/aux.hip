@@ -217,6 +217,32 @@ laswp_setup_kernel(i64 k1, i64 k2, const i64* __restrict__ ipiv, i64 ioff, int i
     // every swap t' targets pv[t'] >= t', so the swaps targeting row t < ns all
     // come before swap t: the last of them is a max
     if (q < ns && pv[q] != q && pv[q] < ns) atomicMax(&prv[pv[q]], q);
+    // swaps grouped by target row: one bitonic sort of (row, swap) keys in
+    // LDS gives every swap its previous / next swap on the same row in O(1)
+    // (the per-thread O(ns) backward / forward scans of the sequence cost
+    // ~100 us per 512-swap plan on the LU panel critical path)
+    __shared__ unsigned long long key[MAXSW];
+    __shared__ int prev_same[MAXSW];
+    __shared__ unsigned char is_last[MAXSW];
+    key[q] = q < ns ? (((unsigned long long)(unsigned)pv[q] << 16) | (unsigned)q) : ~0ull;
+    __syncthreads();
+    for (int kk2 = 2; kk2 <= MAXSW; kk2 <<= 1)
+        for (int jj = kk2 >> 1; jj > 0; jj >>= 1) {
+            const int ixj = q ^ jj;
+            if (ixj > q) {
+                const bool up = (q & kk2) == 0;
+                const unsigned long long a = key[q], b = key[ixj];
+                if ((a > b) == up) { key[q] = b; key[ixj] = a; }
+            }
+            __syncthreads();
+        }
+    if (q < ns) {
+        const unsigned long long me = key[q];
+        const int x = (int)(me & 0xffff);
+        const unsigned long long row = me >> 16;
+        prev_same[x] = (q > 0 && (key[q - 1] >> 16) == row) ? (int)(key[q - 1] & 0xffff) : -1;
+        is_last[x] = !(q + 1 < ns && (key[q + 1] >> 16) == row);
+    }
     __syncthreads();
     // content of row t just before swap t: what the last earlier swap
     // targeting row t put there, i.e. row prv[t]'s content just before swap
@@ -231,17 +257,13 @@ laswp_setup_kernel(i64 k1, i64 k2, const i64* __restrict__ ipiv, i64 ioff, int i
         if (r == q) {
             src = chain(q);
         } else {
-            int kk = -1;
-            for (int x = q - 1; x >= 0; --x)
-                if (pv[x] == r) { kk = x; break; }
+            const int kk = prev_same[q];               // last earlier swap targeting row r
             src = (kk < 0) ? r : chain(kk);
         }
         dst[q] = k1 + q;
         srcv[q] = k1 + src;
         // rows beyond the sequence: emitted by the last swap that targets them
-        bool emit = r >= ns;
-        for (int x = q + 1; emit && x < ns; ++x)
-            if (pv[x] == r) emit = false;
+        const bool emit = r >= ns && is_last[q];
         // fixed_slots: the emitting swap's own slot ns + q (-1 when it emits
         // nothing), so every rank that folds the same sequence numbers the
         // rows identically (the distributed exchange sums slot-wise);

@@ -155,8 +155,10 @@ def _getrf_p1(A, buf, thr, la, nopiv, T=None, no_inv=False):
     rm = T is not None
     ipiv = torch.zeros(max(min(m, n), 1), dtype=torch.int64, device=dev)   # panel-relative per step
     infos = torch.zeros(max(kt, 1), dtype=torch.int64, device=dev)
-    if rm and nloc and m:
-        ops.gecopy(buf[:m, :nloc], T, trans='T')
+    # RowMajor: buf -> T is not a separate pass in front of the
+    # factorization: step 0's panel copies its columns straight from buf,
+    # the panel stream transposes the lookahead columns and the update
+    # stream the rest, overlapping panel 0
     upd = _update_cols_rm if rm else _update_cols
     M = T if rm else buf
     # 32 CUs: the persistent fp64 panel runs <= 32 workgroups (2 rows per thread)
@@ -179,6 +181,13 @@ def _getrf_p1(A, buf, thr, la, nopiv, T=None, no_inv=False):
     inv_min = int(os.environ.get("SLATE_AMD_LU_INV_MIN", "4096")) if rm and not nopiv and not no_inv else 0
     growth = torch.zeros(max(kt, 1), dtype=_native.REAL_OF[dt], device=dev)
     ss.fork()
+    if rm and kt:
+        # the bulk of buf -> T on the stream of step 0's trailing update,
+        # concurrently with panel 0 (which reads buf itself)
+        lcla0 = min(tiles_local_before(1 + la, q, pc) * nb, nloc)
+        if nloc > lcla0:
+            with ss.use(ss.diag if unmasked > 0 else ss.update[0]):
+                ops.gecopy(buf[:m, lcla0:nloc], T[lcla0:nloc, :m], trans='T')
     for k in range(kt):
         _wd.beat(f"getrf step {k}")
         r0 = k * nb
@@ -202,7 +211,10 @@ def _getrf_p1(A, buf, thr, la, nopiv, T=None, no_inv=False):
                     wk = min(nb, n - r0)
                     if rm:
                         Pk = ops.colmajor_empty(mk, wk, dt, dev)
-                        ops.gecopy(T[lck:lck + wk, r0:m], Pk, trans='T')
+                        if k == 0:
+                            ops.gecopy(buf[r0:m, lck:lck + wk], Pk)
+                        else:
+                            ops.gecopy(T[lck:lck + wk, r0:m], Pk, trans='T')
                         ops.getrf(Pk, piv, infos[k:k + 1], threshold=thr, nopiv=nopiv)
                         ops.gecopy(Pk, T[lck:lck + wk, r0:m], trans='T')
                         Lp = Pk[:, 0:kb]
@@ -228,6 +240,8 @@ def _getrf_p1(A, buf, thr, la, nopiv, T=None, no_inv=False):
             # step k-1's trailing update
             if k >= 1 and la > 0:
                 ss.wait(ss.panel, ev_tr[k - 1])
+            if rm and k == 0 and lcla > lc1:
+                ops.gecopy(buf[:m, lc1:lcla], T[lc1:lcla, :m], trans='T')
             if lcla > lc1:
                 upd(M, Lp, sw, r0, kb, m, lc1, lcla, nopiv, Linv)
             ev_panel = ss.event(ss.panel)
