@@ -1,0 +1,202 @@
+/* ScaLAPACK / LAPACK symbols of libslate_amd_native.so from plain C: no
+ * Python, no MPI.  BLACS grid over the native runtime's ranks (torchrun-style
+ * RANK / WORLD_SIZE env), local block-cyclic arrays, then pdpotrf_ +
+ * pdpotrs_, pdgesv_, pdgetrf_ + pdgetrs_, pzgesv_, pdgemm_, pdlange_ and
+ * the LAPACK-style slate_dgetrf_ / slate_dgetrs_.  Each rank checks its own
+ * part of the solution against the known x and prints
+ * "check r<rank> <name> <value>".
+ *
+ *   ./ex_native_scalapack [PxQ]
+ * (reference: scalapack_api/example_pdgetrf.c exercises the same interface) */
+#include <complex.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+void Cblacs_pinfo(int* mypnum, int* nprocs);
+void Cblacs_get(int ctxt, int what, int* val);
+void Cblacs_gridinit(int* ctxt, const char* order, int nprow, int npcol);
+void Cblacs_gridinfo(int ctxt, int* nprow, int* npcol, int* myrow, int* mycol);
+void Cblacs_gridexit(int ctxt);
+int numroc_(const int* n, const int* nb, const int* iproc, const int* isrcproc, const int* nprocs);
+void descinit_(int* desc, const int* m, const int* n, const int* mb, const int* nb, const int* irsrc,
+               const int* icsrc, const int* ictxt, const int* lld, int* info);
+void pdpotrf_(const char* uplo, const int* n, double* a, const int* ia, const int* ja, const int* desca, int* info);
+void pdpotrs_(const char* uplo, const int* n, const int* nrhs, const double* a, const int* ia, const int* ja,
+              const int* desca, double* b, const int* ib, const int* jb, const int* descb, int* info);
+void pdgesv_(const int* n, const int* nrhs, double* a, const int* ia, const int* ja, const int* desca, int* ipiv,
+             double* b, const int* ib, const int* jb, const int* descb, int* info);
+void pdgetrf_(const int* m, const int* n, double* a, const int* ia, const int* ja, const int* desca, int* ipiv,
+              int* info);
+void pdgetrs_(const char* trans, const int* n, const int* nrhs, const double* a, const int* ia, const int* ja,
+              const int* desca, const int* ipiv, double* b, const int* ib, const int* jb, const int* descb,
+              int* info);
+void pzgesv_(const int* n, const int* nrhs, double complex* a, const int* ia, const int* ja, const int* desca,
+             int* ipiv, double complex* b, const int* ib, const int* jb, const int* descb, int* info);
+void pdgemm_(const char* ta, const char* tb, const int* m, const int* n, const int* k, const double* alpha,
+             const double* a, const int* ia, const int* ja, const int* desca, const double* b, const int* ib,
+             const int* jb, const int* descb, const double* beta, double* c, const int* ic, const int* jc,
+             const int* descc);
+double pdlange_(const char* norm, const int* m, const int* n, const double* a, const int* ia, const int* ja,
+                const int* desca, double* work);
+void slate_dgetrf_(const int64_t* m, const int64_t* n, double* a, const int64_t* lda, int64_t* ipiv, int64_t* info);
+void slate_dgetrs_(const char* trans, const int64_t* n, const int64_t* nrhs, const double* a, const int64_t* lda,
+                   const int64_t* ipiv, double* b, const int64_t* ldb, int64_t* info);
+const char* slate_amd_last_error(void);
+void slate_amd_finalize(void);
+
+static int g_rank;
+static int l2g(int l, int nb, int p, int pr) { return ((l / nb) * p + pr) * nb + l % nb; }
+/* global entries: SPD (sym), general diagonally dominant (gen), solution */
+static double sym(int i, int j, int n) { return i == j ? (double)n : 1.0 / (1.0 + abs(i - j)); }
+static double gen(int i, int j, int n) { return i == j ? (double)n : sin(0.7 * i + 0.3 * j); }
+static double xs(int i, int c) { return cos(0.1 * i + c); }
+
+static void check(const char* what, double v) {
+    printf("check r%d %s %.3e\n", g_rank, what, v);
+    fflush(stdout);
+}
+
+int main(int argc, char** argv) {
+    int p = 1, q = 1;
+    if (argc > 1) sscanf(argv[1], "%dx%d", &p, &q);
+    int me, np, ctxt, nprow, npcol, pr, pc, info, zero = 0, one = 1;
+    Cblacs_pinfo(&me, &np);
+    g_rank = me;
+    if (p * q != np) { fprintf(stderr, "grid %dx%d != %d ranks\n", p, q, np); return 2; }
+    Cblacs_get(-1, 0, &ctxt);
+    Cblacs_gridinit(&ctxt, "Col", p, q);
+    Cblacs_gridinfo(ctxt, &nprow, &npcol, &pr, &pc);
+    const int n = 384, nb = 32, nrhs = 3;
+    const int mloc = numroc_(&n, &nb, &pr, &zero, &p), nloc = numroc_(&n, &nb, &pc, &zero, &q);
+    const int rloc = numroc_(&nrhs, &nb, &pc, &zero, &q);
+    int lld = mloc > 1 ? mloc : 1;
+    int desca[9], descb[9];
+    descinit_(desca, &n, &n, &nb, &nb, &zero, &zero, &ctxt, &lld, &info);
+    descinit_(descb, &n, &nrhs, &nb, &nb, &zero, &zero, &ctxt, &lld, &info);
+    double* a = malloc(sizeof(double) * lld * (nloc > 0 ? nloc : 1));
+    double* b = malloc(sizeof(double) * lld * (rloc > 0 ? rloc : 1));
+    int* ipiv = malloc(sizeof(int) * (mloc + nb));
+
+#define FILL_A(f)                                                                                  \
+    for (int lj = 0; lj < nloc; ++lj)                                                              \
+        for (int li = 0; li < mloc; ++li) a[li + lj * lld] = f(l2g(li, nb, p, pr), l2g(lj, nb, q, pc), n);
+#define FILL_B(f)                                                                                  \
+    for (int lc = 0; lc < rloc; ++lc)                                                              \
+        for (int li = 0; li < mloc; ++li) {                                                        \
+            const int gi = l2g(li, nb, p, pr), c = l2g(lc, nb, q, pc);                             \
+            double s = 0;                                                                          \
+            for (int j = 0; j < n; ++j) s += f(gi, j, n) * xs(j, c);                               \
+            b[li + lc * lld] = s;                                                                  \
+        }
+#define ERR_B()                                                                                    \
+    ({                                                                                             \
+        double e = 0, w = 0;                                                                       \
+        for (int lc = 0; lc < rloc; ++lc)                                                          \
+            for (int li = 0; li < mloc; ++li) {                                                    \
+                const double t = xs(l2g(li, nb, p, pr), l2g(lc, nb, q, pc));                       \
+                e += (b[li + lc * lld] - t) * (b[li + lc * lld] - t);                              \
+                w += t * t;                                                                        \
+            }                                                                                      \
+        w > 0 ? sqrt(e / w) : sqrt(e);                                                             \
+    })
+
+    /* Cholesky + solve */
+    FILL_A(sym);
+    FILL_B(sym);
+    pdpotrf_("L", &n, a, &one, &one, desca, &info);
+    if (info) printf("pdpotrf info %d (%s)\n", info, slate_amd_last_error());
+    pdpotrs_("L", &n, &nrhs, a, &one, &one, desca, b, &one, &one, descb, &info);
+    check(info ? "pdpotrs-FAILED" : "pdpotrs", ERR_B());
+    /* upper storage */
+    FILL_A(sym);
+    FILL_B(sym);
+    pdpotrf_("U", &n, a, &one, &one, desca, &info);
+    pdpotrs_("U", &n, &nrhs, a, &one, &one, desca, b, &one, &one, descb, &info);
+    check(info ? "pdpotrs_upper-FAILED" : "pdpotrs_upper", ERR_B());
+
+    /* LU */
+    FILL_A(gen);
+    FILL_B(gen);
+    pdgesv_(&n, &nrhs, a, &one, &one, desca, ipiv, b, &one, &one, descb, &info);
+    if (info) printf("pdgesv info %d (%s)\n", info, slate_amd_last_error());
+    check(info ? "pdgesv-FAILED" : "pdgesv", ERR_B());
+    FILL_A(gen);
+    FILL_B(gen);
+    pdgetrf_(&n, &n, a, &one, &one, desca, ipiv, &info);
+    pdgetrs_("N", &n, &nrhs, a, &one, &one, desca, ipiv, b, &one, &one, descb, &info);
+    check(info ? "pdgetrs-FAILED" : "pdgetrs", ERR_B());
+
+    /* norm and gemm: C = A^T A (one column block checked) */
+    FILL_A(gen);
+    double nrm = pdlange_("F", &n, &n, a, &one, &one, desca, NULL), want = 0;
+    for (int j = 0; j < n; ++j)
+        for (int i = 0; i < n; ++i) want += gen(i, j, n) * gen(i, j, n);
+    check("pdlange_fro", fabs(nrm - sqrt(want)) / sqrt(want));
+    double* c = calloc((size_t)lld * (nloc > 0 ? nloc : 1), sizeof(double));
+    const double alpha = 1.0, beta = 0.0;
+    pdgemm_("T", "N", &n, &n, &n, &alpha, a, &one, &one, desca, a, &one, &one, desca, &beta, c, &one, &one, desca);
+    double ge = 0, gw = 0;
+    for (int lj = 0; lj < nloc; lj += 3)
+        for (int li = 0; li < mloc; li += 3) {
+            const int gi = l2g(li, nb, p, pr), gj = l2g(lj, nb, q, pc);
+            double s = 0;
+            for (int k = 0; k < n; ++k) s += gen(k, gi, n) * gen(k, gj, n);
+            ge += (c[li + lj * lld] - s) * (c[li + lj * lld] - s);
+            gw += s * s;
+        }
+    check("pdgemm_tn", gw > 0 ? sqrt(ge / gw) : sqrt(ge));
+
+    /* complex LU */
+    double complex* za = malloc(sizeof(double complex) * lld * (nloc > 0 ? nloc : 1));
+    double complex* zb = malloc(sizeof(double complex) * lld * (rloc > 0 ? rloc : 1));
+    for (int lj = 0; lj < nloc; ++lj)
+        for (int li = 0; li < mloc; ++li) {
+            const int gi = l2g(li, nb, p, pr), gj = l2g(lj, nb, q, pc);
+            za[li + lj * lld] = gen(gi, gj, n) + I * 0.5 * gen(gj, gi, n);
+        }
+    for (int lc = 0; lc < rloc; ++lc)
+        for (int li = 0; li < mloc; ++li) {
+            const int gi = l2g(li, nb, p, pr), cc = l2g(lc, nb, q, pc);
+            double complex s = 0;
+            for (int j = 0; j < n; ++j) s += (gen(gi, j, n) + I * 0.5 * gen(j, gi, n)) * (xs(j, cc) + I * xs(j, cc + 7));
+            zb[li + lc * lld] = s;
+        }
+    pzgesv_(&n, &nrhs, za, &one, &one, desca, ipiv, zb, &one, &one, descb, &info);
+    double ze = 0, zw = 0;
+    for (int lc = 0; lc < rloc; ++lc)
+        for (int li = 0; li < mloc; ++li) {
+            const int gi = l2g(li, nb, p, pr), cc = l2g(lc, nb, q, pc);
+            const double complex t = xs(gi, cc) + I * xs(gi, cc + 7);
+            ze += cabs(zb[li + lc * lld] - t) * cabs(zb[li + lc * lld] - t);
+            zw += cabs(t) * cabs(t);
+        }
+    check(info ? "pzgesv-FAILED" : "pzgesv", zw > 0 ? sqrt(ze / zw) : sqrt(ze));
+
+    /* LAPACK-style on the global array (every rank the same) */
+    {
+        const int64_t N = 256, NR = 1, L = 256;
+        double* ga = malloc(sizeof(double) * N * N);
+        double* gb = malloc(sizeof(double) * N);
+        int64_t* gp = malloc(sizeof(int64_t) * N);
+        int64_t inf = 0;
+        for (int j = 0; j < N; ++j)
+            for (int i = 0; i < N; ++i) ga[i + j * N] = gen(i, j, (int)N);
+        for (int i = 0; i < N; ++i) {
+            double s = 0;
+            for (int j = 0; j < N; ++j) s += gen(i, j, (int)N) * xs(j, 0);
+            gb[i] = s;
+        }
+        slate_dgetrf_(&N, &N, ga, &L, gp, &inf);
+        slate_dgetrs_("N", &N, &NR, ga, &L, gp, gb, &L, &inf);
+        double e = 0, w = 0;
+        for (int i = 0; i < N; ++i) { e += (gb[i] - xs(i, 0)) * (gb[i] - xs(i, 0)); w += xs(i, 0) * xs(i, 0); }
+        check(inf ? "slate_dgetrf_-FAILED" : "slate_dgetrf_", sqrt(e / w));
+        free(ga); free(gb); free(gp);
+    }
+    Cblacs_gridexit(ctxt);
+    free(a); free(b); free(c); free(za); free(zb); free(ipiv);
+    slate_amd_finalize();
+    return 0;
+}

@@ -1,14 +1,21 @@
 // Python-free C++ use of slate_amd (include/slate_amd/slate_native.hh,
-// libslate_amd_native.so): Cholesky, LU, GEMM and norms on a 2D block-cyclic
-// grid, checked against host references; then the LAPACK-style C ABI; then
-// an optional timing of potrf (argv[2] = n).  Prints "check <name> <value>"
-// lines (relative residuals) and "time potrf n=.. <ms> <TF/s>".
+// libslate_amd_native.so) in the four precisions on a p x q block-cyclic
+// grid: Cholesky, LU, the solves, GEMM (plain and transposed operands), the
+// triangular solve and norms, each checked against a host reference; then
+// the LAPACK-style C ABI (slate_dgesv / slate_zposv / slate_dgemm_); then an
+// optional timing of dpotrf (argv[2] = n).  Prints "check <name>_<x> <value>"
+// lines (x = s, d, c, z; relative residuals) and "time potrf n=.. <ms> <TF/s>".
 //
-//   ./ex_native [PxQ] [n_bench]          (one process per GPU; torchrun env)
+//   ./ex_native [PxQ] [n_bench]      (one process per rank; torchrun-style env;
+//                                     SLATE_AMD_NATIVE_TRANSPORT=host lets the
+//                                     ranks of a grid share one GPU)
 #include <chrono>
 #include <cmath>
+#include <complex>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
+#include <type_traits>
 #include <vector>
 
 #include "slate_amd/slate_native.hh"
@@ -16,141 +23,291 @@
 namespace sn = slate_amd::native;
 
 extern "C" {
-int slate_native_dpotrf(char uplo, int64_t n, double* a, int64_t lda);
-int slate_native_dgesv(int64_t n, int64_t nrhs, double* a, int64_t lda, int64_t* ipiv, double* b, int64_t ldb);
-const char* slate_native_last_error(void);
+int slate_dgesv(int64_t n, int64_t nrhs, double* a, int64_t lda, int64_t* ipiv, double* b, int64_t ldb);
+int slate_zposv(char uplo, int64_t n, int64_t nrhs, double* a, int64_t lda, double* b, int64_t ldb);
+void slate_dgemm_(const char* ta, const char* tb, const int64_t* m, const int64_t* n, const int64_t* k,
+                  const double* alpha, const double* a, const int64_t* lda, const double* b, const int64_t* ldb,
+                  const double* beta, double* c, const int64_t* ldc);
+const char* slate_amd_last_error(void);
 }
 
-static double fro(const std::vector<double>& v) {
-    double s = 0;
-    for (double x : v) s += x * x;
-    return std::sqrt(s);
+template <typename T> struct Name;
+template <> struct Name<float> { static constexpr const char* s = "s"; };
+template <> struct Name<double> { static constexpr const char* s = "d"; };
+template <> struct Name<std::complex<float>> { static constexpr const char* s = "c"; };
+template <> struct Name<std::complex<double>> { static constexpr const char* s = "z"; };
+
+template <typename T> T cj(T x) { return x; }
+template <typename R> std::complex<R> cj(std::complex<R> x) { return std::conj(x); }
+template <typename T> T val(double re, double im) {
+    if constexpr (std::is_floating_point<T>::value) return T(re);
+    else return T(re, im);
+}
+
+// host C = op(A) op(B) (double-precision accumulation)
+template <typename T>
+std::vector<std::complex<double>> mul(char ta, char tb, int64_t m, int64_t n, int64_t k, const std::vector<T>& a,
+                                      int64_t lda, const std::vector<T>& b, int64_t ldb) {
+    auto at = [&](int64_t i, int64_t l) -> std::complex<double> {
+        const T x = ta == 'N' ? a[i + l * lda] : a[l + i * lda];
+        const std::complex<double> v(std::real(x), std::imag(x));
+        return ta == 'C' ? std::conj(v) : v;
+    };
+    auto bt = [&](int64_t l, int64_t j) -> std::complex<double> {
+        const T x = tb == 'N' ? b[l + j * ldb] : b[j + l * ldb];
+        const std::complex<double> v(std::real(x), std::imag(x));
+        return tb == 'C' ? std::conj(v) : v;
+    };
+    std::vector<std::complex<double>> c((size_t)m * n);
+    for (int64_t j = 0; j < n; ++j)
+        for (int64_t i = 0; i < m; ++i) {
+            std::complex<double> s = 0;
+            for (int64_t l = 0; l < k; ++l) s += at(i, l) * bt(l, j);
+            c[i + j * m] = s;
+        }
+    return c;
+}
+
+template <typename T>
+double rel(const std::vector<std::complex<double>>& got_minus_want, const std::vector<std::complex<double>>& want) {
+    double e = 0, w = 0;
+    for (size_t i = 0; i < want.size(); ++i) {
+        e += std::norm(got_minus_want[i]);
+        w += std::norm(want[i]);
+    }
+    return std::sqrt(e / (w > 0 ? w : 1));
+}
+
+template <typename T>
+std::vector<std::complex<double>> widen(const std::vector<T>& v) {
+    std::vector<std::complex<double>> r(v.size());
+    for (size_t i = 0; i < v.size(); ++i) r[i] = {std::real(v[i]), std::imag(v[i])};
+    return r;
+}
+
+template <typename T>
+void run(int p, int q, int me) {
+    const char* x = Name<T>::s;
+    auto report = [&](const char* what, double v) {
+        if (me == 0) std::printf("check %s_%s %.3e\n", what, x, v);
+        std::fflush(stdout);
+    };
+    const int64_t n = 300, nb = 32, nrhs = 5;
+
+    // ---- potrf / posv: || L L^H - A || / || A ||, || A X - B || / || B ||
+    sn::HermitianMatrix<T> A(sn::Uplo::Lower, n, nb, p, q);
+    A.generate(sn::Gen::HermitianPositiveDefinite, 7);
+    std::vector<T> a0((size_t)n * n), l((size_t)n * n);
+    A.to_host(a0.data(), n);
+    for (int64_t j = 0; j < n; ++j)           // full Hermitian host copy
+        for (int64_t i = 0; i < j; ++i) a0[i + j * n] = cj(a0[j + i * n]);
+    int64_t info = sn::potrf(A);
+    A.to_host(l.data(), n);
+    for (int64_t j = 0; j < n; ++j)
+        for (int64_t i = 0; i < j; ++i) l[i + j * n] = T(0);
+    {
+        auto llh = mul<T>('N', 'C', n, n, n, l, n, l, n);
+        auto want = widen(a0);
+        for (size_t i = 0; i < llh.size(); ++i) llh[i] -= want[i];
+        report(info ? "potrf-FAILED" : "potrf", rel<T>(llh, want));
+    }
+    sn::Matrix<T> B(n, nrhs, nb, p, q);
+    B.generate(sn::Gen::Random, 8);
+    std::vector<T> b0((size_t)n * nrhs), xs((size_t)n * nrhs);
+    B.to_host(b0.data(), n);
+    sn::potrs(A, B);
+    B.to_host(xs.data(), n);
+    {
+        auto ax = mul<T>('N', 'N', n, nrhs, n, a0, n, xs, n);
+        auto want = widen(b0);
+        for (size_t i = 0; i < ax.size(); ++i) ax[i] -= want[i];
+        report("potrs", rel<T>(ax, want));
+    }
+
+    // ---- getrf / getrs / gesv on the p x q grid
+    sn::Matrix<T> G(n, n, nb, p, q);
+    G.generate(sn::Gen::Random, 5);
+    std::vector<T> g0((size_t)n * n);
+    G.to_host(g0.data(), n);
+    std::vector<int64_t> ipiv;
+    sn::Matrix<T> X(n, nrhs, nb, p, q);
+    X.generate(sn::Gen::Random, 6);
+    std::vector<T> xb((size_t)n * nrhs), xg((size_t)n * nrhs);
+    X.to_host(xb.data(), n);
+    info = sn::gesv(G, ipiv, X);
+    X.to_host(xg.data(), n);
+    {
+        auto ax = mul<T>('N', 'N', n, nrhs, n, g0, n, xg, n);
+        auto want = widen(xb);
+        for (size_t i = 0; i < ax.size(); ++i) ax[i] -= want[i];
+        report(info ? "gesv-FAILED" : "gesv", rel<T>(ax, want));
+    }
+    // A^H X = B with the same factors
+    X.from_host(xb.data(), n);
+    sn::getrs(sn::Op::ConjTrans, G, ipiv, X);
+    X.to_host(xg.data(), n);
+    {
+        auto ax = mul<T>('C', 'N', n, nrhs, n, g0, n, xg, n);
+        auto want = widen(xb);
+        for (size_t i = 0; i < ax.size(); ++i) ax[i] -= want[i];
+        report("getrs_conjtrans", rel<T>(ax, want));
+    }
+    // rectangular getrf (m > n): || P A - L U || through the host factors
+    {
+        const int64_t m3 = 260, n3 = 180;
+        sn::Matrix<T> R(m3, n3, nb, p, q);
+        R.generate(sn::Gen::Random, 12);
+        std::vector<T> r0((size_t)m3 * n3), lu((size_t)m3 * n3);
+        R.to_host(r0.data(), m3);
+        std::vector<int64_t> pv;
+        info = sn::getrf(R, pv);
+        R.to_host(lu.data(), m3);
+        std::vector<T> L((size_t)m3 * n3, T(0)), U((size_t)n3 * n3, T(0));
+        for (int64_t j = 0; j < n3; ++j)
+            for (int64_t i = 0; i < m3; ++i) {
+                if (i > j) L[i + j * m3] = lu[i + j * m3];
+                else U[i + j * n3] = lu[i + j * m3];
+                if (i == j) L[i + j * m3] = T(1);
+            }
+        for (int64_t i = 0; i < (int64_t)pv.size(); ++i)
+            for (int64_t j = 0; j < n3; ++j) std::swap(r0[i + j * m3], r0[pv[i] + j * m3]);
+        auto prod = mul<T>('N', 'N', m3, n3, n3, L, m3, U, n3);
+        auto want = widen(r0);
+        for (size_t i = 0; i < prod.size(); ++i) prod[i] -= want[i];
+        report(info ? "getrf_rect-FAILED" : "getrf_rect", rel<T>(prod, want));
+    }
+
+    // ---- gemm: C = alpha op(A) op(B) + beta C
+    const int64_t m2 = 150, k2 = 100, n2 = 120;
+    for (int v = 0; v < 2; ++v) {
+        const char ta = v ? 'C' : 'N', tb = v ? 'T' : 'N';
+        sn::Matrix<T> GA(ta == 'N' ? m2 : k2, ta == 'N' ? k2 : m2, nb, p, q);
+        sn::Matrix<T> GB(tb == 'N' ? k2 : n2, tb == 'N' ? n2 : k2, nb, p, q);
+        sn::Matrix<T> GC(m2, n2, nb, p, q);
+        GA.generate(sn::Gen::Random, 1);
+        GB.generate(sn::Gen::Random, 2);
+        GC.generate(sn::Gen::Random, 3);
+        std::vector<T> ha((size_t)m2 * k2), hb((size_t)k2 * n2), hc((size_t)m2 * n2), hc1((size_t)m2 * n2);
+        GA.to_host(ha.data(), GA.m());
+        GB.to_host(hb.data(), GB.m());
+        GC.to_host(hc.data(), m2);
+        const T alpha = val<T>(2.0, 0.5), beta = val<T>(-1.0, 0.25);
+        if (v) sn::gemm(sn::Op::ConjTrans, sn::Op::Trans, alpha, GA, GB, beta, GC);
+        else sn::gemm(alpha, GA, GB, beta, GC);
+        GC.to_host(hc1.data(), m2);
+        auto want = mul<T>(ta, tb, m2, n2, k2, ha, GA.m(), hb, GB.m());
+        const std::complex<double> al(std::real(alpha), std::imag(alpha)), be(std::real(beta), std::imag(beta));
+        std::vector<std::complex<double>> d(want.size());
+        for (size_t i = 0; i < want.size(); ++i) {
+            want[i] = al * want[i] + be * std::complex<double>(std::real(hc[i]), std::imag(hc[i]));
+            d[i] = std::complex<double>(std::real(hc1[i]), std::imag(hc1[i])) - want[i];
+        }
+        report(v ? "gemm_ct" : "gemm", rel<T>(d, want));
+        if (!v) {
+            // ---- norms against the host
+            double mx = 0, fr = 0, one = 0;
+            for (int64_t j = 0; j < k2; ++j) {
+                double cs = 0;
+                for (int64_t i = 0; i < m2; ++i) {
+                    const double a = std::abs(ha[i + j * m2]);
+                    mx = std::fmax(mx, a);
+                    fr += a * a;
+                    cs += a;
+                }
+                one = std::fmax(one, cs);
+            }
+            report("norm_max", std::fabs(sn::norm(sn::Norm::Max, GA) - mx) / mx);
+            report("norm_fro", std::fabs(sn::norm(sn::Norm::Fro, GA) - std::sqrt(fr)) / std::sqrt(fr));
+            report("norm_one", std::fabs(sn::norm(sn::Norm::One, GA) - one) / one);
+        }
+    }
+
+    // ---- trsm: L^H X = alpha B with the Cholesky factor
+    {
+        sn::Matrix<T> Bt(n, nrhs, nb, p, q);
+        Bt.from_host(b0.data(), n);
+        const T alpha = val<T>(1.5, -0.5);
+        sn::trsm(sn::Side::Left, sn::Uplo::Lower, sn::Op::ConjTrans, sn::Diag::NonUnit, alpha, A, Bt);
+        std::vector<T> xt((size_t)n * nrhs);
+        Bt.to_host(xt.data(), n);
+        auto lx = mul<T>('C', 'N', n, nrhs, n, l, n, xt, n);
+        std::vector<std::complex<double>> want(lx.size());
+        const std::complex<double> al(std::real(alpha), std::imag(alpha));
+        for (size_t i = 0; i < lx.size(); ++i) {
+            want[i] = al * std::complex<double>(std::real(b0[i]), std::imag(b0[i]));
+            lx[i] -= want[i];
+        }
+        report("trsm_lc", rel<T>(lx, want));
+    }
 }
 
 int main(int argc, char** argv) {
     int p = 1, q = 1;
     if (argc > 1) std::sscanf(argv[1], "%dx%d", &p, &q);
     const int64_t nbench = argc > 2 ? std::atoll(argv[2]) : 0;
+    const char* only = std::getenv("EX_NATIVE_TYPES");     // e.g. "dz"
+    const std::string types = only && *only ? only : "sdcz";
     try {
         sn::initialize();
         const int me = sn::rank();
-        auto report = [&](const char* what, double v) {
-            if (me == 0) std::printf("check %s %.3e\n", what, v);
-            std::fflush(stdout);
-        };
-        const int64_t n = 700, nb = 64, nrhs = 3;
+        if (me == 0) std::printf("transport %s ranks %d grid %dx%d\n", sn::transport(), sn::size(), p, q);
+        if (types.find('s') != std::string::npos) run<float>(p, q, me);
+        if (types.find('d') != std::string::npos) run<double>(p, q, me);
+        if (types.find('c') != std::string::npos) run<std::complex<float>>(p, q, me);
+        if (types.find('z') != std::string::npos) run<std::complex<double>>(p, q, me);
 
-        // ---- potrf: || L L^T - A || / || A ||
-        sn::HermitianMatrix<double> A(sn::Uplo::Lower, n, nb, p, q);
-        A.generate(sn::Gen::HermitianPositiveDefinite, 7);
-        std::vector<double> a0((size_t)n * n), l((size_t)n * n);
-        A.to_host(a0.data(), n);
-        int64_t info = sn::potrf(A);
-        A.to_host(l.data(), n);
-        std::vector<double> r((size_t)n * n, 0.0);
-        for (int64_t j = 0; j < n; ++j)
-            for (int64_t i = j; i < n; ++i) {
-                double s = 0;
-                for (int64_t k = 0; k <= j; ++k) s += l[i + k * n] * l[j + k * n];
-                r[i + j * n] = s - a0[i + j * n];
-            }
-        std::vector<double> a0l((size_t)n * n, 0.0);
-        for (int64_t j = 0; j < n; ++j)
-            for (int64_t i = j; i < n; ++i) a0l[i + j * n] = a0[i + j * n];
-        report(info ? "potrf-FAILED" : "potrf", fro(r) / fro(a0l));
-
-        // ---- gemm: C = A B - C0 on the grid vs host
-        const int64_t m2 = 300, k2 = 200, n2 = 250;
-        sn::Matrix<double> GA(m2, k2, nb, p, q), GB(k2, n2, nb, p, q), GC(m2, n2, nb, p, q);
-        GA.generate(sn::Gen::Random, 1);
-        GB.generate(sn::Gen::Random, 2);
-        GC.generate(sn::Gen::Random, 3);
-        std::vector<double> ha((size_t)m2 * k2), hb((size_t)k2 * n2), hc((size_t)m2 * n2), hc1((size_t)m2 * n2);
-        GA.to_host(ha.data(), m2);
-        GB.to_host(hb.data(), k2);
-        GC.to_host(hc.data(), m2);
-        sn::gemm(2.0, GA, GB, -1.0, GC);
-        GC.to_host(hc1.data(), m2);
-        double err = 0, ref = 0;
-        for (int64_t j = 0; j < n2; ++j)
-            for (int64_t i = 0; i < m2; ++i) {
-                double s = 0;
-                for (int64_t k = 0; k < k2; ++k) s += ha[i + k * m2] * hb[k + j * k2];
-                const double want = 2.0 * s - hc[i + j * m2];
-                err += (hc1[i + j * m2] - want) * (hc1[i + j * m2] - want);
-                ref += want * want;
-            }
-        report("gemm", std::sqrt(err / ref));
-
-        // ---- norms against the host
-        double mx = 0, fr = 0;
-        for (double x : ha) { mx = std::fmax(mx, std::fabs(x)); fr += x * x; }
-        report("norm_max", std::fabs(sn::norm(sn::Norm::Max, GA) - mx) / mx);
-        report("norm_fro", std::fabs(sn::norm(sn::Norm::Fro, GA) - std::sqrt(fr)) / std::sqrt(fr));
-
-        // ---- getrf on a 1 x (p q) grid: || P A - L U || via a solve
-        sn::Matrix<double> G(n, n, nb, 1, p * q);
-        G.generate(sn::Gen::Random, 5);
-        std::vector<double> g0((size_t)n * n), lu((size_t)n * n);
-        G.to_host(g0.data(), n);
-        std::vector<int64_t> ipiv;
-        info = sn::getrf(G, ipiv);
-        G.to_host(lu.data(), n);
-        // x = random, b = A x; solve with the factors on the host
-        std::vector<double> x(n), b(n, 0.0), y;
-        for (int64_t i = 0; i < n; ++i) x[i] = std::sin(1.0 + i);
-        for (int64_t j = 0; j < n; ++j)
-            for (int64_t i = 0; i < n; ++i) b[i] += g0[i + j * n] * x[j];
-        y = b;
-        for (int64_t i = 0; i < (int64_t)ipiv.size(); ++i) std::swap(y[i], y[ipiv[i]]);
-        for (int64_t j = 0; j < n; ++j)
-            for (int64_t i = j + 1; i < n; ++i) y[i] -= lu[i + j * n] * y[j];
-        for (int64_t j = n - 1; j >= 0; --j) {
-            y[j] /= lu[j + j * n];
-            for (int64_t i = 0; i < j; ++i) y[i] -= lu[i + j * n] * y[j];
-        }
-        double ex = 0, nx = 0;
-        for (int64_t i = 0; i < n; ++i) { ex += (y[i] - x[i]) * (y[i] - x[i]); nx += x[i] * x[i]; }
-        report(info ? "getrf-FAILED" : "getrf", std::sqrt(ex / nx));
-
-        if (p * q == 1) {
-            // ---- posv / gesv (one rank) and the C ABI
-            sn::HermitianMatrix<double> S(sn::Uplo::Lower, n, nb);
-            S.generate(sn::Gen::HermitianPositiveDefinite, 9);
-            std::vector<double> s0((size_t)n * n);
-            S.to_host(s0.data(), n);
-            sn::Matrix<double> B(n, nrhs, nb);
-            B.generate(sn::Gen::Random, 10);
-            std::vector<double> b0((size_t)n * nrhs), xs((size_t)n * nrhs);
-            B.to_host(b0.data(), n);
-            info = sn::posv(S, B);
-            B.to_host(xs.data(), n);
-            double rr = 0, rb = 0;
+        // ---- LAPACK-style C ABI (every rank passes the same global arrays)
+        {
+            const int64_t n = 200, nrhs = 2;
+            std::vector<double> a((size_t)n * n), x((size_t)n * nrhs), b((size_t)n * nrhs, 0.0);
+            for (int64_t j = 0; j < n; ++j)
+                for (int64_t i = 0; i < n; ++i) a[i + j * n] = std::sin(0.37 * i + 1.3 * j) + (i == j ? 4.0 : 0.0);
+            for (int64_t i = 0; i < n * nrhs; ++i) x[i] = std::cos(0.11 * i);
             for (int64_t c = 0; c < nrhs; ++c)
+                for (int64_t j = 0; j < n; ++j)
+                    for (int64_t i = 0; i < n; ++i) b[i + c * n] += a[i + j * n] * x[j + c * n];
+            std::vector<int64_t> piv(n);
+            const int ci = slate_dgesv(n, nrhs, a.data(), n, piv.data(), b.data(), n);
+            double e = 0, w = 0;
+            for (int64_t i = 0; i < n * nrhs; ++i) { e += (b[i] - x[i]) * (b[i] - x[i]); w += x[i] * x[i]; }
+            if (me == 0) std::printf("check capi_dgesv %.3e\n", ci ? 1.0 : std::sqrt(e / w));
+            if (ci && me == 0) std::printf("capi error: %s\n", slate_amd_last_error());
+
+            // Hermitian positive definite complex system through slate_zposv
+            std::vector<std::complex<double>> z((size_t)n * n), zx((size_t)n), zb((size_t)n, 0.0);
+            for (int64_t j = 0; j < n; ++j)
                 for (int64_t i = 0; i < n; ++i) {
-                    double s = 0;
-                    for (int64_t j = 0; j < n; ++j) {
-                        const double aij = i >= j ? s0[i + j * n] : s0[j + i * n];
-                        s += aij * xs[j + c * n];
-                    }
-                    rr += (s - b0[i + c * n]) * (s - b0[i + c * n]);
-                    rb += b0[i + c * n] * b0[i + c * n];
+                    const std::complex<double> v(std::sin(0.3 * i * j + 1.0), i < j ? 0.2 : i > j ? -0.2 : 0.0);
+                    z[i + j * n] = 0.05 * v;
                 }
-            report(info ? "posv-FAILED" : "posv", std::sqrt(rr / rb));
+            for (int64_t j = 0; j < n; ++j)
+                for (int64_t i = 0; i < j; ++i) z[i + j * n] = std::conj(z[j + i * n]);
+            for (int64_t i = 0; i < n; ++i) z[i + i * n] = {double(n) * 0.5, 0.0};
+            for (int64_t i = 0; i < n; ++i) zx[i] = {std::cos(0.2 * i), std::sin(0.1 * i)};
+            for (int64_t j = 0; j < n; ++j)
+                for (int64_t i = 0; i < n; ++i) zb[i] += z[i + j * n] * zx[j];
+            const int zi = slate_zposv('U', n, 1, reinterpret_cast<double*>(z.data()), n,
+                                       reinterpret_cast<double*>(zb.data()), n);
+            double ze = 0, zw = 0;
+            for (int64_t i = 0; i < n; ++i) { ze += std::norm(zb[i] - zx[i]); zw += std::norm(zx[i]); }
+            if (me == 0) std::printf("check capi_zposv %.3e\n", zi ? 1.0 : std::sqrt(ze / zw));
 
-            std::vector<double> ca = g0, cb = b;
-            std::vector<int64_t> cpiv(n);
-            const int ci = slate_native_dgesv(n, 1, ca.data(), n, cpiv.data(), cb.data(), n);
-            double ce = 0;
-            for (int64_t i = 0; i < n; ++i) ce += (cb[i] - x[i]) * (cb[i] - x[i]);
-            report(ci ? "capi_dgesv-FAILED" : "capi_dgesv", std::sqrt(ce / nx));
-
-            std::vector<double> cs = s0;
-            const int cpi = slate_native_dpotrf('L', n, cs.data(), n);
-            double cd = 0;
-            for (int64_t i = 0; i < n; ++i) cd += (cs[i + i * n] - l[i + i * n]) * (cs[i + i * n] - l[i + i * n]);
-            (void)cd;
-            report(cpi ? "capi_dpotrf-FAILED" : "capi_dpotrf_info", (double)cpi);
+            // Fortran-style gemm: C = A^T A
+            std::vector<double> c((size_t)n * n, 0.0);
+            const int64_t nn = n;
+            const double one = 1.0, zero = 0.0;
+            for (int64_t j = 0; j < n; ++j)
+                for (int64_t i = 0; i < n; ++i) a[i + j * n] = std::sin(0.37 * i + 1.3 * j);
+            slate_dgemm_("T", "N", &nn, &nn, &nn, &one, a.data(), &nn, a.data(), &nn, &zero, c.data(), &nn);
+            double ge = 0, gw = 0;
+            for (int64_t j = 0; j < n; j += 7)
+                for (int64_t i = 0; i < n; i += 5) {
+                    double s = 0;
+                    for (int64_t k = 0; k < n; ++k) s += a[k + i * n] * a[k + j * n];
+                    ge += (c[i + j * n] - s) * (c[i + j * n] - s);
+                    gw += s * s;
+                }
+            if (me == 0) std::printf("check capi_dgemm_tn %.3e\n", std::sqrt(ge / gw));
         }
 
         if (nbench > 0) {
@@ -158,7 +315,7 @@ int main(int argc, char** argv) {
             for (int it = 0; it < 3; ++it) {
                 T.generate(sn::Gen::HermitianPositiveDefinite, 11);
                 const auto t0 = std::chrono::steady_clock::now();
-                info = sn::potrf(T);
+                const int64_t info = sn::potrf(T);
                 const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
                 const double tf = (double)nbench * nbench * nbench / 3.0 / (ms * 1e-3) / 1e12;
                 if (me == 0) std::printf("time potrf n=%lld %.2f ms %.2f TF/s info=%lld\n", (long long)nbench, ms, tf,

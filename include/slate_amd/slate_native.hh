@@ -2,17 +2,23 @@
 // linear algebra routines WITHOUT the Python runtime.
 //
 // libslate_amd_native.so is the gfx950 HIP kernels of the package plus a
-// C++ host runtime (process bootstrap, RCCL communicators, HIP stream/event
+// C++ host runtime (process bootstrap, communicators, HIP stream/event
 // lookahead pipelines) -- it links against libamdhip64 and librccl only.
 // It mirrors the reference's public C++ interface for the routines it
 // covers (include/slate/slate.hh: potrf/potrs/posv, getrf/getrs/gesv, gemm,
-// norm; include/slate/Matrix.hh / HermitianMatrix.hh for the matrix types).
+// trsm, norm; include/slate/Matrix.hh / HermitianMatrix.hh for the matrix
+// types), in the four precisions float, double, std::complex<float>,
+// std::complex<double> (src/potrf.cc:285-303 instantiates the same four).
+// The LAPACK (dgetrf_, ...), ScaLAPACK (pdpotrf_, ...) and BLACS symbols of
+// the library call these drivers directly (capi_native.hip).
 //
 // One process per GPU.  The world is taken from the torchrun-style
-// environment (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR; the RCCL unique id
-// travels over a TCP socket on SLATE_AMD_NATIVE_PORT, default MASTER_PORT +
-// 1 -- torchrun's own store holds MASTER_PORT).  A single process needs no
-// environment at all and never initialises RCCL.
+// environment (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR; bootstrap sockets
+// on SLATE_AMD_NATIVE_PORT, default MASTER_PORT + 1 -- torchrun's own store
+// holds MASTER_PORT).  SLATE_AMD_NATIVE_TRANSPORT = rccl (default: RCCL over
+// xGMI) or host (host-staged TCP: several ranks may share one GPU, e.g. a
+// 2 x 2 grid rehearsed on one device).  A single process needs no
+// environment at all and never initialises a transport.
 //
 //   slate_amd::native::initialize();
 //   slate_amd::native::HermitianMatrix<double> A(slate_amd::native::Uplo::Lower, n, nb, p, q);
@@ -25,6 +31,7 @@
 #ifndef SLATE_AMD_NATIVE_HH
 #define SLATE_AMD_NATIVE_HH
 
+#include <complex>
 #include <cstdint>
 #include <memory>
 #include <stdexcept>
@@ -40,7 +47,9 @@ public:
 };
 
 enum class Uplo : char { Lower = 'L', Upper = 'U' };
-enum class Op : char { NoTrans = 'N', Trans = 'T' };
+enum class Op : char { NoTrans = 'N', Trans = 'T', ConjTrans = 'C' };
+enum class Diag : char { NonUnit = 'N', Unit = 'U' };
+enum class Side : char { Left = 'L', Right = 'R' };
 enum class Norm : char { One = '1', Inf = 'I', Fro = 'F', Max = 'M' };
 // matgen kinds (same Philox counter-based generator as the Python package:
 // an entry depends on (seed, global i, global j) only)
@@ -52,10 +61,12 @@ void finalize();              // destroys communicators and streams
 int rank();
 int size();
 const char* version();
+const char* transport();      // "none" (one rank), "rccl" or "host"
 
 struct Options {
     int lookahead = 1;        // SLATE Option::Lookahead
     double pivot_threshold = 1.0;
+    int inner_blocking = 32;  // columns per base block of the distributed LU panel
 };
 
 struct Storage;               // opaque: device buffer, grid, communicators
@@ -78,9 +89,12 @@ public:
     void generate(Gen kind, uint64_t seed);
     // Global column-major host array, identical on every rank (LAPACK
     // layout): copy this rank's block-cyclic part to the device / gather the
-    // whole matrix back to every rank.
+    // whole matrix to every rank (one all-gather of the local blocks).
     void from_host(const T* A, int64_t lda);
     void to_host(T* A, int64_t lda) const;
+    // This rank's local block in ScaLAPACK layout (host, leading dim lld).
+    void from_local_host(const T* Aloc, int64_t lld);
+    void to_local_host(T* Aloc, int64_t lld) const;
     std::shared_ptr<Storage> storage() const { return s_; }
 
 protected:
@@ -99,20 +113,41 @@ private:
     Uplo uplo_ = Uplo::Lower;
 };
 
-// ---- drivers (fp64).  Return LAPACK info (0 = success).
-int64_t potrf(HermitianMatrix<double>& A, const Options& opts = {});
-int64_t potrs(const HermitianMatrix<double>& A, Matrix<double>& B, const Options& opts = {});
-int64_t posv(HermitianMatrix<double>& A, Matrix<double>& B, const Options& opts = {});
-// LU with partial pivoting on 1 x q grids; ipiv (global, 0-based,
+// ---- drivers, T in {float, double, std::complex<float>, std::complex<double>}.
+// Return LAPACK info (0 = success).
+// Cholesky (Lower storage; Upper: factor the conjugate transpose), p x q
+template <typename T> int64_t potrf(HermitianMatrix<T>& A, const Options& opts = {});
+template <typename T> int64_t potrs(const HermitianMatrix<T>& A, Matrix<T>& B, const Options& opts = {});
+template <typename T> int64_t posv(HermitianMatrix<T>& A, Matrix<T>& B, const Options& opts = {});
+// LU with partial pivoting on p x q grids (p > 1: the panel rows stay on
+// their owners, one record all-gather per column); ipiv (global, 0-based,
 // LAPACK-style sequential interchanges) is returned on every rank
-int64_t getrf(Matrix<double>& A, std::vector<int64_t>& ipiv, const Options& opts = {});
-int64_t getrs(const Matrix<double>& A, const std::vector<int64_t>& ipiv, Matrix<double>& B,
+template <typename T> int64_t getrf(Matrix<T>& A, std::vector<int64_t>& ipiv, const Options& opts = {});
+template <typename T>
+int64_t getrs(const Matrix<T>& A, const std::vector<int64_t>& ipiv, Matrix<T>& B, const Options& opts = {});
+// op(A) X = B with the factors of getrf; trans NoTrans or ConjTrans (real
+// types: Trans == ConjTrans)
+template <typename T>
+int64_t getrs(Op trans, const Matrix<T>& A, const std::vector<int64_t>& ipiv, Matrix<T>& B,
               const Options& opts = {});
-int64_t gesv(Matrix<double>& A, std::vector<int64_t>& ipiv, Matrix<double>& B, const Options& opts = {});
-// C = alpha op(A) op(B) + beta C, SUMMA on the grid (op = NoTrans)
-void gemm(double alpha, const Matrix<double>& A, const Matrix<double>& B, double beta, Matrix<double>& C,
+template <typename T> int64_t gesv(Matrix<T>& A, std::vector<int64_t>& ipiv, Matrix<T>& B, const Options& opts = {});
+// C = alpha A B + beta C, SUMMA on the grid with lookahead broadcasts
+template <typename T>
+void gemm(T alpha, const Matrix<T>& A, const Matrix<T>& B, T beta, Matrix<T>& C, const Options& opts = {});
+// C = alpha op(A) op(B) + beta C (transposed operands are redistributed
+// once, tile by tile, then the SUMMA above runs)
+template <typename T>
+void gemm(Op opA, Op opB, T alpha, const Matrix<T>& A, const Matrix<T>& B, T beta, Matrix<T>& C,
           const Options& opts = {});
-double norm(Norm kind, const Matrix<double>& A);
+// B = op(A) (B: n x m for Trans / ConjTrans), same grid and tile size
+template <typename T> void copy(Op op, const Matrix<T>& A, Matrix<T>& B);
+// B = alpha op(A)^{-1} B, A triangular (the uplo triangle of A's storage),
+// Side::Left, op NoTrans or ConjTrans; distributed forward / backward
+// substitution by tile steps
+template <typename T>
+void trsm(Side side, Uplo uplo, Op op, Diag diag, T alpha, const Matrix<T>& A, Matrix<T>& B,
+          const Options& opts = {});
+template <typename T> double norm(Norm kind, const Matrix<T>& A);
 
 }  // namespace native
 }  // namespace slate_amd

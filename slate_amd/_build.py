@@ -54,9 +54,10 @@ def _jobs():
     return max(1, min(16, os.cpu_count() or 4))
 
 
-def _build_module(name, srcdir, exts, compiler, cflags, ldflags, verbose=False, extra_objs=()):
+def _build_module(name, srcdir, exts, compiler, cflags, ldflags, verbose=False, extra_objs=(), extra_deps=()):
     srcs = sorted(sum((glob.glob(os.path.join(srcdir, "*" + e)) for e in exts), []))
-    headers = glob.glob(os.path.join(srcdir, "*.hpp")) + glob.glob(os.path.join(HERE, "csrc", "include", "*.hpp"))
+    headers = (glob.glob(os.path.join(srcdir, "*.hpp")) + glob.glob(os.path.join(HERE, "csrc", "include", "*.hpp"))
+               + list(extra_deps))
     objdir = os.path.join(BUILD, name)
     os.makedirs(objdir, exist_ok=True)
     ext_suffix = ".so"
@@ -138,8 +139,11 @@ def build(verbose=False, hip=True, host=True):
             ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-x", "hip",
              "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROCM, "include")],
             ["--offload-arch=" + ARCH, "-L" + os.path.join(ROCM, "lib"), "-lamdhip64", "-lrccl",
-             "-Wl,-rpath," + os.path.join(ROCM, "lib")], verbose, extra_objs=kobjs))
+             "-Wl,-rpath," + os.path.join(ROCM, "lib")], verbose, extra_objs=kobjs,
+            extra_deps=glob.glob(os.path.join(ROOT, "include", "slate_amd", "*.hh"))
+            + glob.glob(os.path.join(HERE, "csrc", "hip", "*.hpp"))))
         out.append(_build_native_example(verbose))
+        out.append(_build_native_c_example(verbose))
     return out
 
 
@@ -155,6 +159,22 @@ def _build_native_example(verbose=False):
     if _newer(target, [src, lib, hdr]):
         cmd = ["g++", "-O2", "-std=c++17", "-I" + os.path.join(ROOT, "include"), src, "-o", target,
                "-L" + HERE, "-lslate_amd_native", "-Wl,-rpath,$ORIGIN"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        _run(cmd)
+    return target
+
+
+def _build_native_c_example(verbose=False):
+    """examples/c/ex_native_scalapack.c -> slate_amd/ex_native_scalapack: a
+    plain C program calling the ScaLAPACK / BLACS / LAPACK symbols of
+    libslate_amd_native.so (no Python, no MPI)."""
+    src = os.path.join(ROOT, "examples", "c", "ex_native_scalapack.c")
+    lib = os.path.join(HERE, "libslate_amd_native.so")
+    target = os.path.join(HERE, "ex_native_scalapack")
+    if _newer(target, [src, lib]):
+        cmd = ["gcc", "-O2", "-std=gnu11", src, "-o", target, "-L" + HERE, "-lslate_amd_native", "-lm",
+               "-Wl,-rpath,$ORIGIN"]
         if verbose:
             print(" ".join(cmd), flush=True)
         _run(cmd)

@@ -1,26 +1,46 @@
-// C ABI of the native runtime (no Python): LAPACK-style entry points on
-// global column-major host arrays, for C / Fortran applications
-// (reference: lapack_api/lapack_potrf.cc etc. wrap the C++ drivers the same
-// way).  With several ranks (torchrun environment) every rank passes the
-// same global array; the matrix is distributed 1 x WORLD_SIZE (potrf: the
-// grid of SLATE_AMD_NATIVE_GRID=PxQ if set) and the result gathered back.
-// Return value: LAPACK info, or -1000 on a runtime error (message from
-// slate_native_last_error()).
+// C / Fortran ABI of the native runtime -- no Python anywhere.  The same
+// symbols and signatures as include/slate_amd/c_api.h, so a C, C++ or
+// Fortran application links -lslate_amd_native instead of -lslate_amd_c:
+//
+//   * LAPACK-style host-array routines (reference lapack_api/lapack_*.cc):
+//     slate_{s,d}{gemm,potrf,potrs,posv,getrf,getrs,gesv,trsm} +
+//     Fortran aliases slate_?xxx_ (by reference), complex slate_{c,z}potrf,
+//     slate_{c,z}gesv, slate_zposv (interleaved re/im), slate_dlange.  With
+//     several ranks every rank passes the same global array; the matrix is
+//     distributed over all ranks (1 x WORLD_SIZE, or SLATE_AMD_NATIVE_GRID=PxQ)
+//     and the result is gathered back to every rank.
+//   * ScaLAPACK (reference scalapack_api/scalapack_*.cc):
+//     p{s,d,c,z}{potrf,posv,getrf,gesv}_, p{s,d}{potrs,getrs,gemm,trsm,lange}_
+//     on the caller's LOCAL block-cyclic arrays (9-int descriptors), with a
+//     minimal BLACS (Cblacs_* / blacs_*_, numroc_, descinit_) over the native
+//     runtime's ranks.  The operands must be whole matrices (ia = ja = 1,
+//     sizes equal to the descriptor's, mb = nb, rsrc = csrc = 0,
+//     column-major grid); anything else returns an argument error.
+//   * slate_native_* (the earlier entry points; int return = info).
+//
+// info: 0 = success, > 0 numerical failure, < 0 illegal argument,
+// SLATE_AMD_ERR_INTERNAL (-1000000) on a runtime error (message from
+// slate_amd_last_error()).
+#include <algorithm>
+#include <complex>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
 #include <vector>
 
-#include "slate_amd/slate_native.hh"
+#include "native_rt.hpp"
 
 namespace sn = slate_amd::native;
+using sn::i64;
 
 namespace {
-std::string g_err;
+constexpr int ERR_INTERNAL = -1000000;
+thread_local std::string g_err;
 
 void grid_of(int& p, int& q) {
     const int ws = sn::size();
-    p = 1; q = ws;
+    p = 1;
+    q = ws;
     if (const char* g = std::getenv("SLATE_AMD_NATIVE_GRID")) {
         int a = 0, b = 0;
         if (std::sscanf(g, "%dx%d", &a, &b) == 2 && a * b == ws) { p = a; q = b; }
@@ -33,52 +53,120 @@ int64_t nb_of(int64_t n) {
 }
 
 template <typename F>
-int guarded(F&& f) {
+int64_t guarded(F&& f) {
     try {
-        return (int)f();
+        return (int64_t)f();
     } catch (const std::exception& e) {
         g_err = e.what();
-        return -1000;
+        return ERR_INTERNAL;
     }
 }
-}  // namespace
 
-extern "C" {
+char up(char c) { return (c >= 'a' && c <= 'z') ? (char)(c - 32) : c; }
 
-const char* slate_native_last_error(void) { return g_err.c_str(); }
-int slate_native_initialize(void) { return guarded([] { sn::initialize(); return 0; }); }
-void slate_native_finalize(void) { sn::finalize(); }
+template <typename T> T cj(T x) { return x; }
+template <typename R> std::complex<R> cj(std::complex<R> x) { return std::conj(x); }
 
-int slate_native_dpotrf(char uplo, int64_t n, double* a, int64_t lda) {
+// op(a) (rows x cols of the RESULT) into a new column-major array
+template <typename T>
+std::vector<T> host_op(char op, i64 rows, i64 cols, const T* a, i64 lda) {
+    std::vector<T> r((size_t)rows * cols);
+    for (i64 j = 0; j < cols; ++j)
+        for (i64 i = 0; i < rows; ++i)
+            r[i + j * rows] = op == 'N' ? a[i + j * lda] : op == 'T' ? a[j + i * lda] : cj(a[j + i * lda]);
+    return r;
+}
+
+sn::Op op_of(char c) {
+    c = up(c);
+    return c == 'N' ? sn::Op::NoTrans : c == 'T' ? sn::Op::Trans : sn::Op::ConjTrans;
+}
+
+// ------------------------------------------------------------ host arrays
+template <typename T>
+int64_t h_potrf(char uplo, i64 n, T* a, i64 lda) {
+    uplo = up(uplo);
+    if (uplo != 'L' && uplo != 'U') return -1;
+    if (n < 0) return -2;
+    if (lda < std::max<i64>(1, n)) return -4;
+    if (n == 0) return 0;
     return guarded([&]() -> int64_t {
         int p, q;
         grid_of(p, q);
-        std::vector<double> t;
-        if (uplo == 'U' || uplo == 'u') {          // factor A^T = L L^T, return U = L^T
-            t.resize((size_t)n * n);
-            for (int64_t j = 0; j < n; ++j)
-                for (int64_t i = 0; i < n; ++i) t[i + j * n] = a[j + i * lda];
-        }
-        sn::HermitianMatrix<double> A(sn::Uplo::Lower, n, nb_of(n), p, q);
-        if (t.empty()) A.from_host(a, lda); else A.from_host(t.data(), n);
-        const int64_t info = sn::potrf(A);
-        if (t.empty()) {
-            std::vector<double> r((size_t)n * n);
-            A.to_host(r.data(), n);
-            for (int64_t j = 0; j < n; ++j)
-                for (int64_t i = j; i < n; ++i) a[i + j * lda] = r[i + j * n];
+        sn::HermitianMatrix<T> A(sn::Uplo::Lower, n, nb_of(n), p, q);
+        std::vector<T> t;
+        if (uplo == 'U') {            // factor A^H = L L^H (Lower), return U = L^H
+            t = host_op<T>('C', n, n, a, lda);
+            A.from_host(t.data(), n);
         } else {
-            A.to_host(t.data(), n);
-            for (int64_t j = 0; j < n; ++j)
-                for (int64_t i = j; i < n; ++i) a[j + i * lda] = t[i + j * n];
+            A.from_host(a, lda);
         }
+        const int64_t info = sn::potrf(A);
+        std::vector<T> r((size_t)n * n);
+        A.to_host(r.data(), n);
+        for (i64 j = 0; j < n; ++j)
+            for (i64 i = j; i < n; ++i) {
+                if (uplo == 'L') a[i + j * lda] = r[i + j * n];
+                else a[j + i * lda] = cj(r[i + j * n]);
+            }
         return info;
     });
 }
 
-int slate_native_dgetrf(int64_t m, int64_t n, double* a, int64_t lda, int64_t* ipiv) {
+// Lower factor of a (uplo) Cholesky factor held in a host array
+template <typename T>
+std::vector<T> lower_factor(char uplo, i64 n, const T* a, i64 lda) {
+    std::vector<T> L((size_t)n * n, T(0));
+    for (i64 j = 0; j < n; ++j)
+        for (i64 i = j; i < n; ++i) L[i + j * n] = up(uplo) == 'L' ? a[i + j * lda] : cj(a[j + i * lda]);
+    return L;
+}
+
+template <typename T>
+int64_t h_potrs(char uplo, i64 n, i64 nrhs, const T* a, i64 lda, T* b, i64 ldb) {
+    if (up(uplo) != 'L' && up(uplo) != 'U') return -1;
+    if (n < 0) return -2;
+    if (nrhs < 0) return -3;
+    if (lda < std::max<i64>(1, n)) return -5;
+    if (ldb < std::max<i64>(1, n)) return -7;
+    if (n == 0 || nrhs == 0) return 0;
     return guarded([&]() -> int64_t {
-        sn::Matrix<double> A(m, n, nb_of(std::max(m, n)), 1, sn::size());
+        int p, q;
+        grid_of(p, q);
+        const i64 nb = nb_of(n);
+        sn::HermitianMatrix<T> A(sn::Uplo::Lower, n, nb, p, q);
+        sn::Matrix<T> B(n, nrhs, nb, p, q);
+        const std::vector<T> L = lower_factor(uplo, n, a, lda);
+        A.from_host(L.data(), n);
+        B.from_host(b, ldb);
+        sn::potrs(A, B);
+        B.to_host(b, ldb);
+        return 0;
+    });
+}
+
+template <typename T>
+int64_t h_posv(char uplo, i64 n, i64 nrhs, T* a, i64 lda, T* b, i64 ldb) {
+    if (up(uplo) != 'L' && up(uplo) != 'U') return -1;
+    if (n < 0) return -2;
+    if (nrhs < 0) return -3;
+    if (lda < std::max<i64>(1, n)) return -5;
+    if (ldb < std::max<i64>(1, n)) return -7;
+    const int64_t info = h_potrf<T>(uplo, n, a, lda);
+    if (info != 0) return info;
+    return h_potrs<T>(uplo, n, nrhs, a, lda, b, ldb);
+}
+
+template <typename T>
+int64_t h_getrf(i64 m, i64 n, T* a, i64 lda, int64_t* ipiv) {
+    if (m < 0) return -1;
+    if (n < 0) return -2;
+    if (lda < std::max<i64>(1, m)) return -4;
+    if (m == 0 || n == 0) return 0;
+    return guarded([&]() -> int64_t {
+        int p, q;
+        grid_of(p, q);
+        sn::Matrix<T> A(m, n, nb_of(std::max(m, n)), p, q);
         A.from_host(a, lda);
         std::vector<int64_t> piv;
         const int64_t info = sn::getrf(A, piv);
@@ -88,70 +176,666 @@ int slate_native_dgetrf(int64_t m, int64_t n, double* a, int64_t lda, int64_t* i
     });
 }
 
-int slate_native_dgesv(int64_t n, int64_t nrhs, double* a, int64_t lda, int64_t* ipiv, double* b, int64_t ldb) {
+template <typename T>
+int64_t h_getrs(char trans, i64 n, i64 nrhs, const T* a, i64 lda, const int64_t* ipiv, T* b, i64 ldb) {
+    trans = up(trans);
+    if (trans != 'N' && trans != 'T' && trans != 'C') return -1;
+    if (n < 0) return -2;
+    if (nrhs < 0) return -3;
+    if (lda < std::max<i64>(1, n)) return -5;
+    if (ldb < std::max<i64>(1, n)) return -8;
+    if (n == 0 || nrhs == 0) return 0;
     return guarded([&]() -> int64_t {
-        if (sn::size() != 1) throw sn::Error("slate_native_dgesv: one rank");
-        const int64_t nb = nb_of(n);
-        sn::Matrix<double> A(n, n, nb), B(n, nrhs, nb);
+        int p, q;
+        grid_of(p, q);
+        const i64 nb = nb_of(n);
+        sn::Matrix<T> A(n, n, nb, p, q), B(n, nrhs, nb, p, q);
         A.from_host(a, lda);
         B.from_host(b, ldb);
-        std::vector<int64_t> piv;
-        const int64_t info = sn::gesv(A, piv, B);
-        A.to_host(a, lda);
+        std::vector<int64_t> piv((size_t)n);
+        for (i64 i = 0; i < n; ++i) piv[i] = ipiv[i] - 1;
+        sn::Op op = op_of(trans);
+        if (op == sn::Op::Trans && sn::is_cplx<T>()) {
+            // A^T x = b  <=>  A^H conj(x) = conj(b)
+            std::vector<T> cb = host_op<T>('N', n, nrhs, b, ldb);
+            for (auto& x : cb) x = cj(x);
+            B.from_host(cb.data(), n);
+            sn::getrs(sn::Op::ConjTrans, A, piv, B);
+            B.to_host(cb.data(), n);
+            for (i64 j = 0; j < nrhs; ++j)
+                for (i64 i = 0; i < n; ++i) b[i + j * ldb] = cj(cb[i + j * n]);
+            return 0;
+        }
+        sn::getrs(op == sn::Op::Trans ? sn::Op::ConjTrans : op, A, piv, B);
         B.to_host(b, ldb);
+        return 0;
+    });
+}
+
+template <typename T>
+int64_t h_gesv(i64 n, i64 nrhs, T* a, i64 lda, int64_t* ipiv, T* b, i64 ldb) {
+    if (n < 0) return -1;
+    if (nrhs < 0) return -2;
+    if (lda < std::max<i64>(1, n)) return -4;
+    if (ldb < std::max<i64>(1, n)) return -7;
+    if (n == 0) return 0;
+    return guarded([&]() -> int64_t {
+        int p, q;
+        grid_of(p, q);
+        const i64 nb = nb_of(n);
+        sn::Matrix<T> A(n, n, nb, p, q), B(n, std::max<i64>(nrhs, 1), nb, p, q);
+        A.from_host(a, lda);
+        if (nrhs) B.from_host(b, ldb);
+        std::vector<int64_t> piv;
+        const int64_t info = nrhs ? sn::gesv(A, piv, B) : sn::getrf(A, piv);
+        A.to_host(a, lda);
+        if (nrhs) B.to_host(b, ldb);
         for (size_t i = 0; i < piv.size(); ++i) ipiv[i] = piv[i] + 1;
         return info;
     });
 }
 
-int slate_native_dposv(char uplo, int64_t n, int64_t nrhs, double* a, int64_t lda, double* b, int64_t ldb) {
-    return guarded([&]() -> int64_t {
-        if (sn::size() != 1) throw sn::Error("slate_native_dposv: one rank");
-        if (uplo != 'L' && uplo != 'l') throw sn::Error("slate_native_dposv: uplo = 'L'");
-        const int64_t nb = nb_of(n);
-        sn::HermitianMatrix<double> A(sn::Uplo::Lower, n, nb);
-        sn::Matrix<double> B(n, nrhs, nb);
-        A.from_host(a, lda);
-        B.from_host(b, ldb);
-        const int64_t info = sn::posv(A, B);
-        B.to_host(b, ldb);
-        std::vector<double> r((size_t)n * n);
-        A.to_host(r.data(), n);
-        for (int64_t j = 0; j < n; ++j)
-            for (int64_t i = j; i < n; ++i) a[i + j * lda] = r[i + j * n];
-        return info;
-    });
-}
-
-int slate_native_dgemm(int64_t m, int64_t n, int64_t k, double alpha, const double* a, int64_t lda, const double* b,
-                       int64_t ldb, double beta, double* c, int64_t ldc) {
+template <typename T>
+int64_t h_gemm(char ta, char tb, i64 m, i64 n, i64 k, T alpha, const T* a, i64 lda, const T* b, i64 ldb, T beta,
+               T* c, i64 ldc) {
+    ta = up(ta);
+    tb = up(tb);
+    if (ta != 'N' && ta != 'T' && ta != 'C') return -1;
+    if (tb != 'N' && tb != 'T' && tb != 'C') return -2;
+    if (m < 0) return -3;
+    if (n < 0) return -4;
+    if (k < 0) return -5;
+    if (lda < std::max<i64>(1, ta == 'N' ? m : k)) return -8;
+    if (ldb < std::max<i64>(1, tb == 'N' ? k : n)) return -10;
+    if (ldc < std::max<i64>(1, m)) return -13;
+    if (m == 0 || n == 0) return 0;
     return guarded([&]() -> int64_t {
         int p, q;
         grid_of(p, q);
-        const int64_t nb = nb_of(std::max({m, n, k}));
-        sn::Matrix<double> A(m, k, nb, p, q), B(k, n, nb, p, q), C(m, n, nb, p, q);
-        A.from_host(a, lda);
-        B.from_host(b, ldb);
+        const i64 nb = nb_of(std::max({m, n, k}));
+        // op() applied on the host copy (the operands are host arrays anyway)
+        const std::vector<T> ao = host_op<T>(ta, m, k, a, lda);
+        const std::vector<T> bo = host_op<T>(tb, k, n, b, ldb);
+        sn::Matrix<T> A(m, std::max<i64>(k, 1), nb, p, q), B(std::max<i64>(k, 1), n, nb, p, q), C(m, n, nb, p, q);
+        if (k) {
+            A.from_host(ao.data(), m);
+            B.from_host(bo.data(), k);
+        }
         C.from_host(c, ldc);
-        sn::gemm(alpha, A, B, beta, C);
+        sn::gemm(k ? alpha : T(0), A, B, beta, C);
         C.to_host(c, ldc);
         return 0;
     });
 }
 
-double slate_native_dlange(char norm, int64_t m, int64_t n, const double* a, int64_t lda) {
-    double r = -1.0;
-    const int rc = guarded([&]() -> int64_t {
+// B = alpha op(A)^{-1} B (Left) or alpha B op(A)^{-1} (Right)
+template <typename T>
+int64_t h_trsm(char side, char uplo, char ta, char diag, i64 m, i64 n, T alpha, const T* a, i64 lda, T* b,
+               i64 ldb) {
+    side = up(side);
+    uplo = up(uplo);
+    ta = up(ta);
+    diag = up(diag);
+    if (side != 'L' && side != 'R') return -1;
+    if (uplo != 'L' && uplo != 'U') return -2;
+    if (ta != 'N' && ta != 'T' && ta != 'C') return -3;
+    if (diag != 'N' && diag != 'U') return -4;
+    if (m < 0) return -5;
+    if (n < 0) return -6;
+    const i64 na = side == 'L' ? m : n;
+    if (lda < std::max<i64>(1, na)) return -9;
+    if (ldb < std::max<i64>(1, m)) return -11;
+    if (m == 0 || n == 0) return 0;
+    return guarded([&]() -> int64_t {
         int p, q;
         grid_of(p, q);
-        sn::Matrix<double> A(m, n, nb_of(std::max(m, n)), p, q);
+        const i64 nb = nb_of(std::max(m, n));
+        // Right: X op(A) = alpha B  <=>  op(A)^H X^H = conj(alpha) B^H
+        // complex Left Trans: op(A) = A^T = conj(A^H): solve on conj(A)
+        std::vector<T> Ah((size_t)na * na);
+        for (i64 j = 0; j < na; ++j)
+            for (i64 i = 0; i < na; ++i) Ah[i + j * na] = a[i + j * lda];
+        char opc = ta;
+        const bool right = side == 'R';
+        if (right) opc = ta == 'N' ? 'C' : ta == 'C' ? 'N' : 'X';     // X: conj(A) NoTrans
+        else if (ta == 'T' && sn::is_cplx<T>()) opc = 'Y';             // Y: conj(A) ConjTrans
+        else if (ta == 'T') opc = 'C';
+        if (opc == 'X' || opc == 'Y') {
+            for (auto& x : Ah) x = cj(x);
+            opc = opc == 'X' ? 'N' : 'C';
+        }
+        if (right && ta == 'T' && !sn::is_cplx<T>()) opc = 'N';
+        sn::Matrix<T> A(na, na, nb, p, q);
+        A.from_host(Ah.data(), na);
+        const i64 bm = right ? n : m, bn = right ? m : n;
+        std::vector<T> Bh = right ? host_op<T>('C', bm, bn, b, ldb) : host_op<T>('N', bm, bn, b, ldb);
+        sn::Matrix<T> B(bm, bn, nb, p, q);
+        B.from_host(Bh.data(), bm);
+        sn::trsm(sn::Side::Left, uplo == 'L' ? sn::Uplo::Lower : sn::Uplo::Upper,
+                 opc == 'N' ? sn::Op::NoTrans : sn::Op::ConjTrans, diag == 'U' ? sn::Diag::Unit : sn::Diag::NonUnit,
+                 right ? cj(alpha) : alpha, A, B);
+        B.to_host(Bh.data(), bm);
+        for (i64 j = 0; j < n; ++j)
+            for (i64 i = 0; i < m; ++i) b[i + j * ldb] = right ? cj(Bh[j + i * bm]) : Bh[i + j * bm];
+        return 0;
+    });
+}
+
+template <typename T>
+double h_lange(char norm, i64 m, i64 n, const T* a, i64 lda) {
+    if (m == 0 || n == 0) return 0.0;
+    double r = -1.0;
+    const int64_t rc = guarded([&]() -> int64_t {
+        int p, q;
+        grid_of(p, q);
+        sn::Matrix<T> A(m, n, nb_of(std::max(m, n)), p, q);
         A.from_host(a, lda);
-        const char k = (norm == 'm' || norm == 'M') ? 'M' : (norm == 'i' || norm == 'I') ? 'I'
-                     : (norm == 'f' || norm == 'F' || norm == 'e' || norm == 'E') ? 'F' : '1';
+        const char k = up(norm) == 'M' ? 'M' : up(norm) == 'I' ? 'I' : (up(norm) == 'F' || up(norm) == 'E') ? 'F' : '1';
         r = sn::norm((sn::Norm)k, A);
         return 0;
     });
     return rc == 0 ? r : -1.0;
+}
+
+// ------------------------------------------------------------ BLACS / ScaLAPACK
+struct Ctx {
+    int p = 1, q = 1;
+    bool row_major = false;
+};
+std::vector<Ctx>& contexts() {
+    static std::vector<Ctx> c;
+    return c;
+}
+
+const Ctx& ctx_of(int ctxt) {
+    auto& c = contexts();
+    if (ctxt < 0 || ctxt >= (int)c.size()) throw sn::Error("BLACS: unknown context " + std::to_string(ctxt));
+    return c[ctxt];
+}
+
+// device-to-device local copy on the runtime's main stream, completed on
+// return (a null-stream D2D hipMemcpy is not ordered against the drivers'
+// non-blocking streams)
+template <typename T>
+void dev_copy(T* dst, i64 ldd, const T* src, i64 lds, i64 m, i64 n) {
+    if (m > 0 && n > 0)
+        NHIP(hipMemcpy2DAsync(dst, ldd * sizeof(T), src, lds * sizeof(T), m * sizeof(T), n, hipMemcpyDeviceToDevice,
+                              sn::rt().main));
+    NHIP(hipStreamSynchronize(sn::rt().main));
+}
+
+// a native matrix over a ScaLAPACK operand: whole matrix only
+template <typename T>
+sn::Matrix<T> scal_matrix(const int* desc, i64 m, i64 n, int ia, int ja, const T* a) {
+    if (ia != 1 || ja != 1) throw sn::Error("native ScaLAPACK: sub-matrix offsets (ia, ja != 1) not supported");
+    if (desc[2] != m || desc[3] != n) throw sn::Error("native ScaLAPACK: operand must be the whole matrix");
+    if (desc[4] != desc[5]) throw sn::Error("native ScaLAPACK: mb must equal nb");
+    if (desc[6] != 0 || desc[7] != 0) throw sn::Error("native ScaLAPACK: rsrc = csrc = 0 only");
+    const Ctx& c = ctx_of(desc[1]);
+    if (c.row_major && c.p > 1 && c.q > 1) throw sn::Error("native ScaLAPACK: row-major grids not supported");
+    sn::Matrix<T> A(m, n, desc[5], c.p, c.q);
+    if (A.mloc() > desc[8]) throw sn::Error("native ScaLAPACK: lld smaller than the local rows");
+    if (A.mloc() && A.nloc()) A.from_local_host(a, desc[8]);
+    return A;
+}
+template <typename T>
+void scal_back(const sn::Matrix<T>& A, const int* desc, T* a) {
+    if (A.mloc() && A.nloc()) A.to_local_host(a, desc[8]);
+}
+template <typename T>
+sn::HermitianMatrix<T> scal_herm(const int* desc, i64 n, int ia, int ja, const T* a) {
+    sn::Matrix<T> G = scal_matrix<T>(desc, n, n, ia, ja, a);
+    sn::HermitianMatrix<T> H(sn::Uplo::Lower, n, G.nb(), G.p(), G.q());
+    if (H.mloc() && H.nloc())
+        dev_copy(H.data(), H.lld(), G.data(), G.lld(), H.mloc(), H.nloc());
+    return H;
+}
+
+// ScaLAPACK ipiv: local rows' global pivot rows (1-based), replicated over
+// the process columns; <-> the global 0-based sequence of the native driver
+template <typename T>
+void ipiv_to_local(const sn::Matrix<T>& A, const std::vector<int64_t>& piv, int* ipiv) {
+    const int p = A.p(), pr = sn::rank() % p;
+    for (i64 li = 0; li < A.mloc(); ++li) {
+        const i64 g = sn::l2g(li, A.nb(), p, pr);
+        if (g < (i64)piv.size()) ipiv[li] = (int)(piv[g] + 1);
+    }
+}
+template <typename T>
+std::vector<int64_t> ipiv_from_local(const sn::Matrix<T>& A, i64 k, const int* ipiv) {
+    const int p = A.p(), pr = sn::rank() % p;
+    std::vector<int64_t> g((size_t)std::max<i64>(k, 1), 0);
+    for (i64 li = 0; li < A.mloc(); ++li) {
+        const i64 gi = sn::l2g(li, A.nb(), p, pr);
+        if (gi < k) g[gi] = ipiv[li] - 1;
+    }
+    if (p > 1) {       // each global row lives on exactly one process row
+        sn::GridComms* gc = sn::grid_comms(A.p(), A.q());
+        sn::Scratch d(sizeof(int64_t) * g.size(), sn::rt().main);
+        NHIP(hipMemcpyAsync(d.p, g.data(), sizeof(int64_t) * g.size(), hipMemcpyHostToDevice, sn::rt().main));
+        gc->col->allreduce(d.p, g.size(), sn::DT::I64, 's', sn::rt().main);
+        NHIP(hipMemcpyAsync(g.data(), d.p, sizeof(int64_t) * g.size(), hipMemcpyDeviceToHost, sn::rt().main));
+        NHIP(hipStreamSynchronize(sn::rt().main));
+    }
+    g.resize((size_t)k);
+    return g;
+}
+
+template <typename T>
+int p_potrf(char uplo, int n, T* a, int ia, int ja, const int* desca) {
+    uplo = up(uplo);
+    if (uplo != 'L' && uplo != 'U') return -1;
+    if (n == 0) return 0;
+    return (int)guarded([&]() -> int64_t {
+        sn::HermitianMatrix<T> A = scal_herm<T>(desca, n, ia, ja, a);
+        if (uplo == 'U') {
+            sn::Matrix<T> U = scal_matrix<T>(desca, n, n, ia, ja, a);
+            sn::Matrix<T> Lg(n, n, A.nb(), A.p(), A.q());
+            sn::copy(sn::Op::ConjTrans, U, Lg);
+            dev_copy(A.data(), A.lld(), Lg.data(), Lg.lld(), A.mloc(), A.nloc());
+            const int64_t info = sn::potrf(A);
+            sn::copy(sn::Op::ConjTrans, A, U);
+            // only the upper triangle of the caller's array changes
+            std::vector<T> loc((size_t)desca[8] * std::max<i64>(U.nloc(), 1));
+            scal_back(U, desca, loc.data());
+            for (i64 lj = 0; lj < U.nloc(); ++lj)
+                for (i64 li = 0; li < U.mloc(); ++li) {
+                    const i64 gi = sn::l2g(li, U.nb(), U.p(), sn::rank() % U.p());
+                    const i64 gj = sn::l2g(lj, U.nb(), U.q(), sn::rank() / U.p());
+                    if (gi <= gj) a[li + lj * desca[8]] = loc[li + lj * desca[8]];
+                }
+            return info;
+        }
+        const int64_t info = sn::potrf(A);
+        std::vector<T> loc((size_t)desca[8] * std::max<i64>(A.nloc(), 1));
+        scal_back<T>(A, desca, loc.data());
+        for (i64 lj = 0; lj < A.nloc(); ++lj)
+            for (i64 li = 0; li < A.mloc(); ++li) {
+                const i64 gi = sn::l2g(li, A.nb(), A.p(), sn::rank() % A.p());
+                const i64 gj = sn::l2g(lj, A.nb(), A.q(), sn::rank() / A.p());
+                if (gi >= gj) a[li + lj * desca[8]] = loc[li + lj * desca[8]];
+            }
+        return info;
+    });
+}
+
+template <typename T>
+int p_potrs(char uplo, int n, int nrhs, const T* a, int ia, int ja, const int* desca, T* b, int ib, int jb,
+            const int* descb) {
+    uplo = up(uplo);
+    if (uplo != 'L' && uplo != 'U') return -1;
+    if (n == 0 || nrhs == 0) return 0;
+    return (int)guarded([&]() -> int64_t {
+        sn::HermitianMatrix<T> A = scal_herm<T>(desca, n, ia, ja, a);
+        if (uplo == 'U') {
+            sn::Matrix<T> U = scal_matrix<T>(desca, n, n, ia, ja, a);
+            sn::Matrix<T> Lg(n, n, A.nb(), A.p(), A.q());
+            sn::copy(sn::Op::ConjTrans, U, Lg);
+            dev_copy(A.data(), A.lld(), Lg.data(), Lg.lld(), A.mloc(), A.nloc());
+        }
+        sn::Matrix<T> B = scal_matrix<T>(descb, n, nrhs, ib, jb, b);
+        sn::potrs(A, B);
+        scal_back(B, descb, b);
+        return 0;
+    });
+}
+
+template <typename T>
+int p_posv(char uplo, int n, int nrhs, T* a, int ia, int ja, const int* desca, T* b, int ib, int jb,
+           const int* descb) {
+    const int info = p_potrf<T>(uplo, n, a, ia, ja, desca);
+    if (info != 0) return info;
+    return p_potrs<T>(uplo, n, nrhs, a, ia, ja, desca, b, ib, jb, descb);
+}
+
+template <typename T>
+int p_getrf(int m, int n, T* a, int ia, int ja, const int* desca, int* ipiv) {
+    if (m == 0 || n == 0) return 0;
+    return (int)guarded([&]() -> int64_t {
+        sn::Matrix<T> A = scal_matrix<T>(desca, m, n, ia, ja, a);
+        std::vector<int64_t> piv;
+        const int64_t info = sn::getrf(A, piv);
+        scal_back(A, desca, a);
+        ipiv_to_local(A, piv, ipiv);
+        return info;
+    });
+}
+
+template <typename T>
+int p_getrs(char trans, int n, int nrhs, const T* a, int ia, int ja, const int* desca, const int* ipiv, T* b,
+            int ib, int jb, const int* descb) {
+    trans = up(trans);
+    if (trans != 'N' && trans != 'T' && trans != 'C') return -1;
+    if (n == 0 || nrhs == 0) return 0;
+    return (int)guarded([&]() -> int64_t {
+        sn::Matrix<T> A = scal_matrix<T>(desca, n, n, ia, ja, a);
+        sn::Matrix<T> B = scal_matrix<T>(descb, n, nrhs, ib, jb, b);
+        const std::vector<int64_t> piv = ipiv_from_local(A, n, ipiv);
+        if (trans == 'T' && sn::is_cplx<T>()) throw sn::Error("native pgetrs: trans = 'T' of a complex matrix");
+        sn::getrs(trans == 'N' ? sn::Op::NoTrans : sn::Op::ConjTrans, A, piv, B);
+        scal_back(B, descb, b);
+        return 0;
+    });
+}
+
+template <typename T>
+int p_gesv(int n, int nrhs, T* a, int ia, int ja, const int* desca, int* ipiv, T* b, int ib, int jb,
+           const int* descb) {
+    if (n == 0) return 0;
+    return (int)guarded([&]() -> int64_t {
+        sn::Matrix<T> A = scal_matrix<T>(desca, n, n, ia, ja, a);
+        std::vector<int64_t> piv;
+        int64_t info;
+        if (nrhs) {
+            sn::Matrix<T> B = scal_matrix<T>(descb, n, nrhs, ib, jb, b);
+            info = sn::gesv(A, piv, B);
+            scal_back(B, descb, b);
+        } else {
+            info = sn::getrf(A, piv);
+        }
+        scal_back(A, desca, a);
+        ipiv_to_local(A, piv, ipiv);
+        return info;
+    });
+}
+
+template <typename T>
+void p_gemm(char ta, char tb, int m, int n, int k, T alpha, const T* a, int ia, int ja, const int* desca, const T* b,
+            int ib, int jb, const int* descb, T beta, T* c, int ic, int jc, const int* descc) {
+    ta = up(ta);
+    tb = up(tb);
+    if (m == 0 || n == 0) return;
+    const int64_t rc = guarded([&]() -> int64_t {
+        sn::Matrix<T> A = scal_matrix<T>(desca, ta == 'N' ? m : k, ta == 'N' ? k : m, ia, ja, a);
+        sn::Matrix<T> B = scal_matrix<T>(descb, tb == 'N' ? k : n, tb == 'N' ? n : k, ib, jb, b);
+        sn::Matrix<T> C = scal_matrix<T>(descc, m, n, ic, jc, c);
+        sn::gemm(op_of(ta), op_of(tb), alpha, A, B, beta, C);
+        scal_back(C, descc, c);
+        return 0;
+    });
+    if (rc != 0) std::fprintf(stderr, "slate_amd native p?gemm_: %s\n", g_err.c_str());
+}
+
+template <typename T>
+void p_trsm(char side, char uplo, char ta, char diag, int m, int n, T alpha, const T* a, int ia, int ja,
+            const int* desca, T* b, int ib, int jb, const int* descb) {
+    side = up(side);
+    uplo = up(uplo);
+    ta = up(ta);
+    if (m == 0 || n == 0) return;
+    const int64_t rc = guarded([&]() -> int64_t {
+        if (side != 'L') throw sn::Error("native p?trsm_: side = 'L' only");
+        sn::Matrix<T> A = scal_matrix<T>(desca, m, m, ia, ja, a);
+        sn::Matrix<T> B = scal_matrix<T>(descb, m, n, ib, jb, b);
+        sn::trsm(sn::Side::Left, uplo == 'L' ? sn::Uplo::Lower : sn::Uplo::Upper,
+                 ta == 'N' ? sn::Op::NoTrans : sn::Op::ConjTrans, up(diag) == 'U' ? sn::Diag::Unit : sn::Diag::NonUnit,
+                 alpha, A, B);
+        scal_back(B, descb, b);
+        return 0;
+    });
+    if (rc != 0) std::fprintf(stderr, "slate_amd native p?trsm_: %s\n", g_err.c_str());
+}
+
+template <typename T>
+double p_lange(char norm, int m, int n, const T* a, int ia, int ja, const int* desca) {
+    if (m == 0 || n == 0) return 0.0;
+    double r = -1.0;
+    const int64_t rc = guarded([&]() -> int64_t {
+        sn::Matrix<T> A = scal_matrix<T>(desca, m, n, ia, ja, a);
+        const char k = up(norm) == 'M' ? 'M' : up(norm) == 'I' ? 'I' : (up(norm) == 'F' || up(norm) == 'E') ? 'F' : '1';
+        r = sn::norm((sn::Norm)k, A);
+        return 0;
+    });
+    if (rc != 0) std::fprintf(stderr, "slate_amd native p?lange_: %s\n", g_err.c_str());
+    return r;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* slate_amd_last_error(void) { return g_err.c_str(); }
+int slate_amd_initialize(void) { return (int)guarded([] { sn::initialize(); return 0; }); }
+void slate_amd_finalize(void) { sn::finalize(); }
+
+// ---- LAPACK-style, by value
+#define SN_LAPACK(X, T)                                                                                         \
+    int slate_##X##potrf(char uplo, int64_t n, T* a, int64_t lda) { return (int)h_potrf<T>(uplo, n, a, lda); }  \
+    int slate_##X##potrs(char uplo, int64_t n, int64_t nrhs, const T* a, int64_t lda, T* b, int64_t ldb) {      \
+        return (int)h_potrs<T>(uplo, n, nrhs, a, lda, b, ldb);                                                 \
+    }                                                                                                          \
+    int slate_##X##posv(char uplo, int64_t n, int64_t nrhs, T* a, int64_t lda, T* b, int64_t ldb) {            \
+        return (int)h_posv<T>(uplo, n, nrhs, a, lda, b, ldb);                                                  \
+    }                                                                                                          \
+    int slate_##X##getrf(int64_t m, int64_t n, T* a, int64_t lda, int64_t* ipiv) {                             \
+        return (int)h_getrf<T>(m, n, a, lda, ipiv);                                                            \
+    }                                                                                                          \
+    int slate_##X##getrs(char trans, int64_t n, int64_t nrhs, const T* a, int64_t lda, const int64_t* ipiv,    \
+                         T* b, int64_t ldb) {                                                                  \
+        return (int)h_getrs<T>(trans, n, nrhs, a, lda, ipiv, b, ldb);                                          \
+    }                                                                                                          \
+    int slate_##X##gesv(int64_t n, int64_t nrhs, T* a, int64_t lda, int64_t* ipiv, T* b, int64_t ldb) {       \
+        return (int)h_gesv<T>(n, nrhs, a, lda, ipiv, b, ldb);                                                  \
+    }                                                                                                          \
+    int slate_##X##gemm(char ta, char tb, int64_t m, int64_t n, int64_t k, T alpha, const T* a, int64_t lda,   \
+                        const T* b, int64_t ldb, T beta, T* c, int64_t ldc) {                                  \
+        return (int)h_gemm<T>(ta, tb, m, n, k, alpha, a, lda, b, ldb, beta, c, ldc);                           \
+    }                                                                                                          \
+    int slate_##X##trsm(char side, char uplo, char ta, char diag, int64_t m, int64_t n, T alpha, const T* a,   \
+                        int64_t lda, T* b, int64_t ldb) {                                                      \
+        return (int)h_trsm<T>(side, uplo, ta, diag, m, n, alpha, a, lda, b, ldb);                              \
+    }                                                                                                          \
+    double slate_##X##lange(char norm, int64_t m, int64_t n, const T* a, int64_t lda) {                        \
+        return h_lange<T>(norm, m, n, a, lda);                                                                 \
+    }                                                                                                          \
+    void slate_##X##potrf_(const char* uplo, const int64_t* n, T* a, const int64_t* lda, int64_t* info) {      \
+        *info = h_potrf<T>(*uplo, *n, a, *lda);                                                                \
+    }                                                                                                          \
+    void slate_##X##potrs_(const char* uplo, const int64_t* n, const int64_t* nrhs, const T* a,                \
+                           const int64_t* lda, T* b, const int64_t* ldb, int64_t* info) {                     \
+        *info = h_potrs<T>(*uplo, *n, *nrhs, a, *lda, b, *ldb);                                                \
+    }                                                                                                          \
+    void slate_##X##posv_(const char* uplo, const int64_t* n, const int64_t* nrhs, T* a, const int64_t* lda,   \
+                          T* b, const int64_t* ldb, int64_t* info) {                                          \
+        *info = h_posv<T>(*uplo, *n, *nrhs, a, *lda, b, *ldb);                                                 \
+    }                                                                                                          \
+    void slate_##X##getrf_(const int64_t* m, const int64_t* n, T* a, const int64_t* lda, int64_t* ipiv,        \
+                           int64_t* info) {                                                                    \
+        *info = h_getrf<T>(*m, *n, a, *lda, ipiv);                                                             \
+    }                                                                                                          \
+    void slate_##X##getrs_(const char* trans, const int64_t* n, const int64_t* nrhs, const T* a,               \
+                           const int64_t* lda, const int64_t* ipiv, T* b, const int64_t* ldb, int64_t* info) { \
+        *info = h_getrs<T>(*trans, *n, *nrhs, a, *lda, ipiv, b, *ldb);                                         \
+    }                                                                                                          \
+    void slate_##X##gesv_(const int64_t* n, const int64_t* nrhs, T* a, const int64_t* lda, int64_t* ipiv,      \
+                          T* b, const int64_t* ldb, int64_t* info) {                                          \
+        *info = h_gesv<T>(*n, *nrhs, a, *lda, ipiv, b, *ldb);                                                  \
+    }                                                                                                          \
+    void slate_##X##gemm_(const char* ta, const char* tb, const int64_t* m, const int64_t* n,                  \
+                          const int64_t* k, const T* alpha, const T* a, const int64_t* lda, const T* b,        \
+                          const int64_t* ldb, const T* beta, T* c, const int64_t* ldc) {                       \
+        h_gemm<T>(*ta, *tb, *m, *n, *k, *alpha, a, *lda, b, *ldb, *beta, c, *ldc);                             \
+    }                                                                                                          \
+    void slate_##X##trsm_(const char* side, const char* uplo, const char* ta, const char* diag,                \
+                          const int64_t* m, const int64_t* n, const T* alpha, const T* a, const int64_t* lda,  \
+                          T* b, const int64_t* ldb) {                                                          \
+        h_trsm<T>(*side, *uplo, *ta, *diag, *m, *n, *alpha, a, *lda, b, *ldb);                                 \
+    }                                                                                                          \
+    double slate_##X##lange_(const char* norm, const int64_t* m, const int64_t* n, const T* a,                 \
+                             const int64_t* lda) {                                                             \
+        return h_lange<T>(*norm, *m, *n, a, *lda);                                                             \
+    }
+SN_LAPACK(s, float)
+SN_LAPACK(d, double)
+#undef SN_LAPACK
+
+// complex, interleaved (re, im) pairs through pointers to the real type
+#define SN_LAPACK_C(X, R)                                                                                       \
+    int slate_##X##potrf(char uplo, int64_t n, R* a, int64_t lda) {                                            \
+        return (int)h_potrf<std::complex<R>>(uplo, n, reinterpret_cast<std::complex<R>*>(a), lda);            \
+    }                                                                                                          \
+    int slate_##X##posv(char uplo, int64_t n, int64_t nrhs, R* a, int64_t lda, R* b, int64_t ldb) {            \
+        return (int)h_posv<std::complex<R>>(uplo, n, nrhs, reinterpret_cast<std::complex<R>*>(a), lda,        \
+                                            reinterpret_cast<std::complex<R>*>(b), ldb);                       \
+    }                                                                                                          \
+    int slate_##X##getrf(int64_t m, int64_t n, R* a, int64_t lda, int64_t* ipiv) {                             \
+        return (int)h_getrf<std::complex<R>>(m, n, reinterpret_cast<std::complex<R>*>(a), lda, ipiv);         \
+    }                                                                                                          \
+    int slate_##X##gesv(int64_t n, int64_t nrhs, R* a, int64_t lda, int64_t* ipiv, R* b, int64_t ldb) {       \
+        return (int)h_gesv<std::complex<R>>(n, nrhs, reinterpret_cast<std::complex<R>*>(a), lda, ipiv,        \
+                                            reinterpret_cast<std::complex<R>*>(b), ldb);                       \
+    }                                                                                                          \
+    int slate_##X##gemm(char ta, char tb, int64_t m, int64_t n, int64_t k, const R* alpha, const R* a,         \
+                        int64_t lda, const R* b, int64_t ldb, const R* beta, R* c, int64_t ldc) {              \
+        using C = std::complex<R>;                                                                             \
+        return (int)h_gemm<C>(ta, tb, m, n, k, C(alpha[0], alpha[1]), reinterpret_cast<const C*>(a), lda,     \
+                              reinterpret_cast<const C*>(b), ldb, C(beta[0], beta[1]), reinterpret_cast<C*>(c), \
+                              ldc);                                                                            \
+    }                                                                                                          \
+    double slate_##X##lange(char norm, int64_t m, int64_t n, const R* a, int64_t lda) {                        \
+        return h_lange<std::complex<R>>(norm, m, n, reinterpret_cast<const std::complex<R>*>(a), lda);        \
+    }
+SN_LAPACK_C(c, float)
+SN_LAPACK_C(z, double)
+#undef SN_LAPACK_C
+
+// ---- BLACS over the native runtime's ranks
+void Cblacs_pinfo(int* mypnum, int* nprocs) {
+    sn::initialize();
+    *mypnum = sn::rank();
+    *nprocs = sn::size();
+}
+void Cblacs_get(int, int, int* val) { *val = 0; }
+void Cblacs_gridinit(int* ctxt, const char* order, int nprow, int npcol) {
+    Ctx c;
+    c.p = nprow;
+    c.q = npcol;
+    c.row_major = order && (order[0] == 'R' || order[0] == 'r');
+    contexts().push_back(c);
+    *ctxt = (int)contexts().size() - 1;
+}
+void Cblacs_gridinfo(int ctxt, int* nprow, int* npcol, int* myrow, int* mycol) {
+    auto& cs = contexts();
+    if (ctxt < 0 || ctxt >= (int)cs.size()) { *nprow = *npcol = *myrow = *mycol = -1; return; }
+    const Ctx& c = cs[ctxt];
+    const int r = sn::rank();
+    *nprow = c.p;
+    *npcol = c.q;
+    if (r >= c.p * c.q) { *myrow = *mycol = -1; return; }
+    *myrow = c.row_major ? r / c.q : r % c.p;
+    *mycol = c.row_major ? r % c.q : r / c.p;
+}
+void Cblacs_pcoord(int ctxt, int pnum, int* prow, int* pcol) {
+    const Ctx& c = contexts().at(ctxt);
+    *prow = c.row_major ? pnum / c.q : pnum % c.p;
+    *pcol = c.row_major ? pnum % c.q : pnum / c.p;
+}
+void Cblacs_gridexit(int) {}
+void Cblacs_exit(int) {}
+void blacs_pinfo_(int* mypnum, int* nprocs) { Cblacs_pinfo(mypnum, nprocs); }
+void blacs_get_(const int* ctxt, const int* what, int* val) { Cblacs_get(*ctxt, *what, val); }
+void blacs_gridinit_(int* ctxt, const char* order, const int* nprow, const int* npcol) {
+    Cblacs_gridinit(ctxt, order, *nprow, *npcol);
+}
+void blacs_gridinfo_(const int* ctxt, int* nprow, int* npcol, int* myrow, int* mycol) {
+    Cblacs_gridinfo(*ctxt, nprow, npcol, myrow, mycol);
+}
+void blacs_gridexit_(const int*) {}
+void blacs_exit_(const int*) {}
+
+int numroc_(const int* n, const int* nb, const int* iproc, const int* isrcproc, const int* nprocs) {
+    const int mydist = (*nprocs + *iproc - *isrcproc) % *nprocs;
+    return (int)sn::numroc(*n, *nb, mydist, *nprocs);
+}
+void descinit_(int* desc, const int* m, const int* n, const int* mb, const int* nb, const int* irsrc,
+               const int* icsrc, const int* ictxt, const int* lld, int* info) {
+    desc[0] = 1; desc[1] = *ictxt; desc[2] = *m; desc[3] = *n; desc[4] = *mb; desc[5] = *nb;
+    desc[6] = *irsrc; desc[7] = *icsrc; desc[8] = *lld;
+    *info = (*m < 0) ? -2 : (*n < 0) ? -3 : (*mb < 1) ? -4 : (*nb < 1) ? -5 : 0;
+}
+
+// ---- ScaLAPACK (complex arrays as std::complex<R> / interleaved pairs)
+#define SN_SCAL(X, T)                                                                                          \
+    void p##X##potrf_(const char* uplo, const int* n, T* a, const int* ia, const int* ja, const int* desca,   \
+                      int* info) {                                                                         \
+        *info = p_potrf<T>(*uplo, *n, a, *ia, *ja, desca);                                                 \
+    }                                                                                                      \
+    void p##X##potrs_(const char* uplo, const int* n, const int* nrhs, const T* a, const int* ia,             \
+                      const int* ja, const int* desca, T* b, const int* ib, const int* jb, const int* descb,  \
+                      int* info) {                                                                         \
+        *info = p_potrs<T>(*uplo, *n, *nrhs, a, *ia, *ja, desca, b, *ib, *jb, descb);                      \
+    }                                                                                                      \
+    void p##X##posv_(const char* uplo, const int* n, const int* nrhs, T* a, const int* ia, const int* ja,    \
+                     const int* desca, T* b, const int* ib, const int* jb, const int* descb, int* info) {     \
+        *info = p_posv<T>(*uplo, *n, *nrhs, a, *ia, *ja, desca, b, *ib, *jb, descb);                       \
+    }                                                                                                      \
+    void p##X##getrf_(const int* m, const int* n, T* a, const int* ia, const int* ja, const int* desca,      \
+                      int* ipiv, int* info) {                                                              \
+        *info = p_getrf<T>(*m, *n, a, *ia, *ja, desca, ipiv);                                              \
+    }                                                                                                      \
+    void p##X##getrs_(const char* trans, const int* n, const int* nrhs, const T* a, const int* ia,           \
+                      const int* ja, const int* desca, const int* ipiv, T* b, const int* ib, const int* jb,  \
+                      const int* descb, int* info) {                                                       \
+        *info = p_getrs<T>(*trans, *n, *nrhs, a, *ia, *ja, desca, ipiv, b, *ib, *jb, descb);               \
+    }                                                                                                      \
+    void p##X##gesv_(const int* n, const int* nrhs, T* a, const int* ia, const int* ja, const int* desca,    \
+                     int* ipiv, T* b, const int* ib, const int* jb, const int* descb, int* info) {            \
+        *info = p_gesv<T>(*n, *nrhs, a, *ia, *ja, desca, ipiv, b, *ib, *jb, descb);                        \
+    }                                                                                                      \
+    void p##X##gemm_(const char* ta, const char* tb, const int* m, const int* n, const int* k, const T* alpha, \
+                     const T* a, const int* ia, const int* ja, const int* desca, const T* b, const int* ib,   \
+                     const int* jb, const int* descb, const T* beta, T* c, const int* ic, const int* jc,      \
+                     const int* descc) {                                                                   \
+        p_gemm<T>(*ta, *tb, *m, *n, *k, *alpha, a, *ia, *ja, desca, b, *ib, *jb, descb, *beta, c, *ic, *jc,  \
+                  descc);                                                                                  \
+    }                                                                                                      \
+    void p##X##trsm_(const char* side, const char* uplo, const char* ta, const char* diag, const int* m,     \
+                     const int* n, const T* alpha, const T* a, const int* ia, const int* ja, const int* desca, \
+                     T* b, const int* ib, const int* jb, const int* descb) {                                \
+        p_trsm<T>(*side, *uplo, *ta, *diag, *m, *n, *alpha, a, *ia, *ja, desca, b, *ib, *jb, descb);        \
+    }
+SN_SCAL(s, float)
+SN_SCAL(d, double)
+SN_SCAL(c, std::complex<float>)
+SN_SCAL(z, std::complex<double>)
+#undef SN_SCAL
+float pslange_(const char* norm, const int* m, const int* n, const float* a, const int* ia, const int* ja,
+               const int* desca, float*) {
+    return (float)p_lange<float>(*norm, *m, *n, a, *ia, *ja, desca);
+}
+double pdlange_(const char* norm, const int* m, const int* n, const double* a, const int* ia, const int* ja,
+                const int* desca, double*) {
+    return p_lange<double>(*norm, *m, *n, a, *ia, *ja, desca);
+}
+float pclange_(const char* norm, const int* m, const int* n, const std::complex<float>* a, const int* ia,
+               const int* ja, const int* desca, float*) {
+    return (float)p_lange<std::complex<float>>(*norm, *m, *n, a, *ia, *ja, desca);
+}
+double pzlange_(const char* norm, const int* m, const int* n, const std::complex<double>* a, const int* ia,
+                const int* ja, const int* desca, double*) {
+    return p_lange<std::complex<double>>(*norm, *m, *n, a, *ia, *ja, desca);
+}
+
+// ---- earlier native entry points (kept)
+const char* slate_native_last_error(void) { return g_err.c_str(); }
+int slate_native_initialize(void) { return slate_amd_initialize(); }
+void slate_native_finalize(void) { sn::finalize(); }
+int slate_native_dpotrf(char uplo, int64_t n, double* a, int64_t lda) { return (int)h_potrf<double>(uplo, n, a, lda); }
+int slate_native_dgetrf(int64_t m, int64_t n, double* a, int64_t lda, int64_t* ipiv) {
+    return (int)h_getrf<double>(m, n, a, lda, ipiv);
+}
+int slate_native_dgesv(int64_t n, int64_t nrhs, double* a, int64_t lda, int64_t* ipiv, double* b, int64_t ldb) {
+    return (int)h_gesv<double>(n, nrhs, a, lda, ipiv, b, ldb);
+}
+int slate_native_dposv(char uplo, int64_t n, int64_t nrhs, double* a, int64_t lda, double* b, int64_t ldb) {
+    return (int)h_posv<double>(uplo, n, nrhs, a, lda, b, ldb);
+}
+int slate_native_dgemm(int64_t m, int64_t n, int64_t k, double alpha, const double* a, int64_t lda, const double* b,
+                       int64_t ldb, double beta, double* c, int64_t ldc) {
+    return (int)h_gemm<double>('N', 'N', m, n, k, alpha, a, lda, b, ldb, beta, c, ldc);
+}
+double slate_native_dlange(char norm, int64_t m, int64_t n, const double* a, int64_t lda) {
+    return h_lange<double>(norm, m, n, a, lda);
 }
 
 }  // extern "C"

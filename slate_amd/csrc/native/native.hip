@@ -3,80 +3,44 @@
 //
 // The step loops are the same MI355X designs as the Python drivers
 // (slate_amd/models/chol.py, lu.py, blas3.py), written against the HIP
-// runtime and RCCL directly:
-//   * one process per GPU; RCCL world communicator from a TCP-bootstrapped
-//     unique id; row / column communicators by ncclCommSplit (one per grid
-//     dimension, every collective issued from the panel stream in one
-//     program order on all ranks);
-//   * a high-priority panel stream and a low-priority update stream per
-//     process, dependencies as HIP events, no host synchronisation inside a
-//     factorization (info values are read once at the end);
+// runtime and the transport of native_comm.hip directly:
+//   * one process per GPU; world communicator from a TCP-bootstrapped RCCL
+//     unique id (or the host-staged transport); row / column communicators
+//     by split, each driven from ONE stream (collectives keep one order on
+//     every rank and add no hardware queue);
+//   * a high-priority panel stream, a low-priority update stream and a comm
+//     stream per process, dependencies as HIP events, no host
+//     synchronisation inside a factorization (info values are read once at
+//     the end);
 //   * every flop on the hand-written gfx950 kernels of csrc/hip (potrf_mc /
-//     potrf_lds tile Cholesky, trsm_rlt, the persistent LU panel, the MFMA
-//     GEMM with block-cyclic triangular masks).
+//     potrf_lds tile Cholesky, trsm_rlt, the persistent LU panel and the
+//     distributed LU column step, the MFMA GEMM with block-cyclic masks);
+//   * four precisions (s, d, c, z), as the reference instantiates every
+//     routine (src/potrf.cc:285-303).
 // Reference call stacks: src/potrf.cc:22-210, src/getrf.cc:22-244,
-// src/gemmC.cc:39-202 (SLATE's OpenMP task DAGs over MPI).
-#include <arpa/inet.h>
-#include <netdb.h>
-#include <netinet/in.h>
-#include <netinet/tcp.h>
-#include <sys/socket.h>
-#include <unistd.h>
-
+// src/gemmC.cc:39-202, src/work/work_trsm.cc:102-265 (SLATE's OpenMP task
+// DAGs over MPI).
 #include <algorithm>
-#include <chrono>
+#include <functional>
+#include <map>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
-#include <map>
-#include <mutex>
 #include <string>
-#include <thread>
 #include <tuple>
 #include <vector>
 
 #include <hip/hip_ext.h>
-#include <rccl/rccl.h>
 
-#include "../hip/common.hpp"
 #include "../hip/kernels.hpp"
 #include "../hip/launchers.hpp"
-#include "slate_amd/slate_native.hh"
+#include "native_rt.hpp"
 
 namespace slate_amd {
 namespace native {
 
-using slate_hip::i64;
-
-#define NHIP(x)                                                                                          \
-    do {                                                                                                 \
-        hipError_t e_ = (x);                                                                             \
-        if (e_ != hipSuccess) throw Error(std::string("HIP: ") + hipGetErrorString(e_) + " at " #x);     \
-    } while (0)
-#define NCCL(x)                                                                                          \
-    do {                                                                                                 \
-        ncclResult_t r_ = (x);                                                                           \
-        if (r_ != ncclSuccess) throw Error(std::string("RCCL: ") + ncclGetErrorString(r_) + " at " #x);  \
-    } while (0)
-
 // ------------------------------------------------------------ runtime
-struct GridComms {
-    int p = 1, q = 1, pr = 0, pc = 0;
-    ncclComm_t row = nullptr;   // same process row, ranked by pc
-    ncclComm_t col = nullptr;   // same process column, ranked by pr
-};
-
-struct Runtime {
-    bool up = false;
-    int rank = 0, size = 1, local = 0;
-    ncclComm_t world = nullptr;
-    hipStream_t main = nullptr, panel = nullptr, update = nullptr, update_masked = nullptr;
-    void* lu_work = nullptr;
-    std::map<std::pair<int, int>, GridComms> grids;
-    std::mutex mu;
-};
-
-static Runtime& rt() {
+Runtime& rt() {
     static Runtime r;
     return r;
 }
@@ -86,64 +50,6 @@ static int env_int(const char* k, int def) {
     return v && *v ? std::atoi(v) : def;
 }
 
-// rank 0 serves the RCCL unique id on a TCP port; the others connect (with
-// retries: ranks start in any order)
-static void bootstrap(ncclUniqueId* id, int rank, int size) {
-    const char* addr = std::getenv("MASTER_ADDR");
-    if (!addr) addr = "127.0.0.1";
-    const int port = env_int("SLATE_AMD_NATIVE_PORT", env_int("MASTER_PORT", 29500) + 1);
-    if (rank == 0) {
-        NCCL(ncclGetUniqueId(id));
-        int fd = socket(AF_INET, SOCK_STREAM, 0);
-        int one = 1;
-        setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
-        sockaddr_in sa{};
-        sa.sin_family = AF_INET;
-        sa.sin_addr.s_addr = htonl(INADDR_ANY);
-        sa.sin_port = htons((uint16_t)port);
-        if (bind(fd, (sockaddr*)&sa, sizeof(sa)) != 0 || listen(fd, size) != 0)
-            throw Error("native bootstrap: cannot listen on port " + std::to_string(port));
-        for (int r = 1; r < size; ++r) {
-            int c = accept(fd, nullptr, nullptr);
-            if (c < 0) throw Error("native bootstrap: accept failed");
-            size_t off = 0;
-            while (off < sizeof(*id)) {
-                ssize_t w = send(c, (const char*)id + off, sizeof(*id) - off, 0);
-                if (w <= 0) throw Error("native bootstrap: send failed");
-                off += (size_t)w;
-            }
-            close(c);
-        }
-        close(fd);
-        return;
-    }
-    addrinfo hints{}, *res = nullptr;
-    hints.ai_family = AF_INET;
-    hints.ai_socktype = SOCK_STREAM;
-    if (getaddrinfo(addr, std::to_string(port).c_str(), &hints, &res) != 0 || !res)
-        throw Error(std::string("native bootstrap: cannot resolve ") + addr);
-    const auto t0 = std::chrono::steady_clock::now();
-    for (;;) {
-        int fd = socket(AF_INET, SOCK_STREAM, 0);
-        if (connect(fd, res->ai_addr, res->ai_addrlen) == 0) {
-            size_t off = 0;
-            while (off < sizeof(*id)) {
-                ssize_t g = recv(fd, (char*)id + off, sizeof(*id) - off, 0);
-                if (g <= 0) break;
-                off += (size_t)g;
-            }
-            close(fd);
-            if (off == sizeof(*id)) break;
-        } else {
-            close(fd);
-        }
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120))
-            throw Error("native bootstrap: no connection to rank 0");
-        std::this_thread::sleep_for(std::chrono::milliseconds(20));
-    }
-    freeaddrinfo(res);
-}
-
 void initialize() {
     Runtime& R = rt();
     std::lock_guard<std::mutex> g(R.mu);
@@ -151,17 +57,21 @@ void initialize() {
     R.rank = env_int("RANK", 0);
     R.size = env_int("WORLD_SIZE", 1);
     R.local = env_int("LOCAL_RANK", 0);
-    NHIP(hipSetDevice(R.local));
+    int ndev = 1;
+    NHIP(hipGetDeviceCount(&ndev));
+    R.device = env_int("SLATE_AMD_NATIVE_DEVICE", ndev > 0 ? R.local % ndev : 0);
+    NHIP(hipSetDevice(R.device));
     int lo = 0, hi = 0;
     NHIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
     NHIP(hipStreamCreateWithFlags(&R.main, hipStreamNonBlocking));
     NHIP(hipStreamCreateWithPriority(&R.panel, hipStreamNonBlocking, hi));
     NHIP(hipStreamCreateWithPriority(&R.update, hipStreamNonBlocking, lo));
+    NHIP(hipStreamCreateWithPriority(&R.comm, hipStreamNonBlocking, hi));
     // LU: the persistent panel runs <= 32 workgroups; its trailing update
     // leaves those CUs free (same CU mask as the Python driver, streams.py)
     {
         hipDeviceProp_t pr;
-        NHIP(hipGetDeviceProperties(&pr, R.local));
+        NHIP(hipGetDeviceProperties(&pr, R.device));
         const int ncu = pr.multiProcessorCount, reserve = 32;
         std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
         for (int b = reserve; b < ncu; ++b) mask[b / 32] |= 1u << (b % 32);
@@ -170,11 +80,7 @@ void initialize() {
     const size_t lw = slate_hip::getrf_work_bytes();
     NHIP(hipMalloc(&R.lu_work, lw));
     NHIP(hipMemset(R.lu_work, 0, lw));
-    if (R.size > 1) {
-        ncclUniqueId id;
-        bootstrap(&id, R.rank, R.size);
-        NCCL(ncclCommInitRank(&R.world, R.size, id, R.rank));
-    }
+    transport_init(R.rank, R.size);
     R.up = true;
 }
 
@@ -183,64 +89,43 @@ void finalize() {
     std::lock_guard<std::mutex> g(R.mu);
     if (!R.up) return;
     (void)hipDeviceSynchronize();
-    for (auto& kv : R.grids) {
-        if (kv.second.row) ncclCommDestroy(kv.second.row);
-        if (kv.second.col) ncclCommDestroy(kv.second.col);
-    }
     R.grids.clear();
-    if (R.world) ncclCommDestroy(R.world);
-    R.world = nullptr;
+    transport_finalize();
     (void)hipFree(R.lu_work);
-    for (hipStream_t s : {R.main, R.panel, R.update, R.update_masked}) (void)hipStreamDestroy(s);
+    for (hipStream_t s : {R.main, R.panel, R.update, R.update_masked, R.comm}) (void)hipStreamDestroy(s);
     R.up = false;
 }
 
 int rank() { initialize(); return rt().rank; }
 int size() { initialize(); return rt().size; }
 const char* version() { return "slate_amd-native 2026.10.0"; }
+const char* transport() { initialize(); return transport_name(); }
 
 // row / column communicators of a p x q column-major grid (collective:
 // every rank creates the grids in the same order)
-static GridComms* grid_comms(int p, int q) {
+GridComms* grid_comms(int p, int q) {
     Runtime& R = rt();
-    if (p * q != R.size) throw Error("grid " + std::to_string(p) + "x" + std::to_string(q) +
-                                     " does not match " + std::to_string(R.size) + " ranks");
+    if (p * q != R.size)
+        throw Error("grid " + std::to_string(p) + "x" + std::to_string(q) + " does not match " +
+                    std::to_string(R.size) + " ranks");
     auto key = std::make_pair(p, q);
     auto it = R.grids.find(key);
-    if (it != R.grids.end()) return &it->second;
-    GridComms g;
-    g.p = p; g.q = q;
-    g.pr = R.rank % p;
-    g.pc = R.rank / p;
+    if (it != R.grids.end()) return it->second.get();
+    auto g = std::make_unique<GridComms>();
+    g->p = p;
+    g->q = q;
+    g->pr = R.rank % p;
+    g->pc = R.rank / p;
     if (R.size > 1) {
-        NCCL(ncclCommSplit(R.world, g.pr, g.pc, &g.row, nullptr));
-        NCCL(ncclCommSplit(R.world, g.pc, g.pr, &g.col, nullptr));
+        g->row = world_comm()->split(g->pr, g->pc);
+        g->col = world_comm()->split(g->pc, g->pr);
     }
-    return &(R.grids[key] = g);
+    GridComms* out = g.get();
+    R.grids[key] = std::move(g);
+    return out;
 }
 
 // ------------------------------------------------------------ storage
-static i64 numroc(i64 n, i64 nb, int iproc, int nprocs) {
-    const i64 nblocks = n / nb;
-    i64 num = (nblocks / nprocs) * nb;
-    const i64 extra = nblocks % nprocs;
-    if (iproc < extra) num += nb;
-    else if (iproc == extra) num += n % nb;
-    return num;
-}
-static inline i64 l2g(i64 l, i64 nb, int p, int pr) { return ((l / nb) * p + pr) * nb + l % nb; }
-static inline i64 tiles_before(i64 t, int p, int pr) { return t > pr ? (t - pr + p - 1) / p : 0; }
-
-struct Storage {
-    i64 m = 0, n = 0, nb = 1;
-    int p = 1, q = 1, pr = 0, pc = 0;
-    i64 mloc = 0, nloc = 0, lld = 1;
-    size_t esize = 8;
-    void* buf = nullptr;
-    GridComms* gc = nullptr;
-    ~Storage() { if (buf) (void)hipFree(buf); }
-};
-
 template <typename T>
 Matrix<T>::Matrix(int64_t m, int64_t n, int64_t nb, int p, int q) {
     initialize();
@@ -273,8 +158,27 @@ template <typename T> const T* Matrix<T>::data() const { return static_cast<cons
 template <typename T>
 void Matrix<T>::generate(Gen kind, uint64_t seed) {
     Storage& s = *s_;
-    slate_hip::matgen<T>((int)kind, seed, s.mloc, s.nloc, data(), s.lld, s.m, s.n, s.nb, s.p, s.pr, s.nb, s.q, s.pc,
-                         0, 0, 1.0, rt().main);
+    slate_hip::matgen<K<T>>((int)kind, seed, s.mloc, s.nloc, kp(data()), s.lld, s.m, s.n, s.nb, s.p, s.pr, s.nb, s.q,
+                            s.pc, 0, 0, 1.0, rt().main);
+    NHIP(hipStreamSynchronize(rt().main));
+}
+
+template <typename T>
+void Matrix<T>::from_local_host(const T* Aloc, int64_t ld) {
+    const Storage& s = *s_;
+    if (s.mloc && s.nloc)
+        NHIP(hipMemcpy2DAsync(s.buf, s.lld * sizeof(T), Aloc, ld * sizeof(T), s.mloc * sizeof(T), s.nloc,
+                              hipMemcpyHostToDevice, rt().main));
+    NHIP(hipStreamSynchronize(rt().main));
+}
+
+template <typename T>
+void Matrix<T>::to_local_host(T* Aloc, int64_t ld) const {
+    const Storage& s = *s_;
+    NHIP(hipDeviceSynchronize());
+    if (s.mloc && s.nloc)
+        NHIP(hipMemcpy2DAsync(Aloc, ld * sizeof(T), s.buf, s.lld * sizeof(T), s.mloc * sizeof(T), s.nloc,
+                              hipMemcpyDeviceToHost, rt().main));
     NHIP(hipStreamSynchronize(rt().main));
 }
 
@@ -286,85 +190,81 @@ void Matrix<T>::from_host(const T* A, int64_t lda) {
         const i64 gj = l2g(lj, s.nb, s.q, s.pc);
         for (i64 li = 0; li < s.mloc; ++li) loc[li + lj * s.lld] = A[l2g(li, s.nb, s.p, s.pr) + gj * lda];
     }
-    NHIP(hipMemcpy(data(), loc.data(), loc.size() * sizeof(T), hipMemcpyHostToDevice));
+    NHIP(hipMemcpyAsync(data(), loc.data(), loc.size() * sizeof(T), hipMemcpyHostToDevice, rt().main));
+    NHIP(hipStreamSynchronize(rt().main));
 }
 
+// every rank gets the whole matrix: ONE all-gather of the local blocks
+// (padded to the largest local block), each rank scatters them on the host
 template <typename T>
 void Matrix<T>::to_host(T* A, int64_t lda) const {
     const Storage& s = *s_;
     Runtime& R = rt();
-    std::vector<T> loc((size_t)s.lld * std::max<i64>(s.nloc, 1));
     NHIP(hipDeviceSynchronize());
-    NHIP(hipMemcpy(loc.data(), data(), loc.size() * sizeof(T), hipMemcpyDeviceToHost));
-    std::vector<T> g((size_t)s.m * s.n, T(0));
-    for (i64 lj = 0; lj < s.nloc; ++lj) {
-        const i64 gj = l2g(lj, s.nb, s.q, s.pc);
-        for (i64 li = 0; li < s.mloc; ++li) g[l2g(li, s.nb, s.p, s.pr) + gj * s.m] = loc[li + lj * s.lld];
-    }
-    if (R.size > 1 && !g.empty()) {
-        T* d = nullptr;
-        NHIP(hipMalloc(&d, g.size() * sizeof(T)));
-        NHIP(hipMemcpy(d, g.data(), g.size() * sizeof(T), hipMemcpyHostToDevice));
-        NCCL(ncclAllReduce(d, d, g.size(), sizeof(T) == 8 ? ncclFloat64 : ncclFloat32, ncclSum, R.world, R.main));
+    if (R.size == 1) {
+        std::vector<T> loc((size_t)s.lld * std::max<i64>(s.nloc, 1));
+        NHIP(hipMemcpyAsync(loc.data(), s.buf, loc.size() * sizeof(T), hipMemcpyDeviceToHost, R.main));
         NHIP(hipStreamSynchronize(R.main));
-        NHIP(hipMemcpy(g.data(), d, g.size() * sizeof(T), hipMemcpyDeviceToHost));
-        NHIP(hipFree(d));
+        for (i64 j = 0; j < s.nloc; ++j)
+            for (i64 i = 0; i < s.mloc; ++i) A[i + j * lda] = loc[i + j * s.lld];
+        return;
     }
-    for (i64 j = 0; j < s.n; ++j)
-        for (i64 i = 0; i < s.m; ++i) A[i + j * lda] = g[i + j * s.m];
+    i64 mx_m = 0, mx_n = 0;
+    for (int r = 0; r < s.p; ++r) mx_m = std::max(mx_m, numroc(s.m, s.nb, r, s.p));
+    for (int c = 0; c < s.q; ++c) mx_n = std::max(mx_n, numroc(s.n, s.nb, c, s.q));
+    const size_t blk = (size_t)std::max<i64>(mx_m, 1) * std::max<i64>(mx_n, 1) * sizeof(T);
+    Scratch mine(blk, R.main), all(blk * R.size, R.main);
+    if (s.mloc && s.nloc)
+        NHIP(hipMemcpy2DAsync(mine.p, std::max<i64>(mx_m, 1) * sizeof(T), s.buf, s.lld * sizeof(T),
+                              s.mloc * sizeof(T), s.nloc, hipMemcpyDeviceToDevice, R.main));
+    world_comm()->allgather(mine.p, all.p, blk, R.main);
+    std::vector<T> h(blk / sizeof(T) * R.size);
+    NHIP(hipMemcpyAsync(h.data(), all.p, h.size() * sizeof(T), hipMemcpyDeviceToHost, R.main));
+    NHIP(hipStreamSynchronize(R.main));
+    const i64 ldb = std::max<i64>(mx_m, 1);
+    for (int r = 0; r < R.size; ++r) {
+        const int pr = r % s.p, pc = r / s.p;
+        const i64 ml = numroc(s.m, s.nb, pr, s.p), nl = numroc(s.n, s.nb, pc, s.q);
+        const T* b = h.data() + (size_t)r * (blk / sizeof(T));
+        for (i64 lj = 0; lj < nl; ++lj) {
+            const i64 gj = l2g(lj, s.nb, s.q, pc);
+            for (i64 li = 0; li < ml; ++li) A[l2g(li, s.nb, s.p, pr) + gj * lda] = b[li + lj * ldb];
+        }
+    }
 }
-
-template class Matrix<double>;
-template class Matrix<float>;
 
 // ------------------------------------------------------------ helpers
 namespace {
 
-struct Event {
-    hipEvent_t e = nullptr;
-    Event() { NHIP(hipEventCreateWithFlags(&e, hipEventDisableTiming)); }
-    ~Event() { if (e) (void)hipEventDestroy(e); }
-    Event(const Event&) = delete;
-    void record(hipStream_t s) { NHIP(hipEventRecord(e, s)); }
-    void wait(hipStream_t s) const { NHIP(hipStreamWaitEvent(s, e, 0)); }
-};
-
-// one join point: stream b waits for everything issued so far on stream a
-static void join(hipStream_t a, hipStream_t b) {
-    Event ev;
-    ev.record(a);
-    ev.wait(b);
-}
-
-// device scratch freed after the owning stream reaches it (stream-ordered)
-struct Scratch {
-    void* p = nullptr;
-    hipStream_t s = nullptr;
-    Scratch(size_t bytes, hipStream_t st) : s(st) { if (bytes) NHIP(hipMallocAsync(&p, bytes, st)); }
-    ~Scratch() { if (p) (void)hipFreeAsync(p, s); }
-    template <typename T> T* as() { return static_cast<T*>(p); }
-};
-
-static void gemm_d(char ta, char tb, i64 m, i64 n, i64 k, double alpha, const double* A, i64 lda, const double* B,
-                   i64 ldb, double beta, double* C, i64 ldc, hipStream_t s, const slate_hip::TriMask* mask = nullptr) {
+template <typename T>
+void gemm_k(char ta, char tb, i64 m, i64 n, i64 k, T alpha, const T* A, i64 lda, const T* B, i64 ldb, T beta,
+            T* C, i64 ldc, hipStream_t s, const slate_hip::TriMask* mask = nullptr) {
     if (m <= 0 || n <= 0) return;
     slate_hip::GemmCall c;
     c.transA = ta; c.transB = tb; c.m = m; c.n = n; c.k = k;
-    c.alpha_re = alpha; c.beta_re = beta;
+    c.alpha_re = (double)std::real(alpha); c.alpha_im = (double)std::imag(alpha);
+    c.beta_re = (double)std::real(beta); c.beta_im = (double)std::imag(beta);
     c.A = A; c.lda = lda; c.B = B; c.ldb = ldb; c.C = C; c.ldc = ldc;
     if (mask) c.mask = *mask;
-    slate_hip::gemm_real<double>(c, s);
+    if constexpr (is_cplx<T>()) slate_hip::gemm_complex<K<T>>(c, s);
+    else slate_hip::gemm_real<T>(c, s);
 }
 
 // lower-triangle mask of a local block whose (0, 0) is local (r0, c0) of a
 // block-cyclic matrix (the Python drivers' (1, nb, p, pr, q, pc, r0, c0, 0))
-static slate_hip::TriMask lower_mask(i64 nb, int p, int pr, int q, int pc, i64 r0, i64 c0) {
+slate_hip::TriMask lower_mask(i64 nb, int p, int pr, int q, int pc, i64 r0, i64 c0) {
     slate_hip::TriMask t;
     t.mode = 1; t.nb = nb; t.p = p; t.pr = pr; t.q = q; t.pc = pc; t.row_off = r0; t.col_off = c0; t.diag_off = 0;
     return t;
 }
 
-static int64_t read_infos(const i64* d, i64 nt, hipStream_t s, i64 nb) {
+template <typename T>
+void copy2d(T* dst, i64 ldd, const T* src, i64 lds, i64 m, i64 n, hipStream_t s) {
+    if (m > 0 && n > 0)
+        NHIP(hipMemcpy2DAsync(dst, ldd * sizeof(T), src, lds * sizeof(T), m * sizeof(T), n, hipMemcpyDeviceToDevice, s));
+}
+
+int64_t read_infos(const i64* d, i64 nt, hipStream_t s, i64 nb) {
     std::vector<i64> h((size_t)std::max<i64>(nt, 1));
     NHIP(hipMemcpyAsync(h.data(), d, h.size() * sizeof(i64), hipMemcpyDeviceToHost, s));
     NHIP(hipStreamSynchronize(s));
@@ -373,17 +273,15 @@ static int64_t read_infos(const i64* d, i64 nt, hipStream_t s, i64 nb) {
     return 0;
 }
 
-static int64_t reduce_info(int64_t info) {
+int64_t reduce_info(int64_t info) {
     Runtime& R = rt();
     if (R.size == 1) return info;
     const i64 big = (i64)1 << 62;
-    i64* d = nullptr;
-    NHIP(hipMallocAsync(&d, sizeof(i64), R.main));
+    Scratch d(sizeof(i64), R.main);
     i64 v = info > 0 ? info : big;
-    NHIP(hipMemcpyAsync(d, &v, sizeof(i64), hipMemcpyHostToDevice, R.main));
-    NCCL(ncclAllReduce(d, d, 1, ncclInt64, ncclMin, R.world, R.main));
-    NHIP(hipMemcpyAsync(&v, d, sizeof(i64), hipMemcpyDeviceToHost, R.main));
-    NHIP(hipFreeAsync(d, R.main));
+    NHIP(hipMemcpyAsync(d.p, &v, sizeof(i64), hipMemcpyHostToDevice, R.main));
+    world_comm()->allreduce(d.p, 1, DT::I64, 'm', R.main);
+    NHIP(hipMemcpyAsync(&v, d.p, sizeof(i64), hipMemcpyDeviceToHost, R.main));
     NHIP(hipStreamSynchronize(R.main));
     return v >= big ? 0 : v;
 }
@@ -396,14 +294,14 @@ struct ColPlan {
     i64 order_off = 0, order_cnt = 0, tot = 0;
 };
 
-static ColPlan rows_plan(std::vector<i64>& flat, i64 m, i64 nb, int p, int q, int pc, i64 tfirst, i64 tend,
-                         i64 cols_from) {
+ColPlan rows_plan(std::vector<i64>& flat, i64 m, i64 nb, int p, int q, int pc, i64 tfirst, i64 tend, i64 cols_from) {
     auto mb = [&](i64 j) { return std::min(nb, m - j * nb); };
     std::vector<i64> need;
     for (i64 j = cols_from; j < tend; ++j)
         if (j % q == pc) need.push_back(j);
     ColPlan P;
-    P.off.assign(p, 0); P.cnt.assign(p, 0);
+    P.off.assign(p, 0);
+    P.cnt.assign(p, 0);
     std::vector<i64> base(p, 0), start(need.size(), 0);
     i64 pos = 0;
     for (int r = 0; r < p; ++r) {
@@ -433,25 +331,42 @@ static ColPlan rows_plan(std::vector<i64>& flat, i64 m, i64 nb, int p, int q, in
 }
 
 // Lcol (cnt x kb, contiguous) = the panel rows of this rank's local columns
-// of the plan's tile range, from Prow (this process row's panel rows)
-static void assemble_cols(const ColPlan& P, const i64* idx, const double* Prow, i64 ldp, i64 kb, GridComms* gc,
-                          double* Lcol, hipStream_t s) {
+// of the plan's tile range, from Prow (this process row's panel rows); the
+// column broadcasts go on stream s (the column communicator's stream)
+template <typename T>
+void assemble_cols(const ColPlan& P, const i64* idx, const T* Prow, i64 ldp, i64 kb, GridComms* gc, T* Lcol,
+                   hipStream_t s) {
     if (P.tot == 0) return;
-    Scratch R((size_t)P.tot * kb * 8, s);
+    Scratch R((size_t)P.tot * kb * sizeof(T), s);
     i64 pos = 0;
     for (int r = 0; r < gc->p; ++r) {
         const i64 cnt = P.cnt[r];
         if (cnt) {
-            Scratch tmp((size_t)cnt * kb * 8, s);
-            if (gc->pr == r) slate_hip::permute_rows_gather<double>(cnt, kb, Prow, ldp, tmp.as<double>(), cnt, idx + P.off[r], s);
-            if (gc->p > 1) NCCL(ncclBroadcast(tmp.p, tmp.p, (size_t)cnt * kb, ncclFloat64, r, gc->col, s));
-            NHIP(hipMemcpy2DAsync(R.as<double>() + pos, P.tot * 8, tmp.p, cnt * 8, cnt * 8, kb,
-                                  hipMemcpyDeviceToDevice, s));
+            Scratch tmp((size_t)cnt * kb * sizeof(T), s);
+            if (gc->pr == r)
+                slate_hip::permute_rows_gather<K<T>>(cnt, kb, kp(Prow), ldp, kp(tmp.as<T>()), cnt, idx + P.off[r], s);
+            if (gc->p > 1) gc->col->bcast(tmp.p, (size_t)cnt * kb * sizeof(T), r, s);
+            copy2d(R.as<T>() + pos, P.tot, tmp.as<T>(), cnt, cnt, kb, s);
         }
         pos += cnt;
     }
-    slate_hip::permute_rows_gather<double>(P.order_cnt, kb, R.as<double>(), P.tot, Lcol, P.order_cnt,
-                                           idx + P.order_off, s);
+    slate_hip::permute_rows_gather<K<T>>(P.order_cnt, kb, kp(R.as<T>()), P.tot, kp(Lcol), P.order_cnt,
+                                         idx + P.order_off, s);
+}
+
+// tile Cholesky / panel solve: the tuned fp64 kernels, the generic ones else
+template <typename T>
+void potrf_tile_k(i64 n, T* A, i64 lda, i64* info, hipStream_t s) {
+    if constexpr (std::is_same<T, double>::value)
+        if (slate_hip::potrf_fast((int)n, A, lda, info, 0, s)) return;
+    slate_hip::potrf_tile<K<T>>('L', (int)n, kp(A), lda, info, s);
+}
+template <typename T>
+void trsm_rlc(i64 m, i64 n, const T* L, i64 ldl, T* B, i64 ldb, hipStream_t s) {   // B = B L^{-H}
+    if (m <= 0) return;
+    if constexpr (std::is_same<T, double>::value)
+        if (slate_hip::trsm_rlt_fast(m, n, 1.0, L, ldl, B, ldb, false, s)) return;
+    slate_hip::trsm<K<T>>('R', 'L', ctrans<T>(), 'N', m, n, kv(T(1)), kp(L), ldl, kp(B), ldb, s);
 }
 
 }  // namespace
@@ -460,11 +375,13 @@ static void assemble_cols(const ColPlan& P, const i64* idx, const double* Prow, 
 // One rank owning the whole matrix: trailing update per GROUP of 2 tiles
 // (K = 2 nb on the MFMA GEMM), lookahead in groups (chol.py
 // _potrf_1x1_grouped).
-static void potrf_1x1(double* A, i64 lda, i64 n, i64 nb, int la, i64* infos) {
+template <typename T>
+static void potrf_1x1(T* A, i64 lda, i64 n, i64 nb, int la, i64* infos) {
     Runtime& R = rt();
     hipStream_t ps = R.panel, us = R.update;
     const i64 nt = (n + nb - 1) / nb;
     const i64 G = 2;
+    const char ct = ctrans<T>();
     auto off = [&](i64 t) { return std::min(t * nb, n); };
     const i64 ng = (nt + G - 1) / G;
     auto gstart = [&](i64 gi) { return gi < ng ? off(gi * G) : n; };
@@ -480,20 +397,18 @@ static void potrf_1x1(double* A, i64 lda, i64 n, i64 nb, int la, i64* infos) {
             if (cu > c0) {
                 // the group's earlier panels -> column u (rows >= cu)
                 slate_hip::TriMask mk = lower_mask(nb, 1, 0, 1, 0, cu, cu);
-                gemm_d('N', 'T', n - cu, cu1 - cu, cu - c0, -1.0, A + cu + c0 * lda, lda, A + cu + c0 * lda, lda, 1.0,
-                       A + cu + cu * lda, lda, ps, &mk);
+                gemm_k<T>('N', ct, n - cu, cu1 - cu, cu - c0, T(-1), A + cu + c0 * lda, lda, A + cu + c0 * lda, lda,
+                          T(1), A + cu + cu * lda, lda, ps, &mk);
             }
-            slate_hip::potrf_fast((int)(cu1 - cu), A + cu + cu * lda, lda, infos + u, 0, ps);
-            if (n > cu1)
-                slate_hip::trsm_rlt_fast(n - cu1, cu1 - cu, 1.0, A + cu + cu * lda, lda, A + cu1 + cu * lda, lda, false,
-                                         ps);
+            potrf_tile_k<T>(cu1 - cu, A + cu + cu * lda, lda, infos + u, ps);
+            if (n > cu1) trsm_rlc<T>(n - cu1, cu1 - cu, A + cu + cu * lda, lda, A + cu1 + cu * lda, lda, ps);
         }
         // P = A[c0:n, c0:c2]; update columns [lo, hi) (rows >= lo) on stream s
         auto update = [&](i64 lo, i64 hi, hipStream_t s) {
             if (hi <= lo) return;
             slate_hip::TriMask mk = lower_mask(nb, 1, 0, 1, 0, lo, lo);
-            gemm_d('N', 'T', n - lo, hi - lo, c2 - c0, -1.0, A + lo + c0 * lda, lda, A + lo + c0 * lda, lda, 1.0,
-                   A + lo + lo * lda, lda, s, &mk);
+            gemm_k<T>('N', ct, n - lo, hi - lo, c2 - c0, T(-1), A + lo + c0 * lda, lda, A + lo + c0 * lda, lda, T(1),
+                      A + lo + lo * lda, lda, s, &mk);
         };
         const i64 la_end = gstart(gi + 1 + la);
         if (gi >= 1 && la > 0) ev_tr[gi - 1]->wait(ps);
@@ -511,19 +426,25 @@ static void potrf_1x1(double* A, i64 lda, i64 n, i64 nb, int la, i64* infos) {
     join(us, R.main);
 }
 
-// p x q grid (chol.py _potrf_lower without the diag-first stream): panel
-// stream = tile potrf, column bcast of the diagonal tile, trsm, row bcast of
-// the panel, column gathers of the transposed operand, lookahead GEMM; update
-// stream = the trailing GEMMs.  Every collective on the panel stream.
+// p x q grid (chol.py _potrf_lower): panel stream = tile potrf, column bcast
+// of the diagonal tile, trsm, then the TILE-GRANULAR row broadcast of the
+// panel (SLATE listBcastMT, potrf.cc:122-132): chunk 0 = the first tile row,
+// then chunks of 4 tile rows, on the comm stream (the row communicator's
+// stream) while the panel stream runs each chunk's lookahead GEMM as it
+// lands; column gathers of the transposed operands (column communicator,
+// panel stream); update stream = the trailing GEMMs.
+template <typename T>
 static void potrf_grid(Storage& S, int la, i64* infos) {
     Runtime& R = rt();
     GridComms* gc = S.gc;
     const int p = S.p, q = S.q, pr = S.pr, pc = S.pc;
     const i64 nb = S.nb, n = S.n, lld = S.lld;
-    double* buf = static_cast<double*>(S.buf);
+    const char ct = ctrans<T>();
+    T* buf = static_cast<T*>(S.buf);
     const i64 nt = (n + nb - 1) / nb;
     const i64 lr_end = S.mloc, lc_end = S.nloc;
-    hipStream_t ps = R.panel, us = R.update;
+    const i64 chunk_rows = nb * std::max(1, env_int("SLATE_AMD_POTRF_CHUNK", 4));
+    hipStream_t ps = R.panel, us = R.update, cs = R.comm;
     // plans (host, then one upload)
     std::vector<i64> flat;
     std::vector<std::pair<ColPlan, ColPlan>> plans((size_t)nt);
@@ -537,55 +458,87 @@ static void potrf_grid(Storage& S, int la, i64* infos) {
     NHIP(hipMemcpyAsync(idx.p, flat.data(), flat.size() * sizeof(i64), hipMemcpyHostToDevice, ps));
     join(R.main, ps);
     join(R.main, us);
-    std::vector<std::unique_ptr<Event>> ev_tr((size_t)nt);
-    // buffers that the update stream reads are freed on it
+    join(R.main, cs);
+    std::vector<std::unique_ptr<Event>> ev_tr((size_t)nt), ev_used((size_t)nt);
+    // per-step operand buffers shared by the comm, panel and update streams:
+    // a ring of NR sets; set t % NR is rewritten at step t only after the
+    // update stream has finished step t - NR (explicit events -- no reliance
+    // on the stream-ordered allocator's cross-stream reuse rules)
+    const int NR = la + 3;
+    std::vector<std::unique_ptr<Scratch>> ring_p, ring_a, ring_c;
+    for (int r = 0; r < NR; ++r) {
+        ring_p.push_back(std::make_unique<Scratch>((size_t)std::max<i64>(lr_end, 1) * nb * sizeof(T), ps));
+        ring_a.push_back(std::make_unique<Scratch>((size_t)std::max<i64>(lc_end, 1) * nb * sizeof(T), ps));
+        ring_c.push_back(std::make_unique<Scratch>((size_t)std::max<i64>(lc_end, 1) * nb * sizeof(T), ps));
+    }
     for (i64 t = 0; t < nt; ++t) {
         const i64 g = t;
+        if (t >= NR) {
+            ev_used[t - NR]->wait(ps);
+            ev_used[t - NR]->wait(cs);
+        }
         const i64 kb = std::min(nb, n - g * nb);
         const i64 lrg = tiles_before(g, p, pr) * nb, lcg = tiles_before(g, q, pc) * nb;
         const i64 lr1 = std::min(tiles_before(g + 1, p, pr) * nb, lr_end);
         const i64 lc1 = std::min(tiles_before(g + 1, q, pc) * nb, lc_end);
         const bool own_col = (g % q) == pc, own_diag = own_col && (g % p) == pr;
         if (t - la - 1 >= 0) ev_tr[t - la - 1]->wait(ps);
-        if (own_diag) slate_hip::potrf_fast((int)kb, buf + lrg + lcg * lld, lld, infos + t, 0, ps);
+        if (own_diag) potrf_tile_k<T>(kb, buf + lrg + lcg * lld, lld, infos + t, ps);
         const i64 nrow = lr_end - lr1;
         if (own_col) {
-            const double* D = buf + lrg + lcg * lld;
+            const T* D = buf + lrg + lcg * lld;
             i64 ldd = lld;
-            Scratch Dt(p > 1 ? (size_t)kb * kb * 8 : 0, ps);
+            Scratch Dt(p > 1 ? (size_t)kb * kb * sizeof(T) : 0, ps);
             if (p > 1) {
-                if (own_diag)
-                    NHIP(hipMemcpy2DAsync(Dt.p, kb * 8, buf + lrg + lcg * lld, lld * 8, kb * 8, kb,
-                                          hipMemcpyDeviceToDevice, ps));
-                NCCL(ncclBroadcast(Dt.p, Dt.p, (size_t)kb * kb, ncclFloat64, (int)(g % p), gc->col, ps));
-                D = Dt.as<double>();
+                if (own_diag) copy2d(Dt.as<T>(), kb, buf + lrg + lcg * lld, lld, kb, kb, ps);
+                gc->col->bcast(Dt.p, (size_t)kb * kb * sizeof(T), (int)(g % p), ps);
+                D = Dt.as<T>();
                 ldd = kb;
             }
-            if (nrow) slate_hip::trsm_rlt_fast(nrow, kb, 1.0, D, ldd, buf + lr1 + lcg * lld, lld, false, ps);
+            if (nrow) trsm_rlc<T>(nrow, kb, D, ldd, buf + lr1 + lcg * lld, lld, ps);
         }
-        // panel -> row (Prow: nrow x kb, contiguous)
-        auto Prow = std::make_shared<Scratch>((size_t)std::max<i64>(nrow, 1) * kb * 8, ps);
-        const double* P = buf + lr1 + lcg * lld;
+        // panel -> row (Prow: nrow x kb, contiguous), tile-granular chunks
+        Scratch* Prow = ring_p[t % NR].get();
+        const T* P = buf + lr1 + lcg * lld;
         i64 ldp = lld;
-        if (q > 1) {
-            if (own_col && nrow)
-                NHIP(hipMemcpy2DAsync(Prow->p, nrow * 8, buf + lr1 + lcg * lld, lld * 8, nrow * 8, kb,
-                                      hipMemcpyDeviceToDevice, ps));
-            if (nrow) NCCL(ncclBroadcast(Prow->p, Prow->p, (size_t)nrow * kb, ncclFloat64, (int)(g % q), gc->row, ps));
-            P = Prow->as<double>();
-            ldp = nrow;
+        // chunk 0 holds every lookahead tile row this process row owns
+        const i64 first_rows = std::max(nb, std::min(tiles_before(g + 1 + la, p, pr) * nb, lr_end) - lr1);
+        std::vector<std::pair<i64, i64>> chunks;
+        for (i64 a = 0; a < nrow;) {
+            const i64 b = std::min(nrow, a + (a == 0 ? first_rows : chunk_rows));
+            chunks.push_back({a, b});
+            a = b;
         }
-        // transposed operands: lookahead tiles, then the rest
+        std::vector<std::unique_ptr<Event>> landed(chunks.size());
+        if (q > 1) {
+            P = Prow->as<T>();
+            ldp = std::max<i64>(nrow, 1);
+            Event src;
+            src.record(ps);                          // trsm done
+            src.wait(cs);
+            for (size_t ci = 0; ci < chunks.size(); ++ci) {
+                const i64 a = chunks[ci].first, b = chunks[ci].second;
+                auto cb = std::make_unique<Scratch>((size_t)(b - a) * kb * sizeof(T), cs);
+                if (own_col) copy2d(cb->as<T>(), b - a, buf + lr1 + a + lcg * lld, lld, b - a, kb, cs);
+                gc->row->bcast(cb->p, (size_t)(b - a) * kb * sizeof(T), (int)(g % q), cs);
+                copy2d(Prow->as<T>() + a, ldp, cb->as<T>(), b - a, b - a, kb, cs);
+                landed[ci] = std::make_unique<Event>();
+                landed[ci]->record(cs);
+            }
+        }
+        auto land = [&](size_t ci) { if (q > 1) landed[ci]->wait(ps); };
+        if (!chunks.empty()) land(0);
+        // transposed operands: lookahead tiles (in chunk 0), then the rest
         const ColPlan& A1 = plans[t].first;
         const ColPlan& A2 = plans[t].second;
-        auto Lla = std::make_shared<Scratch>((size_t)std::max<i64>(A1.order_cnt, 1) * kb * 8, ps);
-        auto Lcol = std::make_shared<Scratch>((size_t)std::max<i64>(A2.order_cnt, 1) * kb * 8, ps);
+        Scratch* Lla = ring_a[t % NR].get();
+        Scratch* Lcol = ring_c[t % NR].get();
         const i64* d_idx = idx.as<i64>();
-        const double* La;
+        const T* La;
         i64 lda_la;
         if (p > 1 || q > 1) {
-            assemble_cols(A1, d_idx, P, ldp, kb, gc, Lla->as<double>(), ps);
-            La = Lla->as<double>();
+            assemble_cols<T>(A1, d_idx, P, ldp, kb, gc, Lla->as<T>(), ps);
+            La = Lla->as<T>();
             lda_la = std::max<i64>(A1.order_cnt, 1);
         } else {
             La = P;
@@ -593,15 +546,20 @@ static void potrf_grid(Storage& S, int la, i64* infos) {
         }
         const i64 lc_la = std::min(tiles_before(g + 1 + la, q, pc) * nb, lc_end);
         if (t >= 1 && la > 0) ev_tr[t - 1]->wait(ps);
-        if (lc_la > lc1 && nrow) {
-            slate_hip::TriMask mk = lower_mask(nb, p, pr, q, pc, lr1, lc1);
-            gemm_d('N', 'T', nrow, lc_la - lc1, kb, -1.0, P, ldp, La, lda_la, 1.0, buf + lr1 + lc1 * lld, lld, ps, &mk);
+        for (size_t ci = 0; ci < chunks.size(); ++ci) {
+            if (ci) land(ci);
+            const i64 a = chunks[ci].first, b = chunks[ci].second;
+            if (lc_la > lc1) {
+                slate_hip::TriMask mk = lower_mask(nb, p, pr, q, pc, lr1 + a, lc1);
+                gemm_k<T>('N', ct, b - a, lc_la - lc1, kb, T(-1), P + a, ldp, La, lda_la, T(1),
+                          buf + lr1 + a + lc1 * lld, lld, ps, &mk);
+            }
         }
-        const double* Lc;
+        const T* Lc;
         i64 ldlc, loff;
         if (p > 1 || q > 1) {
-            assemble_cols(A2, d_idx, P, ldp, kb, gc, Lcol->as<double>(), ps);
-            Lc = Lcol->as<double>();
+            assemble_cols<T>(A2, d_idx, P, ldp, kb, gc, Lcol->as<T>(), ps);
+            Lc = Lcol->as<T>();
             ldlc = std::max<i64>(A2.order_cnt, 1);
             loff = lc_la;
         } else {
@@ -617,181 +575,518 @@ static void potrf_grid(Storage& S, int la, i64* infos) {
             const i64 c0 = part == 0 ? lc_la : lc_nx, c1 = part == 0 ? lc_nx : lc_end;
             if (c1 > c0 && nrow) {
                 slate_hip::TriMask mk = lower_mask(nb, p, pr, q, pc, lr1, c0);
-                gemm_d('N', 'T', nrow, c1 - c0, kb, -1.0, P, ldp, Lc + (c0 - loff), ldlc, 1.0, buf + lr1 + c0 * lld,
-                       lld, us, &mk);
+                gemm_k<T>('N', ct, nrow, c1 - c0, kb, T(-1), P, ldp, Lc + (c0 - loff), ldlc, T(1),
+                          buf + lr1 + c0 * lld, lld, us, &mk);
             }
             if (part == 0) {
                 ev_tr[t] = std::make_unique<Event>();
                 ev_tr[t]->record(us);
             }
         }
-        // the step's operand buffers are released once the update stream is
-        // past them: move their frees to the update stream
-        Prow->s = us; Lla->s = us; Lcol->s = us;
-        join(ps, us);      // frees on us are ordered after the panel's writes
+        ev_used[t] = std::make_unique<Event>();
+        ev_used[t]->record(us);
     }
     join(ps, R.main);
     join(us, R.main);
+    join(cs, R.main);
+    for (auto* v : {&ring_p, &ring_a, &ring_c})
+        for (auto& x : *v) x->s = R.main;       // freed after every stream joined main
+    idx.s = R.main;
 }
 
-int64_t potrf(HermitianMatrix<double>& A, const Options& opts) {
+template <typename T>
+int64_t potrf(HermitianMatrix<T>& A, const Options& opts) {
     if (A.uplo() != Uplo::Lower) throw Error("native potrf: Lower storage only (use the conjugate transpose)");
     Storage& S = *A.storage();
     Runtime& R = rt();
     const i64 nt = (S.n + S.nb - 1) / S.nb;
     const int la = std::max(0, opts.lookahead);
-    i64* infos = nullptr;
-    NHIP(hipMallocAsync(&infos, sizeof(i64) * std::max<i64>(nt, 1), R.main));
-    NHIP(hipMemsetAsync(infos, 0, sizeof(i64) * std::max<i64>(nt, 1), R.main));
+    Scratch infos(sizeof(i64) * std::max<i64>(nt, 1), R.main);
+    NHIP(hipMemsetAsync(infos.p, 0, sizeof(i64) * std::max<i64>(nt, 1), R.main));
     if (S.p == 1 && S.q == 1 && nt > 2)
-        potrf_1x1(static_cast<double*>(S.buf), S.lld, S.n, S.nb, la, infos);
+        potrf_1x1<T>(static_cast<T*>(S.buf), S.lld, S.n, S.nb, la, infos.as<i64>());
     else
-        potrf_grid(S, la, infos);
-    const int64_t info = read_infos(infos, nt, R.main, S.nb);
-    NHIP(hipFreeAsync(infos, R.main));
+        potrf_grid<T>(S, la, infos.as<i64>());
+    const int64_t info = read_infos(infos.as<i64>(), nt, R.main, S.nb);
     return reduce_info(info);
 }
 
-// ------------------------------------------------------------ solves (one rank)
-static void require_1x1(const Storage& S, const char* what) {
-    if (S.p != 1 || S.q != 1)
-        throw Error(std::string("native ") + what + ": 1 x 1 grids only (the Python package covers p x q)");
+// ------------------------------------------------------------ distributed trsm
+// B = op(A)^{-1} B, Side Left, A the uplo triangle (SLATE work::trsm,
+// src/work/work_trsm.cc:102-265, as a tile-step loop): per step k (forward
+// for Lower/NoTrans, backward for Upper/NoTrans)
+//   diagonal tile A_kk -> process row k%p (row comm); that row solves its
+//   local columns of B_k; X_k -> every process row (column comm); panel
+//   A(:, k) -> every process column (row comm); B_i -= A_ik X_k locally.
+// ConjTrans of a Lower A is a backward Upper solve on A^H, materialised by
+// one tile redistribution (p2p) first.
+template <typename T>
+static void transpose_tiles(const Storage& L, Storage& U, char ct);
+
+template <typename T>
+static void trsm_left(char uplo, char diag, T alpha, const Storage& SA, Storage& SB) {
+    Runtime& R = rt();
+    GridComms* gc = SB.gc;
+    const int p = SB.p, q = SB.q, pr = SB.pr, pc = SB.pc;
+    const i64 nb = SA.nb, n = SA.n, nrhs_loc = SB.nloc;
+    const T* A = static_cast<const T*>(SA.buf);
+    T* B = static_cast<T*>(SB.buf);
+    const i64 lda = SA.lld, ldb = SB.lld;
+    const i64 nt = (n + nb - 1) / nb;
+    hipStream_t s = R.main;
+    if (alpha != T(1) && SB.mloc && nrhs_loc) slate_hip::gescale<K<T>>('G', SB.mloc, nrhs_loc, kv(alpha), kp(B), ldb, s);
+    const bool lower = uplo == 'L';
+    for (i64 st = 0; st < nt; ++st) {
+        const i64 k = lower ? st : nt - 1 - st;
+        const i64 kb = std::min(nb, n - k * nb);
+        const int rk = (int)(k % p), ck = (int)(k % q);
+        const i64 lrk = tiles_before(k, p, pr) * nb, lck = tiles_before(k, q, pc) * nb;
+        // diagonal tile to process row rk
+        Scratch D((size_t)kb * kb * sizeof(T), s);
+        if (pr == rk) {
+            if (pc == ck) copy2d(D.as<T>(), kb, A + lrk + lck * lda, lda, kb, kb, s);
+            if (q > 1) gc->row->bcast(D.p, (size_t)kb * kb * sizeof(T), ck, s);
+            if (nrhs_loc)
+                slate_hip::trsm<K<T>>('L', uplo, 'N', diag, kb, nrhs_loc, kv(T(1)), kp(D.as<T>()), kb,
+                                      kp(B + lrk), ldb, s);
+        }
+        // X_k to every process row
+        Scratch X((size_t)kb * std::max<i64>(nrhs_loc, 1) * sizeof(T), s);
+        if (pr == rk) copy2d(X.as<T>(), kb, B + lrk, ldb, kb, nrhs_loc, s);
+        if (p > 1 && nrhs_loc) gc->col->bcast(X.p, (size_t)kb * nrhs_loc * sizeof(T), rk, s);
+        // panel A(rows after / before k, k) of this process row
+        const i64 r0 = lower ? std::min(tiles_before(k + 1, p, pr) * nb, SA.mloc) : 0;
+        const i64 r1 = lower ? SA.mloc : std::min(tiles_before(k, p, pr) * nb, SA.mloc);
+        const i64 nr = r1 - r0;
+        if (nr <= 0) continue;
+        Scratch Pn((size_t)nr * kb * sizeof(T), s);
+        if (pc == ck) copy2d(Pn.as<T>(), nr, A + r0 + lck * lda, lda, nr, kb, s);
+        if (q > 1) gc->row->bcast(Pn.p, (size_t)nr * kb * sizeof(T), ck, s);
+        if (nrhs_loc)
+            gemm_k<T>('N', 'N', nr, nrhs_loc, kb, T(-1), Pn.as<T>(), nr, X.as<T>(), kb, T(1), B + r0, ldb, s);
+    }
+    NHIP(hipStreamSynchronize(s));
 }
 
-int64_t potrs(const HermitianMatrix<double>& A, Matrix<double>& B, const Options&) {
-    const Storage& S = *A.storage();
-    Storage& T = *B.storage();
-    require_1x1(S, "potrs");
-    require_1x1(T, "potrs");
-    hipStream_t s = rt().main;
-    const double* L = static_cast<const double*>(S.buf);
-    double* X = static_cast<double*>(T.buf);
-    slate_hip::trsm<double>('L', 'L', 'N', 'N', S.n, T.n, 1.0, L, S.lld, X, T.lld, s);
-    slate_hip::trsm<double>('L', 'L', 'T', 'N', S.n, T.n, 1.0, L, S.lld, X, T.lld, s);
+template <typename T>
+void trsm(Side side, Uplo uplo, Op op, Diag diag, T alpha, const Matrix<T>& A, Matrix<T>& B, const Options&) {
+    if (side != Side::Left) throw Error("native trsm: Side::Left");
+    const Storage& SA = *A.storage();
+    Storage& SB = *B.storage();
+    if (SA.m != SA.n || SA.n != SB.m) throw Error("native trsm: dimension mismatch");
+    if (SA.nb != SB.nb || SA.p != SB.p || SA.q != SB.q) throw Error("native trsm: A and B must share grid and nb");
+    NHIP(hipStreamSynchronize(rt().main));
+    if (op == Op::NoTrans) {
+        trsm_left<T>((char)uplo, (char)diag, alpha, SA, SB);
+        return;
+    }
+    if (op == Op::Trans && is_cplx<T>()) throw Error("native trsm: Trans of a complex matrix (use ConjTrans)");
+    // op(A) = A^H: materialise it (the other triangle) and solve NoTrans
+    Matrix<T> At(SA.n, SA.n, SA.nb, SA.p, SA.q);
+    transpose_tiles<T>(SA, *At.storage(), ctrans<T>());
+    trsm_left<T>(uplo == Uplo::Lower ? 'U' : 'L', (char)diag, alpha, *At.storage(), SB);
+}
+
+template <typename T>
+void copy(Op op, const Matrix<T>& A, Matrix<T>& B) {
+    const Storage& SA = *A.storage();
+    Storage& SB = *B.storage();
+    const bool tr = op != Op::NoTrans;
+    if ((tr ? SA.n : SA.m) != SB.m || (tr ? SA.m : SA.n) != SB.n) throw Error("native copy: dimension mismatch");
+    if (SA.nb != SB.nb || SA.p != SB.p || SA.q != SB.q) throw Error("native copy: A and B must share grid and nb");
+    Runtime& R = rt();
+    NHIP(hipStreamSynchronize(R.main));
+    if (!tr) {
+        copy2d(static_cast<T*>(SB.buf), SB.lld, static_cast<const T*>(SA.buf), SA.lld, SA.mloc, SA.nloc, R.main);
+        NHIP(hipStreamSynchronize(R.main));
+        return;
+    }
+    transpose_tiles<T>(SA, SB, (op == Op::ConjTrans && is_cplx<T>()) ? 'C' : 'T');
+}
+
+// tile (i, j) of L (m x n) -> tile (j, i) of U (n x m), transposed ('T') or
+// conjugate-transposed ('C'), for every local tile of L: one batched
+// point-to-point exchange (same-rank tiles are copied locally)
+template <typename T>
+static void transpose_tiles(const Storage& L, Storage& U, char ct) {
+    Runtime& R = rt();
+    hipStream_t s = R.main;
+    const int p = L.p, q = L.q, pr = L.pr, pc = L.pc;
+    const i64 nb = L.nb;
+    const i64 mt = (L.m + nb - 1) / nb, ntl = (L.n + nb - 1) / nb;
+    const T* A = static_cast<const T*>(L.buf);
+    T* B = static_cast<T*>(U.buf);
+    // tile t's extent: rows of L for i, columns of L for j
+    auto mbr = [&](i64 t) { return std::min(nb, L.m - t * nb); };
+    auto mbc = [&](i64 t) { return std::min(nb, L.n - t * nb); };
+    auto owner = [&](i64 i, i64 j) { return (int)(i % p) + (int)(j % q) * p; };
+    struct Item { i64 i, j; };
+    std::map<int, std::vector<Item>> sends, recvs;
+    for (i64 j = 0; j < ntl; ++j)
+        for (i64 i = 0; i < mt; ++i) {
+            const int src = owner(i, j), dst = owner(j, i);
+            if (src == R.rank && dst == R.rank) {
+                const T* a = A + tiles_before(i, p, pr) * nb + tiles_before(j, q, pc) * nb * L.lld;
+                T* b = B + tiles_before(j, p, pr) * nb + tiles_before(i, q, pc) * nb * U.lld;
+                slate_hip::gecopy<K<T>, K<T>>('G', ct, mbc(j), mbr(i), kp(a), L.lld, kp(b), U.lld, s);
+            } else if (src == R.rank) {
+                sends[dst].push_back({i, j});
+            } else if (dst == R.rank) {
+                recvs[src].push_back({i, j});
+            }
+        }
+    std::vector<std::unique_ptr<Scratch>> bufs;
+    std::vector<P2P> ops;
+    std::vector<std::tuple<Scratch*, std::vector<Item>*>> unpack;
+    for (auto& kv2 : sends) {
+        size_t tot = 0;
+        for (auto& it : kv2.second) tot += (size_t)mbr(it.i) * mbc(it.j);
+        bufs.push_back(std::make_unique<Scratch>(tot * sizeof(T), s));
+        size_t off = 0;
+        for (auto& it : kv2.second) {
+            const T* a = A + tiles_before(it.i, p, pr) * nb + tiles_before(it.j, q, pc) * nb * L.lld;
+            copy2d(bufs.back()->as<T>() + off, mbr(it.i), a, L.lld, mbr(it.i), mbc(it.j), s);
+            off += (size_t)mbr(it.i) * mbc(it.j);
+        }
+        ops.push_back({true, kv2.first, bufs.back()->p, tot * sizeof(T)});
+    }
+    for (auto& kv2 : recvs) {
+        size_t tot = 0;
+        for (auto& it : kv2.second) tot += (size_t)mbr(it.i) * mbc(it.j);
+        bufs.push_back(std::make_unique<Scratch>(tot * sizeof(T), s));
+        ops.push_back({false, kv2.first, bufs.back()->p, tot * sizeof(T)});
+        unpack.emplace_back(bufs.back().get(), &kv2.second);
+    }
+    if (!ops.empty()) world_comm()->exchange(ops, s);
+    for (auto& u : unpack) {
+        Scratch* b = std::get<0>(u);
+        size_t off = 0;
+        for (auto& it : *std::get<1>(u)) {
+            T* dst = B + tiles_before(it.j, p, pr) * nb + tiles_before(it.i, q, pc) * nb * U.lld;
+            slate_hip::gecopy<K<T>, K<T>>('G', ct, mbc(it.j), mbr(it.i), kp(b->as<T>() + off), mbr(it.i), kp(dst), U.lld,
+                                          s);
+            off += (size_t)mbr(it.i) * mbc(it.j);
+        }
+    }
     NHIP(hipStreamSynchronize(s));
+}
+
+// ------------------------------------------------------------ solves
+template <typename T>
+int64_t potrs(const HermitianMatrix<T>& A, Matrix<T>& B, const Options& opts) {
+    trsm<T>(Side::Left, Uplo::Lower, Op::NoTrans, Diag::NonUnit, T(1), A, B, opts);
+    trsm<T>(Side::Left, Uplo::Lower, Op::ConjTrans, Diag::NonUnit, T(1), A, B, opts);
     return 0;
 }
 
-int64_t posv(HermitianMatrix<double>& A, Matrix<double>& B, const Options& opts) {
+template <typename T>
+int64_t posv(HermitianMatrix<T>& A, Matrix<T>& B, const Options& opts) {
     const int64_t info = potrf(A, opts);
     if (info == 0) potrs(A, B, opts);
     return info;
 }
 
-// ------------------------------------------------------------ getrf (1 x q)
-int64_t getrf(Matrix<double>& A, std::vector<int64_t>& ipiv_out, const Options& opts) {
+// ------------------------------------------------------------ getrf
+// row interchanges ipiv[k1, k2) (global rows, 0-based, sequential) applied to
+// the local columns [c0, c1) of a p x q matrix: p == 1 a local laswp; p > 1
+// the owner-masked exchange (swap plan folded on the device, pack the rows
+// this rank owns, all-reduce over the process column, unpack) in chunks of
+// at most 512 swaps -- models/lu.py permute_rows / _xchg_update
+template <typename T>
+static void permute_rows_dist(Storage& S, const i64* ipiv_d, i64 k1, i64 k2, i64 c0, i64 c1, int incx, hipStream_t s,
+                              Comm* colc) {
+    if (c1 <= c0 || k2 <= k1) return;
+    T* buf = static_cast<T*>(S.buf);
+    if (S.p == 1) {
+        slate_hip::laswp_off<K<T>>(c1 - c0, kp(buf + c0 * S.lld), S.lld, k1, k2, ipiv_d, 0, s, incx);
+        return;
+    }
+    Scratch plan(slate_hip::swap_plan_bytes(), s);
+    std::vector<std::pair<i64, i64>> ch;
+    for (i64 a = k1; a < k2; a += 512) ch.push_back({a, std::min(k2, a + 512)});
+    if (incx < 0) std::reverse(ch.begin(), ch.end());
+    for (auto& c : ch) {
+        const i64 ns = c.second - c.first, S2 = 2 * ns;
+        slate_hip::swap_plan(c.first, c.second, ipiv_d, 0, incx, plan.p, s);
+        Scratch X((size_t)S2 * (c1 - c0) * sizeof(T), s);
+        slate_hip::xchg_gather<K<T>>(plan.p, S2, c1 - c0, kp(buf + c0 * S.lld), S.lld, kp(X.as<T>()), S2, S.nb, S.p,
+                                     S.pr, s);
+        colc->allreduce(X.p, (size_t)S2 * (c1 - c0), dt_of<T>::v, 's', s);
+        slate_hip::xchg_scatter<K<T>>(plan.p, S2, c1 - c0, kp(X.as<T>()), S2, kp(buf + c0 * S.lld), S.lld, S.nb, S.p,
+                                      S.pr, s);
+    }
+}
+
+// LU of the p x q panel column k (kb columns at local column lck of the
+// process column that owns it): rows stay on their owners, one record
+// all-gather per column (lu_dist_step), recursion halves joined by the
+// owner-masked row exchange; every rank of the column ends with its factored
+// rows in place and the same kb x kb top block T
+template <typename T>
+static void panel_dist(Storage& S, i64 k, i64 kb, i64 lck, i64* ipiv_d, i64* info, double thr, int bw, T* Tt,
+                       hipStream_t s) {
+    const int p = S.p, pr = S.pr;
+    const i64 nb = S.nb, r0 = k * nb;
+    const int rk = (int)(k % p);
+    const i64 lr_k = std::min(tiles_before(k, p, pr) * nb, S.mloc);
+    const i64 nmine = S.mloc - lr_k;
+    T* buf = static_cast<T*>(S.buf);
+    T* W = buf + lr_k + lck * S.lld;
+    const i64 ldw = S.lld;
+    Comm* colc = S.gc->col.get();
+    // panel-relative global rows of my panel rows
+    std::vector<i64> gr((size_t)std::max<i64>(nmine, 1));
+    for (i64 i = 0; i < nmine; ++i) gr[i] = l2g(lr_k + i, nb, p, pr) - r0;
+    Scratch grow(gr.size() * sizeof(i64), s);
+    NHIP(hipMemcpyAsync(grow.p, gr.data(), gr.size() * sizeof(i64), hipMemcpyHostToDevice, s));
+    Scratch part(2 * 1024 * 8 + 64, s);
+    const int b = std::max(1, bw);
+    Scratch recs((size_t)p * (3 + 2 * b) * sizeof(T), s), rec((size_t)(3 + 2 * b) * sizeof(T), s);
+    NHIP(hipMemsetAsync(Tt, 0, (size_t)kb * kb * sizeof(T), s));
+    i64* piv = ipiv_d + r0;                 // panel-relative
+    auto base = [&](i64 c0, i64 c1) {
+        const int recn = 3 + 2 * (int)(c1 - c0);
+        for (i64 j = c0; j <= c1; ++j) {
+            const bool nxt = j < c1;
+            const i64 dl = (pr == rk && nxt) ? j : -1;
+            slate_hip::lu_dist_step<K<T>>(nmine, kp(W + c0 * ldw), ldw, grow.as<i64>(), (int)c0, (int)c1, (int)j,
+                                          j > c0 ? kp(recs.as<T>()) : nullptr, p, kp(Tt), kb, piv, info, 0, thr,
+                                          kp(rec.as<T>()), part.p, dl, s);
+            if (nxt) colc->allgather(rec.p, recs.p, (size_t)recn * sizeof(T), s);
+        }
+    };
+    // interchanges of panel columns [a, e) applied to panel columns [ca, cb);
+    // returns the window rows (new rows a..e) in a buffer of e - a rows
+    auto exchange = [&](i64 a, i64 e, i64 ca, i64 cb, std::unique_ptr<Scratch>& Xout) -> T* {
+        Scratch plan(slate_hip::swap_plan_bytes(), s);
+        slate_hip::swap_plan(r0 + a, r0 + e, ipiv_d, -r0, 1, plan.p, s);
+        const i64 S2 = 2 * (e - a), w = cb - ca;
+        Xout = std::make_unique<Scratch>((size_t)S2 * w * sizeof(T), s);
+        T* X = Xout->as<T>();
+        T* cols = buf + (lck + ca) * S.lld;
+        slate_hip::xchg_gather<K<T>>(plan.p, S2, w, kp(cols), S.lld, kp(X), S2, nb, p, pr, s);
+        colc->allreduce(X, (size_t)S2 * w, dt_of<T>::v, 's', s);
+        slate_hip::xchg_scatter<K<T>>(plan.p, S2, w, kp(X), S2, kp(cols), S.lld, nb, p, pr, s);
+        return X;                           // leading dimension S2
+    };
+    std::function<void(i64, i64)> rec_fn = [&](i64 c0, i64 c1) {
+        if (c1 - c0 <= b) { base(c0, c1); return; }
+        i64 cm = c0 + ((c1 - c0) / 2 + b - 1) / b * b;
+        if (cm >= c1) cm = c1 - b;
+        rec_fn(c0, cm);
+        std::unique_ptr<Scratch> Xs;
+        T* U = exchange(c0, cm, cm, c1, Xs);
+        const i64 ldu = 2 * (cm - c0);
+        slate_hip::trsm<K<T>>('L', 'L', 'N', 'U', cm - c0, c1 - cm, kv(T(1)), kp(Tt + c0 + c0 * kb), kb, kp(U), ldu, s);
+        copy2d(Tt + c0 + cm * kb, kb, U, ldu, cm - c0, c1 - cm, s);
+        if (pr == rk) copy2d(W + c0 + cm * ldw, ldw, U, ldu, cm - c0, c1 - cm, s);
+        const i64 i0 = pr == rk ? cm : 0;
+        if (nmine > i0)
+            gemm_k<T>('N', 'N', nmine - i0, c1 - cm, cm - c0, T(-1), W + i0 + c0 * ldw, ldw, U, ldu, T(1),
+                      W + i0 + cm * ldw, ldw, s);
+        rec_fn(cm, c1);
+        std::unique_ptr<Scratch> X2;
+        T* V = exchange(cm, c1, c0, cm, X2);
+        copy2d(Tt + cm + c0 * kb, kb, V, 2 * (c1 - cm), c1 - cm, cm - c0, s);
+    };
+    rec_fn(0, kb);
+}
+
+template <typename T>
+int64_t getrf(Matrix<T>& A, std::vector<int64_t>& ipiv_out, const Options& opts) {
     Storage& S = *A.storage();
     Runtime& R = rt();
-    if (S.p != 1) throw Error("native getrf: 1 x q grids (the Python package covers p x q)");
     GridComms* gc = S.gc;
-    const int q = S.q, pc = S.pc;
-    const i64 nb = S.nb, m = S.m, n = S.n, lld = S.lld, nloc = S.nloc;
+    const int p = S.p, q = S.q, pr = S.pr, pc = S.pc;
+    const i64 nb = S.nb, m = S.m, n = S.n, lld = S.lld, nloc = S.nloc, mloc = S.mloc;
     const i64 kt = std::min((m + nb - 1) / nb, (n + nb - 1) / nb);
     const int la = std::max(0, opts.lookahead);
-    double* buf = static_cast<double*>(S.buf);
-    hipStream_t ps = R.panel, us = R.update_masked;
+    T* buf = static_cast<T*>(S.buf);
+    hipStream_t ps = R.panel, us = p == 1 ? R.update_masked : R.update;
     const i64 kmin = std::min(m, n);
-    i64 *ipiv = nullptr, *infos = nullptr;
-    NHIP(hipMallocAsync(&ipiv, sizeof(i64) * std::max<i64>(kmin, 1), R.main));
-    NHIP(hipMallocAsync(&infos, sizeof(i64) * std::max<i64>(kt, 1), R.main));
-    NHIP(hipMemsetAsync(ipiv, 0, sizeof(i64) * std::max<i64>(kmin, 1), R.main));
-    NHIP(hipMemsetAsync(infos, 0, sizeof(i64) * std::max<i64>(kt, 1), R.main));
+    Scratch ipiv(sizeof(i64) * std::max<i64>(kmin, 1), R.main), infos(sizeof(i64) * std::max<i64>(kt, 1), R.main);
+    NHIP(hipMemsetAsync(ipiv.p, 0, sizeof(i64) * std::max<i64>(kmin, 1), R.main));
+    NHIP(hipMemsetAsync(infos.p, 0, sizeof(i64) * std::max<i64>(kt, 1), R.main));
+    i64* ipiv_d = ipiv.as<i64>();
     join(R.main, ps);
     join(R.main, us);
-    std::vector<std::unique_ptr<Event>> ev_tr((size_t)kt);
-    // apply step k (pivots, U-row trsm, GEMM) to local columns [c0, c1)
-    auto update_cols = [&](const double* Lp, i64 ldl, i64 r0, i64 kb, i64 c0, i64 c1, hipStream_t s) {
-        if (c1 <= c0) return;
-        double* cols = buf + c0 * lld;
-        slate_hip::laswp_off<double>(c1 - c0, cols, lld, r0, r0 + kb, ipiv, -r0, s);
-        double* Ukk = buf + r0 + c0 * lld;
-        slate_hip::trsm<double>('L', 'L', 'N', 'U', kb, c1 - c0, 1.0, Lp, ldl, Ukk, lld, s);
-        if (m > r0 + kb) gemm_d('N', 'N', m - r0 - kb, c1 - c0, kb, -1.0, Lp + kb, ldl, Ukk, lld, 1.0,
-                                buf + r0 + kb + c0 * lld, lld, s);
-    };
-    for (i64 k = 0; k < kt; ++k) {
-        const i64 r0 = k * nb;
-        const i64 kb = std::min({nb, n - r0, m - r0});
-        const i64 mk = m - r0;
-        const bool own = (k % q) == pc;
-        const i64 lck = tiles_before(k, q, pc) * nb;
-        const i64 lc1 = std::min(tiles_before(k + 1, q, pc) * nb, nloc);
-        const i64 lcla = std::min(tiles_before(k + 1 + la, q, pc) * nb, nloc);
-        if (k - la - 1 >= 0) ev_tr[k - la - 1]->wait(ps);
-        auto Lbuf = std::make_shared<Scratch>(own && q == 1 ? 0 : (size_t)mk * kb * 8, ps);
-        const double* Lp;
-        i64 ldl;
-        if (own) {
-            const i64 wk = std::min(nb, n - r0);
-            slate_hip::getrf_panel_ws<double>(mk, wk, buf + r0 + lck * lld, lld, ipiv + r0, infos + k,
-                                              opts.pivot_threshold, false, R.lu_work, ps);
-            Lp = buf + r0 + lck * lld;
-            ldl = lld;
-            if (q > 1)
-                NHIP(hipMemcpy2DAsync(Lbuf->p, mk * 8, Lp, lld * 8, mk * 8, kb, hipMemcpyDeviceToDevice, ps));
+    if (p == 1) {
+        // ---- 1 x q: full-height panels on their owner (persistent LU
+        //      panel), lookahead; models/lu.py _getrf_p1
+        std::vector<std::unique_ptr<Event>> ev_tr((size_t)kt), ev_used((size_t)kt);
+        // broadcast panels: a ring of NR buffers, slot k % NR rewritten at
+        // step k only after the update stream finished step k - NR
+        const int NR = la + 3;
+        std::vector<std::unique_ptr<Scratch>> ring;
+        if (q > 1)
+            for (int r = 0; r < NR; ++r) ring.push_back(std::make_unique<Scratch>((size_t)m * nb * sizeof(T), ps));
+        auto update_cols = [&](const T* Lp, i64 ldl, i64 r0, i64 kb, i64 c0, i64 c1, hipStream_t s) {
+            if (c1 <= c0) return;
+            T* cols = buf + c0 * lld;
+            slate_hip::laswp_off<K<T>>(c1 - c0, kp(cols), lld, r0, r0 + kb, ipiv_d, -r0, s);
+            T* Ukk = buf + r0 + c0 * lld;
+            slate_hip::trsm<K<T>>('L', 'L', 'N', 'U', kb, c1 - c0, kv(T(1)), kp(Lp), ldl, kp(Ukk), lld, s);
+            if (m > r0 + kb)
+                gemm_k<T>('N', 'N', m - r0 - kb, c1 - c0, kb, T(-1), Lp + kb, ldl, Ukk, lld, T(1),
+                          buf + r0 + kb + c0 * lld, lld, s);
+        };
+        for (i64 k = 0; k < kt; ++k) {
+            const i64 r0 = k * nb;
+            const i64 kb = std::min({nb, n - r0, m - r0});
+            const i64 mk = m - r0;
+            const bool own = (k % q) == pc;
+            const i64 lck = tiles_before(k, q, pc) * nb;
+            const i64 lc1 = std::min(tiles_before(k + 1, q, pc) * nb, nloc);
+            const i64 lcla = std::min(tiles_before(k + 1 + la, q, pc) * nb, nloc);
+            if (k - la - 1 >= 0) ev_tr[k - la - 1]->wait(ps);
+            if (q > 1 && k >= NR) ev_used[k - NR]->wait(ps);
+            T* Lb = q > 1 ? ring[k % NR]->as<T>() : nullptr;
+            const T* Lp = nullptr;
+            i64 ldl = mk;
+            if (own) {
+                const i64 wk = std::min(nb, n - r0);
+                slate_hip::getrf_panel_ws<K<T>>(mk, wk, kp(buf + r0 + lck * lld), lld, ipiv_d + r0,
+                                                infos.as<i64>() + k, opts.pivot_threshold, false, R.lu_work, ps);
+                Lp = buf + r0 + lck * lld;
+                ldl = lld;
+                if (q > 1) copy2d(Lb, mk, Lp, lld, mk, kb, ps);
+            }
+            if (q > 1) {
+                gc->row->bcast(ipiv_d + r0, (size_t)kb * sizeof(i64), (int)(k % q), ps);
+                gc->row->bcast(Lb, (size_t)mk * kb * sizeof(T), (int)(k % q), ps);
+                Lp = Lb;
+                ldl = mk;
+            }
+            if (k >= 1 && la > 0) ev_tr[k - 1]->wait(ps);
+            update_cols(Lp, ldl, r0, kb, lc1, lcla, ps);
+            Event ev_panel;
+            ev_panel.record(ps);
+            ev_panel.wait(us);
+            const i64 lcnx = std::max(std::min(tiles_before(k + 2 + la, q, pc) * nb, nloc), lcla);
+            update_cols(Lp, ldl, r0, kb, lcla, lcnx, us);
+            ev_tr[k] = std::make_unique<Event>();
+            ev_tr[k]->record(us);
+            update_cols(Lp, ldl, r0, kb, lcnx, nloc, us);
+            if (lck > 0) slate_hip::laswp_off<K<T>>(lck, kp(buf), lld, r0, r0 + kb, ipiv_d, -r0, us);
+            ev_used[k] = std::make_unique<Event>();
+            ev_used[k]->record(us);
         }
-        if (q > 1) {
-            NCCL(ncclBroadcast(ipiv + r0, ipiv + r0, (size_t)kb, ncclInt64, (int)(k % q), gc->row, ps));
-            NCCL(ncclBroadcast(Lbuf->p, Lbuf->p, (size_t)mk * kb, ncclFloat64, (int)(k % q), gc->row, ps));
-            Lp = Lbuf->as<double>();
-            ldl = mk;
+        join(us, ps);
+        for (auto& x : ring) x->s = ps;             // ps has joined the update stream
+    } else {
+        // ---- p > 1: distributed panel (rows on their owners), then per
+        //      step ONE row broadcast of [my panel rows | top block |
+        //      pivots] from the panel's process column, the owner-masked row
+        //      exchange of every trailing column, U rows by a trsm on the top
+        //      block, one GEMM (models/lu.py _getrf_general)
+        Comm* colc = gc->col.get();
+        Comm* rowc = gc->row.get();
+        for (i64 k = 0; k < kt; ++k) {
+            const i64 r0 = k * nb;
+            const i64 kb = std::min({nb, n - r0, m - r0});
+            const int ck = (int)(k % q), rk = (int)(k % p);
+            const i64 lr_k = std::min(tiles_before(k, p, pr) * nb, mloc);
+            const i64 lr1 = (pr == rk) ? std::min(lr_k + kb, mloc) : lr_k;
+            const i64 lck = std::min(tiles_before(k, q, pc) * nb, nloc);
+            const i64 lc1 = std::min(tiles_before(k + 1, q, pc) * nb, nloc);
+            const i64 nmine = mloc - lr_k;
+            // pack = [L rows (nmine x kb) | T (kb x kb) | pivots (kb)]
+            const size_t lbytes = (size_t)std::max<i64>(nmine, 0) * kb * sizeof(T);
+            const size_t tbytes = (size_t)kb * kb * sizeof(T);
+            Scratch pack(lbytes + tbytes + (size_t)kb * sizeof(i64) + 64, ps);
+            T* Lp = pack.as<T>();
+            T* Tt = reinterpret_cast<T*>(static_cast<char*>(pack.p) + lbytes);
+            i64* pv = reinterpret_cast<i64*>(static_cast<char*>(pack.p) + lbytes + tbytes);
+            if (pc == ck) {
+                panel_dist<T>(S, k, kb, lck, ipiv_d, infos.as<i64>() + k, opts.pivot_threshold,
+                              opts.inner_blocking, Tt, ps);
+                copy2d(Lp, std::max<i64>(nmine, 1), buf + lr_k + lck * lld, lld, nmine, kb, ps);
+                NHIP(hipMemcpyAsync(pv, ipiv_d + r0, (size_t)kb * sizeof(i64), hipMemcpyDeviceToDevice, ps));
+            }
+            if (q > 1) rowc->bcast(pack.p, lbytes + tbytes + (size_t)kb * sizeof(i64), ck, ps);
+            NHIP(hipMemcpyAsync(ipiv_d + r0, pv, (size_t)kb * sizeof(i64), hipMemcpyDeviceToDevice, ps));
+            // every local column except the panel's own: interchanges, then
+            // (trailing columns) U rows and the update
+            auto trailing = [&](i64 c0, i64 c1) {
+                if (c1 <= c0) return;
+                Scratch plan(slate_hip::swap_plan_bytes(), ps);
+                slate_hip::swap_plan(r0, r0 + kb, ipiv_d, -r0, 1, plan.p, ps);
+                const i64 S2 = 2 * kb, w = c1 - c0;
+                Scratch X((size_t)S2 * w * sizeof(T), ps);
+                T* cols = buf + c0 * lld;
+                slate_hip::xchg_gather<K<T>>(plan.p, S2, w, kp(cols), lld, kp(X.as<T>()), S2, nb, p, pr, ps);
+                colc->allreduce(X.p, (size_t)S2 * w, dt_of<T>::v, 's', ps);
+                slate_hip::xchg_scatter<K<T>>(plan.p, S2, w, kp(X.as<T>()), S2, kp(cols), lld, nb, p, pr, ps);
+                if (c0 >= lc1) {
+                    T* U = X.as<T>();
+                    slate_hip::trsm<K<T>>('L', 'L', 'N', 'U', kb, w, kv(T(1)), kp(Tt), kb, kp(U), S2, ps);
+                    if (pr == rk) copy2d(buf + lr_k + c0 * lld, lld, U, S2, kb, w, ps);
+                    if (mloc > lr1)
+                        gemm_k<T>('N', 'N', mloc - lr1, w, kb, T(-1), Lp + (lr1 - lr_k), std::max<i64>(nmine, 1), U,
+                                  S2, T(1), buf + lr1 + c0 * lld, lld, ps);
+                }
+            };
+            trailing(lc1, nloc);            // the trailing columns
+            trailing(0, lck);               // the factored columns on the left
         }
-        if (k >= 1 && la > 0) ev_tr[k - 1]->wait(ps);
-        update_cols(Lp, ldl, r0, kb, lc1, lcla, ps);
-        Event ev_panel;
-        ev_panel.record(ps);
-        ev_panel.wait(us);
-        const i64 lcnx = std::max(std::min(tiles_before(k + 2 + la, q, pc) * nb, nloc), lcla);
-        update_cols(Lp, ldl, r0, kb, lcla, lcnx, us);
-        ev_tr[k] = std::make_unique<Event>();
-        ev_tr[k]->record(us);
-        update_cols(Lp, ldl, r0, kb, lcnx, nloc, us);
-        if (lck > 0) slate_hip::laswp_off<double>(lck, buf, lld, r0, r0 + kb, ipiv, -r0, us);
-        Lbuf->s = us;
-        join(ps, us);
+        (void)la;
     }
     join(ps, R.main);
     join(us, R.main);
     std::vector<i64> h((size_t)std::max<i64>(kmin, 1));
-    NHIP(hipMemcpyAsync(h.data(), ipiv, h.size() * sizeof(i64), hipMemcpyDeviceToHost, R.main));
-    const int64_t info = read_infos(infos, kt, R.main, nb);
-    NHIP(hipFreeAsync(ipiv, R.main));
-    NHIP(hipFreeAsync(infos, R.main));
-    NHIP(hipStreamSynchronize(R.main));
+    NHIP(hipMemcpyAsync(h.data(), ipiv_d, h.size() * sizeof(i64), hipMemcpyDeviceToHost, R.main));
+    const int64_t info = read_infos(infos.as<i64>(), kt, R.main, nb);
     ipiv_out.assign((size_t)kmin, 0);
     for (i64 i = 0; i < kmin; ++i) ipiv_out[i] = h[i] + (i / nb) * nb;   // panel-relative -> global
     return reduce_info(info);
 }
 
-int64_t getrs(const Matrix<double>& A, const std::vector<int64_t>& ipiv, Matrix<double>& B, const Options&) {
-    const Storage& S = *A.storage();
-    Storage& T = *B.storage();
-    require_1x1(S, "getrs");
-    require_1x1(T, "getrs");
-    hipStream_t s = rt().main;
+// op(A) = P L U: NoTrans X = U^{-1} L^{-1} P^T B; ConjTrans X = P L^{-H}
+// U^{-H} B (the interchanges applied backwards at the end)
+template <typename T>
+int64_t getrs(Op trans, const Matrix<T>& A, const std::vector<int64_t>& ipiv, Matrix<T>& B, const Options& opts) {
+    Storage& SB = *B.storage();
+    Runtime& R = rt();
+    hipStream_t s = R.main;
+    if (trans == Op::Trans && is_cplx<T>()) throw Error("native getrs: Trans of a complex matrix (use ConjTrans)");
     const i64 k = (i64)ipiv.size();
-    i64* d = nullptr;
-    NHIP(hipMallocAsync(&d, sizeof(i64) * std::max<i64>(k, 1), s));
-    NHIP(hipMemcpyAsync(d, ipiv.data(), sizeof(i64) * k, hipMemcpyHostToDevice, s));
-    double* X = static_cast<double*>(T.buf);
-    slate_hip::laswp_off<double>(T.n, X, T.lld, 0, k, d, 0, s);
-    const double* F = static_cast<const double*>(S.buf);
-    slate_hip::trsm<double>('L', 'L', 'N', 'U', S.n, T.n, 1.0, F, S.lld, X, T.lld, s);
-    slate_hip::trsm<double>('L', 'U', 'N', 'N', S.n, T.n, 1.0, F, S.lld, X, T.lld, s);
-    NHIP(hipFreeAsync(d, s));
-    NHIP(hipStreamSynchronize(s));
+    Scratch d(sizeof(i64) * std::max<i64>(k, 1), s);
+    NHIP(hipMemcpyAsync(d.p, ipiv.data(), sizeof(i64) * k, hipMemcpyHostToDevice, s));
+    Comm* colc = SB.gc->col.get();
+    if (trans == Op::NoTrans) {
+        permute_rows_dist<T>(SB, d.as<i64>(), 0, k, 0, SB.nloc, 1, s, colc);
+        NHIP(hipStreamSynchronize(s));
+        trsm<T>(Side::Left, Uplo::Lower, Op::NoTrans, Diag::Unit, T(1), A, B, opts);
+        trsm<T>(Side::Left, Uplo::Upper, Op::NoTrans, Diag::NonUnit, T(1), A, B, opts);
+    } else {
+        trsm<T>(Side::Left, Uplo::Upper, Op::ConjTrans, Diag::NonUnit, T(1), A, B, opts);
+        trsm<T>(Side::Left, Uplo::Lower, Op::ConjTrans, Diag::Unit, T(1), A, B, opts);
+        permute_rows_dist<T>(SB, d.as<i64>(), 0, k, 0, SB.nloc, -1, s, colc);
+        NHIP(hipStreamSynchronize(s));
+    }
     return 0;
 }
 
-int64_t gesv(Matrix<double>& A, std::vector<int64_t>& ipiv, Matrix<double>& B, const Options& opts) {
+template <typename T>
+int64_t getrs(const Matrix<T>& A, const std::vector<int64_t>& ipiv, Matrix<T>& B, const Options& opts) {
+    return getrs<T>(Op::NoTrans, A, ipiv, B, opts);
+}
+
+template <typename T>
+int64_t gesv(Matrix<T>& A, std::vector<int64_t>& ipiv, Matrix<T>& B, const Options& opts) {
     const int64_t info = getrf(A, ipiv, opts);
     if (info == 0) getrs(A, ipiv, B, opts);
     return info;
 }
 
 // ------------------------------------------------------------ gemm (SUMMA)
-void gemm(double alpha, const Matrix<double>& A, const Matrix<double>& B, double beta, Matrix<double>& C,
-          const Options&) {
+// C = alpha A B + beta C: per k the A(:, k) block of this process row
+// (row broadcast) and the B(k, :) block of this process column (column
+// broadcast) -- issued on the comm stream ONE step ahead of the GEMM on the
+// panel stream (double buffers, events): the broadcasts of step k+1 travel
+// while GEMM k runs (SLATE gemmC's lookahead, src/gemmC.cc:104-170)
+template <typename T>
+void gemm(T alpha, const Matrix<T>& A, const Matrix<T>& B, T beta, Matrix<T>& C, const Options& opts) {
     const Storage& SA = *A.storage();
     const Storage& SB = *B.storage();
     Storage& SC = *C.storage();
@@ -799,67 +1094,102 @@ void gemm(double alpha, const Matrix<double>& A, const Matrix<double>& B, double
     if (SA.nb != SB.nb || SA.nb != SC.nb || SA.p != SC.p || SA.q != SC.q || SB.p != SC.p || SB.q != SC.q)
         throw Error("native gemm: A, B, C must share the grid and the tile size");
     Runtime& R = rt();
-    hipStream_t s = R.panel;
+    hipStream_t s = R.panel, cs = R.comm;
     join(R.main, s);
-    const i64 nb = SA.nb, K = SA.n;
+    join(R.main, cs);
+    const i64 nb = SA.nb, Kd = SA.n;
     const int p = SC.p, q = SC.q, pr = SC.pr, pc = SC.pc;
     GridComms* gc = SC.gc;
-    double* Cl = static_cast<double*>(SC.buf);
-    const double* Al = static_cast<const double*>(SA.buf);
-    const double* Bl = static_cast<const double*>(SB.buf);
+    T* Cl = static_cast<T*>(SC.buf);
+    const T* Al = static_cast<const T*>(SA.buf);
+    const T* Bl = static_cast<const T*>(SB.buf);
     if (p == 1 && q == 1) {
-        gemm_d('N', 'N', SC.m, SC.n, K, alpha, Al, SA.lld, Bl, SB.lld, beta, Cl, SC.lld, s);
+        gemm_k<T>('N', 'N', SC.m, SC.n, Kd, alpha, Al, SA.lld, Bl, SB.lld, beta, Cl, SC.lld, s);
     } else {
-        const i64 kt = (K + nb - 1) / nb;
-        for (i64 k = 0; k < kt; ++k) {
-            const i64 kb = std::min(nb, K - k * nb);
-            // A(:, k): this process row's rows, from process column k % q
-            Scratch Ak((size_t)std::max<i64>(SA.mloc, 1) * kb * 8, s);
-            if ((int)(k % q) == pc && SA.mloc)
-                NHIP(hipMemcpy2DAsync(Ak.p, SA.mloc * 8, Al + tiles_before(k, q, pc) * nb * SA.lld, SA.lld * 8,
-                                      SA.mloc * 8, kb, hipMemcpyDeviceToDevice, s));
-            if (q > 1 && SA.mloc)
-                NCCL(ncclBroadcast(Ak.p, Ak.p, (size_t)SA.mloc * kb, ncclFloat64, (int)(k % q), gc->row, s));
-            // B(k, :): this process column's columns, from process row k % p
-            Scratch Bk((size_t)kb * std::max<i64>(SB.nloc, 1) * 8, s);
-            if ((int)(k % p) == pr && SB.nloc)
-                NHIP(hipMemcpy2DAsync(Bk.p, kb * 8, Bl + tiles_before(k, p, pr) * nb, SB.lld * 8, kb * 8, SB.nloc,
-                                      hipMemcpyDeviceToDevice, s));
-            if (p > 1 && SB.nloc)
-                NCCL(ncclBroadcast(Bk.p, Bk.p, (size_t)kb * SB.nloc, ncclFloat64, (int)(k % p), gc->col, s));
-            gemm_d('N', 'N', SC.mloc, SC.nloc, kb, alpha, Ak.as<double>(), std::max<i64>(SA.mloc, 1),
-                   Bk.as<double>(), kb, k == 0 ? beta : 1.0, Cl, SC.lld, s);
+        const i64 kt = (Kd + nb - 1) / nb;
+        const int la = std::max(1, opts.lookahead);
+        const i64 ma = std::max<i64>(SA.mloc, 1), nbl = std::max<i64>(SB.nloc, 1);
+        const int nbuf = la + 1;
+        std::vector<std::unique_ptr<Scratch>> Ab, Bb;
+        for (int b = 0; b < nbuf; ++b) {
+            Ab.push_back(std::make_unique<Scratch>((size_t)ma * nb * sizeof(T), s));
+            Bb.push_back(std::make_unique<Scratch>((size_t)nb * nbl * sizeof(T), s));
         }
-        if (kt == 0 && beta != 1.0)
-            slate_hip::gescale<double>('G', SC.mloc, SC.nloc, beta, Cl, SC.lld, s);
+        join(s, cs);                          // the buffers exist before the comm stream fills them
+        std::vector<std::unique_ptr<Event>> ready((size_t)kt), used((size_t)kt);
+        auto issue = [&](i64 k) {
+            const int b = (int)(k % nbuf);
+            const i64 kb = std::min(nb, Kd - k * nb);
+            if (k >= nbuf) used[k - nbuf]->wait(cs);          // buffer b free again
+            if ((int)(k % q) == pc && SA.mloc)
+                copy2d(Ab[b]->as<T>(), ma, Al + tiles_before(k, q, pc) * nb * SA.lld, SA.lld, SA.mloc, kb, cs);
+            if (q > 1 && SA.mloc) gc->row->bcast(Ab[b]->p, (size_t)ma * kb * sizeof(T), (int)(k % q), cs);
+            if ((int)(k % p) == pr && SB.nloc)
+                copy2d(Bb[b]->as<T>(), kb, Bl + tiles_before(k, p, pr) * nb, SB.lld, kb, SB.nloc, cs);
+            if (p > 1 && SB.nloc) gc->col->bcast(Bb[b]->p, (size_t)kb * SB.nloc * sizeof(T), (int)(k % p), cs);
+            ready[k] = std::make_unique<Event>();
+            ready[k]->record(cs);
+        };
+        for (i64 k = 0; k < std::min<i64>(kt, la); ++k) issue(k);
+        for (i64 k = 0; k < kt; ++k) {
+            if (k + la < kt) issue(k + la);
+            const int b = (int)(k % nbuf);
+            const i64 kb = std::min(nb, Kd - k * nb);
+            ready[k]->wait(s);
+            gemm_k<T>('N', 'N', SC.mloc, SC.nloc, kb, alpha, Ab[b]->as<T>(), ma, Bb[b]->as<T>(), kb,
+                      k == 0 ? beta : T(1), Cl, SC.lld, s);
+            used[k] = std::make_unique<Event>();
+            used[k]->record(s);
+        }
+        if (kt == 0 && beta != T(1))
+            slate_hip::gescale<K<T>>('G', SC.mloc, SC.nloc, kv(beta), kp(Cl), SC.lld, s);
+        for (auto& x : Ab) x->s = s;
+        for (auto& x : Bb) x->s = s;
+        join(cs, s);
     }
     NHIP(hipStreamSynchronize(s));
 }
 
+template <typename T>
+void gemm(Op opA, Op opB, T alpha, const Matrix<T>& A, const Matrix<T>& B, T beta, Matrix<T>& C,
+          const Options& opts) {
+    auto materialise = [](Op op, const Matrix<T>& X) -> Matrix<T> {
+        if (op == Op::NoTrans) return X;
+        const Storage& S = *X.storage();
+        Matrix<T> Y(S.n, S.m, S.nb, S.p, S.q);
+        copy<T>(op, X, Y);
+        return Y;
+    };
+    const Matrix<T> Ao = materialise(opA, A);
+    const Matrix<T> Bo = materialise(opB, B);
+    gemm<T>(alpha, Ao, Bo, beta, C, opts);
+}
+
 // ------------------------------------------------------------ norm
-double norm(Norm kind, const Matrix<double>& A) {
+template <typename T>
+double norm(Norm kind, const Matrix<T>& A) {
+    using Rl = decltype(std::real(T()));
     const Storage& S = *A.storage();
     Runtime& R = rt();
     hipStream_t s = R.main;
     const char k = (char)kind;
     const i64 nout = (k == 'F' ? 2 * S.nloc : S.nloc) + S.mloc;
-    double* out = nullptr;
-    NHIP(hipMallocAsync(&out, sizeof(double) * std::max<i64>(nout, 1), s));
-    NHIP(hipMemsetAsync(out, 0, sizeof(double) * std::max<i64>(nout, 1), s));
-    slate_hip::genorm<double, double>(k, 'G', 'N', 0, S.mloc, S.nloc, static_cast<const double*>(S.buf), S.lld, out,
-                                      s);
-    std::vector<double> h((size_t)std::max<i64>(nout, 1));
-    NHIP(hipMemcpyAsync(h.data(), out, sizeof(double) * h.size(), hipMemcpyDeviceToHost, s));
-    NHIP(hipFreeAsync(out, s));
+    Scratch out(sizeof(Rl) * std::max<i64>(nout, 1), s);
+    NHIP(hipMemsetAsync(out.p, 0, sizeof(Rl) * std::max<i64>(nout, 1), s));
+    slate_hip::genorm<K<T>, Rl>(k, 'G', 'N', 0, S.mloc, S.nloc, kp(static_cast<const T*>(S.buf)), S.lld,
+                                out.as<Rl>(), s);
+    std::vector<Rl> hr((size_t)std::max<i64>(nout, 1));
+    NHIP(hipMemcpyAsync(hr.data(), out.p, sizeof(Rl) * hr.size(), hipMemcpyDeviceToHost, s));
     NHIP(hipStreamSynchronize(s));
+    std::vector<double> h(hr.begin(), hr.end());
     // global vectors for one / inf norms, scalars for max / fro
     std::vector<double> v;
-    ncclRedOp_t op = ncclSum;
+    char op = 's';
     if (k == 'M') {
         double mx = 0;
         for (i64 j = 0; j < S.nloc; ++j) mx = (h[j] != h[j] || h[j] > mx) ? h[j] : mx;
         v = {mx};
-        op = ncclMax;
+        op = 'M';
     } else if (k == '1') {
         v.assign((size_t)S.n, 0.0);
         for (i64 j = 0; j < S.nloc; ++j) v[l2g(j, S.nb, S.q, S.pc)] = h[j];
@@ -878,12 +1208,10 @@ double norm(Norm kind, const Matrix<double>& A) {
         v = {scale * scale * sumsq};
     }
     if (R.size > 1 && !v.empty()) {
-        double* d = nullptr;
-        NHIP(hipMallocAsync(&d, sizeof(double) * v.size(), s));
-        NHIP(hipMemcpyAsync(d, v.data(), sizeof(double) * v.size(), hipMemcpyHostToDevice, s));
-        NCCL(ncclAllReduce(d, d, v.size(), ncclFloat64, op, R.world, s));
-        NHIP(hipMemcpyAsync(v.data(), d, sizeof(double) * v.size(), hipMemcpyDeviceToHost, s));
-        NHIP(hipFreeAsync(d, s));
+        Scratch d(sizeof(double) * v.size(), s);
+        NHIP(hipMemcpyAsync(d.p, v.data(), sizeof(double) * v.size(), hipMemcpyHostToDevice, s));
+        world_comm()->allreduce(d.p, v.size(), DT::F64, op, s);
+        NHIP(hipMemcpyAsync(v.data(), d.p, sizeof(double) * v.size(), hipMemcpyDeviceToHost, s));
         NHIP(hipStreamSynchronize(s));
     }
     if (k == 'F') return std::sqrt(v[0]);
@@ -891,6 +1219,27 @@ double norm(Norm kind, const Matrix<double>& A) {
     for (double x : v) r = (x != x || x > r) ? x : r;
     return r;
 }
+
+// ------------------------------------------------------------ instantiation
+#define SLATE_NATIVE_INST(T)                                                                                   \
+    template class Matrix<T>;                                                                                   \
+    template int64_t potrf<T>(HermitianMatrix<T>&, const Options&);                                            \
+    template int64_t potrs<T>(const HermitianMatrix<T>&, Matrix<T>&, const Options&);                          \
+    template int64_t posv<T>(HermitianMatrix<T>&, Matrix<T>&, const Options&);                                 \
+    template int64_t getrf<T>(Matrix<T>&, std::vector<int64_t>&, const Options&);                              \
+    template int64_t getrs<T>(const Matrix<T>&, const std::vector<int64_t>&, Matrix<T>&, const Options&);      \
+    template int64_t getrs<T>(Op, const Matrix<T>&, const std::vector<int64_t>&, Matrix<T>&, const Options&);  \
+    template int64_t gesv<T>(Matrix<T>&, std::vector<int64_t>&, Matrix<T>&, const Options&);                   \
+    template void gemm<T>(T, const Matrix<T>&, const Matrix<T>&, T, Matrix<T>&, const Options&);               \
+    template void gemm<T>(Op, Op, T, const Matrix<T>&, const Matrix<T>&, T, Matrix<T>&, const Options&);       \
+    template void copy<T>(Op, const Matrix<T>&, Matrix<T>&);                                                   \
+    template void trsm<T>(Side, Uplo, Op, Diag, T, const Matrix<T>&, Matrix<T>&, const Options&);              \
+    template double norm<T>(Norm, const Matrix<T>&);
+SLATE_NATIVE_INST(float)
+SLATE_NATIVE_INST(double)
+SLATE_NATIVE_INST(std::complex<float>)
+SLATE_NATIVE_INST(std::complex<double>)
+#undef SLATE_NATIVE_INST
 
 }  // namespace native
 }  // namespace slate_amd

@@ -1,0 +1,175 @@
+// Internal header of the native (Python-free) runtime: process runtime,
+// communicator transports, distributed storage and small helpers shared by
+// native.hip (drivers), native_comm.hip (transports) and capi_native.hip
+// (C / LAPACK / ScaLAPACK / BLACS ABI).  Not installed.
+#pragma once
+#include <complex>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+#include "../hip/common.hpp"
+#include "slate_amd/slate_native.hh"
+
+namespace slate_amd {
+namespace native {
+
+using slate_hip::i64;
+
+#define NHIP(x)                                                                                          \
+    do {                                                                                                 \
+        hipError_t e_ = (x);                                                                             \
+        if (e_ != hipSuccess) throw ::slate_amd::native::Error(std::string("HIP: ") + hipGetErrorString(e_) + " at " #x);     \
+    } while (0)
+
+// ------------------------------------------------------------ transports
+// A communicator over a subset of the world ranks.  Two implementations:
+//   * RCCL (ncclComm_t, ncclCommSplit for sub-communicators): stream-ordered,
+//     device buffers, one hop over xGMI -- the production transport;
+//   * host-staged TCP (every rank connected to every other at start-up): the
+//     stream is synchronised, buffers go device -> host -> socket -> host ->
+//     device.  It lets several ranks share ONE GPU (RCCL refuses that), so
+//     the p x q drivers run on a one-GPU box (tests) and on machines without
+//     RCCL peers.  SLATE_AMD_NATIVE_TRANSPORT = rccl | host.
+enum class DT : int { F32 = 0, F64 = 1, C32 = 2, C64 = 3, I64 = 4, U8 = 5 };
+inline size_t dt_size(DT d) {
+    switch (d) {
+        case DT::F32: return 4;
+        case DT::F64: return 8;
+        case DT::C32: return 8;
+        case DT::C64: return 16;
+        case DT::I64: return 8;
+        default: return 1;
+    }
+}
+template <typename T> struct dt_of;
+template <> struct dt_of<float> { static constexpr DT v = DT::F32; };
+template <> struct dt_of<double> { static constexpr DT v = DT::F64; };
+template <> struct dt_of<std::complex<float>> { static constexpr DT v = DT::C32; };
+template <> struct dt_of<std::complex<double>> { static constexpr DT v = DT::C64; };
+template <> struct dt_of<int64_t> { static constexpr DT v = DT::I64; };
+
+struct P2P {                       // one point-to-point transfer of a batch
+    bool send;
+    int peer;                      // rank inside the communicator
+    void* buf;                     // device pointer
+    size_t bytes;
+};
+
+class Comm {
+public:
+    int size = 1, rank = 0;
+    std::vector<int> world;        // world rank of each member
+    virtual ~Comm() = default;
+    // all stream-ordered from the caller's point of view (the host transport
+    // synchronises s first and returns with the result in place)
+    virtual void bcast(void* buf, size_t bytes, int root, hipStream_t s) = 0;
+    // op: 's' sum, 'M' max, 'm' min (max / min: real types only)
+    virtual void allreduce(void* buf, size_t count, DT dt, char op, hipStream_t s) = 0;
+    // recv = size blocks of `bytes`, block r from member r
+    virtual void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
+    virtual void exchange(const std::vector<P2P>& ops, hipStream_t s) = 0;
+    // members of this communicator with colour == mine, ordered by key
+    virtual std::unique_ptr<Comm> split(int colour, int key) = 0;
+};
+
+// the world communicator of the selected transport (nullptr: one rank)
+Comm* world_comm();
+void transport_init(int rank, int size);
+void transport_finalize();
+const char* transport_name();
+
+// ------------------------------------------------------------ runtime
+struct GridComms {
+    int p = 1, q = 1, pr = 0, pc = 0;
+    std::unique_ptr<Comm> row;     // same process row, ranked by pc
+    std::unique_ptr<Comm> col;     // same process column, ranked by pr
+};
+
+struct Runtime {
+    bool up = false;
+    int rank = 0, size = 1, local = 0, device = 0;
+    hipStream_t main = nullptr, panel = nullptr, update = nullptr, update_masked = nullptr, comm = nullptr;
+    void* lu_work = nullptr;
+    std::map<std::pair<int, int>, std::unique_ptr<GridComms>> grids;
+    std::mutex mu;
+};
+Runtime& rt();
+GridComms* grid_comms(int p, int q);
+
+// ------------------------------------------------------------ storage
+struct Storage {
+    i64 m = 0, n = 0, nb = 1;
+    int p = 1, q = 1, pr = 0, pc = 0;
+    i64 mloc = 0, nloc = 0, lld = 1;
+    size_t esize = 8;
+    void* buf = nullptr;
+    bool owns = true;
+    GridComms* gc = nullptr;
+    ~Storage() {
+        if (buf && owns) (void)hipFree(buf);
+    }
+};
+
+inline i64 numroc(i64 n, i64 nb, int iproc, int nprocs) {
+    const i64 nblocks = n / nb;
+    i64 num = (nblocks / nprocs) * nb;
+    const i64 extra = nblocks % nprocs;
+    if (iproc < extra) num += nb;
+    else if (iproc == extra) num += n % nb;
+    return num;
+}
+inline i64 l2g(i64 l, i64 nb, int p, int pr) { return ((l / nb) * p + pr) * nb + l % nb; }
+inline i64 tiles_before(i64 t, int p, int pr) { return t > pr ? (t - pr + p - 1) / p : 0; }
+
+// kernel element type of an API type
+template <typename T> struct kt_of { using type = T; };
+template <> struct kt_of<std::complex<float>> { using type = slate_hip::ccplx; };
+template <> struct kt_of<std::complex<double>> { using type = slate_hip::zcplx; };
+template <typename T> using K = typename kt_of<T>::type;
+template <typename T> inline K<T>* kp(T* p) { return reinterpret_cast<K<T>*>(p); }
+template <typename T> inline const K<T>* kp(const T* p) { return reinterpret_cast<const K<T>*>(p); }
+template <typename T> inline K<T> kv(T v) {
+    K<T> r;
+    std::memcpy(&r, &v, sizeof(T));
+    return r;
+}
+template <typename T> constexpr bool is_cplx() { return !std::is_same<T, float>::value && !std::is_same<T, double>::value; }
+template <typename T> constexpr char ctrans() { return is_cplx<T>() ? 'C' : 'T'; }
+
+// ------------------------------------------------------------ small RAII
+struct Event {
+    hipEvent_t e = nullptr;
+    Event() { NHIP(hipEventCreateWithFlags(&e, hipEventDisableTiming)); }
+    ~Event() { if (e) (void)hipEventDestroy(e); }
+    Event(const Event&) = delete;
+    void record(hipStream_t s) { NHIP(hipEventRecord(e, s)); }
+    void wait(hipStream_t s) const { NHIP(hipStreamWaitEvent(s, e, 0)); }
+};
+
+// stream b waits for everything issued so far on stream a
+inline void join(hipStream_t a, hipStream_t b) {
+    Event ev;
+    ev.record(a);
+    ev.wait(b);
+}
+
+// device scratch freed after the owning stream reaches it (stream-ordered)
+struct Scratch {
+    void* p = nullptr;
+    hipStream_t s = nullptr;
+    Scratch(size_t bytes, hipStream_t st) : s(st) { if (bytes) NHIP(hipMallocAsync(&p, bytes, st)); }
+    ~Scratch() { if (p) (void)hipFreeAsync(p, s); }
+    Scratch(const Scratch&) = delete;
+    template <typename T> T* as() { return static_cast<T*>(p); }
+};
+
+}  // namespace native
+}  // namespace slate_amd
