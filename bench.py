@@ -155,6 +155,63 @@ def _residual(args, A, A0, piv, comm, extra=None):
     return float(f"{float(r):.3e}")
 
 
+def _main_native(args):
+    """bench.py --impl native: the same step / timing / JSON contract through
+    libslate_amd_native.so.  This process never touches the GPU; it starts
+    slate_amd/bench_native as a child with the same RANK / WORLD_SIZE /
+    MASTER_* environment (the native runtime bootstraps RCCL itself on
+    MASTER_PORT + 1) and rank 0 prints the JSON line."""
+    import re
+    import subprocess
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.routine not in ("potrf", "getrf", "gemm"):
+        raise SystemExit("--impl native: potrf, getrf or gemm")
+    p, q = grid_for(world, args.routine) if args.grid is None else map(int, args.grid.lower().split("x"))
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "slate_amd", "bench_native")
+    cmd = [exe, args.routine, str(args.n), str(args.nb), str(p), str(q), str(args.lookahead), str(args.warmup),
+           str(args.steps), str(args.check)]
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        print(r.stdout, file=sys.stderr, flush=True)
+        raise SystemExit(r.returncode)
+    if rank != 0:
+        return
+    m = re.search(r"RESULT ms_per_step=(\S+) info=(\S+) resid=(\S+) transport=(\S+)", r.stdout)
+    ms, info, resid, transport = float(m.group(1)), int(m.group(2)), float(m.group(3)), m.group(4)
+    fl = flops(args.routine, args.n)
+    gflops = fl / (ms * 1e-3) / 1e9
+    tol = 3 * 2.0 ** -52
+    resid = resid if args.check else None
+    out = {
+        "metric": f"d{args.routine} GFLOP/s (n={args.n}, nb={args.nb})",
+        "value": round(gflops, 2),
+        "unit": "GFLOP/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "fp64",
+        "data": "synthetic (Philox SPD/rand matrix generated on device)",
+        "impl": f"native C++ library (libslate_amd_native.so, transport {transport})",
+        "pct_fp64_peak": round(100 * gflops / 1e3 / (FP64_PEAK_TF * world), 2),
+        "info_ok": info == 0,
+        "residual": resid,
+        "residual_ok": None if resid is None else bool(resid <= tol),
+        "config": {"model": f"d{args.routine} n={args.n} nb={args.nb}", "global_batch": 1, "seq_len": args.n,
+                   "n": args.n, "nb": args.nb, "grid": f"{p}x{q}", "lookahead": args.lookahead,
+                   "parallelism": f"2d-block-cyclic {p}x{q}"},
+    }
+    print(json.dumps(out), flush=True)
+    if info != 0 or (resid is not None and not resid <= tol):
+        print(f"bench: FAILED correctness check (info={info}, residual={resid}, tol={tol:.2e})",
+              file=sys.stderr, flush=True)
+        sys.exit(1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -172,7 +229,11 @@ def main():
     ap.add_argument("--method", default="pp", choices=["pp", "calu", "nopiv"], help="getrf: pivoting method")
     ap.add_argument("--grid", default=None, help="PxQ override")
     ap.add_argument("--check", type=int, default=1, help="residual check after timing (0 = skip)")
+    ap.add_argument("--impl", default="python", choices=["python", "native"],
+                    help="native: the Python-free C++ library (slate_amd/bench_native, one child per rank)")
     args = ap.parse_args()
+    if args.impl == "native":
+        return _main_native(args)
     # No GPU_MAX_HW_QUEUES override: a process drives the panel, diag and
     # update streams plus the caller's -- the box default of 4 hardware
     # queues.  RCCL adds none: torch runs every synchronous collective on

@@ -92,7 +92,8 @@ void run(int p, int q, int me) {
         if (me == 0) std::printf("check %s_%s %.3e\n", what, x, v);
         std::fflush(stdout);
     };
-    const int64_t n = 300, nb = 32, nrhs = 5;
+    const int64_t n = std::getenv("EX_NATIVE_N") ? std::atoll(std::getenv("EX_NATIVE_N")) : 300;
+    const int64_t nb = std::getenv("EX_NATIVE_NB") ? std::atoll(std::getenv("EX_NATIVE_NB")) : 32, nrhs = 5;
 
     // ---- potrf / posv: || L L^H - A || / || A ||, || A X - B || / || B ||
     sn::HermitianMatrix<T> A(sn::Uplo::Lower, n, nb, p, q);

@@ -62,6 +62,8 @@ int rank();
 int size();
 const char* version();
 const char* transport();      // "none" (one rank), "rccl" or "host"
+void barrier();               // all ranks, device work of this rank completed
+double allreduce_max(double v);   // maximum over all ranks
 
 struct Options {
     int lookahead = 1;        // SLATE Option::Lookahead

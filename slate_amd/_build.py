@@ -143,18 +143,20 @@ def build(verbose=False, hip=True, host=True):
             extra_deps=glob.glob(os.path.join(ROOT, "include", "slate_amd", "*.hh"))
             + glob.glob(os.path.join(HERE, "csrc", "hip", "*.hpp"))))
         out.append(_build_native_example(verbose))
+        out.append(_build_native_example(verbose, "bench_native"))
         out.append(_build_native_c_example(verbose))
     return out
 
 
-def _build_native_example(verbose=False):
-    """examples/cpp/ex_native.cc -> slate_amd/ex_native: a plain g++ C++17
+def _build_native_example(verbose=False, name="ex_native"):
+    """examples/cpp/<name>.cc -> slate_amd/<name>: a plain g++ C++17
     program against include/slate_amd/slate_native.hh and
     libslate_amd_native.so (rpath $ORIGIN), no Python.  Built in-tree next
-    to the library so it travels to the GPU box with the snapshot."""
-    src = os.path.join(ROOT, "examples", "cpp", "ex_native.cc")
+    to the library so it travels to the GPU box with the snapshot
+    (ex_native: the example / tests; bench_native: bench.py --impl native)."""
+    src = os.path.join(ROOT, "examples", "cpp", name + ".cc")
     lib = os.path.join(HERE, "libslate_amd_native.so")
-    target = os.path.join(HERE, "ex_native")
+    target = os.path.join(HERE, name)
     hdr = os.path.join(ROOT, "include", "slate_amd", "slate_native.hh")
     if _newer(target, [src, lib, hdr]):
         cmd = ["g++", "-O2", "-std=c++17", "-I" + os.path.join(ROOT, "include"), src, "-o", target,

@@ -353,17 +353,6 @@ const Ctx& ctx_of(int ctxt) {
     return c[ctxt];
 }
 
-// device-to-device local copy on the runtime's main stream, completed on
-// return (a null-stream D2D hipMemcpy is not ordered against the drivers'
-// non-blocking streams)
-template <typename T>
-void dev_copy(T* dst, i64 ldd, const T* src, i64 lds, i64 m, i64 n) {
-    if (m > 0 && n > 0)
-        NHIP(hipMemcpy2DAsync(dst, ldd * sizeof(T), src, lds * sizeof(T), m * sizeof(T), n, hipMemcpyDeviceToDevice,
-                              sn::rt().main));
-    NHIP(hipStreamSynchronize(sn::rt().main));
-}
-
 // a native matrix over a ScaLAPACK operand: whole matrix only
 template <typename T>
 sn::Matrix<T> scal_matrix(const int* desc, i64 m, i64 n, int ia, int ja, const T* a) {
@@ -386,8 +375,7 @@ template <typename T>
 sn::HermitianMatrix<T> scal_herm(const int* desc, i64 n, int ia, int ja, const T* a) {
     sn::Matrix<T> G = scal_matrix<T>(desc, n, n, ia, ja, a);
     sn::HermitianMatrix<T> H(sn::Uplo::Lower, n, G.nb(), G.p(), G.q());
-    if (H.mloc() && H.nloc())
-        dev_copy(H.data(), H.lld(), G.data(), G.lld(), H.mloc(), H.nloc());
+    sn::copy(sn::Op::NoTrans, G, H);
     return H;
 }
 
@@ -432,7 +420,7 @@ int p_potrf(char uplo, int n, T* a, int ia, int ja, const int* desca) {
             sn::Matrix<T> U = scal_matrix<T>(desca, n, n, ia, ja, a);
             sn::Matrix<T> Lg(n, n, A.nb(), A.p(), A.q());
             sn::copy(sn::Op::ConjTrans, U, Lg);
-            dev_copy(A.data(), A.lld(), Lg.data(), Lg.lld(), A.mloc(), A.nloc());
+            sn::copy(sn::Op::NoTrans, Lg, A);
             const int64_t info = sn::potrf(A);
             sn::copy(sn::Op::ConjTrans, A, U);
             // only the upper triangle of the caller's array changes
@@ -471,7 +459,7 @@ int p_potrs(char uplo, int n, int nrhs, const T* a, int ia, int ja, const int* d
             sn::Matrix<T> U = scal_matrix<T>(desca, n, n, ia, ja, a);
             sn::Matrix<T> Lg(n, n, A.nb(), A.p(), A.q());
             sn::copy(sn::Op::ConjTrans, U, Lg);
-            dev_copy(A.data(), A.lld(), Lg.data(), Lg.lld(), A.mloc(), A.nloc());
+            sn::copy(sn::Op::NoTrans, Lg, A);
         }
         sn::Matrix<T> B = scal_matrix<T>(descb, n, nrhs, ib, jb, b);
         sn::potrs(A, B);

@@ -77,6 +77,8 @@ void initialize() {
         for (int b = reserve; b < ncu; ++b) mask[b / 32] |= 1u << (b % 32);
         NHIP(hipExtStreamCreateWithCUMask(&R.update_masked, (uint32_t)mask.size(), mask.data()));
     }
+    // diagnostics: SLATE_AMD_NATIVE_SERIAL=1 issues everything on one stream
+    if (env_int("SLATE_AMD_NATIVE_SERIAL", 0)) R.panel = R.update = R.update_masked = R.comm = R.main;
     const size_t lw = slate_hip::getrf_work_bytes();
     NHIP(hipMalloc(&R.lu_work, lw));
     NHIP(hipMemset(R.lu_work, 0, lw));
@@ -92,7 +94,10 @@ void finalize() {
     R.grids.clear();
     transport_finalize();
     (void)hipFree(R.lu_work);
-    for (hipStream_t s : {R.main, R.panel, R.update, R.update_masked, R.comm}) (void)hipStreamDestroy(s);
+    std::vector<hipStream_t> ss{R.main, R.panel, R.update, R.update_masked, R.comm};
+    std::sort(ss.begin(), ss.end());
+    ss.erase(std::unique(ss.begin(), ss.end()), ss.end());
+    for (hipStream_t s : ss) (void)hipStreamDestroy(s);
     R.up = false;
 }
 
@@ -100,6 +105,29 @@ int rank() { initialize(); return rt().rank; }
 int size() { initialize(); return rt().size; }
 const char* version() { return "slate_amd-native 2026.10.0"; }
 const char* transport() { initialize(); return transport_name(); }
+
+void barrier() {
+    initialize();
+    Runtime& R = rt();
+    NHIP(hipDeviceSynchronize());
+    if (R.size == 1) return;
+    Scratch d(sizeof(i64), R.main);
+    NHIP(hipMemsetAsync(d.p, 0, sizeof(i64), R.main));
+    world_comm()->allreduce(d.p, 1, DT::I64, 's', R.main);
+    NHIP(hipStreamSynchronize(R.main));
+}
+
+double allreduce_max(double v) {
+    initialize();
+    Runtime& R = rt();
+    if (R.size == 1) return v;
+    Scratch d(sizeof(double), R.main);
+    NHIP(hipMemcpyAsync(d.p, &v, sizeof(double), hipMemcpyHostToDevice, R.main));
+    world_comm()->allreduce(d.p, 1, DT::F64, 'M', R.main);
+    NHIP(hipMemcpyAsync(&v, d.p, sizeof(double), hipMemcpyDeviceToHost, R.main));
+    NHIP(hipStreamSynchronize(R.main));
+    return v;
+}
 
 // row / column communicators of a p x q column-major grid (collective:
 // every rank creates the grids in the same order)
@@ -163,23 +191,37 @@ void Matrix<T>::generate(Gen kind, uint64_t seed) {
     NHIP(hipStreamSynchronize(rt().main));
 }
 
+// host <-> device transfers go through a contiguous staging buffer and the
+// gecopy kernel (no pitched hipMemcpy2D: see copy2d below)
 template <typename T>
 void Matrix<T>::from_local_host(const T* Aloc, int64_t ld) {
     const Storage& s = *s_;
-    if (s.mloc && s.nloc)
-        NHIP(hipMemcpy2DAsync(s.buf, s.lld * sizeof(T), Aloc, ld * sizeof(T), s.mloc * sizeof(T), s.nloc,
-                              hipMemcpyHostToDevice, rt().main));
-    NHIP(hipStreamSynchronize(rt().main));
+    Runtime& R = rt();
+    if (!s.mloc || !s.nloc) return;
+    std::vector<T> h((size_t)s.mloc * s.nloc);
+    for (i64 j = 0; j < s.nloc; ++j)
+        std::memcpy(h.data() + j * s.mloc, Aloc + j * ld, sizeof(T) * s.mloc);
+    Scratch stg(h.size() * sizeof(T), R.main);
+    NHIP(hipMemcpyAsync(stg.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, R.main));
+    slate_hip::gecopy<K<T>, K<T>>('G', 'N', s.mloc, s.nloc, kp(stg.as<T>()), s.mloc, kp(static_cast<T*>(s.buf)),
+                                  s.lld, R.main);
+    NHIP(hipStreamSynchronize(R.main));
 }
 
 template <typename T>
 void Matrix<T>::to_local_host(T* Aloc, int64_t ld) const {
     const Storage& s = *s_;
+    Runtime& R = rt();
     NHIP(hipDeviceSynchronize());
-    if (s.mloc && s.nloc)
-        NHIP(hipMemcpy2DAsync(Aloc, ld * sizeof(T), s.buf, s.lld * sizeof(T), s.mloc * sizeof(T), s.nloc,
-                              hipMemcpyDeviceToHost, rt().main));
-    NHIP(hipStreamSynchronize(rt().main));
+    if (!s.mloc || !s.nloc) return;
+    std::vector<T> h((size_t)s.mloc * s.nloc);
+    Scratch stg(h.size() * sizeof(T), R.main);
+    slate_hip::gecopy<K<T>, K<T>>('G', 'N', s.mloc, s.nloc, kp(static_cast<const T*>(s.buf)), s.lld,
+                                  kp(stg.as<T>()), s.mloc, R.main);
+    NHIP(hipMemcpyAsync(h.data(), stg.p, h.size() * sizeof(T), hipMemcpyDeviceToHost, R.main));
+    NHIP(hipStreamSynchronize(R.main));
+    for (i64 j = 0; j < s.nloc; ++j)
+        std::memcpy(Aloc + j * ld, h.data() + j * s.mloc, sizeof(T) * s.mloc);
 }
 
 template <typename T>
@@ -215,8 +257,8 @@ void Matrix<T>::to_host(T* A, int64_t lda) const {
     const size_t blk = (size_t)std::max<i64>(mx_m, 1) * std::max<i64>(mx_n, 1) * sizeof(T);
     Scratch mine(blk, R.main), all(blk * R.size, R.main);
     if (s.mloc && s.nloc)
-        NHIP(hipMemcpy2DAsync(mine.p, std::max<i64>(mx_m, 1) * sizeof(T), s.buf, s.lld * sizeof(T),
-                              s.mloc * sizeof(T), s.nloc, hipMemcpyDeviceToDevice, R.main));
+        slate_hip::gecopy<K<T>, K<T>>('G', 'N', s.mloc, s.nloc, kp(static_cast<const T*>(s.buf)), s.lld,
+                                      kp(mine.as<T>()), std::max<i64>(mx_m, 1), R.main);
     world_comm()->allgather(mine.p, all.p, blk, R.main);
     std::vector<T> h(blk / sizeof(T) * R.size);
     NHIP(hipMemcpyAsync(h.data(), all.p, h.size() * sizeof(T), hipMemcpyDeviceToHost, R.main));
@@ -258,10 +300,12 @@ slate_hip::TriMask lower_mask(i64 nb, int p, int pr, int q, int pc, i64 r0, i64 
     return t;
 }
 
+// device-to-device block copy: the gecopy kernel (hipMemcpy2DAsync between
+// device pitches gave wrong results on this stack for pitched copies of a
+// few MB -- tools/probe/native_probe.cc)
 template <typename T>
 void copy2d(T* dst, i64 ldd, const T* src, i64 lds, i64 m, i64 n, hipStream_t s) {
-    if (m > 0 && n > 0)
-        NHIP(hipMemcpy2DAsync(dst, ldd * sizeof(T), src, lds * sizeof(T), m * sizeof(T), n, hipMemcpyDeviceToDevice, s));
+    if (m > 0 && n > 0) slate_hip::gecopy<K<T>, K<T>>('G', 'N', m, n, kp(src), lds, kp(dst), ldd, s);
 }
 
 int64_t read_infos(const i64* d, i64 nt, hipStream_t s, i64 nb) {
