@@ -5,7 +5,7 @@
 // between barriers, maximum over ranks.  After the timed region the
 // backward error is checked on the grid with the library itself:
 //   potrf / getrf: X = A \ B through the factors, ||B - A0 X|| / (||A0|| ||X|| n)
-//   gemm:          ||C v - A (B v)|| / (||A|| ||B|| ||v||)
+//   gemm:          ||C v - A (B v)|| / (||A|| ||B|| ||v|| n)
 //
 //   bench_native routine n nb p q lookahead warmup steps check
 // prints "RESULT ms_per_step=<max over ranks> info=<info> resid=<r>"
@@ -76,7 +76,8 @@ int main(int argc, char** argv) {
                 sn::gemm(1.0, A0, BV, 0.0, ABV);
                 sn::gemm(1.0, C, V, -1.0, ABV);            // C v - A (B v)
                 resid = sn::norm(sn::Norm::Fro, ABV) /
-                        (sn::norm(sn::Norm::Fro, A0) * sn::norm(sn::Norm::Fro, B) * sn::norm(sn::Norm::Fro, V));
+                        (sn::norm(sn::Norm::Fro, A0) * sn::norm(sn::Norm::Fro, B) * sn::norm(sn::Norm::Fro, V) *
+                         (double)n);
             } else {
                 sn::copy(sn::Op::NoTrans, V, X);
                 if (chol) sn::potrs(H, X);

@@ -400,7 +400,7 @@ std::vector<int64_t> ipiv_from_local(const sn::Matrix<T>& A, i64 k, const int* i
     if (p > 1) {       // each global row lives on exactly one process row
         sn::GridComms* gc = sn::grid_comms(A.p(), A.q());
         sn::Scratch d(sizeof(int64_t) * g.size(), sn::rt().main);
-        NHIP(hipMemcpyAsync(d.p, g.data(), sizeof(int64_t) * g.size(), hipMemcpyHostToDevice, sn::rt().main));
+        sn::upload(d.p, g.data(), sizeof(int64_t) * g.size(), sn::rt().main);
         gc->col->allreduce(d.p, g.size(), sn::DT::I64, 's', sn::rt().main);
         NHIP(hipMemcpyAsync(g.data(), d.p, sizeof(int64_t) * g.size(), hipMemcpyDeviceToHost, sn::rt().main));
         NHIP(hipStreamSynchronize(sn::rt().main));

@@ -122,7 +122,7 @@ double allreduce_max(double v) {
     Runtime& R = rt();
     if (R.size == 1) return v;
     Scratch d(sizeof(double), R.main);
-    NHIP(hipMemcpyAsync(d.p, &v, sizeof(double), hipMemcpyHostToDevice, R.main));
+    upload(d.p, &v, sizeof(double), R.main);
     world_comm()->allreduce(d.p, 1, DT::F64, 'M', R.main);
     NHIP(hipMemcpyAsync(&v, d.p, sizeof(double), hipMemcpyDeviceToHost, R.main));
     NHIP(hipStreamSynchronize(R.main));
@@ -202,7 +202,7 @@ void Matrix<T>::from_local_host(const T* Aloc, int64_t ld) {
     for (i64 j = 0; j < s.nloc; ++j)
         std::memcpy(h.data() + j * s.mloc, Aloc + j * ld, sizeof(T) * s.mloc);
     Scratch stg(h.size() * sizeof(T), R.main);
-    NHIP(hipMemcpyAsync(stg.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, R.main));
+    upload(stg.p, h.data(), h.size() * sizeof(T), R.main);
     slate_hip::gecopy<K<T>, K<T>>('G', 'N', s.mloc, s.nloc, kp(stg.as<T>()), s.mloc, kp(static_cast<T*>(s.buf)),
                                   s.lld, R.main);
     NHIP(hipStreamSynchronize(R.main));
@@ -232,7 +232,7 @@ void Matrix<T>::from_host(const T* A, int64_t lda) {
         const i64 gj = l2g(lj, s.nb, s.q, s.pc);
         for (i64 li = 0; li < s.mloc; ++li) loc[li + lj * s.lld] = A[l2g(li, s.nb, s.p, s.pr) + gj * lda];
     }
-    NHIP(hipMemcpyAsync(data(), loc.data(), loc.size() * sizeof(T), hipMemcpyHostToDevice, rt().main));
+    upload(data(), loc.data(), loc.size() * sizeof(T), rt().main);
     NHIP(hipStreamSynchronize(rt().main));
 }
 
@@ -323,7 +323,7 @@ int64_t reduce_info(int64_t info) {
     const i64 big = (i64)1 << 62;
     Scratch d(sizeof(i64), R.main);
     i64 v = info > 0 ? info : big;
-    NHIP(hipMemcpyAsync(d.p, &v, sizeof(i64), hipMemcpyHostToDevice, R.main));
+    upload(d.p, &v, sizeof(i64), R.main);
     world_comm()->allreduce(d.p, 1, DT::I64, 'm', R.main);
     NHIP(hipMemcpyAsync(&v, d.p, sizeof(i64), hipMemcpyDeviceToHost, R.main));
     NHIP(hipStreamSynchronize(R.main));
@@ -499,7 +499,7 @@ static void potrf_grid(Storage& S, int la, i64* infos) {
     }
     if (flat.empty()) flat.push_back(0);
     Scratch idx(flat.size() * sizeof(i64), ps);
-    NHIP(hipMemcpyAsync(idx.p, flat.data(), flat.size() * sizeof(i64), hipMemcpyHostToDevice, ps));
+    upload(idx.p, flat.data(), flat.size() * sizeof(i64), ps);
     join(R.main, ps);
     join(R.main, us);
     join(R.main, cs);
@@ -868,7 +868,7 @@ static void permute_rows_dist(Storage& S, const i64* ipiv_d, i64 k1, i64 k2, i64
 // rows in place and the same kb x kb top block T
 template <typename T>
 static void panel_dist(Storage& S, i64 k, i64 kb, i64 lck, i64* ipiv_d, i64* info, double thr, int bw, T* Tt,
-                       hipStream_t s) {
+                       const i64* grow_d, hipStream_t s) {
     const int p = S.p, pr = S.pr;
     const i64 nb = S.nb, r0 = k * nb;
     const int rk = (int)(k % p);
@@ -878,11 +878,6 @@ static void panel_dist(Storage& S, i64 k, i64 kb, i64 lck, i64* ipiv_d, i64* inf
     T* W = buf + lr_k + lck * S.lld;
     const i64 ldw = S.lld;
     Comm* colc = S.gc->col.get();
-    // panel-relative global rows of my panel rows
-    std::vector<i64> gr((size_t)std::max<i64>(nmine, 1));
-    for (i64 i = 0; i < nmine; ++i) gr[i] = l2g(lr_k + i, nb, p, pr) - r0;
-    Scratch grow(gr.size() * sizeof(i64), s);
-    NHIP(hipMemcpyAsync(grow.p, gr.data(), gr.size() * sizeof(i64), hipMemcpyHostToDevice, s));
     Scratch part(2 * 1024 * 8 + 64, s);
     const int b = std::max(1, bw);
     Scratch recs((size_t)p * (3 + 2 * b) * sizeof(T), s), rec((size_t)(3 + 2 * b) * sizeof(T), s);
@@ -893,7 +888,7 @@ static void panel_dist(Storage& S, i64 k, i64 kb, i64 lck, i64* ipiv_d, i64* inf
         for (i64 j = c0; j <= c1; ++j) {
             const bool nxt = j < c1;
             const i64 dl = (pr == rk && nxt) ? j : -1;
-            slate_hip::lu_dist_step<K<T>>(nmine, kp(W + c0 * ldw), ldw, grow.as<i64>(), (int)c0, (int)c1, (int)j,
+            slate_hip::lu_dist_step<K<T>>(nmine, kp(W + c0 * ldw), ldw, grow_d, (int)c0, (int)c1, (int)j,
                                           j > c0 ? kp(recs.as<T>()) : nullptr, p, kp(Tt), kb, piv, info, 0, thr,
                                           kp(rec.as<T>()), part.p, dl, s);
             if (nxt) colc->allgather(rec.p, recs.p, (size_t)recn * sizeof(T), s);
@@ -1025,6 +1020,17 @@ int64_t getrf(Matrix<T>& A, std::vector<int64_t>& ipiv_out, const Options& opts)
         //      block, one GEMM (models/lu.py _getrf_general)
         Comm* colc = gc->col.get();
         Comm* rowc = gc->row.get();
+        // panel-relative global rows of my panel rows, every step, uploaded
+        // once (no host synchronisation inside the loop)
+        std::vector<i64> gflat, goff((size_t)kt + 1, 0);
+        for (i64 k = 0; k < kt; ++k) {
+            const i64 lr_k = std::min(tiles_before(k, p, pr) * nb, mloc);
+            for (i64 i = lr_k; i < mloc; ++i) gflat.push_back(l2g(i, nb, p, pr) - k * nb);
+            goff[k + 1] = (i64)gflat.size();
+        }
+        if (gflat.empty()) gflat.push_back(0);
+        Scratch gall(gflat.size() * sizeof(i64), ps);
+        upload(gall.p, gflat.data(), gflat.size() * sizeof(i64), ps);
         for (i64 k = 0; k < kt; ++k) {
             const i64 r0 = k * nb;
             const i64 kb = std::min({nb, n - r0, m - r0});
@@ -1043,7 +1049,7 @@ int64_t getrf(Matrix<T>& A, std::vector<int64_t>& ipiv_out, const Options& opts)
             i64* pv = reinterpret_cast<i64*>(static_cast<char*>(pack.p) + lbytes + tbytes);
             if (pc == ck) {
                 panel_dist<T>(S, k, kb, lck, ipiv_d, infos.as<i64>() + k, opts.pivot_threshold,
-                              opts.inner_blocking, Tt, ps);
+                              opts.inner_blocking, Tt, gall.as<i64>() + goff[k], ps);
                 copy2d(Lp, std::max<i64>(nmine, 1), buf + lr_k + lck * lld, lld, nmine, kb, ps);
                 NHIP(hipMemcpyAsync(pv, ipiv_d + r0, (size_t)kb * sizeof(i64), hipMemcpyDeviceToDevice, ps));
             }
@@ -1095,7 +1101,7 @@ int64_t getrs(Op trans, const Matrix<T>& A, const std::vector<int64_t>& ipiv, Ma
     if (trans == Op::Trans && is_cplx<T>()) throw Error("native getrs: Trans of a complex matrix (use ConjTrans)");
     const i64 k = (i64)ipiv.size();
     Scratch d(sizeof(i64) * std::max<i64>(k, 1), s);
-    NHIP(hipMemcpyAsync(d.p, ipiv.data(), sizeof(i64) * k, hipMemcpyHostToDevice, s));
+    upload(d.p, ipiv.data(), sizeof(i64) * k, s);
     Comm* colc = SB.gc->col.get();
     if (trans == Op::NoTrans) {
         permute_rows_dist<T>(SB, d.as<i64>(), 0, k, 0, SB.nloc, 1, s, colc);
@@ -1253,7 +1259,7 @@ double norm(Norm kind, const Matrix<T>& A) {
     }
     if (R.size > 1 && !v.empty()) {
         Scratch d(sizeof(double) * v.size(), s);
-        NHIP(hipMemcpyAsync(d.p, v.data(), sizeof(double) * v.size(), hipMemcpyHostToDevice, s));
+        upload(d.p, v.data(), sizeof(double) * v.size(), s);
         world_comm()->allreduce(d.p, v.size(), DT::F64, op, s);
         NHIP(hipMemcpyAsync(v.data(), d.p, sizeof(double) * v.size(), hipMemcpyDeviceToHost, s));
         NHIP(hipStreamSynchronize(s));

@@ -150,7 +150,7 @@ public:
         int* d = nullptr;
         NHIP(hipMalloc(&d, sizeof(int) * n));
         int me = world[rank];
-        NHIP(hipMemcpyAsync(d + r, &me, sizeof(int), hipMemcpyHostToDevice, rt().main));
+        upload(d + r, &me, sizeof(int), rt().main);
         NCCL(ncclAllGather(d + r, d, 1, ncclInt32, out->c, rt().main));
         NHIP(hipMemcpyAsync(out->world.data(), d, sizeof(int) * n, hipMemcpyDeviceToHost, rt().main));
         NHIP(hipStreamSynchronize(rt().main));
@@ -238,7 +238,7 @@ public:
         NHIP(hipStreamSynchronize(s));
     }
     void h2d(void* d, const std::vector<char>& h, size_t bytes, hipStream_t s) {
-        if (bytes) NHIP(hipMemcpyAsync(d, h.data(), bytes, hipMemcpyHostToDevice, s));
+        if (bytes) upload(d, h.data(), bytes, s);
         NHIP(hipStreamSynchronize(s));
     }
     void bcast(void* buf, size_t bytes, int root, hipStream_t s) override {

@@ -5,6 +5,7 @@
 #pragma once
 #include <complex>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -154,6 +155,15 @@ struct Event {
     void wait(hipStream_t s) const { NHIP(hipStreamWaitEvent(s, e, 0)); }
 };
 
+// host -> device upload of a small pageable host array, complete on return
+// (a pageable async copy is not reliably ordered before the next kernels of
+// the stream on this stack: the first potrf_grid read stale plan indices --
+// tools/probe/scal_probe.cc)
+inline void upload(void* d, const void* h, size_t bytes, hipStream_t s) {
+    if (bytes) NHIP(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s));
+    NHIP(hipStreamSynchronize(s));
+}
+
 // stream b waits for everything issued so far on stream a
 inline void join(hipStream_t a, hipStream_t b) {
     Event ev;
@@ -165,7 +175,16 @@ inline void join(hipStream_t a, hipStream_t b) {
 struct Scratch {
     void* p = nullptr;
     hipStream_t s = nullptr;
-    Scratch(size_t bytes, hipStream_t st) : s(st) { if (bytes) NHIP(hipMallocAsync(&p, bytes, st)); }
+    Scratch(size_t bytes, hipStream_t st) : s(st) {
+        if (!bytes) return;
+        NHIP(hipMallocAsync(&p, bytes, st));
+        if (poison()) NHIP(hipMemsetAsync(p, 0xFF, bytes, st));     // NaN: exposes reads before writes
+    }
+    // diagnostics: SLATE_AMD_NATIVE_POISON=1 fills every scratch buffer with NaN
+    static bool poison() {
+        static const bool on = [] { const char* e = std::getenv("SLATE_AMD_NATIVE_POISON"); return e && *e == '1'; }();
+        return on;
+    }
     ~Scratch() { if (p) (void)hipFreeAsync(p, s); }
     Scratch(const Scratch&) = delete;
     template <typename T> T* as() { return static_cast<T*>(p); }

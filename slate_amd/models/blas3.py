@@ -473,13 +473,7 @@ def hemm(side, alpha, A, B, beta, C, opts=None, _sym=False):
             return C
         if _hemm_method(B, opts) == MethodHemm.A:
             return _hemmA(side, alpha, A, B, beta, C, opts, _sym)
-        # hemmC with both triangles materialised once (SLATE broadcasts A
-        # and A^H tiles per step and runs the diagonal tiles on the host,
-        # src/hemmC.cc:147-429): one transposing redistribution, then SUMMA
-        F = _full_from_stored(A, target_slot(C, opts), herm=not _sym)
-        if side == Side.Left:
-            return gemm(alpha, F, B, beta, C, opts)
-        return gemm(alpha, B, F, beta, C, opts)
+        return _hemmC(side, alpha, A, B, beta, C, opts, _sym)
 
 
 def _hemm_method(B, opts):
@@ -488,6 +482,125 @@ def _hemm_method(B, opts):
     if m in (MethodHemm.A, MethodHemm.C):
         return m
     return MethodHemm.A if B.nt() < 2 else MethodHemm.C
+
+
+def _hemmC(side, alpha, A, B, beta, C, opts, sym):
+    """Stationary-C hemm (src/hemmC.cc:147-429) without materialising the
+    full Hermitian matrix: the Right side goes through the transposed Left
+    problem, as _hemmA does."""
+    slot = target_slot(C, opts)
+    if side == Side.Right:
+        cplx = C.storage.dtype.is_complex and not sym
+        tr = (lambda X: X.conj_transpose()) if cplx else (lambda X: X.transpose())
+        cj = (lambda v: complex(v).conjugate()) if cplx else (lambda v: v)
+        Bt = _copy_in(tr(B), C, slot)
+        Ct = _copy_in(tr(C), C, slot)
+        _hemmC_left(cj(alpha), A, Bt, cj(beta), Ct, slot, sym)
+        _copy_out(tr(Ct), C)
+        return C
+    Bw = B if (_at_origin(B) and _same_grid(B, C)) else _copy_in(B, C, slot)
+    Cw = C if _at_origin(C) else _fresh(C, C.m(), C.n(), slot)
+    if Cw is not C and beta != 0:
+        _copy_out(C, Cw)
+    _hemmC_left(alpha, A, Bw, beta, Cw, slot, sym)
+    if Cw is not C:
+        _copy_out(Cw, C)
+    return C
+
+
+# per-rank workspace of the last _hemmC_left call (tests): peak elements
+HEMMC_STATS = {"workspace_elems": 0}
+
+
+def _hemmC_left(alpha, A, B, beta, C, slot, sym):
+    """Left hemmC, SUMMA over k with the block column k of the FULL matrix
+    assembled per step from the stored triangle only (SLATE broadcasts the
+    A(:, k) tiles and the transposed A(k, :) tiles of each step,
+    src/hemmC.cc:147-429).  For stored Lower, block column k is A(i, k)
+    (i >= k, stored, on process column k % q) over op(A(k, i)) (i < k, the
+    stored block row k, op = ^H or ^T).  Per step:
+      1. the block row k goes down each process column (one column
+         broadcast of its mirror-range local columns);
+      2. each rank writes into a zeroed (local rows x kb) buffer the tiles
+         it can: the direct tiles when it is on process column k % q (the
+         diagonal tile symmetrised from its stored triangle), and op() of
+         the mirror tiles whose column lands on its own process column;
+      3. ONE all-reduce over the row communicator completes the block column
+         on every rank of the row (every tile is written by exactly one
+         process column; x + 0 is exact);
+      4. B(k, :) goes down the process columns and ONE GEMM updates the
+         local C.
+    Workspace per rank: (local rows + local cols) x nb -- never the n x n
+    matrix the former full-copy redistribution built."""
+    if not (_same_grid(A, C) and A.global_offsets() == (0, 0) and A.op() == Op.NoTrans
+            and A.local_block(slot).mloc == C.local_block(slot).mloc):
+        A = _copy_herm(A, C, slot)
+    sC = C.storage
+    bc = sC.bc
+    grid = grid_of(C)
+    lbA = A.local_block(slot)
+    lbB = B.local_block(slot)
+    lbC = C.local_block(slot)
+    dev = lbC.data.device
+    dt = sC.dtype
+    nb, p, q, pr, pc = bc.nb, bc.p, bc.q, bc.pr, bc.pc
+    n = A.n()
+    mt = (n + nb - 1) // nb
+    mloc, nlocA, nloc = lbA.mloc, lbA.nloc, lbC.nloc
+    lower = A.uploPhysical() == Uplo.Lower
+    up = 'L' if lower else 'U'
+    other = 'U' if lower else 'L'
+    op = 'T' if (sym or not dt.is_complex) else 'C'
+    Aloc = lbA.data
+    HEMMC_STATS["workspace_elems"] = 0
+    for k in range(mt):
+        kb = min(nb, n - k * nb)
+        rk, ck = k % p, k % q
+        lrk = tiles_local_before(k, p, pr) * nb
+        lck = tiles_local_before(k, q, pc) * nb
+        Acol = ops.colmajor_zeros(mloc, kb, dt, dev)
+        # 2a. direct tiles (stored column block k)
+        if pc == ck and mloc:
+            d0, d1 = (tiles_local_before(k + 1, p, pr) * nb, mloc) if lower else (0, lrk)
+            if d1 > d0:
+                ops.gecopy(Aloc[d0:d1, lck:lck + kb], Acol[d0:d1])
+            if pr == rk:
+                Dk = Aloc[lrk:lrk + kb, lck:lck + kb]
+                Ad = Acol[lrk:lrk + kb]
+                ops.gecopy(Dk, Ad, uplo=up)
+                ops.gecopy(Dk, Ad, uplo=other, trans=op)
+                if op == 'C':
+                    d = torch.diagonal(Ad)
+                    d.copy_(d.real.to(dt))
+        # 1. block row k (its mirror-range local columns) down the column
+        m0, m1 = (0, lck) if lower else (tiles_local_before(k + 1, q, pc) * nb, nlocA)
+        src = Aloc[lrk:lrk + kb, m0:m1] if pr == rk else None
+        Rk = col_bcast(grid, src, rk, kb, m1 - m0, dt, dev) if m1 > m0 else None
+        # 2b. mirror tiles i with i % p == pr and i % q == pc
+        if Rk is not None:
+            tiles = range(pr, k, p) if lower else range(k + 1 + ((pr - k - 1) % p), mt, p)
+            for i in tiles:
+                if i % q != pc:
+                    continue
+                wi = min(nb, n - i * nb)
+                lri = tiles_local_before(i, p, pr) * nb
+                lci = tiles_local_before(i, q, pc) * nb - m0
+                ops.gecopy(Rk[:, lci:lci + wi], Acol[lri:lri + wi], trans=op)
+        # 3. complete the block column along the process row
+        if q > 1 and mloc:
+            grid.row_comm.allreduce(Acol)
+        # 4. B(k, :) down the process columns, one GEMM
+        srcB = lbB.data[lrk:lrk + kb, :] if pr == rk else None
+        Bp = col_bcast(grid, srcB, rk, kb, nloc, dt, dev)
+        HEMMC_STATS["workspace_elems"] = max(HEMMC_STATS["workspace_elems"],
+                                             Acol.numel() + (Rk.numel() if Rk is not None else 0)
+                                             + (Bp.numel() if Bp is not None else 0))
+        if mloc and nloc:
+            ops.gemm(alpha, Acol, Bp, beta if k == 0 else 1.0, lbC.data)
+    if mt == 0 and mloc and nloc:
+        ops.gescale(beta, lbC.data)
+    _done(C)
+    return C
 
 
 def _hemmA(side, alpha, A, B, beta, C, opts, sym):

@@ -318,3 +318,33 @@ def test_gather_to_root():
     """Matrix::gather: the whole matrix on the root only (piece-level
     redistribution onto rank 0, then one send to another root)."""
     run_dist(_gather_roots, 4, 2, 2)
+
+
+def _hemmC_workspace(rank, size, p, q):
+    import torch
+    import slate_amd as sl
+    from slate_amd.core.enums import MethodHemm, Option, Side, Uplo
+    from slate_amd.models import blas3
+    n, nb, w = 96, 8, 40
+    for uplo in (Uplo.Lower, Uplo.Upper):
+        A = sl.HermitianMatrix(uplo, n, nb=nb, p=p, q=q, dtype=torch.complex128)
+        A.insertLocalTiles()
+        sl.generate_matrix(A, "rands", 41)
+        B = sl.Matrix(n, w, nb=nb, p=p, q=q, dtype=torch.complex128)
+        B.insertLocalTiles()
+        sl.generate_matrix(B, "rands", 42)
+        C = sl.Matrix(n, w, nb=nb, p=p, q=q, dtype=torch.complex128)
+        C.insertLocalTiles()
+        sl.hemm(Side.Left, 1.0, A, B, 0.0, C, {Option.MethodHemm: MethodHemm.C})
+        lb = A.local_block()
+        # (local rows + local cols) x nb, never the n x n copy
+        bound = (lb.mloc + lb.nloc + C.local_block().nloc) * nb
+        assert blas3.HEMMC_STATS["workspace_elems"] <= bound, (blas3.HEMMC_STATS, bound)
+        assert blas3.HEMMC_STATS["workspace_elems"] < n * n // (p * q)
+
+
+def test_hemmC_workspace_2x4():
+    """hemmC assembles each block column of the full Hermitian matrix from
+    the stored triangle per step (SLATE src/hemmC.cc:147-429): per-rank
+    workspace O((local rows + local cols) nb), no n x n materialisation."""
+    run_dist(_hemmC_workspace, 8, 2, 4)

@@ -20,6 +20,11 @@ int main(int argc, char** argv) {
     const int64_t n = argc > 2 ? std::atoll(argv[2]) : 384, nb = argc > 3 ? std::atoll(argv[3]) : 32;
     sn::initialize();
     const int me = sn::rank(), pr = me % p, pc = me / p;
+    if (argc > 4 && std::atoi(argv[4])) {          // warm-up factorization first
+        sn::HermitianMatrix<double> W(sn::Uplo::Lower, 4 * nb * p, nb, p, q);
+        W.generate(sn::Gen::HermitianPositiveDefinite, 1);
+        sn::potrf(W);
+    }
     sn::Matrix<double> G(n, n, nb, p, q);
     const int64_t mloc = G.mloc(), nloc = G.nloc(), ld = std::max<int64_t>(mloc, 1);
     std::vector<double> a((size_t)ld * std::max<int64_t>(nloc, 1));
