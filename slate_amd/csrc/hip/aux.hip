@@ -589,8 +589,35 @@ void permute_rows_scatter(i64 m, i64 n, const T* A, i64 lda, T* B, i64 ldb, cons
     HIP_LAUNCH_CHECK();
 }
 
+// B = A where the block-cyclic triangle mask keeps the element, 0 elsewhere
+// (the stored triangle T / strict triangle S of a distributed Hermitian
+// block: the masks of hemmA, formerly torch.where over dense index grids);
+// real_diag: the kept diagonal gets its imaginary part dropped (Hermitian)
+template <typename T>
+__global__ void gecopy_mask_kernel(TriMask mk, i64 m, i64 n, const T* __restrict__ A, i64 lda, T* __restrict__ B,
+                                   i64 ldb, int real_diag) {
+    const i64 i = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    const i64 gr = mk.grow(i);
+    for (i64 j = blockIdx.y; j < n; j += gridDim.y) {
+        T v = mk.keep(i, j) ? A[i + j * lda] : s_zero(T());
+        if (real_diag && gr == mk.gcol(j)) v = s_from_real(T(), s_real(v));
+        B[i + j * ldb] = v;
+    }
+}
+
+template <typename T>
+void gecopy_mask(const TriMask& mk, i64 m, i64 n, const T* A, i64 lda, T* B, i64 ldb, bool real_diag,
+                 hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    hipLaunchKernelGGL(gecopy_mask_kernel<T>, grid2(m, n), dim3(256), 0, s, mk, m, n, A, lda, B, ldb,
+                       real_diag ? 1 : 0);
+    HIP_LAUNCH_CHECK();
+}
+
 #define INST(T)                                                                                   \
     template void permute_rows_scatter<T>(i64, i64, const T*, i64, T*, i64, const i64*, hipStream_t); \
+    template void gecopy_mask<T>(const TriMask&, i64, i64, const T*, i64, T*, i64, bool, hipStream_t);   \
     template void geset<T>(char, i64, i64, T, T, T*, i64, hipStream_t);                           \
     template void gescale<T>(char, i64, i64, T, T*, i64, hipStream_t);                            \
     template void geadd<T>(char, i64, i64, T, const T*, i64, T, T*, i64, hipStream_t);            \

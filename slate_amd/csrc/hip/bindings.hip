@@ -276,6 +276,12 @@ static void register_kernels(py::module& m) {
         dispatch(dt, [&](auto z) { using T = decltype(z);
             geadd<T>(uplo, mm, n, cv<T>(a), P<T>(A), lda, cv<T>(b), P<T>(B), ldb, S(st)); });
     });
+    m.def("gecopy_mask", [](char dt, py::object mask, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t B, i64 ldb,
+                            int real_diag, uintptr_t st) {
+        const TriMask mk = make_mask(mask);
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            gecopy_mask<T>(mk, mm, n, P<T>(A), lda, P<T>(B), ldb, real_diag != 0, S(st)); });
+    });
     m.def("gecopy", [](char ds, char dd, char uplo, char trans, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t B,
                        i64 ldb, uintptr_t st) {
         dispatch(ds, [&](auto zs) { using Ts = decltype(zs);

@@ -39,6 +39,9 @@ template <typename T>
 void geadd(char uplo, i64 m, i64 n, T alpha, const T* A, i64 lda, T beta, T* B, i64 ldb, hipStream_t s);
 template <typename Ts, typename Td>
 void gecopy(char uplo, char trans, i64 m, i64 n, const Ts* A, i64 lda, Td* B, i64 ldb, hipStream_t s);
+template <typename T>
+void gecopy_mask(const TriMask& mk, i64 m, i64 n, const T* A, i64 lda, T* B, i64 ldb, bool real_diag,
+                 hipStream_t s);
 template <typename T, typename R>
 void butterfly(bool trans, bool rows, int depth, i64 nidx, i64 nother, T* A, i64 lda, const R* diag, i64 ldd,
                hipStream_t s);

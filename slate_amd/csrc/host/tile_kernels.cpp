@@ -928,6 +928,24 @@ void register_tile_kernels(py::module& m) {
     m.def("gescale", [](char dt, char uplo, i64 mm, i64 n, std::complex<double> s, uintptr_t A, i64 lda, uintptr_t) {
         dispatch(dt, [&](auto z) { using T = decltype(z); gescale<T>(uplo, mm, n, from_c<T>(s), P<T>(A), lda); });
     });
+    // B = A where the block-cyclic triangle mask keeps the element, 0 else
+    m.def("gecopy_mask", [](char dt, py::object mask, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t B, i64 ldb,
+                            int real_diag, uintptr_t) {
+        const Mask mk = make_mask(mask);
+        dispatch(dt, [&](auto z) {
+            using T = decltype(z);
+            const T* a = P<T>(A);
+            T* b = P<T>(B);
+            for (i64 j = 0; j < n; ++j)
+                for (i64 i = 0; i < mm; ++i) {
+                    T v = mk.keep(i, j) ? a[i + j * lda] : T(0);
+                    if (real_diag && Mask::l2g(i + mk.row_off, mk.nb, mk.p, mk.pr) ==
+                                         Mask::l2g(j + mk.col_off, mk.nb, mk.q, mk.pc))
+                        v = T(real_(v));
+                    b[i + j * ldb] = v;
+                }
+        });
+    });
     m.def("geadd", [](char dt, char uplo, i64 mm, i64 n, std::complex<double> alpha, uintptr_t A, i64 lda,
                       std::complex<double> beta, uintptr_t B, i64 ldb, uintptr_t) {
         dispatch(dt, [&](auto z) {

@@ -637,7 +637,6 @@ def _hemmA_left(alpha, A, B, beta, C, slot, sym):
     row are added into P, and P is reduced along the process row onto the
     owner of C(:, jb) (tile reduce, the reference's listReduce)."""
     import numpy as np
-    from ._panels import _ranges
     if not (_same_grid(A, C) and A.global_offsets() == (0, 0) and A.op() == Op.NoTrans
             and A.local_block(slot).mloc == C.local_block(slot).mloc):
         A = _copy_herm(A, C, slot)
@@ -653,29 +652,24 @@ def _hemmA_left(alpha, A, B, beta, C, slot, sym):
     n = A.n()
     mloc, nlocA = lbA.mloc, lbA.nloc
     lower = A.uploPhysical() == Uplo.Lower
-    gr = torch.from_numpy(_local_globals(mloc, nb, p, pr, n)).to(dev)
-    gc = torch.from_numpy(_local_globals(nlocA, nb, q, pc, n)).to(dev)
-    keep = (gr[:, None] >= gc[None, :]) if lower else (gr[:, None] <= gc[None, :])
-    strict = keep & (gr[:, None] != gc[None, :])
     Aloc = lbA.data
     T = ops.colmajor_empty(mloc, nlocA, dt, dev)
     Sx = ops.colmajor_empty(mloc, nlocA, dt, dev)
     if mloc and nlocA:
-        zero = torch.zeros((), dtype=dt, device=dev)
-        T.copy_(torch.where(keep, Aloc, zero))
-        Sx.copy_(torch.where(strict, Aloc, zero))
-        if dt.is_complex and not sym:
-            d = keep & ~strict
-            T.copy_(torch.where(d, T.real.to(dt), T))
+        # stored triangle / strict stored triangle by the block-cyclic mask
+        # kernel (one launch each)
+        mode = 1 if lower else 2
+        ops.gecopy_mask(Aloc, T, (mode, nb, p, pr, q, pc, 0, 0, 0), real_diag=dt.is_complex and not sym)
+        ops.gecopy_mask(Aloc, Sx, (mode, nb, p, pr, q, pc, 0, 0, -1))
     # rows of Q (my local A column tiles k) that land in my process row:
-    # local A column offset t*nb -> local C row offset of tile k
+    # local A column offset t*nb -> local C row offset of tile k (one
+    # contiguous range per tile)
     ks = np.arange(pc, (n + nb - 1) // nb, q, dtype=np.int64)
     lens = np.minimum(nb, n - ks * nb)
     qoff = np.cumsum(lens) - lens
     mine = ks % p == pr
-    lrow = np.asarray([tiles_local_before(int(k), p, pr) * nb for k in ks[mine]], dtype=np.int64)
-    src_rows = torch.from_numpy(_ranges(qoff[mine], lens[mine])).to(dev)
-    dst_rows = torch.from_numpy(_ranges(lrow, lens[mine])).to(dev)
+    moves = [(int(qo), tiles_local_before(int(k), p, pr) * nb, int(ln))
+             for k, qo, ln in zip(ks[mine], qoff[mine], lens[mine])]
     plan = plan_col_gather(B.storage.tileMb, 0, A.nt(), nb, p, q, pc, dev)
     ct = 'T' if sym else conj_trans(dt)
     for jb in range(C.nt()):
@@ -692,8 +686,8 @@ def _hemmA_left(alpha, A, B, beta, C, slot, sym):
             ops.gemm(1.0, Sx, Prow, 0.0, Q, ct, 'N')
         if p > 1 and nlocA:
             grid.col_comm.allreduce(Q)
-        if src_rows.numel():
-            P.index_add_(0, dst_rows, Q.index_select(0, src_rows))
+        for qo, lr, ln in moves:
+            ops.geadd(1.0, Q[qo:qo + ln], 1.0, P[lr:lr + ln])
         if q > 1 and mloc:
             grid.row_comm.reduce(P, owner)
         if pc == owner and lbC.mloc:
@@ -902,7 +896,9 @@ def _trsmA_left(alpha, A, B, slot):
     lower = A.uplo() == Uplo.Lower
     upl, diag = ('L' if lower else 'U'), A.diag().value
     mt = B.mt()
-    gcols = torch.from_numpy(_local_globals(nloc, nb, q, pc, n)).to(dev)
+    # my local columns of B as (local offset, global offset, width) tile runs
+    cruns = [(tiles_local_before(t, q, pc) * nb, t * nb, min(nb, n - t * nb))
+             for t in range(pc, (n + nb - 1) // nb, q)]
     W = ops.colmajor_zeros(mloc, n, dt, dev)
     for k in (range(mt) if lower else range(mt - 1, -1, -1)):
         kb = B.tileMb(k)
@@ -910,11 +906,10 @@ def _trsmA_left(alpha, A, B, slot):
         dq = k % q
         if k % p == pr:
             S = ops.colmajor_zeros(kb, n, dt, dev)
-            if nloc:
-                S.index_copy_(1, gcols, lbB.data[lrk:lrk + kb, :])
-                if alpha != 1:
-                    ops.gescale(alpha, S)
-            S -= W[lrk:lrk + kb]
+            for lo, go, wd in cruns:
+                ops.gecopy(lbB.data[lrk:lrk + kb, lo:lo + wd], S[:, go:go + wd])
+            # S = alpha B(k, :) - W(k, :)
+            ops.geadd(-1.0, W[lrk:lrk + kb], alpha, S)
             if q > 1:
                 grid.row_comm.reduce(S, dq)
             if pc == dq:
@@ -922,8 +917,8 @@ def _trsmA_left(alpha, A, B, slot):
                 ops.trsm('L', upl, 'N', diag, 1.0, lbA.data[lrk:lrk + kb, lc:lc + kb], S)
             if q > 1:
                 grid.row_comm.bcast(S, dq)
-            if nloc:
-                lbB.data[lrk:lrk + kb, :].copy_(S.index_select(1, gcols))
+            for lo, go, wd in cruns:
+                ops.gecopy(S[:, go:go + wd], lbB.data[lrk:lrk + kb, lo:lo + wd])
             Xk = S
         else:
             Xk = ops.colmajor_empty(kb, n, dt, dev) if pc == dq else None

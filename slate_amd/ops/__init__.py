@@ -531,6 +531,19 @@ def gecopy(A, B, uplo='G', trans='N'):
     return B
 
 
+def gecopy_mask(A, B, mask, real_diag=False):
+    """B = A where the block-cyclic triangle ``mask`` (the GEMM TriMask tuple
+    (mode, nb, p, pr, q, pc, row_off, col_off, diag_off)) keeps the element,
+    0 elsewhere; ``real_diag`` drops the imaginary part of kept diagonal
+    elements (Hermitian).  One kernel launch."""
+    _chk(A); _chk(B, "B")
+    m, n = B.shape
+    if m and n:
+        kmod(B).gecopy_mask(code(B.dtype), tuple(int(x) for x in mask), m, n, A.data_ptr(), ld(A),
+                            B.data_ptr(), ld(B), 1 if real_diag else 0, stream(B))
+    return B
+
+
 def gescale_row_col(equed, r, c, A):
     m, n = A.shape
     if m and n:
