@@ -146,6 +146,31 @@ static void register_kernels(py::module& m) {
                               uintptr_t V, i64 ldv, uintptr_t st) {
         stedc_vectors(n, P<const double>(d), P<const double>(zh), P<const i64>(org), P<const double>(mu), j0, nc,
                       P<double>(V), ldv, S(st)); });
+    // device-resident D&C merges of one tree level (stedc.hip)
+    m.def("stedc_level_prep", [](i64 n, i64 nm, i64 maxs, uintptr_t desc, uintptr_t rho, uintptr_t W, uintptr_t Z,
+                                 uintptr_t dd, uintptr_t zs, uintptr_t ty, uintptr_t order, uintptr_t c,
+                                 uintptr_t keep, uintptr_t rot, uintptr_t cs, uintptr_t sn, uintptr_t meta,
+                                 uintptr_t K, uintptr_t S1, uintptr_t KS1, uintptr_t S2, uintptr_t KS2, uintptr_t D,
+                                 uintptr_t isK, uintptr_t rI, uintptr_t rJ, uintptr_t rC, uintptr_t rS,
+                                 uintptr_t st) {
+        stedc_level_prep(n, nm, maxs, P<const i64>(desc), P<const double>(rho), P<const double>(W),
+                         P<const double>(Z), P<double>(dd), P<double>(zs), P<int>(ty), P<i64>(order), P<i64>(c),
+                         P<int>(keep), P<int>(rot), P<double>(cs), P<double>(sn), reinterpret_cast<void*>(meta),
+                         P<i64>(K), P<i64>(S1), P<i64>(KS1), P<i64>(S2), P<i64>(KS2), P<i64>(D), P<i64>(isK),
+                         P<i64>(rI), P<i64>(rJ), P<double>(rC), P<double>(rS), S(st)); });
+    m.def("stedc_meta_bytes", []() { return (i64)stedc_meta_bytes(); });
+    m.def("stedc_lambda", [](i64 s_, uintptr_t dd, uintptr_t isK, uintptr_t dK, uintptr_t org, uintptr_t mu, int flip,
+                             uintptr_t lam, uintptr_t st) {
+        stedc_lambda(s_, P<const double>(dd), P<const i64>(isK), P<const double>(dK), P<const i64>(org),
+                     P<const double>(mu), flip, P<double>(lam), S(st)); });
+    m.def("stedc_merge2", [](uintptr_t lam, uintptr_t L1, i64 n1, uintptr_t L2, i64 n2, int rev, uintptr_t out,
+                             uintptr_t st) {
+        stedc_merge2(P<const double>(lam), P<const i64>(L1), n1, P<const i64>(L2), n2, rev, P<i64>(out), S(st)); });
+    m.def("cols_copy", [](i64 m_, i64 nc, uintptr_t A, i64 lda, uintptr_t idx, uintptr_t B, i64 ldb, int scatter,
+                          uintptr_t st) {
+        cols_copy(m_, nc, P<const double>(A), lda, P<const i64>(idx), P<double>(B), ldb, scatter != 0, S(st)); });
+    m.def("vec_gather", [](i64 n, uintptr_t x, uintptr_t idx, uintptr_t y, uintptr_t st) {
+        vec_gather(n, P<const double>(x), P<const i64>(idx), P<double>(y), S(st)); });
     m.def("lu_persist_profile", [](int enable) {
         unsigned long long v[8];
         lu_persist_profile(enable, v);

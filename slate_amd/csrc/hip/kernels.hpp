@@ -122,6 +122,20 @@ template <typename T> void trtri(char uplo, char diag, i64 n, T* A, i64 lda, i64
 template <typename T> void tri_inv(char uplo, char diag, i64 n, const T* A, i64 lda, T* W, i64 ldw, hipStream_t s);
 
 // stedc.hip
+// device-resident merges of one D&C tree level (stedc_level_prep: sort,
+// deflation, Givens runs, compacted index sets; meta = MergeMeta per merge)
+void stedc_level_prep(i64 n, i64 nm, i64 maxs, const i64* desc, const double* rho, const double* W, const double* Z,
+                      double* dd, double* zs, int* ty, i64* order, i64* c, int* keep, int* rot, double* cs,
+                      double* sn, void* meta, i64* K, i64* S1, i64* KS1, i64* S2, i64* KS2, i64* D, i64* isK,
+                      i64* rI, i64* rJ, double* rC, double* rS, hipStream_t s);
+size_t stedc_meta_bytes();
+void stedc_lambda(i64 s, const double* dd, const i64* isK, const double* dK, const i64* org, const double* mu,
+                  int flip, double* lam, hipStream_t st);
+void stedc_merge2(const double* lam, const i64* L1, i64 n1, const i64* L2, i64 n2, int rev, i64* out,
+                  hipStream_t st);
+void cols_copy(i64 m, i64 nc, const double* A, i64 lda, const i64* idx, double* B, i64 ldb, bool scatter,
+               hipStream_t st);
+void vec_gather(i64 n, const double* x, const i64* idx, double* y, hipStream_t st);
 void stedc_secular(i64 n, const double* d, const double* z, double rho, double zz, i64* org, double* mu,
                    double* zh, double* V, i64 ldv, hipStream_t s);
 void steqr_leaves(i64 nleaf, const i64* lo, const i64* hi, const double* d, const double* e, double* w, double* Q,

@@ -412,8 +412,9 @@ stedc_runs_kernel(i64 nn, const i64* __restrict__ c, const double* __restrict__ 
                   int* __restrict__ rot, int* __restrict__ keep) {
     const i64 t = (i64)blockIdx.x * 256 + threadIdx.x;
     if (t >= nn) return;
+    // rot[] is zeroed by the caller: a per-thread rot[t] = 0 here could land
+    // after another wave's run head has set rot[t] = 1
     const bool head = t == 0 || !(dd[c[t]] - dd[c[t - 1]] <= tol);
-    rot[t] = 0;
     if (!head) return;
     double acc = z[c[t]];
     int tacc = ty[c[t]];
@@ -495,5 +496,357 @@ void stedc_vectors(i64 n, const double* d, const double* zh, const i64* org, con
     HIP_LAUNCH_CHECK();
 }
 
+
+// ---------------------------------------------------------------------------
+// Device-resident merges (one host round trip per tree LEVEL): the sort,
+// deflation, Givens runs and every index set of all merges of a level are
+// formed on the device; the host reads back one small meta record per merge
+// (sizes) and launches the secular solver / split GEMMs with them.  Replaces
+// the torch argsort / where / index ops and the two host round trips per
+// merge of the former driver (stedc_solve.cc:79-238, laed2 / laed3 roles).
+//
+// Level arrays (length n, a merge [a, b) uses its own slice):
+//   dd, zs, ty   sorted poles, permuted z, column types (1 top, 2 bottom)
+//   order        local source column of sorted position
+//   c, keep, rot, cs, sn   deflation (compacted non-deflated positions)
+//   K, S1, KS1, S2, KS2, D, isK, rI, rJ, rC, rS   compacted index sets
+// desc[mi] = (a, m, b, flip); rho[mi] = |rho|; meta[mi] = MergeMeta.
+struct MergeMeta {
+    i64 nn, k, nrot, n1, n2, nd, pad0, pad1;
+    double tol, zzK;
+};
+
+namespace {
+// v of position t of a child's ascending sequence: [lo, hi) of W, reversed
+// and negated when flip
+__device__ inline double child_val(const double* W, i64 lo, i64 hi, int flip, i64 t) {
+    return flip ? -W[hi - 1 - t] : W[lo + t];
+}
+// number of elements of the child's sequence < v (strict) or <= v
+__device__ inline i64 count_below(const double* W, i64 lo, i64 hi, int flip, double v, bool inclusive) {
+    i64 l = 0, h = hi - lo;
+    while (l < h) {
+        const i64 mid = (l + h) >> 1;
+        const double x = child_val(W, lo, hi, flip, mid);
+        if (inclusive ? (x <= v) : (x < v)) l = mid + 1;
+        else h = mid;
+    }
+    return l;
+}
+
+// exclusive block scan of 0/1 flags for a 1024-thread workgroup; returns the
+// prefix of this thread, total in *tot (LDS)
+__device__ inline int block_scan_1024(int f, int* s_w, int* tot) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int v = f;
+    #pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(v, o, 64);
+        if (lane >= o) v += y;
+    }
+    if (lane == 63) s_w[w] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int i = 0; i < 16; ++i) { const int t = s_w[i]; s_w[i] = acc; acc += t; }
+        *tot = acc;
+    }
+    __syncthreads();
+    const int r = s_w[w] + v - f;
+    __syncthreads();
+    return r;
+}
+}  // namespace
+
+// sorted merge of the two children (each ascending; both reversed and
+// negated when rho < 0): one thread per element, its position = its rank in
+// its own child + its co-rank in the other (binary search)
+__global__ void __launch_bounds__(256)
+stedc_children_kernel(const i64* __restrict__ desc, const double* __restrict__ W, const double* __restrict__ Z,
+                      double* __restrict__ dd, double* __restrict__ zs, int* __restrict__ ty, i64* __restrict__ order) {
+    const i64* dm = desc + 4 * blockIdx.y;
+    const i64 a = dm[0], m = dm[1], b = dm[2];
+    const int flip = (int)dm[3];
+    const i64 i = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (i >= b - a) return;
+    const i64 na = m - a;
+    i64 pos, orig;
+    double v;
+    if (i < na) {
+        v = child_val(W, a, m, flip, i);
+        orig = flip ? m - 1 - i : a + i;
+        pos = i + count_below(W, m, b, flip, v, false);
+    } else {
+        const i64 u = i - na;
+        v = child_val(W, m, b, flip, u);
+        orig = flip ? b - 1 - u : m + u;
+        pos = u + count_below(W, a, m, flip, v, true);
+    }
+    dd[a + pos] = v;
+    zs[a + pos] = Z[orig];
+    ty[a + pos] = orig < m ? 1 : 2;
+    order[a + pos] = orig - a;
+}
+
+// per merge (one 1024-thread workgroup): tolerance, non-deflated positions
+__global__ void __launch_bounds__(1024)
+stedc_deflate_kernel(const i64* __restrict__ desc, const double* __restrict__ rho, const double* __restrict__ dd,
+                     const double* __restrict__ zs, i64* __restrict__ c, MergeMeta* __restrict__ meta) {
+    __shared__ double s_a[16], s_b[16];
+    __shared__ int s_w[16], s_tot;
+    __shared__ double s_tol, s_sq;
+    const i64* dm = desc + 4 * blockIdx.x;
+    const i64 a = dm[0], s = dm[2] - a;
+    const double r = rho[blockIdx.x];
+    double mx = 0.0, zz = 0.0;
+    for (i64 i = threadIdx.x; i < s; i += 1024) {
+        mx = fmax(mx, fabs(dd[a + i]));
+        zz += zs[a + i] * zs[a + i];
+    }
+    mx = wave_max(mx);
+    zz = wave_sum(zz);
+    if ((threadIdx.x & 63) == 0) { s_a[threadIdx.x >> 6] = mx; s_b[threadIdx.x >> 6] = zz; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double M = 0.0, S = 0.0;
+        for (int i = 0; i < 16; ++i) { M = fmax(M, s_a[i]); S += s_b[i]; }
+        s_tol = 8.0 * 2.220446049250313e-16 * fmax(M, r * S);
+        s_sq = sqrt(S);
+    }
+    __syncthreads();
+    const double tol = s_tol, sq = s_sq;
+    i64 base = 0;
+    for (i64 i0 = 0; i0 < s; i0 += 1024) {
+        const i64 i = i0 + threadIdx.x;
+        const int f = (i < s && !(r * fabs(zs[a + i]) * sq <= tol)) ? 1 : 0;
+        const int pre = block_scan_1024(f, s_w, &s_tot);
+        if (f) c[a + base + pre] = i;
+        base += s_tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) { meta[blockIdx.x].nn = base; meta[blockIdx.x].tol = tol; }
+}
+
+// close-pole Givens runs of every merge (stedc_runs_kernel on the merge's
+// slices, sizes from meta)
+__global__ void __launch_bounds__(256)
+stedc_runs_level_kernel(const i64* __restrict__ desc, const MergeMeta* __restrict__ meta, const i64* __restrict__ c,
+                        const double* __restrict__ dd, double* __restrict__ zs, int* __restrict__ ty,
+                        double* __restrict__ cs, double* __restrict__ sn, int* __restrict__ rot,
+                        int* __restrict__ keep) {
+    const i64 a = desc[4 * blockIdx.y];
+    const i64 nn = meta[blockIdx.y].nn;
+    const double tol = meta[blockIdx.y].tol;
+    const i64 t = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (t >= nn) return;
+    const i64* cc = c + a;
+    const double* d = dd + a;
+    double* z = zs + a;
+    int* tt = ty + a;
+    const bool head = t == 0 || !(d[cc[t]] - d[cc[t - 1]] <= tol);    // rot[] zeroed by the caller
+    if (!head) return;
+    double acc = z[cc[t]];
+    int tacc = tt[cc[t]];
+    i64 u = t + 1;
+    while (u < nn && d[cc[u]] - d[cc[u - 1]] <= tol) {
+        const double bb = z[cc[u]];
+        const double rr = hypot(acc, bb);
+        cs[a + u] = rr == 0.0 ? 1.0 : bb / rr;
+        sn[a + u] = rr == 0.0 ? 0.0 : acc / rr;
+        rot[a + u] = 1;
+        z[cc[u - 1]] = 0.0;
+        z[cc[u]] = rr;
+        tacc |= tt[cc[u]];
+        tt[cc[u]] = tacc;
+        keep[a + u - 1] = 0;
+        acc = rr;
+        ++u;
+    }
+    keep[a + u - 1] = 1;
+}
+
+// per merge (one 1024-thread workgroup): compacted index sets and sizes
+__global__ void __launch_bounds__(1024)
+stedc_compact_kernel(const i64* __restrict__ desc, MergeMeta* __restrict__ meta, const i64* __restrict__ c,
+                     const int* __restrict__ keep, const int* __restrict__ rot, const double* __restrict__ cs,
+                     const double* __restrict__ sn, const int* __restrict__ ty, const double* __restrict__ zs,
+                     i64* __restrict__ K, i64* __restrict__ S1, i64* __restrict__ KS1, i64* __restrict__ S2,
+                     i64* __restrict__ KS2, i64* __restrict__ D, i64* __restrict__ isK, i64* __restrict__ rI,
+                     i64* __restrict__ rJ, double* __restrict__ rC, double* __restrict__ rS) {
+    __shared__ int s_w[16], s_tot;
+    __shared__ double s_z[16];
+    const i64* dm = desc + 4 * blockIdx.x;
+    const i64 a = dm[0], s = dm[2] - a;
+    const i64 nn = meta[blockIdx.x].nn;
+    for (i64 i = threadIdx.x; i < s; i += 1024) isK[a + i] = 0;
+    __syncthreads();
+    i64 kb = 0, b1 = 0, b2 = 0, br = 0;
+    double zz = 0.0;
+    for (i64 t0 = 0; t0 < nn; t0 += 1024) {
+        const i64 t = t0 + threadIdx.x;
+        const bool live = t < nn;
+        const i64 col = live ? c[a + t] : 0;
+        const int kf = live && keep[a + t] ? 1 : 0;
+        const int tyv = kf ? ty[a + col] : 0;
+        const int rf = live && rot[a + t] ? 1 : 0;
+        const int pk = block_scan_1024(kf, s_w, &s_tot);
+        const int nk = s_tot;
+        const int f1 = (tyv & 1) ? 1 : 0, f2 = (tyv & 2) ? 1 : 0;
+        const int p1 = block_scan_1024(f1, s_w, &s_tot);
+        const int n1 = s_tot;
+        const int p2 = block_scan_1024(f2, s_w, &s_tot);
+        const int n2 = s_tot;
+        const int pr = block_scan_1024(rf, s_w, &s_tot);
+        const int nr = s_tot;
+        if (kf) {
+            const i64 j = kb + pk;
+            K[a + j] = col;
+            isK[a + col] = j + 1;
+            zz += zs[a + col] * zs[a + col];
+            if (f1) { S1[a + b1 + p1] = j; KS1[a + b1 + p1] = col; }
+            if (f2) { S2[a + b2 + p2] = j; KS2[a + b2 + p2] = col; }
+        }
+        if (rf) {
+            const i64 q = br + pr;
+            rI[a + q] = c[a + t - 1];
+            rJ[a + q] = col;
+            rC[a + q] = cs[a + t];
+            rS[a + q] = sn[a + t];
+        }
+        kb += nk; b1 += n1; b2 += n2; br += nr;
+    }
+    zz = wave_sum(zz);
+    if ((threadIdx.x & 63) == 0) s_z[threadIdx.x >> 6] = zz;
+    __syncthreads();
+    // deflated positions (not in K), ascending
+    i64 bd = 0;
+    for (i64 i0 = 0; i0 < s; i0 += 1024) {
+        const i64 i = i0 + threadIdx.x;
+        const int f = (i < s && isK[a + i] == 0) ? 1 : 0;
+        const int pre = block_scan_1024(f, s_w, &s_tot);
+        if (f) D[a + bd + pre] = i;
+        bd += s_tot;
+    }
+    if (threadIdx.x == 0) {
+        double z2 = 0.0;
+        for (int i = 0; i < 16; ++i) z2 += s_z[i];
+        MergeMeta& M = meta[blockIdx.x];
+        M.k = kb; M.n1 = b1; M.n2 = b2; M.nrot = br; M.nd = bd; M.zzK = z2;
+    }
+}
+
+// lam_i = root of K position (isK - 1) or the deflated pole dd_i; negated
+// when flip; the roots (K order) and the deflated poles (D order) are both
+// ascending before negation: the final order is their merge
+__global__ void __launch_bounds__(256)
+stedc_lambda_kernel(i64 s, const double* __restrict__ dd, const i64* __restrict__ isK, const double* __restrict__ dK,
+                    const i64* __restrict__ org, const double* __restrict__ mu, int flip, double* __restrict__ lam) {
+    const i64 i = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (i >= s) return;
+    const i64 j = isK[i] - 1;
+    const double v = j >= 0 ? dK[org[j]] + mu[j] : dd[i];
+    lam[i] = flip ? -v : v;
+}
+
+__device__ inline double list_val(const double* lam, const i64* L, i64 n, int rev, i64 t) {
+    return lam[L[rev ? n - 1 - t : t]];
+}
+__device__ inline i64 list_count(const double* lam, const i64* L, i64 n, int rev, double v, bool inclusive) {
+    i64 l = 0, h = n;
+    while (l < h) {
+        const i64 mid = (l + h) >> 1;
+        const double x = list_val(lam, L, n, rev, mid);
+        if (inclusive ? (x <= v) : (x < v)) l = mid + 1;
+        else h = mid;
+    }
+    return l;
+}
+
+// merge of two index lists, each ascending in lam (descending when rev):
+// out[pos] = index
+__global__ void __launch_bounds__(256)
+stedc_merge2_kernel(const double* __restrict__ lam, const i64* __restrict__ L1, i64 n1, const i64* __restrict__ L2,
+                    i64 n2, int rev, i64* __restrict__ out) {
+    const i64 i = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n1 + n2) return;
+    if (i < n1) {
+        const double v = list_val(lam, L1, n1, rev, i);
+        out[i + list_count(lam, L2, n2, rev, v, false)] = L1[rev ? n1 - 1 - i : i];
+    } else {
+        const i64 u = i - n1;
+        const double v = list_val(lam, L2, n2, rev, u);
+        out[u + list_count(lam, L1, n1, rev, v, true)] = L2[rev ? n2 - 1 - u : u];
+    }
+}
+
+// B[:, j] = A[:, idx[j]] (gather) or B[:, idx[j]] = A[:, j] (scatter)
+__global__ void __launch_bounds__(256)
+cols_copy_kernel(i64 m, i64 nc, const double* __restrict__ A, i64 lda, const i64* __restrict__ idx,
+                 double* __restrict__ B, i64 ldb, int scatter) {
+    const i64 r = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (r >= m) return;
+    for (i64 j = blockIdx.y; j < nc; j += gridDim.y) {
+        if (scatter) B[r + idx[j] * ldb] = A[r + j * lda];
+        else B[r + j * ldb] = A[r + idx[j] * lda];
+    }
+}
+
+// y[j] = x[idx[j]] (+ offset table for the eigenvalues)
+__global__ void __launch_bounds__(256)
+vec_gather_kernel(i64 n, const double* __restrict__ x, const i64* __restrict__ idx, double* __restrict__ y) {
+    const i64 j = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (j < n) y[j] = x[idx[j]];
+}
+
+void stedc_level_prep(i64 n, i64 nm, i64 maxs, const i64* desc, const double* rho, const double* W, const double* Z,
+                      double* dd, double* zs, int* ty, i64* order, i64* c, int* keep, int* rot, double* cs,
+                      double* sn, void* meta, i64* K, i64* S1, i64* KS1, i64* S2, i64* KS2, i64* D, i64* isK,
+                      i64* rI, i64* rJ, double* rC, double* rS, hipStream_t s) {
+    if (nm <= 0 || maxs <= 0) return;
+    MergeMeta* M = static_cast<MergeMeta*>(meta);
+    HIP_CHECK(hipMemsetAsync(rot, 0, sizeof(int) * (size_t)n, s));
+    const unsigned gx = (unsigned)((maxs + 255) / 256);
+    hipLaunchKernelGGL(stedc_children_kernel, dim3(gx, (unsigned)nm), dim3(256), 0, s, desc, W, Z, dd, zs, ty, order);
+    HIP_LAUNCH_CHECK();
+    hipLaunchKernelGGL(stedc_deflate_kernel, dim3((unsigned)nm), dim3(1024), 0, s, desc, rho, dd, zs, c, M);
+    HIP_LAUNCH_CHECK();
+    hipLaunchKernelGGL(stedc_runs_level_kernel, dim3(gx, (unsigned)nm), dim3(256), 0, s, desc, M, c, dd, zs, ty, cs,
+                       sn, rot, keep);
+    HIP_LAUNCH_CHECK();
+    hipLaunchKernelGGL(stedc_compact_kernel, dim3((unsigned)nm), dim3(1024), 0, s, desc, M, c, keep, rot, cs, sn, ty,
+                       zs, K, S1, KS1, S2, KS2, D, isK, rI, rJ, rC, rS);
+    HIP_LAUNCH_CHECK();
+}
+size_t stedc_meta_bytes() { return sizeof(MergeMeta); }
+
+void stedc_lambda(i64 s, const double* dd, const i64* isK, const double* dK, const i64* org, const double* mu,
+                  int flip, double* lam, hipStream_t st) {
+    if (s <= 0) return;
+    hipLaunchKernelGGL(stedc_lambda_kernel, dim3((unsigned)((s + 255) / 256)), dim3(256), 0, st, s, dd, isK, dK, org,
+                       mu, flip, lam);
+    HIP_LAUNCH_CHECK();
+}
+
+void stedc_merge2(const double* lam, const i64* L1, i64 n1, const i64* L2, i64 n2, int rev, i64* out,
+                  hipStream_t st) {
+    if (n1 + n2 <= 0) return;
+    hipLaunchKernelGGL(stedc_merge2_kernel, dim3((unsigned)((n1 + n2 + 255) / 256)), dim3(256), 0, st, lam, L1, n1,
+                       L2, n2, rev, out);
+    HIP_LAUNCH_CHECK();
+}
+
+void cols_copy(i64 m, i64 nc, const double* A, i64 lda, const i64* idx, double* B, i64 ldb, bool scatter,
+               hipStream_t st) {
+    if (m <= 0 || nc <= 0) return;
+    hipLaunchKernelGGL(cols_copy_kernel, dim3((unsigned)((m + 255) / 256), (unsigned)std::min<i64>(nc, 4096)),
+                       dim3(256), 0, st, m, nc, A, lda, idx, B, ldb, scatter ? 1 : 0);
+    HIP_LAUNCH_CHECK();
+}
+
+void vec_gather(i64 n, const double* x, const i64* idx, double* y, hipStream_t st) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(vec_gather_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, x, idx, y);
+    HIP_LAUNCH_CHECK();
+}
 
 }  // namespace slate_hip

@@ -113,9 +113,13 @@ def stedc_rows(d, e, comm=None, device=None, leaf=None):
         dl = _split_diag(d, e, levels)
         own = [(a, b) for (a, b) in leaves if a < r1 and b > r0] if P > 1 else leaves
         fails = _leaves(own, dl, e, w, Q, r0, r1, dev)
+        ws = _LevelWork(n, dev) if (dev.type == "cuda" and _DEVICE_MERGE) else None
         for t in range(len(levels) - 1, -1, -1):
             mine = [(a, m, b) for (a, m, b) in levels[t] if a < r1 and b > r0]
             W, Z = _level_inputs(levels[t], w, Q, r0, r1, comm, dev)
+            if ws is not None:
+                _merge_level_gpu(mine, e, W, Z, w, Q, r0, r1, ws)
+                continue
             for (a, m, b) in mine:
                 _merge(a, m, b, float(e[m - 1]), W, Z, w, Q, r0, r1, dev)
         _check_leaves(fails, comm if P > 1 else None)
@@ -189,6 +193,138 @@ def _level_inputs(merges, w, Q, r0, r1, comm, dev):
     if P > 1:
         comm.allreduce(buf)
     return W, Z
+
+
+# SLATE_AMD_STEDC_DEVICE_MERGE=0 selects the per-merge driver below (two
+# host round trips per merge, torch index ops) instead of the level-batched
+# device merge
+_DEVICE_MERGE = os.environ.get("SLATE_AMD_STEDC_DEVICE_MERGE", "1") != "0"
+# host round trips of the last stedc_rows call (tests)
+STEDC_STATS = {"host_syncs": 0, "levels": 0}
+
+
+class _LevelWork:
+    """Level-sized device arrays of the device merges (one slice [a, b) per
+    merge), allocated once per stedc call."""
+
+    def __init__(self, n, dev):
+        f64 = dict(dtype=torch.float64, device=dev)
+        i64 = dict(dtype=torch.int64, device=dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        nn = max(n, 1)
+        self.dd, self.zs, self.cs, self.sn, self.rC, self.rS, self.lam = (torch.empty(nn, **f64) for _ in range(7))
+        self.ty, self.keep, self.rot = (torch.empty(nn, **i32) for _ in range(3))
+        (self.order, self.c, self.K, self.S1, self.KS1, self.S2, self.KS2, self.D, self.isK, self.rI, self.rJ,
+         self.o2) = (torch.empty(nn, **i64) for _ in range(12))
+        self.dev = dev
+        self.meta_bytes = int(_hip().stedc_meta_bytes())
+        STEDC_STATS["host_syncs"] = 0
+        STEDC_STATS["levels"] = 0
+
+    def p(self, t, off=0):
+        return t.data_ptr() + off * t.element_size()
+
+
+def _merge_level_gpu(mine, e, W, Z, w, Q, r0, r1, ws):
+    """All merges of one tree level with the sort, deflation, close-pole
+    rotations and every index set formed on the device (stedc_level_prep,
+    csrc/hip/stedc.hip); ONE host read of the per-merge sizes, then per
+    merge: the rotations, the secular solve, laed3's split GEMM in CHUNK
+    column blocks and the final ordering (a two-list merge of the roots and
+    the deflated poles) -- all slate_hip kernels, no torch compute."""
+    if not mine:
+        return
+    H = _hip()
+    dev = ws.dev
+    st = torch.cuda.current_stream(dev).cuda_stream
+    nm = len(mine)
+    rhos = [float(e[m - 1]) for (_, m, _) in mine]
+    desc_h = np.asarray([(a, m, b, 1 if r < 0 else 0) for (a, m, b), r in zip(mine, rhos)], dtype=np.int64)
+    desc = _upload(desc_h.reshape(-1), dev)
+    rho_t = torch.from_numpy(np.abs(np.asarray(rhos, dtype=np.float64))).pin_memory().to(dev, non_blocking=True)
+    meta = torch.empty(nm * ws.meta_bytes, dtype=torch.uint8, device=dev)
+    maxs = max(b - a for (a, _, b) in mine)
+    n = W.numel()
+    H.stedc_level_prep(n, nm, maxs, desc.data_ptr(), rho_t.data_ptr(), W.data_ptr(), Z.data_ptr(), ws.p(ws.dd),
+                       ws.p(ws.zs), ws.p(ws.ty), ws.p(ws.order), ws.p(ws.c), ws.p(ws.keep), ws.p(ws.rot),
+                       ws.p(ws.cs), ws.p(ws.sn), meta.data_ptr(), ws.p(ws.K), ws.p(ws.S1), ws.p(ws.KS1),
+                       ws.p(ws.S2), ws.p(ws.KS2), ws.p(ws.D), ws.p(ws.isK), ws.p(ws.rI), ws.p(ws.rJ),
+                       ws.p(ws.rC), ws.p(ws.rS), st)
+    from ._util import read_to_host
+    mh = read_to_host(meta).numpy().view(np.uint8)          # the level's one host round trip
+    STEDC_STATS["host_syncs"] += 1
+    STEDC_STATS["levels"] += 1
+    rec = mh.reshape(nm, ws.meta_bytes)
+    ints = rec[:, :64].copy().view(np.int64).reshape(nm, 8)
+    dbl = rec[:, 64:80].copy().view(np.float64).reshape(nm, 2)
+    ldq = max(1, Q.stride(1))
+    for t, ((a, m, b), rho) in enumerate(zip(mine, rhos)):
+        _, k, nrot, n1, n2, nd = (int(x) for x in ints[t, :6])
+        zzK = float(dbl[t, 1])
+        flip = 1 if rho < 0 else 0
+        r = abs(rho)
+        s = b - a
+        lo, hi = max(a, r0), min(b, r1)
+        nr = hi - lo
+        qm = Q.data_ptr() + ((lo - r0) + a * ldq) * 8            # Q[lo - r0, a]
+        Qs = ops.colmajor_empty(nr, s, torch.float64, dev)
+        H.cols_copy(nr, s, qm, ldq, ws.p(ws.order, a), Qs.data_ptr(), max(1, nr), 0, st)
+        if nrot and nr:
+            H.rot_cols(nr, Qs.data_ptr(), max(1, nr), nrot, ws.p(ws.rI, a), ws.p(ws.rJ, a), ws.p(ws.rC, a),
+                       ws.p(ws.rS, a), st)
+        dK = torch.empty(max(k, 1), dtype=torch.float64, device=dev)
+        org = torch.empty(max(k, 1), dtype=torch.int64, device=dev)
+        mu = torch.empty(max(k, 1), dtype=torch.float64, device=dev)
+        if k:
+            zK = torch.empty(k, dtype=torch.float64, device=dev)
+            zh = torch.empty(k, dtype=torch.float64, device=dev)
+            H.vec_gather(k, ws.p(ws.dd, a), ws.p(ws.K, a), dK.data_ptr(), st)
+            H.vec_gather(k, ws.p(ws.zs, a), ws.p(ws.K, a), zK.data_ptr(), st)
+            H.stedc_secular(k, dK.data_ptr(), zK.data_ptr(), r, zzK, org.data_ptr(), mu.data_ptr(), zh.data_ptr(),
+                            0, 0, st)
+        H.stedc_lambda(s, ws.p(ws.dd, a), ws.p(ws.isK, a), dK.data_ptr(), org.data_ptr(), mu.data_ptr(), flip,
+                       ws.p(ws.lam, a), st)
+        if k and nr:
+            _merge_gemm_dev(H, ws, Qs, nr, a, k, lo, m, hi, n1, n2, dK, zh, org, mu, st)
+        H.stedc_merge2(ws.p(ws.lam, a), ws.p(ws.K, a), k, ws.p(ws.D, a), nd, flip, ws.p(ws.o2, a), st)
+        H.vec_gather(s, ws.p(ws.lam, a), ws.p(ws.o2, a), w.data_ptr() + a * 8, st)
+        H.cols_copy(nr, s, Qs.data_ptr(), max(1, nr), ws.p(ws.o2, a), qm, ldq, 0, st)
+
+
+def _merge_gemm_dev(H, ws, Qs, nr, a, k, lo, m, hi, n1, n2, dK, zh, org, mu, st):
+    """Qs[:, K] <- Qs[:, K] V in CHUNK column blocks, the rows above m with
+    the K columns nonzero there (S1 / KS1), the rows below with S2 / KS2
+    (the device-built sets of stedc_compact_kernel)."""
+    dev = ws.dev
+    parts = []
+    if lo < m:
+        parts.append((0, min(hi, m) - lo, n1, ws.S1, ws.KS1))
+    if hi > m:
+        parts.append((max(lo, m) - lo, nr, n2, ws.S2, ws.KS2))
+    srcs = []
+    for (ra, rb, ns, S, KS) in parts:
+        if ns == 0:
+            srcs.append(None)
+            continue
+        Ap = ops.colmajor_empty(rb - ra, ns, torch.float64, dev)
+        H.cols_copy(rb - ra, ns, Qs.data_ptr() + ra * 8, max(1, nr), ws.p(KS, a), Ap.data_ptr(), max(1, rb - ra), 0,
+                    st)
+        srcs.append(Ap)
+    for j0 in range(0, k, CHUNK):
+        nc = min(CHUNK, k - j0)
+        V = ops.colmajor_empty(k, nc, torch.float64, dev)
+        H.stedc_vectors(k, dK.data_ptr(), zh.data_ptr(), org.data_ptr(), mu.data_ptr(), j0, nc, V.data_ptr(),
+                        max(1, k), st)
+        for (ra, rb, ns, S, KS), Ap in zip(parts, srcs):
+            out = ops.colmajor_empty(rb - ra, nc, torch.float64, dev)
+            if Ap is not None:
+                Vp = ops.colmajor_empty(ns, nc, torch.float64, dev)
+                ops.row_gather(V, Vp, S[a:a + ns])
+                ops.gemm(1.0, Ap, Vp, 0.0, out)
+            else:
+                ops.geset(0.0, 0.0, out)
+            H.cols_copy(rb - ra, nc, out.data_ptr(), max(1, rb - ra), ws.p(ws.K, a + j0), Qs.data_ptr() + ra * 8,
+                        max(1, nr), 1, st)
 
 
 def _merge(a, m, b, rho, W, Z, w, Q, r0, r1, dev):

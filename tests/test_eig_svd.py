@@ -314,6 +314,46 @@ def test_stedc_gpu_secular(n, leaf):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("case", ["rand", "negative", "zero_e", "deflating", "clustered"])
+def test_stedc_device_merge_one_sync_per_level(monkeypatch, case):
+    """The level-batched device merges (sort, deflation, rotations and index
+    sets on the GPU: stedc_level_prep) read the host ONCE per tree level and
+    agree with the per-merge driver and an fp64 reference."""
+    from slate_amd.models import stedc as SD
+    n = 1500
+    g = torch.Generator().manual_seed(7)
+    d = torch.randn(n, dtype=torch.float64, generator=g)
+    e = torch.randn(n - 1, dtype=torch.float64, generator=g)
+    if case == "negative":
+        e = -e.abs()
+    elif case == "zero_e":
+        e[::97] = 0.0
+        e[500:700] = 0.0
+    elif case == "deflating":
+        d = torch.ones(n, dtype=torch.float64)
+        d[::3] = 2.0
+        e = torch.full((n - 1,), 1e-9, dtype=torch.float64)
+    elif case == "clustered":
+        d = torch.round(d * 4) / 4
+        e = e * 1e-3
+    T = torch.diag(d) + torch.diag(e, 1) + torch.diag(e, -1)
+    wr = torch.linalg.eigvalsh(T)
+    monkeypatch.setattr(SD, "_DEVICE_MERGE", True)
+    w, Z = sl.stedc(d, e, device="cuda", leaf=64)
+    syncs, levels = SD.STEDC_STATS["host_syncs"], SD.STEDC_STATS["levels"]
+    leaves, lv = SD._tree(n, 64)
+    assert levels == len(lv) and syncs == levels, (SD.STEDC_STATS, len(lv))
+    Z = Z.cpu()
+    tol = 1e-13 * n
+    assert (w - wr).abs().max() < tol * max(1.0, wr.abs().max())
+    assert (T @ Z - Z * w).abs().max() < tol * max(1.0, wr.abs().max())
+    assert (Z.T @ Z - torch.eye(n, dtype=torch.float64)).abs().max() < tol
+    monkeypatch.setattr(SD, "_DEVICE_MERGE", False)
+    w2, _ = sl.stedc(d, e, device="cuda", leaf=64)
+    assert (w - w2).abs().max() < tol * max(1.0, wr.abs().max())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("dt", [torch.float64, torch.complex128])
 @pytest.mark.parametrize("n,b", [(300, 32), (517, 64), (200, 64), (1000, 64)])
 def test_unmtr_hb2st_blocked_gpu(monkeypatch, dt, n, b):

@@ -20,8 +20,27 @@ int main(int argc, char** argv) {
     const int64_t n = argc > 2 ? std::atoll(argv[2]) : 384, nb = argc > 3 ? std::atoll(argv[3]) : 32;
     sn::initialize();
     const int me = sn::rank(), pr = me % p, pc = me / p;
-    if (argc > 4 && std::atoi(argv[4])) {          // warm-up factorization first
+    const int warm = argc > 4 ? std::atoi(argv[4]) : 0;
+    if (warm == 1) {                                  // warm-up factorization first
         sn::HermitianMatrix<double> W(sn::Uplo::Lower, 4 * nb * p, nb, p, q);
+        W.generate(sn::Gen::HermitianPositiveDefinite, 1);
+        sn::potrf(W);
+    } else if (warm == 2) {                           // one-tile potrf
+        sn::HermitianMatrix<double> W(sn::Uplo::Lower, nb, nb, p, q);
+        W.generate(sn::Gen::HermitianPositiveDefinite, 1);
+        sn::potrf(W);
+    } else if (warm == 3) {                           // SUMMA gemm
+        sn::Matrix<double> X1(2 * nb * p, 2 * nb * q, nb, p, q), X2(2 * nb * q, 2 * nb, nb, p, q),
+            X3(2 * nb * p, 2 * nb, nb, p, q);
+        X1.generate(sn::Gen::Random, 1);
+        X2.generate(sn::Gen::Random, 2);
+        sn::gemm(1.0, X1, X2, 0.0, X3);
+    } else if (warm == 4) {                           // norm (world all-reduce)
+        sn::Matrix<double> X1(2 * nb * p, 2 * nb * q, nb, p, q);
+        X1.generate(sn::Gen::Random, 1);
+        sn::norm(sn::Norm::Fro, X1);
+    } else if (warm == 5) {                           // two-tile potrf
+        sn::HermitianMatrix<double> W(sn::Uplo::Lower, 2 * nb, nb, p, q);
         W.generate(sn::Gen::HermitianPositiveDefinite, 1);
         sn::potrf(W);
     }
