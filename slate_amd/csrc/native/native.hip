@@ -34,6 +34,7 @@
 
 #include "../hip/kernels.hpp"
 #include "../hip/launchers.hpp"
+#include "../hip/workspace.hpp"
 #include "native_rt.hpp"
 
 namespace slate_amd {
@@ -398,6 +399,40 @@ void assemble_cols(const ColPlan& P, const i64* idx, const T* Prow, i64 ldp, i64
                                          idx + P.order_off, s);
 }
 
+// diagnostics (SLATE_AMD_NATIVE_TRACE=1): synchronise s and print the sum
+// of |x| over an m x n block
+template <typename T>
+void dbg_sum(const char* tag, i64 t, const T* A, i64 ld, i64 m, i64 n, hipStream_t s) {
+    static const bool on = env_int("SLATE_AMD_NATIVE_TRACE", 0) != 0;
+    if (!on) return;
+    NHIP(hipStreamSynchronize(s));
+    double acc = 0;
+    if (m > 0 && n > 0) {
+        std::vector<T> h((size_t)ld * n);
+        NHIP(hipMemcpy(h.data(), A, sizeof(T) * ((size_t)ld * (n - 1) + m), hipMemcpyDeviceToHost));
+        for (i64 j = 0; j < n; ++j)
+            for (i64 i = 0; i < m; ++i) acc += std::abs(h[i + j * ld]);
+    }
+    // the same block read by a KERNEL (one-norm column sums, genorm) -- a
+    // copy engine reads memory, a kernel may read stale cache lines
+    double kacc = 0;
+    if constexpr (std::is_same<T, double>::value) {
+        if (m > 0 && n > 0) {
+            double* d = nullptr;
+            NHIP(hipMalloc(&d, sizeof(double) * (n + m)));
+            NHIP(hipMemset(d, 0, sizeof(double) * (n + m)));
+            slate_hip::genorm<double, double>('1', 'G', 'N', 0, m, n, A, ld, d, s);
+            std::vector<double> h2((size_t)(n + m));
+            NHIP(hipStreamSynchronize(s));
+            NHIP(hipMemcpy(h2.data(), d, sizeof(double) * (n + m), hipMemcpyDeviceToHost));
+            NHIP(hipFree(d));
+            for (i64 j = 0; j < n; ++j) kacc += h2[j];
+        }
+    }
+    std::fprintf(stderr, "TRACE r%d t=%lld %s %lldx%lld %.17g kernel %.17g\n", rt().rank, (long long)t, tag,
+                 (long long)m, (long long)n, acc, kacc);
+}
+
 // tile Cholesky / panel solve: the tuned fp64 kernels, the generic ones else
 template <typename T>
 void potrf_tile_k(i64 n, T* A, i64 lda, i64* info, hipStream_t s) {
@@ -527,7 +562,9 @@ static void potrf_grid(Storage& S, int la, i64* infos) {
         const i64 lc1 = std::min(tiles_before(g + 1, q, pc) * nb, lc_end);
         const bool own_col = (g % q) == pc, own_diag = own_col && (g % p) == pr;
         if (t - la - 1 >= 0) ev_tr[t - la - 1]->wait(ps);
+        if (own_diag) dbg_sum("diag_in", t, buf + lrg + lcg * lld, lld, kb, kb, ps);
         if (own_diag) potrf_tile_k<T>(kb, buf + lrg + lcg * lld, lld, infos + t, ps);
+        if (own_diag) dbg_sum("diag_out", t, buf + lrg + lcg * lld, lld, kb, kb, ps);
         const i64 nrow = lr_end - lr1;
         if (own_col) {
             const T* D = buf + lrg + lcg * lld;
@@ -539,7 +576,13 @@ static void potrf_grid(Storage& S, int la, i64* infos) {
                 D = Dt.as<T>();
                 ldd = kb;
             }
+            dbg_sum("D", t, D, ldd, kb, kb, ps);
+            dbg_sum("panel_in", t, buf + lr1 + lcg * lld, lld, nrow, kb, ps);
             if (nrow) trsm_rlc<T>(nrow, kb, D, ldd, buf + lr1 + lcg * lld, lld, ps);
+            dbg_sum("panel_out", t, buf + lr1 + lcg * lld, lld, nrow, kb, ps);
+            if (env_int("SLATE_AMD_NATIVE_TRACE", 0) && nrow)
+                dbg_sum("Winv", t, static_cast<double*>(slate_hip::workspace(ps, sizeof(double) * 1024, slate_hip::WS_C)),
+                        1024, 1024, 1, ps);
         }
         // panel -> row (Prow: nrow x kb, contiguous), tile-granular chunks
         Scratch* Prow = ring_p[t % NR].get();
@@ -589,6 +632,7 @@ static void potrf_grid(Storage& S, int la, i64* infos) {
             lda_la = ldp;
         }
         const i64 lc_la = std::min(tiles_before(g + 1 + la, q, pc) * nb, lc_end);
+        dbg_sum("La", t, La, lda_la, lc_la - lc1, kb, ps);
         if (t >= 1 && la > 0) ev_tr[t - 1]->wait(ps);
         for (size_t ci = 0; ci < chunks.size(); ++ci) {
             if (ci) land(ci);
@@ -599,6 +643,7 @@ static void potrf_grid(Storage& S, int la, i64* infos) {
                           buf + lr1 + a + lc1 * lld, lld, ps, &mk);
             }
         }
+        dbg_sum("la_out", t, buf + lr1 + lc1 * lld, lld, nrow, lc_la - lc1, ps);
         const T* Lc;
         i64 ldlc, loff;
         if (p > 1 || q > 1) {
@@ -1051,10 +1096,10 @@ int64_t getrf(Matrix<T>& A, std::vector<int64_t>& ipiv_out, const Options& opts)
                 panel_dist<T>(S, k, kb, lck, ipiv_d, infos.as<i64>() + k, opts.pivot_threshold,
                               opts.inner_blocking, Tt, gall.as<i64>() + goff[k], ps);
                 copy2d(Lp, std::max<i64>(nmine, 1), buf + lr_k + lck * lld, lld, nmine, kb, ps);
-                NHIP(hipMemcpyAsync(pv, ipiv_d + r0, (size_t)kb * sizeof(i64), hipMemcpyDeviceToDevice, ps));
+                dcopy(pv, ipiv_d + r0, (size_t)kb * sizeof(i64), ps);
             }
             if (q > 1) rowc->bcast(pack.p, lbytes + tbytes + (size_t)kb * sizeof(i64), ck, ps);
-            NHIP(hipMemcpyAsync(ipiv_d + r0, pv, (size_t)kb * sizeof(i64), hipMemcpyDeviceToDevice, ps));
+            dcopy(ipiv_d + r0, pv, (size_t)kb * sizeof(i64), ps);
             // every local column except the panel's own: interchanges, then
             // (trailing columns) U rows and the update
             auto trailing = [&](i64 c0, i64 c1) {

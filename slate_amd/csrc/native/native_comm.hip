@@ -122,7 +122,7 @@ public:
     }
     void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
         if (size == 1) {
-            if (recv != send && bytes) NHIP(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, s));
+            if (recv != send && bytes) dcopy(recv, send, bytes, s);
             return;
         }
         if (bytes) NCCL(ncclAllGather(send, recv, bytes, ncclUint8, c, s));

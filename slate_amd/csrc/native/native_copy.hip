@@ -1,0 +1,68 @@
+// Host -> device and device -> device byte copies of the native runtime BY
+// KERNEL.  A copy-engine write into device memory whose lines a kernel on
+// another XCD read earlier was not seen by the next kernel on this stack
+// (gfx950: eight XCDs with their own L2): the first potrf_grid of a process
+// got a received diagonal tile with stale lines in the triangular inverse
+// (tools/probe/scal_probe.cc, profiles/r4/native_first_call.md).  A kernel
+// that reads the source and stores the destination keeps every write on the
+// normal L2 write-back / invalidate path of kernel boundaries.
+#include <cstring>
+#include <mutex>
+
+#include "native_rt.hpp"
+
+namespace slate_amd {
+namespace native {
+
+__global__ void __launch_bounds__(256)
+copy_words_kernel(const unsigned long long* __restrict__ src, unsigned long long* __restrict__ dst, size_t nw) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nw; i += (size_t)gridDim.x * 256) dst[i] = src[i];
+}
+
+__global__ void __launch_bounds__(256)
+copy_bytes_kernel(const unsigned char* __restrict__ src, unsigned char* __restrict__ dst, size_t nb) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nb; i += (size_t)gridDim.x * 256) dst[i] = src[i];
+}
+
+static void launch_copy(void* d, const void* s, size_t bytes, hipStream_t st) {
+    if (!bytes) return;
+    const bool words = ((reinterpret_cast<uintptr_t>(d) | reinterpret_cast<uintptr_t>(s) | bytes) & 7) == 0;
+    const size_t n = words ? bytes / 8 : bytes;
+    const unsigned g = (unsigned)std::min<size_t>((n + 255) / 256, 4096);
+    if (words)
+        hipLaunchKernelGGL(copy_words_kernel, dim3(g), dim3(256), 0, st,
+                           static_cast<const unsigned long long*>(s), static_cast<unsigned long long*>(d), n);
+    else
+        hipLaunchKernelGGL(copy_bytes_kernel, dim3(g), dim3(256), 0, st, static_cast<const unsigned char*>(s),
+                           static_cast<unsigned char*>(d), n);
+    NHIP(hipGetLastError());
+}
+
+// pinned staging buffer (grown on demand; one upload at a time: the caller's
+// stream is synchronised before the buffer is reused)
+static std::mutex g_pin_mu;
+static void* g_pin = nullptr;
+static size_t g_pin_cap = 0;
+
+void upload(void* d, const void* h, size_t bytes, hipStream_t s) {
+    if (!bytes) {
+        NHIP(hipStreamSynchronize(s));
+        return;
+    }
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    if (g_pin_cap < bytes) {
+        if (g_pin) NHIP(hipHostFree(g_pin));
+        g_pin_cap = std::max(bytes, (size_t)1 << 20);
+        NHIP(hipHostMalloc(&g_pin, g_pin_cap, hipHostMallocDefault));
+    }
+    std::memcpy(g_pin, h, bytes);
+    void* dp = nullptr;
+    NHIP(hipHostGetDevicePointer(&dp, g_pin, 0));
+    launch_copy(d, dp, bytes, s);
+    NHIP(hipStreamSynchronize(s));
+}
+
+void dcopy(void* d, const void* s, size_t bytes, hipStream_t st) { launch_copy(d, s, bytes, st); }
+
+}  // namespace native
+}  // namespace slate_amd

@@ -155,14 +155,11 @@ struct Event {
     void wait(hipStream_t s) const { NHIP(hipStreamWaitEvent(s, e, 0)); }
 };
 
-// host -> device upload of a small pageable host array, complete on return
-// (a pageable async copy is not reliably ordered before the next kernels of
-// the stream on this stack: the first potrf_grid read stale plan indices --
-// tools/probe/scal_probe.cc)
-inline void upload(void* d, const void* h, size_t bytes, hipStream_t s) {
-    if (bytes) NHIP(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s));
-    NHIP(hipStreamSynchronize(s));
-}
+// host -> device upload, complete on return, and device -> device copies:
+// kernel copies (native_copy.hip) -- never a copy-engine write into device
+// memory that kernels on other XCDs may hold in their L2
+void upload(void* d, const void* h, size_t bytes, hipStream_t s);
+void dcopy(void* d, const void* src, size_t bytes, hipStream_t s);
 
 // stream b waits for everything issued so far on stream a
 inline void join(hipStream_t a, hipStream_t b) {

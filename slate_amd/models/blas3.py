@@ -809,10 +809,10 @@ def _tri_left(kind, alpha, A, B, slot, opts):
     A = _tri_work(A, B, slot)
     if kind == "sm" and _trsm_method(B, opts) == MethodTrsm.A:
         return _trsmA_left(alpha, A, B, slot)
-    return _tri_left_panels(kind, alpha, A, B, slot)
+    return _tri_left_panels(kind, alpha, A, B, slot, opts)
 
 
-def _tri_left_panels(kind, alpha, A, B, slot):
+def _tri_left_panels(kind, alpha, A, B, slot, opts=None):
     """Stationary-B Left trmm / trsm (src/work/work_trmm.cc,
     src/work/work_trsm.cc:102-265) with A and B tile-row aligned.  Step k:
     the block column A(:, k) goes along each process row (one row
@@ -839,27 +839,56 @@ def _tri_left_panels(kind, alpha, A, B, slot):
     if solve and alpha != 1 and mloc and nloc:
         ops.gescale(alpha, lbB.data)
     forward = lower if solve else not lower
-    for k in (range(mt) if forward else range(mt - 1, -1, -1)):
+    steps = list(range(mt) if forward else range(mt - 1, -1, -1))
+    # lookahead (SLATE work_trsm's lookahead tasks, work_trsm.cc:102-265):
+    # the A block column of step k + 1 .. k + la travels along the process
+    # row on the panel stream (the row communicator's one stream) while the
+    # solve / column broadcast / GEMM of step k run on the update stream (the
+    # column communicator's) -- A never depends on B, so the prefetch is
+    # always legal
+    la = max(0, int(get_option(opts, Option.Lookahead, 1)))
+    ss = StreamSet(dev, reserve_cus=0)
+    ss.fork()
+    us = ss.update[0]
+    fetched = {}
+
+    def fetch(i):
+        k = steps[i]
+        kb = B.tileMb(k)
+        lc = tiles_local_before(k, q, pc) * nb - lbA.col_off
+        with ss.use(ss.panel):
+            src = lbA.data[:, lc:lc + kb] if k % q == pc else None
+            P = row_bcast(grid, src, k % q, mloc, kb, dt, dev)
+            fetched[i] = (P, ss.event(ss.panel))
+
+    for i in range(min(la + 1, len(steps))):
+        fetch(i)
+    for i, k in enumerate(steps):
+        Prow, ev = fetched.pop(i)
         kb = B.tileMb(k)
         lrk = tiles_local_before(k, p, pr) * nb
         own = k % p == pr
-        lc = tiles_local_before(k, q, pc) * nb - lbA.col_off
-        src = lbA.data[:, lc:lc + kb] if k % q == pc else None
-        Prow = row_bcast(grid, src, k % q, mloc, kb, dt, dev)
         r0, r1 = (tiles_local_before(k + 1, p, pr) * nb, mloc) if lower else (0, lrk)
-        Bk = lbB.data[lrk:lrk + kb, :] if own else None
-        if solve:
-            if own and nloc:
-                ops.trsm('L', upl, 'N', diag, 1.0, Prow[lrk:lrk + kb], Bk)
-            Xk = col_bcast(grid, Bk, k % p, kb, nloc, dt, dev)
-            if r1 > r0 and nloc:
-                ops.gemm(-1.0, Prow[r0:r1], Xk, 1.0, lbB.data[r0:r1])
-        else:
-            Xk = col_bcast(grid, Bk, k % p, kb, nloc, dt, dev)
-            if r1 > r0 and nloc:
-                ops.gemm(alpha, Prow[r0:r1], Xk, 1.0, lbB.data[r0:r1])
-            if own and nloc:
-                ops.trmm('L', upl, 'N', diag, alpha, Prow[lrk:lrk + kb], Bk)
+        with ss.use(us):
+            ss.wait(us, ev)
+            if Prow is not None and Prow.is_cuda:
+                Prow.record_stream(us)
+            Bk = lbB.data[lrk:lrk + kb, :] if own else None
+            if solve:
+                if own and nloc:
+                    ops.trsm('L', upl, 'N', diag, 1.0, Prow[lrk:lrk + kb], Bk)
+                Xk = col_bcast(grid, Bk, k % p, kb, nloc, dt, dev)
+                if r1 > r0 and nloc:
+                    ops.gemm(-1.0, Prow[r0:r1], Xk, 1.0, lbB.data[r0:r1])
+            else:
+                Xk = col_bcast(grid, Bk, k % p, kb, nloc, dt, dev)
+                if r1 > r0 and nloc:
+                    ops.gemm(alpha, Prow[r0:r1], Xk, 1.0, lbB.data[r0:r1])
+                if own and nloc:
+                    ops.trmm('L', upl, 'N', diag, alpha, Prow[lrk:lrk + kb], Bk)
+        if i + la + 1 < len(steps):
+            fetch(i + la + 1)
+    ss.join()
     _done(B)
     return B
 
