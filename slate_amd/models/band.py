@@ -20,10 +20,11 @@ slab of its band tiles):
   columns cannot share a launch).  The owner of column k + 1 updates it
   first, so its next panel overlaps the other ranks' updates.  Cost
   O(n kl (kl + ku)), memory O(n (kl + ku)).
-* solves: the right-hand side is replicated (O(n nrhs), vectors only) and
-  swept tile by tile; the owner of each factor column applies it and
-  broadcasts the rows it changed (kb + bandwidth rows), so every rank's
-  copy stays exact; each rank finally keeps its own part of B.
+* solves: the right-hand side stays 1-D row-cyclic over the ranks (tile
+  row i with the owner of band column i); each step's window of kb +
+  bandwidth rows is gathered point-to-point onto the owner of the factor
+  column, solved / updated there and scattered back (_DistX) -- per-rank
+  memory O(local rows + one window), never the replicated n x nrhs B.
 * products: B and C move to 1-D row-cyclic work layouts matched to the
   band's column ownership (one redistribution each); each rank multiplies
   its slabs and the partial blocks travel point-to-point to the owners of
@@ -147,17 +148,6 @@ def _cm_copy(D, dev):
     return X
 
 
-def _replicated(B, dev):
-    """B (thin right-hand side) replicated on every rank, column-major."""
-    from .aux import allgather_dense
-    return _cm_copy(allgather_dense(B), dev)
-
-
-def _store(B, X):
-    from .aux import from_dense
-    from_dense(B, X)
-
-
 # ------------------------------------------------------------------ LU
 def gbtrf(A, pivots: Pivots, opts=None) -> int:
     """Band LU with partial pivoting (pivots: global 0-based rows).  The
@@ -226,9 +216,90 @@ def gbtrf(A, pivots: Pivots, opts=None) -> int:
         return info
 
 
-def _lower_fwd(s, buf, X, kd, unit, gpiv=None):
+class _DistX:
+    """A right-hand side kept 1-D row-cyclic over the band's ranks (tile row
+    i on rank i % Q, the owner of band tile column i): the triangular sweeps
+    move only the rows of each step's window -- gathered point-to-point onto
+    the column's owner, solved / updated there, scattered back -- so no rank
+    ever holds the n x nrhs right-hand side (the former solves replicated
+    it, docs/INVENTORY.md).  Per-rank workspace: the local rows plus one
+    window of (kb + bandwidth) rows."""
+
+    def __init__(self, B, s, dev):
+        from ..parallel.redist import redistribute_pieces
+        self.s, self.dev = s, dev
+        self.dt = s.dtype
+        self.m, self.w = B.m(), B.n()
+        self.M = _row_cyclic(self.m, self.w, s, self.dt, dev)
+        redistribute_pieces(B, self.M)
+        self.X = self.M.local_block().data
+        self.peak = 0
+
+    def segs(self, lo, hi):
+        nb, Q = self.s.band_nb, self.s.Q
+        for t in range(lo // nb, -(-hi // nb)):
+            a, b = max(lo, t * nb), min(hi, (t + 1) * nb)
+            if b > a:
+                yield t % Q, a, b, _lrow(self.s, t) + a - t * nb
+
+    def gather(self, lo, hi, root):
+        """rows [lo, hi) on ``root`` (None elsewhere)"""
+        me = self.s.rank
+        W = ops.colmajor_empty(hi - lo, self.w, self.dt, self.dev) if me == root else None
+        sends, shapes, dest = {}, {}, {}
+        for r, a, b, l in self.segs(lo, hi):
+            if r == root:
+                if me == root:
+                    W[a - lo:b - lo].copy_(self.X[l:l + b - a])
+            elif me == r:
+                sends.setdefault(root, []).append(self.X[l:l + b - a])
+            elif me == root:
+                shapes.setdefault(r, []).append((b - a, self.w))
+                dest.setdefault(r, []).append(a - lo)
+        got = _exchange_pieces(self.s, sends, shapes, self.dt, self.dev)
+        for r, lst in got.items():
+            for t, o in zip(lst, dest[r]):
+                W[o:o + t.shape[0]].copy_(t)
+        if W is not None:
+            self.peak = max(self.peak, W.numel())
+        return W
+
+    def scatter(self, W, lo, hi, root):
+        me = self.s.rank
+        sends, shapes, dest = {}, {}, {}
+        for r, a, b, l in self.segs(lo, hi):
+            if r == root:
+                if me == root:
+                    self.X[l:l + b - a].copy_(W[a - lo:b - lo])
+            elif me == root:
+                sends.setdefault(r, []).append(W[a - lo:b - lo])
+            elif me == r:
+                shapes.setdefault(root, []).append((b - a, self.w))
+                dest.setdefault(root, []).append(l)
+        got = _exchange_pieces(self.s, sends, shapes, self.dt, self.dev)
+        for r, lst in got.items():
+            for t, l in zip(lst, dest[r]):
+                self.X[l:l + t.shape[0]].copy_(t)
+
+    def store(self, B):
+        from ..parallel.redist import redistribute_pieces
+        self.M.storage.mark_local_modified(self.M.storage.origin_slot)
+        redistribute_pieces(self.M, B)
+
+
+# per-rank peak window (elements) of the last band solve (tests)
+BAND_SOLVE_STATS = {"window_elems": 0, "local_elems": 0}
+
+
+def _note(Xd):
+    BAND_SOLVE_STATS["window_elems"] = max(BAND_SOLVE_STATS["window_elems"], Xd.peak)
+    BAND_SOLVE_STATS["local_elems"] = max(BAND_SOLVE_STATS["local_elems"], Xd.X.numel())
+
+
+def _lower_fwd(s, buf, Xd, kd, unit, gpiv=None):
     """X := L^{-1} X (L lower band, bandwidth kd, in the slabs; with gbtrf
-    pivots applied step by step when gpiv is given).  Right-looking."""
+    pivots applied step by step when gpiv is given).  Right-looking: the
+    window [r0, r0 + kb + kd) goes to the owner of column k and back."""
     n, nb, Q, me = s.n, s.band_nb, s.Q, s.rank
     diag = 'U' if unit else 'N'
     for k in range(-(-min(s.m, n) // nb)):
@@ -236,17 +307,19 @@ def _lower_fwd(s, buf, X, kd, unit, gpiv=None):
         kb = min(nb, n - r0)
         rend = min(n, r0 + kb + kd)
         owner = k % Q
+        W = Xd.gather(r0, rend, owner)
         if me == owner:
             if gpiv is not None:
-                ops.laswp(X, gpiv, r0, r0 + kb)
+                ops.laswp(W, gpiv[r0:r0 + kb], 0, kb, ioff=r0)
             Pk = _col_block(s, buf, k, r0, rend)[:, :kb]
-            ops.trsm('L', 'L', 'N', diag, 1.0, Pk[:kb], X[r0:r0 + kb])
+            ops.trsm('L', 'L', 'N', diag, 1.0, Pk[:kb], W[:kb])
             if rend > r0 + kb:
-                ops.gemm(-1.0, Pk[kb:], X[r0:r0 + kb], 1.0, X[r0 + kb:rend])
-        _bcast_rows(s.comm, X, r0, rend, owner)
+                ops.gemm(-1.0, Pk[kb:], W[:kb], 1.0, W[kb:])
+        Xd.scatter(W, r0, rend, owner)
+    _note(Xd)
 
 
-def _lower_bwd_op(s, buf, X, kd, unit, opch):
+def _lower_bwd_op(s, buf, Xd, kd, unit, opch):
     """X := op(L)^{-1} X, op = T or C: left-looking, last tile first."""
     n, nb, Q, me = s.n, s.band_nb, s.Q, s.rank
     diag = 'U' if unit else 'N'
@@ -255,15 +328,17 @@ def _lower_bwd_op(s, buf, X, kd, unit, opch):
         kb = min(nb, n - r0)
         rend = min(n, r0 + kb + kd)
         owner = k % Q
+        W = Xd.gather(r0, rend, owner)
         if me == owner:
             Pk = _col_block(s, buf, k, r0, rend)[:, :kb]
             if rend > r0 + kb:
-                ops.gemm(-1.0, Pk[kb:], X[r0 + kb:rend], 1.0, X[r0:r0 + kb], transA=opch)
-            ops.trsm('L', 'L', opch, diag, 1.0, Pk[:kb], X[r0:r0 + kb])
-        _bcast_rows(s.comm, X, r0, r0 + kb, owner)
+                ops.gemm(-1.0, Pk[kb:], W[kb:], 1.0, W[:kb], transA=opch)
+            ops.trsm('L', 'L', opch, diag, 1.0, Pk[:kb], W[:kb])
+        Xd.scatter(W[:kb] if W is not None else None, r0, r0 + kb, owner)
+    _note(Xd)
 
 
-def _upper_bwd(s, buf, X, ku, unit):
+def _upper_bwd(s, buf, Xd, ku, unit):
     """X := U^{-1} X (U upper band, bandwidth ku): right-looking, last tile first."""
     n, nb, Q, me = s.n, s.band_nb, s.Q, s.rank
     diag = 'U' if unit else 'N'
@@ -272,15 +347,17 @@ def _upper_bwd(s, buf, X, ku, unit):
         kb = min(nb, n - r0)
         top = max(0, r0 - ku)
         owner = k % Q
+        W = Xd.gather(top, r0 + kb, owner)
         if me == owner:
             Uk = _col_block(s, buf, k, top, r0 + kb)[:, :kb]
-            ops.trsm('L', 'U', 'N', diag, 1.0, Uk[r0 - top:], X[r0:r0 + kb])
+            ops.trsm('L', 'U', 'N', diag, 1.0, Uk[r0 - top:], W[r0 - top:])
             if r0 > top:
-                ops.gemm(-1.0, Uk[:r0 - top], X[r0:r0 + kb], 1.0, X[top:r0])
-        _bcast_rows(s.comm, X, top, r0 + kb, owner)
+                ops.gemm(-1.0, Uk[:r0 - top], W[r0 - top:], 1.0, W[:r0 - top])
+        Xd.scatter(W, top, r0 + kb, owner)
+    _note(Xd)
 
 
-def _upper_fwd_op(s, buf, X, ku, unit, opch):
+def _upper_fwd_op(s, buf, Xd, ku, unit, opch):
     """X := op(U)^{-1} X, op = T or C: left-looking, first tile first."""
     n, nb, Q, me = s.n, s.band_nb, s.Q, s.rank
     diag = 'U' if unit else 'N'
@@ -289,12 +366,14 @@ def _upper_fwd_op(s, buf, X, ku, unit, opch):
         kb = min(nb, n - r0)
         top = max(0, r0 - ku)
         owner = k % Q
+        W = Xd.gather(top, r0 + kb, owner)
         if me == owner:
             Uk = _col_block(s, buf, k, top, r0 + kb)[:, :kb]
             if r0 > top:
-                ops.gemm(-1.0, Uk[:r0 - top], X[top:r0], 1.0, X[r0:r0 + kb], transA=opch)
-            ops.trsm('L', 'U', opch, diag, 1.0, Uk[r0 - top:], X[r0:r0 + kb])
-        _bcast_rows(s.comm, X, r0, r0 + kb, owner)
+                ops.gemm(-1.0, Uk[:r0 - top], W[:r0 - top], 1.0, W[r0 - top:], transA=opch)
+            ops.trsm('L', 'U', opch, diag, 1.0, Uk[r0 - top:], W[r0 - top:])
+        Xd.scatter(W[r0 - top:] if W is not None else None, r0, r0 + kb, owner)
+    _note(Xd)
 
 
 def gbtrs(A, pivots, B, opts=None):
@@ -303,10 +382,11 @@ def gbtrs(A, pivots, B, opts=None):
     with trace_block("gbtrs"):
         s, slot, buf = _slab(A)
         kl, kuf = _bands(A)                 # after gbtrf: ku = kl + ku (fill)
-        X = _replicated(B, buf.device)
-        _lower_fwd(s, buf, X, kl, True, pivots.device(buf.device))
-        _upper_bwd(s, buf, X, kuf, False)
-        _store(B, X)
+        BAND_SOLVE_STATS.update(window_elems=0, local_elems=0)
+        Xd = _DistX(B, s, buf.device)
+        _lower_fwd(s, buf, Xd, kl, True, pivots.device(buf.device))
+        _upper_bwd(s, buf, Xd, kuf, False)
+        Xd.store(B)
         return 0
 
 
@@ -423,10 +503,11 @@ def pbtrs(A, B, opts=None):
             raise SlateError("pbtrs: factor with pbtrf first")
         s, slot, buf = _slab(L)
         kd = L.bandwidth()
-        X = _replicated(B, buf.device)
-        _lower_fwd(s, buf, X, kd, False)
-        _lower_bwd_op(s, buf, X, kd, False, conj_trans(s.dtype))
-        _store(B, X)
+        BAND_SOLVE_STATS.update(window_elems=0, local_elems=0)
+        Xd = _DistX(B, s, buf.device)
+        _lower_fwd(s, buf, Xd, kd, False)
+        _lower_bwd_op(s, buf, Xd, kd, False, conj_trans(s.dtype))
+        Xd.store(B)
         return 0
 
 
@@ -450,41 +531,38 @@ def tbsm(side, alpha, A, B, pivots=None, opts=None):
         opA = A.op()
         unit = getattr(A, "_diag", Diag.NonUnit) == Diag.Unit
         kd = A._kl if up == Uplo.Lower else A._ku
+        BAND_SOLVE_STATS.update(window_elems=0, local_elems=0)
         if side == Side.Right:
-            # X op(A) = alpha B  <=>  op(A)^T X^T = alpha B^T
-            from .aux import allgather_dense, from_dense
-            Bt = allgather_dense(B).mT.to(buf.device)
-            X = ops.colmajor_empty(Bt.shape[0], Bt.shape[1], Bt.dtype, buf.device)
-            X.copy_(Bt)
+            # X op(A) = alpha B  <=>  op(A)^T X^T = alpha B^T: B^T goes to the
+            # row-cyclic layout by one transposing redistribution
+            from .blas3 import _copy_out
             opT = {Op.NoTrans: 'T', Op.Trans: 'N', Op.ConjTrans: 'N'}[opA]
             conj = opA == Op.ConjTrans
-            if conj:
-                X.copy_(X.conj())
-            _tri_dispatch(s, buf, X, up, opT, kd, unit, None)
-            if conj:
-                X.copy_(X.conj())
-            if alpha != 1.0:
-                ops.gescale(alpha, X)
-            from_dense(B, X.mT)
+            Xd = _DistX(B.conj_transpose() if conj else B.transpose(), s, buf.device)
+            _tri_dispatch(s, buf, Xd, up, opT, kd, unit, None)
+            if alpha != 1.0 and Xd.X.numel():
+                ops.gescale(complex(alpha).conjugate() if conj else alpha, Xd.X)
+            Xd.M.storage.mark_local_modified(Xd.M.storage.origin_slot)
+            _copy_out(Xd.M.conj_transpose() if conj else Xd.M.transpose(), B)
             return 0
-        X = _replicated(B, buf.device)
-        if alpha != 1.0:
-            ops.gescale(alpha, X)
+        Xd = _DistX(B, s, buf.device)
+        if alpha != 1.0 and Xd.X.numel():
+            ops.gescale(alpha, Xd.X)
         opch = {Op.NoTrans: 'N', Op.Trans: 'T', Op.ConjTrans: 'C'}[opA]
-        _tri_dispatch(s, buf, X, up, opch, kd, unit, pivots.device(buf.device) if pivots is not None else None)
-        _store(B, X)
+        _tri_dispatch(s, buf, Xd, up, opch, kd, unit, pivots.device(buf.device) if pivots is not None else None)
+        Xd.store(B)
         return 0
 
 
-def _tri_dispatch(s, buf, X, up, opch, kd, unit, gpiv):
+def _tri_dispatch(s, buf, Xd, up, opch, kd, unit, gpiv):
     if up == Uplo.Lower and opch == 'N':
-        _lower_fwd(s, buf, X, kd, unit, gpiv)
+        _lower_fwd(s, buf, Xd, kd, unit, gpiv)
     elif up == Uplo.Lower:
-        _lower_bwd_op(s, buf, X, kd, unit, opch)
+        _lower_bwd_op(s, buf, Xd, kd, unit, opch)
     elif opch == 'N':
-        _upper_bwd(s, buf, X, kd, unit)
+        _upper_bwd(s, buf, Xd, kd, unit)
     else:
-        _upper_fwd_op(s, buf, X, kd, unit, opch)
+        _upper_fwd_op(s, buf, Xd, kd, unit, opch)
 
 
 # ------------------------------------------------------------------ BLAS-3

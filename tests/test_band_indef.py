@@ -448,3 +448,33 @@ def test_hesv_gpu():
     assert sl.hesv(S, sl.Pivots(), None, None, None, B) == 0
     X = D(B)
     assert ((Sf @ X - Bd).abs().max() / (Sf.abs().max() * X.abs().max() * n)).item() < 1e-13
+
+
+def _band_solve_workspace(rank, size, p, q):
+    from slate_amd.models import band as BM
+    n, nb, kl, ku, nrhs = 257, 16, 21, 9, 7
+    A = sl.BandMatrix(n, n, kl, ku, nb=nb, p=p, q=q)
+    A.insertLocalTiles()
+    sl.generate_matrix(A, "rands", 31)
+    sl.band_mask(A)
+    A0 = D(A).clone()
+    B = sl.Matrix(n, nrhs, nb=nb, p=p, q=q)
+    B.insertLocalTiles()
+    sl.generate_matrix(B, "rands", 32)
+    B0 = D(B).clone()
+    piv = sl.Pivots()
+    assert sl.gbsv(A, piv, B) == 0
+    X = D(B)
+    assert (A0 @ X - B0).abs().max() / (A0.abs().max() * X.abs().max() * n) < 1e-15
+    st = BM.BAND_SOLVE_STATS
+    # one window of (kb + bandwidth) rows and this rank's tile rows -- never
+    # the n x nrhs right-hand side
+    assert st["window_elems"] <= (nb + kl + (kl + ku) + nb) * nrhs, st
+    assert st["local_elems"] <= -(-(-(-n // nb)) // size) * nb * nrhs, st
+    assert st["window_elems"] + st["local_elems"] < n * nrhs, st
+
+
+def test_band_solve_no_rhs_replication_8_ranks():
+    """gbtrs / pbtrs / tbsm keep the right-hand side 1-D row-cyclic; each
+    step gathers only its window onto the factor column's owner."""
+    run_dist(_band_solve_workspace, 8, 2, 4)
