@@ -1,0 +1,78 @@
+// Device scratch allocator of the kernel library and the native runtime:
+// hipMalloc'd blocks cached in a size-keyed free list, reuse ordered by HIP
+// events (a block freed on stream f and taken on stream s makes s wait for
+// the free's event; same-stream reuse is ordered by the stream itself).
+//
+// Why not the stream-ordered pool (hipMallocAsync): on this stack the FIRST
+// kernel reads of freshly mapped pool memory returned stale lines (zeros)
+// for data that a previous kernel or copy of the same stream had written --
+// the native 2 x 1 potrf's received diagonal tile read as zero by the
+// triangular inverse (tools/probe/scal_probe.cc; SLATE_AMD_NATIVE_NOPOOL
+// runs were clean).  hipMalloc'd memory never showed it.
+#pragma once
+#include <map>
+#include <mutex>
+#include <unordered_map>
+
+#include "common.hpp"
+
+namespace slate_hip {
+
+struct DevBlock {
+    void* p;
+    hipStream_t s;
+    hipEvent_t ev;
+};
+
+struct DevAlloc {
+    std::mutex mu;
+    std::multimap<size_t, DevBlock> free_;        // rounded size -> block
+    std::unordered_map<void*, size_t> size_;      // live and cached blocks
+    size_t reserved = 0;
+};
+
+inline DevAlloc& dev_allocator() {
+    static DevAlloc* a = new DevAlloc();          // never destroyed: blocks may outlive static teardown
+    return *a;
+}
+
+inline size_t dev_round(size_t b) {
+    if (b <= 4096) return (b + 255) & ~(size_t)255;
+    size_t p = 4096;
+    while (p * 2 <= b) p *= 2;
+    const size_t step = p / 8;
+    return (b + step - 1) / step * step;
+}
+
+inline void* dev_alloc(size_t bytes, hipStream_t s) {
+    if (bytes == 0) return nullptr;
+    DevAlloc& A = dev_allocator();
+    const size_t r = dev_round(bytes);
+    std::lock_guard<std::mutex> g(A.mu);
+    for (auto it = A.free_.lower_bound(r); it != A.free_.end() && it->first < 2 * r; ++it) {
+        DevBlock b = it->second;
+        A.free_.erase(it);
+        if (b.s != s) HIP_CHECK(hipStreamWaitEvent(s, b.ev, 0));
+        HIP_CHECK(hipEventDestroy(b.ev));
+        return b.p;
+    }
+    void* p = nullptr;
+    HIP_CHECK(hipMalloc(&p, r));
+    A.size_[p] = r;
+    A.reserved += r;
+    return p;
+}
+
+inline void dev_free(void* p, hipStream_t s) {
+    if (!p) return;
+    DevAlloc& A = dev_allocator();
+    std::lock_guard<std::mutex> g(A.mu);
+    auto it = A.size_.find(p);
+    if (it == A.size_.end()) throw std::invalid_argument("dev_free: unknown block");
+    hipEvent_t ev;
+    HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    HIP_CHECK(hipEventRecord(ev, s));
+    A.free_.insert({it->second, DevBlock{p, s, ev}});
+}
+
+}  // namespace slate_hip

@@ -282,11 +282,11 @@ void trtri(char uplo, char diag, i64 n, T* A, i64 lda, i64* info, hipStream_t s)
         return;
     }
     T* I = nullptr;
-    HIP_CHECK(hipMallocAsync((void**)&I, sizeof(T) * n * n, s));
+    I = static_cast<T*>(dev_alloc(sizeof(T) * n * n, s));
     geset<T>('G', n, n, s_zero(T()), s_from_real(T(), 1), I, n, s);
     trsm<T>('L', uplo, 'N', diag, n, n, s_from_real(T(), 1), A, lda, I, n, s);
     gecopy<T, T>(uplo, 'N', n, n, I, n, A, lda, s);
-    HIP_CHECK(hipFreeAsync(I, s));
+    dev_free(I, s);
 }
 
 #define INST(T) \

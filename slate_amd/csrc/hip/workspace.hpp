@@ -1,12 +1,13 @@
 // Per-stream grow-only device workspaces for multi-kernel launchers
 // (trsm, trtri, potrf tile, getrf panel).  Reuse on the same stream is safe by
-// stream order; different streams get different buffers; growth frees the
-// old buffer stream-ordered.  Avoids a hipMallocAsync/hipFreeAsync pair per
-// call on the factorization critical path.
+// stream order; different streams get different buffers; growth returns the
+// old buffer to the event-ordered cache of devalloc.hpp.  Avoids an
+// allocation per call on the factorization critical path.
 #pragma once
 #include <mutex>
 #include <unordered_map>
 #include "common.hpp"
+#include "devalloc.hpp"
 
 namespace slate_hip {
 
@@ -27,9 +28,9 @@ inline void* workspace(hipStream_t s, size_t bytes, int slot) {
     std::lock_guard<std::mutex> g(mu);
     auto& e = cache[WsKey{s, slot}];
     if (e.second < bytes) {
-        if (e.first) HIP_CHECK(hipFreeAsync(e.first, s));
+        if (e.first) dev_free(e.first, s);
         size_t nb = std::max(bytes, e.second * 2);
-        HIP_CHECK(hipMallocAsync(&e.first, nb, s));
+        e.first = dev_alloc(nb, s);
         e.second = nb;
     }
     return e.first;

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../hip/common.hpp"
+#include "../hip/devalloc.hpp"
 #include "slate_amd/slate_native.hh"
 
 namespace slate_amd {
@@ -168,13 +169,15 @@ inline void join(hipStream_t a, hipStream_t b) {
     ev.wait(b);
 }
 
-// device scratch freed after the owning stream reaches it (stream-ordered)
+// device scratch: cached hipMalloc'd blocks, reuse ordered by events
+// (csrc/hip/devalloc.hpp -- not the stream-ordered pool); freed after the
+// owning stream reaches the destructor's point
 struct Scratch {
     void* p = nullptr;
     hipStream_t s = nullptr;
     Scratch(size_t bytes, hipStream_t st) : s(st) {
         if (!bytes) return;
-        NHIP(hipMallocAsync(&p, bytes, st));
+        p = slate_hip::dev_alloc(bytes, st);
         if (poison()) NHIP(hipMemsetAsync(p, 0xFF, bytes, st));     // NaN: exposes reads before writes
     }
     // diagnostics: SLATE_AMD_NATIVE_POISON=1 fills every scratch buffer with NaN
@@ -182,7 +185,7 @@ struct Scratch {
         static const bool on = [] { const char* e = std::getenv("SLATE_AMD_NATIVE_POISON"); return e && *e == '1'; }();
         return on;
     }
-    ~Scratch() { if (p) (void)hipFreeAsync(p, s); }
+    ~Scratch() { if (p) slate_hip::dev_free(p, s); }
     Scratch(const Scratch&) = delete;
     template <typename T> T* as() { return static_cast<T*>(p); }
 };

@@ -2,7 +2,7 @@ import os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
 from tests.test_native_gpu import _run_ranks, ROOT
 exe = os.path.join(ROOT, "slate_amd", "scal_probe")
-variants = [("2x1", "0", {}), ("1x2", "0", {}), ("2x2", "0", {})]
+variants = [("2x1", "0", {}), ("2x2", "0", {}), ("1x2", "0", {})]
 for it in range(int(sys.argv[1])):
     for grid, warm, v in variants:
         p, q = map(int, grid.split("x"))
