@@ -165,12 +165,14 @@ def _main_native(args):
     import subprocess
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.routine not in ("potrf", "getrf", "gemm"):
-        raise SystemExit("--impl native: potrf, getrf or gemm")
+    if args.routine not in ("potrf", "getrf", "gemm", "geqrf"):
+        raise SystemExit("--impl native: potrf, getrf, gemm or geqrf")
     p, q = grid_for(world, args.routine) if args.grid is None else map(int, args.grid.lower().split("x"))
+    if args.routine == "geqrf" and args.grid is None:
+        p, q = 1, world                     # the native geqrf distributes whole columns (1 x q)
     exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "slate_amd", "bench_native")
     cmd = [exe, args.routine, str(args.n), str(args.nb), str(p), str(q), str(args.lookahead), str(args.warmup),
-           str(args.steps), str(args.check)]
+           str(args.steps), str(args.check), str(args.m or args.n)]
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if r.returncode != 0:
         print(r.stdout, file=sys.stderr, flush=True)
@@ -179,12 +181,13 @@ def _main_native(args):
         return
     m = re.search(r"RESULT ms_per_step=(\S+) info=(\S+) resid=(\S+) transport=(\S+)", r.stdout)
     ms, info, resid, transport = float(m.group(1)), int(m.group(2)), float(m.group(3)), m.group(4)
-    fl = flops(args.routine, args.n)
+    fl = flops(args.routine, args.n, args.m)
     gflops = fl / (ms * 1e-3) / 1e9
     tol = 3 * 2.0 ** -52
     resid = resid if args.check else None
     out = {
-        "metric": f"d{args.routine} GFLOP/s (n={args.n}, nb={args.nb})",
+        "metric": (f"d{args.routine} GFLOP/s (m={args.m or args.n}, n={args.n}, nb={args.nb})"
+                   if args.routine == "geqrf" else f"d{args.routine} GFLOP/s (n={args.n}, nb={args.nb})"),
         "value": round(gflops, 2),
         "unit": "GFLOP/s",
         "n_gpus": world,

@@ -7,7 +7,10 @@
 //   potrf / getrf: X = A \ B through the factors, ||B - A0 X|| / (||A0|| ||X|| n)
 //   gemm:          ||C v - A (B v)|| / (||A|| ||B|| ||v|| n)
 //
-//   bench_native routine n nb p q lookahead warmup steps check
+//   geqrf:         gels of a consistent system B = A0 X0,
+//                  ||A0^H (A0 X - B)|| / (||A0||^2 ||X|| m)
+//
+//   bench_native routine n nb p q lookahead warmup steps check [m]
 // prints "RESULT ms_per_step=<max over ranks> info=<info> resid=<r>"
 #include <chrono>
 #include <cmath>
@@ -31,13 +34,17 @@ int main(int argc, char** argv) {
     sn::Options opts;
     opts.lookahead = std::atoi(argv[6]);
     const int warmup = std::atoi(argv[7]), steps = std::atoi(argv[8]), check = std::atoi(argv[9]);
+    const int64_t mrows = argc > 10 ? std::atoll(argv[10]) : n;
     try {
         sn::initialize();
         const int me = sn::rank();
         const bool chol = routine == "potrf";
         const sn::Gen kind = chol ? sn::Gen::HermitianPositiveDefinite : sn::Gen::Random;
-        sn::Matrix<double> A0(n, n, nb, p, q);
+        const bool qr = routine == "geqrf";
+        sn::Matrix<double> A0(qr ? mrows : n, n, nb, p, q);
         A0.generate(kind, 7);
+        sn::Matrix<double> Aq = qr ? sn::Matrix<double>(mrows, n, nb, p, q) : sn::Matrix<double>();
+        sn::QRFactors<double> F;
         sn::HermitianMatrix<double> H(sn::Uplo::Lower, n, nb, p, q);
         sn::Matrix<double> G(n, n, nb, p, q), B, C;
         if (routine == "gemm") {
@@ -54,6 +61,9 @@ int main(int argc, char** argv) {
             } else if (routine == "getrf") {
                 sn::copy(sn::Op::NoTrans, A0, G);
                 info = sn::getrf(G, ipiv, opts);
+            } else if (qr) {
+                sn::copy(sn::Op::NoTrans, A0, Aq);
+                info = sn::geqrf(Aq, F, opts);
             } else {
                 sn::gemm(1.0, A0, B, 0.0, C, opts);
             }
@@ -70,7 +80,23 @@ int main(int argc, char** argv) {
             const int64_t nr = 1;
             sn::Matrix<double> V(n, nr, nb, p, q), X(n, nr, nb, p, q);
             V.generate(sn::Gen::Random, 5);
-            if (routine == "gemm") {
+            if (qr) {
+                sn::Matrix<double> X0(n, nr, nb, p, q), B(mrows, nr, nb, p, q), R(mrows, nr, nb, p, q), G2(n, nr, nb, p, q);
+                X0.generate(sn::Gen::Random, 5);
+                sn::gemm(1.0, A0, X0, 0.0, B);
+                sn::copy(sn::Op::NoTrans, B, R);
+                sn::copy(sn::Op::NoTrans, A0, Aq);
+                sn::gels(Aq, R);                                    // X in R(0:n)
+                sn::Matrix<double> X(n, nr, nb, p, q), E(mrows, nr, nb, p, q);
+                std::vector<double> hx((size_t)mrows);
+                R.to_host(hx.data(), mrows);
+                X.from_host(hx.data(), n);
+                sn::copy(sn::Op::NoTrans, B, E);
+                sn::gemm(1.0, A0, X, -1.0, E);                      // A0 X - B
+                sn::gemm(sn::Op::ConjTrans, sn::Op::NoTrans, 1.0, A0, E, 0.0, G2);
+                const double na = sn::norm(sn::Norm::Fro, A0);
+                resid = sn::norm(sn::Norm::Fro, G2) / (na * na * sn::norm(sn::Norm::Fro, X) * (double)mrows);
+            } else if (routine == "gemm") {
                 sn::Matrix<double> BV(n, nr, nb, p, q), ABV(n, nr, nb, p, q);
                 sn::gemm(1.0, B, V, 0.0, BV);
                 sn::gemm(1.0, A0, BV, 0.0, ABV);

@@ -223,6 +223,33 @@ void run(int p, int q, int me) {
         }
     }
 
+    // ---- gels on the 1 x (p q) grid (geqrf distributes whole columns):
+    // consistent system B = A X0 -> X0; inconsistent -> A^H (A X - B) = 0
+    {
+        const int64_t m4 = 330, n4 = 120, r4 = 3;
+        sn::Matrix<T> G4(m4, n4, nb, 1, p * q), X0(n4, r4, nb, 1, p * q), B4(m4, r4, nb, 1, p * q);
+        G4.generate(sn::Gen::Random, 21);
+        X0.generate(sn::Gen::Random, 22);
+        std::vector<T> g4((size_t)m4 * n4), x0((size_t)n4 * r4);
+        G4.to_host(g4.data(), m4);
+        X0.to_host(x0.data(), n4);
+        auto b4 = mul<T>('N', 'N', m4, r4, n4, g4, m4, x0, n4);
+        std::vector<T> bh((size_t)m4 * r4);
+        for (size_t i = 0; i < bh.size(); ++i) bh[i] = val<T>(b4[i].real(), b4[i].imag());
+        B4.from_host(bh.data(), m4);
+        sn::gels(G4, B4);
+        std::vector<T> xg4((size_t)m4 * r4);
+        B4.to_host(xg4.data(), m4);
+        double e = 0, w = 0;
+        for (int64_t c = 0; c < r4; ++c)
+            for (int64_t i = 0; i < n4; ++i) {
+                e += std::norm(std::complex<double>(std::real(xg4[i + c * m4]) - std::real(x0[i + c * n4]),
+                                                    std::imag(xg4[i + c * m4]) - std::imag(x0[i + c * n4])));
+                w += std::norm(std::complex<double>(std::real(x0[i + c * n4]), std::imag(x0[i + c * n4])));
+            }
+        report("gels", std::sqrt(e / w));
+    }
+
     // ---- trsm: L^H X = alpha B with the Cholesky factor
     {
         sn::Matrix<T> Bt(n, nrhs, nb, p, q);

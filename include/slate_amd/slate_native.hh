@@ -151,6 +151,21 @@ void trsm(Side side, Uplo uplo, Op op, Diag diag, T alpha, const Matrix<T>& A, M
           const Options& opts = {});
 template <typename T> double norm(Norm kind, const Matrix<T>& A);
 
+// Householder QR on 1 x q grids (one process row: every rank holds whole
+// columns): A = Q R, R in the upper triangle, the reflectors below it;
+// F keeps the per-panel compact-WY factors T (device).  unmqr applies
+// op(Q) (NoTrans or ConjTrans; real types: Trans == ConjTrans) from the
+// left; gels solves min ||A X - B|| for m >= n (X in the top n rows of BX).
+struct QRData;
+template <typename T>
+struct QRFactors {
+    std::shared_ptr<QRData> d;
+};
+template <typename T> int64_t geqrf(Matrix<T>& A, QRFactors<T>& F, const Options& opts = {});
+template <typename T>
+void unmqr(Op op, const Matrix<T>& A, const QRFactors<T>& F, Matrix<T>& C, const Options& opts = {});
+template <typename T> int64_t gels(Matrix<T>& A, Matrix<T>& BX, const Options& opts = {});
+
 }  // namespace native
 }  // namespace slate_amd
 

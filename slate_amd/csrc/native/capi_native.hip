@@ -3,14 +3,14 @@
 // Fortran application links -lslate_amd_native instead of -lslate_amd_c:
 //
 //   * LAPACK-style host-array routines (reference lapack_api/lapack_*.cc):
-//     slate_{s,d}{gemm,potrf,potrs,posv,getrf,getrs,gesv,trsm} +
+//     slate_{s,d}{gemm,potrf,potrs,posv,getrf,getrs,gesv,trsm,gels} +
 //     Fortran aliases slate_?xxx_ (by reference), complex slate_{c,z}potrf,
 //     slate_{c,z}gesv, slate_zposv (interleaved re/im), slate_dlange.  With
 //     several ranks every rank passes the same global array; the matrix is
 //     distributed over all ranks (1 x WORLD_SIZE, or SLATE_AMD_NATIVE_GRID=PxQ)
 //     and the result is gathered back to every rank.
 //   * ScaLAPACK (reference scalapack_api/scalapack_*.cc):
-//     p{s,d,c,z}{potrf,posv,getrf,gesv}_, p{s,d}{potrs,getrs,gemm,trsm,lange}_
+//     p{s,d,c,z}{potrf,posv,getrf,gesv,potrs,getrs,gemm,trsm,gels,lange}_ (gels: 1 x q grids)
 //     on the caller's LOCAL block-cyclic arrays (9-int descriptors), with a
 //     minimal BLACS (Cblacs_* / blacs_*_, numroc_, descinit_) over the native
 //     runtime's ranks.  The operands must be whole matrices (ia = ja = 1,
@@ -321,6 +321,29 @@ int64_t h_trsm(char side, char uplo, char ta, char diag, i64 m, i64 n, T alpha, 
     });
 }
 
+// least squares, trans = 'N', m >= n: X in the top n rows of b
+template <typename T>
+int64_t h_gels(char trans, i64 m, i64 n, i64 nrhs, T* a, i64 lda, T* b, i64 ldb) {
+    if (up(trans) != 'N') return -1;
+    if (m < 0) return -2;
+    if (n < 0 || n > m) return -3;
+    if (nrhs < 0) return -4;
+    if (lda < std::max<i64>(1, m)) return -6;
+    if (ldb < std::max<i64>(1, m)) return -8;
+    if (m == 0 || n == 0 || nrhs == 0) return 0;
+    return guarded([&]() -> int64_t {
+        const int q = sn::size();                 // 1 x P: geqrf distributes columns
+        const i64 nb = nb_of(std::max(m, n));
+        sn::Matrix<T> A(m, n, nb, 1, q), B(m, nrhs, nb, 1, q);
+        A.from_host(a, lda);
+        B.from_host(b, ldb);
+        sn::gels(A, B);
+        A.to_host(a, lda);
+        B.to_host(b, ldb);
+        return 0;
+    });
+}
+
 template <typename T>
 double h_lange(char norm, i64 m, i64 n, const T* a, i64 lda) {
     if (m == 0 || n == 0) return 0.0;
@@ -564,6 +587,29 @@ void p_trsm(char side, char uplo, char ta, char diag, int m, int n, T alpha, con
     if (rc != 0) std::fprintf(stderr, "slate_amd native p?trsm_: %s\n", g_err.c_str());
 }
 
+// p?gels_ on a 1 x q grid (geqrf distributes whole columns); lwork = -1
+// is a workspace query (the library allocates its own: returns 1)
+template <typename T>
+int p_gels(char trans, int m, int n, int nrhs, T* a, int ia, int ja, const int* desca, T* b, int ib, int jb,
+           const int* descb, T* work, int lwork) {
+    if (lwork == -1) {
+        if (work) work[0] = T(1);
+        return 0;
+    }
+    if (up(trans) != 'N') return -1;
+    if (n > m) return -3;
+    if (m == 0 || n == 0 || nrhs == 0) return 0;
+    return (int)guarded([&]() -> int64_t {
+        sn::Matrix<T> A = scal_matrix<T>(desca, m, n, ia, ja, a);
+        sn::Matrix<T> B = scal_matrix<T>(descb, m, nrhs, ib, jb, b);
+        if (A.p() != 1) throw sn::Error("native p?gels_: a 1 x q BLACS grid (one process row)");
+        sn::gels(A, B);
+        scal_back(A, desca, a);
+        scal_back(B, descb, b);
+        return 0;
+    });
+}
+
 template <typename T>
 double p_lange(char norm, int m, int n, const T* a, int ia, int ja, const int* desca) {
     if (m == 0 || n == 0) return 0.0;
@@ -615,6 +661,13 @@ void slate_amd_finalize(void) { sn::finalize(); }
     }                                                                                                          \
     double slate_##X##lange(char norm, int64_t m, int64_t n, const T* a, int64_t lda) {                        \
         return h_lange<T>(norm, m, n, a, lda);                                                                 \
+    }                                                                                                          \
+    int slate_##X##gels(char trans, int64_t m, int64_t n, int64_t nrhs, T* a, int64_t lda, T* b, int64_t ldb) { \
+        return (int)h_gels<T>(trans, m, n, nrhs, a, lda, b, ldb);                                             \
+    }                                                                                                          \
+    void slate_##X##gels_(const char* trans, const int64_t* m, const int64_t* n, const int64_t* nrhs, T* a,     \
+                          const int64_t* lda, T* b, const int64_t* ldb, int64_t* info) {                      \
+        *info = h_gels<T>(*trans, *m, *n, *nrhs, a, *lda, b, *ldb);                                            \
     }                                                                                                          \
     void slate_##X##potrf_(const char* uplo, const int64_t* n, T* a, const int64_t* lda, int64_t* info) {      \
         *info = h_potrf<T>(*uplo, *n, a, *lda);                                                                \
@@ -682,6 +735,10 @@ SN_LAPACK(d, double)
     }                                                                                                          \
     double slate_##X##lange(char norm, int64_t m, int64_t n, const R* a, int64_t lda) {                        \
         return h_lange<std::complex<R>>(norm, m, n, reinterpret_cast<const std::complex<R>*>(a), lda);        \
+    }                                                                                                          \
+    int slate_##X##gels(char trans, int64_t m, int64_t n, int64_t nrhs, R* a, int64_t lda, R* b, int64_t ldb) { \
+        return (int)h_gels<std::complex<R>>(trans, m, n, nrhs, reinterpret_cast<std::complex<R>*>(a), lda,    \
+                                            reinterpret_cast<std::complex<R>*>(b), ldb);                       \
     }
 SN_LAPACK_C(c, float)
 SN_LAPACK_C(z, double)
@@ -776,6 +833,11 @@ void descinit_(int* desc, const int* m, const int* n, const int* mb, const int* 
                      const int* descc) {                                                                   \
         p_gemm<T>(*ta, *tb, *m, *n, *k, *alpha, a, *ia, *ja, desca, b, *ib, *jb, descb, *beta, c, *ic, *jc,  \
                   descc);                                                                                  \
+    }                                                                                                      \
+    void p##X##gels_(const char* t, const int* m, const int* n, const int* nrhs, T* a, const int* ia,        \
+                     const int* ja, const int* desca, T* b, const int* ib, const int* jb, const int* descb,   \
+                     T* work, const int* lwork, int* info) {                                               \
+        *info = p_gels<T>(*t, *m, *n, *nrhs, a, *ia, *ja, desca, b, *ib, *jb, descb, work, *lwork);        \
     }                                                                                                      \
     void p##X##trsm_(const char* side, const char* uplo, const char* ta, const char* diag, const int* m,     \
                      const int* n, const T* alpha, const T* a, const int* ia, const int* ja, const int* desca, \

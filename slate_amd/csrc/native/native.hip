@@ -83,6 +83,9 @@ void initialize() {
     const size_t lw = slate_hip::getrf_work_bytes();
     NHIP(hipMalloc(&R.lu_work, lw));
     NHIP(hipMemset(R.lu_work, 0, lw));
+    const size_t qw = std::max<size_t>(64, slate_hip::geqrf_work_bytes());
+    NHIP(hipMalloc(&R.qr_work, qw));
+    NHIP(hipMemset(R.qr_work, 0, qw));
     transport_init(R.rank, R.size);
     R.up = true;
 }
@@ -95,6 +98,7 @@ void finalize() {
     R.grids.clear();
     transport_finalize();
     (void)hipFree(R.lu_work);
+    (void)hipFree(R.qr_work);
     std::vector<hipStream_t> ss{R.main, R.panel, R.update, R.update_masked, R.comm};
     std::sort(ss.begin(), ss.end());
     ss.erase(std::unique(ss.begin(), ss.end()), ss.end());
@@ -1315,6 +1319,153 @@ double norm(Norm kind, const Matrix<T>& A) {
     return r;
 }
 
+// ------------------------------------------------------------ QR (1 x q)
+// models/qr.py _geqrf_p1 in C++: panel on its owner (geqrf_panel_ws: the
+// CholeskyQR2 / recursive MFMA panel), V and T along the process row, the
+// block reflector applied as C -= V op(T) (V^H C) -- lookahead columns on
+// the panel stream, the bulk on the update stream.  Reference:
+// src/geqrf.cc:137-295 (1-D column distribution = its p = 1 case).
+struct QRData {
+    std::vector<i64> r0, kb;
+    std::vector<std::shared_ptr<Scratch>> T;     // kb x kb upper factor per panel
+};
+
+template <typename T>
+static void apply_panel(const T* V, i64 ldv, const T* Vh, const T* Tm, i64 kb, T* C, i64 ldc, i64 m, i64 n,
+                        bool conjT, hipStream_t s) {
+    if (m <= 0 || n <= 0 || kb <= 0) return;
+    Scratch W((size_t)kb * n * sizeof(T), s);
+    if (Vh) gemm_k<T>('N', 'N', kb, n, m, T(1), Vh, kb, C, ldc, T(0), W.as<T>(), kb, s);
+    else gemm_k<T>(ctrans<T>(), 'N', kb, n, m, T(1), V, ldv, C, ldc, T(0), W.as<T>(), kb, s);
+    slate_hip::trmm<K<T>>('L', 'U', conjT ? ctrans<T>() : 'N', 'N', kb, n, kv(T(1)), kp(Tm), kb, kp(W.as<T>()), kb,
+                          s);
+    gemm_k<T>('N', 'N', m, n, kb, T(-1), V, ldv, W.as<T>(), kb, T(1), C, ldc, s);
+}
+
+template <typename T>
+int64_t geqrf(Matrix<T>& A, QRFactors<T>& F, const Options& opts) {
+    Storage& S = *A.storage();
+    if (S.p != 1) throw Error("native geqrf: one process row (p = 1) -- 1 x q grids");
+    Runtime& R = rt();
+    GridComms* gc = S.gc;
+    const int q = S.q, pc = S.pc;
+    const i64 nb = S.nb, m = S.m, n = S.n, lld = S.lld, nloc = S.nloc;
+    const i64 kt = std::min((m + nb - 1) / nb, (n + nb - 1) / nb);
+    const int la = std::max(0, opts.lookahead);
+    const char ct = ctrans<T>();
+    T* buf = static_cast<T*>(S.buf);
+    hipStream_t ps = R.panel, us = R.update;
+    F.d = std::make_shared<QRData>();
+    join(R.main, ps);
+    join(R.main, us);
+    const int NR = la + 3;
+    std::vector<std::unique_ptr<Scratch>> ringV, ringH;
+    for (int r = 0; r < NR; ++r) {
+        ringV.push_back(std::make_unique<Scratch>((size_t)std::max<i64>(m, 1) * nb * sizeof(T), ps));
+        ringH.push_back(std::make_unique<Scratch>((size_t)std::max<i64>(m, 1) * nb * sizeof(T), ps));
+    }
+    std::vector<std::unique_ptr<Event>> ev_tr((size_t)kt), ev_used((size_t)kt);
+    for (i64 k = 0; k < kt; ++k) {
+        const i64 r0 = k * nb;
+        const i64 kb = std::min({nb, n - r0, m - r0});
+        const i64 mk = m - r0;
+        const bool own = (k % q) == pc;
+        const i64 lck = tiles_before(k, q, pc) * nb;
+        const i64 lc1 = std::min(tiles_before(k + 1, q, pc) * nb, nloc);
+        const i64 lcla = std::min(tiles_before(k + 1 + la, q, pc) * nb, nloc);
+        if (k - la - 1 >= 0) ev_tr[k - la - 1]->wait(ps);
+        if (k >= NR) ev_used[k - NR]->wait(ps);
+        auto Tk = std::make_shared<Scratch>((size_t)kb * kb * sizeof(T), ps);
+        Scratch tau((size_t)kb * sizeof(T), ps);
+        T* V = ringV[k % NR]->as<T>();
+        if (own)
+            slate_hip::geqrf_panel_ws<K<T>>(mk, kb, kp(buf + r0 + lck * lld), lld, kp(tau.as<T>()), kp(Tk->as<T>()),
+                                            kb, kp(V), mk, R.qr_work, ps);
+        if (q > 1) {
+            gc->row->bcast(V, (size_t)mk * kb * sizeof(T), (int)(k % q), ps);
+            gc->row->bcast(Tk->p, (size_t)kb * kb * sizeof(T), (int)(k % q), ps);
+        }
+        // explicit V^H for tall panels: the V^H C GEMMs run as NN
+        const T* Vh = nullptr;
+        if (mk >= 4096 && nloc > lc1) {
+            T* H = ringH[k % NR]->as<T>();
+            slate_hip::gecopy<K<T>, K<T>>('G', ct, kb, mk, kp(V), mk, kp(H), kb, ps);
+            Vh = H;
+        }
+        if (k >= 1 && la > 0) ev_tr[k - 1]->wait(ps);
+        if (own && lck + kb < lc1)
+            apply_panel<T>(V, mk, Vh, Tk->as<T>(), kb, buf + r0 + (lck + kb) * lld, lld, mk, lc1 - lck - kb, true, ps);
+        if (lcla > lc1) apply_panel<T>(V, mk, Vh, Tk->as<T>(), kb, buf + r0 + lc1 * lld, lld, mk, lcla - lc1, true, ps);
+        Event ev_panel;
+        ev_panel.record(ps);
+        ev_panel.wait(us);
+        const i64 lcnx = std::max(std::min(tiles_before(k + 2 + la, q, pc) * nb, nloc), lcla);
+        apply_panel<T>(V, mk, Vh, Tk->as<T>(), kb, buf + r0 + lcla * lld, lld, mk, lcnx - lcla, true, us);
+        ev_tr[k] = std::make_unique<Event>();
+        ev_tr[k]->record(us);
+        apply_panel<T>(V, mk, Vh, Tk->as<T>(), kb, buf + r0 + lcnx * lld, lld, mk, nloc - lcnx, true, us);
+        ev_used[k] = std::make_unique<Event>();
+        ev_used[k]->record(us);
+        tau.s = us;
+        F.d->r0.push_back(r0);
+        F.d->kb.push_back(kb);
+        F.d->T.push_back(Tk);
+    }
+    join(ps, R.main);
+    join(us, R.main);
+    for (auto* v : {&ringV, &ringH})
+        for (auto& x : *v) x->s = R.main;
+    NHIP(hipStreamSynchronize(R.main));
+    return 0;
+}
+
+// C = op(Q) C, Q from geqrf (A's reflectors, F's T factors); the V of each
+// panel is rebuilt from A on its owner and broadcast along the process row
+template <typename T>
+void unmqr(Op op, const Matrix<T>& A, const QRFactors<T>& F, Matrix<T>& C, const Options&) {
+    const Storage& SA = *A.storage();
+    Storage& SC = *C.storage();
+    if (!F.d) throw Error("native unmqr: factor with geqrf first");
+    if (SA.p != 1 || SC.p != 1 || SA.q != SC.q || SA.nb != SC.nb || SA.m != SC.m)
+        throw Error("native unmqr: A and C on the same 1 x q grid with m rows");
+    if (op == Op::Trans && is_cplx<T>()) throw Error("native unmqr: Trans of a complex Q (use ConjTrans)");
+    Runtime& R = rt();
+    hipStream_t s = R.main;
+    const int q = SA.q, pc = SA.pc;
+    const i64 nb = SA.nb, m = SA.m;
+    const T* Abuf = static_cast<const T*>(SA.buf);
+    T* Cbuf = static_cast<T*>(SC.buf);
+    const i64 np = (i64)F.d->T.size();
+    const bool conjT = op != Op::NoTrans;
+    NHIP(hipStreamSynchronize(s));
+    for (i64 i = 0; i < np; ++i) {
+        const i64 k = conjT ? i : np - 1 - i;
+        const i64 r0 = F.d->r0[k], kb = F.d->kb[k], mk = m - r0;
+        const i64 lck = tiles_before(k, q, pc) * nb;
+        Scratch V((size_t)mk * kb * sizeof(T), s);
+        if ((k % q) == pc) slate_hip::v_explicit<K<T>>(mk, kb, kp(Abuf + r0 + lck * SA.lld), SA.lld, kp(V.as<T>()), mk, s);
+        if (q > 1) SA.gc->row->bcast(V.p, (size_t)mk * kb * sizeof(T), (int)(k % q), s);
+        apply_panel<T>(V.as<T>(), mk, nullptr, static_cast<const T*>(F.d->T[k]->p), kb, Cbuf + r0, SC.lld, mk, SC.nloc, conjT, s);
+    }
+    NHIP(hipStreamSynchronize(s));
+}
+
+// min ||A X - B||, m >= n: A = Q R, Q^H B, R X = (Q^H B)(0:n) -- X in the top
+// n rows of BX
+template <typename T>
+int64_t gels(Matrix<T>& A, Matrix<T>& BX, const Options& opts) {
+    const Storage& SA = *A.storage();
+    Storage& SB = *BX.storage();
+    if (SA.m < SA.n) throw Error("native gels: m >= n (overdetermined / square) only");
+    if (SB.m != SA.m || SB.nb != SA.nb || SB.p != SA.p || SB.q != SA.q)
+        throw Error("native gels: BX must be m x nrhs on A's grid");
+    QRFactors<T> F;
+    geqrf<T>(A, F, opts);
+    unmqr<T>(Op::ConjTrans, A, F, BX, opts);
+    trsm_left<T>('U', 'N', T(1), SA, SB);
+    return 0;
+}
+
 // ------------------------------------------------------------ instantiation
 #define SLATE_NATIVE_INST(T)                                                                                   \
     template class Matrix<T>;                                                                                   \
@@ -1329,7 +1480,10 @@ double norm(Norm kind, const Matrix<T>& A) {
     template void gemm<T>(Op, Op, T, const Matrix<T>&, const Matrix<T>&, T, Matrix<T>&, const Options&);       \
     template void copy<T>(Op, const Matrix<T>&, Matrix<T>&);                                                   \
     template void trsm<T>(Side, Uplo, Op, Diag, T, const Matrix<T>&, Matrix<T>&, const Options&);              \
-    template double norm<T>(Norm, const Matrix<T>&);
+    template double norm<T>(Norm, const Matrix<T>&);                                                         \
+    template int64_t geqrf<T>(Matrix<T>&, QRFactors<T>&, const Options&);                                      \
+    template void unmqr<T>(Op, const Matrix<T>&, const QRFactors<T>&, Matrix<T>&, const Options&);             \
+    template int64_t gels<T>(Matrix<T>&, Matrix<T>&, const Options&);
 SLATE_NATIVE_INST(float)
 SLATE_NATIVE_INST(double)
 SLATE_NATIVE_INST(std::complex<float>)

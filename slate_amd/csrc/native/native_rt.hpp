@@ -100,6 +100,7 @@ struct Runtime {
     int rank = 0, size = 1, local = 0, device = 0;
     hipStream_t main = nullptr, panel = nullptr, update = nullptr, update_masked = nullptr, comm = nullptr;
     void* lu_work = nullptr;
+    void* qr_work = nullptr;
     std::map<std::pair<int, int>, std::unique_ptr<GridComms>> grids;
     std::mutex mu;
 };
@@ -185,7 +186,9 @@ struct Scratch {
         static const bool on = [] { const char* e = std::getenv("SLATE_AMD_NATIVE_POISON"); return e && *e == '1'; }();
         return on;
     }
-    ~Scratch() { if (p) slate_hip::dev_free(p, s); }
+    // a buffer that outlives finalize() (e.g. QRFactors held by the caller)
+    // must not record on its destroyed stream
+    ~Scratch() { if (p) slate_hip::dev_free(p, rt().up ? s : nullptr); }
     Scratch(const Scratch&) = delete;
     template <typename T> T* as() { return static_cast<T*>(p); }
 };

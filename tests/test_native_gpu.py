@@ -42,10 +42,11 @@ def test_native_library_exports_lapack_scalapack_blacs():
     nm = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True).stdout
     names = {l.split()[-1] for l in nm.splitlines() if l.split()}
     want = ["Cblacs_gridinit", "Cblacs_gridinfo", "blacs_gridinfo_", "numroc_", "descinit_",
-            "slate_dgesv", "slate_dgetrf_", "slate_zposv", "slate_sgemm_", "slate_dtrsm_"]
+            "slate_dgesv", "slate_dgetrf_", "slate_zposv", "slate_sgemm_", "slate_dtrsm_", "slate_dgels",
+            "slate_zgels", "slate_dgels_"]
     for x in "sdcz":
         want += [f"p{x}potrf_", f"p{x}posv_", f"p{x}getrf_", f"p{x}gesv_", f"p{x}getrs_", f"p{x}gemm_",
-                 f"p{x}trsm_", f"p{x}lange_"]
+                 f"p{x}trsm_", f"p{x}lange_", f"p{x}gels_"]
     missing = [w for w in want if w not in names]
     assert not missing, missing
 
@@ -105,7 +106,7 @@ def _checks(out):
 def _assert_checks(checks, out):
     names = [f"{w}_{x}" for x in "sdcz" for w in ("potrf", "potrs", "gesv", "getrs_conjtrans", "getrf_rect",
                                                    "gemm", "gemm_ct", "norm_max", "norm_fro", "norm_one",
-                                                   "trsm_lc")]
+                                                   "trsm_lc", "gels")]
     for name in names:
         assert name in checks, (name, out)
         assert float(checks[name]) < TOL[name[-1]], (name, checks[name])
