@@ -10,6 +10,7 @@
 // triangular inverse (tools/probe/scal_probe.cc; SLATE_AMD_NATIVE_NOPOOL
 // runs were clean).  hipMalloc'd memory never showed it.
 #pragma once
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <unordered_map>
@@ -44,18 +45,39 @@ inline size_t dev_round(size_t b) {
     return (b + step - 1) / step * step;
 }
 
+// Reuse order: a block freed on the same stream (ordered by the stream), then
+// a block of another stream whose free has already completed; only when the
+// cache holds more than dev_cap() bytes does a stream wait on another stream's
+// pending free -- otherwise the panel and update streams of a lookahead
+// driver would be chained through their scratch (a false dependency that
+// serialises them).
+inline size_t dev_cap() {
+    static const size_t cap = [] {
+        const char* e = std::getenv("SLATE_AMD_DEVALLOC_CAP_MB");
+        return (size_t)(e ? std::atoll(e) : 16384) << 20;
+    }();
+    return cap;
+}
+
 inline void* dev_alloc(size_t bytes, hipStream_t s) {
     if (bytes == 0) return nullptr;
     DevAlloc& A = dev_allocator();
     const size_t r = dev_round(bytes);
     std::lock_guard<std::mutex> g(A.mu);
-    for (auto it = A.free_.lower_bound(r); it != A.free_.end() && it->first < 2 * r; ++it) {
+    auto take = [&](std::multimap<size_t, DevBlock>::iterator it, bool wait) {
         DevBlock b = it->second;
         A.free_.erase(it);
-        if (b.s != s) HIP_CHECK(hipStreamWaitEvent(s, b.ev, 0));
+        if (wait) HIP_CHECK(hipStreamWaitEvent(s, b.ev, 0));
         HIP_CHECK(hipEventDestroy(b.ev));
         return b.p;
-    }
+    };
+    const auto lo = A.free_.lower_bound(r);
+    for (auto it = lo; it != A.free_.end() && it->first < 2 * r; ++it)
+        if (it->second.s == s) return take(it, false);
+    for (auto it = lo; it != A.free_.end() && it->first < 2 * r; ++it)
+        if (hipEventQuery(it->second.ev) == hipSuccess) return take(it, false);
+    if (A.reserved + r > dev_cap())
+        for (auto it = lo; it != A.free_.end() && it->first < 2 * r; ++it) return take(it, true);
     void* p = nullptr;
     HIP_CHECK(hipMalloc(&p, r));
     A.size_[p] = r;

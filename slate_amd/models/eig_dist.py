@@ -309,13 +309,16 @@ def heev_dist(A, Lambda=None, Z=None, opts=None):
             w = E.sterf(d, e)
         else:
             dt = s.dtype
+            # the reflectors (~n^2/2 words) go device to device over the
+            # communicator; only O(n) vectors take the host path above
             if comm.rank == 0:
                 parts = (F2.V, F2.tau, F2.row, F2.length, F2.sweep_ptr, F2.phase)
             else:
-                parts = (torch.zeros(cnt, nb, dtype=dt), torch.zeros(cnt, dtype=dt),
-                         torch.zeros(cnt, dtype=torch.int64), torch.zeros(cnt, dtype=torch.int64),
-                         torch.zeros(max(n, 1), dtype=torch.int64), torch.ones(n, dtype=dt))
-            parts = tuple(_bcast_host(comm, t.contiguous(), 0) for t in parts)
+                parts = (torch.zeros(cnt, nb, dtype=dt, device=dev), torch.zeros(cnt, dtype=dt, device=dev),
+                         torch.zeros(cnt, dtype=torch.int64, device=dev),
+                         torch.zeros(cnt, dtype=torch.int64, device=dev),
+                         torch.zeros(max(n, 1), dtype=torch.int64, device=dev), torch.ones(n, dtype=dt, device=dev))
+            parts = tuple(_bcast_dev(comm, t, 0, dev) for t in parts)
             F2 = E.Hb2stFactors(parts[0], parts[1], parts[2], parts[3], parts[4], cnt, parts[5])
             # Q2 on this rank's columns of a 1 x P column-cyclic Z, then onto Z's grid
             P = comm.size
@@ -362,10 +365,28 @@ def heev_dist(A, Lambda=None, Z=None, opts=None):
         return w
 
 
+# bytes each path moved (tests: the host path carries O(n) words only)
+BCAST_STATS = {"host_bytes": 0, "host_max": 0, "dev_bytes": 0}
+
+
 def _bcast_host(comm, t, root):
-    """Broadcast a host tensor (staged through the GPU under RCCL)."""
+    """Broadcast a small host tensor (staged through the GPU under RCCL)."""
     if comm.size == 1:
         return t
     x = t.clone()
+    nbytes = x.numel() * x.element_size()
+    BCAST_STATS["host_bytes"] += nbytes
+    BCAST_STATS["host_max"] = max(BCAST_STATS["host_max"], nbytes)
+    comm.bcast(x, root)
+    return x
+
+
+def _bcast_dev(comm, t, root, dev):
+    """Broadcast a tensor that lives on ``dev`` (the GPU under RCCL: no host
+    staging; the root's tensor is moved there once if it is not)."""
+    if comm.size == 1:
+        return t
+    x = t.to(dev).contiguous()
+    BCAST_STATS["dev_bytes"] += x.numel() * x.element_size()
     comm.bcast(x, root)
     return x

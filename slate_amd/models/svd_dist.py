@@ -43,6 +43,7 @@ from ..core.options import get_option
 from ..core.storage import numroc
 from ..utils.trace import trace_block
 from ._panels import panel_allgather
+from .eig_dist import _bcast_dev, _bcast_host   # O(n) vectors via host, the reflectors device to device
 from ._util import conj_trans, grid_of, target_slot, tiles_local_before
 
 
@@ -289,12 +290,6 @@ def _apply_right(G, Fac, Zt):
     sZ.mark_local_modified(sZ.origin_slot)
 
 
-def _bcast_host(comm, t, root):
-    if comm.size == 1:
-        return t
-    x = t.clone()
-    comm.bcast(x, root)
-    return x
 
 
 def svd_dist(A, S=None, U=None, VH=None, opts=None):
@@ -342,21 +337,22 @@ def svd_dist(A, S=None, U=None, VH=None, opts=None):
         if not (wantU or wantV):
             sv, _, _ = SV.bdsqr(d, e, False, False)
         else:
+            dev = G.storage.local[G.storage.origin_slot].device
             parts = []
             for which, cnt in (("U", int(meta[0])), ("V", int(meta[1]))):
                 if comm.rank == 0:
                     F = getattr(F2, which)
-                    t = tuple(x.cpu() for x in (F.V, F.tau, F.row, F.length, F.sweep_ptr))
+                    t = (F.V, F.tau, F.row, F.length, F.sweep_ptr)
                 else:
-                    t = (torch.zeros(cnt, band, dtype=dt), torch.zeros(cnt, dtype=dt),
-                         torch.zeros(cnt, dtype=torch.int64), torch.zeros(cnt, dtype=torch.int64),
-                         torch.zeros(max(k, 1), dtype=torch.int64))
-                t = tuple(_bcast_host(comm, x.contiguous(), 0) for x in t)
+                    t = (torch.zeros(cnt, band, dtype=dt, device=dev), torch.zeros(cnt, dtype=dt, device=dev),
+                         torch.zeros(cnt, dtype=torch.int64, device=dev),
+                         torch.zeros(cnt, dtype=torch.int64, device=dev),
+                         torch.zeros(max(k, 1), dtype=torch.int64, device=dev))
+                t = tuple(_bcast_dev(comm, x, 0, dev) for x in t)
                 parts.append(Hb2stFactors(t[0], t[1], t[2], t[3], t[4], cnt, None))
             FU, FV = parts
             pu = _bcast_host(comm, F2.pu if comm.rank == 0 else torch.ones(k, dtype=dt), 0)
             pv = _bcast_host(comm, F2.pv if comm.rank == 0 else torch.ones(k, dtype=dt), 0)
-            dev = G.storage.local[G.storage.origin_slot].device
             # bdsqr on this rank's rows of U / columns of V^H (a P x 1 layout)
             Lu = _general(G, k, k, band, P, 1, GridOrder.Col)
             lb = Lu.local_block()

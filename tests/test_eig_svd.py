@@ -124,7 +124,14 @@ def test_svd_vals_bdsqr():
 
 
 def _dist_eig(rank, size, p, q):
+    from slate_amd.models import eig_dist
+    eig_dist.BCAST_STATS.update(host_bytes=0, host_max=0, dev_bytes=0)
     _check_heev(90, 16, torch.float64, Uplo.Lower, MethodEig.DC, p, q)
+    st = dict(eig_dist.BCAST_STATS)
+    # stage-2 reflectors (~n^2/2 words) go on the device path; the host path
+    # carries only O(n) vectors (d, e, count)
+    assert st["host_max"] <= 8 * 90, st
+    assert st["dev_bytes"] >= 8 * 90 * 16, st
     A = sl.Matrix(70, 50, nb=16, p=p, q=q)
     A.insertLocalTiles()
     sl.generate_matrix(A, "rands", 9)
