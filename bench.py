@@ -224,7 +224,7 @@ def main():
     # (its parser takes --n / --m for ambiguous prefixes of its own options)
     ap.add_argument("--n", "--size", dest="n", type=int, default=32768)
     ap.add_argument("--m", "--rows", dest="m", type=int, default=None)
-    ap.add_argument("--nb", type=int, default=512)
+    ap.add_argument("--nb", type=int, default=None, help="tile size (default: 256 for geqrf, 512 otherwise -- BASELINE)")
     ap.add_argument("--routine", default="potrf", choices=["potrf", "getrf", "gemm", "geqrf", "heev"])
     ap.add_argument("--vectors", type=int, default=1, help="heev: 1 = eigenvectors (dsyevd), 0 = values only")
     ap.add_argument("--band", type=int, default=0, help="heev: stage-1 bandwidth (default min(nb, 64))")
@@ -235,6 +235,8 @@ def main():
     ap.add_argument("--impl", default="python", choices=["python", "native"],
                     help="native: the Python-free C++ library (slate_amd/bench_native, one child per rank)")
     args = ap.parse_args()
+    if args.nb is None:
+        args.nb = 256 if args.routine == "geqrf" else 512
     if args.impl == "native":
         return _main_native(args)
     # No GPU_MAX_HW_QUEUES override: a process drives the panel, diag and

@@ -85,11 +85,17 @@ def _getrf(A, pivots, opts, mode):
     _check_view(A)
     bc = s.bc
     slot = target_slot(A, opts)
-    buf = s.prepare_local(slot)
     if bc.mb != bc.nb:
         raise SlateError("getrf: square tiles required")
     thr = float(get_option(opts, Option.PivotThreshold, 1.0))
     la = max(0, int(get_option(opts, Option.Lookahead, 1)))
+    if mode == "pp":
+        ooc = _maybe_ooc(A, s, slot, thr, la)
+        if ooc is not None:
+            if pivots is not None:
+                pivots.set(ooc[1], bc.nb)
+            return ooc[0]
+    buf = s.prepare_local(slot)
     if bc.p == 1 and mode != "calu":
         info, ipiv = None, None
         if _rowmajor_ok(buf, bc):
@@ -107,6 +113,25 @@ def _getrf(A, pivots, opts, mode):
     if pivots is not None and ipiv is not None:
         pivots.set(ipiv, bc.nb)
     return info
+
+
+def _maybe_ooc(A, s, slot, thr, la):
+    """Host-origin matrix on one rank, larger than the device budget (or
+    SLATE_AMD_OOC_COLS set): the left-looking out-of-core LU streams block
+    columns instead of staging the whole local buffer (models/ooc.py).
+    Returns (info, ipiv) or None for the in-core path."""
+    from .ooc import getrf_ooc, ooc_applicable, ooc_block_columns
+    if not ooc_applicable(A, s, slot):
+        return None
+    from ..core.storage import HOST
+    dev = torch.device("cuda", torch.cuda.current_device())
+    W = ooc_block_columns(s.m, s.n, s.bc.nb, s.dtype, dev, 5)
+    if not W or W >= s.n:
+        return None
+    s.sync_origin()
+    res = getrf_ooc(s.local[HOST][:s.m, :s.n], s.m, s.n, s.bc.nb, W, dev, thr, la)
+    s.mark_local_modified(HOST)
+    return res
 
 
 # ------------------------------------------------------------------ p == 1

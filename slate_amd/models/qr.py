@@ -98,17 +98,37 @@ def geqrf(A, T: TriangularFactors, opts=None) -> int:
         if bc.mb != bc.nb:
             raise SlateError("geqrf: square tiles required")
         slot = target_slot(A, opts)
-        buf = s.prepare_local(slot)
         la = max(0, int(get_option(opts, Option.Lookahead, 1)))
         T.clear()
         T.nb = bc.nb
         T.kind = "qr"
+        if _maybe_ooc(A, s, slot, T, la):
+            return 0
+        buf = s.prepare_local(slot)
         if bc.p == 1:
             _geqrf_p1(A, buf, T, la)
         else:
             _geqrf_general(A, buf, T, la)
         s.mark_local_modified(slot)
     return 0
+
+
+def _maybe_ooc(A, s, slot, T, la):
+    """Host-origin matrix on one rank, larger than the device budget (or
+    SLATE_AMD_OOC_COLS set): the left-looking out-of-core QR streams block
+    columns (models/ooc.py).  True when it ran."""
+    from .ooc import geqrf_ooc, ooc_applicable, ooc_block_columns
+    if not ooc_applicable(A, s, slot):
+        return False
+    from ..core.storage import HOST
+    dev = torch.device("cuda", torch.cuda.current_device())
+    W = ooc_block_columns(s.m, s.n, s.bc.nb, s.dtype, dev, 5)
+    if not W or W >= s.n:
+        return False
+    s.sync_origin()
+    T.extend(geqrf_ooc(s.local[HOST][:s.m, :s.n], s.m, s.n, s.bc.nb, W, dev, la))
+    s.mark_local_modified(HOST)
+    return True
 
 
 # panels at least this tall get an explicit V^H (SLATE_AMD_QR_VH_ROWS; 0 = never)

@@ -216,3 +216,73 @@ def test_potrf_out_of_core(W, monkeypatch):
     L = torch.tril(A.storage.local[A.storage.origin_slot][:n, :n])
     S = torch.tril(S0) + torch.tril(S0, -1).mT
     assert ((L @ L.mT - S).norm() / S.norm()).item() < 1e-14
+
+
+@pytest.mark.parametrize("shape,W", [((3000, 3000), 512), ((3300, 2200), 768), ((1800, 2600), 512)],
+                         ids=["sq", "tall", "wide"])
+def test_getrf_out_of_core(shape, W, monkeypatch):
+    """Host-origin LU with forced out-of-core block columns (models/ooc.py):
+    the streamed left-looking factorization with deferred row re-ordering
+    reproduces P A = L U, and its pivots drive getrs."""
+    monkeypatch.setenv("SLATE_AMD_OOC_COLS", str(W))
+    m, n = shape
+    nb = 256
+    A = sl.Matrix(m, n, nb=nb)
+    A.insertLocalTiles()                                # host origin
+    sl.generate_matrix(A, "rand", seed=5)
+    H = A.storage.local[A.storage.origin_slot]
+    A0 = H[:m, :n].clone()
+    piv = sl.Pivots()
+    assert sl.getrf(A, piv, {sl.Option.Target: sl.Target.Devices}) == 0
+    F = A.storage.local[A.storage.origin_slot][:m, :n]
+    k = min(m, n)
+    L = torch.tril(F[:, :k], -1) + torch.eye(m, k, dtype=F.dtype)
+    U = torch.triu(F[:k, :])
+    PA = A0.clone()
+    for i, r in enumerate(piv.ipiv.tolist()):
+        if r != i:
+            PA[[i, r]] = PA[[r, i]]
+    assert ((L @ U - PA).norm() / A0.norm()).item() < 1e-14
+    # the in-core factorization picks the same pivots
+    monkeypatch.delenv("SLATE_AMD_OOC_COLS")
+    B = sl.Matrix(m, n, nb=nb)
+    B.insertLocalTiles()
+    sl.generate_matrix(B, "rand", seed=5)
+    piv2 = sl.Pivots()
+    assert sl.getrf(B, piv2, {sl.Option.Target: sl.Target.Devices}) == 0
+    assert torch.equal(piv.ipiv, piv2.ipiv)
+
+
+@pytest.mark.parametrize("shape,W", [((3000, 2000), 512), ((2400, 2400), 768)], ids=["tall", "sq"])
+def test_geqrf_out_of_core(shape, W, monkeypatch):
+    """Host-origin QR with forced out-of-core block columns: R matches the
+    in-core factor and unmqr with the streamed factors reproduces A."""
+    monkeypatch.setenv("SLATE_AMD_OOC_COLS", str(W))
+    m, n = shape
+    nb = 256
+    A = sl.Matrix(m, n, nb=nb)
+    A.insertLocalTiles()
+    sl.generate_matrix(A, "rand", seed=6)
+    A0 = A.storage.local[A.storage.origin_slot][:m, :n].clone()
+    T = sl.TriangularFactors()
+    assert sl.geqrf(A, T, {sl.Option.Target: sl.Target.Devices}) == 0
+    monkeypatch.delenv("SLATE_AMD_OOC_COLS")
+    F = A.storage.local[A.storage.origin_slot][:m, :n].clone()
+    R = torch.triu(F[:n, :])
+    # Q R = A: apply Q to [R; 0] with the streamed factors
+    C = sl.Matrix(m, n, nb=nb)
+    C.insertLocalTiles()
+    C.storage.local[C.storage.origin_slot][:m, :n].zero_()
+    C.storage.local[C.storage.origin_slot][:n, :n].copy_(R)
+    sl.unmqr(sl.Side.Left, sl.Op.NoTrans, A, T, C, {sl.Option.Target: sl.Target.Devices})
+    QR = C.storage.local[C.storage.origin_slot][:m, :n]
+    assert ((QR - A0).norm() / A0.norm()).item() < 1e-14
+    # R agrees with the in-core factor up to row signs
+    B = sl.Matrix(m, n, nb=nb)
+    B.insertLocalTiles()
+    sl.generate_matrix(B, "rand", seed=6)
+    T2 = sl.TriangularFactors()
+    sl.geqrf(B, T2, {sl.Option.Target: sl.Target.Devices})
+    B.storage.sync_origin()                             # the in-core factor lives on the device
+    R2 = torch.triu(B.storage.local[B.storage.origin_slot][:n, :n])
+    assert ((R.abs() - R2.abs()).norm() / R2.norm()).item() < 1e-12
