@@ -185,33 +185,6 @@ def unmtr_he2hb(F: He2hbFactors, Z: torch.Tensor):
     return Z
 
 
-def form_q1(F: He2hbFactors, n, dtype, device):
-    """Q1 = Q_0 Q_1 ... of he2hb as an explicit n x n matrix (the panels
-    applied to the identity last-to-first, grouped as in unmtr_he2hb).  A
-    group starting at row r0 only meets columns >= r0 (everything left of
-    them is still the identity there), so each product runs on Q[r0:, r0:]:
-    half the flops of a back-transform of a full Z.  heev forms Q1 on a side
-    stream while the bulge chase (which occupies about half the CUs) runs,
-    and the eigenvectors are then Z = Q1 (Q2 Z_tri): one GEMM on the
-    critical path instead of the stage-1 back-transform."""
-    from .qr import _apply_qh, _vh
-    Q = ops.colmajor_empty(n, n, dtype, device)
-    ops.geset(0.0, 1.0, Q)
-    panels = F.panels
-    grp = max(1, int(os.environ.get("SLATE_AMD_UNMTR_HE2HB_GROUP", "4")))
-    i1 = len(panels)
-    while i1 > 0:
-        i0 = max(0, i1 - grp)
-        if i1 - i0 == 1:
-            r0, V, T = panels[i0]
-            _apply_qh(V, T, Q[r0:, r0:], conj=False, Vh=_vh(V))
-        else:
-            r0, Vg, Tg = _merge_reflectors(panels[i0:i1])
-            _apply_qh(Vg, Tg, Q[r0:, r0:], conj=False, Vh=_vh(Vg))
-        i1 = i0
-    return Q
-
-
 def _merge_reflectors(group):
     """One block reflector for the product H_0 H_1 ... of consecutive panel
     reflectors (r_i, V_i, T_i) (V_i explicit, rows r_i..n-1; T_i upper)."""
@@ -605,18 +578,8 @@ def heev(A, Lambda=None, Z=None, opts=None):
             scale = 1.0 / amax
             Af.mul_(scale)
         F1 = he2hb(Af, nb)
-        want = Z is not None
-        # Q1 explicitly on a side stream, overlapping the bulge chase
-        # (SLATE_AMD_HEEV_Q1=0: back-transform Z by the stage-1 panels instead)
-        q1 = None
-        if want and Af.is_cuda and n > 0 and os.environ.get("SLATE_AMD_HEEV_Q1", "1") != "0":
-            cur = torch.cuda.current_stream(dev)
-            side = torch.cuda.Stream(device=dev)
-            side.wait_stream(cur)
-            with torch.cuda.stream(side), trace_block("heev::form_q1"):
-                Q1 = form_q1(F1, n, Af.dtype, dev)
-            q1 = (Q1, side)
         d, e, F2 = hb2st(_band_only(Af, nb), nb, device=Af.device if Af.is_cuda else None)
+        want = Z is not None
         if not want:
             w = sterf(d, e)
         elif method in (MethodEig.QR, 'Q', "qr"):
@@ -632,15 +595,7 @@ def heev(A, Lambda=None, Z=None, opts=None):
                 torch.zeros(n, 0, dtype=Af.dtype, device=dev)
             Zl = _cm(Zl.clone())
             unmtr_hb2st(F2, Zl)
-            if q1 is not None:
-                Q1, side = q1
-                cur.wait_stream(side)
-                Q1.record_stream(cur)
-                Zq = ops.colmajor_empty(n, Zl.shape[1], Zl.dtype, dev)
-                ops.gemm(1.0, Q1, Zl, 0.0, Zq)
-                Zl = Zq
-            else:
-                unmtr_he2hb(F1, Zl)
+            unmtr_he2hb(F1, Zl)
             _scatter_cols(Z, Zl, cols)
         if Lambda is not None:
             Lambda.copy_(w.to(Lambda.dtype).to(Lambda.device))
