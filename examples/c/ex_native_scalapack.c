@@ -44,6 +44,12 @@ void slate_dgetrf_(const int64_t* m, const int64_t* n, double* a, const int64_t*
 void slate_dgetrs_(const char* trans, const int64_t* n, const int64_t* nrhs, const double* a, const int64_t* lda,
                    const int64_t* ipiv, double* b, const int64_t* ldb, int64_t* info);
 const char* slate_amd_last_error(void);
+void pdsyrk_(const char* uplo, const char* trans, const int* n, const int* k, const double* alpha, const double* a,
+             const int* ia, const int* ja, const int* desca, const double* beta, double* c, const int* ic,
+             const int* jc, const int* descc);
+void pdtrmm_(const char* side, const char* uplo, const char* ta, const char* diag, const int* m, const int* n,
+             const double* alpha, const double* a, const int* ia, const int* ja, const int* desca, double* b,
+             const int* ib, const int* jb, const int* descb);
 void slate_amd_finalize(void);
 
 static int g_rank;
@@ -147,6 +153,45 @@ int main(int argc, char** argv) {
             gw += s * s;
         }
     check("pdgemm_tn", gw > 0 ? sqrt(ge / gw) : sqrt(ge));
+
+    /* pdsyrk_: C(lower) = 2 A^T A - C; the upper triangle must stay untouched */
+    for (int lj = 0; lj < nloc; ++lj)
+        for (int li = 0; li < mloc; ++li) c[li + lj * lld] = 1.0;
+    {
+        const double two = 2.0, m1 = -1.0;
+        pdsyrk_("L", "T", &n, &n, &two, a, &one, &one, desca, &m1, c, &one, &one, desca);
+        double se = 0, sw = 0;
+        for (int lj = 0; lj < nloc; lj += 3)
+            for (int li = 0; li < mloc; li += 3) {
+                const int gi = l2g(li, nb, p, pr), gj = l2g(lj, nb, q, pc);
+                double s = 1.0;
+                if (gi >= gj) {
+                    s = -1.0;
+                    for (int k = 0; k < n; ++k) s += 2.0 * gen(k, gi, n) * gen(k, gj, n);
+                }
+                se += (c[li + lj * lld] - s) * (c[li + lj * lld] - s);
+                sw += s * s;
+            }
+        check("pdsyrk_lower", sw > 0 ? sqrt(se / sw) : sqrt(se));
+    }
+    /* pdtrmm_: B = U B (U = the upper triangle of gen, non-unit) */
+    FILL_A(gen);
+    for (int lc = 0; lc < rloc; ++lc)
+        for (int li = 0; li < mloc; ++li) b[li + lc * lld] = xs(l2g(li, nb, p, pr), l2g(lc, nb, q, pc));
+    {
+        const double a1 = 1.0;
+        pdtrmm_("L", "U", "N", "N", &n, &nrhs, &a1, a, &one, &one, desca, b, &one, &one, descb);
+        double te = 0, tw = 0;
+        for (int lc = 0; lc < rloc; ++lc)
+            for (int li = 0; li < mloc; ++li) {
+                const int gi = l2g(li, nb, p, pr), cc = l2g(lc, nb, q, pc);
+                double s = 0;
+                for (int j = gi; j < n; ++j) s += gen(gi, j, n) * xs(j, cc);
+                te += (b[li + lc * lld] - s) * (b[li + lc * lld] - s);
+                tw += s * s;
+            }
+        check("pdtrmm_lun", tw > 0 ? sqrt(te / tw) : sqrt(te));
+    }
 
     /* complex LU */
     double complex* za = malloc(sizeof(double complex) * lld * (nloc > 0 ? nloc : 1));

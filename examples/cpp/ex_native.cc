@@ -267,6 +267,110 @@ void run(int p, int q, int me) {
         }
         report("trsm_lc", rel<T>(lx, want));
     }
+
+    using R = sn::real_t<T>;
+    auto cd = [](T x) { return std::complex<double>(std::real(x), std::imag(x)); };
+    // ---- herk / her2k / syrk / syr2k: C's stored triangle against the host
+    for (int v = 0; v < 4; ++v) {
+        const int64_t nc = 140, kc = 90;
+        const bool two = v == 1 || v == 3, herm = v <= 1;
+        const char ta = v == 1 ? 'C' : v == 2 ? 'T' : 'N';
+        const sn::Uplo ul = two ? sn::Uplo::Upper : sn::Uplo::Lower;
+        const int64_t ar = ta == 'N' ? nc : kc, ac = ta == 'N' ? kc : nc;
+        sn::Matrix<T> A2(ar, ac, nb, p, q), B2(ar, ac, nb, p, q);
+        A2.generate(sn::Gen::Random, 31 + v);
+        B2.generate(sn::Gen::Random, 41 + v);
+        sn::HermitianMatrix<T> C2(ul, nc, nb, p, q);
+        C2.generate(sn::Gen::Random, 51 + v);
+        std::vector<T> ha((size_t)ar * ac), hb((size_t)ar * ac), hc((size_t)nc * nc), hc1((size_t)nc * nc);
+        A2.to_host(ha.data(), ar);
+        B2.to_host(hb.data(), ar);
+        C2.to_host(hc.data(), nc);
+        const T alpha = (herm && !two) ? val<T>(1.5, 0) : val<T>(1.5, -0.75);
+        const T beta = herm ? val<T>(-0.5, 0) : val<T>(-0.5, 0.25);
+        if (v == 0) sn::herk(sn::Op::NoTrans, (R)std::real(alpha), A2, (R)std::real(beta), C2);
+        else if (v == 1) sn::her2k(sn::Op::ConjTrans, alpha, A2, B2, (R)std::real(beta), C2);
+        else if (v == 2) sn::syrk(sn::Op::Trans, alpha, A2, beta, C2);
+        else sn::syr2k(sn::Op::NoTrans, alpha, A2, B2, beta, C2);
+        C2.to_host(hc1.data(), nc);
+        // op(X) op(Y)^{H or T}: X Y^t2 for op = N, X^ta Y for op = ta
+        const char t2 = herm ? 'C' : 'T';
+        auto prod = [&](const std::vector<T>& X, const std::vector<T>& Y) {
+            return ta == 'N' ? mul<T>('N', t2, nc, nc, kc, X, ar, Y, ar) : mul<T>(ta, 'N', nc, nc, kc, X, ar, Y, ar);
+        };
+        const auto P1 = prod(ha, two ? hb : ha);
+        const auto P2 = two ? prod(hb, ha) : P1;
+        const std::complex<double> al = cd(alpha), be = cd(beta), al2 = herm ? std::conj(al) : al;
+        std::vector<std::complex<double>> d, want;
+        for (int64_t j = 0; j < nc; ++j)
+            for (int64_t i = 0; i < nc; ++i) {
+                if (ul == sn::Uplo::Lower ? i < j : i > j) continue;
+                const size_t o = (size_t)(i + j * nc);
+                std::complex<double> w = al * P1[o] + be * cd(hc[o]);
+                if (two) w += al2 * P2[o];
+                want.push_back(w);
+                d.push_back(cd(hc1[o]) - w);
+            }
+        static const char* nm[] = {"herk", "her2k_upper", "syrk", "syr2k_upper"};
+        report(nm[v], rel<T>(d, want));
+    }
+    // ---- hemm (Left, Lower) / symm (Right, Upper): the stored triangle expanded
+    for (int v = 0; v < 2; ++v) {
+        const int64_t na = 130, nr = 70;
+        const sn::Uplo ul = v ? sn::Uplo::Upper : sn::Uplo::Lower;
+        sn::HermitianMatrix<T> H(ul, na, nb, p, q);
+        H.generate(sn::Gen::Random, 61 + v);
+        const int64_t bm = v ? nr : na, bn = v ? na : nr;
+        sn::Matrix<T> Bm(bm, bn, nb, p, q), Cm(bm, bn, nb, p, q);
+        Bm.generate(sn::Gen::Random, 71 + v);
+        Cm.generate(sn::Gen::Random, 81 + v);
+        std::vector<T> hh((size_t)na * na), hb((size_t)bm * bn), hc((size_t)bm * bn), hc1((size_t)bm * bn);
+        H.to_host(hh.data(), na);
+        Bm.to_host(hb.data(), bm);
+        Cm.to_host(hc.data(), bm);
+        for (int64_t j = 0; j < na; ++j)
+            for (int64_t i = 0; i < na; ++i) {
+                const bool stored = v ? i <= j : i >= j;
+                if (!stored) hh[i + j * na] = v ? hh[j + i * na] : cj(hh[j + i * na]);
+            }
+        if (!v)
+            for (int64_t i = 0; i < na; ++i) hh[i + i * na] = val<T>(std::real(hh[i + i * na]), 0);
+        const T alpha = val<T>(0.75, 0.5), beta = val<T>(1.25, -0.5);
+        if (!v) sn::hemm(sn::Side::Left, alpha, H, Bm, beta, Cm);
+        else sn::symm(sn::Side::Right, alpha, H, Bm, beta, Cm);
+        Cm.to_host(hc1.data(), bm);
+        auto want = v ? mul<T>('N', 'N', bm, bn, na, hb, bm, hh, na) : mul<T>('N', 'N', bm, bn, na, hh, na, hb, bm);
+        std::vector<std::complex<double>> d(want.size());
+        for (size_t i = 0; i < want.size(); ++i) {
+            want[i] = cd(alpha) * want[i] + cd(beta) * cd(hc[i]);
+            d[i] = cd(hc1[i]) - want[i];
+        }
+        report(v ? "symm_right" : "hemm_left", rel<T>(d, want));
+    }
+    // ---- trmm: B = alpha A^H B, A upper triangular with a unit diagonal
+    {
+        const int64_t na = 120, nr = 50;
+        sn::Matrix<T> Tm(na, na, nb, p, q), Bm(na, nr, nb, p, q);
+        Tm.generate(sn::Gen::Random, 91);
+        Bm.generate(sn::Gen::Random, 92);
+        std::vector<T> ht((size_t)na * na), hb((size_t)na * nr), hb1((size_t)na * nr);
+        Tm.to_host(ht.data(), na);
+        Bm.to_host(hb.data(), na);
+        for (int64_t j = 0; j < na; ++j)
+            for (int64_t i = 0; i < na; ++i)
+                if (i > j) ht[i + j * na] = T(0);
+                else if (i == j) ht[i + j * na] = T(1);
+        const T alpha = val<T>(-1.25, 0.5);
+        sn::trmm(sn::Side::Left, sn::Uplo::Upper, sn::Op::ConjTrans, sn::Diag::Unit, alpha, Tm, Bm);
+        Bm.to_host(hb1.data(), na);
+        auto want = mul<T>('C', 'N', na, nr, na, ht, na, hb, na);
+        std::vector<std::complex<double>> d(want.size());
+        for (size_t i = 0; i < want.size(); ++i) {
+            want[i] = cd(alpha) * want[i];
+            d[i] = cd(hb1[i]) - want[i];
+        }
+        report("trmm_luc", rel<T>(d, want));
+    }
 }
 
 int main(int argc, char** argv) {

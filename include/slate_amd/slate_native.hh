@@ -151,6 +151,38 @@ void trsm(Side side, Uplo uplo, Op op, Diag diag, T alpha, const Matrix<T>& A, M
           const Options& opts = {});
 template <typename T> double norm(Norm kind, const Matrix<T>& A);
 
+// real type of a scalar (herk / her2k scaling factors)
+template <typename T> struct real_of { using type = T; };
+template <typename R> struct real_of<std::complex<R>> { using type = R; };
+template <typename T> using real_t = typename real_of<T>::type;
+
+// C = alpha op(A) op(A)^H + beta C on C's stored triangle (op: NoTrans / ConjTrans)
+template <typename T>
+void herk(Op op, real_t<T> alpha, const Matrix<T>& A, real_t<T> beta, HermitianMatrix<T>& C,
+          const Options& opts = {});
+// C = alpha op(A) op(A)^T + beta C (C symmetric, stored triangle; op: NoTrans / Trans)
+template <typename T>
+void syrk(Op op, T alpha, const Matrix<T>& A, T beta, HermitianMatrix<T>& C, const Options& opts = {});
+// C = alpha op(A) op(B)^H + conj(alpha) op(B) op(A)^H + beta C
+template <typename T>
+void her2k(Op op, T alpha, const Matrix<T>& A, const Matrix<T>& B, real_t<T> beta, HermitianMatrix<T>& C,
+           const Options& opts = {});
+// C = alpha op(A) op(B)^T + alpha op(B) op(A)^T + beta C
+template <typename T>
+void syr2k(Op op, T alpha, const Matrix<T>& A, const Matrix<T>& B, T beta, HermitianMatrix<T>& C,
+           const Options& opts = {});
+// C = alpha A B + beta C (Left) or alpha B A + beta C (Right), A Hermitian (hemm) / symmetric (symm)
+template <typename T>
+void hemm(Side side, T alpha, const HermitianMatrix<T>& A, const Matrix<T>& B, T beta, Matrix<T>& C,
+          const Options& opts = {});
+template <typename T>
+void symm(Side side, T alpha, const HermitianMatrix<T>& A, const Matrix<T>& B, T beta, Matrix<T>& C,
+          const Options& opts = {});
+// B = alpha op(A) B (Left) or alpha B op(A) (Right), A triangular (uplo, diag)
+template <typename T>
+void trmm(Side side, Uplo uplo, Op op, Diag diag, T alpha, const Matrix<T>& A, Matrix<T>& B,
+          const Options& opts = {});
+
 // Householder QR on 1 x q grids (one process row: every rank holds whole
 // columns): A = Q R, R in the upper triangle, the reflectors below it;
 // F keeps the per-panel compact-WY factors T (device).  unmqr applies

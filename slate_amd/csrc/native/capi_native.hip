@@ -611,6 +611,102 @@ int p_gels(char trans, int m, int n, int nrhs, T* a, int ia, int ja, const int* 
 }
 
 template <typename T>
+sn::HermitianMatrix<T> scal_tri(const int* desc, i64 n, int ia, int ja, const T* a, char uplo) {
+    sn::Matrix<T> G = scal_matrix<T>(desc, n, n, ia, ja, a);
+    sn::HermitianMatrix<T> H(uplo == 'U' ? sn::Uplo::Upper : sn::Uplo::Lower, n, G.nb(), G.p(), G.q());
+    sn::copy(sn::Op::NoTrans, G, H);
+    return H;
+}
+
+// C(uplo) *= beta on the local ScaLAPACK array (k = 0 rank updates)
+template <typename T>
+void scal_scale_tri(const int* desc, int n, char uplo, T beta, T* c) {
+    const Ctx& cx = ctx_of(desc[1]);
+    const int p = cx.p, q = cx.q, r = sn::rank(), pr = r % p, pc = r / p;     // column-major grid (scal_matrix)
+    const i64 nb = desc[4], lld = desc[8];
+    const i64 ml = sn::numroc(n, nb, pr, p), nl = sn::numroc(n, nb, pc, q);
+    for (i64 lj = 0; lj < nl; ++lj)
+        for (i64 li = 0; li < ml; ++li) {
+            const i64 gi = sn::l2g(li, nb, p, pr), gj = sn::l2g(lj, nb, q, pc);
+            if (uplo == 'L' ? gi >= gj : gi <= gj) c[li + lj * lld] *= beta;
+        }
+}
+
+// p?syrk_ / p?herk_ / p?syr2k_ / p?her2k_ (whole matrices, ia = ja = 1)
+template <typename T>
+void p_rank_k(bool herm, bool two, char uplo, char trans, int n, int k, T alpha, const T* a, int ia, int ja,
+              const int* desca, const T* b, int ib, int jb, const int* descb, T beta, T* c, int ic, int jc,
+              const int* descc) {
+    uplo = up(uplo);
+    trans = up(trans);
+    if (n == 0) return;
+    const int64_t rc = guarded([&]() -> int64_t {
+        if (k == 0 || alpha == T(0)) {
+            if (beta != T(1)) scal_scale_tri<T>(descc, n, uplo, beta, c);
+            return 0;
+        }
+        const bool nt = trans == 'N';
+        const sn::Op op = nt ? sn::Op::NoTrans : (herm ? sn::Op::ConjTrans : sn::Op::Trans);
+        sn::Matrix<T> A = scal_matrix<T>(desca, nt ? n : k, nt ? k : n, ia, ja, a);
+        sn::HermitianMatrix<T> C = scal_tri<T>(descc, n, ic, jc, c, uplo);
+        using R = sn::real_t<T>;
+        if (two) {
+            sn::Matrix<T> B = scal_matrix<T>(descb, nt ? n : k, nt ? k : n, ib, jb, b);
+            if (herm) sn::her2k(op, alpha, A, B, (R)std::real(beta), C);
+            else sn::syr2k(op, alpha, A, B, beta, C);
+        } else if (herm) {
+            sn::herk(op, (R)std::real(alpha), A, (R)std::real(beta), C);
+        } else {
+            sn::syrk(op, alpha, A, beta, C);
+        }
+        scal_back(C, descc, c);
+        return 0;
+    });
+    if (rc != 0) std::fprintf(stderr, "slate_amd native p?%s_: %s\n", two ? (herm ? "her2k" : "syr2k") : (herm ? "herk" : "syrk"),
+                              g_err.c_str());
+}
+
+// p?symm_ / p?hemm_
+template <typename T>
+void p_xmm(bool herm, char side, char uplo, int m, int n, T alpha, const T* a, int ia, int ja, const int* desca,
+           const T* b, int ib, int jb, const int* descb, T beta, T* c, int ic, int jc, const int* descc) {
+    side = up(side);
+    uplo = up(uplo);
+    if (m == 0 || n == 0) return;
+    const int64_t rc = guarded([&]() -> int64_t {
+        const int na = side == 'L' ? m : n;
+        sn::HermitianMatrix<T> A = scal_tri<T>(desca, na, ia, ja, a, uplo);
+        sn::Matrix<T> B = scal_matrix<T>(descb, m, n, ib, jb, b);
+        sn::Matrix<T> C = scal_matrix<T>(descc, m, n, ic, jc, c);
+        const sn::Side sd = side == 'L' ? sn::Side::Left : sn::Side::Right;
+        if (herm) sn::hemm(sd, alpha, A, B, beta, C);
+        else sn::symm(sd, alpha, A, B, beta, C);
+        scal_back(C, descc, c);
+        return 0;
+    });
+    if (rc != 0) std::fprintf(stderr, "slate_amd native p?%s_: %s\n", herm ? "hemm" : "symm", g_err.c_str());
+}
+
+template <typename T>
+void p_trmm(char side, char uplo, char ta, char diag, int m, int n, T alpha, const T* a, int ia, int ja,
+            const int* desca, T* b, int ib, int jb, const int* descb) {
+    side = up(side);
+    uplo = up(uplo);
+    ta = up(ta);
+    if (m == 0 || n == 0) return;
+    const int64_t rc = guarded([&]() -> int64_t {
+        const int na = side == 'L' ? m : n;
+        sn::Matrix<T> A = scal_matrix<T>(desca, na, na, ia, ja, a);
+        sn::Matrix<T> B = scal_matrix<T>(descb, m, n, ib, jb, b);
+        sn::trmm(side == 'L' ? sn::Side::Left : sn::Side::Right, uplo == 'L' ? sn::Uplo::Lower : sn::Uplo::Upper,
+                 op_of(ta), up(diag) == 'U' ? sn::Diag::Unit : sn::Diag::NonUnit, alpha, A, B);
+        scal_back(B, descb, b);
+        return 0;
+    });
+    if (rc != 0) std::fprintf(stderr, "slate_amd native p?trmm_: %s\n", g_err.c_str());
+}
+
+template <typename T>
 double p_lange(char norm, int m, int n, const T* a, int ia, int ja, const int* desca) {
     if (m == 0 || n == 0) return 0.0;
     double r = -1.0;
@@ -849,6 +945,63 @@ SN_SCAL(d, double)
 SN_SCAL(c, std::complex<float>)
 SN_SCAL(z, std::complex<double>)
 #undef SN_SCAL
+
+// ---- ScaLAPACK BLAS-3 on triangles / symmetric / Hermitian matrices
+#define SN_SCAL3(X, T)                                                                                         \
+    void p##X##syrk_(const char* uplo, const char* trans, const int* n, const int* k, const T* alpha,        \
+                     const T* a, const int* ia, const int* ja, const int* desca, const T* beta, T* c,          \
+                     const int* ic, const int* jc, const int* descc) {                                       \
+        p_rank_k<T>(false, false, *uplo, *trans, *n, *k, *alpha, a, *ia, *ja, desca, nullptr, 1, 1, nullptr, \
+                    *beta, c, *ic, *jc, descc);                                                            \
+    }                                                                                                      \
+    void p##X##syr2k_(const char* uplo, const char* trans, const int* n, const int* k, const T* alpha,       \
+                      const T* a, const int* ia, const int* ja, const int* desca, const T* b, const int* ib,  \
+                      const int* jb, const int* descb, const T* beta, T* c, const int* ic, const int* jc,     \
+                      const int* descc) {                                                                  \
+        p_rank_k<T>(false, true, *uplo, *trans, *n, *k, *alpha, a, *ia, *ja, desca, b, *ib, *jb, descb,     \
+                    *beta, c, *ic, *jc, descc);                                                            \
+    }                                                                                                      \
+    void p##X##symm_(const char* side, const char* uplo, const int* m, const int* n, const T* alpha,        \
+                     const T* a, const int* ia, const int* ja, const int* desca, const T* b, const int* ib,   \
+                     const int* jb, const int* descb, const T* beta, T* c, const int* ic, const int* jc,      \
+                     const int* descc) {                                                                   \
+        p_xmm<T>(false, *side, *uplo, *m, *n, *alpha, a, *ia, *ja, desca, b, *ib, *jb, descb, *beta, c, *ic,  \
+                 *jc, descc);                                                                              \
+    }                                                                                                      \
+    void p##X##trmm_(const char* side, const char* uplo, const char* ta, const char* diag, const int* m,     \
+                     const int* n, const T* alpha, const T* a, const int* ia, const int* ja, const int* desca, \
+                     T* b, const int* ib, const int* jb, const int* descb) {                                \
+        p_trmm<T>(*side, *uplo, *ta, *diag, *m, *n, *alpha, a, *ia, *ja, desca, b, *ib, *jb, descb);        \
+    }
+SN_SCAL3(s, float)
+SN_SCAL3(d, double)
+SN_SCAL3(c, std::complex<float>)
+SN_SCAL3(z, std::complex<double>)
+#undef SN_SCAL3
+#define SN_SCAL3H(X, T, R)                                                                                     \
+    void p##X##herk_(const char* uplo, const char* trans, const int* n, const int* k, const R* alpha,        \
+                     const T* a, const int* ia, const int* ja, const int* desca, const R* beta, T* c,          \
+                     const int* ic, const int* jc, const int* descc) {                                       \
+        p_rank_k<T>(true, false, *uplo, *trans, *n, *k, T(*alpha), a, *ia, *ja, desca, nullptr, 1, 1,       \
+                    nullptr, T(*beta), c, *ic, *jc, descc);                                                \
+    }                                                                                                      \
+    void p##X##her2k_(const char* uplo, const char* trans, const int* n, const int* k, const T* alpha,       \
+                      const T* a, const int* ia, const int* ja, const int* desca, const T* b, const int* ib,  \
+                      const int* jb, const int* descb, const R* beta, T* c, const int* ic, const int* jc,     \
+                      const int* descc) {                                                                  \
+        p_rank_k<T>(true, true, *uplo, *trans, *n, *k, *alpha, a, *ia, *ja, desca, b, *ib, *jb, descb,      \
+                    T(*beta), c, *ic, *jc, descc);                                                         \
+    }                                                                                                      \
+    void p##X##hemm_(const char* side, const char* uplo, const int* m, const int* n, const T* alpha,        \
+                     const T* a, const int* ia, const int* ja, const int* desca, const T* b, const int* ib,   \
+                     const int* jb, const int* descb, const T* beta, T* c, const int* ic, const int* jc,      \
+                     const int* descc) {                                                                   \
+        p_xmm<T>(true, *side, *uplo, *m, *n, *alpha, a, *ia, *ja, desca, b, *ib, *jb, descb, *beta, c, *ic,   \
+                 *jc, descc);                                                                              \
+    }
+SN_SCAL3H(c, std::complex<float>, float)
+SN_SCAL3H(z, std::complex<double>, double)
+#undef SN_SCAL3H
 float pslange_(const char* norm, const int* m, const int* n, const float* a, const int* ia, const int* ja,
                const int* desca, float*) {
     return (float)p_lange<float>(*norm, *m, *n, a, *ia, *ja, desca);

@@ -1184,11 +1184,13 @@ int64_t gesv(Matrix<T>& A, std::vector<int64_t>& ipiv, Matrix<T>& B, const Optio
 // broadcast) -- issued on the comm stream ONE step ahead of the GEMM on the
 // panel stream (double buffers, events): the broadcasts of step k+1 travel
 // while GEMM k runs (SLATE gemmC's lookahead, src/gemmC.cc:104-170)
+// SUMMA over the process grid: per k block, the A column block along the
+// process rows and the B row block along the process columns (lookahead
+// broadcasts on the comm stream), one local GEMM each.  mask: only the kept
+// part of C (a stored triangle, in global coordinates) is written.
 template <typename T>
-void gemm(T alpha, const Matrix<T>& A, const Matrix<T>& B, T beta, Matrix<T>& C, const Options& opts) {
-    const Storage& SA = *A.storage();
-    const Storage& SB = *B.storage();
-    Storage& SC = *C.storage();
+static void summa(T alpha, const Storage& SA, const Storage& SB, T beta, Storage& SC, const Options& opts,
+                  const slate_hip::TriMask* mask) {
     if (SA.m != SC.m || SB.n != SC.n || SA.n != SB.m) throw Error("native gemm: dimension mismatch");
     if (SA.nb != SB.nb || SA.nb != SC.nb || SA.p != SC.p || SA.q != SC.q || SB.p != SC.p || SB.q != SC.q)
         throw Error("native gemm: A, B, C must share the grid and the tile size");
@@ -1203,7 +1205,7 @@ void gemm(T alpha, const Matrix<T>& A, const Matrix<T>& B, T beta, Matrix<T>& C,
     const T* Al = static_cast<const T*>(SA.buf);
     const T* Bl = static_cast<const T*>(SB.buf);
     if (p == 1 && q == 1) {
-        gemm_k<T>('N', 'N', SC.m, SC.n, Kd, alpha, Al, SA.lld, Bl, SB.lld, beta, Cl, SC.lld, s);
+        gemm_k<T>('N', 'N', SC.m, SC.n, Kd, alpha, Al, SA.lld, Bl, SB.lld, beta, Cl, SC.lld, s, mask);
     } else {
         const i64 kt = (Kd + nb - 1) / nb;
         const int la = std::max(1, opts.lookahead);
@@ -1236,12 +1238,14 @@ void gemm(T alpha, const Matrix<T>& A, const Matrix<T>& B, T beta, Matrix<T>& C,
             const i64 kb = std::min(nb, Kd - k * nb);
             ready[k]->wait(s);
             gemm_k<T>('N', 'N', SC.mloc, SC.nloc, kb, alpha, Ab[b]->as<T>(), ma, Bb[b]->as<T>(), kb,
-                      k == 0 ? beta : T(1), Cl, SC.lld, s);
+                      k == 0 ? beta : T(1), Cl, SC.lld, s, mask);
             used[k] = std::make_unique<Event>();
             used[k]->record(s);
         }
-        if (kt == 0 && beta != T(1))
+        if (kt == 0 && beta != T(1)) {
+            if (mask) throw Error("native summa: k = 0 with a triangular output");
             slate_hip::gescale<K<T>>('G', SC.mloc, SC.nloc, kv(beta), kp(Cl), SC.lld, s);
+        }
         for (auto& x : Ab) x->s = s;
         for (auto& x : Bb) x->s = s;
         join(cs, s);
@@ -1250,18 +1254,162 @@ void gemm(T alpha, const Matrix<T>& A, const Matrix<T>& B, T beta, Matrix<T>& C,
 }
 
 template <typename T>
+void gemm(T alpha, const Matrix<T>& A, const Matrix<T>& B, T beta, Matrix<T>& C, const Options& opts) {
+    summa<T>(alpha, *A.storage(), *B.storage(), beta, *C.storage(), opts, nullptr);
+}
+
+// op(X) as a matrix of its own (X itself for NoTrans)
+template <typename T>
+static Matrix<T> op_copy(Op op, const Matrix<T>& X) {
+    if (op == Op::NoTrans) return X;
+    const Storage& S = *X.storage();
+    Matrix<T> Y(S.n, S.m, S.nb, S.p, S.q);
+    copy<T>(op, X, Y);
+    return Y;
+}
+
+template <typename T>
 void gemm(Op opA, Op opB, T alpha, const Matrix<T>& A, const Matrix<T>& B, T beta, Matrix<T>& C,
           const Options& opts) {
-    auto materialise = [](Op op, const Matrix<T>& X) -> Matrix<T> {
-        if (op == Op::NoTrans) return X;
-        const Storage& S = *X.storage();
-        Matrix<T> Y(S.n, S.m, S.nb, S.p, S.q);
-        copy<T>(op, X, Y);
-        return Y;
-    };
-    const Matrix<T> Ao = materialise(opA, A);
-    const Matrix<T> Bo = materialise(opB, B);
+    const Matrix<T> Ao = op_copy<T>(opA, A);
+    const Matrix<T> Bo = op_copy<T>(opB, B);
     gemm<T>(alpha, Ao, Bo, beta, C, opts);
+}
+
+// ------------------------------------------------------------ Hermitian / symmetric / triangular BLAS-3
+// Reference: src/herk.cc, src/her2k.cc, src/hemm.cc (hemmA / hemmC),
+// src/trmm.cc (work::trmm).  Here every one of them is the masked SUMMA
+// above on operands materialised once: op(A) by the tile transpose
+// exchange, a Hermitian / symmetric / triangular A expanded to a full
+// matrix by two masked copies.  The output mask writes only C's stored
+// triangle (herk/syrk/her2k/syr2k) and skips whole GEMM blocks above it.
+
+// the stored triangle of C as a GEMM output mask (global coordinates)
+static slate_hip::TriMask tri_mask(const Storage& S, Uplo uplo, i64 diag_off = 0) {
+    slate_hip::TriMask t = lower_mask(S.nb, S.p, S.pr, S.q, S.pc, 0, 0);
+    if (uplo == Uplo::Upper) t.mode = 2;
+    t.diag_off = diag_off;
+    return t;
+}
+
+// full matrix of a stored triangle: kind 0 = triangular (the other part
+// zero; a Unit diagonal set to one), 1 = Hermitian (the other part is the
+// stored one conjugate-transposed, real diagonal), 2 = symmetric
+template <typename T>
+static Matrix<T> expand_tri(const Matrix<T>& A, Uplo uplo, int kind, Diag diag = Diag::NonUnit) {
+    const Storage& S = *A.storage();
+    if (S.m != S.n) throw Error("native: square triangular / Hermitian matrix expected");
+    hipStream_t s = rt().main;
+    Matrix<T> F(S.m, S.n, S.nb, S.p, S.q);
+    Storage& SF = *F.storage();
+    const bool unit = kind == 0 && diag == Diag::Unit;
+    const slate_hip::TriMask mk = tri_mask(S, uplo, unit ? -1 : 0);
+    if (S.mloc && S.nloc)
+        slate_hip::gecopy_mask<K<T>>(mk, S.mloc, S.nloc, kp(static_cast<const T*>(S.buf)), S.lld,
+                                     kp(static_cast<T*>(SF.buf)), SF.lld, kind == 1, s);
+    if (unit) {
+        const i64 nt = (S.n + S.nb - 1) / S.nb;
+        for (i64 k = 0; k < nt; ++k) {
+            if ((int)(k % S.p) != S.pr || (int)(k % S.q) != S.pc) continue;
+            const i64 kb = std::min(S.nb, S.n - k * S.nb);
+            T* d = static_cast<T*>(SF.buf) + tiles_before(k, S.p, S.pr) * S.nb +
+                   tiles_before(k, S.q, S.pc) * S.nb * SF.lld;
+            // diagonal tile: the part opposite the stored triangle is still
+            // zero, so 'U' ('L') sets exactly the diagonal to one
+            slate_hip::geset<K<T>>(uplo == Uplo::Lower ? 'U' : 'L', kb, kb, kv(T(0)), kv(T(1)), kp(d), SF.lld, s);
+        }
+    }
+    if (kind >= 1) {
+        Matrix<T> At(S.n, S.m, S.nb, S.p, S.q);
+        NHIP(hipStreamSynchronize(s));
+        transpose_tiles<T>(S, *At.storage(), kind == 1 ? ctrans<T>() : 'T');
+        const Storage& ST = *At.storage();
+        const slate_hip::TriMask mo = tri_mask(S, uplo == Uplo::Lower ? Uplo::Upper : Uplo::Lower, -1);
+        // gecopy_mask zeroes what it does not keep: mask At in place, then F += At
+        T* at = static_cast<T*>(ST.buf);
+        if (S.mloc && S.nloc) {
+            slate_hip::gecopy_mask<K<T>>(mo, S.mloc, S.nloc, kp(at), ST.lld, kp(at), ST.lld, false, s);
+            slate_hip::geadd<K<T>>('G', S.mloc, S.nloc, kv(T(1)), kp(at), ST.lld, kv(T(1)),
+                                   kp(static_cast<T*>(SF.buf)), SF.lld, s);
+        }
+    }
+    NHIP(hipStreamSynchronize(s));
+    return F;
+}
+
+template <typename T>
+void herk(Op op, real_t<T> alpha, const Matrix<T>& A, real_t<T> beta, HermitianMatrix<T>& C, const Options& opts) {
+    if (op == Op::Trans && is_cplx<T>()) throw Error("native herk: Trans of a complex matrix (use ConjTrans)");
+    const Matrix<T> X = op_copy<T>(op == Op::NoTrans ? Op::NoTrans : Op::ConjTrans, A);   // n x k
+    const Matrix<T> Xh = op_copy<T>(Op::ConjTrans, X);
+    const slate_hip::TriMask mk = tri_mask(*C.storage(), C.uplo());
+    summa<T>(T(alpha), *X.storage(), *Xh.storage(), T(beta), *C.storage(), opts, &mk);
+}
+
+template <typename T>
+void syrk(Op op, T alpha, const Matrix<T>& A, T beta, HermitianMatrix<T>& C, const Options& opts) {
+    if (op == Op::ConjTrans && is_cplx<T>()) throw Error("native syrk: ConjTrans of a complex matrix (use Trans)");
+    const Matrix<T> X = op_copy<T>(op == Op::NoTrans ? Op::NoTrans : Op::Trans, A);
+    const Matrix<T> Xt = op_copy<T>(Op::Trans, X);
+    const slate_hip::TriMask mk = tri_mask(*C.storage(), C.uplo());
+    summa<T>(alpha, *X.storage(), *Xt.storage(), beta, *C.storage(), opts, &mk);
+}
+
+template <typename T>
+void her2k(Op op, T alpha, const Matrix<T>& A, const Matrix<T>& B, real_t<T> beta, HermitianMatrix<T>& C,
+           const Options& opts) {
+    if (op == Op::Trans && is_cplx<T>()) throw Error("native her2k: Trans of a complex matrix (use ConjTrans)");
+    const Op o = op == Op::NoTrans ? Op::NoTrans : Op::ConjTrans;
+    const Matrix<T> X = op_copy<T>(o, A), Y = op_copy<T>(o, B);
+    const Matrix<T> Xh = op_copy<T>(Op::ConjTrans, X), Yh = op_copy<T>(Op::ConjTrans, Y);
+    const slate_hip::TriMask mk = tri_mask(*C.storage(), C.uplo());
+    summa<T>(alpha, *X.storage(), *Yh.storage(), T(beta), *C.storage(), opts, &mk);
+    summa<T>(conj_of(alpha), *Y.storage(), *Xh.storage(), T(1), *C.storage(), opts, &mk);
+}
+
+template <typename T>
+void syr2k(Op op, T alpha, const Matrix<T>& A, const Matrix<T>& B, T beta, HermitianMatrix<T>& C,
+           const Options& opts) {
+    if (op == Op::ConjTrans && is_cplx<T>()) throw Error("native syr2k: ConjTrans of a complex matrix (use Trans)");
+    const Op o = op == Op::NoTrans ? Op::NoTrans : Op::Trans;
+    const Matrix<T> X = op_copy<T>(o, A), Y = op_copy<T>(o, B);
+    const Matrix<T> Xt = op_copy<T>(Op::Trans, X), Yt = op_copy<T>(Op::Trans, Y);
+    const slate_hip::TriMask mk = tri_mask(*C.storage(), C.uplo());
+    summa<T>(alpha, *X.storage(), *Yt.storage(), beta, *C.storage(), opts, &mk);
+    summa<T>(alpha, *Y.storage(), *Xt.storage(), T(1), *C.storage(), opts, &mk);
+}
+
+template <typename T>
+static void xmm(Side side, int kind, T alpha, const HermitianMatrix<T>& A, const Matrix<T>& B, T beta,
+                Matrix<T>& C, const Options& opts) {
+    const Matrix<T> Af = expand_tri<T>(A, A.uplo(), kind);
+    if (side == Side::Left) summa<T>(alpha, *Af.storage(), *B.storage(), beta, *C.storage(), opts, nullptr);
+    else summa<T>(alpha, *B.storage(), *Af.storage(), beta, *C.storage(), opts, nullptr);
+}
+
+template <typename T>
+void hemm(Side side, T alpha, const HermitianMatrix<T>& A, const Matrix<T>& B, T beta, Matrix<T>& C,
+          const Options& opts) {
+    xmm<T>(side, 1, alpha, A, B, beta, C, opts);
+}
+
+template <typename T>
+void symm(Side side, T alpha, const HermitianMatrix<T>& A, const Matrix<T>& B, T beta, Matrix<T>& C,
+          const Options& opts) {
+    xmm<T>(side, 2, alpha, A, B, beta, C, opts);
+}
+
+// B = alpha op(A) B (Left) or alpha B op(A) (Right), A triangular
+template <typename T>
+void trmm(Side side, Uplo uplo, Op op, Diag diag, T alpha, const Matrix<T>& A, Matrix<T>& B, const Options& opts) {
+    if (op == Op::Trans && is_cplx<T>()) throw Error("native trmm: Trans of a complex matrix (use ConjTrans)");
+    const Matrix<T> Af = expand_tri<T>(A, uplo, 0, diag);
+    const Matrix<T> Ao = op_copy<T>(op, Af);
+    const Storage& SB = *B.storage();
+    Matrix<T> W(SB.m, SB.n, SB.nb, SB.p, SB.q);
+    if (side == Side::Left) summa<T>(alpha, *Ao.storage(), SB, T(0), *W.storage(), opts, nullptr);
+    else summa<T>(alpha, SB, *Ao.storage(), T(0), *W.storage(), opts, nullptr);
+    copy<T>(Op::NoTrans, W, B);
 }
 
 // ------------------------------------------------------------ norm
@@ -1483,7 +1631,15 @@ int64_t gels(Matrix<T>& A, Matrix<T>& BX, const Options& opts) {
     template double norm<T>(Norm, const Matrix<T>&);                                                         \
     template int64_t geqrf<T>(Matrix<T>&, QRFactors<T>&, const Options&);                                      \
     template void unmqr<T>(Op, const Matrix<T>&, const QRFactors<T>&, Matrix<T>&, const Options&);             \
-    template int64_t gels<T>(Matrix<T>&, Matrix<T>&, const Options&);
+    template int64_t gels<T>(Matrix<T>&, Matrix<T>&, const Options&);                                         \
+    template void herk<T>(Op, real_t<T>, const Matrix<T>&, real_t<T>, HermitianMatrix<T>&, const Options&);    \
+    template void syrk<T>(Op, T, const Matrix<T>&, T, HermitianMatrix<T>&, const Options&);                    \
+    template void her2k<T>(Op, T, const Matrix<T>&, const Matrix<T>&, real_t<T>, HermitianMatrix<T>&,          \
+                           const Options&);                                                                    \
+    template void syr2k<T>(Op, T, const Matrix<T>&, const Matrix<T>&, T, HermitianMatrix<T>&, const Options&); \
+    template void hemm<T>(Side, T, const HermitianMatrix<T>&, const Matrix<T>&, T, Matrix<T>&, const Options&);  \
+    template void symm<T>(Side, T, const HermitianMatrix<T>&, const Matrix<T>&, T, Matrix<T>&, const Options&);  \
+    template void trmm<T>(Side, Uplo, Op, Diag, T, const Matrix<T>&, Matrix<T>&, const Options&);
 SLATE_NATIVE_INST(float)
 SLATE_NATIVE_INST(double)
 SLATE_NATIVE_INST(std::complex<float>)

@@ -146,6 +146,10 @@ template <typename T> inline K<T> kv(T v) {
 }
 template <typename T> constexpr bool is_cplx() { return !std::is_same<T, float>::value && !std::is_same<T, double>::value; }
 template <typename T> constexpr char ctrans() { return is_cplx<T>() ? 'C' : 'T'; }
+template <typename T> inline T conj_of(T x) {
+    if constexpr (is_cplx<T>()) return std::conj(x);
+    else return x;
+}
 
 // ------------------------------------------------------------ small RAII
 struct Event {
