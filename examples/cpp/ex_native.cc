@@ -371,6 +371,40 @@ void run(int p, int q, int me) {
         }
         report("trmm_luc", rel<T>(d, want));
     }
+    // ---- mixed precision (double / complex<double>): low-precision factors +
+    // refinement must reach the working-precision residual
+    if constexpr (std::is_same<T, double>::value || std::is_same<T, std::complex<double>>::value) {
+        const int64_t nm = 200;
+        for (int v = 0; v < 2; ++v) {
+            sn::Matrix<T> Bm(nm, nrhs, nb, p, q), Xm(nm, nrhs, nb, p, q);
+            Bm.generate(sn::Gen::Random, 101 + v);
+            std::vector<T> ha((size_t)nm * nm), hb((size_t)nm * nrhs), hx((size_t)nm * nrhs);
+            Bm.to_host(hb.data(), nm);
+            int iter = -100;
+            int64_t inf;
+            if (v == 0) {
+                sn::HermitianMatrix<T> Hm(sn::Uplo::Lower, nm, nb, p, q);
+                Hm.generate(sn::Gen::HermitianPositiveDefinite, 103);
+                Hm.to_host(ha.data(), nm);
+                for (int64_t j = 0; j < nm; ++j)
+                    for (int64_t i = 0; i < j; ++i) ha[i + j * nm] = cj(ha[j + i * nm]);
+                inf = sn::posv_mixed(Hm, Bm, Xm, iter);
+            } else {
+                sn::Matrix<T> Gm(nm, nm, nb, p, q);
+                Gm.generate(sn::Gen::DiagDominant, 104);     // well conditioned: the refinement converges
+                Gm.to_host(ha.data(), nm);
+                std::vector<int64_t> pv;
+                inf = sn::gesv_mixed(Gm, pv, Bm, Xm, iter);
+            }
+            Xm.to_host(hx.data(), nm);
+            auto ax = mul<T>('N', 'N', nm, nrhs, nm, ha, nm, hx, nm);
+            auto want = widen(hb);
+            for (size_t i = 0; i < ax.size(); ++i) ax[i] -= want[i];
+            if (me == 0) std::printf("mixed %s iter %d info %lld\n", v ? "gesv" : "posv", iter, (long long)inf);
+            report(inf || iter < 0 ? (v ? "gesv_mixed-FAILED" : "posv_mixed-FAILED") : (v ? "gesv_mixed" : "posv_mixed"),
+                   rel<T>(ax, want));
+        }
+    }
 }
 
 int main(int argc, char** argv) {

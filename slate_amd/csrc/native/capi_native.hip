@@ -157,6 +157,73 @@ int64_t h_posv(char uplo, i64 n, i64 nrhs, T* a, i64 lda, T* b, i64 ldb) {
     return h_potrs<T>(uplo, n, nrhs, a, lda, b, ldb);
 }
 
+// LAPACK dsposv / zcposv and dsgesv / zcgesv: A unchanged unless the
+// working-precision fallback ran (then it holds the factors), X = A^-1 B
+template <typename T>
+int64_t h_posv_mixed(char uplo, i64 n, i64 nrhs, T* a, i64 lda, const T* b, i64 ldb, T* x, i64 ldx, int* iter) {
+    uplo = up(uplo);
+    if (uplo != 'L' && uplo != 'U') return -1;
+    if (n < 0) return -2;
+    if (nrhs < 0) return -3;
+    if (lda < std::max<i64>(1, n)) return -5;
+    if (ldb < std::max<i64>(1, n)) return -7;
+    if (ldx < std::max<i64>(1, n)) return -9;
+    if (n == 0 || nrhs == 0) return 0;
+    return guarded([&]() -> int64_t {
+        int p, q;
+        grid_of(p, q);
+        const i64 nb = nb_of(n);
+        sn::Matrix<T> G(n, n, nb, p, q);
+        G.from_host(a, lda);
+        sn::HermitianMatrix<T> A(sn::Uplo::Lower, n, nb, p, q);
+        if (uplo == 'U') sn::copy(sn::Op::ConjTrans, G, A);       // the stored upper triangle, as lower
+        else sn::copy(sn::Op::NoTrans, G, A);
+        sn::Matrix<T> B(n, nrhs, nb, p, q), X(n, nrhs, nb, p, q);
+        B.from_host(b, ldb);
+        const int64_t info = sn::posv_mixed(A, B, X, *iter);
+        X.to_host(x, ldx);
+        if (*iter < 0) {                                          // fallback: A holds the Cholesky factor
+            if (uplo == 'U') {
+                sn::copy(sn::Op::ConjTrans, A, G);
+                std::vector<T> f((size_t)n * n);
+                G.to_host(f.data(), n);
+                for (i64 j = 0; j < n; ++j)
+                    for (i64 i = 0; i <= j; ++i) a[i + j * lda] = f[i + j * n];
+            } else {
+                std::vector<T> f((size_t)n * n);
+                A.to_host(f.data(), n);
+                for (i64 j = 0; j < n; ++j)
+                    for (i64 i = j; i < n; ++i) a[i + j * lda] = f[i + j * n];
+            }
+        }
+        return info;
+    });
+}
+
+template <typename T>
+int64_t h_gesv_mixed(i64 n, i64 nrhs, T* a, i64 lda, int64_t* ipiv, const T* b, i64 ldb, T* x, i64 ldx, int* iter) {
+    if (n < 0) return -1;
+    if (nrhs < 0) return -2;
+    if (lda < std::max<i64>(1, n)) return -4;
+    if (ldb < std::max<i64>(1, n)) return -7;
+    if (ldx < std::max<i64>(1, n)) return -9;
+    if (n == 0 || nrhs == 0) return 0;
+    return guarded([&]() -> int64_t {
+        int p, q;
+        grid_of(p, q);
+        const i64 nb = nb_of(n);
+        sn::Matrix<T> A(n, n, nb, p, q), B(n, nrhs, nb, p, q), X(n, nrhs, nb, p, q);
+        A.from_host(a, lda);
+        B.from_host(b, ldb);
+        std::vector<int64_t> piv;
+        const int64_t info = sn::gesv_mixed(A, piv, B, X, *iter);
+        X.to_host(x, ldx);
+        if (*iter < 0) A.to_host(a, lda);
+        for (size_t i = 0; i < piv.size(); ++i) ipiv[i] = piv[i] + 1;
+        return info;
+    });
+}
+
 template <typename T>
 int64_t h_getrf(i64 m, i64 n, T* a, i64 lda, int64_t* ipiv) {
     if (m < 0) return -1;
@@ -839,6 +906,28 @@ SN_LAPACK(d, double)
 SN_LAPACK_C(c, float)
 SN_LAPACK_C(z, double)
 #undef SN_LAPACK_C
+
+// ---- mixed precision, LAPACK names (dsposv, dsgesv, zcposv, zcgesv), by value
+int slate_dsposv(char uplo, int64_t n, int64_t nrhs, double* a, int64_t lda, const double* b, int64_t ldb, double* x,
+                 int64_t ldx, int* iter) {
+    return (int)h_posv_mixed<double>(uplo, n, nrhs, a, lda, b, ldb, x, ldx, iter);
+}
+int slate_dsgesv(int64_t n, int64_t nrhs, double* a, int64_t lda, int64_t* ipiv, const double* b, int64_t ldb,
+                 double* x, int64_t ldx, int* iter) {
+    return (int)h_gesv_mixed<double>(n, nrhs, a, lda, ipiv, b, ldb, x, ldx, iter);
+}
+int slate_zcposv(char uplo, int64_t n, int64_t nrhs, double* a, int64_t lda, const double* b, int64_t ldb,
+                 double* x, int64_t ldx, int* iter) {
+    using Z = std::complex<double>;
+    return (int)h_posv_mixed<Z>(uplo, n, nrhs, reinterpret_cast<Z*>(a), lda, reinterpret_cast<const Z*>(b), ldb,
+                                reinterpret_cast<Z*>(x), ldx, iter);
+}
+int slate_zcgesv(int64_t n, int64_t nrhs, double* a, int64_t lda, int64_t* ipiv, const double* b, int64_t ldb,
+                 double* x, int64_t ldx, int* iter) {
+    using Z = std::complex<double>;
+    return (int)h_gesv_mixed<Z>(n, nrhs, reinterpret_cast<Z*>(a), lda, ipiv, reinterpret_cast<const Z*>(b), ldb,
+                                reinterpret_cast<Z*>(x), ldx, iter);
+}
 
 // ---- BLACS over the native runtime's ranks
 void Cblacs_pinfo(int* mypnum, int* nprocs) {

@@ -21,6 +21,7 @@
 // src/gemmC.cc:39-202, src/work/work_trsm.cc:102-265 (SLATE's OpenMP task
 // DAGs over MPI).
 #include <algorithm>
+#include <limits>
 #include <functional>
 #include <map>
 #include <cmath>
@@ -1412,6 +1413,111 @@ void trmm(Side side, Uplo uplo, Op op, Diag diag, T alpha, const Matrix<T>& A, M
     copy<T>(Op::NoTrans, W, B);
 }
 
+// ------------------------------------------------------------ mixed precision
+// Reference: src/posv_mixed.cc, src/gesv_mixed.cc (LAPACK dsposv / dsgesv):
+// factor in the lower precision (half the bytes, ~2x the MFMA rate), then
+// iterative refinement in the working precision, R = B - A X with the
+// full-precision A; fall back to the working-precision solve when the
+// low-precision factorization fails or 30 steps do not converge
+// (iter < 0 then, as in LAPACK).
+template <typename T> struct lower_prec;
+template <> struct lower_prec<double> { using type = float; };
+template <> struct lower_prec<std::complex<double>> { using type = std::complex<float>; };
+
+template <typename Hi, typename Lo>
+static void convert(const Matrix<Hi>& A, Matrix<Lo>& B) {
+    const Storage& SA = *A.storage();
+    const Storage& SB = *B.storage();
+    if (SA.m != SB.m || SA.n != SB.n || SA.nb != SB.nb || SA.p != SB.p || SA.q != SB.q)
+        throw Error("native convert: same shape and grid");
+    hipStream_t s = rt().main;
+    if (SA.mloc && SA.nloc)
+        slate_hip::gecopy<K<Hi>, K<Lo>>('G', 'N', SA.mloc, SA.nloc, kp(static_cast<const Hi*>(SA.buf)), SA.lld,
+                                        kp(static_cast<Lo*>(SB.buf)), SB.lld, s);
+    NHIP(hipStreamSynchronize(s));
+}
+
+// X += D (same grid)
+template <typename T>
+static void add_to(const Matrix<T>& D, Matrix<T>& X) {
+    const Storage& SD = *D.storage();
+    const Storage& SX = *X.storage();
+    hipStream_t s = rt().main;
+    if (SX.mloc && SX.nloc)
+        slate_hip::geadd<K<T>>('G', SX.mloc, SX.nloc, kv(T(1)), kp(static_cast<const T*>(SD.buf)), SD.lld, kv(T(1)),
+                               kp(static_cast<T*>(SX.buf)), SX.lld, s);
+    NHIP(hipStreamSynchronize(s));
+}
+
+// shared refinement loop: solve_lo(R_lo) overwrites R_lo with op^-1 R_lo in
+// the low precision; Af is the full working-precision matrix
+template <typename T, typename Solve>
+static bool refine(const Matrix<T>& Af, const Matrix<T>& B, Matrix<T>& X, int& iter, Solve&& solve_lo,
+                   const Options& opts) {
+    using Lo = typename lower_prec<T>::type;
+    using Rl = real_t<T>;
+    const Storage& SB = *B.storage();
+    const i64 n = Af.storage()->n;
+    const double eps = std::numeric_limits<Rl>::epsilon();
+    const double cte = norm<T>(Norm::Max, Af) * eps * std::sqrt((double)n);
+    Matrix<Lo> Rlo(SB.m, SB.n, SB.nb, SB.p, SB.q);
+    convert<T, Lo>(B, Rlo);
+    solve_lo(Rlo);
+    convert<Lo, T>(Rlo, X);
+    Matrix<T> R(SB.m, SB.n, SB.nb, SB.p, SB.q), D(SB.m, SB.n, SB.nb, SB.p, SB.q);
+    const int itermax = 30;
+    for (int it = 0; it <= itermax; ++it) {
+        copy<T>(Op::NoTrans, B, R);
+        gemm<T>(T(-1), Af, X, T(1), R, opts);                   // R = B - A X
+        if (norm<T>(Norm::Max, R) <= norm<T>(Norm::Max, X) * cte) {
+            iter = it;
+            return true;
+        }
+        if (it == itermax) break;
+        convert<T, Lo>(R, Rlo);
+        solve_lo(Rlo);
+        convert<Lo, T>(Rlo, D);
+        add_to<T>(D, X);
+    }
+    return false;
+}
+
+template <typename T>
+int64_t posv_mixed(HermitianMatrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, const Options& opts) {
+    using Lo = typename lower_prec<T>::type;
+    const Storage& SA = *A.storage();
+    HermitianMatrix<Lo> Al(A.uplo(), SA.n, SA.nb, SA.p, SA.q);
+    convert<T, Lo>(A, Al);
+    iter = 0;
+    if (potrf<Lo>(Al, opts) == 0) {
+        const Matrix<T> Af = expand_tri<T>(A, A.uplo(), 1);
+        if (refine<T>(Af, B, X, iter, [&](Matrix<Lo>& R) { potrs<Lo>(Al, R, opts); }, opts)) return 0;
+        iter = -31;
+    } else {
+        iter = -3;                                              // LAPACK: the low-precision factorization failed
+    }
+    copy<T>(Op::NoTrans, B, X);
+    return posv<T>(A, X, opts);
+}
+
+template <typename T>
+int64_t gesv_mixed(Matrix<T>& A, std::vector<int64_t>& ipiv, Matrix<T>& B, Matrix<T>& X, int& iter,
+                   const Options& opts) {
+    using Lo = typename lower_prec<T>::type;
+    const Storage& SA = *A.storage();
+    Matrix<Lo> Al(SA.m, SA.n, SA.nb, SA.p, SA.q);
+    convert<T, Lo>(A, Al);
+    iter = 0;
+    if (getrf<Lo>(Al, ipiv, opts) == 0) {
+        if (refine<T>(A, B, X, iter, [&](Matrix<Lo>& R) { getrs<Lo>(Al, ipiv, R, opts); }, opts)) return 0;
+        iter = -31;
+    } else {
+        iter = -3;
+    }
+    copy<T>(Op::NoTrans, B, X);
+    return gesv<T>(A, ipiv, X, opts);
+}
+
 // ------------------------------------------------------------ norm
 template <typename T>
 double norm(Norm kind, const Matrix<T>& A) {
@@ -1645,6 +1751,13 @@ SLATE_NATIVE_INST(double)
 SLATE_NATIVE_INST(std::complex<float>)
 SLATE_NATIVE_INST(std::complex<double>)
 #undef SLATE_NATIVE_INST
+#define SLATE_NATIVE_MIXED(T)                                                                                  \
+    template int64_t posv_mixed<T>(HermitianMatrix<T>&, Matrix<T>&, Matrix<T>&, int&, const Options&);        \
+    template int64_t gesv_mixed<T>(Matrix<T>&, std::vector<int64_t>&, Matrix<T>&, Matrix<T>&, int&,          \
+                                   const Options&);
+SLATE_NATIVE_MIXED(double)
+SLATE_NATIVE_MIXED(std::complex<double>)
+#undef SLATE_NATIVE_MIXED
 
 }  // namespace native
 }  // namespace slate_amd

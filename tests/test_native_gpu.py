@@ -43,7 +43,7 @@ def test_native_library_exports_lapack_scalapack_blacs():
     names = {l.split()[-1] for l in nm.splitlines() if l.split()}
     want = ["Cblacs_gridinit", "Cblacs_gridinfo", "blacs_gridinfo_", "numroc_", "descinit_",
             "slate_dgesv", "slate_dgetrf_", "slate_zposv", "slate_sgemm_", "slate_dtrsm_", "slate_dgels",
-            "slate_zgels", "slate_dgels_"]
+            "slate_zgels", "slate_dgels_", "slate_dsposv", "slate_dsgesv", "slate_zcposv", "slate_zcgesv"]
     for x in "sdcz":
         want += [f"p{x}potrf_", f"p{x}posv_", f"p{x}getrf_", f"p{x}gesv_", f"p{x}getrs_", f"p{x}gemm_",
                  f"p{x}trsm_", f"p{x}lange_", f"p{x}gels_", f"p{x}syrk_", f"p{x}syr2k_", f"p{x}symm_",
@@ -111,6 +111,9 @@ def _assert_checks(checks, out):
                                                    "trsm_lc", "gels", "herk", "her2k_upper", "syrk",
                                                    "syr2k_upper", "hemm_left", "symm_right", "trmm_luc")]
     for name in names:
+        assert name in checks, (name, out)
+        assert float(checks[name]) < TOL[name[-1]], (name, checks[name])
+    for name in [f"{w}_{x}" for x in "dz" for w in ("posv_mixed", "gesv_mixed")]:
         assert name in checks, (name, out)
         assert float(checks[name]) < TOL[name[-1]], (name, checks[name])
     for name in ("capi_dgesv", "capi_zposv", "capi_dgemm_tn"):
