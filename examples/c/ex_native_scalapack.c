@@ -13,6 +13,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 void Cblacs_pinfo(int* mypnum, int* nprocs);
 void Cblacs_get(int ctxt, int what, int* val);
@@ -50,6 +51,12 @@ void pdsyrk_(const char* uplo, const char* trans, const int* n, const int* k, co
 void pdtrmm_(const char* side, const char* uplo, const char* ta, const char* diag, const int* m, const int* n,
              const double* alpha, const double* a, const int* ia, const int* ja, const int* desca, double* b,
              const int* ib, const int* jb, const int* descb);
+void pdpotri_(const char* uplo, const int* n, double* a, const int* ia, const int* ja, const int* desca, int* info);
+void pdgetri_(const int* n, double* a, const int* ia, const int* ja, const int* desca, const int* ipiv, double* work,
+              const int* lwork, int* iwork, const int* liwork, int* info);
+void pdsymm_(const char* side, const char* uplo, const int* m, const int* n, const double* alpha, const double* a,
+             const int* ia, const int* ja, const int* desca, const double* b, const int* ib, const int* jb,
+             const int* descb, const double* beta, double* c, const int* ic, const int* jc, const int* descc);
 void slate_amd_finalize(void);
 
 static int g_rank;
@@ -121,6 +128,33 @@ int main(int argc, char** argv) {
     pdpotrf_("U", &n, a, &one, &one, desca, &info);
     pdpotrs_("U", &n, &nrhs, a, &one, &one, desca, b, &one, &one, descb, &info);
     check(info ? "pdpotrs_upper-FAILED" : "pdpotrs_upper", ERR_B());
+
+    /* inverses: x = A^-1 (A x) through pdsymm_ / pdgemm_ */
+    {
+        double* t = calloc((size_t)lld * (rloc > 0 ? rloc : 1), sizeof(double));
+        const double a1 = 1.0, b0 = 0.0;
+        int lw = -1, liw = -1;
+        double wq;
+        int iwq;
+        FILL_A(sym);
+        FILL_B(sym);
+        pdpotrf_("L", &n, a, &one, &one, desca, &info);
+        pdpotri_("L", &n, a, &one, &one, desca, &info);
+        pdsymm_("L", "L", &n, &nrhs, &a1, a, &one, &one, desca, b, &one, &one, descb, &b0, t, &one, &one, descb);
+        memcpy(b, t, sizeof(double) * lld * (rloc > 0 ? rloc : 1));
+        check(info ? "pdpotri-FAILED" : "pdpotri", ERR_B());
+        FILL_A(gen);
+        FILL_B(gen);
+        pdgetrf_(&n, &n, a, &one, &one, desca, ipiv, &info);
+        pdgetri_(&n, a, &one, &one, desca, ipiv, &wq, &lw, &iwq, &liw, &info);   /* workspace query */
+        lw = 1;
+        liw = 1;
+        pdgetri_(&n, a, &one, &one, desca, ipiv, &wq, &lw, &iwq, &liw, &info);
+        pdgemm_("N", "N", &n, &nrhs, &n, &a1, a, &one, &one, desca, b, &one, &one, descb, &b0, t, &one, &one, descb);
+        memcpy(b, t, sizeof(double) * lld * (rloc > 0 ? rloc : 1));
+        check(info ? "pdgetri-FAILED" : "pdgetri", ERR_B());
+        free(t);
+    }
 
     /* LU */
     FILL_A(gen);

@@ -371,6 +371,36 @@ void run(int p, int q, int me) {
         }
         report("trmm_luc", rel<T>(d, want));
     }
+    // ---- inverses: || A A^-1 - I || through the host
+    for (int v = 0; v < 2; ++v) {
+        const int64_t ni = 150;
+        std::vector<T> h0((size_t)ni * ni), hi((size_t)ni * ni);
+        if (v == 0) {
+            sn::HermitianMatrix<T> Hm(sn::Uplo::Lower, ni, nb, p, q);
+            Hm.generate(sn::Gen::HermitianPositiveDefinite, 111);
+            Hm.to_host(h0.data(), ni);
+            for (int64_t j = 0; j < ni; ++j)
+                for (int64_t i = 0; i < j; ++i) h0[i + j * ni] = cj(h0[j + i * ni]);
+            sn::potrf(Hm);
+            sn::potri(Hm);
+            Hm.to_host(hi.data(), ni);
+            for (int64_t j = 0; j < ni; ++j)
+                for (int64_t i = 0; i < j; ++i) hi[i + j * ni] = cj(hi[j + i * ni]);
+        } else {
+            sn::Matrix<T> Gm(ni, ni, nb, p, q);
+            Gm.generate(sn::Gen::DiagDominant, 112);
+            Gm.to_host(h0.data(), ni);
+            std::vector<int64_t> pv;
+            sn::getrf(Gm, pv);
+            sn::getri(Gm, pv);
+            Gm.to_host(hi.data(), ni);
+        }
+        auto prod = mul<T>('N', 'N', ni, ni, ni, h0, ni, hi, ni);
+        std::vector<std::complex<double>> eye(prod.size());
+        for (int64_t i = 0; i < ni; ++i) eye[(size_t)(i + i * ni)] = 1.0;
+        for (size_t i = 0; i < prod.size(); ++i) prod[i] -= eye[i];
+        report(v ? "getri" : "potri", rel<T>(prod, eye));
+    }
     // ---- mixed precision (double / complex<double>): low-precision factors +
     // refinement must reach the working-precision residual
     if constexpr (std::is_same<T, double>::value || std::is_same<T, std::complex<double>>::value) {

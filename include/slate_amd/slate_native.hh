@@ -188,6 +188,10 @@ void trmm(Side side, Uplo uplo, Op op, Diag diag, T alpha, const Matrix<T>& A, M
 // F keeps the per-panel compact-WY factors T (device).  unmqr applies
 // op(Q) (NoTrans or ConjTrans; real types: Trans == ConjTrans) from the
 // left; gels solves min ||A X - B|| for m >= n (X in the top n rows of BX).
+// inverses from the factors: potri after potrf (stored triangle), getri after getrf
+template <typename T> int64_t potri(HermitianMatrix<T>& A, const Options& opts = {});
+template <typename T> int64_t getri(Matrix<T>& A, const std::vector<int64_t>& ipiv, const Options& opts = {});
+
 // mixed precision (double / complex<double> only): factor in float /
 // complex<float>, refine in the working precision; X = A^-1 B, B unchanged;
 // iter = refinement steps, < 0 when the working-precision solve ran instead

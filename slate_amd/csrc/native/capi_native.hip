@@ -699,6 +699,50 @@ void scal_scale_tri(const int* desc, int n, char uplo, T beta, T* c) {
         }
 }
 
+// p?potri_: the inverse from the Cholesky factor, over the uplo triangle
+template <typename T>
+int p_potri(char uplo, int n, T* a, int ia, int ja, const int* desca) {
+    uplo = up(uplo);
+    if (uplo != 'L' && uplo != 'U') return -1;
+    if (n == 0) return 0;
+    return (int)guarded([&]() -> int64_t {
+        sn::Matrix<T> G = scal_matrix<T>(desca, n, n, ia, ja, a);
+        sn::HermitianMatrix<T> L(sn::Uplo::Lower, n, G.nb(), G.p(), G.q());
+        sn::copy(uplo == 'U' ? sn::Op::ConjTrans : sn::Op::NoTrans, G, L);   // U = L^H: the factor as lower
+        sn::potri(L);
+        sn::copy(uplo == 'U' ? sn::Op::ConjTrans : sn::Op::NoTrans, L, G);
+        std::vector<T> loc((size_t)desca[8] * std::max<i64>(G.nloc(), 1));
+        scal_back(G, desca, loc.data());
+        const int p = G.p(), r = sn::rank();
+        for (i64 lj = 0; lj < G.nloc(); ++lj)
+            for (i64 li = 0; li < G.mloc(); ++li) {
+                const i64 gi = sn::l2g(li, G.nb(), p, r % p), gj = sn::l2g(lj, G.nb(), G.q(), r / p);
+                if (uplo == 'L' ? gi >= gj : gi <= gj) a[li + lj * desca[8]] = loc[li + lj * desca[8]];
+            }
+        return 0;
+    });
+}
+
+// p?getri_: the inverse from the LU factors and ScaLAPACK pivots; lwork /
+// liwork = -1 are workspace queries (the library allocates its own)
+template <typename T>
+int p_getri(int n, T* a, int ia, int ja, const int* desca, const int* ipiv, T* work, int lwork, int* iwork,
+            int liwork) {
+    if (lwork == -1 || liwork == -1) {
+        if (work) work[0] = T(1);
+        if (iwork) iwork[0] = 1;
+        return 0;
+    }
+    if (n == 0) return 0;
+    return (int)guarded([&]() -> int64_t {
+        sn::Matrix<T> A = scal_matrix<T>(desca, n, n, ia, ja, a);
+        const std::vector<int64_t> piv = ipiv_from_local(A, n, ipiv);
+        sn::getri(A, piv);
+        scal_back(A, desca, a);
+        return 0;
+    });
+}
+
 // p?syrk_ / p?herk_ / p?syr2k_ / p?her2k_ (whole matrices, ia = ja = 1)
 template <typename T>
 void p_rank_k(bool herm, bool two, char uplo, char trans, int n, int k, T alpha, const T* a, int ia, int ja,
@@ -1061,6 +1105,14 @@ SN_SCAL(z, std::complex<double>)
                      const int* n, const T* alpha, const T* a, const int* ia, const int* ja, const int* desca, \
                      T* b, const int* ib, const int* jb, const int* descb) {                                \
         p_trmm<T>(*side, *uplo, *ta, *diag, *m, *n, *alpha, a, *ia, *ja, desca, b, *ib, *jb, descb);        \
+    }                                                                                                      \
+    void p##X##potri_(const char* uplo, const int* n, T* a, const int* ia, const int* ja, const int* desca,   \
+                      int* info) {                                                                         \
+        *info = p_potri<T>(*uplo, *n, a, *ia, *ja, desca);                                                 \
+    }                                                                                                      \
+    void p##X##getri_(const int* n, T* a, const int* ia, const int* ja, const int* desca, const int* ipiv,  \
+                      T* work, const int* lwork, int* iwork, const int* liwork, int* info) {                \
+        *info = p_getri<T>(*n, a, *ia, *ja, desca, ipiv, work, *lwork, iwork, *liwork);                    \
     }
 SN_SCAL3(s, float)
 SN_SCAL3(d, double)

@@ -1413,6 +1413,67 @@ void trmm(Side side, Uplo uplo, Op op, Diag diag, T alpha, const Matrix<T>& A, M
     copy<T>(Op::NoTrans, W, B);
 }
 
+// ------------------------------------------------------------ inverses
+// Reference: src/potri.cc (trtri + trtrm), src/getri.cc.  Here the inverse
+// is the solve against the identity with the existing factors (potrs /
+// getrs: two triangular solves over n right-hand sides on the grid),
+// written back over the factors.
+
+// n x n identity on A's grid
+template <typename T>
+static Matrix<T> identity_like(const Storage& S) {
+    Matrix<T> I(S.n, S.n, S.nb, S.p, S.q);
+    Storage& SI = *I.storage();
+    hipStream_t s = rt().main;
+    const i64 nt = (S.n + S.nb - 1) / S.nb;
+    for (i64 k = 0; k < nt; ++k) {
+        if ((int)(k % S.p) != S.pr || (int)(k % S.q) != S.pc) continue;
+        const i64 kb = std::min(S.nb, S.n - k * S.nb);
+        T* d = static_cast<T*>(SI.buf) + tiles_before(k, S.p, S.pr) * S.nb + tiles_before(k, S.q, S.pc) * S.nb * SI.lld;
+        slate_hip::geset<K<T>>('G', kb, kb, kv(T(0)), kv(T(1)), kp(d), SI.lld, s);
+    }
+    NHIP(hipStreamSynchronize(s));
+    return I;
+}
+
+// A^-1 from the Cholesky factor in A (potrf first); the stored triangle
+// of A receives the inverse
+template <typename T>
+int64_t potri(HermitianMatrix<T>& A, const Options& opts) {
+    const Storage& S = *A.storage();
+    Matrix<T> X = identity_like<T>(S);
+    potrs<T>(A, X, opts);
+    const slate_hip::TriMask mk = tri_mask(S, A.uplo());
+    hipStream_t s = rt().main;
+    const Storage& SX = *X.storage();
+    if (S.mloc && S.nloc) {
+        // stored triangle <- X, the other part of A unchanged: mask X in place, zero A's triangle, add
+        T* x = static_cast<T*>(SX.buf);
+        slate_hip::gecopy_mask<K<T>>(mk, S.mloc, S.nloc, kp(x), SX.lld, kp(x), SX.lld, true, s);
+        Matrix<T> Keep(S.m, S.n, S.nb, S.p, S.q);
+        const Storage& SK = *Keep.storage();
+        const slate_hip::TriMask other = tri_mask(S, A.uplo() == Uplo::Lower ? Uplo::Upper : Uplo::Lower, -1);
+        slate_hip::gecopy_mask<K<T>>(other, S.mloc, S.nloc, kp(static_cast<const T*>(S.buf)), S.lld,
+                                     kp(static_cast<T*>(SK.buf)), SK.lld, false, s);
+        slate_hip::geadd<K<T>>('G', S.mloc, S.nloc, kv(T(1)), kp(x), SX.lld, kv(T(1)), kp(static_cast<T*>(SK.buf)),
+                               SK.lld, s);
+        copy2d(static_cast<T*>(S.buf), S.lld, static_cast<const T*>(SK.buf), SK.lld, S.mloc, S.nloc, s);
+    }
+    NHIP(hipStreamSynchronize(s));
+    return 0;
+}
+
+// A^-1 from the LU factors in A and ipiv (getrf first), over A
+template <typename T>
+int64_t getri(Matrix<T>& A, const std::vector<int64_t>& ipiv, const Options& opts) {
+    const Storage& S = *A.storage();
+    if (S.m != S.n) throw Error("native getri: square matrix");
+    Matrix<T> X = identity_like<T>(S);
+    getrs<T>(A, ipiv, X, opts);
+    copy<T>(Op::NoTrans, X, A);
+    return 0;
+}
+
 // ------------------------------------------------------------ mixed precision
 // Reference: src/posv_mixed.cc, src/gesv_mixed.cc (LAPACK dsposv / dsgesv):
 // factor in the lower precision (half the bytes, ~2x the MFMA rate), then
@@ -1745,7 +1806,9 @@ int64_t gels(Matrix<T>& A, Matrix<T>& BX, const Options& opts) {
     template void syr2k<T>(Op, T, const Matrix<T>&, const Matrix<T>&, T, HermitianMatrix<T>&, const Options&); \
     template void hemm<T>(Side, T, const HermitianMatrix<T>&, const Matrix<T>&, T, Matrix<T>&, const Options&);  \
     template void symm<T>(Side, T, const HermitianMatrix<T>&, const Matrix<T>&, T, Matrix<T>&, const Options&);  \
-    template void trmm<T>(Side, Uplo, Op, Diag, T, const Matrix<T>&, Matrix<T>&, const Options&);
+    template void trmm<T>(Side, Uplo, Op, Diag, T, const Matrix<T>&, Matrix<T>&, const Options&);             \
+    template int64_t potri<T>(HermitianMatrix<T>&, const Options&);                                           \
+    template int64_t getri<T>(Matrix<T>&, const std::vector<int64_t>&, const Options&);
 SLATE_NATIVE_INST(float)
 SLATE_NATIVE_INST(double)
 SLATE_NATIVE_INST(std::complex<float>)

@@ -47,7 +47,7 @@ def test_native_library_exports_lapack_scalapack_blacs():
     for x in "sdcz":
         want += [f"p{x}potrf_", f"p{x}posv_", f"p{x}getrf_", f"p{x}gesv_", f"p{x}getrs_", f"p{x}gemm_",
                  f"p{x}trsm_", f"p{x}lange_", f"p{x}gels_", f"p{x}syrk_", f"p{x}syr2k_", f"p{x}symm_",
-                 f"p{x}trmm_"]
+                 f"p{x}trmm_", f"p{x}potri_", f"p{x}getri_"]
     want += ["pcherk_", "pzherk_", "pcher2k_", "pzher2k_", "pchemm_", "pzhemm_"]
     missing = [w for w in want if w not in names]
     assert not missing, missing
@@ -109,7 +109,8 @@ def _assert_checks(checks, out):
     names = [f"{w}_{x}" for x in "sdcz" for w in ("potrf", "potrs", "gesv", "getrs_conjtrans", "getrf_rect",
                                                    "gemm", "gemm_ct", "norm_max", "norm_fro", "norm_one",
                                                    "trsm_lc", "gels", "herk", "her2k_upper", "syrk",
-                                                   "syr2k_upper", "hemm_left", "symm_right", "trmm_luc")]
+                                                   "syr2k_upper", "hemm_left", "symm_right", "trmm_luc",
+                                                   "potri", "getri")]
     for name in names:
         assert name in checks, (name, out)
         assert float(checks[name]) < TOL[name[-1]], (name, checks[name])
@@ -163,7 +164,7 @@ def test_native_scalapack_from_c_without_python(grid):
         outs = [(r.returncode, r.stdout + r.stderr)]
     else:
         outs = _run_ranks(CEXE, [grid], p * q)
-    names = ("pdpotrs", "pdpotrs_upper", "pdgesv", "pdgetrs", "pdlange_fro", "pdgemm_tn", "pdsyrk_lower", "pdtrmm_lun",
+    names = ("pdpotrs", "pdpotrs_upper", "pdgesv", "pdgetrs", "pdlange_fro", "pdgemm_tn", "pdsyrk_lower", "pdtrmm_lun", "pdpotri", "pdgetri",
              "pzgesv", "slate_dgetrf_")
     for rank, (rc, out) in enumerate(outs):
         print(out)
