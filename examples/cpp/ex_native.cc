@@ -346,6 +346,15 @@ void run(int p, int q, int me) {
             d[i] = cd(hc1[i]) - want[i];
         }
         report(v ? "symm_right" : "hemm_left", rel<T>(d, want));
+        // the structured norm of the stored triangle against the host full matrix
+        double one = 0;
+        for (int64_t j = 0; j < na; ++j) {
+            double cs = 0;
+            for (int64_t i = 0; i < na; ++i) cs += std::abs(hh[i + j * na]);
+            one = std::fmax(one, cs);
+        }
+        const double nrm = v ? sn::norm_symmetric(sn::Norm::One, H) : sn::norm(sn::Norm::One, H);
+        report(v ? "norm_sym_one" : "norm_herm_one", std::fabs(nrm - one) / one);
     }
     // ---- trmm: B = alpha A^H B, A upper triangular with a unit diagonal
     {
@@ -370,6 +379,10 @@ void run(int p, int q, int me) {
             d[i] = cd(hb1[i]) - want[i];
         }
         report("trmm_luc", rel<T>(d, want));
+        double fr = 0;
+        for (const T& e : ht) fr += std::norm(e);
+        report("norm_tri_fro", std::fabs(sn::norm_triangular(sn::Norm::Fro, sn::Uplo::Upper, sn::Diag::Unit, Tm) -
+                                         std::sqrt(fr)) / std::sqrt(fr));
     }
     // ---- inverses: || A A^-1 - I || through the host
     for (int v = 0; v < 2; ++v) {

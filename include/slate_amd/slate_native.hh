@@ -151,6 +151,11 @@ void trsm(Side side, Uplo uplo, Op op, Diag diag, T alpha, const Matrix<T>& A, M
           const Options& opts = {});
 template <typename T> double norm(Norm kind, const Matrix<T>& A);
 
+// norms of a stored triangle: Hermitian, symmetric, triangular (square)
+template <typename T> double norm(Norm kind, const HermitianMatrix<T>& A);
+template <typename T> double norm_symmetric(Norm kind, const HermitianMatrix<T>& A);
+template <typename T> double norm_triangular(Norm kind, Uplo uplo, Diag diag, const Matrix<T>& A);
+
 // real type of a scalar (herk / her2k scaling factors)
 template <typename T> struct real_of { using type = T; };
 template <typename R> struct real_of<std::complex<R>> { using type = R; };

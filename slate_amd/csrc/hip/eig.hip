@@ -225,7 +225,11 @@ INST2(float) INST2(double) INST2(ccplx) INST2(zcplx)
 namespace {
 constexpr int TB = 64;            // band / sweeps per block
 constexpr int TCW = 64;           // Z columns per workgroup
-constexpr int SV = TB + 2;        // LDS row pitch of the raw reflectors
+// LDS row pitch of the raw reflectors: = 3 (mod 32) doubles.  The W = V^T Z
+// A-operand read Vr[(16 wr + li) SV + w - 16 wr - li] (w = k0 + lk) of a
+// half-wave then lands on double (SV - 1) li + lk = 2 li + lk (mod 32): 32
+// distinct bank pairs (TB + 2 gave li + lk: 2-way, PMC 24 % conflict cycles)
+constexpr int SV = TB + 3;
 // LDS column pitch of the Z window (column-major): = 2 (mod 32) doubles, so
 // the B-operand reads Zs[(16 j + li) SZ + row(lk)] of a half-wave (li 0..15,
 // lk 0..1) land on 2 li + lk = 32 distinct bank pairs (2 TB + 4 = 4 mod 32

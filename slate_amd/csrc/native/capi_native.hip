@@ -817,6 +817,27 @@ void p_trmm(char side, char uplo, char ta, char diag, int m, int n, T alpha, con
     if (rc != 0) std::fprintf(stderr, "slate_amd native p?trmm_: %s\n", g_err.c_str());
 }
 
+// p?lansy_ / p?lanhe_ / p?lantr_ (square triangular)
+template <typename T>
+double p_lan_struct(int kind, char norm, char uplo, char diag, int n, const T* a, int ia, int ja, const int* desca) {
+    if (n == 0) return 0.0;
+    double r = -1.0;
+    const int64_t rc = guarded([&]() -> int64_t {
+        const char k = up(norm) == 'M' ? 'M' : up(norm) == 'I' ? 'I' : (up(norm) == 'F' || up(norm) == 'E') ? 'F' : '1';
+        const sn::Uplo ul = up(uplo) == 'U' ? sn::Uplo::Upper : sn::Uplo::Lower;
+        if (kind == 0) {
+            sn::Matrix<T> A = scal_matrix<T>(desca, n, n, ia, ja, a);
+            r = sn::norm_triangular((sn::Norm)k, ul, up(diag) == 'U' ? sn::Diag::Unit : sn::Diag::NonUnit, A);
+        } else {
+            sn::HermitianMatrix<T> A = scal_tri<T>(desca, n, ia, ja, a, up(uplo));
+            r = kind == 1 ? sn::norm((sn::Norm)k, A) : sn::norm_symmetric((sn::Norm)k, A);
+        }
+        return 0;
+    });
+    if (rc != 0) std::fprintf(stderr, "slate_amd native p?lan*_: %s\n", g_err.c_str());
+    return r;
+}
+
 template <typename T>
 double p_lange(char norm, int m, int n, const T* a, int ia, int ja, const int* desca) {
     if (m == 0 || n == 0) return 0.0;
@@ -1158,6 +1179,33 @@ float pclange_(const char* norm, const int* m, const int* n, const std::complex<
 double pzlange_(const char* norm, const int* m, const int* n, const std::complex<double>* a, const int* ia,
                 const int* ja, const int* desca, double*) {
     return p_lange<std::complex<double>>(*norm, *m, *n, a, *ia, *ja, desca);
+}
+
+#define SN_LAN(X, T, R)                                                                                        \
+    R p##X##lansy_(const char* norm, const char* uplo, const int* n, const T* a, const int* ia, const int* ja, \
+                   const int* desca, R*) {                                                                   \
+        return (R)p_lan_struct<T>(2, *norm, *uplo, 'N', *n, a, *ia, *ja, desca);                            \
+    }                                                                                                        \
+    R p##X##lantr_(const char* norm, const char* uplo, const char* diag, const int* m, const int* n,          \
+                   const T* a, const int* ia, const int* ja, const int* desca, R*) {                         \
+        if (*m != *n) {                                                                                      \
+            g_err = "native p?lantr_: square matrices only";                                                 \
+            return (R)-1;                                                                                    \
+        }                                                                                                    \
+        return (R)p_lan_struct<T>(0, *norm, *uplo, *diag, *n, a, *ia, *ja, desca);                          \
+    }
+SN_LAN(s, float, float)
+SN_LAN(d, double, double)
+SN_LAN(c, std::complex<float>, float)
+SN_LAN(z, std::complex<double>, double)
+#undef SN_LAN
+float pclanhe_(const char* norm, const char* uplo, const int* n, const std::complex<float>* a, const int* ia,
+               const int* ja, const int* desca, float*) {
+    return (float)p_lan_struct<std::complex<float>>(1, *norm, *uplo, 'N', *n, a, *ia, *ja, desca);
+}
+double pzlanhe_(const char* norm, const char* uplo, const int* n, const std::complex<double>* a, const int* ia,
+                const int* ja, const int* desca, double*) {
+    return p_lan_struct<std::complex<double>>(1, *norm, *uplo, 'N', *n, a, *ia, *ja, desca);
 }
 
 // ---- earlier native entry points (kept)

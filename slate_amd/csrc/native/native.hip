@@ -1413,6 +1413,21 @@ void trmm(Side side, Uplo uplo, Op op, Diag diag, T alpha, const Matrix<T>& A, M
     copy<T>(Op::NoTrans, W, B);
 }
 
+// norms of the structured matrices (src/norm.cc: henorm / synorm / trnorm):
+// the stored triangle expanded to the full matrix, then the general norm
+template <typename T>
+double norm(Norm kind, const HermitianMatrix<T>& A) {
+    return norm<T>(kind, expand_tri<T>(A, A.uplo(), 1));
+}
+template <typename T>
+double norm_symmetric(Norm kind, const HermitianMatrix<T>& A) {
+    return norm<T>(kind, expand_tri<T>(A, A.uplo(), 2));
+}
+template <typename T>
+double norm_triangular(Norm kind, Uplo uplo, Diag diag, const Matrix<T>& A) {
+    return norm<T>(kind, expand_tri<T>(A, uplo, 0, diag));
+}
+
 // ------------------------------------------------------------ inverses
 // Reference: src/potri.cc (trtri + trtrm), src/getri.cc.  Here the inverse
 // is the solve against the identity with the existing factors (potrs /
@@ -1808,7 +1823,10 @@ int64_t gels(Matrix<T>& A, Matrix<T>& BX, const Options& opts) {
     template void symm<T>(Side, T, const HermitianMatrix<T>&, const Matrix<T>&, T, Matrix<T>&, const Options&);  \
     template void trmm<T>(Side, Uplo, Op, Diag, T, const Matrix<T>&, Matrix<T>&, const Options&);             \
     template int64_t potri<T>(HermitianMatrix<T>&, const Options&);                                           \
-    template int64_t getri<T>(Matrix<T>&, const std::vector<int64_t>&, const Options&);
+    template int64_t getri<T>(Matrix<T>&, const std::vector<int64_t>&, const Options&);                        \
+    template double norm<T>(Norm, const HermitianMatrix<T>&);                                                 \
+    template double norm_symmetric<T>(Norm, const HermitianMatrix<T>&);                                       \
+    template double norm_triangular<T>(Norm, Uplo, Diag, const Matrix<T>&);
 SLATE_NATIVE_INST(float)
 SLATE_NATIVE_INST(double)
 SLATE_NATIVE_INST(std::complex<float>)

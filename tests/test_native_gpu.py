@@ -47,8 +47,9 @@ def test_native_library_exports_lapack_scalapack_blacs():
     for x in "sdcz":
         want += [f"p{x}potrf_", f"p{x}posv_", f"p{x}getrf_", f"p{x}gesv_", f"p{x}getrs_", f"p{x}gemm_",
                  f"p{x}trsm_", f"p{x}lange_", f"p{x}gels_", f"p{x}syrk_", f"p{x}syr2k_", f"p{x}symm_",
-                 f"p{x}trmm_", f"p{x}potri_", f"p{x}getri_"]
-    want += ["pcherk_", "pzherk_", "pcher2k_", "pzher2k_", "pchemm_", "pzhemm_"]
+                 f"p{x}trmm_", f"p{x}potri_", f"p{x}getri_", f"p{x}lansy_",
+                 f"p{x}lantr_"]
+    want += ["pclanhe_", "pzlanhe_", "pcherk_", "pzherk_", "pcher2k_", "pzher2k_", "pchemm_", "pzhemm_"]
     missing = [w for w in want if w not in names]
     assert not missing, missing
 
@@ -110,7 +111,8 @@ def _assert_checks(checks, out):
                                                    "gemm", "gemm_ct", "norm_max", "norm_fro", "norm_one",
                                                    "trsm_lc", "gels", "herk", "her2k_upper", "syrk",
                                                    "syr2k_upper", "hemm_left", "symm_right", "trmm_luc",
-                                                   "potri", "getri")]
+                                                   "potri", "getri", "norm_herm_one", "norm_sym_one",
+                                                   "norm_tri_fro")]
     for name in names:
         assert name in checks, (name, out)
         assert float(checks[name]) < TOL[name[-1]], (name, checks[name])
