@@ -319,6 +319,12 @@ unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const
     const int ncw = (int)min((i64)TCW, ncols - c0);
     // window row w of group t lives in Zs at column-major row ((w >> 6) + t) & 1) * 64 + (w & 63)
     auto zrow = [](int w, i64 t) { return (int)((((w >> 6) + t) & 1) * TB + (w & (TB - 1))); };
+    // Zs element (column c, physical row r): the row's lowest bit flipped
+    // for columns 8..15 of every 16, so the accumulator stores (16
+    // contiguous lanes = 16 columns of one row, ds_write banks (a/4) mod 32)
+    // put columns c and c + 8 on different banks; every read pattern stays
+    // conflict-free (a permutation inside aligned row pairs)
+    auto zi = [](int c, int r) { return c * SZ + (r ^ ((c >> 3) & 1)); };
     // register staging (software pipeline): thread (wv, lane) moves element
     // (row lane, column wv + 8 i) of a Z half and reflector element
     // (jj = wv + 8 i, vi = lane) of a group, i < 8
@@ -341,14 +347,14 @@ unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const
     };
     auto put_z = [&](int phys) {
         #pragma unroll
-        for (int i = 0; i < PR; ++i) Zs[(wv + 8 * i) * SZ + phys * TB + lane] = pz[i];
+        for (int i = 0; i < PR; ++i) Zs[zi(wv + 8 * i, phys * TB + lane)] = pz[i];
     };
     auto store_half = [&](i64 row0, int phys) {
         #pragma unroll
         for (int i = 0; i < PR; ++i) {
             const int cc = wv + 8 * i;
             const i64 row = row0 + lane;
-            if (cc < ncw && row < n) Z[(c0 + cc) * ldz + row] = Zs[cc * SZ + phys * TB + lane];
+            if (cc < ncw && row < n) Z[(c0 + cc) * ldz + row] = Zs[zi(cc, phys * TB + lane)];
         }
     };
     for (i64 J = (nsw - 1) / TB; J >= 0; --J) {
@@ -396,7 +402,7 @@ unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const
                 const int pr = zrow(w, t);
                 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
-                    const double b = Zs[(16 * (2 * wc + j) + li) * SZ + pr];
+                    const double b = Zs[zi(16 * (2 * wc + j) + li, pr)];
                     acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[j], 0, 0, 0);
                 }
             }
@@ -415,7 +421,7 @@ unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const
                     for (int j = 0; j < 2; ++j)
                         #pragma unroll
                         for (int r = 0; r < 4; ++r)
-                            zc[ri][j][r] = Zs[(16 * (2 * wc + j) + li) * SZ + zrow(32 * wr + 16 * ri + lk + 4 * r, t)];
+                            zc[ri][j][r] = Zs[zi(16 * (2 * wc + j) + li, zrow(32 * wr + 16 * ri + lk + 4 * r, t))];
                 #pragma unroll
                 for (int k0 = 0; k0 < TB; k0 += 4) {
                     const int jj = k0 + lk;
@@ -436,7 +442,7 @@ unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const
                     for (int j = 0; j < 2; ++j)
                         #pragma unroll
                         for (int r = 0; r < 4; ++r)
-                            Zs[(16 * (2 * wc + j) + li) * SZ + zrow(32 * wr + 16 * ri + lk + 4 * r, t)] = zc[ri][j][r];
+                            Zs[zi(16 * (2 * wc + j) + li, zrow(32 * wr + 16 * ri + lk + 4 * r, t))] = zc[ri][j][r];
             }
             __syncthreads();
             if (more) {
