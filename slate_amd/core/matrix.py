@@ -861,7 +861,7 @@ class Pivots:
         dev = torch.device(dev)
         if self._dev is None or self._dev.device != dev:
             src = self._dev if self._dev is not None else self._host
-            self._dev = src.to(dev)
+            self._dev = src.to(dev, non_blocking=src.device.type == "cpu" and src.is_pinned())
         return self._dev
 
     def __len__(self):

@@ -55,6 +55,19 @@ def _dense_hermitian(A):
     from .aux import allgather_dense
     D = allgather_dense(A)
     up = A.uploPhysical()
+    if up in (Uplo.Lower, Uplo.Upper) and D.dim() == 2 and D.shape[0] == D.shape[1]:
+        # stored triangle (real diagonal) + the strict opposite triangle of
+        # D^H: four slate kernels, no torch compute on the device
+        n = D.shape[0]
+        D = _cm(D)
+        keep = 1 if up == Uplo.Lower else 2
+        H = ops.colmajor_empty(n, n, D.dtype, D.device)
+        T = ops.colmajor_empty(n, n, D.dtype, D.device)
+        ops.gecopy_mask(D, H, (keep, 1 << 40, 1, 0, 1, 0, 0, 0, 0), real_diag=True)
+        ops.gecopy(D, T, trans=conj_trans(D.dtype))
+        ops.gecopy_mask(T, T, (3 - keep, 1 << 40, 1, 0, 1, 0, 0, 0, -1))
+        ops.geadd(1.0, T, 1.0, H)
+        return H
     if up == Uplo.Lower:
         L = torch.tril(D)
     elif up == Uplo.Upper:
@@ -155,10 +168,10 @@ def he2hb(Af: torch.Tensor, nb: int):
 
 
 def _zero_strict_lower(P):
+    """P's strictly lower part set to zero in place (one slate kernel)."""
     m, k = P.shape
-    if m > 1:
-        mask = torch.ones(m, k, dtype=torch.bool, device=P.device).tril(-1)
-        P.masked_fill_(mask, 0)
+    if m > 1 and k:
+        ops.gecopy_mask(P, P, (2, 1 << 40, 1, 0, 1, 0, 0, 0, 0))
 
 
 def unmtr_he2hb(F: He2hbFactors, Z: torch.Tensor):
@@ -337,18 +350,23 @@ def unmtr_hb2st(F: Hb2stFactors, Z: torch.Tensor):
     if Z.is_cuda and n > 1 and F.count > 0 and Z.shape[0] == n and \
             os.environ.get("SLATE_AMD_UNMTR_BLOCKED", "1") != "0":
         # all sweeps in one launch, blocks of b sweeps (csrc/hip/eig.hip)
-        spd = F.sweep_ptr.to(dev).contiguous()
-        ntd = (spd[1:] - spd[:-1]).contiguous()
+        # the schedule's index arrays on the host (O(n) ints), uploaded once
+        import numpy as np
+        sph = F.sweep_ptr.cpu().numpy().astype(np.int64)
+        nth = (sph[1:] - sph[:-1]).astype(np.int64)
+        up = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.int64)).to(dev)
+        spd, ntd = up(sph), up(nth)
         if Z.dtype == torch.float64 and b == 64 and os.environ.get("SLATE_AMD_UNMTR_MFMA", "1") != "0":
             # groups of b reflectors as block reflectors I - V T V^H on MFMA:
             # group g = (block J, task t); T of every group built once
             nsw = n - 1
-            TJ = ntd[::b].contiguous()
-            ng = int(TJ.sum())
-            gJ = torch.repeat_interleave(torch.arange(TJ.numel(), device=dev), TJ)
-            gptr = torch.zeros(TJ.numel() + 1, dtype=torch.int64, device=dev)
-            gptr[1:] = torch.cumsum(TJ, 0)
-            gt = torch.arange(ng, device=dev) - gptr[gJ]
+            TJh = nth[::b]
+            ng = int(TJh.sum())
+            gJh = np.repeat(np.arange(TJh.size, dtype=np.int64), TJh)
+            gptrh = np.zeros(TJh.size + 1, dtype=np.int64)
+            gptrh[1:] = np.cumsum(TJh)
+            gth = np.arange(ng, dtype=np.int64) - gptrh[gJh]
+            gJ, gptr, gt = up(gJh), up(gptrh), up(gth)
             Tg = torch.empty(max(ng, 1) * 2 * b * b, dtype=torch.float64, device=dev)   # Y = V T per group
             with trace_block("unmtr_hb2st"):
                 _native.hip().unmtr_hb2st_mfma(n, Z.shape[1], Z.data_ptr(), max(1, Z.stride(1)),
@@ -572,7 +590,8 @@ def heev(A, Lambda=None, Z=None, opts=None):
         Af = _cm(_dense_hermitian(A).to(dev))
         n = Af.shape[0]
         # scale to a safe range (heev.cc:66-80)
-        amax = Af.abs().max().item() if n else 0.0
+        from ._util import read_to_host
+        amax = float(read_to_host(ops.genorm_local('M', Af)[0]).max()) if n else 0.0
         scale = 1.0
         if amax > 0 and (amax < 1e-140 or amax > 1e140):
             scale = 1.0 / amax
@@ -603,10 +622,12 @@ def heev(A, Lambda=None, Z=None, opts=None):
 
 
 def _band_only(Af, nb):
+    """Copy of Af restricted to the band |i - j| <= nb (two masked copies)."""
     n = Af.shape[0]
-    i = torch.arange(n, device=Af.device)
-    mask = (i[:, None] - i[None, :]).abs() <= nb
-    return torch.where(mask, Af, torch.zeros_like(Af))
+    B = ops.colmajor_empty(n, n, Af.dtype, Af.device)
+    ops.gecopy_mask(Af, B, (2, 1 << 40, 1, 0, 1, 0, 0, 0, nb))        # i <= j + nb
+    ops.gecopy_mask(B, B, (1, 1 << 40, 1, 0, 1, 0, 0, 0, nb))         # i + nb >= j
+    return B
 
 
 def _my_cols(Z):

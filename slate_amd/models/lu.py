@@ -319,7 +319,7 @@ def _getrf_p1(A, buf, thr, la, nopiv, T=None, no_inv=False):
     if rm and nloc and m:
         ops.gecopy(T, buf[:m, :nloc], trans='T')
     if nopiv:
-        glob = torch.arange(min(m, n), dtype=torch.int64, device=dev)
+        glob = _identity_pivots(min(m, n), dev)
     else:
         glob = _global_pivots(ipiv[:min(m, n)], nb)
     info = _reduce_info(A, infos, kt, nb)
@@ -362,9 +362,19 @@ def _native_mod(t):
 
 
 def _global_pivots(ipiv, nb):
-    """Panel-relative pivots (panel k starts at row k*nb) -> global rows (device op)."""
-    idx = torch.arange(ipiv.numel(), dtype=torch.int64, device=ipiv.device)
-    return ipiv + torch.div(idx, nb, rounding_mode="floor") * nb
+    """Panel-relative pivots (panel k starts at row k*nb) -> global rows, as
+    a pinned host tensor: read once at the end of the factorization next to
+    the info values (no torch index kernels on the device; Pivots uploads it
+    again, non-blocking, when a solve needs it there)."""
+    from ._util import read_to_host
+    h = read_to_host(ipiv).numpy()
+    g = h + (np.arange(h.size, dtype=np.int64) // nb) * nb
+    return torch.from_numpy(g).pin_memory() if ipiv.is_cuda else torch.from_numpy(g)
+
+
+def _identity_pivots(k, dev):
+    t = torch.arange(k, dtype=torch.int64)
+    return t.pin_memory() if dev.type == "cuda" else t
 
 
 def _update_cols(buf, Lp, ipiv, r0, kb, m, c0, c1, nopiv, Linv=None):
@@ -607,7 +617,7 @@ def _getrf_general(A, buf, thr, la, mode, leaf):
                           0, lc_k, colu, k, "left")
     ss.join()
     if mode == "nopiv":
-        glob = torch.arange(min(m, n), dtype=torch.int64, device=dev)
+        glob = _identity_pivots(min(m, n), dev)
     else:
         glob = _global_pivots(ipiv[:min(m, n)], nb)
     info = _reduce_info(A, infos, kt, nb)
