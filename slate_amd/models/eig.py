@@ -214,8 +214,7 @@ def _merge_reflectors(group):
         kb = V.shape[1]
         off = r - r0
         Vg[off:, c:c + kb].copy_(V)
-        Ti = torch.triu(T[:kb, :kb])
-        Tg[c:c + kb, c:c + kb].copy_(Ti)
+        ops.gecopy_mask(T[:kb, :kb], Tg[c:c + kb, c:c + kb], (2, 1 << 40, 1, 0, 1, 0, 0, 0, 0))   # triu
         if c:
             # T12 = -T_prev (V_prev^H V_i) T_i over the rows V_i spans
             S = ops.colmajor_empty(c, kb, dt, dev)
@@ -610,8 +609,11 @@ def heev(A, Lambda=None, Z=None, opts=None):
         if want:
             # back-transform only this rank's columns of Z
             cols = _my_cols(Z)
-            Zl = _cm(Zt.to(dev)[:, cols].to(Af.dtype)) if len(cols) else \
-                torch.zeros(n, 0, dtype=Af.dtype, device=dev)
+            if cols == list(range(n)):                # every column local: no gather
+                Zl = _cm(Zt.to(dev).to(Af.dtype))
+            else:
+                Zl = _cm(Zt.to(dev)[:, cols].to(Af.dtype)) if len(cols) else \
+                    torch.zeros(n, 0, dtype=Af.dtype, device=dev)
             Zl = _cm(Zl.clone())
             unmtr_hb2st(F2, Zl)
             unmtr_he2hb(F1, Zl)
@@ -645,8 +647,11 @@ def _scatter_cols(Z, Zl, cols):
     lb = Z.local_block()
     if s.bc is None or lb.mloc == 0 or lb.nloc == 0:
         return
-    rows = torch.tensor([lb.global_row(i) for i in range(lb.mloc)], device=Zl.device)
-    lb.data.copy_(Zl[rows].to(lb.data.device, lb.data.dtype))
+    rows = [lb.global_row(i) for i in range(lb.mloc)]
+    if rows == list(range(Zl.shape[0])):
+        lb.data.copy_(Zl.to(lb.data.device, lb.data.dtype))           # all rows local: a plain copy
+    else:
+        lb.data.copy_(Zl[torch.tensor(rows, device=Zl.device)].to(lb.data.device, lb.data.dtype))
     s.mark_local_modified(s.origin_slot)
 
 

@@ -16,8 +16,10 @@ import slate_amd as sl
 pytestmark = pytest.mark.gpu
 
 # data movement / initialisation kernels (torch fills for zero-initialised
-# workspaces, copies between layouts, runtime memcpy / memset)
-_ALLOWED = re.compile(r"slate_hip|[Cc]opy|[Mm]emcpy|[Mm]emset|FillFunctor|fill_kernel|__amd_rocclr")
+# workspaces, copies between layouts, runtime memcpy / memset, and indexed
+# gathers / scatters -- pure data movement, no arithmetic)
+_ALLOWED = re.compile(r"slate_hip|[Cc]opy|[Mm]emcpy|[Mm]emset|FillFunctor|fill_kernel|__amd_rocclr|"
+                      r"index_put_kernel_impl|index_kernel_impl<")
 
 
 def _kernels(fn):
@@ -70,4 +72,26 @@ def test_factorizations_launch_only_own_kernels(routine):
         fn = lambda: sl.geqrf(A, T, _dev())
     names = _kernels(fn)
     assert any("slate_hip" in k for k in names), names      # the profiler saw the device work
+    assert not _foreign(names), _foreign(names)
+
+
+def test_heev_launches_only_own_kernels():
+    """dsyevd with vectors on one GPU: stage 1, the chase, divide & conquer
+    and both back-transforms run slate kernels only (plus copies)."""
+    n = 1024
+    dev = torch.device("cuda", 0)
+
+    def problem():
+        A = sl.HermitianMatrix(sl.Uplo.Lower, n, nb=256, device=dev)
+        A.insertLocalTiles(device=dev)
+        sl.generate_matrix(A, "rands", seed=5)
+        Z = sl.Matrix(n, n, nb=256, device=dev)
+        Z.insertLocalTiles(device=dev)
+        return A, Z
+
+    A, Z = problem()
+    sl.heev(A, None, Z, _dev())                      # warm-up: workspaces, caches
+    A, Z = problem()
+    names = _kernels(lambda: sl.heev(A, None, Z, _dev()))
+    assert any("hb2st" in k for k in names), names
     assert not _foreign(names), _foreign(names)
