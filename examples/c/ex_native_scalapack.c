@@ -57,6 +57,13 @@ void pdgetri_(const int* n, double* a, const int* ia, const int* ja, const int* 
 void pdsymm_(const char* side, const char* uplo, const int* m, const int* n, const double* alpha, const double* a,
              const int* ia, const int* ja, const int* desca, const double* b, const int* ib, const int* jb,
              const int* descb, const double* beta, double* c, const int* ic, const int* jc, const int* descc);
+void pdlaset_(const char* uplo, const int* m, const int* n, const double* alpha, const double* beta, double* a,
+              const int* ia, const int* ja, const int* desca);
+void pdlacpy_(const char* uplo, const int* m, const int* n, const double* a, const int* ia, const int* ja,
+              const int* desca, double* b, const int* ib, const int* jb, const int* descb);
+void pdgeadd_(const char* trans, const int* m, const int* n, const double* alpha, const double* a, const int* ia,
+              const int* ja, const int* desca, const double* beta, double* c, const int* ic, const int* jc,
+              const int* descc);
 void slate_amd_finalize(void);
 
 static int g_rank;
@@ -128,6 +135,23 @@ int main(int argc, char** argv) {
     pdpotrf_("U", &n, a, &one, &one, desca, &info);
     pdpotrs_("U", &n, &nrhs, a, &one, &one, desca, b, &one, &one, descb, &info);
     check(info ? "pdpotrs_upper-FAILED" : "pdpotrs_upper", ERR_B());
+
+    /* aux: pdlaset_ (0.5 off the diagonal, 3 on it), pdlacpy_, pdgeadd_ (C = 2 A - C = A) */
+    {
+        const double h = 0.5, three = 3.0, two = 2.0, m1 = -1.0;
+        double* c2 = calloc((size_t)lld * (nloc > 0 ? nloc : 1), sizeof(double));
+        pdlaset_("G", &n, &n, &h, &three, a, &one, &one, desca);
+        pdlacpy_("G", &n, &n, a, &one, &one, desca, c2, &one, &one, desca);
+        pdgeadd_("N", &n, &n, &two, a, &one, &one, desca, &m1, c2, &one, &one, desca);
+        double ae = 0;
+        for (int lj = 0; lj < nloc; ++lj)
+            for (int li = 0; li < mloc; ++li) {
+                const double want = l2g(li, nb, p, pr) == l2g(lj, nb, q, pc) ? 3.0 : 0.5;
+                ae = fmax(ae, fabs(c2[li + lj * lld] - want));
+            }
+        check("pdlaset_lacpy_geadd", ae);
+        free(c2);
+    }
 
     /* inverses: x = A^-1 (A x) through pdsymm_ / pdgemm_ */
     {

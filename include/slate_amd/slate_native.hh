@@ -151,6 +151,10 @@ void trsm(Side side, Uplo uplo, Op op, Diag diag, T alpha, const Matrix<T>& A, M
           const Options& opts = {});
 template <typename T> double norm(Norm kind, const Matrix<T>& A);
 
+// B = alpha A + beta B; A = offdiag everywhere, diag on the global diagonal
+template <typename T> void add(T alpha, const Matrix<T>& A, T beta, Matrix<T>& B);
+template <typename T> void set(T offdiag, T diag, Matrix<T>& A);
+
 // norms of a stored triangle: Hermitian, symmetric, triangular (square)
 template <typename T> double norm(Norm kind, const HermitianMatrix<T>& A);
 template <typename T> double norm_symmetric(Norm kind, const HermitianMatrix<T>& A);

@@ -1181,6 +1181,53 @@ double pzlange_(const char* norm, const int* m, const int* n, const std::complex
     return p_lange<std::complex<double>>(*norm, *m, *n, a, *ia, *ja, desca);
 }
 
+// p?geadd_ (sub(C) = beta sub(C) + alpha op(sub(A)); op = N), p?laset_, p?lacpy_ (uplo 'G')
+#define SN_AUX(X, T)                                                                                           \
+    void p##X##geadd_(const char* trans, const int* m, const int* n, const T* alpha, const T* a, const int* ia, \
+                      const int* ja, const int* desca, const T* beta, T* c, const int* ic, const int* jc,     \
+                      const int* descc) {                                                                  \
+        if (*m == 0 || *n == 0) return;                                                                    \
+        const int64_t rc = guarded([&]() -> int64_t {                                                      \
+            if (up(*trans) != 'N') throw sn::Error("native p?geadd_: trans = 'N' only");                  \
+            sn::Matrix<T> A = scal_matrix<T>(desca, *m, *n, *ia, *ja, a);                                   \
+            sn::Matrix<T> C = scal_matrix<T>(descc, *m, *n, *ic, *jc, c);                                   \
+            sn::add(*alpha, A, *beta, C);                                                                  \
+            scal_back(C, descc, c);                                                                        \
+            return 0;                                                                                      \
+        });                                                                                                \
+        if (rc != 0) std::fprintf(stderr, "slate_amd native p?geadd_: %s\n", g_err.c_str());              \
+    }                                                                                                      \
+    void p##X##laset_(const char* uplo, const int* m, const int* n, const T* alpha, const T* beta, T* a,     \
+                      const int* ia, const int* ja, const int* desca) {                                    \
+        if (*m == 0 || *n == 0) return;                                                                    \
+        const int64_t rc = guarded([&]() -> int64_t {                                                      \
+            if (up(*uplo) != 'G' && up(*uplo) != 'A') throw sn::Error("native p?laset_: uplo = 'G' only"); \
+            sn::Matrix<T> A = scal_matrix<T>(desca, *m, *n, *ia, *ja, a);                                   \
+            sn::set(*alpha, *beta, A);                                                                     \
+            scal_back(A, desca, a);                                                                        \
+            return 0;                                                                                      \
+        });                                                                                                \
+        if (rc != 0) std::fprintf(stderr, "slate_amd native p?laset_: %s\n", g_err.c_str());              \
+    }                                                                                                      \
+    void p##X##lacpy_(const char* uplo, const int* m, const int* n, const T* a, const int* ia, const int* ja, \
+                      const int* desca, T* b, const int* ib, const int* jb, const int* descb) {             \
+        if (*m == 0 || *n == 0) return;                                                                    \
+        const int64_t rc = guarded([&]() -> int64_t {                                                      \
+            if (up(*uplo) != 'G' && up(*uplo) != 'A') throw sn::Error("native p?lacpy_: uplo = 'G' only"); \
+            sn::Matrix<T> A = scal_matrix<T>(desca, *m, *n, *ia, *ja, a);                                   \
+            sn::Matrix<T> B = scal_matrix<T>(descb, *m, *n, *ib, *jb, b);                                   \
+            sn::copy(sn::Op::NoTrans, A, B);                                                               \
+            scal_back(B, descb, b);                                                                        \
+            return 0;                                                                                      \
+        });                                                                                                \
+        if (rc != 0) std::fprintf(stderr, "slate_amd native p?lacpy_: %s\n", g_err.c_str());              \
+    }
+SN_AUX(s, float)
+SN_AUX(d, double)
+SN_AUX(c, std::complex<float>)
+SN_AUX(z, std::complex<double>)
+#undef SN_AUX
+
 #define SN_LAN(X, T, R)                                                                                        \
     R p##X##lansy_(const char* norm, const char* uplo, const int* n, const T* a, const int* ia, const int* ja, \
                    const int* desca, R*) {                                                                   \

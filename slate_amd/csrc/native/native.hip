@@ -1428,6 +1428,38 @@ double norm_triangular(Norm kind, Uplo uplo, Diag diag, const Matrix<T>& A) {
     return norm<T>(kind, expand_tri<T>(A, uplo, 0, diag));
 }
 
+// ------------------------------------------------------------ aux (src/add.cc, src/set.cc)
+// B = alpha A + beta B (same grid): one local kernel
+template <typename T>
+void add(T alpha, const Matrix<T>& A, T beta, Matrix<T>& B) {
+    const Storage& SA = *A.storage();
+    const Storage& SB = *B.storage();
+    if (SA.m != SB.m || SA.n != SB.n || SA.nb != SB.nb || SA.p != SB.p || SA.q != SB.q)
+        throw Error("native add: A and B must share shape, grid and nb");
+    hipStream_t s = rt().main;
+    if (SB.mloc && SB.nloc)
+        slate_hip::geadd<K<T>>('G', SB.mloc, SB.nloc, kv(alpha), kp(static_cast<const T*>(SA.buf)), SA.lld, kv(beta),
+                               kp(static_cast<T*>(SB.buf)), SB.lld, s);
+    NHIP(hipStreamSynchronize(s));
+}
+
+// A = offdiag off the global diagonal, diag on it
+template <typename T>
+void set(T offdiag, T diag, Matrix<T>& A) {
+    const Storage& S = *A.storage();
+    hipStream_t s = rt().main;
+    T* a = static_cast<T*>(S.buf);
+    if (S.mloc && S.nloc) slate_hip::geset<K<T>>('G', S.mloc, S.nloc, kv(offdiag), kv(offdiag), kp(a), S.lld, s);
+    const i64 nt = (std::min(S.m, S.n) + S.nb - 1) / S.nb;
+    for (i64 k = 0; k < nt; ++k) {
+        if ((int)(k % S.p) != S.pr || (int)(k % S.q) != S.pc) continue;
+        const i64 mb = std::min(S.nb, S.m - k * S.nb), nbk = std::min(S.nb, S.n - k * S.nb);
+        T* d = a + tiles_before(k, S.p, S.pr) * S.nb + tiles_before(k, S.q, S.pc) * S.nb * S.lld;
+        slate_hip::geset<K<T>>('G', mb, nbk, kv(offdiag), kv(diag), kp(d), S.lld, s);
+    }
+    NHIP(hipStreamSynchronize(s));
+}
+
 // ------------------------------------------------------------ inverses
 // Reference: src/potri.cc (trtri + trtrm), src/getri.cc.  Here the inverse
 // is the solve against the identity with the existing factors (potrs /
@@ -1826,7 +1858,9 @@ int64_t gels(Matrix<T>& A, Matrix<T>& BX, const Options& opts) {
     template int64_t getri<T>(Matrix<T>&, const std::vector<int64_t>&, const Options&);                        \
     template double norm<T>(Norm, const HermitianMatrix<T>&);                                                 \
     template double norm_symmetric<T>(Norm, const HermitianMatrix<T>&);                                       \
-    template double norm_triangular<T>(Norm, Uplo, Diag, const Matrix<T>&);
+    template double norm_triangular<T>(Norm, Uplo, Diag, const Matrix<T>&);                                   \
+    template void add<T>(T, const Matrix<T>&, T, Matrix<T>&);                                                 \
+    template void set<T>(T, T, Matrix<T>&);
 SLATE_NATIVE_INST(float)
 SLATE_NATIVE_INST(double)
 SLATE_NATIVE_INST(std::complex<float>)

@@ -48,7 +48,7 @@ def test_native_library_exports_lapack_scalapack_blacs():
         want += [f"p{x}potrf_", f"p{x}posv_", f"p{x}getrf_", f"p{x}gesv_", f"p{x}getrs_", f"p{x}gemm_",
                  f"p{x}trsm_", f"p{x}lange_", f"p{x}gels_", f"p{x}syrk_", f"p{x}syr2k_", f"p{x}symm_",
                  f"p{x}trmm_", f"p{x}potri_", f"p{x}getri_", f"p{x}lansy_",
-                 f"p{x}lantr_"]
+                 f"p{x}lantr_", f"p{x}geadd_", f"p{x}laset_", f"p{x}lacpy_"]
     want += ["pclanhe_", "pzlanhe_", "pcherk_", "pzherk_", "pcher2k_", "pzher2k_", "pchemm_", "pzhemm_"]
     missing = [w for w in want if w not in names]
     assert not missing, missing
@@ -166,7 +166,7 @@ def test_native_scalapack_from_c_without_python(grid):
         outs = [(r.returncode, r.stdout + r.stderr)]
     else:
         outs = _run_ranks(CEXE, [grid], p * q)
-    names = ("pdpotrs", "pdpotrs_upper", "pdgesv", "pdgetrs", "pdlange_fro", "pdgemm_tn", "pdsyrk_lower", "pdtrmm_lun", "pdpotri", "pdgetri",
+    names = ("pdpotrs", "pdpotrs_upper", "pdgesv", "pdgetrs", "pdlange_fro", "pdgemm_tn", "pdsyrk_lower", "pdtrmm_lun", "pdpotri", "pdgetri", "pdlaset_lacpy_geadd",
              "pzgesv", "slate_dgetrf_")
     for rank, (rc, out) in enumerate(outs):
         print(out)
