@@ -282,7 +282,10 @@ def _hb2st_device(B: torch.Tensor, nb: int, dev):
     lag = max(3, int(os.environ.get("SLATE_AMD_HB2ST_LAG", 3)))
     if os.environ.get("SLATE_AMD_HB2ST_EARLY", "1") != "0":
         lag = 2
-    nwg = int(min(max(nsw, 1), props.multi_processor_count, max(8, nt0 // lag + 8)))
+    # ~nt0 / 3 workgroups: fewer sweeps in flight than the lag allows leave
+    # more L2 / memory bandwidth to the ones that are (dsyevd n = 16384,
+    # profiles/r4: 100 workgroups 2.089-2.102 s, 136 = nt0 / lag + 8: 2.128-2.148 s)
+    nwg = int(min(max(nsw, 1), props.multi_processor_count, max(8, min(nt0 // lag + 8, nt0 // 3 + 15))))
     nwg = int(os.environ.get("SLATE_AMD_HB2ST_WG", nwg))
     with trace_block("hb2st"):
         if nsw > 0:
