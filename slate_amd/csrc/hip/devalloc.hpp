@@ -59,6 +59,20 @@ inline size_t dev_cap() {
     return cap;
 }
 
+inline size_t dev_trim_locked(DevAlloc& A) {
+    size_t freed = 0;
+    for (auto& kv : A.free_) {
+        HIP_CHECK(hipEventSynchronize(kv.second.ev));
+        HIP_CHECK(hipEventDestroy(kv.second.ev));
+        HIP_CHECK(hipFree(kv.second.p));
+        A.size_.erase(kv.second.p);
+        A.reserved -= kv.first;
+        freed += kv.first;
+    }
+    A.free_.clear();
+    return freed;
+}
+
 inline void* dev_alloc(size_t bytes, hipStream_t s) {
     if (bytes == 0) return nullptr;
     DevAlloc& A = dev_allocator();
@@ -79,10 +93,25 @@ inline void* dev_alloc(size_t bytes, hipStream_t s) {
     if (A.reserved + r > dev_cap())
         for (auto it = lo; it != A.free_.end() && it->first < 2 * r; ++it) return take(it, true);
     void* p = nullptr;
-    HIP_CHECK(hipMalloc(&p, r));
+    if (hipMalloc(&p, r) != hipSuccess) {
+        // out of device memory: give every cached block back to the driver
+        // (each waited for: its last user may still be running) and retry once
+        (void)hipGetLastError();
+        dev_trim_locked(A);
+        p = nullptr;
+        HIP_CHECK(hipMalloc(&p, r));
+    }
     A.size_[p] = r;
     A.reserved += r;
     return p;
+}
+
+// Release every cached (free) block to the driver; live blocks are kept.
+// Called on hipMalloc failure and by the native runtime's finalize().
+inline size_t dev_trim() {
+    DevAlloc& A = dev_allocator();
+    std::lock_guard<std::mutex> g(A.mu);
+    return dev_trim_locked(A);
 }
 
 inline void dev_free(void* p, hipStream_t s) {

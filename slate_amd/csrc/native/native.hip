@@ -69,18 +69,8 @@ void initialize() {
     NHIP(hipStreamCreateWithPriority(&R.panel, hipStreamNonBlocking, hi));
     NHIP(hipStreamCreateWithPriority(&R.update, hipStreamNonBlocking, lo));
     NHIP(hipStreamCreateWithPriority(&R.comm, hipStreamNonBlocking, hi));
-    // LU: the persistent panel runs <= 32 workgroups; its trailing update
-    // leaves those CUs free (same CU mask as the Python driver, streams.py)
-    {
-        hipDeviceProp_t pr;
-        NHIP(hipGetDeviceProperties(&pr, R.device));
-        const int ncu = pr.multiProcessorCount, reserve = 32;
-        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-        for (int b = reserve; b < ncu; ++b) mask[b / 32] |= 1u << (b % 32);
-        NHIP(hipExtStreamCreateWithCUMask(&R.update_masked, (uint32_t)mask.size(), mask.data()));
-    }
     // diagnostics: SLATE_AMD_NATIVE_SERIAL=1 issues everything on one stream
-    if (env_int("SLATE_AMD_NATIVE_SERIAL", 0)) R.panel = R.update = R.update_masked = R.comm = R.main;
+    if (env_int("SLATE_AMD_NATIVE_SERIAL", 0)) R.panel = R.update = R.comm = R.main;
     const size_t lw = slate_hip::getrf_work_bytes();
     NHIP(hipMalloc(&R.lu_work, lw));
     NHIP(hipMemset(R.lu_work, 0, lw));
@@ -100,12 +90,47 @@ void finalize() {
     transport_finalize();
     (void)hipFree(R.lu_work);
     (void)hipFree(R.qr_work);
-    std::vector<hipStream_t> ss{R.main, R.panel, R.update, R.update_masked, R.comm};
+    slate_hip::dev_trim();              // cached scratch blocks back to the driver
+    std::vector<hipStream_t> ss{R.main, R.panel, R.update, R.comm};
     std::sort(ss.begin(), ss.end());
     ss.erase(std::unique(ss.begin(), ss.end()), ss.end());
     for (hipStream_t s : ss) (void)hipStreamDestroy(s);
     R.up = false;
 }
+
+void set_update_reservation(int cus) {
+    Runtime& R = rt();
+    if (cus == R.update_res || R.update == R.main) return;
+    NHIP(hipStreamSynchronize(R.update));
+    NHIP(hipStreamDestroy(R.update));
+    hipDeviceProp_t pr;
+    NHIP(hipGetDeviceProperties(&pr, R.device));
+    const int ncu = pr.multiProcessorCount;
+    if (cus > 0 && cus < ncu) {
+        // the first mask bits map round-robin to the 8 XCDs: the reserved CUs
+        // are spread evenly (same mask as the Python driver, streams.py)
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+        for (int b = cus; b < ncu; ++b) mask[b / 32] |= 1u << (b % 32);
+        NHIP(hipExtStreamCreateWithCUMask(&R.update, (uint32_t)mask.size(), mask.data()));
+    } else {
+        int lo = 0, hi = 0;
+        NHIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        NHIP(hipStreamCreateWithPriority(&R.update, hipStreamNonBlocking, lo));
+        cus = 0;
+    }
+    R.update_res = cus;
+}
+
+namespace {
+// RAII: the LU trailing update leaves the persistent panel's CUs free for the
+// duration of one factorization, then the update stream is unmasked again
+struct UpdateReservation {
+    explicit UpdateReservation(int cus) { set_update_reservation(cus); }
+    ~UpdateReservation() {
+        try { set_update_reservation(0); } catch (...) {}
+    }
+};
+}  // namespace
 
 int rank() { initialize(); return rt().rank; }
 int size() { initialize(); return rt().size; }
@@ -991,7 +1016,8 @@ int64_t getrf(Matrix<T>& A, std::vector<int64_t>& ipiv_out, const Options& opts)
     const i64 kt = std::min((m + nb - 1) / nb, (n + nb - 1) / nb);
     const int la = std::max(0, opts.lookahead);
     T* buf = static_cast<T*>(S.buf);
-    hipStream_t ps = R.panel, us = p == 1 ? R.update_masked : R.update;
+    UpdateReservation reserve(p == 1 ? 32 : 0);   // the persistent panel's CUs (p = 1)
+    hipStream_t ps = R.panel, us = R.update;
     const i64 kmin = std::min(m, n);
     Scratch ipiv(sizeof(i64) * std::max<i64>(kmin, 1), R.main), infos(sizeof(i64) * std::max<i64>(kt, 1), R.main);
     NHIP(hipMemsetAsync(ipiv.p, 0, sizeof(i64) * std::max<i64>(kmin, 1), R.main));

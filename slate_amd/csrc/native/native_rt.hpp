@@ -98,13 +98,19 @@ struct GridComms {
 struct Runtime {
     bool up = false;
     int rank = 0, size = 1, local = 0, device = 0;
-    hipStream_t main = nullptr, panel = nullptr, update = nullptr, update_masked = nullptr, comm = nullptr;
+    hipStream_t main = nullptr, panel = nullptr, update = nullptr, comm = nullptr;
+    int update_res = 0;     // CUs the live update stream leaves free (set_update_reservation)
     void* lu_work = nullptr;
     void* qr_work = nullptr;
     std::map<std::pair<int, int>, std::unique_ptr<GridComms>> grids;
     std::mutex mu;
 };
 Runtime& rt();
+// Re-create the update stream so that it leaves `cus` compute units free of
+// its workgroups (0: unmasked).  Drains the old stream first.  The process
+// keeps FOUR streams (main, panel, update, comm) -- the box's hardware queues.
+void set_update_reservation(int cus);
+
 GridComms* grid_comms(int p, int q);
 
 // ------------------------------------------------------------ storage

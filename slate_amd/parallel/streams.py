@@ -68,19 +68,49 @@ class StreamSet:
                 sh = dict(panel=torch.cuda.Stream(device=device, priority=-1),
                           diag=torch.cuda.Stream(device=device, priority=-1), update={})
                 _SHARED[str(device)] = sh
-            # one update stream per CU reservation (a shared one
-            # kept the mask of whichever pipeline ran first, e.g. geqrf after
-            # getrf inherited its 32-CU reservation).  A pipeline drives only
-            # its own set -- panel, diag, one update stream -- plus the
-            # caller's stream: 4, the box's hardware queues (check_census).
-            up = sh["update"].get(self.reserve_cus)
-            if up is None:
-                up = sh["update"][self.reserve_cus] = self._update_stream(device, self.reserve_cus)
+            # ONE update stream per device, shared by every pipeline: with
+            # panel, diag and the caller's stream that is 4, the box's
+            # hardware queues (one stream per CU reservation made
+            # 5, and the high-priority panel stream could share a queue with
+            # bulk GEMMs).  A pipeline whose reservation differs from the
+            # live stream's replaces it at its fork (_retarget), so the
+            # first pipeline's mask never leaks into the next.
+            if "upd" not in sh:
+                sh["upd"] = (self.reserve_cus, self._update_stream(device, self.reserve_cus))
+            self._sh = sh
             self.panel, self.diag = sh["panel"], sh["diag"]
-            self.update = [up] * n_update
+            self.n_update = n_update
         else:
             self.panel = self.diag = None
             self.update = [None] * n_update
+
+    def __getattr__(self, name):
+        # ``update`` of a GPU pipeline set: the device's live update stream
+        if name == "update" and "_sh" in self.__dict__:
+            return [self._sh["upd"][1]] * self.n_update
+        raise AttributeError(name)
+
+    # pipelines between a fork and its join, per device (a nested pipeline
+    # keeps the live update stream: its outer pipeline still holds it)
+    _open = {}
+
+    def _retarget(self):
+        """Make the live update stream carry this set's CU reservation.  Only
+        outside every open pipeline of the device; the old stream's work is
+        drained first (a reservation switch happens once per change of
+        factorization kind, never inside a step) and a CU-masked stream is
+        destroyed, so the process never holds more than one update stream."""
+        sh = self.__dict__.get("_sh")
+        if sh is None or sh["upd"][0] == self.reserve_cus or StreamSet._open.get(str(self.device), 0):
+            return
+        if torch.cuda.is_current_stream_capturing():
+            return                      # capture: keep the live stream (no sync allowed)
+        old_res, old = sh["upd"]
+        torch.cuda.synchronize(self.device)
+        sh["upd"] = (self.reserve_cus, self._update_stream(self.device, self.reserve_cus))
+        if old_res > 0 and isinstance(old, torch.cuda.ExternalStream):
+            from .. import _native
+            _native.hip().stream_destroy(old.cuda_stream)
 
     @staticmethod
     def _update_stream(device, reserve):
@@ -137,15 +167,14 @@ class StreamSet:
         return len(ids)
 
     def check_census(self):
-        """Raise if this process drives more work streams than the hardware
-        queues it may map them to (MAX_WORK_STREAMS)."""
+        """Raise if this process drives more work streams on the device than
+        the hardware queues it may map them to (MAX_WORK_STREAMS): every
+        pipeline stream of the process plus ONE caller stream (whichever
+        stream the caller enqueues on).  RCCL adds none: synchronous
+        collectives run on the issuing stream (nccl_stream_probe)."""
         if self.gpu and not self.serial:
-            # this pipeline's own streams plus ONE caller stream (whichever
-            # stream the caller enqueues on -- a side stream of theirs is
-            # as legitimate as the default one).  RCCL adds none: synchronous
-            # collectives run on the issuing stream (nccl_stream_probe).
             cur = torch.cuda.current_stream(self.device)
-            n = len([st for st in self._members() if st != cur]) + 1
+            n = len([st for st in StreamSet.streams_of(self.device) if st != cur]) + 1
             if n > MAX_WORK_STREAMS:
                 from ..core.exceptions import SlateError
                 raise SlateError(f"{n} work streams on {self.device} > {MAX_WORK_STREAMS}")
@@ -183,8 +212,12 @@ class StreamSet:
         HIP stream-capture of Option.UseGraph does not survive."""
         if not self.gpu:
             return
+        if not self.serial:
+            self._retarget()
         self.check_census()
         members = self._members(diag)
+        key = str(self.device)
+        StreamSet._open[key] = StreamSet._open.get(key, 0) + 1
         if not hasattr(self, "_fstack"):
             self._fstack = []
         self._fstack.append(members)           # fork / join pairs nest
@@ -198,6 +231,9 @@ class StreamSet:
             return
         cur = torch.cuda.current_stream(self.device)
         stack = getattr(self, "_fstack", None)
+        if stack:
+            key = str(self.device)
+            StreamSet._open[key] = max(0, StreamSet._open.get(key, 0) - 1)
         for s in (stack.pop() if stack else self._members()):
             if s != cur:
                 cur.wait_event(self.event(s))

@@ -128,17 +128,27 @@ def test_stream_census():
     sl.generate_matrix(Q, "rands", seed=3)
     sl.geqrf(Q, sl.TriangularFactors())
     torch.cuda.synchronize()
-    # every pipeline drives its own set (panel, diag, one update stream per
-    # CU reservation) plus the caller's stream: at most the 4 hardware queues
+    # process-wide: panel, diag and ONE update stream plus the caller's
+    # stream -- at most the 4 hardware queues
     sets = [s for s in StreamSet._cache.values() if s.gpu and not s.serial]
     assert sets
+    assert StreamSet.census(dev) <= MAX_WORK_STREAMS
+    assert len(StreamSet.streams_of(dev)) <= MAX_WORK_STREAMS - 1
     for s in sets:
-        assert len(s._members()) + 1 <= MAX_WORK_STREAMS
         s.check_census()
-    # getrf (32 reserved CUs) and potrf / geqrf (none) use different update
-    # streams (the first pipeline's mask no longer leaks)
+    # the live update stream carries the reservation of the last pipeline
+    # (geqrf: none), not the first one's 32 CUs
     ups = {id(s.update[0]) for s in sets}
-    assert len(ups) == len({s.reserve_cus for s in sets})
+    assert len(ups) == 1
+    assert sets[0]._sh["upd"][0] == 0
+    # back to getrf: the stream is replaced again, results unchanged
+    A2 = sl.Matrix(n, n, nb=nb, device=dev)
+    A2.insertLocalTiles(device=dev)
+    sl.generate_matrix(A2, "rands", seed=2)
+    assert sl.getrf(A2, sl.Pivots()) == 0
+    torch.cuda.synchronize()
+    assert StreamSet.census(dev) <= MAX_WORK_STREAMS
+    assert torch.equal(A.storage.local[A.storage.origin_slot], A2.storage.local[A2.storage.origin_slot])
 
 
 def test_potrf_use_graph():
