@@ -64,6 +64,12 @@ void pdlacpy_(const char* uplo, const int* m, const int* n, const double* a, con
 void pdgeadd_(const char* trans, const int* m, const int* n, const double* alpha, const double* a, const int* ia,
               const int* ja, const int* desca, const double* beta, double* c, const int* ic, const int* jc,
               const int* descc);
+void pztrsm_(const char* side, const char* uplo, const char* ta, const char* diag, const int* m, const int* n,
+             const double complex* alpha, const double complex* a, const int* ia, const int* ja, const int* desca,
+             double complex* b, const int* ib, const int* jb, const int* descb);
+void pdtrsm_(const char* side, const char* uplo, const char* ta, const char* diag, const int* m, const int* n,
+             const double* alpha, const double* a, const int* ia, const int* ja, const int* desca, double* b,
+             const int* ib, const int* jb, const int* descb);
 void slate_amd_finalize(void);
 
 static int g_rank;
@@ -251,6 +257,126 @@ int main(int argc, char** argv) {
         check("pdtrmm_lun", tw > 0 ? sqrt(te / tw) : sqrt(te));
     }
 
+    /* sub-matrix operands (ia = ja = nb + 1, size not a multiple of nb;
+     * reference scalapack_api/scalapack_slate.hh:81-120): the result must
+     * match the sub-problem and nothing outside the sub-matrix may change */
+    {
+        const int o = nb + 1, ms = n - nb - 21, o0 = o - 1;
+        const double a1 = 1.0, b0 = 0.0;
+        double* c3 = malloc(sizeof(double) * lld * (nloc > 0 ? nloc : 1));
+        FILL_A(gen);
+        for (int k = 0; k < lld * nloc; ++k) c3[k] = 7.0;
+        pdgemm_("T", "N", &ms, &ms, &ms, &a1, a, &o, &o, desca, a, &o, &o, desca, &b0, c3, &o, &o, desca);
+        double se = 0, sw = 0, out = 0;
+        for (int lj = 0; lj < nloc; ++lj)
+            for (int li = 0; li < mloc; ++li) {
+                const int gi = l2g(li, nb, p, pr), gj = l2g(lj, nb, q, pc);
+                const double v = c3[li + lj * lld];
+                if (gi >= o0 && gi < o0 + ms && gj >= o0 && gj < o0 + ms) {
+                    if ((li + lj) % 5) continue;
+                    double t = 0;
+                    for (int k = 0; k < ms; ++k) t += gen(o0 + k, gi, n) * gen(o0 + k, gj, n);
+                    se += (v - t) * (v - t);
+                    sw += t * t;
+                } else {
+                    out = fmax(out, fabs(v - 7.0));
+                }
+            }
+        check("pdgemm_sub", (sw > 0 ? sqrt(se / sw) : sqrt(se)) + out);
+        /* pdpotrf_ + pdpotrs_ on A(o:o+ms-1, o:o+ms-1), B(o:o+ms-1, 1:nrhs) */
+        FILL_A(sym);
+        for (int lc = 0; lc < rloc; ++lc)
+            for (int li = 0; li < mloc; ++li) {
+                const int gi = l2g(li, nb, p, pr), cc = l2g(lc, nb, q, pc);
+                double t = -5.0;                       /* rows outside the sub-matrix: sentinel */
+                if (gi >= o0 && gi < o0 + ms) {
+                    t = 0;
+                    for (int j = 0; j < ms; ++j) t += sym(gi, o0 + j, n) * xs(o0 + j, cc);
+                }
+                b[li + lc * lld] = t;
+            }
+        pdpotrf_("L", &ms, a, &o, &o, desca, &info);
+        int one_ = 1;
+        pdpotrs_("L", &ms, &nrhs, a, &o, &o, desca, b, &o, &one_, descb, &info);
+        double pe = 0, pw = 0, pout = 0;
+        for (int lc = 0; lc < rloc; ++lc)
+            for (int li = 0; li < mloc; ++li) {
+                const int gi = l2g(li, nb, p, pr), cc = l2g(lc, nb, q, pc);
+                if (gi >= o0 && gi < o0 + ms) {
+                    const double t = xs(gi, cc);
+                    pe += (b[li + lc * lld] - t) * (b[li + lc * lld] - t);
+                    pw += t * t;
+                } else {
+                    pout = fmax(pout, fabs(b[li + lc * lld] + 5.0));
+                }
+            }
+        /* the strict upper triangle and everything outside the sub-matrix: untouched */
+        for (int lj = 0; lj < nloc; ++lj)
+            for (int li = 0; li < mloc; ++li) {
+                const int gi = l2g(li, nb, p, pr), gj = l2g(lj, nb, q, pc);
+                const int inside = gi >= o0 && gi < o0 + ms && gj >= o0 && gj < o0 + ms;
+                if (!inside || gi < gj) pout = fmax(pout, fabs(a[li + lj * lld] - sym(gi, gj, n)));
+            }
+        check(info ? "pdpotrs_sub-FAILED" : "pdpotrs_sub", (pw > 0 ? sqrt(pe / pw) : sqrt(pe)) + pout);
+        /* pdgetrf_ + pdgetrs_ on the same sub-matrix (ipiv tied to A) */
+        FILL_A(gen);
+        for (int lc = 0; lc < rloc; ++lc)
+            for (int li = 0; li < mloc; ++li) {
+                const int gi = l2g(li, nb, p, pr), cc = l2g(lc, nb, q, pc);
+                double t = -5.0;
+                if (gi >= o0 && gi < o0 + ms) {
+                    t = 0;
+                    for (int j = 0; j < ms; ++j) t += gen(gi, o0 + j, n) * xs(o0 + j, cc);
+                }
+                b[li + lc * lld] = t;
+            }
+        pdgetrf_(&ms, &ms, a, &o, &o, desca, ipiv, &info);
+        pdgetrs_("N", &ms, &nrhs, a, &o, &o, desca, ipiv, b, &o, &one_, descb, &info);
+        pe = pw = pout = 0;
+        for (int lc = 0; lc < rloc; ++lc)
+            for (int li = 0; li < mloc; ++li) {
+                const int gi = l2g(li, nb, p, pr), cc = l2g(lc, nb, q, pc);
+                if (gi >= o0 && gi < o0 + ms) {
+                    const double t = xs(gi, cc);
+                    pe += (b[li + lc * lld] - t) * (b[li + lc * lld] - t);
+                    pw += t * t;
+                } else {
+                    pout = fmax(pout, fabs(b[li + lc * lld] + 5.0));
+                }
+            }
+        check(info ? "pdgetrs_sub-FAILED" : "pdgetrs_sub", (pw > 0 ? sqrt(pe / pw) : sqrt(pe)) + pout);
+        free(c3);
+    }
+
+    /* pdtrsm_ Right: X U = B (U = the upper triangle of gen) on an nrhs x n
+     * right-hand side stored in the columns of an n x n array */
+    {
+        const double a1 = 1.0;
+        const int nr = 40;                 /* rows of X */
+        double* xb = malloc(sizeof(double) * lld * (nloc > 0 ? nloc : 1));
+        FILL_A(gen);
+        for (int lj = 0; lj < nloc; ++lj)
+            for (int li = 0; li < mloc; ++li) {
+                const int gi = l2g(li, nb, p, pr), gj = l2g(lj, nb, q, pc);
+                double t = 0;
+                if (gi < nr)
+                    for (int k = 0; k <= gj; ++k) t += xs(k, gi) * gen(k, gj, n);
+                xb[li + lj * lld] = t;
+            }
+        pdtrsm_("R", "U", "N", "N", &nr, &n, &a1, a, &one, &one, desca, xb, &one, &one, desca);
+        double te = 0, tw = 0;
+        for (int lj = 0; lj < nloc; ++lj)
+            for (int li = 0; li < mloc; ++li) {
+                const int gi = l2g(li, nb, p, pr), gj = l2g(lj, nb, q, pc);
+                if (gi >= nr) continue;
+                const double t = xs(gj, gi);
+                te += (xb[li + lj * lld] - t) * (xb[li + lj * lld] - t);
+                tw += t * t;
+            }
+        check("pdtrsm_right", tw > 0 ? sqrt(te / tw) : sqrt(te));
+        free(xb);
+    }
+
     /* complex LU */
     double complex* za = malloc(sizeof(double complex) * lld * (nloc > 0 ? nloc : 1));
     double complex* zb = malloc(sizeof(double complex) * lld * (rloc > 0 ? rloc : 1));
@@ -276,6 +402,33 @@ int main(int argc, char** argv) {
             zw += cabs(t) * cabs(t);
         }
     check(info ? "pzgesv-FAILED" : "pzgesv", zw > 0 ? sqrt(ze / zw) : sqrt(ze));
+    /* pztrsm_ TRANSA = 'T' (no conjugation): L^T X = B, L = the lower triangle of za */
+    for (int lj = 0; lj < nloc; ++lj)
+        for (int li = 0; li < mloc; ++li) {
+            const int gi = l2g(li, nb, p, pr), gj = l2g(lj, nb, q, pc);
+            za[li + lj * lld] = gen(gi, gj, n) + I * 0.5 * gen(gj, gi, n);
+        }
+    for (int lc = 0; lc < rloc; ++lc)
+        for (int li = 0; li < mloc; ++li) {
+            const int gi = l2g(li, nb, p, pr), cc = l2g(lc, nb, q, pc);
+            double complex s = 0;
+            for (int k = gi; k < n; ++k)       /* (L^T)(gi, k) = L(k, gi), k >= gi */
+                s += (gen(k, gi, n) + I * 0.5 * gen(gi, k, n)) * (xs(k, cc) + I * xs(k, cc + 7));
+            zb[li + lc * lld] = s;
+        }
+    {
+        const double complex z1 = 1.0;
+        pztrsm_("L", "L", "T", "N", &n, &nrhs, &z1, za, &one, &one, desca, zb, &one, &one, descb);
+        ze = zw = 0;
+        for (int lc = 0; lc < rloc; ++lc)
+            for (int li = 0; li < mloc; ++li) {
+                const int gi = l2g(li, nb, p, pr), cc = l2g(lc, nb, q, pc);
+                const double complex t = xs(gi, cc) + I * xs(gi, cc + 7);
+                ze += cabs(zb[li + lc * lld] - t) * cabs(zb[li + lc * lld] - t);
+                zw += cabs(t) * cabs(t);
+            }
+        check("pztrsm_trans", zw > 0 ? sqrt(ze / zw) : sqrt(ze));
+    }
 
     /* LAPACK-style on the global array (every rank the same) */
     {

@@ -599,9 +599,14 @@ __global__ void gecopy_mask_kernel(TriMask mk, i64 m, i64 n, const T* __restrict
     const i64 i = (i64)blockIdx.x * 256 + threadIdx.x;
     if (i >= m) return;
     const i64 gr = mk.grow(i);
+    // real_diag bit 0: real diagonal; bit 1: merge (B keeps its value
+    // outside the mask instead of zero)
+    const bool merge = (real_diag & 2) != 0;
     for (i64 j = blockIdx.y; j < n; j += gridDim.y) {
-        T v = mk.keep(i, j) ? A[i + j * lda] : s_zero(T());
-        if (real_diag && gr == mk.gcol(j)) v = s_from_real(T(), s_real(v));
+        const bool kp = mk.keep(i, j);
+        if (merge && !kp) continue;
+        T v = kp ? A[i + j * lda] : s_zero(T());
+        if ((real_diag & 1) && gr == mk.gcol(j)) v = s_from_real(T(), s_real(v));
         B[i + j * ldb] = v;
     }
 }
@@ -614,10 +619,17 @@ void gecopy_mask(const TriMask& mk, i64 m, i64 n, const T* A, i64 lda, T* B, i64
                        real_diag ? 1 : 0);
     HIP_LAUNCH_CHECK();
 }
+template <typename T>
+void gecopy_mask_merge(const TriMask& mk, i64 m, i64 n, const T* A, i64 lda, T* B, i64 ldb, hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    hipLaunchKernelGGL(gecopy_mask_kernel<T>, grid2(m, n), dim3(256), 0, s, mk, m, n, A, lda, B, ldb, 2);
+    HIP_LAUNCH_CHECK();
+}
 
 #define INST(T)                                                                                   \
     template void permute_rows_scatter<T>(i64, i64, const T*, i64, T*, i64, const i64*, hipStream_t); \
     template void gecopy_mask<T>(const TriMask&, i64, i64, const T*, i64, T*, i64, bool, hipStream_t);   \
+    template void gecopy_mask_merge<T>(const TriMask&, i64, i64, const T*, i64, T*, i64, hipStream_t);   \
     template void geset<T>(char, i64, i64, T, T, T*, i64, hipStream_t);                           \
     template void gescale<T>(char, i64, i64, T, T*, i64, hipStream_t);                            \
     template void geadd<T>(char, i64, i64, T, const T*, i64, T, T*, i64, hipStream_t);            \

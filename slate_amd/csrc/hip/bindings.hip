@@ -263,6 +263,29 @@ static void register_kernels(py::module& m) {
             lu_dist_step<T>(nr, P<T>(W), ldw, P<const i64>(grow), c0, c1, j, P<const T>(recs), p, P<T>(Tt), ldt,
                             P<i64>(ipiv), P<i64>(info), info_off, thr, P<T>(rec), (void*)part, diag_local, S(st)); });
     });
+    m.def("lu_dist_base", [](char dt, i64 nr, uintptr_t W, i64 ldw, uintptr_t grow, int c0, int c1, uintptr_t Tt,
+                             i64 ldt, uintptr_t ipiv, uintptr_t info, i64 info_off, double thr, uintptr_t mbox, int p,
+                             int me, uintptr_t part, long long seq0, int has_diag, uintptr_t err, int G, uintptr_t st) {
+        LuPeer pe{P<const unsigned long long>(mbox), p, me, P<char>(part), seq0, has_diag, P<unsigned long long>(err)};
+        dispatch(dt, [&](auto z) { using T = decltype(z);
+            lu_dist_base<T>(nr, P<T>(W), ldw, P<const i64>(grow), c0, c1, P<T>(Tt), ldt, P<i64>(ipiv), P<i64>(info),
+                            info_off, thr, pe, G, S(st)); });
+    });
+    m.def("lu_peer_sizes", []() {
+        return py::make_tuple((i64)lu_peer_mailbox_bytes(), (i64)lu_peer_part_bytes(), lu_peer_max_b(), lu_peer_max_p());
+    });
+    m.def("lu_peer_alloc", [](i64 bytes) {
+        char h[64];
+        void* p = lu_peer_alloc((size_t)bytes, h);
+        return py::make_tuple((uintptr_t)p, py::bytes(h, 64));
+    });
+    m.def("lu_peer_open", [](py::bytes h) {
+        std::string hs = h;
+        if (hs.size() != 64) throw std::invalid_argument("lu_peer_open: 64-byte handle expected");
+        return (uintptr_t)lu_peer_open(hs.data());
+    });
+    m.def("lu_peer_close", [](uintptr_t p) { lu_peer_close((void*)p); });
+    m.def("lu_peer_free", [](uintptr_t p) { lu_peer_free((void*)p); });
     m.def("row_gather", [](char dt, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t B, i64 ldb, uintptr_t perm,
                            uintptr_t st) {
         dispatch(dt, [&](auto z) { using T = decltype(z);

@@ -42,6 +42,9 @@ void gecopy(char uplo, char trans, i64 m, i64 n, const Ts* A, i64 lda, Td* B, i6
 template <typename T>
 void gecopy_mask(const TriMask& mk, i64 m, i64 n, const T* A, i64 lda, T* B, i64 ldb, bool real_diag,
                  hipStream_t s);
+// the same, B unchanged outside the mask
+template <typename T>
+void gecopy_mask_merge(const TriMask& mk, i64 m, i64 n, const T* A, i64 lda, T* B, i64 ldb, hipStream_t s);
 template <typename T, typename R>
 void butterfly(bool trans, bool rows, int depth, i64 nidx, i64 nother, T* A, i64 lda, const R* diag, i64 ldd,
                hipStream_t s);
@@ -92,6 +95,28 @@ template <typename T>
 void lu_dist_step(i64 nr, T* W, i64 ldw, const i64* grow, int c0, int c1, int j, const T* recs, int p, T* Tt,
                   i64 ldt, i64* ipiv, i64* info, i64 info_off, double thr, T* rec, void* part, i64 diag_local,
                   hipStream_t s);
+
+// lu_dist.hip: device-resident b-column base block of the same panel; the
+// column peers exchange their records through peer-mapped mailboxes
+struct LuPeer {
+    const unsigned long long* mbox;  // device array [p]: mailbox base of each column peer (mbox[me] = own)
+    int p, me;
+    char* part;                      // this rank's partial slots (lu_peer_part_bytes, zeroed once)
+    long long seq0;                  // host sequence number: column j of the call tags seq0 + (j - c0) + 1
+    int has_diag;                    // this rank holds the panel's top rows (local row j = panel row j)
+    unsigned long long* err;         // set non-zero on a timed-out wait
+};
+size_t lu_peer_mailbox_bytes();
+size_t lu_peer_part_bytes();
+int lu_peer_max_b();
+int lu_peer_max_p();
+void* lu_peer_alloc(size_t bytes, void* handle64);
+void* lu_peer_open(const void* handle64);
+void lu_peer_close(void* p);
+void lu_peer_free(void* p);
+template <typename T>
+void lu_dist_base(i64 nr, T* W, i64 ldw, const i64* grow, int c0, int c1, T* Tt, i64 ldt, i64* ipiv, i64* info,
+                  i64 info_off, double thr, const LuPeer& pe, int G, hipStream_t s);
 
 // geqrf.hip
 template <typename T>

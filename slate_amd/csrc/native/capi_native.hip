@@ -13,9 +13,10 @@
 //     p{s,d,c,z}{potrf,posv,getrf,gesv,potrs,getrs,gemm,trsm,gels,lange}_ (gels: 1 x q grids)
 //     on the caller's LOCAL block-cyclic arrays (9-int descriptors), with a
 //     minimal BLACS (Cblacs_* / blacs_*_, numroc_, descinit_) over the native
-//     runtime's ranks.  The operands must be whole matrices (ia = ja = 1,
-//     sizes equal to the descriptor's, mb = nb, rsrc = csrc = 0,
-//     column-major grid); anything else returns an argument error.
+//     runtime's ranks.  Operands are any sub-matrix A(ia:ia+m-1, ja:ja+n-1)
+//     of a descriptor (any MB / NB, RSRC / CSRC, row- or column-major grid):
+//     whole aligned matrices are a local copy, the rest is redistributed
+//     point to point (scal_move).
 //   * slate_native_* (the earlier entry points; int return = info).
 //
 // info: 0 = success, > 0 numerical failure, < 0 illegal argument,
@@ -24,10 +25,14 @@
 #include <algorithm>
 #include <complex>
 #include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
 #include <cstdlib>
 #include <string>
 #include <vector>
 
+#include "../hip/kernels.hpp"
 #include "native_rt.hpp"
 
 namespace sn = slate_amd::native;
@@ -443,23 +448,188 @@ const Ctx& ctx_of(int ctxt) {
     return c[ctxt];
 }
 
-// a native matrix over a ScaLAPACK operand: whole matrix only
+// ---- ScaLAPACK operands.  The whole-matrix, aligned case (ia = ja = 1,
+// sizes equal to the descriptor's, MB = NB, RSRC = CSRC = 0, column-major
+// grid) is a local copy of the caller's array.  Anything else -- a
+// sub-matrix A(ia:ia+m-1, ja:ja+n-1) at any offset, MB != NB, a non-zero
+// source process, a row-major BLACS grid (reference
+// scalapack_api/scalapack_slate.hh:81-120 takes the same operands) -- is
+// redistributed into an aligned m x n native matrix (tile NB, column-major
+// grid) and back: each rank sends the values it owns straight to their new
+// owner, in a canonical order (global column-major over the elements a
+// source / destination pair shares), so only values travel.
+struct ScalLay {
+    i64 M, N, mb, nb, lld;
+    int rsrc, csrc, p, q;
+    bool rowmaj;
+    int orow(i64 gi) const { return (int)((gi / mb + rsrc) % p); }
+    int ocol(i64 gj) const { return (int)((gj / nb + csrc) % q); }
+    static i64 g2l(i64 g, i64 b, int np) { return (g / (b * np)) * b + g % b; }
+    int rank_of(int r, int c) const { return rowmaj ? r * q + c : r + c * p; }
+    void coords(int rank, int& r, int& c) const {
+        if (rowmaj) { r = rank / q; c = rank % q; } else { r = rank % p; c = rank / p; }
+    }
+};
+ScalLay scal_lay(const int* desc) {
+    const Ctx& c = ctx_of(desc[1]);
+    return ScalLay{desc[2], desc[3], desc[4], desc[5], desc[8], desc[6], desc[7], c.p, c.q, c.row_major};
+}
+struct SubInfo {
+    std::weak_ptr<sn::Storage> st;
+    std::vector<int> desc;
+    i64 i0, j0;                 // 0-based origin of the sub-matrix
+};
+std::map<const sn::Storage*, SubInfo>& sub_registry() {
+    static std::map<const sn::Storage*, SubInfo> r;
+    return r;
+}
+const SubInfo* sub_of(const sn::Storage* s) {
+    auto& r = sub_registry();
+    auto it = r.find(s);
+    if (it == r.end()) return nullptr;
+    auto sp = it->second.st.lock();
+    if (!sp || sp.get() != s) { r.erase(it); return nullptr; }
+    return &it->second;
+}
+bool scal_aligned(const int* desc, i64 m, i64 n, int ia, int ja) {
+    const Ctx& c = ctx_of(desc[1]);
+    return ia == 1 && ja == 1 && desc[2] == m && desc[3] == n && desc[4] == desc[5] && desc[6] == 0 && desc[7] == 0 &&
+           !(c.row_major && c.p > 1 && c.q > 1);
+}
+
+// move the m x n sub-matrix at (i0, j0) of the ScaLAPACK layout L (host local
+// array a of this rank) to / from the aligned native matrix B (host local
+// array b, leading dimension ldb)
+template <typename T>
+void scal_move(const ScalLay& L, i64 i0, i64 j0, i64 m, i64 n, T* a, const sn::Storage& B, T* b, i64 ldb,
+               bool to_native) {
+    const int me = sn::rank(), ws = sn::size();
+    int myr, myc;
+    L.coords(me, myr, myc);
+    const bool in_grid = me < L.p * L.q;
+    const int P = B.p, Q = B.q, bpr = B.pr, bpc = B.pc;
+    const i64 bnb = B.nb;
+    // source-layout side: my local elements of the sub-matrix, column-major
+    std::vector<std::vector<T>> sbuf((size_t)ws);
+    std::vector<size_t> cnt_src((size_t)ws, 0), cnt_dst((size_t)ws, 0);
+    auto src_walk = [&](auto&& f) {
+        if (!in_grid) return;
+        for (i64 sj = 0; sj < n; ++sj) {
+            const i64 gj = j0 + sj;
+            if (L.ocol(gj) != myc) continue;
+            const i64 lj = ScalLay::g2l(gj, L.nb, L.q);
+            const int dc = (int)((sj / bnb) % Q);
+            for (i64 si = 0; si < m; ++si) {
+                const i64 gi = i0 + si;
+                if (L.orow(gi) != myr) continue;
+                const int d = (int)((si / bnb) % P) + dc * P;
+                f(d, a + ScalLay::g2l(gi, L.mb, L.p) + lj * L.lld);
+            }
+        }
+    };
+    // native side: my local elements of B, column-major over the sub-matrix
+    auto dst_walk = [&](auto&& f) {
+        for (i64 lj = 0; lj < B.nloc; ++lj) {
+            const i64 sj = sn::l2g(lj, bnb, Q, bpc);
+            const int sc = L.ocol(j0 + sj);
+            for (i64 li = 0; li < B.mloc; ++li) {
+                const i64 si = sn::l2g(li, bnb, P, bpr);
+                f(L.rank_of(L.orow(i0 + si), sc), b + li + lj * ldb);
+            }
+        }
+    };
+    // pack (values in canonical order), self part copied directly
+    std::vector<std::vector<T>> rbuf((size_t)ws);
+    if (to_native) {
+        src_walk([&](int d, T* x) { sbuf[d].push_back(*x); });
+        dst_walk([&](int s, T*) { ++cnt_dst[s]; });
+        for (int r = 0; r < ws; ++r) rbuf[r].resize(cnt_dst[r]);
+    } else {
+        dst_walk([&](int s, T* x) { sbuf[s].push_back(*x); });
+        src_walk([&](int d, T*) { ++cnt_src[d]; });
+        for (int r = 0; r < ws; ++r) rbuf[r].resize(cnt_src[r]);
+    }
+    rbuf[me] = sbuf[me];
+    if (ws > 1) {
+        sn::Comm* w = sn::world_comm();
+        hipStream_t st = sn::rt().main;
+        size_t tot = 0;
+        std::vector<size_t> soff((size_t)ws), roff((size_t)ws);
+        for (int r = 0; r < ws; ++r) { soff[r] = tot; tot += sbuf[r].size() * sizeof(T); }
+        const size_t sb = tot;
+        for (int r = 0; r < ws; ++r) { roff[r] = tot; tot += rbuf[r].size() * sizeof(T); }
+        sn::Scratch d(std::max<size_t>(tot, 64), st);
+        std::vector<char> h(std::max<size_t>(sb, 1));
+        for (int r = 0; r < ws; ++r)
+            if (!sbuf[r].empty()) std::memcpy(h.data() + soff[r], sbuf[r].data(), sbuf[r].size() * sizeof(T));
+        if (sb) sn::upload(d.p, h.data(), sb, st);
+        std::vector<sn::P2P> ops;
+        for (int r = 0; r < ws; ++r) {
+            if (r == me) continue;
+            if (!sbuf[r].empty()) ops.push_back({true, r, static_cast<char*>(d.p) + soff[r], sbuf[r].size() * sizeof(T)});
+            if (!rbuf[r].empty()) ops.push_back({false, r, static_cast<char*>(d.p) + roff[r], rbuf[r].size() * sizeof(T)});
+        }
+        if (!ops.empty()) w->exchange(ops, st);
+        std::vector<char> hr(std::max<size_t>(tot - sb, 1));
+        if (tot > sb) NHIP(hipMemcpyAsync(hr.data(), static_cast<char*>(d.p) + sb, tot - sb, hipMemcpyDeviceToHost, st));
+        NHIP(hipStreamSynchronize(st));
+        for (int r = 0; r < ws; ++r)
+            if (r != me && !rbuf[r].empty())
+                std::memcpy(rbuf[r].data(), hr.data() + (roff[r] - sb), rbuf[r].size() * sizeof(T));
+    }
+    std::vector<size_t> pos((size_t)ws, 0);
+    if (to_native) dst_walk([&](int s, T* x) { *x = rbuf[s][pos[s]++]; });
+    else src_walk([&](int d, T* x) { *x = rbuf[d][pos[d]++]; });
+}
+
+// a native matrix over a ScaLAPACK operand (any sub-matrix, see above)
 template <typename T>
 sn::Matrix<T> scal_matrix(const int* desc, i64 m, i64 n, int ia, int ja, const T* a) {
-    if (ia != 1 || ja != 1) throw sn::Error("native ScaLAPACK: sub-matrix offsets (ia, ja != 1) not supported");
-    if (desc[2] != m || desc[3] != n) throw sn::Error("native ScaLAPACK: operand must be the whole matrix");
-    if (desc[4] != desc[5]) throw sn::Error("native ScaLAPACK: mb must equal nb");
-    if (desc[6] != 0 || desc[7] != 0) throw sn::Error("native ScaLAPACK: rsrc = csrc = 0 only");
+    if (ia < 1 || ja < 1 || ia - 1 + m > desc[2] || ja - 1 + n > desc[3])
+        throw sn::Error("native ScaLAPACK: sub-matrix outside the descriptor's matrix");
+    if (desc[4] < 1 || desc[5] < 1) throw sn::Error("native ScaLAPACK: bad block sizes");
     const Ctx& c = ctx_of(desc[1]);
-    if (c.row_major && c.p > 1 && c.q > 1) throw sn::Error("native ScaLAPACK: row-major grids not supported");
+    if (scal_aligned(desc, m, n, ia, ja)) {
+        sn::Matrix<T> A(m, n, desc[5], c.p, c.q);
+        if (A.mloc() > desc[8]) throw sn::Error("native ScaLAPACK: lld smaller than the local rows");
+        if (A.mloc() && A.nloc()) A.from_local_host(a, desc[8]);
+        return A;
+    }
+    const ScalLay L = scal_lay(desc);
     sn::Matrix<T> A(m, n, desc[5], c.p, c.q);
-    if (A.mloc() > desc[8]) throw sn::Error("native ScaLAPACK: lld smaller than the local rows");
-    if (A.mloc() && A.nloc()) A.from_local_host(a, desc[8]);
+    const sn::Storage& S = *A.storage();
+    std::vector<T> loc((size_t)std::max<i64>(S.mloc, 1) * std::max<i64>(S.nloc, 1));
+    scal_move<T>(L, ia - 1, ja - 1, m, n, const_cast<T*>(a), S, loc.data(), std::max<i64>(S.mloc, 1), true);
+    if (A.mloc() && A.nloc()) A.from_local_host(loc.data(), std::max<i64>(S.mloc, 1));
+    sub_registry()[A.storage().get()] = SubInfo{A.storage(), std::vector<int>(desc, desc + 9), ia - 1, ja - 1};
     return A;
 }
+// the native result back into the caller's array: exactly the elements of
+// the sub-matrix change
 template <typename T>
 void scal_back(const sn::Matrix<T>& A, const int* desc, T* a) {
-    if (A.mloc() && A.nloc()) A.to_local_host(a, desc[8]);
+    const SubInfo* si = sub_of(A.storage().get());
+    if (!si) {
+        if (A.mloc() && A.nloc()) A.to_local_host(a, desc[8]);
+        return;
+    }
+    const sn::Storage& S = *A.storage();
+    std::vector<T> loc((size_t)std::max<i64>(S.mloc, 1) * std::max<i64>(S.nloc, 1));
+    if (A.mloc() && A.nloc()) A.to_local_host(loc.data(), std::max<i64>(S.mloc, 1));
+    scal_move<T>(scal_lay(si->desc.data()), si->i0, si->j0, A.m(), A.n(), a, S, loc.data(), std::max<i64>(S.mloc, 1),
+                 false);
+}
+// dst's uplo triangle (global, diagonal included) := src's (same distribution)
+template <typename T>
+void tri_into(char uplo, const sn::Matrix<T>& src, sn::Matrix<T>& dst) {
+    const sn::Storage& S = *dst.storage();
+    if (!S.mloc || !S.nloc) return;
+    slate_hip::TriMask mk;
+    mk.mode = uplo == 'L' ? 1 : 2;
+    mk.p = S.p; mk.pr = S.pr; mk.q = S.q; mk.pc = S.pc; mk.nb = S.nb;
+    slate_hip::gecopy_mask_merge<sn::K<T>>(mk, S.mloc, S.nloc, sn::kp(src.data()), src.lld(), sn::kp(dst.data()),
+                                           S.lld, sn::rt().main);
+    NHIP(hipStreamSynchronize(sn::rt().main));
 }
 template <typename T>
 sn::HermitianMatrix<T> scal_herm(const int* desc, i64 n, int ia, int ja, const T* a) {
@@ -469,33 +639,42 @@ sn::HermitianMatrix<T> scal_herm(const int* desc, i64 n, int ia, int ja, const T
     return H;
 }
 
-// ScaLAPACK ipiv: local rows' global pivot rows (1-based), replicated over
-// the process columns; <-> the global 0-based sequence of the native driver
+// ScaLAPACK ipiv (tied to the descriptor's matrix): entry of local row li of
+// the global row ia-1+k = 1-based global row that row was swapped with
+// (ia-1 + the sub-matrix pivot + 1); <-> the 0-based sub-matrix sequence of
+// the native driver, replicated over the process columns
 template <typename T>
-void ipiv_to_local(const sn::Matrix<T>& A, const std::vector<int64_t>& piv, int* ipiv) {
-    const int p = A.p(), pr = sn::rank() % p;
-    for (i64 li = 0; li < A.mloc(); ++li) {
-        const i64 g = sn::l2g(li, A.nb(), p, pr);
-        if (g < (i64)piv.size()) ipiv[li] = (int)(piv[g] + 1);
+void ipiv_to_local(const sn::Matrix<T>& A, const int* desc, int ia, const std::vector<int64_t>& piv, int* ipiv) {
+    const ScalLay L = scal_lay(desc);
+    int myr, myc;
+    L.coords(sn::rank(), myr, myc);
+    if (sn::rank() >= L.p * L.q) return;
+    for (size_t k = 0; k < piv.size(); ++k) {
+        const i64 g = ia - 1 + (i64)k;
+        if (L.orow(g) == myr) ipiv[ScalLay::g2l(g, L.mb, L.p)] = (int)(ia + piv[k]);
     }
 }
 template <typename T>
-std::vector<int64_t> ipiv_from_local(const sn::Matrix<T>& A, i64 k, const int* ipiv) {
-    const int p = A.p(), pr = sn::rank() % p;
+std::vector<int64_t> ipiv_from_local(const sn::Matrix<T>& A, const int* desc, int ia, int ja, i64 k,
+                                     const int* ipiv) {
+    const ScalLay L = scal_lay(desc);
+    int myr, myc;
+    L.coords(sn::rank(), myr, myc);
     std::vector<int64_t> g((size_t)std::max<i64>(k, 1), 0);
-    for (i64 li = 0; li < A.mloc(); ++li) {
-        const i64 gi = sn::l2g(li, A.nb(), p, pr);
-        if (gi < k) g[gi] = ipiv[li] - 1;
-    }
-    if (p > 1) {       // each global row lives on exactly one process row
-        sn::GridComms* gc = sn::grid_comms(A.p(), A.q());
+    if (sn::rank() < L.p * L.q && myc == L.ocol(ja - 1))      // the panel's process column
+        for (i64 kk = 0; kk < k; ++kk) {
+            const i64 gi = ia - 1 + kk;
+            if (L.orow(gi) == myr) g[kk] = ipiv[ScalLay::g2l(gi, L.mb, L.p)] - ia;
+        }
+    if (sn::size() > 1) {       // one owner per entry: a sum over the world
         sn::Scratch d(sizeof(int64_t) * g.size(), sn::rt().main);
         sn::upload(d.p, g.data(), sizeof(int64_t) * g.size(), sn::rt().main);
-        gc->col->allreduce(d.p, g.size(), sn::DT::I64, 's', sn::rt().main);
+        sn::world_comm()->allreduce(d.p, g.size(), sn::DT::I64, 's', sn::rt().main);
         NHIP(hipMemcpyAsync(g.data(), d.p, sizeof(int64_t) * g.size(), hipMemcpyDeviceToHost, sn::rt().main));
         NHIP(hipStreamSynchronize(sn::rt().main));
     }
     g.resize((size_t)k);
+    (void)A;
     return g;
 }
 
@@ -505,34 +684,20 @@ int p_potrf(char uplo, int n, T* a, int ia, int ja, const int* desca) {
     if (uplo != 'L' && uplo != 'U') return -1;
     if (n == 0) return 0;
     return (int)guarded([&]() -> int64_t {
-        sn::HermitianMatrix<T> A = scal_herm<T>(desca, n, ia, ja, a);
-        if (uplo == 'U') {
-            sn::Matrix<T> U = scal_matrix<T>(desca, n, n, ia, ja, a);
-            sn::Matrix<T> Lg(n, n, A.nb(), A.p(), A.q());
-            sn::copy(sn::Op::ConjTrans, U, Lg);
-            sn::copy(sn::Op::NoTrans, Lg, A);
-            const int64_t info = sn::potrf(A);
-            sn::copy(sn::Op::ConjTrans, A, U);
-            // only the upper triangle of the caller's array changes
-            std::vector<T> loc((size_t)desca[8] * std::max<i64>(U.nloc(), 1));
-            scal_back(U, desca, loc.data());
-            for (i64 lj = 0; lj < U.nloc(); ++lj)
-                for (i64 li = 0; li < U.mloc(); ++li) {
-                    const i64 gi = sn::l2g(li, U.nb(), U.p(), sn::rank() % U.p());
-                    const i64 gj = sn::l2g(lj, U.nb(), U.q(), sn::rank() / U.p());
-                    if (gi <= gj) a[li + lj * desca[8]] = loc[li + lj * desca[8]];
-                }
-            return info;
-        }
+        // the factor as Lower storage (Upper: L = U^H), then only the uplo
+        // triangle of the caller's sub-matrix changes
+        sn::Matrix<T> G = scal_matrix<T>(desca, n, n, ia, ja, a);
+        sn::HermitianMatrix<T> A(sn::Uplo::Lower, n, G.nb(), G.p(), G.q());
+        sn::copy(uplo == 'U' ? sn::Op::ConjTrans : sn::Op::NoTrans, G, A);
         const int64_t info = sn::potrf(A);
-        std::vector<T> loc((size_t)desca[8] * std::max<i64>(A.nloc(), 1));
-        scal_back<T>(A, desca, loc.data());
-        for (i64 lj = 0; lj < A.nloc(); ++lj)
-            for (i64 li = 0; li < A.mloc(); ++li) {
-                const i64 gi = sn::l2g(li, A.nb(), A.p(), sn::rank() % A.p());
-                const i64 gj = sn::l2g(lj, A.nb(), A.q(), sn::rank() / A.p());
-                if (gi >= gj) a[li + lj * desca[8]] = loc[li + lj * desca[8]];
-            }
+        if (uplo == 'U') {
+            sn::Matrix<T> Ut(n, n, G.nb(), G.p(), G.q());
+            sn::copy(sn::Op::ConjTrans, A, Ut);
+            tri_into<T>('U', Ut, G);
+        } else {
+            tri_into<T>('L', A, G);
+        }
+        scal_back(G, desca, a);
         return info;
     });
 }
@@ -574,7 +739,7 @@ int p_getrf(int m, int n, T* a, int ia, int ja, const int* desca, int* ipiv) {
         std::vector<int64_t> piv;
         const int64_t info = sn::getrf(A, piv);
         scal_back(A, desca, a);
-        ipiv_to_local(A, piv, ipiv);
+        ipiv_to_local(A, desca, ia, piv, ipiv);
         return info;
     });
 }
@@ -588,7 +753,7 @@ int p_getrs(char trans, int n, int nrhs, const T* a, int ia, int ja, const int* 
     return (int)guarded([&]() -> int64_t {
         sn::Matrix<T> A = scal_matrix<T>(desca, n, n, ia, ja, a);
         sn::Matrix<T> B = scal_matrix<T>(descb, n, nrhs, ib, jb, b);
-        const std::vector<int64_t> piv = ipiv_from_local(A, n, ipiv);
+        const std::vector<int64_t> piv = ipiv_from_local(A, desca, ia, ja, n, ipiv);
         if (trans == 'T' && sn::is_cplx<T>()) throw sn::Error("native pgetrs: trans = 'T' of a complex matrix");
         sn::getrs(trans == 'N' ? sn::Op::NoTrans : sn::Op::ConjTrans, A, piv, B);
         scal_back(B, descb, b);
@@ -612,7 +777,7 @@ int p_gesv(int n, int nrhs, T* a, int ia, int ja, const int* desca, int* ipiv, T
             info = sn::getrf(A, piv);
         }
         scal_back(A, desca, a);
-        ipiv_to_local(A, piv, ipiv);
+        ipiv_to_local(A, desca, ia, piv, ipiv);
         return info;
     });
 }
@@ -634,21 +799,63 @@ void p_gemm(char ta, char tb, int m, int n, int k, T alpha, const T* a, int ia, 
     if (rc != 0) std::fprintf(stderr, "slate_amd native p?gemm_: %s\n", g_err.c_str());
 }
 
+// conj(A) in place (host round trip of the local block: compat path only)
+template <typename T>
+void conj_inplace(sn::Matrix<T>& A) {
+    if constexpr (sn::is_cplx<T>()) {
+        if (!A.mloc() || !A.nloc()) return;
+        std::vector<T> h((size_t)A.mloc() * A.nloc());
+        A.to_local_host(h.data(), A.mloc());
+        for (auto& x : h) x = std::conj(x);
+        A.from_local_host(h.data(), A.mloc());
+    }
+}
+
+// B = alpha op(A)^{-1} B (Left) or alpha B op(A)^{-1} (Right), TRANSA N / T / C.
+// The native solve is Left with NoTrans / ConjTrans: a complex Trans solves
+// with conj(A) and ConjTrans (A^T = conj(A)^H); Right: X op(A) = alpha B <=>
+// op(A)^H X^H = conj(alpha) B^H
 template <typename T>
 void p_trsm(char side, char uplo, char ta, char diag, int m, int n, T alpha, const T* a, int ia, int ja,
             const int* desca, T* b, int ib, int jb, const int* descb) {
     side = up(side);
     uplo = up(uplo);
     ta = up(ta);
+    diag = up(diag);
     if (m == 0 || n == 0) return;
     const int64_t rc = guarded([&]() -> int64_t {
-        if (side != 'L') throw sn::Error("native p?trsm_: side = 'L' only");
-        sn::Matrix<T> A = scal_matrix<T>(desca, m, m, ia, ja, a);
+        if (side != 'L' && side != 'R') throw sn::Error("native p?trsm_: SIDE must be L or R");
+        if (uplo != 'L' && uplo != 'U') throw sn::Error("native p?trsm_: UPLO must be L or U");
+        if (ta != 'N' && ta != 'T' && ta != 'C') throw sn::Error("native p?trsm_: TRANSA must be N, T or C");
+        if (diag != 'N' && diag != 'U') throw sn::Error("native p?trsm_: DIAG must be N or U");
+        const bool right = side == 'R';
+        const int na = right ? n : m;
+        sn::Matrix<T> A = scal_matrix<T>(desca, na, na, ia, ja, a);
         sn::Matrix<T> B = scal_matrix<T>(descb, m, n, ib, jb, b);
-        sn::trsm(sn::Side::Left, uplo == 'L' ? sn::Uplo::Lower : sn::Uplo::Upper,
-                 ta == 'N' ? sn::Op::NoTrans : sn::Op::ConjTrans, up(diag) == 'U' ? sn::Diag::Unit : sn::Diag::NonUnit,
-                 alpha, A, B);
-        scal_back(B, descb, b);
+        // effective left operation on A: 'N', 'C', or conj(A) with 'N' / 'C'
+        char opc;
+        bool conjA = false;
+        if (!right) {
+            opc = ta == 'N' ? 'N' : 'C';
+            conjA = ta == 'T' && sn::is_cplx<T>();
+        } else {
+            opc = ta == 'N' ? 'C' : 'N';            // (op A)^H
+            conjA = ta == 'T' && sn::is_cplx<T>();  // (A^T)^H = conj(A)
+        }
+        if (conjA) conj_inplace(A);
+        const sn::Uplo ul = uplo == 'L' ? sn::Uplo::Lower : sn::Uplo::Upper;
+        const sn::Diag dg = diag == 'U' ? sn::Diag::Unit : sn::Diag::NonUnit;
+        const sn::Op op = opc == 'N' ? sn::Op::NoTrans : sn::Op::ConjTrans;
+        if (!right) {
+            sn::trsm(sn::Side::Left, ul, op, dg, alpha, A, B);
+            scal_back(B, descb, b);
+        } else {
+            sn::Matrix<T> Bh(n, m, B.nb(), B.p(), B.q());
+            sn::copy(sn::Op::ConjTrans, B, Bh);
+            sn::trsm(sn::Side::Left, ul, op, dg, sn::conj_of(alpha), A, Bh);
+            sn::copy(sn::Op::ConjTrans, Bh, B);
+            scal_back(B, descb, b);
+        }
         return 0;
     });
     if (rc != 0) std::fprintf(stderr, "slate_amd native p?trsm_: %s\n", g_err.c_str());
@@ -685,18 +892,23 @@ sn::HermitianMatrix<T> scal_tri(const int* desc, i64 n, int ia, int ja, const T*
     return H;
 }
 
-// C(uplo) *= beta on the local ScaLAPACK array (k = 0 rank updates)
+// C(uplo) *= beta on the caller's sub-matrix (k = 0 rank updates)
 template <typename T>
-void scal_scale_tri(const int* desc, int n, char uplo, T beta, T* c) {
-    const Ctx& cx = ctx_of(desc[1]);
-    const int p = cx.p, q = cx.q, r = sn::rank(), pr = r % p, pc = r / p;     // column-major grid (scal_matrix)
-    const i64 nb = desc[4], lld = desc[8];
-    const i64 ml = sn::numroc(n, nb, pr, p), nl = sn::numroc(n, nb, pc, q);
-    for (i64 lj = 0; lj < nl; ++lj)
-        for (i64 li = 0; li < ml; ++li) {
-            const i64 gi = sn::l2g(li, nb, p, pr), gj = sn::l2g(lj, nb, q, pc);
-            if (uplo == 'L' ? gi >= gj : gi <= gj) c[li + lj * lld] *= beta;
+void scal_scale_tri(const int* desc, int n, int ic, int jc, char uplo, T beta, T* c) {
+    const ScalLay L = scal_lay(desc);
+    int myr, myc;
+    L.coords(sn::rank(), myr, myc);
+    if (sn::rank() >= L.p * L.q) return;
+    for (i64 sj = 0; sj < n; ++sj) {
+        const i64 gj = jc - 1 + sj;
+        if (L.ocol(gj) != myc) continue;
+        const i64 lj = ScalLay::g2l(gj, L.nb, L.q);
+        for (i64 si = 0; si < n; ++si) {
+            const i64 gi = ic - 1 + si;
+            if (L.orow(gi) != myr || (uplo == 'L' ? si < sj : si > sj)) continue;
+            c[ScalLay::g2l(gi, L.mb, L.p) + lj * L.lld] *= beta;
         }
+    }
 }
 
 // p?potri_: the inverse from the Cholesky factor, over the uplo triangle
@@ -710,15 +922,10 @@ int p_potri(char uplo, int n, T* a, int ia, int ja, const int* desca) {
         sn::HermitianMatrix<T> L(sn::Uplo::Lower, n, G.nb(), G.p(), G.q());
         sn::copy(uplo == 'U' ? sn::Op::ConjTrans : sn::Op::NoTrans, G, L);   // U = L^H: the factor as lower
         sn::potri(L);
-        sn::copy(uplo == 'U' ? sn::Op::ConjTrans : sn::Op::NoTrans, L, G);
-        std::vector<T> loc((size_t)desca[8] * std::max<i64>(G.nloc(), 1));
-        scal_back(G, desca, loc.data());
-        const int p = G.p(), r = sn::rank();
-        for (i64 lj = 0; lj < G.nloc(); ++lj)
-            for (i64 li = 0; li < G.mloc(); ++li) {
-                const i64 gi = sn::l2g(li, G.nb(), p, r % p), gj = sn::l2g(lj, G.nb(), G.q(), r / p);
-                if (uplo == 'L' ? gi >= gj : gi <= gj) a[li + lj * desca[8]] = loc[li + lj * desca[8]];
-            }
+        sn::Matrix<T> R(n, n, G.nb(), G.p(), G.q());
+        sn::copy(uplo == 'U' ? sn::Op::ConjTrans : sn::Op::NoTrans, L, R);
+        tri_into<T>(uplo, R, G);
+        scal_back(G, desca, a);
         return 0;
     });
 }
@@ -736,7 +943,7 @@ int p_getri(int n, T* a, int ia, int ja, const int* desca, const int* ipiv, T* w
     if (n == 0) return 0;
     return (int)guarded([&]() -> int64_t {
         sn::Matrix<T> A = scal_matrix<T>(desca, n, n, ia, ja, a);
-        const std::vector<int64_t> piv = ipiv_from_local(A, n, ipiv);
+        const std::vector<int64_t> piv = ipiv_from_local(A, desca, ia, ja, n, ipiv);
         sn::getri(A, piv);
         scal_back(A, desca, a);
         return 0;
@@ -753,7 +960,7 @@ void p_rank_k(bool herm, bool two, char uplo, char trans, int n, int k, T alpha,
     if (n == 0) return;
     const int64_t rc = guarded([&]() -> int64_t {
         if (k == 0 || alpha == T(0)) {
-            if (beta != T(1)) scal_scale_tri<T>(descc, n, uplo, beta, c);
+            if (beta != T(1)) scal_scale_tri<T>(descc, n, ic, jc, uplo, beta, c);
             return 0;
         }
         const bool nt = trans == 'N';

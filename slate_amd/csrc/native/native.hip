@@ -86,6 +86,17 @@ void finalize() {
     std::lock_guard<std::mutex> g(R.mu);
     if (!R.up) return;
     (void)hipDeviceSynchronize();
+    if (R.size > 1 && world_comm()) {
+        // no rank unmaps a mailbox a peer's kernel may still post into
+        bool peers = false;
+        for (auto& g : R.grids) peers = peers || (g.second && g.second->colpeer);
+        if (peers) {
+            Scratch d(sizeof(i64), R.main);
+            NHIP(hipMemsetAsync(d.p, 0, sizeof(i64), R.main));
+            world_comm()->allreduce(d.p, 1, DT::I64, 's', R.main);
+            NHIP(hipStreamSynchronize(R.main));
+        }
+    }
     R.grids.clear();
     transport_finalize();
     (void)hipFree(R.lu_work);
@@ -119,6 +130,54 @@ void set_update_reservation(int cus) {
         cus = 0;
     }
     R.update_res = cus;
+}
+
+PeerBox::~PeerBox() {
+    (void)hipDeviceSynchronize();
+    for (void* p : opened) slate_hip::lu_peer_close(p);
+    if (own) slate_hip::lu_peer_free(own);
+    (void)hipFree(mbox_d);
+    (void)hipFree(part);
+    (void)hipFree(err);
+}
+
+PeerBox* peer_box(Comm* c, std::unique_ptr<PeerBox>& slot, hipStream_t s) {
+    if (slot) return slot.get();
+    const char* e = std::getenv("SLATE_AMD_LU_PEER");
+    if ((e && e[0] == '0') || !c || c->size < 2 || c->size > slate_hip::lu_peer_max_p()) return nullptr;
+    auto pb = std::make_unique<PeerBox>();
+    char h[64];
+    pb->own = slate_hip::lu_peer_alloc(slate_hip::lu_peer_mailbox_bytes(), h);
+    // the 64-byte handles travel once over the communicator itself
+    Scratch hs(64 * (size_t)(c->size + 1), s);
+    upload(static_cast<char*>(hs.p) + 64 * c->size, h, 64, s);
+    c->allgather(static_cast<char*>(hs.p) + 64 * c->size, hs.p, 64, s);
+    std::vector<char> all((size_t)64 * c->size);
+    NHIP(hipMemcpyAsync(all.data(), hs.p, all.size(), hipMemcpyDeviceToHost, s));
+    NHIP(hipStreamSynchronize(s));
+    std::vector<unsigned long long> ptrs((size_t)c->size);
+    for (int r = 0; r < c->size; ++r) {
+        if (r == c->rank) ptrs[r] = (unsigned long long)(uintptr_t)pb->own;
+        else {
+            void* q = slate_hip::lu_peer_open(all.data() + 64 * (size_t)r);
+            pb->opened.push_back(q);
+            ptrs[r] = (unsigned long long)(uintptr_t)q;
+        }
+    }
+    NHIP(hipMalloc(&pb->mbox_d, ptrs.size() * sizeof(unsigned long long)));
+    NHIP(hipMemcpy(pb->mbox_d, ptrs.data(), ptrs.size() * sizeof(unsigned long long), hipMemcpyHostToDevice));
+    NHIP(hipMalloc(&pb->part, slate_hip::lu_peer_part_bytes()));
+    NHIP(hipMemset(pb->part, 0, slate_hip::lu_peer_part_bytes()));
+    NHIP(hipMalloc(&pb->err, sizeof(unsigned long long)));
+    NHIP(hipMemset(pb->err, 0, sizeof(unsigned long long)));
+    NHIP(hipDeviceSynchronize());
+    // every member has mapped every mailbox before any kernel posts into one
+    Scratch d(sizeof(i64), s);
+    NHIP(hipMemsetAsync(d.p, 0, sizeof(i64), s));
+    c->allreduce(d.p, 1, DT::I64, 's', s);
+    NHIP(hipStreamSynchronize(s));
+    slot = std::move(pb);
+    return slot.get();
 }
 
 namespace {
@@ -958,7 +1017,19 @@ static void panel_dist(Storage& S, i64 k, i64 kb, i64 lck, i64* ipiv_d, i64* inf
     Scratch recs((size_t)p * (3 + 2 * b) * sizeof(T), s), rec((size_t)(3 + 2 * b) * sizeof(T), s);
     NHIP(hipMemsetAsync(Tt, 0, (size_t)kb * kb * sizeof(T), s));
     i64* piv = ipiv_d + r0;                 // panel-relative
+    PeerBox* pbx = b <= slate_hip::lu_peer_max_b() ? peer_box(colc, S.gc->colpeer, s) : nullptr;
     auto base = [&](i64 c0, i64 c1) {
+        if (pbx) {
+            // ONE persistent launch per block; the column peers trade their
+            // records through the peer-mapped mailboxes (no host round trip)
+            slate_hip::LuPeer pe{pbx->mbox_d, p, colc->rank, pbx->part, pbx->seq, pr == rk ? 1 : 0, pbx->err};
+            pbx->seq += (c1 - c0) + 1;
+            ++pbx->launches;
+            const int G = (int)std::max<i64>(1, std::min<i64>(64, (nmine + 1023) / 1024));
+            slate_hip::lu_dist_base<K<T>>(nmine, kp(nmine ? W + c0 * ldw : buf), ldw, grow_d, (int)c0, (int)c1, kp(Tt),
+                                          kb, piv, info, 0, thr, pe, G, s);
+            return;
+        }
         const int recn = 3 + 2 * (int)(c1 - c0);
         for (i64 j = c0; j <= c1; ++j) {
             const bool nxt = j < c1;
@@ -1162,6 +1233,11 @@ int64_t getrf(Matrix<T>& A, std::vector<int64_t>& ipiv_out, const Options& opts)
     std::vector<i64> h((size_t)std::max<i64>(kmin, 1));
     NHIP(hipMemcpyAsync(h.data(), ipiv_d, h.size() * sizeof(i64), hipMemcpyDeviceToHost, R.main));
     const int64_t info = read_infos(infos.as<i64>(), kt, R.main, nb);
+    if (p > 1 && gc->colpeer) {
+        unsigned long long e = 0;
+        NHIP(hipMemcpy(&e, gc->colpeer->err, sizeof(e), hipMemcpyDeviceToHost));
+        if (e) throw Error("native getrf: peer mailbox exchange timed out (a column peer never posted its record)");
+    }
     ipiv_out.assign((size_t)kmin, 0);
     for (i64 i = 0; i < kmin; ++i) ipiv_out[i] = h[i] + (i / nb) * nb;   // panel-relative -> global
     return reduce_info(info);

@@ -89,10 +89,27 @@ void transport_finalize();
 const char* transport_name();
 
 // ------------------------------------------------------------ runtime
+// Peer-mapped mailboxes of one communicator (csrc/hip/lu_dist.hip
+// lu_dist_base_kernel; Python twin: parallel/peer.py): my uncached mailbox,
+// exported by IPC handle, and every peer's mailbox opened in my address
+// space.  Created collectively on first use; SLATE_AMD_LU_PEER=0 disables.
+struct PeerBox {
+    void* own = nullptr;
+    std::vector<void*> opened;
+    unsigned long long* mbox_d = nullptr;   // device array [size]: mailbox of each member
+    char* part = nullptr;                   // intra-rank partial slots
+    unsigned long long* err = nullptr;      // timeout word
+    long long seq = 0;                      // next sequence base (identical on every member)
+    long long launches = 0;
+    ~PeerBox();
+};
+PeerBox* peer_box(Comm* c, std::unique_ptr<PeerBox>& slot, hipStream_t s);
+
 struct GridComms {
     int p = 1, q = 1, pr = 0, pc = 0;
     std::unique_ptr<Comm> row;     // same process row, ranked by pc
     std::unique_ptr<Comm> col;     // same process column, ranked by pr
+    std::unique_ptr<PeerBox> colpeer;   // mailboxes of the column (distributed LU panel)
 };
 
 struct Runtime {

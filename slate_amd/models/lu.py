@@ -35,6 +35,7 @@ from ..core.exceptions import SlateError
 from ..core.matrix import Matrix, Pivots, TriangularMatrix
 from ..core.options import get_option
 from ..core.storage import DEV, l2g, local_start
+from ..parallel.peer import PeerMailbox
 from ..parallel.streams import StreamSet
 from ..utils.trace import trace_block
 from ._util import grid_of, target_slot, tiles_local_before
@@ -621,6 +622,8 @@ def _getrf_general(A, buf, thr, la, mode, leaf):
     else:
         glob = _global_pivots(ipiv[:min(m, n)], nb)
     info = _reduce_info(A, infos, kt, nb)
+    for peer in ctx.get("peers", ()):
+        peer.check()                  # a timed-out in-kernel peer exchange fails loudly
     return info, glob
 
 
@@ -834,7 +837,22 @@ def _panel_pp_dist(ctx, st, ipiv, Lp, pv):
     mod = kmod(buf)
     cd = code(dt)
 
+    peer = PeerMailbox.of(colc, dev) if (b <= 64 and PeerMailbox.enabled(colc, buf)) else None
+    if peer is not None:
+        ctx.setdefault("peers", set()).add(peer)
+
     def base(c0, c1):
+        if peer is not None:
+            # ONE persistent launch for the block: the column peers trade their
+            # records through peer-mapped mailboxes (parallel/peer.py)
+            G = max(1, min(64, -(-nmine // 1024)))
+            mod.lu_dist_base(cd, nmine, W[:, c0:c1].data_ptr() if nmine else buf.data_ptr(), ldw, grow.data_ptr(),
+                             c0, c1, T.data_ptr(), max(1, kb), piv.data_ptr(), info.data_ptr(), 0, float(thr),
+                             peer.mbox.data_ptr(), p, colc.rank, peer.part.data_ptr(), peer.next_seq(c1 - c0),
+                             int(pr == rk), peer.err.data_ptr(), G, stream(buf))
+            LU_DIST_STATS["base_launches"] += 1
+            LU_DIST_STATS["columns"] += c1 - c0
+            return
         recn = 3 + 2 * (c1 - c0)
         recs = None
         for j in range(c0, c1 + 1):
@@ -848,6 +866,7 @@ def _panel_pp_dist(ctx, st, ipiv, Lp, pv):
             if nxt:
                 recs = colc.allgather(rec).contiguous()
                 LU_DIST_STATS["columns"] += 1
+                LU_DIST_STATS["record_allgathers"] += 1
                 LU_DIST_STATS["record_bytes"] += recs.numel() * recs.element_size()
 
     def exchange(a, bnd, ca, cb):
@@ -860,6 +879,7 @@ def _panel_pp_dist(ctx, st, ipiv, Lp, pv):
         colc.allreduce(X)
         ops.xchg_scatter(plan, X, cols, nb, p, pr)
         LU_DIST_STATS["exchange_bytes"] += X.numel() * X.element_size()
+        LU_DIST_STATS["exchanges"] += 1
         return X[0:bnd - a]
 
     def rec(c0, c1):
@@ -890,7 +910,8 @@ def _panel_pp_dist(ctx, st, ipiv, Lp, pv):
 
 # counters of the distributed panel on this rank (tests): columns factored,
 # record bytes all-gathered, exchange bytes all-reduced
-LU_DIST_STATS = {"columns": 0, "record_bytes": 0, "exchange_bytes": 0}
+LU_DIST_STATS = {"columns": 0, "record_bytes": 0, "exchange_bytes": 0, "base_launches": 0, "exchanges": 0,
+                 "record_allgathers": 0}
 
 
 def _panel_nopiv(ctx, st, ipiv, Lp, pv):

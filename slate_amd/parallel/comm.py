@@ -396,6 +396,11 @@ def init(backend: Optional[str] = None):
 
 def finalize():
     global _WORLD
+    from .peer import PeerMailbox
+    if PeerMailbox._live:
+        if _dist_ready():
+            dist.barrier()            # every peer's kernels are done with my mailbox
+        PeerMailbox.release_all()
     if _dist_ready():
         dist.destroy_process_group()
     _WORLD = None

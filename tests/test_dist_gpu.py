@@ -223,3 +223,44 @@ def _check_grid_gpu(rank, size, p, q):
 @pytest.mark.parametrize("grid", [(2, 1), (1, 2), (2, 2)], ids=lambda g: f"{g[0]}x{g[1]}")
 def test_multirank_one_gpu(grid):
     run_dist(_check_grid_gpu, grid[0] * grid[1], *grid, timeout=240)
+
+
+def _check_lu_peer(rank, size, p, q):
+    """The device-resident panel (peer-mapped mailboxes, one persistent launch
+    per 32-column block) against the host-issued record all-gather: the
+    same pivots and bit-identical factors, and no per-column collective."""
+    import os
+    from slate_amd.models import lu as lu_mod
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    n, nb = 1024, 256
+    os.environ["SLATE_AMD_LU_PANEL_GATHER"] = "0"
+    out = {}
+    for mode in ("0", "1"):
+        os.environ["SLATE_AMD_LU_PEER"] = mode
+        for k in lu_mod.LU_DIST_STATS:
+            lu_mod.LU_DIST_STATS[k] = 0
+        A = sl.Matrix(n, n, nb=nb, p=p, q=q, device=dev)
+        A.insertLocalTiles(device=0)
+        sl.generate_matrix(A, "rands", 11)
+        piv = sl.Pivots()
+        assert sl.getrf(A, piv, {Option.Lookahead: 1}) == 0
+        torch.cuda.synchronize()
+        out[mode] = (A.storage.local[A.storage.origin_slot].clone(), piv.ipiv.clone(), dict(lu_mod.LU_DIST_STATS))
+    os.environ["SLATE_AMD_LU_PEER"] = "1"
+    f0, p0, st0 = out["0"]
+    f1, p1, st1 = out["1"]
+    assert torch.equal(p0.cpu(), p1.cpu())
+    assert torch.equal(f0, f1), (f0 - f1).abs().max().item()
+    panels = n // nb
+    # host-issued form: one record all-gather per panel column
+    assert st0["record_allgathers"] == st0["columns"] > 0, st0
+    # device form: no per-column collective, kb / 32 launches per panel
+    assert st1["record_allgathers"] == 0 and st1["columns"] == st0["columns"], st1
+    assert st1["base_launches"] <= panels * (nb // 32), st1
+    print(f"rank {rank}: peer LU stats {st1} (host form {st0})")
+
+
+@pytest.mark.parametrize("grid", [(2, 1), (2, 2)], ids=lambda g: f"{g[0]}x{g[1]}")
+def test_lu_panel_peer_mailbox(grid):
+    run_dist(_check_lu_peer, grid[0] * grid[1], *grid, timeout=240)

@@ -153,7 +153,7 @@ def test_native_example_grids_host_transport(grid):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("grid", ["1x1", "2x2"])
+@pytest.mark.parametrize("grid", ["1x1", "2x2", "2x1"])
 def test_native_scalapack_from_c_without_python(grid):
     """pdpotrf_/pdgesv_/pdgetrf_/pzgesv_/pdgemm_/pdlange_ and slate_dgetrf_
     called from plain C on local block-cyclic arrays."""
@@ -167,7 +167,7 @@ def test_native_scalapack_from_c_without_python(grid):
     else:
         outs = _run_ranks(CEXE, [grid], p * q)
     names = ("pdpotrs", "pdpotrs_upper", "pdgesv", "pdgetrs", "pdlange_fro", "pdgemm_tn", "pdsyrk_lower", "pdtrmm_lun", "pdpotri", "pdgetri", "pdlaset_lacpy_geadd",
-             "pzgesv", "slate_dgetrf_")
+             "pzgesv", "slate_dgetrf_", "pdgemm_sub", "pdpotrs_sub", "pdgetrs_sub", "pdtrsm_right", "pztrsm_trans")
     for rank, (rc, out) in enumerate(outs):
         print(out)
         assert rc == 0, out
