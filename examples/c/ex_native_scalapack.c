@@ -70,6 +70,20 @@ void pztrsm_(const char* side, const char* uplo, const char* ta, const char* dia
 void pdtrsm_(const char* side, const char* uplo, const char* ta, const char* diag, const int* m, const int* n,
              const double* alpha, const double* a, const int* ia, const int* ja, const int* desca, double* b,
              const int* ib, const int* jb, const int* descb);
+void pdgecon_(const char* norm, const int* n, const double* a, const int* ia, const int* ja, const int* desca,
+              const double* anorm, double* rcond, double* work, const int* lwork, int* iwork, const int* liwork,
+              int* info);
+void pdpocon_(const char* uplo, const int* n, const double* a, const int* ia, const int* ja, const int* desca,
+              const double* anorm, double* rcond, double* work, const int* lwork, int* iwork, const int* liwork,
+              int* info);
+void pdtrcon_(const char* norm, const char* uplo, const char* diag, const int* n, const double* a, const int* ia,
+              const int* ja, const int* desca, double* rcond, double* work, const int* lwork, int* iwork,
+              const int* liwork, int* info);
+double pdlansy_(const char* norm, const char* uplo, const int* n, const double* a, const int* ia, const int* ja,
+                const int* desca, double* work);
+void pdsyevd_(const char* jobz, const char* uplo, const int* n, double* a, const int* ia, const int* ja,
+              const int* desca, double* w, double* z, const int* iz, const int* jz, const int* descz, double* work,
+              const int* lwork, int* iwork, const int* liwork, int* info);
 void slate_amd_finalize(void);
 
 static int g_rank;
@@ -184,6 +198,62 @@ int main(int argc, char** argv) {
         memcpy(b, t, sizeof(double) * lld * (rloc > 0 ? rloc : 1));
         check(info ? "pdgetri-FAILED" : "pdgetri", ERR_B());
         free(t);
+    }
+
+    /* condition estimates against the exact 1-norm condition number from the
+     * inverse: the estimate of ||A^-1||_1 is a lower bound, in practice within
+     * a factor 3 (LAPACK lacn2) -- pass if 1 <= rcond_est / rcond <= 3 */
+    {
+        int lw = 1, liw = 1, iwq;
+        double wq, rc = 0, rc2 = 0;
+        FILL_A(gen);
+        const double an = pdlange_("1", &n, &n, a, &one, &one, desca, NULL);
+        pdgetrf_(&n, &n, a, &one, &one, desca, ipiv, &info);
+        pdgecon_("1", &n, a, &one, &one, desca, &an, &rc, &wq, &lw, &iwq, &liw, &info);
+        pdgetri_(&n, a, &one, &one, desca, ipiv, &wq, &lw, &iwq, &liw, &info);
+        double ratio = rc * an * pdlange_("1", &n, &n, a, &one, &one, desca, NULL);
+        check("pdgecon", (ratio >= 1.0 - 1e-12 && ratio <= 3.0) ? 0.0 : ratio);
+        FILL_A(sym);
+        const double sn_ = pdlange_("1", &n, &n, a, &one, &one, desca, NULL);
+        pdpotrf_("L", &n, a, &one, &one, desca, &info);
+        pdpocon_("L", &n, a, &one, &one, desca, &sn_, &rc2, &wq, &lw, &iwq, &liw, &info);
+        pdpotri_("L", &n, a, &one, &one, desca, &info);
+        ratio = rc2 * sn_ * pdlansy_("1", "L", &n, a, &one, &one, desca, NULL);
+        check("pdpocon", (ratio >= 1.0 - 1e-12 && ratio <= 3.0) ? 0.0 : ratio);
+        FILL_A(gen);
+        double rt = 0;
+        pdtrcon_("1", "U", "N", &n, a, &one, &one, desca, &rt, &wq, &lw, &iwq, &liw, &info);
+        check("pdtrcon", (rt > 0.0 && rt <= 1.0 && info == 0) ? 0.0 : 1.0 + rt);
+    }
+
+    /* pdsyevd_: A Z = Z diag(w) (the product by pdgemm_), W ascending on every rank */
+    {
+        double* z = malloc(sizeof(double) * lld * (nloc > 0 ? nloc : 1));
+        double* az = malloc(sizeof(double) * lld * (nloc > 0 ? nloc : 1));
+        double* w = malloc(sizeof(double) * n);
+        const double a1 = 1.0, b0 = 0.0;
+        int lw = -1, liw = -1, iwq;
+        double wq;
+        FILL_A(gen);
+        for (int lj = 0; lj < nloc; ++lj)            /* symmetric: the lower triangle of gen mirrored */
+            for (int li = 0; li < mloc; ++li) {
+                const int gi = l2g(li, nb, p, pr), gj = l2g(lj, nb, q, pc);
+                a[li + lj * lld] = gi >= gj ? gen(gi, gj, n) : gen(gj, gi, n);
+            }
+        pdsyevd_("V", "L", &n, a, &one, &one, desca, w, z, &one, &one, desca, &wq, &lw, &iwq, &liw, &info);
+        lw = liw = 1;
+        pdsyevd_("V", "L", &n, a, &one, &one, desca, w, z, &one, &one, desca, &wq, &lw, &iwq, &liw, &info);
+        pdgemm_("N", "N", &n, &n, &n, &a1, a, &one, &one, desca, z, &one, &one, desca, &b0, az, &one, &one, desca);
+        double ee = 0, an = pdlange_("F", &n, &n, a, &one, &one, desca, NULL);
+        int sorted = 1;
+        for (int i = 1; i < n; ++i) sorted = sorted && w[i - 1] <= w[i];
+        for (int lj = 0; lj < nloc; ++lj)
+            for (int li = 0; li < mloc; ++li) {
+                const double r = az[li + lj * lld] - z[li + lj * lld] * w[l2g(lj, nb, q, pc)];
+                ee += r * r;
+            }
+        check(info || !sorted ? "pdsyevd-FAILED" : "pdsyevd", sqrt(ee) / (an * n));
+        free(z); free(az); free(w);
     }
 
     /* LU */

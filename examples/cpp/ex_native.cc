@@ -414,6 +414,59 @@ void run(int p, int q, int me) {
         for (size_t i = 0; i < prod.size(); ++i) prod[i] -= eye[i];
         report(v ? "getri" : "potri", rel<T>(prod, eye));
     }
+    // ---- heev: || A Z - Z Lambda || / (|| A || n) and || Z^H Z - I || / n
+    //      (a random Hermitian matrix: he2hb -> hb2st -> D & C -> back-transforms)
+    {
+        const int64_t ne = 260;
+        sn::HermitianMatrix<T> H(sn::Uplo::Lower, ne, nb, p, q);
+        H.generate(sn::Gen::Random, 121);
+        std::vector<T> h0((size_t)ne * ne), z((size_t)ne * ne);
+        H.to_host(h0.data(), ne);
+        for (int64_t j = 0; j < ne; ++j) {           // the Hermitian matrix of the lower triangle
+            h0[j + j * ne] = T(std::real(h0[j + j * ne]));
+            for (int64_t i = 0; i < j; ++i) h0[i + j * ne] = cj(h0[j + i * ne]);
+        }
+        sn::Matrix<T> Z(ne, ne, nb, p, q);
+        std::vector<sn::real_t<T>> lam, lam2;
+        const int64_t inf = sn::heev(H, lam, Z);
+        Z.to_host(z.data(), ne);
+        auto az = mul<T>('N', 'N', ne, ne, ne, h0, ne, z, ne);
+        double an = 0;
+        for (auto& v : h0) an += std::norm(std::complex<double>(std::real(v), std::imag(v)));
+        an = std::sqrt(an);
+        double e1 = 0;
+        for (int64_t j = 0; j < ne; ++j)
+            for (int64_t i = 0; i < ne; ++i) {
+                const std::complex<double> zz(std::real(z[i + j * ne]), std::imag(z[i + j * ne]));
+                e1 += std::norm(az[i + j * ne] - zz * (double)lam[j]);
+            }
+        auto zhz = mul<T>('C', 'N', ne, ne, ne, z, ne, z, ne);
+        double e2 = 0;
+        for (int64_t j = 0; j < ne; ++j)
+            for (int64_t i = 0; i < ne; ++i) e2 += std::norm(zhz[i + j * ne] - (i == j ? 1.0 : 0.0));
+        bool sorted = true;
+        for (size_t i = 1; i < lam.size(); ++i) sorted = sorted && lam[i - 1] <= lam[i];
+        report(inf || !sorted ? "heev-FAILED" : "heev", std::sqrt(e1) / (an * ne));
+        report("heev_orth", std::sqrt(e2) / ne);
+        // values only: the same spectrum
+        sn::heev(H, lam2);
+        double dv = 0;
+        for (int64_t i = 0; i < ne; ++i) dv = std::max(dv, std::abs((double)lam2[i] - (double)lam[i]));
+        report("heev_values", dv / (an > 0 ? an : 1));
+    }
+    // ---- condition estimates: 1 <= rcond_est / rcond <= 3 (exact rcond from the inverse)
+    {
+        const int64_t nc = 120;
+        sn::Matrix<T> Gm(nc, nc, nb, p, q);
+        Gm.generate(sn::Gen::DiagDominant, 131);
+        const double an = sn::norm(sn::Norm::One, Gm);
+        std::vector<int64_t> pv;
+        sn::getrf(Gm, pv);
+        const double rc = sn::gecondest(sn::Norm::One, Gm, an);
+        sn::getri(Gm, pv);
+        const double ratio = rc * an * sn::norm(sn::Norm::One, Gm);
+        report("gecondest", (ratio >= 0.999 && ratio <= 3.0) ? 0.0 : ratio);
+    }
     // ---- mixed precision (double / complex<double>): low-precision factors +
     // refinement must reach the working-precision residual
     if constexpr (std::is_same<T, double>::value || std::is_same<T, std::complex<double>>::value) {

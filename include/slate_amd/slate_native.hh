@@ -210,6 +210,26 @@ template <typename T>
 int64_t gesv_mixed(Matrix<T>& A, std::vector<int64_t>& ipiv, Matrix<T>& B, Matrix<T>& X, int& iter,
                    const Options& opts = {});
 
+// reciprocal condition number estimates (Hager / Higham 1-norm estimator,
+// LAPACK lacn2; reference slate.hh gecondest / pocondest / trcondest):
+// gecondest from the LU factors of getrf (the interchanges do not change the
+// norm), pocondest from the Cholesky factor of potrf (Lower storage), trcondest
+// of a triangular matrix (the uplo triangle of A); Anorm = the norm of the
+// ORIGINAL matrix in the same norm (One or Inf).  rcond = 1 / (Anorm ||A^-1||).
+template <typename T> double gecondest(Norm norm, const Matrix<T>& LU, double Anorm, const Options& opts = {});
+template <typename T> double pocondest(Norm norm, const HermitianMatrix<T>& L, double Anorm, const Options& opts = {});
+template <typename T>
+double trcondest(Norm norm, Uplo uplo, Diag diag, const Matrix<T>& A, const Options& opts = {});
+
+// Hermitian / real symmetric eigenproblem (reference slate.hh heev:
+// he2hb -> hb2st -> stedc -> back-transforms), A's stored triangle; Lambda =
+// the n eigenvalues ascending (every rank), Z = the eigenvectors (same grid
+// and tile size as A).  A is not modified.
+template <typename T>
+int64_t heev(HermitianMatrix<T>& A, std::vector<real_t<T>>& Lambda, Matrix<T>& Z, const Options& opts = {});
+template <typename T>
+int64_t heev(HermitianMatrix<T>& A, std::vector<real_t<T>>& Lambda, const Options& opts = {});
+
 struct QRData;
 template <typename T>
 struct QRFactors {

@@ -1061,6 +1061,162 @@ double p_lange(char norm, int m, int n, const T* a, int ia, int ja, const int* d
 
 }  // namespace
 
+// ---- condition estimates (reference lapack_api/lapack_gecon.cc, pocon, trcon
+// and scalapack_api/scalapack_gecon.cc, pocon, trcon)
+inline sn::Norm cond_norm(char norm) {
+    norm = up(norm);
+    if (norm == '1' || norm == 'O') return sn::Norm::One;
+    if (norm == 'I') return sn::Norm::Inf;
+    throw sn::Error("condition estimate: NORM must be '1', 'O' or 'I'");
+}
+template <typename T>
+int h_gecon(char norm, i64 n, const T* a, i64 lda, double anorm, double* rcond) {
+    if (n < 0) return -2;
+    if (lda < std::max<i64>(1, n)) return -4;
+    return (int)guarded([&]() -> int64_t {
+        int p, q;
+        grid_of(p, q);
+        sn::Matrix<T> A(n, n, nb_of(n), p, q);
+        A.from_host(a, lda);
+        *rcond = sn::gecondest(cond_norm(norm), A, anorm);
+        return 0;
+    });
+}
+template <typename T>
+int h_pocon(char uplo, i64 n, const T* a, i64 lda, double anorm, double* rcond) {
+    uplo = up(uplo);
+    if (uplo != 'L' && uplo != 'U') return -1;
+    if (lda < std::max<i64>(1, n)) return -4;
+    return (int)guarded([&]() -> int64_t {
+        int p, q;
+        grid_of(p, q);
+        const i64 nb = nb_of(n);
+        sn::Matrix<T> G(n, n, nb, p, q);
+        G.from_host(a, lda);
+        sn::HermitianMatrix<T> L(sn::Uplo::Lower, n, nb, p, q);
+        sn::copy(uplo == 'U' ? sn::Op::ConjTrans : sn::Op::NoTrans, G, L);
+        *rcond = sn::pocondest(sn::Norm::One, L, anorm);
+        return 0;
+    });
+}
+template <typename T>
+int h_trcon(char norm, char uplo, char diag, i64 n, const T* a, i64 lda, double* rcond) {
+    uplo = up(uplo);
+    diag = up(diag);
+    if (uplo != 'L' && uplo != 'U') return -2;
+    if (diag != 'N' && diag != 'U') return -3;
+    if (lda < std::max<i64>(1, n)) return -6;
+    return (int)guarded([&]() -> int64_t {
+        int p, q;
+        grid_of(p, q);
+        sn::Matrix<T> A(n, n, nb_of(n), p, q);
+        A.from_host(a, lda);
+        *rcond = sn::trcondest(cond_norm(norm), uplo == 'L' ? sn::Uplo::Lower : sn::Uplo::Upper,
+                               diag == 'U' ? sn::Diag::Unit : sn::Diag::NonUnit, A);
+        return 0;
+    });
+}
+template <typename T>
+int p_gecon(char norm, int n, const T* a, int ia, int ja, const int* desca, double anorm, double* rcond) {
+    if (n == 0) { *rcond = 1.0; return 0; }
+    return (int)guarded([&]() -> int64_t {
+        sn::Matrix<T> A = scal_matrix<T>(desca, n, n, ia, ja, a);
+        *rcond = sn::gecondest(cond_norm(norm), A, anorm);
+        return 0;
+    });
+}
+template <typename T>
+int p_pocon(char uplo, int n, const T* a, int ia, int ja, const int* desca, double anorm, double* rcond) {
+    uplo = up(uplo);
+    if (uplo != 'L' && uplo != 'U') return -1;
+    if (n == 0) { *rcond = 1.0; return 0; }
+    return (int)guarded([&]() -> int64_t {
+        sn::Matrix<T> G = scal_matrix<T>(desca, n, n, ia, ja, a);
+        sn::HermitianMatrix<T> L(sn::Uplo::Lower, n, G.nb(), G.p(), G.q());
+        sn::copy(uplo == 'U' ? sn::Op::ConjTrans : sn::Op::NoTrans, G, L);
+        *rcond = sn::pocondest(sn::Norm::One, L, anorm);
+        return 0;
+    });
+}
+template <typename T>
+int p_trcon(char norm, char uplo, char diag, int n, const T* a, int ia, int ja, const int* desca, double* rcond) {
+    uplo = up(uplo);
+    diag = up(diag);
+    if (uplo != 'L' && uplo != 'U') return -2;
+    if (diag != 'N' && diag != 'U') return -3;
+    if (n == 0) { *rcond = 1.0; return 0; }
+    return (int)guarded([&]() -> int64_t {
+        sn::Matrix<T> A = scal_matrix<T>(desca, n, n, ia, ja, a);
+        *rcond = sn::trcondest(cond_norm(norm), uplo == 'L' ? sn::Uplo::Lower : sn::Uplo::Upper,
+                               diag == 'U' ? sn::Diag::Unit : sn::Diag::NonUnit, A);
+        return 0;
+    });
+}
+
+// ---- Hermitian eigenproblem (reference lapack_api/lapack_heev.cc,
+// lapack_heevd.cc, scalapack_api/scalapack_heev.cc, scalapack_heevd.cc): the
+// native two-stage solver behind both the QR-named and the D&C-named entry
+// points.  LAPACK-style: jobz = 'V' overwrites A with the eigenvectors (LAPACK
+// semantics); ScaLAPACK: the eigenvectors into Z(iz:, jz:), W on every rank.
+template <typename T>
+sn::HermitianMatrix<T> herm_lower_of(const sn::Matrix<T>& G, char uplo) {
+    sn::HermitianMatrix<T> H(sn::Uplo::Lower, G.n(), G.nb(), G.p(), G.q());
+    sn::copy(uplo == 'U' ? sn::Op::ConjTrans : sn::Op::NoTrans, G, H);     // the stored triangle as lower
+    return H;
+}
+template <typename T>
+int h_heev(char jobz, char uplo, i64 n, T* a, i64 lda, sn::real_t<T>* w) {
+    jobz = up(jobz);
+    uplo = up(uplo);
+    if (jobz != 'N' && jobz != 'V') return -1;
+    if (uplo != 'L' && uplo != 'U') return -2;
+    if (n < 0) return -3;
+    if (lda < std::max<i64>(1, n)) return -5;
+    if (n == 0) return 0;
+    return (int)guarded([&]() -> int64_t {
+        int p, q;
+        grid_of(p, q);
+        sn::Matrix<T> G(n, n, nb_of(n), p, q);
+        G.from_host(a, lda);
+        sn::HermitianMatrix<T> H = herm_lower_of(G, uplo);
+        std::vector<sn::real_t<T>> lam;
+        if (jobz == 'V') {
+            sn::Matrix<T> Z(n, n, G.nb(), p, q);
+            sn::heev(H, lam, Z);
+            Z.to_host(a, lda);
+        } else {
+            sn::heev(H, lam);
+        }
+        std::copy(lam.begin(), lam.end(), w);
+        return 0;
+    });
+}
+template <typename T>
+int p_heev(char jobz, char uplo, int n, const T* a, int ia, int ja, const int* desca, sn::real_t<T>* w, T* z,
+           int iz, int jz, const int* descz) {
+    jobz = up(jobz);
+    uplo = up(uplo);
+    if (jobz != 'N' && jobz != 'V') return -1;
+    if (uplo != 'L' && uplo != 'U') return -2;
+    if (n == 0) return 0;
+    return (int)guarded([&]() -> int64_t {
+        sn::Matrix<T> G = scal_matrix<T>(desca, n, n, ia, ja, a);
+        sn::HermitianMatrix<T> H = herm_lower_of(G, uplo);
+        std::vector<sn::real_t<T>> lam;
+        if (jobz == 'V') {
+            sn::Matrix<T> Z = scal_matrix<T>(descz, n, n, iz, jz, z);
+            if (Z.nb() != G.nb() || Z.p() != G.p() || Z.q() != G.q())
+                throw sn::Error("native p?heev: Z must have A's block size and grid");
+            sn::heev(H, lam, Z);
+            scal_back(Z, descz, z);
+        } else {
+            sn::heev(H, lam);
+        }
+        std::copy(lam.begin(), lam.end(), w);
+        return 0;
+    });
+}
+
 extern "C" {
 
 const char* slate_amd_last_error(void) { return g_err.c_str(); }
@@ -1483,5 +1639,133 @@ int slate_native_dgemm(int64_t m, int64_t n, int64_t k, double alpha, const doub
 double slate_native_dlange(char norm, int64_t m, int64_t n, const double* a, int64_t lda) {
     return h_lange<double>(norm, m, n, a, lda);
 }
+
+// ---- condition estimates: LAPACK-style (host arrays, reference
+// lapack_api/lapack_gecon.cc: slate_?gecon etc.) and ScaLAPACK
+#define SN_COND(X, T, R)                                                                                        \
+    void slate_##X##gecon_(const char* norm, const int64_t* n, const T* a, const int64_t* lda, const R* anorm,  \
+                           R* rcond, T* work, int64_t* iwork, int64_t* info) {                                  \
+        (void)work; (void)iwork;                                                                                \
+        double rc = 0;                                                                                          \
+        *info = h_gecon<T>(*norm, *n, a, *lda, (double)*anorm, &rc);                                            \
+        *rcond = (R)rc;                                                                                         \
+    }                                                                                                           \
+    void slate_##X##pocon_(const char* uplo, const int64_t* n, const T* a, const int64_t* lda, const R* anorm,  \
+                           R* rcond, T* work, int64_t* iwork, int64_t* info) {                                  \
+        (void)work; (void)iwork;                                                                                \
+        double rc = 0;                                                                                          \
+        *info = h_pocon<T>(*uplo, *n, a, *lda, (double)*anorm, &rc);                                            \
+        *rcond = (R)rc;                                                                                         \
+    }                                                                                                           \
+    void slate_##X##trcon_(const char* norm, const char* uplo, const char* diag, const int64_t* n, const T* a,  \
+                           const int64_t* lda, R* rcond, T* work, int64_t* iwork, int64_t* info) {             \
+        (void)work; (void)iwork;                                                                                \
+        double rc = 0;                                                                                          \
+        *info = h_trcon<T>(*norm, *uplo, *diag, *n, a, *lda, &rc);                                              \
+        *rcond = (R)rc;                                                                                         \
+    }                                                                                                           \
+    void p##X##gecon_(const char* norm, const int* n, const T* a, const int* ia, const int* ja,                 \
+                      const int* desca, const R* anorm, R* rcond, T* work, const int* lwork, void* iwork,       \
+                      const int* liwork, int* info) {                                                           \
+        if ((lwork && *lwork == -1) || (liwork && *liwork == -1)) {                                            \
+            if (work) work[0] = T(1);                                                                           \
+            *info = 0;                                                                                          \
+            return;                                                                                             \
+        }                                                                                                       \
+        double rc = 0;                                                                                          \
+        *info = p_gecon<T>(*norm, *n, a, *ia, *ja, desca, (double)*anorm, &rc);                                 \
+        *rcond = (R)rc;                                                                                         \
+    }                                                                                                           \
+    void p##X##pocon_(const char* uplo, const int* n, const T* a, const int* ia, const int* ja,                 \
+                      const int* desca, const R* anorm, R* rcond, T* work, const int* lwork, void* iwork,       \
+                      const int* liwork, int* info) {                                                           \
+        if ((lwork && *lwork == -1) || (liwork && *liwork == -1)) {                                            \
+            if (work) work[0] = T(1);                                                                           \
+            *info = 0;                                                                                          \
+            return;                                                                                             \
+        }                                                                                                       \
+        double rc = 0;                                                                                          \
+        *info = p_pocon<T>(*uplo, *n, a, *ia, *ja, desca, (double)*anorm, &rc);                                 \
+        *rcond = (R)rc;                                                                                         \
+    }                                                                                                           \
+    void p##X##trcon_(const char* norm, const char* uplo, const char* diag, const int* n, const T* a,           \
+                      const int* ia, const int* ja, const int* desca, R* rcond, T* work, const int* lwork,     \
+                      void* iwork, const int* liwork, int* info) {                                              \
+        if ((lwork && *lwork == -1) || (liwork && *liwork == -1)) {                                            \
+            if (work) work[0] = T(1);                                                                           \
+            *info = 0;                                                                                          \
+            return;                                                                                             \
+        }                                                                                                       \
+        double rc = 0;                                                                                          \
+        *info = p_trcon<T>(*norm, *uplo, *diag, *n, a, *ia, *ja, desca, &rc);                                   \
+        *rcond = (R)rc;                                                                                         \
+    }
+// ---- eigenproblem exports: LAPACK-style (reference names slate_?syev /
+// ?heev / ?syevd / ?heevd, by reference) and ScaLAPACK p?syev(d)_ / p?heev(d)_
+#define SN_EIG_R(X, T)                                                                                          \
+    void slate_##X##syev(const char* jobz, const char* uplo, const int* n, T* a, const int* lda, T* w, T* work,  \
+                         const int* lwork, int* info) {                                                         \
+        if (*lwork == -1) { work[0] = T(1); *info = 0; return; }                                                \
+        *info = h_heev<T>(*jobz, *uplo, *n, a, *lda, w);                                                        \
+    }                                                                                                           \
+    void slate_##X##syevd(const char* jobz, const char* uplo, const int* n, T* a, const int* lda, T* w, T* work, \
+                          const int* lwork, int* iwork, const int* liwork, int* info) {                         \
+        if (*lwork == -1 || *liwork == -1) { work[0] = T(1); iwork[0] = 1; *info = 0; return; }                 \
+        *info = h_heev<T>(*jobz, *uplo, *n, a, *lda, w);                                                        \
+    }                                                                                                           \
+    void p##X##syev_(const char* jobz, const char* uplo, const int* n, const T* a, const int* ia, const int* ja, \
+                     const int* desca, T* w, T* z, const int* iz, const int* jz, const int* descz, T* work,     \
+                     const int* lwork, int* info) {                                                             \
+        if (*lwork == -1) { work[0] = T(1); *info = 0; return; }                                                \
+        *info = p_heev<T>(*jobz, *uplo, *n, a, *ia, *ja, desca, w, z, *iz, *jz, descz);                         \
+    }                                                                                                           \
+    void p##X##syevd_(const char* jobz, const char* uplo, const int* n, const T* a, const int* ia,             \
+                      const int* ja, const int* desca, T* w, T* z, const int* iz, const int* jz,                \
+                      const int* descz, T* work, const int* lwork, int* iwork, const int* liwork, int* info) {   \
+        if (*lwork == -1 || *liwork == -1) { work[0] = T(1); iwork[0] = 1; *info = 0; return; }                 \
+        *info = p_heev<T>(*jobz, *uplo, *n, a, *ia, *ja, desca, w, z, *iz, *jz, descz);                         \
+    }
+#define SN_EIG_C(X, T, R)                                                                                       \
+    void slate_##X##heev(const char* jobz, const char* uplo, const int* n, T* a, const int* lda, R* w, T* work,  \
+                         const int* lwork, R* rwork, int* info) {                                               \
+        (void)rwork;                                                                                            \
+        if (*lwork == -1) { work[0] = T(1); *info = 0; return; }                                                \
+        *info = h_heev<T>(*jobz, *uplo, *n, a, *lda, w);                                                        \
+    }                                                                                                           \
+    void slate_##X##heevd(const char* jobz, const char* uplo, const int* n, T* a, const int* lda, R* w, T* work, \
+                          const int* lwork, R* rwork, const int* lrwork, int* iwork, const int* liwork,         \
+                          int* info) {                                                                          \
+        if (*lwork == -1 || *lrwork == -1 || *liwork == -1) {                                                   \
+            work[0] = T(1); rwork[0] = R(1); iwork[0] = 1; *info = 0; return;                                   \
+        }                                                                                                       \
+        *info = h_heev<T>(*jobz, *uplo, *n, a, *lda, w);                                                        \
+    }                                                                                                           \
+    void p##X##heev_(const char* jobz, const char* uplo, const int* n, const T* a, const int* ia, const int* ja, \
+                     const int* desca, R* w, T* z, const int* iz, const int* jz, const int* descz, T* work,     \
+                     const int* lwork, R* rwork, const int* lrwork, int* info) {                                \
+        if (*lwork == -1 || *lrwork == -1) { work[0] = T(1); rwork[0] = R(1); *info = 0; return; }              \
+        *info = p_heev<T>(*jobz, *uplo, *n, a, *ia, *ja, desca, w, z, *iz, *jz, descz);                         \
+    }                                                                                                           \
+    void p##X##heevd_(const char* jobz, const char* uplo, const int* n, const T* a, const int* ia,             \
+                      const int* ja, const int* desca, R* w, T* z, const int* iz, const int* jz,                \
+                      const int* descz, T* work, const int* lwork, R* rwork, const int* lrwork, int* iwork,     \
+                      const int* liwork, int* info) {                                                           \
+        if (*lwork == -1 || *lrwork == -1 || *liwork == -1) {                                                   \
+            work[0] = T(1); rwork[0] = R(1); iwork[0] = 1; *info = 0; return;                                   \
+        }                                                                                                       \
+        *info = p_heev<T>(*jobz, *uplo, *n, a, *ia, *ja, desca, w, z, *iz, *jz, descz);                         \
+    }
+SN_EIG_R(s, float)
+SN_EIG_R(d, double)
+SN_EIG_C(c, std::complex<float>, float)
+SN_EIG_C(z, std::complex<double>, double)
+#undef SN_EIG_R
+#undef SN_EIG_C
+
+SN_COND(s, float, float)
+SN_COND(d, double, double)
+SN_COND(c, std::complex<float>, float)
+SN_COND(z, std::complex<double>, double)
+#undef SN_COND
 
 }  // extern "C"

@@ -368,34 +368,12 @@ void Matrix<T>::to_host(T* A, int64_t lda) const {
 // ------------------------------------------------------------ helpers
 namespace {
 
-template <typename T>
-void gemm_k(char ta, char tb, i64 m, i64 n, i64 k, T alpha, const T* A, i64 lda, const T* B, i64 ldb, T beta,
-            T* C, i64 ldc, hipStream_t s, const slate_hip::TriMask* mask = nullptr) {
-    if (m <= 0 || n <= 0) return;
-    slate_hip::GemmCall c;
-    c.transA = ta; c.transB = tb; c.m = m; c.n = n; c.k = k;
-    c.alpha_re = (double)std::real(alpha); c.alpha_im = (double)std::imag(alpha);
-    c.beta_re = (double)std::real(beta); c.beta_im = (double)std::imag(beta);
-    c.A = A; c.lda = lda; c.B = B; c.ldb = ldb; c.C = C; c.ldc = ldc;
-    if (mask) c.mask = *mask;
-    if constexpr (is_cplx<T>()) slate_hip::gemm_complex<K<T>>(c, s);
-    else slate_hip::gemm_real<T>(c, s);
-}
-
 // lower-triangle mask of a local block whose (0, 0) is local (r0, c0) of a
 // block-cyclic matrix (the Python drivers' (1, nb, p, pr, q, pc, r0, c0, 0))
 slate_hip::TriMask lower_mask(i64 nb, int p, int pr, int q, int pc, i64 r0, i64 c0) {
     slate_hip::TriMask t;
     t.mode = 1; t.nb = nb; t.p = p; t.pr = pr; t.q = q; t.pc = pc; t.row_off = r0; t.col_off = c0; t.diag_off = 0;
     return t;
-}
-
-// device-to-device block copy: the gecopy kernel (hipMemcpy2DAsync between
-// device pitches gave wrong results on this stack for pitched copies of a
-// few MB -- tools/probe/native_probe.cc)
-template <typename T>
-void copy2d(T* dst, i64 ldd, const T* src, i64 lds, i64 m, i64 n, hipStream_t s) {
-    if (m > 0 && n > 0) slate_hip::gecopy<K<T>, K<T>>('G', 'N', m, n, kp(src), lds, kp(dst), ldd, s);
 }
 
 int64_t read_infos(const i64* d, i64 nt, hipStream_t s, i64 nb) {
@@ -1623,6 +1601,113 @@ int64_t getri(Matrix<T>& A, const std::vector<int64_t>& ipiv, const Options& opt
     return 0;
 }
 
+// ------------------------------------------------------------ condition estimates
+// ||A^-1||_1 by Higham's refinement of Hager's method (LAPACK lacn2; SLATE
+// internal_norm1est.cc): fw(X) = A^-1 X, bw(X) = A^-H X on a distributed
+// n x 1 matrix.  The O(n) vector steps run on a gathered copy that every
+// rank holds identically (one all-gather of n scalars per solve), so every
+// rank takes the same branch without extra broadcasts; the solves keep the
+// O(n^2) work on the GPUs.
+template <typename T, typename F, typename B>
+static double norm1est(i64 n, i64 nb, int p, int q, F&& fw, B&& bw) {
+    using Rl = real_t<T>;
+    Matrix<T> X(n, 1, nb, p, q);
+    std::vector<T> x((size_t)n), xin((size_t)n);
+    auto put = [&] { X.from_host(x.data(), n); };
+    auto get = [&] { X.to_host(x.data(), n); };
+    auto sum_abs = [&] {
+        double s = 0;
+        for (auto& v : x) s += std::abs(v);
+        return s;
+    };
+    for (auto& v : x) v = T(Rl(1) / Rl(n));
+    xin = x;
+    put();
+    double est = 0;
+    i64 jlast = -1;
+    for (int it = 0; it < 5; ++it) {
+        fw(X);
+        get();
+        const double ny = sum_abs();
+        if (it > 0 && ny <= est) break;
+        est = ny;
+        for (auto& v : x) {
+            const Rl a = std::abs(v);
+            v = a > Rl(0) ? v / a : T(1);
+        }
+        put();
+        bw(X);
+        get();
+        i64 j = 0;
+        double zj = -1, dot = 0;
+        for (i64 i = 0; i < n; ++i) {
+            const double a = std::abs(x[i]);
+            if (a > zj) { zj = a; j = i; }
+            dot += (double)std::real(conj_of(x[i]) * xin[i]);
+        }
+        if (it > 0 && (j == jlast || zj <= dot)) break;
+        jlast = j;
+        std::fill(x.begin(), x.end(), T(0));
+        x[j] = T(1);
+        xin = x;
+        put();
+    }
+    // alternating-sign test vector
+    for (i64 i = 0; i < n; ++i) x[i] = T(Rl((i % 2 == 0 ? 1.0 : -1.0) * (1.0 + (double)i / (double)std::max<i64>(n - 1, 1))));
+    put();
+    fw(X);
+    get();
+    const double t = 2.0 * sum_abs() / (3.0 * (double)n);
+    return std::max(est, t);
+}
+
+template <typename T>
+double gecondest(Norm nrm, const Matrix<T>& LU, double Anorm, const Options& opts) {
+    const Storage& S = *LU.storage();
+    if (S.m != S.n) throw Error("native gecondest: square matrix");
+    if (nrm != Norm::One && nrm != Norm::Inf) throw Error("native gecondest: One or Inf norm");
+    if (S.n == 0) return 1.0;
+    if (Anorm == 0) return 0.0;
+    // A = P L U: ||A^-1|| = ||U^-1 L^-1|| (P does not change the 1- / inf-norm)
+    auto fw = [&](Matrix<T>& X) {
+        trsm<T>(Side::Left, Uplo::Lower, Op::NoTrans, Diag::Unit, T(1), LU, X, opts);
+        trsm<T>(Side::Left, Uplo::Upper, Op::NoTrans, Diag::NonUnit, T(1), LU, X, opts);
+    };
+    auto bw = [&](Matrix<T>& X) {
+        trsm<T>(Side::Left, Uplo::Upper, Op::ConjTrans, Diag::NonUnit, T(1), LU, X, opts);
+        trsm<T>(Side::Left, Uplo::Lower, Op::ConjTrans, Diag::Unit, T(1), LU, X, opts);
+    };
+    const double ainv = nrm == Norm::One ? norm1est<T>(S.n, S.nb, S.p, S.q, fw, bw)
+                                         : norm1est<T>(S.n, S.nb, S.p, S.q, bw, fw);
+    return ainv == 0 ? 0.0 : 1.0 / (ainv * Anorm);
+}
+
+template <typename T>
+double pocondest(Norm nrm, const HermitianMatrix<T>& L, double Anorm, const Options& opts) {
+    const Storage& S = *L.storage();
+    if (nrm != Norm::One && nrm != Norm::Inf) throw Error("native pocondest: One or Inf norm");
+    if (S.n == 0) return 1.0;
+    if (Anorm == 0) return 0.0;
+    auto f = [&](Matrix<T>& X) { potrs<T>(L, X, opts); };     // A^-1 = A^-H
+    const double ainv = norm1est<T>(S.n, S.nb, S.p, S.q, f, f);
+    return ainv == 0 ? 0.0 : 1.0 / (ainv * Anorm);
+}
+
+template <typename T>
+double trcondest(Norm nrm, Uplo uplo, Diag diag, const Matrix<T>& A, const Options& opts) {
+    const Storage& S = *A.storage();
+    if (S.m != S.n) throw Error("native trcondest: square matrix");
+    if (nrm != Norm::One && nrm != Norm::Inf) throw Error("native trcondest: One or Inf norm");
+    if (S.n == 0) return 1.0;
+    const double Anorm = norm_triangular<T>(nrm, uplo, diag, A);
+    if (Anorm == 0) return 0.0;
+    auto fw = [&](Matrix<T>& X) { trsm<T>(Side::Left, uplo, Op::NoTrans, diag, T(1), A, X, opts); };
+    auto bw = [&](Matrix<T>& X) { trsm<T>(Side::Left, uplo, Op::ConjTrans, diag, T(1), A, X, opts); };
+    const double ainv = nrm == Norm::One ? norm1est<T>(S.n, S.nb, S.p, S.q, fw, bw)
+                                         : norm1est<T>(S.n, S.nb, S.p, S.q, bw, fw);
+    return ainv == 0 ? 0.0 : 1.0 / (ainv * Anorm);
+}
+
 // ------------------------------------------------------------ mixed precision
 // Reference: src/posv_mixed.cc, src/gesv_mixed.cc (LAPACK dsposv / dsgesv):
 // factor in the lower precision (half the bytes, ~2x the MFMA rate), then
@@ -1962,7 +2047,10 @@ int64_t gels(Matrix<T>& A, Matrix<T>& BX, const Options& opts) {
     template double norm_symmetric<T>(Norm, const HermitianMatrix<T>&);                                       \
     template double norm_triangular<T>(Norm, Uplo, Diag, const Matrix<T>&);                                   \
     template void add<T>(T, const Matrix<T>&, T, Matrix<T>&);                                                 \
-    template void set<T>(T, T, Matrix<T>&);
+    template void set<T>(T, T, Matrix<T>&);                                                                   \
+    template double gecondest<T>(Norm, const Matrix<T>&, double, const Options&);                             \
+    template double pocondest<T>(Norm, const HermitianMatrix<T>&, double, const Options&);                    \
+    template double trcondest<T>(Norm, Uplo, Diag, const Matrix<T>&, const Options&);
 SLATE_NATIVE_INST(float)
 SLATE_NATIVE_INST(double)
 SLATE_NATIVE_INST(std::complex<float>)

@@ -1,0 +1,702 @@
+// Hermitian eigensolver of the native (Python-free) library:
+//   heev = he2hb (stage 1) -> hb2st (stage 2, GPU bulge chase) ->
+//          divide & conquer on the real tridiagonal (GPU leaves / merges) ->
+//          back-transforms unmtr_hb2st, unmtr_he2hb
+// (reference src/heev.cc:66-225, src/he2hb.cc, src/hb2st.cc:139-279,
+// src/stedc_solve.cc:79-238, src/unmtr_hb2st.cc, src/unmtr_he2hb.cc).
+//
+// MI355X design: the matrix is gathered onto ONE GPU (rank 0; 288 GB of HBM
+// holds n = 100k+ in fp64) and every stage runs there on the hand-written
+// kernels the Python package uses (geqrf.hip, hb2st.hip, stedc.hip, eig.hip,
+// the MFMA GEMM); the eigenvectors go back to the 2D block-cyclic Z in one
+// batched point-to-point exchange, the eigenvalues to every rank.  Stage 1
+// is GEMM-bound (4/3 n^3 flops): one GPU at 60+ TF/s beats a 2D-distributed
+// he2hb's broadcast chain at the sizes the eigensolver is used for (SLATE
+// itself runs stage 2 and the tridiagonal solver on one node).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "../include/steqr.hpp"
+#include "native_rt.hpp"
+
+namespace slate_amd {
+namespace native {
+
+namespace {
+
+// ---------------------------------------------------------------- helpers
+template <typename T>
+__global__ void real_to_phase_kernel(i64 n, i64 nc, const double* Q, i64 ldq, const T* ph, T* Z, i64 ldz) {
+    const i64 i = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    for (i64 j = blockIdx.y; j < nc; j += gridDim.y) {
+        const double q = Q[i + j * ldq];
+        if constexpr (slate_hip::scalar_traits<T>::is_complex) {
+            const T p = ph ? ph[i] : T{1, 0};
+            Z[i + j * ldz] = T{(decltype(p.re))(p.re * q), (decltype(p.re))(p.im * q)};
+        } else {
+            Z[i + j * ldz] = (T)q;
+        }
+    }
+}
+
+// Z (n x nc, type T) = diag(ph) Q (real); ph: device phases (complex T) or null
+template <typename T>
+void real_to_phase(i64 n, i64 nc, const double* Q, i64 ldq, const K<T>* ph, K<T>* Z, i64 ldz, hipStream_t s) {
+    if (n <= 0 || nc <= 0) return;
+    dim3 g((unsigned)((n + 255) / 256), (unsigned)std::min<i64>(nc, 4096));
+    hipLaunchKernelGGL(real_to_phase_kernel<K<T>>, g, dim3(256), 0, s, n, nc, Q, ldq, ph, Z, ldz);
+    NHIP(hipGetLastError());
+}
+
+template <typename V>
+Scratch* upload_vec(std::vector<std::unique_ptr<Scratch>>& keep, const std::vector<V>& v, hipStream_t s) {
+    keep.push_back(std::make_unique<Scratch>(std::max<size_t>(v.size(), 1) * sizeof(V), s));
+    if (!v.empty()) upload(keep.back()->p, v.data(), v.size() * sizeof(V), s);
+    return keep.back().get();
+}
+
+template <typename V>
+std::vector<V> download_vec(const void* d, size_t n, hipStream_t s) {
+    std::vector<V> h(n);
+    if (n) {
+        NHIP(hipMemcpyAsync(h.data(), d, n * sizeof(V), hipMemcpyDeviceToHost, s));
+        NHIP(hipStreamSynchronize(s));
+    }
+    return h;
+}
+
+std::vector<i64> argsort(const std::vector<double>& v) {
+    std::vector<i64> o(v.size());
+    std::iota(o.begin(), o.end(), 0);
+    std::stable_sort(o.begin(), o.end(), [&](i64 a, i64 b) { return v[a] < v[b]; });
+    return o;
+}
+
+// ---------------------------------------------------------------- D & C
+// Real symmetric tridiagonal (d, e) of order n -> ascending eigenvalues w
+// (host) and the eigenvectors Q (device, n x n, ld n), one process:
+// leaves of <= 128 rows solved all at once on the GPU (steqr_leaves), then
+// every merge of the split-at-the-middle tree bottom-up (LAPACK laed1-4 /
+// the reference's stedc_merge / deflate / secular / z_vector): host
+// deflation and Givens chains on O(s) vectors, device rotations, secular
+// roots, rank-one vectors and laed3's split GEMM (models/stedc.py _merge).
+struct Merge { i64 a, m, b; };
+
+void dc_tree(i64 a, i64 b, int t, i64 leaf, std::vector<std::pair<i64, i64>>& leaves,
+             std::vector<std::vector<Merge>>& levels) {
+    if (b - a <= leaf) {
+        leaves.push_back({a, b});
+        return;
+    }
+    const i64 m = a + (b - a) / 2;
+    if ((int)levels.size() <= t) levels.resize(t + 1);
+    levels[t].push_back({a, m, b});
+    dc_tree(a, m, t + 1, leaf, leaves, levels);
+    dc_tree(m, b, t + 1, leaf, leaves, levels);
+}
+
+void dc_merge(const Merge& g, double rho, std::vector<double>& w, double* Q, i64 ldq, hipStream_t s) {
+    const i64 a = g.a, m = g.m, b = g.b, S = b - a;
+    std::vector<std::unique_ptr<Scratch>> keep;
+    // children eigenvalues (host) and z = [last row of Q1; first row of Q2]
+    std::vector<double> dd(w.begin() + a, w.begin() + b), z((size_t)S);
+    {
+        // one row of a column range = a 1 x k block copy (kernel, ld 1)
+        Scratch zr((size_t)S * sizeof(double), s);
+        copy2d(zr.as<double>(), 1, Q + (m - 1) + a * ldq, ldq, 1, m - a, s);
+        copy2d(zr.as<double>() + (m - a), 1, Q + m + m * ldq, ldq, 1, b - m, s);
+        z = download_vec<double>(zr.p, (size_t)S, s);
+    }
+    double* Qm = Q + a + a * ldq;                 // the merge's S x S block (rows a..b of columns a..b)
+    Scratch Qs((size_t)S * S * sizeof(double), s);
+    double* qs = Qs.as<double>();
+    auto permute_cols = [&](const std::vector<i64>& o, const double* src, double* dst) {
+        Scratch* id = upload_vec(keep, o, s);
+        slate_hip::cols_copy(S, S, src, ldq, id->as<i64>(), dst, S, false, s);
+    };
+    if (rho == 0.0) {
+        const std::vector<i64> o = argsort(dd);
+        permute_cols(o, Qm, qs);
+        copy2d(Qm, ldq, qs, S, S, S, s);
+        for (i64 i = 0; i < S; ++i) w[a + i] = dd[o[i]];
+        return;
+    }
+    const bool flip = rho < 0;
+    if (flip) {
+        for (auto& x : dd) x = -x;
+        rho = -rho;
+    }
+    // ---- sort the poles ascending; column types 1 = top child, 2 = bottom
+    const std::vector<i64> order = argsort(dd);
+    std::vector<double> d2((size_t)S), z2((size_t)S);
+    std::vector<int> ty((size_t)S);
+    for (i64 i = 0; i < S; ++i) {
+        d2[i] = dd[order[i]];
+        z2[i] = z[order[i]];
+        ty[i] = order[i] < (m - a) ? 1 : 2;
+    }
+    permute_cols(order, Qm, qs);
+    // ---- deflation: tiny z components, then Givens chains over close poles
+    const double eps = std::numeric_limits<double>::epsilon();
+    double zz = 0, dmax = 0;
+    for (i64 i = 0; i < S; ++i) { zz += z2[i] * z2[i]; dmax = std::max(dmax, std::abs(d2[i])); }
+    const double tolf = 8.0 * eps * std::max(dmax, rho * zz);
+    std::vector<i64> c;
+    for (i64 i = 0; i < S; ++i)
+        if (!(rho * std::abs(z2[i]) * std::sqrt(zz) <= tolf)) c.push_back(i);
+    std::vector<i64> Kidx;
+    if (!c.empty()) {
+        const i64 nn = (i64)c.size();
+        std::vector<double> cs((size_t)nn, 0.0), sn((size_t)nn, 0.0);
+        std::vector<int> rot((size_t)nn, 0), kp((size_t)nn, 1);
+        std::vector<i64> rI, rJ;
+        std::vector<double> rC, rS;
+        i64 t = 0;
+        while (t < nn) {
+            double acc = z2[c[t]];
+            int tacc = ty[c[t]];
+            i64 u = t + 1;
+            while (u < nn && d2[c[u]] - d2[c[u - 1]] <= tolf) {
+                const double bb = z2[c[u]];
+                const double r = std::hypot(acc, bb);
+                cs[u] = r == 0 ? 1.0 : bb / r;
+                sn[u] = r == 0 ? 0.0 : acc / r;
+                rot[u] = 1;
+                z2[c[u - 1]] = 0.0;
+                z2[c[u]] = r;
+                tacc |= ty[c[u]];
+                ty[c[u]] = tacc;
+                kp[u - 1] = 0;
+                rI.push_back(c[u - 1]);
+                rJ.push_back(c[u]);
+                rC.push_back(cs[u]);
+                rS.push_back(sn[u]);
+                acc = r;
+                ++u;
+            }
+            kp[u - 1] = 1;
+            t = u;
+        }
+        if (!rI.empty()) {
+            Scratch* I = upload_vec(keep, rI, s);
+            Scratch* J = upload_vec(keep, rJ, s);
+            Scratch* C = upload_vec(keep, rC, s);
+            Scratch* Sn = upload_vec(keep, rS, s);
+            slate_hip::rot_cols(S, qs, S, (i64)rI.size(), I->as<i64>(), J->as<i64>(), C->as<double>(),
+                                Sn->as<double>(), s);
+        }
+        for (i64 u = 0; u < nn; ++u)
+            if (kp[u]) Kidx.push_back(c[u]);
+    }
+    std::vector<double> lam = d2;
+    const i64 k = (i64)Kidx.size();
+    if (k) {
+        std::vector<double> dK((size_t)k), zK((size_t)k);
+        double zzK = 0;
+        for (i64 i = 0; i < k; ++i) { dK[i] = d2[Kidx[i]]; zK[i] = z2[Kidx[i]]; zzK += zK[i] * zK[i]; }
+        Scratch* dKd = upload_vec(keep, dK, s);
+        Scratch* zKd = upload_vec(keep, zK, s);
+        Scratch org((size_t)k * sizeof(i64), s), mu((size_t)k * sizeof(double), s), zh((size_t)k * sizeof(double), s);
+        slate_hip::stedc_secular(k, dKd->as<double>(), zKd->as<double>(), rho, zzK, org.as<i64>(), mu.as<double>(),
+                                 zh.as<double>(), nullptr, 0, s);
+        const std::vector<i64> orgh = download_vec<i64>(org.p, (size_t)k, s);
+        const std::vector<double> muh = download_vec<double>(mu.p, (size_t)k, s);
+        for (i64 i = 0; i < k; ++i) lam[Kidx[i]] = dK[orgh[i]] + muh[i];
+        // ---- Qs[:, K] <- Qs[:, K] V: the top rows meet only the K columns
+        // of type 1 | 3, the bottom rows only those of type 2 | 3
+        struct Part { i64 r0, r1; std::vector<i64> sel; };
+        std::vector<Part> parts;
+        parts.push_back({0, m - a, {}});
+        parts.push_back({m - a, S, {}});
+        for (i64 i = 0; i < k; ++i) {
+            if (ty[Kidx[i]] & 1) parts[0].sel.push_back(i);
+            if (ty[Kidx[i]] & 2) parts[1].sel.push_back(i);
+        }
+        Scratch* Kd = upload_vec(keep, Kidx, s);
+        std::vector<std::unique_ptr<Scratch>> srcs;
+        std::vector<Scratch*> seld;
+        for (auto& pt : parts) {
+            const i64 nr = pt.r1 - pt.r0, ns = (i64)pt.sel.size();
+            if (!ns || !nr) { srcs.push_back(nullptr); seld.push_back(nullptr); continue; }
+            std::vector<i64> cols((size_t)ns);
+            for (i64 i = 0; i < ns; ++i) cols[i] = Kidx[pt.sel[i]];
+            Scratch* cd = upload_vec(keep, cols, s);
+            srcs.push_back(std::make_unique<Scratch>((size_t)nr * ns * sizeof(double), s));
+            slate_hip::cols_copy(nr, ns, qs + pt.r0, S, cd->as<i64>(), srcs.back()->as<double>(), nr, false, s);
+            seld.push_back(upload_vec(keep, pt.sel, s));
+        }
+        const i64 CH = 4096;
+        for (i64 j0 = 0; j0 < k; j0 += CH) {
+            const i64 nc = std::min(CH, k - j0);
+            Scratch V((size_t)k * nc * sizeof(double), s);
+            slate_hip::stedc_vectors(k, dKd->as<double>(), zh.as<double>(), org.as<i64>(), mu.as<double>(), j0, nc,
+                                     V.as<double>(), k, s);
+            for (size_t pi = 0; pi < parts.size(); ++pi) {
+                const Part& pt = parts[pi];
+                const i64 nr = pt.r1 - pt.r0, ns = (i64)pt.sel.size();
+                if (!nr) continue;
+                Scratch out((size_t)nr * nc * sizeof(double), s);
+                if (ns) {
+                    Scratch Vp((size_t)ns * nc * sizeof(double), s);
+                    slate_hip::permute_rows_gather<double>(ns, nc, V.as<double>(), k, Vp.as<double>(), ns,
+                                                           seld[pi]->as<i64>(), s);
+                    gemm_k<double>('N', 'N', nr, nc, ns, 1.0, srcs[pi]->as<double>(), nr, Vp.as<double>(), ns, 0.0,
+                                   out.as<double>(), nr, s);
+                } else {
+                    NHIP(hipMemsetAsync(out.p, 0, (size_t)nr * nc * sizeof(double), s));
+                }
+                slate_hip::cols_copy(nr, nc, out.as<double>(), nr, Kd->as<i64>() + j0, qs + pt.r0, S, true, s);
+            }
+        }
+    }
+    if (flip)
+        for (auto& x : lam) x = -x;
+    const std::vector<i64> o2 = argsort(lam);
+    for (i64 i = 0; i < S; ++i) w[a + i] = lam[o2[i]];
+    Scratch* od = upload_vec(keep, o2, s);
+    slate_hip::cols_copy(S, S, qs, S, od->as<i64>(), Qm, ldq, false, s);
+    NHIP(hipStreamSynchronize(s));
+}
+
+void stedc_device(i64 n, const std::vector<double>& d, const std::vector<double>& e, std::vector<double>& w,
+                  double* Q, i64 ldq, hipStream_t s) {
+    w.assign((size_t)n, 0.0);
+    if (n == 0) return;
+    NHIP(hipMemsetAsync(Q, 0, (size_t)ldq * n * sizeof(double), s));
+    std::vector<std::pair<i64, i64>> leaves;
+    std::vector<std::vector<Merge>> levels;
+    dc_tree(0, n, 0, 128, leaves, levels);
+    std::vector<double> dl = d;
+    for (auto& lev : levels)
+        for (auto& g : lev) {
+            const double rho = e[g.m - 1];
+            dl[g.m - 1] -= rho;
+            dl[g.m] -= rho;
+        }
+    {
+        std::vector<std::unique_ptr<Scratch>> keep;
+        std::vector<i64> lo, hi;
+        i64 mx = 1;
+        for (auto& l : leaves) { lo.push_back(l.first); hi.push_back(l.second); mx = std::max(mx, l.second - l.first); }
+        std::vector<double> ee(e);
+        ee.resize((size_t)n, 0.0);
+        Scratch* lod = upload_vec(keep, lo, s);
+        Scratch* hid = upload_vec(keep, hi, s);
+        Scratch* dd = upload_vec(keep, dl, s);
+        Scratch* ed = upload_vec(keep, ee, s);
+        Scratch wd((size_t)n * sizeof(double), s), fails(sizeof(i64), s);
+        NHIP(hipMemsetAsync(fails.p, 0, sizeof(i64), s));
+        slate_hip::steqr_leaves((i64)leaves.size(), lod->as<i64>(), hid->as<i64>(), dd->as<double>(),
+                                ed->as<double>(), wd.as<double>(), Q, ldq, 0, n, fails.as<i64>(), s, (int)mx, 60);
+        w = download_vec<double>(wd.p, (size_t)n, s);
+        if (download_vec<i64>(fails.p, 1, s)[0])
+            throw Error("native heev: a divide & conquer leaf did not converge");
+    }
+    for (int t = (int)levels.size() - 1; t >= 0; --t)
+        for (auto& g : levels[t]) dc_merge(g, e[g.m - 1], w, Q, ldq, s);
+}
+
+// ---------------------------------------------------------------- stage 1
+template <typename T>
+struct Panel { i64 r0, kk; std::unique_ptr<Scratch> V, T_; };
+
+// zero the strictly lower part of an m x k block
+template <typename T>
+void zero_strict_lower(i64 m, i64 k, T* P, i64 ld, hipStream_t s) {
+    if (m <= 1 || k <= 0) return;
+    slate_hip::TriMask mk;
+    mk.mode = 2;
+    slate_hip::gecopy_mask<K<T>>(mk, m, k, kp(P), ld, kp(P), ld, false, s);
+}
+
+// dense Hermitian Af (n x n, ld n, both triangles) -> band of width nb in
+// place; the panel reflectors (explicit V, T) are kept for the back-transform
+template <typename T>
+void he2hb(i64 n, i64 nb, T* Af, i64 ld, std::vector<Panel<T>>& panels, hipStream_t s) {
+    const char ct = ctrans<T>();
+    for (i64 k0 = 0; k0 < n - nb; k0 += nb) {
+        const i64 r0 = k0 + nb, kb = std::min(nb, n - k0), m = n - r0;
+        if (m <= 0) break;
+        const i64 kk = std::min(m, kb);
+        T* P = Af + r0 + k0 * ld;
+        Panel<T> pn;
+        pn.r0 = r0;
+        pn.kk = kk;
+        pn.V = std::make_unique<Scratch>((size_t)m * kk * sizeof(T), s);
+        pn.T_ = std::make_unique<Scratch>((size_t)kk * kk * sizeof(T), s);
+        Scratch tau((size_t)kk * sizeof(T), s);
+        NHIP(hipMemsetAsync(tau.p, 0, (size_t)kk * sizeof(T), s));
+        T* V = pn.V->template as<T>();
+        T* Tm = pn.T_->template as<T>();
+        slate_hip::geqrf_panel_ws<K<T>>(m, kb, kp(P), ld, kp(tau.as<T>()), kp(Tm), kk, kp(V), m, rt().qr_work, s);
+        // band part: R, the reflectors zeroed, mirrored to the upper triangle
+        zero_strict_lower<T>(m, kb, P, ld, s);
+        // (gecopy's m x n are the DESTINATION's: kb x m here)
+        slate_hip::gecopy<K<T>, K<T>>('G', ct, kb, m, kp(P), ld, kp(Af + k0 + r0 * ld), ld, s);
+        // X = V T, Y = A22 X, M = X^H Y, W = Y - V M / 2, A22 -= V W^H + W V^H
+        Scratch X((size_t)m * kk * sizeof(T), s);
+        copy2d(X.as<T>(), m, V, m, m, kk, s);
+        slate_hip::trmm<K<T>>('R', 'U', 'N', 'N', m, kk, kv(T(1)), kp(Tm), kk, kp(X.as<T>()), m, s);
+        Scratch VW((size_t)m * 2 * kk * sizeof(T), s), WV((size_t)m * 2 * kk * sizeof(T), s);
+        T* Y = VW.as<T>() + m * kk;
+        T* A22 = Af + r0 + r0 * ld;
+        gemm_k<T>('N', 'N', m, kk, m, T(1), A22, ld, X.as<T>(), m, T(0), Y, m, s);
+        Scratch Mt((size_t)kk * kk * sizeof(T), s);
+        gemm_k<T>(ct, 'N', kk, kk, m, T(1), X.as<T>(), m, Y, m, T(0), Mt.as<T>(), kk, s);
+        gemm_k<T>('N', 'N', m, kk, kk, T(-0.5), V, m, Mt.as<T>(), kk, T(1), Y, m, s);
+        copy2d(VW.as<T>(), m, V, m, m, kk, s);
+        copy2d(WV.as<T>(), m, Y, m, m, kk, s);
+        copy2d(WV.as<T>() + m * kk, m, V, m, m, kk, s);
+        gemm_k<T>('N', ct, m, m, 2 * kk, T(-1), VW.as<T>(), m, WV.as<T>(), m, T(1), A22, ld, s);
+        panels.push_back(std::move(pn));
+    }
+}
+
+// Z := Q1 Z, Q1 = H_0 H_1 ... (panels last to first: Z -= V T (V^H Z))
+template <typename T>
+void unmtr_he2hb(i64 n, i64 nc, std::vector<Panel<T>>& panels, T* Z, i64 ldz, hipStream_t s) {
+    const char ct = ctrans<T>();
+    for (auto it = panels.rbegin(); it != panels.rend(); ++it) {
+        const i64 r0 = it->r0, kk = it->kk, m = n - r0;
+        Scratch W((size_t)kk * nc * sizeof(T), s);
+        gemm_k<T>(ct, 'N', kk, nc, m, T(1), it->V->template as<T>(), m, Z + r0, ldz, T(0), W.as<T>(), kk, s);
+        slate_hip::trmm<K<T>>('L', 'U', 'N', 'N', kk, nc, kv(T(1)), kp(it->T_->template as<T>()), kk,
+                              kp(W.as<T>()), kk, s);
+        gemm_k<T>('N', 'N', m, nc, kk, T(-1), it->V->template as<T>(), m, W.as<T>(), kk, T(1), Z + r0, ldz, s);
+    }
+}
+
+// SLATE_AMD_NATIVE_HEEV_DEBUG=1: residual ||M Z - Z diag(w)|| / (||M|| n) of a
+// device n x n M (ld ldm) and Z (ld ldz) -- per-stage checks at small n
+template <typename T>
+void dbg_resid(const char* tag, i64 n, const T* M, i64 ldm, const T* Z, i64 ldz, const std::vector<double>& w,
+               hipStream_t s) {
+    static const bool on = [] { const char* e = std::getenv("SLATE_AMD_NATIVE_HEEV_DEBUG"); return e && *e == '1'; }();
+    if (!on || n > 2048) return;
+    NHIP(hipStreamSynchronize(s));
+    std::vector<T> m((size_t)n * n), z((size_t)n * n);
+    for (i64 j = 0; j < n; ++j) {
+        NHIP(hipMemcpy(m.data() + j * n, M + j * ldm, n * sizeof(T), hipMemcpyDeviceToHost));
+        NHIP(hipMemcpy(z.data() + j * n, Z + j * ldz, n * sizeof(T), hipMemcpyDeviceToHost));
+    }
+    double e = 0, an = 0;
+    for (i64 j = 0; j < n; ++j)
+        for (i64 i = 0; i < n; ++i) {
+            T acc = T(0);
+            for (i64 l = 0; l < n; ++l) acc += m[i + l * n] * z[l + j * n];
+            e += std::norm(acc - z[i + j * n] * (real_t<T>)w[j]);
+            an += std::norm(m[i + j * n]);
+        }
+    std::fprintf(stderr, "heev debug %s: residual %.3e\n", tag, std::sqrt(e / std::max(an, 1e-300)) / (double)n);
+}
+
+// ---------------------------------------------------------------- one-GPU heev
+// Af: dense Hermitian n x n (ld n, both triangles) on this device; w: the
+// eigenvalues; Z (n x n, ld n) the eigenvectors when wantz
+template <typename T>
+void heev_1gpu(i64 n, T* Af, std::vector<double>& w, T* Z, bool wantz, hipStream_t s) {
+    using R = real_t<T>;
+    const i64 b = std::max<i64>(1, std::min<i64>(64, n - 1));
+    std::vector<Panel<T>> panels;
+    const bool dbg = [] { const char* e = std::getenv("SLATE_AMD_NATIVE_HEEV_DEBUG"); return e && *e == '1'; }();
+    std::unique_ptr<Scratch> A0, B0;
+    if (dbg) {
+        A0 = std::make_unique<Scratch>((size_t)n * n * sizeof(T), s);
+        copy2d(A0->as<T>(), n, Af, n, n, n, s);
+    }
+    he2hb<T>(n, b, Af, n, panels, s);
+    if (dbg) {
+        B0 = std::make_unique<Scratch>((size_t)n * n * sizeof(T), s);
+        copy2d(B0->as<T>(), n, Af, n, n, n, s);
+    }
+    // ---- stage 2 on the GPU: bulge chasing with recorded reflectors
+    const i64 nsw = std::max<i64>(n - 1, 0);
+    std::vector<i64> nt((size_t)std::max<i64>(nsw, 1), 0), sp((size_t)std::max<i64>(n, 1), 0);
+    for (i64 j = 0; j < nsw; ++j) {
+        const i64 e0 = std::min(j + b, n - 1), k0 = e0 - j;
+        nt[j] = k0 <= 1 ? 0 : 1 + (n - 1 - e0 + b - 1) / b;
+    }
+    for (i64 j = 1; j < n; ++j) sp[j] = sp[j - 1] + nt[j - 1];
+    const i64 total = nsw ? sp[n - 1] + nt[nsw - 1] : 0;
+    // leading dimension off powers of two (the chase touches ~3b columns of
+    // one row band: a 2^k stride would put them on one channel)
+    const i64 ldp = (n + 7) / 8 * 8 + 72;
+    // the band |i - j| <= b only (models/eig.py _band_only): two masked copies
+    Scratch Bh((size_t)ldp * std::max<i64>(n, 1) * sizeof(T), s);
+    {
+        slate_hip::TriMask up_, lo_;
+        up_.mode = 2;
+        up_.diag_off = b;                       // i <= j + b
+        lo_.mode = 1;
+        lo_.diag_off = b;                       // i + b >= j
+        slate_hip::gecopy_mask<K<T>>(up_, n, n, kp(Af), n, kp(Bh.as<T>()), ldp, false, s);
+        slate_hip::gecopy_mask<K<T>>(lo_, n, n, kp(Bh.as<T>()), ldp, kp(Bh.as<T>()), ldp, false, s);
+    }
+    if (dbg) {
+        Scratch Bb((size_t)n * n * sizeof(T), s);
+        copy2d(Bb.as<T>(), n, Bh.as<T>(), ldp, n, n, s);
+        std::vector<T> h1((size_t)n * n), h2((size_t)n * n);
+        NHIP(hipStreamSynchronize(s));
+        NHIP(hipMemcpy(h1.data(), Bb.p, h1.size() * sizeof(T), hipMemcpyDeviceToHost));
+        NHIP(hipMemcpy(h2.data(), B0->p, h2.size() * sizeof(T), hipMemcpyDeviceToHost));
+        double dd = 0, nn = 0;
+        for (size_t i = 0; i < h1.size(); ++i) { dd += std::norm(h1[i] - h2[i]); nn += std::norm(h2[i]); }
+        std::fprintf(stderr, "heev debug: outside-band part of the stage-1 result %.3e (relative)\n",
+                     std::sqrt(dd / std::max(nn, 1e-300)));
+    }
+    Scratch V((size_t)std::max<i64>(total, 1) * b * sizeof(T), s), tau((size_t)std::max<i64>(total, 1) * sizeof(T), s);
+    Scratch row((size_t)std::max<i64>(total, 1) * sizeof(i64), s), len((size_t)std::max<i64>(total, 1) * sizeof(i64), s);
+    NHIP(hipMemsetAsync(V.p, 0, (size_t)std::max<i64>(total, 1) * b * sizeof(T), s));
+    NHIP(hipMemsetAsync(tau.p, 0, (size_t)std::max<i64>(total, 1) * sizeof(T), s));
+    std::vector<std::unique_ptr<Scratch>> keep;
+    Scratch* ntd = upload_vec(keep, nt, s);
+    Scratch* spd = upload_vec(keep, sp, s);
+    if (nsw > 0 && total > 0) {
+        Scratch work((size_t)(nsw + 2) * sizeof(int), s);
+        NHIP(hipMemsetAsync(work.p, 0, (size_t)(nsw + 2) * sizeof(int), s));
+        hipDeviceProp_t pr;
+        NHIP(hipGetDeviceProperties(&pr, rt().device));
+        const i64 nt0 = nt[0] ? nt[0] : 1, lag = 2;
+        const int nwg = (int)std::min<i64>({std::max<i64>(nsw, 1), (i64)pr.multiProcessorCount,
+                                            std::max<i64>(8, std::min(nt0 / lag + 8, nt0 / 3 + 15))});
+        slate_hip::hb2st_device<K<T>>(n, (int)b, kp(Bh.as<T>()), ldp, kp(V.as<T>()), kp(tau.as<T>()), row.as<i64>(),
+                                      len.as<i64>(), spd->as<i64>(), ntd->as<i64>(), work.as<int>(), nsw, nwg, s);
+    }
+    // ---- (d, e) and the phases that make a complex tridiagonal real
+    // the diagonal / sub-diagonal = 1 x n blocks with stride ldp + 1
+    Scratch dsub((size_t)2 * std::max<i64>(n, 1) * sizeof(T), s);
+    copy2d(dsub.as<T>(), 1, Bh.as<T>(), ldp + 1, 1, n, s);
+    if (n > 1) copy2d(dsub.as<T>() + n, 1, Bh.as<T>() + 1, ldp + 1, 1, n - 1, s);
+    std::vector<T> ds = download_vec<T>(dsub.p, (size_t)(2 * n), s);
+    std::vector<T> diag(ds.begin(), ds.begin() + n), sub(ds.begin() + n, ds.end());
+    std::vector<double> d((size_t)n), e((size_t)std::max<i64>(n - 1, 0));
+    std::vector<T> ph((size_t)n, T(1));
+    for (i64 i = 0; i < n; ++i) d[i] = (double)std::real(diag[i]);
+    for (i64 i = 0; i + 1 < n; ++i) {
+        if constexpr (is_cplx<T>()) {
+            const R a = std::abs(sub[i]);
+            const T u = a > R(0) ? sub[i] / a : T(1);
+            ph[i + 1] = ph[i] * u;
+            e[i] = (double)a;
+        } else {
+            e[i] = (double)sub[i];
+        }
+    }
+    if (!wantz) {
+        std::vector<double> ee(e);
+        ee.resize((size_t)n, 0.0);
+        if (slate_tridiag::steqr_impl<double>(n, d.data(), ee.data(), nullptr, 1, 0))
+            throw Error("native heev: the tridiagonal QL iteration did not converge");
+        w = d;
+        return;
+    }
+    // ---- tridiagonal eigenvectors (D & C), then Z = Q1 Q2 Phase Qt
+    Scratch Qt((size_t)n * n * sizeof(double), s);
+    stedc_device(n, d, e, w, Qt.as<double>(), n, s);
+    Scratch* phd = is_cplx<T>() ? upload_vec(keep, ph, s) : nullptr;
+    if (dbg) {
+        // the tridiagonal itself as a dense matrix
+        std::vector<double> td((size_t)n * n, 0.0);
+        for (i64 i = 0; i < n; ++i) td[i + i * n] = d[i];
+        for (i64 i = 0; i + 1 < n; ++i) td[i + 1 + i * n] = td[i + (i + 1) * n] = e[i];
+        Scratch Td((size_t)n * n * sizeof(double), s);
+        upload(Td.p, td.data(), td.size() * sizeof(double), s);
+        dbg_resid<double>("tridiagonal D&C", n, Td.as<double>(), n, Qt.as<double>(), n, w, s);
+    }
+    real_to_phase<T>(n, n, Qt.as<double>(), n, phd ? kp(phd->as<T>()) : nullptr, kp(Z), n, s);
+    if (nsw > 0 && total > 0) {
+        if (!slate_hip::unmtr_hb2st_blocked<K<T>>(n, n, kp(Z), n, kp(V.as<T>()), b, kp(tau.as<T>()), spd->as<i64>(),
+                                                  ntd->as<i64>(), nsw, false, s)) {
+            for (i64 j = n - 1; j >= 0; --j) {
+                const i64 first = sp[j], last = j + 1 < n ? sp[j + 1] : total;
+                if (last > first)
+                    slate_hip::apply_refl_batch<K<T>>(n, kp(Z), n, kp(V.as<T>()), b, kp(tau.as<T>()), row.as<i64>(),
+                                                      len.as<i64>(), first, last - first, false, s);
+            }
+        }
+    }
+    if (dbg) dbg_resid<T>("band (after unmtr_hb2st)", n, B0->as<T>(), n, Z, n, w, s);
+    unmtr_he2hb<T>(n, n, panels, Z, n, s);
+    if (dbg) dbg_resid<T>("dense (after unmtr_he2hb)", n, A0->as<T>(), n, Z, n, w, s);
+    NHIP(hipStreamSynchronize(s));
+}
+
+// ---------------------------------------------------------------- gather / scatter
+// every rank's local block -> rank 0's dense n x n (ld n) device copy
+template <typename T>
+void gather_root(const Storage& S, T* D, hipStream_t s) {
+    Runtime& R = rt();
+    const int P = S.p * S.q;
+    const i64 nb = S.nb;
+    auto place = [&](const T* blk, i64 ldb, int pr, int pc) {
+        const i64 ml = numroc(S.m, nb, pr, S.p), nl = numroc(S.n, nb, pc, S.q);
+        for (i64 lj = 0; lj < nl; lj += nb)
+            for (i64 li = 0; li < ml; li += nb) {
+                const i64 gi = l2g(li, nb, S.p, pr), gj = l2g(lj, nb, S.q, pc);
+                copy2d(D + gi + gj * S.m, S.m, blk + li + lj * ldb, ldb, std::min(nb, ml - li), std::min(nb, nl - lj),
+                       s);
+            }
+    };
+    if (P == 1) {
+        place(static_cast<const T*>(S.buf), S.lld, 0, 0);
+        return;
+    }
+    std::vector<std::unique_ptr<Scratch>> bufs;
+    std::vector<P2P> ops;
+    std::vector<std::tuple<int, int, int, Scratch*>> got;
+    if (R.rank == 0) {
+        place(static_cast<const T*>(S.buf), S.lld, S.pr, S.pc);
+        for (int r = 1; r < P; ++r) {
+            const int pr = r % S.p, pc = r / S.p;
+            const i64 ml = numroc(S.m, nb, pr, S.p), nl = numroc(S.n, nb, pc, S.q);
+            if (!ml || !nl) continue;
+            bufs.push_back(std::make_unique<Scratch>((size_t)ml * nl * sizeof(T), s));
+            ops.push_back({false, r, bufs.back()->p, (size_t)ml * nl * sizeof(T)});
+            got.emplace_back(r, pr, pc, bufs.back().get());
+        }
+    } else if (S.mloc && S.nloc) {
+        bufs.push_back(std::make_unique<Scratch>((size_t)S.mloc * S.nloc * sizeof(T), s));
+        copy2d(bufs.back()->as<T>(), S.mloc, static_cast<const T*>(S.buf), S.lld, S.mloc, S.nloc, s);
+        ops.push_back({true, 0, bufs.back()->p, (size_t)S.mloc * S.nloc * sizeof(T)});
+    }
+    if (!ops.empty()) world_comm()->exchange(ops, s);
+    for (auto& g : got) {
+        const int pr = std::get<1>(g);
+        place(std::get<3>(g)->template as<T>(), numroc(S.m, nb, pr, S.p), pr, std::get<2>(g));
+    }
+    NHIP(hipStreamSynchronize(s));
+}
+
+// rank 0's dense n x n (ld n) device matrix -> every rank's local block of Z
+template <typename T>
+void scatter_root(const T* D, Storage& S, hipStream_t s) {
+    Runtime& R = rt();
+    const int P = S.p * S.q;
+    const i64 nb = S.nb;
+    auto take = [&](T* blk, i64 ldb, int pr, int pc) {
+        const i64 ml = numroc(S.m, nb, pr, S.p), nl = numroc(S.n, nb, pc, S.q);
+        for (i64 lj = 0; lj < nl; lj += nb)
+            for (i64 li = 0; li < ml; li += nb) {
+                const i64 gi = l2g(li, nb, S.p, pr), gj = l2g(lj, nb, S.q, pc);
+                copy2d(blk + li + lj * ldb, ldb, D + gi + gj * S.m, S.m, std::min(nb, ml - li), std::min(nb, nl - lj),
+                       s);
+            }
+    };
+    if (P == 1) {
+        take(static_cast<T*>(S.buf), S.lld, 0, 0);
+        NHIP(hipStreamSynchronize(s));
+        return;
+    }
+    std::vector<std::unique_ptr<Scratch>> bufs;
+    std::vector<P2P> ops;
+    Scratch* mine = nullptr;
+    if (R.rank == 0) {
+        take(static_cast<T*>(S.buf), S.lld, S.pr, S.pc);
+        for (int r = 1; r < P; ++r) {
+            const int pr = r % S.p, pc = r / S.p;
+            const i64 ml = numroc(S.m, nb, pr, S.p), nl = numroc(S.n, nb, pc, S.q);
+            if (!ml || !nl) continue;
+            bufs.push_back(std::make_unique<Scratch>((size_t)ml * nl * sizeof(T), s));
+            take(bufs.back()->as<T>(), ml, pr, pc);
+            ops.push_back({true, r, bufs.back()->p, (size_t)ml * nl * sizeof(T)});
+        }
+    } else if (S.mloc && S.nloc) {
+        bufs.push_back(std::make_unique<Scratch>((size_t)S.mloc * S.nloc * sizeof(T), s));
+        mine = bufs.back().get();
+        ops.push_back({false, 0, mine->p, (size_t)S.mloc * S.nloc * sizeof(T)});
+    }
+    if (!ops.empty()) world_comm()->exchange(ops, s);
+    if (mine) copy2d(static_cast<T*>(S.buf), S.lld, mine->as<T>(), S.mloc, S.mloc, S.nloc, s);
+    NHIP(hipStreamSynchronize(s));
+}
+
+// the full Hermitian (both triangles, real diagonal) from its uplo triangle
+template <typename T>
+void symmetrize(i64 n, T* D, Uplo uplo, hipStream_t s) {
+    if (n <= 0) return;
+    Scratch Tt((size_t)n * n * sizeof(T), s);
+    slate_hip::TriMask keep, other;
+    keep.mode = uplo == Uplo::Lower ? 1 : 2;
+    other.mode = uplo == Uplo::Lower ? 2 : 1;
+    other.diag_off = -1;                    // the strict opposite triangle
+    slate_hip::gecopy_mask<K<T>>(keep, n, n, kp(D), n, kp(D), n, true, s);           // stored triangle, real diagonal
+    slate_hip::gecopy<K<T>, K<T>>('G', ctrans<T>(), n, n, kp(D), n, kp(Tt.as<T>()), n, s);
+    slate_hip::gecopy_mask_merge<K<T>>(other, n, n, kp(Tt.as<T>()), n, kp(D), n, s);
+}
+
+template <typename T>
+int64_t heev_impl(HermitianMatrix<T>& A, std::vector<real_t<T>>& Lambda, Matrix<T>* Z) {
+    Runtime& R = rt();
+    const Storage& SA = *A.storage();
+    if (SA.m != SA.n) throw Error("native heev: square matrix");
+    const i64 n = SA.n;
+    hipStream_t s = R.main;
+    NHIP(hipStreamSynchronize(s));
+    if (Z) {
+        const Storage& SZ = *Z->storage();
+        if (SZ.m != n || SZ.n != n || SZ.p != SA.p || SZ.q != SA.q || SZ.nb != SA.nb)
+            throw Error("native heev: Z must be n x n on A's grid and tile size");
+    }
+    std::vector<double> w((size_t)n, 0.0);
+    std::unique_ptr<Scratch> D, Zd;
+    int64_t err = 0;
+    std::string msg;
+    if (R.rank == 0) D = std::make_unique<Scratch>((size_t)std::max<i64>(n, 1) * n * sizeof(T), s);
+    gather_root<T>(SA, D ? D->as<T>() : nullptr, s);
+    if (R.rank == 0) {
+        try {
+            symmetrize<T>(n, D->as<T>(), A.uplo(), s);
+            if (Z) Zd = std::make_unique<Scratch>((size_t)std::max<i64>(n, 1) * n * sizeof(T), s);
+            heev_1gpu<T>(n, D->as<T>(), w, Zd ? Zd->as<T>() : nullptr, Z != nullptr, s);
+        } catch (const std::exception& e) {
+            err = 1;
+            msg = e.what();
+        }
+    }
+    // the eigenvalues (and the error flag) to every rank
+    if (R.size > 1) {
+        Scratch b((size_t)(n + 1) * sizeof(double), s);
+        std::vector<double> h(w);
+        h.push_back((double)err);
+        upload(b.p, h.data(), h.size() * sizeof(double), s);
+        world_comm()->bcast(b.p, h.size() * sizeof(double), 0, s);
+        h = download_vec<double>(b.p, h.size(), s);
+        err = (int64_t)h.back();
+        h.pop_back();
+        w = h;
+    }
+    if (err) {
+        if (Z && R.size > 1) {}       // nothing scattered: every rank throws
+        throw Error(R.rank == 0 ? msg : std::string("native heev failed on rank 0"));
+    }
+    if (Z) scatter_root<T>(Zd ? Zd->as<T>() : nullptr, *Z->storage(), s);
+    Lambda.assign(w.begin(), w.end());
+    return 0;
+}
+
+}  // namespace
+
+template <typename T>
+int64_t heev(HermitianMatrix<T>& A, std::vector<real_t<T>>& Lambda, Matrix<T>& Z, const Options&) {
+    return heev_impl<T>(A, Lambda, &Z);
+}
+template <typename T>
+int64_t heev(HermitianMatrix<T>& A, std::vector<real_t<T>>& Lambda, const Options&) {
+    return heev_impl<T>(A, Lambda, nullptr);
+}
+
+#define SLATE_NATIVE_EIG_INST(T)                                                                            \
+    template int64_t heev<T>(HermitianMatrix<T>&, std::vector<real_t<T>>&, Matrix<T>&, const Options&);    \
+    template int64_t heev<T>(HermitianMatrix<T>&, std::vector<real_t<T>>&, const Options&);
+SLATE_NATIVE_EIG_INST(float)
+SLATE_NATIVE_EIG_INST(double)
+SLATE_NATIVE_EIG_INST(std::complex<float>)
+SLATE_NATIVE_EIG_INST(std::complex<double>)
+#undef SLATE_NATIVE_EIG_INST
+
+}  // namespace native
+}  // namespace slate_amd

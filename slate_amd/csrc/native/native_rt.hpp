@@ -18,6 +18,8 @@
 
 #include "../hip/common.hpp"
 #include "../hip/devalloc.hpp"
+#include "../hip/kernels.hpp"
+#include "../hip/launchers.hpp"
 #include "slate_amd/slate_native.hh"
 
 namespace slate_amd {
@@ -219,6 +221,31 @@ struct Scratch {
     Scratch(const Scratch&) = delete;
     template <typename T> T* as() { return static_cast<T*>(p); }
 };
+
+// ------------------------------------------------------------ kernel helpers
+// (shared by the driver files native.hip / native_eig.hip)
+template <typename T>
+inline void gemm_k(char ta, char tb, i64 m, i64 n, i64 k, T alpha, const T* A, i64 lda, const T* B, i64 ldb, T beta,
+            T* C, i64 ldc, hipStream_t s, const slate_hip::TriMask* mask = nullptr) {
+    if (m <= 0 || n <= 0) return;
+    slate_hip::GemmCall c;
+    c.transA = ta; c.transB = tb; c.m = m; c.n = n; c.k = k;
+    c.alpha_re = (double)std::real(alpha); c.alpha_im = (double)std::imag(alpha);
+    c.beta_re = (double)std::real(beta); c.beta_im = (double)std::imag(beta);
+    c.A = A; c.lda = lda; c.B = B; c.ldb = ldb; c.C = C; c.ldc = ldc;
+    if (mask) c.mask = *mask;
+    if constexpr (is_cplx<T>()) slate_hip::gemm_complex<K<T>>(c, s);
+    else slate_hip::gemm_real<T>(c, s);
+}
+
+// device-to-device block copy: the gecopy kernel (hipMemcpy2DAsync between
+// device pitches gave wrong results on this stack for pitched copies of a
+// few MB -- tools/probe/native_probe.cc)
+template <typename T>
+inline void copy2d(T* dst, i64 ldd, const T* src, i64 lds, i64 m, i64 n, hipStream_t s) {
+    if (m > 0 && n > 0) slate_hip::gecopy<K<T>, K<T>>('G', 'N', m, n, kp(src), lds, kp(dst), ldd, s);
+}
+
 
 }  // namespace native
 }  // namespace slate_amd
