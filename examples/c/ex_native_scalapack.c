@@ -84,6 +84,10 @@ double pdlansy_(const char* norm, const char* uplo, const int* n, const double* 
 void pdsyevd_(const char* jobz, const char* uplo, const int* n, double* a, const int* ia, const int* ja,
               const int* desca, double* w, double* z, const int* iz, const int* jz, const int* descz, double* work,
               const int* lwork, int* iwork, const int* liwork, int* info);
+void pdgesvd_(const char* jobu, const char* jobvt, const int* m, const int* n, double* a, const int* ia,
+              const int* ja, const int* desca, double* s, double* u, const int* iu, const int* ju, const int* descu,
+              double* vt, const int* ivt, const int* jvt, const int* descvt, double* work, const int* lwork,
+              int* info);
 void slate_amd_finalize(void);
 
 static int g_rank;
@@ -254,6 +258,37 @@ int main(int argc, char** argv) {
             }
         check(info || !sorted ? "pdsyevd-FAILED" : "pdsyevd", sqrt(ee) / (an * n));
         free(z); free(az); free(w);
+    }
+
+    /* pdgesvd_: A = U diag(s) VT on the whole n x n matrix (A U-check via pdgemm_) */
+    {
+        double* u = malloc(sizeof(double) * lld * (nloc > 0 ? nloc : 1));
+        double* vt = malloc(sizeof(double) * lld * (nloc > 0 ? nloc : 1));
+        double* us = malloc(sizeof(double) * lld * (nloc > 0 ? nloc : 1));
+        double* sv = malloc(sizeof(double) * n);
+        const double a1 = 1.0, b0 = 0.0;
+        int lw = -1;
+        double wq;
+        FILL_A(gen);
+        pdgesvd_("V", "V", &n, &n, a, &one, &one, desca, sv, u, &one, &one, desca, vt, &one, &one, desca, &wq, &lw,
+                 &info);
+        lw = 1;
+        pdgesvd_("V", "V", &n, &n, a, &one, &one, desca, sv, u, &one, &one, desca, vt, &one, &one, desca, &wq, &lw,
+                 &info);
+        for (int lj = 0; lj < nloc; ++lj)
+            for (int li = 0; li < mloc; ++li) us[li + lj * lld] = u[li + lj * lld] * sv[l2g(lj, nb, q, pc)];
+        pdgemm_("N", "N", &n, &n, &n, &a1, us, &one, &one, desca, vt, &one, &one, desca, &b0, a, &one, &one, desca);
+        double ee = 0, ww = 0;
+        int desc_ok = 1;
+        for (int i = 1; i < n; ++i) desc_ok = desc_ok && sv[i - 1] >= sv[i];
+        for (int lj = 0; lj < nloc; ++lj)
+            for (int li = 0; li < mloc; ++li) {
+                const double t = gen(l2g(li, nb, p, pr), l2g(lj, nb, q, pc), n);
+                ee += (a[li + lj * lld] - t) * (a[li + lj * lld] - t);
+                ww += t * t;
+            }
+        check(info || !desc_ok ? "pdgesvd-FAILED" : "pdgesvd", sqrt(ee / ww));
+        free(u); free(vt); free(us); free(sv);
     }
 
     /* LU */

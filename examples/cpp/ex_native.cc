@@ -454,6 +454,43 @@ void run(int p, int q, int me) {
         for (int64_t i = 0; i < ne; ++i) dv = std::max(dv, std::abs((double)lam2[i] - (double)lam[i]));
         report("heev_values", dv / (an > 0 ? an : 1));
     }
+    // ---- svd: || A - U S V^H || / || A ||, || U^H U - I ||, || V V^H - I ||
+    //      (tall and wide; values only must give the same spectrum)
+    for (int wide = 0; wide < 2; ++wide) {
+        const int64_t ms = wide ? 170 : 290, ns = wide ? 250 : 210, ks = std::min(ms, ns);
+        sn::Matrix<T> Am(ms, ns, nb, p, q), U(ms, ks, nb, p, q), VH(ks, ns, nb, p, q);
+        Am.generate(sn::Gen::Random, 141 + wide);
+        std::vector<T> a((size_t)ms * ns), u((size_t)ms * ks), vh((size_t)ks * ns);
+        Am.to_host(a.data(), ms);
+        std::vector<sn::real_t<T>> sv, sv2;
+        const int64_t inf = sn::svd(Am, sv, U, VH);
+        U.to_host(u.data(), ms);
+        VH.to_host(vh.data(), ks);
+        std::vector<T> us((size_t)ms * ks);
+        for (int64_t j = 0; j < ks; ++j)
+            for (int64_t i = 0; i < ms; ++i) us[i + j * ms] = u[i + j * ms] * (sn::real_t<T>)sv[j];
+        auto usv = mul<T>('N', 'N', ms, ns, ks, us, ms, vh, ks);
+        auto want = widen(a);
+        for (size_t i = 0; i < usv.size(); ++i) usv[i] -= want[i];
+        bool desc = true;
+        for (size_t i = 1; i < sv.size(); ++i) desc = desc && sv[i - 1] >= sv[i];
+        report(inf || !desc ? (wide ? "svd_wide-FAILED" : "svd-FAILED") : (wide ? "svd_wide" : "svd"), rel<T>(usv, want));
+        auto uhu = mul<T>('C', 'N', ks, ks, ms, u, ms, u, ms);
+        auto vvh = mul<T>('N', 'C', ks, ks, ns, vh, ks, vh, ks);
+        double eo = 0;
+        for (int64_t j = 0; j < ks; ++j)
+            for (int64_t i = 0; i < ks; ++i) {
+                const double id = i == j ? 1.0 : 0.0;
+                eo += std::norm(uhu[i + j * ks] - id) + std::norm(vvh[i + j * ks] - id);
+            }
+        report(wide ? "svd_wide_orth" : "svd_orth", std::sqrt(eo) / ks);
+        if (!wide) {
+            sn::svd(Am, sv2);
+            double dv = 0;
+            for (int64_t i = 0; i < ks; ++i) dv = std::max(dv, std::abs((double)sv2[i] - (double)sv[i]));
+            report("svd_values", dv / std::max(1.0, (double)sv[0]));
+        }
+    }
     // ---- condition estimates: 1 <= rcond_est / rcond <= 3 (exact rcond from the inverse)
     {
         const int64_t nc = 120;

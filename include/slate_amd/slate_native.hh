@@ -230,6 +230,14 @@ int64_t heev(HermitianMatrix<T>& A, std::vector<real_t<T>>& Lambda, Matrix<T>& Z
 template <typename T>
 int64_t heev(HermitianMatrix<T>& A, std::vector<real_t<T>>& Lambda, const Options& opts = {});
 
+// singular value decomposition A = U diag(S) VH (reference slate.hh svd:
+// ge2tb -> tb2bd -> bdsqr -> back-transforms): S the min(m, n) singular
+// values descending (every rank), U m x min(m, n), VH min(m, n) x n on A's
+// grid and tile size.  A is not modified.
+template <typename T>
+int64_t svd(Matrix<T>& A, std::vector<real_t<T>>& S, Matrix<T>& U, Matrix<T>& VH, const Options& opts = {});
+template <typename T> int64_t svd(Matrix<T>& A, std::vector<real_t<T>>& S, const Options& opts = {});
+
 struct QRData;
 template <typename T>
 struct QRFactors {

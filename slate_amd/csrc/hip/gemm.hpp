@@ -144,7 +144,13 @@ struct Stage {
     }
 };
 
-template <typename T, bool TA, bool TB, int BM, int BN, int BK, bool PTRS, int WVM = 2, int WVN = 2, int OCC = 2>
+// PF: operand prefetch depth in K steps.  1: the next step's global loads
+// are issued at the top of the current step (one register set);
+// 2: two steps ahead (two register sets, main loop unrolled by two so every
+// set is statically indexed) -- a whole step more latency cover for the
+// L2-missing operand loads of the wide trailing updates.
+template <typename T, bool TA, bool TB, int BM, int BN, int BK, bool PTRS, int WVM = 2, int WVN = 2, int OCC = 2,
+          int PF = 1>
 __global__ void __launch_bounds__(64 * WVM * WVN, OCC)
 gemm_real_kernel(GemmArgs<T> a) {
     using MF = mfma_real<T>;
@@ -209,23 +215,7 @@ gemm_real_kernel(GemmArgs<T> a) {
     SA sa; SB sb;
     const i64 K = a.k;
     const int nk = (int)((K + BK - 1) / BK);
-    if (nk > 0) {
-        sa.load(A, a.lda, m0, 0, a.m, K, a.vecA, tid);
-        sb.load(B, a.ldb, n0, 0, a.n, K, a.vecB, tid);
-        sa.store(smem, tid);
-        sb.store(smem + LA, tid);
-    }
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-        T* cur = smem + (kt & 1) * (LA + LB);
-        T* nxt = smem + ((kt + 1) & 1) * (LA + LB);
-        const bool more = kt + 1 < nk;
-        if (more) {
-            sa.load(A, a.lda, m0, (i64)(kt + 1) * BK, a.m, K, a.vecA, tid);
-            sb.load(B, a.ldb, n0, (i64)(kt + 1) * BK, a.n, K, a.vecB, tid);
-        }
-        const T* la = cur;
-        const T* lb = cur + LA;
+    auto compute = [&](const T* la, const T* lb) {
         #pragma unroll
         for (int kk = 0; kk < BK / 4; ++kk) {
             const int kq = kk * 4 + (lane >> 4);
@@ -239,11 +229,59 @@ gemm_real_kernel(GemmArgs<T> a) {
                 #pragma unroll
                 for (int j = 0; j < NI; ++j) acc[i][j] = MF::mma(xb[j], ya[i], acc[i][j]);
         }
-        if (more) {
-            sa.store(nxt, tid);
-            sb.store(nxt + LA, tid);
+    };
+    if (nk > 0) {
+        sa.load(A, a.lda, m0, 0, a.m, K, a.vecA, tid);
+        sb.load(B, a.ldb, n0, 0, a.n, K, a.vecB, tid);
+        sa.store(smem, tid);
+        sb.store(smem + LA, tid);
+    }
+    if constexpr (PF == 1) {
+        __syncthreads();
+        for (int kt = 0; kt < nk; ++kt) {
+            T* cur = smem + (kt & 1) * (LA + LB);
+            T* nxt = smem + ((kt + 1) & 1) * (LA + LB);
+            const bool more = kt + 1 < nk;
+            if (more) {
+                sa.load(A, a.lda, m0, (i64)(kt + 1) * BK, a.m, K, a.vecA, tid);
+                sb.load(B, a.ldb, n0, (i64)(kt + 1) * BK, a.n, K, a.vecB, tid);
+            }
+            compute(cur, cur + LA);
+            if (more) {
+                sa.store(nxt, tid);
+                sb.store(nxt + LA, tid);
+            }
+            __syncthreads();
+        }
+    } else {
+        SA sa2; SB sb2;
+        if (nk > 1) {
+            sa2.load(A, a.lda, m0, (i64)BK, a.m, K, a.vecA, tid);
+            sb2.load(B, a.ldb, n0, (i64)BK, a.n, K, a.vecB, tid);
         }
         __syncthreads();
+        // step kt: (na, nb_) hold step kt + 1 (in flight), (fa, fb) are free
+        // (their step is in LDS already) and take step kt + 2
+        auto step = [&](int kt, SA& na, SB& nb_, SA& fa, SB& fb) {
+            T* cur = smem + (kt & 1) * (LA + LB);
+            T* nxt = smem + ((kt + 1) & 1) * (LA + LB);
+            if (kt + 2 < nk) {
+                fa.load(A, a.lda, m0, (i64)(kt + 2) * BK, a.m, K, a.vecA, tid);
+                fb.load(B, a.ldb, n0, (i64)(kt + 2) * BK, a.n, K, a.vecB, tid);
+            }
+            compute(cur, cur + LA);
+            if (kt + 1 < nk) {
+                na.store(nxt, tid);
+                nb_.store(nxt + LA, tid);
+            }
+            __syncthreads();
+        };
+        int kt = 0;
+        for (; kt + 1 < nk; kt += 2) {
+            step(kt, sa2, sb2, sa, sb);
+            step(kt + 1, sa, sb, sa2, sb2);
+        }
+        if (kt < nk) step(kt, sa2, sb2, sa, sb);
     }
 
     // epilogue

@@ -151,8 +151,13 @@ static void launch_real(const GemmArgs<T>& a0, int batch, hipStream_t s) {
     if (gm == 0 || gn == 0 || batch == 0) return;
     i64 nblk = gm * gn;
     if (i64 t = tri_blocks(a, BM, BN)) { a.remap = 2; nblk = t; }
+    // Two register stages for fp64 NN (tools/exp/gemm_pf_r5.hip on MI355X:
+    // 31744^2 x 512 59.2 -> 62.9 TF/s, 16384^2 x 4096 63.5 -> 68.4 TF/s); the
+    // NT form loses with it (61.3 -> 56.3 TF/s), so it keeps one.
+    constexpr int PF = (sizeof(T) == 8 && !TA && !TB) ? 2 : 1;
     dim3 grid((unsigned)nblk, (unsigned)batch);
-    hipLaunchKernelGGL((gemm_real_kernel<T, TA, TB, BM, BN, BK, PTRS, WVM, WVN>), grid, dim3(64 * WVM * WVN), 0, s, a);
+    hipLaunchKernelGGL((gemm_real_kernel<T, TA, TB, BM, BN, BK, PTRS, WVM, WVN, 2, PF>), grid, dim3(64 * WVM * WVN), 0, s,
+                       a);
     HIP_LAUNCH_CHECK();
 }
 

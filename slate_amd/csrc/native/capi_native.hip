@@ -1217,6 +1217,72 @@ int p_heev(char jobz, char uplo, int n, const T* a, int ia, int ja, const int* d
     });
 }
 
+// ---- SVD (reference lapack_api/lapack_gesvd.cc, scalapack_api/scalapack_gesvd.cc):
+// jobu / jobvt 'N' (none), 'V' or 'S' (the min(m, n) singular vectors);
+// 'A' (full square factors) only when m == n (LAPACK) and 'O' is not offered
+inline bool svd_job(char j, bool& want) {
+    j = up(j);
+    want = j == 'V' || j == 'S' || j == 'A';
+    return j == 'N' || j == 'V' || j == 'S' || j == 'A';
+}
+template <typename T>
+int h_gesvd(char jobu, char jobvt, i64 m, i64 n, T* a, i64 lda, sn::real_t<T>* sv, T* u, i64 ldu, T* vt, i64 ldvt) {
+    bool wu = false, wv = false;
+    if (!svd_job(jobu, wu)) return -1;
+    if (!svd_job(jobvt, wv)) return -2;
+    if ((up(jobu) == 'A' && m > n) || (up(jobvt) == 'A' && n > m)) return -1;
+    if (m < 0) return -3;
+    if (n < 0) return -4;
+    if (lda < std::max<i64>(1, m)) return -6;
+    const i64 k = std::min(m, n);
+    if (wu && ldu < std::max<i64>(1, m)) return -9;
+    if (wv && ldvt < std::max<i64>(1, k)) return -11;
+    if (k == 0) return 0;
+    return (int)guarded([&]() -> int64_t {
+        int p, q;
+        grid_of(p, q);
+        const i64 nb = nb_of(std::max(m, n));
+        sn::Matrix<T> A(m, n, nb, p, q);
+        A.from_host(a, lda);
+        std::vector<sn::real_t<T>> S;
+        if (wu || wv) {
+            sn::Matrix<T> U(m, k, nb, p, q), VH(k, n, nb, p, q);
+            sn::svd(A, S, U, VH);
+            if (wu) U.to_host(u, ldu);
+            if (wv) VH.to_host(vt, ldvt);
+        } else {
+            sn::svd(A, S);
+        }
+        std::copy(S.begin(), S.end(), sv);
+        return 0;
+    });
+}
+template <typename T>
+int p_gesvd(char jobu, char jobvt, int m, int n, const T* a, int ia, int ja, const int* desca, sn::real_t<T>* sv,
+            T* u, int iu, int ju, const int* descu, T* vt, int ivt, int jvt, const int* descvt) {
+    bool wu = false, wv = false;
+    if (!svd_job(jobu, wu) || up(jobu) == 'A') return -1;
+    if (!svd_job(jobvt, wv) || up(jobvt) == 'A') return -2;
+    const int k = std::min(m, n);
+    if (k == 0) return 0;
+    return (int)guarded([&]() -> int64_t {
+        sn::Matrix<T> A = scal_matrix<T>(desca, m, n, ia, ja, a);
+        std::vector<sn::real_t<T>> S;
+        if (wu || wv) {
+            sn::Matrix<T> U = wu ? scal_matrix<T>(descu, m, k, iu, ju, u) : sn::Matrix<T>(m, k, A.nb(), A.p(), A.q());
+            sn::Matrix<T> VH = wv ? scal_matrix<T>(descvt, k, n, ivt, jvt, vt) : sn::Matrix<T>(k, n, A.nb(), A.p(), A.q());
+            if (U.nb() != A.nb() || VH.nb() != A.nb()) throw sn::Error("native p?gesvd: U / VT must have A's block size");
+            sn::svd(A, S, U, VH);
+            if (wu) scal_back(U, descu, u);
+            if (wv) scal_back(VH, descvt, vt);
+        } else {
+            sn::svd(A, S);
+        }
+        std::copy(S.begin(), S.end(), sv);
+        return 0;
+    });
+}
+
 extern "C" {
 
 const char* slate_amd_last_error(void) { return g_err.c_str(); }
@@ -1755,6 +1821,44 @@ double slate_native_dlange(char norm, int64_t m, int64_t n, const double* a, int
         }                                                                                                       \
         *info = p_heev<T>(*jobz, *uplo, *n, a, *ia, *ja, desca, w, z, *iz, *jz, descz);                         \
     }
+#define SN_SVD_R(X, T)                                                                                          \
+    void slate_##X##gesvd(const char* jobu, const char* jobvt, const int* m, const int* n, T* a, const int* lda,   \
+                          T* s, T* u, const int* ldu, T* vt, const int* ldvt, T* work, const int* lwork, int* info) { \
+        if (*lwork == -1) { work[0] = T(1); *info = 0; return; }                                                \
+        *info = h_gesvd<T>(*jobu, *jobvt, *m, *n, a, *lda, s, u, *ldu, vt, *ldvt);                              \
+    }                                                                                                           \
+    void p##X##gesvd_(const char* jobu, const char* jobvt, const int* m, const int* n, const T* a, const int* ia, \
+                      const int* ja, const int* desca, T* s, T* u, const int* iu, const int* ju, const int* descu, \
+                      T* vt, const int* ivt, const int* jvt, const int* descvt, T* work, const int* lwork,       \
+                      int* info) {                                                                              \
+        if (*lwork == -1) { work[0] = T(1); *info = 0; return; }                                                \
+        *info = p_gesvd<T>(*jobu, *jobvt, *m, *n, a, *ia, *ja, desca, s, u, *iu, *ju, descu, vt, *ivt, *jvt,     \
+                           descvt);                                                                             \
+    }
+#define SN_SVD_C(X, T, R)                                                                                       \
+    void slate_##X##gesvd(const char* jobu, const char* jobvt, const int* m, const int* n, T* a, const int* lda,   \
+                          R* s, T* u, const int* ldu, T* vt, const int* ldvt, T* work, const int* lwork, R* rwork, \
+                          int* info) {                                                                          \
+        (void)rwork;                                                                                            \
+        if (*lwork == -1) { work[0] = T(1); *info = 0; return; }                                                \
+        *info = h_gesvd<T>(*jobu, *jobvt, *m, *n, a, *lda, s, u, *ldu, vt, *ldvt);                              \
+    }                                                                                                           \
+    void p##X##gesvd_(const char* jobu, const char* jobvt, const int* m, const int* n, const T* a, const int* ia, \
+                      const int* ja, const int* desca, R* s, T* u, const int* iu, const int* ju, const int* descu, \
+                      T* vt, const int* ivt, const int* jvt, const int* descvt, T* work, const int* lwork,       \
+                      R* rwork, int* info) {                                                                    \
+        (void)rwork;                                                                                            \
+        if (*lwork == -1) { work[0] = T(1); *info = 0; return; }                                                \
+        *info = p_gesvd<T>(*jobu, *jobvt, *m, *n, a, *ia, *ja, desca, s, u, *iu, *ju, descu, vt, *ivt, *jvt,     \
+                           descvt);                                                                             \
+    }
+SN_SVD_R(s, float)
+SN_SVD_R(d, double)
+SN_SVD_C(c, std::complex<float>, float)
+SN_SVD_C(z, std::complex<double>, double)
+#undef SN_SVD_R
+#undef SN_SVD_C
+
 SN_EIG_R(s, float)
 SN_EIG_R(d, double)
 SN_EIG_C(c, std::complex<float>, float)

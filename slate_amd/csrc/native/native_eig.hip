@@ -1,9 +1,12 @@
-// Hermitian eigensolver of the native (Python-free) library:
+// Hermitian eigensolver and SVD of the native (Python-free) library:
 //   heev = he2hb (stage 1) -> hb2st (stage 2, GPU bulge chase) ->
 //          divide & conquer on the real tridiagonal (GPU leaves / merges) ->
 //          back-transforms unmtr_hb2st, unmtr_he2hb
+//   svd  = ge2tb (stage 1) -> tb2bd (stage 2, GPU bulge chase) -> bdsqr
+//          (host implicit QR) -> back-transforms unmbr_tb2bd, unmbr_ge2tb
 // (reference src/heev.cc:66-225, src/he2hb.cc, src/hb2st.cc:139-279,
-// src/stedc_solve.cc:79-238, src/unmtr_hb2st.cc, src/unmtr_he2hb.cc).
+// src/stedc_solve.cc:79-238, src/unmtr_hb2st.cc, src/unmtr_he2hb.cc,
+// src/svd.cc:155-364, src/ge2tb.cc, src/tb2bd.cc, src/bdsqr.cc).
 //
 // MI355X design: the matrix is gathered onto ONE GPU (rank 0; 288 GB of HBM
 // holds n = 100k+ in fp64) and every stage runs there on the hand-written
@@ -19,6 +22,7 @@
 #include <numeric>
 #include <vector>
 
+#include "../include/bdsqr.hpp"
 #include "../include/steqr.hpp"
 #include "native_rt.hpp"
 
@@ -678,7 +682,272 @@ int64_t heev_impl(HermitianMatrix<T>& A, std::vector<real_t<T>>& Lambda, Matrix<
     return 0;
 }
 
+// ---------------------------------------------------------------- SVD
+// C -= V op(T) (V^H C), op(T) = T^H (apply Q^H, conj) or T (apply Q)
+template <typename T>
+void apply_qh(i64 m, i64 kk, const T* V, const T* Tm, T* C, i64 ldc, i64 nc, bool conj, hipStream_t s) {
+    if (m <= 0 || nc <= 0 || kk <= 0) return;
+    const char ct = ctrans<T>();
+    Scratch W((size_t)kk * nc * sizeof(T), s);
+    gemm_k<T>(ct, 'N', kk, nc, m, T(1), V, m, C, ldc, T(0), W.as<T>(), kk, s);
+    slate_hip::trmm<K<T>>('L', 'U', conj ? ct : 'N', 'N', kk, nc, kv(T(1)), kp(Tm), kk, kp(W.as<T>()), kk, s);
+    gemm_k<T>('N', 'N', m, nc, kk, T(-1), V, m, W.as<T>(), kk, T(1), C, ldc, s);
+}
+
+// dense m x n (m >= n, ld lda) -> upper band of width nb in place:
+// A = Ql B Qr^H (left: column-panel QR reflectors, right: row-panel LQ)
+template <typename T>
+void ge2tb(i64 m, i64 n, i64 nb, T* A, i64 lda, std::vector<Panel<T>>& left, std::vector<Panel<T>>& right,
+           hipStream_t s) {
+    const char ct = ctrans<T>();
+    for (i64 k0 = 0; k0 < n; k0 += nb) {
+        const i64 kb = std::min(nb, n - k0), mp = m - k0, kk = std::min(mp, kb);
+        T* P = A + k0 + k0 * lda;
+        Panel<T> L;
+        L.r0 = k0;
+        L.kk = kk;
+        L.V = std::make_unique<Scratch>((size_t)mp * kk * sizeof(T), s);
+        L.T_ = std::make_unique<Scratch>((size_t)kk * kk * sizeof(T), s);
+        {
+            Scratch tau((size_t)kk * sizeof(T), s);
+            NHIP(hipMemsetAsync(tau.p, 0, (size_t)kk * sizeof(T), s));
+            slate_hip::geqrf_panel_ws<K<T>>(mp, kb, kp(P), lda, kp(tau.as<T>()), kp(L.T_->template as<T>()), kk,
+                                            kp(L.V->template as<T>()), mp, rt().qr_work, s);
+        }
+        if (k0 + kb < n)
+            apply_qh<T>(mp, kk, L.V->template as<T>(), L.T_->template as<T>(), A + k0 + (k0 + kb) * lda, lda,
+                        n - k0 - kb, true, s);
+        zero_strict_lower<T>(mp, kb, P, lda, s);
+        left.push_back(std::move(L));
+        const i64 c0 = k0 + kb;
+        if (c0 >= n) continue;
+        const i64 w = n - c0, kr = std::min(w, kb);
+        T* X = A + k0 + c0 * lda;                     // kb x w
+        Scratch Xh((size_t)w * kb * sizeof(T), s);    // X^H: w x kb
+        slate_hip::gecopy<K<T>, K<T>>('G', ct, w, kb, kp(X), lda, kp(Xh.as<T>()), w, s);
+        Panel<T> Rt;
+        Rt.r0 = c0;
+        Rt.kk = kr;
+        Rt.V = std::make_unique<Scratch>((size_t)w * kr * sizeof(T), s);
+        Rt.T_ = std::make_unique<Scratch>((size_t)kr * kr * sizeof(T), s);
+        {
+            Scratch tau((size_t)kr * sizeof(T), s);
+            NHIP(hipMemsetAsync(tau.p, 0, (size_t)kr * sizeof(T), s));
+            slate_hip::geqrf_panel_ws<K<T>>(w, kb, kp(Xh.as<T>()), w, kp(tau.as<T>()), kp(Rt.T_->template as<T>()),
+                                            kr, kp(Rt.V->template as<T>()), w, rt().qr_work, s);
+        }
+        zero_strict_lower<T>(w, kb, Xh.as<T>(), w, s);
+        slate_hip::gecopy<K<T>, K<T>>('G', ct, kb, w, kp(Xh.as<T>()), w, kp(X), lda, s);
+        const i64 mr = m - k0 - kb;
+        if (mr > 0) {
+            // C -= (C V T) V^H on the rows below the panel
+            T* C = A + (k0 + kb) + c0 * lda;
+            Scratch W((size_t)mr * kr * sizeof(T), s);
+            gemm_k<T>('N', 'N', mr, kr, w, T(1), C, lda, Rt.V->template as<T>(), w, T(0), W.as<T>(), mr, s);
+            slate_hip::trmm<K<T>>('R', 'U', 'N', 'N', mr, kr, kv(T(1)), kp(Rt.T_->template as<T>()), kr,
+                                  kp(W.as<T>()), mr, s);
+            gemm_k<T>('N', ct, mr, w, kr, T(-1), W.as<T>(), mr, Rt.V->template as<T>(), w, T(1), C, lda, s);
+        }
+        right.push_back(std::move(Rt));
+    }
+}
+
+// one GPU: A (m x n, m >= n, ld m) -> s (descending), U (m x n, ld m) and
+// V (n x n, ld n) with A = U diag(s) V^H (wantu / wantv)
+template <typename T>
+void svd_1gpu(i64 m, i64 n, T* A, std::vector<double>& sv, T* U, T* V, bool wantu, bool wantv, hipStream_t s) {
+    using R = real_t<T>;
+    const i64 b = std::max<i64>(1, std::min<i64>(64, n));
+    std::vector<Panel<T>> left, right;
+    ge2tb<T>(m, n, b, A, m, left, right, s);
+    // the k x k upper band (0 <= j - i <= b) into a padded working copy
+    const i64 k = n, ldp = (k + 7) / 8 * 8 + 72;
+    Scratch Bh((size_t)ldp * std::max<i64>(k, 1) * sizeof(T), s);
+    {
+        slate_hip::TriMask up_, lo_;
+        up_.mode = 2;                           // i <= j
+        lo_.mode = 1;
+        lo_.diag_off = b;                       // i + b >= j
+        slate_hip::gecopy_mask<K<T>>(up_, k, k, kp(A), m, kp(Bh.as<T>()), ldp, false, s);
+        slate_hip::gecopy_mask<K<T>>(lo_, k, k, kp(Bh.as<T>()), ldp, kp(Bh.as<T>()), ldp, false, s);
+    }
+    const i64 nsw = std::max<i64>(k - 1, 0);
+    std::vector<i64> nt((size_t)std::max<i64>(nsw, 1), 0), sp((size_t)std::max<i64>(k, 1), 0);
+    for (i64 j = 0; j < nsw; ++j) {
+        const i64 ce0 = std::min(j + b, k - 1);
+        nt[j] = 1 + (k - 1 - ce0 + b - 1) / b;
+    }
+    for (i64 j = 1; j < k; ++j) sp[j] = sp[j - 1] + nt[j - 1];
+    const i64 total = nsw ? sp[k - 1] + nt[nsw - 1] : 0, cap = std::max<i64>(total, 1);
+    auto store = [&](std::vector<std::unique_ptr<Scratch>>& st) {
+        st.push_back(std::make_unique<Scratch>((size_t)cap * b * sizeof(T), s));
+        st.push_back(std::make_unique<Scratch>((size_t)cap * sizeof(T), s));
+        st.push_back(std::make_unique<Scratch>((size_t)cap * sizeof(i64), s));
+        st.push_back(std::make_unique<Scratch>((size_t)cap * sizeof(i64), s));
+        NHIP(hipMemsetAsync(st[0]->p, 0, (size_t)cap * b * sizeof(T), s));
+        NHIP(hipMemsetAsync(st[1]->p, 0, (size_t)cap * sizeof(T), s));
+    };
+    std::vector<std::unique_ptr<Scratch>> Us, Vs, keep;
+    store(Us);
+    store(Vs);
+    Scratch* ntd = upload_vec(keep, nt, s);
+    Scratch* spd = upload_vec(keep, sp, s);
+    if (nsw > 0) {
+        Scratch work((size_t)(nsw + 2) * sizeof(int), s);
+        NHIP(hipMemsetAsync(work.p, 0, (size_t)(nsw + 2) * sizeof(int), s));
+        hipDeviceProp_t pr;
+        NHIP(hipGetDeviceProperties(&pr, rt().device));
+        const i64 nt0 = nt[0] ? nt[0] : 1;
+        const int nwg = (int)std::min<i64>({std::max<i64>(nsw, 1), (i64)pr.multiProcessorCount,
+                                            std::max<i64>(8, nt0 / 4 + 8)});
+        slate_hip::tb2bd_device<K<T>>(k, (int)b, kp(Bh.as<T>()), ldp, kp(Us[0]->as<T>()), kp(Us[1]->as<T>()),
+                                      Us[2]->as<i64>(), Us[3]->as<i64>(), kp(Vs[0]->as<T>()), kp(Vs[1]->as<T>()),
+                                      Vs[2]->as<i64>(), Vs[3]->as<i64>(), spd->as<i64>(), ntd->as<i64>(),
+                                      work.as<int>(), nsw, nwg, s);
+    }
+    // diagonal / super-diagonal, and the phases of a complex bidiagonal
+    Scratch dsub((size_t)2 * std::max<i64>(k, 1) * sizeof(T), s);
+    copy2d(dsub.as<T>(), 1, Bh.as<T>(), ldp + 1, 1, k, s);
+    if (k > 1) copy2d(dsub.as<T>() + k, 1, Bh.as<T>() + ldp, ldp + 1, 1, k - 1, s);
+    const std::vector<T> ds = download_vec<T>(dsub.p, (size_t)(2 * k), s);
+    std::vector<double> d((size_t)k), e((size_t)std::max<i64>(k, 1), 0.0);
+    std::vector<T> pu((size_t)k, T(1)), pv((size_t)k, T(1));
+    for (i64 i = 0; i < k; ++i) {
+        if constexpr (is_cplx<T>()) {
+            const T x = ds[i] * pv[i];
+            const R ax = std::abs(x);
+            pu[i] = ax > R(0) ? x / ax : T(1);
+            d[i] = (double)ax;
+            if (i < k - 1) {
+                const T y = std::conj(pu[i]) * ds[k + i];
+                const R ay = std::abs(y);
+                pv[i + 1] = ay > R(0) ? std::conj(y / ay) : T(1);
+                e[i] = (double)ay;
+            }
+        } else {
+            d[i] = (double)ds[i];
+            if (i < k - 1) e[i] = (double)ds[k + i];
+        }
+    }
+    std::vector<double> Uh(wantu ? (size_t)k * k : 0, 0.0), VTh(wantv ? (size_t)k * k : 0, 0.0);
+    for (i64 i = 0; i < k && wantu; ++i) Uh[i + i * k] = 1.0;
+    for (i64 i = 0; i < k && wantv; ++i) VTh[i + i * k] = 1.0;
+    if (slate_tridiag::bdsqr_impl(k, d.data(), e.data(), wantu ? Uh.data() : nullptr, k, wantu ? k : 0,
+                                  wantv ? VTh.data() : nullptr, k, wantv ? k : 0))
+        throw Error("native svd: the bidiagonal QR iteration did not converge");
+    sv = d;
+    auto back = [&](std::vector<std::unique_ptr<Scratch>>& F, const std::vector<double>& Qh, const std::vector<T>& ph,
+                    T* Z, i64 ldz, std::vector<Panel<T>>& panels) {
+        Scratch* q = upload_vec(keep, Qh, s);
+        Scratch* phd = is_cplx<T>() ? upload_vec(keep, ph, s) : nullptr;
+        real_to_phase<T>(k, k, q->as<double>(), k, phd ? kp(phd->as<T>()) : nullptr, kp(Z), ldz, s);
+        if (nsw > 0 &&
+            !slate_hip::unmtr_hb2st_blocked<K<T>>(k, k, kp(Z), ldz, kp(F[0]->as<T>()), b, kp(F[1]->as<T>()),
+                                                  spd->as<i64>(), ntd->as<i64>(), nsw, false, s)) {
+            for (i64 j = k - 1; j >= 0; --j) {
+                const i64 first = sp[j], last = j + 1 < k ? sp[j + 1] : total;
+                if (last > first)
+                    slate_hip::apply_refl_batch<K<T>>(k, kp(Z), ldz, kp(F[0]->as<T>()), b, kp(F[1]->as<T>()),
+                                                      F[2]->as<i64>(), F[3]->as<i64>(), first, last - first, false, s);
+            }
+        }
+        for (auto it = panels.rbegin(); it != panels.rend(); ++it) {
+            const i64 mr = (&panels == &left ? m : k) - it->r0;
+            apply_qh<T>(mr, it->kk, it->V->template as<T>(), it->T_->template as<T>(), Z + it->r0, ldz, k, false, s);
+        }
+    };
+    if (wantu) {
+        NHIP(hipMemsetAsync(U, 0, (size_t)m * k * sizeof(T), s));
+        back(Us, Uh, pu, U, m, left);
+    }
+    if (wantv) {
+        std::vector<double> Vh((size_t)k * k);                 // V = VT^T (real)
+        for (i64 j = 0; j < k; ++j)
+            for (i64 i = 0; i < k; ++i) Vh[i + j * k] = VTh[j + i * k];
+        back(Vs, Vh, pv, V, k, right);
+    }
+    NHIP(hipStreamSynchronize(s));
+}
+
+template <typename T>
+int64_t svd_impl(Matrix<T>& A, std::vector<real_t<T>>& S, Matrix<T>* U, Matrix<T>* VH) {
+    Runtime& R = rt();
+    const Storage& SA = *A.storage();
+    const i64 m0 = SA.m, n0 = SA.n, k = std::min(m0, n0);
+    hipStream_t s = R.main;
+    NHIP(hipStreamSynchronize(s));
+    if (U) {
+        const Storage& SU = *U->storage();
+        if (SU.m != m0 || SU.n != k || SU.p != SA.p || SU.q != SA.q || SU.nb != SA.nb)
+            throw Error("native svd: U must be m x min(m, n) on A's grid and tile size");
+    }
+    if (VH) {
+        const Storage& SV = *VH->storage();
+        if (SV.m != k || SV.n != n0 || SV.p != SA.p || SV.q != SA.q || SV.nb != SA.nb)
+            throw Error("native svd: VH must be min(m, n) x n on A's grid and tile size");
+    }
+    std::vector<double> sv((size_t)k, 0.0);
+    std::unique_ptr<Scratch> D, Du, Dv;
+    int64_t err = 0;
+    std::string msg;
+    if (R.rank == 0) D = std::make_unique<Scratch>((size_t)std::max<i64>(m0 * n0, 1) * sizeof(T), s);
+    gather_root<T>(SA, D ? D->as<T>() : nullptr, s);
+    if (R.rank == 0 && k > 0) {
+        try {
+            const bool tr = m0 < n0;             // factor A^H = V S U^H when wide
+            const i64 m = tr ? n0 : m0, n = tr ? m0 : n0;
+            Scratch At((size_t)m * n * sizeof(T), s);
+            if (tr) slate_hip::gecopy<K<T>, K<T>>('G', ctrans<T>(), m, n, kp(D->as<T>()), m0, kp(At.as<T>()), m, s);
+            else copy2d(At.as<T>(), m, D->as<T>(), m0, m, n, s);
+            const bool wu = tr ? VH != nullptr : U != nullptr, wv = tr ? U != nullptr : VH != nullptr;
+            Scratch Zu((size_t)(wu ? m * n : 1) * sizeof(T), s), Zv((size_t)(wv ? n * n : 1) * sizeof(T), s);
+            svd_1gpu<T>(m, n, At.as<T>(), sv, Zu.as<T>(), Zv.as<T>(), wu, wv, s);
+            // outputs of op(A): not transposed U = Zu (m x k), VH = Zv^H;
+            // transposed U = Zv (k x k), VH = Zu^H (k x n0)
+            if (U) {
+                Du = std::make_unique<Scratch>((size_t)m0 * k * sizeof(T), s);
+                if (tr) copy2d(Du->as<T>(), m0, Zv.as<T>(), n, m0, k, s);
+                else copy2d(Du->as<T>(), m0, Zu.as<T>(), m, m0, k, s);
+            }
+            if (VH) {
+                Dv = std::make_unique<Scratch>((size_t)k * n0 * sizeof(T), s);
+                if (tr) slate_hip::gecopy<K<T>, K<T>>('G', ctrans<T>(), k, n0, kp(Zu.as<T>()), m, kp(Dv->as<T>()), k, s);
+                else slate_hip::gecopy<K<T>, K<T>>('G', ctrans<T>(), k, n0, kp(Zv.as<T>()), n, kp(Dv->as<T>()), k, s);
+            }
+            NHIP(hipStreamSynchronize(s));
+        } catch (const std::exception& e) {
+            err = 1;
+            msg = e.what();
+        }
+    }
+    if (R.size > 1) {
+        Scratch bb((size_t)(k + 1) * sizeof(double), s);
+        std::vector<double> h(sv);
+        h.push_back((double)err);
+        upload(bb.p, h.data(), h.size() * sizeof(double), s);
+        world_comm()->bcast(bb.p, h.size() * sizeof(double), 0, s);
+        h = download_vec<double>(bb.p, h.size(), s);
+        err = (int64_t)h.back();
+        h.pop_back();
+        sv = h;
+    }
+    if (err) throw Error(R.rank == 0 ? msg : std::string("native svd failed on rank 0"));
+    if (U) scatter_root<T>(Du ? Du->as<T>() : nullptr, *U->storage(), s);
+    if (VH) scatter_root<T>(Dv ? Dv->as<T>() : nullptr, *VH->storage(), s);
+    S.assign(sv.begin(), sv.end());
+    return 0;
+}
+
 }  // namespace
+
+template <typename T>
+int64_t svd(Matrix<T>& A, std::vector<real_t<T>>& S, Matrix<T>& U, Matrix<T>& VH, const Options&) {
+    return svd_impl<T>(A, S, &U, &VH);
+}
+template <typename T>
+int64_t svd(Matrix<T>& A, std::vector<real_t<T>>& S, const Options&) {
+    return svd_impl<T>(A, S, nullptr, nullptr);
+}
 
 template <typename T>
 int64_t heev(HermitianMatrix<T>& A, std::vector<real_t<T>>& Lambda, Matrix<T>& Z, const Options&) {
@@ -691,7 +960,9 @@ int64_t heev(HermitianMatrix<T>& A, std::vector<real_t<T>>& Lambda, const Option
 
 #define SLATE_NATIVE_EIG_INST(T)                                                                            \
     template int64_t heev<T>(HermitianMatrix<T>&, std::vector<real_t<T>>&, Matrix<T>&, const Options&);    \
-    template int64_t heev<T>(HermitianMatrix<T>&, std::vector<real_t<T>>&, const Options&);
+    template int64_t heev<T>(HermitianMatrix<T>&, std::vector<real_t<T>>&, const Options&);                \
+    template int64_t svd<T>(Matrix<T>&, std::vector<real_t<T>>&, Matrix<T>&, Matrix<T>&, const Options&);  \
+    template int64_t svd<T>(Matrix<T>&, std::vector<real_t<T>>&, const Options&);
 SLATE_NATIVE_EIG_INST(float)
 SLATE_NATIVE_EIG_INST(double)
 SLATE_NATIVE_EIG_INST(std::complex<float>)

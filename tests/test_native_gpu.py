@@ -51,7 +51,8 @@ def test_native_library_exports_lapack_scalapack_blacs():
                  f"p{x}lantr_", f"p{x}geadd_", f"p{x}laset_", f"p{x}lacpy_", f"p{x}gecon_", f"p{x}pocon_",
                  f"p{x}trcon_", f"slate_{x}gecon_", f"slate_{x}pocon_", f"slate_{x}trcon_"]
     want += ["pssyevd_", "pdsyevd_", "pcheevd_", "pzheevd_", "pssyev_", "pdsyev_", "pcheev_", "pzheev_",
-             "slate_dsyev", "slate_dsyevd", "slate_zheev", "slate_zheevd"]
+             "slate_dsyev", "slate_dsyevd", "slate_zheev", "slate_zheevd", "psgesvd_", "pdgesvd_", "pcgesvd_",
+             "pzgesvd_", "slate_dgesvd", "slate_zgesvd"]
     want += ["pclanhe_", "pzlanhe_", "pcherk_", "pzherk_", "pcher2k_", "pzher2k_", "pchemm_", "pzhemm_"]
     missing = [w for w in want if w not in names]
     assert not missing, missing
@@ -116,7 +117,8 @@ def _assert_checks(checks, out):
                                                    "syr2k_upper", "hemm_left", "symm_right", "trmm_luc",
                                                    "potri", "getri", "norm_herm_one", "norm_sym_one",
                                                    "norm_tri_fro", "heev", "heev_orth", "heev_values",
-                                                   "gecondest")]
+                                                   "gecondest", "svd", "svd_orth", "svd_wide", "svd_wide_orth",
+                                                   "svd_values")]
     for name in names:
         assert name in checks, (name, out)
         assert float(checks[name]) < TOL[name[-1]], (name, checks[name])
@@ -172,7 +174,7 @@ def test_native_scalapack_from_c_without_python(grid):
         outs = _run_ranks(CEXE, [grid], p * q)
     names = ("pdpotrs", "pdpotrs_upper", "pdgesv", "pdgetrs", "pdlange_fro", "pdgemm_tn", "pdsyrk_lower", "pdtrmm_lun", "pdpotri", "pdgetri", "pdlaset_lacpy_geadd",
              "pzgesv", "slate_dgetrf_", "pdgemm_sub", "pdpotrs_sub", "pdgetrs_sub", "pdtrsm_right", "pztrsm_trans",
-             "pdgecon", "pdpocon", "pdtrcon", "pdsyevd")
+             "pdgecon", "pdpocon", "pdtrcon", "pdsyevd", "pdgesvd")
     for rank, (rc, out) in enumerate(outs):
         print(out)
         assert rc == 0, out
