@@ -88,6 +88,9 @@ void pdgesvd_(const char* jobu, const char* jobvt, const int* m, const int* n, d
               const int* ja, const int* desca, double* s, double* u, const int* iu, const int* ju, const int* descu,
               double* vt, const int* ivt, const int* jvt, const int* descvt, double* work, const int* lwork,
               int* info);
+void pdgels_(const char* trans, const int* m, const int* n, const int* nrhs, double* a, const int* ia, const int* ja,
+             const int* desca, double* b, const int* ib, const int* jb, const int* descb, double* work,
+             const int* lwork, int* info);
 void slate_amd_finalize(void);
 
 static int g_rank;
@@ -302,6 +305,18 @@ int main(int argc, char** argv) {
     pdgetrf_(&n, &n, a, &one, &one, desca, ipiv, &info);
     pdgetrs_("N", &n, &nrhs, a, &one, &one, desca, ipiv, b, &one, &one, descb, &info);
     check(info ? "pdgetrs-FAILED" : "pdgetrs", ERR_B());
+
+    /* least squares through QR (TSQR panels when p > 1): a consistent square system */
+    {
+        int lw = -1;
+        double wq;
+        FILL_A(gen);
+        FILL_B(gen);
+        pdgels_("N", &n, &n, &nrhs, a, &one, &one, desca, b, &one, &one, descb, &wq, &lw, &info);
+        lw = 1;
+        pdgels_("N", &n, &n, &nrhs, a, &one, &one, desca, b, &one, &one, descb, &wq, &lw, &info);
+        check(info ? "pdgels-FAILED" : "pdgels", ERR_B());
+    }
 
     /* norm and gemm: C = A^T A (one column block checked) */
     FILL_A(gen);

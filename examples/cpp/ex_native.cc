@@ -250,6 +250,50 @@ void run(int p, int q, int me) {
         report("gels", std::sqrt(e / w));
     }
 
+    // ---- geqrf on the p x q grid (TSQR panels when p > 1): || Q R - A || / || A ||
+    // through unmqr(NoTrans) of [R; 0], tall and wide; then gels on the grid
+    for (int shape = 0; shape < 2; ++shape) {
+        const int64_t m5 = shape ? 100 : 330, n5 = shape ? 150 : 120;
+        sn::Matrix<T> G5(m5, n5, nb, p, q), C5(m5, n5, nb, p, q);
+        G5.generate(sn::Gen::Random, 31);
+        std::vector<T> g5((size_t)m5 * n5), f5((size_t)m5 * n5), qr5((size_t)m5 * n5);
+        G5.to_host(g5.data(), m5);
+        sn::QRFactors<T> F5;
+        sn::geqrf(G5, F5);
+        G5.to_host(f5.data(), m5);
+        for (int64_t j = 0; j < n5; ++j)
+            for (int64_t i = j + 1; i < m5; ++i) f5[i + j * m5] = T(0);
+        C5.from_host(f5.data(), m5);
+        sn::unmqr(sn::Op::NoTrans, G5, F5, C5);
+        C5.to_host(qr5.data(), m5);
+        auto want = widen(g5), got = widen(qr5);
+        for (size_t i = 0; i < got.size(); ++i) got[i] -= want[i];
+        report(shape ? "geqrf_wide" : "geqrf", rel<T>(got, want));
+    }
+    {
+        const int64_t m6 = 330, n6 = 120, r6 = 3;
+        sn::Matrix<T> G6(m6, n6, nb, p, q), X6(n6, r6, nb, p, q), B6(m6, r6, nb, p, q);
+        G6.generate(sn::Gen::Random, 41);
+        X6.generate(sn::Gen::Random, 42);
+        std::vector<T> g6((size_t)m6 * n6), x6((size_t)n6 * r6);
+        G6.to_host(g6.data(), m6);
+        X6.to_host(x6.data(), n6);
+        auto b6 = mul<T>('N', 'N', m6, r6, n6, g6, m6, x6, n6);
+        std::vector<T> bh((size_t)m6 * r6), xg6((size_t)m6 * r6);
+        for (size_t i = 0; i < bh.size(); ++i) bh[i] = val<T>(b6[i].real(), b6[i].imag());
+        B6.from_host(bh.data(), m6);
+        sn::gels(G6, B6);
+        B6.to_host(xg6.data(), m6);
+        double e = 0, w = 0;
+        for (int64_t c = 0; c < r6; ++c)
+            for (int64_t i = 0; i < n6; ++i) {
+                e += std::norm(std::complex<double>(std::real(xg6[i + c * m6]) - std::real(x6[i + c * n6]),
+                                                    std::imag(xg6[i + c * m6]) - std::imag(x6[i + c * n6])));
+                w += std::norm(std::complex<double>(std::real(x6[i + c * n6]), std::imag(x6[i + c * n6])));
+            }
+        report("gels_grid", std::sqrt(e / w));
+    }
+
     // ---- trsm: L^H X = alpha B with the Cholesky factor
     {
         sn::Matrix<T> Bt(n, nrhs, nb, p, q);

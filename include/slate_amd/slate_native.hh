@@ -192,9 +192,11 @@ template <typename T>
 void trmm(Side side, Uplo uplo, Op op, Diag diag, T alpha, const Matrix<T>& A, Matrix<T>& B,
           const Options& opts = {});
 
-// Householder QR on 1 x q grids (one process row: every rank holds whole
-// columns): A = Q R, R in the upper triangle, the reflectors below it;
-// F keeps the per-panel compact-WY factors T (device).  unmqr applies
+// Householder QR on any p x q grid: A = Q R, R in the upper triangle, the
+// reflectors below it; F keeps the per-panel compact-WY factors T (device).
+// With p > 1 process rows each panel is a TSQR -- every rank of the panel's
+// process column factors its own rows, the stacked R factors are reduced by
+// one more QR, and F also keeps that tree's reflectors.  unmqr applies
 // op(Q) (NoTrans or ConjTrans; real types: Trans == ConjTrans) from the
 // left; gels solves min ||A X - B|| for m >= n (X in the top n rows of BX).
 // inverses from the factors: potri after potrf (stored triangle), getri after getrf

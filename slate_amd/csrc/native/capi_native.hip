@@ -10,7 +10,7 @@
 //     distributed over all ranks (1 x WORLD_SIZE, or SLATE_AMD_NATIVE_GRID=PxQ)
 //     and the result is gathered back to every rank.
 //   * ScaLAPACK (reference scalapack_api/scalapack_*.cc):
-//     p{s,d,c,z}{potrf,posv,getrf,gesv,potrs,getrs,gemm,trsm,gels,lange}_ (gels: 1 x q grids)
+//     p{s,d,c,z}{potrf,posv,getrf,gesv,potrs,getrs,gemm,trsm,gels,lange}_
 //     on the caller's LOCAL block-cyclic arrays (9-int descriptors), with a
 //     minimal BLACS (Cblacs_* / blacs_*_, numroc_, descinit_) over the native
 //     runtime's ranks.  Operands are any sub-matrix A(ia:ia+m-1, ja:ja+n-1)
@@ -861,8 +861,10 @@ void p_trsm(char side, char uplo, char ta, char diag, int m, int n, T alpha, con
     if (rc != 0) std::fprintf(stderr, "slate_amd native p?trsm_: %s\n", g_err.c_str());
 }
 
-// p?gels_ on a 1 x q grid (geqrf distributes whole columns); lwork = -1
-// is a workspace query (the library allocates its own: returns 1)
+// p?gels_ on any BLACS grid (p > 1: TSQR panels -- R in A's upper triangle
+// as ScaLAPACK's, the entries below it hold the TSQR tree's local reflectors,
+// not ScaLAPACK's Householder vectors); lwork = -1 is a workspace query (the
+// library allocates its own: returns 1)
 template <typename T>
 int p_gels(char trans, int m, int n, int nrhs, T* a, int ia, int ja, const int* desca, T* b, int ib, int jb,
            const int* descb, T* work, int lwork) {
@@ -876,7 +878,6 @@ int p_gels(char trans, int m, int n, int nrhs, T* a, int ia, int ja, const int* 
     return (int)guarded([&]() -> int64_t {
         sn::Matrix<T> A = scal_matrix<T>(desca, m, n, ia, ja, a);
         sn::Matrix<T> B = scal_matrix<T>(descb, m, nrhs, ib, jb, b);
-        if (A.p() != 1) throw sn::Error("native p?gels_: a 1 x q BLACS grid (one process row)");
         sn::gels(A, B);
         scal_back(A, desca, a);
         scal_back(B, descb, b);

@@ -237,6 +237,9 @@ GridComms* grid_comms(int p, int q) {
     if (R.size > 1) {
         g->row = world_comm()->split(g->pr, g->pc);
         g->col = world_comm()->split(g->pc, g->pr);
+        // the update stream's twin of `col` (an RCCL communicator is driven
+        // from one stream: the TSQR trailing all-reduces run beside the panel's)
+        if (p > 1) g->colu = world_comm()->split(g->pc, g->pr);
     }
     GridComms* out = g.get();
     R.grids[key] = std::move(g);
@@ -1877,6 +1880,10 @@ double norm(Norm kind, const Matrix<T>& A) {
 struct QRData {
     std::vector<i64> r0, kb;
     std::vector<std::shared_ptr<Scratch>> T;     // kb x kb upper factor per panel
+    // p > 1 (TSQR): this rank's local reflector count km <= kb per panel (T is
+    // km x km) and the tree over the stacked R factors, ks reflectors (0: no
+    // tree) -- fac = [T km x km | tau km | Vh km x ks | Th ks x ks | tauh ks]
+    std::vector<i64> km, ks;
 };
 
 template <typename T>
@@ -1891,10 +1898,159 @@ static void apply_panel(const T* V, i64 ldv, const T* Vh, const T* Tm, i64 kb, T
     gemm_k<T>('N', 'N', m, n, kb, T(-1), V, ldv, W.as<T>(), kb, T(1), C, ldc, s);
 }
 
+// C = Q_k^H C (conj) or Q_k C for this rank's rows >= tile k of one column
+// range: Q_k = diag(Q_r) Q^ -- the local block reflector (V, Tk: km
+// columns), then the tree on the top km rows (Vt km x ks, Th ks x ks) whose
+// V^H C is one all-reduce over the process column `col`
+template <typename T>
+static void tsqr_apply(const T* V, i64 ldv, const T* Vhx, const T* Tk, i64 km, const T* Vt, const T* Th, i64 ks,
+                       T* C, i64 ldc, i64 mr, i64 nc, bool conj, Comm* col, hipStream_t s) {
+    if (nc <= 0) return;
+    if (conj && km && mr) apply_panel<T>(V, ldv, Vhx, Tk, km, C, ldc, mr, nc, true, s);
+    if (ks) {
+        Scratch W((size_t)ks * nc * sizeof(T), s);
+        if (km) gemm_k<T>(ctrans<T>(), 'N', ks, nc, km, T(1), Vt, km, C, ldc, T(0), W.as<T>(), ks, s);
+        else slate_hip::geset<K<T>>('G', ks, nc, kv(T(0)), kv(T(0)), kp(W.as<T>()), ks, s);
+        col->allreduce(W.p, (size_t)ks * nc, dt_of<T>::v, 's', s);
+        slate_hip::trmm<K<T>>('L', 'U', conj ? ctrans<T>() : 'N', 'N', ks, nc, kv(T(1)), kp(Th), ks,
+                              kp(W.as<T>()), ks, s);
+        if (km) gemm_k<T>('N', 'N', km, nc, ks, T(-1), Vt, km, W.as<T>(), ks, T(1), C, ldc, s);
+    }
+    if (!conj && km && mr) apply_panel<T>(V, ldv, nullptr, Tk, km, C, ldc, mr, nc, false, s);
+}
+
+// p > 1 process rows: models/qr.py _geqrf_general in C++ -- the panel's
+// process column runs a TSQR (local QR of each rank's panel rows, all-gather
+// of the R factors, redundant QR of the stack; R^ lands over R of the rank
+// owning tile k), the factors travel along the process row, every rank
+// applies diag(Q_r) then the tree.  Reference: src/geqrf.cc:137-295 with
+// internal_ttqrt.cc (its tree of triangle-triangle reductions).
+template <typename T>
+static int64_t geqrf_tsqr(Storage& S, QRFactors<T>& F, const Options& opts) {
+    Runtime& R = rt();
+    GridComms* gc = S.gc;
+    const int p = S.p, q = S.q, pr = S.pr, pc = S.pc;
+    const i64 nb = S.nb, m = S.m, n = S.n, lld = S.lld, mloc = S.mloc, nloc = S.nloc;
+    const i64 kt = std::min((m + nb - 1) / nb, (n + nb - 1) / nb);
+    const int la = std::max(0, opts.lookahead);
+    const char ct = ctrans<T>();
+    T* buf = static_cast<T*>(S.buf);
+    hipStream_t ps = R.panel, us = R.update;
+    Comm* colc = gc->col.get();
+    Comm* colu = gc->colu.get();
+    std::vector<i64> nloc_r(p);
+    for (int r = 0; r < p; ++r) nloc_r[r] = numroc(m, nb, r, p);
+    F.d = std::make_shared<QRData>();
+    join(R.main, ps);
+    join(R.main, us);
+    const int NR = la + 3;
+    std::vector<std::unique_ptr<Scratch>> ringV, ringH;
+    for (int r = 0; r < NR; ++r) {
+        ringV.push_back(std::make_unique<Scratch>((size_t)std::max<i64>(mloc, 1) * nb * sizeof(T), ps));
+        ringH.push_back(std::make_unique<Scratch>((size_t)std::max<i64>(mloc, 1) * nb * sizeof(T), ps));
+    }
+    std::vector<std::unique_ptr<Event>> ev_tr((size_t)kt), ev_used((size_t)kt);
+    for (i64 k = 0; k < kt; ++k) {
+        const i64 r0 = k * nb;
+        const i64 kb = std::min({nb, n - r0, m - r0});
+        const int rk = (int)(k % p), ck = (int)(k % q);
+        const i64 lr_k = std::min(tiles_before(k, p, pr) * nb, mloc);
+        const i64 lc_k = std::min(tiles_before(k, q, pc) * nb, nloc);
+        const i64 lc1 = std::min(tiles_before(k + 1, q, pc) * nb, nloc);
+        const i64 lcla = std::min(tiles_before(k + 1 + la, q, pc) * nb, nloc);
+        const i64 lcnx = std::max(std::min(tiles_before(k + 2 + la, q, pc) * nb, nloc), lcla);
+        std::vector<i64> kr(p), soff(p);
+        int holders = 0;
+        for (int r = 0; r < p; ++r) {
+            const i64 cnt = nloc_r[r] - std::min(tiles_before(k, p, r) * nb, nloc_r[r]);
+            kr[r] = std::min(cnt, kb);
+            holders += kr[r] > 0;
+        }
+        i64 tot = 0;
+        for (int i = 0; i < p; ++i) {        // rk first: its top rows receive R^
+            const int r = (rk + i) % p;
+            soff[r] = tot;
+            tot += kr[r];
+        }
+        const i64 ks = holders > 1 ? std::min(tot, kb) : 0;
+        const i64 nmine = mloc - lr_k, km = kr[pr];
+        if (k - la - 1 >= 0) ev_tr[k - la - 1]->wait(ps);
+        if (k >= NR) ev_used[k - NR]->wait(ps);
+        const size_t oT = 0, oTau = oT + km * km, oVt = oTau + km, oTh = oVt + km * ks, oTauh = oTh + ks * ks,
+                     nfac = oTauh + ks;
+        auto fac = std::make_shared<Scratch>(std::max<size_t>(nfac, 1) * sizeof(T), ps);
+        T* f = fac->as<T>();
+        T* V = ringV[k % NR]->as<T>();
+        T* mine = buf + lr_k + lc_k * lld;
+        if (pc == ck) {
+            if (nmine)
+                slate_hip::geqrf_panel_ws<K<T>>(nmine, kb, kp(mine), lld, kp(f + oTau), kp(f + oT), km, kp(V), nmine,
+                                                R.qr_work, ps);
+            if (ks) {
+                Scratch Rb((size_t)kb * kb * sizeof(T), ps), allR((size_t)p * kb * kb * sizeof(T), ps);
+                Scratch St((size_t)tot * kb * sizeof(T), ps), Vf((size_t)tot * ks * sizeof(T), ps);
+                slate_hip::geset<K<T>>('G', kb, kb, kv(T(0)), kv(T(0)), kp(Rb.as<T>()), kb, ps);
+                if (km) slate_hip::gecopy<K<T>, K<T>>('U', 'N', km, kb, kp(mine), lld, kp(Rb.as<T>()), kb, ps);
+                colc->allgather(Rb.p, allR.p, (size_t)kb * kb * sizeof(T), ps);
+                for (int r = 0; r < p; ++r)
+                    if (kr[r])
+                        slate_hip::gecopy<K<T>, K<T>>('G', 'N', kr[r], kb, kp(allR.as<T>() + (size_t)r * kb * kb), kb,
+                                                      kp(St.as<T>() + soff[r]), tot, ps);
+                slate_hip::geqrf_panel_ws<K<T>>(tot, kb, kp(St.as<T>()), tot, kp(f + oTauh), kp(f + oTh), ks,
+                                                kp(Vf.as<T>()), tot, R.qr_work, ps);
+                if (km)
+                    slate_hip::gecopy<K<T>, K<T>>('G', 'N', km, ks, kp(Vf.as<T>() + soff[pr]), tot, kp(f + oVt), km,
+                                                  ps);
+                // R^ over R_rk; the local reflectors below the diagonal stay
+                if (pr == rk) slate_hip::gecopy<K<T>, K<T>>('U', 'N', ks, kb, kp(St.as<T>()), tot, kp(mine), lld, ps);
+            }
+        }
+        if (q > 1) {
+            gc->row->bcast(f, nfac * sizeof(T), ck, ps);
+            if (nmine && km) gc->row->bcast(V, (size_t)nmine * km * sizeof(T), ck, ps);
+        }
+        const T* Vhx = nullptr;
+        if (nmine >= 4096 && km && nloc > lc1) {
+            T* H = ringH[k % NR]->as<T>();
+            slate_hip::gecopy<K<T>, K<T>>('G', ct, km, nmine, kp(V), nmine, kp(H), km, ps);
+            Vhx = H;
+        }
+        auto upd = [&](i64 c0, i64 c1, Comm* cm, hipStream_t s) {
+            tsqr_apply<T>(V, nmine, Vhx, f + oT, km, f + oVt, f + oTh, ks, buf + lr_k + c0 * lld, lld, nmine, c1 - c0,
+                          true, cm, s);
+        };
+        if (k >= 1 && la > 0) ev_tr[k - 1]->wait(ps);
+        // (wide matrix, last panel: the tile's columns beyond kb are trailing too)
+        if (pc == ck && lc_k + kb < lc1) upd(lc_k + kb, lc1, colc, ps);
+        upd(lc1, lcla, colc, ps);
+        Event ev_panel;
+        ev_panel.record(ps);
+        ev_panel.wait(us);
+        upd(lcla, lcnx, colu, us);
+        ev_tr[k] = std::make_unique<Event>();
+        ev_tr[k]->record(us);
+        upd(lcnx, nloc, colu, us);
+        ev_used[k] = std::make_unique<Event>();
+        ev_used[k]->record(us);
+        fac->s = us;
+        F.d->r0.push_back(r0);
+        F.d->kb.push_back(kb);
+        F.d->km.push_back(km);
+        F.d->ks.push_back(ks);
+        F.d->T.push_back(fac);
+    }
+    join(ps, R.main);
+    join(us, R.main);
+    for (auto* v : {&ringV, &ringH})
+        for (auto& x : *v) x->s = R.main;
+    NHIP(hipStreamSynchronize(R.main));
+    return 0;
+}
+
 template <typename T>
 int64_t geqrf(Matrix<T>& A, QRFactors<T>& F, const Options& opts) {
     Storage& S = *A.storage();
-    if (S.p != 1) throw Error("native geqrf: one process row (p = 1) -- 1 x q grids");
+    if (S.p != 1) return geqrf_tsqr<T>(S, F, opts);
     Runtime& R = rt();
     GridComms* gc = S.gc;
     const int q = S.q, pc = S.pc;
@@ -1958,6 +2114,8 @@ int64_t geqrf(Matrix<T>& A, QRFactors<T>& F, const Options& opts) {
         tau.s = us;
         F.d->r0.push_back(r0);
         F.d->kb.push_back(kb);
+        F.d->km.push_back(kb);
+        F.d->ks.push_back(0);
         F.d->T.push_back(Tk);
     }
     join(ps, R.main);
@@ -1975,13 +2133,13 @@ void unmqr(Op op, const Matrix<T>& A, const QRFactors<T>& F, Matrix<T>& C, const
     const Storage& SA = *A.storage();
     Storage& SC = *C.storage();
     if (!F.d) throw Error("native unmqr: factor with geqrf first");
-    if (SA.p != 1 || SC.p != 1 || SA.q != SC.q || SA.nb != SC.nb || SA.m != SC.m)
-        throw Error("native unmqr: A and C on the same 1 x q grid with m rows");
+    if (SA.p != SC.p || SA.q != SC.q || SA.nb != SC.nb || SA.m != SC.m)
+        throw Error("native unmqr: A and C on the same grid with m rows");
     if (op == Op::Trans && is_cplx<T>()) throw Error("native unmqr: Trans of a complex Q (use ConjTrans)");
     Runtime& R = rt();
     hipStream_t s = R.main;
-    const int q = SA.q, pc = SA.pc;
-    const i64 nb = SA.nb, m = SA.m;
+    const int p = SA.p, q = SA.q, pr = SA.pr, pc = SA.pc;
+    const i64 nb = SA.nb;
     const T* Abuf = static_cast<const T*>(SA.buf);
     T* Cbuf = static_cast<T*>(SC.buf);
     const i64 np = (i64)F.d->T.size();
@@ -1989,12 +2147,18 @@ void unmqr(Op op, const Matrix<T>& A, const QRFactors<T>& F, Matrix<T>& C, const
     NHIP(hipStreamSynchronize(s));
     for (i64 i = 0; i < np; ++i) {
         const i64 k = conjT ? i : np - 1 - i;
-        const i64 r0 = F.d->r0[k], kb = F.d->kb[k], mk = m - r0;
+        const i64 km = F.d->km[k], ks = F.d->ks[k];
+        const i64 lr_k = std::min(tiles_before(k, p, pr) * nb, SA.mloc), mr = SA.mloc - lr_k;
         const i64 lck = tiles_before(k, q, pc) * nb;
-        Scratch V((size_t)mk * kb * sizeof(T), s);
-        if ((k % q) == pc) slate_hip::v_explicit<K<T>>(mk, kb, kp(Abuf + r0 + lck * SA.lld), SA.lld, kp(V.as<T>()), mk, s);
-        if (q > 1) SA.gc->row->bcast(V.p, (size_t)mk * kb * sizeof(T), (int)(k % q), s);
-        apply_panel<T>(V.as<T>(), mk, nullptr, static_cast<const T*>(F.d->T[k]->p), kb, Cbuf + r0, SC.lld, mk, SC.nloc, conjT, s);
+        // the local reflectors (unit lower trapezoidal; on the rank owning
+        // tile k R^ sits over them, which v_explicit never reads)
+        Scratch V((size_t)std::max<i64>(mr * km, 1) * sizeof(T), s);
+        if ((k % q) == pc && mr && km)
+            slate_hip::v_explicit<K<T>>(mr, km, kp(Abuf + lr_k + lck * SA.lld), SA.lld, kp(V.as<T>()), mr, s);
+        if (q > 1 && mr && km) SA.gc->row->bcast(V.p, (size_t)mr * km * sizeof(T), (int)(k % q), s);
+        const T* f = static_cast<const T*>(F.d->T[k]->p);
+        tsqr_apply<T>(V.as<T>(), mr, nullptr, f, km, f + km * km + km, f + km * km + km + km * ks, ks,
+                      Cbuf + lr_k, SC.lld, mr, SC.nloc, conjT, SA.gc ? SA.gc->col.get() : nullptr, s);
     }
     NHIP(hipStreamSynchronize(s));
 }

@@ -111,6 +111,7 @@ struct GridComms {
     int p = 1, q = 1, pr = 0, pc = 0;
     std::unique_ptr<Comm> row;     // same process row, ranked by pc
     std::unique_ptr<Comm> col;     // same process column, ranked by pr
+    std::unique_ptr<Comm> colu;    // a second `col` for the update stream (p > 1)
     std::unique_ptr<PeerBox> colpeer;   // mailboxes of the column (distributed LU panel)
 };
 

@@ -117,7 +117,7 @@ def _assert_checks(checks, out):
                                                    "syr2k_upper", "hemm_left", "symm_right", "trmm_luc",
                                                    "potri", "getri", "norm_herm_one", "norm_sym_one",
                                                    "norm_tri_fro", "heev", "heev_orth", "heev_values",
-                                                   "gecondest", "svd", "svd_orth", "svd_wide", "svd_wide_orth",
+                                                   "gecondest", "svd", "svd_orth", "svd_wide", "svd_wide_orth", "geqrf", "geqrf_wide", "gels_grid",
                                                    "svd_values")]
     for name in names:
         assert name in checks, (name, out)
@@ -174,7 +174,7 @@ def test_native_scalapack_from_c_without_python(grid):
         outs = _run_ranks(CEXE, [grid], p * q)
     names = ("pdpotrs", "pdpotrs_upper", "pdgesv", "pdgetrs", "pdlange_fro", "pdgemm_tn", "pdsyrk_lower", "pdtrmm_lun", "pdpotri", "pdgetri", "pdlaset_lacpy_geadd",
              "pzgesv", "slate_dgetrf_", "pdgemm_sub", "pdpotrs_sub", "pdgetrs_sub", "pdtrsm_right", "pztrsm_trans",
-             "pdgecon", "pdpocon", "pdtrcon", "pdsyevd", "pdgesvd")
+             "pdgecon", "pdpocon", "pdtrcon", "pdsyevd", "pdgesvd", "pdgels")
     for rank, (rc, out) in enumerate(outs):
         print(out)
         assert rc == 0, out
