@@ -3,6 +3,7 @@
 #pragma once
 #include <cstdlib>
 #include "gemm.hpp"
+#include "gemm_glds.hpp"
 #include "launchers.hpp"
 #include "workspace.hpp"
 
@@ -125,6 +126,35 @@ static i64 tri_blocks(const GemmArgs<T>& a, int BM, int BN) {
     return sup * 64;
 }
 
+// fp64 with K % 16 == 0 and 16-byte aligned operands: the LDS-DMA staged
+// kernel (gemm_glds.hpp), 128 x 128 x 16, 2 x 4 waves, two LDS stages, two
+// workgroups per CU.  Measured on MI355X against the register-staged kernel
+// (tools/exp/dgemm_glds_r5.hip, profiles/r5/dgemm_glds.txt): 31744^2 x 512
+// NT 61.1 -> 67.1 TF/s, x 1024 NT 63.8 -> 69.7, NN x 512 62.6 -> 65.8,
+// 16384^2 x 4096 NN 68.9 -> 70.6, NT 65.3 -> 71.3; bit-identical results.
+// SLATE_AMD_GEMM_GLDS=0 selects the register-staged kernel.
+static inline bool gemm_glds_enabled() {
+    static const bool v = [] {
+        const char* e = std::getenv("SLATE_AMD_GEMM_GLDS");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
+template <bool TA, bool TB>
+static void launch_glds(const GemmArgs<double>& a, i64 nblk, int batch, hipStream_t s) {
+    constexpr int BM = 128, BN = 128, WVM = 2, WVN = 4, S = 2, OCC = 2;
+    auto K = gemm_f64_glds_kernel<TA, TB, BM, BN, WVM, WVN, S, OCC>;
+    constexpr size_t lds = glds_lds_bytes<BM, BN, TA, TB, S>();
+    static const bool attr = [&] {
+        return hipFuncSetAttribute((const void*)K, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) ==
+               hipSuccess;
+    }();
+    (void)attr;
+    hipLaunchKernelGGL(K, dim3((unsigned)nblk, (unsigned)batch), dim3(64 * WVM * WVN), lds, s, a);
+    HIP_LAUNCH_CHECK();
+}
+
 template <typename T, bool TA, bool TB, bool PTRS>
 static void launch_real(const GemmArgs<T>& a0, int batch, hipStream_t s) {
     GemmArgs<T> a = a0;
@@ -151,6 +181,12 @@ static void launch_real(const GemmArgs<T>& a0, int batch, hipStream_t s) {
     if (gm == 0 || gn == 0 || batch == 0) return;
     i64 nblk = gm * gn;
     if (i64 t = tri_blocks(a, BM, BN)) { a.remap = 2; nblk = t; }
+    if constexpr (sizeof(T) == 8 && !PTRS) {
+        if (a.k > 0 && a.k % 16 == 0 && a.vecA && a.vecB && gemm_glds_enabled()) {
+            launch_glds<TA, TB>(a, nblk, batch, s);
+            return;
+        }
+    }
     // Two register stages for fp64 NN (tools/exp/gemm_pf_r5.hip on MI355X:
     // 31744^2 x 512 59.2 -> 62.9 TF/s, 16384^2 x 4096 63.5 -> 68.4 TF/s); the
     // NT form loses with it (61.3 -> 56.3 TF/s), so it keeps one.
