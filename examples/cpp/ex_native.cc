@@ -311,6 +311,28 @@ void run(int p, int q, int me) {
         }
         report("trsm_lc", rel<T>(lx, want));
     }
+    // ---- trsm on the stored triangle: L^T X = alpha B (left), X op(L) = alpha C (right)
+    for (int v = 0; v < 3; ++v) {
+        const bool right = v > 0;
+        const int64_t rm = right ? 7 : n, rn = right ? n : nrhs;
+        sn::Matrix<T> Bt(rm, rn, nb, p, q);
+        Bt.generate(sn::Gen::Random, 61 + v);
+        std::vector<T> hb((size_t)rm * rn), xt((size_t)rm * rn);
+        Bt.to_host(hb.data(), rm);
+        const T alpha = val<T>(0.75, 0.5);
+        const sn::Op op = v == 0 ? sn::Op::Trans : v == 1 ? sn::Op::NoTrans : sn::Op::ConjTrans;
+        sn::trsm(right ? sn::Side::Right : sn::Side::Left, sn::Uplo::Lower, op, sn::Diag::NonUnit, alpha, A, Bt);
+        Bt.to_host(xt.data(), rm);
+        const char oc = v == 0 ? 'T' : v == 1 ? 'N' : 'C';
+        auto lx = right ? mul<T>('N', oc, rm, rn, n, xt, rm, l, n) : mul<T>(oc, 'N', rm, rn, n, l, n, xt, rm);
+        std::vector<std::complex<double>> want(lx.size());
+        const std::complex<double> al(std::real(alpha), std::imag(alpha));
+        for (size_t i = 0; i < lx.size(); ++i) {
+            want[i] = al * std::complex<double>(std::real(hb[i]), std::imag(hb[i]));
+            lx[i] -= want[i];
+        }
+        report(v == 0 ? "trsm_lt" : v == 1 ? "trsm_rn" : "trsm_rc", rel<T>(lx, want));
+    }
 
     using R = sn::real_t<T>;
     auto cd = [](T x) { return std::complex<double>(std::real(x), std::imag(x)); };

@@ -143,7 +143,8 @@ static inline bool gemm_glds_enabled() {
 
 template <bool TA, bool TB>
 static void launch_glds(const GemmArgs<double>& a, i64 nblk, int batch, hipStream_t s) {
-    constexpr int BM = 128, BN = 128, WVM = 2, WVN = 4, S = 2, OCC = 2;
+    // NN: 4 x 2 waves (+0.7 % at 16384^2 x 4096 / 31744^2 x 512), else 2 x 4
+    constexpr int BM = 128, BN = 128, WVM = (!TA && !TB) ? 4 : 2, WVN = 8 / WVM, S = 2, OCC = 2;
     auto K = gemm_f64_glds_kernel<TA, TB, BM, BN, WVM, WVN, S, OCC>;
     constexpr size_t lds = glds_lds_bytes<BM, BN, TA, TB, S>();
     static const bool attr = [&] {

@@ -827,23 +827,95 @@ static void trsm_left(char uplo, char diag, T alpha, const Storage& SA, Storage&
     NHIP(hipStreamSynchronize(s));
 }
 
+// B = op(A)^{-1} B with op(A) = A^T (tr 'T') or A^H (tr 'C'), on the stored
+// triangle -- no transposed copy of A.  Column-oriented ("left-looking")
+// substitution: op(A)'s row k is A's column k, so per step k (backward for
+// Lower, forward for Upper)
+//   column k of A beyond the diagonal -> every process column (row comm);
+//   W = A(beyond, k)^op B(beyond) locally (the rows beyond k already hold
+//   their final X), summed over the process column (one nb x nrhs
+//   all-reduce); process row k%p: B_k -= W, B_k = op(A_kk)^{-1} B_k.
+// Per step O(local rows x nb) extra memory.  Reference: the transposed view
+// of src/work/work_trsm.cc:102-265 (its tileBcast then fetches A(k, i)).
 template <typename T>
-void trsm(Side side, Uplo uplo, Op op, Diag diag, T alpha, const Matrix<T>& A, Matrix<T>& B, const Options&) {
-    if (side != Side::Left) throw Error("native trsm: Side::Left");
+static void trsm_left_t(char uplo, char diag, char tr, T alpha, const Storage& SA, Storage& SB) {
+    Runtime& R = rt();
+    GridComms* gc = SB.gc;
+    const int p = SB.p, q = SB.q, pr = SB.pr, pc = SB.pc;
+    const i64 nb = SA.nb, n = SA.n, nrhs_loc = SB.nloc;
+    const T* A = static_cast<const T*>(SA.buf);
+    T* B = static_cast<T*>(SB.buf);
+    const i64 lda = SA.lld, ldb = SB.lld;
+    const i64 nt = (n + nb - 1) / nb;
+    hipStream_t s = R.main;
+    if (alpha != T(1) && SB.mloc && nrhs_loc) slate_hip::gescale<K<T>>('G', SB.mloc, nrhs_loc, kv(alpha), kp(B), ldb, s);
+    const bool lower = uplo == 'L';
+    const i64 mloc_n = std::min(SA.mloc, numroc(n, nb, pr, p));
+    for (i64 st = 0; st < nt; ++st) {
+        const i64 k = lower ? nt - 1 - st : st;
+        const i64 kb = std::min(nb, n - k * nb);
+        const int rk = (int)(k % p), ck = (int)(k % q);
+        const i64 lrk = tiles_before(k, p, pr) * nb, lck = tiles_before(k, q, pc) * nb;
+        // this process row's rows of op(A)'s row k beyond the diagonal
+        const i64 r0 = lower ? std::min(tiles_before(k + 1, p, pr) * nb, mloc_n) : 0;
+        const i64 r1 = lower ? mloc_n : std::min(tiles_before(k, p, pr) * nb, mloc_n);
+        const i64 nr = std::max<i64>(r1 - r0, 0);
+        Scratch W((size_t)kb * std::max<i64>(nrhs_loc, 1) * sizeof(T), s);
+        if (p > 1 || nr > 0) {
+            Scratch Pn((size_t)std::max<i64>(nr, 1) * kb * sizeof(T), s);
+            if (nr > 0) {
+                if (pc == ck) copy2d(Pn.as<T>(), nr, A + r0 + lck * lda, lda, nr, kb, s);
+                if (q > 1) gc->row->bcast(Pn.p, (size_t)nr * kb * sizeof(T), ck, s);
+            }
+            if (nrhs_loc) {
+                if (nr > 0)
+                    gemm_k<T>(tr, 'N', kb, nrhs_loc, nr, T(1), Pn.as<T>(), nr, B + r0, ldb, T(0), W.as<T>(), kb, s);
+                else
+                    slate_hip::geset<K<T>>('G', kb, nrhs_loc, kv(T(0)), kv(T(0)), kp(W.as<T>()), kb, s);
+                if (p > 1) gc->col->allreduce(W.p, (size_t)kb * nrhs_loc, dt_of<T>::v, 's', s);
+            }
+        }
+        if (pr == rk) {
+            Scratch D((size_t)kb * kb * sizeof(T), s);
+            if (pc == ck) copy2d(D.as<T>(), kb, A + lrk + lck * lda, lda, kb, kb, s);
+            if (q > 1) gc->row->bcast(D.p, (size_t)kb * kb * sizeof(T), ck, s);
+            if (nrhs_loc) {
+                if (p > 1 || nr > 0)
+                    slate_hip::geadd<K<T>>('G', kb, nrhs_loc, kv(T(-1)), kp(W.as<T>()), kb, kv(T(1)), kp(B + lrk), ldb,
+                                           s);
+                slate_hip::trsm<K<T>>('L', uplo, tr, diag, kb, nrhs_loc, kv(T(1)), kp(D.as<T>()), kb, kp(B + lrk),
+                                      ldb, s);
+            }
+        }
+    }
+    NHIP(hipStreamSynchronize(s));
+}
+
+template <typename T>
+void trsm(Side side, Uplo uplo, Op op, Diag diag, T alpha, const Matrix<T>& A, Matrix<T>& B, const Options& opts) {
     const Storage& SA = *A.storage();
     Storage& SB = *B.storage();
-    if (SA.m != SA.n || SA.n != SB.m) throw Error("native trsm: dimension mismatch");
+    const bool left = side == Side::Left;
+    if (SA.m != SA.n || SA.n != (left ? SB.m : SB.n)) throw Error("native trsm: dimension mismatch");
     if (SA.nb != SB.nb || SA.p != SB.p || SA.q != SB.q) throw Error("native trsm: A and B must share grid and nb");
     NHIP(hipStreamSynchronize(rt().main));
+    if (!left) {
+        // X op(A) = alpha B  <=>  op(A)^T X^T = alpha B^T  (N, T), A X^H = conj(alpha) B^H (C):
+        // a left solve on the transposed right-hand side
+        const bool ch = op == Op::ConjTrans && is_cplx<T>();
+        const Op bt = ch ? Op::ConjTrans : Op::Trans;
+        Matrix<T> Y(SB.n, SB.m, SB.nb, SB.p, SB.q);
+        copy<T>(bt, B, Y);
+        const Op lop = op == Op::NoTrans ? Op::Trans : Op::NoTrans;
+        trsm<T>(Side::Left, uplo, lop, diag, ch ? conj_of(alpha) : alpha, A, Y, opts);
+        copy<T>(bt, Y, B);
+        return;
+    }
     if (op == Op::NoTrans) {
         trsm_left<T>((char)uplo, (char)diag, alpha, SA, SB);
         return;
     }
-    if (op == Op::Trans && is_cplx<T>()) throw Error("native trsm: Trans of a complex matrix (use ConjTrans)");
-    // op(A) = A^H: materialise it (the other triangle) and solve NoTrans
-    Matrix<T> At(SA.n, SA.n, SA.nb, SA.p, SA.q);
-    transpose_tiles<T>(SA, *At.storage(), ctrans<T>());
-    trsm_left<T>(uplo == Uplo::Lower ? 'U' : 'L', (char)diag, alpha, *At.storage(), SB);
+    trsm_left_t<T>((char)uplo, (char)diag, (op == Op::ConjTrans && is_cplx<T>()) ? 'C' : 'T', alpha, SA, SB);
 }
 
 template <typename T>
