@@ -141,10 +141,14 @@ static inline bool gemm_glds_enabled() {
     return v;
 }
 
-template <bool TA, bool TB>
+// BM = 128: 128 x 128 tiles, NN on 4 x 2 waves (+0.7 % at 16384^2 x 4096 /
+// 31744^2 x 512), else 2 x 4; BM = 64: 64 x 64 tiles on 2 x 2 waves, four
+// workgroups per CU -- for outputs of fewer than 512 128 x 128 tiles
+// (1024^2 x 1024: 15 -> 45 TF/s, 2048^2: 59 -> 64; profiles/r5/dgemm_glds_small.txt)
+template <bool TA, bool TB, int BM>
 static void launch_glds(const GemmArgs<double>& a, i64 nblk, int batch, hipStream_t s) {
-    // NN: 4 x 2 waves (+0.7 % at 16384^2 x 4096 / 31744^2 x 512), else 2 x 4
-    constexpr int BM = 128, BN = 128, WVM = (!TA && !TB) ? 4 : 2, WVN = 8 / WVM, S = 2, OCC = 2;
+    constexpr int BN = BM, WVM = BM == 64 ? 2 : (!TA && !TB) ? 4 : 2, WVN = BM == 64 ? 2 : 8 / WVM, S = 2,
+                  OCC = BM == 64 ? 4 : 2;
     auto K = gemm_f64_glds_kernel<TA, TB, BM, BN, WVM, WVN, S, OCC>;
     constexpr size_t lds = glds_lds_bytes<BM, BN, TA, TB, S>();
     static const bool attr = [&] {
@@ -161,7 +165,13 @@ static void launch_real(const GemmArgs<T>& a0, int batch, hipStream_t s) {
     GemmArgs<T> a = a0;
     if constexpr (sizeof(T) == 8) {
         const i64 g128 = ((a.m + 127) / 128) * ((a.n + 127) / 128) * batch;
-        if (g128 < gemm_small_tiles()) {
+        if (!PTRS && g128 < 512 && a.k > 0 && a.k % 16 == 0 && a.vecA && a.vecB && gemm_glds_enabled()) {
+            const i64 gm = (a.m + 63) / 64, gn = (a.n + 63) / 64;
+            if (gm == 0 || gn == 0 || batch == 0) return;
+            launch_glds<TA, TB, 64>(a, gm * gn, batch, s);
+            return;
+        }
+        if (g128 < gemm_small_tiles() && !(a.k > 0 && a.k % 16 == 0 && a.vecA && a.vecB && gemm_glds_enabled())) {
             constexpr int BM = 64, BN = 64, BK = 8;
             const i64 gm = (a.m + BM - 1) / BM, gn = (a.n + BN - 1) / BN;
             if (gm == 0 || gn == 0 || batch == 0) return;
@@ -184,7 +194,7 @@ static void launch_real(const GemmArgs<T>& a0, int batch, hipStream_t s) {
     if (i64 t = tri_blocks(a, BM, BN)) { a.remap = 2; nblk = t; }
     if constexpr (sizeof(T) == 8 && !PTRS) {
         if (a.k > 0 && a.k % 16 == 0 && a.vecA && a.vecB && gemm_glds_enabled()) {
-            launch_glds<TA, TB>(a, nblk, batch, s);
+            launch_glds<TA, TB, 128>(a, nblk, batch, s);
             return;
         }
     }

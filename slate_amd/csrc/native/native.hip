@@ -782,24 +782,32 @@ int64_t potrf(HermitianMatrix<T>& A, const Options& opts) {
 template <typename T>
 static void transpose_tiles(const Storage& L, Storage& U, char ct);
 
+// tri: the right-hand side is triangular in tile granularity and stays so
+// (an identity solved into an inverse factor): 1 = only rhs tile columns
+// <= k are touched at step k (Lower), 2 = only those >= k (Upper) -- n^3/3
+// flops for L^{-1} instead of n^3
 template <typename T>
-static void trsm_left(char uplo, char diag, T alpha, const Storage& SA, Storage& SB) {
+static void trsm_left(char uplo, char diag, T alpha, const Storage& SA, Storage& SB, int tri = 0) {
     Runtime& R = rt();
     GridComms* gc = SB.gc;
     const int p = SB.p, q = SB.q, pr = SB.pr, pc = SB.pc;
-    const i64 nb = SA.nb, n = SA.n, nrhs_loc = SB.nloc;
+    const i64 nb = SA.nb, n = SA.n, nrhs_all = SB.nloc;
     const T* A = static_cast<const T*>(SA.buf);
-    T* B = static_cast<T*>(SB.buf);
+    T* B0 = static_cast<T*>(SB.buf);
     const i64 lda = SA.lld, ldb = SB.lld;
     const i64 nt = (n + nb - 1) / nb;
     hipStream_t s = R.main;
-    if (alpha != T(1) && SB.mloc && nrhs_loc) slate_hip::gescale<K<T>>('G', SB.mloc, nrhs_loc, kv(alpha), kp(B), ldb, s);
+    if (alpha != T(1) && SB.mloc && nrhs_all) slate_hip::gescale<K<T>>('G', SB.mloc, nrhs_all, kv(alpha), kp(B0), ldb, s);
     const bool lower = uplo == 'L';
     for (i64 st = 0; st < nt; ++st) {
         const i64 k = lower ? st : nt - 1 - st;
         const i64 kb = std::min(nb, n - k * nb);
         const int rk = (int)(k % p), ck = (int)(k % q);
         const i64 lrk = tiles_before(k, p, pr) * nb, lck = tiles_before(k, q, pc) * nb;
+        const i64 c0 = tri == 2 ? std::min(tiles_before(k, q, pc) * nb, nrhs_all) : 0;
+        const i64 c1 = tri == 1 ? std::min(tiles_before(k + 1, q, pc) * nb, nrhs_all) : nrhs_all;
+        const i64 nrhs_loc = std::max<i64>(c1 - c0, 0);
+        T* B = B0 + c0 * ldb;
         // diagonal tile to process row rk
         Scratch D((size_t)kb * kb * sizeof(T), s);
         if (pr == rk) {
@@ -1344,9 +1352,13 @@ int64_t gesv(Matrix<T>& A, std::vector<int64_t>& ipiv, Matrix<T>& B, const Optio
 // process rows and the B row block along the process columns (lookahead
 // broadcasts on the comm stream), one local GEMM each.  mask: only the kept
 // part of C (a stored triangle, in global coordinates) is written.
+// kstruct: A's column block k / B's row block k only reach C's tiles <= k
+// (1: X^H X of a lower X, X X^H of an upper X) or >= k (2: X^H X of an
+// upper X): step k updates only that corner of C, so a triangular product
+// costs a third of the full one (C starts at beta = 0)
 template <typename T>
 static void summa(T alpha, const Storage& SA, const Storage& SB, T beta, Storage& SC, const Options& opts,
-                  const slate_hip::TriMask* mask) {
+                  const slate_hip::TriMask* mask, int kstruct = 0) {
     if (SA.m != SC.m || SB.n != SC.n || SA.n != SB.m) throw Error("native gemm: dimension mismatch");
     if (SA.nb != SB.nb || SA.nb != SC.nb || SA.p != SC.p || SA.q != SC.q || SB.p != SC.p || SB.q != SC.q)
         throw Error("native gemm: A, B, C must share the grid and the tile size");
@@ -1360,7 +1372,12 @@ static void summa(T alpha, const Storage& SA, const Storage& SB, T beta, Storage
     T* Cl = static_cast<T*>(SC.buf);
     const T* Al = static_cast<const T*>(SA.buf);
     const T* Bl = static_cast<const T*>(SB.buf);
-    if (p == 1 && q == 1) {
+    if (kstruct) {
+        if (beta != T(0)) throw Error("native summa: a triangular-structured product starts from beta = 0");
+        if (SC.mloc && SC.nloc) slate_hip::geset<K<T>>('G', SC.mloc, SC.nloc, kv(T(0)), kv(T(0)), kp(Cl), SC.lld, s);
+        beta = T(1);
+    }
+    if (p == 1 && q == 1 && !kstruct) {
         gemm_k<T>('N', 'N', SC.m, SC.n, Kd, alpha, Al, SA.lld, Bl, SB.lld, beta, Cl, SC.lld, s, mask);
     } else {
         const i64 kt = (Kd + nb - 1) / nb;
@@ -1393,8 +1410,25 @@ static void summa(T alpha, const Storage& SA, const Storage& SB, T beta, Storage
             const int b = (int)(k % nbuf);
             const i64 kb = std::min(nb, Kd - k * nb);
             ready[k]->wait(s);
-            gemm_k<T>('N', 'N', SC.mloc, SC.nloc, kb, alpha, Ab[b]->as<T>(), ma, Bb[b]->as<T>(), kb,
-                      k == 0 ? beta : T(1), Cl, SC.lld, s, mask);
+            i64 r0 = 0, r1 = SC.mloc, c0 = 0, c1 = SC.nloc;
+            if (kstruct == 1) {
+                r1 = std::min(tiles_before(k + 1, p, pr) * nb, SC.mloc);
+                c1 = std::min(tiles_before(k + 1, q, pc) * nb, SC.nloc);
+            } else if (kstruct == 2) {
+                r0 = std::min(tiles_before(k, p, pr) * nb, SC.mloc);
+                c0 = std::min(tiles_before(k, q, pc) * nb, SC.nloc);
+            }
+            slate_hip::TriMask mk2{};
+            const slate_hip::TriMask* mp = mask;
+            if (mask) {
+                mk2 = *mask;
+                mk2.row_off += r0;
+                mk2.col_off += c0;
+                mp = &mk2;
+            }
+            if (r1 > r0 && c1 > c0)
+                gemm_k<T>('N', 'N', r1 - r0, c1 - c0, kb, alpha, Ab[b]->as<T>() + r0, ma, Bb[b]->as<T>() + c0 * kb, kb,
+                          k == 0 ? beta : T(1), Cl + r0 + c0 * SC.lld, SC.lld, s, mp);
             used[k] = std::make_unique<Event>();
             used[k]->record(s);
         }
@@ -1639,40 +1673,99 @@ static Matrix<T> identity_like(const Storage& S) {
 }
 
 // A^-1 from the Cholesky factor in A (potrf first); the stored triangle
-// of A receives the inverse
+// of A receives the inverse.  src/potri.cc's trtri + trtrm: X = L^{-1} by
+// the tile-triangular forward solve of the identity (n^3 / 3 flops), then
+// A^{-1} = X^H X by the K-structured masked SUMMA (n^3 / 3) -- Upper: X =
+// U^{-1}, A^{-1} = X X^H.
 template <typename T>
 int64_t potri(HermitianMatrix<T>& A, const Options& opts) {
     const Storage& S = *A.storage();
+    const bool lower = A.uplo() == Uplo::Lower;
     Matrix<T> X = identity_like<T>(S);
-    potrs<T>(A, X, opts);
+    NHIP(hipStreamSynchronize(rt().main));
+    trsm_left<T>(lower ? 'L' : 'U', 'N', T(1), S, *X.storage(), lower ? 1 : 2);
+    const Matrix<T> Xh = op_copy<T>(Op::ConjTrans, X);
+    Matrix<T> C(S.n, S.n, S.nb, S.p, S.q);
     const slate_hip::TriMask mk = tri_mask(S, A.uplo());
+    if (lower) summa<T>(T(1), *Xh.storage(), *X.storage(), T(0), *C.storage(), opts, &mk, 1);
+    else summa<T>(T(1), *X.storage(), *Xh.storage(), T(0), *C.storage(), opts, &mk, 1);
     hipStream_t s = rt().main;
-    const Storage& SX = *X.storage();
-    if (S.mloc && S.nloc) {
-        // stored triangle <- X, the other part of A unchanged: mask X in place, zero A's triangle, add
-        T* x = static_cast<T*>(SX.buf);
-        slate_hip::gecopy_mask<K<T>>(mk, S.mloc, S.nloc, kp(x), SX.lld, kp(x), SX.lld, true, s);
-        Matrix<T> Keep(S.m, S.n, S.nb, S.p, S.q);
-        const Storage& SK = *Keep.storage();
-        const slate_hip::TriMask other = tri_mask(S, A.uplo() == Uplo::Lower ? Uplo::Upper : Uplo::Lower, -1);
-        slate_hip::gecopy_mask<K<T>>(other, S.mloc, S.nloc, kp(static_cast<const T*>(S.buf)), S.lld,
-                                     kp(static_cast<T*>(SK.buf)), SK.lld, false, s);
-        slate_hip::geadd<K<T>>('G', S.mloc, S.nloc, kv(T(1)), kp(x), SX.lld, kv(T(1)), kp(static_cast<T*>(SK.buf)),
-                               SK.lld, s);
-        copy2d(static_cast<T*>(S.buf), S.lld, static_cast<const T*>(SK.buf), SK.lld, S.mloc, S.nloc, s);
-    }
+    const Storage& SC = *C.storage();
+    // stored triangle <- C (real diagonal), the other triangle of A untouched
+    if (S.mloc && S.nloc)
+        slate_hip::gecopy_mask_merge<K<T>>(mk, S.mloc, S.nloc, kp(static_cast<const T*>(SC.buf)), SC.lld,
+                                           kp(static_cast<T*>(S.buf)), S.lld, s);
     NHIP(hipStreamSynchronize(s));
     return 0;
 }
 
-// A^-1 from the LU factors in A and ipiv (getrf first), over A
+// A^-1 from the LU factors in A and ipiv (getrf first), over A: P A = L U,
+// so A^-1 = U^{-1} L^{-1} P -- X = L^{-1} by the tile-triangular solve of the
+// identity (n^3 / 3 flops), X = U^{-1} X (n^3), then the columns of X move
+// to their permuted places inside each process row (one exchange on the row
+// communicator).  Reference: src/getri.cc (trtri + trsm + column swaps).
 template <typename T>
 int64_t getri(Matrix<T>& A, const std::vector<int64_t>& ipiv, const Options& opts) {
-    const Storage& S = *A.storage();
+    Storage& S = *A.storage();
     if (S.m != S.n) throw Error("native getri: square matrix");
+    (void)opts;
+    const i64 n = S.n, nb = S.nb;
+    const int q = S.q, pc = S.pc;
     Matrix<T> X = identity_like<T>(S);
-    getrs<T>(A, ipiv, X, opts);
-    copy<T>(Op::NoTrans, X, A);
+    Storage& SX = *X.storage();
+    NHIP(hipStreamSynchronize(rt().main));
+    trsm_left<T>('L', 'U', T(1), S, SX, 1);
+    trsm_left<T>('U', 'N', T(1), S, SX, 0);
+    // (P A)(i, :) = A(v[i], :)  =>  A^{-1}(:, v[i]) = X(:, i)
+    std::vector<i64> v((size_t)n), w((size_t)n);
+    for (i64 i = 0; i < n; ++i) v[i] = i;
+    for (i64 i = 0; i < (i64)ipiv.size() && i < n; ++i) std::swap(v[i], v[ipiv[i]]);
+    for (i64 i = 0; i < n; ++i) w[v[i]] = i;
+    auto owner = [&](i64 g) { return (int)((g / nb) % q); };
+    auto local = [&](i64 g) { return (g / nb / q) * nb + g % nb; };
+    hipStream_t s = rt().main;
+    const i64 m = S.mloc;
+    const size_t es = sizeof(T);
+    // destination columns of this rank grouped by the source's process column
+    // (each list in increasing destination order -- the sender packs the same order)
+    std::vector<std::vector<i64>> rd((size_t)q), rs((size_t)q), sd((size_t)q), ss((size_t)q);
+    for (i64 lc = 0; lc < S.nloc; ++lc) {
+        const i64 j = l2g(lc, nb, q, pc), i = w[j];
+        rd[owner(i)].push_back(lc);
+        rs[owner(i)].push_back(local(i));
+    }
+    for (i64 j = 0; j < n; ++j) {          // what this rank sends: sources it owns, by destination
+        const i64 i = w[j];
+        if (owner(i) == pc && owner(j) != pc) ss[owner(j)].push_back(local(i));
+    }
+    if (m > 0 && !rd[pc].empty())
+        copy_cols(S.buf, S.lld, rd[pc].data(), SX.buf, SX.lld, rs[pc].data(), m, es, (i64)rd[pc].size(), s);
+    if (q > 1 && m > 0) {
+        std::vector<std::unique_ptr<Scratch>> bufs;
+        std::vector<P2P> ops;
+        std::vector<std::pair<int, Scratch*>> unpack;
+        for (int d = 0; d < q; ++d) {
+            if (d == pc || ss[d].empty()) continue;
+            bufs.push_back(std::make_unique<Scratch>(es * m * ss[d].size(), s));
+            std::vector<i64> seq(ss[d].size());
+            for (size_t c = 0; c < seq.size(); ++c) seq[c] = (i64)c;
+            copy_cols(bufs.back()->p, m, seq.data(), SX.buf, SX.lld, ss[d].data(), m, es, (i64)seq.size(), s);
+            ops.push_back({true, d, bufs.back()->p, es * m * ss[d].size()});
+        }
+        for (int src = 0; src < q; ++src) {
+            if (src == pc || rd[src].empty()) continue;
+            bufs.push_back(std::make_unique<Scratch>(es * m * rd[src].size(), s));
+            ops.push_back({false, src, bufs.back()->p, es * m * rd[src].size()});
+            unpack.emplace_back(src, bufs.back().get());
+        }
+        if (!ops.empty()) S.gc->row->exchange(ops, s);
+        for (auto& u : unpack) {
+            std::vector<i64> seq(rd[u.first].size());
+            for (size_t c = 0; c < seq.size(); ++c) seq[c] = (i64)c;
+            copy_cols(S.buf, S.lld, rd[u.first].data(), u.second->p, m, seq.data(), m, es, (i64)seq.size(), s);
+        }
+    }
+    NHIP(hipStreamSynchronize(s));
     return 0;
 }
 

@@ -8,6 +8,7 @@
 // normal L2 write-back / invalidate path of kernel boundaries.
 #include <cstring>
 #include <mutex>
+#include <vector>
 
 #include "native_rt.hpp"
 
@@ -63,6 +64,35 @@ void upload(void* d, const void* h, size_t bytes, hipStream_t s) {
 }
 
 void dcopy(void* d, const void* s, size_t bytes, hipStream_t st) { launch_copy(d, s, bytes, st); }
+
+// dst[:, didx[c]] = src[:, sidx[c]], columns of mw 4-byte words
+__global__ void __launch_bounds__(256)
+copy_cols_kernel(const unsigned* __restrict__ src, i64 lds, const i64* __restrict__ sidx, unsigned* __restrict__ dst,
+                 i64 ldd, const i64* __restrict__ didx, i64 mw, i64 ncols) {
+    for (i64 c = blockIdx.y; c < ncols; c += gridDim.y) {
+        const unsigned* a = src + sidx[c] * lds;
+        unsigned* b = dst + didx[c] * ldd;
+        for (i64 i = (i64)blockIdx.x * 256 + threadIdx.x; i < mw; i += (i64)gridDim.x * 256) b[i] = a[i];
+    }
+}
+
+void copy_cols(void* dst, i64 ldd, const i64* didx, const void* src, i64 lds, const i64* sidx, i64 m, size_t esize,
+               i64 ncols, hipStream_t s) {
+    if (ncols <= 0 || m <= 0) return;
+    const size_t w = esize / 4;
+    std::vector<i64> h(2 * (size_t)ncols);
+    std::memcpy(h.data(), sidx, sizeof(i64) * ncols);
+    std::memcpy(h.data() + ncols, didx, sizeof(i64) * ncols);
+    Scratch ix(sizeof(i64) * h.size(), s);
+    upload(ix.p, h.data(), sizeof(i64) * h.size(), s);
+    const i64 mw = m * (i64)w;
+    const unsigned gx = (unsigned)std::min<i64>((mw + 255) / 256, 64), gy = (unsigned)std::min<i64>(ncols, 16384);
+    hipLaunchKernelGGL(copy_cols_kernel, dim3(gx, gy), dim3(256), 0, s, static_cast<const unsigned*>(src),
+                       lds * (i64)w, ix.as<i64>(), static_cast<unsigned*>(dst), ldd * (i64)w, ix.as<i64>() + ncols, mw,
+                       ncols);
+    NHIP(hipGetLastError());
+    NHIP(hipStreamSynchronize(s));
+}
 
 }  // namespace native
 }  // namespace slate_amd

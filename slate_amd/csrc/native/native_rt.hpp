@@ -192,6 +192,10 @@ struct Event {
 // memory that kernels on other XCDs may hold in their L2
 void upload(void* d, const void* h, size_t bytes, hipStream_t s);
 void dcopy(void* d, const void* src, size_t bytes, hipStream_t s);
+// dst[:, didx[c]] = src[:, sidx[c]] for c < ncols (m elements of esize bytes
+// per column; host index lists); complete on return
+void copy_cols(void* dst, i64 ldd, const i64* didx, const void* src, i64 lds, const i64* sidx, i64 m, size_t esize,
+               i64 ncols, hipStream_t s);
 
 // stream b waits for everything issued so far on stream a
 inline void join(hipStream_t a, hipStream_t b) {
