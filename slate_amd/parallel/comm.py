@@ -350,7 +350,142 @@ class _SelfComm(Comm):
         self._subcache = {}
 
 
+class LoopbackComm(Comm):
+    """Rehearsal transport: ONE process plays world rank ``rank`` of a
+    ``size``-rank job (SLATE_AMD_LOOPBACK=size:rank, or ``loopback()``).
+    Every collective becomes a same-size local device copy on the issuing
+    stream -- the bytes a real collective would land in this rank's buffers
+    -- so the rank's own kernel DAG runs at its true local shapes and
+    stream order on one GPU; received data is this rank's own (values, not
+    the peers').  ``LOG`` records (op, communicator size, bytes, stream
+    handle) for the communication-cost model of tools/r5/loopback_critpath.py."""
+
+    LOG: list = []
+    _scratch: dict = {}
+
+    def __init__(self, size, rank, ranks=None):
+        self.world_rank = rank
+        self.ranks = list(range(size)) if ranks is None else list(ranks)
+        self.size = len(self.ranks)
+        self.rank = self.ranks.index(rank) if rank in self.ranks else -1
+        self.group = None
+        self.backend = "loopback"
+        self._subcache = {}
+
+    def _log(self, op, t):
+        nbytes = t.numel() * t.element_size() if isinstance(t, torch.Tensor) else 0
+        st = torch.cuda.current_stream(t.device).cuda_stream if isinstance(t, torch.Tensor) and t.is_cuda else 0
+        LoopbackComm.LOG.append((op, self.size, nbytes, st))
+
+    @classmethod
+    def _tmp(cls, t):
+        key = (str(t.device), t.dtype)
+        buf = cls._scratch.get(key)
+        if buf is None or buf.numel() < t.numel():
+            buf = cls._scratch[key] = torch.empty(max(t.numel(), 1 << 16), dtype=t.dtype, device=t.device)
+        return buf[: t.numel()]
+
+    def _land(self, t):
+        """t receives its own bytes again: one read + one write of t."""
+        if t.numel() == 0:
+            return t
+        fv = self._flat_view(t)
+        src = fv.reshape(-1) if fv is not None else t.contiguous().reshape(-1)
+        tmp = self._tmp(src)
+        tmp.copy_(src)
+        if fv is not None:
+            src.copy_(tmp)
+        else:
+            t.copy_(tmp.view(t.shape))
+        return t
+
+    def barrier(self):
+        return None
+
+    def bcast(self, t, root, async_op=False):
+        self._log("bcast", t)
+        if self.size > 1 and self.rank != root:
+            self._land(t)
+        return None
+
+    def allreduce(self, t, op="sum"):
+        self._log("allreduce", t)
+        if self.size > 1:
+            self._land(t)
+        return t
+
+    def allreduce_scalar(self, v, op="sum", dtype=torch.float64, device=None):
+        return v
+
+    def maxloc(self, value, index):
+        return value, index
+
+    def allgather(self, t):
+        self._log("allgather", t)
+        return t.unsqueeze(0).expand((self.size,) + tuple(t.shape)).contiguous()
+
+    def allgatherv(self, t):
+        self._log("allgatherv", t)
+        return [t.clone() for _ in range(self.size)]
+
+    def reduce(self, t, root, op="sum"):
+        self._log("reduce", t)
+        if self.size > 1 and self.rank == root:
+            self._land(t)
+        return t
+
+    def send(self, t, dst, tag=0):
+        self._log("send", t)
+
+    def recv(self, t, src, tag=0):
+        self._log("recv", t)
+        return self._land(t) if self.size > 1 else t
+
+    def sendrecv(self, send_t, dst, recv_t, src):
+        self._log("sendrecv", recv_t)
+        if recv_t.shape == send_t.shape:
+            recv_t.copy_(send_t)
+        else:
+            self._land(recv_t)
+        return recv_t
+
+    def exchange(self, sends, recvs):
+        pool = {}
+        for t in sends.values():
+            pool.setdefault(t.numel(), t)
+        for t in recvs.values():
+            self._log("exchange", t)
+            d = pool.get(t.numel())
+            if d is not None and d.dtype == t.dtype:
+                t.copy_(d.reshape(t.shape) if d.is_contiguous() else d.contiguous().reshape(t.shape))
+            else:
+                self._land(t)
+
+    def bcast_object(self, obj, root):
+        return obj
+
+    def split(self, color_of_rank, tag=""):
+        key = (tuple(color_of_rank), tag)
+        if key in self._subcache:
+            return self._subcache[key]
+        mine = None
+        if self.rank >= 0:
+            c = color_of_rank[self.rank]
+            members = [self.ranks[r] for r in range(self.size) if color_of_rank[r] == c]
+            mine = LoopbackComm(0, self.world_rank, members) if len(members) > 1 else _SelfComm(self.world_rank)
+        self._subcache[key] = mine
+        return mine
+
+
 _WORLD = None
+
+
+def loopback(size: int, rank: int) -> Comm:
+    """Make the world a LoopbackComm (this process plays ``rank`` of ``size``)."""
+    global _WORLD
+    _WORLD = LoopbackComm(size, rank)
+    ProcessGrid._cache.clear()
+    return _WORLD
 
 
 def self_comm() -> Comm:
@@ -362,6 +497,13 @@ def self_comm() -> Comm:
 def world() -> Comm:
     """The global communicator (all ranks; a size-1 comm without torch.distributed)."""
     global _WORLD
+    if isinstance(_WORLD, LoopbackComm):
+        return _WORLD
+    lb = os.environ.get("SLATE_AMD_LOOPBACK")
+    if lb and _WORLD is None:
+        size, rank = (int(x) for x in lb.split(":"))
+        _WORLD = LoopbackComm(size, rank)
+        return _WORLD
     if _WORLD is None or (_dist_ready() and _WORLD.size != dist.get_world_size()):
         _WORLD = Comm() if _dist_ready() else _SelfComm(0)
     return _WORLD

@@ -46,7 +46,8 @@ class PeerMailbox:
         """Device mailboxes for this communicator and tensor: GPU tensors,
         2 <= size <= the kernel's peer limit; SLATE_AMD_LU_PEER=0 keeps the
         host-issued record all-gather."""
-        if os.environ.get("SLATE_AMD_LU_PEER", "1") == "0" or not t.is_cuda or comm.size < 2:
+        if os.environ.get("SLATE_AMD_LU_PEER", "1") == "0" or not t.is_cuda or comm.size < 2 or \
+                getattr(comm, "backend", "") == "loopback":
             return False
         from .. import _native
         return comm.size <= _native.hip().lu_peer_sizes()[3]
