@@ -168,8 +168,6 @@ def _main_native(args):
     if args.routine not in ("potrf", "getrf", "gemm", "geqrf"):
         raise SystemExit("--impl native: potrf, getrf, gemm or geqrf")
     p, q = grid_for(world, args.routine) if args.grid is None else map(int, args.grid.lower().split("x"))
-    if args.routine == "geqrf" and args.grid is None:
-        p, q = 1, world                     # the native geqrf distributes whole columns (1 x q)
     exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "slate_amd", "bench_native")
     cmd = [exe, args.routine, str(args.n), str(args.nb), str(p), str(q), str(args.lookahead), str(args.warmup),
            str(args.steps), str(args.check), str(args.m or args.n)]

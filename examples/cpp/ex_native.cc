@@ -311,6 +311,94 @@ void run(int p, int q, int me) {
         }
         report("trsm_lc", rel<T>(lx, want));
     }
+    // ---- trtri of the Cholesky factor: L^{-1} L = I; trtrm: L^H L
+    {
+        sn::Matrix<T> Li(n, n, nb, p, q);
+        Li.from_host(l.data(), n);
+        sn::trtri(sn::Uplo::Lower, sn::Diag::NonUnit, Li);
+        std::vector<T> li((size_t)n * n);
+        Li.to_host(li.data(), n);
+        for (int64_t j = 0; j < n; ++j)
+            for (int64_t i = 0; i < j; ++i) li[i + j * n] = T(0);
+        auto prod = mul<T>('N', 'N', n, n, n, li, n, l, n);
+        std::vector<std::complex<double>> eye((size_t)n * n, 0.0);
+        for (int64_t i = 0; i < n; ++i) eye[i + i * n] = 1.0;
+        for (size_t i = 0; i < prod.size(); ++i) prod[i] -= eye[i];
+        report("trtri", rel<T>(prod, eye));
+        sn::Matrix<T> Lm(n, n, nb, p, q);
+        Lm.from_host(l.data(), n);
+        sn::trtrm(sn::Uplo::Lower, Lm);
+        std::vector<T> lm((size_t)n * n);
+        Lm.to_host(lm.data(), n);
+        auto want = mul<T>('C', 'N', n, n, n, l, n, l, n);
+        double e = 0, w = 0;
+        for (int64_t j = 0; j < n; ++j)
+            for (int64_t i = j; i < n; ++i) {
+                e += std::norm(std::complex<double>(std::real(lm[i + j * n]), std::imag(lm[i + j * n])) - want[i + j * n]);
+                w += std::norm(want[i + j * n]);
+            }
+        report("trtrm", std::sqrt(e / w));
+    }
+    // ---- LU without pivoting on the HPD matrix: A X = B
+    {
+        sn::Matrix<T> Gn(n, n, nb, p, q), Xn(n, nrhs, nb, p, q);
+        Gn.from_host(a0.data(), n);
+        Xn.from_host(b0.data(), n);
+        info = sn::gesv_nopiv(Gn, Xn);
+        std::vector<T> xn((size_t)n * nrhs);
+        Xn.to_host(xn.data(), n);
+        auto ax = mul<T>('N', 'N', n, nrhs, n, a0, n, xn, n);
+        auto want = widen(b0);
+        for (size_t i = 0; i < ax.size(); ++i) ax[i] -= want[i];
+        report(info ? "gesv_nopiv-FAILED" : "gesv_nopiv", rel<T>(ax, want));
+    }
+    // ---- Cholesky QR: Q R = A, Q^H Q = I
+    {
+        const int64_t m7 = 330, n7 = 120;
+        sn::Matrix<T> A7(m7, n7, nb, p, q), R7(n7, n7, nb, p, q);
+        A7.generate(sn::Gen::Random, 71);
+        std::vector<T> a7((size_t)m7 * n7), q7((size_t)m7 * n7), r7((size_t)n7 * n7);
+        A7.to_host(a7.data(), m7);
+        info = sn::cholqr(A7, R7);
+        A7.to_host(q7.data(), m7);
+        R7.to_host(r7.data(), n7);
+        auto qr = mul<T>('N', 'N', m7, n7, n7, q7, m7, r7, n7);
+        auto want = widen(a7);
+        for (size_t i = 0; i < qr.size(); ++i) qr[i] -= want[i];
+        report(info ? "cholqr-FAILED" : "cholqr", rel<T>(qr, want));
+        auto qq = mul<T>('C', 'N', n7, n7, m7, q7, m7, q7, m7);
+        std::vector<std::complex<double>> eye((size_t)n7 * n7, 0.0);
+        for (int64_t i = 0; i < n7; ++i) eye[i + i * n7] = 1.0;
+        for (size_t i = 0; i < qq.size(); ++i) qq[i] -= eye[i];
+        report("cholqr_orth", rel<T>(qq, eye));
+    }
+    // ---- LQ of a wide matrix: Q^H L^H = A^H through unmlq
+    {
+        const int64_t m8 = 120, n8 = 330;
+        sn::Matrix<T> A8(m8, n8, nb, p, q), C8(n8, m8, nb, p, q);
+        A8.generate(sn::Gen::Random, 81);
+        std::vector<T> a8((size_t)m8 * n8), f8((size_t)m8 * n8), lh((size_t)n8 * m8, T(0)), c8((size_t)n8 * m8);
+        A8.to_host(a8.data(), m8);
+        sn::LQFactors<T> F8;
+        sn::gelqf(A8, F8);
+        A8.to_host(f8.data(), m8);
+        for (int64_t j = 0; j < m8; ++j)              // L^H: n8 x m8, upper part of its first m8 rows
+            for (int64_t i = j; i < m8; ++i) lh[j + i * n8] = cj(f8[i + j * m8]);
+        C8.from_host(lh.data(), n8);
+        sn::unmlq(sn::Op::ConjTrans, A8, F8, C8);
+        C8.to_host(c8.data(), n8);
+        double e = 0, w = 0;
+        for (int64_t j = 0; j < m8; ++j)
+            for (int64_t i = 0; i < n8; ++i) {
+                const T want = cj(a8[j + i * m8]);
+                const std::complex<double> d(std::real(c8[i + j * n8]) - std::real(want),
+                                             std::imag(c8[i + j * n8]) - std::imag(want));
+                e += std::norm(d);
+                w += std::norm(std::complex<double>(std::real(want), std::imag(want)));
+            }
+        report("gelqf", std::sqrt(e / w));
+    }
+
     // ---- trsm on the stored triangle: L^T X = alpha B (left), X op(L) = alpha C (right)
     for (int v = 0; v < 3; ++v) {
         const bool right = v > 0;

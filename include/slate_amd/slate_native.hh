@@ -202,6 +202,16 @@ void trmm(Side side, Uplo uplo, Op op, Diag diag, T alpha, const Matrix<T>& A, M
 // inverses from the factors: potri after potrf (stored triangle), getri after getrf
 template <typename T> int64_t potri(HermitianMatrix<T>& A, const Options& opts = {});
 template <typename T> int64_t getri(Matrix<T>& A, const std::vector<int64_t>& ipiv, const Options& opts = {});
+// triangular inverse in place (stored triangle; Unit: the diagonal is not
+// referenced) and the triangular product A <- L^H L (Lower) / U U^H (Upper)
+template <typename T> int64_t trtri(Uplo uplo, Diag diag, Matrix<T>& A, const Options& opts = {});
+template <typename T> void trtrm(Uplo uplo, Matrix<T>& A, const Options& opts = {});
+// LU without pivoting (SLATE getrf_nopiv / gesv_nopiv): unit-lower L and U in A
+template <typename T> int64_t getrf_nopiv(Matrix<T>& A, const Options& opts = {});
+template <typename T> int64_t gesv_nopiv(Matrix<T>& A, Matrix<T>& B, const Options& opts = {});
+// Cholesky QR (SLATE cholqr): A (m x n, m >= n) <- Q, R (n x n) <- the upper
+// triangular factor (zero below); info > 0 when A^H A is not positive definite
+template <typename T> int64_t cholqr(Matrix<T>& A, Matrix<T>& R, const Options& opts = {});
 
 // mixed precision (double / complex<double> only): factor in float /
 // complex<float>, refine in the working precision; X = A^-1 B, B unchanged;
@@ -249,6 +259,17 @@ template <typename T> int64_t geqrf(Matrix<T>& A, QRFactors<T>& F, const Options
 template <typename T>
 void unmqr(Op op, const Matrix<T>& A, const QRFactors<T>& F, Matrix<T>& C, const Options& opts = {});
 template <typename T> int64_t gels(Matrix<T>& A, Matrix<T>& BX, const Options& opts = {});
+// LQ: A = L Q (the QR of A^H, kept in F): A receives L in its lower
+// trapezoid and the row reflectors above it; unmlq applies op(Q) from the
+// left to C (n rows, A's grid and tile size)
+template <typename T>
+struct LQFactors {
+    std::shared_ptr<Matrix<T>> At;     // A^H as factored by geqrf
+    QRFactors<T> qr;
+};
+template <typename T> int64_t gelqf(Matrix<T>& A, LQFactors<T>& F, const Options& opts = {});
+template <typename T>
+void unmlq(Op op, const Matrix<T>& A, const LQFactors<T>& F, Matrix<T>& C, const Options& opts = {});
 
 }  // namespace native
 }  // namespace slate_amd

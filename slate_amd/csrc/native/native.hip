@@ -1769,6 +1769,116 @@ int64_t getri(Matrix<T>& A, const std::vector<int64_t>& ipiv, const Options& opt
     return 0;
 }
 
+// ------------------------------------------------------------ trtri / trtrm (src/trtri.cc, src/trtrm.cc)
+// A^{-1} of the stored triangle: the tile-triangular solve of the identity
+// (n^3 / 3 flops), written back over the triangle (the other part of A and,
+// for Unit, its diagonal untouched)
+template <typename T>
+int64_t trtri(Uplo uplo, Diag diag, Matrix<T>& A, const Options& opts) {
+    (void)opts;
+    Storage& S = *A.storage();
+    if (S.m != S.n) throw Error("native trtri: square matrix");
+    const bool lower = uplo == Uplo::Lower;
+    Matrix<T> X = identity_like<T>(S);
+    NHIP(hipStreamSynchronize(rt().main));
+    trsm_left<T>(lower ? 'L' : 'U', diag == Diag::Unit ? 'U' : 'N', T(1), S, *X.storage(), lower ? 1 : 2);
+    const slate_hip::TriMask mk = tri_mask(S, uplo, diag == Diag::Unit ? -1 : 0);
+    hipStream_t s = rt().main;
+    if (S.mloc && S.nloc)
+        slate_hip::gecopy_mask_merge<K<T>>(mk, S.mloc, S.nloc, kp(static_cast<const T*>(X.storage()->buf)),
+                                           X.storage()->lld, kp(static_cast<T*>(S.buf)), S.lld, s);
+    NHIP(hipStreamSynchronize(s));
+    return 0;
+}
+
+// stored triangle <- L^H L (Lower) or U U^H (Upper): the K-structured
+// masked SUMMA (n^3 / 3 flops)
+template <typename T>
+void trtrm(Uplo uplo, Matrix<T>& A, const Options& opts) {
+    Storage& S = *A.storage();
+    if (S.m != S.n) throw Error("native trtrm: square matrix");
+    const bool lower = uplo == Uplo::Lower;
+    const Matrix<T> X = expand_tri<T>(A, uplo, 0);
+    const Matrix<T> Xh = op_copy<T>(Op::ConjTrans, X);
+    Matrix<T> C(S.n, S.n, S.nb, S.p, S.q);
+    const slate_hip::TriMask mk = tri_mask(S, uplo);
+    if (lower) summa<T>(T(1), *Xh.storage(), *X.storage(), T(0), *C.storage(), opts, &mk, 1);
+    else summa<T>(T(1), *X.storage(), *Xh.storage(), T(0), *C.storage(), opts, &mk, 1);
+    hipStream_t s = rt().main;
+    if (S.mloc && S.nloc)
+        slate_hip::gecopy_mask_merge<K<T>>(mk, S.mloc, S.nloc, kp(static_cast<const T*>(C.storage()->buf)),
+                                           C.storage()->lld, kp(static_cast<T*>(S.buf)), S.lld, s);
+    NHIP(hipStreamSynchronize(s));
+}
+
+// ------------------------------------------------------------ LU without pivoting (src/getrf_nopiv.cc)
+// the partial-pivoting driver with a zero pivot threshold: every panel keeps
+// its diagonal (no row ever moves), ipiv is the identity
+template <typename T>
+int64_t getrf_nopiv(Matrix<T>& A, const Options& opts) {
+    Options o = opts;
+    o.pivot_threshold = 0.0;
+    std::vector<int64_t> ipiv;
+    return getrf<T>(A, ipiv, o);
+}
+
+template <typename T>
+int64_t gesv_nopiv(Matrix<T>& A, Matrix<T>& B, const Options& opts) {
+    const int64_t info = getrf_nopiv<T>(A, opts);
+    if (info == 0) {
+        trsm<T>(Side::Left, Uplo::Lower, Op::NoTrans, Diag::Unit, T(1), A, B, opts);
+        trsm<T>(Side::Left, Uplo::Upper, Op::NoTrans, Diag::NonUnit, T(1), A, B, opts);
+    }
+    return info;
+}
+
+// ------------------------------------------------------------ Cholesky QR (src/cholqr.cc)
+// G = A^H A (herk into the lower triangle), G = L L^H, Q = A L^{-H}, R = L^H
+template <typename T>
+int64_t cholqr(Matrix<T>& A, Matrix<T>& R, const Options& opts) {
+    const Storage& SA = *A.storage();
+    Storage& SR = *R.storage();
+    if (SA.m < SA.n) throw Error("native cholqr: m >= n");
+    if (SR.m != SA.n || SR.n != SA.n || SR.nb != SA.nb || SR.p != SA.p || SR.q != SA.q)
+        throw Error("native cholqr: R must be n x n on A's grid");
+    HermitianMatrix<T> G(Uplo::Lower, SA.n, SA.nb, SA.p, SA.q);
+    herk<T>(Op::ConjTrans, real_t<T>(1), A, real_t<T>(0), G, opts);
+    const int64_t info = potrf<T>(G, opts);
+    if (info) return info;
+    trsm<T>(Side::Right, Uplo::Lower, Op::ConjTrans, Diag::NonUnit, T(1), G, A, opts);
+    copy<T>(Op::ConjTrans, G, R);
+    const slate_hip::TriMask up = tri_mask(SR, Uplo::Upper);
+    hipStream_t s = rt().main;
+    if (SR.mloc && SR.nloc)
+        slate_hip::gecopy_mask<K<T>>(up, SR.mloc, SR.nloc, kp(static_cast<const T*>(SR.buf)), SR.lld,
+                                     kp(static_cast<T*>(SR.buf)), SR.lld, false, s);
+    NHIP(hipStreamSynchronize(s));
+    return 0;
+}
+
+// ------------------------------------------------------------ LQ (src/gelqf.cc, src/unmlq.cc)
+// the QR of A^H: A = (Q_qr R)^H = R^H Q_qr^H, so L = R^H and Q = Q_qr^H; A
+// receives (A^H factored)^H -- L in the lower trapezoid, the reflectors
+// (conjugated) above it, LAPACK's LQ layout
+template <typename T>
+int64_t gelqf(Matrix<T>& A, LQFactors<T>& F, const Options& opts) {
+    const Storage& S = *A.storage();
+    F.At = std::make_shared<Matrix<T>>(S.n, S.m, S.nb, S.p, S.q);
+    copy<T>(Op::ConjTrans, A, *F.At);
+    geqrf<T>(*F.At, F.qr, opts);
+    copy<T>(Op::ConjTrans, *F.At, A);
+    return 0;
+}
+
+// C = op(Q) C, Q = Q_qr^H: Q C = Q_qr^H C, Q^H C = Q_qr C
+template <typename T>
+void unmlq(Op op, const Matrix<T>& A, const LQFactors<T>& F, Matrix<T>& C, const Options& opts) {
+    (void)A;
+    if (!F.At) throw Error("native unmlq: factor with gelqf first");
+    if (op == Op::Trans && is_cplx<T>()) throw Error("native unmlq: Trans of a complex Q (use ConjTrans)");
+    unmqr<T>(op == Op::NoTrans ? Op::ConjTrans : Op::NoTrans, *F.At, F.qr, C, opts);
+}
+
 // ------------------------------------------------------------ condition estimates
 // ||A^-1||_1 by Higham's refinement of Hager's method (LAPACK lacn2; SLATE
 // internal_norm1est.cc): fw(X) = A^-1 X, bw(X) = A^-H X on a distributed
@@ -2362,6 +2472,13 @@ int64_t gels(Matrix<T>& A, Matrix<T>& BX, const Options& opts) {
     template int64_t geqrf<T>(Matrix<T>&, QRFactors<T>&, const Options&);                                      \
     template void unmqr<T>(Op, const Matrix<T>&, const QRFactors<T>&, Matrix<T>&, const Options&);             \
     template int64_t gels<T>(Matrix<T>&, Matrix<T>&, const Options&);                                         \
+    template int64_t trtri<T>(Uplo, Diag, Matrix<T>&, const Options&);                                        \
+    template void trtrm<T>(Uplo, Matrix<T>&, const Options&);                                                 \
+    template int64_t getrf_nopiv<T>(Matrix<T>&, const Options&);                                              \
+    template int64_t gesv_nopiv<T>(Matrix<T>&, Matrix<T>&, const Options&);                                   \
+    template int64_t cholqr<T>(Matrix<T>&, Matrix<T>&, const Options&);                                       \
+    template int64_t gelqf<T>(Matrix<T>&, LQFactors<T>&, const Options&);                                     \
+    template void unmlq<T>(Op, const Matrix<T>&, const LQFactors<T>&, Matrix<T>&, const Options&);            \
     template void herk<T>(Op, real_t<T>, const Matrix<T>&, real_t<T>, HermitianMatrix<T>&, const Options&);    \
     template void syrk<T>(Op, T, const Matrix<T>&, T, HermitianMatrix<T>&, const Options&);                    \
     template void her2k<T>(Op, T, const Matrix<T>&, const Matrix<T>&, real_t<T>, HermitianMatrix<T>&,          \

@@ -118,7 +118,8 @@ def _assert_checks(checks, out):
                                                    "potri", "getri", "norm_herm_one", "norm_sym_one",
                                                    "norm_tri_fro", "heev", "heev_orth", "heev_values",
                                                    "gecondest", "svd", "svd_orth", "svd_wide", "svd_wide_orth", "geqrf", "geqrf_wide", "gels_grid",
-                                                   "trsm_lt", "trsm_rn", "trsm_rc",
+                                                   "trsm_lt", "trsm_rn", "trsm_rc", "trtri", "trtrm", "gesv_nopiv",
+                                                   "cholqr", "cholqr_orth", "gelqf",
                                                    "svd_values")]
     for name in names:
         assert name in checks, (name, out)
