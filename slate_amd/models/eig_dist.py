@@ -180,9 +180,13 @@ def he2hb_dist(F, opts=None):
 
 def gather_band(F, root=0):
     """The Hermitian band of the reduced F (tile diagonal, lower triangle +
-    the R blocks of the sub-diagonal tiles) as a dense host n x n matrix on
-    ``root`` (both triangles; None elsewhere).  Each rank contributes the
-    band tiles it owns to a (2 nb) x n stack; one sum-reduction, O(n nb)."""
+    the R blocks of the sub-diagonal tiles) as a dense n x n matrix on
+    ``root``'s device (both triangles; None elsewhere), the stage-2 chase's
+    input.  Each rank contributes the band tiles it owns to a (2 nb) x n
+    stack; one sum-reduction, O(n nb) traffic.  The root assembles it with
+    kernels on the device -- no host n x n (SLATE he2hbGather,
+    HermitianBandMatrix.hh:310, gathers into band storage; the GPU chase
+    works on a dense window of the band)."""
     s = F.storage
     bc = s.bc
     nb, p, q, pr, pc = bc.nb, bc.p, bc.q, bc.pr, bc.pc
@@ -208,20 +212,23 @@ def gather_band(F, root=0):
         comm.reduce(stack, root)
     if comm.rank != root:
         return None
-    St = stack.cpu()
-    B = torch.zeros(n, n, dtype=dt)
+    big = 1 << 40
+    lower = (1, big, 1, 0, 1, 0, 0, 0, 0)         # row >= col (TriMask tuple)
+    supper = (2, big, 1, 0, 1, 0, 0, 0, -1)       # row < col
+    B = ops.colmajor_zeros(n, n, dt, dev)
     for k in range(nt):
         c0 = k * nb
         kb = min(nb, n - c0)
-        B[c0:c0 + kb, c0:c0 + kb] = St[0:kb, c0:c0 + kb]
+        ops.gecopy_mask(stack[0:kb, c0:c0 + kb], B[c0:c0 + kb, c0:c0 + kb], lower, real_diag=True)
         if k + 1 < nt:
             kr = min(nb, n - (k + 1) * nb)
-            B[c0 + nb:c0 + nb + kr, c0:c0 + kb] = St[nb:nb + kr, c0:c0 + kb]
-    L = torch.tril(B)
-    H = L + torch.tril(L, -1).mH
-    if H.is_complex():
-        H.diagonal().imag.zero_()
-    return H.t().contiguous().t()
+            ops.gecopy(stack[nb:nb + kr, c0:c0 + kb], B[c0 + nb:c0 + nb + kr, c0:c0 + kb], uplo='U')
+    # the upper triangle: the strictly lower band conjugate-transposed
+    Bt = ops.colmajor_empty(n, n, dt, dev)
+    ops.gecopy(B, Bt, trans=conj_trans(dt))
+    ops.gecopy_mask(Bt, Bt, supper)
+    ops.geadd(1.0, Bt, 1.0, B)
+    return B
 
 
 def unmtr_he2hb_dist(F, Fac: He2hbDistFactors, Z):
