@@ -103,18 +103,21 @@ def trtrm(A, opts=None) -> int:
         if _single(A):
             lb = A.local_block()
             F = lb.data[:n, :n]
+            big = 1 << 40
+            tri = (1 if uplo == Uplo.Lower else 2, big, 1, 0, 1, 0, 0, 0, 0)      # the stored triangle
+            other = (2 if uplo == Uplo.Lower else 1, big, 1, 0, 1, 0, 0, 0, -1)   # the rest, strictly
+            X = ops.colmajor_empty(n, n, F.dtype, F.device)
+            ops.gecopy_mask(F, X, tri)                           # X = tril(F) / triu(F)
             if uplo == Uplo.Lower:
-                L = torch.tril(F)
-                X = ops.colmajor_empty(n, n, F.dtype, F.device)
-                X.copy_(L)
                 ops.trmm('L', 'L', ct, 'N', 1.0, F, X)          # X = L^H L
-                F.copy_(torch.where(torch.ones_like(F, dtype=torch.bool).tril(), X, F))
             else:
-                U = torch.triu(F)
-                X = ops.colmajor_empty(n, n, F.dtype, F.device)
-                X.copy_(U)
                 ops.trmm('R', 'U', ct, 'N', 1.0, F, X)          # X = U U^H
-                F.copy_(torch.where(torch.ones_like(F, dtype=torch.bool).triu(), X, F))
+            # F's stored triangle <- X, its other part unchanged (kernels only)
+            W = ops.colmajor_empty(n, n, F.dtype, F.device)
+            ops.gecopy_mask(F, W, other)
+            ops.gecopy_mask(X, X, tri)
+            ops.geadd(1.0, W, 1.0, X)
+            F.copy_(X)
             s.mark_local_modified(s.origin_slot)
             return 0
         # distributed: X = stored triangle of A (zeros elsewhere), then the
