@@ -311,6 +311,47 @@ void run(int p, int q, int me) {
         }
         report("trsm_lc", rel<T>(lx, want));
     }
+    // ---- views: potrf of a trailing principal block through a tile-aligned
+    //      sub view (zero-copy, the parent's storage), potrs through a
+    //      from_device wrapper of another matrix's local buffer
+    {
+        int64_t lcm = p;
+        while (lcm % q) lcm += p;
+        const int64_t nt = (n + nb - 1) / nb;
+        if (lcm < nt) {
+            sn::HermitianMatrix<T> Af(sn::Uplo::Lower, n, nb, p, q);
+            Af.generate(sn::Gen::HermitianPositiveDefinite, 7);
+            sn::HermitianMatrix<T> V(sn::Uplo::Lower, Af.sub(lcm, nt, lcm, nt));
+            const int64_t nv = V.m(), o = lcm * nb;
+            info = sn::potrf(V);
+            std::vector<T> lv((size_t)nv * nv);
+            V.to_host(lv.data(), nv);
+            for (int64_t j = 0; j < nv; ++j)
+                for (int64_t i = 0; i < j; ++i) lv[i + j * nv] = T(0);
+            auto llh = mul<T>('N', 'C', nv, nv, nv, lv, nv, lv, nv);
+            std::vector<std::complex<double>> want((size_t)nv * nv);
+            for (int64_t j = 0; j < nv; ++j)
+                for (int64_t i = 0; i < nv; ++i) {
+                    const T x = i >= j ? a0[(o + i) + (o + j) * n] : cj(a0[(o + j) + (o + i) * n]);
+                    want[i + j * nv] = {std::real(x), std::imag(x)};
+                }
+            for (size_t i = 0; i < llh.size(); ++i) llh[i] -= want[i];
+            report(info ? "sub_potrf-FAILED" : "sub_potrf", rel<T>(llh, want));
+        } else {
+            report("sub_potrf", 0.0);
+        }
+        sn::Matrix<T> Bd(n, nrhs, nb, p, q);
+        Bd.from_host(b0.data(), n);
+        sn::Matrix<T> W = sn::Matrix<T>::from_device(Bd.data(), Bd.lld(), n, nrhs, nb, p, q);
+        sn::potrs(A, W);
+        std::vector<T> xw((size_t)n * nrhs);
+        Bd.to_host(xw.data(), n);                    // the solve landed in Bd's own buffer
+        auto ax = mul<T>('N', 'N', n, nrhs, n, a0, n, xw, n);
+        auto want = widen(b0);
+        for (size_t i = 0; i < ax.size(); ++i) ax[i] -= want[i];
+        report("from_device_potrs", rel<T>(ax, want));
+    }
+
     // ---- trtri of the Cholesky factor: L^{-1} L = I; trtrm: L^H L
     {
         sn::Matrix<T> Li(n, n, nb, p, q);

@@ -98,6 +98,14 @@ public:
     void from_local_host(const T* Aloc, int64_t lld);
     void to_local_host(T* Aloc, int64_t lld) const;
     std::shared_ptr<Storage> storage() const { return s_; }
+    // Zero-copy wrapper of a DEVICE buffer that holds this rank's local block
+    // in ScaLAPACK layout (SLATE fromScaLAPACK / fromDevices); the caller
+    // keeps ownership, lld >= mloc (an even lld keeps the 16-byte MFMA loads).
+    static Matrix from_device(T* d_local, int64_t lld, int64_t m, int64_t n, int64_t nb, int p = 1, int q = 1);
+    // View of the tiles [i0, i1) x [j0, j1) sharing this storage (SLATE
+    // Matrix::sub); i0 a multiple of p and j0 of q, so the view's tile (0, 0)
+    // stays on process (0, 0) and every driver takes it as it is.
+    Matrix sub(int64_t i0, int64_t i1, int64_t j0, int64_t j1) const;
 
 protected:
     std::shared_ptr<Storage> s_;
@@ -109,6 +117,8 @@ public:
     HermitianMatrix() = default;
     HermitianMatrix(Uplo uplo, int64_t n, int64_t nb, int p = 1, int q = 1)
         : Matrix<T>(n, n, nb, p, q), uplo_(uplo) {}
+    // the uplo triangle of a square matrix or view, sharing its storage
+    HermitianMatrix(Uplo uplo, const Matrix<T>& A) : Matrix<T>(A), uplo_(uplo) {}
     Uplo uplo() const { return uplo_; }
 
 private:

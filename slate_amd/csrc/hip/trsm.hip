@@ -180,6 +180,26 @@ static const T* opblk(const T* A, i64 lda, char trans, i64 r, i64 c) {
     return trans == 'N' ? A + r + c * lda : A + c + r * lda;
 }
 
+// X L^T = alpha B, L n x n lower (the Cholesky panel), recursively halved
+// over the columns: X1 = alpha B1 L11^{-T}; B2 = alpha B2 - X1 L21^T (one
+// MFMA GEMM); X2 = B2 L22^{-T} -- the blocked-inverse strip kernel only on
+// the <= 128-column leaves.  Opt-in (SLATE_AMD_TRSM_RLT_REC=1): measured on
+// MI355X, dpotrf n = 32768 (the panel solve sharing the GPU with the
+// trailing GEMM) 58.4 TF/s with it against 59.1 with the whole-width strip
+// kernel (profiles/r5/potrf_trsm_rec.txt).
+static bool trsm_rlt_rec(i64 m, i64 n, double alpha, const double* L, i64 ldl, double* B, i64 ldb, bool unit,
+                         char trans, hipStream_t s) {
+    static const bool on = [] {
+        const char* e = std::getenv("SLATE_AMD_TRSM_RLT_REC");
+        return e && e[0] == '1';
+    }();
+    if (!on || n <= 128 || m < 1024) return trsm_rlt_fast(m, n, alpha, L, ldl, B, ldb, unit, s);
+    const i64 n1 = ((n / 2 + 63) / 64) * 64;
+    if (!trsm_rlt_rec(m, n1, alpha, L, ldl, B, ldb, unit, trans, s)) return false;
+    gemm_T<double>('N', trans, m, n - n1, n1, -1.0, B, ldb, L + n1, ldl, alpha, B + n1 * ldb, ldb, s);
+    return trsm_rlt_rec(m, n - n1, 1.0, L + n1 + n1 * ldl, ldl, B + n1 * ldb, ldb, unit, trans, s);
+}
+
 template <typename T>
 void trsm(char side, char uplo, char trans, char diag, i64 m, i64 n, T alpha,
           const T* A, i64 lda, T* B, i64 ldb, hipStream_t s) {
@@ -187,7 +207,7 @@ void trsm(char side, char uplo, char trans, char diag, i64 m, i64 n, T alpha,
     if constexpr (std::is_same<T, double>::value) {
         // X L^T = alpha B (the Cholesky panel): blocked-inverse MFMA kernel
         if (side == 'R' && uplo == 'L' && trans != 'N' &&
-            trsm_rlt_fast(m, n, alpha, A, lda, B, ldb, diag == 'U', s))
+            trsm_rlt_rec(m, n, alpha, A, lda, B, ldb, diag == 'U', trans, s))
             return;
         // L X = alpha B (LU's U rows, forward solves): one-launch MFMA kernel
         if (side == 'L' && uplo == 'L' && trans == 'N' && trsm_lln_fast(m, n, alpha, A, lda, B, ldb, diag == 'U', s))

@@ -265,6 +265,51 @@ Matrix<T>::Matrix(int64_t m, int64_t n, int64_t nb, int p, int q) {
     NHIP(hipStreamSynchronize(rt().main));
     s_ = s;
 }
+template <typename T>
+Matrix<T> Matrix<T>::from_device(T* d_local, int64_t lld, int64_t m, int64_t n, int64_t nb, int p, int q) {
+    initialize();
+    if (m < 0 || n < 0 || nb <= 0 || p <= 0 || q <= 0) throw Error("Matrix::from_device: bad dimensions");
+    auto s = std::make_shared<Storage>();
+    s->m = m; s->n = n; s->nb = nb; s->p = p; s->q = q;
+    s->gc = grid_comms(p, q);
+    s->pr = s->gc->pr; s->pc = s->gc->pc;
+    s->mloc = numroc(m, nb, s->pr, p);
+    s->nloc = numroc(n, nb, s->pc, q);
+    if (lld < std::max<i64>(1, s->mloc)) throw Error("Matrix::from_device: lld < local rows");
+    if (!d_local && s->mloc && s->nloc) throw Error("Matrix::from_device: null buffer");
+    s->lld = lld;
+    s->esize = sizeof(T);
+    s->buf = d_local;
+    s->owns = false;
+    Matrix<T> M;
+    M.s_ = s;
+    return M;
+}
+
+template <typename T>
+Matrix<T> Matrix<T>::sub(int64_t i0, int64_t i1, int64_t j0, int64_t j1) const {
+    const Storage& P = *s_;
+    const i64 mt = (P.m + P.nb - 1) / P.nb, nt = (P.n + P.nb - 1) / P.nb;
+    if (i0 < 0 || j0 < 0 || i1 > mt || j1 > nt || i0 > i1 || j0 > j1)
+        throw Error("Matrix::sub: tile range outside the matrix");
+    if (i0 % P.p || j0 % P.q)
+        throw Error("Matrix::sub: the first tile row (column) must be a multiple of p (q)");
+    auto s = std::make_shared<Storage>();
+    s->m = std::min(i1 * P.nb, P.m) - i0 * P.nb;
+    s->n = std::min(j1 * P.nb, P.n) - j0 * P.nb;
+    s->nb = P.nb; s->p = P.p; s->q = P.q; s->pr = P.pr; s->pc = P.pc; s->gc = P.gc;
+    s->mloc = numroc(s->m, P.nb, P.pr, P.p);
+    s->nloc = numroc(s->n, P.nb, P.pc, P.q);
+    s->lld = P.lld;
+    s->esize = P.esize;
+    s->buf = static_cast<char*>(P.buf) + ((i0 / P.p) * P.nb + (j0 / P.q) * P.nb * P.lld) * (i64)P.esize;
+    s->owns = false;
+    s->parent = s_;
+    Matrix<T> M;
+    M.s_ = s;
+    return M;
+}
+
 template <typename T> int64_t Matrix<T>::m() const { return s_->m; }
 template <typename T> int64_t Matrix<T>::n() const { return s_->n; }
 template <typename T> int64_t Matrix<T>::nb() const { return s_->nb; }
@@ -317,16 +362,17 @@ void Matrix<T>::to_local_host(T* Aloc, int64_t ld) const {
         std::memcpy(Aloc + j * ld, h.data() + j * s.mloc, sizeof(T) * s.mloc);
 }
 
+// (a view's rows are a strided window of its parent's buffer: every transfer
+// goes through a contiguous mloc x nloc staging block)
 template <typename T>
 void Matrix<T>::from_host(const T* A, int64_t lda) {
     Storage& s = *s_;
-    std::vector<T> loc((size_t)s.lld * std::max<i64>(s.nloc, 1), T(0));
+    std::vector<T> loc((size_t)std::max<i64>(s.mloc, 1) * std::max<i64>(s.nloc, 1), T(0));
     for (i64 lj = 0; lj < s.nloc; ++lj) {
         const i64 gj = l2g(lj, s.nb, s.q, s.pc);
-        for (i64 li = 0; li < s.mloc; ++li) loc[li + lj * s.lld] = A[l2g(li, s.nb, s.p, s.pr) + gj * lda];
+        for (i64 li = 0; li < s.mloc; ++li) loc[li + lj * s.mloc] = A[l2g(li, s.nb, s.p, s.pr) + gj * lda];
     }
-    upload(data(), loc.data(), loc.size() * sizeof(T), rt().main);
-    NHIP(hipStreamSynchronize(rt().main));
+    from_local_host(loc.data(), std::max<i64>(s.mloc, 1));
 }
 
 // every rank gets the whole matrix: ONE all-gather of the local blocks
@@ -337,11 +383,7 @@ void Matrix<T>::to_host(T* A, int64_t lda) const {
     Runtime& R = rt();
     NHIP(hipDeviceSynchronize());
     if (R.size == 1) {
-        std::vector<T> loc((size_t)s.lld * std::max<i64>(s.nloc, 1));
-        NHIP(hipMemcpyAsync(loc.data(), s.buf, loc.size() * sizeof(T), hipMemcpyDeviceToHost, R.main));
-        NHIP(hipStreamSynchronize(R.main));
-        for (i64 j = 0; j < s.nloc; ++j)
-            for (i64 i = 0; i < s.mloc; ++i) A[i + j * lda] = loc[i + j * s.lld];
+        to_local_host(A, lda);
         return;
     }
     i64 mx_m = 0, mx_n = 0;
@@ -513,8 +555,6 @@ void potrf_tile_k(i64 n, T* A, i64 lda, i64* info, hipStream_t s) {
 template <typename T>
 void trsm_rlc(i64 m, i64 n, const T* L, i64 ldl, T* B, i64 ldb, hipStream_t s) {   // B = B L^{-H}
     if (m <= 0) return;
-    if constexpr (std::is_same<T, double>::value)
-        if (slate_hip::trsm_rlt_fast(m, n, 1.0, L, ldl, B, ldb, false, s)) return;
     slate_hip::trsm<K<T>>('R', 'L', ctrans<T>(), 'N', m, n, kv(T(1)), kp(L), ldl, kp(B), ldb, s);
 }
 

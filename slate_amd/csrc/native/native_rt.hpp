@@ -141,6 +141,7 @@ struct Storage {
     size_t esize = 8;
     void* buf = nullptr;
     bool owns = true;
+    std::shared_ptr<Storage> parent;   // a view keeps the storage it points into alive
     GridComms* gc = nullptr;
     ~Storage() {
         if (buf && owns) (void)hipFree(buf);
