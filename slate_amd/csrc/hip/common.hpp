@@ -191,6 +191,18 @@ struct TriMask {
 // XCD-aware bijective remap of a 1-D block id: blocks b and b+8 share an
 // XCD (round-robin dispatch), so give each XCD a contiguous chunk of the
 // logical tile order (see guide T1, bijective variant).
+// Bijective interleave of n rows in chunks of G: row b = q G + t -> t-th
+// chunk (of ceil / floor n / G rows) + q.  Consecutive rows of a tile group
+// land spread over the whole range: a group of a triangular-masked launch
+// then holds long and short block rows alike (balanced XCD chunks).
+__device__ inline int row_interleave(int b, int n, int G) {
+    if (n <= G) return b;
+    const int q = n / G, r = n % G;
+    const int t = b % G, idx = b / G;
+    const int base = (t < r) ? t * (q + 1) : r * (q + 1) + (t - r) * q;
+    return base + idx;
+}
+
 __device__ inline int xcd_remap(int b, int nblocks) {
     const int NX = 8;
     if (nblocks < NX) return b;

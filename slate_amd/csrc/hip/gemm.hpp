@@ -47,6 +47,11 @@ template <> struct mfma_real<float> {
     __device__ static inline int drow(int lane, int r) { return 4 * (lane >> 4) + r; }
 };
 
+// remap 4: the kept blocks of a lower-masked output form a staircase (block
+// row r keeps block columns [0, ncol[r]), ncol non-decreasing); the grid
+// covers only those, in the grouped column-major order
+constexpr int GEMM_STAIR_MAX = 512;
+
 template <typename T>
 struct GemmArgs {
     i64 m, n, k;
@@ -60,10 +65,40 @@ struct GemmArgs {
     int vecA, vecB;          // 16-byte vector loads allowed
     int group_m;             // tile-order group size
     int remap;               // 0: plain order; 1: XCD-chunked grouped order (full output);
+                             // 3: the same with row-interleaved groups (triangular masks);
                              // 2: compact lower triangle of 8x8 super-tiles (set by launch_real)
     TriMask mask;
     const int* gate;         // optional device predicate (GemmCall::gate)
+    unsigned short ncol[GEMM_STAIR_MAX];   // remap 4: kept block columns per block row
 };
+
+// remap 4: kept block lin (grouped column-major order over the staircase) ->
+// (bm, bn).  A group of G block rows holds sum ncol blocks; inside it column
+// c is kept by the rows with ncol > c -- the group's last k rows.
+template <typename GA>
+__device__ inline void stair_block(const GA& a, int lin, int gm, int& bm, int& bn) {
+    const int G = a.group_m;
+    int rem = lin, r0 = 0;
+    for (;;) {
+        const int r1 = min(gm, r0 + G);
+        int cnt = 0;
+        for (int r = r0; r < r1; ++r) cnt += a.ncol[r];
+        if (rem < cnt || r1 >= gm) break;
+        rem -= cnt;
+        r0 = r1;
+    }
+    const int r1 = min(gm, r0 + G);
+    for (int c = 0;; ++c) {
+        int k = 0;
+        for (int r = r0; r < r1; ++r) k += a.ncol[r] > c;
+        if (rem < k || k == 0) {
+            bm = r1 - k + rem;
+            bn = c;
+            return;
+        }
+        rem -= k;
+    }
+}
 
 // ---------------------------------------------------------------------------
 // Operand loader: stages an R x BK slab of op(X) into LDS.
@@ -173,7 +208,10 @@ gemm_real_kernel(GemmArgs<T> a) {
 
     const int gm = (int)((a.m + BM - 1) / BM), gn = (int)((a.n + BN - 1) / BN);
     int bm, bn;
-    if (a.remap == 2) {
+    if (a.remap == 4) {
+        stair_block(a, xcd_remap(blockIdx.x, gridDim.x), gm, bm, bn);
+        if (bm >= gm || bn >= gn) return;
+    } else if (a.remap == 2) {
         // compact lower triangle (launcher checked that no tile above the
         // diagonal holds a kept element): the grid covers only the 8 x 8
         // super-tiles I >= J, column by column, so the XCD chunks stay
@@ -197,6 +235,9 @@ gemm_real_kernel(GemmArgs<T> a) {
         int gsz = min(gm - first, G);
         int inner = lin - grp * G * gn;
         bm = first + inner % gsz; bn = inner / gsz;
+        // remap 3 (triangular masks): the grouped rows interleaved over the
+        // whole range, so every XCD chunk holds a balanced share of kept blocks
+        if (a.remap == 3) bm = row_interleave(bm, gm, G);
     }
     const i64 m0 = (i64)bm * BM, n0 = (i64)bn * BN;
     if (a.mask.skip_block(m0, min(m0 + BM, a.m), n0, min(n0 + BN, a.n))) return;
@@ -339,7 +380,7 @@ gemm_complex_kernel(GemmArgs<T> a) {
     const int G = a.group_m;
     int grp = lin / (G * gn), first = grp * G, gsz = min(gm - first, G);
     int inner = lin - grp * G * gn;
-    const int bm = first + inner % gsz, bn = inner / gsz;
+    const int bm = a.remap == 3 ? row_interleave(first + inner % gsz, gm, G) : first + inner % gsz, bn = inner / gsz;
     const i64 m0 = (i64)bm * BM, n0 = (i64)bn * BN;
     if (a.mask.skip_block(m0, min(m0 + BM, a.m), n0, min(n0 + BN, a.n))) return;
 

@@ -106,7 +106,10 @@ __global__ void __launch_bounds__(64 * WVM * WVN, OCC) gemm_f64_glds_kernel(Gemm
 
     const int gm = (int)((a.m + BM - 1) / BM), gn = (int)((a.n + BN - 1) / BN);
     int bm, bn;
-    if (a.remap == 2) {
+    if (a.remap == 4) {
+        stair_block(a, xcd_remap(blockIdx.x, gridDim.x), gm, bm, bn);
+        if (bm >= gm || bn >= gn) return;
+    } else if (a.remap == 2) {
         const int lin = xcd_remap(blockIdx.x, gridDim.x);
         const int s = lin >> 6, w = lin & 63;
         const int gsm = (gm + 7) >> 3;
@@ -123,6 +126,7 @@ __global__ void __launch_bounds__(64 * WVM * WVN, OCC) gemm_f64_glds_kernel(Gemm
         const int inner = lin - grp * G * gn;
         bm = first + inner % gsz;
         bn = inner / gsz;
+        if (a.remap == 3) bm = row_interleave(bm, gm, G);
     }
     const i64 m0 = (i64)bm * BM, n0 = (i64)bn * BN;
     if (a.mask.skip_block(m0, min(m0 + BM, a.m), n0, min(n0 + BN, a.n))) return;

@@ -105,6 +105,27 @@ static bool gemm_splitk(const GemmCall& c, int tile, hipStream_t s, Launch&& lau
 // (tools/exp/gemm_trimask.py, 128 x 128 tiles, k = 512): 31744 x 30720
 // 59.0 -> 59.6 TF/s, 8192 x 7168 53.3 -> 54.7 TF/s; used for the 128 x 128
 // variant only.
+// triangular-masked launches that are not the compact triangle: XCD chunks
+// over row-interleaved groups (3, balanced and L2-local) or the plain order
+// (0); SLATE_AMD_GEMM_MASK_REMAP overrides
+static inline int gemm_mask_remap() {
+    static const int v = [] {
+        const char* e = std::getenv("SLATE_AMD_GEMM_MASK_REMAP");
+        return e ? std::atoi(e) : 3;
+    }();
+    return v;
+}
+
+// tile-order group height (block rows swept together); SLATE_AMD_GEMM_GROUP overrides 8
+static inline int gemm_group() {
+    static const int v = [] {
+        const char* e = std::getenv("SLATE_AMD_GEMM_GROUP");
+        const int g = e ? std::atoi(e) : 8;
+        return g >= 1 ? g : 8;
+    }();
+    return v;
+}
+
 static inline bool gemm_tri_enabled() {
     const char* e = std::getenv("SLATE_AMD_GEMM_TRI");  // read per launch: tests and sweeps toggle it
     return !(e && e[0] == '0');
@@ -160,6 +181,44 @@ static void launch_glds(const GemmArgs<double>& a, i64 nblk, int batch, hipStrea
     HIP_LAUNCH_CHECK();
 }
 
+// remap 4 (gemm.hpp stair_block): a lower mask whose kept blocks per block
+// row are a prefix (block-cyclic lower triangles of a rank's local block:
+// global rows and columns grow with local ones); the grid then holds only
+// the kept blocks, so the resident workgroups stay within a few tile groups
+// (L2 reuse) instead of spreading over every group the skipped blocks race
+// through.  Measured on MI355X, the 2x4 dpotrf trailing update of rank 0
+// (15872 x 7168 x 512, 47 % kept): see profiles/r5/masked_gemm_stair.txt.
+// Returns the kept block count (0: not eligible).  SLATE_AMD_GEMM_STAIR=0
+// disables.
+template <typename T>
+static i64 stair_blocks(GemmArgs<T>& a, int BM, int BN, int batch) {
+    static const bool on = [] {
+        const char* e = std::getenv("SLATE_AMD_GEMM_STAIR");
+        return !(e && e[0] == '0');
+    }();
+    const TriMask& k = a.mask;
+    if (!on || k.mode != 1 || batch != 1) return 0;
+    const i64 gm = (a.m + BM - 1) / BM, gn = (a.n + BN - 1) / BN;
+    if (gm > GEMM_STAIR_MAX || gn > 65535 || gm * gn < 256) return 0;
+    i64 total = 0, prev = 0;
+    for (i64 r = 0; r < gm; ++r) {
+        const i64 r0 = r * BM, r1 = std::min(r0 + BM, a.m);
+        // first skipped block column (skips are monotone in bn: gcol grows)
+        i64 lo = 0, hi = gn;
+        while (lo < hi) {
+            const i64 mid = (lo + hi) / 2;
+            const i64 c0 = mid * BN;
+            if (k.skip_block(r0, r1, c0, std::min(c0 + BN, a.n))) hi = mid;
+            else lo = mid + 1;
+        }
+        if (lo < prev) return 0;     // not a staircase
+        a.ncol[r] = (unsigned short)lo;
+        prev = lo;
+        total += lo;
+    }
+    return total;
+}
+
 template <typename T, bool TA, bool TB, bool PTRS>
 static void launch_real(const GemmArgs<T>& a0, int batch, hipStream_t s) {
     GemmArgs<T> a = a0;
@@ -168,7 +227,9 @@ static void launch_real(const GemmArgs<T>& a0, int batch, hipStream_t s) {
         if (!PTRS && g128 < 512 && a.k > 0 && a.k % 16 == 0 && a.vecA && a.vecB && gemm_glds_enabled()) {
             const i64 gm = (a.m + 63) / 64, gn = (a.n + 63) / 64;
             if (gm == 0 || gn == 0 || batch == 0) return;
-            launch_glds<TA, TB, 64>(a, gm * gn, batch, s);
+            i64 nb64 = gm * gn;
+            if (i64 t = stair_blocks(a, 64, 64, batch)) { a.remap = 4; nb64 = t; }
+            launch_glds<TA, TB, 64>(a, nb64, batch, s);
             return;
         }
         if (g128 < gemm_small_tiles() && !(a.k > 0 && a.k % 16 == 0 && a.vecA && a.vecB && gemm_glds_enabled())) {
@@ -191,7 +252,16 @@ static void launch_real(const GemmArgs<T>& a0, int batch, hipStream_t s) {
     i64 gm = (a.m + BM - 1) / BM, gn = (a.n + BN - 1) / BN;
     if (gm == 0 || gn == 0 || batch == 0) return;
     i64 nblk = gm * gn;
-    if (i64 t = tri_blocks(a, BM, BN)) { a.remap = 2; nblk = t; }
+    {
+        // the exact staircase when it launches clearly fewer blocks than the
+        // compact 8 x 8 super-tile triangle (block-cyclic grids: 3248 vs
+        // 5824 blocks for the 2x4 step above; a one-rank triangle: ~3 %)
+        const i64 t = tri_blocks(a, BM, BN);
+        GemmArgs<T> b = a;
+        const i64 t2 = stair_blocks(b, BM, BN, batch);
+        if (t2 && (!t || t2 < t - t / 8)) { a = b; a.remap = 4; nblk = t2; }
+        else if (t) { a.remap = 2; nblk = t; }
+    }
     if constexpr (sizeof(T) == 8 && !PTRS) {
         if (a.k > 0 && a.k % 16 == 0 && a.vecA && a.vecB && gemm_glds_enabled()) {
             launch_glds<TA, TB, 128>(a, nblk, batch, s);
@@ -242,9 +312,9 @@ void gemm_real(const GemmCall& c, hipStream_t s) {
     // checked conservatively by the caller via c.vec_ok.
     a.vecA = c.vec_ok && (c.lda % VEC == 0) && (ptrs || (aligned16(c.A) && c.strideA % VEC == 0));
     a.vecB = c.vec_ok && (c.ldb % VEC == 0) && (ptrs || (aligned16(c.B) && c.strideB % VEC == 0));
-    a.group_m = 8;
+    a.group_m = gemm_group();
     a.mask = c.mask;
-    a.remap = c.mask.mode == 0 ? 1 : 0;
+    a.remap = c.mask.mode == 0 ? 1 : gemm_mask_remap();
     a.gate = c.gate;
     if (c.m <= 0 || c.n <= 0) return;
     dispatch_real<T>(c.transA != 'N', c.transB != 'N', ptrs, a, (int)c.batch, s);
@@ -291,9 +361,9 @@ void gemm_complex(const GemmCall& c, hipStream_t s) {
     const bool ptrs = c.Aptrs != nullptr;
     a.vecA = c.vec_ok && (c.lda % VEC == 0) && (ptrs || (aligned16(c.A) && c.strideA % VEC == 0));
     a.vecB = c.vec_ok && (c.ldb % VEC == 0) && (ptrs || (aligned16(c.B) && c.strideB % VEC == 0));
-    a.group_m = 8;
+    a.group_m = gemm_group();
     a.mask = c.mask;
-    a.remap = c.mask.mode == 0 ? 1 : 0;
+    a.remap = c.mask.mode == 0 ? 1 : gemm_mask_remap();
     a.gate = c.gate;
     if (c.m <= 0 || c.n <= 0) return;
     if (ptrs) dispatch_cplx<T, true>(c.transA, c.transB, a, (int)c.batch, s);
