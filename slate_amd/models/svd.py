@@ -258,10 +258,11 @@ def svd(A, S=None, U=None, VH=None, opts=None):
             Ad.mul_(scale)
         F1 = ge2tb(Ad, nb)
         k = n
-        band = Ad[:k, :k]
-        i = torch.arange(k, device=band.device)
-        dlt = i[None, :] - i[:, None]
-        band = torch.where((dlt >= 0) & (dlt <= nb), band, torch.zeros_like(band))
+        # the upper band 0 <= j - i <= nb of the reduced matrix (two masked
+        # copies: upper triangle, then rows within nb of the diagonal)
+        band = ops.colmajor_empty(k, k, Ad.dtype, Ad.device)
+        ops.gecopy_mask(Ad[:k, :k], band, (2, 1 << 40, 1, 0, 1, 0, 0, 0, 0))
+        ops.gecopy_mask(band, band, (1, 1 << 40, 1, 0, 1, 0, 0, 0, nb))
         d, e, F2 = tb2bd(band, nb)
         wantU = U is not None
         wantV = VH is not None

@@ -198,15 +198,15 @@ def gather_upper_band(G, root=0):
         comm.reduce(stack, root)
     if comm.rank != root:
         return None
-    St = stack.cpu()
-    B = torch.zeros(n, n, dtype=dt)
+    # assembled on the root's device by masked copies (no host n x n)
+    B = ops.colmajor_zeros(n, n, dt, dev)
     for j in range(nt):
         c0 = j * nb
         kb = min(nb, n - c0)
-        B[c0:c0 + kb, c0:c0 + kb] = torch.triu(St[nb:nb + kb, c0:c0 + kb])
+        ops.gecopy(stack[nb:nb + kb, c0:c0 + kb], B[c0:c0 + kb, c0:c0 + kb], uplo='U')
         if j >= 1:
-            B[c0 - nb:c0, c0:c0 + kb] = torch.tril(St[0:nb, c0:c0 + kb])
-    return B.t().contiguous().t()
+            ops.gecopy(stack[0:nb, c0:c0 + kb], B[c0 - nb:c0, c0:c0 + kb], uplo='L')
+    return B
 
 
 def _apply_left(G, Fac, Z):
