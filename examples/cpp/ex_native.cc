@@ -135,7 +135,16 @@ void run(int p, int q, int me) {
     X.generate(sn::Gen::Random, 6);
     std::vector<T> xb((size_t)n * nrhs), xg((size_t)n * nrhs);
     X.to_host(xb.data(), n);
+    sn::lu_exchange_stats(nullptr, nullptr);
     info = sn::gesv(G, ipiv, X);
+    {
+        // p > 1: only the rows that change process row travel
+        long long xb = 0, xr = 0;
+        sn::lu_exchange_stats(&xb, &xr);
+        const bool ok = xb <= xr * G.nloc() * (long long)sizeof(T);
+        report("lu_xchg_bound", ok ? 0.0 : 1.0);
+        if (me == 0 && p > 1) std::printf("lu exchange: %lld bytes sent, %lld rows crossed, nloc %lld\n", xb, xr, (long long)G.nloc());
+    }
     X.to_host(xg.data(), n);
     {
         auto ax = mul<T>('N', 'N', n, nrhs, n, g0, n, xg, n);

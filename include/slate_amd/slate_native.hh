@@ -212,6 +212,9 @@ void trmm(Side side, Uplo uplo, Op op, Diag diag, T alpha, const Matrix<T>& A, M
 // inverses from the factors: potri after potrf (stored triangle), getri after getrf
 template <typename T> int64_t potri(HermitianMatrix<T>& A, const Options& opts = {});
 template <typename T> int64_t getri(Matrix<T>& A, const std::vector<int64_t>& ipiv, const Options& opts = {});
+// p > 1 getrf moves only the rows that change process row: bytes this rank
+// sent and rows that crossed since the previous call
+void lu_exchange_stats(long long* bytes, long long* rows);
 // triangular inverse in place (stored triangle; Unit: the diagonal is not
 // referenced) and the triangular product A <- L^H L (Lower) / U U^H (Upper)
 template <typename T> int64_t trtri(Uplo uplo, Diag diag, Matrix<T>& A, const Options& opts = {});

@@ -21,6 +21,7 @@
 // src/gemmC.cc:39-202, src/work/work_trsm.cc:102-265 (SLATE's OpenMP task
 // DAGs over MPI).
 #include <algorithm>
+#include <atomic>
 #include <limits>
 #include <functional>
 #include <map>
@@ -1096,6 +1097,113 @@ static void permute_rows_dist(Storage& S, const i64* ipiv_d, i64 k1, i64 k2, i64
     }
 }
 
+// Exact row moves of one LU step for p > 1 (models/lu.py _p2p_rows /
+// internal::permuteRows): the step's swap sequence folded on the host into
+// (destination, source) global rows; rows staying inside this process row
+// move locally, rows changing process row travel point-to-point (one
+// batched exchange on the column communicator, rows in destination order
+// on both sides) -- only the rows that change owner move, over every local
+// column range at once.  g_lu_xchg counts the bytes this rank sent.
+static std::vector<std::pair<i64, i64>> fold_moves(const std::vector<i64>& pv, i64 r0) {
+    std::map<i64, i64> cur;                  // position -> original row now there
+    for (size_t i = 0; i < pv.size(); ++i) {
+        const i64 a = r0 + (i64)i, b = r0 + pv[i];
+        if (a == b) continue;
+        const i64 ca = cur.count(a) ? cur[a] : a, cb = cur.count(b) ? cur[b] : b;
+        cur[a] = cb;
+        cur[b] = ca;
+    }
+    std::vector<std::pair<i64, i64>> mv;
+    for (auto& x : cur)
+        if (x.first != x.second) mv.push_back(x);
+    return mv;                               // sorted by destination
+}
+
+static std::atomic<long long> g_lu_xchg_bytes{0}, g_lu_xchg_rows{0};
+
+template <typename T>
+static void p2p_rows(Storage& S, const std::vector<std::pair<i64, i64>>& mv,
+                     const std::vector<std::pair<i64, i64>>& ranges, Comm* colc, hipStream_t s) {
+    i64 W = 0;
+    for (auto& r : ranges) W += std::max<i64>(r.second - r.first, 0);
+    if (W == 0 || mv.empty()) return;
+    const i64 nb = S.nb;
+    const int p = S.p, pr = S.pr;
+    auto own = [&](i64 g) { return (int)((g / nb) % p); };
+    auto loc = [&](i64 g) { return (g / (nb * p)) * nb + g % nb; };
+    std::map<int, std::vector<i64>> sends, recvs;
+    std::vector<i64> ld, ls;
+    long long cross = 0;
+    for (auto& x : mv) {
+        const int od = own(x.first), os = own(x.second);
+        cross += od != os;
+        if (os == pr && od != pr) sends[od].push_back(loc(x.second));
+        else if (od == pr && os != pr) recvs[os].push_back(loc(x.first));
+        else if (od == pr && os == pr) { ld.push_back(loc(x.first)); ls.push_back(loc(x.second)); }
+    }
+    // every index list in one upload: [sends per peer | recvs per peer | ls | ld]
+    std::vector<i64> flat;
+    std::vector<std::pair<int, size_t>> soff, roff;
+    for (auto& kv2 : sends) { soff.push_back({kv2.first, flat.size()}); flat.insert(flat.end(), kv2.second.begin(), kv2.second.end()); }
+    for (auto& kv2 : recvs) { roff.push_back({kv2.first, flat.size()}); flat.insert(flat.end(), kv2.second.begin(), kv2.second.end()); }
+    const size_t lso = flat.size();
+    flat.insert(flat.end(), ls.begin(), ls.end());
+    const size_t ldo = flat.size();
+    flat.insert(flat.end(), ld.begin(), ld.end());
+    if (flat.empty()) return;
+    Scratch idx(flat.size() * sizeof(i64), s);
+    upload(idx.p, flat.data(), flat.size() * sizeof(i64), s);
+    const i64* id = idx.as<i64>();
+    T* buf = static_cast<T*>(S.buf);
+    // gather c rows (local indices at id + o) of every range into X (c x W)
+    auto gather = [&](T* X, i64 c, size_t o) {
+        i64 off = 0;
+        for (auto& r : ranges) {
+            const i64 w = r.second - r.first;
+            if (w <= 0) continue;
+            slate_hip::permute_rows_gather<K<T>>(c, w, kp(buf + r.first * S.lld), S.lld, kp(X + off * c), c, id + o, s);
+            off += w;
+        }
+    };
+    auto scatter = [&](const T* X, i64 c, size_t o) {
+        i64 off = 0;
+        for (auto& r : ranges) {
+            const i64 w = r.second - r.first;
+            if (w <= 0) continue;
+            slate_hip::permute_rows_scatter<K<T>>(c, w, kp(X + off * c), c, kp(buf + r.first * S.lld), S.lld, id + o, s);
+            off += w;
+        }
+    };
+    std::vector<std::unique_ptr<Scratch>> bufs;
+    std::vector<P2P> ops;
+    std::vector<std::tuple<Scratch*, i64, size_t>> unpack;
+    long long sent = 0;
+    for (auto& so : soff) {
+        const i64 c = (i64)sends[so.first].size();
+        bufs.push_back(std::make_unique<Scratch>((size_t)c * W * sizeof(T), s));
+        gather(bufs.back()->as<T>(), c, so.second);
+        ops.push_back({true, so.first, bufs.back()->p, (size_t)c * W * sizeof(T)});
+        sent += (long long)c * W * sizeof(T);
+    }
+    for (auto& ro : roff) {
+        const i64 c = (i64)recvs[ro.first].size();
+        bufs.push_back(std::make_unique<Scratch>((size_t)c * W * sizeof(T), s));
+        ops.push_back({false, ro.first, bufs.back()->p, (size_t)c * W * sizeof(T)});
+        unpack.emplace_back(bufs.back().get(), c, ro.second);
+    }
+    const i64 nl = (i64)ls.size();
+    std::unique_ptr<Scratch> tmp;
+    if (nl) {                                // all local sources read before any is overwritten
+        tmp = std::make_unique<Scratch>((size_t)nl * W * sizeof(T), s);
+        gather(tmp->as<T>(), nl, lso);
+    }
+    if (!ops.empty()) colc->exchange(ops, s);
+    for (auto& u : unpack) scatter(std::get<0>(u)->as<T>(), std::get<1>(u), std::get<2>(u));
+    if (nl) scatter(tmp->as<T>(), nl, ldo);
+    g_lu_xchg_bytes += sent;
+    g_lu_xchg_rows += cross;
+}
+
 // LU of the p x q panel column k (kb columns at local column lck of the
 // process column that owns it): rows stay on their owners, one record
 // all-gather per column (lu_dist_step), recursion halves joined by the
@@ -1176,6 +1284,13 @@ static void panel_dist(Storage& S, i64 k, i64 kb, i64 lck, i64* ipiv_d, i64* inf
         copy2d(Tt + cm + c0 * kb, kb, V, 2 * (c1 - cm), c1 - cm, cm - c0, s);
     };
     rec_fn(0, kb);
+}
+
+// bytes this rank sent and rows that changed process row in the exact LU
+// row exchanges since the last call (tests, examples)
+void lu_exchange_stats(long long* bytes, long long* rows) {
+    if (bytes) *bytes = g_lu_xchg_bytes.exchange(0);
+    if (rows) *rows = g_lu_xchg_rows.exchange(0);
 }
 
 template <typename T>
@@ -1268,6 +1383,12 @@ int64_t getrf(Matrix<T>& A, std::vector<int64_t>& ipiv_out, const Options& opts)
         //      block, one GEMM (models/lu.py _getrf_general)
         Comm* colc = gc->col.get();
         Comm* rowc = gc->row.get();
+        // SLATE_AMD_NATIVE_LU_XCHG=allreduce: the owner-masked all-reduce of
+        // 2 kb rows x every local column per step instead of the exact moves
+        static const bool p2p = [] {
+            const char* e = std::getenv("SLATE_AMD_NATIVE_LU_XCHG");
+            return !(e && std::strcmp(e, "allreduce") == 0);
+        }();
         // panel-relative global rows of my panel rows, every step, uploaded
         // once (no host synchronisation inside the loop)
         std::vector<i64> gflat, goff((size_t)kt + 1, 0);
@@ -1303,6 +1424,29 @@ int64_t getrf(Matrix<T>& A, std::vector<int64_t>& ipiv_out, const Options& opts)
             }
             if (q > 1) rowc->bcast(pack.p, lbytes + tbytes + (size_t)kb * sizeof(i64), ck, ps);
             dcopy(ipiv_d + r0, pv, (size_t)kb * sizeof(i64), ps);
+            if (p2p) {
+                // exact moves: the step's pivots to the host (this path runs
+                // on one stream, the panel's, so the wait costs no overlap)
+                std::vector<i64> hpv((size_t)kb);
+                NHIP(hipMemcpyAsync(hpv.data(), pv, (size_t)kb * sizeof(i64), hipMemcpyDeviceToHost, ps));
+                NHIP(hipStreamSynchronize(ps));
+                p2p_rows<T>(S, fold_moves(hpv, r0), {{lc1, nloc}, {0, lck}}, colc, ps);
+                const i64 w = nloc - lc1;
+                if (w > 0) {
+                    // U rows on the window's process row, then down the column
+                    Scratch Ub((size_t)kb * w * sizeof(T), ps);
+                    if (pr == rk) {
+                        slate_hip::trsm<K<T>>('L', 'L', 'N', 'U', kb, w, kv(T(1)), kp(Tt), kb,
+                                              kp(buf + lr_k + lc1 * lld), lld, ps);
+                        copy2d(Ub.as<T>(), kb, buf + lr_k + lc1 * lld, lld, kb, w, ps);
+                    }
+                    colc->bcast(Ub.p, (size_t)kb * w * sizeof(T), rk, ps);
+                    if (mloc > lr1)
+                        gemm_k<T>('N', 'N', mloc - lr1, w, kb, T(-1), Lp + (lr1 - lr_k), std::max<i64>(nmine, 1),
+                                  Ub.as<T>(), kb, T(1), buf + lr1 + lc1 * lld, lld, ps);
+                }
+                continue;
+            }
             // every local column except the panel's own: interchanges, then
             // (trailing columns) U rows and the update
             auto trailing = [&](i64 c0, i64 c1) {

@@ -119,7 +119,7 @@ def _assert_checks(checks, out):
                                                    "norm_tri_fro", "heev", "heev_orth", "heev_values",
                                                    "gecondest", "svd", "svd_orth", "svd_wide", "svd_wide_orth", "geqrf", "geqrf_wide", "gels_grid",
                                                    "trsm_lt", "trsm_rn", "trsm_rc", "trtri", "trtrm", "gesv_nopiv",
-                                                   "cholqr", "cholqr_orth", "gelqf", "sub_potrf", "from_device_potrs",
+                                                   "cholqr", "cholqr_orth", "gelqf", "sub_potrf", "from_device_potrs", "lu_xchg_bound",
                                                    "svd_values")]
     for name in names:
         assert name in checks, (name, out)
