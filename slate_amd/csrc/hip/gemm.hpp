@@ -51,6 +51,7 @@ template <> struct mfma_real<float> {
 // row r keeps block columns [0, ncol[r]), ncol non-decreasing); the grid
 // covers only those, in the grouped column-major order
 constexpr int GEMM_STAIR_MAX = 512;
+constexpr int GEMM_STAIR_GROUPS = 128;   // remap 4: at most this many row groups
 
 template <typename T>
 struct GemmArgs {
@@ -70,34 +71,44 @@ struct GemmArgs {
     TriMask mask;
     const int* gate;         // optional device predicate (GemmCall::gate)
     unsigned short ncol[GEMM_STAIR_MAX];   // remap 4: kept block columns per block row
+    unsigned gpre[GEMM_STAIR_GROUPS + 1];  // remap 4: kept blocks before each row group
 };
 
 // remap 4: kept block lin (grouped column-major order over the staircase) ->
-// (bm, bn).  A group of G block rows holds sum ncol blocks; inside it column
-// c is kept by the rows with ncol > c -- the group's last k rows.
+// (bm, bn).  A group of G block rows holds gpre[g + 1] - gpre[g] blocks
+// (prefix sums filled by the launcher); inside it column c is kept by the
+// rows with ncol > c -- the group's last k rows -- and the blocks before
+// column c number F(c) = sum_r min(ncol[r], c).  Both searches are binary
+// (O(log) scalar loads per block: the former linear walk cost up to
+// gn * G dependent loads per workgroup, measurable on tall local blocks).
 template <typename GA>
 __device__ inline void stair_block(const GA& a, int lin, int gm, int& bm, int& bn) {
     const int G = a.group_m;
-    int rem = lin, r0 = 0;
-    for (;;) {
-        const int r1 = min(gm, r0 + G);
-        int cnt = 0;
-        for (int r = r0; r < r1; ++r) cnt += a.ncol[r];
-        if (rem < cnt || r1 >= gm) break;
-        rem -= cnt;
-        r0 = r1;
+    const int ng = (gm + G - 1) / G;
+    int lo = 0, hi = ng - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((int)a.gpre[mid] <= lin) lo = mid;
+        else hi = mid - 1;
     }
-    const int r1 = min(gm, r0 + G);
-    for (int c = 0;; ++c) {
-        int k = 0;
-        for (int r = r0; r < r1; ++r) k += a.ncol[r] > c;
-        if (rem < k || k == 0) {
-            bm = r1 - k + rem;
-            bn = c;
-            return;
-        }
-        rem -= k;
+    int rem = lin - (int)a.gpre[lo];
+    const int r0 = lo * G, r1 = min(gm, r0 + G);
+    auto F = [&](int c) {
+        int f = 0;
+        for (int r = r0; r < r1; ++r) f += min((int)a.ncol[r], c);
+        return f;
+    };
+    int cl = 0, ch = (int)a.ncol[r1 - 1] - 1;
+    while (cl < ch) {
+        const int mid = (cl + ch + 1) >> 1;
+        if (F(mid) <= rem) cl = mid;
+        else ch = mid - 1;
     }
+    rem -= F(cl);
+    int k = 0;
+    for (int r = r0; r < r1; ++r) k += (int)a.ncol[r] > cl;
+    bm = rem < k ? r1 - k + rem : gm;    // gm: out of range (never for lin < total)
+    bn = cl;
 }
 
 // ---------------------------------------------------------------------------

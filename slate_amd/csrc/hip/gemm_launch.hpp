@@ -199,7 +199,8 @@ static i64 stair_blocks(GemmArgs<T>& a, int BM, int BN, int batch) {
     const TriMask& k = a.mask;
     if (!on || k.mode != 1 || batch != 1) return 0;
     const i64 gm = (a.m + BM - 1) / BM, gn = (a.n + BN - 1) / BN;
-    if (gm > GEMM_STAIR_MAX || gn > 65535 || gm * gn < 256) return 0;
+    const int G = a.group_m >= 1 ? a.group_m : 1;
+    if (gm > GEMM_STAIR_MAX || gn > 65535 || gm * gn < 256 || (gm + G - 1) / G > GEMM_STAIR_GROUPS) return 0;
     i64 total = 0, prev = 0;
     for (i64 r = 0; r < gm; ++r) {
         const i64 r0 = r * BM, r1 = std::min(r0 + BM, a.m);
@@ -213,9 +214,11 @@ static i64 stair_blocks(GemmArgs<T>& a, int BM, int BN, int batch) {
         }
         if (lo < prev) return 0;     // not a staircase
         a.ncol[r] = (unsigned short)lo;
+        if (r % G == 0) a.gpre[r / G] = (unsigned)total;
         prev = lo;
         total += lo;
     }
+    a.gpre[(gm + G - 1) / G] = (unsigned)total;
     return total;
 }
 

@@ -139,6 +139,18 @@ def _potrf_lower(A, opts):
     # tile rows per row-broadcast chunk after the first (SLATE_AMD_POTRF_CHUNK)
     chunk_tiles = max(1, int(os.environ.get("SLATE_AMD_POTRF_CHUNK", "4")))
     esz = torch.empty(0, dtype=dtype).element_size()
+    # step pairs (SLATE_AMD_POTRF_PAIR=1, lookahead 1 with diag-first): the
+    # trailing update of the pair's first step is deferred and applied with
+    # the second's as ONE K = 2 nb GEMM; the second step's lookahead column
+    # and diagonal tile take the deferred panel as an extra K = nb product
+    # (panel / diag streams, off the big GEMM).  Opt-in: once the exact
+    # staircase grid stopped losing L2 reuse on tall / wide local blocks
+    # (K = 512 trailing GEMM of 1x2 rank 0 at n = 32768: 42 -> 59 TF/s), the
+    # extra panel-stream products cost more than K = 1024 gains -- loopback
+    # n = 32768 rank 0: 1x2 118.8 ms off vs 124.0 on, 2x2 64.4 vs 68.2, 2x4
+    # 38.8 vs 41.4, 2x1 114.8 vs 112.3 (profiles/r5/critpath_2x4.md)
+    pair = la == 1 and diag_first and os.environ.get("SLATE_AMD_POTRF_PAIR", "0") == "1"
+    pend = None
     POTRF_BCAST_STATS.clear()
     ss.fork()
     for t in range(nt):
@@ -154,6 +166,8 @@ def _potrf_lower(A, opts):
         lr1, lc1 = min(lr1, lr_end), min(lc1, lc_end)
         own_col = (g % q) == pc
         own_diag = own_col and (g % p) == pr
+        prev, pend = pend, None
+        defer = pair and prev is None and t + 1 < nt
         with ss.use(ss.panel):
             # panel column g: every trailing update of steps <= t-la-1 (the
             # first column of step t-la-1's trailing update is this one)
@@ -216,6 +230,9 @@ def _potrf_lower(A, opts):
                             with trace_block("potrf::diag_first"):
                                 if pc == g1 % q:
                                     D1 = buf[lr1:lr1 + kb1, lc1:lc1 + kb1]
+                                    if prev is not None:
+                                        Pp = prev["Prow"][lr1 - prev["lr1"]:lr1 - prev["lr1"] + kb1]
+                                        ops.gemm(-1.0, Pp, Pp, 1.0, D1, 'N', ct, (1, 1 << 40, 1, 0, 1, 0, 0, 0, 0))
                                     ops.gemm(-1.0, Pt, Pt, 1.0, D1, 'N', ct, (1, 1 << 40, 1, 0, 1, 0, 0, 0, 0))
                                     ops.potrf('L', D1, infos[t + 1:t + 2])
                                     ev_diag[t + 1] = ss.event(ss.diag)
@@ -233,25 +250,33 @@ def _potrf_lower(A, opts):
             if t >= 1 and la > 0:
                 ss.wait(ss.panel, ev_tr[t - 1])
             diag_done = bool(kb1 and t + 1 in ev_diag and pr == (g + 1) % p and pc == (g + 1) % q)
+            # the lookahead column's products: the deferred panel of the
+            # pair's first step (its rows from local row lr1, its transposed
+            # rows from local column lc1), then this step's panel
+            srcs = [(Prow, Lla, 0, 0)]
+            if prev is not None:
+                srcs.insert(0, (prev["Prow"], prev["Lcol"], lr1 - prev["lr1"], lc1 - prev["loff"]))
             for ci, (ra, rb) in enumerate(chunks):
                 if ci:
                     land(ci)
                 if lc_la <= lc1:
                     continue
-                if diag_done:
-                    # the diagonal tile of g+1 is already updated and factored:
-                    # its column below it, then the other lookahead columns
-                    a1 = max(ra, kb1)
-                    if rb > a1:
-                        ops.gemm(-1.0, Prow[a1:rb], Lla[0:kb1], 1.0, buf[lr1 + a1:lr1 + rb, lc1:lc1 + kb1], 'N', ct,
-                                 (1, nb, p, pr, q, pc, lr1 + a1, lc1, 0))
-                    if lc_la > lc1 + kb1:
-                        ops.gemm(-1.0, Prow[ra:rb], Lla[kb1:lc_la - lc1], 1.0, buf[lr1 + ra:lr1 + rb, lc1 + kb1:lc_la],
-                                 'N', ct, (1, nb, p, pr, q, pc, lr1 + ra, lc1 + kb1, 0))
-                else:
-                    mask = (1, nb, p, pr, q, pc, lr1 + ra, lc1, 0)
-                    ops.gemm(-1.0, Prow[ra:rb], Lla[0:lc_la - lc1], 1.0, buf[lr1 + ra:lr1 + rb, lc1:lc_la], 'N', ct,
-                             mask)
+                for Pk, Lk, o, lo in srcs:
+                    if diag_done:
+                        # the diagonal tile of g+1 is already updated and factored:
+                        # its column below it, then the other lookahead columns
+                        a1 = max(ra, kb1)
+                        if rb > a1:
+                            ops.gemm(-1.0, Pk[o + a1:o + rb], Lk[lo:lo + kb1], 1.0, buf[lr1 + a1:lr1 + rb, lc1:lc1 + kb1],
+                                     'N', ct, (1, nb, p, pr, q, pc, lr1 + a1, lc1, 0))
+                        if lc_la > lc1 + kb1:
+                            ops.gemm(-1.0, Pk[o + ra:o + rb], Lk[lo + kb1:lo + lc_la - lc1], 1.0,
+                                     buf[lr1 + ra:lr1 + rb, lc1 + kb1:lc_la], 'N', ct,
+                                     (1, nb, p, pr, q, pc, lr1 + ra, lc1 + kb1, 0))
+                    else:
+                        mask = (1, nb, p, pr, q, pc, lr1 + ra, lc1, 0)
+                        ops.gemm(-1.0, Pk[o + ra:o + rb], Lk[lo:lo + lc_la - lc1], 1.0, buf[lr1 + ra:lr1 + rb, lc1:lc_la],
+                                 'N', ct, mask)
             # the trailing update's transposed rows: gathered over the same
             # column communicator, from the panel stream, AFTER the lookahead
             # update (off the critical chain; one issue order of collectives
@@ -262,8 +287,36 @@ def _potrf_lower(A, opts):
             else:
                 loff = lc1
             ev_panel = ss.event(ss.panel)
-        # trailing update
         us = ss.update[0]
+        if defer:
+            # the pair's first step: its trailing update waits for the second
+            pend = {"Prow": Prow, "Lcol": Lcol, "lr1": lr1, "loff": loff, "lcg": lcg, "own_col": own_col}
+            if Prow.is_cuda:
+                for x in (Prow, Lcol):
+                    x.record_stream(ss.diag)
+                    x.record_stream(us)
+            with ss.use(us):
+                ev_tr[t] = ss.event(us)
+            continue
+        if prev is not None and nrow and lc_end > lc_la:
+            # K = 2 kb operands: [deferred panel | this panel], rows from lr1,
+            # transposed rows from local column lc_la (= loff)
+            with ss.use(us):
+                ss.wait(us, ev_panel)
+                Pp, Lp = prev["Prow"], prev["Lcol"]
+                if q == 1:
+                    # both panel columns are local and adjacent
+                    Prow = buf[lr1:lr_end, prev["lcg"]:lcg + kb]
+                else:
+                    Pc = ops.colmajor_empty(nrow, Pp.shape[1] + kb, dtype, dev)
+                    Pc[:, :Pp.shape[1]].copy_(Pp[lr1 - prev["lr1"]:])
+                    Pc[:, Pp.shape[1]:].copy_(Prow)
+                    Prow = Pc
+                Lc = ops.colmajor_empty(lc_end - loff, Lp.shape[1] + kb, dtype, dev)
+                Lc[:, :Lp.shape[1]].copy_(Lp[loff - prev["loff"]:])
+                Lc[:, Lp.shape[1]:].copy_(Lcol[:lc_end - loff])
+                Lcol = Lc
+        # trailing update
         with ss.use(us):
             ss.wait(us, ev_panel)
             # split: column g+1+la first (the next step's newest lookahead

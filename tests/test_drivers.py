@@ -79,17 +79,20 @@ def check_herk_trsm_trmm(p, q, dt=torch.float64):
 
 
 def check_potrf(p, q, dt=torch.float64, uplo=Uplo.Lower):
-    n, nb = 96, 16
-    A = herm(n, nb, 11, p, q, dt, uplo)
-    Af = full_herm(A)
-    assert sl.potrf(A) == 0
-    F = D(A)
-    if uplo == Uplo.Lower:
-        L = torch.tril(F)
-        close(L @ L.mH, Af, 1e-12)
-    else:
-        U = torch.triu(F)
-        close(U.mH @ U, Af, 1e-12)
+    # n = 100: an odd tile count with a ragged last tile (the unpaired last
+    # step of the step-pair trailing update, chol.py)
+    for n in (100, 96):
+        nb = 16
+        A = herm(n, nb, 11, p, q, dt, uplo)
+        Af = full_herm(A)
+        assert sl.potrf(A) == 0
+        F = D(A)
+        if uplo == Uplo.Lower:
+            L = torch.tril(F)
+            close(L @ L.mH, Af, 1e-12)
+        else:
+            U = torch.triu(F)
+            close(U.mH @ U, Af, 1e-12)
     B = mat(n, 5, nb, 12, p, q, dt)
     Bd = D(B)
     sl.potrs(A, B)
@@ -340,3 +343,16 @@ def test_potrf_tile_granular_bcast_2x4():
 def test_eight_ranks(grid):
     """The 8-GPU node's grids (BASELINE: 2x4), rehearsed with 8 gloo ranks."""
     run_dist(_run_8, 8, *grid, timeout=600)
+
+
+def _potrf_pairs(rank, size, p, q):
+    check_potrf(p, q)
+    check_potrf(p, q, torch.complex128)
+
+
+@pytest.mark.parametrize("grid", [(1, 2), (2, 1), (2, 2)], ids=lambda g: f"{g[0]}x{g[1]}")
+def test_potrf_step_pairs(grid, monkeypatch):
+    """SLATE_AMD_POTRF_PAIR=1 (chol.py): the deferred K = 2 nb trailing
+    update, odd and even tile counts, real and complex."""
+    monkeypatch.setenv("SLATE_AMD_POTRF_PAIR", "1")
+    run_dist(_potrf_pairs, grid[0] * grid[1], *grid)

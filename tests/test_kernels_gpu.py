@@ -123,6 +123,26 @@ def test_gemm_trimask_compact_blockcyclic(p, pr, q, pc, roff, coff):
     assert (C - exp).abs().max() < 1e-12
 
 
+@pytest.mark.parametrize("p,pr,q,pc,m,n", [
+    (1, 0, 2, 0, 32256, 15872), (1, 0, 2, 1, 20000, 9000), (2, 0, 1, 0, 15872, 31744), (4, 1, 2, 1, 3000, 2500),
+    (1, 0, 4, 2, 1500, 700)])
+def test_gemm_stair_exact_grid(p, pr, q, pc, m, n):
+    # the exact staircase launch (remap 4: host prefix sums per row group,
+    # binary searches per block) on tall / wide / ragged local blocks, both
+    # tile sizes; every kept element updated once, every skipped one intact
+    nb = 512
+    A, B, C = cm(m, 16, torch.float64, 7), cm(n, 16, torch.float64, 8), cm(m, n, torch.float64, 9)
+    C0 = C.clone()
+    ops.gemm(1.0, A, B, 1.0, C, 'N', 'T', mask=(1, nb, p, pr, q, pc, 0, 0, 0))
+    full = C0 + A @ B.mT
+    lr = torch.arange(m, device="cuda")
+    lc = torch.arange(n, device="cuda")
+    gr = ((lr // nb) * p + pr) * nb + lr % nb
+    gc = ((lc // nb) * q + pc) * nb + lc % nb
+    exp = torch.where(gr[:, None] >= gc[None, :], full, C0)
+    assert (C - exp).abs().max() < 1e-12
+
+
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("uplo", ["L", "U"])
 def test_potrf_tile(dt, uplo):
