@@ -183,6 +183,28 @@ __global__ void zero_words_kernel(unsigned long long* p, long long n) {
     if (i < n) p[i] = 0ull;
 }
 
+// Link-time stand-in for the loopback transport (parallel/comm.py): one
+// wave holds the issuing stream for `ticks` of the constant wall clock, as
+// a collective of that duration would; time-bound, so every wave exits.
+__global__ void spin_ticks_kernel(unsigned long long ticks) {
+    const unsigned long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+void spin_ns(double ns, hipStream_t s) {
+    static const double rate_khz = [] {
+        int dev = 0, khz = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
+            khz <= 0)
+            khz = 100000;
+        return (double)khz;
+    }();
+    if (!(ns > 0)) return;
+    const double capped = ns < 2e9 ? ns : 2e9;      // at most 2 s per call
+    hipLaunchKernelGGL(spin_ticks_kernel, dim3(1), dim3(64), 0, s, (unsigned long long)(capped * rate_khz * 1e-6));
+    HIP_LAUNCH_CHECK();
+}
+
 struct SwapPlan {                // folded permutation of one swap sequence
     int nt;
     int pad;

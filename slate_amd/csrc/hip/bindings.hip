@@ -286,6 +286,7 @@ static void register_kernels(py::module& m) {
     });
     m.def("lu_peer_close", [](uintptr_t p) { lu_peer_close((void*)p); });
     m.def("lu_peer_free", [](uintptr_t p) { lu_peer_free((void*)p); });
+    m.def("spin_ns", [](double ns, uintptr_t st) { spin_ns(ns, S(st)); });
     m.def("row_gather", [](char dt, i64 mm, i64 n, uintptr_t A, i64 lda, uintptr_t B, i64 ldb, uintptr_t perm,
                            uintptr_t st) {
         dispatch(dt, [&](auto z) { using T = decltype(z);

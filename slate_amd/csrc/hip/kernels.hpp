@@ -54,6 +54,7 @@ template <typename T>
 void laswp(i64 n, T* A, i64 lda, i64 k1, i64 k2, const i64* ipiv, int incx, hipStream_t s);
 template <typename T>
 void permute_rows_scatter(i64 m, i64 n, const T* A, i64 lda, T* B, i64 ldb, const i64* perm, hipStream_t s);
+void spin_ns(double ns, hipStream_t s);   // aux.hip: hold the stream for ns (loopback link model)
 template <typename T>
 void permute_rows_gather(i64 m, i64 n, const T* A, i64 lda, T* B, i64 ldb, const i64* perm, hipStream_t s);
 

@@ -228,6 +228,13 @@ def laswp_cols_plan(A, plan):
     return A
 
 
+def spin_ns(ns, like):
+    """Hold the current stream of ``like``'s device for ``ns`` nanoseconds
+    (one-wave wall-clock spin; the loopback transport's link model)."""
+    if like.is_cuda and ns > 0:
+        kmod(like).spin_ns(float(ns), stream(like))
+
+
 def row_gather(A, B, perm):
     """B[i, :] = A[perm[i], :]."""
     m, n = B.shape

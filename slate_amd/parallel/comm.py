@@ -372,10 +372,34 @@ class LoopbackComm(Comm):
         self.backend = "loopback"
         self._subcache = {}
 
+    # SLATE_AMD_LOOPBACK_LINK="alpha_us,beta_GBps": every collective also
+    # holds its issuing stream for its modelled duration (a one-wave spin
+    # kernel, ops.spin_ns) -- the link cost then lands where the DAG puts
+    # it: overlapped behind other streams' kernels or on the critical chain,
+    # instead of being added up afterwards.  bcast / reduce: alpha + B/beta;
+    # allreduce: alpha + 2 B/beta; allgather(v): alpha + (P-1) B/beta.
+    _link = None
+    _LINK_FACTOR = {"bcast": 1.0, "reduce": 1.0, "allreduce": 2.0}
+
+    @classmethod
+    def link(cls):
+        if cls._link is None:
+            e = os.environ.get("SLATE_AMD_LOOPBACK_LINK", "")
+            cls._link = (False,)
+            if e:
+                a, b = (float(x) for x in e.split(",")[:2])
+                cls._link = (True, a * 1e-6, b * 1e9)
+        return cls._link
+
     def _log(self, op, t):
         nbytes = t.numel() * t.element_size() if isinstance(t, torch.Tensor) else 0
         st = torch.cuda.current_stream(t.device).cuda_stream if isinstance(t, torch.Tensor) and t.is_cuda else 0
         LoopbackComm.LOG.append((op, self.size, nbytes, st))
+        lk = self.link()
+        if lk[0] and st and self.size > 1:
+            f = self._LINK_FACTOR.get(op, float(self.size - 1))
+            from .. import ops
+            ops.spin_ns((lk[1] + f * nbytes / lk[2]) * 1e9, t)
 
     @classmethod
     def _tmp(cls, t):

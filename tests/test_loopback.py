@@ -68,3 +68,25 @@ def test_loopback_single_rank_matches_plain():
     sl.potrf(B)
     got = B.storage.local[B.storage.origin_slot]
     assert torch.equal(torch.tril(got), torch.tril(want))
+
+
+@pytest.mark.gpu
+def test_loopback_link_model_holds_stream(monkeypatch):
+    """SLATE_AMD_LOOPBACK_LINK: a bcast holds its issuing stream for
+    alpha + bytes / beta (the spin kernel, aux.hip spin_ticks_kernel)."""
+    monkeypatch.setenv("SLATE_AMD_LOOPBACK_LINK", "100,1")      # 100 us + 1 GB/s
+    C.LoopbackComm._link = None
+    try:
+        comm = C.LoopbackComm(2, 1)
+        t = torch.zeros(1 << 17, dtype=torch.float64, device="cuda")     # 1 MiB -> ~1.05 ms + 0.1
+        comm.bcast(t, 0)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        comm.bcast(t, 0)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1)
+        assert 1.1 < ms < 2.0, ms
+    finally:
+        C.LoopbackComm._link = None

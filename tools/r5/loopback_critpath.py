@@ -120,9 +120,33 @@ def main():
     ap.add_argument("--lookahead", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--link", default=None,
+                    help="alpha_us,beta_GBps: model every collective IN the DAG (a spin kernel of its "
+                         "duration on its issuing stream, parallel/comm.py LoopbackComm) and report the "
+                         "measured time as the projection")
     args = ap.parse_args()
     p, q = map(int, args.grid.lower().split("x"))
+    if args.link:
+        from slate_amd.parallel.comm import LoopbackComm
+        os.environ["SLATE_AMD_LOOPBACK_LINK"] = args.link
+        LoopbackComm._link = None
     res = [run_rank(args, int(r), p, q) for r in args.ranks.split(",")]
+    if args.link:
+        a_us, b_gb = args.link.split(",")[:2]
+        lines = [f"## {args.routine} n={args.n} nb={args.nb} grid {p}x{q} lookahead {args.lookahead}: in-DAG link "
+                 f"model alpha {a_us} us, beta {b_gb} GB/s (loopback, 1 MI355X)", ""]
+        worst = max(x["t"] for x in res)
+        for x in res:
+            lines.append(f"- rank {x['rank']} ({x['pr']},{x['pc']}): {x['t'] * 1e3:.1f} ms")
+        fl = res[0]["flops"]
+        lines.append(f"- job (max over simulated ranks): {worst * 1e3:.1f} ms = {fl / worst / 1e12:.1f} TF/s "
+                     f"({100 * fl / worst / (p * q * PEAK):.1f} % of {p * q} x 78.6)")
+        text = "\n".join(lines)
+        print(text, flush=True)
+        if args.out:
+            with open(args.out, "a") as f:
+                f.write(text + "\n\n")
+        return
     lines = [f"## {args.routine} n={args.n} nb={args.nb} grid {p}x{q} lookahead {args.lookahead} (loopback, 1 MI355X)", ""]
     lines.append("| rank (pr,pc) | local block | loopback ms | chain comm ms (opt / pess) | update comm ms (opt / pess) |"
                  " projected ms (opt / pess) | projected TF/s job (opt / pess) | % of 8-GPU peak (opt / pess) |")
