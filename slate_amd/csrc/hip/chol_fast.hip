@@ -396,6 +396,82 @@ trsm_rlt_kernel(i64 m, int n, double alpha, const double* __restrict__ L, i64 ld
     }
 }
 
+// ---------------------------------------------------------------- trsm_rlt_ks
+// The same solve with the K range of every strip update split over KS waves
+// (partial sums reduced through LDS) and RS = 8 / (2 KS) row strips of 16
+// per workgroup: per-step latency, not flops, bounds the whole-width kernel
+// above (a 64-row block walks n / 32 steps whose strip updates are chains
+// of K / 32 dependent load -> MFMA rounds: ~150 us at n = 512 for ANY
+// m <= 16384 on MI355X, tools/r5/trsm_probe.py), so a KS-way split shortens
+// every chain KS times and the grid holds KS times as many workgroups.
+template <int KS>
+__global__ void __launch_bounds__(512, 2)
+trsm_rlt_ks_kernel(i64 m, int n, double alpha, const double* __restrict__ L, i64 ldl,
+                   const double* __restrict__ Winv, double* __restrict__ B, i64 ldb, const int* gate) {
+    constexpr int RS = 4 / KS, BM = 16 * RS;
+    if (gate && *gate == 0) return;
+    __shared__ double R[32][BM + 16];                       // R[c][r] (pitch 16 mod 32, see above)
+    __shared__ d4 red[KS > 1 ? (KS - 1) * RS * 2 : 1][64];  // partial sums of the waves kh > 0
+    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int st = w % RS, tt = (w / RS) & 1, kh = w / (2 * RS);
+    const i64 r0 = (i64)blockIdx.x * BM;
+    const int mr = (int)min((i64)BM, m - r0);
+    const int ml = 16 * st + (lane & 15);
+    const i64 rx = r0 + min(ml, mr - 1);
+    for (int c0 = 0; c0 < n; c0 += 32) {
+        const int jb = min(32, n - c0);
+        d4 acc1[1][1] = {{d4{0, 0, 0, 0}}};
+        if (c0 > 0) {
+            // this wave's share of K = c0, in whole 32-wide chunks (strip_update
+            // with U = 8 consumes k in steps of 32)
+            const int nc = c0 / 32, k0 = 32 * ((nc * kh) / KS), k1 = 32 * ((nc * (kh + 1)) / KS);
+            if (k1 > k0) {
+                const int xr[1] = {(int)(rx - r0)};
+                const int yr[1] = {min(16 * tt + (lane & 15), n - 1 - c0)};
+                strip_update<1, 1, 8>(acc1, B + r0 + (i64)k0 * ldb, xr, ldb, L + c0 + (i64)k0 * ldl, yr, ldl,
+                                      k1 - k0, lane);
+            }
+        }
+        if (KS > 1) {
+            if (kh > 0) red[((kh - 1) * 2 + tt) * RS + st][lane] = acc1[0][0];
+            __syncthreads();
+            if (kh == 0) {
+                #pragma unroll
+                for (int h = 1; h < KS; ++h) {
+                    const d4 v = red[((h - 1) * 2 + tt) * RS + st][lane];
+                    #pragma unroll
+                    for (int r = 0; r < 4; ++r) acc1[0][0][r] += v[r];
+                }
+            }
+        }
+        if (kh == 0) {
+            #pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int c = 16 * tt + (lane >> 4) + 4 * r;
+                double v = 0.0;
+                if (ml < mr && c < jb) v = alpha * B[(r0 + ml) + (i64)(c0 + c) * ldb] - acc1[0][0][r];
+                R[c][ml] = v;
+            }
+        }
+        __syncthreads();
+        if (kh == 0) {
+            const double* W = Winv + (i64)(c0 / 32) * 1024;
+            d4 x = {0, 0, 0, 0};
+            #pragma unroll
+            for (int k = 0; k < 32; k += 4) {
+                const int kk = k + (lane >> 4);
+                x = mma(W[(16 * tt + (lane & 15)) + 32 * kk], R[kk][ml], x);
+            }
+            #pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int c = 16 * tt + (lane >> 4) + 4 * r;
+                if (ml < mr && c < jb) B[(r0 + ml) + (i64)(c0 + c) * ldb] = x[r];
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // ---------------------------------------------------------------- trsm_lln
 // L X = alpha B (L: m x m lower, B: m x n), X overwrites B -- the U rows of
 // LU (L unit lower) and the forward solves.  Every workgroup owns 64 columns
@@ -497,8 +573,25 @@ bool trsm_rlt_fast(i64 m, i64 n, double alpha, const double* L, i64 ldl, double*
     double* W = static_cast<double*>(workspace(s, sizeof(double) * (size_t)nbj * 1024, WS_C));
     hipLaunchKernelGGL(tri_inv32_kernel, dim3(nbj), dim3(64), 0, s, (int)n, L, ldl, W, unit, gate);
     HIP_LAUNCH_CHECK();
-    hipLaunchKernelGGL(trsm_rlt_kernel, dim3((unsigned)((m + TBM - 1) / TBM)), dim3(512), 0, s, m, (int)n, alpha, L,
-                       ldl, (const double*)W, B, ldb, gate);
+    // K splits of the strip updates (1: the whole-width kernel, 64-row
+    // blocks; 2: 32-row blocks; 4: 16-row blocks).  Default by m, measured
+    // alone at n = 512 (tools/r5/trsm_probe.py, profiles/r5/trsm_ks.txt):
+    // m = 4096: 185 / 131 / 99 us, 8192: 175 / 121 / 123, 16384: 185 / 185
+    // / 221, 32256: 309 / 334 / 410.  SLATE_AMD_TRSM_KS=1|2|4 overrides.
+    const int ks = [m] {      // read per launch: tests toggle it
+        const char* e = std::getenv("SLATE_AMD_TRSM_KS");
+        const int v = e ? std::atoi(e) : (m <= 6144 ? 4 : m <= 12288 ? 2 : 1);
+        return (v == 2 || v == 4) ? v : 1;
+    }();
+    if (ks == 2)
+        hipLaunchKernelGGL(trsm_rlt_ks_kernel<2>, dim3((unsigned)((m + 31) / 32)), dim3(512), 0, s, m, (int)n, alpha,
+                           L, ldl, (const double*)W, B, ldb, gate);
+    else if (ks == 4)
+        hipLaunchKernelGGL(trsm_rlt_ks_kernel<4>, dim3((unsigned)((m + 15) / 16)), dim3(512), 0, s, m, (int)n, alpha,
+                           L, ldl, (const double*)W, B, ldb, gate);
+    else
+        hipLaunchKernelGGL(trsm_rlt_kernel, dim3((unsigned)((m + TBM - 1) / TBM)), dim3(512), 0, s, m, (int)n, alpha,
+                           L, ldl, (const double*)W, B, ldb, gate);
     HIP_LAUNCH_CHECK();
     return true;
 }

@@ -410,8 +410,9 @@ class LoopbackComm(Comm):
         return buf[: t.numel()]
 
     def _land(self, t):
-        """t receives its own bytes again: one read + one write of t."""
-        if t.numel() == 0:
+        """t receives its own bytes again: one read + one write of t (not
+        with the link model, whose spin stands for the whole transfer)."""
+        if t.numel() == 0 or self.link()[0]:
             return t
         fv = self._flat_view(t)
         src = fv.reshape(-1) if fv is not None else t.contiguous().reshape(-1)

@@ -192,8 +192,11 @@ def test_potrf_tile_fp64_fast_info(bad):
 
 @pytest.mark.parametrize("m,n", [(1, 1), (64, 32), (65, 33), (1000, 512), (4097, 100), (300, 1000)])
 @pytest.mark.parametrize("diag", ["N", "U"])
-def test_trsm_rlt_fp64_fast(m, n, diag):
-    # X L^T = alpha B: the Cholesky panel solve (tri_inv32 + trsm_rlt kernels)
+@pytest.mark.parametrize("ks", ["1", "2", "4"])
+def test_trsm_rlt_fp64_fast(m, n, diag, ks, monkeypatch):
+    # X L^T = alpha B: the Cholesky panel solve (tri_inv32 + trsm_rlt kernels;
+    # SLATE_AMD_TRSM_KS: the K-split variants, 32- and 16-row blocks)
+    monkeypatch.setenv("SLATE_AMD_TRSM_KS", ks)
     T = torch.tril(ref(cm(n, n, torch.float64, 41))) / n + 2 * torch.eye(n, dtype=torch.float64, device="cuda")
     Tu = T.clone()
     if diag == 'U':
