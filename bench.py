@@ -9,8 +9,7 @@ LAPACK/SLATE convention n^3/3 + n^2/2 + n/6 (docs/latex/flops.tex:103).
 
 Launch: python bench.py [--gpus N --steps K --warmup W]
         (N>1 via torchrun: one process per GPU, RCCL over xGMI)
-Grid:   1x1, 2x1 (potrf; getrf/gemm 1x2), 2x2, 2x4 for 1, 2, 4, 8 GPUs
-        (BASELINE: 2x4 at 8).
+Grid:   1x1, 1x2, 2x2, 2x4 for 1, 2, 4, 8 GPUs (BASELINE: 2x4 at 8).
 Data:   synthetic SPD matrix (Hermitian rands + n*I, Philox, generated on
         device); random-init of the named config, no external data.
 """
@@ -44,17 +43,11 @@ def flops(routine, n, m=None):
 
 def grid_for(n, routine="potrf"):
     """Default process grid per GPU count.  potrf/getrf/gemm: as square as
-    possible with q >= p (BASELINE: 2x4 at 8 GPUs), potrf at 2 GPUs 2x1; geqrf (tall-skinny QR,
+    possible with q >= p (BASELINE: 2x4 at 8 GPUs); geqrf (tall-skinny QR,
     m = 8n): one process column (p = N) -- the TSQR tree spans all GPUs and
     the trailing update needs no row broadcast."""
     if routine == "geqrf":
         return (n, 1)
-    if routine == "potrf" and n == 2:
-        # 2 GPUs: one process column -- the panel's transposed rows travel
-        # down the column while no row broadcast is needed; loopback
-        # projection at n = 32768 (profiles/r5/critpath_2x4.md): 2x1
-        # 146 ms vs 1x2 153 ms optimistic, 208 vs 218 pessimistic
-        return (2, 1)
     return {1: (1, 1), 2: (1, 2), 4: (2, 2), 8: (2, 4)}.get(n, (1, n))
 
 

@@ -633,7 +633,7 @@ static void potrf_grid(Storage& S, int la, i64* infos) {
     T* buf = static_cast<T*>(S.buf);
     const i64 nt = (n + nb - 1) / nb;
     const i64 lr_end = S.mloc, lc_end = S.nloc;
-    const i64 chunk_rows = nb * std::max(1, env_int("SLATE_AMD_POTRF_CHUNK", 4));
+    const i64 chunk_rows = nb * std::max(1, env_int("SLATE_AMD_POTRF_CHUNK", 16));
     hipStream_t ps = R.panel, us = R.update, cs = R.comm;
     // plans (host, then one upload)
     std::vector<i64> flat;

@@ -136,8 +136,11 @@ def _potrf_lower(A, opts):
     diag_first = la >= 1 and nt > 1 and os.environ.get("SLATE_AMD_POTRF_DIAGFIRST", "1") != "0"
     ev_diag = {}
     ev_tr = {}
-    # tile rows per row-broadcast chunk after the first (SLATE_AMD_POTRF_CHUNK)
-    chunk_tiles = max(1, int(os.environ.get("SLATE_AMD_POTRF_CHUNK", "4")))
+    # tile rows per row-broadcast chunk after the first (SLATE_AMD_POTRF_CHUNK):
+    # 16 -- under the in-DAG link model (loopback_critpath.py --link, 2x4 at
+    # n = 32768) 4-tile chunks cost 49.6 / 88.7 ms (10 us, 150 GB/s / 25 us,
+    # 50 GB/s), 8: 47.5 / 84.5, 16: 45.9 / 82.6, 32-64: the same as 16
+    chunk_tiles = max(1, int(os.environ.get("SLATE_AMD_POTRF_CHUNK", "16")))
     esz = torch.empty(0, dtype=dtype).element_size()
     # step pairs (SLATE_AMD_POTRF_PAIR=1, lookahead 1 with diag-first): the
     # trailing update of the pair's first step is deferred and applied with
@@ -277,17 +280,31 @@ def _potrf_lower(A, opts):
                         mask = (1, nb, p, pr, q, pc, lr1 + ra, lc1, 0)
                         ops.gemm(-1.0, Pk[o + ra:o + rb], Lk[lo:lo + lc_la - lc1], 1.0, buf[lr1 + ra:lr1 + rb, lc1:lc_la],
                                  'N', ct, mask)
-            # the trailing update's transposed rows: gathered over the same
-            # column communicator, from the panel stream, AFTER the lookahead
-            # update (off the critical chain; one issue order of collectives
-            # on every rank, no second communicator per dimension)
-            if plans is not None:
-                Lcol = assemble_cols(plans[t][1], Prow, grid, p, kb, dtype, dev)
-                loff = lc_la            # Lcol row 0 = local column lc_la
-            else:
-                loff = lc1
             ev_panel = ss.event(ss.panel)
         us = ss.update[0]
+        # the trailing update's transposed rows: gathered from the UPDATE
+        # stream over the grid's second column communicator (col_comm_u, one
+        # issue order on every rank), so the next step's panel no longer
+        # queues behind the step's biggest column broadcast (2x4 at n =
+        # 32768 under the in-DAG link model: profiles/r5/critpath_2x4.md);
+        # -- when q > 1 (one process column: the update stream already carries
+        # all the GEMM work, and 2x1 lost 123 -> 142 ms with it);
+        # SLATE_AMD_POTRF_LCOL_U=0|1 forces the panel stream / update stream
+        if plans is not None:
+            lcol_u = os.environ.get("SLATE_AMD_POTRF_LCOL_U", "1" if q > 1 else "0") != "0"
+            st_l = us if lcol_u else ss.panel
+            with ss.use(st_l):
+                if lcol_u:
+                    ss.wait(us, ev_panel)
+                    if Prow.is_cuda:
+                        Prow.record_stream(us)
+                Lcol = assemble_cols(plans[t][1], Prow, grid, p, kb, dtype, dev,
+                                     comm=grid.col_comm_u if lcol_u else None)
+                if not lcol_u:
+                    ev_panel = ss.event(ss.panel)
+            loff = lc_la            # Lcol row 0 = local column lc_la
+        else:
+            loff = lc1
         if defer:
             # the pair's first step: its trailing update waits for the second
             pend = {"Prow": Prow, "Lcol": Lcol, "lr1": lr1, "loff": loff, "lcg": lcg, "own_col": own_col}

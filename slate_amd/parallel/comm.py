@@ -396,7 +396,7 @@ class LoopbackComm(Comm):
         st = torch.cuda.current_stream(t.device).cuda_stream if isinstance(t, torch.Tensor) and t.is_cuda else 0
         LoopbackComm.LOG.append((op, self.size, nbytes, st))
         lk = self.link()
-        if lk[0] and st and self.size > 1:
+        if lk[0] and isinstance(t, torch.Tensor) and t.is_cuda and self.size > 1:
             f = self._LINK_FACTOR.get(op, float(self.size - 1))
             from .. import ops
             ops.spin_ns((lk[1] + f * nbytes / lk[2]) * 1e9, t)

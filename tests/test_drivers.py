@@ -335,7 +335,8 @@ def test_lu_distributed_panel_2x4():
     run_dist(_lu_no_panel_allgather, 8, 2, 4, timeout=600)
 
 
-def test_potrf_tile_granular_bcast_2x4():
+def test_potrf_tile_granular_bcast_2x4(monkeypatch):
+    monkeypatch.setenv("SLATE_AMD_POTRF_CHUNK", "4")    # the mechanism (default 16: fewer, larger messages)
     run_dist(_potrf_bcast_granularity, 8, 2, 4, timeout=600)
 
 
