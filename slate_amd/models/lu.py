@@ -96,6 +96,13 @@ def _getrf(A, pivots, opts, mode):
             if pivots is not None:
                 pivots.set(ooc[1], bc.nb)
             return ooc[0]
+    if getattr(s.comm, "backend", "") == "loopback" and s.comm.size > 1 and mode != "nopiv":
+        # the loopback transport feeds a rank its own bytes back: broadcast
+        # pivots and the peers' pivot records are then this rank's own
+        # (uninitialised) buffers, and the row exchange indexes past the
+        # local block (a device fault on MI355X, tools/r5/gpu_az.sh) --
+        # refuse instead of faulting
+        raise SlateError("pivoted getrf cannot run under the loopback transport (pivots need the peers' data)")
     buf = s.prepare_local(slot)
     if bc.p == 1 and mode != "calu":
         info, ipiv = None, None

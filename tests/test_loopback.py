@@ -90,3 +90,14 @@ def test_loopback_link_model_holds_stream(monkeypatch):
         assert 1.1 < ms < 2.0, ms
     finally:
         C.LoopbackComm._link = None
+
+
+def test_loopback_refuses_pivoted_getrf():
+    """Pivoted LU needs the peers' pivot data: under the loopback transport
+    it raises instead of running a row exchange planned from this rank's own
+    bytes (which indexed past the local block on the GPU)."""
+    C.loopback(8, 0)
+    A = sl.Matrix(256, 256, nb=64, p=2, q=4)
+    A.insertLocalTiles()
+    with pytest.raises(sl.SlateError):
+        sl.getrf(A, sl.Pivots())

@@ -53,6 +53,12 @@ def run_rank(args, r, p, q):
         sl.generate_matrix(A, "poev", seed=7)
         run = lambda: sl.potrf(A, opts)          # noqa: E731
         flops = n ** 3 / 3
+    elif args.routine == "getrf":
+        A = sl.Matrix(n, n, nb=nb, p=p, q=q, device=dev)
+        A.insertLocalTiles(device=dev)
+        sl.generate_matrix(A, "rands", seed=7)
+        run = lambda: sl.getrf(A, sl.Pivots(), opts)     # noqa: E731
+        flops = 2 * n ** 3 / 3
     else:
         A = sl.Matrix(n, n, nb=nb, p=p, q=q, device=dev)
         A.insertLocalTiles(device=dev)
@@ -112,7 +118,7 @@ def model(res, scen):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--routine", default="potrf", choices=["potrf", "gemm"])
+    ap.add_argument("--routine", default="potrf", choices=["potrf", "getrf", "gemm"])
     ap.add_argument("--n", type=int, default=32768)
     ap.add_argument("--nb", type=int, default=512)
     ap.add_argument("--grid", default="2x4")
