@@ -493,7 +493,8 @@ ColPlan rows_plan(std::vector<i64>& flat, i64 m, i64 nb, int p, int q, int pc, i
 // column broadcasts go on stream s (the column communicator's stream)
 template <typename T>
 void assemble_cols(const ColPlan& P, const i64* idx, const T* Prow, i64 ldp, i64 kb, GridComms* gc, T* Lcol,
-                   hipStream_t s) {
+                   hipStream_t s, Comm* col = nullptr) {
+    if (!col) col = gc->col.get();
     if (P.tot == 0) return;
     Scratch R((size_t)P.tot * kb * sizeof(T), s);
     i64 pos = 0;
@@ -503,7 +504,7 @@ void assemble_cols(const ColPlan& P, const i64* idx, const T* Prow, i64 ldp, i64
             Scratch tmp((size_t)cnt * kb * sizeof(T), s);
             if (gc->pr == r)
                 slate_hip::permute_rows_gather<K<T>>(cnt, kb, kp(Prow), ldp, kp(tmp.as<T>()), cnt, idx + P.off[r], s);
-            if (gc->p > 1) gc->col->bcast(tmp.p, (size_t)cnt * kb * sizeof(T), r, s);
+            if (gc->p > 1) col->bcast(tmp.p, (size_t)cnt * kb * sizeof(T), r, s);
             copy2d(R.as<T>() + pos, P.tot, tmp.as<T>(), cnt, cnt, kb, s);
         }
         pos += cnt;
@@ -619,10 +620,11 @@ static void potrf_1x1(T* A, i64 lda, i64 n, i64 nb, int la, i64* infos) {
 // p x q grid (chol.py _potrf_lower): panel stream = tile potrf, column bcast
 // of the diagonal tile, trsm, then the TILE-GRANULAR row broadcast of the
 // panel (SLATE listBcastMT, potrf.cc:122-132): chunk 0 = the first tile row,
-// then chunks of 4 tile rows, on the comm stream (the row communicator's
+// then chunks of 16 tile rows, on the comm stream (the row communicator's
 // stream) while the panel stream runs each chunk's lookahead GEMM as it
-// lands; column gathers of the transposed operands (column communicator,
-// panel stream); update stream = the trailing GEMMs.
+// lands; column gathers of the lookahead's transposed operands (column
+// communicator, panel stream); update stream = the trailing transposed
+// rows (second column communicator, q > 1) and the trailing GEMMs.
 template <typename T>
 static void potrf_grid(Storage& S, int la, i64* infos) {
     Runtime& R = rt();
@@ -757,8 +759,21 @@ static void potrf_grid(Storage& S, int la, i64* infos) {
         dbg_sum("la_out", t, buf + lr1 + lc1 * lld, lld, nrow, lc_la - lc1, ps);
         const T* Lc;
         i64 ldlc, loff;
+        // q > 1: the trailing transposed rows are gathered from the UPDATE
+        // stream over the second column communicator (chol.py, same choice;
+        // SLATE_AMD_POTRF_LCOL_U=0 keeps them on the panel stream)
+        static const bool lcol_u_env = env_int("SLATE_AMD_POTRF_LCOL_U", 1) != 0;
+        const bool lcol_u = lcol_u_env && q > 1 && (p == 1 || gc->colu);
+        Event ev_panel;
+        if (lcol_u) {
+            ev_panel.record(ps);
+            ev_panel.wait(us);
+        }
         if (p > 1 || q > 1) {
-            assemble_cols<T>(A2, d_idx, P, ldp, kb, gc, Lcol->as<T>(), ps);
+            if (lcol_u)
+                assemble_cols<T>(A2, d_idx, P, ldp, kb, gc, Lcol->as<T>(), us, p > 1 ? gc->colu.get() : nullptr);
+            else
+                assemble_cols<T>(A2, d_idx, P, ldp, kb, gc, Lcol->as<T>(), ps);
             Lc = Lcol->as<T>();
             ldlc = std::max<i64>(A2.order_cnt, 1);
             loff = lc_la;
@@ -767,9 +782,10 @@ static void potrf_grid(Storage& S, int la, i64* infos) {
             ldlc = ldp;
             loff = lc1;
         }
-        Event ev_panel;
-        ev_panel.record(ps);
-        ev_panel.wait(us);
+        if (!lcol_u) {
+            ev_panel.record(ps);
+            ev_panel.wait(us);
+        }
         const i64 lc_nx = std::max(std::min(tiles_before(g + 2 + la, q, pc) * nb, lc_end), lc_la);
         for (int part = 0; part < 2; ++part) {
             const i64 c0 = part == 0 ? lc_la : lc_nx, c1 = part == 0 ? lc_nx : lc_end;
