@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdio>
 #include <random>
+#include <string>
 #include <vector>
 using namespace slate_hip;
 
@@ -50,7 +51,15 @@ void glds_launch(const GemmArgs<double>& a0) {
 
 struct Var { const char* name; void (*nt)(const GemmArgs<double>&); void (*nn)(const GemmArgs<double>&); };
 
-int main() {
+template <bool TB>
+void small_launch(const GemmArgs<double>& a) {
+    const int gm = (a.m + 63) / 64, gn = (a.n + 63) / 64;
+    hipLaunchKernelGGL((gemm_real_kernel<double, false, TB, 64, 64, 8, false, 2, 2, 2, 1>), dim3(gm * gn, 1), dim3(256),
+                       0, 0, a);
+}
+
+int main(int argc, char** argv) {
+    const bool small = argc > 1 && std::string(argv[1]) == "small";
     const long N = 32768, KMAX = 4096;
     double *A, *B, *C, *C2;
     hipMalloc(&A, N * KMAX * 8);
@@ -69,16 +78,20 @@ int main() {
         }
         for (long off = 0; off < N * N; off += N * 64) hipMemcpy(C + off, h.data(), N * 64 * 8, hipMemcpyHostToDevice);
     }
-    const Var vars[] = {
-        {"glds 128x128 2x4 S2 occ2", glds_launch<true, 128, 128, 2, 4, 2, 2>, glds_launch<false, 128, 128, 2, 4, 2, 2>},
-        {"glds 128x128 4x2 S2 occ2", glds_launch<true, 128, 128, 4, 2, 2, 2>, glds_launch<false, 128, 128, 4, 2, 2, 2>},
-        {"glds 2x4 S2 occ2 prio", glds_launch<true, 128, 128, 2, 4, 2, 2, 1>, glds_launch<false, 128, 128, 2, 4, 2, 2, 1>},
-        {"glds 2x4 S2 occ2 group4", glds_launch<true, 128, 128, 2, 4, 2, 2, 0, 4>,
-         glds_launch<false, 128, 128, 2, 4, 2, 2, 0, 4>},
-        {"glds 2x4 S2 occ2 group16", glds_launch<true, 128, 128, 2, 4, 2, 2, 0, 16>,
-         glds_launch<false, 128, 128, 2, 4, 2, 2, 0, 16>},
+    const Var big_vars[] = {
+        {"glds 128x128 2x4 S2 occ2", glds_launch<true, 128, 128, 2, 4, 2, 2>, glds_launch<false, 128, 128, 4, 2, 2, 2>},
+    };
+    const Var small_vars[] = {
+        {"64x64 register-staged", small_launch<true>, small_launch<false>},
+        {"glds 128x128 2x4 S2 occ2", glds_launch<true, 128, 128, 2, 4, 2, 2>, glds_launch<false, 128, 128, 4, 2, 2, 2>},
+        {"glds 64x64 2x2 S2 occ4", glds_launch<true, 64, 64, 2, 2, 2, 4>, glds_launch<false, 64, 64, 2, 2, 2, 4>},
+        {"glds 64x64 2x2 S3 occ3", glds_launch<true, 64, 64, 2, 2, 3, 3>, glds_launch<false, 64, 64, 2, 2, 3, 3>},
         {"glds 128x64 2x2 S2 occ3", glds_launch<true, 128, 64, 2, 2, 2, 3>, glds_launch<false, 128, 64, 2, 2, 2, 3>},
     };
+    const Var* vars_p = small ? small_vars : big_vars;
+    const int nvars = small ? 5 : 1;
+    struct VarList { const Var* b; const Var* e; const Var* begin() const { return b; } const Var* end() const { return e; } };
+    const VarList vars{vars_p, vars_p + nvars};
     auto mk = [&](long m, long n, long k, bool tb, double alpha, double beta, double* c, long ldc) {
         GemmArgs<double> a{};
         a.m = m; a.n = n; a.k = k; a.alpha = alpha; a.beta = beta;
@@ -118,16 +131,28 @@ int main() {
             }
     }
     struct Shape { long m, n, k; bool tb; const char* what; };
-    const Shape shapes[] = {
+    const Shape big_shapes[] = {
         {31744, 31744, 512, true, "trailing NT k=512"},
-        {31744, 31744, 1024, true, "trailing NT k=1024"},
-        {31744, 31744, 512, false, "trailing NN k=512"},
         {16384, 16384, 4096, false, "NN k=4096"},
-        {16384, 16384, 4096, true, "NT k=4096"},
     };
+    const Shape small_shapes[] = {
+        {8192, 8192, 1024, true, "tail NT 8192 k=1024"},
+        {4096, 4096, 1024, true, "tail NT 4096 k=1024"},
+        {2048, 2048, 1024, true, "tail NT 2048 k=1024"},
+        {1024, 1024, 1024, true, "tail NT 1024 k=1024"},
+        {4096, 4096, 512, true, "tail NT 4096 k=512"},
+        {32768, 512, 512, true, "column NT 32768x512"},
+        {16384, 1024, 1024, true, "column NT 16384x1024"},
+        {32768, 1024, 512, true, "lookahead NT 32768x1024"},
+        {8192, 8192, 512, false, "tail NN 8192 k=512"},
+        {4096, 4096, 512, false, "tail NN 4096 k=512"},
+        {32768, 512, 512, false, "column NN 32768x512"},
+    };
+    struct ShapeList { const Shape* b; const Shape* e; const Shape* begin() const { return b; } const Shape* end() const { return e; } };
+    const ShapeList shapes = small ? ShapeList{small_shapes, small_shapes + 11} : ShapeList{big_shapes, big_shapes + 2};
     for (const auto& s : shapes) {
         const double fl = 2.0 * s.m * s.n * s.k;
-        const int reps = std::max(2, (int)(2e12 / fl));
+        const int reps = std::max(5, (int)(1e12 / fl));
         auto a = mk(s.m, s.n, s.k, s.tb, -1.0, 1.0, C, N);
         for (int round = 0; round < 2; ++round) {
             float ms = timed(s.tb ? ref_launch<true, 1> : ref_launch<false, 2>, a, reps);
