@@ -8,7 +8,9 @@ local buffer and IS inside the timed region -- conservative).  Flops use the
 LAPACK/SLATE convention n^3/3 + n^2/2 + n/6 (docs/latex/flops.tex:103).
 
 Launch: python bench.py [--gpus N --steps K --warmup W]
-        (N>1 via torchrun: one process per GPU, RCCL over xGMI)
+        N>1: one process per GPU, RCCL over xGMI -- either under an external
+        torchrun (WORLD_SIZE set, must equal N) or, without one, bench.py
+        starts the N ranks itself before any GPU call (_self_launch).
 Grid:   1x1, 1x2, 2x2, 2x4 for 1, 2, 4, 8 GPUs (BASELINE: 2x4 at 8).
 Data:   synthetic SPD matrix (Hermitian rands + n*I, Philox, generated on
         device); random-init of the named config, no external data.
@@ -213,6 +215,46 @@ def _main_native(args):
         sys.exit(1)
 
 
+def _free_port_pair():
+    """A port P with P and P + 1 both free on 127.0.0.1."""
+    import socket
+    for _ in range(64):
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        try:
+            with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+                s.bind(("127.0.0.1", port + 1))
+            return port
+        except OSError:
+            continue
+    raise SystemExit("bench: no free port pair on 127.0.0.1")
+
+
+def _self_launch(nproc):
+    """``--gpus N`` (N > 1) started without a launcher: start N ranks here,
+    one process per GPU (rank r -> LOCAL_RANK r -> GPU r), the way the
+    reference's tester is started per rank by mpirun
+    (/root/reference/test/run_tests.py:171-175).  This parent never touches
+    the GPU (no HIP call happens before or after the spawn: torch is only
+    imported) and never exec()s -- the ranks are children of a
+    torch.distributed.run child; rank 0's JSON line goes straight to our
+    stdout, and any rank failing makes this process exit non-zero.
+    MASTER_PORT + 1 stays free for the native runtime's own bootstrap
+    (--impl native)."""
+    import subprocess
+    port = _free_port_pair()
+    cmd =[sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    r = subprocess.run(cmd, env=env)
+    if r.returncode != 0:
+        print(f"bench: {nproc}-rank launch failed (exit {r.returncode})", file=sys.stderr, flush=True)
+    sys.exit(r.returncode)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -235,6 +277,13 @@ def main():
     args = ap.parse_args()
     if args.nb is None:
         args.nb = 256 if args.routine == "geqrf" else 512
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return _self_launch(args.gpus)
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
+    if env_world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE {env_world} (one rank per GPU)")
     if args.impl == "native":
         return _main_native(args)
     # No GPU_MAX_HW_QUEUES override: a process drives the panel, diag and
@@ -247,8 +296,8 @@ def main():
     comm = sl.init()
     world = comm.size
     rank = comm.rank
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but the communicator has {world} ranks")
     p, q = grid_for(world, args.routine) if args.grid is None else map(int, args.grid.lower().split("x"))
     gpu = torch.cuda.is_available()
     dev = torch.device("cuda", torch.cuda.current_device()) if gpu else torch.device("cpu")

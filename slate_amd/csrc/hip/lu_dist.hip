@@ -439,7 +439,9 @@ lu_dist_base_kernel(i64 nr, T* W, i64 ldw, const i64* __restrict__ grow, int c0,
                 wave_acquire<AG>();
                 double v = -1.0;
                 long long gi = (long long)1 << 62;
-                int who = 0;
+                // the lane's own partial: `who` travels with (v, gi) so the
+                // posted candidate row is the winner's, not workgroup 0's
+                int who = lane < G ? lane : 0;
                 if (lane < G) {
                     const PartHdr* h = reinterpret_cast<const PartHdr*>(part_slot(pe.part, par, lane));
                     v = get_d<AG>(&h->v);

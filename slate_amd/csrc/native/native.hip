@@ -143,6 +143,9 @@ PeerBox::~PeerBox() {
 }
 
 PeerBox* peer_box(Comm* c, std::unique_ptr<PeerBox>& slot, hipStream_t s) {
+    if (slot && slot->dead)
+        throw Error("native getrf: this grid's peer mailboxes timed out earlier (sequence tags no longer agree "
+                    "across ranks); build a new grid to continue");
     if (slot) return slot.get();
     const char* e = std::getenv("SLATE_AMD_LU_PEER");
     if ((e && e[0] == '0') || !c || c->size < 2 || c->size > slate_hip::lu_peer_max_p()) return nullptr;
@@ -1497,7 +1500,10 @@ int64_t getrf(Matrix<T>& A, std::vector<int64_t>& ipiv_out, const Options& opts)
     if (p > 1 && gc->colpeer) {
         unsigned long long e = 0;
         NHIP(hipMemcpy(&e, gc->colpeer->err, sizeof(e), hipMemcpyDeviceToHost));
-        if (e) throw Error("native getrf: peer mailbox exchange timed out (a column peer never posted its record)");
+        if (e) {
+            gc->colpeer->dead = true;     // sticky: every later use raises instead of waiting on stale tags
+            throw Error("native getrf: peer mailbox exchange timed out (a column peer never posted its record)");
+        }
     }
     ipiv_out.assign((size_t)kmin, 0);
     for (i64 i = 0; i < kmin; ++i) ipiv_out[i] = h[i] + (i / nb) * nb;   // panel-relative -> global

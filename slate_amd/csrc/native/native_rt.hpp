@@ -103,6 +103,7 @@ struct PeerBox {
     unsigned long long* err = nullptr;      // timeout word
     long long seq = 0;                      // next sequence base (identical on every member)
     long long launches = 0;
+    bool dead = false;                      // a kernel timed out: tags no longer agree, never reuse
     ~PeerBox();
 };
 PeerBox* peer_box(Comm* c, std::unique_ptr<PeerBox>& slot, hipStream_t s);

@@ -22,6 +22,40 @@ Design for the 8-GPU xGMI node (every GPU pair has a dedicated link):
   index, NaN wins -- same as SLATE's `mpi_max_nan`).
 * ``Comm`` with size 1 short-circuits every call (no process group needed),
   so the single-GPU bench path has zero communication overhead.
+
+Issue order across communicators (why the pipelines cannot deadlock)
+--------------------------------------------------------------------
+A pipelined driver issues collectives on several communicators from
+several HIP streams: e.g. distributed potrf uses ``col_comm`` on the panel
+stream, ``row_comm`` on the diag stream and ``col_comm_u`` (same members as
+``col_comm``, its own RCCL communicator) on the update stream.  torch runs a
+synchronous RCCL collective on the issuing stream, and with
+GPU_MAX_HW_QUEUES=4 two of those streams may share one hardware queue, whose
+packets execute in submission order.  So two ranks that submitted two
+collectives of different communicators in OPPOSITE orders into one shared
+queue would each wait inside the first for the other: a deadlock no timeout
+on a single communicator explains.
+
+The drivers rule that out by construction: every rank runs the same
+deterministic step loop, and the collectives of step t are issued in one
+fixed global sequence (potrf: column broadcast of the diagonal tile, the row
+broadcast chunks, the panel-stream column gathers, then the update-stream
+column gathers) of which each rank issues the subsequence it is a member
+of -- rank-dependent branches (``own_col``, ``own_diag``) only select
+compute, or select whole collectives for ALL members of their communicator
+alike (``own_col`` is the same on every member of ``col_comm``).  Hence all
+ranks' issue orders are restrictions of one total order, so whatever
+queue sharing HIP picks, the earliest unfinished collective in that order has
+nothing unfinished ahead of it in any member's queue except compute (which
+finishes) -- it completes, and induction covers the rest.  Cross-stream
+event waits only point backwards in issue order, so they keep the argument.
+``ORDER_LOG`` records, per rank, the (communicator, sequence number) of
+every collective in issue order; tests/test_comm_order.py gathers the logs of
+gloo 2x2 / 2x4 runs of potrf, getrf, geqrf and gemm and checks that their
+union is acyclic (one global order exists).  All sub-communicators of a grid,
+the update stream's included, are created eagerly in ``ProcessGrid``: RCCL
+communicator creation is itself collective over the world and must not run
+interleaved with a pipeline's in-flight collectives.
 """
 from __future__ import annotations
 
@@ -37,6 +71,16 @@ from ..utils import watchdog as _wd
 
 # per-communicator issuing streams while "on" (tests: one stream per comm)
 STREAM_LOG = {"on": False, "used": {}}
+# issue-order log while "on": ((members, tag), kind, seq) per collective or
+# matched point-to-point pair, in this rank's issue order (tests)
+ORDER_LOG = {"on": False, "ops": [], "seq": {}}
+
+
+def _order(key, kind):
+    if ORDER_LOG["on"]:
+        n = ORDER_LOG["seq"].get(key, 0)
+        ORDER_LOG["seq"][key] = n + 1
+        ORDER_LOG["ops"].append((key, kind, n))
 
 
 def _dist_ready() -> bool:
@@ -66,10 +110,25 @@ class Comm:
         self.rank = self.ranks.index(self.world_rank) if self.world_rank in self.ranks else -1
         self.backend = dist.get_backend(self.group) if (_dist_ready() and self.size > 1) else "self"
         self._subcache = {}
+        self.tag = ""
 
     # -- helpers ---------------------------------------------------------
     def _g(self, r):
         return self.ranks[r]
+
+    def _key(self):
+        return (tuple(self.ranks), getattr(self, "tag", ""))
+
+    def _ord(self, kind, peer=None):
+        """Issue-order log (module docstring): collectives are keyed by the
+        communicator, point-to-point traffic by the communicator and the
+        (unordered) rank pair."""
+        if ORDER_LOG["on"] and self.size > 1:
+            if peer is None:
+                _order(self._key(), kind)
+            else:
+                a, b = sorted((self.world_rank, self._g(peer)))
+                _order(self._key() + (a, b), "p2p")
 
     def _note(self, t):
         """Stream log (tests): torch runs a synchronous RCCL collective on
@@ -111,6 +170,7 @@ class Comm:
     @_wd.watched("comm.barrier")
     def barrier(self):
         _wd.beat("comm.barrier")
+        self._ord("barrier")
         if self.size > 1:
             if self.backend == "nccl":
                 # device-side barrier: tiny allreduce on the current stream
@@ -124,6 +184,7 @@ class Comm:
         """Broadcast t from comm-rank root (in place)."""
         _wd.beat("comm.bcast")
         self._note(t)
+        self._ord("bcast")
         if self.size == 1:
             return None
         try:
@@ -147,6 +208,7 @@ class Comm:
     def allreduce(self, t: torch.Tensor, op: str = "sum"):
         _wd.beat("comm.allreduce")
         self._note(t)
+        self._ord("allreduce")
         if self.size == 1:
             return t
         rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
@@ -182,6 +244,7 @@ class Comm:
         """Global (max value, index of max) over ranks; NaN wins, ties -> lowest index."""
         if self.size == 1:
             return value, index
+        self._ord("maxloc")
         dev = "cuda" if self.backend == "nccl" else "cpu"
         t = torch.tensor([[float(value), float(index)]], dtype=torch.float64, device=dev)
         out = [torch.empty_like(t) for _ in range(self.size)]
@@ -198,6 +261,7 @@ class Comm:
         """Concatenate equal-size tensors from all ranks along a new dim 0."""
         _wd.beat("comm.allgather")
         self._note(t)
+        self._ord("allgather")
         if self.size == 1:
             return t.unsqueeze(0)
         x, _ = self._prep(t.contiguous())
@@ -232,6 +296,7 @@ class Comm:
     def reduce(self, t: torch.Tensor, root: int, op="sum"):
         _wd.beat("comm.reduce")
         self._note(t)
+        self._ord("reduce")
         if self.size == 1:
             return t
         x, staged = self._prep(t.contiguous())
@@ -245,6 +310,7 @@ class Comm:
     def send(self, t: torch.Tensor, dst: int, tag: int = 0):
         _wd.beat("comm.send")
         self._note(t)
+        self._ord("p2p", dst)
         if self.size == 1:
             return
         x, _ = self._prep(t.contiguous())
@@ -255,6 +321,7 @@ class Comm:
     def recv(self, t: torch.Tensor, src: int, tag: int = 0):
         _wd.beat("comm.recv")
         self._note(t)
+        self._ord("p2p", src)
         if self.size == 1:
             return t
         x, _ = self._prep(t if t.is_contiguous() else t.contiguous())
@@ -271,6 +338,8 @@ class Comm:
         """Simultaneous exchange (MPI_Sendrecv) via batched p2p."""
         _wd.beat("comm.sendrecv")
         self._note(send_t)
+        for r in sorted({dst, src}):
+            self._ord("p2p", r)
         if self.size == 1:
             recv_t.copy_(send_t)
             return recv_t
@@ -289,6 +358,8 @@ class Comm:
         _wd.beat("comm.exchange")
         for t in list(sends.values()) + list(recvs.values()):
             self._note(t)
+        for r in sorted(set(sends) | set(recvs)):
+            self._ord("p2p", r)
         if self.size == 1 or (not sends and not recvs):
             return
         ops, fix = [], []
@@ -309,6 +380,7 @@ class Comm:
     def bcast_object(self, obj, root: int):
         if self.size == 1:
             return obj
+        self._ord("bcast_object")
         lst = [obj]
         dist.broadcast_object_list(lst, src=self._g(root), group=self.group)
         return lst[0]
@@ -335,6 +407,7 @@ class Comm:
                 g = None
             if self.rank >= 0 and color_of_rank[self.rank] == c:
                 mine = Comm(g, members) if len(members) > 1 else _SelfComm(self.world_rank)
+                mine.tag = tag
         self._subcache[key] = mine
         return mine
 
@@ -608,15 +681,15 @@ class ProcessGrid:
         self.row_comm = comm.split(rows)
         self.col_comm = comm.split(cols)
         self._rows, self._cols = rows, cols
-        self._col_comm_u = None
+        # the update stream's column communicator, created HERE with the
+        # others (not lazily inside a pipeline: communicator creation is a
+        # world collective, see the module docstring)
+        self._col_comm_u = comm.split(cols, tag="update") if p > 1 else self.col_comm
 
     @property
     def col_comm_u(self):
-        """Second column communicator for collectives issued from the
-        low-priority update stream (created on first use: every rank of the
-        grid runs the same driver code, so creation stays collective)."""
-        if self._col_comm_u is None:
-            self._col_comm_u = self.comm.split(self._cols, tag="update")
+        """Second column communicator, for collectives issued from the
+        low-priority update stream."""
         return self._col_comm_u
 
     def coords(self, rank):

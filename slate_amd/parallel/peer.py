@@ -34,6 +34,10 @@ class PeerMailbox:
     def of(cls, comm, device):
         """The communicator's mailbox on ``device`` (kept on the communicator
         object, so a new communicator never inherits a stale one)."""
+        if comm.__dict__.get("_peer_mailbox_dead"):
+            from ..core.exceptions import SlateError
+            raise SlateError("peer mailboxes of this communicator timed out earlier; their sequence tags no longer "
+                             "agree across ranks -- build a new process grid (communicator) to continue")
         boxes = comm.__dict__.setdefault("_peer_mailboxes", {})
         mb = boxes.get(str(device))
         if mb is None:
@@ -92,10 +96,18 @@ class PeerMailbox:
 
     def check(self):
         """Raise if a kernel of this communicator timed out waiting for a peer
-        (reads one device word: call where the driver synchronises anyway)."""
+        (reads one device word: call where the driver synchronises anyway).
+        The error word is sticky and the ranks' host sequence counters may no
+        longer agree after a timeout, so the communicator is marked: every
+        later use of its mailboxes raises instead of waiting on tags that
+        never come.  The mapped buffers stay allocated -- a peer
+        may still store into them -- until release_all() at finalize."""
         if int(self.err.item()) != 0:
             from ..core.exceptions import SlateError
-            raise SlateError("peer mailbox exchange timed out (a column peer never posted its record)")
+            self.comm.__dict__["_peer_mailbox_dead"] = True
+            self.comm.__dict__.pop("_peer_mailboxes", None)
+            raise SlateError("peer mailbox exchange timed out (a column peer never posted its record); "
+                             "this communicator's mailboxes are retired")
 
     def close(self):
         torch.cuda.synchronize(self.device)

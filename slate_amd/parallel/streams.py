@@ -98,8 +98,13 @@ class StreamSet:
         """Make the live update stream carry this set's CU reservation.  Only
         outside every open pipeline of the device; the old stream's work is
         drained first (a reservation switch happens once per change of
-        factorization kind, never inside a step) and a CU-masked stream is
-        destroyed, so the process never holds more than one update stream."""
+        factorization kind, never inside a step).  The retired stream is
+        PARKED, not destroyed: tensors that outlive their driver (geqrf's T
+        factors, ...) may have recorded it with the caching allocator, which
+        records an event on it when they are freed.  A parked
+        stream carries no work and is reused when its reservation comes
+        back, so the process holds at most one stream per reservation and
+        drives exactly one update stream."""
         sh = self.__dict__.get("_sh")
         if sh is None or sh["upd"][0] == self.reserve_cus or StreamSet._open.get(str(self.device), 0):
             return
@@ -107,10 +112,12 @@ class StreamSet:
             return                      # capture: keep the live stream (no sync allowed)
         old_res, old = sh["upd"]
         torch.cuda.synchronize(self.device)
-        sh["upd"] = (self.reserve_cus, self._update_stream(self.device, self.reserve_cus))
-        if old_res > 0 and isinstance(old, torch.cuda.ExternalStream):
-            from .. import _native
-            _native.hip().stream_destroy(old.cuda_stream)
+        parked = sh.setdefault("parked", {})
+        parked[old_res] = old
+        new = parked.pop(self.reserve_cus, None)
+        if new is None:
+            new = self._update_stream(self.device, self.reserve_cus)
+        sh["upd"] = (self.reserve_cus, new)
 
     @staticmethod
     def _update_stream(device, reserve):

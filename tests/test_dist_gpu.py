@@ -225,15 +225,19 @@ def test_multirank_one_gpu(grid):
     run_dist(_check_grid_gpu, grid[0] * grid[1], *grid, timeout=240)
 
 
-def _check_lu_peer(rank, size, p, q):
+def _check_lu_peer(rank, size, p, q, n=1024):
     """The device-resident panel (peer-mapped mailboxes, one persistent launch
     per 32-column block) against the host-issued record all-gather: the
-    same pivots and bit-identical factors, and no per-column collective."""
+    same pivots and bit-identical factors, and no per-column collective.
+    n = 4096 on 2x1 gives each rank more than 1024 panel rows, so the panel
+    runs G > 1 workgroups per rank and the leader's arg-max over their
+    partials is exercised (the winner's candidate row)."""
     import os
     from slate_amd.models import lu as lu_mod
+    from slate_amd.models.aux import allgather_dense as D
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    n, nb = 1024, 256
+    nb = 256
     os.environ["SLATE_AMD_LU_PANEL_GATHER"] = "0"
     out = {}
     for mode in ("0", "1"):
@@ -243,9 +247,12 @@ def _check_lu_peer(rank, size, p, q):
         A = sl.Matrix(n, n, nb=nb, p=p, q=q, device=dev)
         A.insertLocalTiles(device=0)
         sl.generate_matrix(A, "rands", 11)
+        A0 = D(A)
         piv = sl.Pivots()
         assert sl.getrf(A, piv, {Option.Lookahead: 1}) == 0
         torch.cuda.synchronize()
+        r, L = _lu_residual(A0, D(A), piv, n)
+        assert r < 1e-12 and L.abs().max().item() <= 1.0 + 1e-12, (mode, r)
         out[mode] = (A.storage.local[A.storage.origin_slot].clone(), piv.ipiv.clone(), dict(lu_mod.LU_DIST_STATS))
     os.environ["SLATE_AMD_LU_PEER"] = "1"
     f0, p0, st0 = out["0"]
@@ -261,6 +268,7 @@ def _check_lu_peer(rank, size, p, q):
     print(f"rank {rank}: peer LU stats {st1} (host form {st0})")
 
 
-@pytest.mark.parametrize("grid", [(2, 1), (2, 2)], ids=lambda g: f"{g[0]}x{g[1]}")
-def test_lu_panel_peer_mailbox(grid):
-    run_dist(_check_lu_peer, grid[0] * grid[1], *grid, timeout=240)
+@pytest.mark.parametrize("grid,n", [((2, 1), 1024), ((2, 2), 1024), ((2, 1), 4096)],
+                         ids=lambda g: f"{g[0]}x{g[1]}" if isinstance(g, tuple) else f"n{g}")
+def test_lu_panel_peer_mailbox(grid, n):
+    run_dist(_check_lu_peer, grid[0] * grid[1], *grid, n, timeout=240)

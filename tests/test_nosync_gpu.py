@@ -151,6 +151,43 @@ def test_stream_census():
     assert torch.equal(A.storage.local[A.storage.origin_slot], A2.storage.local[A2.storage.origin_slot])
 
 
+def test_retired_update_stream_outlives_its_tensors():
+    """a tensor that recorded the CU-masked update stream
+    (getrf's) and outlives the driver is freed after geqrf switched the live
+    update stream to another reservation: the retired stream is parked, not
+    destroyed, so the allocator's free-time event record is valid; getrf
+    then gets the same parked stream back."""
+    from slate_amd.parallel.streams import StreamSet
+    dev = torch.device("cuda")
+    n, nb = 1024, 256
+    A = sl.Matrix(n, n, nb=nb, device=dev)
+    A.insertLocalTiles(device=dev)
+    sl.generate_matrix(A, "rands", seed=2)
+    assert sl.getrf(A, sl.Pivots()) == 0
+    sets = [s for s in StreamSet._cache.values() if s.gpu and not s.serial]
+    masked = sets[0]._sh["upd"][1]
+    keep = torch.empty(1 << 20, dtype=torch.float64, device=dev)
+    with torch.cuda.stream(masked):
+        keep.fill_(1.0)
+    keep.record_stream(masked)
+    Q = sl.Matrix(4 * n, n // 2, nb=128, device=dev)
+    Q.insertLocalTiles(device=dev)
+    sl.generate_matrix(Q, "rands", seed=3)
+    T = sl.TriangularFactors()
+    sl.geqrf(Q, T)
+    assert sets[0]._sh["upd"][1] is not masked
+    del keep                                  # event recorded on the parked stream
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    A2 = sl.Matrix(n, n, nb=nb, device=dev)
+    A2.insertLocalTiles(device=dev)
+    sl.generate_matrix(A2, "rands", seed=2)
+    assert sl.getrf(A2, sl.Pivots()) == 0
+    assert sets[0]._sh["upd"][1] is masked    # reused, not a new stream per switch
+    del T
+    torch.cuda.synchronize()
+
+
 def test_potrf_use_graph():
     """Option.UseGraph: the one-rank potrf is captured once into a hipGraph
     and replayed; every replay on fresh input matches the eager factor and
