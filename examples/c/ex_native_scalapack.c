@@ -45,6 +45,9 @@ void slate_dgetrf_(const int64_t* m, const int64_t* n, double* a, const int64_t*
 void slate_dgetrs_(const char* trans, const int64_t* n, const int64_t* nrhs, const double* a, const int64_t* lda,
                    const int64_t* ipiv, double* b, const int64_t* ldb, int64_t* info);
 const char* slate_amd_last_error(void);
+void pdsgesv_(const int* n, const int* nrhs, double* a, const int* ia, const int* ja, const int* desca, int* ipiv,
+              const double* b, const int* ib, const int* jb, const int* descb, double* x, const int* ix,
+              const int* jx, const int* descx, int* iter, int* info);
 void pdsyrk_(const char* uplo, const char* trans, const int* n, const int* k, const double* alpha, const double* a,
              const int* ia, const int* ja, const int* desca, const double* beta, double* c, const int* ic,
              const int* jc, const int* descc);
@@ -305,6 +308,18 @@ int main(int argc, char** argv) {
     pdgetrf_(&n, &n, a, &one, &one, desca, ipiv, &info);
     pdgetrs_("N", &n, &nrhs, a, &one, &one, desca, ipiv, b, &one, &one, descb, &info);
     check(info ? "pdgetrs-FAILED" : "pdgetrs", ERR_B());
+    /* mixed precision: single-precision LU, double refinement (X = A^-1 B, B kept) */
+    {
+        FILL_A(gen);
+        FILL_B(gen);
+        double* x = malloc(sizeof(double) * lld * (rloc > 0 ? rloc : 1));
+        int iter = -100;
+        pdsgesv_(&n, &nrhs, a, &one, &one, desca, ipiv, b, &one, &one, descb, x, &one, &one, descb, &iter, &info);
+        if (info) printf("pdsgesv info %d (%s)\n", info, slate_amd_last_error());
+        memcpy(b, x, sizeof(double) * lld * (rloc > 0 ? rloc : 1));
+        check(info || iter < 0 ? "pdsgesv-FAILED" : "pdsgesv", ERR_B());
+        free(x);
+    }
 
     /* least squares through QR (TSQR panels when p > 1): a consistent square system */
     {

@@ -145,6 +145,7 @@ def build(verbose=False, hip=True, host=True):
         out.append(_build_native_example(verbose))
         out.append(_build_native_example(verbose, "bench_native"))
         out.append(_build_native_c_example(verbose))
+        out.append(_build_native_c_example(verbose, "ex_native_lapack"))
     return out
 
 
@@ -167,13 +168,13 @@ def _build_native_example(verbose=False, name="ex_native"):
     return target
 
 
-def _build_native_c_example(verbose=False):
-    """examples/c/ex_native_scalapack.c -> slate_amd/ex_native_scalapack: a
-    plain C program calling the ScaLAPACK / BLACS / LAPACK symbols of
-    libslate_amd_native.so (no Python, no MPI)."""
-    src = os.path.join(ROOT, "examples", "c", "ex_native_scalapack.c")
+def _build_native_c_example(verbose=False, name="ex_native_scalapack"):
+    """examples/c/<name>.c -> slate_amd/<name>: a plain C program calling the
+    ScaLAPACK / BLACS / LAPACK / handle symbols of libslate_amd_native.so (no
+    Python, no MPI)."""
+    src = os.path.join(ROOT, "examples", "c", name + ".c")
     lib = os.path.join(HERE, "libslate_amd_native.so")
-    target = os.path.join(HERE, "ex_native_scalapack")
+    target = os.path.join(HERE, name)
     if _newer(target, [src, lib]):
         cmd = ["gcc", "-O2", "-std=gnu11", src, "-o", target, "-L" + HERE, "-lslate_amd_native", "-lm",
                "-Wl,-rpath,$ORIGIN"]

@@ -38,55 +38,10 @@
 namespace sn = slate_amd::native;
 using sn::i64;
 
+#include "capi_util.hpp"
+using namespace slate_amd::native::capi;
+
 namespace {
-constexpr int ERR_INTERNAL = -1000000;
-thread_local std::string g_err;
-
-void grid_of(int& p, int& q) {
-    const int ws = sn::size();
-    p = 1;
-    q = ws;
-    if (const char* g = std::getenv("SLATE_AMD_NATIVE_GRID")) {
-        int a = 0, b = 0;
-        if (std::sscanf(g, "%dx%d", &a, &b) == 2 && a * b == ws) { p = a; q = b; }
-    }
-}
-
-int64_t nb_of(int64_t n) {
-    if (const char* e = std::getenv("SLATE_AMD_NATIVE_NB")) return std::max<int64_t>(16, std::atoll(e));
-    return n >= 8192 ? 512 : (n >= 1024 ? 256 : 64);
-}
-
-template <typename F>
-int64_t guarded(F&& f) {
-    try {
-        return (int64_t)f();
-    } catch (const std::exception& e) {
-        g_err = e.what();
-        return ERR_INTERNAL;
-    }
-}
-
-char up(char c) { return (c >= 'a' && c <= 'z') ? (char)(c - 32) : c; }
-
-template <typename T> T cj(T x) { return x; }
-template <typename R> std::complex<R> cj(std::complex<R> x) { return std::conj(x); }
-
-// op(a) (rows x cols of the RESULT) into a new column-major array
-template <typename T>
-std::vector<T> host_op(char op, i64 rows, i64 cols, const T* a, i64 lda) {
-    std::vector<T> r((size_t)rows * cols);
-    for (i64 j = 0; j < cols; ++j)
-        for (i64 i = 0; i < rows; ++i)
-            r[i + j * rows] = op == 'N' ? a[i + j * lda] : op == 'T' ? a[j + i * lda] : cj(a[j + i * lda]);
-    return r;
-}
-
-sn::Op op_of(char c) {
-    c = up(c);
-    return c == 'N' ? sn::Op::NoTrans : c == 'T' ? sn::Op::Trans : sn::Op::ConjTrans;
-}
-
 // ------------------------------------------------------------ host arrays
 template <typename T>
 int64_t h_potrf(char uplo, i64 n, T* a, i64 lda) {
@@ -731,6 +686,35 @@ int p_posv(char uplo, int n, int nrhs, T* a, int ia, int ja, const int* desca, T
     return p_potrs<T>(uplo, n, nrhs, a, ia, ja, desca, b, ib, jb, descb);
 }
 
+// p?gesv_mixed (reference scalapack_api/scalapack_gesv_mixed.cc): factor in
+// the lower precision, refine in the working one; X = A^-1 B, B unchanged
+template <typename T>
+int p_gesv_mixed(int n, int nrhs, T* a, int ia, int ja, const int* desca, int* ipiv, const T* b, int ib, int jb,
+                 const int* descb, T* x, int ix, int jx, const int* descx, int* iter) {
+    if (n < 0) return -1;
+    if (nrhs < 0) return -2;
+    *iter = 0;
+    if (n == 0 || nrhs == 0) return 0;
+    return (int)guarded([&]() -> int64_t {
+        sn::Matrix<T> A = scal_matrix<T>(desca, n, n, ia, ja, a);
+        sn::Matrix<T> B = scal_matrix<T>(descb, n, nrhs, ib, jb, b);
+        sn::Matrix<T> X = scal_matrix<T>(descx, n, nrhs, ix, jx, x);
+        if (B.nb() != A.nb() || X.nb() != A.nb() || B.p() != A.p() || X.p() != A.p() || B.q() != A.q() ||
+            X.q() != A.q())
+            throw sn::Error("native p?gesv_mixed: B and X must have A's block size and grid");
+        std::vector<int64_t> piv;
+        int it = 0;
+        const int64_t info = sn::gesv_mixed<T>(A, piv, B, X, it);
+        *iter = it;
+        scal_back(X, descx, x);
+        if (it < 0) {            // the working-precision fallback factored A (LAPACK dsgesv semantics)
+            scal_back(A, desca, a);
+            ipiv_to_local(A, desca, ia, piv, ipiv);
+        }
+        return info;
+    });
+}
+
 template <typename T>
 int p_getrf(int m, int n, T* a, int ia, int ja, const int* desca, int* ipiv) {
     if (m == 0 || n == 0) return 0;
@@ -1285,6 +1269,19 @@ int p_gesvd(char jobu, char jobvt, int m, int n, const T* a, int ia, int ja, con
 }
 
 extern "C" {
+
+void pdsgesv_(const int* n, const int* nrhs, double* a, const int* ia, const int* ja, const int* desca, int* ipiv,
+              const double* b, const int* ib, const int* jb, const int* descb, double* x, const int* ix,
+              const int* jx, const int* descx, int* iter, int* info) {
+    *info = p_gesv_mixed<double>(*n, *nrhs, a, *ia, *ja, desca, ipiv, b, *ib, *jb, descb, x, *ix, *jx, descx, iter);
+}
+void pzcgesv_(const int* n, const int* nrhs, std::complex<double>* a, const int* ia, const int* ja,
+              const int* desca, int* ipiv, const std::complex<double>* b, const int* ib, const int* jb,
+              const int* descb, std::complex<double>* x, const int* ix, const int* jx, const int* descx, int* iter,
+              int* info) {
+    *info = p_gesv_mixed<std::complex<double>>(*n, *nrhs, a, *ia, *ja, desca, ipiv, b, *ib, *jb, descb, x, *ix, *jx,
+                                               descx, iter);
+}
 
 const char* slate_amd_last_error(void) { return g_err.c_str(); }
 int slate_amd_initialize(void) { return (int)guarded([] { sn::initialize(); return 0; }); }

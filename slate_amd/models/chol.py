@@ -508,6 +508,24 @@ def _potrf_info(s, infos, g0, nt):
     return info
 
 
+def _group_schedule(nt, G):
+    """Tile groups of the one-rank potrf: G tiles per group (K = G nb
+    trailing GEMMs), except the first SLATE_AMD_POTRF_HEAD and the last
+    SLATE_AMD_POTRF_TAIL tiles, which go one per group.  At both ends the
+    update stream idles behind the panel chain (kernel trace of the n =
+    32768 bench, profiles/r6/potrf_1gpu_update_stream_gaps.txt: 2.6 ms idle
+    in the first 10 % of the span, 7.0 ms in the last 10 %): a one-tile
+    group halves that chain where the trailing GEMM is too small to hide it."""
+    head = max(0, int(os.environ.get("SLATE_AMD_POTRF_HEAD", "0")))
+    tail = max(0, int(os.environ.get("SLATE_AMD_POTRF_TAIL", "0")))
+    head = min(head, nt)
+    tail = min(tail, nt - head)
+    out = [[t] for t in range(head)]
+    out += [list(range(t, min(t + G, nt - tail))) for t in range(head, nt - tail, G)]
+    out += [[t] for t in range(nt - tail, nt)]
+    return out
+
+
 def _potrf_1x1_grouped(A, s, buf, nb, g0, nt, R_end, la, G, ss, infos, ct, dev, serial=False):
     """One rank owning the whole matrix: panels are factored one tile at a
     time, but the trailing update is applied once per GROUP of G tiles with
@@ -520,7 +538,7 @@ def _potrf_1x1_grouped(A, s, buf, nb, g0, nt, R_end, la, G, ss, infos, ct, dev, 
     ``la`` groups' columns; the update stream does the rest, first the
     columns of group g + la + 1 (event), then everything else."""
     off = lambda t: s.row_offsets[min(g0 + t, g0 + nt)] if g0 + t < g0 + nt else R_end   # noqa: E731
-    groups = [list(range(t, min(t + G, nt))) for t in range(0, nt, G)]
+    groups = _group_schedule(nt, G)
     ng = len(groups)
     gstart = lambda gi: off(groups[gi][0]) if gi < ng else R_end     # noqa: E731
     end = R_end

@@ -54,6 +54,15 @@ def test_native_library_exports_lapack_scalapack_blacs():
              "slate_dsyev", "slate_dsyevd", "slate_zheev", "slate_zheevd", "psgesvd_", "pdgesvd_", "pcgesvd_",
              "pzgesvd_", "slate_dgesvd", "slate_zgesvd"]
     want += ["pclanhe_", "pzlanhe_", "pcherk_", "pzherk_", "pcher2k_", "pzher2k_", "pchemm_", "pzhemm_"]
+    # the LAPACK-style families that lived only in the
+    # CPython-backed ABI, and the mixed-precision ScaLAPACK solvers
+    for x in "sdcz":
+        want += [f"slate_{x}{w}" for w in ("trmm", "syrk", "syr2k", "symm", "getri", "potri", "lansy", "lantr")]
+    for x in "cz":
+        want += [f"slate_{x}{w}" for w in ("herk", "her2k", "hemm", "lanhe")]
+    for x in "sd":
+        want += [f"slate_{x}{w}_" for w in ("trmm", "syrk", "syr2k", "symm", "getri", "potri", "lansy", "lantr")]
+    want += ["pdsgesv_", "pzcgesv_"]
     missing = [w for w in want if w not in names]
     assert not missing, missing
 
@@ -160,6 +169,29 @@ def test_native_example_grids_host_transport(grid):
     _assert_checks(_checks(out0), out0)
 
 
+LEXE = os.path.join(ROOT, "slate_amd", "ex_native_lapack")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nranks", [1, 2])
+def test_native_lapack_more_from_c(nranks):
+    """slate_?trmm/syrk/syr2k/symm/getri/potri/lansy/lantr and the complex
+    herk/her2k/hemm/lanhe of libslate_amd_native.so, from plain C against
+    naive host loops (1 rank, and 2 ranks over the host transport)."""
+    assert os.path.exists(LEXE), "slate_amd/ex_native_lapack not built"
+    ldd = subprocess.run(["ldd", LEXE], capture_output=True, text=True, env=_clean_env()).stdout
+    assert "python" not in ldd.lower(), ldd
+    if nranks == 1:
+        r = subprocess.run([LEXE, "200"], capture_output=True, text=True, env=_clean_env(), timeout=240)
+        outs = [(r.returncode, r.stdout + r.stderr)]
+    else:
+        outs = _run_ranks(LEXE, ["150"], nranks)
+    for rc, out in outs:
+        print(out)
+        assert rc == 0 and "all checks passed" in out, out
+        assert len(_checks(out)) >= 20, out
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("grid", ["1x1", "2x2", "2x1"])
 def test_native_scalapack_from_c_without_python(grid):
@@ -176,7 +208,7 @@ def test_native_scalapack_from_c_without_python(grid):
         outs = _run_ranks(CEXE, [grid], p * q)
     names = ("pdpotrs", "pdpotrs_upper", "pdgesv", "pdgetrs", "pdlange_fro", "pdgemm_tn", "pdsyrk_lower", "pdtrmm_lun", "pdpotri", "pdgetri", "pdlaset_lacpy_geadd",
              "pzgesv", "slate_dgetrf_", "pdgemm_sub", "pdpotrs_sub", "pdgetrs_sub", "pdtrsm_right", "pztrsm_trans",
-             "pdgecon", "pdpocon", "pdtrcon", "pdsyevd", "pdgesvd", "pdgels")
+             "pdgecon", "pdpocon", "pdtrcon", "pdsyevd", "pdgesvd", "pdgels", "pdsgesv")
     for rank, (rc, out) in enumerate(outs):
         print(out)
         assert rc == 0, out
