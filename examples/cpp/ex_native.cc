@@ -741,6 +741,102 @@ void run(int p, int q, int me) {
             report(inf || iter < 0 ? (v ? "gesv_mixed-FAILED" : "posv_mixed-FAILED") : (v ? "gesv_mixed" : "posv_mixed"),
                    rel<T>(ax, want));
         }
+        // GMRES-IR: the same systems through restarted GMRES preconditioned
+        // by the low-precision factors
+        for (int v = 0; v < 2; ++v) {
+            sn::Matrix<T> Bm(nm, 3, nb, p, q), Xm(nm, 3, nb, p, q);
+            Bm.generate(sn::Gen::Random, 105 + v);
+            std::vector<T> ha((size_t)nm * nm), hb((size_t)nm * 3), hx((size_t)nm * 3);
+            Bm.to_host(hb.data(), nm);
+            int iter = -100;
+            int64_t inf;
+            if (v == 0) {
+                sn::HermitianMatrix<T> Hm(sn::Uplo::Lower, nm, nb, p, q);
+                Hm.generate(sn::Gen::HermitianPositiveDefinite, 107);
+                Hm.to_host(ha.data(), nm);
+                for (int64_t j = 0; j < nm; ++j)
+                    for (int64_t i = 0; i < j; ++i) ha[i + j * nm] = cj(ha[j + i * nm]);
+                inf = sn::posv_mixed_gmres(Hm, Bm, Xm, iter);
+            } else {
+                sn::Matrix<T> Gm(nm, nm, nb, p, q);
+                Gm.generate(sn::Gen::DiagDominant, 108);
+                Gm.to_host(ha.data(), nm);
+                std::vector<int64_t> pv;
+                inf = sn::gesv_mixed_gmres(Gm, pv, Bm, Xm, iter);
+            }
+            Xm.to_host(hx.data(), nm);
+            auto ax = mul<T>('N', 'N', nm, 3, nm, ha, nm, hx, nm);
+            auto want = widen(hb);
+            for (size_t i = 0; i < ax.size(); ++i) ax[i] -= want[i];
+            if (me == 0) std::printf("gmres %s iter %d info %lld\n", v ? "gesv" : "posv", iter, (long long)inf);
+            report(inf || iter < 0 ? (v ? "gesv_gmres-FAILED" : "posv_gmres-FAILED") : (v ? "gesv_gmres" : "posv_gmres"),
+                   rel<T>(ax, want));
+        }
+    }
+    // ---- gesv_rbt: random butterflies + LU without pivoting + refinement
+    //      (n not a multiple of the butterfly unit: the padded path)
+    {
+        const int64_t nr = 150;
+        sn::Matrix<T> Gm(nr, nr, nb, p, q), Bm(nr, nrhs, nb, p, q);
+        Gm.generate(sn::Gen::Random, 151);
+        Bm.generate(sn::Gen::Random, 152);
+        std::vector<T> ha((size_t)nr * nr), hb((size_t)nr * nrhs), hx((size_t)nr * nrhs);
+        Gm.to_host(ha.data(), nr);
+        Bm.to_host(hb.data(), nr);
+        const int64_t inf = sn::gesv_rbt(Gm, Bm);
+        Bm.to_host(hx.data(), nr);
+        auto ax = mul<T>('N', 'N', nr, nrhs, nr, ha, nr, hx, nr);
+        auto want = widen(hb);
+        for (size_t i = 0; i < ax.size(); ++i) ax[i] -= want[i];
+        report(inf ? "gesv_rbt-FAILED" : "gesv_rbt", rel<T>(ax, want));
+    }
+    // ---- hegv: A Z = B Z Lambda (itype 1), A B Z = Z Lambda (2),
+    //      B A Z = Z Lambda (3); B Lower and Upper; || residual || / (|| A || || B || n)
+    for (int v = 0; v < 3; ++v) {
+        const int64_t ng = 140;
+        const int64_t itype = v + 1;
+        const sn::Uplo ub = v == 1 ? sn::Uplo::Upper : sn::Uplo::Lower;
+        sn::HermitianMatrix<T> Ah(sn::Uplo::Lower, ng, nb, p, q);
+        Ah.generate(sn::Gen::Random, 161 + v);
+        sn::HermitianMatrix<T> Bl(sn::Uplo::Lower, ng, nb, p, q);
+        Bl.generate(sn::Gen::HermitianPositiveDefinite, 171 + v);
+        std::vector<T> ha((size_t)ng * ng), hbm((size_t)ng * ng), z((size_t)ng * ng);
+        Ah.to_host(ha.data(), ng);
+        Bl.to_host(hbm.data(), ng);
+        for (int64_t j = 0; j < ng; ++j) {
+            ha[j + j * ng] = T(std::real(ha[j + j * ng]));
+            hbm[j + j * ng] = T(std::real(hbm[j + j * ng]));
+            for (int64_t i = 0; i < j; ++i) {
+                ha[i + j * ng] = cj(ha[j + i * ng]);
+                hbm[i + j * ng] = cj(hbm[j + i * ng]);
+            }
+        }
+        sn::HermitianMatrix<T> Bh(ub, ng, nb, p, q);
+        Bh.from_host(hbm.data(), ng);
+        Ah.from_host(ha.data(), ng);
+        sn::Matrix<T> Z(ng, ng, nb, p, q);
+        std::vector<sn::real_t<T>> lam;
+        const int64_t inf = sn::hegv(itype, Ah, Bh, lam, Z);
+        Z.to_host(z.data(), ng);
+        std::vector<std::complex<double>> lhs, rhs;
+        if (itype == 1) {
+            lhs = mul<T>('N', 'N', ng, ng, ng, ha, ng, z, ng);
+            rhs = mul<T>('N', 'N', ng, ng, ng, hbm, ng, z, ng);
+        } else {
+            std::vector<T> prod((size_t)ng * ng);
+            auto in = mul<T>('N', 'N', ng, ng, ng, itype == 2 ? hbm : ha, ng, z, ng);
+            for (size_t i = 0; i < prod.size(); ++i) prod[i] = val<T>(in[i].real(), in[i].imag());
+            lhs = mul<T>('N', 'N', ng, ng, ng, itype == 2 ? ha : hbm, ng, prod, ng);
+            rhs = widen(z);
+        }
+        double e = 0, an = 0, bn = 0;
+        for (int64_t j = 0; j < ng; ++j)
+            for (int64_t i = 0; i < ng; ++i) e += std::norm(lhs[i + j * ng] - rhs[i + j * ng] * (double)lam[j]);
+        for (size_t i = 0; i < ha.size(); ++i) { an += std::norm(ha[i]); bn += std::norm(hbm[i]); }
+        bool sorted = true;
+        for (size_t i = 1; i < lam.size(); ++i) sorted = sorted && lam[i - 1] <= lam[i];
+        const char* nm3[] = {"hegv1", "hegv2_upper", "hegv3"};
+        report(inf || !sorted ? "hegv-FAILED" : nm3[v], std::sqrt(e) / (std::sqrt(an) * std::sqrt(bn) * ng));
     }
 }
 

@@ -69,6 +69,9 @@ struct Options {
     int lookahead = 1;        // SLATE Option::Lookahead
     double pivot_threshold = 1.0;
     int inner_blocking = 32;  // columns per base block of the distributed LU panel
+    int depth = 2;            // SLATE Option::Depth: butterfly levels of gesv_rbt (1..4)
+    int max_iterations = 30;  // SLATE Option::MaxIterations: refinement / GMRES steps
+    int restart = 30;         // GMRES restart length (gesv/posv_mixed_gmres)
 };
 
 struct Storage;               // opaque: device buffer, grid, communicators
@@ -262,6 +265,50 @@ int64_t heev(HermitianMatrix<T>& A, std::vector<real_t<T>>& Lambda, const Option
 template <typename T>
 int64_t svd(Matrix<T>& A, std::vector<real_t<T>>& S, Matrix<T>& U, Matrix<T>& VH, const Options& opts = {});
 template <typename T> int64_t svd(Matrix<T>& A, std::vector<real_t<T>>& S, const Options& opts = {});
+
+// ---- round 6: generalized eigenproblem, GMRES-IR, random butterfly transform
+// hegst (reference slate.hh:1138): reduce the generalized Hermitian-definite
+// problem to standard form with the Cholesky factor of B held in L (potrf of
+// B, its stored triangle): itype 1 A <- L^-1 A L^-H (Lower) / U^-H A U^-1
+// (Upper); itype 2, 3 A <- L^H A L / U A U^H.  A's stored triangle is
+// referenced, the full Hermitian result is written.
+template <typename T>
+void hegst(int64_t itype, HermitianMatrix<T>& A, const HermitianMatrix<T>& L, const Options& opts = {});
+// hegv (slate.hh:1082): A x = lambda B x (itype 1), A B x = lambda x (2),
+// B A x = lambda x (3); B is overwritten by its Cholesky factor, A by the
+// standard-form matrix; Z (A's grid) the B-normalised eigenvectors.  info
+// > 0: B not positive definite (n + the potrf info, as LAPACK)
+template <typename T>
+int64_t hegv(int64_t itype, HermitianMatrix<T>& A, HermitianMatrix<T>& B, std::vector<real_t<T>>& Lambda,
+             Matrix<T>& Z, const Options& opts = {});
+template <typename T>
+int64_t hegv(int64_t itype, HermitianMatrix<T>& A, HermitianMatrix<T>& B, std::vector<real_t<T>>& Lambda,
+             const Options& opts = {});
+// GMRES-based iterative refinement (src/gesv_mixed_gmres.cc,
+// posv_mixed_gmres.cc): the low-precision factors precondition restarted
+// GMRES on the working-precision system, one right-hand side at a time.
+// double / complex<double>; iter = total GMRES steps (< 0: fell back to the
+// working-precision solve)
+template <typename T>
+int64_t gesv_mixed_gmres(Matrix<T>& A, std::vector<int64_t>& ipiv, Matrix<T>& B, Matrix<T>& X, int& iter,
+                         const Options& opts = {});
+template <typename T>
+int64_t posv_mixed_gmres(HermitianMatrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, const Options& opts = {});
+// random butterfly transform + LU without pivoting + refinement
+// (src/gesv_rbt.cc): B <- A^-1 B; A is overwritten by the factors of the
+// transformed (and, when n is not a multiple of the butterfly unit, padded)
+// matrix only if n already is that multiple -- otherwise A is unchanged
+template <typename T> int64_t gesv_rbt(Matrix<T>& A, Matrix<T>& B, const Options& opts = {});
+// Hermitian indefinite solve (slate.hh hesv): A X = B for the Hermitian A of
+// the stored triangle, B <- X.  Here the full Hermitian matrix is solved by
+// LU with partial pivoting (A receives those factors); the communication-
+// avoiding Aasen hetrf of the Python package is not native yet.
+template <typename T> int64_t hesv(HermitianMatrix<T>& A, Matrix<T>& B, const Options& opts = {});
+// A <- (numer / denom) A (slate.hh scale), computed without forming the ratio
+// when it would overflow
+template <typename T> void scale(real_t<T> numer, real_t<T> denom, Matrix<T>& A);
+// LU solve with the factors of getrf_nopiv
+template <typename T> int64_t getrs_nopiv(const Matrix<T>& A, Matrix<T>& B, const Options& opts = {});
 
 struct QRData;
 template <typename T>

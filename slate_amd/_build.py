@@ -146,6 +146,7 @@ def build(verbose=False, hip=True, host=True):
         out.append(_build_native_example(verbose, "bench_native"))
         out.append(_build_native_c_example(verbose))
         out.append(_build_native_c_example(verbose, "ex_native_lapack"))
+        out.append(_build_native_c_example(verbose, "ex_native_handles"))
     return out
 
 
@@ -176,7 +177,8 @@ def _build_native_c_example(verbose=False, name="ex_native_scalapack"):
     lib = os.path.join(HERE, "libslate_amd_native.so")
     target = os.path.join(HERE, name)
     if _newer(target, [src, lib]):
-        cmd = ["gcc", "-O2", "-std=gnu11", src, "-o", target, "-L" + HERE, "-lslate_amd_native", "-lm",
+        cmd = ["gcc", "-O2", "-std=gnu11", src, "-o", target, "-I" + os.path.join(ROOT, "include"),
+               "-L" + HERE, "-lslate_amd_native", "-lm",
                "-Wl,-rpath,$ORIGIN"]
         if verbose:
             print(" ".join(cmd), flush=True)

@@ -1692,7 +1692,7 @@ static slate_hip::TriMask tri_mask(const Storage& S, Uplo uplo, i64 diag_off = 0
 // zero; a Unit diagonal set to one), 1 = Hermitian (the other part is the
 // stored one conjugate-transposed, real diagonal), 2 = symmetric
 template <typename T>
-static Matrix<T> expand_tri(const Matrix<T>& A, Uplo uplo, int kind, Diag diag = Diag::NonUnit) {
+Matrix<T> expand_tri(const Matrix<T>& A, Uplo uplo, int kind, Diag diag) {
     const Storage& S = *A.storage();
     if (S.m != S.n) throw Error("native: square triangular / Hermitian matrix expected");
     hipStream_t s = rt().main;
@@ -2702,7 +2702,8 @@ int64_t gels(Matrix<T>& A, Matrix<T>& BX, const Options& opts) {
     template void set<T>(T, T, Matrix<T>&);                                                                   \
     template double gecondest<T>(Norm, const Matrix<T>&, double, const Options&);                             \
     template double pocondest<T>(Norm, const HermitianMatrix<T>&, double, const Options&);                    \
-    template double trcondest<T>(Norm, Uplo, Diag, const Matrix<T>&, const Options&);
+    template double trcondest<T>(Norm, Uplo, Diag, const Matrix<T>&, const Options&);                         \
+    template Matrix<T> expand_tri<T>(const Matrix<T>&, Uplo, int, Diag);
 SLATE_NATIVE_INST(float)
 SLATE_NATIVE_INST(double)
 SLATE_NATIVE_INST(std::complex<float>)

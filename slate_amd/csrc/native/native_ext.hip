@@ -1,0 +1,578 @@
+// Native drivers added in round 6: the generalized Hermitian-definite
+// eigenproblem (hegst / hegv), GMRES-based mixed-precision refinement
+// (gesv_mixed_gmres / posv_mixed_gmres) and the random butterfly transform
+// solver (gesv_rbt, getrs_nopiv).  Reference: src/hegst.cc, src/hegv.cc,
+// src/gesv_mixed_gmres.cc, src/posv_mixed_gmres.cc, src/gesv_rbt.cc,
+// src/gerbt.cc (include/slate/slate.hh:540, 558, 688, 1082, 1138).
+//
+// Design (MI355X): every O(n^3) step is an existing distributed driver of
+// native.hip (potrf, trsm, trmm, heev, getrf_nopiv on the MFMA kernels).
+// The GMRES Krylov basis lives in ONE device buffer per rank -- the local
+// rows of the restart + 1 basis vectors side by side -- so the classical
+// Gram-Schmidt projections are one batched GEMV kernel and one all-reduce of
+// j + 1 scalars per pass (two passes, CGS2), and only the (restart + 1) x
+// restart Hessenberg least-squares problem runs on the host (Givens), as in
+// the reference.  The butterflies run as the one-pass register kernel of
+// csrc/hip/aux.hip on each rank's local rows: the order is padded to a
+// multiple of 2^depth nb lcm(p, q), so every butterfly partner is local.
+#include <algorithm>
+#include <cmath>
+#include <limits>
+#include <numeric>
+#include <random>
+#include <vector>
+
+#include "../hip/kernels.hpp"
+#include "native_rt.hpp"
+
+namespace slate_amd {
+namespace native {
+
+namespace {
+
+using slate_hip::s_add;
+using slate_hip::s_conj;
+using slate_hip::s_from_real;
+using slate_hip::s_mul;
+using slate_hip::s_sub;
+
+// ------------------------------------------------------------ small vector kernels
+// h[i] = sum_r conj(V[r + i ldv]) w[r], i < nv: one workgroup per basis vector
+template <typename KT>
+__global__ void __launch_bounds__(256) multi_dotc_kernel(i64 m, const KT* __restrict__ V, i64 ldv,
+                                                         const KT* __restrict__ w, KT* __restrict__ h) {
+    __shared__ KT red[256];
+    const int i = blockIdx.x;
+    KT acc = s_from_real(KT(), 0);
+    for (i64 r = threadIdx.x; r < m; r += 256) acc = s_add(acc, s_mul(s_conj(V[r + i * ldv]), w[r]));
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] = s_add(red[threadIdx.x], red[threadIdx.x + s]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) h[i] = red[0];
+}
+
+// w[r] += alpha sum_i V[r + i ldv] h[i] (h on the device)
+template <typename KT>
+__global__ void __launch_bounds__(256) multi_axpy_kernel(i64 m, int nv, KT alpha, const KT* __restrict__ V, i64 ldv,
+                                                         const KT* __restrict__ h, KT* __restrict__ w) {
+    const i64 r = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (r >= m) return;
+    KT acc = s_from_real(KT(), 0);
+    for (int i = 0; i < nv; ++i) acc = s_add(acc, s_mul(V[r + i * ldv], h[i]));
+    w[r] = s_add(w[r], s_mul(alpha, acc));
+}
+
+template <typename T>
+void multi_dotc(i64 m, int nv, const T* V, i64 ldv, const T* w, T* h_d, hipStream_t s) {
+    if (m > 0 && nv > 0) hipLaunchKernelGGL(multi_dotc_kernel<K<T>>, dim3(nv), dim3(256), 0, s, m, kp(V), ldv, kp(w), kp(h_d));
+    else if (nv > 0) NHIP(hipMemsetAsync(h_d, 0, sizeof(T) * nv, s));
+}
+
+template <typename T>
+void multi_axpy(i64 m, int nv, T alpha, const T* V, i64 ldv, const T* h_d, T* w, hipStream_t s) {
+    if (m > 0 && nv > 0)
+        hipLaunchKernelGGL(multi_axpy_kernel<K<T>>, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, m, nv,
+                           kv(alpha), kp(V), ldv, kp(h_d), kp(w));
+}
+
+// sum over all ranks of a device array (in place), then to the host
+template <typename T>
+std::vector<T> allsum(T* d, int n, hipStream_t s) {
+    if (Comm* w = world_comm()) w->allreduce(d, (size_t)n, dt_of<T>::v, 's', s);
+    std::vector<T> h((size_t)n);
+    NHIP(hipMemcpyAsync(h.data(), d, sizeof(T) * n, hipMemcpyDeviceToHost, s));
+    NHIP(hipStreamSynchronize(s));
+    return h;
+}
+
+// ------------------------------------------------------------ distributed n x 1 vectors
+// The basis / work vectors of GMRES: n x 1 matrices on A's grid, i.e. the
+// local rows live on process column 0 (other ranks hold no rows).  Column
+// c of an n x k matrix B sits on process column (c / nb) % q at the SAME
+// local rows, so moving it is one broadcast of mloc elements over the row
+// communicator.
+template <typename T>
+struct VecSet {
+    i64 n = 0, mloc = 0, ld = 1;
+    int count = 0;
+    Scratch buf;
+    const Storage* shape = nullptr;
+    VecSet(const Storage& S, int cnt, hipStream_t s)
+        : n(S.m), mloc(S.pc == 0 ? S.mloc : 0), ld(std::max<i64>(1, (S.mloc + 15) / 16 * 16)), count(cnt),
+          buf(sizeof(T) * (size_t)std::max<i64>(1, (S.pc == 0 ? ld : 1) * cnt), s), shape(&S) {
+        NHIP(hipMemsetAsync(buf.p, 0, sizeof(T) * (size_t)std::max<i64>(1, (S.pc == 0 ? ld : 1) * cnt), s));
+    }
+    T* col(int i) { return buf.as<T>() + (mloc ? (i64)i * ld : 0); }
+    // n x 1 Matrix over vector i (zero-copy)
+    Matrix<T> mat(int i) {
+        return Matrix<T>::from_device(col(i), ld, n, 1, shape->nb, shape->p, shape->q);
+    }
+};
+
+// dst (mloc on process column 0) <- column c of B
+template <typename T>
+void get_col(const Storage& SB, i64 c, T* dst, hipStream_t s) {
+    const int pcc = (int)((c / SB.nb) % SB.q);
+    const i64 lc = (c / SB.nb) / SB.q * SB.nb + c % SB.nb;
+    if (SB.q == 1) {
+        copy2d(dst, SB.lld, static_cast<const T*>(SB.buf) + lc * SB.lld, SB.lld, SB.mloc, 1, s);
+        return;
+    }
+    Scratch t(sizeof(T) * std::max<i64>(1, SB.mloc), s);
+    if (SB.pc == pcc) copy2d(t.as<T>(), SB.mloc, static_cast<const T*>(SB.buf) + lc * SB.lld, SB.lld, SB.mloc, 1, s);
+    if (SB.mloc) SB.gc->row->bcast(t.p, sizeof(T) * SB.mloc, pcc, s);
+    if (SB.pc == 0) copy2d(dst, SB.mloc, t.as<T>(), SB.mloc, SB.mloc, 1, s);
+    NHIP(hipStreamSynchronize(s));
+}
+
+// column c of B <- src (mloc on process column 0)
+template <typename T>
+void put_col(const T* src, Storage& SB, i64 c, hipStream_t s) {
+    const int pcc = (int)((c / SB.nb) % SB.q);
+    const i64 lc = (c / SB.nb) / SB.q * SB.nb + c % SB.nb;
+    if (SB.q == 1) {
+        copy2d(static_cast<T*>(SB.buf) + lc * SB.lld, SB.lld, src, SB.lld, SB.mloc, 1, s);
+        return;
+    }
+    Scratch t(sizeof(T) * std::max<i64>(1, SB.mloc), s);
+    if (SB.pc == 0) copy2d(t.as<T>(), SB.mloc, src, SB.mloc, SB.mloc, 1, s);
+    if (SB.mloc) SB.gc->row->bcast(t.p, sizeof(T) * SB.mloc, 0, s);
+    if (SB.pc == pcc) copy2d(static_cast<T*>(SB.buf) + lc * SB.lld, SB.lld, t.as<T>(), SB.mloc, SB.mloc, 1, s);
+    NHIP(hipStreamSynchronize(s));
+}
+
+template <typename T> struct lower_of;
+template <> struct lower_of<double> { using type = float; };
+template <> struct lower_of<std::complex<double>> { using type = std::complex<float>; };
+
+template <typename Hi, typename Lo>
+void convert_local(const Storage& SA, Storage& SB, hipStream_t s) {
+    if (SA.mloc && SA.nloc)
+        slate_hip::gecopy<K<Hi>, K<Lo>>('G', 'N', SA.mloc, SA.nloc, kp(static_cast<const Hi*>(SA.buf)), SA.lld,
+                                        kp(static_cast<Lo*>(SB.buf)), SB.lld, s);
+}
+
+template <typename T>
+double vnorm2(VecSet<T>& W, int i, Scratch& hd, hipStream_t s) {
+    multi_dotc<T>(W.mloc, 1, W.col(i), W.ld, W.col(i), hd.as<T>(), s);
+    return std::sqrt(std::max(0.0, (double)std::real(allsum<T>(hd.as<T>(), 1, s)[0])));
+}
+
+template <typename T>
+void vscale(VecSet<T>& W, int i, T a, hipStream_t s) {
+    if (W.mloc) slate_hip::gescale<K<T>>('G', W.mloc, 1, kv(a), kp(W.col(i)), W.ld, s);
+}
+
+template <typename T>
+double vmax(VecSet<T>& W, int i) {
+    return norm<T>(Norm::Max, W.mat(i));
+}
+
+// complex Givens rotation zeroing b in (a, b): c real, s complex
+template <typename T>
+void givens(T a, T b, double& c, T& sn, T& r) {
+    const double aa = std::abs(a), bb = std::abs(b);
+    if (bb == 0) { c = 1; sn = T(0); r = a; return; }
+    if (aa == 0) { c = 0; sn = T(1); r = b; return; }
+    const double nrm = std::hypot(aa, bb);
+    const T alpha = a / aa;
+    c = aa / nrm;
+    sn = alpha * conj_of(b) / nrm;
+    r = alpha * nrm;
+}
+
+// restarted right-preconditioned GMRES on A M^-1 u = r for every column of
+// X (A X = B), started from the low-precision solution already in X
+template <typename T, typename Apply, typename Precond>
+int gmres_ir(const Storage& SB, Matrix<T>& X, Apply&& apply_a, Precond&& precond, double anorm, const Options& opts,
+             bool& converged_all) {
+    hipStream_t s = rt().main;
+    const i64 n = SB.m;
+    const int itermax = std::max(1, opts.max_iterations);
+    const int restart = std::max(1, std::min(opts.restart, itermax));
+    const double eps = std::numeric_limits<real_t<T>>::epsilon();
+    const double cte = anorm * eps * std::sqrt((double)n);
+    Matrix<T> Bcol(n, 1, SB.nb, SB.p, SB.q);
+    VecSet<T> V(*Bcol.storage(), restart + 1, s), Z(*Bcol.storage(), restart, s), Wv(*Bcol.storage(), 2, s);
+    Scratch hd(sizeof(T) * (restart + 2), s);
+    int total = 0;
+    converged_all = true;
+    Storage& SX = *X.storage();
+    for (i64 col = 0; col < SB.n; ++col) {
+        // Wv[1] = b, V[0] (scratch) = x
+        get_col<T>(SB, col, Wv.col(1), s);
+        Matrix<T> xcol(n, 1, SB.nb, SB.p, SB.q);
+        get_col<T>(SX, col, xcol.data(), s);
+        bool conv = false;
+        int steps = 0;
+        while (steps < itermax) {
+            // r = b - A x
+            copy2d(Wv.col(0), Wv.ld, Wv.col(1), Wv.ld, Wv.mloc, 1, s);
+            Matrix<T> r = Wv.mat(0);
+            apply_a(T(-1), xcol, T(1), r);
+            if (vmax<T>(Wv, 0) <= norm<T>(Norm::Max, xcol) * cte) { conv = true; break; }
+            const double beta = vnorm2<T>(Wv, 0, hd, s);
+            if (beta == 0) { conv = true; break; }
+            copy2d(V.col(0), V.ld, Wv.col(0), Wv.ld, V.mloc, 1, s);
+            vscale<T>(V, 0, T(1.0 / beta), s);
+            std::vector<T> H((size_t)(restart + 1) * restart, T(0)), g((size_t)restart + 1, T(0)), sn((size_t)restart);
+            std::vector<double> cs((size_t)restart);
+            g[0] = T(beta);
+            int k = 0;
+            for (int j = 0; j < restart && steps < itermax; ++j) {
+                Matrix<T> vj = V.mat(j), zj = Z.mat(j), w = Wv.mat(0);
+                precond(vj, zj);                                   // z_j = M^-1 v_j
+                apply_a(T(1), zj, T(0), w);                        // w = A z_j
+                std::vector<T> hs((size_t)j + 1, T(0));
+                for (int pass = 0; pass < 2; ++pass) {             // CGS2
+                    multi_dotc<T>(V.mloc, j + 1, V.col(0), V.ld, Wv.col(0), hd.as<T>(), s);
+                    const std::vector<T> h = allsum<T>(hd.as<T>(), j + 1, s);
+                    multi_axpy<T>(V.mloc, j + 1, T(-1), V.col(0), V.ld, hd.as<T>(), Wv.col(0), s);
+                    for (int i = 0; i <= j; ++i) hs[i] += h[i];
+                }
+                const double hn = vnorm2<T>(Wv, 0, hd, s);
+                auto Hat = [&](int r, int c) -> T& { return H[(size_t)r + (size_t)c * (restart + 1)]; };
+                for (int i = 0; i <= j; ++i) Hat(i, j) = hs[i];
+                Hat(j + 1, j) = T(hn);
+                for (int i = 0; i < j; ++i) {                      // previous rotations
+                    const T a = Hat(i, j), b = Hat(i + 1, j);
+                    Hat(i, j) = cs[i] * a + sn[i] * b;
+                    Hat(i + 1, j) = -conj_of(sn[i]) * a + cs[i] * b;
+                }
+                T r;
+                givens<T>(Hat(j, j), Hat(j + 1, j), cs[j], sn[j], r);
+                Hat(j, j) = r;
+                Hat(j + 1, j) = T(0);
+                g[j + 1] = -conj_of(sn[j]) * g[j];
+                g[j] = cs[j] * g[j];
+                k = j + 1;
+                ++steps;
+                ++total;
+                if (hn == 0 || std::abs(g[j + 1]) <= 1e-14 * beta) break;
+                copy2d(V.col(j + 1), V.ld, Wv.col(0), Wv.ld, V.mloc, 1, s);
+                vscale<T>(V, j + 1, T(1.0 / hn), s);
+            }
+            // y = R^-1 g (host back substitution), x += Z y
+            std::vector<T> y((size_t)k, T(0));
+            for (int i = k - 1; i >= 0; --i) {
+                T acc = g[i];
+                for (int c = i + 1; c < k; ++c) acc -= H[(size_t)i + (size_t)c * (restart + 1)] * y[c];
+                y[i] = acc / H[(size_t)i + (size_t)i * (restart + 1)];
+            }
+            upload(hd.p, y.data(), sizeof(T) * k, s);
+            multi_axpy<T>(Z.mloc, k, T(1), Z.col(0), Z.ld, hd.as<T>(), xcol.data(), s);
+            NHIP(hipStreamSynchronize(s));
+        }
+        if (!conv) {
+            // the final check after the last correction
+            copy2d(Wv.col(0), Wv.ld, Wv.col(1), Wv.ld, Wv.mloc, 1, s);
+            Matrix<T> r = Wv.mat(0);
+            apply_a(T(-1), xcol, T(1), r);
+            conv = vmax<T>(Wv, 0) <= norm<T>(Norm::Max, xcol) * cte;
+        }
+        converged_all = converged_all && conv;
+        put_col<T>(xcol.data(), SX, col, s);
+    }
+    return total;
+}
+
+// ------------------------------------------------------------ butterflies
+// diagonals of W = W_depth ... W_1 of order N: exp(r / 10), r uniform in
+// [-1/2, 1/2) (Baboulin et al.), identical on every rank (seeded)
+std::vector<double> butterfly_diag(i64 N, int depth, uint64_t seed) {
+    std::mt19937_64 g(seed);
+    std::uniform_real_distribution<double> u(-0.5, 0.5);
+    std::vector<double> d((size_t)N * depth);
+    for (auto& x : d) x = std::exp(u(g) / 10.0);
+    return d;
+}
+
+i64 rbt_size(i64 n, int depth, i64 nb, int p, int q) {
+    const i64 l = (i64)p / std::gcd(p, q) * q;
+    const i64 unit = ((i64)1 << depth) * nb * l;
+    return std::max(unit, (n + unit - 1) / unit * unit);
+}
+
+// M := op(W) M (rows) or M op(W)^T (columns), op(W) = W^T when trans, on
+// the local block: the diagonal entries of this rank's global indices
+template <typename T>
+void apply_w(const std::vector<double>& diag, int depth, Storage& S, bool trans, bool rows, hipStream_t s) {
+    using R = real_t<T>;
+    const i64 nidx = rows ? S.mloc : S.nloc, nother = rows ? S.nloc : S.mloc;
+    if (!nidx || !nother) return;
+    const i64 Nglob = rows ? S.m : S.n;
+    std::vector<R> loc((size_t)nidx * depth);
+    for (i64 i = 0; i < nidx; ++i) {
+        const i64 gi = rows ? l2g(i, S.nb, S.p, S.pr) : l2g(i, S.nb, S.q, S.pc);
+        for (int l = 0; l < depth; ++l) loc[(size_t)l * nidx + i] = (R)diag[(size_t)l * Nglob + gi];
+    }
+    Scratch dd(sizeof(R) * loc.size(), s);
+    upload(dd.p, loc.data(), sizeof(R) * loc.size(), s);
+    slate_hip::butterfly<K<T>, R>(trans, rows, depth, nidx, nother, kp(static_cast<T*>(S.buf)), S.lld, dd.as<R>(), nidx,
+                                  s);
+    NHIP(hipStreamSynchronize(s));
+}
+
+// N x k copy of M (n x k, same grid / nb): the global indices < n map to the
+// same process and local position, so it is one local block copy
+template <typename T>
+Matrix<T> padded(const Matrix<T>& M, i64 N, i64 k, bool identity) {
+    const Storage& S = *M.storage();
+    Matrix<T> P(N, k, S.nb, S.p, S.q);
+    if (identity) set<T>(T(0), T(1), P);
+    hipStream_t s = rt().main;
+    copy2d(P.data(), P.lld(), static_cast<const T*>(S.buf), S.lld, S.mloc, S.nloc, s);
+    NHIP(hipStreamSynchronize(s));
+    return P;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------ hegst / hegv
+template <typename T>
+void hegst(int64_t itype, HermitianMatrix<T>& A, const HermitianMatrix<T>& L, const Options& opts) {
+    if (itype < 1 || itype > 3) throw Error("native hegst: itype must be 1, 2 or 3");
+    const Storage& SA = *A.storage();
+    const Storage& SL = *L.storage();
+    if (SA.n != SL.n || SA.nb != SL.nb || SA.p != SL.p || SA.q != SL.q)
+        throw Error("native hegst: A and B must be n x n on one grid / tile size");
+    // the full Hermitian A, transformed in place, written back over A
+    Matrix<T> F = expand_tri<T>(A, A.uplo(), 1);
+    const bool lower = L.uplo() == Uplo::Lower;
+    const Uplo u = L.uplo();
+    // with B = L L^H (Lower) or U^H U (Upper, L := U^H): ops on "L" / "L^H"
+    const Op opL = lower ? Op::NoTrans : Op::ConjTrans, opLH = lower ? Op::ConjTrans : Op::NoTrans;
+    if (itype == 1) {
+        trsm<T>(Side::Left, u, opL, Diag::NonUnit, T(1), L, F, opts);     // L^-1 A
+        trsm<T>(Side::Right, u, opLH, Diag::NonUnit, T(1), L, F, opts);   // (L^-1 A) L^-H
+    } else {
+        trmm<T>(Side::Left, u, opLH, Diag::NonUnit, T(1), L, F, opts);    // L^H A
+        trmm<T>(Side::Right, u, opL, Diag::NonUnit, T(1), L, F, opts);    // (L^H A) L
+    }
+    copy<T>(Op::NoTrans, F, A);
+}
+
+template <typename T>
+static int64_t hegv_impl(int64_t itype, HermitianMatrix<T>& A, HermitianMatrix<T>& B, std::vector<real_t<T>>& Lambda,
+                         Matrix<T>* Z, const Options& opts) {
+    // the Cholesky driver factors Lower storage: an Upper B (= U^H U) is
+    // factored as its conjugate transpose, L = U^H, and U written back
+    const bool upper = B.uplo() == Uplo::Upper;
+    HermitianMatrix<T> L = B;
+    if (upper) {
+        Matrix<T> Bt(B.n(), B.n(), B.nb(), B.p(), B.q());
+        copy<T>(Op::ConjTrans, B, Bt);
+        L = HermitianMatrix<T>(Uplo::Lower, Bt);
+    }
+    const int64_t info = potrf<T>(L, opts);
+    if (info) return A.n() + info;
+    if (upper) copy<T>(Op::ConjTrans, L, B);
+    hegst<T>(itype, A, L, opts);
+    const int64_t ie = Z ? heev<T>(A, Lambda, *Z, opts) : heev<T>(A, Lambda, opts);
+    if (ie || !Z) return ie;
+    if (itype == 3) trmm<T>(Side::Left, Uplo::Lower, Op::NoTrans, Diag::NonUnit, T(1), L, *Z, opts);   // x = L y
+    else trsm<T>(Side::Left, Uplo::Lower, Op::ConjTrans, Diag::NonUnit, T(1), L, *Z, opts);            // x = L^-H y
+    return 0;
+}
+
+template <typename T>
+int64_t hegv(int64_t itype, HermitianMatrix<T>& A, HermitianMatrix<T>& B, std::vector<real_t<T>>& Lambda,
+             Matrix<T>& Z, const Options& opts) {
+    return hegv_impl<T>(itype, A, B, Lambda, &Z, opts);
+}
+template <typename T>
+int64_t hegv(int64_t itype, HermitianMatrix<T>& A, HermitianMatrix<T>& B, std::vector<real_t<T>>& Lambda,
+             const Options& opts) {
+    return hegv_impl<T>(itype, A, B, Lambda, nullptr, opts);
+}
+
+// ------------------------------------------------------------ GMRES-IR
+template <typename T>
+int64_t gesv_mixed_gmres(Matrix<T>& A, std::vector<int64_t>& ipiv, Matrix<T>& B, Matrix<T>& X, int& iter,
+                         const Options& opts) {
+    using Lo = typename lower_of<T>::type;
+    const Storage& SA = *A.storage();
+    hipStream_t s = rt().main;
+    Matrix<Lo> Al(SA.m, SA.n, SA.nb, SA.p, SA.q);
+    convert_local<T, Lo>(SA, *Al.storage(), s);
+    NHIP(hipStreamSynchronize(s));
+    iter = 0;
+    if (getrf<Lo>(Al, ipiv, opts) == 0) {
+        const Storage& SB = *B.storage();
+        // x0 = (LU)^-1 b in the low precision
+        Matrix<Lo> Xl(SB.m, SB.n, SB.nb, SB.p, SB.q);
+        convert_local<T, Lo>(SB, *Xl.storage(), s);
+        NHIP(hipStreamSynchronize(s));
+        getrs<Lo>(Al, ipiv, Xl, opts);
+        convert_local<Lo, T>(*Xl.storage(), *X.storage(), s);
+        NHIP(hipStreamSynchronize(s));
+        auto apply = [&](T alpha, const Matrix<T>& x, T beta, Matrix<T>& y) { gemm<T>(alpha, A, x, beta, y, opts); };
+        auto precond = [&](const Matrix<T>& v, Matrix<T>& z) {
+            const Storage& SV = *v.storage();
+            Matrix<Lo> t(SV.m, 1, SV.nb, SV.p, SV.q);
+            convert_local<T, Lo>(SV, *t.storage(), s);
+            NHIP(hipStreamSynchronize(s));
+            getrs<Lo>(Al, ipiv, t, opts);
+            convert_local<Lo, T>(*t.storage(), *z.storage(), s);
+            NHIP(hipStreamSynchronize(s));
+        };
+        bool ok = false;
+        const int it = gmres_ir<T>(SB, X, apply, precond, norm<T>(Norm::Max, A), opts, ok);
+        if (ok) { iter = it; return 0; }
+        iter = -31;
+    } else {
+        iter = -3;
+    }
+    copy<T>(Op::NoTrans, B, X);
+    return gesv<T>(A, ipiv, X, opts);
+}
+
+template <typename T>
+int64_t posv_mixed_gmres(HermitianMatrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, const Options& opts) {
+    using Lo = typename lower_of<T>::type;
+    const Storage& SA = *A.storage();
+    hipStream_t s = rt().main;
+    HermitianMatrix<Lo> Al(A.uplo(), SA.n, SA.nb, SA.p, SA.q);
+    convert_local<T, Lo>(SA, *Al.storage(), s);
+    NHIP(hipStreamSynchronize(s));
+    iter = 0;
+    if (potrf<Lo>(Al, opts) == 0) {
+        const Storage& SB = *B.storage();
+        Matrix<Lo> Xl(SB.m, SB.n, SB.nb, SB.p, SB.q);
+        convert_local<T, Lo>(SB, *Xl.storage(), s);
+        NHIP(hipStreamSynchronize(s));
+        potrs<Lo>(Al, Xl, opts);
+        convert_local<Lo, T>(*Xl.storage(), *X.storage(), s);
+        NHIP(hipStreamSynchronize(s));
+        const Matrix<T> Af = expand_tri<T>(A, A.uplo(), 1);
+        auto apply = [&](T alpha, const Matrix<T>& x, T beta, Matrix<T>& y) { gemm<T>(alpha, Af, x, beta, y, opts); };
+        auto precond = [&](const Matrix<T>& v, Matrix<T>& z) {
+            const Storage& SV = *v.storage();
+            Matrix<Lo> t(SV.m, 1, SV.nb, SV.p, SV.q);
+            convert_local<T, Lo>(SV, *t.storage(), s);
+            NHIP(hipStreamSynchronize(s));
+            potrs<Lo>(Al, t, opts);
+            convert_local<Lo, T>(*t.storage(), *z.storage(), s);
+            NHIP(hipStreamSynchronize(s));
+        };
+        bool ok = false;
+        const int it = gmres_ir<T>(SB, X, apply, precond, norm<T>(Norm::Max, Af), opts, ok);
+        if (ok) { iter = it; return 0; }
+        iter = -31;
+    } else {
+        iter = -3;
+    }
+    copy<T>(Op::NoTrans, B, X);
+    return posv<T>(A, X, opts);
+}
+
+// ------------------------------------------------------------ RBT
+template <typename T>
+int64_t getrs_nopiv(const Matrix<T>& A, Matrix<T>& B, const Options& opts) {
+    trsm<T>(Side::Left, Uplo::Lower, Op::NoTrans, Diag::Unit, T(1), A, B, opts);
+    trsm<T>(Side::Left, Uplo::Upper, Op::NoTrans, Diag::NonUnit, T(1), A, B, opts);
+    return 0;
+}
+
+template <typename T>
+int64_t gesv_rbt(Matrix<T>& A, Matrix<T>& B, const Options& opts) {
+    const Storage& SA = *A.storage();
+    const Storage& SB = *B.storage();
+    if (SA.m != SA.n || SB.m != SA.n) throw Error("native gesv_rbt: A n x n, B n x nrhs");
+    if (SB.nb != SA.nb || SB.p != SA.p || SB.q != SA.q) throw Error("native gesv_rbt: A and B share grid and nb");
+    hipStream_t s = rt().main;
+    const int depth = std::max(1, std::min(4, opts.depth));
+    const i64 n = SA.n, N = rbt_size(n, depth, SA.nb, SA.p, SA.q);
+    Matrix<T> A0(n, n, SA.nb, SA.p, SA.q);
+    copy<T>(Op::NoTrans, A, A0);
+    Matrix<T> Ap = N == n ? A : padded<T>(A, N, N, true);
+    const std::vector<double> U = butterfly_diag(N, depth, 7), V = butterfly_diag(N, depth, 8);
+    apply_w<T>(U, depth, *Ap.storage(), true, true, s);      // U^T A
+    apply_w<T>(V, depth, *Ap.storage(), true, false, s);     // (U^T A) V
+    Options o = opts;
+    const int64_t info = getrf_nopiv<T>(Ap, o);
+    if (info) return info;
+    // x = V (LU)^-1 U^T r on the padded order
+    auto solve = [&](const Matrix<T>& R, Matrix<T>& D) {
+        Matrix<T> Y = padded<T>(R, N, R.n(), false);
+        apply_w<T>(U, depth, *Y.storage(), true, true, s);
+        getrs_nopiv<T>(Ap, Y, o);
+        apply_w<T>(V, depth, *Y.storage(), false, true, s);
+        Storage& SD = *D.storage();
+        copy2d(static_cast<T*>(SD.buf), SD.lld, Y.data(), Y.lld(), SD.mloc, SD.nloc, s);
+        NHIP(hipStreamSynchronize(s));
+    };
+    Matrix<T> X(n, SB.n, SB.nb, SB.p, SB.q), R(n, SB.n, SB.nb, SB.p, SB.q), D(n, SB.n, SB.nb, SB.p, SB.q);
+    solve(B, X);
+    const double eps = std::numeric_limits<real_t<T>>::epsilon();
+    const double cte = norm<T>(Norm::Max, A0) * eps * std::sqrt((double)n);
+    const int itermax = std::min(opts.max_iterations, 10);
+    for (int it = 0; it <= itermax; ++it) {
+        copy<T>(Op::NoTrans, B, R);
+        gemm<T>(T(-1), A0, X, T(1), R, opts);                 // R = B - A X
+        if (norm<T>(Norm::Max, R) <= norm<T>(Norm::Max, X) * cte || it == itermax) break;
+        solve(R, D);
+        add<T>(T(1), D, T(1), X);
+    }
+    copy<T>(Op::NoTrans, X, B);
+    return 0;
+}
+
+// ------------------------------------------------------------ hesv / scale
+template <typename T>
+int64_t hesv(HermitianMatrix<T>& A, Matrix<T>& B, const Options& opts) {
+    Matrix<T> F = expand_tri<T>(A, A.uplo(), 1);
+    std::vector<int64_t> ipiv;
+    const int64_t info = gesv<T>(F, ipiv, B, opts);
+    copy<T>(Op::NoTrans, F, A);
+    return info;
+}
+
+template <typename T>
+void scale(real_t<T> numer, real_t<T> denom, Matrix<T>& A) {
+    using R = real_t<T>;
+    if (denom == R(0)) throw Error("native scale: denom == 0");
+    const Storage& S = *A.storage();
+    hipStream_t s = rt().main;
+    // numer / denom in up to two factors so that neither overflows
+    R f1 = numer / denom, f2 = R(1);
+    if (!std::isfinite((double)f1) && std::isfinite((double)numer)) {
+        f1 = numer / R(2);
+        f2 = R(2) / denom;
+    }
+    if (S.mloc && S.nloc) {
+        slate_hip::gescale<K<T>>('G', S.mloc, S.nloc, kv(T(f1)), kp(static_cast<T*>(S.buf)), S.lld, s);
+        if (f2 != R(1)) slate_hip::gescale<K<T>>('G', S.mloc, S.nloc, kv(T(f2)), kp(static_cast<T*>(S.buf)), S.lld, s);
+    }
+    NHIP(hipStreamSynchronize(s));
+}
+
+// ------------------------------------------------------------ instantiation
+#define SLATE_NATIVE_EXT(T)                                                                                    \
+    template void hegst<T>(int64_t, HermitianMatrix<T>&, const HermitianMatrix<T>&, const Options&);            \
+    template int64_t hegv<T>(int64_t, HermitianMatrix<T>&, HermitianMatrix<T>&, std::vector<real_t<T>>&,        \
+                             Matrix<T>&, const Options&);                                                       \
+    template int64_t hegv<T>(int64_t, HermitianMatrix<T>&, HermitianMatrix<T>&, std::vector<real_t<T>>&,        \
+                             const Options&);                                                                   \
+    template int64_t gesv_rbt<T>(Matrix<T>&, Matrix<T>&, const Options&);                                      \
+    template int64_t getrs_nopiv<T>(const Matrix<T>&, Matrix<T>&, const Options&);                             \
+    template int64_t hesv<T>(HermitianMatrix<T>&, Matrix<T>&, const Options&);                                 \
+    template void scale<T>(real_t<T>, real_t<T>, Matrix<T>&);
+SLATE_NATIVE_EXT(float)
+SLATE_NATIVE_EXT(double)
+SLATE_NATIVE_EXT(std::complex<float>)
+SLATE_NATIVE_EXT(std::complex<double>)
+#undef SLATE_NATIVE_EXT
+#define SLATE_NATIVE_GMRES(T)                                                                                  \
+    template int64_t gesv_mixed_gmres<T>(Matrix<T>&, std::vector<int64_t>&, Matrix<T>&, Matrix<T>&, int&,      \
+                                         const Options&);                                                       \
+    template int64_t posv_mixed_gmres<T>(HermitianMatrix<T>&, Matrix<T>&, Matrix<T>&, int&, const Options&);
+SLATE_NATIVE_GMRES(double)
+SLATE_NATIVE_GMRES(std::complex<double>)
+#undef SLATE_NATIVE_GMRES
+
+}  // namespace native
+}  // namespace slate_amd

@@ -253,6 +253,10 @@ inline void copy2d(T* dst, i64 ldd, const T* src, i64 lds, i64 m, i64 n, hipStre
     if (m > 0 && n > 0) slate_hip::gecopy<K<T>, K<T>>('G', 'N', m, n, kp(src), lds, kp(dst), ldd, s);
 }
 
+// full matrix of a stored triangle (native.hip): kind 0 = triangular (the
+// other part zero, a Unit diagonal set to one), 1 = Hermitian, 2 = symmetric
+template <typename T>
+Matrix<T> expand_tri(const Matrix<T>& A, Uplo uplo, int kind, Diag diag = Diag::NonUnit);
 
 }  // namespace native
 }  // namespace slate_amd

@@ -129,11 +129,11 @@ def _assert_checks(checks, out):
                                                    "gecondest", "svd", "svd_orth", "svd_wide", "svd_wide_orth", "geqrf", "geqrf_wide", "gels_grid",
                                                    "trsm_lt", "trsm_rn", "trsm_rc", "trtri", "trtrm", "gesv_nopiv",
                                                    "cholqr", "cholqr_orth", "gelqf", "sub_potrf", "from_device_potrs", "lu_xchg_bound",
-                                                   "svd_values")]
+                                                   "svd_values", "gesv_rbt", "hegv1", "hegv2_upper", "hegv3")]
     for name in names:
         assert name in checks, (name, out)
         assert float(checks[name]) < TOL[name[-1]], (name, checks[name])
-    for name in [f"{w}_{x}" for x in "dz" for w in ("posv_mixed", "gesv_mixed")]:
+    for name in [f"{w}_{x}" for x in "dz" for w in ("posv_mixed", "gesv_mixed", "posv_gmres", "gesv_gmres")]:
         assert name in checks, (name, out)
         assert float(checks[name]) < TOL[name[-1]], (name, checks[name])
     for name in ("capi_dgesv", "capi_zposv", "capi_dgemm_tn"):
@@ -190,6 +190,33 @@ def test_native_lapack_more_from_c(nranks):
         print(out)
         assert rc == 0 and "all checks passed" in out, out
         assert len(_checks(out)) >= 20, out
+
+
+HEXE = os.path.join(ROOT, "slate_amd", "ex_native_handles")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("grid", ["1x1", "2x2"])
+def test_native_handle_capi_from_c(grid):
+    """The opaque-handle C API (slate_amd_matrix_create, _posv, _gesv,
+    _gemm on transposed views, _unmqr left / right, _heev, _hegv, mixed /
+    GMRES / RBT solvers, ...) served by libslate_amd_native.so: no Python in
+    the process (the CPython-embedding libslate_amd_c.so is deprecated)."""
+    assert os.path.exists(HEXE), "slate_amd/ex_native_handles not built"
+    ldd = subprocess.run(["ldd", HEXE], capture_output=True, text=True, env=_clean_env()).stdout
+    assert "python" not in ldd.lower() and "libslate_amd_c" not in ldd, ldd
+    p, q = map(int, grid.split("x"))
+    if p * q == 1:
+        r = subprocess.run([HEXE, grid], capture_output=True, text=True, env=_clean_env(), timeout=240)
+        outs = [(r.returncode, r.stdout + r.stderr)]
+    else:
+        outs = _run_ranks(HEXE, [grid], p * q)
+    for rc, out in outs:
+        print(out)
+        assert rc == 0, out
+    out0 = outs[0][1]
+    assert "all checks passed" in out0, out0
+    assert len(_checks(out0)) >= 25, out0
 
 
 @pytest.mark.gpu
