@@ -850,6 +850,26 @@ int main(int argc, char** argv) {
         sn::initialize();
         const int me = sn::rank();
         if (me == 0) std::printf("transport %s ranks %d grid %dx%d\n", sn::transport(), sn::size(), p, q);
+        if (const char* tp = std::getenv("EX_NATIVE_TRACE")) {
+            // traced dpotrf + dgetrf (lookahead 1): a Chrome trace of every
+            // rank's panel / bcast / lookahead / update spans, and the timers
+            const int64_t n = 2048, nb = 128;
+            sn::HermitianMatrix<double> A(sn::Uplo::Lower, n, nb, p, q);
+            A.generate(sn::Gen::HermitianPositiveDefinite, 3);
+            sn::Matrix<double> G(n, n, nb, p, q);
+            G.generate(sn::Gen::Random, 4);
+            sn::clear_timers();
+            sn::trace::on();
+            const int64_t i1 = sn::potrf(A);
+            std::vector<int64_t> piv;
+            const int64_t i2 = sn::getrf(G, piv);
+            sn::trace::finish(tp);
+            for (const auto& kv : sn::timers())
+                if (me == 0) std::printf("timer %s %.6f\n", kv.first.c_str(), kv.second);
+            if (me == 0) std::printf("traced potrf info %lld getrf info %lld -> %s\n", (long long)i1, (long long)i2, tp);
+            sn::finalize();
+            return (i1 || i2) ? 1 : 0;
+        }
         if (types.find('s') != std::string::npos) run<float>(p, q, me);
         if (types.find('d') != std::string::npos) run<double>(p, q, me);
         if (types.find('c') != std::string::npos) run<std::complex<float>>(p, q, me);

@@ -33,6 +33,7 @@
 
 #include <complex>
 #include <cstdint>
+#include <map>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -64,6 +65,23 @@ const char* version();
 const char* transport();      // "none" (one rank), "rccl" or "host"
 void barrier();               // all ranks, device work of this rank completed
 double allreduce_max(double v);   // maximum over all ranks
+
+// tracing (SLATE Trace, src/auxiliary/Trace.cc): host spans and per-stream
+// device spans of the drivers' phases (potrf::panel / bcast / lookahead /
+// update, getrf::panel / update, gemm::summa, ...); finish() gathers every
+// rank's events to rank 0, which writes one Chrome trace-event JSON (pid =
+// rank, tid = stream).  SLATE_AMD_NATIVE_TRACE=<path> traces from
+// initialize() to finalize().
+namespace trace {
+void on();
+void off();
+bool enabled();
+void finish(const std::string& path);     // collective
+}  // namespace trace
+// seconds per traced scope name (slate::timers): host wall time of every
+// scope, and "<name>@device" device time of the spans resolved so far
+std::map<std::string, double> timers();
+void clear_timers();
 
 struct Options {
     int lookahead = 1;        // SLATE Option::Lookahead

@@ -53,7 +53,16 @@ static int env_int(const char* k, int def) {
     return v && *v ? std::atoi(v) : def;
 }
 
+static void initialize_rt();
+
 void initialize() {
+    if (rt().up) return;
+    initialize_rt();
+    static std::once_flag traced;
+    std::call_once(traced, [] { trace_rt::auto_start(); });
+}
+
+static void initialize_rt() {
     Runtime& R = rt();
     std::lock_guard<std::mutex> g(R.mu);
     if (R.up) return;
@@ -83,6 +92,7 @@ void initialize() {
 }
 
 void finalize() {
+    if (rt().up) trace_rt::auto_finish();
     Runtime& R = rt();
     std::lock_guard<std::mutex> g(R.mu);
     if (!R.up) return;
@@ -516,11 +526,11 @@ void assemble_cols(const ColPlan& P, const i64* idx, const T* Prow, i64 ldp, i64
                                          idx + P.order_off, s);
 }
 
-// diagnostics (SLATE_AMD_NATIVE_TRACE=1): synchronise s and print the sum
+// diagnostics (SLATE_AMD_NATIVE_DEBUG_SUMS=1): synchronise s and print the sum
 // of |x| over an m x n block
 template <typename T>
 void dbg_sum(const char* tag, i64 t, const T* A, i64 ld, i64 m, i64 n, hipStream_t s) {
-    static const bool on = env_int("SLATE_AMD_NATIVE_TRACE", 0) != 0;
+    static const bool on = env_int("SLATE_AMD_NATIVE_DEBUG_SUMS", 0) != 0;
     if (!on) return;
     NHIP(hipStreamSynchronize(s));
     double acc = 0;
@@ -586,6 +596,8 @@ static void potrf_1x1(T* A, i64 lda, i64 n, i64 nb, int la, i64* infos) {
         const i64 c0 = gstart(gi), c2 = gstart(gi + 1);
         const i64 tfirst = gi * G, tlast = std::min(nt, tfirst + G);
         if (gi - la - 1 >= 0) ev_tr[gi - la - 1]->wait(ps);
+        {
+        NTRACE("potrf::panel", ps);
         for (i64 u = tfirst; u < tlast; ++u) {
             const i64 cu = off(u), cu1 = off(u + 1);
             if (cu > c0) {
@@ -597,6 +609,7 @@ static void potrf_1x1(T* A, i64 lda, i64 n, i64 nb, int la, i64* infos) {
             potrf_tile_k<T>(cu1 - cu, A + cu + cu * lda, lda, infos + u, ps);
             if (n > cu1) trsm_rlc<T>(n - cu1, cu1 - cu, A + cu + cu * lda, lda, A + cu1 + cu * lda, lda, ps);
         }
+        }
         // P = A[c0:n, c0:c2]; update columns [lo, hi) (rows >= lo) on stream s
         auto update = [&](i64 lo, i64 hi, hipStream_t s) {
             if (hi <= lo) return;
@@ -606,10 +619,14 @@ static void potrf_1x1(T* A, i64 lda, i64 n, i64 nb, int la, i64* infos) {
         };
         const i64 la_end = gstart(gi + 1 + la);
         if (gi >= 1 && la > 0) ev_tr[gi - 1]->wait(ps);
-        update(c2, la_end, ps);
+        {
+            NTRACE("potrf::lookahead", ps);
+            update(c2, la_end, ps);
+        }
         Event ev_panel;
         ev_panel.record(ps);
         ev_panel.wait(us);
+        NTRACE("potrf::update", us);
         const i64 nx_end = std::max(gstart(gi + 2 + la), la_end);
         update(la_end, nx_end, us);
         ev_tr[gi] = std::make_unique<Event>();
@@ -678,6 +695,7 @@ static void potrf_grid(Storage& S, int la, i64* infos) {
         const i64 lc1 = std::min(tiles_before(g + 1, q, pc) * nb, lc_end);
         const bool own_col = (g % q) == pc, own_diag = own_col && (g % p) == pr;
         if (t - la - 1 >= 0) ev_tr[t - la - 1]->wait(ps);
+        std::unique_ptr<trace_rt::Scope> sp_panel(trace_rt::g_on ? new trace_rt::Scope("potrf::panel", ps) : nullptr);
         if (own_diag) dbg_sum("diag_in", t, buf + lrg + lcg * lld, lld, kb, kb, ps);
         if (own_diag) potrf_tile_k<T>(kb, buf + lrg + lcg * lld, lld, infos + t, ps);
         if (own_diag) dbg_sum("diag_out", t, buf + lrg + lcg * lld, lld, kb, kb, ps);
@@ -696,10 +714,11 @@ static void potrf_grid(Storage& S, int la, i64* infos) {
             dbg_sum("panel_in", t, buf + lr1 + lcg * lld, lld, nrow, kb, ps);
             if (nrow) trsm_rlc<T>(nrow, kb, D, ldd, buf + lr1 + lcg * lld, lld, ps);
             dbg_sum("panel_out", t, buf + lr1 + lcg * lld, lld, nrow, kb, ps);
-            if (env_int("SLATE_AMD_NATIVE_TRACE", 0) && nrow)
+            if (env_int("SLATE_AMD_NATIVE_DEBUG_SUMS", 0) && nrow)
                 dbg_sum("Winv", t, static_cast<double*>(slate_hip::workspace(ps, sizeof(double) * 1024, slate_hip::WS_C)),
                         1024, 1024, 1, ps);
         }
+        sp_panel.reset();
         // panel -> row (Prow: nrow x kb, contiguous), tile-granular chunks
         Scratch* Prow = ring_p[t % NR].get();
         const T* P = buf + lr1 + lcg * lld;
@@ -719,6 +738,7 @@ static void potrf_grid(Storage& S, int la, i64* infos) {
             Event src;
             src.record(ps);                          // trsm done
             src.wait(cs);
+            NTRACE("potrf::bcast", cs);
             for (size_t ci = 0; ci < chunks.size(); ++ci) {
                 const i64 a = chunks[ci].first, b = chunks[ci].second;
                 auto cb = std::make_unique<Scratch>((size_t)(b - a) * kb * sizeof(T), cs);
@@ -731,6 +751,7 @@ static void potrf_grid(Storage& S, int la, i64* infos) {
         }
         auto land = [&](size_t ci) { if (q > 1) landed[ci]->wait(ps); };
         if (!chunks.empty()) land(0);
+        std::unique_ptr<trace_rt::Scope> sp_la(trace_rt::g_on ? new trace_rt::Scope("potrf::lookahead", ps) : nullptr);
         // transposed operands: lookahead tiles (in chunk 0), then the rest
         const ColPlan& A1 = plans[t].first;
         const ColPlan& A2 = plans[t].second;
@@ -759,6 +780,7 @@ static void potrf_grid(Storage& S, int la, i64* infos) {
                           buf + lr1 + a + lc1 * lld, lld, ps, &mk);
             }
         }
+        sp_la.reset();
         dbg_sum("la_out", t, buf + lr1 + lc1 * lld, lld, nrow, lc_la - lc1, ps);
         const T* Lc;
         i64 ldlc, loff;
@@ -790,6 +812,7 @@ static void potrf_grid(Storage& S, int la, i64* infos) {
             ev_panel.wait(us);
         }
         const i64 lc_nx = std::max(std::min(tiles_before(g + 2 + la, q, pc) * nb, lc_end), lc_la);
+        NTRACE("potrf::update", us);
         for (int part = 0; part < 2; ++part) {
             const i64 c0 = part == 0 ? lc_la : lc_nx, c1 = part == 0 ? lc_nx : lc_end;
             if (c1 > c0 && nrow) {
@@ -816,6 +839,7 @@ static void potrf_grid(Storage& S, int la, i64* infos) {
 template <typename T>
 int64_t potrf(HermitianMatrix<T>& A, const Options& opts) {
     if (A.uplo() != Uplo::Lower) throw Error("native potrf: Lower storage only (use the conjugate transpose)");
+    NTRACE("potrf", nullptr);
     Storage& S = *A.storage();
     Runtime& R = rt();
     const i64 nt = (S.n + S.nb - 1) / S.nb;
@@ -961,6 +985,7 @@ static void trsm_left_t(char uplo, char diag, char tr, T alpha, const Storage& S
 
 template <typename T>
 void trsm(Side side, Uplo uplo, Op op, Diag diag, T alpha, const Matrix<T>& A, Matrix<T>& B, const Options& opts) {
+    NTRACE("trsm", nullptr);
     const Storage& SA = *A.storage();
     Storage& SB = *B.storage();
     const bool left = side == Side::Left;
@@ -1314,6 +1339,7 @@ void lu_exchange_stats(long long* bytes, long long* rows) {
 
 template <typename T>
 int64_t getrf(Matrix<T>& A, std::vector<int64_t>& ipiv_out, const Options& opts) {
+    NTRACE("getrf", nullptr);
     Storage& S = *A.storage();
     Runtime& R = rt();
     GridComms* gc = S.gc;
@@ -1364,6 +1390,7 @@ int64_t getrf(Matrix<T>& A, std::vector<int64_t>& ipiv_out, const Options& opts)
             T* Lb = q > 1 ? ring[k % NR]->as<T>() : nullptr;
             const T* Lp = nullptr;
             i64 ldl = mk;
+            std::unique_ptr<trace_rt::Scope> sp_panel(trace_rt::g_on ? new trace_rt::Scope("getrf::panel", ps) : nullptr);
             if (own) {
                 const i64 wk = std::min(nb, n - r0);
                 slate_hip::getrf_panel_ws<K<T>>(mk, wk, kp(buf + r0 + lck * lld), lld, ipiv_d + r0,
@@ -1378,12 +1405,17 @@ int64_t getrf(Matrix<T>& A, std::vector<int64_t>& ipiv_out, const Options& opts)
                 Lp = Lb;
                 ldl = mk;
             }
+            sp_panel.reset();
             if (k >= 1 && la > 0) ev_tr[k - 1]->wait(ps);
-            update_cols(Lp, ldl, r0, kb, lc1, lcla, ps);
+            {
+                NTRACE("getrf::lookahead", ps);
+                update_cols(Lp, ldl, r0, kb, lc1, lcla, ps);
+            }
             Event ev_panel;
             ev_panel.record(ps);
             ev_panel.wait(us);
             const i64 lcnx = std::max(std::min(tiles_before(k + 2 + la, q, pc) * nb, nloc), lcla);
+            NTRACE("getrf::update", us);
             update_cols(Lp, ldl, r0, kb, lcla, lcnx, us);
             ev_tr[k] = std::make_unique<Event>();
             ev_tr[k]->record(us);
@@ -1435,12 +1467,15 @@ int64_t getrf(Matrix<T>& A, std::vector<int64_t>& ipiv_out, const Options& opts)
             T* Lp = pack.as<T>();
             T* Tt = reinterpret_cast<T*>(static_cast<char*>(pack.p) + lbytes);
             i64* pv = reinterpret_cast<i64*>(static_cast<char*>(pack.p) + lbytes + tbytes);
+            std::unique_ptr<trace_rt::Scope> sp_panel(trace_rt::g_on ? new trace_rt::Scope("getrf::panel", ps) : nullptr);
             if (pc == ck) {
                 panel_dist<T>(S, k, kb, lck, ipiv_d, infos.as<i64>() + k, opts.pivot_threshold,
                               opts.inner_blocking, Tt, gall.as<i64>() + goff[k], ps);
                 copy2d(Lp, std::max<i64>(nmine, 1), buf + lr_k + lck * lld, lld, nmine, kb, ps);
                 dcopy(pv, ipiv_d + r0, (size_t)kb * sizeof(i64), ps);
             }
+            sp_panel.reset();
+            NTRACE("getrf::update", ps);
             if (q > 1) rowc->bcast(pack.p, lbytes + tbytes + (size_t)kb * sizeof(i64), ck, ps);
             dcopy(ipiv_d + r0, pv, (size_t)kb * sizeof(i64), ps);
             if (p2p) {
@@ -1572,6 +1607,7 @@ static void summa(T alpha, const Storage& SA, const Storage& SB, T beta, Storage
     hipStream_t s = R.panel, cs = R.comm;
     join(R.main, s);
     join(R.main, cs);
+    NTRACE("gemm::summa", s);
     const i64 nb = SA.nb, Kd = SA.n;
     const int p = SC.p, q = SC.q, pr = SC.pr, pc = SC.pc;
     GridComms* gc = SC.gc;
@@ -2530,6 +2566,7 @@ static int64_t geqrf_tsqr(Storage& S, QRFactors<T>& F, const Options& opts) {
 
 template <typename T>
 int64_t geqrf(Matrix<T>& A, QRFactors<T>& F, const Options& opts) {
+    NTRACE("geqrf", nullptr);
     Storage& S = *A.storage();
     if (S.p != 1) return geqrf_tsqr<T>(S, F, opts);
     Runtime& R = rt();

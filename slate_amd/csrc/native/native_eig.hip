@@ -412,7 +412,10 @@ void heev_1gpu(i64 n, T* Af, std::vector<double>& w, T* Z, bool wantz, hipStream
         A0 = std::make_unique<Scratch>((size_t)n * n * sizeof(T), s);
         copy2d(A0->as<T>(), n, Af, n, n, n, s);
     }
-    he2hb<T>(n, b, Af, n, panels, s);
+    {
+        NTRACE("heev::he2hb", s);
+        he2hb<T>(n, b, Af, n, panels, s);
+    }
     if (dbg) {
         B0 = std::make_unique<Scratch>((size_t)n * n * sizeof(T), s);
         copy2d(B0->as<T>(), n, Af, n, n, n, s);
@@ -467,6 +470,7 @@ void heev_1gpu(i64 n, T* Af, std::vector<double>& w, T* Z, bool wantz, hipStream
         const i64 nt0 = nt[0] ? nt[0] : 1, lag = 2;
         const int nwg = (int)std::min<i64>({std::max<i64>(nsw, 1), (i64)pr.multiProcessorCount,
                                             std::max<i64>(8, std::min(nt0 / lag + 8, nt0 / 3 + 15))});
+        NTRACE("heev::hb2st", s);
         slate_hip::hb2st_device<K<T>>(n, (int)b, kp(Bh.as<T>()), ldp, kp(V.as<T>()), kp(tau.as<T>()), row.as<i64>(),
                                       len.as<i64>(), spd->as<i64>(), ntd->as<i64>(), work.as<int>(), nsw, nwg, s);
     }
@@ -500,7 +504,10 @@ void heev_1gpu(i64 n, T* Af, std::vector<double>& w, T* Z, bool wantz, hipStream
     }
     // ---- tridiagonal eigenvectors (D & C), then Z = Q1 Q2 Phase Qt
     Scratch Qt((size_t)n * n * sizeof(double), s);
-    stedc_device(n, d, e, w, Qt.as<double>(), n, s);
+    {
+        NTRACE("heev::stedc", s);
+        stedc_device(n, d, e, w, Qt.as<double>(), n, s);
+    }
     Scratch* phd = is_cplx<T>() ? upload_vec(keep, ph, s) : nullptr;
     if (dbg) {
         // the tridiagonal itself as a dense matrix
@@ -511,6 +518,7 @@ void heev_1gpu(i64 n, T* Af, std::vector<double>& w, T* Z, bool wantz, hipStream
         upload(Td.p, td.data(), td.size() * sizeof(double), s);
         dbg_resid<double>("tridiagonal D&C", n, Td.as<double>(), n, Qt.as<double>(), n, w, s);
     }
+    NTRACE("heev::back_transform", s);
     real_to_phase<T>(n, n, Qt.as<double>(), n, phd ? kp(phd->as<T>()) : nullptr, kp(Z), n, s);
     if (nsw > 0 && total > 0) {
         if (!slate_hip::unmtr_hb2st_blocked<K<T>>(n, n, kp(Z), n, kp(V.as<T>()), b, kp(tau.as<T>()), spd->as<i64>(),
@@ -634,6 +642,7 @@ void symmetrize(i64 n, T* D, Uplo uplo, hipStream_t s) {
 
 template <typename T>
 int64_t heev_impl(HermitianMatrix<T>& A, std::vector<real_t<T>>& Lambda, Matrix<T>* Z) {
+    NTRACE("heev", nullptr);
     Runtime& R = rt();
     const Storage& SA = *A.storage();
     if (SA.m != SA.n) throw Error("native heev: square matrix");
@@ -871,6 +880,7 @@ void svd_1gpu(i64 m, i64 n, T* A, std::vector<double>& sv, T* U, T* V, bool want
 
 template <typename T>
 int64_t svd_impl(Matrix<T>& A, std::vector<real_t<T>>& S, Matrix<T>* U, Matrix<T>* VH) {
+    NTRACE("svd", nullptr);
     Runtime& R = rt();
     const Storage& SA = *A.storage();
     const i64 m0 = SA.m, n0 = SA.n, k = std::min(m0, n0);

@@ -253,6 +253,32 @@ inline void copy2d(T* dst, i64 ldd, const T* src, i64 lds, i64 m, i64 n, hipStre
     if (m > 0 && n > 0) slate_hip::gecopy<K<T>, K<T>>('G', 'N', m, n, kp(src), lds, kp(dst), ldd, s);
 }
 
+// ------------------------------------------------------------ tracing (native_trace.hip)
+namespace trace_rt {
+extern bool g_on;
+// one traced scope: a host span, and with a stream a device span (timing
+// event pair around the work enqueued on it meanwhile); the name must be a
+// string literal.  Costs one branch when tracing is off.
+class Scope {
+public:
+    explicit Scope(const char* name, hipStream_t s = nullptr);
+    ~Scope();
+    Scope(const Scope&) = delete;
+    Scope& operator=(const Scope&) = delete;
+
+private:
+    const char* name_;
+    hipStream_t s_;
+    hipEvent_t evb_ = nullptr, eve_ = nullptr;
+    double t0_ = -1;
+};
+void auto_start();     // SLATE_AMD_NATIVE_TRACE=<path> (initialize)
+void auto_finish();    // (finalize)
+}  // namespace trace_rt
+#define NTRACE_CAT2(a, b) a##b
+#define NTRACE_CAT(a, b) NTRACE_CAT2(a, b)
+#define NTRACE(name, stream) ::slate_amd::native::trace_rt::Scope NTRACE_CAT(ntrace_scope_, __LINE__)(name, stream)
+
 // full matrix of a stored triangle (native.hip): kind 0 = triangular (the
 // other part zero, a Unit diagonal set to one), 1 = Hermitian, 2 = symmetric
 template <typename T>

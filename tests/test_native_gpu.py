@@ -196,6 +196,40 @@ HEXE = os.path.join(ROOT, "slate_amd", "ex_native_handles")
 
 
 @pytest.mark.gpu
+def test_native_trace_chrome_json(tmp_path):
+    """Native tracing (SLATE Trace): a traced dpotrf + dgetrf on a 2 x 2 grid
+    (host transport) gathers every rank's host and per-stream device spans
+    to rank 0, which writes one Chrome trace-event JSON; timers() reports the
+    phases (host and @device seconds)."""
+    import json
+    path = str(tmp_path / "native_trace.json")
+    port = _free_port_block(4)
+    procs = []
+    for r in range(4):
+        env = _clean_env(r, 4, port, "host")
+        env["EX_NATIVE_TRACE"] = path
+        procs.append(subprocess.Popen([EXE, "2x2"], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                                      env=env))
+    outs = [p.communicate(timeout=240)[0] for p in procs]
+    for p, out in zip(procs, outs):
+        assert p.returncode == 0, out
+    print(outs[0])
+    ev = json.load(open(path))["traceEvents"]
+    spans = [e for e in ev if e.get("ph") == "X"]
+    assert {e["pid"] for e in spans} == {0, 1, 2, 3}
+    names = {e["name"] for e in spans}
+    for nm in ("potrf", "potrf::panel", "potrf::bcast", "potrf::lookahead", "potrf::update", "getrf",
+               "getrf::panel", "getrf::update"):
+        assert nm in names, (nm, sorted(names))
+    # device spans sit on the stream tracks (tid 1 panel, 2 update, 3 comm)
+    tids = {(e["name"], e["tid"]) for e in spans}
+    assert ("potrf::panel", 1) in tids and ("potrf::update", 2) in tids and ("potrf::bcast", 3) in tids, tids
+    assert all(e["dur"] >= 0 for e in spans)
+    timers = dict(re.findall(r"^timer (\S+) (\S+)$", outs[0], re.M))
+    assert float(timers["potrf"]) > 0 and float(timers["potrf::update@device"]) > 0, timers
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("grid", ["1x1", "2x2"])
 def test_native_handle_capi_from_c(grid):
     """The opaque-handle C API (slate_amd_matrix_create, _posv, _gesv,
