@@ -790,6 +790,105 @@ void run(int p, int q, int me) {
         for (size_t i = 0; i < ax.size(); ++i) ax[i] -= want[i];
         report(inf ? "gesv_rbt-FAILED" : "gesv_rbt", rel<T>(ax, want));
     }
+    // ---- matrix model: transposed views, structured types, slice, emptyLike
+    {
+        const int64_t ma = 170, ka = 90, na = 130;
+        sn::Matrix<T> A(ka, ma, nb, p, q), B(na, ka, nb, p, q), C(ma, na, nb, p, q);
+        A.generate(sn::Gen::Random, 181);
+        B.generate(sn::Gen::Random, 182);
+        std::vector<T> ha((size_t)ka * ma), hb((size_t)na * ka), hc((size_t)ma * na);
+        A.to_host(ha.data(), ka);
+        B.to_host(hb.data(), na);
+        // C = A^H B^T through views (no copies by the caller)
+        sn::gemm(T(1), sn::conj_transpose(A), sn::transpose(B), T(0), C);
+        C.to_host(hc.data(), ma);
+        auto want = mul<T>('C', 'T', ma, na, ka, ha, ka, hb, na);
+        std::vector<std::complex<double>> d(want.size());
+        for (size_t i = 0; i < want.size(); ++i) d[i] = std::complex<double>(std::real(hc[i]), std::imag(hc[i])) - want[i];
+        report("view_gemm", rel<T>(d, want));
+        const auto At = sn::transpose(A);
+        report("view_dims", (At.m() == ma && At.n() == ka && At.op() == sn::Op::Trans &&
+                             sn::transpose(At).op() == sn::Op::NoTrans) ? 0.0 : 1.0);
+        // ||A^T||_1 = ||A||_inf
+        report("view_norm", std::fabs(sn::norm(sn::Norm::One, At) - sn::norm(sn::Norm::Inf, A)) /
+                                sn::norm(sn::Norm::Inf, A));
+        // a view where the driver cannot take one: rejected, not misread
+        bool threw = false;
+        try {
+            sn::HermitianMatrix<T> Hv(sn::Uplo::Lower, sn::transpose(sn::Matrix<T>(na, na, nb, p, q)));
+            sn::potrf(Hv);
+        } catch (const sn::Error&) {
+            threw = true;
+        }
+        report("view_rejected", threw ? 0.0 : 1.0);
+        // TriangularMatrix: X = L^-H B with trsm on the conj_transpose VIEW of L
+        const int64_t nt_ = 120, nr = 7;
+        sn::TriangularMatrix<T> L(sn::Uplo::Lower, sn::Diag::NonUnit, nt_, nb, p, q);
+        L.generate(sn::Gen::Random, 183);
+        std::vector<T> hl((size_t)nt_ * nt_);
+        L.to_host(hl.data(), nt_);
+        for (int64_t j = 0; j < nt_; ++j)
+            for (int64_t i = 0; i < nt_; ++i) {
+                if (i < j) hl[i + j * nt_] = T(0);
+                if (i == j) hl[i + j * nt_] += T((double)nt_);
+            }
+        L.from_host(hl.data(), nt_);
+        sn::Matrix<T> X(nt_, nr, nb, p, q);
+        X.generate(sn::Gen::Random, 184);
+        std::vector<T> hx0((size_t)nt_ * nr), hx((size_t)nt_ * nr);
+        X.to_host(hx0.data(), nt_);
+        const auto LH = sn::conj_transpose(L);
+        report("tri_view_uplo", LH.uplo() == sn::Uplo::Upper && LH.uplo_physical() == sn::Uplo::Lower ? 0.0 : 1.0);
+        sn::trsm(sn::Side::Left, T(1), LH, X);
+        X.to_host(hx.data(), nt_);
+        auto lx = mul<T>('C', 'N', nt_, nr, nt_, hl, nt_, hx, nt_);
+        auto wx = widen(hx0);
+        for (size_t i = 0; i < lx.size(); ++i) lx[i] -= wx[i];
+        report("tri_view_trsm", rel<T>(lx, wx));
+        // trapezoid norm (m != n, unit diagonal): host reference
+        sn::TrapezoidMatrix<T> Z(sn::Uplo::Upper, sn::Diag::Unit, 90, 150, nb, p, q);
+        Z.generate(sn::Gen::Random, 185);
+        std::vector<T> hz((size_t)90 * 150);
+        Z.to_host(hz.data(), 90);
+        double fro = 0;
+        for (int64_t j = 0; j < 150; ++j)
+            for (int64_t i = 0; i < 90; ++i)
+                fro += i < j ? std::norm(std::complex<double>(std::real(hz[i + j * 90]), std::imag(hz[i + j * 90])))
+                             : (i == j ? 1.0 : 0.0);
+        report("trapezoid_norm", std::fabs(sn::norm(sn::Norm::Fro, Z) - std::sqrt(fro)) / std::sqrt(fro));
+        // slice at odd offsets, modify, write back
+        sn::Matrix<T> G(200, 160, nb, p, q);
+        G.generate(sn::Gen::Random, 186);
+        std::vector<T> hg((size_t)200 * 160), hs((size_t)67 * 45), hg2((size_t)200 * 160);
+        G.to_host(hg.data(), 200);
+        sn::Matrix<T> Sl = G.slice(13, 80, 29, 74);
+        Sl.to_host(hs.data(), 67);
+        double ds = 0;
+        for (int64_t j = 0; j < 45; ++j)
+            for (int64_t i = 0; i < 67; ++i) ds += std::abs(std::complex<double>(std::real(hs[i + j * 67] - hg[13 + i + (29 + j) * 200]),
+                                                                               std::imag(hs[i + j * 67] - hg[13 + i + (29 + j) * 200])));
+        sn::scale<T>((sn::real_t<T>)2, (sn::real_t<T>)1, Sl);
+        G.set_slice(13, 29, Sl);
+        G.to_host(hg2.data(), 200);
+        for (int64_t j = 0; j < 160; ++j)
+            for (int64_t i = 0; i < 200; ++i) {
+                const bool in = i >= 13 && i < 80 && j >= 29 && j < 74;
+                const T w = in ? hg[i + j * 200] * (sn::real_t<T>)2 : hg[i + j * 200];
+                ds += std::abs(std::complex<double>(std::real(hg2[i + j * 200] - w), std::imag(hg2[i + j * 200] - w)));
+            }
+        report("slice_roundtrip", ds);
+        const auto E = sn::transpose(G).emptyLike();
+        report("empty_like", (E.m() == 160 && E.n() == 200 && sn::norm(sn::Norm::Max, E) == 0.0) ? 0.0 : 1.0);
+        // SymmetricMatrix overloads: C = A A^T (syrk) and symm against gemm
+        sn::SymmetricMatrix<T> Sy(sn::Uplo::Lower, na, nb, p, q);
+        sn::syrk(T(1), B, T(0), Sy);
+        sn::Matrix<T> F(na, na, nb, p, q), I(na, na, nb, p, q), F2(na, na, nb, p, q);
+        sn::set(T(0), T(1), I);
+        sn::symm(sn::Side::Left, T(1), Sy, I, T(0), F);             // the full symmetric matrix
+        sn::gemm(T(1), B, sn::transpose(B), T(0), F2);
+        sn::add(T(-1), F2, T(1), F);
+        report("sym_syrk_symm", sn::norm(sn::Norm::Max, F) / sn::norm(sn::Norm::Max, F2));
+    }
     // ---- hegv: A Z = B Z Lambda (itype 1), A B Z = Z Lambda (2),
     //      B A Z = Z Lambda (3); B Lower and Upper; || residual || / (|| A || || B || n)
     for (int v = 0; v < 3; ++v) {

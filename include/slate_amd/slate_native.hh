@@ -99,12 +99,15 @@ class Matrix {
 public:
     Matrix() = default;
     Matrix(int64_t m, int64_t n, int64_t nb, int p = 1, int q = 1);
+    // dimensions of the matrix as seen through its op (a transposed view of
+    // an m x n matrix is n x m); nb / p / q / mloc / nloc / lld / data refer
+    // to the storage
     int64_t m() const;
     int64_t n() const;
     int64_t nb() const;
     int p() const;
     int q() const;
-    int64_t mloc() const;     // local rows / columns of this rank
+    int64_t mloc() const;     // local rows / columns of this rank (storage)
     int64_t nloc() const;
     int64_t lld() const;      // leading dimension of the local buffer
     T* data();                // device pointer to the local buffer
@@ -118,7 +121,11 @@ public:
     // This rank's local block in ScaLAPACK layout (host, leading dim lld).
     void from_local_host(const T* Aloc, int64_t lld);
     void to_local_host(T* Aloc, int64_t lld) const;
-    std::shared_ptr<Storage> storage() const { return s_; }
+    // the storage of a plain (op NoTrans) matrix; a transposed view throws:
+    // every driver that does not take op(A) directly rejects views instead
+    // of silently reading the untransposed data (materialise with copy())
+    std::shared_ptr<Storage> storage() const;
+    std::shared_ptr<Storage> storage_any() const { return s_; }
     // Zero-copy wrapper of a DEVICE buffer that holds this rank's local block
     // in ScaLAPACK layout (SLATE fromScaLAPACK / fromDevices); the caller
     // keeps ownership, lld >= mloc (an even lld keeps the 16-byte MFMA loads).
@@ -127,10 +134,49 @@ public:
     // Matrix::sub); i0 a multiple of p and j0 of q, so the view's tile (0, 0)
     // stays on process (0, 0) and every driver takes it as it is.
     Matrix sub(int64_t i0, int64_t i1, int64_t j0, int64_t j1) const;
+    // The elements [i0, i1) x [j0, j1) at ANY offset (SLATE Matrix::slice):
+    // a block-cyclic layout cannot start inside a tile, so this is a copy on
+    // the same grid and tile size (each value travels to its new owner,
+    // nothing else); set_slice writes such a matrix back at (i0, j0).
+    Matrix slice(int64_t i0, int64_t i1, int64_t j0, int64_t j1) const;
+    void set_slice(int64_t i0, int64_t j0, const Matrix& S);
+    // a zeroed matrix of the same (op-applied) shape, grid and tile size
+    // (SLATE emptyLike)
+    Matrix emptyLike() const;
+    // transposition state (SLATE BaseMatrix::op): transpose() /
+    // conj_transpose() below return views sharing the storage
+    Op op() const { return op_; }
+    // the same storage seen untransposed
+    Matrix base() const {
+        Matrix b(*this);
+        b.op_ = Op::NoTrans;
+        return b;
+    }
+    // compose the view's op with o (T T = N, C C = N; a conjugation alone
+    // is not a view and throws)
+    void apply_op(Op o);
 
 protected:
     std::shared_ptr<Storage> s_;
+    Op op_ = Op::NoTrans;
 };
+
+// transposed / conjugate-transposed VIEWS (SLATE transpose / conj_transpose,
+// BaseMatrix.hh:768-795): same storage, same class (a TriangularMatrix stays
+// one, its logical uplo flips).  gemm, copy, trsm, trmm, herk / syrk,
+// her2k / syr2k, norm and add take views directly; other drivers reject them.
+template <typename MT>
+MT transpose(const MT& A) {
+    MT B(A);
+    B.apply_op(Op::Trans);
+    return B;
+}
+template <typename MT>
+MT conj_transpose(const MT& A) {
+    MT B(A);
+    B.apply_op(Op::ConjTrans);
+    return B;
+}
 
 template <typename T>
 class HermitianMatrix : public Matrix<T> {
@@ -141,6 +187,47 @@ public:
     // the uplo triangle of a square matrix or view, sharing its storage
     HermitianMatrix(Uplo uplo, const Matrix<T>& A) : Matrix<T>(A), uplo_(uplo) {}
     Uplo uplo() const { return uplo_; }
+
+private:
+    Uplo uplo_ = Uplo::Lower;
+};
+
+// structured matrices (SLATE TrapezoidMatrix / TriangularMatrix /
+// SymmetricMatrix, include/slate/TriangularMatrix.hh:30-684): a general
+// storage plus the referenced triangle; uplo() is the LOGICAL triangle of
+// the (possibly transposed) view, uplo_physical() the stored one
+inline Uplo flip_uplo(Uplo u) { return u == Uplo::Lower ? Uplo::Upper : Uplo::Lower; }
+template <typename T>
+class TrapezoidMatrix : public Matrix<T> {
+public:
+    TrapezoidMatrix() = default;
+    TrapezoidMatrix(Uplo uplo, Diag diag, int64_t m, int64_t n, int64_t nb, int p = 1, int q = 1)
+        : Matrix<T>(m, n, nb, p, q), uplo_(uplo), diag_(diag) {}
+    TrapezoidMatrix(Uplo uplo, Diag diag, const Matrix<T>& A) : Matrix<T>(A), uplo_(uplo), diag_(diag) {}
+    Uplo uplo() const { return this->op() == Op::NoTrans ? uplo_ : flip_uplo(uplo_); }
+    Uplo uplo_physical() const { return uplo_; }
+    Diag diag() const { return diag_; }
+
+private:
+    Uplo uplo_ = Uplo::Lower;
+    Diag diag_ = Diag::NonUnit;
+};
+template <typename T>
+class TriangularMatrix : public TrapezoidMatrix<T> {
+public:
+    TriangularMatrix() = default;
+    TriangularMatrix(Uplo uplo, Diag diag, int64_t n, int64_t nb, int p = 1, int q = 1)
+        : TrapezoidMatrix<T>(uplo, diag, n, n, nb, p, q) {}
+    TriangularMatrix(Uplo uplo, Diag diag, const Matrix<T>& A) : TrapezoidMatrix<T>(uplo, diag, A) {}
+};
+template <typename T>
+class SymmetricMatrix : public Matrix<T> {
+public:
+    SymmetricMatrix() = default;
+    SymmetricMatrix(Uplo uplo, int64_t n, int64_t nb, int p = 1, int q = 1) : Matrix<T>(n, n, nb, p, q), uplo_(uplo) {}
+    SymmetricMatrix(Uplo uplo, const Matrix<T>& A) : Matrix<T>(A), uplo_(uplo) {}
+    Uplo uplo() const { return this->op() == Op::NoTrans ? uplo_ : flip_uplo(uplo_); }
+    Uplo uplo_physical() const { return uplo_; }
 
 private:
     Uplo uplo_ = Uplo::Lower;
@@ -327,6 +414,29 @@ template <typename T> int64_t hesv(HermitianMatrix<T>& A, Matrix<T>& B, const Op
 template <typename T> void scale(real_t<T> numer, real_t<T> denom, Matrix<T>& A);
 // LU solve with the factors of getrf_nopiv
 template <typename T> int64_t getrs_nopiv(const Matrix<T>& A, Matrix<T>& B, const Options& opts = {});
+
+// ---- SLATE-style overloads on the structured types (slate.hh trsm / trmm /
+// trtri / norm / symm / syrk / herk / syr2k / her2k taking
+// TriangularMatrix / SymmetricMatrix / HermitianMatrix operands); op(A) of a
+// view is honoured
+template <typename T>
+void trsm(Side side, T alpha, const TriangularMatrix<T>& A, Matrix<T>& B, const Options& opts = {});
+template <typename T>
+void trmm(Side side, T alpha, const TriangularMatrix<T>& A, Matrix<T>& B, const Options& opts = {});
+template <typename T> int64_t trtri(TriangularMatrix<T>& A, const Options& opts = {});
+template <typename T> double norm(Norm kind, const TrapezoidMatrix<T>& A);
+template <typename T> double norm(Norm kind, const SymmetricMatrix<T>& A);
+template <typename T>
+void symm(Side side, T alpha, const SymmetricMatrix<T>& A, const Matrix<T>& B, T beta, Matrix<T>& C,
+          const Options& opts = {});
+template <typename T> void syrk(T alpha, const Matrix<T>& A, T beta, SymmetricMatrix<T>& C, const Options& opts = {});
+template <typename T>
+void herk(real_t<T> alpha, const Matrix<T>& A, real_t<T> beta, HermitianMatrix<T>& C, const Options& opts = {});
+template <typename T>
+void syr2k(T alpha, const Matrix<T>& A, const Matrix<T>& B, T beta, SymmetricMatrix<T>& C, const Options& opts = {});
+template <typename T>
+void her2k(T alpha, const Matrix<T>& A, const Matrix<T>& B, real_t<T> beta, HermitianMatrix<T>& C,
+           const Options& opts = {});
 
 struct QRData;
 template <typename T>

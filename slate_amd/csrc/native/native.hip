@@ -302,6 +302,7 @@ Matrix<T> Matrix<T>::from_device(T* d_local, int64_t lld, int64_t m, int64_t n, 
 
 template <typename T>
 Matrix<T> Matrix<T>::sub(int64_t i0, int64_t i1, int64_t j0, int64_t j1) const {
+    (void)storage();           // plain matrices only (a view throws)
     const Storage& P = *s_;
     const i64 mt = (P.m + P.nb - 1) / P.nb, nt = (P.n + P.nb - 1) / P.nb;
     if (i0 < 0 || j0 < 0 || i1 > mt || j1 > nt || i0 > i1 || j0 > j1)
@@ -324,8 +325,18 @@ Matrix<T> Matrix<T>::sub(int64_t i0, int64_t i1, int64_t j0, int64_t j1) const {
     return M;
 }
 
-template <typename T> int64_t Matrix<T>::m() const { return s_->m; }
-template <typename T> int64_t Matrix<T>::n() const { return s_->n; }
+template <typename T> int64_t Matrix<T>::m() const { return op_ == Op::NoTrans ? s_->m : s_->n; }
+template <typename T> int64_t Matrix<T>::n() const { return op_ == Op::NoTrans ? s_->n : s_->m; }
+template <typename T>
+std::shared_ptr<Storage> Matrix<T>::storage() const {
+    if (op_ != Op::NoTrans)
+        throw Error("native: this routine does not take a transposed view (materialise it with copy())");
+    return s_;
+}
+template <typename T>
+void Matrix<T>::apply_op(Op o) {
+    op_ = compose_op<T>(o, op_);
+}
 template <typename T> int64_t Matrix<T>::nb() const { return s_->nb; }
 template <typename T> int Matrix<T>::p() const { return s_->p; }
 template <typename T> int Matrix<T>::q() const { return s_->q; }
@@ -337,6 +348,7 @@ template <typename T> const T* Matrix<T>::data() const { return static_cast<cons
 
 template <typename T>
 void Matrix<T>::generate(Gen kind, uint64_t seed) {
+    (void)storage();           // plain matrices only (a view throws)
     Storage& s = *s_;
     slate_hip::matgen<K<T>>((int)kind, seed, s.mloc, s.nloc, kp(data()), s.lld, s.m, s.n, s.nb, s.p, s.pr, s.nb, s.q,
                             s.pc, 0, 0, 1.0, rt().main);
@@ -347,6 +359,7 @@ void Matrix<T>::generate(Gen kind, uint64_t seed) {
 // gecopy kernel (no pitched hipMemcpy2D: see copy2d below)
 template <typename T>
 void Matrix<T>::from_local_host(const T* Aloc, int64_t ld) {
+    (void)storage();           // plain matrices only (a view throws)
     const Storage& s = *s_;
     Runtime& R = rt();
     if (!s.mloc || !s.nloc) return;
@@ -362,6 +375,7 @@ void Matrix<T>::from_local_host(const T* Aloc, int64_t ld) {
 
 template <typename T>
 void Matrix<T>::to_local_host(T* Aloc, int64_t ld) const {
+    (void)storage();           // plain matrices only (a view throws)
     const Storage& s = *s_;
     Runtime& R = rt();
     NHIP(hipDeviceSynchronize());
@@ -380,6 +394,7 @@ void Matrix<T>::to_local_host(T* Aloc, int64_t ld) const {
 // goes through a contiguous mloc x nloc staging block)
 template <typename T>
 void Matrix<T>::from_host(const T* A, int64_t lda) {
+    (void)storage();           // plain matrices only (a view throws)
     Storage& s = *s_;
     std::vector<T> loc((size_t)std::max<i64>(s.mloc, 1) * std::max<i64>(s.nloc, 1), T(0));
     for (i64 lj = 0; lj < s.nloc; ++lj) {
@@ -393,6 +408,7 @@ void Matrix<T>::from_host(const T* A, int64_t lda) {
 // (padded to the largest local block), each rank scatters them on the host
 template <typename T>
 void Matrix<T>::to_host(T* A, int64_t lda) const {
+    (void)storage();           // plain matrices only (a view throws)
     const Storage& s = *s_;
     Runtime& R = rt();
     NHIP(hipDeviceSynchronize());
@@ -427,13 +443,6 @@ void Matrix<T>::to_host(T* A, int64_t lda) const {
 // ------------------------------------------------------------ helpers
 namespace {
 
-// lower-triangle mask of a local block whose (0, 0) is local (r0, c0) of a
-// block-cyclic matrix (the Python drivers' (1, nb, p, pr, q, pc, r0, c0, 0))
-slate_hip::TriMask lower_mask(i64 nb, int p, int pr, int q, int pc, i64 r0, i64 c0) {
-    slate_hip::TriMask t;
-    t.mode = 1; t.nb = nb; t.p = p; t.pr = pr; t.q = q; t.pc = pc; t.row_off = r0; t.col_off = c0; t.diag_off = 0;
-    return t;
-}
 
 int64_t read_infos(const i64* d, i64 nt, hipStream_t s, i64 nb) {
     std::vector<i64> h((size_t)std::max<i64>(nt, 1));
@@ -984,8 +993,10 @@ static void trsm_left_t(char uplo, char diag, char tr, T alpha, const Storage& S
 }
 
 template <typename T>
-void trsm(Side side, Uplo uplo, Op op, Diag diag, T alpha, const Matrix<T>& A, Matrix<T>& B, const Options& opts) {
+void trsm(Side side, Uplo uplo, Op op, Diag diag, T alpha, const Matrix<T>& Av, Matrix<T>& B, const Options& opts) {
     NTRACE("trsm", nullptr);
+    op = compose_op<T>(op, Av.op());
+    const Matrix<T> A = Av.base();
     const Storage& SA = *A.storage();
     Storage& SB = *B.storage();
     const bool left = side == Side::Left;
@@ -1012,7 +1023,9 @@ void trsm(Side side, Uplo uplo, Op op, Diag diag, T alpha, const Matrix<T>& A, M
 }
 
 template <typename T>
-void copy(Op op, const Matrix<T>& A, Matrix<T>& B) {
+void copy(Op op, const Matrix<T>& Av, Matrix<T>& B) {
+    op = compose_op<T>(op, Av.op());
+    const Matrix<T> A = Av.base();
     const Storage& SA = *A.storage();
     Storage& SB = *B.storage();
     const bool tr = op != Op::NoTrans;
@@ -1687,12 +1700,19 @@ static void summa(T alpha, const Storage& SA, const Storage& SB, T beta, Storage
 
 template <typename T>
 void gemm(T alpha, const Matrix<T>& A, const Matrix<T>& B, T beta, Matrix<T>& C, const Options& opts) {
+    if (A.op() != Op::NoTrans || B.op() != Op::NoTrans) {
+        gemm<T>(A.op(), B.op(), alpha, A.base(), B.base(), beta, C, opts);
+        return;
+    }
     summa<T>(alpha, *A.storage(), *B.storage(), beta, *C.storage(), opts, nullptr);
 }
 
 // op(X) as a matrix of its own (X itself for NoTrans)
 template <typename T>
-static Matrix<T> op_copy(Op op, const Matrix<T>& X) {
+static Matrix<T> op_copy(Op op, const Matrix<T>& Xv) {
+    // op(X) of a view X = op'(base) with op' = op composed with the view's op
+    op = compose_op<T>(op, Xv.op());
+    const Matrix<T> X = Xv.base();
     if (op == Op::NoTrans) return X;
     const Storage& S = *X.storage();
     Matrix<T> Y(S.n, S.m, S.nb, S.p, S.q);
@@ -1833,7 +1853,9 @@ void symm(Side side, T alpha, const HermitianMatrix<T>& A, const Matrix<T>& B, T
 
 // B = alpha op(A) B (Left) or alpha B op(A) (Right), A triangular
 template <typename T>
-void trmm(Side side, Uplo uplo, Op op, Diag diag, T alpha, const Matrix<T>& A, Matrix<T>& B, const Options& opts) {
+void trmm(Side side, Uplo uplo, Op op, Diag diag, T alpha, const Matrix<T>& Av, Matrix<T>& B, const Options& opts) {
+    op = compose_op<T>(op, Av.op());
+    const Matrix<T> A = Av.base();
     if (op == Op::Trans && is_cplx<T>()) throw Error("native trmm: Trans of a complex matrix (use ConjTrans)");
     const Matrix<T> Af = expand_tri<T>(A, uplo, 0, diag);
     const Matrix<T> Ao = op_copy<T>(op, Af);
@@ -1862,7 +1884,8 @@ double norm_triangular(Norm kind, Uplo uplo, Diag diag, const Matrix<T>& A) {
 // ------------------------------------------------------------ aux (src/add.cc, src/set.cc)
 // B = alpha A + beta B (same grid): one local kernel
 template <typename T>
-void add(T alpha, const Matrix<T>& A, T beta, Matrix<T>& B) {
+void add(T alpha, const Matrix<T>& Av, T beta, Matrix<T>& B) {
+    const Matrix<T> A = op_copy<T>(Op::NoTrans, Av);     // a view is materialised once
     const Storage& SA = *A.storage();
     const Storage& SB = *B.storage();
     if (SA.m != SB.m || SA.n != SB.n || SA.nb != SB.nb || SA.p != SB.p || SA.q != SB.q)
@@ -2335,8 +2358,11 @@ int64_t gesv_mixed(Matrix<T>& A, std::vector<int64_t>& ipiv, Matrix<T>& B, Matri
 
 // ------------------------------------------------------------ norm
 template <typename T>
-double norm(Norm kind, const Matrix<T>& A) {
+double norm(Norm kind, const Matrix<T>& Av) {
     using Rl = decltype(std::real(T()));
+    if (Av.op() != Op::NoTrans && (kind == Norm::One || kind == Norm::Inf))
+        kind = kind == Norm::One ? Norm::Inf : Norm::One;       // ||A^T||_1 = ||A||_inf
+    const Matrix<T> A = Av.base();
     const Storage& S = *A.storage();
     Runtime& R = rt();
     hipStream_t s = R.main;

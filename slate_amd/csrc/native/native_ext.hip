@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "../hip/kernels.hpp"
+#include "capi_util.hpp"
 #include "native_rt.hpp"
 
 namespace slate_amd {
@@ -550,6 +551,124 @@ void scale(real_t<T> numer, real_t<T> denom, Matrix<T>& A) {
     NHIP(hipStreamSynchronize(s));
 }
 
+// ------------------------------------------------------------ matrix model
+// Matrix::slice / set_slice: the element range at any offset moves to / from
+// a new aligned matrix of the same grid and tile size with the value
+// redistribution of the ScaLAPACK shims (capi_util.hpp scal_move: every
+// value goes straight to its new owner, host-staged)
+template <typename T>
+Matrix<T> Matrix<T>::slice(int64_t i0, int64_t i1, int64_t j0, int64_t j1) const {
+    const Storage& S = *storage();
+    if (i0 < 0 || j0 < 0 || i1 > S.m || j1 > S.n || i0 > i1 || j0 > j1) throw Error("Matrix::slice: range outside");
+    Matrix<T> R(i1 - i0, j1 - j0, S.nb, S.p, S.q);
+    const Storage& SR = *R.storage();
+    const i64 lda = std::max<i64>(S.mloc, 1), ldr = std::max<i64>(SR.mloc, 1);
+    std::vector<T> a((size_t)lda * std::max<i64>(S.nloc, 1)), r((size_t)ldr * std::max<i64>(SR.nloc, 1));
+    if (S.mloc && S.nloc) to_local_host(a.data(), lda);
+    const capi::ScalLay L{S.m, S.n, S.nb, S.nb, lda, 0, 0, S.p, S.q, false};
+    capi::scal_move<T>(L, i0, j0, i1 - i0, j1 - j0, a.data(), SR, r.data(), ldr, true);
+    if (SR.mloc && SR.nloc) R.from_local_host(r.data(), ldr);
+    return R;
+}
+
+template <typename T>
+void Matrix<T>::set_slice(int64_t i0, int64_t j0, const Matrix<T>& Sv) {
+    const Storage& S = *storage();
+    const Matrix<T> Sm = Sv.op() == Op::NoTrans ? Sv : [&] {
+        Matrix<T> M(Sv.m(), Sv.n(), Sv.nb(), Sv.p(), Sv.q());
+        copy<T>(Op::NoTrans, Sv, M);
+        return M;
+    }();
+    const Storage& SR = *Sm.storage();
+    if (SR.p != S.p || SR.q != S.q || SR.nb != S.nb) throw Error("Matrix::set_slice: same grid and tile size");
+    if (i0 < 0 || j0 < 0 || i0 + SR.m > S.m || j0 + SR.n > S.n) throw Error("Matrix::set_slice: range outside");
+    const i64 lda = std::max<i64>(S.mloc, 1), ldr = std::max<i64>(SR.mloc, 1);
+    std::vector<T> a((size_t)lda * std::max<i64>(S.nloc, 1)), r((size_t)ldr * std::max<i64>(SR.nloc, 1));
+    if (S.mloc && S.nloc) to_local_host(a.data(), lda);
+    if (SR.mloc && SR.nloc) Sm.to_local_host(r.data(), ldr);
+    const capi::ScalLay L{S.m, S.n, S.nb, S.nb, lda, 0, 0, S.p, S.q, false};
+    capi::scal_move<T>(L, i0, j0, SR.m, SR.n, a.data(), SR, r.data(), ldr, false);
+    if (S.mloc && S.nloc) from_local_host(a.data(), lda);
+}
+
+template <typename T>
+Matrix<T> Matrix<T>::emptyLike() const {
+    return Matrix<T>(m(), n(), nb(), p(), q());
+}
+
+// structured overloads: the stored triangle and the view's op map onto the
+// enum-argument drivers (trsm / trmm take op(A) of a view directly)
+template <typename T>
+void trsm(Side side, T alpha, const TriangularMatrix<T>& A, Matrix<T>& B, const Options& opts) {
+    trsm<T>(side, A.uplo_physical(), Op::NoTrans, A.diag(), alpha, A, B, opts);
+}
+template <typename T>
+void trmm(Side side, T alpha, const TriangularMatrix<T>& A, Matrix<T>& B, const Options& opts) {
+    trmm<T>(side, A.uplo_physical(), Op::NoTrans, A.diag(), alpha, A, B, opts);
+}
+template <typename T>
+int64_t trtri(TriangularMatrix<T>& A, const Options& opts) {
+    Matrix<T>& M = A;
+    return trtri<T>(A.uplo_physical(), A.diag(), M, opts);
+}
+// trapezoid / triangular norm: the stored trapezoid of any m x n (masked
+// copy, a Unit diagonal set), then the general norm -- of op(A) for a view
+template <typename T>
+double norm(Norm kind, const TrapezoidMatrix<T>& A) {
+    const Matrix<T> B = A.base();
+    const Storage& S = *B.storage();
+    if (S.m == S.n) {
+        const Matrix<T> F = expand_tri<T>(B, A.uplo_physical(), 0, A.diag());
+        return norm<T>(kind, A.op() == Op::NoTrans ? F : transpose(F));
+    }
+    Matrix<T> F(S.m, S.n, S.nb, S.p, S.q);
+    Storage& SF = *F.storage();
+    hipStream_t s = rt().main;
+    slate_hip::TriMask mk = lower_mask(S.nb, S.p, S.pr, S.q, S.pc, 0, 0);
+    if (A.uplo_physical() == Uplo::Upper) mk.mode = 2;
+    const bool unit = A.diag() == Diag::Unit;
+    mk.diag_off = unit ? -1 : 0;
+    if (S.mloc && S.nloc)
+        slate_hip::gecopy_mask<K<T>>(mk, S.mloc, S.nloc, kp(static_cast<const T*>(S.buf)), S.lld,
+                                     kp(static_cast<T*>(SF.buf)), SF.lld, false, s);
+    NHIP(hipStreamSynchronize(s));
+    if (unit) {
+        // ones on the global diagonal: F += I (the masked copy left it zero)
+        Matrix<T> I(S.m, S.n, S.nb, S.p, S.q);
+        set<T>(T(0), T(1), I);
+        add<T>(T(1), I, T(1), F);
+    }
+    return norm<T>(kind, A.op() == Op::NoTrans ? F : transpose(F));
+}
+template <typename T>
+double norm(Norm kind, const SymmetricMatrix<T>& A) {
+    return norm_symmetric<T>(kind, HermitianMatrix<T>(A.uplo_physical(), A.base()));
+}
+template <typename T>
+void symm(Side side, T alpha, const SymmetricMatrix<T>& A, const Matrix<T>& B, T beta, Matrix<T>& C,
+          const Options& opts) {
+    symm<T>(side, alpha, HermitianMatrix<T>(A.uplo_physical(), A.base()), B, beta, C, opts);
+}
+template <typename T>
+void syrk(T alpha, const Matrix<T>& A, T beta, SymmetricMatrix<T>& C, const Options& opts) {
+    HermitianMatrix<T> H(C.uplo_physical(), C.base());
+    syrk<T>(Op::NoTrans, alpha, A, beta, H, opts);
+}
+template <typename T>
+void herk(real_t<T> alpha, const Matrix<T>& A, real_t<T> beta, HermitianMatrix<T>& C, const Options& opts) {
+    herk<T>(Op::NoTrans, alpha, A, beta, C, opts);
+}
+template <typename T>
+void syr2k(T alpha, const Matrix<T>& A, const Matrix<T>& B, T beta, SymmetricMatrix<T>& C, const Options& opts) {
+    HermitianMatrix<T> H(C.uplo_physical(), C.base());
+    syr2k<T>(Op::NoTrans, alpha, A, B, beta, H, opts);
+}
+template <typename T>
+void her2k(T alpha, const Matrix<T>& A, const Matrix<T>& B, real_t<T> beta, HermitianMatrix<T>& C,
+           const Options& opts) {
+    her2k<T>(Op::NoTrans, alpha, A, B, beta, C, opts);
+}
+
 // ------------------------------------------------------------ instantiation
 #define SLATE_NATIVE_EXT(T)                                                                                    \
     template void hegst<T>(int64_t, HermitianMatrix<T>&, const HermitianMatrix<T>&, const Options&);            \
@@ -560,7 +679,20 @@ void scale(real_t<T> numer, real_t<T> denom, Matrix<T>& A) {
     template int64_t gesv_rbt<T>(Matrix<T>&, Matrix<T>&, const Options&);                                      \
     template int64_t getrs_nopiv<T>(const Matrix<T>&, Matrix<T>&, const Options&);                             \
     template int64_t hesv<T>(HermitianMatrix<T>&, Matrix<T>&, const Options&);                                 \
-    template void scale<T>(real_t<T>, real_t<T>, Matrix<T>&);
+    template void scale<T>(real_t<T>, real_t<T>, Matrix<T>&);                                                  \
+    template Matrix<T> Matrix<T>::slice(int64_t, int64_t, int64_t, int64_t) const;                             \
+    template void Matrix<T>::set_slice(int64_t, int64_t, const Matrix<T>&);                                    \
+    template Matrix<T> Matrix<T>::emptyLike() const;                                                           \
+    template void trsm<T>(Side, T, const TriangularMatrix<T>&, Matrix<T>&, const Options&);                   \
+    template void trmm<T>(Side, T, const TriangularMatrix<T>&, Matrix<T>&, const Options&);                   \
+    template int64_t trtri<T>(TriangularMatrix<T>&, const Options&);                                          \
+    template double norm<T>(Norm, const TrapezoidMatrix<T>&);                                                 \
+    template double norm<T>(Norm, const SymmetricMatrix<T>&);                                                 \
+    template void symm<T>(Side, T, const SymmetricMatrix<T>&, const Matrix<T>&, T, Matrix<T>&, const Options&); \
+    template void syrk<T>(T, const Matrix<T>&, T, SymmetricMatrix<T>&, const Options&);                        \
+    template void herk<T>(real_t<T>, const Matrix<T>&, real_t<T>, HermitianMatrix<T>&, const Options&);        \
+    template void syr2k<T>(T, const Matrix<T>&, const Matrix<T>&, T, SymmetricMatrix<T>&, const Options&);     \
+    template void her2k<T>(T, const Matrix<T>&, const Matrix<T>&, real_t<T>, HermitianMatrix<T>&, const Options&);
 SLATE_NATIVE_EXT(float)
 SLATE_NATIVE_EXT(double)
 SLATE_NATIVE_EXT(std::complex<float>)

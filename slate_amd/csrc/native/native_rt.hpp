@@ -174,6 +174,17 @@ template <typename T> inline K<T> kv(T v) {
 }
 template <typename T> constexpr bool is_cplx() { return !std::is_same<T, float>::value && !std::is_same<T, double>::value; }
 template <typename T> constexpr char ctrans() { return is_cplx<T>() ? 'C' : 'T'; }
+// op(view(A)) for a view whose op is `view` (real types: ConjTrans == Trans):
+// T T = C C = NoTrans; a conjugation without transposition is not a view
+template <typename T> inline Op compose_op(Op outer, Op view) {
+    auto canon = [](Op o) { return (!is_cplx<T>() && o == Op::ConjTrans) ? Op::Trans : o; };
+    outer = canon(outer);
+    view = canon(view);
+    if (view == Op::NoTrans) return outer;
+    if (outer == Op::NoTrans) return view;
+    if (outer == view) return Op::NoTrans;
+    throw Error("native: conj(A) (a conjugate without transpose) is not a view");
+}
 template <typename T> inline T conj_of(T x) {
     if constexpr (is_cplx<T>()) return std::conj(x);
     else return x;
@@ -278,6 +289,14 @@ void auto_finish();    // (finalize)
 #define NTRACE_CAT2(a, b) a##b
 #define NTRACE_CAT(a, b) NTRACE_CAT2(a, b)
 #define NTRACE(name, stream) ::slate_amd::native::trace_rt::Scope NTRACE_CAT(ntrace_scope_, __LINE__)(name, stream)
+
+// lower-triangle mask of a local block whose (0, 0) is local (r0, c0) of a
+// block-cyclic matrix (the Python drivers' (1, nb, p, pr, q, pc, r0, c0, 0))
+inline slate_hip::TriMask lower_mask(i64 nb, int p, int pr, int q, int pc, i64 r0, i64 c0) {
+    slate_hip::TriMask t;
+    t.mode = 1; t.nb = nb; t.p = p; t.pr = pr; t.q = q; t.pc = pc; t.row_off = r0; t.col_off = c0; t.diag_off = 0;
+    return t;
+}
 
 // full matrix of a stored triangle (native.hip): kind 0 = triangular (the
 // other part zero, a Unit diagonal set to one), 1 = Hermitian, 2 = symmetric

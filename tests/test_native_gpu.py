@@ -129,7 +129,10 @@ def _assert_checks(checks, out):
                                                    "gecondest", "svd", "svd_orth", "svd_wide", "svd_wide_orth", "geqrf", "geqrf_wide", "gels_grid",
                                                    "trsm_lt", "trsm_rn", "trsm_rc", "trtri", "trtrm", "gesv_nopiv",
                                                    "cholqr", "cholqr_orth", "gelqf", "sub_potrf", "from_device_potrs", "lu_xchg_bound",
-                                                   "svd_values", "gesv_rbt", "hegv1", "hegv2_upper", "hegv3")]
+                                                   "svd_values", "gesv_rbt", "hegv1", "hegv2_upper", "hegv3",
+                                                   "view_gemm", "view_dims", "view_norm", "view_rejected",
+                                                   "tri_view_uplo", "tri_view_trsm", "trapezoid_norm",
+                                                   "slice_roundtrip", "empty_like", "sym_syrk_symm")]
     for name in names:
         assert name in checks, (name, out)
         assert float(checks[name]) < TOL[name[-1]], (name, checks[name])
