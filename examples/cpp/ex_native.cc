@@ -790,6 +790,127 @@ void run(int p, int q, int me) {
         for (size_t i = 0; i < ax.size(); ++i) ax[i] -= want[i];
         report(inf ? "gesv_rbt-FAILED" : "gesv_rbt", rel<T>(ax, want));
     }
+    // ---- band matrices (compact 1-D column-tile storage): pbsv (Lower and
+    //      Upper), gbsv, tbsm, gbmm, hbmm against dense host products
+    {
+        const int64_t nbd = 300, kd = 40, kl = 35, ku = 20, nrb = 3;
+        auto resid = [&](const std::vector<T>& Ad, const std::vector<T>& X, const std::vector<T>& B0, int64_t nrr) {
+            auto ax = mul<T>('N', 'N', nbd, nrr, nbd, Ad, nbd, X, nbd);
+            auto w = widen(B0);
+            for (size_t i = 0; i < ax.size(); ++i) ax[i] -= w[i];
+            return rel<T>(ax, w);
+        };
+        for (int up = 0; up < 2; ++up) {
+            sn::HermitianBandMatrix<T> Hb(sn::Uplo::Lower, nbd, kd, nb);
+            Hb.generate(sn::Gen::HermitianPositiveDefinite, 191);
+            std::vector<T> hl((size_t)nbd * nbd), hf((size_t)nbd * nbd);
+            Hb.to_host(hl.data(), nbd);
+            for (int64_t j = 0; j < nbd; ++j)
+                for (int64_t i = 0; i < nbd; ++i) {
+                    const T v = i >= j ? hl[i + j * nbd] : cj(hl[j + i * nbd]);
+                    hf[i + j * nbd] = i == j ? T(std::real(v)) : v;
+                }
+            sn::HermitianBandMatrix<T> Hu(up ? sn::Uplo::Upper : sn::Uplo::Lower, nbd, kd, nb);
+            Hu.from_host(hf.data(), nbd);
+            sn::Matrix<T> Bm(nbd, nrb, nb, p, q);
+            Bm.generate(sn::Gen::Random, 192);
+            std::vector<T> b0((size_t)nbd * nrb), x((size_t)nbd * nrb);
+            Bm.to_host(b0.data(), nbd);
+            const int64_t inf = sn::pbsv(Hu, Bm);
+            Bm.to_host(x.data(), nbd);
+            report(inf ? "pbsv-FAILED" : (up ? "pbsv_upper" : "pbsv"), resid(hf, x, b0, nrb));
+        }
+        {
+            sn::BandMatrix<T> Gb(nbd, nbd, kl, ku, nb);
+            Gb.generate(sn::Gen::Random, 193);
+            std::vector<T> ga((size_t)nbd * nbd);
+            Gb.to_host(ga.data(), nbd);
+            // gbmm first (A unfactored): C = alpha A B + beta C
+            sn::Matrix<T> Bm(nbd, nrb, nb, p, q), Cm(nbd, nrb, nb, p, q);
+            Bm.generate(sn::Gen::Random, 194);
+            Cm.generate(sn::Gen::Random, 195);
+            std::vector<T> hb((size_t)nbd * nrb), hc((size_t)nbd * nrb), hc1((size_t)nbd * nrb);
+            Bm.to_host(hb.data(), nbd);
+            Cm.to_host(hc.data(), nbd);
+            const T al = val<T>(0.75, -0.5), be = val<T>(-1.5, 0.25);
+            sn::gbmm(al, Gb, Bm, be, Cm);
+            Cm.to_host(hc1.data(), nbd);
+            auto ab = mul<T>('N', 'N', nbd, nrb, nbd, ga, nbd, hb, nbd);
+            std::vector<std::complex<double>> d(ab.size()), w(ab.size());
+            for (size_t i = 0; i < ab.size(); ++i) {
+                w[i] = std::complex<double>(std::real(al), std::imag(al)) * ab[i] +
+                       std::complex<double>(std::real(be), std::imag(be)) *
+                           std::complex<double>(std::real(hc[i]), std::imag(hc[i]));
+                d[i] = std::complex<double>(std::real(hc1[i]), std::imag(hc1[i])) - w[i];
+            }
+            report("gbmm", rel<T>(d, w));
+            std::vector<int64_t> pv;
+            Bm.from_host(hb.data(), nbd);
+            const int64_t inf = sn::gbsv(Gb, pv, Bm);
+            std::vector<T> x((size_t)nbd * nrb);
+            Bm.to_host(x.data(), nbd);
+            // backward error ||A X - B|| / (||A|| ||X||): the random band is
+            // not diagonally dominant, so partial pivoting really pivots
+            {
+                auto ax = mul<T>('N', 'N', nbd, nrb, nbd, ga, nbd, x, nbd);
+                double e = 0, an = 0, xn = 0;
+                for (size_t i = 0; i < ax.size(); ++i)
+                    e += std::norm(ax[i] - std::complex<double>(std::real(hb[i]), std::imag(hb[i])));
+                for (const T& v : ga) an += std::norm(std::complex<double>(std::real(v), std::imag(v)));
+                for (const T& v : x) xn += std::norm(std::complex<double>(std::real(v), std::imag(v)));
+                report(inf ? "gbsv-FAILED" : "gbsv", std::sqrt(e / (an * xn)));
+            }
+        }
+        {
+            // hbmm Left / Right on the HPD band against the dense Hermitian product
+            sn::HermitianBandMatrix<T> Hb(sn::Uplo::Lower, nbd, kd, nb);
+            Hb.generate(sn::Gen::Random, 196);
+            std::vector<T> hl((size_t)nbd * nbd), hf((size_t)nbd * nbd);
+            Hb.to_host(hl.data(), nbd);
+            for (int64_t j = 0; j < nbd; ++j)
+                for (int64_t i = 0; i < nbd; ++i) {
+                    const T v = i >= j ? hl[i + j * nbd] : cj(hl[j + i * nbd]);
+                    hf[i + j * nbd] = i == j ? T(std::real(v)) : v;
+                }
+            Hb.from_host(hf.data(), nbd);                // real diagonal
+            for (int sd = 0; sd < 2; ++sd) {
+                const int64_t rm = sd ? nrb : nbd, rn = sd ? nbd : nrb;
+                sn::Matrix<T> Bm(rm, rn, nb, p, q), Cm(rm, rn, nb, p, q);
+                Bm.generate(sn::Gen::Random, 197);
+                std::vector<T> hb((size_t)rm * rn), hc((size_t)rm * rn);
+                Bm.to_host(hb.data(), rm);
+                sn::hbmm(sd ? sn::Side::Right : sn::Side::Left, T(1), Hb, Bm, T(0), Cm);
+                Cm.to_host(hc.data(), rm);
+                auto want = sd ? mul<T>('N', 'N', rm, rn, nbd, hb, rm, hf, nbd) : mul<T>('N', 'N', rm, rn, nbd, hf, nbd, hb, rm);
+                std::vector<std::complex<double>> d(want.size());
+                for (size_t i = 0; i < want.size(); ++i) d[i] = std::complex<double>(std::real(hc[i]), std::imag(hc[i])) - want[i];
+                report(sd ? "hbmm_right" : "hbmm_left", rel<T>(d, want));
+            }
+        }
+        {
+            // tbsm: upper triangular band, op = ConjTrans, alpha != 1
+            sn::TriangularBandMatrix<T> Tb(sn::Uplo::Upper, sn::Diag::NonUnit, nbd, kd, nb);
+            std::vector<T> ht((size_t)nbd * nbd, T(0));
+            for (int64_t j = 0; j < nbd; ++j)
+                for (int64_t i = std::max<int64_t>(0, j - kd); i <= j; ++i)
+                    ht[i + j * nbd] = i == j ? T(4.0 + 0.01 * j) : val<T>(std::sin(0.3 * i + 0.7 * j) * 0.05, 0.02);
+            Tb.from_host(ht.data(), nbd);
+            sn::Matrix<T> Bm(nbd, nrb, nb, p, q);
+            Bm.generate(sn::Gen::Random, 198);
+            std::vector<T> hb((size_t)nbd * nrb), x((size_t)nbd * nrb);
+            Bm.to_host(hb.data(), nbd);
+            const T al = val<T>(2.0, 0.0);
+            sn::tbsm(sn::Side::Left, sn::Op::ConjTrans, al, Tb, Bm);
+            Bm.to_host(x.data(), nbd);
+            auto tx = mul<T>('C', 'N', nbd, nrb, nbd, ht, nbd, x, nbd);
+            auto w = widen(hb);
+            for (size_t i = 0; i < tx.size(); ++i) {
+                w[i] *= 2.0;
+                tx[i] -= w[i];
+            }
+            report("tbsm_upper_conj", rel<T>(tx, w));
+        }
+    }
     // ---- matrix model: transposed views, structured types, slice, emptyLike
     {
         const int64_t ma = 170, ka = 90, na = 130;

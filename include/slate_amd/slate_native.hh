@@ -90,6 +90,8 @@ struct Options {
     int depth = 2;            // SLATE Option::Depth: butterfly levels of gesv_rbt (1..4)
     int max_iterations = 30;  // SLATE Option::MaxIterations: refinement / GMRES steps
     int restart = 30;         // GMRES restart length (gesv/posv_mixed_gmres)
+    int lu_method = 0;        // SLATE MethodLU: 0 partial pivoting, 1 CALU (tournament pivoting)
+    int calu_leaf = 2048;     // rows per first-round CALU play-off (>= 2 nb is enforced)
 };
 
 struct Storage;               // opaque: device buffer, grid, communicators
@@ -327,6 +329,12 @@ void lu_exchange_stats(long long* bytes, long long* rows);
 // referenced) and the triangular product A <- L^H L (Lower) / U U^H (Upper)
 template <typename T> int64_t trtri(Uplo uplo, Diag diag, Matrix<T>& A, const Options& opts = {});
 template <typename T> void trtrm(Uplo uplo, Matrix<T>& A, const Options& opts = {});
+// LU with tournament pivoting (SLATE getrf_tntpiv, MethodLU::CALU): every
+// panel's pivot rows are chosen by a play-off -- partial-pivoting LU of
+// row blocks, the winners of each block (on every rank of the panel's
+// process column) meet in the next round, the last round runs redundantly
+// on the column -- then the panel is factored without further pivoting.
+template <typename T> int64_t getrf_tntpiv(Matrix<T>& A, std::vector<int64_t>& ipiv, const Options& opts = {});
 // LU without pivoting (SLATE getrf_nopiv / gesv_nopiv): unit-lower L and U in A
 template <typename T> int64_t getrf_nopiv(Matrix<T>& A, const Options& opts = {});
 template <typename T> int64_t gesv_nopiv(Matrix<T>& A, Matrix<T>& B, const Options& opts = {});
@@ -437,6 +445,91 @@ void syr2k(T alpha, const Matrix<T>& A, const Matrix<T>& B, T beta, SymmetricMat
 template <typename T>
 void her2k(T alpha, const Matrix<T>& A, const Matrix<T>& B, real_t<T> beta, HermitianMatrix<T>& C,
            const Options& opts = {});
+
+// ---- band matrices (SLATE BandMatrix / HermitianBandMatrix /
+// TriangularBandMatrix, include/slate/BandMatrix.hh; drivers slate.hh gbtrf /
+// gbtrs / gbsv :568, pbtrf / pbtrs / pbsv :708, tbsm :304, gbmm :179,
+// hbmm :215).  Compact storage: tile columns are dealt 1-D cyclically over
+// ALL ranks (column tile k on rank k % size) and each local tile column is
+// ONE contiguous device slab of its band tiles, (klt + kut + 1) nb rows --
+// memory O(n (kl + ku)) per job, never the dense n x n.  A factorization
+// step is one panel on its owner (GPU potrf + trsm, or the persistent LU
+// panel over the kb + kl rows that can be non-zero), one broadcast of the
+// panel (and pivots), then every rank updates its own tile columns inside
+// the band window with one MFMA GEMM each.  Solves and products keep the
+// dense operand replicated on every rank (host-staged, O(n nrhs)), which
+// is what band problems with few right-hand sides need.
+struct BandStorage;
+template <typename T>
+class BandMatrix {
+public:
+    BandMatrix() = default;
+    // m x n, lower / upper bandwidths kl / ku, nb x nb tiles
+    BandMatrix(int64_t m, int64_t n, int64_t kl, int64_t ku, int64_t nb);
+    int64_t m() const;
+    int64_t n() const;
+    int64_t nb() const;
+    int64_t lower_bandwidth() const;
+    int64_t upper_bandwidth() const;
+    // the band of a dense column-major host array (identical on every
+    // rank); to_host writes the band (zeros elsewhere) on every rank
+    void from_host(const T* A, int64_t lda);
+    void to_host(T* A, int64_t lda) const;
+    // Philox entries of the band (Gen kinds as Matrix::generate)
+    void generate(Gen kind, uint64_t seed);
+    std::shared_ptr<BandStorage> storage() const { return s_; }
+
+protected:
+    std::shared_ptr<BandStorage> s_;
+    BandMatrix(int64_t m, int64_t n, int64_t kl, int64_t ku, int64_t nb, int64_t ku_alloc);
+};
+// Hermitian band: the uplo triangle of bandwidth kd (stored as the lower
+// band; an Upper matrix is read / written as its conjugate transpose)
+template <typename T>
+class HermitianBandMatrix : public BandMatrix<T> {
+public:
+    HermitianBandMatrix() = default;
+    HermitianBandMatrix(Uplo uplo, int64_t n, int64_t kd, int64_t nb);
+    Uplo uplo() const { return uplo_; }
+    int64_t kd() const { return this->lower_bandwidth(); }
+    void from_host(const T* A, int64_t lda);
+    void to_host(T* A, int64_t lda) const;
+
+private:
+    Uplo uplo_ = Uplo::Lower;
+};
+template <typename T>
+class TriangularBandMatrix : public BandMatrix<T> {
+public:
+    TriangularBandMatrix() = default;
+    TriangularBandMatrix(Uplo uplo, Diag diag, int64_t n, int64_t kd, int64_t nb);
+    Uplo uplo() const { return uplo_; }
+    Diag diag() const { return diag_; }
+
+private:
+    Uplo uplo_ = Uplo::Lower;
+    Diag diag_ = Diag::NonUnit;
+};
+// band LU with partial pivoting: ipiv global 0-based (LAPACK gbtrf order);
+// the upper bandwidth grows to kl + ku (allocated by the constructor)
+template <typename T> int64_t gbtrf(BandMatrix<T>& A, std::vector<int64_t>& ipiv, const Options& opts = {});
+template <typename T>
+int64_t gbtrs(const BandMatrix<T>& A, const std::vector<int64_t>& ipiv, Matrix<T>& B, const Options& opts = {});
+template <typename T>
+int64_t gbsv(BandMatrix<T>& A, std::vector<int64_t>& ipiv, Matrix<T>& B, const Options& opts = {});
+// band Cholesky A = L L^H (Upper: U^H U)
+template <typename T> int64_t pbtrf(HermitianBandMatrix<T>& A, const Options& opts = {});
+template <typename T> int64_t pbtrs(const HermitianBandMatrix<T>& A, Matrix<T>& B, const Options& opts = {});
+template <typename T> int64_t pbsv(HermitianBandMatrix<T>& A, Matrix<T>& B, const Options& opts = {});
+// B = alpha op(A)^-1 B (Side::Left; op NoTrans or ConjTrans)
+template <typename T>
+void tbsm(Side side, Op op, T alpha, const TriangularBandMatrix<T>& A, Matrix<T>& B, const Options& opts = {});
+// C = alpha A B + beta C (band A); hbmm: A Hermitian band, Left or Right
+template <typename T>
+void gbmm(T alpha, const BandMatrix<T>& A, const Matrix<T>& B, T beta, Matrix<T>& C, const Options& opts = {});
+template <typename T>
+void hbmm(Side side, T alpha, const HermitianBandMatrix<T>& A, const Matrix<T>& B, T beta, Matrix<T>& C,
+          const Options& opts = {});
 
 struct QRData;
 template <typename T>

@@ -132,7 +132,9 @@ def _assert_checks(checks, out):
                                                    "svd_values", "gesv_rbt", "hegv1", "hegv2_upper", "hegv3",
                                                    "view_gemm", "view_dims", "view_norm", "view_rejected",
                                                    "tri_view_uplo", "tri_view_trsm", "trapezoid_norm",
-                                                   "slice_roundtrip", "empty_like", "sym_syrk_symm")]
+                                                   "slice_roundtrip", "empty_like", "sym_syrk_symm",
+                                                   "pbsv", "pbsv_upper", "gbmm", "gbsv", "hbmm_left", "hbmm_right",
+                                                   "tbsm_upper_conj")]
     for name in names:
         assert name in checks, (name, out)
         assert float(checks[name]) < TOL[name[-1]], (name, checks[name])
