@@ -412,10 +412,19 @@ int64_t posv_mixed_gmres(HermitianMatrix<T>& A, Matrix<T>& B, Matrix<T>& X, int&
 // transformed (and, when n is not a multiple of the butterfly unit, padded)
 // matrix only if n already is that multiple -- otherwise A is unchanged
 template <typename T> int64_t gesv_rbt(Matrix<T>& A, Matrix<T>& B, const Options& opts = {});
-// Hermitian indefinite solve (slate.hh hesv): A X = B for the Hermitian A of
-// the stored triangle, B <- X.  Here the full Hermitian matrix is solved by
-// LU with partial pivoting (A receives those factors); the communication-
-// avoiding Aasen hetrf of the Python package is not native yet.
+// Hermitian indefinite factorization (slate.hh hetrf :804, hetrs, hesv):
+// blocked left-looking Aasen, P A P^H = L T L^H with T Hermitian block
+// tridiagonal (bandwidth nb), T then factored by the band LU (gbtrf).  The
+// factorization runs on the device of every rank over the gathered matrix
+// (the distributed Aasen is the Python package's hetrf_dist); T's band LU
+// and the solves use the native band drivers.  F keeps L, P and T's LU.
+struct IndefData;
+template <typename T>
+struct IndefiniteFactors {
+    std::shared_ptr<IndefData> d;
+};
+template <typename T> int64_t hetrf(const HermitianMatrix<T>& A, IndefiniteFactors<T>& F, const Options& opts = {});
+template <typename T> int64_t hetrs(const IndefiniteFactors<T>& F, Matrix<T>& B, const Options& opts = {});
 template <typename T> int64_t hesv(HermitianMatrix<T>& A, Matrix<T>& B, const Options& opts = {});
 // A <- (numer / denom) A (slate.hh scale), computed without forming the ratio
 // when it would overflow
@@ -477,6 +486,9 @@ public:
     void to_host(T* A, int64_t lda) const;
     // Philox entries of the band (Gen kinds as Matrix::generate)
     void generate(Gen kind, uint64_t seed);
+    // LAPACK band layout (gbtrf's AB): A(i, j) = AB(ldab_off + i - j, j),
+    // ldab_off = ku (or any larger offset), every rank the same host array
+    void from_host_band(const T* AB, int64_t ldab, int64_t ldab_off);
     std::shared_ptr<BandStorage> storage() const { return s_; }
 
 protected:

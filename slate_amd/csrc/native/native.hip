@@ -1350,6 +1350,184 @@ void lu_exchange_stats(long long* bytes, long long* rows) {
     if (rows) *rows = g_lu_xchg_rows.exchange(0);
 }
 
+// ------------------------------------------------------------ CALU (tournament pivoting)
+// Reference: src/getrf_tntpiv.cc, src/internal/internal_getrf_tntpiv.cc
+// (Grigori, Demmel, Xiang).  The play-offs are the persistent partial-
+// pivoting LU panel on row blocks; the winners' ORIGINAL rows meet in the
+// next round (device row gathers), the winners of the last round, in its
+// pivot order, become the panel's LAPACK-style interchanges.
+
+// one play-off: partial-pivoting LU of a copy of the R x w rows A (ld lda);
+// the min(R, kb) winners (row indices into A) in pivot order; with keep the
+// factored copy (ld R, rows permuted) stays in *keep
+template <typename T>
+static std::vector<i64> calu_playoff(i64 R, i64 w, i64 kb, const T* A, i64 lda, double thr, i64* info_d,
+                                     std::unique_ptr<Scratch>* keep, hipStream_t s) {
+    const i64 c = std::min(R, kb);
+    auto W = std::make_unique<Scratch>(sizeof(T) * std::max<i64>(R, 1) * w, s);
+    copy2d(W->as<T>(), R, A, lda, R, w, s);
+    Scratch lp(sizeof(i64) * std::max<i64>(c, 1), s);
+    NHIP(hipMemsetAsync(lp.p, 0, sizeof(i64) * std::max<i64>(c, 1), s));
+    slate_hip::getrf_panel_ws<K<T>>(R, std::min(w, kb), kp(W->as<T>()), R, lp.as<i64>(), info_d, thr, false,
+                                    rt().lu_work, s);
+    std::vector<i64> h((size_t)std::max<i64>(c, 1));
+    NHIP(hipMemcpyAsync(h.data(), lp.p, sizeof(i64) * h.size(), hipMemcpyDeviceToHost, s));
+    NHIP(hipStreamSynchronize(s));
+    std::vector<i64> idx((size_t)R);
+    for (i64 i = 0; i < R; ++i) idx[i] = i;
+    for (i64 i = 0; i < c; ++i) std::swap(idx[i], idx[h[i]]);
+    idx.resize((size_t)c);
+    if (keep) *keep = std::move(W);
+    return idx;
+}
+
+// rows sel (into A, ld lda) gathered into a new |sel| x w block
+template <typename T>
+static std::unique_ptr<Scratch> calu_gather(const std::vector<i64>& sel, i64 w, const T* A, i64 lda, hipStream_t s) {
+    const i64 r = (i64)sel.size();
+    auto C = std::make_unique<Scratch>(sizeof(T) * std::max<i64>(r, 1) * w, s);
+    Scratch pd(sizeof(i64) * std::max<i64>(r, 1), s);
+    upload(pd.p, sel.data(), sizeof(i64) * r, s);
+    slate_hip::permute_rows_gather<K<T>>(r, w, kp(A), lda, kp(C->as<T>()), r, pd.as<i64>(), s);
+    NHIP(hipStreamSynchronize(s));
+    return C;
+}
+
+// local tournament over the R rows of A: at most kb nominees (indices into
+// A); every round plays blocks of `leaf` (>= 2 kb) rows
+template <typename T>
+static std::vector<i64> calu_local(i64 R, i64 w, i64 kb, const T* A, i64 lda, double thr, i64 leaf, i64* info_d,
+                                   hipStream_t s) {
+    std::vector<i64> cand;
+    for (i64 a = 0; a < R; a += leaf) {
+        const i64 r = std::min(leaf, R - a);
+        for (i64 i : calu_playoff<T>(r, w, kb, A + a, lda, thr, info_d, nullptr, s)) cand.push_back(a + i);
+    }
+    while ((i64)cand.size() > kb) {
+        std::vector<i64> next;
+        for (size_t g = 0; g < cand.size(); g += (size_t)leaf) {
+            const size_t e = std::min(cand.size(), g + (size_t)leaf);
+            std::vector<i64> grp(cand.begin() + g, cand.begin() + e);
+            auto C = calu_gather<T>(grp, w, A, lda, s);
+            for (i64 i : calu_playoff<T>((i64)grp.size(), w, kb, C->template as<T>(), (i64)grp.size(), thr, info_d, nullptr, s))
+                next.push_back(grp[i]);
+        }
+        cand.swap(next);
+    }
+    return cand;
+}
+
+// selected rows (pivot order, panel-relative) -> LAPACK sequential interchanges
+static std::vector<i64> calu_ipiv(const std::vector<i64>& sel, i64 mk) {
+    std::vector<i64> at((size_t)mk), pos((size_t)mk), piv(sel.size());
+    for (i64 i = 0; i < mk; ++i) at[i] = pos[i] = i;
+    for (size_t i = 0; i < sel.size(); ++i) {
+        const i64 p = pos[sel[i]];
+        piv[i] = p;
+        const i64 ri = at[i], rp = at[p];
+        std::swap(at[i], at[p]);
+        pos[ri] = p;
+        pos[rp] = (i64)i;
+    }
+    return piv;
+}
+
+// 1 x q: the panel (mk x wk at A) on one rank
+template <typename T>
+static void calu_panel_1(i64 mk, i64 wk, T* A, i64 lda, i64* piv_d, i64* info, double thr, i64 leaf, hipStream_t s) {
+    const i64 kb = std::min(mk, wk);
+    Scratch dinfo(sizeof(i64), s);
+    NHIP(hipMemsetAsync(dinfo.p, 0, sizeof(i64), s));
+    std::vector<i64> sel = calu_local<T>(mk, wk, kb, A, lda, thr, std::max<i64>(leaf, 2 * kb), dinfo.as<i64>(), s);
+    if ((i64)sel.size() > kb) sel.resize((size_t)kb);
+    const std::vector<i64> piv = calu_ipiv(sel, mk);
+    upload(piv_d, piv.data(), sizeof(i64) * piv.size(), s);
+    slate_hip::laswp_off<K<T>>(wk, kp(A), lda, 0, (i64)piv.size(), piv_d, 0, s);
+    Scratch np(sizeof(i64) * std::max<i64>(kb, 1), s);
+    slate_hip::getrf_panel_ws<K<T>>(mk, wk, kp(A), lda, np.as<i64>(), info, thr, true, rt().lu_work, s);
+}
+
+// p > 1: local play-offs on every rank of the panel's process column, ONE
+// all-gather of the (<= kb) nominees per rank, the final round redundantly
+// on the column; then the exact row exchange of the panel columns, U11 / L11
+// from the final round, L21 = A21 U11^-1 (same outputs as panel_dist)
+template <typename T>
+static void calu_panel_dist(Storage& S, i64 k, i64 kb, i64 lck, i64* ipiv_d, i64* info, double thr, i64 leaf, T* Tt,
+                            hipStream_t s) {
+    const int p = S.p, pr = S.pr;
+    const i64 nb = S.nb, r0 = k * nb;
+    const int rk = (int)(k % p);
+    const i64 lr_k = std::min(tiles_before(k, p, pr) * nb, S.mloc);
+    const i64 nmine = S.mloc - lr_k;
+    T* buf = static_cast<T*>(S.buf);
+    T* W = buf + lr_k + lck * S.lld;
+    Comm* colc = S.gc->col.get();
+    Scratch dinfo(sizeof(i64), s);
+    NHIP(hipMemsetAsync(dinfo.p, 0, sizeof(i64), s));
+    std::vector<i64> loc;
+    if (nmine) loc = calu_local<T>(nmine, kb, kb, W, S.lld, thr, std::max<i64>(leaf, 2 * kb), dinfo.as<i64>(), s);
+    // pack: kb x kb nominee rows (ld kb) + kb panel-relative global row ids (-1: none)
+    const size_t rb = sizeof(T) * kb * kb, ib = sizeof(i64) * kb, pkb = rb + ib;
+    Scratch pk(pkb, s), all(pkb * p, s);
+    NHIP(hipMemsetAsync(pk.p, 0, pkb, s));
+    std::vector<i64> gid((size_t)kb, -1);
+    for (size_t i = 0; i < loc.size(); ++i) gid[i] = l2g(lr_k + loc[i], nb, p, pr) - r0;
+    if (!loc.empty()) {
+        auto C = calu_gather<T>(loc, kb, W, S.lld, s);
+        copy2d(pk.as<T>(), kb, C->template as<T>(), (i64)loc.size(), (i64)loc.size(), kb, s);
+    }
+    upload(static_cast<char*>(pk.p) + rb, gid.data(), ib, s);
+    colc->allgather(pk.p, all.p, pkb, s);
+    std::vector<i64> gall((size_t)kb * p);
+    for (int r = 0; r < p; ++r)
+        NHIP(hipMemcpyAsync(gall.data() + (size_t)r * kb, static_cast<char*>(all.p) + pkb * r + rb, ib,
+                            hipMemcpyDeviceToHost, s));
+    NHIP(hipStreamSynchronize(s));
+    // the stack of every rank's nominees, in rank order
+    std::vector<i64> sg;
+    i64 tot = 0;
+    for (int r = 0; r < p; ++r)
+        for (i64 i = 0; i < kb; ++i)
+            if (gall[(size_t)r * kb + i] >= 0) ++tot;
+    Scratch stk(sizeof(T) * std::max<i64>(tot, 1) * kb, s);
+    i64 o = 0;
+    for (int r = 0; r < p; ++r) {
+        i64 c = 0;
+        while (c < kb && gall[(size_t)r * kb + c] >= 0) ++c;
+        copy2d(stk.as<T>() + o, tot, reinterpret_cast<T*>(static_cast<char*>(all.p) + pkb * r), kb, c, kb, s);
+        for (i64 i = 0; i < c; ++i) sg.push_back(gall[(size_t)r * kb + i]);
+        o += c;
+    }
+    std::unique_ptr<Scratch> F;
+    const std::vector<i64> win = calu_playoff<T>(tot, kb, kb, stk.as<T>(), tot, thr, info, &F, s);
+    std::vector<i64> sel;
+    for (i64 i : win) sel.push_back(sg[i]);
+    const std::vector<i64> piv = calu_ipiv(sel, S.m - r0);
+    upload(ipiv_d + r0, piv.data(), sizeof(i64) * piv.size(), s);
+    // LU11 (the final round's top kb rows) -> Tt
+    copy2d(Tt, kb, F->as<T>(), tot, kb, kb, s);
+    // the winners into the panel's top rows (owner-masked all-reduce exchange)
+    Scratch plan(slate_hip::swap_plan_bytes(), s);
+    slate_hip::swap_plan(r0, r0 + kb, ipiv_d, -r0, 1, plan.p, s);
+    const i64 S2 = 2 * kb;
+    Scratch X((size_t)S2 * kb * sizeof(T), s);
+    T* cols = buf + lck * S.lld;
+    slate_hip::xchg_gather<K<T>>(plan.p, S2, kb, kp(cols), S.lld, kp(X.as<T>()), S2, nb, p, pr, s);
+    colc->allreduce(X.p, (size_t)S2 * kb, dt_of<T>::v, 's', s);
+    slate_hip::xchg_scatter<K<T>>(plan.p, S2, kb, kp(X.as<T>()), S2, kp(cols), S.lld, nb, p, pr, s);
+    if (pr == rk) copy2d(W, S.lld, Tt, kb, kb, kb, s);
+    const i64 i0 = pr == rk ? kb : 0;
+    if (nmine > i0)
+        slate_hip::trsm<K<T>>('R', 'U', 'N', 'N', nmine - i0, kb, kv(T(1)), kp(Tt), kb, kp(W + i0), S.lld, s);
+}
+
+template <typename T>
+int64_t getrf_tntpiv(Matrix<T>& A, std::vector<int64_t>& ipiv, const Options& opts) {
+    Options o = opts;
+    o.lu_method = 1;
+    return getrf<T>(A, ipiv, o);
+}
+
 template <typename T>
 int64_t getrf(Matrix<T>& A, std::vector<int64_t>& ipiv_out, const Options& opts) {
     NTRACE("getrf", nullptr);
@@ -1406,8 +1584,12 @@ int64_t getrf(Matrix<T>& A, std::vector<int64_t>& ipiv_out, const Options& opts)
             std::unique_ptr<trace_rt::Scope> sp_panel(trace_rt::g_on ? new trace_rt::Scope("getrf::panel", ps) : nullptr);
             if (own) {
                 const i64 wk = std::min(nb, n - r0);
-                slate_hip::getrf_panel_ws<K<T>>(mk, wk, kp(buf + r0 + lck * lld), lld, ipiv_d + r0,
-                                                infos.as<i64>() + k, opts.pivot_threshold, false, R.lu_work, ps);
+                if (opts.lu_method == 1)
+                    calu_panel_1<T>(mk, wk, buf + r0 + lck * lld, lld, ipiv_d + r0, infos.as<i64>() + k,
+                                    opts.pivot_threshold, opts.calu_leaf, ps);
+                else
+                    slate_hip::getrf_panel_ws<K<T>>(mk, wk, kp(buf + r0 + lck * lld), lld, ipiv_d + r0,
+                                                    infos.as<i64>() + k, opts.pivot_threshold, false, R.lu_work, ps);
                 Lp = buf + r0 + lck * lld;
                 ldl = lld;
                 if (q > 1) copy2d(Lb, mk, Lp, lld, mk, kb, ps);
@@ -1482,8 +1664,12 @@ int64_t getrf(Matrix<T>& A, std::vector<int64_t>& ipiv_out, const Options& opts)
             i64* pv = reinterpret_cast<i64*>(static_cast<char*>(pack.p) + lbytes + tbytes);
             std::unique_ptr<trace_rt::Scope> sp_panel(trace_rt::g_on ? new trace_rt::Scope("getrf::panel", ps) : nullptr);
             if (pc == ck) {
-                panel_dist<T>(S, k, kb, lck, ipiv_d, infos.as<i64>() + k, opts.pivot_threshold,
-                              opts.inner_blocking, Tt, gall.as<i64>() + goff[k], ps);
+                if (opts.lu_method == 1)
+                    calu_panel_dist<T>(S, k, kb, lck, ipiv_d, infos.as<i64>() + k, opts.pivot_threshold,
+                                       opts.calu_leaf, Tt, ps);
+                else
+                    panel_dist<T>(S, k, kb, lck, ipiv_d, infos.as<i64>() + k, opts.pivot_threshold,
+                                  opts.inner_blocking, Tt, gall.as<i64>() + goff[k], ps);
                 copy2d(Lp, std::max<i64>(nmine, 1), buf + lr_k + lck * lld, lld, nmine, kb, ps);
                 dcopy(pv, ipiv_d + r0, (size_t)kb * sizeof(i64), ps);
             }
@@ -2744,6 +2930,7 @@ int64_t gels(Matrix<T>& A, Matrix<T>& BX, const Options& opts) {
     template int64_t trtri<T>(Uplo, Diag, Matrix<T>&, const Options&);                                        \
     template void trtrm<T>(Uplo, Matrix<T>&, const Options&);                                                 \
     template int64_t getrf_nopiv<T>(Matrix<T>&, const Options&);                                              \
+    template int64_t getrf_tntpiv<T>(Matrix<T>&, std::vector<int64_t>&, const Options&);                      \
     template int64_t gesv_nopiv<T>(Matrix<T>&, Matrix<T>&, const Options&);                                   \
     template int64_t cholqr<T>(Matrix<T>&, Matrix<T>&, const Options&);                                       \
     template int64_t gelqf<T>(Matrix<T>&, LQFactors<T>&, const Options&);                                     \

@@ -482,7 +482,7 @@ def _rows_global(lr0, lr1, nb, p, pr, r0, dev):
 
 
 def _getrf_general(A, buf, thr, la, mode, leaf):
-    """p x q grid, host-synchronisation free, with lookahead.
+    """p x q grid with lookahead; the host waits only for pivots (see below).
 
     step k (panel column k, owned by process column ck = k % q):
       panel stream (high priority):
@@ -509,10 +509,16 @@ def _getrf_general(A, buf, thr, la, mode, leaf):
         rows that change process row (_p2p_rows), the U row then goes down
         the column in one broadcast (SLATE internal::permuteRows +
         tileBcast, getrf.cc:155-215).  Its plan needs the pivots on the
-        host: they travel through a pinned buffer and are read one step
-        late, when the panel that produced them has finished, so the host
-        never waits on the critical path.  The left columns' interchanges
-        are applied once, after the loop, in step order."""
+        host (RCCL point-to-point sizes are host arguments): they travel
+        through a pinned buffer and are read one step late -- the host
+        blocks on the PREVIOUS step's panel event (``_moves_of``) while the
+        GPU still holds this step's panel, lookahead update and the previous
+        bulk update in its queues, so the wait costs host run-ahead (at most
+        one step), not GPU time.  A device-planned alternative exists for
+        the lookahead columns (the owner-masked all-reduce above); for the
+        bulk it moves 2 kb rows x every local column per step instead of
+        only the rows that change process row.  The left columns'
+        interchanges are applied once, after the loop, in step order."""
     s = A.storage
     bc = s.bc
     grid = grid_of(A)
