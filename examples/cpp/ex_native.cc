@@ -790,6 +790,61 @@ void run(int p, int q, int me) {
         for (size_t i = 0; i < ax.size(); ++i) ax[i] -= want[i];
         report(inf ? "gesv_rbt-FAILED" : "gesv_rbt", rel<T>(ax, want));
     }
+    // ---- Hermitian indefinite (Aasen hetrf + band LU of T): hesv backward error
+    {
+        const int64_t nh = 230;                  // not a multiple of nb: the padded order
+        sn::HermitianMatrix<T> Hm(sn::Uplo::Lower, nh, nb, p, q);
+        Hm.generate(sn::Gen::Random, 205);
+        std::vector<T> ha((size_t)nh * nh);
+        Hm.to_host(ha.data(), nh);
+        for (int64_t j = 0; j < nh; ++j) {
+            ha[j + j * nh] = T(std::real(ha[j + j * nh]));
+            for (int64_t i = 0; i < j; ++i) ha[i + j * nh] = cj(ha[j + i * nh]);
+        }
+        sn::Matrix<T> Bm(nh, nrhs, nb, p, q);
+        Bm.generate(sn::Gen::Random, 206);
+        std::vector<T> hb((size_t)nh * nrhs), x((size_t)nh * nrhs);
+        Bm.to_host(hb.data(), nh);
+        const int64_t inf = sn::hesv(Hm, Bm);
+        Bm.to_host(x.data(), nh);
+        auto ax = mul<T>('N', 'N', nh, nrhs, nh, ha, nh, x, nh);
+        double e = 0, an = 0, xn = 0;
+        for (size_t i = 0; i < ax.size(); ++i) e += std::norm(ax[i] - std::complex<double>(std::real(hb[i]), std::imag(hb[i])));
+        for (const T& v : ha) an += std::norm(std::complex<double>(std::real(v), std::imag(v)));
+        for (const T& v : x) xn += std::norm(std::complex<double>(std::real(v), std::imag(v)));
+        report(inf ? "hesv-FAILED" : "hesv", std::sqrt(e / (an * xn)));
+    }
+    // ---- CALU (getrf_tntpiv): || P A - L U || / || A || from the host factors,
+    //      with a small play-off leaf so several rounds run
+    {
+        const int64_t nc = 260;
+        sn::Matrix<T> Gm(nc, nc, nb, p, q);
+        Gm.generate(sn::Gen::Random, 201);
+        std::vector<T> g0((size_t)nc * nc), lu((size_t)nc * nc);
+        Gm.to_host(g0.data(), nc);
+        std::vector<int64_t> pv;
+        sn::Options o;
+        o.calu_leaf = 64;
+        const int64_t inf = sn::getrf_tntpiv(Gm, pv, o);
+        Gm.to_host(lu.data(), nc);
+        std::vector<T> L((size_t)nc * nc, T(0)), U((size_t)nc * nc, T(0)), PA(g0);
+        for (int64_t j = 0; j < nc; ++j)
+            for (int64_t i = 0; i < nc; ++i) {
+                if (i > j) L[i + j * nc] = lu[i + j * nc];
+                else U[i + j * nc] = lu[i + j * nc];
+                if (i == j) L[i + j * nc] = T(1);
+            }
+        for (int64_t i = 0; i < nc; ++i)
+            if (pv[i] != i)
+                for (int64_t j = 0; j < nc; ++j) std::swap(PA[i + j * nc], PA[pv[i] + j * nc]);
+        auto lu2 = mul<T>('N', 'N', nc, nc, nc, L, nc, U, nc);
+        auto w = widen(PA);
+        for (size_t i = 0; i < lu2.size(); ++i) lu2[i] -= w[i];
+        double lmax = 0;
+        for (const T& v : L) lmax = std::max(lmax, (double)std::abs(v));
+        report(inf ? "getrf_tntpiv-FAILED" : "getrf_tntpiv", rel<T>(lu2, w));
+        report("tntpiv_growth", lmax <= 64.0 ? 0.0 : lmax);     // tournament pivots keep |L| modest
+    }
     // ---- band matrices (compact 1-D column-tile storage): pbsv (Lower and
     //      Upper), gbsv, tbsm, gbmm, hbmm against dense host products
     {

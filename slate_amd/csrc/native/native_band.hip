@@ -214,6 +214,10 @@ void BandMatrix<T>::from_host(const T* A, int64_t lda) {
     fill_slabs<T>(*s_, [&](i64 i, i64 j) { return A[i + j * lda]; });
 }
 template <typename T>
+void BandMatrix<T>::from_host_band(const T* AB, int64_t ldab, int64_t off) {
+    fill_slabs<T>(*s_, [&](i64 i, i64 j) { return AB[(off + i - j) + j * ldab]; });
+}
+template <typename T>
 void BandMatrix<T>::to_host(T* A, int64_t lda) const {
     const BandStorage& S = *s_;
     gather_slabs<T>(S, A, lda, S.m, S.n, [&](std::vector<T>& f, i64 i, i64 j, T v) { f[(size_t)(i + j * S.m)] = v; });

@@ -523,12 +523,227 @@ int64_t gesv_rbt(Matrix<T>& A, Matrix<T>& B, const Options& opts) {
 }
 
 // ------------------------------------------------------------ hesv / scale
+// ------------------------------------------------------------ Aasen (hetrf / hetrs / hesv)
+// Reference: src/hetrf.cc (communication-avoiding blocked Aasen, host only
+// in the reference: "GPU version not yet implemented", hetrf.cc:23), the
+// band T factored by gbtrf (hetrf.cc:511), src/hetrs.cc:94-105.  Python twin:
+// models/hetrf.py aasen().  Step J (block column j0:j1, H = T L^H):
+//   H(0:J, J)  three strided-BATCHED MFMA GEMMs over the block tridiagonal T;
+//   T(J, J)    = L(J,J)^-1 (A(J,J) - L(J,0:J) H(0:J,J) - L(J,J) T(J,J-1)
+//                L(J,J-1)^H) L(J,J)^-H, symmetrised;
+//   panel      = A(j1:, J) - L(j1:, 0:j1) H(0:j1, J), GPU partial-pivoting
+//                LU -> L(j1:, J+1), T(J+1, J) = U L(J,J)^-H;
+//   symmetric interchange of the trailing A (row swaps, conjugate
+//   transpose, row swaps).
+struct IndefData {
+    i64 n = 0, N = 0, nb = 0;
+    char dtype = 0;
+    std::shared_ptr<void> L;        // Scratch: N x N unit lower (first block column [I; 0])
+    std::vector<i64> perm;          // row i of P A is row perm[i] of A
+    std::shared_ptr<void> Tband;    // BandMatrix<T>: gbtrf factors of T
+    std::vector<int64_t> Tpiv;
+    int p = 1, q = 1;
+};
+
+namespace {
+
+template <typename T>
+void gemm_batched(char ta, char tb, i64 m, i64 n, i64 k, T alpha, const T* A, i64 lda, i64 sa, const T* B, i64 ldb,
+                  i64 sb, T beta, T* C, i64 ldc, i64 sc, i64 batch, hipStream_t s) {
+    if (m <= 0 || n <= 0 || batch <= 0) return;
+    slate_hip::GemmCall c;
+    c.transA = ta; c.transB = tb; c.m = m; c.n = n; c.k = k;
+    c.alpha_re = (double)std::real(alpha); c.alpha_im = (double)std::imag(alpha);
+    c.beta_re = (double)std::real(beta); c.beta_im = (double)std::imag(beta);
+    c.A = A; c.lda = lda; c.strideA = sa; c.B = B; c.ldb = ldb; c.strideB = sb;
+    c.C = C; c.ldc = ldc; c.strideC = sc; c.batch = batch;
+    if constexpr (is_cplx<T>()) slate_hip::gemm_complex<K<T>>(c, s);
+    else slate_hip::gemm_real<T>(c, s);
+}
+
+template <typename T>
+void aasen(i64 N, i64 nb, T* Af, T* L, T* Td, T* Tl, i64* piv_rel, i64* info, hipStream_t s) {
+    const i64 NT = N / nb;
+    const char ct = ctrans<T>();
+    Scratch Xs(sizeof(T) * N * nb, s), Hs(sizeof(T) * N * nb, s), S(sizeof(T) * nb * nb, s),
+        tmp(sizeof(T) * nb * nb, s), Wt(sizeof(T) * N * N, s);
+    T* xs = Xs.as<T>();
+    T* hs = Hs.as<T>();
+    T* sm = S.as<T>();
+    T* tp = tmp.as<T>();
+    NHIP(hipMemsetAsync(xs, 0, sizeof(T) * N * nb, s));
+    NHIP(hipMemsetAsync(hs, 0, sizeof(T) * N * nb, s));
+    auto td = [&](i64 I) { return Td + I * nb * nb; };
+    auto tl = [&](i64 I) { return Tl + I * nb * nb; };
+    for (i64 J = 0; J < NT; ++J) {
+        const i64 j0 = J * nb, j1 = j0 + nb;
+        // X = L(J, 0:J+1)^H, then H(I, J) = Td[I] X[I] + Tl[I] X[I-1] + Tl[I+1]^H X[I+1], I < J
+        slate_hip::gecopy<K<T>, K<T>>('G', 'C', j1, nb, kp(L + j0), N, kp(xs), N, s);
+        if (J > 0) {
+            gemm_batched<T>('N', 'N', nb, nb, nb, T(1), td(0), nb, nb * nb, xs, N, nb, T(0), hs, N, nb, J, s);
+            if (J > 1)
+                gemm_batched<T>('N', 'N', nb, nb, nb, T(1), tl(1), nb, nb * nb, xs, N, nb, T(1), hs + nb, N, nb, J - 1, s);
+            gemm_batched<T>(ct, 'N', nb, nb, nb, T(1), tl(1), nb, nb * nb, xs + nb, N, nb, T(1), hs, N, nb, J, s);
+        }
+        // T(J, J)
+        copy2d(sm, nb, Af + j0 + j0 * N, N, nb, nb, s);
+        const T* Ljj = L + j0 + j0 * N;
+        if (J > 0) {
+            gemm_k<T>('N', 'N', nb, nb, j0, T(-1), L + j0, N, hs, N, T(1), sm, nb, s);
+            gemm_k<T>('N', 'N', nb, nb, nb, T(1), tl(J), nb, xs + j0 - nb, N, T(0), tp, nb, s);
+            gemm_k<T>('N', 'N', nb, nb, nb, T(-1), Ljj, N, tp, nb, T(1), sm, nb, s);
+            slate_hip::trsm<K<T>>('L', 'L', 'N', 'U', nb, nb, kv(T(1)), kp(Ljj), N, kp(sm), nb, s);
+            slate_hip::trsm<K<T>>('R', 'L', ct, 'U', nb, nb, kv(T(1)), kp(Ljj), N, kp(sm), nb, s);
+        }
+        slate_hip::gecopy<K<T>, K<T>>('G', 'C', nb, nb, kp(sm), nb, kp(tp), nb, s);
+        slate_hip::geadd<K<T>>('G', nb, nb, kv(T(0.5)), kp(tp), nb, kv(T(0.5)), kp(sm), nb, s);
+        copy2d(td(J), nb, sm, nb, nb, nb, s);
+        gemm_k<T>('N', 'N', nb, nb, nb, T(1), sm, nb, xs + j0, N, T(0), hs + j0, N, s);
+        if (J > 0) gemm_k<T>('N', 'N', nb, nb, nb, T(1), tl(J), nb, xs + j0 - nb, N, T(1), hs + j0, N, s);
+        if (J == NT - 1) break;
+        // panel: A(j1:, J) -= L(j1:, 0:j1) H(0:j1, J), LU with partial pivoting
+        T* Wp = Af + j1 + j0 * N;
+        const i64 mp = N - j1;
+        gemm_k<T>('N', 'N', mp, nb, j1, T(-1), L + j1, N, hs, N, T(1), Wp, N, s);
+        i64* piv = piv_rel + j1;
+        slate_hip::getrf_panel_ws<K<T>>(mp, nb, kp(Wp), N, piv, info + J, 1.0, false, rt().lu_work, s);
+        slate_hip::v_explicit<K<T>>(mp, nb, kp(Wp), N, kp(L + j1 + j1 * N), N, s);
+        T* T1 = tl(J + 1);
+        NHIP(hipMemsetAsync(T1, 0, sizeof(T) * nb * nb, s));
+        slate_hip::gecopy<K<T>, K<T>>('U', 'N', nb, nb, kp(Wp), N, kp(T1), nb, s);
+        slate_hip::trsm<K<T>>('R', 'L', ct, 'U', nb, nb, kv(T(1)), kp(Ljj), N, kp(T1), nb, s);
+        // symmetric interchange: L's rows, then the trailing Hermitian block
+        slate_hip::laswp_off<K<T>>(j1, kp(L + j1), N, 0, nb, piv, 0, s);
+        T* Str = Af + j1 + j1 * N;
+        slate_hip::laswp_off<K<T>>(mp, kp(Str), N, 0, nb, piv, 0, s);
+        slate_hip::gecopy<K<T>, K<T>>('G', 'C', mp, mp, kp(Str), N, kp(Wt.as<T>()), N, s);
+        slate_hip::laswp_off<K<T>>(mp, kp(Wt.as<T>()), N, 0, nb, piv, 0, s);
+        copy2d(Str, N, Wt.as<T>(), N, mp, mp, s);
+    }
+}
+
+}  // namespace
+
+template <typename T>
+int64_t hetrf(const HermitianMatrix<T>& A, IndefiniteFactors<T>& F, const Options&) {
+    NTRACE("hetrf", nullptr);
+    const Storage& SA = *A.storage();
+    hipStream_t s = rt().main;
+    const i64 n = SA.n;
+    const i64 nb = std::max<i64>(8, std::min<i64>(SA.nb, 256));
+    const i64 N = std::max<i64>(nb, (n + nb - 1) / nb * nb), NT = N / nb;
+    // the full Hermitian matrix on every rank, padded with an identity block
+    std::vector<T> h((size_t)N * N, T(0));
+    {
+        std::vector<T> a((size_t)std::max<i64>(n, 1) * std::max<i64>(n, 1));
+        A.to_host(a.data(), std::max<i64>(n, 1));
+        const bool lo = A.uplo() == Uplo::Lower;
+        for (i64 j = 0; j < n; ++j)
+            for (i64 i = 0; i < n; ++i) {
+                const bool stored = lo ? i >= j : i <= j;
+                const T v = stored ? a[i + j * n] : conj_of(a[j + i * n]);
+                h[i + j * N] = i == j ? T(std::real(v)) : v;
+            }
+        for (i64 i = n; i < N; ++i) h[i + i * N] = T(1);
+    }
+    Scratch Af(sizeof(T) * N * N, s);
+    upload(Af.p, h.data(), sizeof(T) * N * N, s);
+    auto Ls = std::make_shared<Scratch>(sizeof(T) * N * N, s);
+    NHIP(hipMemsetAsync(Ls->p, 0, sizeof(T) * N * N, s));
+    slate_hip::geset<K<T>>('G', nb, nb, kv(T(0)), kv(T(1)), kp(Ls->as<T>()), N, s);
+    Scratch Td(sizeof(T) * nb * nb * NT, s), Tl(sizeof(T) * nb * nb * (NT + 1), s);
+    NHIP(hipMemsetAsync(Td.p, 0, sizeof(T) * nb * nb * NT, s));
+    NHIP(hipMemsetAsync(Tl.p, 0, sizeof(T) * nb * nb * (NT + 1), s));
+    Scratch piv(sizeof(i64) * N, s), inf(sizeof(i64) * NT, s);
+    NHIP(hipMemsetAsync(piv.p, 0, sizeof(i64) * N, s));
+    NHIP(hipMemsetAsync(inf.p, 0, sizeof(i64) * NT, s));
+    aasen<T>(N, nb, Af.as<T>(), Ls->as<T>(), Td.as<T>(), Tl.as<T>(), piv.as<i64>(), inf.as<i64>(), s);
+    // the permutation (block 0 keeps its rows; block J + 1's pivots are
+    // relative to row (J + 1) nb)
+    std::vector<i64> pr((size_t)N);
+    NHIP(hipMemcpyAsync(pr.data(), piv.p, sizeof(i64) * N, hipMemcpyDeviceToHost, s));
+    std::vector<T> htd((size_t)nb * nb * NT), htl((size_t)nb * nb * (NT + 1));
+    NHIP(hipMemcpyAsync(htd.data(), Td.p, sizeof(T) * htd.size(), hipMemcpyDeviceToHost, s));
+    NHIP(hipMemcpyAsync(htl.data(), Tl.p, sizeof(T) * htl.size(), hipMemcpyDeviceToHost, s));
+    NHIP(hipStreamSynchronize(s));
+    auto d = std::make_shared<IndefData>();
+    d->n = n; d->N = N; d->nb = nb; d->p = SA.p; d->q = SA.q;
+    d->perm.resize((size_t)N);
+    for (i64 i = 0; i < N; ++i) d->perm[i] = i;
+    for (i64 i = nb; i < N; ++i) {
+        const i64 j = (i / nb) * nb + pr[i];
+        if (j != i) std::swap(d->perm[i], d->perm[j]);
+    }
+    // T (kl = ku = nb) in LAPACK band layout, then its band LU
+    const i64 ldab = 3 * nb + 1, off = nb;      // AB(off + i - j, j)
+    std::vector<T> ab((size_t)ldab * N, T(0));
+    for (i64 J = 0; J < NT; ++J)
+        for (i64 c = 0; c < nb; ++c)
+            for (i64 r = 0; r < nb; ++r) {
+                const i64 i = J * nb + r, j = J * nb + c;
+                ab[(off + i - j) + j * ldab] = htd[(size_t)J * nb * nb + r + c * nb];
+                if (J + 1 < NT) {
+                    const T lo = htl[(size_t)(J + 1) * nb * nb + r + c * nb];     // T(J+1, J)(r, c)
+                    const i64 il = (J + 1) * nb + r;
+                    if (il - j <= nb) ab[(off + il - j) + j * ldab] = lo;
+                    const i64 ju = (J + 1) * nb + r, iu = J * nb + c;            // T(J, J+1) = T(J+1, J)^H
+                    if (ju - iu <= nb) ab[(off + iu - ju) + ju * ldab] = conj_of(lo);
+                }
+            }
+    auto Tb = std::make_shared<BandMatrix<T>>(N, N, nb, nb, nb);
+    Tb->from_host_band(ab.data(), ldab, off);
+    const int64_t info = gbtrf<T>(*Tb, d->Tpiv);
+    d->L = Ls;
+    d->Tband = Tb;
+    F.d = d;
+    return info;
+}
+
+template <typename T>
+int64_t hetrs(const IndefiniteFactors<T>& F, Matrix<T>& B, const Options&) {
+    NTRACE("hetrs", nullptr);
+    if (!F.d) throw Error("native hetrs: factors of hetrf expected");
+    const IndefData& d = *F.d;
+    hipStream_t s = rt().main;
+    const i64 n = d.n, N = d.N, nr = B.n();
+    if (B.m() != n) throw Error("native hetrs: B must have n rows");
+    const T* L = static_cast<Scratch*>(d.L.get())->template as<T>();
+    std::vector<T> hb((size_t)std::max<i64>(n, 1) * std::max<i64>(nr, 1));
+    B.to_host(hb.data(), std::max<i64>(n, 1));
+    // P b (padded rows zero)
+    std::vector<T> y((size_t)N * nr, T(0));
+    for (i64 c = 0; c < nr; ++c)
+        for (i64 i = 0; i < N; ++i) {
+            const i64 src = d.perm[i];
+            y[i + c * N] = src < n ? hb[src + c * n] : T(0);
+        }
+    Scratch Y(sizeof(T) * std::max<i64>(N * nr, 1), s);
+    upload(Y.p, y.data(), sizeof(T) * N * nr, s);
+    slate_hip::trsm<K<T>>('L', 'L', 'N', 'U', N, nr, kv(T(1)), kp(L), N, kp(Y.as<T>()), N, s);
+    // T z = y with the band LU of T (any grid: B's)
+    Matrix<T> Z(N, nr, B.nb(), B.p(), B.q());
+    NHIP(hipMemcpyAsync(y.data(), Y.p, sizeof(T) * N * nr, hipMemcpyDeviceToHost, s));
+    NHIP(hipStreamSynchronize(s));
+    Z.from_host(y.data(), N);
+    gbtrs<T>(*static_cast<BandMatrix<T>*>(d.Tband.get()), d.Tpiv, Z);
+    Z.to_host(y.data(), N);
+    upload(Y.p, y.data(), sizeof(T) * N * nr, s);
+    slate_hip::trsm<K<T>>('L', 'L', ctrans<T>(), 'U', N, nr, kv(T(1)), kp(L), N, kp(Y.as<T>()), N, s);
+    NHIP(hipMemcpyAsync(y.data(), Y.p, sizeof(T) * N * nr, hipMemcpyDeviceToHost, s));
+    NHIP(hipStreamSynchronize(s));
+    // x = P^T z
+    for (i64 c = 0; c < nr; ++c)
+        for (i64 i = 0; i < N; ++i)
+            if (d.perm[i] < n) hb[d.perm[i] + c * n] = y[i + c * N];
+    B.from_host(hb.data(), std::max<i64>(n, 1));
+    return 0;
+}
+
 template <typename T>
 int64_t hesv(HermitianMatrix<T>& A, Matrix<T>& B, const Options& opts) {
-    Matrix<T> F = expand_tri<T>(A, A.uplo(), 1);
-    std::vector<int64_t> ipiv;
-    const int64_t info = gesv<T>(F, ipiv, B, opts);
-    copy<T>(Op::NoTrans, F, A);
+    IndefiniteFactors<T> F;
+    const int64_t info = hetrf<T>(A, F, opts);
+    if (info == 0) hetrs<T>(F, B, opts);
     return info;
 }
 
@@ -679,6 +894,8 @@ void her2k(T alpha, const Matrix<T>& A, const Matrix<T>& B, real_t<T> beta, Herm
     template int64_t gesv_rbt<T>(Matrix<T>&, Matrix<T>&, const Options&);                                      \
     template int64_t getrs_nopiv<T>(const Matrix<T>&, Matrix<T>&, const Options&);                             \
     template int64_t hesv<T>(HermitianMatrix<T>&, Matrix<T>&, const Options&);                                 \
+    template int64_t hetrf<T>(const HermitianMatrix<T>&, IndefiniteFactors<T>&, const Options&);               \
+    template int64_t hetrs<T>(const IndefiniteFactors<T>&, Matrix<T>&, const Options&);                        \
     template void scale<T>(real_t<T>, real_t<T>, Matrix<T>&);                                                  \
     template Matrix<T> Matrix<T>::slice(int64_t, int64_t, int64_t, int64_t) const;                             \
     template void Matrix<T>::set_slice(int64_t, int64_t, const Matrix<T>&);                                    \
