@@ -45,6 +45,10 @@ int slate_zgetrf(int64_t m, int64_t n, double* a, int64_t lda, int64_t* ipiv);
 int slate_zgetri(int64_t n, double* a, int64_t lda, const int64_t* ipiv);
 double slate_zlanhe(char norm, char uplo, int64_t n, const double* a, int64_t lda);
 double slate_clantr(char norm, char uplo, char diag, int64_t m, int64_t n, const float* a, int64_t lda);
+int slate_dgecon(char norm, int64_t n, const double* a, int64_t lda, double anorm, double* rcond);
+int slate_dtrcon(char norm, char uplo, char diag, int64_t n, const double* a, int64_t lda, double* rcond);
+void slate_dsyev_(const char* jobz, const char* uplo, const int64_t* n, double* a, const int64_t* lda, double* w,
+                  int64_t* info);
 const char* slate_amd_last_error(void);
 
 static int g_fail = 0;
@@ -314,6 +318,52 @@ int main(int argc, char** argv) {
         free(W);
         free(Y);
         free(H);
+    }
+    /* condition estimates (slate_dgecon / slate_dtrcon) against the exact
+     * rcond from the inverse; the Fortran alias slate_dsyev_ by its trace */
+    {
+        double* F = malloc(sizeof(double) * n * n);
+        double* G = malloc(sizeof(double) * n * n);
+        double anorm = 0;
+        for (int j = 0; j < n; ++j) {
+            double cs = 0;
+            for (int i = 0; i < n; ++i) {
+                F[i + j * n] = rnd(i, j, 7) + (i == j ? 3.0 : 0.0);
+                cs += fabs(F[i + j * n]);
+            }
+            anorm = fmax(anorm, cs);
+        }
+        memcpy(G, F, sizeof(double) * n * n);
+        slate_dgetrf(n, n, F, n, ipiv);
+        double rc = -1;
+        const int ci = slate_dgecon('1', n, F, n, anorm, &rc);
+        slate_dgetri(n, F, n, ipiv);
+        double inorm = 0;
+        for (int j = 0; j < n; ++j) {
+            double cs = 0;
+            for (int i = 0; i < n; ++i) cs += fabs(F[i + j * n]);
+            inorm = fmax(inorm, cs);
+        }
+        const double ratio = rc * anorm * inorm;
+        check("slate_dgecon_ratio", (ci == 0 && ratio >= 0.999 && ratio <= 3.0) ? 0.0 : 1.0, 0.5);
+        /* a unit upper triangle: rcond in (0, 1] */
+        double rt = -1;
+        const int ti = slate_dtrcon('1', 'U', 'U', n, G, n, &rt);
+        check("slate_dtrcon_range", (ti == 0 && rt > 0 && rt <= 1.0) ? 0.0 : 1.0, 0.5);
+        /* dsyev_: eigenvalues of the symmetric part sum to its trace */
+        for (int j = 0; j < n; ++j)
+            for (int i = 0; i < n; ++i) F[i + j * n] = 0.5 * (G[i + j * n] + G[j + i * n]);
+        double tr = 0;
+        for (int i = 0; i < n; ++i) tr += F[i + i * n];
+        double* w = malloc(sizeof(double) * n);
+        int64_t nn = n, info = -1;
+        slate_dsyev_("N", "L", &nn, F, &nn, w, &info);
+        double sw = 0;
+        for (int i = 0; i < n; ++i) sw += w[i];
+        check("slate_dsyev_trace", info == 0 ? fabs(sw - tr) / fabs(tr) : 1.0, 1e-10);
+        free(w);
+        free(G);
+        free(F);
     }
     if (g_fail) fprintf(stderr, "last error: %s\n", slate_amd_last_error());
     printf(g_fail ? "ex_native_lapack: FAILED\n" : "ex_native_lapack: all checks passed\n");

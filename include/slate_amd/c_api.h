@@ -2,7 +2,9 @@
  * src/c_api/wrappers.cc, include/slate/c_api/*.h, and the Fortran-callable
  * LAPACK API, lapack_api/).
  *
- * Link with -lslate_amd_c (built in-tree as slate_amd/libslate_amd_c.so).
+ * Link with -lslate_amd_native (slate_amd/libslate_amd_native.so: every
+ * symbol below, no Python runtime).  The CPython-embedding
+ * slate_amd/libslate_amd_c.so exports the same names and is deprecated.
  * The library embeds the Python runtime of slate_amd: call
  * slate_amd_initialize() once (it is also called lazily), and
  * slate_amd_finalize() at exit.  Arrays are column-major with leading

@@ -3,7 +3,9 @@
 // include/slate/slate.hh:41-1367 and the matrix classes of
 // include/slate/Matrix.hh / HermitianMatrix.hh / TriangularMatrix.hh).
 //
-// Header-only, over the handle C API of c_api.h (link -lslate_amd_c).  One
+// Header-only, over the handle C API of c_api.h: link -lslate_amd_native
+// (the Python-free native library, csrc/native/capi_handles.hip; the
+// CPython-backed -lslate_amd_c is deprecated).  One
 // process per GPU; the p x q grid spans every rank started with RANK /
 // WORLD_SIZE / MASTER_ADDR / MASTER_PORT (torchrun convention).  A matrix
 // object owns a handle; sub-matrix and transposed views share the parent's

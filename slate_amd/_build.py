@@ -144,19 +144,21 @@ def build(verbose=False, hip=True, host=True):
             + glob.glob(os.path.join(HERE, "csrc", "hip", "*.hpp"))))
         out.append(_build_native_example(verbose))
         out.append(_build_native_example(verbose, "bench_native"))
+        # the header-only C++ API (slate_amd.hh) over the NATIVE handle C API
+        out.append(_build_native_example(verbose, "ex_cpp_api_native", "ex_cpp_api"))
         out.append(_build_native_c_example(verbose))
         out.append(_build_native_c_example(verbose, "ex_native_lapack"))
         out.append(_build_native_c_example(verbose, "ex_native_handles"))
     return out
 
 
-def _build_native_example(verbose=False, name="ex_native"):
+def _build_native_example(verbose=False, name="ex_native", src_name=None):
     """examples/cpp/<name>.cc -> slate_amd/<name>: a plain g++ C++17
     program against include/slate_amd/slate_native.hh and
     libslate_amd_native.so (rpath $ORIGIN), no Python.  Built in-tree next
     to the library so it travels to the GPU box with the snapshot
     (ex_native: the example / tests; bench_native: bench.py --impl native)."""
-    src = os.path.join(ROOT, "examples", "cpp", name + ".cc")
+    src = os.path.join(ROOT, "examples", "cpp", (src_name or name) + ".cc")
     lib = os.path.join(HERE, "libslate_amd_native.so")
     target = os.path.join(HERE, name)
     hdr = os.path.join(ROOT, "include", "slate_amd", "slate_native.hh")

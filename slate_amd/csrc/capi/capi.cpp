@@ -1,3 +1,8 @@
+// DEPRECATED (round 6): libslate_amd_native.so now exports every symbol of
+// this library (LAPACK-style, ScaLAPACK, BLACS and the matrix handles,
+// csrc/native/capi_*.hip) without a Python runtime; link -lslate_amd_native.
+// This CPython-embedding ABI stays only for the host-target (CPU) path.
+//
 // C ABI of slate_amd (include/slate_amd/c_api.h): embeds the CPython
 // runtime that drives the framework and forwards each call, with raw
 // pointers passed as integers, to slate_amd.compat.capi_bridge.call().

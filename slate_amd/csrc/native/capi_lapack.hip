@@ -231,6 +231,39 @@ double h_lantr(char norm, char uplo, char diag, i64 m, i64 n, const T* a, i64 ld
     return rc == 0 ? r : -1.0;
 }
 
+// condition estimates from host factors (reference lapack_api/lapack_gecon.cc,
+// _pocon.cc, _trcon.cc): rcond through the native estimators
+template <typename T>
+int64_t h_con(char kind, char norm, char uplo, char diag, i64 n, const T* a, i64 lda, double anorm, T* rcond) {
+    if (n < 0) return -2;
+    if (lda < std::max<i64>(1, n)) return -4;
+    if (n == 0) { *rcond = T(1); return 0; }
+    return guarded([&]() -> int64_t {
+        int p, q;
+        grid_of(p, q);
+        const sn::Norm nk = up(norm) == 'I' ? sn::Norm::Inf : sn::Norm::One;
+        double rc = 0;
+        if (kind == 'G') {
+            sn::Matrix<T> A(n, n, nb_of(n), p, q);
+            A.from_host(a, lda);
+            rc = sn::gecondest<T>(nk, A, anorm);
+        } else if (kind == 'P') {
+            // the Cholesky factor as Lower storage (Upper: its conjugate transpose)
+            std::vector<T> l = up(uplo) == 'U' ? host_op<T>('C', n, n, a, lda) : std::vector<T>(a, a + 0);
+            sn::HermitianMatrix<T> L(sn::Uplo::Lower, n, nb_of(n), p, q);
+            if (up(uplo) == 'U') L.from_host(l.data(), n);
+            else L.from_host(a, lda);
+            rc = sn::pocondest<T>(nk, L, anorm);
+        } else {
+            sn::Matrix<T> A(n, n, nb_of(n), p, q);
+            A.from_host(a, lda);
+            rc = sn::trcondest<T>(nk, uplo_of(uplo), diag_of(diag), A);
+        }
+        *rcond = T(rc);
+        return 0;
+    });
+}
+
 }  // namespace
 
 extern "C" {
@@ -371,4 +404,48 @@ SN_LAPACK2_C(c, float)
 SN_LAPACK2_C(z, double)
 #undef SN_LAPACK2_C
 
+
+#define SN_CON(X, T)                                                                                            \
+    int slate_##X##gecon(char norm, int64_t n, const T* a, int64_t lda, T anorm, T* rcond) {                   \
+        return (int)h_con<T>('G', norm, 'L', 'N', n, a, lda, (double)anorm, rcond);                            \
+    }                                                                                                          \
+    int slate_##X##pocon(char uplo, int64_t n, const T* a, int64_t lda, T anorm, T* rcond) {                   \
+        return (int)h_con<T>('P', '1', uplo, 'N', n, a, lda, (double)anorm, rcond);                            \
+    }                                                                                                          \
+    int slate_##X##trcon(char norm, char uplo, char diag, int64_t n, const T* a, int64_t lda, T* rcond) {      \
+        return (int)h_con<T>('T', norm, uplo, diag, n, a, lda, 0.0, rcond);                                    \
+    }
+SN_CON(s, float)
+SN_CON(d, double)
+#undef SN_CON
+
+// Fortran-callable aliases of the C ABI (c_api.h: every argument by reference)
+int slate_dsgesv(int64_t n, int64_t nrhs, double* a, int64_t lda, int64_t* ipiv, const double* b, int64_t ldb,
+                 double* x, int64_t ldx, int* iter);
+void slate_dsgesv_(const int64_t* n, const int64_t* nrhs, double* a, const int64_t* lda, int64_t* ipiv,
+                   const double* b, const int64_t* ldb, double* x, const int64_t* ldx, int64_t* iter, int64_t* info) {
+    int it = 0;
+    *info = slate_dsgesv(*n, *nrhs, a, *lda, ipiv, b, *ldb, x, *ldx, &it);
+    if (iter) *iter = it;
+}
+void slate_dsyev(const char* jobz, const char* uplo, const int* n, double* a, const int* lda, double* w, double* work,
+                 const int* lwork, int* info);
+void slate_dsyevd(const char* jobz, const char* uplo, const int* n, double* a, const int* lda, double* w,
+                  double* work, const int* lwork, int* iwork, const int* liwork, int* info);
+void slate_dsyev_(const char* jobz, const char* uplo, const int64_t* n, double* a, const int64_t* lda, double* w,
+                  int64_t* info) {
+    const int nn = (int)*n, ll = (int)*lda, lw = 1;
+    int inf = 0;
+    double wk = 0;
+    slate_dsyev(jobz, uplo, &nn, a, &ll, w, &wk, &lw, &inf);
+    *info = inf;
+}
+void slate_dsyevd_(const char* jobz, const char* uplo, const int64_t* n, double* a, const int64_t* lda, double* w,
+                   int64_t* info) {
+    const int nn = (int)*n, ll = (int)*lda, lw = 1, liw = 1;
+    int inf = 0, iw = 0;
+    double wk = 0;
+    slate_dsyevd(jobz, uplo, &nn, a, &ll, w, &wk, &lw, &iw, &liw, &inf);
+    *info = inf;
+}
 }  // extern "C"

@@ -378,6 +378,12 @@ def _row_chunks(nrow, nb, la, p, ch):
     return out
 
 
+# SLATE_AMD_BCAST_SA=1: the row broadcasts of the panel (q >= 3) as a direct
+# scatter + all-gather (Comm.bcast_sa): 2 B / q per xGMI link instead of B
+# (per-link projection: profiles/r6/critpath_2x4_links.md)
+_BCAST_SA = __import__("os").environ.get("SLATE_AMD_BCAST_SA", "0") == "1"
+
+
 def _bcast_panel_rows(grid, q, buf, lr1, lr_end, lcg, kb, own_col, root, chunks, dtype, dev, st, ss):
     """Issue every chunk's row broadcast on the DIAG stream -- the row
     communicator's one stream (torch runs a synchronous RCCL collective on
@@ -403,7 +409,10 @@ def _bcast_panel_rows(grid, q, buf, lr1, lr_end, lcg, kb, own_col, root, chunks,
             ss.wait(ss.diag, ev_src)
             if cb.is_cuda:
                 cb.record_stream(ss.diag)
-            grid.row_comm.bcast(cb, root)
+            if _BCAST_SA and q >= 3:
+                grid.row_comm.bcast_sa(cb, root)
+            else:
+                grid.row_comm.bcast(cb, root)
             ev = ss.event(ss.diag)
         pend.append((a, b, cb, ev))
         nbytes = (b - a) * kb * esz

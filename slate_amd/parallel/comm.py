@@ -204,6 +204,66 @@ class Comm:
         except Exception as e:  # noqa: BLE001
             raise CommError(f"bcast failed: {e}") from e
 
+    @_wd.watched("comm.bcast_sa")
+    def bcast_sa(self, t: torch.Tensor, root: int):
+        """Broadcast t from comm-rank root in two DIRECT phases -- scatter
+        (the root sends piece j of t to member j) then all-gather (every
+        member sends its piece to every other member) -- as grouped
+        point-to-point transfers.  On the xGMI mesh every GPU pair has its
+        own link, so each link carries 2 B / size bytes instead of the B of
+        a ring / tree broadcast and a receiver ingests over size - 1 links at
+        once (profiles/r6/critpath_2x4_links.md).  size <= 2: plain bcast.
+        One issue-order key, like bcast (the two phases are issued by every
+        member in the same order)."""
+        _wd.beat("comm.bcast_sa")
+        self._note(t)
+        if self.size <= 2:
+            return self.bcast(t, root)
+        self._ord("bcast")
+        try:
+            fv = self._flat_view(t)
+            src = fv if fv is not None else t.contiguous()
+            x, staged = self._prep(src)
+            flat = x.reshape(-1)
+            n, P, me = flat.numel(), self.size, self.rank
+            L = -(-n // P)
+
+            def piece(j):
+                return flat[min(n, j * L):min(n, (j + 1) * L)]
+
+            def run(ops):
+                if ops:
+                    for w in dist.batch_isend_irecv(ops):
+                        w.wait()
+            # phase 1: scatter from the root
+            ops = []
+            if me == root:
+                ops = [dist.P2POp(dist.isend, piece(j), self._g(j), self.group)
+                       for j in range(P) if j != root and piece(j).numel()]
+            elif piece(me).numel():
+                ops = [dist.P2POp(dist.irecv, piece(me), self._g(root), self.group)]
+            run(ops)
+            # phase 2: every rank's piece to every member except itself and
+            # the root (which holds everything); the root sends its own piece
+            ops = []
+            for k in range(P):
+                if k == me or k == root:
+                    continue
+                if piece(me).numel():
+                    ops.append(dist.P2POp(dist.isend, piece(me), self._g(k), self.group))
+            if me != root:
+                for r in range(P):
+                    if r != me and piece(r).numel():
+                        ops.append(dist.P2POp(dist.irecv, piece(r), self._g(r), self.group))
+            run(ops)
+            if x is not src:
+                src.copy_(x)
+            if fv is None:
+                t.copy_(src)
+            return None
+        except Exception as e:  # noqa: BLE001
+            raise CommError(f"bcast_sa failed: {e}") from e
+
     @_wd.watched("comm.allreduce")
     def allreduce(self, t: torch.Tensor, op: str = "sum"):
         _wd.beat("comm.allreduce")
@@ -452,6 +512,9 @@ class LoopbackComm(Comm):
     # instead of being added up afterwards.  bcast / reduce: alpha + B/beta;
     # allreduce: alpha + 2 B/beta; allgather(v): alpha + (P-1) B/beta.
     _link = None
+    # bytes on the BUSIEST link per byte of the message (ring / pipelined
+    # tree collectives: every link of the ring carries the whole message;
+    # bcast_sa: 2 / size, see Comm.bcast_sa); bcast_sa pays alpha twice
     _LINK_FACTOR = {"bcast": 1.0, "reduce": 1.0, "allreduce": 2.0}
 
     @classmethod
@@ -470,9 +533,12 @@ class LoopbackComm(Comm):
         LoopbackComm.LOG.append((op, self.size, nbytes, st))
         lk = self.link()
         if lk[0] and isinstance(t, torch.Tensor) and t.is_cuda and self.size > 1:
-            f = self._LINK_FACTOR.get(op, float(self.size - 1))
+            if op == "bcast_sa":
+                f, a = 2.0 / self.size, 2 * lk[1]
+            else:
+                f, a = self._LINK_FACTOR.get(op, float(self.size - 1)), lk[1]
             from .. import ops
-            ops.spin_ns((lk[1] + f * nbytes / lk[2]) * 1e9, t)
+            ops.spin_ns((a + f * nbytes / lk[2]) * 1e9, t)
 
     @classmethod
     def _tmp(cls, t):
@@ -503,6 +569,14 @@ class LoopbackComm(Comm):
     def bcast(self, t, root, async_op=False):
         self._log("bcast", t)
         if self.size > 1 and self.rank != root:
+            self._land(t)
+        return None
+
+    def bcast_sa(self, t, root):
+        if self.size <= 2:
+            return self.bcast(t, root)
+        self._log("bcast_sa", t)
+        if self.rank != root:
             self._land(t)
         return None
 

@@ -198,6 +198,33 @@ def test_native_lapack_more_from_c(nranks):
 
 
 HEXE = os.path.join(ROOT, "slate_amd", "ex_native_handles")
+CPPEXE = os.path.join(ROOT, "slate_amd", "ex_cpp_api_native")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("grid", ["1x1", "2x2"])
+def test_cpp_header_api_over_native(grid):
+    """The header-only C++ API (include/slate_amd/slate_amd.hh) linked
+    against libslate_amd_native.so instead of the deprecated CPython-backed
+    libslate_amd_c.so: posv / gesv / getri / trmm / trsm / herk / gels /
+    heev / svd_vals / gesv_mixed with sub-matrix and transposed views."""
+    assert os.path.exists(CPPEXE), "slate_amd/ex_cpp_api_native not built"
+    ldd = subprocess.run(["ldd", CPPEXE], capture_output=True, text=True, env=_clean_env()).stdout
+    assert "python" not in ldd.lower() and "libslate_amd_c" not in ldd, ldd
+    p, q = map(int, grid.split("x"))
+    if p * q == 1:
+        r = subprocess.run([CPPEXE, grid], capture_output=True, text=True, env=_clean_env(), timeout=240)
+        outs = [(r.returncode, r.stdout + r.stderr)]
+    else:
+        outs = _run_ranks(CPPEXE, [grid], p * q)
+    for rc, out in outs:
+        print(out)
+        assert rc == 0, out
+        lines = [ln for ln in out.splitlines() if ln.startswith("rank ") and "iterations" not in ln]
+        assert len(lines) == 9, out
+        for ln in lines:
+            assert "FAILED" not in ln, ln
+            assert float(ln.split()[-1]) < 1e-10, ln
 
 
 @pytest.mark.gpu

@@ -147,6 +147,15 @@ def main():
         fl = res[0]["flops"]
         lines.append(f"- job (max over simulated ranks): {worst * 1e3:.1f} ms = {fl / worst / 1e12:.1f} TF/s "
                      f"({100 * fl / worst / (p * q * PEAK):.1f} % of {p * q} x 78.6)")
+        # per-link accounting: the bytes each collective puts on its BUSIEST
+        # link (ring / pipelined bcast, reduce: the message; allreduce: 2x;
+        # all-gather: (size - 1)x; the direct bcast_sa: 2 / size of it)
+        from slate_amd.parallel.comm import LoopbackComm
+        for x in res:
+            for (st, op, size), (c, b) in sorted(x["agg"].items()):
+                f = (2.0 / size) if op == "bcast_sa" else LoopbackComm._LINK_FACTOR.get(op, float(size - 1))
+                lines.append(f"  - rank {x['rank']}: {st} {op} over {size}: {c} calls, {b / 2 ** 20:.1f} MiB, "
+                             f"busiest link {f * b / 2 ** 20:.1f} MiB")
         text = "\n".join(lines)
         print(text, flush=True)
         if args.out:
