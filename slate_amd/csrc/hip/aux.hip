@@ -103,6 +103,12 @@ __global__ void scale_row_col_kernel(char equed, i64 m, i64 n, const R* r, const
     if (i >= m) return;
     for (i64 j = blockIdx.y; j < n; j += gridDim.y) {
         R s = R(1);
+        if (equed == 'S') {            // sign: a / |a|, 1 where a = 0 (condest's sign vector)
+            const T a = A[i + j * lda];
+            const R m = s_abs(a);
+            A[i + j * lda] = m > R(0) ? s_mul(s_from_real(T(), R(1) / m), a) : s_from_real(T(), R(1));
+            continue;
+        }
         if (equed == 'R' || equed == 'B') s *= r[i];
         if (equed == 'C' || equed == 'B') s *= c[j];
         A[i + j * lda] = s_mul(s_from_real(T(), s), A[i + j * lda]);

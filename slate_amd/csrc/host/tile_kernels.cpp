@@ -912,6 +912,12 @@ void register_tile_kernels(py::module& m) {
             for (i64 j = 0; j < n; ++j)
                 for (i64 i = 0; i < mm; ++i) {
                     R sfac = 1;
+                    if (equed == 'S') {
+                        T& a = P<T>(A)[i + j * lda];
+                        const R mg = std::abs(a);
+                        a = mg > R(0) ? a / mg : T(1);
+                        continue;
+                    }
                     if (equed == 'R' || equed == 'B') sfac *= rr[i];
                     if (equed == 'C' || equed == 'B') sfac *= cc[j];
                     P<T>(A)[i + j * lda] *= sfac;

@@ -236,8 +236,15 @@ def rows_global(lr0, lr1, nb, p, pr, r0, dev):
         if torch.device(dev).type == "cuda":
             g = g.pin_memory().to(dev, non_blocking=True)
         _GROWS[key] = tab = g
-    v = tab[lr0:lr1]
-    return v - r0 if r0 else v
+    if not r0:
+        return tab[lr0:lr1]
+    # shifted rows: formed on the host and uploaded pinned / non-blocking (a
+    # device subtraction would be torch compute in the step loop)
+    lr = np.arange(lr0, lr1, dtype=np.int64)
+    g = torch.from_numpy(((lr // nb) * p + pr) * nb + lr % nb - r0)
+    if torch.device(dev).type == "cuda":
+        g = g.pin_memory().to(dev, non_blocking=True)
+    return g
 
 
 def panel_allgather(colc, buf, mloc, t0, lc, kb, nb, p, pr, nloc_r, dt, dev):

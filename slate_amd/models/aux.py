@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import math
 
+import numpy as np
 import torch
 
 from .. import ops
@@ -493,55 +494,57 @@ def norm(norm_type, A, opts=None, scope=NormScope.Matrix):
                     yield blk, u, gr, gc
     rdt = torch.float64 if s.dtype in (torch.float64, torch.complex128) else torch.float32
     code = {Norm.Max: 'M', Norm.One: '1', Norm.Inf: 'I', Norm.Fro: 'F'}[nt]
-    colv = torch.zeros(n_g * (2 if code == 'F' else 1), dtype=rdt, device=dev)
-    rowv = torch.zeros(m_g, dtype=rdt, device=dev)
-    if True:
-        for blk, u, gr, gc in pieces():
-            gc_t = torch.as_tensor(gc, device=dev)
-            gr_t = torch.as_tensor(gr, device=dev)
-            on_diag = u != 'G'
-            if herm and code in ('1', 'I'):
-                if on_diag:
-                    c, r = ops.genorm_local('1', blk, uplo=u, herm=hv)
-                else:
-                    c, _ = ops.genorm_local('1', blk)
-                    _, r = ops.genorm_local('I', blk)
-                colv.index_add_(0, gc_t, c)
-                rowv.index_add_(0, gr_t, r)
-                continue
-            c, r = ops.genorm_local(code, blk, uplo=u, diag=diag, herm=hv if on_diag else 0)
-            if code == 'M':
-                colv.index_put_((gc_t,), torch.maximum(colv[gc_t], c))
-                if torch.isnan(c).any():
-                    colv[gc_t] = torch.where(torch.isnan(c), c, colv[gc_t])
-            elif code == 'F':
-                cv = colv.view(n_g, 2)
-                ss = c[:, 0] ** 2 * c[:, 1]
-                cv[gc_t, 1] += ss * (2 if (herm and not on_diag) else 1)
+    # every piece's per-column / per-row contributions come from the genorm
+    # kernels; they are O(m + n) numbers, combined on the HOST (numpy) -- no
+    # torch arithmetic on the device -- and reduced over the ranks as one
+    # small device tensor (RCCL) per quantity
+    colv = np.zeros(n_g, dtype=np.float64)
+    rowv = np.zeros(m_g, dtype=np.float64)
+    mx, fro2, nan = 0.0, 0.0, False
+    for blk, u, gr, gc in pieces():
+        on_diag = u != 'G'
+        if herm and code in ('1', 'I'):
+            if on_diag:
+                c, r = ops.genorm_local('1', blk, uplo=u, herm=hv)
             else:
-                colv.index_add_(0, gc_t, c)
-                rowv.index_add_(0, gr_t, r)
+                c, _ = ops.genorm_local('1', blk)
+                _, r = ops.genorm_local('I', blk)
+            np.add.at(colv, np.asarray(gc), c.cpu().double().numpy())
+            np.add.at(rowv, np.asarray(gr), r.cpu().double().numpy())
+            continue
+        c, r = ops.genorm_local(code, blk, uplo=u, diag=diag, herm=hv if on_diag else 0)
+        if code == 'M':
+            v = float(ops.genorm_local('M', c.view(-1, 1))[0][0]) if c.numel() else 0.0   # NaN propagates
+            if v != v:
+                nan = True
+            else:
+                mx = max(mx, v)
+        elif code == 'F':
+            ch = c.cpu().double().numpy()
+            fro2 += float(np.sum(ch[:, 0] ** 2 * ch[:, 1])) * (2 if (herm and not on_diag) else 1)
+        else:
+            np.add.at(colv, np.asarray(gc), c.cpu().double().numpy())
+            np.add.at(rowv, np.asarray(gr), r.cpu().double().numpy())
+
+    def _reduce(x, op):
+        if comm.size == 1:
+            return x
+        t = torch.from_numpy(np.ascontiguousarray(x, dtype=np.float64)).to(dev)
+        comm.allreduce(t, op)
+        return t.cpu().numpy()
     if code == 'M':
-        if comm.size > 1:
-            comm.allreduce(colv, "max")
-        v = colv.max() if colv.numel() else torch.zeros((), dtype=rdt)
-        if torch.isnan(colv).any():
-            return float("nan")
-        return float(v)
+        out = _reduce(np.asarray([mx, 1.0 if nan else 0.0]), "max")
+        return float("nan") if out[1] > 0 else float(out[0])
     if code == 'F':
-        tot = colv.view(n_g, 2)[:, 1].sum().reshape(1)
-        if comm.size > 1:
-            comm.allreduce(tot, "sum")
-        return float(torch.sqrt(tot))
-    if comm.size > 1:
-        comm.allreduce(colv, "sum")
-        comm.allreduce(rowv, "sum")
+        return float(np.sqrt(_reduce(np.asarray([fro2]), "sum")[0]))
+    colv = _reduce(colv, "sum")
+    rowv = _reduce(rowv, "sum")
     if herm:
         tot = colv + (rowv if m_g == n_g else 0)
-        return float(tot.max()) if tot.numel() else 0.0
+        return float(tot.max()) if tot.size else 0.0
     if code == '1':
-        return float(colv.max()) if colv.numel() else 0.0
-    return float(rowv.max()) if rowv.numel() else 0.0
+        return float(colv.max()) if colv.size else 0.0
+    return float(rowv.max()) if rowv.size else 0.0
 
 
 def _piece_globals(blk, lb):
@@ -554,25 +557,33 @@ def _piece_globals(blk, lb):
 
 
 def _dense_norm(nt, D, A):
+    """Norm of the gathered op(A) for storages without a 2D block-cyclic map,
+    through the same genorm kernels as the distributed path (the stored
+    triangle is masked inside the kernel, no dense rebuild)."""
+    m, n = D.shape
+    if not (m and n):
+        return 0.0
     kind = _diag_kind(A)
-    if kind in ("hermitian", "symmetric"):
-        L = torch.tril(D) if A.uploPhysical() == Uplo.Lower else torch.triu(D)
-        if kind == "hermitian":
-            # only the real part of the diagonal is referenced (LAPACK lanhe)
-            D = L + L.mH
-            D.diagonal().copy_(torch.diagonal(L).real.to(D.dtype))
-        else:
-            D = L + L.transpose(0, 1) - torch.diag(torch.diagonal(L))
-    elif kind == "trapezoid":
-        D = torch.tril(D) if A.uploPhysical() == Uplo.Lower else torch.triu(D)
-    a = D.abs()
-    if nt == Norm.Max:
-        return float(a.max()) if a.numel() else 0.0
-    if nt == Norm.One:
-        return float(a.sum(0).max()) if a.numel() else 0.0
-    if nt == Norm.Inf:
-        return float(a.sum(1).max()) if a.numel() else 0.0
-    return float(torch.sqrt((a * a).sum()))
+    herm = kind in ("hermitian", "symmetric")
+    u = 'G' if kind == "general" else A.uplo().value      # D is op(A): logical triangle
+    hv = (2 if kind == "hermitian" and D.is_complex() else 1) if herm else 0
+    diag = 'U' if getattr(A, "_diag", None) is not None and A._diag.value == 'U' and kind == "trapezoid" else 'N'
+    code = {Norm.Max: 'M', Norm.One: '1', Norm.Inf: 'I', Norm.Fro: 'F'}[nt]
+    if D.stride(0) != 1:
+        # row-major D is the column-major D^T: same |entries| transposed, so
+        # the stored triangle flips and One <-> Inf (|conj| = || for Hermitian)
+        D = D.transpose(0, 1)
+        u = {'L': 'U', 'U': 'L'}.get(u, u)
+        code = {'1': 'I', 'I': '1'}.get(code, code)
+    if herm and code in ('1', 'I'):
+        c, r = ops.genorm_local('1', D, uplo=u, herm=hv)
+        return float((c + r).max())
+    c, r = ops.genorm_local(code, D, uplo=u, diag=diag, herm=hv)
+    if code == 'M':
+        return float("nan") if bool(torch.isnan(c).any()) else float(c.max())
+    if code == 'F':
+        return float(torch.sqrt((c[:, 0] ** 2 * c[:, 1]).sum()))
+    return float(c.max()) if code == '1' else float(r.max())
 
 
 def colNorms(norm_type, A, opts=None):

@@ -202,11 +202,11 @@ def gbtrf(A, pivots: Pivots, opts=None) -> int:
                     s.tileInsert(i, j, slot, data=_col_block(s, buf, j, s.row_offsets[i], s.row_offsets[i + 1])[:, :s.tileNb(j)])
         s.mark_local_modified(slot)
         A.setUpperBandwidth(kl + ku)
-        glob = ipiv.clone()
+        glob = ipiv.cpu().clone()              # panel-relative -> global: host pass
         for k in range(kt):
             r0 = k * nb
             glob[r0:r0 + min(nb, mn - r0)] += r0
-        pivots.set(glob[:mn], nb)
+        pivots.set(glob[:mn].to(ipiv.device), nb)
         iv = infos[:kt].cpu().tolist()
         info = next((k * nb + v for k, v in enumerate(iv) if v > 0), 0)
         if comm.size > 1:
@@ -675,11 +675,11 @@ def _band_product(s, buf, Bl, Cl, w, mode, up=None):
         got = _exchange_pieces(s, snd, rsh, dt, dev)
         for (i, j) in mine:
             r0, r1 = tile_rows(i)
-            Cl[_lrow(s, i):_lrow(s, i) + (r1 - r0)] += piece(i, j)
+            ops.geadd(1.0, piece(i, j), 1.0, Cl[_lrow(s, i):_lrow(s, i) + (r1 - r0)])
         for r, lst in shapes.items():
             for (i, j), T in zip(lst, got[r]):
                 r0, r1 = tile_rows(i)
-                Cl[_lrow(s, i):_lrow(s, i) + (r1 - r0)] += T
+                ops.geadd(1.0, T, 1.0, Cl[_lrow(s, i):_lrow(s, i) + (r1 - r0)])
     # ---- 'T' part: B tiles (i) of column j's window from owner(i) to owner(j)
     if do_t:
         sends, shapes = {}, {}

@@ -17,6 +17,7 @@ import torch
 
 from ..core.enums import Diag, Norm, Op, Side, Uplo
 from ..core.matrix import Matrix, TriangularMatrix
+from .. import ops
 from ..utils.trace import trace_block
 
 
@@ -48,6 +49,11 @@ class _DistVec:
     def v(self):
         return self.lb.data[:self.lb.mloc, 0] if self.owner else None
 
+    @property
+    def col(self):
+        """the local part as a column-major mloc x 1 block (kernel operand)"""
+        return self.lb.data[:self.lb.mloc, :1] if self.owner else None
+
     def fill(self, fn):
         """v[i] = fn(global index tensor) (host values)."""
         if self.owner:
@@ -55,7 +61,7 @@ class _DistVec:
         self.X.storage.mark_local_modified(self.X.storage.origin_slot)
 
     def sum_abs(self):
-        loc = float(self.v.abs().sum()) if self.owner else 0.0
+        loc = float(ops.genorm_local('1', self.col)[0][0]) if self.owner else 0.0
         return self.comm.allreduce_scalar(loc) if self.comm.size > 1 else loc
 
     def argmax_abs(self):
@@ -71,17 +77,16 @@ class _DistVec:
         """sum_i real(conj(v_i) x_i) with x given by its global-index function."""
         loc = 0.0
         if self.owner:
-            x = fn_x(self.rows).to(self.v.dtype).to(self.v.device)
-            loc = float((self.v.conj() * x).real.sum())
+            x = fn_x(self.rows).to(self.v.dtype).to(self.v.device).view(-1, 1)
+            d = torch.zeros(1, 1, dtype=self.v.dtype, device=self.v.device)
+            ops.gemm(1.0, self.col, x, 0.0, d, transA='C')       # v^H x
+            loc = float(d[0, 0].real)
         return self.comm.allreduce_scalar(loc) if self.comm.size > 1 else loc
 
     def to_sign(self):
         """v := v / |v| (1 where v = 0), in place on the local part."""
-        if self.owner:
-            v = self.v
-            a = v.abs()
-            one = torch.ones_like(v)
-            v.copy_(torch.where(a > 0, v / torch.where(a > 0, a, torch.ones_like(a)).to(v.dtype), one))
+        if self.owner and self.v.numel():
+            ops.gescale_row_col('S', None, None, self.col)
         self.X.storage.mark_local_modified(self.X.storage.origin_slot)
 
 

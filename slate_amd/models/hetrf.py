@@ -78,7 +78,7 @@ def aasen(Af: torch.Tensor, nb: int):
     S = ops.colmajor_empty(nb, nb, dt, dev)
     tmp = ops.colmajor_empty(nb, nb, dt, dev)
     Wt = ops.colmajor_empty(N, N, dt, dev)                     # transpose workspace
-    ipiv = torch.arange(N, dtype=torch.int64, device=dev)     # block 0: no interchanges
+    ipiv = torch.arange(N, dtype=torch.int64).to(dev)         # block 0: no interchanges (host iota, one copy)
     info = torch.zeros(max(NT, 1), dtype=torch.int64, device=dev)
     for J in range(NT):
         j0, j1 = J * nb, (J + 1) * nb
@@ -130,7 +130,11 @@ def aasen(Af: torch.Tensor, nb: int):
             ops.gecopy(Str, Wv, trans='C')
             ops.laswp(Wv, piv, 0, nb)
             Str.copy_(Wv)
-            ipiv[j1:j1 + nb] += j1
+    # panel-relative -> global interchange indices: one host pass (the caller
+    # reads ipiv on the host anyway)
+    ipiv = ipiv.cpu()
+    for j1 in range(nb, N, nb):
+        ipiv[j1:j1 + nb] += j1
     return L, Td, Tl, ipiv
 
 
@@ -209,14 +213,18 @@ def hetrf(A, pivots: Pivots = None, T=None, pivots2=None, H=None, opts=None):
         info = gbtrf(Tb, Tpiv)
         A._hetrf = IndefiniteFactors(L, Tb, Tpiv, perm, n, N, nb, Td, Tl)
         # L below the first block column, shifted one block left (SLATE layout)
-        out = torch.zeros(n, n, dtype=dt, device=dev)
+        # (triangle copies and clears are tile-kernel launches: gecopy / geset)
+        out = ops.colmajor_zeros(n, n, dt, dev)
         if N > nb:
-            sh = torch.tril(L[nb:, nb:], -1)
-            out[nb:n, 0:n - nb] = sh[:n - nb, :n - nb]
+            ov = out[nb:n, 0:n - nb]
+            ops.gecopy(L[nb:n, nb:n], ov, uplo='L')
+            ops.geset(0.0, 0.0, ov, uplo='U')           # strictly lower part of L only
         for J in range(N // nb):
             r0, r1 = J * nb, min(n, (J + 1) * nb)
             if r0 < n:
-                out[r0:r1, r0:r1] = torch.tril(_blk(Td, J, nb))[:r1 - r0, :r1 - r0]
+                ob = out[r0:r1, r0:r1]
+                ops.geset(0.0, 0.0, ob)
+                ops.gecopy(_blk(Td, J, nb)[:r1 - r0, :r1 - r0], ob, uplo='L')
         up = A.uploPhysical()
         from_dense(A, out if up != Uplo.Upper else out.mH)
         if pivots is not None:

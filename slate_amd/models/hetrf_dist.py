@@ -180,13 +180,13 @@ def hetrf_dist(A, opts=None):
                 if pc == cJ:
                     lcJ = tiles_local_before(J, q, pc) * nb
                     if nmine:
-                        W += fl[lr1:mloc, lcJ:lcJ + nb]
+                        ops.geadd(1.0, fl[lr1:mloc, lcJ:lcJ + nb], 1.0, W)
                     Pn, rows_of = _gather_panel(W, grid, J + 1, nb, p, pr, N, mloc, dt, dev)
                     piv = piv_t[:nb]
                     ops.getrf(Pn, piv, piv_t[nb:nb + 1])
                     Lfull = ops.colmajor_zeros(N - j1, nb, dt, dev)
                     ops.v_explicit(Pn, Lfull)
-                    T1.copy_(torch.triu(Pn[0:nb]))
+                    ops.gecopy(Pn[0:nb], T1, uplo='U')                   # T1 zero below
                     ops.trsm('R', 'L', ct, 'U', 1.0, Ljj, T1)
                     # this process row's rows of the new L block column
                     Lpan = ops.colmajor_empty(nmine, nb, dt, dev)

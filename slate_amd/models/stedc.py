@@ -113,7 +113,7 @@ def stedc_rows(d, e, comm=None, device=None, leaf=None):
         dl = _split_diag(d, e, levels)
         own = [(a, b) for (a, b) in leaves if a < r1 and b > r0] if P > 1 else leaves
         fails = _leaves(own, dl, e, w, Q, r0, r1, dev)
-        ws = _LevelWork(n, dev) if (dev.type == "cuda" and _DEVICE_MERGE) else None
+        ws = _LevelWork(n, dev) if dev.type == "cuda" else None
         for t in range(len(levels) - 1, -1, -1):
             mine = [(a, m, b) for (a, m, b) in levels[t] if a < r1 and b > r0]
             W, Z = _level_inputs(levels[t], w, Q, r0, r1, comm, dev)
@@ -195,10 +195,10 @@ def _level_inputs(merges, w, Q, r0, r1, comm, dev):
     return W, Z
 
 
-# SLATE_AMD_STEDC_DEVICE_MERGE=0 selects the per-merge driver below (two
-# host round trips per merge, torch index ops) instead of the level-batched
-# device merge
-_DEVICE_MERGE = os.environ.get("SLATE_AMD_STEDC_DEVICE_MERGE", "1") != "0"
+# On a GPU every merge level runs the level-batched device merge
+# (_merge_level_gpu: slate_hip kernels only).  The per-merge driver _merge
+# below is the HOST path (CPU devices: gloo tests, host-only builds); it is
+# never used for device-resident Q.
 # host round trips of the last stedc_rows call (tests)
 STEDC_STATS = {"host_syncs": 0, "levels": 0}
 
@@ -328,7 +328,10 @@ def _merge_gemm_dev(H, ws, Qs, nr, a, k, lo, m, hi, n1, n2, dK, zh, org, mu, st)
 
 
 def _merge(a, m, b, rho, W, Z, w, Q, r0, r1, dev):
-    """One merge on this rank's rows of [a, b): see the module docstring."""
+    """One merge on this rank's rows of [a, b) (HOST path: CPU tensors; the
+    GPU runs _merge_level_gpu): see the module docstring."""
+    if dev.type != "cpu":
+        raise SlateError("stedc: the per-merge host path takes CPU tensors (GPU merges are level-batched)")
     s = b - a
     dd = W[a:b].clone()
     z = Z[a:b].clone()

@@ -345,7 +345,6 @@ def test_stedc_device_merge_one_sync_per_level(monkeypatch, case):
         e = e * 1e-3
     T = torch.diag(d) + torch.diag(e, 1) + torch.diag(e, -1)
     wr = torch.linalg.eigvalsh(T)
-    monkeypatch.setattr(SD, "_DEVICE_MERGE", True)
     w, Z = sl.stedc(d, e, device="cuda", leaf=64)
     syncs, levels = SD.STEDC_STATS["host_syncs"], SD.STEDC_STATS["levels"]
     leaves, lv = SD._tree(n, 64)
@@ -355,8 +354,7 @@ def test_stedc_device_merge_one_sync_per_level(monkeypatch, case):
     assert (w - wr).abs().max() < tol * max(1.0, wr.abs().max())
     assert (T @ Z - Z * w).abs().max() < tol * max(1.0, wr.abs().max())
     assert (Z.T @ Z - torch.eye(n, dtype=torch.float64)).abs().max() < tol
-    monkeypatch.setattr(SD, "_DEVICE_MERGE", False)
-    w2, _ = sl.stedc(d, e, device="cuda", leaf=64)
+    w2, _ = sl.stedc(d, e, device="cpu", leaf=64)          # the host per-merge path
     assert (w - w2).abs().max() < tol * max(1.0, wr.abs().max())
 
 

@@ -95,3 +95,67 @@ def test_heev_launches_only_own_kernels():
     names = _kernels(lambda: sl.heev(A, None, Z, _dev()))
     assert any("hb2st" in k for k in names), names
     assert not _foreign(names), _foreign(names)
+
+
+def test_hetrf_launches_only_own_kernels():
+    """Blocked Aasen + band LU of T + the solve on one GPU (hesv)."""
+    n, nb = 512, 64
+    dev = torch.device("cuda", 0)
+
+    def problem():
+        A = sl.HermitianMatrix(sl.Uplo.Lower, n, nb=nb, device=dev)
+        A.insertLocalTiles(device=dev)
+        sl.generate_matrix(A, "rands", 8)
+        B = sl.Matrix(n, 3, nb=nb, device=dev)
+        B.insertLocalTiles(device=dev)
+        sl.generate_matrix(B, "rands", 9)
+        return A, B
+
+    A, B = problem()
+    sl.hesv(A, sl.Pivots(), None, None, None, B)     # warm-up
+    A, B = problem()
+    names = _kernels(lambda: sl.hesv(A, sl.Pivots(), None, None, None, B))
+    assert any("slate_hip" in k for k in names), names
+    assert not _foreign(names), _foreign(names)
+
+
+def _census_two_ranks(rank, size):
+    """2 ranks sharing cuda:0 over gloo: the distributed heev (he2hb on the
+    grid, band gathered, chase, row-distributed D&C, grid back-transforms)
+    and the distributed Aasen hetrf launch only slate kernels and copies."""
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    n, nb = 384, 64
+    out = {}
+
+    def heev_problem():
+        H = sl.HermitianMatrix(sl.Uplo.Lower, n, nb=nb, p=2, q=1, device=dev)
+        H.insertLocalTiles(device=0)
+        sl.generate_matrix(H, "rands", 6)
+        Z = sl.Matrix(n, n, nb=nb, p=2, q=1, device=dev)
+        Z.insertLocalTiles(device=0)
+        return H, Z
+
+    H, Z = heev_problem()
+    sl.heev(H, None, Z)                               # warm-up
+    H, Z = heev_problem()
+    out["heev"] = _kernels(lambda: sl.heev(H, None, Z))
+
+    def hetrf_problem():
+        A = sl.HermitianMatrix(sl.Uplo.Lower, n, nb=nb, p=2, q=1, device=dev)
+        A.insertLocalTiles(device=0)
+        sl.generate_matrix(A, "rands", 8)
+        return A
+
+    A = hetrf_problem()
+    sl.hetrf(A, sl.Pivots())
+    A = hetrf_problem()
+    out["hetrf"] = _kernels(lambda: sl.hetrf(A, sl.Pivots()))
+    for k, names in out.items():
+        assert any("slate_hip" in x for x in names), (rank, k, names)
+        assert not _foreign(names), (rank, k, _foreign(names))
+
+
+def test_distributed_heev_hetrf_launch_only_own_kernels():
+    from dist_util import run_dist
+    run_dist(_census_two_ranks, 2, timeout=240)
