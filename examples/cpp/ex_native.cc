@@ -657,6 +657,35 @@ void run(int p, int q, int me) {
         double dv = 0;
         for (int64_t i = 0; i < ne; ++i) dv = std::max(dv, std::abs((double)lam2[i] - (double)lam[i]));
         report("heev_values", dv / (an > 0 ? an : 1));
+        // p x q grids run the distributed solver (no n x n on any rank): the
+        // one-GPU solver behind a gather must give the same spectrum
+        if (p * q > 1) {
+            setenv("SLATE_AMD_NATIVE_HEEV", "gather", 1);
+            std::vector<sn::real_t<T>> lam3;
+            sn::heev(H, lam3);
+            unsetenv("SLATE_AMD_NATIVE_HEEV");
+            double dg = 0;
+            for (int64_t i = 0; i < ne; ++i) dg = std::max(dg, std::abs((double)lam3[i] - (double)lam[i]));
+            report("heev_grid_vs_gather", dg / (an > 0 ? an : 1));
+        }
+    }
+    // ---- redistribute: onto another tile size and grid shape and back
+    {
+        const int64_t mr = 203, nr = 150;
+        sn::Matrix<T> A0(mr, nr, nb, p, q), A1(mr, nr, 37, q, p), A2(mr, nr, nb, p, q);
+        A0.generate(sn::Gen::Random, 131);
+        sn::redistribute(A0, A1);
+        sn::redistribute(A1, A2);
+        std::vector<T> h0((size_t)mr * nr), h1((size_t)mr * nr), h2((size_t)mr * nr);
+        A0.to_host(h0.data(), mr);
+        A1.to_host(h1.data(), mr);
+        A2.to_host(h2.data(), mr);
+        double d1 = 0, d2 = 0;
+        for (size_t i = 0; i < h0.size(); ++i) {
+            d1 = std::max(d1, (double)std::abs(h1[i] - h0[i]));
+            d2 = std::max(d2, (double)std::abs(h2[i] - h0[i]));
+        }
+        report("redistribute", d1 + d2);
     }
     // ---- svd: || A - U S V^H || / || A ||, || U^H U - I ||, || V V^H - I ||
     //      (tall and wide; values only must give the same spectrum)

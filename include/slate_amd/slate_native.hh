@@ -263,6 +263,10 @@ void gemm(Op opA, Op opB, T alpha, const Matrix<T>& A, const Matrix<T>& B, T bet
           const Options& opts = {});
 // B = op(A) (B: n x m for Trans / ConjTrans), same grid and tile size
 template <typename T> void copy(Op op, const Matrix<T>& A, Matrix<T>& B);
+// B = A between ANY two block-cyclic layouts of the same global shape (tile
+// sizes and p x q grids may differ): one batched point-to-point exchange of
+// the separable owner blocks (SLATE redistribute, slate.hh:426)
+template <typename T> void redistribute(const Matrix<T>& A, Matrix<T>& B);
 // B = alpha op(A)^{-1} B, A triangular (the uplo triangle of A's storage),
 // Side::Left, op NoTrans or ConjTrans; distributed forward / backward
 // substitution by tile steps

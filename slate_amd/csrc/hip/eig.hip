@@ -82,7 +82,7 @@ template <typename T, int B>
 __global__ void __launch_bounds__(256)
 unmtr_hb2st_blk_kernel(i64 n, i64 ncols, T* __restrict__ Z, i64 ldz, const T* __restrict__ V,
                        const T* __restrict__ tau, const i64* __restrict__ sp, const i64* __restrict__ nt,
-                       i64 nsw, int conj_tau) {
+                       i64 nsw, int conj_tau, i64 Jlo, i64 Jhi, i64 slot0) {
     // 8 threads per column, B/4 window rows each (2B-row window); 32 columns
     constexpr int TPC = 8, CW = 32, NT = TPC * CW, RPT = 2 * B / TPC, HALF = TPC / 2;
     __shared__ T Vs[B * B];
@@ -94,7 +94,9 @@ unmtr_hb2st_blk_kernel(i64 n, i64 ncols, T* __restrict__ Z, i64 ldz, const T* __
     const bool colok = col < ncols;
     T* zc = Z + (colok ? col : 0) * ldz;
     T z[RPT];
-    for (i64 J = (nsw - 1) / B; J >= 0; --J) {
+    // sweep blocks [Jlo, Jhi] only; V / tau hold the slots from slot0 on (a
+    // chunk of the reflectors: the distributed back-transform streams them)
+    for (i64 J = min(Jhi, (nsw - 1) / B); J >= Jlo; --J) {
         const i64 j0 = J * B, jn = min((i64)B, nsw - j0);
         const i64 TJ = nt[j0];                      // tasks per sweep do not grow with j
         if (TJ <= 0) continue;
@@ -111,14 +113,14 @@ unmtr_hb2st_blk_kernel(i64 n, i64 ncols, T* __restrict__ Z, i64 ldz, const T* __
                 i64 slot = -1;
                 if (jj < jn && t < nt[j0 + jj]) slot = sp[j0 + jj] + t;
                 sslot[jj] = slot;
-                const T tv = slot >= 0 ? tau[slot] : s_zero(T());
+                const T tv = slot >= 0 ? tau[slot - slot0] : s_zero(T());
                 taus[jj] = conj_tau ? s_conj(tv) : tv;
             }
             __syncthreads();
             for (int idx = tid; idx < B * B; idx += NT) {
                 const int jj = idx / B, vi = idx - jj * B;
                 const i64 slot = sslot[jj];
-                Vs[idx] = slot >= 0 ? V[slot * B + vi] : s_zero(T());
+                Vs[idx] = slot >= 0 ? V[(slot - slot0) * B + vi] : s_zero(T());
             }
             __syncthreads();
             for (int jj = B - 1; jj >= 0; --jj) {
@@ -182,16 +184,16 @@ unmtr_hb2st_blk_kernel(i64 n, i64 ncols, T* __restrict__ Z, i64 ldz, const T* __
 }
 
 template <typename T>
-bool unmtr_hb2st_blocked(i64 n, i64 ncols, T* Z, i64 ldz, const T* V, i64 b, const T* tau, const i64* sp,
-                         const i64* nt, i64 nsw, bool conj_tau, hipStream_t s) {
-    if (ncols <= 0 || nsw <= 0) return true;
+bool unmtr_hb2st_blocked_range(i64 n, i64 ncols, T* Z, i64 ldz, const T* V, i64 b, const T* tau, const i64* sp,
+                               const i64* nt, i64 nsw, bool conj_tau, i64 Jlo, i64 Jhi, i64 slot0, hipStream_t s) {
+    if (ncols <= 0 || nsw <= 0 || Jhi < Jlo) return true;
     dim3 grid((unsigned)((ncols + 31) / 32));     // 32 columns, 256 threads per workgroup
     if (b == 64) {
         hipLaunchKernelGGL((unmtr_hb2st_blk_kernel<T, 64>), grid, dim3(256), 0, s, n, ncols, Z, ldz, V, tau, sp,
-                           nt, nsw, conj_tau ? 1 : 0);
+                           nt, nsw, conj_tau ? 1 : 0, Jlo, Jhi, slot0);
     } else if (b == 32) {
         hipLaunchKernelGGL((unmtr_hb2st_blk_kernel<T, 32>), grid, dim3(256), 0, s, n, ncols, Z, ldz, V, tau, sp,
-                           nt, nsw, conj_tau ? 1 : 0);
+                           nt, nsw, conj_tau ? 1 : 0, Jlo, Jhi, slot0);
     } else {
         return false;                               // caller falls back to one launch per sweep
     }
@@ -199,9 +201,17 @@ bool unmtr_hb2st_blocked(i64 n, i64 ncols, T* Z, i64 ldz, const T* V, i64 b, con
     return true;
 }
 
+template <typename T>
+bool unmtr_hb2st_blocked(i64 n, i64 ncols, T* Z, i64 ldz, const T* V, i64 b, const T* tau, const i64* sp,
+                         const i64* nt, i64 nsw, bool conj_tau, hipStream_t s) {
+    return unmtr_hb2st_blocked_range<T>(n, ncols, Z, ldz, V, b, tau, sp, nt, nsw, conj_tau, 0, (i64)1 << 60, 0, s);
+}
+
 #define INST2(T) \
     template bool unmtr_hb2st_blocked<T>(i64, i64, T*, i64, const T*, i64, const T*, const i64*, const i64*, i64, \
-                                         bool, hipStream_t);
+                                         bool, hipStream_t); \
+    template bool unmtr_hb2st_blocked_range<T>(i64, i64, T*, i64, const T*, i64, const T*, const i64*, const i64*, \
+                                               i64, bool, i64, i64, i64, hipStream_t);
 INST2(float) INST2(double) INST2(ccplx) INST2(zcplx)
 #undef INST2
 

@@ -140,6 +140,11 @@ void apply_refl_batch(i64 ncols, T* Z, i64 ldz, const T* V, i64 b, const T* tau,
 template <typename T>
 bool unmtr_hb2st_blocked(i64 n, i64 ncols, T* Z, i64 ldz, const T* V, i64 b, const T* tau, const i64* sp,
                          const i64* nt, i64 nsw, bool conj_tau, hipStream_t s);
+// sweep blocks [Jlo, Jhi] of b sweeps only, V / tau holding the slots from
+// slot0 on (a streamed chunk of the reflectors)
+template <typename T>
+bool unmtr_hb2st_blocked_range(i64 n, i64 ncols, T* Z, i64 ldz, const T* V, i64 b, const T* tau, const i64* sp,
+                               const i64* nt, i64 nsw, bool conj_tau, i64 Jlo, i64 Jhi, i64 slot0, hipStream_t s);
 bool unmtr_hb2st_mfma(i64 n, i64 ncols, double* Z, i64 ldz, const double* V, i64 b, const double* tau,
                       const i64* sp, const i64* nt, const i64* gJ, const i64* gt, const i64* gptr, i64 ngroups,
                       double* Tg, i64 nsw, hipStream_t s);

@@ -18,6 +18,7 @@
 // itself runs stage 2 and the tridiagonal solver on one node).
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <numeric>
 #include <vector>
@@ -103,30 +104,35 @@ void dc_tree(i64 a, i64 b, int t, i64 leaf, std::vector<std::pair<i64, i64>>& le
     dc_tree(m, b, t + 1, leaf, leaves, levels);
 }
 
-void dc_merge(const Merge& g, double rho, std::vector<double>& w, double* Q, i64 ldq, hipStream_t s) {
+// One merge on the rows [r0, r1) of the eigenvector matrix that this process
+// holds (Q: those rows of every column, ld ldq; the whole matrix for one
+// process).  z = [last row of the top child's vectors, first row of the
+// bottom child's] (host, b - a entries, identical on every rank), so the
+// host deflation / secular logic gives the same eigenvalues everywhere and
+// each rank updates only its rows: permutations, rotations and laed3's split
+// GEMM act on nr = |[a, b) n [r0, r1)| rows (models/stedc.py _merge).
+void dc_merge_rows(const Merge& g, double rho, std::vector<double>& w, const std::vector<double>& z, double* Q,
+                   i64 ldq, i64 r0, i64 r1, hipStream_t s) {
     const i64 a = g.a, m = g.m, b = g.b, S = b - a;
+    const i64 lo = std::max(a, r0), hi = std::min(b, r1), nr = std::max<i64>(hi - lo, 0);
+    const i64 split = std::min(std::max<i64>(m - lo, 0), nr);     // local rows [0, split) are the top child's
     std::vector<std::unique_ptr<Scratch>> keep;
-    // children eigenvalues (host) and z = [last row of Q1; first row of Q2]
-    std::vector<double> dd(w.begin() + a, w.begin() + b), z((size_t)S);
-    {
-        // one row of a column range = a 1 x k block copy (kernel, ld 1)
-        Scratch zr((size_t)S * sizeof(double), s);
-        copy2d(zr.as<double>(), 1, Q + (m - 1) + a * ldq, ldq, 1, m - a, s);
-        copy2d(zr.as<double>() + (m - a), 1, Q + m + m * ldq, ldq, 1, b - m, s);
-        z = download_vec<double>(zr.p, (size_t)S, s);
-    }
-    double* Qm = Q + a + a * ldq;                 // the merge's S x S block (rows a..b of columns a..b)
-    Scratch Qs((size_t)S * S * sizeof(double), s);
+    std::vector<double> dd(w.begin() + a, w.begin() + b);
+    double* Qm = Q + (lo - r0) + a * ldq;          // my rows of the merge's columns
+    const i64 lds = std::max<i64>(nr, 1);
+    Scratch Qs((size_t)lds * S * sizeof(double), s);
     double* qs = Qs.as<double>();
-    auto permute_cols = [&](const std::vector<i64>& o, const double* src, double* dst) {
+    auto permute_cols = [&](const std::vector<i64>& o, const double* src, i64 ld_src, double* dst, i64 ld_dst) {
+        if (!nr) return;
         Scratch* id = upload_vec(keep, o, s);
-        slate_hip::cols_copy(S, S, src, ldq, id->as<i64>(), dst, S, false, s);
+        slate_hip::cols_copy(nr, S, src, ld_src, id->as<i64>(), dst, ld_dst, false, s);
     };
     if (rho == 0.0) {
         const std::vector<i64> o = argsort(dd);
-        permute_cols(o, Qm, qs);
-        copy2d(Qm, ldq, qs, S, S, S, s);
+        permute_cols(o, Qm, ldq, qs, lds);
+        if (nr) copy2d(Qm, ldq, qs, lds, nr, S, s);
         for (i64 i = 0; i < S; ++i) w[a + i] = dd[o[i]];
+        NHIP(hipStreamSynchronize(s));
         return;
     }
     const bool flip = rho < 0;
@@ -143,7 +149,7 @@ void dc_merge(const Merge& g, double rho, std::vector<double>& w, double* Q, i64
         z2[i] = z[order[i]];
         ty[i] = order[i] < (m - a) ? 1 : 2;
     }
-    permute_cols(order, Qm, qs);
+    permute_cols(order, Qm, ldq, qs, lds);
     // ---- deflation: tiny z components, then Givens chains over close poles
     const double eps = std::numeric_limits<double>::epsilon();
     double zz = 0, dmax = 0;
@@ -185,12 +191,12 @@ void dc_merge(const Merge& g, double rho, std::vector<double>& w, double* Q, i64
             kp[u - 1] = 1;
             t = u;
         }
-        if (!rI.empty()) {
+        if (!rI.empty() && nr) {
             Scratch* I = upload_vec(keep, rI, s);
             Scratch* J = upload_vec(keep, rJ, s);
             Scratch* C = upload_vec(keep, rC, s);
             Scratch* Sn = upload_vec(keep, rS, s);
-            slate_hip::rot_cols(S, qs, S, (i64)rI.size(), I->as<i64>(), J->as<i64>(), C->as<double>(),
+            slate_hip::rot_cols(nr, qs, lds, (i64)rI.size(), I->as<i64>(), J->as<i64>(), C->as<double>(),
                                 Sn->as<double>(), s);
         }
         for (i64 u = 0; u < nn; ++u)
@@ -214,46 +220,50 @@ void dc_merge(const Merge& g, double rho, std::vector<double>& w, double* Q, i64
         // of type 1 | 3, the bottom rows only those of type 2 | 3
         struct Part { i64 r0, r1; std::vector<i64> sel; };
         std::vector<Part> parts;
-        parts.push_back({0, m - a, {}});
-        parts.push_back({m - a, S, {}});
+        parts.push_back({0, split, {}});
+        parts.push_back({split, nr, {}});
         for (i64 i = 0; i < k; ++i) {
             if (ty[Kidx[i]] & 1) parts[0].sel.push_back(i);
             if (ty[Kidx[i]] & 2) parts[1].sel.push_back(i);
         }
-        Scratch* Kd = upload_vec(keep, Kidx, s);
-        std::vector<std::unique_ptr<Scratch>> srcs;
-        std::vector<Scratch*> seld;
-        for (auto& pt : parts) {
-            const i64 nr = pt.r1 - pt.r0, ns = (i64)pt.sel.size();
-            if (!ns || !nr) { srcs.push_back(nullptr); seld.push_back(nullptr); continue; }
-            std::vector<i64> cols((size_t)ns);
-            for (i64 i = 0; i < ns; ++i) cols[i] = Kidx[pt.sel[i]];
-            Scratch* cd = upload_vec(keep, cols, s);
-            srcs.push_back(std::make_unique<Scratch>((size_t)nr * ns * sizeof(double), s));
-            slate_hip::cols_copy(nr, ns, qs + pt.r0, S, cd->as<i64>(), srcs.back()->as<double>(), nr, false, s);
-            seld.push_back(upload_vec(keep, pt.sel, s));
-        }
-        const i64 CH = 4096;
-        for (i64 j0 = 0; j0 < k; j0 += CH) {
-            const i64 nc = std::min(CH, k - j0);
-            Scratch V((size_t)k * nc * sizeof(double), s);
-            slate_hip::stedc_vectors(k, dKd->as<double>(), zh.as<double>(), org.as<i64>(), mu.as<double>(), j0, nc,
-                                     V.as<double>(), k, s);
-            for (size_t pi = 0; pi < parts.size(); ++pi) {
-                const Part& pt = parts[pi];
-                const i64 nr = pt.r1 - pt.r0, ns = (i64)pt.sel.size();
-                if (!nr) continue;
-                Scratch out((size_t)nr * nc * sizeof(double), s);
-                if (ns) {
-                    Scratch Vp((size_t)ns * nc * sizeof(double), s);
-                    slate_hip::permute_rows_gather<double>(ns, nc, V.as<double>(), k, Vp.as<double>(), ns,
-                                                           seld[pi]->as<i64>(), s);
-                    gemm_k<double>('N', 'N', nr, nc, ns, 1.0, srcs[pi]->as<double>(), nr, Vp.as<double>(), ns, 0.0,
-                                   out.as<double>(), nr, s);
-                } else {
-                    NHIP(hipMemsetAsync(out.p, 0, (size_t)nr * nc * sizeof(double), s));
+        if (nr) {
+            Scratch* Kd = upload_vec(keep, Kidx, s);
+            std::vector<std::unique_ptr<Scratch>> srcs;
+            std::vector<Scratch*> seld;
+            for (auto& pt : parts) {
+                const i64 np = pt.r1 - pt.r0, ns = (i64)pt.sel.size();
+                if (!ns || !np) { srcs.push_back(nullptr); seld.push_back(nullptr); continue; }
+                std::vector<i64> cols((size_t)ns);
+                for (i64 i = 0; i < ns; ++i) cols[i] = Kidx[pt.sel[i]];
+                Scratch* cd = upload_vec(keep, cols, s);
+                srcs.push_back(std::make_unique<Scratch>((size_t)np * ns * sizeof(double), s));
+                slate_hip::cols_copy(np, ns, qs + pt.r0, lds, cd->as<i64>(), srcs.back()->as<double>(), np, false, s);
+                seld.push_back(upload_vec(keep, pt.sel, s));
+            }
+            // rank-one vector columns per chunk: at most ~the merge block's
+            // size (a row-distributed merge holds only nr of the S rows)
+            const i64 CH = std::max<i64>(256, std::min<i64>(4096, (nr * S) / std::max<i64>(k, 1)));
+            for (i64 j0 = 0; j0 < k; j0 += CH) {
+                const i64 nc = std::min(CH, k - j0);
+                Scratch V((size_t)k * nc * sizeof(double), s);
+                slate_hip::stedc_vectors(k, dKd->as<double>(), zh.as<double>(), org.as<i64>(), mu.as<double>(), j0,
+                                         nc, V.as<double>(), k, s);
+                for (size_t pi = 0; pi < parts.size(); ++pi) {
+                    const Part& pt = parts[pi];
+                    const i64 np = pt.r1 - pt.r0, ns = (i64)pt.sel.size();
+                    if (!np) continue;
+                    Scratch out((size_t)np * nc * sizeof(double), s);
+                    if (ns) {
+                        Scratch Vp((size_t)ns * nc * sizeof(double), s);
+                        slate_hip::permute_rows_gather<double>(ns, nc, V.as<double>(), k, Vp.as<double>(), ns,
+                                                               seld[pi]->as<i64>(), s);
+                        gemm_k<double>('N', 'N', np, nc, ns, 1.0, srcs[pi]->as<double>(), np, Vp.as<double>(), ns,
+                                       0.0, out.as<double>(), np, s);
+                    } else {
+                        NHIP(hipMemsetAsync(out.p, 0, (size_t)np * nc * sizeof(double), s));
+                    }
+                    slate_hip::cols_copy(np, nc, out.as<double>(), np, Kd->as<i64>() + j0, qs + pt.r0, lds, true, s);
                 }
-                slate_hip::cols_copy(nr, nc, out.as<double>(), nr, Kd->as<i64>() + j0, qs + pt.r0, S, true, s);
             }
         }
     }
@@ -261,16 +271,27 @@ void dc_merge(const Merge& g, double rho, std::vector<double>& w, double* Q, i64
         for (auto& x : lam) x = -x;
     const std::vector<i64> o2 = argsort(lam);
     for (i64 i = 0; i < S; ++i) w[a + i] = lam[o2[i]];
-    Scratch* od = upload_vec(keep, o2, s);
-    slate_hip::cols_copy(S, S, qs, S, od->as<i64>(), Qm, ldq, false, s);
+    if (nr) {
+        Scratch* od = upload_vec(keep, o2, s);
+        slate_hip::cols_copy(nr, S, qs, lds, od->as<i64>(), Qm, ldq, false, s);
+    }
     NHIP(hipStreamSynchronize(s));
 }
 
-void stedc_device(i64 n, const std::vector<double>& d, const std::vector<double>& e, std::vector<double>& w,
-                  double* Q, i64 ldq, hipStream_t s) {
+// Divide & conquer with the eigenvector matrix distributed by ROWS: this
+// process holds rows [r0, r1) of every column (Q, ld ldq), w (all n
+// eigenvalues) ends identical on every rank.  Every rank solves every leaf
+// (their eigenvalues are needed by all; only its rows of the leaf vectors
+// are stored), and per tree level ONE all-reduce of n doubles over `comm`
+// assembles the merges' z vectors from the rows' owners (the reference's
+// stedc_z_vector.cc:94 MPI_Allreduce).  comm == nullptr: one process, all
+// rows (r0 = 0, r1 = n).
+void stedc_rows(i64 n, const std::vector<double>& d, const std::vector<double>& e, std::vector<double>& w,
+                double* Q, i64 ldq, i64 r0, i64 r1, Comm* comm, hipStream_t s) {
     w.assign((size_t)n, 0.0);
     if (n == 0) return;
-    NHIP(hipMemsetAsync(Q, 0, (size_t)ldq * n * sizeof(double), s));
+    const i64 nr = std::max<i64>(r1 - r0, 0);
+    if (nr) NHIP(hipMemsetAsync(Q, 0, (size_t)ldq * n * sizeof(double), s));
     std::vector<std::pair<i64, i64>> leaves;
     std::vector<std::vector<Merge>> levels;
     dc_tree(0, n, 0, 128, leaves, levels);
@@ -295,13 +316,33 @@ void stedc_device(i64 n, const std::vector<double>& d, const std::vector<double>
         Scratch wd((size_t)n * sizeof(double), s), fails(sizeof(i64), s);
         NHIP(hipMemsetAsync(fails.p, 0, sizeof(i64), s));
         slate_hip::steqr_leaves((i64)leaves.size(), lod->as<i64>(), hid->as<i64>(), dd->as<double>(),
-                                ed->as<double>(), wd.as<double>(), Q, ldq, 0, n, fails.as<i64>(), s, (int)mx, 60);
+                                ed->as<double>(), wd.as<double>(), Q, ldq, r0, r1, fails.as<i64>(), s, (int)mx, 60);
         w = download_vec<double>(wd.p, (size_t)n, s);
         if (download_vec<i64>(fails.p, 1, s)[0])
             throw Error("native heev: a divide & conquer leaf did not converge");
     }
-    for (int t = (int)levels.size() - 1; t >= 0; --t)
-        for (auto& g : levels[t]) dc_merge(g, e[g.m - 1], w, Q, ldq, s);
+    Scratch zb((size_t)n * sizeof(double), s);
+    for (int t = (int)levels.size() - 1; t >= 0; --t) {
+        // z of every merge of this level from the owners of rows m - 1 and m
+        NHIP(hipMemsetAsync(zb.p, 0, (size_t)n * sizeof(double), s));
+        double* z = zb.as<double>();
+        for (auto& g : levels[t]) {
+            if (g.m - 1 >= r0 && g.m - 1 < r1)
+                copy2d(z + g.a, 1, Q + (g.m - 1 - r0) + g.a * ldq, ldq, 1, g.m - g.a, s);
+            if (g.m >= r0 && g.m < r1) copy2d(z + g.m, 1, Q + (g.m - r0) + g.m * ldq, ldq, 1, g.b - g.m, s);
+        }
+        if (comm && comm->size > 1) comm->allreduce(zb.p, (size_t)n, DT::F64, 's', s);
+        const std::vector<double> zh = download_vec<double>(zb.p, (size_t)n, s);
+        for (auto& g : levels[t])
+            dc_merge_rows(g, e[g.m - 1], w, std::vector<double>(zh.begin() + g.a, zh.begin() + g.b), Q, ldq, r0, r1,
+                          s);
+    }
+}
+
+// one process: every row
+void stedc_device(i64 n, const std::vector<double>& d, const std::vector<double>& e, std::vector<double>& w,
+                  double* Q, i64 ldq, hipStream_t s) {
+    stedc_rows(n, d, e, w, Q, ldq, 0, n, nullptr, s);
 }
 
 // ---------------------------------------------------------------- stage 1
@@ -640,13 +681,433 @@ void symmetrize(i64 n, T* D, Uplo uplo, hipStream_t s) {
     slate_hip::gecopy_mask_merge<K<T>>(other, n, n, kp(Tt.as<T>()), n, kp(D), n, s);
 }
 
+// ================================================================ heev on a p x q grid
+// No rank ever holds an n x n matrix (models/eig_dist.py is the Python twin;
+// reference src/heev.cc:132-205, src/he2hb.cc:26-677, he2hbGather of
+// HermitianBandMatrix.hh:310, src/unmtr_hb2st.cc, src/unmtr_he2hb.cc):
+//   * F = A with both triangles on A's grid with tile b = 64 (redistribute);
+//   * he2hb_grid: per panel the tile column is all-gathered inside its
+//     process column and QR-factored there (redundantly, deterministic
+//     kernels), the factored rows written back (R + reflectors, the SLATE
+//     layout), V and T broadcast along the process rows; Y = A22 V T is one
+//     local GEMM summed over the process row, M = (V T)^H Y summed over the
+//     process column, W = Y - V M / 2 assembled by one column all-reduce,
+//     and A22 -= [V W] [W V]^H is one local GEMM of inner size 2b;
+//   * the band (O(n b) words) is summed to every rank; rank 0 chases it on
+//     the GPU in a SKEWED band layout (element (i, j) at off + i + j lda with
+//     lda = 4b + 8: the chase only touches |i - j| < 2b, so the dense-window
+//     kernel runs on (4b + 9) n words instead of n^2);
+//   * divide & conquer with the eigenvector rows distributed (stedc_rows);
+//   * Q2 (the chase's reflectors) on a 1 x P column-cyclic Z, the reflectors
+//     streamed from rank 0 in chunks of sweep blocks (never all n^2 / 2 words
+//     at once); Q1 on F's grid, the panel reflectors read back from F and
+//     broadcast along the process rows; Z onto the caller's layout.
+// Every layout change is one redistribute() (separable owner blocks, one
+// batched point-to-point exchange).
+template <typename T>
+struct GPanel { i64 k, r0, kk; std::unique_ptr<Scratch> T_; };
+
+template <typename T>
+__global__ void band_from_stack_kernel(i64 n, int b, const T* __restrict__ st, i64 lds, T* __restrict__ A, i64 lda) {
+    // one thread per (i - j, j) with |i - j| <= b; the stack holds, per tile
+    // column k (columns k b ..), the diagonal tile's lower triangle in rows
+    // [0, b) and the sub-diagonal R block's upper triangle in rows [b, 2b)
+    const i64 j = blockIdx.x;
+    const int dlt = (int)threadIdx.x - b;              // i - j
+    if (j >= n || threadIdx.x > 2 * b) return;
+    const i64 i = j + dlt;
+    if (i < 0 || i >= n) return;
+    const i64 r = i > j ? i : j, c = i > j ? j : i;    // the lower-triangle element
+    const i64 c0 = (c / b) * b;
+    const T v = (r < c0 + b) ? st[(r - c0) + c * lds] : st[b + (r - c0 - b) + c * lds];
+    T out = v;
+    if (i == j) {
+        if constexpr (slate_hip::scalar_traits<T>::is_complex) out.im = 0;
+    } else if (i < j) {
+        out = slate_hip::s_conj(v);
+    }
+    A[i + j * lda] = out;
+}
+
+template <typename T>
+void he2hb_grid(Storage& F, std::vector<GPanel<T>>& pans, hipStream_t s) {
+    GridComms* gc = F.gc;
+    const int p = F.p, q = F.q, pr = F.pr, pc = F.pc;
+    const i64 nb = F.nb, n = F.n, mloc = F.mloc, nloc = F.nloc, lld = F.lld;
+    const i64 nt = (n + nb - 1) / nb;
+    T* buf = static_cast<T*>(F.buf);
+    const char ct = ctrans<T>();
+    const size_t es = sizeof(T);
+    std::vector<std::unique_ptr<Scratch>> keep;
+    for (i64 k = 0; k + 1 < nt; ++k) {
+        keep.clear();
+        const i64 r0 = (k + 1) * nb, kb = std::min(nb, n - k * nb), m2 = n - r0, kk = std::min(m2, kb);
+        const int ck = (int)(k % q);
+        const i64 lr0 = std::min(tiles_before(k + 1, p, pr) * nb, mloc), nmine = mloc - lr0;
+        const i64 lc_k = tiles_before(k, q, pc) * nb;
+        const i64 lc1 = std::min(tiles_before(k + 1, q, pc) * nb, nloc), ncl = nloc - lc1;
+        std::vector<i64> rowidx((size_t)nmine), colidx((size_t)ncl);
+        for (i64 r = 0; r < nmine; ++r) rowidx[r] = l2g(lr0 + r, nb, p, pr) - r0;
+        for (i64 c = 0; c < ncl; ++c) colidx[c] = l2g(lc1 + c, nb, q, pc) - r0;
+        i64* rid = upload_vec(keep, rowidx, s)->template as<i64>();
+        i64* cid = upload_vec(keep, colidx, s)->template as<i64>();
+        Scratch VT((size_t)(m2 * kk + kk * kk) * es, s);
+        T* Vf = VT.as<T>();
+        T* Tk = Vf + m2 * kk;
+        if (pc == ck) {
+            // the panel rows of every process row, padded to the longest
+            std::vector<i64> cnt((size_t)p);
+            i64 maxc = 1;
+            for (int r = 0; r < p; ++r) {
+                const i64 ml = numroc(n, nb, r, p);
+                cnt[r] = ml - std::min(tiles_before(k + 1, p, r) * nb, ml);
+                maxc = std::max(maxc, cnt[r]);
+            }
+            Scratch snd((size_t)maxc * kb * es, s), rcv((size_t)p * maxc * kb * es, s);
+            copy2d(snd.as<T>(), maxc, buf + lr0 + lc_k * lld, lld, nmine, kb, s);
+            if (p > 1) gc->col->allgather(snd.p, rcv.p, (size_t)maxc * kb * es, s);
+            else dcopy(rcv.p, snd.p, (size_t)maxc * kb * es, s);
+            Scratch Pf((size_t)m2 * kb * es, s), tau((size_t)kk * es, s);
+            for (int r = 0; r < p; ++r) {
+                if (!cnt[r]) continue;
+                const i64 l0 = std::min(tiles_before(k + 1, p, r) * nb, numroc(n, nb, r, p));
+                std::vector<i64> g((size_t)cnt[r]);
+                for (i64 i = 0; i < cnt[r]; ++i) g[i] = l2g(l0 + i, nb, p, r) - r0;
+                slate_hip::permute_rows_scatter<K<T>>(cnt[r], kb, kp(rcv.as<T>() + (i64)r * maxc * kb), maxc,
+                                                      kp(Pf.as<T>()), m2, upload_vec(keep, g, s)->template as<i64>(),
+                                                      s);
+            }
+            NHIP(hipMemsetAsync(tau.p, 0, (size_t)kk * es, s));
+            slate_hip::geqrf_panel_ws<K<T>>(m2, kb, kp(Pf.as<T>()), m2, kp(tau.as<T>()), kp(Tk), kk, kp(Vf), m2,
+                                            rt().qr_work, s);
+            // R and the reflectors back into this rank's rows of the panel
+            slate_hip::permute_rows_gather<K<T>>(nmine, kb, kp(Pf.as<T>()), m2, kp(buf + lr0 + lc_k * lld), lld, rid,
+                                                 s);
+        }
+        if (q > 1) gc->row->bcast(VT.p, (size_t)(m2 * kk + kk * kk) * es, ck, s);
+        GPanel<T> pn{k, r0, kk, std::make_unique<Scratch>((size_t)kk * kk * es, s)};
+        copy2d(pn.T_->template as<T>(), kk, Tk, kk, kk, kk, s);
+        pans.push_back(std::move(pn));
+        // X = V T (every rank, m2 x kk)
+        Scratch X((size_t)m2 * kk * es, s);
+        copy2d(X.as<T>(), m2, Vf, m2, m2, kk, s);
+        slate_hip::trmm<K<T>>('R', 'U', 'N', 'N', m2, kk, kv(T(1)), kp(Tk), kk, kp(X.as<T>()), m2, s);
+        // Y = A22 X(my columns), summed over the process row
+        const i64 ldy = std::max<i64>(nmine, 1);
+        Scratch VW((size_t)ldy * 2 * kk * es, s);       // [V_mine | W_mine]
+        T* Vl = VW.as<T>();
+        T* Y = Vl + ldy * kk;
+        if (nmine) {
+            if (ncl) {
+                Scratch Xc((size_t)ncl * kk * es, s);
+                slate_hip::permute_rows_gather<K<T>>(ncl, kk, kp(X.as<T>()), m2, kp(Xc.as<T>()), ncl, cid, s);
+                gemm_k<T>('N', 'N', nmine, kk, ncl, T(1), buf + lr0 + lc1 * lld, lld, Xc.as<T>(), ncl, T(0), Y, ldy, s);
+            } else {
+                slate_hip::geset<K<T>>('G', nmine, kk, kv(T(0)), kv(T(0)), kp(Y), ldy, s);
+            }
+            if (q > 1) gc->row->allreduce(Y, (size_t)(ldy * kk), dt_of<T>::v, 's', s);
+        }
+        // M = X(my rows)^H Y, summed over the process column
+        Scratch M((size_t)kk * kk * es, s);
+        if (nmine) {
+            Scratch Xl((size_t)nmine * kk * es, s);
+            slate_hip::permute_rows_gather<K<T>>(nmine, kk, kp(X.as<T>()), m2, kp(Xl.as<T>()), nmine, rid, s);
+            gemm_k<T>(ct, 'N', kk, kk, nmine, T(1), Xl.as<T>(), nmine, Y, ldy, T(0), M.as<T>(), kk, s);
+            slate_hip::permute_rows_gather<K<T>>(nmine, kk, kp(Vf), m2, kp(Vl), ldy, rid, s);
+        } else {
+            slate_hip::geset<K<T>>('G', kk, kk, kv(T(0)), kv(T(0)), kp(M.as<T>()), kk, s);
+        }
+        if (p > 1) gc->col->allreduce(M.p, (size_t)(kk * kk), dt_of<T>::v, 's', s);
+        // W = Y - V M / 2, then the full W (m2 x kk) by one column all-reduce
+        if (nmine) gemm_k<T>('N', 'N', nmine, kk, kk, T(-0.5), Vl, ldy, M.as<T>(), kk, T(1), Y, ldy, s);
+        Scratch Wf((size_t)m2 * kk * es, s);
+        NHIP(hipMemsetAsync(Wf.p, 0, (size_t)m2 * kk * es, s));
+        if (nmine) slate_hip::permute_rows_scatter<K<T>>(nmine, kk, kp(Y), ldy, kp(Wf.as<T>()), m2, rid, s);
+        if (p > 1) gc->col->allreduce(Wf.p, (size_t)(m2 * kk), dt_of<T>::v, 's', s);
+        // A22 -= [V W] [W V]^H over my trailing block (one GEMM, inner 2 kk)
+        if (nmine && ncl) {
+            Scratch WV((size_t)ncl * 2 * kk * es, s);
+            slate_hip::permute_rows_gather<K<T>>(ncl, kk, kp(Wf.as<T>()), m2, kp(WV.as<T>()), ncl, cid, s);
+            slate_hip::permute_rows_gather<K<T>>(ncl, kk, kp(Vf), m2, kp(WV.as<T>() + ncl * kk), ncl, cid, s);
+            gemm_k<T>('N', ct, nmine, ncl, 2 * kk, T(-1), Vl, ldy, WV.as<T>(), ncl, T(1), buf + lr0 + lc1 * lld, lld, s);
+        }
+        NHIP(hipStreamSynchronize(s));
+    }
+}
+
+// Z := Q1 Z on F's grid (Z shares F's layout); panels last to first
+template <typename T>
+void unmtr_he2hb_grid(const Storage& F, std::vector<GPanel<T>>& pans, Storage& Zs, hipStream_t s) {
+    GridComms* gc = F.gc;
+    const int p = F.p, q = F.q, pr = F.pr, pc = F.pc;
+    const i64 nb = F.nb, mloc = F.mloc, lld = F.lld, nz = Zs.nloc, ldz = Zs.lld;
+    const T* fb = static_cast<const T*>(F.buf);
+    T* Z = static_cast<T*>(Zs.buf);
+    const char ct = ctrans<T>();
+    const size_t es = sizeof(T);
+    for (auto it = pans.rbegin(); it != pans.rend(); ++it) {
+        const i64 k = it->k, kk = it->kk;
+        const int ck = (int)(k % q);
+        const i64 lr0 = std::min(tiles_before(k + 1, p, pr) * nb, mloc), nmine = mloc - lr0;
+        const i64 lc_k = tiles_before(k, q, pc) * nb;
+        Scratch Vl((size_t)std::max<i64>(nmine, 1) * kk * es, s);
+        if (nmine) {
+            if (pc == ck) {
+                if (pr == (int)((k + 1) % p))
+                    slate_hip::v_explicit<K<T>>(nmine, kk, kp(fb + lr0 + lc_k * lld), lld, kp(Vl.as<T>()), nmine, s);
+                else
+                    copy2d(Vl.as<T>(), nmine, fb + lr0 + lc_k * lld, lld, nmine, kk, s);
+            }
+            if (q > 1) gc->row->bcast(Vl.p, (size_t)nmine * kk * es, ck, s);
+        }
+        if (!nz) continue;
+        Scratch W((size_t)kk * nz * es, s);
+        if (nmine) gemm_k<T>(ct, 'N', kk, nz, nmine, T(1), Vl.as<T>(), nmine, Z + lr0, ldz, T(0), W.as<T>(), kk, s);
+        else slate_hip::geset<K<T>>('G', kk, nz, kv(T(0)), kv(T(0)), kp(W.as<T>()), kk, s);
+        if (p > 1) gc->col->allreduce(W.p, (size_t)(kk * nz), dt_of<T>::v, 's', s);
+        slate_hip::trmm<K<T>>('L', 'U', 'N', 'N', kk, nz, kv(T(1)), kp(it->T_->template as<T>()), kk,
+                              kp(W.as<T>()), kk, s);
+        if (nmine) gemm_k<T>('N', 'N', nmine, nz, kk, T(-1), Vl.as<T>(), nmine, W.as<T>(), kk, T(1), Z + lr0, ldz, s);
+        NHIP(hipStreamSynchronize(s));
+    }
+}
+
+// peak device memory of the last heev_grid call on this rank (tests)
+size_t g_heev_grid_peak = 0;
+
+template <typename T>
+int64_t heev_grid(HermitianMatrix<T>& A, std::vector<real_t<T>>& Lambda, Matrix<T>* Z) {
+    NTRACE("heev", nullptr);
+    using Rl = real_t<T>;
+    Runtime& R = rt();
+    hipStream_t s = R.main;
+    const Storage& SA = *A.storage();
+    const i64 n = SA.n, b = 64;
+    const int p = SA.p, q = SA.q, P = R.size;
+    Comm* world = world_comm();
+    size_t free0 = 0, total0 = 0, low = (size_t)-1;
+    auto mark = [&] {
+        size_t f = 0, t = 0;
+        NHIP(hipMemGetInfo(&f, &t));
+        low = std::min(low, f);
+    };
+    NHIP(hipStreamSynchronize(s));
+    NHIP(hipMemGetInfo(&free0, &total0));
+    // ---- F: both triangles, tile b, A's grid
+    Matrix<T> F(n, n, b, p, q);
+    {
+        const Matrix<T> Af = expand_tri<T>(A, A.uplo(), 1);
+        redistribute<T>(Af, F);
+        mark();
+    }
+    std::vector<GPanel<T>> pans;
+    {
+        NTRACE("heev::he2hb", s);
+        he2hb_grid<T>(*F.storage(), pans, s);
+    }
+    mark();
+    // ---- the band to every rank (O(n b)), stage 2 on rank 0
+    const Storage& SF = *F.storage();
+    const i64 nt = (n + b - 1) / b;
+    Scratch stack((size_t)2 * b * n * sizeof(T), s);
+    NHIP(hipMemsetAsync(stack.p, 0, (size_t)2 * b * n * sizeof(T), s));
+    for (i64 k = 0; k < nt; ++k) {
+        if ((int)(k % q) != SF.pc) continue;
+        const i64 c0 = k * b, kb = std::min(b, n - c0), lc = tiles_before(k, q, SF.pc) * b;
+        const T* fb = static_cast<const T*>(SF.buf);
+        if ((int)(k % p) == SF.pr)
+            copy2d(stack.as<T>() + c0 * 2 * b, 2 * b, fb + tiles_before(k, p, SF.pr) * b + lc * SF.lld, SF.lld, kb, kb, s);
+        if (k + 1 < nt && (int)((k + 1) % p) == SF.pr)
+            copy2d(stack.as<T>() + b + c0 * 2 * b, 2 * b, fb + tiles_before(k + 1, p, SF.pr) * b + lc * SF.lld, SF.lld,
+                   std::min(b, n - (k + 1) * b), kb, s);
+    }
+    if (P > 1) world->allreduce(stack.p, (size_t)(2 * b * n), dt_of<T>::v, 's', s);
+    const i64 nsw = std::max<i64>(n - 1, 0);
+    std::vector<i64> ntk((size_t)std::max<i64>(nsw, 1), 0), sp((size_t)std::max<i64>(n, 1), 0);
+    for (i64 j = 0; j < nsw; ++j) {
+        const i64 e0 = std::min(j + b, n - 1), k0 = e0 - j;
+        ntk[j] = k0 <= 1 ? 0 : 1 + (n - 1 - e0 + b - 1) / b;
+    }
+    for (i64 j = 1; j < n; ++j) sp[j] = sp[j - 1] + ntk[j - 1];
+    const i64 total = nsw ? sp[n - 1] + ntk[nsw - 1] : 0;
+    std::vector<std::unique_ptr<Scratch>> keep;
+    Scratch* ntd = upload_vec(keep, ntk, s);
+    Scratch* spd = upload_vec(keep, sp, s);
+    const bool cplx = is_cplx<T>();
+    // host record broadcast from rank 0: d (n), e (n - 1), phases (2n), error
+    std::vector<double> rec((size_t)(n + std::max<i64>(n - 1, 0) + 2 * n + 1), 0.0);
+    std::unique_ptr<Scratch> V2, tau2;
+    std::string msg;
+    if (R.rank == 0) {
+        try {
+            NTRACE("heev::hb2st", s);
+            const i64 lda = 4 * b + 8, off = 2 * b;
+            const size_t words = (size_t)(off + lda * n + 16);
+            Scratch Bh(words * sizeof(T), s);
+            NHIP(hipMemsetAsync(Bh.p, 0, words * sizeof(T), s));
+            T* Ab = Bh.as<T>() + off;
+            hipLaunchKernelGGL(band_from_stack_kernel<K<T>>, dim3((unsigned)n), dim3((unsigned)(2 * b + 1)), 0, s,
+                               n, (int)b, kp(stack.as<T>()), 2 * b, kp(Ab), lda);
+            NHIP(hipGetLastError());
+            V2 = std::make_unique<Scratch>((size_t)std::max<i64>(total, 1) * b * sizeof(T), s);
+            tau2 = std::make_unique<Scratch>((size_t)std::max<i64>(total, 1) * sizeof(T), s);
+            Scratch row((size_t)std::max<i64>(total, 1) * sizeof(i64), s), len((size_t)std::max<i64>(total, 1) * sizeof(i64), s);
+            NHIP(hipMemsetAsync(V2->p, 0, (size_t)std::max<i64>(total, 1) * b * sizeof(T), s));
+            NHIP(hipMemsetAsync(tau2->p, 0, (size_t)std::max<i64>(total, 1) * sizeof(T), s));
+            if (nsw > 0 && total > 0) {
+                Scratch work((size_t)(nsw + 2) * sizeof(int), s);
+                NHIP(hipMemsetAsync(work.p, 0, (size_t)(nsw + 2) * sizeof(int), s));
+                hipDeviceProp_t prp;
+                NHIP(hipGetDeviceProperties(&prp, R.device));
+                const i64 nt0 = ntk[0] ? ntk[0] : 1, lag = 2;
+                const int nwg = (int)std::min<i64>({std::max<i64>(nsw, 1), (i64)prp.multiProcessorCount,
+                                                    std::max<i64>(8, std::min(nt0 / lag + 8, nt0 / 3 + 15))});
+                slate_hip::hb2st_device<K<T>>(n, (int)b, kp(Ab), lda, kp(V2->template as<T>()),
+                                              kp(tau2->template as<T>()), row.as<i64>(), len.as<i64>(),
+                                              spd->as<i64>(), ntd->as<i64>(), work.as<int>(), nsw, nwg, s);
+            }
+            Scratch dsub((size_t)2 * n * sizeof(T), s);
+            copy2d(dsub.as<T>(), 1, Ab, lda + 1, 1, n, s);
+            if (n > 1) copy2d(dsub.as<T>() + n, 1, Ab + 1, lda + 1, 1, n - 1, s);
+            const std::vector<T> ds = download_vec<T>(dsub.p, (size_t)(2 * n), s);
+            std::vector<T> ph((size_t)n, T(1));
+            for (i64 i = 0; i < n; ++i) rec[i] = (double)std::real(ds[i]);
+            for (i64 i = 0; i + 1 < n; ++i) {
+                const T sub = ds[n + i];
+                if constexpr (is_cplx<T>()) {
+                    const Rl a = std::abs(sub);
+                    const T u = a > Rl(0) ? sub / a : T(1);
+                    ph[i + 1] = ph[i] * u;
+                    rec[n + i] = (double)a;
+                } else {
+                    rec[n + i] = (double)sub;
+                }
+            }
+            const i64 po = n + std::max<i64>(n - 1, 0);
+            for (i64 i = 0; i < n; ++i) {
+                rec[po + 2 * i] = (double)std::real(ph[i]);
+                rec[po + 2 * i + 1] = (double)std::imag(ph[i]);
+            }
+            mark();
+        } catch (const std::exception& e) {
+            rec.back() = 1;
+            msg = e.what();
+        }
+    }
+    if (P > 1) {
+        Scratch rb(rec.size() * sizeof(double), s);
+        if (R.rank == 0) upload(rb.p, rec.data(), rec.size() * sizeof(double), s);
+        world->bcast(rb.p, rec.size() * sizeof(double), 0, s);
+        rec = download_vec<double>(rb.p, rec.size(), s);
+    }
+    if (rec.back() != 0) throw Error(R.rank == 0 ? msg : std::string("native heev: stage 2 failed on rank 0"));
+    std::vector<double> d(rec.begin(), rec.begin() + n), e(rec.begin() + n, rec.begin() + n + std::max<i64>(n - 1, 0));
+    std::vector<double> w;
+    if (!Z) {
+        std::vector<double> ee(e);
+        ee.resize((size_t)n, 0.0);
+        if (slate_tridiag::steqr_impl<double>(n, d.data(), ee.data(), nullptr, 1, 0))
+            throw Error("native heev: the tridiagonal QL iteration did not converge");
+        Lambda.assign(d.begin(), d.end());
+        return 0;
+    }
+    // ---- tridiagonal eigenvectors, rows distributed: rank r rows [r mb, ...)
+    const i64 mb = (n + P - 1) / P;
+    Matrix<T> Zrow(n, n, mb, P, 1);
+    {
+        NTRACE("heev::stedc", s);
+        const Storage& SR = *Zrow.storage();
+        const i64 r0 = std::min<i64>((i64)R.rank * mb, n), nr = SR.mloc;
+        Scratch Qr((size_t)std::max<i64>(nr, 1) * n * sizeof(double), s);
+        stedc_rows(n, d, e, w, Qr.as<double>(), std::max<i64>(nr, 1), r0, r0 + nr, world, s);
+        mark();
+        std::vector<T> ph((size_t)n);
+        const i64 po = n + std::max<i64>(n - 1, 0);
+        for (i64 i = 0; i < n; ++i) {
+            if constexpr (is_cplx<T>()) ph[i] = T((Rl)rec[po + 2 * i], (Rl)rec[po + 2 * i + 1]);
+            else ph[i] = T(1);
+        }
+        Scratch* phd = cplx ? upload_vec(keep, ph, s) : nullptr;
+        if (nr) real_to_phase<T>(nr, n, Qr.as<double>(), std::max<i64>(nr, 1), phd ? kp(phd->as<T>() + r0) : nullptr,
+                                 kp(static_cast<T*>(SR.buf)), SR.lld, s);
+        NHIP(hipStreamSynchronize(s));
+    }
+    // ---- Q2 on a 1 x P column-cyclic Z, reflectors streamed from rank 0
+    Matrix<T> Zc(n, n, b, 1, P);
+    redistribute<T>(Zrow, Zc);
+    Zrow = Matrix<T>();
+    {
+        NTRACE("heev::unmtr_hb2st", s);
+        Storage& SC = *Zc.storage();
+        const i64 ncols = SC.nloc;
+        const i64 nblk = nsw > 0 ? (nsw - 1) / b + 1 : 0;
+        const i64 G = std::max<i64>(1, ncols / 256);          // sweep blocks per chunk (~ <= a quarter of Zc's block)
+        for (i64 Jhi = nblk - 1; Jhi >= 0 && total > 0; Jhi -= G) {
+            const i64 Jlo = std::max<i64>(0, Jhi - G + 1);
+            const i64 s0 = sp[Jlo * b], s1 = (Jhi + 1) * b < nsw ? sp[(Jhi + 1) * b] : total;
+            if (s1 <= s0) continue;
+            const i64 cnt = s1 - s0;
+            std::unique_ptr<Scratch> vb, tb;
+            T* Vc = nullptr;
+            T* tc = nullptr;
+            if (R.rank == 0) {
+                Vc = V2->template as<T>() + s0 * b;
+                tc = tau2->template as<T>() + s0;
+            } else {
+                vb = std::make_unique<Scratch>((size_t)cnt * b * sizeof(T), s);
+                tb = std::make_unique<Scratch>((size_t)cnt * sizeof(T), s);
+                Vc = vb->template as<T>();
+                tc = tb->template as<T>();
+            }
+            if (P > 1) {
+                world->bcast(Vc, (size_t)cnt * b * sizeof(T), 0, s);
+                world->bcast(tc, (size_t)cnt * sizeof(T), 0, s);
+            }
+            if (ncols)
+                slate_hip::unmtr_hb2st_blocked_range<K<T>>(n, ncols, kp(static_cast<T*>(SC.buf)), SC.lld, kp(Vc), b,
+                                                           kp(tc), spd->as<i64>(), ntd->as<i64>(), nsw, false, Jlo,
+                                                           Jhi, s0, s);
+            mark();
+            NHIP(hipStreamSynchronize(s));
+        }
+    }
+    V2.reset();
+    tau2.reset();
+    // ---- Q1 on F's grid, then the caller's layout
+    Matrix<T> Zg(n, n, b, p, q);
+    redistribute<T>(Zc, Zg);
+    Zc = Matrix<T>();
+    {
+        NTRACE("heev::unmtr_he2hb", s);
+        unmtr_he2hb_grid<T>(*F.storage(), pans, *Zg.storage(), s);
+    }
+    mark();
+    redistribute<T>(Zg, *Z);
+    g_heev_grid_peak = free0 > low ? free0 - low : 0;
+    if (const char* mr = std::getenv("SLATE_AMD_NATIVE_MEMREPORT"); mr && *mr == '1') {
+        const double blk = (double)SA.mloc * (double)SA.nloc * sizeof(T);
+        std::fprintf(stderr, "rank %d: heev grid %dx%d n=%lld: peak device growth %.1f MB = %.2f x local block "
+                     "(%.1f MB); n^2 = %.1f MB\n", R.rank, p, q, (long long)n, g_heev_grid_peak / 1e6,
+                     blk > 0 ? g_heev_grid_peak / blk : 0.0, blk / 1e6, (double)n * n * sizeof(T) / 1e6);
+    }
+    Lambda.assign(w.begin(), w.end());
+    return 0;
+}
+
 template <typename T>
 int64_t heev_impl(HermitianMatrix<T>& A, std::vector<real_t<T>>& Lambda, Matrix<T>* Z) {
-    NTRACE("heev", nullptr);
     Runtime& R = rt();
     const Storage& SA = *A.storage();
     if (SA.m != SA.n) throw Error("native heev: square matrix");
     const i64 n = SA.n;
+    {
+        // p x q grids: the distributed solver (no n x n anywhere) unless
+        // SLATE_AMD_NATIVE_HEEV=gather (the one-GPU solver behind a gather)
+        const bool gather = [] { const char* e = std::getenv("SLATE_AMD_NATIVE_HEEV"); return e && !std::strcmp(e, "gather"); }();
+        const bool zok = !Z || (Z->storage()->m == n && Z->storage()->n == n);
+        if (R.size > 1 && SA.p * SA.q == R.size && n > 2 * 64 && !gather && zok) return heev_grid<T>(A, Lambda, Z);
+    }
+    NTRACE("heev", nullptr);
     hipStream_t s = R.main;
     NHIP(hipStreamSynchronize(s));
     if (Z) {

@@ -170,7 +170,7 @@ def hetrf_dist(A, opts=None):
                 W = ops.colmajor_zeros(nmine, nb, dt, dev)
                 if nmine and lc1:
                     Hsel = ops.colmajor_empty(lc1, nb, dt, dev)
-                    Hsel.copy_(Hs.index_select(0, gcol[:lc1]))
+                    ops.row_gather(Hs, Hsel, gcol[:lc1])
                     ops.gemm(-1.0, ll[lr1:mloc, :lc1], Hsel, 0.0, W)
                 if q > 1 and nmine:
                     grid.row_comm.reduce(W, cJ)

@@ -235,6 +235,21 @@ def spin_ns(ns, like):
         kmod(like).spin_ns(float(ns), stream(like))
 
 
+def cols_move(A, B, idx, scatter=False):
+    """B[:, j] = A[:, idx[j]] (gather) or B[:, idx[j]] = A[:, j] (scatter):
+    one launch of the device column-copy kernel, elements of 8 or 16 bytes
+    moved as doubles (callers with other element sizes or CPU tensors use
+    torch's index ops)."""
+    _chk(A); _chk(B, "B")
+    k = A.element_size() // 8
+    nc = (B if not scatter else A).shape[1]
+    if A.shape[0] == 0 or nc == 0:
+        return B
+    _native.hip().cols_copy(A.shape[0] * k, nc, A.data_ptr(), ld(A) * k, idx.data_ptr(), B.data_ptr(), ld(B) * k,
+                            1 if scatter else 0, stream(B))
+    return B
+
+
 def row_gather(A, B, perm):
     """B[i, :] = A[perm[i], :]."""
     m, n = B.shape

@@ -69,16 +69,26 @@ def exchange_lines(comm, data, moves, nb, p, me, axis=0):
     if data.is_cuda:
         idx = idx.pin_memory().to(dev, non_blocking=True)
 
+    # device columns of 8 / 16-byte elements move by the column-copy kernel
+    # (buffer = the c columns back to back); other cases by torch index ops
+    kcols = data.is_cuda and data.element_size() in (8, 16) and data.stride(0) == 1
+
     def gather(ix):
         if axis == 0:
             t = torch.empty(w, ix.numel(), dtype=dt, device=dev)      # (w, c): column-major c x w
             ops.row_gather(data, t.t(), ix)
+            return t
+        if kcols:
+            t = torch.empty(w, ix.numel(), dtype=dt, device=dev)
+            ops.cols_move(data, t.view(ix.numel(), w).t(), ix)        # column j at offset j w
             return t
         return data.index_select(1, ix).contiguous()                  # (w, c): the c columns
 
     def scatter(buf, ix):
         if axis == 0:
             ops.row_scatter(buf.t(), data, ix)
+        elif kcols:
+            ops.cols_move(buf.view(ix.numel(), w).t(), data, ix, scatter=True)
         else:
             data.index_copy_(1, ix, buf)
 

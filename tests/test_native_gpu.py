@@ -134,7 +134,8 @@ def _assert_checks(checks, out):
                                                    "tri_view_uplo", "tri_view_trsm", "trapezoid_norm",
                                                    "slice_roundtrip", "empty_like", "sym_syrk_symm",
                                                    "pbsv", "pbsv_upper", "gbmm", "gbsv", "hbmm_left", "hbmm_right",
-                                                   "tbsm_upper_conj", "getrf_tntpiv", "tntpiv_growth", "hesv")]
+                                                   "tbsm_upper_conj", "getrf_tntpiv", "tntpiv_growth", "hesv",
+                                                   "redistribute")]
     for name in names:
         assert name in checks, (name, out)
         assert float(checks[name]) < TOL[name[-1]], (name, checks[name])
@@ -171,7 +172,13 @@ def test_native_example_grids_host_transport(grid):
     out0 = outs[0][1]
     print(out0)
     assert f"transport host ranks {p * q} grid {grid}" in out0
-    _assert_checks(_checks(out0), out0)
+    checks = _checks(out0)
+    _assert_checks(checks, out0)
+    # the distributed heev (no n x n on any rank) against the gather path
+    for x in "sdcz":
+        name = f"heev_grid_vs_gather_{x}"
+        assert name in checks, (name, out0)
+        assert float(checks[name]) < TOL[x], (name, checks[name])
 
 
 LEXE = os.path.join(ROOT, "slate_amd", "ex_native_lapack")
