@@ -10,6 +10,9 @@
 //   geqrf:         gels of a consistent system B = A0 X0,
 //                  ||A0^H (A0 X - B)|| / (||A0||^2 ||X|| m)
 //
+//   heev:          Z V against Z (Lambda V) through A for 4 random vectors,
+//                  ||A Z V - Z Lambda V|| / (||A|| ||V|| n) (no n x n host data)
+//
 //   bench_native routine n nb p q lookahead warmup steps check [m]
 // prints "RESULT ms_per_step=<max over ranks> info=<info> resid=<r>"
 #include <chrono>
@@ -54,8 +57,19 @@ int main(int argc, char** argv) {
         }
         std::vector<int64_t> ipiv;
         int64_t info = 0;
+        const bool eig = routine == "heev";
+        sn::HermitianMatrix<double> He;
+        sn::Matrix<double> Ze;
+        std::vector<double> lam;
+        if (eig) {
+            He = sn::HermitianMatrix<double>(sn::Uplo::Lower, n, nb, p, q);
+            Ze = sn::Matrix<double>(n, n, nb, p, q);
+        }
         auto step = [&]() {
-            if (chol) {
+            if (eig) {
+                sn::copy(sn::Op::NoTrans, A0, He);
+                info = sn::heev(He, lam, Ze, opts);
+            } else if (chol) {
                 sn::copy(sn::Op::NoTrans, A0, H);
                 info = sn::potrf(H, opts);
             } else if (routine == "getrf") {
@@ -80,7 +94,23 @@ int main(int argc, char** argv) {
             const int64_t nr = 1;
             sn::Matrix<double> V(n, nr, nb, p, q), X(n, nr, nb, p, q);
             V.generate(sn::Gen::Random, 5);
-            if (qr) {
+            if (eig) {
+                const int64_t nv = 4;
+                std::vector<double> hv((size_t)n * nv), hl((size_t)n * nv);
+                sn::Matrix<double> Vr(n, nv, nb, p, q), LV(n, nv, nb, p, q), ZV(n, nv, nb, p, q),
+                    AZV(n, nv, nb, p, q), ZLV(n, nv, nb, p, q);
+                Vr.generate(sn::Gen::Random, 6);
+                Vr.to_host(hv.data(), n);
+                for (int64_t j = 0; j < nv; ++j)
+                    for (int64_t i = 0; i < n; ++i) hl[i + j * n] = lam[i] * hv[i + j * n];
+                LV.from_host(hl.data(), n);
+                sn::gemm(1.0, Ze, Vr, 0.0, ZV);
+                sn::hemm(sn::Side::Left, 1.0, He, ZV, 0.0, AZV);
+                sn::gemm(1.0, Ze, LV, 0.0, ZLV);
+                sn::add(-1.0, ZLV, 1.0, AZV);
+                resid = sn::norm(sn::Norm::Fro, AZV) /
+                        (sn::norm(sn::Norm::Fro, A0) * sn::norm(sn::Norm::Fro, Vr) * (double)n);
+            } else if (qr) {
                 sn::Matrix<double> X0(n, nr, nb, p, q), B(mrows, nr, nb, p, q), R(mrows, nr, nb, p, q), G2(n, nr, nb, p, q);
                 X0.generate(sn::Gen::Random, 5);
                 sn::gemm(1.0, A0, X0, 0.0, B);

@@ -14,6 +14,7 @@
 #include <map>
 #include <mutex>
 #include <unordered_map>
+#include <unordered_set>
 
 #include "common.hpp"
 
@@ -29,6 +30,7 @@ struct DevAlloc {
     std::mutex mu;
     std::multimap<size_t, DevBlock> free_;        // rounded size -> block
     std::unordered_map<void*, size_t> size_;      // live and cached blocks
+    std::unordered_set<void*> cached_;            // blocks in free_ (double-free check)
     size_t reserved = 0;
 };
 
@@ -66,6 +68,7 @@ inline size_t dev_trim_locked(DevAlloc& A) {
         HIP_CHECK(hipEventDestroy(kv.second.ev));
         HIP_CHECK(hipFree(kv.second.p));
         A.size_.erase(kv.second.p);
+        A.cached_.erase(kv.second.p);
         A.reserved -= kv.first;
         freed += kv.first;
     }
@@ -81,6 +84,7 @@ inline void* dev_alloc(size_t bytes, hipStream_t s) {
     auto take = [&](std::multimap<size_t, DevBlock>::iterator it, bool wait) {
         DevBlock b = it->second;
         A.free_.erase(it);
+        A.cached_.erase(b.p);
         if (wait) HIP_CHECK(hipStreamWaitEvent(s, b.ev, 0));
         HIP_CHECK(hipEventDestroy(b.ev));
         return b.p;
@@ -120,6 +124,7 @@ inline void dev_free(void* p, hipStream_t s) {
     std::lock_guard<std::mutex> g(A.mu);
     auto it = A.size_.find(p);
     if (it == A.size_.end()) throw std::invalid_argument("dev_free: unknown block");
+    if (!A.cached_.insert(p).second) throw std::logic_error("dev_free: block freed twice");
     hipEvent_t ev;
     HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     HIP_CHECK(hipEventRecord(ev, s));

@@ -43,6 +43,30 @@ inline i64 hb_lds_bytes() {
 }
 }
 
+__global__ void hb_copy_tail(const unsigned* __restrict__ src, unsigned* __restrict__ dst) { *dst = *src; }
+
+// Working-copy transfers by KERNEL, not hipMemcpyAsync: a copy-engine write
+// into A is not seen by a later kernel that still holds A's old lines in an
+// XCD's L2 (the band buffer is typically a reused cached block; its pre-chase
+// contents were read back instead of the chased band -- native heev probe,
+// profiles/r6).  A kernel's stores take the normal write-back path.
+__global__ void __launch_bounds__(256)
+hb_copy_words(const unsigned long long* __restrict__ src, unsigned long long* __restrict__ dst, size_t nw) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nw; i += (size_t)gridDim.x * 256) dst[i] = src[i];
+}
+inline void hb_copy(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    const size_t nw = bytes / 8;            // element sizes 4 / 8 / 16: pad odd fp32 counts below
+    if (nw) {
+        const unsigned g = (unsigned)std::min<size_t>((nw + 255) / 256, 8192);
+        hipLaunchKernelGGL(hb_copy_words, dim3(g), dim3(256), 0, s, static_cast<const unsigned long long*>(src),
+                           static_cast<unsigned long long*>(dst), nw);
+    }
+    if (bytes % 8)                          // one trailing 4-byte word (fp32, odd count)
+        hipLaunchKernelGGL(hb_copy_tail, dim3(1), dim3(1), 0, s, static_cast<const unsigned*>(src) + 2 * nw,
+                           static_cast<unsigned*>(dst) + 2 * nw);
+    HIP_LAUNCH_CHECK();
+}
+
 // 2-D block moves between global memory and LDS: lanes run along the rows
 // (coalesced), waves along the columns; the (row group, column) pair index
 // is wave-uniform, so the index arithmetic stays on the scalar unit, and U
@@ -444,7 +468,7 @@ hb2st_kernel(i64 n, int b, T* __restrict__ A, i64 lda, T* __restrict__ V, T* __r
 
 template <typename T>
 void hb2st_device(i64 n, int b, T* A, i64 lda, T* V, T* tau, i64* row, i64* len, const i64* sweep_ptr,
-                  const i64* ntask, int* work, i64 nsw, int nwg, hipStream_t s, i64* prof) {
+                  const i64* ntask, int* work, i64 nsw, int nwg, hipStream_t s, i64* prof, i64 extent) {
     if (nsw <= 0) return;
     if (b > HMAXB) throw std::invalid_argument("hb2st_device: bandwidth > 128");
     // work = [ticket, done[0..nsw)] zero-initialised by the caller
@@ -458,11 +482,11 @@ void hb2st_device(i64 n, int b, T* A, i64 lda, T* V, T* tau, i64* row, i64* len,
         return strcmp(e, "finegrained") == 0 ? 1 : 0;
     }();
     T* W = A;
-    const size_t bytes = sizeof(T) * (size_t)lda * (size_t)n;
+    const size_t bytes = sizeof(T) * (extent > 0 ? (size_t)extent : (size_t)lda * (size_t)n);
     if (mode) {
         HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&W), bytes,
                                         mode == 2 ? hipDeviceMallocUncached : hipDeviceMallocFinegrained));
-        HIP_CHECK(hipMemcpyAsync(W, A, bytes, hipMemcpyDeviceToDevice, s));
+        hb_copy(W, A, bytes, s);
     }
     // threads per workgroup: the task's window moves are latency bound (loads
     // in flight per workgroup), SLATE_AMD_HB2ST_THREADS = 256 | 512 | 1024;
@@ -508,7 +532,7 @@ void hb2st_device(i64 n, int b, T* A, i64 lda, T* V, T* tau, i64* row, i64* len,
     else launch(hb2st_kernel<T, 256>, 256);
     HIP_LAUNCH_CHECK();
     if (mode) {
-        HIP_CHECK(hipMemcpyAsync(A, W, bytes, hipMemcpyDeviceToDevice, s));
+        hb_copy(A, W, bytes, s);
         HIP_CHECK(hipStreamSynchronize(s));
         HIP_CHECK(hipFree(W));
     }
@@ -697,7 +721,7 @@ void tb2bd_device(i64 n, int b, T* A, i64 lda, T* UV, T* Utau, i64* Urow, i64* U
     T* W = nullptr;
     const size_t bytes = sizeof(T) * (size_t)lda * (size_t)n;
     HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&W), bytes, hipDeviceMallocUncached));
-    HIP_CHECK(hipMemcpyAsync(W, A, bytes, hipMemcpyDeviceToDevice, s));
+    hb_copy(W, A, bytes, s);
     // 1024 threads (the window moves are latency bound, as hb2st); lag 4:
     // with the exact windows task t of sweep j stays inside
     // [j + (t - 1) b + 1, j + (t + 2) b] and sweep j-1's tasks from t + 4 on
@@ -714,7 +738,7 @@ void tb2bd_device(i64 n, int b, T* A, i64 lda, T* UV, T* Utau, i64* Urow, i64* U
     hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(HT), HLDS, s, n, b, W, lda, UV, Utau, Urow, Ulen, VV, Vtau,
                        Vrow, Vlen, sweep_ptr, ntask, work, work + 1, nsw, lag, HLDS);
     HIP_LAUNCH_CHECK();
-    HIP_CHECK(hipMemcpyAsync(A, W, bytes, hipMemcpyDeviceToDevice, s));
+    hb_copy(A, W, bytes, s);
     HIP_CHECK(hipStreamSynchronize(s));
     HIP_CHECK(hipFree(W));
 }
@@ -727,7 +751,7 @@ INST(float) INST(double) INST(ccplx) INST(zcplx)
 
 #define INST(T) \
     template void hb2st_device<T>(i64, int, T*, i64, T*, T*, i64*, i64*, const i64*, const i64*, int*, i64, int, \
-                                  hipStream_t, i64*);
+                                  hipStream_t, i64*, i64);
 INST(float) INST(double) INST(ccplx) INST(zcplx)
 #undef INST
 

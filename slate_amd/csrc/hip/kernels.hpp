@@ -130,7 +130,8 @@ void tpqrt_panel(i64 m, i64 l, i64 j0, int ib, T* A, i64 lda, T* B, i64 ldb, T* 
                  i64 ldt, hipStream_t s);
 template <typename T>
 void hb2st_device(i64 n, int b, T* A, i64 lda, T* V, T* tau, i64* row, i64* len, const i64* sweep_ptr,
-                  const i64* ntask, int* work, i64 nsw, int nwg, hipStream_t s, i64* prof = nullptr);
+                  const i64* ntask, int* work, i64 nsw, int nwg, hipStream_t s, i64* prof = nullptr,
+                  i64 extent = 0);   // elements of A addressed (0: lda n; a skewed band layout passes its own)
 template <typename T>
 void tb2bd_device(i64 n, int b, T* A, i64 lda, T* UV, T* Utau, i64* Urow, i64* Ulen, T* VV, T* Vtau, i64* Vrow,
                   i64* Vlen, const i64* sweep_ptr, const i64* ntask, int* work, i64 nsw, int nwg, hipStream_t s);

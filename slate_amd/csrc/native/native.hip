@@ -103,7 +103,7 @@ void finalize() {
         for (auto& g : R.grids) peers = peers || (g.second && g.second->colpeer);
         if (peers) {
             Scratch d(sizeof(i64), R.main);
-            NHIP(hipMemsetAsync(d.p, 0, sizeof(i64), R.main));
+            dzero(d.p, sizeof(i64), R.main);
             world_comm()->allreduce(d.p, 1, DT::I64, 's', R.main);
             NHIP(hipStreamSynchronize(R.main));
         }
@@ -187,7 +187,7 @@ PeerBox* peer_box(Comm* c, std::unique_ptr<PeerBox>& slot, hipStream_t s) {
     NHIP(hipDeviceSynchronize());
     // every member has mapped every mailbox before any kernel posts into one
     Scratch d(sizeof(i64), s);
-    NHIP(hipMemsetAsync(d.p, 0, sizeof(i64), s));
+    dzero(d.p, sizeof(i64), s);
     c->allreduce(d.p, 1, DT::I64, 's', s);
     NHIP(hipStreamSynchronize(s));
     slot = std::move(pb);
@@ -216,7 +216,7 @@ void barrier() {
     NHIP(hipDeviceSynchronize());
     if (R.size == 1) return;
     Scratch d(sizeof(i64), R.main);
-    NHIP(hipMemsetAsync(d.p, 0, sizeof(i64), R.main));
+    dzero(d.p, sizeof(i64), R.main);
     world_comm()->allreduce(d.p, 1, DT::I64, 's', R.main);
     NHIP(hipStreamSynchronize(R.main));
 }
@@ -275,7 +275,7 @@ Matrix<T>::Matrix(int64_t m, int64_t n, int64_t nb, int p, int q) {
     s->esize = sizeof(T);
     const size_t bytes = (size_t)s->lld * std::max<i64>(s->nloc, 1) * sizeof(T);
     NHIP(hipMalloc(&s->buf, bytes));
-    NHIP(hipMemsetAsync(s->buf, 0, bytes, rt().main));
+    dzero(s->buf, bytes, rt().main);
     NHIP(hipStreamSynchronize(rt().main));
     s_ = s;
 }
@@ -854,7 +854,7 @@ int64_t potrf(HermitianMatrix<T>& A, const Options& opts) {
     const i64 nt = (S.n + S.nb - 1) / S.nb;
     const int la = std::max(0, opts.lookahead);
     Scratch infos(sizeof(i64) * std::max<i64>(nt, 1), R.main);
-    NHIP(hipMemsetAsync(infos.p, 0, sizeof(i64) * std::max<i64>(nt, 1), R.main));
+    dzero(infos.p, sizeof(i64) * std::max<i64>(nt, 1), R.main);
     if (S.p == 1 && S.q == 1 && nt > 2)
         potrf_1x1<T>(static_cast<T*>(S.buf), S.lld, S.n, S.nb, la, infos.as<i64>());
     else
@@ -1281,7 +1281,7 @@ static void panel_dist(Storage& S, i64 k, i64 kb, i64 lck, i64* ipiv_d, i64* inf
     Scratch part(2 * 1024 * 8 + 64, s);
     const int b = std::max(1, bw);
     Scratch recs((size_t)p * (3 + 2 * b) * sizeof(T), s), rec((size_t)(3 + 2 * b) * sizeof(T), s);
-    NHIP(hipMemsetAsync(Tt, 0, (size_t)kb * kb * sizeof(T), s));
+    dzero(Tt, (size_t)kb * kb * sizeof(T), s);
     i64* piv = ipiv_d + r0;                 // panel-relative
     PeerBox* pbx = b <= slate_hip::lu_peer_max_b() ? peer_box(colc, S.gc->colpeer, s) : nullptr;
     auto base = [&](i64 c0, i64 c1) {
@@ -1367,7 +1367,7 @@ static std::vector<i64> calu_playoff(i64 R, i64 w, i64 kb, const T* A, i64 lda, 
     auto W = std::make_unique<Scratch>(sizeof(T) * std::max<i64>(R, 1) * w, s);
     copy2d(W->as<T>(), R, A, lda, R, w, s);
     Scratch lp(sizeof(i64) * std::max<i64>(c, 1), s);
-    NHIP(hipMemsetAsync(lp.p, 0, sizeof(i64) * std::max<i64>(c, 1), s));
+    dzero(lp.p, sizeof(i64) * std::max<i64>(c, 1), s);
     slate_hip::getrf_panel_ws<K<T>>(R, std::min(w, kb), kp(W->as<T>()), R, lp.as<i64>(), info_d, thr, false,
                                     rt().lu_work, s);
     std::vector<i64> h((size_t)std::max<i64>(c, 1));
@@ -1437,7 +1437,7 @@ template <typename T>
 static void calu_panel_1(i64 mk, i64 wk, T* A, i64 lda, i64* piv_d, i64* info, double thr, i64 leaf, hipStream_t s) {
     const i64 kb = std::min(mk, wk);
     Scratch dinfo(sizeof(i64), s);
-    NHIP(hipMemsetAsync(dinfo.p, 0, sizeof(i64), s));
+    dzero(dinfo.p, sizeof(i64), s);
     std::vector<i64> sel = calu_local<T>(mk, wk, kb, A, lda, thr, std::max<i64>(leaf, 2 * kb), dinfo.as<i64>(), s);
     if ((i64)sel.size() > kb) sel.resize((size_t)kb);
     const std::vector<i64> piv = calu_ipiv(sel, mk);
@@ -1463,13 +1463,13 @@ static void calu_panel_dist(Storage& S, i64 k, i64 kb, i64 lck, i64* ipiv_d, i64
     T* W = buf + lr_k + lck * S.lld;
     Comm* colc = S.gc->col.get();
     Scratch dinfo(sizeof(i64), s);
-    NHIP(hipMemsetAsync(dinfo.p, 0, sizeof(i64), s));
+    dzero(dinfo.p, sizeof(i64), s);
     std::vector<i64> loc;
     if (nmine) loc = calu_local<T>(nmine, kb, kb, W, S.lld, thr, std::max<i64>(leaf, 2 * kb), dinfo.as<i64>(), s);
     // pack: kb x kb nominee rows (ld kb) + kb panel-relative global row ids (-1: none)
     const size_t rb = sizeof(T) * kb * kb, ib = sizeof(i64) * kb, pkb = rb + ib;
     Scratch pk(pkb, s), all(pkb * p, s);
-    NHIP(hipMemsetAsync(pk.p, 0, pkb, s));
+    dzero(pk.p, pkb, s);
     std::vector<i64> gid((size_t)kb, -1);
     for (size_t i = 0; i < loc.size(); ++i) gid[i] = l2g(lr_k + loc[i], nb, p, pr) - r0;
     if (!loc.empty()) {
@@ -1543,8 +1543,8 @@ int64_t getrf(Matrix<T>& A, std::vector<int64_t>& ipiv_out, const Options& opts)
     hipStream_t ps = R.panel, us = R.update;
     const i64 kmin = std::min(m, n);
     Scratch ipiv(sizeof(i64) * std::max<i64>(kmin, 1), R.main), infos(sizeof(i64) * std::max<i64>(kt, 1), R.main);
-    NHIP(hipMemsetAsync(ipiv.p, 0, sizeof(i64) * std::max<i64>(kmin, 1), R.main));
-    NHIP(hipMemsetAsync(infos.p, 0, sizeof(i64) * std::max<i64>(kt, 1), R.main));
+    dzero(ipiv.p, sizeof(i64) * std::max<i64>(kmin, 1), R.main);
+    dzero(infos.p, sizeof(i64) * std::max<i64>(kt, 1), R.main);
     i64* ipiv_d = ipiv.as<i64>();
     join(R.main, ps);
     join(R.main, us);
@@ -2555,7 +2555,7 @@ double norm(Norm kind, const Matrix<T>& Av) {
     const char k = (char)kind;
     const i64 nout = (k == 'F' ? 2 * S.nloc : S.nloc) + S.mloc;
     Scratch out(sizeof(Rl) * std::max<i64>(nout, 1), s);
-    NHIP(hipMemsetAsync(out.p, 0, sizeof(Rl) * std::max<i64>(nout, 1), s));
+    dzero(out.p, sizeof(Rl) * std::max<i64>(nout, 1), s);
     slate_hip::genorm<K<T>, Rl>(k, 'G', 'N', 0, S.mloc, S.nloc, kp(static_cast<const T*>(S.buf)), S.lld,
                                 out.as<Rl>(), s);
     std::vector<Rl> hr((size_t)std::max<i64>(nout, 1));

@@ -153,7 +153,7 @@ BandMatrix<T>::BandMatrix(int64_t m, int64_t n, int64_t kl, int64_t ku, int64_t 
     s->ncl = s->nt > R.rank ? (s->nt - R.rank + R.size - 1) / R.size : 0;
     const size_t bytes = sizeof(T) * (size_t)std::max<i64>(1, s->ncl) * s->H * nb;
     NHIP(hipMalloc(&s->buf, bytes));
-    NHIP(hipMemsetAsync(s->buf, 0, bytes, R.main));
+    dzero(s->buf, bytes, R.main);
     NHIP(hipStreamSynchronize(R.main));
     s_ = s;
 }
@@ -270,7 +270,7 @@ int64_t pbtrf(HermitianBandMatrix<T>& A, const Options&) {
     const i64 n = S.n, nb = S.nb, nt = S.nt, H = S.H;
     const char ct = ctrans<T>();
     Scratch infos(sizeof(i64) * std::max<i64>(nt, 1), s);
-    NHIP(hipMemsetAsync(infos.p, 0, sizeof(i64) * std::max<i64>(nt, 1), s));
+    dzero(infos.p, sizeof(i64) * std::max<i64>(nt, 1), s);
     Scratch P(sizeof(T) * (S.klt + 1) * nb * nb, s);
     for (i64 k = 0; k < nt; ++k) {
         const i64 r0 = k * nb, kb = S.kb(k), r1 = std::min(n, (k + S.klt + 1) * nb), mk = r1 - r0;
@@ -345,7 +345,7 @@ int64_t gbtrf(BandMatrix<T>& A, std::vector<int64_t>& ipiv, const Options& opts)
     const i64 kt = std::min(S.mt, S.nt);
     const i64 PH = (S.klt + 1) * nb;
     Scratch infos(sizeof(i64) * std::max<i64>(kt, 1), s);
-    NHIP(hipMemsetAsync(infos.p, 0, sizeof(i64) * std::max<i64>(kt, 1), s));
+    dzero(infos.p, sizeof(i64) * std::max<i64>(kt, 1), s);
     Scratch pall(sizeof(i64) * std::max<i64>(kt * nb, 1), s);      // panel-relative pivots of every step
     Scratch P(sizeof(T) * PH * nb + sizeof(i64) * nb + 64, s);
     T* Pp = P.as<T>();

@@ -65,6 +65,25 @@ void upload(void* d, const void* h, size_t bytes, hipStream_t s) {
 
 void dcopy(void* d, const void* s, size_t bytes, hipStream_t st) { launch_copy(d, s, bytes, st); }
 
+__global__ void __launch_bounds__(256) zero_words_kernel(unsigned long long* __restrict__ d, size_t nw) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nw; i += (size_t)gridDim.x * 256) d[i] = 0ull;
+}
+__global__ void __launch_bounds__(256) zero_bytes_kernel(unsigned char* __restrict__ d, size_t nb) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nb; i += (size_t)gridDim.x * 256) d[i] = 0;
+}
+
+void dzero(void* d, size_t bytes, hipStream_t st) {
+    if (!bytes || !d) return;
+    const bool words = ((reinterpret_cast<uintptr_t>(d) | bytes) & 7) == 0;
+    const size_t n = words ? bytes / 8 : bytes;
+    const unsigned g = (unsigned)std::min<size_t>((n + 255) / 256, 4096);
+    if (words)
+        hipLaunchKernelGGL(zero_words_kernel, dim3(g), dim3(256), 0, st, static_cast<unsigned long long*>(d), n);
+    else
+        hipLaunchKernelGGL(zero_bytes_kernel, dim3(g), dim3(256), 0, st, static_cast<unsigned char*>(d), n);
+    NHIP(hipGetLastError());
+}
+
 // dst[:, didx[c]] = src[:, sidx[c]], columns of mw 4-byte words
 __global__ void __launch_bounds__(256)
 copy_cols_kernel(const unsigned* __restrict__ src, i64 lds, const i64* __restrict__ sidx, unsigned* __restrict__ dst,

@@ -242,7 +242,9 @@ void dc_merge_rows(const Merge& g, double rho, std::vector<double>& w, const std
             }
             // rank-one vector columns per chunk: at most ~the merge block's
             // size (a row-distributed merge holds only nr of the S rows)
-            const i64 CH = std::max<i64>(256, std::min<i64>(4096, (nr * S) / std::max<i64>(k, 1)));
+            static const i64 chdiv = [] { const char* e = std::getenv("SLATE_AMD_DC_CHDIV"); return e ? std::atoll(e) : 4; }();
+            const i64 CH = chdiv <= 0 ? 4096
+                                      : std::max<i64>(256, std::min<i64>(4096, (nr * S) / (chdiv * std::max<i64>(k, 1))));
             for (i64 j0 = 0; j0 < k; j0 += CH) {
                 const i64 nc = std::min(CH, k - j0);
                 Scratch V((size_t)k * nc * sizeof(double), s);
@@ -260,7 +262,7 @@ void dc_merge_rows(const Merge& g, double rho, std::vector<double>& w, const std
                         gemm_k<double>('N', 'N', np, nc, ns, 1.0, srcs[pi]->as<double>(), np, Vp.as<double>(), ns,
                                        0.0, out.as<double>(), np, s);
                     } else {
-                        NHIP(hipMemsetAsync(out.p, 0, (size_t)np * nc * sizeof(double), s));
+                        dzero(out.p, (size_t)np * nc * sizeof(double), s);
                     }
                     slate_hip::cols_copy(np, nc, out.as<double>(), np, Kd->as<i64>() + j0, qs + pt.r0, lds, true, s);
                 }
@@ -291,7 +293,7 @@ void stedc_rows(i64 n, const std::vector<double>& d, const std::vector<double>& 
     w.assign((size_t)n, 0.0);
     if (n == 0) return;
     const i64 nr = std::max<i64>(r1 - r0, 0);
-    if (nr) NHIP(hipMemsetAsync(Q, 0, (size_t)ldq * n * sizeof(double), s));
+    if (nr) dzero(Q, (size_t)ldq * n * sizeof(double), s);
     std::vector<std::pair<i64, i64>> leaves;
     std::vector<std::vector<Merge>> levels;
     dc_tree(0, n, 0, 128, leaves, levels);
@@ -314,7 +316,7 @@ void stedc_rows(i64 n, const std::vector<double>& d, const std::vector<double>& 
         Scratch* dd = upload_vec(keep, dl, s);
         Scratch* ed = upload_vec(keep, ee, s);
         Scratch wd((size_t)n * sizeof(double), s), fails(sizeof(i64), s);
-        NHIP(hipMemsetAsync(fails.p, 0, sizeof(i64), s));
+        dzero(fails.p, sizeof(i64), s);
         slate_hip::steqr_leaves((i64)leaves.size(), lod->as<i64>(), hid->as<i64>(), dd->as<double>(),
                                 ed->as<double>(), wd.as<double>(), Q, ldq, r0, r1, fails.as<i64>(), s, (int)mx, 60);
         w = download_vec<double>(wd.p, (size_t)n, s);
@@ -324,7 +326,7 @@ void stedc_rows(i64 n, const std::vector<double>& d, const std::vector<double>& 
     Scratch zb((size_t)n * sizeof(double), s);
     for (int t = (int)levels.size() - 1; t >= 0; --t) {
         // z of every merge of this level from the owners of rows m - 1 and m
-        NHIP(hipMemsetAsync(zb.p, 0, (size_t)n * sizeof(double), s));
+        dzero(zb.p, (size_t)n * sizeof(double), s);
         double* z = zb.as<double>();
         for (auto& g : levels[t]) {
             if (g.m - 1 >= r0 && g.m - 1 < r1)
@@ -374,7 +376,7 @@ void he2hb(i64 n, i64 nb, T* Af, i64 ld, std::vector<Panel<T>>& panels, hipStrea
         pn.V = std::make_unique<Scratch>((size_t)m * kk * sizeof(T), s);
         pn.T_ = std::make_unique<Scratch>((size_t)kk * kk * sizeof(T), s);
         Scratch tau((size_t)kk * sizeof(T), s);
-        NHIP(hipMemsetAsync(tau.p, 0, (size_t)kk * sizeof(T), s));
+        dzero(tau.p, (size_t)kk * sizeof(T), s);
         T* V = pn.V->template as<T>();
         T* Tm = pn.T_->template as<T>();
         slate_hip::geqrf_panel_ws<K<T>>(m, kb, kp(P), ld, kp(tau.as<T>()), kp(Tm), kk, kp(V), m, rt().qr_work, s);
@@ -498,14 +500,14 @@ void heev_1gpu(i64 n, T* Af, std::vector<double>& w, T* Z, bool wantz, hipStream
     }
     Scratch V((size_t)std::max<i64>(total, 1) * b * sizeof(T), s), tau((size_t)std::max<i64>(total, 1) * sizeof(T), s);
     Scratch row((size_t)std::max<i64>(total, 1) * sizeof(i64), s), len((size_t)std::max<i64>(total, 1) * sizeof(i64), s);
-    NHIP(hipMemsetAsync(V.p, 0, (size_t)std::max<i64>(total, 1) * b * sizeof(T), s));
-    NHIP(hipMemsetAsync(tau.p, 0, (size_t)std::max<i64>(total, 1) * sizeof(T), s));
+    dzero(V.p, (size_t)std::max<i64>(total, 1) * b * sizeof(T), s);
+    dzero(tau.p, (size_t)std::max<i64>(total, 1) * sizeof(T), s);
     std::vector<std::unique_ptr<Scratch>> keep;
     Scratch* ntd = upload_vec(keep, nt, s);
     Scratch* spd = upload_vec(keep, sp, s);
     if (nsw > 0 && total > 0) {
         Scratch work((size_t)(nsw + 2) * sizeof(int), s);
-        NHIP(hipMemsetAsync(work.p, 0, (size_t)(nsw + 2) * sizeof(int), s));
+        dzero(work.p, (size_t)(nsw + 2) * sizeof(int), s);
         hipDeviceProp_t pr;
         NHIP(hipGetDeviceProperties(&pr, rt().device));
         const i64 nt0 = nt[0] ? nt[0] : 1, lag = 2;
@@ -694,7 +696,7 @@ void symmetrize(i64 n, T* D, Uplo uplo, hipStream_t s) {
 //     process column, W = Y - V M / 2 assembled by one column all-reduce,
 //     and A22 -= [V W] [W V]^H is one local GEMM of inner size 2b;
 //   * the band (O(n b) words) is summed to every rank; rank 0 chases it on
-//     the GPU in a SKEWED band layout (element (i, j) at off + i + j lda with
+//     the GPU in a SKEWED band layout (element (i, j) at i + j lda with
 //     lda = 4b + 8: the chase only touches |i - j| < 2b, so the dense-window
 //     kernel runs on (4b + 9) n words instead of n^2);
 //   * divide & conquer with the eigenvector rows distributed (stedc_rows);
@@ -777,7 +779,7 @@ void he2hb_grid(Storage& F, std::vector<GPanel<T>>& pans, hipStream_t s) {
                                                       kp(Pf.as<T>()), m2, upload_vec(keep, g, s)->template as<i64>(),
                                                       s);
             }
-            NHIP(hipMemsetAsync(tau.p, 0, (size_t)kk * es, s));
+            dzero(tau.p, (size_t)kk * es, s);
             slate_hip::geqrf_panel_ws<K<T>>(m2, kb, kp(Pf.as<T>()), m2, kp(tau.as<T>()), kp(Tk), kk, kp(Vf), m2,
                                             rt().qr_work, s);
             // R and the reflectors back into this rank's rows of the panel
@@ -821,7 +823,7 @@ void he2hb_grid(Storage& F, std::vector<GPanel<T>>& pans, hipStream_t s) {
         // W = Y - V M / 2, then the full W (m2 x kk) by one column all-reduce
         if (nmine) gemm_k<T>('N', 'N', nmine, kk, kk, T(-0.5), Vl, ldy, M.as<T>(), kk, T(1), Y, ldy, s);
         Scratch Wf((size_t)m2 * kk * es, s);
-        NHIP(hipMemsetAsync(Wf.p, 0, (size_t)m2 * kk * es, s));
+        dzero(Wf.p, (size_t)m2 * kk * es, s);
         if (nmine) slate_hip::permute_rows_scatter<K<T>>(nmine, kk, kp(Y), ldy, kp(Wf.as<T>()), m2, rid, s);
         if (p > 1) gc->col->allreduce(Wf.p, (size_t)(m2 * kk), dt_of<T>::v, 's', s);
         // A22 -= [V W] [W V]^H over my trailing block (one GEMM, inner 2 kk)
@@ -893,6 +895,14 @@ int64_t heev_grid(HermitianMatrix<T>& A, std::vector<real_t<T>>& Lambda, Matrix<
     };
     NHIP(hipStreamSynchronize(s));
     NHIP(hipMemGetInfo(&free0, &total0));
+    // diagnostics: SLATE_AMD_HEEV_GRID_STOP=k returns after stage k (bisection)
+    const int stop = [] { const char* e = std::getenv("SLATE_AMD_HEEV_GRID_STOP"); return e ? std::atoi(e) : 0; }();
+    auto stop_at = [&](int k) {
+        if (stop != k) return false;
+        NHIP(hipStreamSynchronize(s));
+        Lambda.assign((size_t)n, 0);
+        return true;
+    };
     // ---- F: both triangles, tile b, A's grid
     Matrix<T> F(n, n, b, p, q);
     {
@@ -900,17 +910,19 @@ int64_t heev_grid(HermitianMatrix<T>& A, std::vector<real_t<T>>& Lambda, Matrix<
         redistribute<T>(Af, F);
         mark();
     }
+    if (stop_at(1)) return 0;
     std::vector<GPanel<T>> pans;
     {
         NTRACE("heev::he2hb", s);
         he2hb_grid<T>(*F.storage(), pans, s);
     }
     mark();
+    if (stop_at(2)) return 0;
     // ---- the band to every rank (O(n b)), stage 2 on rank 0
     const Storage& SF = *F.storage();
     const i64 nt = (n + b - 1) / b;
     Scratch stack((size_t)2 * b * n * sizeof(T), s);
-    NHIP(hipMemsetAsync(stack.p, 0, (size_t)2 * b * n * sizeof(T), s));
+    dzero(stack.p, (size_t)2 * b * n * sizeof(T), s);
     for (i64 k = 0; k < nt; ++k) {
         if ((int)(k % q) != SF.pc) continue;
         const i64 c0 = k * b, kb = std::min(b, n - c0), lc = tiles_before(k, q, SF.pc) * b;
@@ -941,22 +953,31 @@ int64_t heev_grid(HermitianMatrix<T>& A, std::vector<real_t<T>>& Lambda, Matrix<
     if (R.rank == 0) {
         try {
             NTRACE("heev::hb2st", s);
-            const i64 lda = 4 * b + 8, off = 2 * b;
-            const size_t words = (size_t)(off + lda * n + 16);
+            // element (i, j), |i - j| < 2b, at i + j lda: row i - j of column j
+            // of a band of leading dimension lda + 1; the highest address is
+            // (n - 1)(lda + 1), so the chase gets that extent (not lda n)
+            const i64 lda = 4 * b + 8;
+            const i64 extent = (n - 1) * (lda + 1) + 1;
+            const size_t words = (size_t)(extent + 16);
             Scratch Bh(words * sizeof(T), s);
-            NHIP(hipMemsetAsync(Bh.p, 0, words * sizeof(T), s));
-            T* Ab = Bh.as<T>() + off;
+            dzero(Bh.p, words * sizeof(T), s);
+            T* Ab = Bh.as<T>();
             hipLaunchKernelGGL(band_from_stack_kernel<K<T>>, dim3((unsigned)n), dim3((unsigned)(2 * b + 1)), 0, s,
                                n, (int)b, kp(stack.as<T>()), 2 * b, kp(Ab), lda);
             NHIP(hipGetLastError());
+            if (const char* dump = std::getenv("SLATE_AMD_NATIVE_HEEV_DUMP"); dump && *dump) {
+                const std::vector<T> hb = download_vec<T>(Bh.p, words, s);
+                std::FILE* f = std::fopen((std::string(dump) + "/skew.bin").c_str(), "wb");
+                if (f) { std::fwrite(hb.data(), sizeof(T), hb.size(), f); std::fclose(f); }
+            }
             V2 = std::make_unique<Scratch>((size_t)std::max<i64>(total, 1) * b * sizeof(T), s);
             tau2 = std::make_unique<Scratch>((size_t)std::max<i64>(total, 1) * sizeof(T), s);
             Scratch row((size_t)std::max<i64>(total, 1) * sizeof(i64), s), len((size_t)std::max<i64>(total, 1) * sizeof(i64), s);
-            NHIP(hipMemsetAsync(V2->p, 0, (size_t)std::max<i64>(total, 1) * b * sizeof(T), s));
-            NHIP(hipMemsetAsync(tau2->p, 0, (size_t)std::max<i64>(total, 1) * sizeof(T), s));
+            dzero(V2->p, (size_t)std::max<i64>(total, 1) * b * sizeof(T), s);
+            dzero(tau2->p, (size_t)std::max<i64>(total, 1) * sizeof(T), s);
             if (nsw > 0 && total > 0) {
                 Scratch work((size_t)(nsw + 2) * sizeof(int), s);
-                NHIP(hipMemsetAsync(work.p, 0, (size_t)(nsw + 2) * sizeof(int), s));
+                dzero(work.p, (size_t)(nsw + 2) * sizeof(int), s);
                 hipDeviceProp_t prp;
                 NHIP(hipGetDeviceProperties(&prp, R.device));
                 const i64 nt0 = ntk[0] ? ntk[0] : 1, lag = 2;
@@ -964,7 +985,8 @@ int64_t heev_grid(HermitianMatrix<T>& A, std::vector<real_t<T>>& Lambda, Matrix<
                                                     std::max<i64>(8, std::min(nt0 / lag + 8, nt0 / 3 + 15))});
                 slate_hip::hb2st_device<K<T>>(n, (int)b, kp(Ab), lda, kp(V2->template as<T>()),
                                               kp(tau2->template as<T>()), row.as<i64>(), len.as<i64>(),
-                                              spd->as<i64>(), ntd->as<i64>(), work.as<int>(), nsw, nwg, s);
+                                              spd->as<i64>(), ntd->as<i64>(), work.as<int>(), nsw, nwg, s, nullptr,
+                                              extent);
             }
             Scratch dsub((size_t)2 * n * sizeof(T), s);
             copy2d(dsub.as<T>(), 1, Ab, lda + 1, 1, n, s);
@@ -1001,8 +1023,17 @@ int64_t heev_grid(HermitianMatrix<T>& A, std::vector<real_t<T>>& Lambda, Matrix<
         rec = download_vec<double>(rb.p, rec.size(), s);
     }
     if (rec.back() != 0) throw Error(R.rank == 0 ? msg : std::string("native heev: stage 2 failed on rank 0"));
+    if (const char* dump = std::getenv("SLATE_AMD_NATIVE_HEEV_DUMP"); dump && *dump && R.rank == 0) {
+        // diagnostics: the gathered band stack (2b x n) and (d, e), raw binary
+        const std::vector<T> hs = download_vec<T>(stack.p, (size_t)(2 * b * n), s);
+        std::FILE* f = std::fopen((std::string(dump) + "/stack.bin").c_str(), "wb");
+        if (f) { std::fwrite(hs.data(), sizeof(T), hs.size(), f); std::fclose(f); }
+        f = std::fopen((std::string(dump) + "/de.bin").c_str(), "wb");
+        if (f) { std::fwrite(rec.data(), sizeof(double), (size_t)(2 * n - 1), f); std::fclose(f); }
+    }
     std::vector<double> d(rec.begin(), rec.begin() + n), e(rec.begin() + n, rec.begin() + n + std::max<i64>(n - 1, 0));
     std::vector<double> w;
+    if (stop_at(3)) return 0;
     if (!Z) {
         std::vector<double> ee(e);
         ee.resize((size_t)n, 0.0);
@@ -1014,13 +1045,23 @@ int64_t heev_grid(HermitianMatrix<T>& A, std::vector<real_t<T>>& Lambda, Matrix<
     // ---- tridiagonal eigenvectors, rows distributed: rank r rows [r mb, ...)
     const i64 mb = (n + P - 1) / P;
     Matrix<T> Zrow(n, n, mb, P, 1);
+    if (stop_at(31)) return 0;
     {
         NTRACE("heev::stedc", s);
         const Storage& SR = *Zrow.storage();
         const i64 r0 = std::min<i64>((i64)R.rank * mb, n), nr = SR.mloc;
         Scratch Qr((size_t)std::max<i64>(nr, 1) * n * sizeof(double), s);
-        stedc_rows(n, d, e, w, Qr.as<double>(), std::max<i64>(nr, 1), r0, r0 + nr, world, s);
+        if (std::getenv("SLATE_AMD_HEEV_GRID_DCFULL")) {
+            // diagnostics: the one-process D&C (all rows) on every rank
+            Scratch Qf((size_t)n * n * sizeof(double), s);
+            stedc_rows(n, d, e, w, Qf.as<double>(), n, 0, n, nullptr, s);
+            if (nr) copy2d(Qr.as<double>(), std::max<i64>(nr, 1), Qf.as<double>() + r0, n, nr, n, s);
+            NHIP(hipStreamSynchronize(s));
+        } else {
+            stedc_rows(n, d, e, w, Qr.as<double>(), std::max<i64>(nr, 1), r0, r0 + nr, world, s);
+        }
         mark();
+        if (stop_at(32)) return 0;
         std::vector<T> ph((size_t)n);
         const i64 po = n + std::max<i64>(n - 1, 0);
         for (i64 i = 0; i < n; ++i) {
@@ -1031,6 +1072,10 @@ int64_t heev_grid(HermitianMatrix<T>& A, std::vector<real_t<T>>& Lambda, Matrix<
         if (nr) real_to_phase<T>(nr, n, Qr.as<double>(), std::max<i64>(nr, 1), phd ? kp(phd->as<T>() + r0) : nullptr,
                                  kp(static_cast<T*>(SR.buf)), SR.lld, s);
         NHIP(hipStreamSynchronize(s));
+    }
+    if (stop_at(4)) {
+        if (std::getenv("SLATE_AMD_HEEV_GRID_TRIM")) { NHIP(hipDeviceSynchronize()); slate_hip::dev_trim(); }
+        return 0;
     }
     // ---- Q2 on a 1 x P column-cyclic Z, reflectors streamed from rank 0
     Matrix<T> Zc(n, n, b, 1, P);
@@ -1073,6 +1118,7 @@ int64_t heev_grid(HermitianMatrix<T>& A, std::vector<real_t<T>>& Lambda, Matrix<
     }
     V2.reset();
     tau2.reset();
+    if (stop_at(5)) return 0;
     // ---- Q1 on F's grid, then the caller's layout
     Matrix<T> Zg(n, n, b, p, q);
     redistribute<T>(Zc, Zg);
@@ -1180,7 +1226,7 @@ void ge2tb(i64 m, i64 n, i64 nb, T* A, i64 lda, std::vector<Panel<T>>& left, std
         L.T_ = std::make_unique<Scratch>((size_t)kk * kk * sizeof(T), s);
         {
             Scratch tau((size_t)kk * sizeof(T), s);
-            NHIP(hipMemsetAsync(tau.p, 0, (size_t)kk * sizeof(T), s));
+            dzero(tau.p, (size_t)kk * sizeof(T), s);
             slate_hip::geqrf_panel_ws<K<T>>(mp, kb, kp(P), lda, kp(tau.as<T>()), kp(L.T_->template as<T>()), kk,
                                             kp(L.V->template as<T>()), mp, rt().qr_work, s);
         }
@@ -1202,7 +1248,7 @@ void ge2tb(i64 m, i64 n, i64 nb, T* A, i64 lda, std::vector<Panel<T>>& left, std
         Rt.T_ = std::make_unique<Scratch>((size_t)kr * kr * sizeof(T), s);
         {
             Scratch tau((size_t)kr * sizeof(T), s);
-            NHIP(hipMemsetAsync(tau.p, 0, (size_t)kr * sizeof(T), s));
+            dzero(tau.p, (size_t)kr * sizeof(T), s);
             slate_hip::geqrf_panel_ws<K<T>>(w, kb, kp(Xh.as<T>()), w, kp(tau.as<T>()), kp(Rt.T_->template as<T>()),
                                             kr, kp(Rt.V->template as<T>()), w, rt().qr_work, s);
         }
@@ -1254,8 +1300,8 @@ void svd_1gpu(i64 m, i64 n, T* A, std::vector<double>& sv, T* U, T* V, bool want
         st.push_back(std::make_unique<Scratch>((size_t)cap * sizeof(T), s));
         st.push_back(std::make_unique<Scratch>((size_t)cap * sizeof(i64), s));
         st.push_back(std::make_unique<Scratch>((size_t)cap * sizeof(i64), s));
-        NHIP(hipMemsetAsync(st[0]->p, 0, (size_t)cap * b * sizeof(T), s));
-        NHIP(hipMemsetAsync(st[1]->p, 0, (size_t)cap * sizeof(T), s));
+        dzero(st[0]->p, (size_t)cap * b * sizeof(T), s);
+        dzero(st[1]->p, (size_t)cap * sizeof(T), s);
     };
     std::vector<std::unique_ptr<Scratch>> Us, Vs, keep;
     store(Us);
@@ -1264,7 +1310,7 @@ void svd_1gpu(i64 m, i64 n, T* A, std::vector<double>& sv, T* U, T* V, bool want
     Scratch* spd = upload_vec(keep, sp, s);
     if (nsw > 0) {
         Scratch work((size_t)(nsw + 2) * sizeof(int), s);
-        NHIP(hipMemsetAsync(work.p, 0, (size_t)(nsw + 2) * sizeof(int), s));
+        dzero(work.p, (size_t)(nsw + 2) * sizeof(int), s);
         hipDeviceProp_t pr;
         NHIP(hipGetDeviceProperties(&pr, rt().device));
         const i64 nt0 = nt[0] ? nt[0] : 1;
@@ -1327,7 +1373,7 @@ void svd_1gpu(i64 m, i64 n, T* A, std::vector<double>& sv, T* U, T* V, bool want
         }
     };
     if (wantu) {
-        NHIP(hipMemsetAsync(U, 0, (size_t)m * k * sizeof(T), s));
+        dzero(U, (size_t)m * k * sizeof(T), s);
         back(Us, Uh, pu, U, m, left);
     }
     if (wantv) {

@@ -69,7 +69,7 @@ __global__ void __launch_bounds__(256) multi_axpy_kernel(i64 m, int nv, KT alpha
 template <typename T>
 void multi_dotc(i64 m, int nv, const T* V, i64 ldv, const T* w, T* h_d, hipStream_t s) {
     if (m > 0 && nv > 0) hipLaunchKernelGGL(multi_dotc_kernel<K<T>>, dim3(nv), dim3(256), 0, s, m, kp(V), ldv, kp(w), kp(h_d));
-    else if (nv > 0) NHIP(hipMemsetAsync(h_d, 0, sizeof(T) * nv, s));
+    else if (nv > 0) dzero(h_d, sizeof(T) * nv, s);
 }
 
 template <typename T>
@@ -104,7 +104,7 @@ struct VecSet {
     VecSet(const Storage& S, int cnt, hipStream_t s)
         : n(S.m), mloc(S.pc == 0 ? S.mloc : 0), ld(std::max<i64>(1, (S.mloc + 15) / 16 * 16)), count(cnt),
           buf(sizeof(T) * (size_t)std::max<i64>(1, (S.pc == 0 ? ld : 1) * cnt), s), shape(&S) {
-        NHIP(hipMemsetAsync(buf.p, 0, sizeof(T) * (size_t)std::max<i64>(1, (S.pc == 0 ? ld : 1) * cnt), s));
+        dzero(buf.p, sizeof(T) * (size_t)std::max<i64>(1, (S.pc == 0 ? ld : 1) * cnt), s);
     }
     T* col(int i) { return buf.as<T>() + (mloc ? (i64)i * ld : 0); }
     // n x 1 Matrix over vector i (zero-copy)
@@ -571,8 +571,8 @@ void aasen(i64 N, i64 nb, T* Af, T* L, T* Td, T* Tl, i64* piv_rel, i64* info, hi
     T* hs = Hs.as<T>();
     T* sm = S.as<T>();
     T* tp = tmp.as<T>();
-    NHIP(hipMemsetAsync(xs, 0, sizeof(T) * N * nb, s));
-    NHIP(hipMemsetAsync(hs, 0, sizeof(T) * N * nb, s));
+    dzero(xs, sizeof(T) * N * nb, s);
+    dzero(hs, sizeof(T) * N * nb, s);
     auto td = [&](i64 I) { return Td + I * nb * nb; };
     auto tl = [&](i64 I) { return Tl + I * nb * nb; };
     for (i64 J = 0; J < NT; ++J) {
@@ -609,7 +609,7 @@ void aasen(i64 N, i64 nb, T* Af, T* L, T* Td, T* Tl, i64* piv_rel, i64* info, hi
         slate_hip::getrf_panel_ws<K<T>>(mp, nb, kp(Wp), N, piv, info + J, 1.0, false, rt().lu_work, s);
         slate_hip::v_explicit<K<T>>(mp, nb, kp(Wp), N, kp(L + j1 + j1 * N), N, s);
         T* T1 = tl(J + 1);
-        NHIP(hipMemsetAsync(T1, 0, sizeof(T) * nb * nb, s));
+        dzero(T1, sizeof(T) * nb * nb, s);
         slate_hip::gecopy<K<T>, K<T>>('U', 'N', nb, nb, kp(Wp), N, kp(T1), nb, s);
         slate_hip::trsm<K<T>>('R', 'L', ct, 'U', nb, nb, kv(T(1)), kp(Ljj), N, kp(T1), nb, s);
         // symmetric interchange: L's rows, then the trailing Hermitian block
@@ -649,14 +649,14 @@ int64_t hetrf(const HermitianMatrix<T>& A, IndefiniteFactors<T>& F, const Option
     Scratch Af(sizeof(T) * N * N, s);
     upload(Af.p, h.data(), sizeof(T) * N * N, s);
     auto Ls = std::make_shared<Scratch>(sizeof(T) * N * N, s);
-    NHIP(hipMemsetAsync(Ls->p, 0, sizeof(T) * N * N, s));
+    dzero(Ls->p, sizeof(T) * N * N, s);
     slate_hip::geset<K<T>>('G', nb, nb, kv(T(0)), kv(T(1)), kp(Ls->as<T>()), N, s);
     Scratch Td(sizeof(T) * nb * nb * NT, s), Tl(sizeof(T) * nb * nb * (NT + 1), s);
-    NHIP(hipMemsetAsync(Td.p, 0, sizeof(T) * nb * nb * NT, s));
-    NHIP(hipMemsetAsync(Tl.p, 0, sizeof(T) * nb * nb * (NT + 1), s));
+    dzero(Td.p, sizeof(T) * nb * nb * NT, s);
+    dzero(Tl.p, sizeof(T) * nb * nb * (NT + 1), s);
     Scratch piv(sizeof(i64) * N, s), inf(sizeof(i64) * NT, s);
-    NHIP(hipMemsetAsync(piv.p, 0, sizeof(i64) * N, s));
-    NHIP(hipMemsetAsync(inf.p, 0, sizeof(i64) * NT, s));
+    dzero(piv.p, sizeof(i64) * N, s);
+    dzero(inf.p, sizeof(i64) * NT, s);
     aasen<T>(N, nb, Af.as<T>(), Ls->as<T>(), Td.as<T>(), Tl.as<T>(), piv.as<i64>(), inf.as<i64>(), s);
     // the permutation (block 0 keeps its rows; block J + 1's pivots are
     // relative to row (J + 1) nb)

@@ -205,6 +205,11 @@ struct Event {
 // memory that kernels on other XCDs may hold in their L2
 void upload(void* d, const void* h, size_t bytes, hipStream_t s);
 void dcopy(void* d, const void* src, size_t bytes, hipStream_t s);
+// zero fill BY KERNEL (stream-ordered): hipMemsetAsync may run on a copy
+// engine, whose writes a later kernel does not see while an XCD's L2 still
+// holds the buffer's old lines (cached scratch blocks are reused: stale
+// progress counters of a bulge chase made it skip its waits)
+void dzero(void* d, size_t bytes, hipStream_t s);
 // dst[:, didx[c]] = src[:, sidx[c]] for c < ncols (m elements of esize bytes
 // per column; host index lists); complete on return
 void copy_cols(void* dst, i64 ldd, const i64* didx, const void* src, i64 lds, const i64* sidx, i64 m, size_t esize,
@@ -226,7 +231,7 @@ struct Scratch {
     Scratch(size_t bytes, hipStream_t st) : s(st) {
         if (!bytes) return;
         p = slate_hip::dev_alloc(bytes, st);
-        if (poison()) NHIP(hipMemsetAsync(p, 0xFF, bytes, st));     // NaN: exposes reads before writes
+        if (poison()) NHIP(hipMemsetAsync(p, 0xFF, bytes, st));     // NaN: exposes reads before writes (diagnostics)
     }
     // diagnostics: SLATE_AMD_NATIVE_POISON=1 fills every scratch buffer with NaN
     static bool poison() {
