@@ -537,6 +537,14 @@ void heev_1gpu(i64 n, T* Af, std::vector<double>& w, T* Z, bool wantz, hipStream
             e[i] = (double)sub[i];
         }
     }
+    if (const char* dump = std::getenv("SLATE_AMD_NATIVE_HEEV_DUMP"); dump && *dump) {
+        std::FILE* f = std::fopen((std::string(dump) + "/de1.bin").c_str(), "wb");
+        if (f) {
+            std::fwrite(d.data(), sizeof(double), d.size(), f);
+            std::fwrite(e.data(), sizeof(double), e.size(), f);
+            std::fclose(f);
+        }
+    }
     if (!wantz) {
         std::vector<double> ee(e);
         ee.resize((size_t)n, 0.0);
@@ -1056,6 +1064,12 @@ int64_t heev_grid(HermitianMatrix<T>& A, std::vector<real_t<T>>& Lambda, Matrix<
             Scratch Qf((size_t)n * n * sizeof(double), s);
             stedc_rows(n, d, e, w, Qf.as<double>(), n, 0, n, nullptr, s);
             if (nr) copy2d(Qr.as<double>(), std::max<i64>(nr, 1), Qf.as<double>() + r0, n, nr, n, s);
+            NHIP(hipStreamSynchronize(s));
+        } else if (const char* dm = std::getenv("SLATE_AMD_HEEV_GRID_DCMODE"); dm && !std::strcmp(dm, "nocomm")) {
+            stedc_rows(n, d, e, w, Qr.as<double>(), std::max<i64>(nr, 1), r0, r0 + nr, nullptr, s);
+        } else if (dm && !std::strcmp(dm, "fullcomm")) {
+            Scratch Qf((size_t)n * n * sizeof(double), s);
+            stedc_rows(n, d, e, w, Qf.as<double>(), n, 0, n, world, s);
             NHIP(hipStreamSynchronize(s));
         } else {
             stedc_rows(n, d, e, w, Qr.as<double>(), std::max<i64>(nr, 1), r0, r0 + nr, world, s);
