@@ -21,6 +21,7 @@
 #include <cstdio>
 #include <cstring>
 #include <numeric>
+#include <type_traits>
 #include <vector>
 
 #include "../include/bdsqr.hpp"
@@ -403,10 +404,54 @@ void he2hb(i64 n, i64 nb, T* Af, i64 ld, std::vector<Panel<T>>& panels, hipStrea
     }
 }
 
-// Z := Q1 Z, Q1 = H_0 H_1 ... (panels last to first: Z -= V T (V^H Z))
+// Z := Q1 Z, Q1 = H_0 H_1 ... (panels last to first: Z -= V T (V^H Z)).
+// Groups of G = SLATE_AMD_UNMTR_HE2HB_GROUP (default 4) consecutive panels
+// are merged into ONE block reflector I - Vg Tg Vg^H (forward larft merge,
+// Tg = [[T1, -T1 V1^H V2 T2], [0, T2]]): Z streams once per group with
+// K = G nb instead of once per panel with K = nb (models/eig.py
+// unmtr_he2hb / _merge_reflectors).
 template <typename T>
 void unmtr_he2hb(i64 n, i64 nc, std::vector<Panel<T>>& panels, T* Z, i64 ldz, hipStream_t s) {
     const char ct = ctrans<T>();
+    static const i64 G = [] { const char* e = std::getenv("SLATE_AMD_UNMTR_HE2HB_GROUP"); return e ? std::max(1, std::atoi(e)) : 4; }();
+    if (G > 1 && nc > 0) {
+        i64 i1 = (i64)panels.size();
+        while (i1 > 0) {
+            const i64 i0 = std::max<i64>(0, i1 - G);
+            const i64 r0 = panels[i0].r0, m = n - r0;
+            i64 kt = 0;
+            for (i64 i = i0; i < i1; ++i) kt += panels[i].kk;
+            Scratch Vg((size_t)m * kt * sizeof(T), s), Tg((size_t)kt * kt * sizeof(T), s);
+            dzero(Vg.p, (size_t)m * kt * sizeof(T), s);
+            dzero(Tg.p, (size_t)kt * kt * sizeof(T), s);
+            T* vg = Vg.as<T>();
+            T* tg = Tg.as<T>();
+            i64 c = 0;
+            for (i64 i = i0; i < i1; ++i) {
+                const Panel<T>& pn = panels[i];
+                const i64 kb = pn.kk, off = pn.r0 - r0, mi = n - pn.r0;
+                const T* Vi = pn.V->template as<T>();
+                const T* Ti = pn.T_->template as<T>();
+                copy2d(vg + off + c * m, m, Vi, mi, mi, kb, s);
+                copy2d(tg + c + c * kt, kt, Ti, kb, kb, kb, s);      // T_i is upper triangular (lower zero)
+                if (c) {
+                    // T12 = -T_prev (V_prev^H V_i) T_i over the rows V_i spans
+                    Scratch S1((size_t)c * kb * sizeof(T), s), S2((size_t)c * kb * sizeof(T), s);
+                    gemm_k<T>(ct, 'N', c, kb, mi, T(1), vg + off, m, Vi, mi, T(0), S1.as<T>(), c, s);
+                    gemm_k<T>('N', 'N', c, kb, c, T(1), tg, kt, S1.as<T>(), c, T(0), S2.as<T>(), c, s);
+                    gemm_k<T>('N', 'N', c, kb, kb, T(-1), S2.as<T>(), c, Ti, kb, T(0), tg + c * kt, kt, s);
+                }
+                c += kb;
+            }
+            // Z(r0:, :) -= Vg Tg (Vg^H Z(r0:, :))
+            Scratch W((size_t)kt * nc * sizeof(T), s), W2((size_t)kt * nc * sizeof(T), s);
+            gemm_k<T>(ct, 'N', kt, nc, m, T(1), vg, m, Z + r0, ldz, T(0), W.as<T>(), kt, s);
+            gemm_k<T>('N', 'N', kt, nc, kt, T(1), tg, kt, W.as<T>(), kt, T(0), W2.as<T>(), kt, s);
+            gemm_k<T>('N', 'N', m, nc, kt, T(-1), vg, m, W2.as<T>(), kt, T(1), Z + r0, ldz, s);
+            i1 = i0;
+        }
+        return;
+    }
     for (auto it = panels.rbegin(); it != panels.rend(); ++it) {
         const i64 r0 = it->r0, kk = it->kk, m = n - r0;
         Scratch W((size_t)kk * nc * sizeof(T), s);
@@ -571,7 +616,33 @@ void heev_1gpu(i64 n, T* Af, std::vector<double>& w, T* Z, bool wantz, hipStream
     }
     NTRACE("heev::back_transform", s);
     real_to_phase<T>(n, n, Qt.as<double>(), n, phd ? kp(phd->as<T>()) : nullptr, kp(Z), n, s);
-    if (nsw > 0 && total > 0) {
+    bool q2_done = false;
+    if constexpr (std::is_same<T, double>::value) {
+        // fp64, b = 64: groups of b reflectors (sweep block J, task t) as
+        // block reflectors I - V T V^H on MFMA (eig.hip unmtr_hb2st_mfma,
+        // the Python path's form; the register-window kernel below is the
+        // other precisions' path)
+        if (b == 64 && nsw > 0 && total > 0) {
+            std::vector<i64> gJ, gt, gptr(1, 0);
+            for (i64 J = 0; J * b < nsw; ++J) {
+                const i64 TJ = nt[(size_t)(J * b)];
+                for (i64 t = 0; t < TJ; ++t) { gJ.push_back(J); gt.push_back(t); }
+                gptr.push_back(gptr.back() + TJ);
+            }
+            const i64 ng = (i64)gJ.size();
+            if (ng > 0) {
+                Scratch* gJd = upload_vec(keep, gJ, s);
+                Scratch* gtd = upload_vec(keep, gt, s);
+                Scratch* gpd = upload_vec(keep, gptr, s);
+                Scratch Tg((size_t)ng * 2 * b * b * sizeof(double), s);
+                q2_done = slate_hip::unmtr_hb2st_mfma(n, n, Z, n, V.as<double>(), b, tau.as<double>(), spd->as<i64>(),
+                                                      ntd->as<i64>(), gJd->as<i64>(), gtd->as<i64>(), gpd->as<i64>(), ng,
+                                                      Tg.as<double>(), nsw, s);
+                NHIP(hipStreamSynchronize(s));
+            }
+        }
+    }
+    if (nsw > 0 && total > 0 && !q2_done) {
         if (!slate_hip::unmtr_hb2st_blocked<K<T>>(n, n, kp(Z), n, kp(V.as<T>()), b, kp(tau.as<T>()), spd->as<i64>(),
                                                   ntd->as<i64>(), nsw, false, s)) {
             for (i64 j = n - 1; j >= 0; --j) {
