@@ -21,6 +21,7 @@
 // src/gemmC.cc:39-202, src/work/work_trsm.cc:102-265 (SLATE's OpenMP task
 // DAGs over MPI).
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <limits>
 #include <functional>
@@ -1528,6 +1529,153 @@ int64_t getrf_tntpiv(Matrix<T>& A, std::vector<int64_t>& ipiv, const Options& op
     return getrf<T>(A, ipiv, o);
 }
 
+// 1 x q LU with RowMajor rows (SLATE getrf.cc:51-55 on GPUs; models/lu.py
+// _getrf_p1 with T): the local block is factored TRANSPOSED, T = buf^T
+// (nloc x m, ld ldt), so a row interchange of A swaps two contiguous columns
+// of T (whole cache lines, one folded swap plan per step for every column
+// range) and the trailing update is the NT GEMM T22 -= U12^T L21^T.  Each
+// panel is copied out column-major into a ring slot for the persistent
+// panel kernel and written back transposed.  Wide trailing ranges take the
+// U rows from the explicit L11 inverse (one GEMM instead of the blocked
+// substitution); buf stays intact until the final copy back, so a step
+// whose inverse grew beyond SLATE_AMD_LU_INV_GROWTH (1e6) makes the caller
+// redo the factorization with the substitution (returns true).
+template <typename T>
+static bool getrf_p1_rm(Storage& S, int la, double thr, i64* ipiv_d, i64* infos, bool no_inv) {
+    using Rl = real_t<T>;
+    Runtime& R = rt();
+    GridComms* gc = S.gc;
+    const int q = S.q, pc = S.pc;
+    const i64 nb = S.nb, m = S.m, n = S.n, lld = S.lld, nloc = S.nloc;
+    const i64 kt = std::min((m + nb - 1) / nb, (n + nb - 1) / nb);
+    T* buf = static_cast<T*>(S.buf);
+    hipStream_t ps = R.panel, us = R.update;
+    const i64 ldt = std::max<i64>(1, (nloc + 7) / 8 * 8);
+    Scratch Tm((size_t)ldt * std::max<i64>(m, 1) * sizeof(T), R.main);
+    T* Tt = Tm.as<T>();
+    const i64 inv_min = no_inv ? 0 : env_int("SLATE_AMD_LU_INV_MIN", 4096);
+    Scratch growth(sizeof(Rl) * (size_t)std::max<i64>(kt, 1), R.main);
+    dzero(growth.p, sizeof(Rl) * (size_t)std::max<i64>(kt, 1), R.main);
+    join(R.main, ps);
+    join(R.main, us);
+    const int NR = la + 3;
+    std::vector<std::unique_ptr<Scratch>> ring;
+    for (int r = 0; r < NR; ++r) ring.push_back(std::make_unique<Scratch>((size_t)std::max<i64>(m, 1) * nb * sizeof(T), ps));
+    std::vector<std::unique_ptr<Scratch>> plans((size_t)kt), linv((size_t)kt);
+    std::vector<std::unique_ptr<Event>> ev_tr((size_t)kt), ev_used((size_t)kt);
+    std::vector<std::array<i64, 2>> left;            // (step, left columns)
+    const i64 tail = (i64)(kt * 0.6);
+    // buf -> T: the bulk on the update stream, concurrently with panel 0
+    // (which reads buf itself); the lookahead columns on the panel stream
+    const i64 lcla0 = std::min(tiles_before(1 + la, q, pc) * nb, nloc);
+    if (nloc > lcla0 && m > 0)
+        slate_hip::gecopy<K<T>, K<T>>('G', 'T', nloc - lcla0, m, kp(buf + lcla0 * lld), lld, kp(Tt + lcla0), ldt, us);
+    for (i64 k = 0; k < kt; ++k) {
+        const i64 r0 = k * nb;
+        const i64 kb = std::min({nb, n - r0, m - r0});
+        const i64 mk = m - r0;
+        const bool own = (k % q) == pc;
+        const i64 lck = tiles_before(k, q, pc) * nb;
+        const i64 lc1 = std::min(tiles_before(k + 1, q, pc) * nb, nloc);
+        const i64 lcla = std::min(tiles_before(k + 1 + la, q, pc) * nb, nloc);
+        if (k - la - 1 >= 0) ev_tr[k - la - 1]->wait(ps);
+        if (k >= NR) ev_used[k - NR]->wait(ps);
+        T* Lp = ring[k % NR]->as<T>();
+        const i64 ldl = mk;
+        {
+            NTRACE("getrf::panel", ps);
+            if (own) {
+                const i64 wk = std::min(nb, n - r0);
+                if (k == 0) copy2d(Lp, ldl, buf + r0 + lck * lld, lld, mk, wk, ps);
+                else slate_hip::gecopy<K<T>, K<T>>('G', 'T', mk, wk, kp(Tt + lck + r0 * ldt), ldt, kp(Lp), ldl, ps);
+                slate_hip::getrf_panel_ws<K<T>>(mk, wk, kp(Lp), ldl, ipiv_d + r0, infos + k, thr, false, R.lu_work, ps);
+                slate_hip::gecopy<K<T>, K<T>>('G', 'T', wk, mk, kp(Lp), ldl, kp(Tt + lck + r0 * ldt), ldt, ps);
+            }
+            if (q > 1) {
+                gc->row->bcast(ipiv_d + r0, (size_t)kb * sizeof(i64), (int)(k % q), ps);
+                gc->row->bcast(Lp, (size_t)mk * kb * sizeof(T), (int)(k % q), ps);
+            }
+            plans[k] = std::make_unique<Scratch>(slate_hip::swap_plan_bytes(), ps);
+            slate_hip::swap_plan(r0, r0 + kb, ipiv_d, -r0, 1, plans[k]->p, ps);
+        }
+        const T* Li = nullptr;
+        if (inv_min && nloc - lcla >= inv_min && kb == nb) {
+            linv[k] = std::make_unique<Scratch>((size_t)kb * kb * sizeof(T), ps);
+            slate_hip::tri_inv<K<T>>('L', 'U', kb, kp(Lp), ldl, kp(linv[k]->template as<T>()), kb, ps);
+            Scratch cm((size_t)(2 * kb + 2) * sizeof(Rl), ps), c1v((size_t)(kb + 2) * sizeof(Rl), ps);
+            slate_hip::genorm<K<T>, Rl>('M', 'G', 'N', 0, kb, kb, kp(linv[k]->template as<T>()), kb, cm.as<Rl>(), ps);
+            slate_hip::genorm<Rl, Rl>('M', 'G', 'N', 0, kb, 1, cm.as<Rl>(), kb, c1v.as<Rl>(), ps);
+            dcopy(growth.as<Rl>() + k, c1v.p, sizeof(Rl), ps);
+            Li = linv[k]->template as<T>();
+        }
+        const void* plan = plans[k]->p;
+        auto update = [&](i64 c0, i64 c1, hipStream_t s) {
+            if (c1 <= c0) return;
+            const i64 w = c1 - c0;
+            slate_hip::laswp_cols_plan<K<T>>(w, kp(Tt + c0), ldt, plan, s);
+            T* Ut = Tt + c0 + r0 * ldt;
+            if (Li) {
+                Scratch tmp((size_t)w * kb * sizeof(T), s);
+                copy2d(tmp.as<T>(), w, Ut, ldt, w, kb, s);
+                gemm_k<T>('N', 'T', w, kb, kb, T(1), tmp.as<T>(), w, Li, kb, T(0), Ut, ldt, s);
+            } else {
+                slate_hip::trsm<K<T>>('R', 'L', 'T', 'U', w, kb, kv(T(1)), kp(Lp), ldl, kp(Ut), ldt, s);
+            }
+            if (m > r0 + kb)
+                gemm_k<T>('N', 'T', w, m - r0 - kb, kb, T(-1), Ut, ldt, Lp + kb, ldl, T(1), Tt + c0 + (r0 + kb) * ldt,
+                          ldt, s);
+        };
+        if (k >= 1 && la > 0) ev_tr[k - 1]->wait(ps);
+        if (k == 0 && lcla > lc1)
+            slate_hip::gecopy<K<T>, K<T>>('G', 'T', lcla - lc1, m, kp(buf + lc1 * lld), lld, kp(Tt + lc1), ldt, ps);
+        {
+            NTRACE("getrf::lookahead", ps);
+            update(lc1, lcla, ps);
+        }
+        Event ev_panel;
+        ev_panel.record(ps);
+        ev_panel.wait(us);
+        const i64 lcnx = std::max(std::min(tiles_before(k + 2 + la, q, pc) * nb, nloc), lcla);
+        {
+            NTRACE("getrf::update", us);
+            update(lcla, lcnx, us);
+            ev_tr[k] = std::make_unique<Event>();
+            ev_tr[k]->record(us);
+            update(lcnx, nloc, us);
+        }
+        // the factored columns left of the panel: their interchanges are
+        // deferred into the panel-bound tail and spread over its steps
+        if (lck > 0) left.push_back({k, lck});
+        if (k >= tail) {
+            const i64 todo = ((i64)left.size() + std::max<i64>(1, kt - k) - 1) / std::max<i64>(1, kt - k);
+            for (i64 t = 0; t < todo && !left.empty(); ++t) {
+                const auto it = left.front();
+                left.erase(left.begin());
+                slate_hip::laswp_cols_plan<K<T>>(it[1], kp(Tt), ldt, plans[it[0]]->p, us);
+            }
+        }
+        ev_used[k] = std::make_unique<Event>();
+        ev_used[k]->record(us);
+    }
+    for (auto& it : left) slate_hip::laswp_cols_plan<K<T>>(it[1], kp(Tt), ldt, plans[it[0]]->p, us);
+    join(us, ps);
+    join(ps, R.main);
+    for (auto& x : ring) x->s = R.main;
+    for (auto& x : plans) if (x) x->s = R.main;
+    for (auto& x : linv) if (x) x->s = R.main;
+    if (inv_min) {
+        const double lim = [] { const char* e = std::getenv("SLATE_AMD_LU_INV_GROWTH"); return e ? std::atof(e) : 1e6; }();
+        std::vector<Rl> g((size_t)std::max<i64>(kt, 1));
+        NHIP(hipMemcpyAsync(g.data(), growth.p, g.size() * sizeof(Rl), hipMemcpyDeviceToHost, R.main));
+        NHIP(hipStreamSynchronize(R.main));
+        for (Rl v : g)
+            if (!((double)v <= lim)) return true;       // NaN or too large: redo with the substitution
+    }
+    if (nloc && m) slate_hip::gecopy<K<T>, K<T>>('G', 'T', m, nloc, kp(Tt), ldt, kp(buf), lld, R.main);
+    NHIP(hipStreamSynchronize(R.main));
+    return false;
+}
+
 template <typename T>
 int64_t getrf(Matrix<T>& A, std::vector<int64_t>& ipiv_out, const Options& opts) {
     NTRACE("getrf", nullptr);
@@ -1548,7 +1696,14 @@ int64_t getrf(Matrix<T>& A, std::vector<int64_t>& ipiv_out, const Options& opts)
     i64* ipiv_d = ipiv.as<i64>();
     join(R.main, ps);
     join(R.main, us);
-    if (p == 1) {
+    const bool rowmajor = p == 1 && opts.lu_method != 1 && kt > 0 && env_int("SLATE_AMD_NATIVE_LU_ROWMAJOR", 1) != 0;
+    if (rowmajor) {
+        if (getrf_p1_rm<T>(S, la, opts.pivot_threshold, ipiv_d, infos.as<i64>(), false)) {
+            dzero(ipiv.p, sizeof(i64) * std::max<i64>(kmin, 1), R.main);
+            dzero(infos.p, sizeof(i64) * std::max<i64>(kt, 1), R.main);
+            getrf_p1_rm<T>(S, la, opts.pivot_threshold, ipiv_d, infos.as<i64>(), true);
+        }
+    } else if (p == 1) {
         // ---- 1 x q: full-height panels on their owner (persistent LU
         //      panel), lookahead; models/lu.py _getrf_p1
         std::vector<std::unique_ptr<Event>> ev_tr((size_t)kt), ev_used((size_t)kt);
