@@ -58,7 +58,14 @@ def _upper_to_lower(A, fn, opts):
 
 
 def potrf(A, opts=None) -> int:
-    """Cholesky factorization A = L L^H (or U^H U). Returns info (0 = ok)."""
+    """Cholesky factorization A = L L^H (or U^H U). Returns info (0 = ok).
+
+    Memory: a host-origin matrix larger than the device budget is factored
+    OUT OF CORE (left-looking block-column streaming) on ONE rank only.  On a
+    p x q grid with p q > 1 every rank stages its whole local block on its
+    GPU (288 GB of HBM3E per MI355X: a 2 x 4 grid holds n ~ 160k fp64 in
+    core); a larger problem needs a larger grid (SLATE's workspace streaming
+    for p x q, BaseMatrix.hh:2640-2781, is not implemented)."""
     if A.uplo() == Uplo.Upper and A.op() == Op.NoTrans:
         return _upper_to_lower(A, potrf, opts)
     if A.op() != Op.NoTrans:

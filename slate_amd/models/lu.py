@@ -43,7 +43,14 @@ from ..utils import watchdog as _wd
 
 
 def getrf(A, pivots: Pivots, opts=None) -> int:
-    """LU factorization P A = L U; returns info (0 = success)."""
+    """LU factorization P A = L U; returns info (0 = success).
+
+    Memory: a host-origin matrix larger than the device budget is factored
+    OUT OF CORE (left-looking block-column streaming) on ONE rank only.  On a
+    p x q grid with p q > 1 every rank stages its whole local block on its
+    GPU (288 GB of HBM3E per MI355X: a 2 x 4 grid holds n ~ 160k fp64 in
+    core); a larger problem needs a larger grid (SLATE's workspace streaming
+    for p x q, BaseMatrix.hh:2640-2781, is not implemented)."""
     method = get_option(opts, Option.MethodLU, MethodLU.PartialPiv)
     if method == MethodLU.NoPiv:
         return getrf_nopiv(A, opts)

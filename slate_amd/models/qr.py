@@ -87,7 +87,14 @@ def _check(A):
 # ------------------------------------------------------------------ geqrf
 def geqrf(A, T: TriangularFactors, opts=None) -> int:
     """A = Q R.  R overwrites the upper triangle, reflectors the lower part;
-    T receives the per-panel block-reflector factors."""
+    T receives the per-panel block-reflector factors.
+
+    Memory: a host-origin matrix larger than the device budget is factored
+    OUT OF CORE (left-looking block-column streaming) on ONE rank only.  On a
+    p x q grid with p q > 1 every rank stages its whole local block on its
+    GPU (288 GB of HBM3E per MI355X: a 2 x 4 grid holds n ~ 160k fp64 in
+    core); a larger problem needs a larger grid (SLATE's workspace streaming
+    for p x q, BaseMatrix.hh:2640-2781, is not implemented)."""
     s = A.storage
     if s.bc is None:
         from .aux import run_on_block_cyclic
