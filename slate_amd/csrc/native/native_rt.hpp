@@ -121,6 +121,7 @@ struct Runtime {
     int rank = 0, size = 1, local = 0, device = 0;
     hipStream_t main = nullptr, panel = nullptr, update = nullptr, comm = nullptr;
     int update_res = 0;     // CUs the live update stream leaves free (set_update_reservation)
+    std::map<int, hipStream_t> parked;   // update streams of the other reservations (kept, not destroyed)
     void* lu_work = nullptr;
     void* qr_work = nullptr;
     std::map<std::pair<int, int>, std::unique_ptr<GridComms>> grids;
