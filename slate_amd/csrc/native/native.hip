@@ -79,7 +79,12 @@ static void initialize_rt() {
     NHIP(hipStreamCreateWithFlags(&R.main, hipStreamNonBlocking));
     NHIP(hipStreamCreateWithPriority(&R.panel, hipStreamNonBlocking, hi));
     NHIP(hipStreamCreateWithPriority(&R.update, hipStreamNonBlocking, lo));
-    NHIP(hipStreamCreateWithPriority(&R.comm, hipStreamNonBlocking, hi));
+    // one rank: no collectives, so no comm stream of its own -- the box has
+    // 4 hardware queues, and a 5th stream (the CU-masked update stream is
+    // created next to the plain one) could put the high-priority panel
+    // stream on the queue of the bulk GEMMs (ADVICE r4 for the Python path)
+    if (R.size > 1) NHIP(hipStreamCreateWithPriority(&R.comm, hipStreamNonBlocking, hi));
+    else R.comm = R.main;
     // diagnostics: SLATE_AMD_NATIVE_SERIAL=1 issues everything on one stream
     if (env_int("SLATE_AMD_NATIVE_SERIAL", 0)) R.panel = R.update = R.comm = R.main;
     const size_t lw = slate_hip::getrf_work_bytes();
@@ -125,9 +130,11 @@ void finalize() {
 }
 
 // The update streams of each reservation are created once per process and
-// kept (parked), as the Python StreamSet does: re-creating the masked stream
-// per factorization cost 3 % of a native dgetrf (n = 32768: 662.8 -> 642.2
-// ms per step with the stream kept, profiles/r6/getrf_reservation_keep.txt).
+// kept (parked) on one rank: re-creating the masked stream per
+// factorization cost 3 % of a native dgetrf, and a fifth stream next to a
+// comm stream of its own put the panel stream on the bulk GEMMs' hardware
+// queue (the box has 4): dgetrf n = 32768 36.5 -> 43.3 TF/s with the comm
+// stream aliased to main on one rank (profiles/r6/getrf_reservation_keep.txt).
 void set_update_reservation(int cus) {
     Runtime& R = rt();
     if (cus == R.update_res || R.update == R.main) return;
@@ -140,7 +147,11 @@ void set_update_reservation(int cus) {
     if (!(cus > 0 && cus < ncu)) cus = 0;
     if (cus == R.update_res) return;
     NHIP(hipStreamSynchronize(R.update));
-    R.parked[R.update_res] = R.update;
+    // one rank (comm = main): park the old stream -- 4 streams in all.  With a
+    // comm stream of its own a parked 5th stream could share a hardware
+    // queue with the panel stream: destroy it instead
+    if (R.size == 1) R.parked[R.update_res] = R.update;
+    else NHIP(hipStreamDestroy(R.update));
     auto it = R.parked.find(cus);
     if (it != R.parked.end() && it->second) {
         R.update = it->second;
