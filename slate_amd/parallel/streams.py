@@ -15,6 +15,7 @@ path every call is a no-op and work runs in program order.
 """
 from __future__ import annotations
 
+import os
 import contextlib
 
 import torch
@@ -28,6 +29,7 @@ import torch
 # communicators queued behind one another in different orders on different
 # ranks can deadlock).
 _SHARED = {}
+_SHIFT_STREAMS = []        # idle streams of SLATE_AMD_QUEUE_SHIFT (kept alive)
 MAX_WORK_STREAMS = 4
 
 
@@ -136,6 +138,12 @@ class StreamSet:
                 idx = device.index if device.index is not None else torch.cuda.current_device()
                 ncu = H.cu_count(idx)
                 if 0 < reserve < ncu:
+                    # SLATE_AMD_QUEUE_SHIFT=k (diagnostics): create k idle
+                    # streams first, moving the update stream to another of
+                    # the box's 4 hardware queues (streams map round-robin)
+                    shift = int(os.environ.get("SLATE_AMD_QUEUE_SHIFT", "0"))
+                    for _ in range(max(0, shift)):
+                        _SHIFT_STREAMS.append(H.stream_create(idx))
                     words = [0] * ((ncu + 31) // 32)
                     for b in range(reserve, ncu):
                         words[b // 32] |= 1 << (b % 32)
