@@ -916,7 +916,12 @@ void he2hb_grid(Storage& F, std::vector<GPanel<T>>& pans, hipStream_t s) {
     }
 }
 
-// Z := Q1 Z on F's grid (Z shares F's layout); panels last to first
+// Z := Q1 Z on F's grid (Z shares F's layout); panels last to first, G
+// consecutive panels merged into one block reflector (as the one-GPU
+// unmtr_he2hb): Vg = this rank's rows of the group's reflectors (each
+// panel's rows broadcast along the process row from its owner column),
+// Tg from the forward larft merge with V_prev^H V_i summed over the process
+// column -- one W = Vg^H Z all-reduce per group instead of per panel.
 template <typename T>
 void unmtr_he2hb_grid(const Storage& F, std::vector<GPanel<T>>& pans, Storage& Zs, hipStream_t s) {
     GridComms* gc = F.gc;
@@ -926,6 +931,76 @@ void unmtr_he2hb_grid(const Storage& F, std::vector<GPanel<T>>& pans, Storage& Z
     T* Z = static_cast<T*>(Zs.buf);
     const char ct = ctrans<T>();
     const size_t es = sizeof(T);
+    static const i64 G = [] { const char* e = std::getenv("SLATE_AMD_UNMTR_HE2HB_GROUP"); return e ? std::max(1, std::atoi(e)) : 4; }();
+    // this rank's rows of panel i's reflectors (nmine_i x kk_i, ld max(nmine_i, 1)), every rank of the row
+    auto panel_rows = [&](const GPanel<T>& pn, i64& lr0, i64& nmine) {
+        const i64 k = pn.k, kk = pn.kk;
+        const int ck = (int)(k % q);
+        lr0 = std::min(tiles_before(k + 1, p, pr) * nb, mloc);
+        nmine = mloc - lr0;
+        const i64 lc_k = tiles_before(k, q, pc) * nb;
+        auto V = std::make_unique<Scratch>((size_t)std::max<i64>(nmine, 1) * kk * es, s);
+        if (nmine) {
+            if (pc == ck) {
+                if (pr == (int)((k + 1) % p))
+                    slate_hip::v_explicit<K<T>>(nmine, kk, kp(fb + lr0 + lc_k * lld), lld, kp(V->template as<T>()),
+                                                nmine, s);
+                else
+                    copy2d(V->template as<T>(), nmine, fb + lr0 + lc_k * lld, lld, nmine, kk, s);
+            }
+            if (q > 1) gc->row->bcast(V->p, (size_t)nmine * kk * es, ck, s);
+        }
+        return V;
+    };
+    if (G > 1) {
+        i64 i1 = (i64)pans.size();
+        while (i1 > 0) {
+            const i64 i0 = std::max<i64>(0, i1 - G);
+            i64 kt = 0;
+            for (i64 i = i0; i < i1; ++i) kt += pans[i].kk;
+            const i64 lrg = std::min(tiles_before(pans[i0].k + 1, p, pr) * nb, mloc), mg = mloc - lrg;
+            const i64 ldv = std::max<i64>(mg, 1);
+            Scratch Vg((size_t)ldv * kt * es, s), Tg((size_t)kt * kt * es, s);
+            dzero(Vg.p, (size_t)ldv * kt * es, s);
+            dzero(Tg.p, (size_t)kt * kt * es, s);
+            T* vg = Vg.as<T>();
+            T* tg = Tg.as<T>();
+            i64 c = 0;
+            for (i64 i = i0; i < i1; ++i) {
+                i64 lr0 = 0, nmine = 0;
+                const auto V = panel_rows(pans[i], lr0, nmine);
+                const i64 kb = pans[i].kk, off = lr0 - lrg;
+                if (nmine) copy2d(vg + off + c * ldv, ldv, V->template as<T>(), nmine, nmine, kb, s);
+                copy2d(tg + c + c * kt, kt, pans[i].T_->template as<T>(), kb, kb, kb, s);
+                if (c) {
+                    // T12 = -T_prev (V_prev^H V_i) T_i, V_prev^H V_i summed over the process column
+                    Scratch S1((size_t)c * kb * es, s), S2((size_t)c * kb * es, s);
+                    if (nmine)
+                        gemm_k<T>(ct, 'N', c, kb, nmine, T(1), vg + off, ldv, V->template as<T>(), nmine, T(0),
+                                  S1.as<T>(), c, s);
+                    else
+                        slate_hip::geset<K<T>>('G', c, kb, kv(T(0)), kv(T(0)), kp(S1.as<T>()), c, s);
+                    if (p > 1) gc->col->allreduce(S1.p, (size_t)(c * kb), dt_of<T>::v, 's', s);
+                    gemm_k<T>('N', 'N', c, kb, c, T(1), tg, kt, S1.as<T>(), c, T(0), S2.as<T>(), c, s);
+                    gemm_k<T>('N', 'N', c, kb, kb, T(-1), S2.as<T>(), c, pans[i].T_->template as<T>(), kb, T(0),
+                              tg + c * kt, kt, s);
+                }
+                c += kb;
+                NHIP(hipStreamSynchronize(s));
+            }
+            if (nz) {
+                Scratch W((size_t)kt * nz * es, s), W2((size_t)kt * nz * es, s);
+                if (mg) gemm_k<T>(ct, 'N', kt, nz, mg, T(1), vg, ldv, Z + lrg, ldz, T(0), W.as<T>(), kt, s);
+                else slate_hip::geset<K<T>>('G', kt, nz, kv(T(0)), kv(T(0)), kp(W.as<T>()), kt, s);
+                if (p > 1) gc->col->allreduce(W.p, (size_t)(kt * nz), dt_of<T>::v, 's', s);
+                gemm_k<T>('N', 'N', kt, nz, kt, T(1), tg, kt, W.as<T>(), kt, T(0), W2.as<T>(), kt, s);
+                if (mg) gemm_k<T>('N', 'N', mg, nz, kt, T(-1), vg, ldv, W2.as<T>(), kt, T(1), Z + lrg, ldz, s);
+            }
+            NHIP(hipStreamSynchronize(s));
+            i1 = i0;
+        }
+        return;
+    }
     for (auto it = pans.rbegin(); it != pans.rend(); ++it) {
         const i64 k = it->k, kk = it->kk;
         const int ck = (int)(k % q);
