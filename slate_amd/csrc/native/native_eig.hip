@@ -366,6 +366,12 @@ void zero_strict_lower(i64 m, i64 k, T* P, i64 ld, hipStream_t s) {
 template <typename T>
 void he2hb(i64 n, i64 nb, T* Af, i64 ld, std::vector<Panel<T>>& panels, hipStream_t s) {
     const char ct = ctrans<T>();
+    // per-call workspaces sized for the first (largest) panel: no allocation
+    // inside the panel loop (the loop is launch-bound at the small panels)
+    const i64 mmax = std::max<i64>(n - nb, 1);
+    Scratch tau((size_t)nb * sizeof(T), s), X((size_t)mmax * nb * sizeof(T), s),
+        VW((size_t)mmax * 2 * nb * sizeof(T), s), WV((size_t)mmax * 2 * nb * sizeof(T), s),
+        Mt((size_t)nb * nb * sizeof(T), s);
     for (i64 k0 = 0; k0 < n - nb; k0 += nb) {
         const i64 r0 = k0 + nb, kb = std::min(nb, n - k0), m = n - r0;
         if (m <= 0) break;
@@ -376,7 +382,6 @@ void he2hb(i64 n, i64 nb, T* Af, i64 ld, std::vector<Panel<T>>& panels, hipStrea
         pn.kk = kk;
         pn.V = std::make_unique<Scratch>((size_t)m * kk * sizeof(T), s);
         pn.T_ = std::make_unique<Scratch>((size_t)kk * kk * sizeof(T), s);
-        Scratch tau((size_t)kk * sizeof(T), s);
         dzero(tau.p, (size_t)kk * sizeof(T), s);
         T* V = pn.V->template as<T>();
         T* Tm = pn.T_->template as<T>();
@@ -386,14 +391,11 @@ void he2hb(i64 n, i64 nb, T* Af, i64 ld, std::vector<Panel<T>>& panels, hipStrea
         // (gecopy's m x n are the DESTINATION's: kb x m here)
         slate_hip::gecopy<K<T>, K<T>>('G', ct, kb, m, kp(P), ld, kp(Af + k0 + r0 * ld), ld, s);
         // X = V T, Y = A22 X, M = X^H Y, W = Y - V M / 2, A22 -= V W^H + W V^H
-        Scratch X((size_t)m * kk * sizeof(T), s);
         copy2d(X.as<T>(), m, V, m, m, kk, s);
         slate_hip::trmm<K<T>>('R', 'U', 'N', 'N', m, kk, kv(T(1)), kp(Tm), kk, kp(X.as<T>()), m, s);
-        Scratch VW((size_t)m * 2 * kk * sizeof(T), s), WV((size_t)m * 2 * kk * sizeof(T), s);
         T* Y = VW.as<T>() + m * kk;
         T* A22 = Af + r0 + r0 * ld;
         gemm_k<T>('N', 'N', m, kk, m, T(1), A22, ld, X.as<T>(), m, T(0), Y, m, s);
-        Scratch Mt((size_t)kk * kk * sizeof(T), s);
         gemm_k<T>(ct, 'N', kk, kk, m, T(1), X.as<T>(), m, Y, m, T(0), Mt.as<T>(), kk, s);
         gemm_k<T>('N', 'N', m, kk, kk, T(-0.5), V, m, Mt.as<T>(), kk, T(1), Y, m, s);
         copy2d(VW.as<T>(), m, V, m, m, kk, s);
