@@ -1827,6 +1827,9 @@ int64_t getrf(Matrix<T>& A, std::vector<int64_t>& ipiv_out, const Options& opts)
         if (gflat.empty()) gflat.push_back(0);
         Scratch gall(gflat.size() * sizeof(i64), ps);
         upload(gall.p, gflat.data(), gflat.size() * sizeof(i64), ps);
+        std::vector<std::unique_ptr<Event>> ev_tr((size_t)kt);
+        std::vector<std::unique_ptr<Scratch>> packs;        // step packs still read by the update stream
+        if (p2p && la > 0) join(ps, us);
         for (i64 k = 0; k < kt; ++k) {
             const i64 r0 = k * nb;
             const i64 kb = std::min({nb, n - r0, m - r0});
@@ -1859,26 +1862,57 @@ int64_t getrf(Matrix<T>& A, std::vector<int64_t>& ipiv_out, const Options& opts)
             if (q > 1) rowc->bcast(pack.p, lbytes + tbytes + (size_t)kb * sizeof(i64), ck, ps);
             dcopy(ipiv_d + r0, pv, (size_t)kb * sizeof(i64), ps);
             if (p2p) {
-                // exact moves: the step's pivots to the host (this path runs
-                // on one stream, the panel's, so the wait costs no overlap)
+                // exact moves: the step's pivots to the host (a wait on the
+                // panel stream only: the update stream keeps running the
+                // previous step's trailing GEMM meanwhile)
                 std::vector<i64> hpv((size_t)kb);
                 NHIP(hipMemcpyAsync(hpv.data(), pv, (size_t)kb * sizeof(i64), hipMemcpyDeviceToHost, ps));
                 NHIP(hipStreamSynchronize(ps));
-                p2p_rows<T>(S, fold_moves(hpv, r0), {{lc1, nloc}, {0, lck}}, colc, ps);
-                const i64 w = nloc - lc1;
-                if (w > 0) {
-                    // U rows on the window's process row, then down the column
-                    Scratch Ub((size_t)kb * w * sizeof(T), ps);
+                const auto mv = fold_moves(hpv, r0);
+                // U rows of columns [c0, c1) on the window's process row, down
+                // the column over `cc`, then the GEMM -- on stream s
+                auto urows = [&](i64 c0, i64 c1, Comm* cc, hipStream_t s) {
+                    const i64 w = c1 - c0;
+                    if (w <= 0) return;
+                    Scratch Ub((size_t)kb * w * sizeof(T), s);
                     if (pr == rk) {
                         slate_hip::trsm<K<T>>('L', 'L', 'N', 'U', kb, w, kv(T(1)), kp(Tt), kb,
-                                              kp(buf + lr_k + lc1 * lld), lld, ps);
-                        copy2d(Ub.as<T>(), kb, buf + lr_k + lc1 * lld, lld, kb, w, ps);
+                                              kp(buf + lr_k + c0 * lld), lld, s);
+                        copy2d(Ub.as<T>(), kb, buf + lr_k + c0 * lld, lld, kb, w, s);
                     }
-                    colc->bcast(Ub.p, (size_t)kb * w * sizeof(T), rk, ps);
+                    cc->bcast(Ub.p, (size_t)kb * w * sizeof(T), rk, s);
                     if (mloc > lr1)
                         gemm_k<T>('N', 'N', mloc - lr1, w, kb, T(-1), Lp + (lr1 - lr_k), std::max<i64>(nmine, 1),
-                                  Ub.as<T>(), kb, T(1), buf + lr1 + lc1 * lld, lld, ps);
+                                  Ub.as<T>(), kb, T(1), buf + lr1 + c0 * lld, lld, s);
+                };
+                if (la == 0) {
+                    p2p_rows<T>(S, mv, {{lc1, nloc}, {0, lck}}, colc, ps);
+                    urows(lc1, nloc, colc, ps);
+                    continue;
                 }
+                // lookahead (models/lu.py _getrf_general; SLATE getrf.cc:85-235):
+                // the next la tile columns on the panel stream over the column
+                // communicator, the rest on the update stream over its own
+                // second column communicator (two streams never share one
+                // communicator); the panel of step k+1 then only waits for
+                // this step's lookahead columns
+                const i64 lcla = std::min(tiles_before(k + 1 + la, q, pc) * nb, nloc);
+                if (k >= 1) ev_tr[k - 1]->wait(ps);        // the newest lookahead column was step k-1's trailing
+                p2p_rows<T>(S, mv, {{lc1, lcla}}, colc, ps);
+                urows(lc1, lcla, colc, ps);
+                Event ev_la;
+                ev_la.record(ps);
+                ev_la.wait(us);
+                packs.push_back(std::make_unique<Scratch>(0, ps));
+                packs.back()->p = pack.p;                      // the pack stays alive for the update stream
+                pack.p = nullptr;
+                Comm* colu = gc->colu ? gc->colu.get() : colc;
+                p2p_rows<T>(S, mv, {{lcla, nloc}, {0, lck}}, colu, us);
+                const i64 lcnx = std::max(std::min(tiles_before(k + 2 + la, q, pc) * nb, nloc), lcla);
+                urows(lcla, lcnx, colu, us);
+                ev_tr[k] = std::make_unique<Event>();
+                ev_tr[k]->record(us);
+                urows(lcnx, nloc, colu, us);
                 continue;
             }
             // every local column except the panel's own: interchanges, then
@@ -1905,7 +1939,7 @@ int64_t getrf(Matrix<T>& A, std::vector<int64_t>& ipiv_out, const Options& opts)
             trailing(lc1, nloc);            // the trailing columns
             trailing(0, lck);               // the factored columns on the left
         }
-        (void)la;
+        if (!packs.empty()) join(us, ps);                  // the packs are freed on ps after the update stream's last use
     }
     join(ps, R.main);
     join(us, R.main);
