@@ -488,6 +488,19 @@ void dbg_resid(const char* tag, i64 n, const T* M, i64 ldm, const T* Z, i64 ldz,
     std::fprintf(stderr, "heev debug %s: residual %.3e\n", tag, std::sqrt(e / std::max(an, 1e-300)) / (double)n);
 }
 
+// the band |i - j| <= b of the dense Af (both triangles) into the skewed
+// band layout of the chase (element (i, j) at i + j ldb, ldb = 4b + 8; see
+// heev_grid): one block per column, a thread per diagonal offset
+template <typename T>
+__global__ void band_from_dense_kernel(i64 n, int b, const T* __restrict__ A, i64 lda, T* __restrict__ B, i64 ldb) {
+    const i64 j = blockIdx.x;
+    const int dlt = (int)threadIdx.x - b;
+    if (j >= n || threadIdx.x > 2 * b) return;
+    const i64 i = j + dlt;
+    if (i < 0 || i >= n) return;
+    B[i + j * ldb] = A[i + j * lda];
+}
+
 // ---------------------------------------------------------------- one-GPU heev
 // Af: dense Hermitian n x n (ld n, both triangles) on this device; w: the
 // eigenvalues; Z (n x n, ld n) the eigenvectors when wantz
@@ -521,10 +534,23 @@ void heev_1gpu(i64 n, T* Af, std::vector<double>& w, T* Z, bool wantz, hipStream
     const i64 total = nsw ? sp[n - 1] + nt[nsw - 1] : 0;
     // leading dimension off powers of two (the chase touches ~3b columns of
     // one row band: a 2^k stride would put them on one channel)
-    const i64 ldp = (n + 7) / 8 * 8 + 72;
+    // skewed band layout (default; SLATE_AMD_NATIVE_HB2ST_SKEW=0: the dense
+    // n x n copy): the chase touches |i - j| < 2b only, so the band of
+    // (4b + 9) n words replaces the n^2 working copy and keeps a task's
+    // window contiguous
+    static const bool skew = [] { const char* e = std::getenv("SLATE_AMD_NATIVE_HB2ST_SKEW"); return !(e && e[0] == '0'); }() && !dbg;
+    const i64 ldp = skew ? 4 * b + 8 : (n + 7) / 8 * 8 + 72;
+    const i64 extent = skew ? (n - 1) * (ldp + 1) + 1 : ldp * std::max<i64>(n, 1);
     // the band |i - j| <= b only (models/eig.py _band_only): two masked copies
-    Scratch Bh((size_t)ldp * std::max<i64>(n, 1) * sizeof(T), s);
-    {
+    Scratch Bh((size_t)(extent + 16) * sizeof(T), s);
+    if (skew) {
+        dzero(Bh.p, (size_t)(extent + 16) * sizeof(T), s);
+        if (n > 0) {
+            hipLaunchKernelGGL(band_from_dense_kernel<K<T>>, dim3((unsigned)n), dim3((unsigned)(2 * b + 1)), 0, s, n,
+                               (int)b, kp(Af), n, kp(Bh.as<T>()), ldp);
+            NHIP(hipGetLastError());
+        }
+    } else {
         slate_hip::TriMask up_, lo_;
         up_.mode = 2;
         up_.diag_off = b;                       // i <= j + b
@@ -562,7 +588,8 @@ void heev_1gpu(i64 n, T* Af, std::vector<double>& w, T* Z, bool wantz, hipStream
                                             std::max<i64>(8, std::min(nt0 / lag + 8, nt0 / 3 + 15))});
         NTRACE("heev::hb2st", s);
         slate_hip::hb2st_device<K<T>>(n, (int)b, kp(Bh.as<T>()), ldp, kp(V.as<T>()), kp(tau.as<T>()), row.as<i64>(),
-                                      len.as<i64>(), spd->as<i64>(), ntd->as<i64>(), work.as<int>(), nsw, nwg, s);
+                                      len.as<i64>(), spd->as<i64>(), ntd->as<i64>(), work.as<int>(), nsw, nwg, s,
+                                      nullptr, extent);
     }
     // ---- (d, e) and the phases that make a complex tridiagonal real
     // the diagonal / sub-diagonal = 1 x n blocks with stride ldp + 1
