@@ -281,6 +281,121 @@ void dc_merge_rows(const Merge& g, double rho, std::vector<double>& w, const std
     NHIP(hipStreamSynchronize(s));
 }
 
+// One tree LEVEL of merges with the sort, deflation, close-pole rotations
+// and every index set formed on the device (stedc_level_prep), ONE host read
+// of the per-merge sizes, then per merge the rotations, the secular solve,
+// laed3's split GEMM and the final ordering -- models/stedc.py
+// _merge_level_gpu, for one process (all rows).  wd: the device copy of the
+// eigenvalues (updated in place), Q: n x n (ld ldq).
+struct LevelWork {
+    std::vector<std::unique_ptr<Scratch>> keep;
+    double *dd, *zs, *cs, *sn, *rC, *rS, *lam;
+    int *ty, *kp_, *rot;
+    i64 *order, *c, *K, *S1, *KS1, *S2, *KS2, *D, *isK, *rI, *rJ, *o2;
+    LevelWork(i64 n, hipStream_t s) {
+        const size_t nn = (size_t)std::max<i64>(n, 1);
+        auto f = [&](size_t es) { keep.push_back(std::make_unique<Scratch>(nn * es, s)); return keep.back()->p; };
+        dd = (double*)f(8); zs = (double*)f(8); cs = (double*)f(8); sn = (double*)f(8); rC = (double*)f(8);
+        rS = (double*)f(8); lam = (double*)f(8);
+        ty = (int*)f(4); kp_ = (int*)f(4); rot = (int*)f(4);
+        order = (i64*)f(8); c = (i64*)f(8); K = (i64*)f(8); S1 = (i64*)f(8); KS1 = (i64*)f(8); S2 = (i64*)f(8);
+        KS2 = (i64*)f(8); D = (i64*)f(8); isK = (i64*)f(8); rI = (i64*)f(8); rJ = (i64*)f(8); o2 = (i64*)f(8);
+    }
+};
+
+void dc_level_device(const std::vector<Merge>& lev, const std::vector<double>& e, LevelWork& ws, const double* W,
+                     const double* Z, double* wd, double* Q, i64 ldq, i64 n, hipStream_t s) {
+    const i64 nm = (i64)lev.size();
+    if (!nm) return;
+    std::vector<std::unique_ptr<Scratch>> keep;
+    std::vector<i64> desc;
+    std::vector<double> rhos;
+    i64 maxs = 1;
+    for (auto& g : lev) {
+        const double r = e[g.m - 1];
+        desc.insert(desc.end(), {g.a, g.m, g.b, r < 0 ? 1 : 0});
+        rhos.push_back(std::abs(r));
+        maxs = std::max(maxs, g.b - g.a);
+    }
+    Scratch* descd = upload_vec(keep, desc, s);
+    Scratch* rhod = upload_vec(keep, rhos, s);
+    const size_t mb = slate_hip::stedc_meta_bytes();
+    Scratch meta((size_t)nm * mb, s);
+    slate_hip::stedc_level_prep(n, nm, maxs, descd->as<i64>(), rhod->as<double>(), W, Z, ws.dd, ws.zs, ws.ty,
+                                ws.order, ws.c, ws.kp_, ws.rot, ws.cs, ws.sn, meta.p, ws.K, ws.S1, ws.KS1, ws.S2,
+                                ws.KS2, ws.D, ws.isK, ws.rI, ws.rJ, ws.rC, ws.rS, s);
+    const std::vector<unsigned char> mh = download_vec<unsigned char>(meta.p, (size_t)nm * mb, s);
+    for (i64 t = 0; t < nm; ++t) {
+        const Merge& g = lev[(size_t)t];
+        const i64 a = g.a, m = g.m, b = g.b, S = b - a;
+        i64 ints[8];
+        double dbl[2];
+        std::memcpy(ints, mh.data() + (size_t)t * mb, sizeof ints);
+        std::memcpy(dbl, mh.data() + (size_t)t * mb + 64, sizeof dbl);
+        const i64 k = ints[1], nrot = ints[2], n1 = ints[3], n2 = ints[4], nd = ints[5];
+        const double zzK = dbl[1];
+        const int flip = e[m - 1] < 0 ? 1 : 0;
+        const double r = std::abs(e[m - 1]);
+        double* qm = Q + a + a * ldq;                          // rows a..b of columns a..b
+        Scratch Qs((size_t)S * S * sizeof(double), s);
+        slate_hip::cols_copy(S, S, qm, ldq, ws.order + a, Qs.as<double>(), S, false, s);
+        if (nrot) slate_hip::rot_cols(S, Qs.as<double>(), S, nrot, ws.rI + a, ws.rJ + a, ws.rC + a, ws.rS + a, s);
+        Scratch dK((size_t)std::max<i64>(k, 1) * 8, s), org((size_t)std::max<i64>(k, 1) * 8, s),
+            mu((size_t)std::max<i64>(k, 1) * 8, s), zK((size_t)std::max<i64>(k, 1) * 8, s),
+            zh((size_t)std::max<i64>(k, 1) * 8, s);
+        if (k) {
+            slate_hip::vec_gather(k, ws.dd + a, ws.K + a, dK.as<double>(), s);
+            slate_hip::vec_gather(k, ws.zs + a, ws.K + a, zK.as<double>(), s);
+            slate_hip::stedc_secular(k, dK.as<double>(), zK.as<double>(), r, zzK, org.as<i64>(), mu.as<double>(),
+                                     zh.as<double>(), nullptr, 0, s);
+        }
+        slate_hip::stedc_lambda(S, ws.dd + a, ws.isK + a, dK.as<double>(), org.as<i64>(), mu.as<double>(), flip,
+                                ws.lam + a, s);
+        if (k) {
+            // Qs[:, K] <- Qs[:, K] V: rows above m with the K columns nonzero
+            // there (S1 / KS1), rows below with S2 / KS2; V in column chunks
+            struct Part { i64 ra, rb, ns; i64 *Sx, *KSx; };
+            std::vector<Part> parts{{0, m - a, n1, ws.S1, ws.KS1}, {m - a, S, n2, ws.S2, ws.KS2}};
+            std::vector<std::unique_ptr<Scratch>> srcs;
+            for (auto& pt : parts) {
+                if (!pt.ns || pt.rb <= pt.ra) { srcs.push_back(nullptr); continue; }
+                const i64 np = pt.rb - pt.ra;
+                srcs.push_back(std::make_unique<Scratch>((size_t)np * pt.ns * 8, s));
+                slate_hip::cols_copy(np, pt.ns, Qs.as<double>() + pt.ra, S, pt.KSx + a, srcs.back()->as<double>(), np,
+                                     false, s);
+            }
+            const i64 CH = 4096;
+            for (i64 j0 = 0; j0 < k; j0 += CH) {
+                const i64 nc = std::min(CH, k - j0);
+                Scratch V((size_t)k * nc * 8, s);
+                slate_hip::stedc_vectors(k, dK.as<double>(), zh.as<double>(), org.as<i64>(), mu.as<double>(), j0, nc,
+                                         V.as<double>(), k, s);
+                for (size_t pi = 0; pi < parts.size(); ++pi) {
+                    const Part& pt = parts[pi];
+                    const i64 np = pt.rb - pt.ra;
+                    if (np <= 0) continue;
+                    Scratch out((size_t)np * nc * 8, s);
+                    if (srcs[pi]) {
+                        Scratch Vp((size_t)pt.ns * nc * 8, s);
+                        slate_hip::permute_rows_gather<double>(pt.ns, nc, V.as<double>(), k, Vp.as<double>(), pt.ns,
+                                                               pt.Sx + a, s);
+                        gemm_k<double>('N', 'N', np, nc, pt.ns, 1.0, srcs[pi]->as<double>(), np, Vp.as<double>(),
+                                       pt.ns, 0.0, out.as<double>(), np, s);
+                    } else {
+                        dzero(out.p, (size_t)np * nc * 8, s);
+                    }
+                    slate_hip::cols_copy(np, nc, out.as<double>(), np, ws.K + a + j0, Qs.as<double>() + pt.ra, S, true,
+                                         s);
+                }
+            }
+        }
+        slate_hip::stedc_merge2(ws.lam + a, ws.K + a, k, ws.D + a, nd, flip, ws.o2 + a, s);
+        slate_hip::vec_gather(S, ws.lam + a, ws.o2 + a, wd + a, s);
+        slate_hip::cols_copy(S, S, Qs.as<double>(), S, ws.o2 + a, qm, ldq, false, s);
+    }
+    NHIP(hipStreamSynchronize(s));
+}
+
 // Divide & conquer with the eigenvector matrix distributed by ROWS: this
 // process holds rows [r0, r1) of every column (Q, ld ldq), w (all n
 // eigenvalues) ends identical on every rank.  Every rank solves every leaf
@@ -325,6 +440,26 @@ void stedc_rows(i64 n, const std::vector<double>& d, const std::vector<double>& 
             throw Error("native heev: a divide & conquer leaf did not converge");
     }
     Scratch zb((size_t)n * sizeof(double), s);
+    // one process, all rows: the level-batched device merges (default;
+    // SLATE_AMD_NATIVE_DC_DEVICE=0 keeps the per-merge host logic below)
+    static const bool dev_merge = [] { const char* e = std::getenv("SLATE_AMD_NATIVE_DC_DEVICE"); return !(e && e[0] == '0'); }();
+    if (dev_merge && !comm && r0 == 0 && r1 == n) {
+        LevelWork ws(n, s);
+        Scratch wdv((size_t)n * sizeof(double), s), Wl((size_t)n * sizeof(double), s);
+        upload(wdv.p, w.data(), (size_t)n * sizeof(double), s);
+        for (int t = (int)levels.size() - 1; t >= 0; --t) {
+            dzero(zb.p, (size_t)n * sizeof(double), s);
+            double* z = zb.as<double>();
+            for (auto& g : levels[t]) {
+                copy2d(z + g.a, 1, Q + (g.m - 1) + g.a * ldq, ldq, 1, g.m - g.a, s);
+                copy2d(z + g.m, 1, Q + g.m + g.m * ldq, ldq, 1, g.b - g.m, s);
+            }
+            dcopy(Wl.p, wdv.p, (size_t)n * sizeof(double), s);      // the children's eigenvalues of this level
+            dc_level_device(levels[t], e, ws, Wl.as<double>(), z, wdv.as<double>(), Q, ldq, n, s);
+        }
+        w = download_vec<double>(wdv.p, (size_t)n, s);
+        return;
+    }
     for (int t = (int)levels.size() - 1; t >= 0; --t) {
         // z of every merge of this level from the owners of rows m - 1 and m
         dzero(zb.p, (size_t)n * sizeof(double), s);
@@ -407,7 +542,7 @@ void he2hb(i64 n, i64 nb, T* Af, i64 ld, std::vector<Panel<T>>& panels, hipStrea
 }
 
 // Z := Q1 Z, Q1 = H_0 H_1 ... (panels last to first: Z -= V T (V^H Z)).
-// Groups of G = SLATE_AMD_UNMTR_HE2HB_GROUP (default 4) consecutive panels
+// Groups of G = SLATE_AMD_UNMTR_HE2HB_GROUP (default 8 here) consecutive panels
 // are merged into ONE block reflector I - Vg Tg Vg^H (forward larft merge,
 // Tg = [[T1, -T1 V1^H V2 T2], [0, T2]]): Z streams once per group with
 // K = G nb instead of once per panel with K = nb (models/eig.py
@@ -415,7 +550,7 @@ void he2hb(i64 n, i64 nb, T* Af, i64 ld, std::vector<Panel<T>>& panels, hipStrea
 template <typename T>
 void unmtr_he2hb(i64 n, i64 nc, std::vector<Panel<T>>& panels, T* Z, i64 ldz, hipStream_t s) {
     const char ct = ctrans<T>();
-    static const i64 G = [] { const char* e = std::getenv("SLATE_AMD_UNMTR_HE2HB_GROUP"); return e ? std::max(1, std::atoi(e)) : 4; }();
+    static const i64 G = [] { const char* e = std::getenv("SLATE_AMD_UNMTR_HE2HB_GROUP"); return e ? std::max(1, std::atoi(e)) : 8; }();
     if (G > 1 && nc > 0) {
         i64 i1 = (i64)panels.size();
         while (i1 > 0) {
