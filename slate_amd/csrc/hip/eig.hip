@@ -473,11 +473,17 @@ unmtr_hb2st_mfma_kernel(i64 n, i64 ncols, double* __restrict__ Z, i64 ldz, const
 
 bool unmtr_hb2st_mfma(i64 n, i64 ncols, double* Z, i64 ldz, const double* V, i64 b, const double* tau,
                       const i64* sp, const i64* nt, const i64* gJ, const i64* gt, const i64* gptr, i64 ngroups,
-                      double* Tg, i64 nsw, hipStream_t s) {
+                      double* Tg, i64 nsw, hipStream_t s, int phase) {
+    // phase bit 1: build the groups' Y = V T into Tg; bit 2: apply them (the
+    // native heev builds Tg on a side stream while the tridiagonal D & C runs)
     if (b != TB) return false;
     if (ncols <= 0 || nsw <= 0 || ngroups <= 0) return true;
-    hipLaunchKernelGGL(hb2st_tfac_kernel, dim3((unsigned)ngroups), dim3(256), 0, s, V, tau, sp, nt, gJ, gt, nsw, Tg);
-    HIP_LAUNCH_CHECK();
+    if (phase & 1) {
+        hipLaunchKernelGGL(hb2st_tfac_kernel, dim3((unsigned)ngroups), dim3(256), 0, s, V, tau, sp, nt, gJ, gt, nsw,
+                           Tg);
+        HIP_LAUNCH_CHECK();
+    }
+    if (!(phase & 2)) return true;
     hipLaunchKernelGGL(unmtr_hb2st_mfma_kernel, dim3((unsigned)((ncols + TCW - 1) / TCW)), dim3(512), 0, s, n, ncols,
                        Z, ldz, V, sp, nt, gptr, Tg, nsw);
     HIP_LAUNCH_CHECK();

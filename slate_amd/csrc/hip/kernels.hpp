@@ -148,7 +148,7 @@ bool unmtr_hb2st_blocked_range(i64 n, i64 ncols, T* Z, i64 ldz, const T* V, i64 
                                const i64* nt, i64 nsw, bool conj_tau, i64 Jlo, i64 Jhi, i64 slot0, hipStream_t s);
 bool unmtr_hb2st_mfma(i64 n, i64 ncols, double* Z, i64 ldz, const double* V, i64 b, const double* tau,
                       const i64* sp, const i64* nt, const i64* gJ, const i64* gt, const i64* gptr, i64 ngroups,
-                      double* Tg, i64 nsw, hipStream_t s);
+                      double* Tg, i64 nsw, hipStream_t s, int phase = 3);
 template <typename T> void v_explicit(i64 m, i64 n, const T* A, i64 lda, T* V, i64 ldv, hipStream_t s);
 template <typename T> void trtri(char uplo, char diag, i64 n, T* A, i64 lda, i64* info, hipStream_t s);
 template <typename T> void tri_inv(char uplo, char diag, i64 n, const T* A, i64 lda, T* W, i64 ldw, hipStream_t s);

@@ -548,45 +548,94 @@ void he2hb(i64 n, i64 nb, T* Af, i64 ld, std::vector<Panel<T>>& panels, hipStrea
 // K = G nb instead of once per panel with K = nb (models/eig.py
 // unmtr_he2hb / _merge_reflectors).
 template <typename T>
+struct QGroup { i64 r0, m, kt; std::unique_ptr<Scratch> Vg, Tg; };
+
+inline i64 unmtr_he2hb_group() {
+    static const i64 G = [] { const char* e = std::getenv("SLATE_AMD_UNMTR_HE2HB_GROUP"); return e ? std::max(1, std::atoi(e)) : 8; }();
+    return G;
+}
+
+// the merged groups, last group first.  The buffers are allocated on
+// stream sa (the stream that later applies and frees them); the merge work
+// (he2hb_groups_fill) runs on sw, ordered after sa by the event `ready`
+template <typename T>
+std::vector<QGroup<T>> he2hb_groups(i64 n, std::vector<Panel<T>>& panels, i64 G, hipStream_t sa, hipStream_t sw,
+                                    hipEvent_t ready) {
+    std::vector<QGroup<T>> gs;
+    for (i64 i1 = (i64)panels.size(); i1 > 0;) {
+        const i64 i0 = std::max<i64>(0, i1 - G);
+        QGroup<T> g;
+        g.r0 = panels[i0].r0;
+        g.m = n - g.r0;
+        g.kt = 0;
+        for (i64 i = i0; i < i1; ++i) g.kt += panels[i].kk;
+        g.Vg = std::make_unique<Scratch>((size_t)g.m * g.kt * sizeof(T), sa);
+        g.Tg = std::make_unique<Scratch>((size_t)g.kt * g.kt * sizeof(T), sa);
+        gs.push_back(std::move(g));
+        i1 = i0;
+    }
+    if (sw != sa) {
+        NHIP(hipEventRecord(ready, sa));
+        NHIP(hipStreamWaitEvent(sw, ready, 0));
+    }
+    return gs;
+}
+
+template <typename T>
+void he2hb_groups_fill(i64 n, std::vector<Panel<T>>& panels, i64 G, std::vector<QGroup<T>>& gs, hipStream_t sw) {
+    const char ct = ctrans<T>();
+    i64 i1 = (i64)panels.size();
+    for (auto& g : gs) {
+        const i64 i0 = std::max<i64>(0, i1 - G), r0 = g.r0, m = g.m, kt = g.kt;
+        T* vg = g.Vg->template as<T>();
+        T* tg = g.Tg->template as<T>();
+        dzero(vg, (size_t)m * kt * sizeof(T), sw);
+        dzero(tg, (size_t)kt * kt * sizeof(T), sw);
+        i64 c = 0;
+        for (i64 i = i0; i < i1; ++i) {
+            const Panel<T>& pn = panels[i];
+            const i64 kb = pn.kk, off = pn.r0 - r0, mi = n - pn.r0;
+            const T* Vi = pn.V->template as<T>();
+            const T* Ti = pn.T_->template as<T>();
+            copy2d(vg + off + c * m, m, Vi, mi, mi, kb, sw);
+            copy2d(tg + c + c * kt, kt, Ti, kb, kb, kb, sw);      // T_i is upper triangular (lower zero)
+            if (c) {
+                // T12 = -T_prev (V_prev^H V_i) T_i over the rows V_i spans
+                Scratch S1((size_t)c * kb * sizeof(T), sw), S2((size_t)c * kb * sizeof(T), sw);
+                gemm_k<T>(ct, 'N', c, kb, mi, T(1), vg + off, m, Vi, mi, T(0), S1.as<T>(), c, sw);
+                gemm_k<T>('N', 'N', c, kb, c, T(1), tg, kt, S1.as<T>(), c, T(0), S2.as<T>(), c, sw);
+                gemm_k<T>('N', 'N', c, kb, kb, T(-1), S2.as<T>(), c, Ti, kb, T(0), tg + c * kt, kt, sw);
+            }
+            c += kb;
+        }
+        i1 = i0;
+    }
+}
+
+// Z(r0:, :) -= Vg Tg (Vg^H Z(r0:, :)) per group, on s
+template <typename T>
+void apply_groups(i64 nc, std::vector<QGroup<T>>& gs, T* Z, i64 ldz, hipStream_t s) {
+    const char ct = ctrans<T>();
+    if (nc <= 0) return;
+    for (auto& g : gs) {
+        const i64 kt = g.kt, m = g.m;
+        T* vg = g.Vg->template as<T>();
+        T* tg = g.Tg->template as<T>();
+        Scratch W((size_t)kt * nc * sizeof(T), s), W2((size_t)kt * nc * sizeof(T), s);
+        gemm_k<T>(ct, 'N', kt, nc, m, T(1), vg, m, Z + g.r0, ldz, T(0), W.as<T>(), kt, s);
+        gemm_k<T>('N', 'N', kt, nc, kt, T(1), tg, kt, W.as<T>(), kt, T(0), W2.as<T>(), kt, s);
+        gemm_k<T>('N', 'N', m, nc, kt, T(-1), vg, m, W2.as<T>(), kt, T(1), Z + g.r0, ldz, s);
+    }
+}
+
+template <typename T>
 void unmtr_he2hb(i64 n, i64 nc, std::vector<Panel<T>>& panels, T* Z, i64 ldz, hipStream_t s) {
     const char ct = ctrans<T>();
-    static const i64 G = [] { const char* e = std::getenv("SLATE_AMD_UNMTR_HE2HB_GROUP"); return e ? std::max(1, std::atoi(e)) : 8; }();
+    const i64 G = unmtr_he2hb_group();
     if (G > 1 && nc > 0) {
-        i64 i1 = (i64)panels.size();
-        while (i1 > 0) {
-            const i64 i0 = std::max<i64>(0, i1 - G);
-            const i64 r0 = panels[i0].r0, m = n - r0;
-            i64 kt = 0;
-            for (i64 i = i0; i < i1; ++i) kt += panels[i].kk;
-            Scratch Vg((size_t)m * kt * sizeof(T), s), Tg((size_t)kt * kt * sizeof(T), s);
-            dzero(Vg.p, (size_t)m * kt * sizeof(T), s);
-            dzero(Tg.p, (size_t)kt * kt * sizeof(T), s);
-            T* vg = Vg.as<T>();
-            T* tg = Tg.as<T>();
-            i64 c = 0;
-            for (i64 i = i0; i < i1; ++i) {
-                const Panel<T>& pn = panels[i];
-                const i64 kb = pn.kk, off = pn.r0 - r0, mi = n - pn.r0;
-                const T* Vi = pn.V->template as<T>();
-                const T* Ti = pn.T_->template as<T>();
-                copy2d(vg + off + c * m, m, Vi, mi, mi, kb, s);
-                copy2d(tg + c + c * kt, kt, Ti, kb, kb, kb, s);      // T_i is upper triangular (lower zero)
-                if (c) {
-                    // T12 = -T_prev (V_prev^H V_i) T_i over the rows V_i spans
-                    Scratch S1((size_t)c * kb * sizeof(T), s), S2((size_t)c * kb * sizeof(T), s);
-                    gemm_k<T>(ct, 'N', c, kb, mi, T(1), vg + off, m, Vi, mi, T(0), S1.as<T>(), c, s);
-                    gemm_k<T>('N', 'N', c, kb, c, T(1), tg, kt, S1.as<T>(), c, T(0), S2.as<T>(), c, s);
-                    gemm_k<T>('N', 'N', c, kb, kb, T(-1), S2.as<T>(), c, Ti, kb, T(0), tg + c * kt, kt, s);
-                }
-                c += kb;
-            }
-            // Z(r0:, :) -= Vg Tg (Vg^H Z(r0:, :))
-            Scratch W((size_t)kt * nc * sizeof(T), s), W2((size_t)kt * nc * sizeof(T), s);
-            gemm_k<T>(ct, 'N', kt, nc, m, T(1), vg, m, Z + r0, ldz, T(0), W.as<T>(), kt, s);
-            gemm_k<T>('N', 'N', kt, nc, kt, T(1), tg, kt, W.as<T>(), kt, T(0), W2.as<T>(), kt, s);
-            gemm_k<T>('N', 'N', m, nc, kt, T(-1), vg, m, W2.as<T>(), kt, T(1), Z + r0, ldz, s);
-            i1 = i0;
-        }
+        auto gs = he2hb_groups<T>(n, panels, G, s, s, nullptr);
+        he2hb_groups_fill<T>(n, panels, G, gs, s);
+        apply_groups<T>(nc, gs, Z, ldz, s);
         return;
     }
     for (auto it = panels.rbegin(); it != panels.rend(); ++it) {
@@ -713,6 +762,22 @@ void heev_1gpu(i64 n, T* Af, std::vector<double>& w, T* Z, bool wantz, hipStream
     std::vector<std::unique_ptr<Scratch>> keep;
     Scratch* ntd = upload_vec(keep, nt, s);
     Scratch* spd = upload_vec(keep, sp, s);
+    // side stream: the Q1 group merges run during the chase (which fills
+    // ~100 of the 256 CUs) and the Q2 T factors during the D & C
+    // (SLATE_AMD_NATIVE_HEEV_OVERLAP=0: everything on s)
+    static const bool ovl_env = [] { const char* e = std::getenv("SLATE_AMD_NATIVE_HEEV_OVERLAP"); return !(e && e[0] == '0'); }();
+    hipStream_t side = rt().panel;
+    const i64 G1 = unmtr_he2hb_group();
+    const bool overlap = ovl_env && wantz && !dbg && G1 > 1 && side != nullptr && side != s;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    if (overlap)
+        for (auto& e : ev) NHIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    struct EvGuard {
+        hipEvent_t* e;
+        ~EvGuard() { for (int i = 0; i < 3; ++i) if (e[i]) (void)hipEventDestroy(e[i]); }
+    } ev_guard{ev};
+    std::vector<QGroup<T>> q1g;
+    if (overlap) q1g = he2hb_groups<T>(n, panels, G1, s, side, ev[0]);
     if (nsw > 0 && total > 0) {
         Scratch work((size_t)(nsw + 2) * sizeof(int), s);
         dzero(work.p, (size_t)(nsw + 2) * sizeof(int), s);
@@ -726,6 +791,7 @@ void heev_1gpu(i64 n, T* Af, std::vector<double>& w, T* Z, bool wantz, hipStream
                                       len.as<i64>(), spd->as<i64>(), ntd->as<i64>(), work.as<int>(), nsw, nwg, s,
                                       nullptr, extent);
     }
+    if (overlap) he2hb_groups_fill<T>(n, panels, G1, q1g, side);
     // ---- (d, e) and the phases that make a complex tridiagonal real
     // the diagonal / sub-diagonal = 1 x n blocks with stride ldp + 1
     Scratch dsub((size_t)2 * std::max<i64>(n, 1) * sizeof(T), s);
@@ -763,6 +829,39 @@ void heev_1gpu(i64 n, T* Af, std::vector<double>& w, T* Z, bool wantz, hipStream
         return;
     }
     // ---- tridiagonal eigenvectors (D & C), then Z = Q1 Q2 Phase Qt
+    // fp64, b = 64: groups of b reflectors (sweep block J, task t) as block
+    // reflectors I - V T V^H on MFMA (eig.hip unmtr_hb2st_mfma, the Python
+    // path's form; the register-window kernel below is the other
+    // precisions' path).  Their T factors are built first -- on the side
+    // stream, during the D & C, when overlapping
+    std::vector<i64> gJ, gt, gptr(1, 0);
+    std::unique_ptr<Scratch> Tg;
+    Scratch *gJd = nullptr, *gtd = nullptr, *gpd = nullptr;
+    const bool mfma_q2 = std::is_same<T, double>::value && b == 64 && nsw > 0 && total > 0;
+    if (mfma_q2) {
+        for (i64 J = 0; J * b < nsw; ++J) {
+            const i64 TJ = nt[(size_t)(J * b)];
+            for (i64 t = 0; t < TJ; ++t) { gJ.push_back(J); gt.push_back(t); }
+            gptr.push_back(gptr.back() + TJ);
+        }
+        if (!gJ.empty()) {
+            gJd = upload_vec(keep, gJ, s);
+            gtd = upload_vec(keep, gt, s);
+            gpd = upload_vec(keep, gptr, s);
+            Tg = std::make_unique<Scratch>(gJ.size() * 2 * b * b * sizeof(double), s);
+            hipStream_t st = s;
+            if (overlap) {
+                NHIP(hipEventRecord(ev[1], s));
+                NHIP(hipStreamWaitEvent(side, ev[1], 0));
+                st = side;
+            }
+            if constexpr (std::is_same<T, double>::value)
+                slate_hip::unmtr_hb2st_mfma(n, n, nullptr, n, V.as<double>(), b, tau.as<double>(), spd->as<i64>(),
+                                            ntd->as<i64>(), gJd->as<i64>(), gtd->as<i64>(), gpd->as<i64>(),
+                                            (i64)gJ.size(), Tg->as<double>(), nsw, st, 1);
+        }
+    }
+    if (overlap) NHIP(hipEventRecord(ev[2], side));
     Scratch Qt((size_t)n * n * sizeof(double), s);
     {
         NTRACE("heev::stedc", s);
@@ -780,30 +879,16 @@ void heev_1gpu(i64 n, T* Af, std::vector<double>& w, T* Z, bool wantz, hipStream
     }
     NTRACE("heev::back_transform", s);
     real_to_phase<T>(n, n, Qt.as<double>(), n, phd ? kp(phd->as<T>()) : nullptr, kp(Z), n, s);
+    // the side stream's Q1 merges and Q2 T factors are done before the
+    // applies
+    if (overlap) NHIP(hipStreamWaitEvent(s, ev[2], 0));
     bool q2_done = false;
     if constexpr (std::is_same<T, double>::value) {
-        // fp64, b = 64: groups of b reflectors (sweep block J, task t) as
-        // block reflectors I - V T V^H on MFMA (eig.hip unmtr_hb2st_mfma,
-        // the Python path's form; the register-window kernel below is the
-        // other precisions' path)
-        if (b == 64 && nsw > 0 && total > 0) {
-            std::vector<i64> gJ, gt, gptr(1, 0);
-            for (i64 J = 0; J * b < nsw; ++J) {
-                const i64 TJ = nt[(size_t)(J * b)];
-                for (i64 t = 0; t < TJ; ++t) { gJ.push_back(J); gt.push_back(t); }
-                gptr.push_back(gptr.back() + TJ);
-            }
-            const i64 ng = (i64)gJ.size();
-            if (ng > 0) {
-                Scratch* gJd = upload_vec(keep, gJ, s);
-                Scratch* gtd = upload_vec(keep, gt, s);
-                Scratch* gpd = upload_vec(keep, gptr, s);
-                Scratch Tg((size_t)ng * 2 * b * b * sizeof(double), s);
-                q2_done = slate_hip::unmtr_hb2st_mfma(n, n, Z, n, V.as<double>(), b, tau.as<double>(), spd->as<i64>(),
-                                                      ntd->as<i64>(), gJd->as<i64>(), gtd->as<i64>(), gpd->as<i64>(), ng,
-                                                      Tg.as<double>(), nsw, s);
-                NHIP(hipStreamSynchronize(s));
-            }
+        if (mfma_q2) {
+            q2_done = gJ.empty() ||
+                      slate_hip::unmtr_hb2st_mfma(n, n, Z, n, V.as<double>(), b, tau.as<double>(), spd->as<i64>(),
+                                                  ntd->as<i64>(), gJd->as<i64>(), gtd->as<i64>(), gpd->as<i64>(),
+                                                  (i64)gJ.size(), Tg->as<double>(), nsw, s, 2);
         }
     }
     if (nsw > 0 && total > 0 && !q2_done) {
@@ -818,7 +903,8 @@ void heev_1gpu(i64 n, T* Af, std::vector<double>& w, T* Z, bool wantz, hipStream
         }
     }
     if (dbg) dbg_resid<T>("band (after unmtr_hb2st)", n, B0->as<T>(), n, Z, n, w, s);
-    unmtr_he2hb<T>(n, n, panels, Z, n, s);
+    if (overlap) apply_groups<T>(n, q1g, Z, n, s);
+    else unmtr_he2hb<T>(n, n, panels, Z, n, s);
     if (dbg) dbg_resid<T>("dense (after unmtr_he2hb)", n, A0->as<T>(), n, Z, n, w, s);
     NHIP(hipStreamSynchronize(s));
 }
