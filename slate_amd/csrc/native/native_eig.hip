@@ -497,30 +497,66 @@ void zero_strict_lower(i64 m, i64 k, T* P, i64 ld, hipStream_t s) {
 }
 
 // dense Hermitian Af (n x n, ld n, both triangles) -> band of width nb in
-// place; the panel reflectors (explicit V, T) are kept for the back-transform
+// place; the panel reflectors (explicit V, T) are kept for the back-transform.
+// Lookahead (models/eig.py he2hb's pipelining; SLATE_AMD_NATIVE_HE2HB_LOOKAHEAD=0
+// disables): the rank-2k update of step k first updates the next panel's
+// columns, and that panel's QR runs on the side stream (rt().panel) while the
+// bulk of the update streams the rest of A22
 template <typename T>
 void he2hb(i64 n, i64 nb, T* Af, i64 ld, std::vector<Panel<T>>& panels, hipStream_t s) {
     const char ct = ctrans<T>();
+    static const bool la_env = [] { const char* e = std::getenv("SLATE_AMD_NATIVE_HE2HB_LOOKAHEAD"); return !(e && e[0] == '0'); }();
+    hipStream_t side = rt().panel;
+    const bool la = la_env && side != nullptr && side != s;
+    hipEvent_t ev_upd = nullptr, ev_qr = nullptr;
+    if (la) {
+        NHIP(hipEventCreateWithFlags(&ev_upd, hipEventDisableTiming));
+        NHIP(hipEventCreateWithFlags(&ev_qr, hipEventDisableTiming));
+    }
+    struct EvGuard {
+        hipEvent_t a, b;
+        ~EvGuard() { if (a) (void)hipEventDestroy(a); if (b) (void)hipEventDestroy(b); }
+    } ev_guard{ev_upd, ev_qr};
     // per-call workspaces sized for the first (largest) panel: no allocation
     // inside the panel loop (the loop is launch-bound at the small panels)
     const i64 mmax = std::max<i64>(n - nb, 1);
     Scratch tau((size_t)nb * sizeof(T), s), X((size_t)mmax * nb * sizeof(T), s),
         VW((size_t)mmax * 2 * nb * sizeof(T), s), WV((size_t)mmax * 2 * nb * sizeof(T), s),
         Mt((size_t)nb * nb * sizeof(T), s);
+    auto make_panel = [&](i64 k0) {
+        const i64 r0 = k0 + nb, kb = std::min(nb, n - k0), m = n - r0;
+        Panel<T> pn;
+        pn.r0 = r0;
+        pn.kk = std::min(m, kb);
+        pn.V = std::make_unique<Scratch>((size_t)m * pn.kk * sizeof(T), s);
+        pn.T_ = std::make_unique<Scratch>((size_t)pn.kk * pn.kk * sizeof(T), s);
+        return pn;
+    };
+    auto panel_qr = [&](i64 k0, Panel<T>& pn, hipStream_t st) {
+        const i64 r0 = k0 + nb, kb = std::min(nb, n - k0), m = n - r0;
+        dzero(tau.p, (size_t)pn.kk * sizeof(T), st);
+        slate_hip::geqrf_panel_ws<K<T>>(m, kb, kp(Af + r0 + k0 * ld), ld, kp(tau.as<T>()),
+                                        kp(pn.T_->template as<T>()), pn.kk, kp(pn.V->template as<T>()), m,
+                                        rt().qr_work, st);
+    };
+    bool have_next = false;      // panels.back() is the next panel, factored on the side stream
+    Panel<T> next;
     for (i64 k0 = 0; k0 < n - nb; k0 += nb) {
         const i64 r0 = k0 + nb, kb = std::min(nb, n - k0), m = n - r0;
         if (m <= 0) break;
         const i64 kk = std::min(m, kb);
         T* P = Af + r0 + k0 * ld;
         Panel<T> pn;
-        pn.r0 = r0;
-        pn.kk = kk;
-        pn.V = std::make_unique<Scratch>((size_t)m * kk * sizeof(T), s);
-        pn.T_ = std::make_unique<Scratch>((size_t)kk * kk * sizeof(T), s);
-        dzero(tau.p, (size_t)kk * sizeof(T), s);
+        if (have_next) {
+            pn = std::move(next);
+            NHIP(hipStreamWaitEvent(s, ev_qr, 0));
+            have_next = false;
+        } else {
+            pn = make_panel(k0);
+            panel_qr(k0, pn, s);
+        }
         T* V = pn.V->template as<T>();
         T* Tm = pn.T_->template as<T>();
-        slate_hip::geqrf_panel_ws<K<T>>(m, kb, kp(P), ld, kp(tau.as<T>()), kp(Tm), kk, kp(V), m, rt().qr_work, s);
         // band part: R, the reflectors zeroed, mirrored to the upper triangle
         zero_strict_lower<T>(m, kb, P, ld, s);
         // (gecopy's m x n are the DESTINATION's: kb x m here)
@@ -536,9 +572,24 @@ void he2hb(i64 n, i64 nb, T* Af, i64 ld, std::vector<Panel<T>>& panels, hipStrea
         copy2d(VW.as<T>(), m, V, m, m, kk, s);
         copy2d(WV.as<T>(), m, Y, m, m, kk, s);
         copy2d(WV.as<T>() + m * kk, m, V, m, m, kk, s);
-        gemm_k<T>('N', ct, m, m, 2 * kk, T(-1), VW.as<T>(), m, WV.as<T>(), m, T(1), A22, ld, s);
+        // the next panel: columns r0 .. r0 + kbn of A22, rows r0 + nb ..
+        const i64 k1 = r0, kbn = std::min(nb, n - k1), mn = n - (k1 + nb);
+        if (la && mn > 0 && kbn < m) {
+            gemm_k<T>('N', ct, m, kbn, 2 * kk, T(-1), VW.as<T>(), m, WV.as<T>(), m, T(1), A22, ld, s);
+            next = make_panel(k1);                    // allocated on s before the event
+            NHIP(hipEventRecord(ev_upd, s));
+            NHIP(hipStreamWaitEvent(side, ev_upd, 0));
+            panel_qr(k1, next, side);
+            NHIP(hipEventRecord(ev_qr, side));
+            have_next = true;
+            gemm_k<T>('N', ct, m, m - kbn, 2 * kk, T(-1), VW.as<T>(), m, WV.as<T>() + kbn, m, T(1), A22 + kbn * ld,
+                      ld, s);
+        } else {
+            gemm_k<T>('N', ct, m, m, 2 * kk, T(-1), VW.as<T>(), m, WV.as<T>(), m, T(1), A22, ld, s);
+        }
         panels.push_back(std::move(pn));
     }
+    if (have_next) NHIP(hipStreamWaitEvent(s, ev_qr, 0));     // (not reached: the loop consumes it)
 }
 
 // Z := Q1 Z, Q1 = H_0 H_1 ... (panels last to first: Z -= V T (V^H Z)).
