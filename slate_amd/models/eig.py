@@ -183,8 +183,15 @@ def unmtr_he2hb(F: He2hbFactors, Z: torch.Tensor):
     group with K = 4 nb instead of once per panel with K = nb."""
     with trace_block("unmtr_he2hb"):
         from .qr import _apply_qh, _vh
+        groups = getattr(F, "groups", None)
+        if groups is not None and Z.is_cuda:
+            # built ahead on the side stream (premerge_groups)
+            torch.cuda.current_stream(Z.device).wait_event(F.ready)
+            for r0, Vg, Tg, Vh in groups:
+                _apply_qh(Vg, Tg, Z[r0:, :], conj=False, Vh=Vh)
+            return Z
         panels = F.panels
-        grp = max(1, int(os.environ.get("SLATE_AMD_UNMTR_HE2HB_GROUP", "4" if Z.is_cuda else "1")))
+        grp = _he2hb_group(Z.is_cuda)
         i1 = len(panels)
         while i1 > 0:
             i0 = max(0, i1 - grp)
@@ -196,6 +203,48 @@ def unmtr_he2hb(F: He2hbFactors, Z: torch.Tensor):
                 _apply_qh(Vg, Tg, Z[r0:, :], conj=False, Vh=_vh(Vg))
             i1 = i0
     return Z
+
+
+def _he2hb_group(gpu):
+    return max(1, int(os.environ.get("SLATE_AMD_UNMTR_HE2HB_GROUP", "4" if gpu else "1")))
+
+
+def premerge_groups(F: He2hbFactors, device):
+    """Build unmtr_he2hb's merged block reflectors (and their explicit V^H)
+    on the pipeline's panel stream, right after he2hb: they then run while
+    the bulge chase holds ~100 of the 256 CUs instead of after it.
+    unmtr_he2hb waits for F.ready before applying them.  No-op off the GPU,
+    on a serial stream set or with SLATE_AMD_HEEV_OVERLAP=0."""
+    if device.type != "cuda" or os.environ.get("SLATE_AMD_HEEV_OVERLAP", "1") == "0":
+        return
+    from ..parallel.streams import StreamSet
+    from .qr import _vh
+    ss = StreamSet(device, reserve_cus=0)
+    main = torch.cuda.current_stream(device)
+    side = ss.panel
+    if side is None or side == main:
+        return
+    side.wait_event(ss.event(main))
+    panels, grp, out = F.panels, _he2hb_group(True), []
+    with torch.cuda.stream(side):
+        for _, V, T in panels:
+            V.record_stream(side)
+            T.record_stream(side)
+        i1 = len(panels)
+        while i1 > 0:
+            i0 = max(0, i1 - grp)
+            if i1 - i0 == 1:
+                r0, Vg, Tg = panels[i0]
+            else:
+                r0, Vg, Tg = _merge_reflectors(panels[i0:i1])
+            Vh = _vh(Vg)
+            for t in (Vg, Tg, Vh):
+                if t is not None:
+                    t.record_stream(main)
+            out.append((r0, Vg, Tg, Vh))
+            i1 = i0
+    F.groups = out
+    F.ready = ss.event(side)
 
 
 def _merge_reflectors(group):
@@ -599,6 +648,8 @@ def heev(A, Lambda=None, Z=None, opts=None):
             scale = 1.0 / amax
             Af.mul_(scale)
         F1 = he2hb(Af, nb)
+        if Z is not None:
+            premerge_groups(F1, Af.device)
         d, e, F2 = hb2st(_band_only(Af, nb), nb, device=Af.device if Af.is_cuda else None)
         want = Z is not None
         if not want:
