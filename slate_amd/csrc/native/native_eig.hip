@@ -835,8 +835,12 @@ void heev_1gpu(i64 n, T* Af, std::vector<double>& w, T* Z, bool wantz, hipStream
         hipDeviceProp_t pr;
         NHIP(hipGetDeviceProperties(&pr, rt().device));
         const i64 nt0 = nt[0] ? nt[0] : 1, lag = 2;
-        const int nwg = (int)std::min<i64>({std::max<i64>(nsw, 1), (i64)pr.multiProcessorCount,
-                                            std::max<i64>(8, std::min(nt0 / lag + 8, nt0 / 3 + 15))});
+        int nwg = (int)std::min<i64>({std::max<i64>(nsw, 1), (i64)pr.multiProcessorCount,
+                                      std::max<i64>(8, std::min(nt0 / lag + 8, nt0 / 3 + 15))});
+        // diagnostics: SLATE_AMD_HB2ST_NWG overrides the chase's workgroup count
+        // (clamped to [1, min(sweeps, CUs)]: every workgroup must be resident)
+        if (const char* e = std::getenv("SLATE_AMD_HB2ST_NWG"); e && std::atoi(e) > 0)
+            nwg = (int)std::min<i64>({(i64)std::atoi(e), std::max<i64>(nsw, 1), (i64)pr.multiProcessorCount});
         NTRACE("heev::hb2st", s);
         slate_hip::hb2st_device<K<T>>(n, (int)b, kp(Bh.as<T>()), ldp, kp(V.as<T>()), kp(tau.as<T>()), row.as<i64>(),
                                       len.as<i64>(), spd->as<i64>(), ntd->as<i64>(), work.as<int>(), nsw, nwg, s,
