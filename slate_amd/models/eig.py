@@ -177,10 +177,10 @@ def _zero_strict_lower(P):
 def unmtr_he2hb(F: He2hbFactors, Z: torch.Tensor):
     """Z := Q1 Z (Q1 = Q_0 Q_1 ... from he2hb): panels applied last-to-first.
 
-    On a GPU, groups of SLATE_AMD_UNMTR_HE2HB_GROUP (default 4) consecutive
+    On a GPU, groups of SLATE_AMD_UNMTR_HE2HB_GROUP (default 8) consecutive
     panels are merged into one block reflector I - V T V^H (forward larft
     merge, T = [[T1, -T1 V1^H V2 T2], [0, T2]]): Z is streamed once per
-    group with K = 4 nb instead of once per panel with K = nb."""
+    group with K = 8 nb instead of once per panel with K = nb."""
     with trace_block("unmtr_he2hb"):
         from .qr import _apply_qh, _vh
         groups = getattr(F, "groups", None)
@@ -206,7 +206,9 @@ def unmtr_he2hb(F: He2hbFactors, Z: torch.Tensor):
 
 
 def _he2hb_group(gpu):
-    return max(1, int(os.environ.get("SLATE_AMD_UNMTR_HE2HB_GROUP", "4" if gpu else "1")))
+    # 8 panels per block reflector on a GPU: dsyevd n = 16384 1.995 s (4) ->
+    # 1.984 s (8), profiles/r6/heev/py_group_4_vs_8.txt
+    return max(1, int(os.environ.get("SLATE_AMD_UNMTR_HE2HB_GROUP", "8" if gpu else "1")))
 
 
 def premerge_groups(F: He2hbFactors, device):

@@ -556,7 +556,7 @@ def test_hb2st_gpu_matches_host_chase(early, lag, reuse, monkeypatch):
     assert (e.cpu().abs() - e2.cpu().abs()).abs().max().item() / scale < 1e-11
 
 
-@pytest.mark.parametrize("group", ["1", "3", "4"])
+@pytest.mark.parametrize("group", ["1", "3", "4", "8"])
 @pytest.mark.parametrize("dt", [torch.float64, torch.complex128])
 def test_unmtr_he2hb_grouped_panels(group, dt, monkeypatch):
     """Stage-1 back-transform with consecutive panels merged into one block
